@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Bench: committed ops applied/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+Workload (BASELINE.json configs[1]): a DistributedAtomicLong client-model stream —
+Get(50) + CompareAndSet(52) of java.lang.Long values, ~10% stale CASes — of 100M committed entries over
+65,536 AtomicValueState resources per GPU.  A "step" = one cc_apply_batch over the whole 100M-entry batch
+with its columns already resident in HBM (state carries over from step to step, as a replica's would).
+
+Multi-GPU (torchrun, one process per GPU, RCCL): resources shard by id (rank r owns global ids
+r, r+N, ...; weak scaling: every rank applies its own 100M-entry stream over its own 65,536 resources);
+after every batch the applied-index watermark is all-gathered over RCCL — the only
+cross-GPU exchange on this path.
+
+roofline: per-kernel device time from HIP events recorded on the launch stream over the timed region
+(cc_profile_*), dominant kernel, algorithmic bytes = 39 B/commit x commits per launch.
+cpu_baseline: the oracle (C++ restatement of the Java apply path, single thread) timed on this host
+over a bounded prefix of the same stream (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "committed ops applied/sec (1 and 8 GPUs) + % of HBM GB/s roofline"
+B_OP_C2 = 39  # index 8 + res 4 + op 1 + flags 1 + expect 8 + update 8 in, status 1 + value 8 out
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--commits", type=int, default=100_000_000)
+    ap.add_argument("--resources", type=int, default=65536)
+    ap.add_argument("--sub-batch", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=100_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from copycat_amd import abi
+    from copycat_amd.engine import DeviceBatch, Engine
+    from copycat_amd.workload import SEED_C2, atomic_long_stream
+
+    n, R = args.commits, args.resources
+    t_gen = time.time()
+    batch = atomic_long_stream(n, resources=R, seed=SEED_C2 + rank, index0=1)
+    t_gen = time.time() - t_gen
+    db = DeviceBatch.upload(batch, device=dev, columns=("index", "inst", "op", "flags", "a", "b"))
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    value = torch.zeros(n, dtype=torch.int64, device=dev)
+
+    E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch)
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E.instance_open_range(0, R, 0, 1 + rank, 1 + rank)
+    stream = torch.cuda.current_stream(dev)
+    wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
+    wm_local = db.cols["index"][n - 1:n].view(torch.int64)
+
+    def step():
+        E.apply(db, status, value, stream=stream)
+        if dist is not None:  # applied-index watermark exchange (RCCL all-gather over xGMI)
+            dist.all_gather_into_tensor(wm_all, wm_local)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if not args.no_profile:
+        E.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    E.sync()  # surfaces device-side errors
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    prof = E.profile_read() if not args.no_profile else {}
+    # sanity: the result columns are the real per-commit results (spot-check CAS success share on rank 0)
+    st_h = status[: min(n, 1_000_000)].cpu().numpy()
+    ok_share = float(np.mean(abi.status_code(st_h) == abi.CC_ST_OK))
+
+    total_commits = n * args.steps * world
+    value_ops = total_commits / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    roofline = None
+    if prof:
+        dom = max(prof, key=lambda k: prof[k][0])
+        ms_tot, launches = prof[dom]
+        commits_per_launch = n * args.steps / max(launches, 1)
+        avg_ms = ms_tot / max(launches, 1)
+        achieved = B_OP_C2 * commits_per_launch / (avg_ms * 1e-3) / 1e9
+        roofline = {
+            "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+            "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
+            "pipeline_achieved_gbps": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9, 1),
+            "pipeline_frac": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.oracle_py import Oracle
+
+        m = min(n, args.cpu_sample)
+        sample = batch.slice(0, m)
+        O = Oracle(R, R)
+        for r in range(R):
+            O.resource_create(r, abi.CC_RES_VALUE)
+            O.instance_open(r, r, 1 + r, 1)
+        tc = time.perf_counter()
+        O.apply(sample)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+               "sample": f"first {m:,} commits of the same c2 stream, C++ restatement of the Java apply path "
+                         f"(oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value_ops, 1), "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "c2: DistributedAtomicLong Get/CompareAndSet client-model stream, "
+                                   f"{n:,} committed entries over {R:,} AtomicValueState resources per GPU",
+                       "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
+                       "sub_batch": args.sub_batch or "default(16M)", "ok_status_share": round(ok_share, 4),
+                       "gen_s": round(t_gen, 2)},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,57 @@
+"""In-tree build of the native libraries (no JIT cache: the .so files travel with the repo snapshot).
+
+  libcopycat_apply.so     hipcc --offload-arch=gfx950: the engine (HIP kernels + C-ABI)
+  libcopycat_workload.so  g++: synthetic committed-command stream generators for benches/tests
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+
+ENGINE_SRCS = ["engine.hip", "partition.hip", "apply_value.hip", "quorum.hip"]
+ENGINE_HDRS = ["common.h", "engine_internal.h"]
+ENGINE_SO = os.path.join(HERE, "libcopycat_apply.so")
+WORKLOAD_SO = os.path.join(HERE, "libcopycat_workload.so")
+ARCH = os.environ.get("CC_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"build failed: {' '.join(cmd)}")
+
+
+def build_engine(force=False):
+    deps = [os.path.join(CSRC, f) for f in ENGINE_SRCS + ENGINE_HDRS] + [os.path.join(ROOT, "include", "copycat_apply.h")]
+    if force or _stale(ENGINE_SO, deps):
+        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+              *ENGINE_SRCS, "-o", ENGINE_SO])
+    return ENGINE_SO
+
+
+def build_workload(force=False):
+    src = os.path.join(CSRC, "workload.cpp")
+    if force or _stale(WORKLOAD_SO, [src]):
+        _run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "workload.cpp",
+              "-o", WORKLOAD_SO])
+    return WORKLOAD_SO
+
+
+def build_all(force=False):
+    return build_engine(force), build_workload(force)
+
+
+if __name__ == "__main__":
+    print(build_all(force="--force" in sys.argv))

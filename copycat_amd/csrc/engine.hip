@@ -1,0 +1,482 @@
+// engine.hip — the C-ABI of include/copycat_apply.h: engine handle, resource/instance registry, and the
+// batched apply driver (partition.hip -> apply_*.hip per sub-batch).
+//
+// Reference interface replaced: the Copycat StateMachine that ResourceManager implements
+// (manager/src/main/java/io/atomix/manager/ResourceManager.java:35-264), applying committed entries
+// one by one through ResourceManagerStateMachineExecutor.execute (:90-102) and
+// ResourceStateMachineExecutor.executeCommand/executeQuery (resource/.../ResourceStateMachineExecutor.java:73-91).
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "engine_internal.h"
+
+using namespace cc;
+
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* what, hipError_t e = hipSuccess) {
+  char buf[512];
+  if (e != hipSuccess)
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  else
+    snprintf(buf, sizeof buf, "%s", what);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHECK(x)                                        \
+  do {                                                     \
+    hipError_t _e = (x);                                   \
+    if (_e != hipSuccess) return set_err(CC_ERR_HIP, #x, _e); \
+  } while (0)
+
+struct cc_engine {
+  cc_config cfg{};
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t last_stream = nullptr;
+  uint32_t nb = 0, nbits = 0;
+  uint64_t sub_batch = 0, max_tiles = 0;
+  // host mirrors of the registry
+  std::vector<uint8_t> res_type;     // [nb*64]
+  std::vector<uint8_t> bucket_type;  // [nb] (a bucket holds one resource type)
+  std::vector<uint32_t> bucket_live; // live resources per bucket
+  std::vector<uint32_t> inst_res;    // [max_inst]
+  std::vector<uint64_t> inst_id, inst_client;
+  // device registry + state
+  uint32_t* d_inst_res = nullptr;
+  uint8_t* d_res_type = nullptr;
+  uint32_t* d_val_meta = nullptr;
+  uint64_t* d_val_v = nullptr;
+  // workspace
+  uint32_t* d_counts = nullptr;
+  uint32_t* d_tot = nullptr;
+  uint32_t* d_base = nullptr;
+  uint64_t* d_st_meta = nullptr;
+  u64x2* d_st_ab = nullptr;
+  uint32_t* d_err = nullptr;
+  uint64_t applied = 0;
+  bool applied_pending = false;
+  uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
+  // per-kernel profiling (cc_profile_enable)
+  bool prof_on = false;
+  std::vector<hipEvent_t> ev_pool;
+  struct Pending { int kernel; hipEvent_t a, b; };
+  std::vector<Pending> pending;
+  hipEvent_t open_ev[K_NUM] = {};
+  double prof_ms[K_NUM] = {};
+  uint64_t prof_n[K_NUM] = {};
+};
+
+static hipEvent_t take_event(cc_engine* e) {
+  if (!e->ev_pool.empty()) {
+    hipEvent_t ev = e->ev_pool.back();
+    e->ev_pool.pop_back();
+    return ev;
+  }
+  hipEvent_t ev = nullptr;
+  (void)hipEventCreate(&ev);
+  return ev;
+}
+
+static void mark_fn(void* ctx, int k, int begin, hipStream_t st) {
+  cc_engine* e = (cc_engine*)ctx;
+  hipEvent_t ev = take_event(e);
+  (void)hipEventRecord(ev, st);
+  if (begin) {
+    e->open_ev[k] = ev;
+  } else {
+    e->pending.push_back({k, e->open_ev[k], ev});
+    e->open_ev[k] = nullptr;
+  }
+}
+
+static Marker marker_of(cc_engine* e) { return Marker{e->prof_on ? &mark_fn : nullptr, e}; }
+
+static void drain_profile(cc_engine* e) {
+  for (auto& p : e->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      e->prof_ms[p.kernel] += ms;
+      e->prof_n[p.kernel] += 1;
+    }
+    e->ev_pool.push_back(p.a);
+    e->ev_pool.push_back(p.b);
+  }
+  e->pending.clear();
+}
+
+static void free_all(cc_engine* e) {
+  drain_profile(e);
+  for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  e->ev_pool.clear();
+  void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta, e->d_val_v, e->d_counts, e->d_tot,
+                  e->d_base,     e->d_st_meta,  e->d_st_ab,    e->d_err,   e->d_last_index};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+}
+
+extern "C" int cc_abi_version(void) { return CC_ABI_VERSION; }
+extern "C" const char* cc_last_error(void) { return g_err.c_str(); }
+
+extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
+  if (!cfg || !out) return set_err(CC_ERR_INVALID, "null config");
+  if (cfg->max_resources == 0 || cfg->max_resources > (uint32_t)kMaxBuckets * kResPerBucket)
+    return set_err(CC_ERR_CAPACITY, "max_resources must be in [1, 262144]");
+  if (cfg->max_instances == 0 || cfg->max_batch == 0) return set_err(CC_ERR_INVALID, "max_instances/max_batch must be > 0");
+  cc_engine* e = new cc_engine();
+  e->cfg = *cfg;
+  e->device = cfg->device;
+  hipError_t he = hipSetDevice(e->device);
+  if (he != hipSuccess) { delete e; return set_err(CC_ERR_HIP, "hipSetDevice", he); }
+  e->nb = (cfg->max_resources + kResPerBucket - 1) / kResPerBucket;
+  e->nbits = 0;
+  while ((1u << e->nbits) < e->nb) ++e->nbits;
+  e->sub_batch = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
+  e->sub_batch = std::min<uint64_t>(e->sub_batch, cfg->max_batch);
+  e->sub_batch = std::max<uint64_t>(e->sub_batch, 1);
+  if (e->sub_batch > 0xFFFFFFFFull) e->sub_batch = 0xFFFFFFFFull & ~(uint64_t)(kTile - 1);
+  e->max_tiles = (e->sub_batch + kTile - 1) / kTile;
+  const uint64_t slots = (uint64_t)e->nb * kResPerBucket;
+  e->res_type.assign(slots, CC_RES_NONE);
+  e->bucket_type.assign(e->nb, CC_RES_NONE);
+  e->bucket_live.assign(e->nb, 0);
+  e->inst_res.assign(cfg->max_instances, kNoRes);
+  e->inst_id.assign(cfg->max_instances, 0);
+  e->inst_client.assign(cfg->max_instances, 0);
+  auto fail = [&](const char* what, hipError_t x) {
+    free_all(e);
+    delete e;
+    return set_err(CC_ERR_HIP, what, x);
+  };
+#define ALLOC(p, bytes)                                   \
+  do {                                                    \
+    hipError_t x = hipMalloc((void**)&(p), (bytes));      \
+    if (x != hipSuccess) return fail("hipMalloc " #p, x); \
+  } while (0)
+  ALLOC(e->d_inst_res, sizeof(uint32_t) * cfg->max_instances);
+  ALLOC(e->d_res_type, slots);
+  ALLOC(e->d_val_meta, sizeof(uint32_t) * slots);
+  ALLOC(e->d_val_v, sizeof(uint64_t) * slots);
+  ALLOC(e->d_counts, sizeof(uint32_t) * e->max_tiles * e->nb);
+  ALLOC(e->d_tot, sizeof(uint32_t) * e->nb);
+  ALLOC(e->d_base, sizeof(uint32_t) * e->nb);
+  ALLOC(e->d_st_meta, sizeof(uint64_t) * e->sub_batch);
+  ALLOC(e->d_st_ab, sizeof(u64x2) * e->sub_batch);
+  ALLOC(e->d_err, sizeof(uint32_t));
+  ALLOC(e->d_last_index, sizeof(uint64_t));
+#undef ALLOC
+  if ((he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", he);
+  e->last_stream = e->own_stream;
+  if ((he = hipMemset(e->d_inst_res, 0xFF, sizeof(uint32_t) * cfg->max_instances)) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_res_type, 0, slots)) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_val_meta, 0, sizeof(uint32_t) * slots)) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_val_v, 0, sizeof(uint64_t) * slots)) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
+  if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
+  *out = e;
+  return CC_OK;
+}
+
+extern "C" int cc_engine_destroy(cc_engine* e) {
+  if (!e) return CC_ERR_INVALID;
+  (void)hipSetDevice(e->device);
+  if (e->last_stream) (void)hipStreamSynchronize(e->last_stream);
+  free_all(e);
+  delete e;
+  return CC_OK;
+}
+
+extern "C" void* cc_engine_stream(cc_engine* e) { return e ? (void*)e->own_stream : nullptr; }
+
+static int check_device_err(cc_engine* e) {
+  uint32_t err = 0;
+  HIPCHECK(hipMemcpy(&err, e->d_err, sizeof err, hipMemcpyDeviceToHost));
+  if (err) {
+    HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
+    if (err & kErrUnsupported)
+      return set_err(CC_ERR_UNSUPPORTED, "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten)");
+    return set_err(CC_ERR_STATE, "device-side check failed");
+  }
+  return CC_OK;
+}
+
+extern "C" int cc_sync(cc_engine* e) {
+  if (!e) return CC_ERR_INVALID;
+  HIPCHECK(hipSetDevice(e->device));
+  HIPCHECK(hipStreamSynchronize(e->last_stream));
+  if (e->applied_pending) {
+    uint64_t li = 0;
+    HIPCHECK(hipMemcpy(&li, e->d_last_index, sizeof li, hipMemcpyDeviceToHost));
+    e->applied = std::max(e->applied, li);
+    e->applied_pending = false;
+  }
+  return check_device_err(e);
+}
+
+// Registry updates are control-plane (the reference runs them as log commands too: ResourceManager.java:77-235);
+// the host orders them against batches, so they first drain the stream the last batch ran on.
+static int quiesce(cc_engine* e) {
+  HIPCHECK(hipSetDevice(e->device));
+  HIPCHECK(hipStreamSynchronize(e->last_stream));
+  return CC_OK;
+}
+
+static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
+  if (type != CC_RES_VALUE)
+    return set_err(CC_ERR_UNSUPPORTED, "this build applies AtomicValue resources on the GPU; map/lock/election/group are not built yet");
+  const uint64_t end = (uint64_t)first + count;
+  if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");
+  for (uint64_t s = first; s < end; ++s) {
+    if (e->res_type[s] != CC_RES_NONE) return set_err(CC_ERR_INVALID, "resource slot already in use");
+    const uint32_t b = (uint32_t)(s / kResPerBucket);
+    if (e->bucket_type[b] != CC_RES_NONE && e->bucket_type[b] != type)
+      return set_err(CC_ERR_INVALID, "a 64-slot bucket holds one resource type (allocate slots per type in groups of 64)");
+  }
+  int rc = quiesce(e);
+  if (rc) return rc;
+  for (uint64_t s = first; s < end; ++s) {
+    e->res_type[s] = (uint8_t)type;
+    const uint32_t b = (uint32_t)(s / kResPerBucket);
+    e->bucket_type[b] = (uint8_t)type;
+    e->bucket_live[b]++;
+  }
+  HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
+  // fresh state: AtomicValueState() {value = null; current = null}
+  HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
+  HIPCHECK(hipMemset(e->d_val_v + first, 0, sizeof(uint64_t) * count));
+  return CC_OK;
+}
+
+extern "C" int cc_resource_create(cc_engine* e, uint32_t slot, uint32_t type) {
+  if (!e) return CC_ERR_INVALID;
+  return create_range(e, slot, 1, type);
+}
+
+extern "C" int cc_resource_create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
+  if (!e) return CC_ERR_INVALID;
+  return create_range(e, first, count, type);
+}
+
+extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
+  if (!e || slot >= e->cfg.max_resources || e->res_type[slot] == CC_RES_NONE) return set_err(CC_ERR_INVALID, "unknown resource slot");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
+  e->res_type[slot] = CC_RES_NONE;
+  const uint32_t b = slot / kResPerBucket;
+  if (--e->bucket_live[b] == 0) e->bucket_type[b] = CC_RES_NONE;
+  HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
+  HIPCHECK(hipMemset(e->d_val_v + slot, 0, sizeof(uint64_t)));
+  const uint32_t none = kNoRes;
+  for (uint32_t i = 0; i < e->cfg.max_instances; ++i)
+    if (e->inst_res[i] == slot) {
+      e->inst_res[i] = kNoRes;
+      HIPCHECK(hipMemcpy(e->d_inst_res + i, &none, sizeof none, hipMemcpyHostToDevice));
+    }
+  return CC_OK;
+}
+
+static int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint32_t res_stride,
+                      uint64_t id_first, uint64_t client) {
+  const uint64_t end = (uint64_t)first + count;
+  if (end > e->cfg.max_instances) return set_err(CC_ERR_CAPACITY, "instance slot out of range");
+  for (uint64_t k = 0; k < count; ++k) {
+    const uint64_t r = (uint64_t)res_first + k * res_stride;
+    if (r >= e->cfg.max_resources || e->res_type[r] == CC_RES_NONE) return set_err(CC_ERR_INVALID, "instance on unknown resource");
+    if (e->inst_res[first + k] != kNoRes) return set_err(CC_ERR_INVALID, "instance slot already open");
+  }
+  int rc = quiesce(e);
+  if (rc) return rc;
+  for (uint64_t k = 0; k < count; ++k) {
+    e->inst_res[first + k] = (uint32_t)(res_first + k * res_stride);
+    e->inst_id[first + k] = id_first + k;
+    e->inst_client[first + k] = client;
+  }
+  HIPCHECK(hipMemcpy(e->d_inst_res + first, e->inst_res.data() + first, sizeof(uint32_t) * count, hipMemcpyHostToDevice));
+  return CC_OK;
+}
+
+extern "C" int cc_instance_open(cc_engine* e, uint32_t inst, uint32_t res_slot, uint64_t instance_id, uint64_t client_session) {
+  if (!e) return CC_ERR_INVALID;
+  return open_range(e, inst, 1, res_slot, 0, instance_id, client_session);
+}
+
+extern "C" int cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint64_t id_first,
+                                      uint64_t client_session) {
+  if (!e) return CC_ERR_INVALID;
+  return open_range(e, first, count, res_first, 1, id_first, client_session);
+}
+
+extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const cc_results* out, const cc_events* ev,
+                              void* stream) {
+  (void)ev;
+  if (!e || !c || !out) return set_err(CC_ERR_INVALID, "null argument");
+  if (n == 0) return CC_OK;
+  if (n > e->cfg.max_batch) return set_err(CC_ERR_CAPACITY, "batch larger than max_batch");
+  if (!c->inst || !c->op || !c->flags || !c->a || !c->b || !out->status || !out->value)
+    return set_err(CC_ERR_INVALID, "inst/op/flags/a/b columns and status/value outputs are required");
+  HIPCHECK(hipSetDevice(e->device));
+  hipStream_t st = stream ? (hipStream_t)stream : e->own_stream;
+  if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
+  e->last_stream = st;
+  for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
+    const uint64_t hi = std::min(n, lo + e->sub_batch);
+    PartArgs pa{};
+    pa.inst = c->inst;
+    pa.op = c->op;
+    pa.flags = c->flags;
+    pa.a = c->a;
+    pa.b = c->b;
+    pa.lo = lo;
+    pa.n = hi;
+    pa.inst_res = e->d_inst_res;
+    pa.max_inst = e->cfg.max_instances;
+    pa.nb = e->nb;
+    pa.nbits = e->nbits;
+    pa.counts = e->d_counts;
+    pa.tot = e->d_tot;
+    pa.base = e->d_base;
+    pa.st_meta = e->d_st_meta;
+    pa.st_ab = e->d_st_ab;
+    pa.out_status = out->status;
+    pa.out_value = out->value;
+    pa.mark = marker_of(e);
+    if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
+    ValueArgs va{};
+    va.st_meta = e->d_st_meta;
+    va.st_ab = e->d_st_ab;
+    va.base = e->d_base;
+    va.tot = e->d_tot;
+    va.nb = e->nb;
+    va.val_meta = e->d_val_meta;
+    va.val_v = e->d_val_v;
+    va.out_status = out->status + lo;
+    va.out_value = out->value + lo;
+    va.err = e->d_err;
+    va.mark = marker_of(e);
+    if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
+  }
+  if (c->index) {  // the applied watermark = index of the batch's last entry
+    HIPCHECK(hipMemcpyAsync(e->d_last_index, c->index + (n - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    e->applied_pending = true;
+  }
+  return CC_OK;
+}
+
+extern "C" int cc_apply_batch_host(cc_engine* e, const cc_batch* h, uint64_t n, const cc_results* hout) {
+  if (!e || !h || !hout) return set_err(CC_ERR_INVALID, "null argument");
+  if (n == 0) return CC_OK;
+  HIPCHECK(hipSetDevice(e->device));
+  struct Col {
+    const void* src;
+    size_t esz;
+    void* dev;
+  } cols[9] = {{h->index, 8, nullptr}, {h->time, 8, nullptr}, {h->inst, 4, nullptr}, {h->op, 1, nullptr}, {h->flags, 1, nullptr},
+               {h->key, 8, nullptr},   {h->a, 8, nullptr},    {h->b, 8, nullptr},    {h->aux, 8, nullptr}};
+  hipStream_t st = e->own_stream;
+  if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
+  e->last_stream = st;
+  int rc = CC_OK;
+  uint8_t* d_status = nullptr;
+  uint64_t* d_value = nullptr;
+  for (auto& col : cols) {
+    if (!col.src) continue;
+    if (hipMalloc(&col.dev, col.esz * n) != hipSuccess) { rc = set_err(CC_ERR_HIP, "hipMalloc column"); goto done; }
+    if (hipMemcpyAsync(col.dev, col.src, col.esz * n, hipMemcpyHostToDevice, st) != hipSuccess) {
+      rc = set_err(CC_ERR_HIP, "H2D");
+      goto done;
+    }
+  }
+  if (hipMalloc(&d_status, n) != hipSuccess || hipMalloc(&d_value, 8 * n) != hipSuccess) {
+    rc = set_err(CC_ERR_HIP, "hipMalloc results");
+    goto done;
+  }
+  {
+    cc_batch d{};
+    d.index = (const uint64_t*)cols[0].dev;
+    d.time = (const uint64_t*)cols[1].dev;
+    d.inst = (const uint32_t*)cols[2].dev;
+    d.op = (const uint8_t*)cols[3].dev;
+    d.flags = (const uint8_t*)cols[4].dev;
+    d.key = (const uint64_t*)cols[5].dev;
+    d.a = (const uint64_t*)cols[6].dev;
+    d.b = (const uint64_t*)cols[7].dev;
+    d.aux = (const uint64_t*)cols[8].dev;
+    cc_results r{d_status, d_value};
+    rc = cc_apply_batch(e, &d, n, &r, nullptr, st);
+    if (rc) goto done;
+    if (hipMemcpyAsync(hout->status, d_status, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(hout->value, d_value, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess) {
+      rc = set_err(CC_ERR_HIP, "D2H");
+      goto done;
+    }
+    rc = cc_sync(e);
+  }
+done:
+  (void)hipStreamSynchronize(st);
+  for (auto& col : cols)
+    if (col.dev) (void)hipFree(col.dev);
+  if (d_status) (void)hipFree(d_status);
+  if (d_value) (void)hipFree(d_value);
+  return rc;
+}
+
+extern "C" int cc_applied_index(cc_engine* e, uint64_t* out) {
+  if (!e || !out) return CC_ERR_INVALID;
+  int rc = cc_sync(e);
+  *out = e->applied;
+  return rc;
+}
+
+extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* h_tag, uint64_t* h_value,
+                                   uint8_t* h_has_current) {
+  if (!e || (uint64_t)first + count > e->cfg.max_resources) return set_err(CC_ERR_INVALID, "range");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  std::vector<uint32_t> meta(count);
+  HIPCHECK(hipMemcpy(meta.data(), e->d_val_meta + first, sizeof(uint32_t) * count, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(h_value, e->d_val_v + first, sizeof(uint64_t) * count, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < count; ++i) {
+    const bool live = e->res_type[first + i] == CC_RES_VALUE;
+    h_tag[i] = live ? (uint8_t)(meta[i] & 0xFF) : 0;
+    h_has_current[i] = live ? (uint8_t)((meta[i] >> 8) & 1) : 0;
+    if (!live) h_value[i] = 0;
+  }
+  return CC_OK;
+}
+
+static const char* kKernelNames[K_NUM] = {"k_part_count", "k_part_scan", "k_part_base", "k_part_scatter", "k_apply_value"};
+
+extern "C" int cc_profile_enable(cc_engine* e, int on) {
+  if (!e) return CC_ERR_INVALID;
+  e->prof_on = on != 0;
+  return CC_OK;
+}
+
+extern "C" int cc_profile_reset(cc_engine* e) {
+  if (!e) return CC_ERR_INVALID;
+  HIPCHECK(hipSetDevice(e->device));
+  drain_profile(e);
+  for (int k = 0; k < K_NUM; ++k) {
+    e->prof_ms[k] = 0;
+    e->prof_n[k] = 0;
+  }
+  return CC_OK;
+}
+
+extern "C" int cc_profile_read(cc_engine* e, int kernel, double* total_ms, uint64_t* launches, const char** name) {
+  if (!e || kernel < 0 || kernel >= K_NUM) return CC_ERR_INVALID;
+  HIPCHECK(hipSetDevice(e->device));
+  drain_profile(e);
+  if (total_ms) *total_ms = e->prof_ms[kernel];
+  if (launches) *launches = e->prof_n[kernel];
+  if (name) *name = kKernelNames[kernel];
+  return CC_OK;
+}

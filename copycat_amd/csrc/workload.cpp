@@ -1,0 +1,123 @@
+// workload.cpp — deterministic synthetic committed-command streams (host side, seeded splitmix64).
+//
+// These are the benches' and tests' inputs, not part of the apply path.  Each generator writes SoA columns
+// in the layout of cc_batch (include/copycat_apply.h).
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/copycat_apply.h"
+
+namespace {
+struct SplitMix64 {
+  uint64_t s;
+  explicit SplitMix64(uint64_t seed) : s(seed) {}
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  uint64_t below(uint64_t n) { return (uint64_t)(((unsigned __int128)next() * n) >> 64); }
+};
+}  // namespace
+
+extern "C" {
+
+// Config 2 stream: DistributedAtomicLong "add delta" client model (DistributedAtomicLong.java:117-146).
+// Each add on a uniformly chosen resource r emits, in log order:
+//   fresh cache (prob 1 - p_cold - p_stale):  CompareAndSet(E, E' + delta)             -> succeeds
+//   cold cache  (prob p_cold):                Get; CompareAndSet(E, E' + delta)        -> succeeds
+//   stale cache (prob p_stale):               CompareAndSet(stale, stale + delta) -> fails; Get; CAS(E, E'+delta)
+// where E is the current value (null for a fresh resource, A4) and E' = E != null ? E : 0; delta ~ U[-1000, 1000].
+// Values are java.lang.Long.  Instance slot = first_inst + r.  Returns the number of rows written (= n).
+uint64_t wl_atomic_long(uint64_t n, uint32_t resources, uint32_t first_inst, uint64_t seed, uint32_t p_cold_ppm,
+                        uint32_t p_stale_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
+                        uint8_t* op, uint8_t* flags, uint64_t* a, uint64_t* b) {
+  SplitMix64 rng(seed);
+  std::vector<uint8_t> tag(resources, CC_TAG_NULL);
+  std::vector<int64_t> val(resources, 0);
+  uint64_t i = 0;
+  auto emit = [&](uint32_t r, uint8_t o, uint8_t ta, uint64_t pa, uint8_t tb, uint64_t pb) {
+    if (i >= n) return;
+    if (index) index[i] = index0 + i;
+    if (time) time[i] = (index0 + i) / 1024;  // ~1 ms of log time per 1024 entries
+    inst[i] = first_inst + r;
+    op[i] = o;
+    flags[i] = CC_FLAGS(ta, tb, 0);
+    a[i] = pa;
+    b[i] = pb;
+    ++i;
+  };
+  auto cas = [&](uint32_t r, uint8_t et, int64_t ev, int64_t delta) {
+    const int64_t base = et == CC_TAG_NULL ? 0 : ev;
+    const int64_t upd = (int64_t)((uint64_t)base + (uint64_t)delta);  // wrapping Long add
+    emit(r, CC_OP_VALUE_CAS, et, (uint64_t)ev, CC_TAG_LONG, (uint64_t)upd);
+    const bool ok = (tag[r] == CC_TAG_NULL && et == CC_TAG_NULL) || (tag[r] != CC_TAG_NULL && et == tag[r] && ev == val[r]);
+    if (ok) {
+      tag[r] = CC_TAG_LONG;
+      val[r] = upd;
+    }
+    return ok;
+  };
+  while (i < n) {
+    const uint32_t r = (uint32_t)rng.below(resources);
+    const int64_t delta = (int64_t)rng.below(2001) - 1000;
+    const uint64_t u = rng.below(1000000);
+    if (u < p_stale_ppm) {
+      const int64_t stale = (tag[r] == CC_TAG_NULL ? 0 : val[r]) + 1 + (int64_t)rng.below(1000);
+      cas(r, CC_TAG_LONG, stale, delta);  // fails
+      emit(r, CC_OP_VALUE_GET, 0, 0, 0, 0);
+      cas(r, tag[r], tag[r] == CC_TAG_NULL ? 0 : val[r], delta);
+    } else if (u < (uint64_t)p_stale_ppm + p_cold_ppm) {
+      emit(r, CC_OP_VALUE_GET, 0, 0, 0, 0);
+      cas(r, tag[r], tag[r] == CC_TAG_NULL ? 0 : val[r], delta);
+    } else {
+      cas(r, tag[r], tag[r] == CC_TAG_NULL ? 0 : val[r], delta);
+    }
+  }
+  return i;
+}
+
+// Adversarial AtomicValue stream for parity tests: every op (Get/Set/CAS/GetAndSet/Delete), every value tag
+// (NULL/LONG/INT/BOOL/HANDLE) over a tiny value domain (so equals hits and misses), unknown instance slots,
+// ops of other resource types (UNKNOWN_OP), and a hot set of `hot` resources receiving p_hot_ppm of the rows
+// (long same-slot chains inside one 64-row step).
+uint64_t wl_value_random(uint64_t n, uint32_t resources, uint32_t first_inst, uint32_t max_inst, uint64_t seed,
+                         uint32_t hot, uint32_t p_hot_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
+                         uint8_t* op, uint8_t* flags, uint64_t* a, uint64_t* b) {
+  SplitMix64 rng(seed);
+  static const uint8_t ops[] = {CC_OP_VALUE_GET, CC_OP_VALUE_SET, CC_OP_VALUE_CAS, CC_OP_VALUE_CAS, CC_OP_VALUE_CAS,
+                                CC_OP_VALUE_GETANDSET, CC_OP_VALUE_GET};
+  auto rand_val = [&](uint8_t& t, uint64_t& p) {
+    const uint64_t k = rng.below(16);
+    t = k < 3 ? CC_TAG_NULL : (k < 11 ? CC_TAG_LONG : (k < 13 ? CC_TAG_INT : (k < 15 ? CC_TAG_BOOL : CC_TAG_HANDLE)));
+    p = t == CC_TAG_BOOL ? rng.below(2) : rng.below(4);
+    if (t == CC_TAG_NULL) p = rng.next();  // non-canonical payload under NULL must be ignored
+    if (t == CC_TAG_LONG && rng.below(8) == 0) p = ~p;  // negative longs
+    if (t == CC_TAG_INT && (p & 1)) p = (uint64_t)(int64_t)(int32_t)(0x80000000u | (uint32_t)p);
+  };
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t r = hot && rng.below(1000000) < p_hot_ppm ? (uint32_t)rng.below(hot) : (uint32_t)rng.below(resources);
+    uint64_t k = rng.below(1000);
+    uint8_t o = ops[rng.below(sizeof ops)];
+    uint32_t s = first_inst + r;
+    if (k < 3) s = max_inst + (uint32_t)rng.below(1000);                     // beyond the table
+    else if (k < 6) o = (uint8_t)(60 + rng.below(13));                       // a MapState op on a value resource
+    else if (k < 8) o = CC_OP_DELETE;                                        // DeleteCommand
+    uint8_t ta, tb;
+    uint64_t pa, pb;
+    rand_val(ta, pa);
+    rand_val(tb, pb);
+    if (index) index[i] = index0 + i;
+    if (time) time[i] = (index0 + i) / 1024;
+    inst[i] = s;
+    op[i] = o;
+    flags[i] = CC_FLAGS(ta, tb, 0);
+    a[i] = pa;
+    b[i] = pb;
+  }
+  return n;
+}
+
+}  // extern "C"

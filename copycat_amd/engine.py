@@ -1,0 +1,226 @@
+"""ctypes binding of libcopycat_apply.so — the host mirror of the reference's state-machine interface.
+
+`Engine` plays the role of the Copycat `StateMachine` the reference's ResourceManager implements
+(manager/src/main/java/io/atomix/manager/ResourceManager.java:35-264): resources and instance sessions are
+registered (getResource/createResource/deleteResource), then committed entries are applied — here a whole
+batch per call instead of one `operateResource` per entry (:56-72).  Per-commit exceptions come back as
+status codes (abi.CC_ST_*), never as a failed call.
+
+The HIP library is the only compute path: if it is missing or fails to load, importing this module raises.
+Torch is used only as the device allocator / stream provider (it is imported first so that the engine and
+torch share one HIP runtime instance).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import torch  # noqa: F401  (shared HIP runtime; device memory and streams)
+
+from . import abi
+from .batch import Batch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_HERE, "libcopycat_apply.so")
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__(f"cc error {rc}: {msg}")
+        self.rc = rc
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(SO_PATH):
+            raise ImportError(f"{SO_PATH} is missing: build it with `python -m copycat_amd.build` (hipcc, gfx950)")
+        L = C.CDLL(SO_PATH)
+        P, i32, u32, u64 = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64
+        sig = {
+            "cc_abi_version": (i32, []),
+            "cc_last_error": (C.c_char_p, []),
+            "cc_engine_create": (i32, [P, P]),
+            "cc_engine_destroy": (i32, [P]),
+            "cc_sync": (i32, [P]),
+            "cc_engine_stream": (P, [P]),
+            "cc_resource_create": (i32, [P, u32, u32]),
+            "cc_resource_create_range": (i32, [P, u32, u32, u32]),
+            "cc_resource_delete": (i32, [P, u32]),
+            "cc_instance_open": (i32, [P, u32, u32, u64, u64]),
+            "cc_instance_open_range": (i32, [P, u32, u32, u32, u64, u64]),
+            "cc_apply_batch": (i32, [P, P, u64, P, P, P]),
+            "cc_apply_batch_host": (i32, [P, P, u64, P]),
+            "cc_applied_index": (i32, [P, P]),
+            "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
+            "cc_quorum_commit": (i32, [P, u32, u64, P, P, P, P]),
+            "cc_expire_sweep": (i32, [P, u64, u64, u64, P, P, P]),
+            "cc_profile_enable": (i32, [P, i32]),
+            "cc_profile_reset": (i32, [P]),
+            "cc_profile_read": (i32, [P, i32, P, P, P]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.cc_abi_version() != abi.CC_ABI_VERSION:
+            raise ImportError("libcopycat_apply.so ABI version mismatch")
+        _LIB = L
+    return _LIB
+
+
+def _check(rc):
+    if rc != abi.CC_OK:
+        raise EngineError(rc, lib().cc_last_error().decode(errors="replace"))
+
+
+def _np(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _dptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return C.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+
+class DeviceBatch:
+    """Batch columns resident in HBM (torch tensors on a HIP device)."""
+
+    TORCH_DT = {"u8": torch.uint64, "u4": torch.uint32, "u1": torch.uint8}
+
+    def __init__(self, cols, n):
+        self.cols = cols
+        self.n = n
+
+    @classmethod
+    def upload(cls, b: Batch, device="cuda", columns=None):
+        cols = {}
+        for name, dt in abi.BATCH_COLUMNS:
+            if columns is not None and name not in columns:
+                continue
+            arr = getattr(b, name)
+            cols[name] = torch.from_numpy(arr.view({"u8": np.int64, "u4": np.int32, "u1": np.uint8}[dt])).to(
+                device, non_blocking=False).view(cls.TORCH_DT[dt])
+        return cls(cols, len(b))
+
+    def struct(self):
+        s = abi.cc_batch()
+        for name, _ in abi.BATCH_COLUMNS:
+            t = self.cols.get(name)
+            setattr(s, name, t.data_ptr() if t is not None else None)
+        return s
+
+
+class Engine:
+    def __init__(self, max_resources, max_instances, max_batch, device=0, flags=abi.CC_CFG_TIMERS_DEFERRED,
+                 sub_batch=0, max_events=0, map_capacity=0):
+        L = lib()
+        cfg = abi.cc_config()
+        cfg.max_resources = max_resources
+        cfg.max_instances = max_instances
+        cfg.max_batch = max_batch
+        cfg.max_events = max_events
+        cfg.map_capacity = map_capacity
+        cfg.device = device
+        cfg.flags = flags
+        cfg.sub_batch = sub_batch
+        h = C.c_void_p()
+        _check(L.cc_engine_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+        self.max_resources = max_resources
+        self.device = device
+        self.L = L
+
+    def close(self):
+        if self.h:
+            self.L.cc_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- registry (ResourceManager control commands, host side) --------------------------------------
+    def resource_create(self, slot, rtype):
+        _check(self.L.cc_resource_create(self.h, slot, rtype))
+
+    def resource_create_range(self, first, count, rtype):
+        _check(self.L.cc_resource_create_range(self.h, first, count, rtype))
+
+    def resource_delete(self, slot):
+        _check(self.L.cc_resource_delete(self.h, slot))
+
+    def instance_open(self, inst, res, instance_id, client):
+        _check(self.L.cc_instance_open(self.h, inst, res, instance_id, client))
+
+    def instance_open_range(self, first, count, res_first, id_first, client):
+        _check(self.L.cc_instance_open_range(self.h, first, count, res_first, id_first, client))
+
+    # ---- the hot path ----------------------------------------------------------------------------------
+    def apply(self, db: DeviceBatch, status, value, stream=None):
+        """Apply device-resident columns; `status` (uint8) / `value` (uint64) are device tensors of n rows."""
+        s = db.struct()
+        r = abi.cc_results(status.data_ptr(), value.data_ptr())
+        _check(self.L.cc_apply_batch(self.h, C.byref(s), db.n, C.byref(r), None, _stream_ptr(stream)))
+
+    def apply_host(self, b: Batch):
+        """PCIe-inclusive path: host columns in, host results out (H2D + apply + D2H + sync)."""
+        n = len(b)
+        status = np.zeros(n, np.uint8)
+        value = np.zeros(n, np.uint64)
+        s = abi.cc_batch()
+        for name, _ in abi.BATCH_COLUMNS:
+            setattr(s, name, getattr(b, name).ctypes.data)
+        r = abi.cc_results(status.ctypes.data, value.ctypes.data)
+        _check(self.L.cc_apply_batch_host(self.h, C.byref(s), n, C.byref(r)))
+        return status, value
+
+    def sync(self):
+        _check(self.L.cc_sync(self.h))
+
+    def stream(self):
+        return self.L.cc_engine_stream(self.h)
+
+    def applied_index(self):
+        out = C.c_uint64()
+        _check(self.L.cc_applied_index(self.h, C.byref(out)))
+        return out.value
+
+    # ---- per-kernel HIP-event timing ------------------------------------------------------------------
+    def profile(self, on=True):
+        _check(self.L.cc_profile_enable(self.h, 1 if on else 0))
+        _check(self.L.cc_profile_reset(self.h))
+
+    def profile_read(self):
+        """{kernel name: (total device ms, launches)} since the last profile() call (synchronizes)."""
+        out = {}
+        for k in range(5):
+            ms, n, name = C.c_double(), C.c_uint64(), C.c_char_p()
+            _check(self.L.cc_profile_read(self.h, k, C.byref(ms), C.byref(n), C.byref(name)))
+            out[name.value.decode()] = (ms.value, n.value)
+        return out
+
+    def value_state(self, first=0, count=None):
+        count = self.max_resources - first if count is None else count
+        tag, val, cur = np.zeros(count, np.uint8), np.zeros(count, np.uint64), np.zeros(count, np.uint8)
+        _check(self.L.cc_read_value_state(self.h, first, count, _np(tag), _np(val), _np(cur)))
+        return tag, val, cur
+
+
+def quorum_commit(match, term_start, commit_in, commit_out, stream=None):
+    """match: (replicas, groups) uint64 device tensor; others (groups,) uint64 device tensors."""
+    replicas, groups = match.shape
+    _check(lib().cc_quorum_commit(_dptr(match), replicas, groups, _dptr(term_start), _dptr(commit_in), _dptr(commit_out),
+                                  _stream_ptr(stream)))
+
+
+def expire_sweep(last, now, timeout, bitmap, count, stream=None):
+    _check(lib().cc_expire_sweep(_dptr(last), last.numel(), now, timeout, _dptr(bitmap), _dptr(count),
+                                 _stream_ptr(stream)))

@@ -1,0 +1,81 @@
+"""Synthetic committed-command streams, generated natively and deterministically.
+
+Streams are host numpy columns (Batch); benches upload them once so the timed region starts with the
+columns resident in HBM.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .batch import Batch
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        from .build import WORKLOAD_SO, build_workload
+
+        if not os.path.exists(WORKLOAD_SO):
+            build_workload()
+        L = C.CDLL(WORKLOAD_SO)
+        P, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        L.wl_atomic_long.restype = u64
+        L.wl_atomic_long.argtypes = [u64, u32, u32, u64, u32, u32, u64] + [P] * 7
+        L.wl_value_random.restype = u64
+        L.wl_value_random.argtypes = [u64, u32, u32, u32, u64, u32, u32, u64] + [P] * 7
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+SEED_C2 = 0xA700000 + 2  # seed = 0xA70_0000 + config#
+
+
+def atomic_long_stream(n, resources=65536, first_inst=0, seed=SEED_C2, p_cold=0.2, p_stale=0.1, index0=1):
+    """Config 2: DistributedAtomicLong add/CAS client model over `resources` AtomicValueState instances."""
+    b = Batch(n)
+    lib().wl_atomic_long(n, resources, first_inst, seed, int(p_cold * 1e6), int(p_stale * 1e6), index0,
+                         _p(b.index), _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.a), _p(b.b))
+    return b
+
+
+def value_random_stream(n, resources, max_inst, first_inst=0, seed=1, hot=0, p_hot=0.0, index0=1):
+    """Adversarial AtomicValue stream for parity tests (all ops/tags, unknown sessions, wrong-type ops)."""
+    b = Batch(n)
+    lib().wl_value_random(n, resources, first_inst, max_inst, seed, hot, int(p_hot * 1e6), index0,
+                          _p(b.index), _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.a), _p(b.b))
+    return b
+
+
+SEED_C4 = 0xA700000 + 4
+
+
+def quorum_groups(groups, replicas=5, seed=SEED_C4):
+    """Config 4a: per group leader lastIndex L ~ U[1e6, 2e6); follower matchIndex = L - U[0, 64);
+    termStart = L - U[0, 128); oldCommit = L - U[0, 96).  Returns (match[replicas, groups], term_start, commit_in)."""
+    rng = np.random.default_rng(seed)
+    last = rng.integers(1_000_000, 2_000_000, groups, dtype=np.uint64)
+    match = np.empty((replicas, groups), np.uint64)
+    match[0] = last
+    for r in range(1, replicas):
+        match[r] = last - rng.integers(0, 64, groups, dtype=np.uint64)
+    term_start = last - rng.integers(0, 128, groups, dtype=np.uint64)
+    commit_in = last - rng.integers(0, 96, groups, dtype=np.uint64)
+    return match, term_start, commit_in
+
+
+def expiry_sessions(sessions, timeout=5000, now=10_000_000, seed=SEED_C4 + 1):
+    """Config 4b: lastKeepAlive = now - U[0, 2*timeout)."""
+    rng = np.random.default_rng(seed)
+    last = now - rng.integers(0, 2 * timeout, sessions, dtype=np.uint64)
+    return last, now, timeout
+
+
+__all__ = ["atomic_long_stream", "value_random_stream", "quorum_groups", "expiry_sessions", "abi"]

@@ -1,0 +1,255 @@
+/*
+ * copycat_apply.h — C-ABI of the MI355X batched commit-apply engine.
+ *
+ * This is the drop-in boundary for ONE hot path of madjam/copycat (Atomix 0.1.0 on Copycat 1.0.0-beta4):
+ * applying a batch of committed Raft log entries to many multiplexed resource state machines.
+ * In the reference that path is, per committed entry, on one state-machine thread:
+ *
+ *   Copycat apply loop [not vendored]
+ *     -> ResourceManager.operateResource           manager/src/main/java/io/atomix/manager/ResourceManager.java:56-72
+ *     -> ResourceManagerStateMachineExecutor.execute manager/.../ResourceManagerStateMachineExecutor.java:90-102
+ *     -> ResourceStateMachineExecutor.executeCommand resource/.../ResourceStateMachineExecutor.java:73-91
+ *     -> AtomicValueState / MapState / LockState / LeaderElectionState / MembershipGroupState methods
+ *
+ * The engine replaces that chain for a whole batch: the host encodes the batch into the SoA columns of
+ * cc_batch (one row per commit, in log order) and calls cc_apply_batch(); hand-written gfx950 kernels
+ * produce one (status, value) row per commit plus an event stream.
+ *
+ * Conventions
+ *  - Every call returns an int: CC_OK (0) or a negative CC_ERR_* code.  Per-commit failures (the Java
+ *    exceptions) never fail the call: they are reported in the commit's status byte.
+ *  - A handle is used from one host thread at a time (the reference applies on one thread too).
+ *  - Pointers named d_* are device (HBM) pointers; h_* are host pointers.  `stream` is a hipStream_t
+ *    passed as void* (NULL = the legacy default stream).  Device calls are stream-ordered and
+ *    asynchronous; results are final after cc_sync() or a sync on the caller's stream.
+ *  - No torch, no C++ types: plain C so that a JNI / Panama FFM / ctypes stub can bind it
+ *    (INTEGRATION.md shows the bindings).
+ */
+#ifndef COPYCAT_APPLY_H
+#define COPYCAT_APPLY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CC_ABI_VERSION 1
+
+/* ---- return codes ------------------------------------------------------------------------------ */
+#define CC_OK               0
+#define CC_ERR_INVALID     -1  /* bad argument / handle */
+#define CC_ERR_HIP         -2  /* HIP runtime error (message: cc_last_error) */
+#define CC_ERR_CAPACITY    -3  /* batch / resource / instance / table capacity exceeded */
+#define CC_ERR_UNSUPPORTED -4  /* an op or resource type this build does not run on the GPU */
+#define CC_ERR_STATE       -5  /* engine state corrupt (a device-side check failed) */
+
+/* ---- resource (state machine) types; ResourceManager.getResource instantiates one per key ----------
+ * ResourceManager.java:92 `commit.operation().type().newInstance()`                                    */
+#define CC_RES_NONE      0
+#define CC_RES_VALUE     1  /* AtomicValueState  atomic/.../state/AtomicValueState.java:32 (also DistributedAtomicLong) */
+#define CC_RES_MAP       2  /* MapState          collections/.../state/MapState.java:32 */
+#define CC_RES_LOCK      3  /* LockState         coordination/.../state/LockState.java:33 */
+#define CC_RES_ELECTION  4  /* LeaderElectionState coordination/.../state/LeaderElectionState.java:31 */
+#define CC_RES_GROUP     5  /* MembershipGroupState coordination/.../state/MembershipGroupState.java:33 */
+
+/* ---- op codes = Catalyst @SerializeWith ids of the inner operation ------------- */
+#define CC_OP_DELETE            1   /* ResourceStateMachine.DeleteCommand (no wire id) ResourceStateMachine.java:53 */
+/* AtomicValueCommands.java:93-260 */
+#define CC_OP_VALUE_GET        50   /* query */
+#define CC_OP_VALUE_SET        51
+#define CC_OP_VALUE_CAS        52   /* CompareAndSet(expect=a, update=b) */
+#define CC_OP_VALUE_GETANDSET  53
+#define CC_OP_VALUE_LISTEN     54
+#define CC_OP_VALUE_UNLISTEN   55
+/* MapCommands.java:134-450 */
+#define CC_OP_MAP_CONTAINSKEY   60  /* query */
+#define CC_OP_MAP_CONTAINSVALUE 61  /* query */
+#define CC_OP_MAP_PUT           62
+#define CC_OP_MAP_PUTIFABSENT   63
+#define CC_OP_MAP_GET           64  /* query */
+#define CC_OP_MAP_GETORDEFAULT  65  /* query */
+#define CC_OP_MAP_REMOVE        66
+#define CC_OP_MAP_REMOVEIFPRESENT 67
+#define CC_OP_MAP_REPLACE       68
+#define CC_OP_MAP_REPLACEIFPRESENT 69
+#define CC_OP_MAP_ISEMPTY       70  /* query */
+#define CC_OP_MAP_SIZE          71  /* query */
+#define CC_OP_MAP_CLEAR         72
+/* LeaderElectionCommands.java:80-99 */
+#define CC_OP_ELECT_LISTEN     110
+#define CC_OP_ELECT_UNLISTEN   111
+#define CC_OP_ELECT_ISLEADER   112  /* query */
+/* LockCommands.java:59-93 */
+#define CC_OP_LOCK_LOCK        115
+#define CC_OP_LOCK_UNLOCK      116
+/* MembershipGroupCommands.java:62-140 */
+#define CC_OP_GROUP_JOIN       120
+#define CC_OP_GROUP_LEAVE      121
+#define CC_OP_GROUP_SCHEDULE   122
+#define CC_OP_GROUP_EXECUTE    123
+
+/* ---- canonical tagged values: Java equals == (tag, payload) equality ---------- */
+#define CC_TAG_NULL    0
+#define CC_TAG_LONG    1   /* java.lang.Long, payload = two's complement i64 */
+#define CC_TAG_INT     2   /* java.lang.Integer, payload = sign-extended i32 */
+#define CC_TAG_BOOL    3   /* java.lang.Boolean, payload 0/1 */
+#define CC_TAG_HANDLE  4   /* host-interned object (String, Runnable callback ...) */
+#define CC_TAG_SET     5   /* result only: Set<Long> of MembershipGroupState.join; payload = member count,
+                              members are written to the aux-result stream */
+
+/* flags column: bits 0-2 tag(a), bits 3-5 tag(b), bits 6-7 key tag (keys are never null,
+ * KeyCommand asserts notNull MapCommands.java:77): 0 LONG, 1 INT, 2 BOOL, 3 HANDLE.               */
+#define CC_FLAGS(tag_a, tag_b, ktag) ((uint8_t)(((tag_a) & 7u) | (((tag_b) & 7u) << 3) | (((ktag) & 3u) << 6)))
+#define CC_FLAG_TAG_A(f) ((f) & 7u)
+#define CC_FLAG_TAG_B(f) (((f) >> 3) & 7u)
+#define CC_FLAG_KTAG(f)  (((f) >> 6) & 3u)
+
+/* ---- per-commit status (the Java exception class) ----------------------------------
+ * status byte = code | (result tag << 4)                                                          */
+#define CC_ST_OK               0
+#define CC_ST_UNKNOWN_SESSION  1  /* ResourceManagerException "unknown resource session" ResourceManager.java:65 */
+#define CC_ST_UNKNOWN_OP       2  /* IllegalStateException "unknown operation type" ResourceStateMachineExecutor.java:78 */
+#define CC_ST_ILLEGAL_STATE    3  /* IllegalStateException "not the lock holder" LockState.java:70 */
+#define CC_ST_ILLEGAL_ARGUMENT 4  /* IllegalArgumentException "unknown member" MembershipGroupState.java:89,112 */
+#define CC_ST_NULL_POINTER     5  /* NullPointerException in MapState.containsValue MapState.java:52 */
+#define CC_ST_TYPE_MISMATCH    6  /* ResourceManagerException "inconsistent resource type" ResourceManager.java:120,181 */
+#define CC_ST_UNKNOWN_RESOURCE 7  /* ResourceManagerException "unknown resource" ResourceManager.java:216 */
+#define CC_STATUS(code, tag)   ((uint8_t)(((code) & 15u) | (((tag) & 15u) << 4)))
+#define CC_STATUS_CODE(s)      ((s) & 15u)
+#define CC_STATUS_TAG(s)       (((s) >> 4) & 15u)
+
+/* ---- event codes: Session.publish(event, msg) -> InstanceEvent{instance, msg}
+ * ManagedResourceSession.java:64-71, InstanceEvent.java:29-80                                     */
+#define CC_EV_CHANGE   1  /* AtomicValueState.change  AtomicValueState.java:68-72 */
+#define CC_EV_LOCK     2  /* LockState "lock" true/false LockState.java:44,47,79 */
+#define CC_EV_ELECT    3  /* LeaderElectionState "elect"(epoch=leader index) LeaderElectionState.java:44,60,80 */
+#define CC_EV_JOIN     4  /* MembershipGroupState "join"(instance) :55 */
+#define CC_EV_LEAVE    5  /* MembershipGroupState "leave"(instance) :40,75 */
+#define CC_EV_EXECUTE  6  /* MembershipGroupState "execute"(callback) :95,115 */
+
+/* event source */
+#define CC_EVSRC_COMMIT 0  /* published while applying commit `pos` */
+#define CC_EVSRC_TIMER  1  /* published by a timer that fired at commit `pos` */
+#define CC_EVSRC_CLOSE  2  /* published by a session close/expire fan-out */
+
+/* ---- engine configuration ------------------------------------------------------------------------ */
+typedef struct cc_config {
+  uint32_t max_resources;   /* resource slots (ResourceManager.resources)                      */
+  uint32_t max_instances;   /* instance-session slots (ResourceManager.sessions)               */
+  uint64_t max_batch;       /* max commits per cc_apply_batch call                               */
+  uint64_t max_events;      /* capacity of the device event stream per batch                      */
+  uint64_t map_capacity;    /* total map entries across all CC_RES_MAP resources (0 = none)       */
+  int32_t  device;          /* HIP device ordinal                                                  */
+  uint32_t flags;           /* CC_CFG_* */
+  uint64_t sub_batch;       /* commits per internal sub-batch (0 = engine default; sized to keep the
+                               partition staging resident in the 256 MiB Infinity Cache)           */
+  uint64_t reserved[4];
+} cc_config;
+
+#define CC_CFG_TIMERS_DEFERRED 1u  /* manager-mode timer order (A8): due timers fire after the commit
+                                      that advanced time (ResourceManagerStateMachineExecutor.java:104-109) */
+
+/* ---- one batch of committed entries, SoA, log order ------------------------------------------------
+ * Row i is InstanceCommand/InstanceQuery{instance, op} of log entry index[i]
+ * (InstanceOperation.java:59-69; ResourceManagerCommit.index/time ResourceManagerCommit.java:54-66).
+ * Columns an op does not use may hold anything; pointers of columns no op in the batch uses may be NULL. */
+typedef struct cc_batch {
+  const uint64_t* index;  /* log index (Commit.index())                                         */
+  const uint64_t* time;   /* log time, ms (Commit.time()); drives TTL / timeout timers           */
+  const uint32_t* inst;   /* instance-session slot (InstanceOperation.resource -> sessions map)  */
+  const uint8_t*  op;     /* CC_OP_*                                                              */
+  const uint8_t*  flags;  /* CC_FLAGS(tag a, tag b, key tag)                                      */
+  const uint64_t* key;    /* map key / group member instance slot                                 */
+  const uint64_t* a;      /* value / expect / default-less operand                                */
+  const uint64_t* b;      /* update / replace / default operand                                   */
+  const uint64_t* aux;    /* ttl / lock timeout / schedule delay (signed i64)                     */
+} cc_batch;
+
+/* per-commit results (caller-allocated, n rows) */
+typedef struct cc_results {
+  uint8_t*  status;       /* CC_STATUS(code, result tag) */
+  uint64_t* value;        /* result payload                */
+} cc_results;
+
+/* event stream (caller-allocated, capacity rows); count written to *count (device u64) */
+typedef struct cc_events {
+  uint32_t* pos;          /* batch row that produced the event                          */
+  uint32_t* target;       /* instance slot whose session receives it                    */
+  uint8_t*  code;         /* CC_EV_*                                                     */
+  uint8_t*  src;          /* CC_EVSRC_*                                                  */
+  uint8_t*  tag;          /* payload tag                                                 */
+  uint64_t* payload;
+  uint64_t  capacity;
+  uint64_t* count;        /* device pointer: number of events written (may exceed capacity:
+                             then the call returns CC_ERR_CAPACITY on sync)                */
+} cc_events;
+
+typedef struct cc_engine cc_engine;
+
+/* ---- lifecycle ------------------------------------------------------------------------------------ */
+int  cc_abi_version(void);
+const char* cc_last_error(void);
+/* ResourceManager constructor + StateMachine.configure (ResourceManager.java:35-50) */
+int  cc_engine_create(const cc_config* cfg, cc_engine** out);
+int  cc_engine_destroy(cc_engine* e);
+int  cc_sync(cc_engine* e);
+/* The engine's stream (hipStream_t as void*). */
+void* cc_engine_stream(cc_engine* e);
+
+/* ---- resource and instance registry (host-side control commands) --------------------------------
+ * New resource: ResourceManager.getResource/createResource new-key branch (ResourceManager.java:84-100,157-176);
+ * the engine allocates state for `slot` (chosen by the host: resource id -> dense slot).       */
+int  cc_resource_create(cc_engine* e, uint32_t slot, uint32_t type);
+/* Bulk form: slots [first, first+count) all of `type`.  A 64-slot bucket (slot/64) holds one type. */
+int  cc_resource_create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type);
+/* ResourceManager.deleteResource (ResourceManager.java:212-235): delete() state, cancel timers,
+ * and close every instance slot registered to the resource.                                   */
+int  cc_resource_delete(cc_engine* e, uint32_t slot);
+/* A ManagedResourceSession (ResourceManager.java:103-106,128-131,189-190): instance slot -> resource slot,
+ * owned by client session `client_session`; `instance_id` is the Java instance id (= creating commit index). */
+int  cc_instance_open(cc_engine* e, uint32_t inst, uint32_t res_slot, uint64_t instance_id, uint64_t client_session);
+/* Bulk form: instance slot first+k -> resource slot res_first+k, instance id id_first+k, one client session. */
+int  cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint64_t id_first,
+                            uint64_t client_session);
+
+/* ---- the hot path --------------------------------------------------------------------------------
+ * Apply n committed entries (device-resident columns) in log order.  Replaces the per-entry chain
+ * ResourceManager.operateResource (ResourceManager.java:56-72) -> executors -> state machine method.
+ * `events` may be NULL when no op in the batch publishes (then publishing ops fail with CC_ERR_UNSUPPORTED). */
+int  cc_apply_batch(cc_engine* e, const cc_batch* d_cols, uint64_t n, const cc_results* d_out,
+                    const cc_events* d_events, void* stream);
+/* Same with host columns/results: H2D, apply, D2H, sync (PCIe-inclusive path). */
+int  cc_apply_batch_host(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out);
+/* Highest log index applied so far (the applied watermark; all-gathered across GPUs by the host). */
+int  cc_applied_index(cc_engine* e, uint64_t* out);
+
+/* ---- state readback for parity checks ------------------------------------------------------------ */
+/* AtomicValueState {value, current != null} for slots [first, first+count) (AtomicValueState.java:34-35) */
+int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* h_tag, uint64_t* h_value,
+                         uint8_t* h_has_current);
+
+/* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
+ * kernel ids: 0 k_part_count, 1 k_part_scan, 2 k_part_base, 3 k_part_scatter, 4 k_apply_value.           */
+#define CC_PROFILE_KERNELS 5
+int  cc_profile_enable(cc_engine* e, int on);
+int  cc_profile_reset(cc_engine* e);
+/* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */
+int  cc_profile_read(cc_engine* e, int kernel, double* total_ms, uint64_t* launches, const char** name);
+
+/* ---- leader quorum commit index (Copycat leader [not vendored]) ------------------------
+ * Per group g: N = the quorum-th largest of d_match[r*groups + g], r < replicas (r = 0 is the leader's
+ * last log index), quorum = replicas/2 + 1; new = (N >= d_term_start[g] && N > d_commit_in[g]) ? N : d_commit_in[g]. */
+int  cc_quorum_commit(const uint64_t* d_match, uint32_t replicas, uint64_t groups, const uint64_t* d_term_start,
+                      const uint64_t* d_commit_in, uint64_t* d_commit_out, void* stream);
+
+/* ---- session / lease expiry sweep (Copycat sessions [not vendored]) ---------------------
+ * Session s is expired iff now - d_last[s] > timeout (signed difference; a keep-alive in the future never
+ * expires).  Bit s of d_bitmap (u64 words, LSB first) is set for expired sessions; *d_count (u64) += expired. */
+int  cc_expire_sweep(const uint64_t* d_last, uint64_t sessions, uint64_t now, uint64_t timeout,
+                     uint64_t* d_bitmap, uint64_t* d_count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COPYCAT_APPLY_H */

@@ -1,0 +1,991 @@
+// oracle.cpp — CPU restatement of the reference commit-apply path.  TEST INFRASTRUCTURE ONLY (see oracle.h).
+//
+// Every state-machine method below cites the Java method it restates (paths relative to the reference
+// root).  Values are canonical tagged values (tag, payload): Java `equals` on boxed values becomes exact
+// (tag, payload) equality.  Commit objects are represented by their log index
+// and instance slot; `commit.clean()` matters only where the reference can clean one twice (the
+// ResourceManagerCommit assert `Assert.state(open, "commit closed")`, ResourceManagerCommit.java:79-83).
+#include "oracle.h"
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace {
+
+struct TV {
+  uint8_t tag = CC_TAG_NULL;
+  uint64_t v = 0;
+};
+inline bool tv_null(const TV& x) { return x.tag == CC_TAG_NULL; }
+// x.equals(y) for a non-null receiver x (Long/Integer/Boolean.equals are type-sensitive, A15).
+inline bool tv_equals(const TV& x, const TV& y) { return x.tag == y.tag && x.v == y.v; }
+inline TV tv(uint8_t tag, uint64_t v) { TV t; t.tag = tag; t.v = tag == CC_TAG_NULL ? 0 : v; return t; }
+
+// Key tags in the flags column map to value tags (keys are never null: MapCommands.java:77).
+inline uint8_t ktag_to_tag(uint8_t k) {
+  static const uint8_t m[4] = {CC_TAG_LONG, CC_TAG_INT, CC_TAG_BOOL, CC_TAG_HANDLE};
+  return m[k & 3];
+}
+
+// ---- java.util.HashMap iteration order (for outputs that depend on it) -----------------------------
+// Order = (bucket index under the current table capacity, insertion order within the bucket).  The
+// table starts at 16, doubles when ++size > 0.75*cap (HashMap.putVal/resize), never shrinks; a resize
+// splits each bucket preserving relative order; re-putting an existing key keeps its node.  Tree bins
+// (>= 8 colliding keys) are not modelled.  hashCode: Long (int)(v^(v>>>32)); Integer v; Boolean
+// 1231/1237; HANDLE keys use the Long formula on the handle (documented assumption).
+inline uint32_t java_hash(uint8_t tag, uint64_t v) {
+  int32_t h;
+  switch (tag) {
+    case CC_TAG_INT: h = (int32_t)(uint32_t)v; break;
+    case CC_TAG_BOOL: h = v ? 1231 : 1237; break;
+    default: h = (int32_t)(uint32_t)(v ^ (v >> 32)); break;
+  }
+  uint32_t u = (uint32_t)h;
+  return u ^ (u >> 16);
+}
+struct JavaOrder {
+  uint32_t cap = 16, thr = 12, size = 0;
+  uint64_t next_seq = 0;
+  uint64_t on_insert() {  // a NEW key
+    uint64_t s = next_seq++;
+    if (++size > thr) { cap <<= 1; thr <<= 1; }
+    return s;
+  }
+  void on_remove() { --size; }
+  uint64_t order_key(uint32_t hash, uint64_t seq) const { return ((uint64_t)(hash & (cap - 1)) << 40) | seq; }
+};
+
+struct Commit {  // a retained commit: index + instance-session slot
+  uint64_t index = 0;
+  uint32_t inst = 0;
+  bool cleaned = false;
+};
+
+// AtomicValueState.java:32-36
+struct ValueSM {
+  TV value;
+  bool has_current = false;
+  Commit current;
+  std::vector<std::pair<uint32_t, uint64_t>> listeners;  // (instance slot, listen index); insertion order
+};
+
+struct MapKey {
+  uint8_t tag;
+  uint64_t k;
+  bool operator==(const MapKey& o) const { return tag == o.tag && k == o.k; }
+};
+struct MapKeyHash {
+  size_t operator()(const MapKey& x) const { return (size_t)(x.k * 0x9E3779B97F4A7C15ull) ^ x.tag; }
+};
+// MapState.Value{commit, timer} MapState.java:279-287
+struct MapEntry {
+  TV value;
+  uint64_t commit_index = 0;
+  uint64_t timer = 0;  // 0 = none
+  uint64_t seq = 0;    // Java HashMap insertion order
+};
+struct MapSM {
+  std::unordered_map<MapKey, MapEntry, MapKeyHash> m;
+  JavaOrder order;
+};
+
+// LockState.java:33-36
+struct LockSM {
+  bool held = false;
+  Commit lock;
+  std::deque<Commit> queue;
+  std::unordered_map<uint64_t, uint64_t> timers;  // commit index -> timer id
+};
+
+// LeaderElectionState.java:31-33 (LinkedHashMap<Long, Commit> = insertion-ordered vector)
+struct ElectionSM {
+  bool has_leader = false;
+  Commit leader;
+  std::vector<std::pair<uint64_t, Commit>> listeners;  // (instance id, listen commit)
+};
+
+// MembershipGroupState.java:33-34 (HashMap<Long, Commit>)
+struct GroupSM {
+  std::unordered_map<uint64_t, Commit> members;  // instance id -> join commit
+};
+
+struct Resource {
+  bool exists = false;
+  uint32_t type = CC_RES_NONE;
+  uint64_t id = 0;   // resource id (= creating commit index under the manager)
+  uint64_t key = 0;  // interned key handle
+  bool has_key = false;
+  std::unordered_map<uint64_t, uint64_t> sessions;  // ResourceHolder.sessions: client session -> instance id
+  ValueSM v;
+  MapSM m;
+  LockSM l;
+  ElectionSM e;
+  GroupSM g;
+};
+
+struct Inst {  // ResourceManager.SessionHolder + ManagedResourceSession
+  bool open = false;
+  uint32_t res = 0;
+  uint64_t id = 0;      // instance id (ManagedResourceSession.id())
+  uint64_t client = 0;  // parent client session id
+};
+
+enum TimerKind : uint8_t { T_MAP_TTL = 1, T_MAP_REPLACE_TTL = 2, T_LOCK_TIMEOUT = 3, T_GROUP_SCHEDULE = 4 };
+struct Timer {
+  uint64_t id = 0, deadline = 0;
+  uint32_t res = 0;
+  uint8_t kind = 0;
+  MapKey key{0, 0};
+  uint64_t commit_index = 0;
+  uint64_t member = 0;
+  TV callback;
+};
+
+struct Event {
+  uint32_t pos, target;
+  uint8_t code, src, tag;
+  uint64_t payload;
+};
+
+}  // namespace
+
+struct orc {
+  uint32_t max_res, max_inst, flags;
+  std::vector<Resource> res;
+  std::vector<Inst> inst;
+  std::unordered_map<uint64_t, uint32_t> inst_by_id;  // ResourceManager.sessions key -> slot
+  JavaOrder sessions_order;                            // HashMap order of ResourceManager.sessions
+  std::unordered_map<uint64_t, uint64_t> inst_seq;     // instance id -> insertion seq
+  std::unordered_map<uint64_t, uint64_t> keys;         // ResourceManager.keys: key -> resource id
+  std::unordered_map<uint64_t, uint32_t> res_by_id;    // ResourceManager.resources: id -> slot
+  std::map<std::pair<uint64_t, uint64_t>, Timer> timers;  // (deadline, id) -> timer
+  std::unordered_map<uint64_t, uint64_t> timer_deadline;  // id -> deadline
+  uint64_t next_timer = 1;
+  uint64_t clock = 0;
+  uint64_t applied = 0;
+  std::vector<Event> events;
+  std::vector<std::pair<uint32_t, uint64_t>> aux;
+  uint32_t cur_pos = 0;
+  uint8_t cur_src = CC_EVSRC_COMMIT;
+
+  void publish(uint32_t target, uint8_t code, TV payload) {
+    events.push_back(Event{cur_pos, target, code, cur_src, payload.tag, payload.v});
+  }
+
+  // ---- timers: deterministic executor clock (Copycat ServerStateMachineExecutor, not vendored) ------
+  uint64_t schedule(uint64_t delay, Timer t) {
+    t.id = next_timer++;
+    t.deadline = clock + delay;
+    timers.emplace(std::make_pair(t.deadline, t.id), t);
+    timer_deadline[t.id] = t.deadline;
+    return t.id;
+  }
+  void cancel(uint64_t id) {
+    auto it = timer_deadline.find(id);
+    if (it == timer_deadline.end()) return;
+    timers.erase(std::make_pair(it->second, id));
+    timer_deadline.erase(it);
+  }
+  void fire_due() {
+    uint8_t saved = cur_src;
+    cur_src = CC_EVSRC_TIMER;
+    while (!timers.empty() && timers.begin()->first.first <= clock) {
+      Timer t = timers.begin()->second;
+      timers.erase(timers.begin());
+      timer_deadline.erase(t.id);
+      run_timer(t);
+    }
+    cur_src = saved;
+  }
+  void run_timer(const Timer& t) {
+    Resource& r = res[t.res];
+    if (!r.exists) return;
+    switch (t.kind) {
+      case T_MAP_TTL:          // MapState.java:91-93,119-121,218-220: map.remove(key).commit.clean()
+      case T_MAP_REPLACE_TTL: {  // MapState.java:189-192: map.remove(key); commit.clean()
+        auto it = r.m.m.find(t.key);
+        if (it != r.m.m.end()) { r.m.m.erase(it); r.m.order.on_remove(); }
+        break;
+      }
+      case T_LOCK_TIMEOUT: {   // LockState.java:54-58 (silent, A7)
+        r.l.timers.erase(t.commit_index);
+        for (auto it = r.l.queue.begin(); it != r.l.queue.end(); ++it)
+          if (it->index == t.commit_index) { r.l.queue.erase(it); break; }
+        break;
+      }
+      case T_GROUP_SCHEDULE: {  // MembershipGroupState.java:92-98
+        auto it = r.g.members.find(t.member);
+        if (it != r.g.members.end()) publish(it->second.inst, CC_EV_EXECUTE, t.callback);
+        break;
+      }
+    }
+  }
+  void cancel_resource_timers(uint32_t slot) {  // ResourceManagerStateMachineExecutor.close :137-140
+    std::vector<uint64_t> ids;
+    for (auto& kv : timers) if (kv.second.res == slot) ids.push_back(kv.second.id);
+    for (uint64_t id : ids) cancel(id);
+  }
+
+  // ---- registry ------------------------------------------------------------------------------------
+  void register_instance(uint32_t slot, uint32_t rslot, uint64_t id, uint64_t client) {
+    Inst& in = inst[slot];
+    in.open = true; in.res = rslot; in.id = id; in.client = client;
+    inst_by_id[id] = slot;
+    inst_seq[id] = sessions_order.on_insert();
+  }
+  void unregister_instance(uint32_t slot) {
+    Inst& in = inst[slot];
+    if (!in.open) return;
+    in.open = false;
+    inst_by_id.erase(in.id);
+    inst_seq.erase(in.id);
+    sessions_order.on_remove();
+  }
+  int alloc_res_slot() {
+    for (uint32_t s = 0; s < max_res; ++s) if (!res[s].exists) return (int)s;
+    return -1;
+  }
+  int alloc_inst_slot() {
+    for (uint32_t s = 0; s < max_inst; ++s) if (!inst[s].open) return (int)s;
+    return -1;
+  }
+  void init_resource(uint32_t slot, uint32_t type, uint64_t id) {
+    Resource fresh;
+    res[slot] = std::move(fresh);
+    res[slot].exists = true;
+    res[slot].type = type;
+    res[slot].id = id;
+    res_by_id[id] = slot;
+  }
+
+  // ---- state machine delete() overrides ----------------------------------------------------------------
+  // returns a status code (the reference can throw "commit closed" from a double clean)
+  uint8_t sm_delete(uint32_t slot) {
+    Resource& r = res[slot];
+    switch (r.type) {
+      case CC_RES_VALUE:  // AtomicValueState.delete :146-157 (timer is always null, A2)
+        if (r.v.has_current) { r.v.has_current = false; r.v.value = TV(); }
+        return CC_ST_OK;
+      case CC_RES_MAP: {  // MapState.delete :264-274
+        for (auto& kv : r.m.m) if (kv.second.timer) cancel(kv.second.timer);
+        for (size_t i = 0; i < r.m.m.size(); ++i) r.m.order.on_remove();
+        r.m.m.clear();
+        return CC_ST_OK;
+      }
+      case CC_RES_LOCK: {  // LockState.delete :87-98 — `lock` is cleaned but NOT nulled
+        uint8_t st = CC_ST_OK;
+        if (r.l.held) {
+          if (r.l.lock.cleaned) return CC_ST_ILLEGAL_STATE;  // ResourceManagerCommit.clean: "commit closed"
+          r.l.lock.cleaned = true;
+        }
+        r.l.queue.clear();
+        for (auto& kv : r.l.timers) cancel(kv.second);
+        r.l.timers.clear();
+        return st;
+      }
+      case CC_RES_ELECTION: {  // LeaderElectionState.delete :100-108 — `leader` cleaned, NOT nulled
+        if (r.e.has_leader) {
+          if (r.e.leader.cleaned) return CC_ST_ILLEGAL_STATE;
+          r.e.leader.cleaned = true;
+        }
+        r.e.listeners.clear();
+        return CC_ST_OK;
+      }
+      case CC_RES_GROUP:  // MembershipGroupState.delete :121-125
+        r.g.members.clear();
+        return CC_ST_OK;
+    }
+    return CC_ST_OK;
+  }
+
+  // ---- StateMachine.close(Session) overrides (ResourceManager.close fan-out) ---------------------------
+  // returns false if the close threw (aborts the ResourceManager.close loop; unpinned)
+  bool sm_close(uint32_t islot) {
+    Inst& in = inst[islot];
+    Resource& r = res[in.res];
+    switch (r.type) {
+      case CC_RES_VALUE: {  // AtomicValueState.listen onClose hook :43-48 (parent session closed)
+        auto& L = r.v.listeners;
+        L.erase(std::remove_if(L.begin(), L.end(), [&](const std::pair<uint32_t, uint64_t>& p) { return p.first == islot; }),
+                L.end());
+        return true;
+      }
+      case CC_RES_ELECTION: {  // LeaderElectionState.close :35-52
+        ElectionSM& e = r.e;
+        if (e.has_leader && e.leader.inst == islot) {
+          if (e.leader.cleaned) return false;  // leader.clean() throws "commit closed"
+          e.has_leader = false;
+          if (!e.listeners.empty()) {
+            e.leader = e.listeners.front().second;
+            e.has_leader = true;
+            e.listeners.erase(e.listeners.begin());
+            publish(e.leader.inst, CC_EV_ELECT, tv(CC_TAG_LONG, e.leader.index));
+          }
+        } else {
+          for (auto it = e.listeners.begin(); it != e.listeners.end(); ++it)
+            if (it->first == in.id) { e.listeners.erase(it); break; }
+        }
+        return true;
+      }
+      case CC_RES_GROUP: {  // MembershipGroupState.close :36-42 — publishes leave even for non-members (A10)
+        r.g.members.erase(in.id);
+        for (auto& kv : r.g.members) publish(kv.second.inst, CC_EV_LEAVE, tv(CC_TAG_LONG, in.id));
+        return true;
+      }
+      default:
+        return true;  // MapState / LockState have no close handler (A11)
+    }
+  }
+
+  // ---- one commit ------------------------------------------------------------------------------------
+  struct Row {
+    uint64_t index, time, key, a, b, aux;
+    uint32_t inst;
+    uint8_t op, flags;
+  };
+
+  // ResourceManager.operateResource :56-72 -> executors :90-102 / :73-91 -> state machine method
+  void apply_one(const Row& c, uint8_t& status, uint64_t& value) {
+    status = CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+    value = 0;
+    if (c.inst >= max_inst || !inst[c.inst].open) {  // sessions.get(instanceId) == null
+      status = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
+      return;
+    }
+    const Inst& in = inst[c.inst];
+    Resource& r = res[in.res];
+    if (!r.exists) {  // holder left behind by a failed deleteResource: resource.executor NPE (:71)
+      status = CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
+      return;
+    }
+    TV a = tv(CC_FLAG_TAG_A(c.flags), c.a);
+    TV b = tv(CC_FLAG_TAG_B(c.flags), c.b);
+    auto ret = [&](uint8_t code, TV v) { status = CC_STATUS(code, v.tag); value = v.v; };
+
+    if (c.op == CC_OP_DELETE) {  // ResourceStateMachine.init DeleteCommand :34-40
+      ret(sm_delete(in.res), TV());
+      return;
+    }
+    switch (r.type) {
+      case CC_RES_VALUE: {
+        ValueSM& s = r.v;
+        switch (c.op) {
+          case CC_OP_VALUE_GET:  // AtomicValueState.get :77-83
+            ret(CC_ST_OK, s.has_current ? s.value : TV());
+            return;
+          case CC_OP_VALUE_SET:  // set :114-118 (cleanCurrent; value = v; setCurrent)
+            s.value = a;
+            s.has_current = true;
+            s.current = Commit{c.index, c.inst, false};
+            value_change(s);
+            ret(CC_ST_OK, TV());
+            return;
+          case CC_OP_VALUE_CAS: {  // compareAndSet :123-133
+            bool eq = (tv_null(s.value) && tv_null(a)) || (!tv_null(s.value) && !tv_null(a) && tv_equals(s.value, a));
+            if (eq) {
+              s.value = b;
+              s.has_current = true;
+              s.current = Commit{c.index, c.inst, false};
+              value_change(s);
+            }
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, eq ? 1 : 0));
+            return;
+          }
+          case CC_OP_VALUE_GETANDSET: {  // getAndSet :138-144
+            TV prev = s.value;
+            s.value = a;
+            s.has_current = true;
+            s.current = Commit{c.index, c.inst, false};
+            value_change(s);
+            ret(CC_ST_OK, prev);
+            return;
+          }
+          case CC_OP_VALUE_LISTEN: {  // listen :41-49 (listeners.put(session, commit))
+            bool found = false;
+            for (auto& p : s.listeners) if (p.first == c.inst) { p.second = c.index; found = true; }
+            if (!found) s.listeners.emplace_back(c.inst, c.index);
+            ret(CC_ST_OK, TV());
+            return;
+          }
+          case CC_OP_VALUE_UNLISTEN: {  // unlisten :54-63
+            for (auto it = s.listeners.begin(); it != s.listeners.end(); ++it)
+              if (it->first == c.inst) { s.listeners.erase(it); break; }
+            ret(CC_ST_OK, TV());
+            return;
+          }
+        }
+        break;
+      }
+      case CC_RES_MAP: {
+        MapSM& s = r.m;
+        MapKey k{ktag_to_tag(CC_FLAG_KTAG(c.flags)), c.key};
+        int64_t ttl = (int64_t)c.aux;
+        switch (c.op) {
+          case CC_OP_MAP_CONTAINSKEY:  // containsKey :38-44
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, s.m.count(k) ? 1 : 0));
+            return;
+          case CC_OP_MAP_CONTAINSVALUE: {  // containsValue :49-60 — iterates in HashMap order; a stored
+            // null value NPEs on `.equals` before a later match is reached (A5).
+            std::vector<std::pair<uint64_t, const MapEntry*>> ord;
+            ord.reserve(s.m.size());
+            for (auto& kv : s.m)
+              ord.emplace_back(s.order.order_key(java_hash(kv.first.tag, kv.first.k), kv.second.seq), &kv.second);
+            std::sort(ord.begin(), ord.end(), [](const std::pair<uint64_t, const MapEntry*>& x,
+                                                 const std::pair<uint64_t, const MapEntry*>& y) { return x.first < y.first; });
+            for (auto& p : ord) {
+              if (tv_null(p.second->value)) { ret(CC_ST_NULL_POINTER, TV()); return; }
+              if (tv_equals(p.second->value, a)) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 1)); return; }
+            }
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
+            return;
+          }
+          case CC_OP_MAP_GET: {  // get :65-72 (a key mapped to null is present, A6)
+            auto it = s.m.find(k);
+            ret(CC_ST_OK, it != s.m.end() ? it->second.value : TV());
+            return;
+          }
+          case CC_OP_MAP_GETORDEFAULT: {  // getOrDefault :77-84 (default = operand a)
+            auto it = s.m.find(k);
+            ret(CC_ST_OK, it != s.m.end() ? it->second.value : a);
+            return;
+          }
+          case CC_OP_MAP_PUT: {  // put :89-110
+            uint64_t timer = 0;
+            if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
+            auto it = s.m.find(k);
+            if (it != s.m.end()) {
+              if (it->second.timer) cancel(it->second.timer);
+              TV prev = it->second.value;
+              it->second.value = a; it->second.commit_index = c.index; it->second.timer = timer;
+              ret(CC_ST_OK, prev);
+            } else {
+              MapEntry e; e.value = a; e.commit_index = c.index; e.timer = timer; e.seq = s.order.on_insert();
+              s.m.emplace(k, e);
+              ret(CC_ST_OK, TV());
+            }
+            return;
+          }
+          case CC_OP_MAP_PUTIFABSENT: {  // putIfAbsent :115-133
+            auto it = s.m.find(k);
+            if (it == s.m.end()) {
+              uint64_t timer = 0;
+              if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
+              MapEntry e; e.value = a; e.commit_index = c.index; e.timer = timer; e.seq = s.order.on_insert();
+              s.m.emplace(k, e);
+              ret(CC_ST_OK, TV());
+            } else {
+              ret(CC_ST_OK, it->second.value);
+            }
+            return;
+          }
+          case CC_OP_MAP_REMOVE: {  // remove :138-154
+            auto it = s.m.find(k);
+            if (it != s.m.end()) {
+              if (it->second.timer) cancel(it->second.timer);
+              TV prev = it->second.value;
+              s.m.erase(it); s.order.on_remove();
+              ret(CC_ST_OK, prev);
+            } else {
+              ret(CC_ST_OK, TV());
+            }
+            return;
+          }
+          case CC_OP_MAP_REMOVEIFPRESENT: {  // removeIfPresent :159-178
+            auto it = s.m.find(k);
+            bool fail = it == s.m.end() || (tv_null(it->second.value) && !tv_null(a)) ||
+                        (!tv_null(it->second.value) && !tv_equals(it->second.value, a));
+            if (fail) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 0)); return; }
+            if (it->second.timer) cancel(it->second.timer);
+            s.m.erase(it); s.order.on_remove();
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, 1));
+            return;
+          }
+          case CC_OP_MAP_REPLACE: {  // replace :183-202
+            auto it = s.m.find(k);
+            if (it != s.m.end()) {
+              if (it->second.timer) cancel(it->second.timer);
+              uint64_t timer = 0;
+              if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_REPLACE_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
+              TV prev = it->second.value;
+              it->second.value = a; it->second.commit_index = c.index; it->second.timer = timer;
+              ret(CC_ST_OK, prev);
+            } else {
+              ret(CC_ST_OK, TV());
+            }
+            return;
+          }
+          case CC_OP_MAP_REPLACEIFPRESENT: {  // replaceIfPresent :207-228 (stores `value`=a, compares `replace`=b, A1)
+            auto it = s.m.find(k);
+            if (it == s.m.end()) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 0)); return; }
+            const TV& cur = it->second.value;
+            bool ok = (tv_null(cur) && tv_null(b)) || (!tv_null(cur) && tv_equals(cur, b));
+            if (ok) {
+              if (it->second.timer) cancel(it->second.timer);
+              uint64_t timer = 0;
+              if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
+              it->second.value = a; it->second.commit_index = c.index; it->second.timer = timer;
+              ret(CC_ST_OK, tv(CC_TAG_BOOL, 1));
+            } else {
+              ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
+            }
+            return;
+          }
+          case CC_OP_MAP_ISEMPTY:  // isEmpty :244-250
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, s.m.empty() ? 1 : 0));
+            return;
+          case CC_OP_MAP_SIZE:  // size :233-239 (int)
+            ret(CC_ST_OK, tv(CC_TAG_INT, (uint64_t)(int64_t)(int32_t)s.m.size()));
+            return;
+          case CC_OP_MAP_CLEAR:  // clear :255-261 -> delete()
+            sm_delete(in.res);
+            ret(CC_ST_OK, TV());
+            return;
+        }
+        break;
+      }
+      case CC_RES_LOCK: {
+        LockSM& s = r.l;
+        switch (c.op) {
+          case CC_OP_LOCK_LOCK: {  // LockState.lock :41-61 (timeout: -1 forever, 0 try, >0 ms)
+            int64_t timeout = (int64_t)c.aux;
+            if (!s.held) {
+              s.held = true;
+              s.lock = Commit{c.index, c.inst, false};
+              publish(c.inst, CC_EV_LOCK, tv(CC_TAG_BOOL, 1));
+            } else if (timeout == 0) {
+              publish(c.inst, CC_EV_LOCK, tv(CC_TAG_BOOL, 0));
+            } else {
+              s.queue.push_back(Commit{c.index, c.inst, false});
+              if (timeout > 0) {
+                Timer t; t.res = in.res; t.kind = T_LOCK_TIMEOUT; t.commit_index = c.index;
+                s.timers[c.index] = schedule((uint64_t)timeout, t);
+              }
+            }
+            ret(CC_ST_OK, TV());
+            return;
+          }
+          case CC_OP_LOCK_UNLOCK: {  // LockState.unlock :66-85
+            if (s.held) {
+              if (s.lock.inst != c.inst) { ret(CC_ST_ILLEGAL_STATE, TV()); return; }  // "not the lock holder"
+              if (s.lock.cleaned) { ret(CC_ST_ILLEGAL_STATE, TV()); return; }        // "commit closed" (after delete)
+              if (s.queue.empty()) {
+                s.held = false;
+              } else {
+                s.lock = s.queue.front();
+                s.queue.pop_front();
+                auto t = s.timers.find(s.lock.index);
+                if (t != s.timers.end()) { cancel(t->second); s.timers.erase(t); }
+                publish(s.lock.inst, CC_EV_LOCK, tv(CC_TAG_BOOL, 1));
+              }
+            }
+            ret(CC_ST_OK, TV());
+            return;
+          }
+        }
+        break;
+      }
+      case CC_RES_ELECTION: {
+        ElectionSM& s = r.e;
+        switch (c.op) {
+          case CC_OP_ELECT_LISTEN: {  // listen :57-66
+            if (!s.has_leader) {
+              s.has_leader = true;
+              s.leader = Commit{c.index, c.inst, false};
+              publish(c.inst, CC_EV_ELECT, tv(CC_TAG_LONG, c.index));
+            } else {
+              bool found = false;
+              for (auto& p : s.listeners) if (p.first == in.id) { found = true; break; }
+              if (!found) s.listeners.emplace_back(in.id, Commit{c.index, c.inst, false});  // may be the leader's own session (A9)
+            }
+            ret(CC_ST_OK, TV());
+            return;
+          }
+          case CC_OP_ELECT_UNLISTEN: {  // unlisten :71-91
+            if (s.has_leader && s.leader.inst == c.inst) {
+              if (s.leader.cleaned) { ret(CC_ST_ILLEGAL_STATE, TV()); return; }  // "commit closed"
+              s.has_leader = false;
+              if (!s.listeners.empty()) {
+                s.leader = s.listeners.front().second;
+                s.has_leader = true;
+                s.listeners.erase(s.listeners.begin());
+                publish(s.leader.inst, CC_EV_ELECT, tv(CC_TAG_LONG, s.leader.index));
+              }
+            } else {
+              for (auto it = s.listeners.begin(); it != s.listeners.end(); ++it)
+                if (it->first == in.id) { s.listeners.erase(it); break; }
+            }
+            ret(CC_ST_OK, TV());
+            return;
+          }
+          case CC_OP_ELECT_ISLEADER: {  // isLeader :96-98 — epoch is not serialized, so 0 (A3)
+            bool r2 = s.has_leader && s.leader.inst == c.inst && s.leader.index == 0;
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, r2 ? 1 : 0));
+            return;
+          }
+        }
+        break;
+      }
+      case CC_RES_GROUP: {
+        GroupSM& s = r.g;
+        switch (c.op) {
+          case CC_OP_GROUP_JOIN: {  // join :47-64
+            uint64_t sid = in.id;
+            auto it = s.members.find(sid);
+            if (it != s.members.end()) {
+              it->second = Commit{c.index, c.inst, false};  // previous.clean()
+            } else {
+              s.members.emplace(sid, Commit{c.index, c.inst, false});
+              for (auto& kv : s.members)
+                if (kv.second.index != c.index) publish(kv.second.inst, CC_EV_JOIN, tv(CC_TAG_LONG, sid));
+            }
+            std::vector<uint64_t> ids;
+            ids.reserve(s.members.size());
+            for (auto& kv : s.members) ids.push_back(kv.first);
+            std::sort(ids.begin(), ids.end());
+            for (uint64_t id : ids) aux.emplace_back(cur_pos, id);
+            ret(CC_ST_OK, tv(CC_TAG_SET, ids.size()));
+            return;
+          }
+          case CC_OP_GROUP_LEAVE: {  // leave :69-81
+            uint64_t sid = in.id;
+            auto it = s.members.find(sid);
+            if (it != s.members.end()) {
+              s.members.erase(it);
+              for (auto& kv : s.members) publish(kv.second.inst, CC_EV_LEAVE, tv(CC_TAG_LONG, sid));
+            }
+            ret(CC_ST_OK, TV());
+            return;
+          }
+          case CC_OP_GROUP_SCHEDULE: {  // schedule :86-103 (member = key, callback = a, delay = aux)
+            if (!s.members.count(c.key)) { ret(CC_ST_ILLEGAL_ARGUMENT, TV()); return; }
+            Timer t; t.res = in.res; t.kind = T_GROUP_SCHEDULE; t.member = c.key; t.callback = a; t.commit_index = c.index;
+            int64_t delay = (int64_t)c.aux;
+            schedule(delay > 0 ? (uint64_t)delay : 0, t);
+            ret(CC_ST_OK, TV());
+            return;
+          }
+          case CC_OP_GROUP_EXECUTE: {  // execute :108-119
+            auto it = s.members.find(c.key);
+            if (it == s.members.end()) { ret(CC_ST_ILLEGAL_ARGUMENT, TV()); return; }
+            publish(it->second.inst, CC_EV_EXECUTE, a);
+            ret(CC_ST_OK, TV());
+            return;
+          }
+        }
+        break;
+      }
+    }
+    // ResourceStateMachineExecutor.executeCommand :78 / ResourceManagerStateMachineExecutor.execute :96
+    ret(CC_ST_UNKNOWN_OP, TV());
+  }
+
+  // AtomicValueState.change :68-72 (HashMap<Session> order is identity-hash based: compare per target)
+  void value_change(ValueSM& s) {
+    for (auto& p : s.listeners) publish(p.first, CC_EV_CHANGE, s.value);
+  }
+};
+
+extern "C" {
+
+orc* orc_create(uint32_t max_resources, uint32_t max_instances, uint32_t flags) {
+  orc* o = new orc();
+  o->max_res = max_resources;
+  o->max_inst = max_instances;
+  o->flags = flags;
+  o->res.resize(max_resources);
+  o->inst.resize(max_instances);
+  return o;
+}
+void orc_destroy(orc* o) { delete o; }
+
+int orc_resource_create(orc* o, uint32_t slot, uint32_t type) {
+  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_GROUP || o->res[slot].exists) return CC_ERR_INVALID;
+  o->init_resource(slot, type, slot);
+  return CC_OK;
+}
+
+int orc_resource_delete(orc* o, uint32_t slot) {
+  if (!o || slot >= o->max_res || !o->res[slot].exists) return CC_ERR_INVALID;
+  uint8_t st;
+  uint64_t id = o->res[slot].id;
+  return orc_delete_resource(o, id, &st) == CC_OK && CC_STATUS_CODE(st) == CC_ST_OK ? CC_OK : CC_ERR_INVALID;
+}
+
+int orc_instance_open(orc* o, uint32_t inst, uint32_t res, uint64_t instance_id, uint64_t client_session) {
+  if (!o || inst >= o->max_inst || res >= o->max_res || !o->res[res].exists || o->inst[inst].open) return CC_ERR_INVALID;
+  if (o->inst_by_id.count(instance_id)) return CC_ERR_INVALID;
+  o->register_instance(inst, res, instance_id, client_session);
+  return CC_OK;
+}
+
+// ResourceManager.getResource :77-143
+int orc_get_resource(orc* o, uint64_t key, uint32_t type, uint64_t client, uint64_t index, uint64_t* instance_id,
+                     uint32_t* inst_slot, uint8_t* status) {
+  *status = CC_STATUS(CC_ST_OK, CC_TAG_LONG);
+  auto kit = o->keys.find(key);
+  if (kit == o->keys.end()) {
+    int rs = o->alloc_res_slot(), is = o->alloc_inst_slot();
+    if (rs < 0 || is < 0) return CC_ERR_CAPACITY;
+    uint64_t rid = index;  // resource id = index of the creating commit (:87)
+    o->keys[key] = rid;
+    o->init_resource((uint32_t)rs, type, rid);
+    o->res[rs].key = key; o->res[rs].has_key = true;
+    o->register_instance((uint32_t)is, (uint32_t)rs, index, client);  // instance id = commit index (:103)
+    o->res[rs].sessions[client] = index;
+    *instance_id = index; *inst_slot = (uint32_t)is;
+    return CC_OK;
+  }
+  auto rit = o->res_by_id.find(kit->second);
+  if (rit == o->res_by_id.end() || o->res[rit->second].type != type) {  // :119-121
+    *status = CC_STATUS(CC_ST_TYPE_MISMATCH, CC_TAG_NULL);
+    return CC_OK;
+  }
+  Resource& r = o->res[rit->second];
+  auto hit = r.sessions.find(client);
+  if (hit == r.sessions.end()) {  // :126-136
+    int is = o->alloc_inst_slot();
+    if (is < 0) return CC_ERR_CAPACITY;
+    o->register_instance((uint32_t)is, rit->second, index, client);
+    r.sessions[client] = index;
+    *instance_id = index; *inst_slot = (uint32_t)is;
+  } else {  // :137-141
+    *instance_id = hit->second;
+    *inst_slot = o->inst_by_id[hit->second];
+  }
+  return CC_OK;
+}
+
+// ResourceManager.createResource :148-196 (a new instance every time, not added to resource.sessions)
+int orc_create_resource(orc* o, uint64_t key, uint32_t type, uint64_t client, uint64_t index, uint64_t* instance_id,
+                        uint32_t* inst_slot, uint8_t* status) {
+  *status = CC_STATUS(CC_ST_OK, CC_TAG_LONG);
+  uint32_t rslot;
+  auto kit = o->keys.find(key);
+  if (kit == o->keys.end()) {
+    int rs = o->alloc_res_slot();
+    if (rs < 0) return CC_ERR_CAPACITY;
+    o->keys[key] = index;
+    o->init_resource((uint32_t)rs, type, index);
+    o->res[rs].key = key; o->res[rs].has_key = true;
+    rslot = (uint32_t)rs;
+  } else {
+    auto rit = o->res_by_id.find(kit->second);
+    if (rit == o->res_by_id.end() || o->res[rit->second].type != type) {
+      *status = CC_STATUS(CC_ST_TYPE_MISMATCH, CC_TAG_NULL);
+      return CC_OK;
+    }
+    rslot = rit->second;
+  }
+  int is = o->alloc_inst_slot();
+  if (is < 0) return CC_ERR_CAPACITY;
+  o->register_instance((uint32_t)is, rslot, index, client);
+  *instance_id = index; *inst_slot = (uint32_t)is;
+  return CC_OK;
+}
+
+// ResourceManager.deleteResource :212-235 (looked up as a RESOURCE id although clients send the instance id, A13)
+int orc_delete_resource(orc* o, uint64_t resource_id, uint8_t* status) {
+  auto rit = o->res_by_id.find(resource_id);
+  if (rit == o->res_by_id.end()) { *status = CC_STATUS(CC_ST_UNKNOWN_RESOURCE, CC_TAG_NULL); return CC_OK; }
+  uint32_t slot = rit->second;
+  o->res_by_id.erase(rit);
+  Resource& r = o->res[slot];
+  uint8_t st = o->sm_delete(slot);   // resource.stateMachine.delete()
+  if (CC_STATUS_CODE(st) != CC_ST_OK) {
+    // delete() threw after resources.remove(): keys, timers and instance holders are left behind; a later
+    // commit on such an instance hits `resources.get(...) == null` -> NullPointerException (:62,71).
+    r.exists = false;
+    *status = st;
+    return CC_OK;
+  }
+  o->cancel_resource_timers(slot);   // resource.executor.close()
+  if (r.has_key) o->keys.erase(r.key);
+  for (uint32_t i = 0; i < o->max_inst; ++i)
+    if (o->inst[i].open && o->inst[i].res == slot) o->unregister_instance(i);
+  r.exists = false;
+  *status = CC_STATUS_CODE(st) == CC_ST_OK ? CC_STATUS(CC_ST_OK, CC_TAG_BOOL) : st;
+  return CC_OK;
+}
+
+int orc_resource_exists(orc* o, uint64_t key) { return o->keys.count(key) ? 1 : 0; }  // :201-207
+int orc_inst_slot_of(orc* o, uint64_t id) { auto it = o->inst_by_id.find(id); return it == o->inst_by_id.end() ? -1 : (int)it->second; }
+int orc_res_slot_of(orc* o, uint64_t id) { auto it = o->res_by_id.find(id); return it == o->res_by_id.end() ? -1 : (int)it->second; }
+
+int orc_apply(orc* o, const cc_batch* cols, uint64_t n, uint8_t* status, uint64_t* value) {
+  if (!o || !cols || !cols->inst || !cols->op) return CC_ERR_INVALID;
+  const bool deferred = (o->flags & ORC_TIMERS_DEFERRED) != 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    orc::Row r;
+    r.index = cols->index ? cols->index[i] : 0;
+    r.time = cols->time ? cols->time[i] : 0;
+    r.inst = cols->inst[i];
+    r.op = cols->op[i];
+    r.flags = cols->flags ? cols->flags[i] : 0;
+    r.key = cols->key ? cols->key[i] : 0;
+    r.a = cols->a ? cols->a[i] : 0;
+    r.b = cols->b ? cols->b[i] : 0;
+    r.aux = cols->aux ? cols->aux[i] : 0;
+    o->cur_pos = (uint32_t)i;
+    if (r.time > o->clock) o->clock = r.time;
+    if (!deferred && !o->timers.empty()) o->fire_due();
+    o->cur_src = CC_EVSRC_COMMIT;
+    o->apply_one(r, status[i], value[i]);
+    if (deferred && !o->timers.empty()) o->fire_due();
+    if (r.index > o->applied) o->applied = r.index;
+  }
+  return CC_OK;
+}
+
+int orc_advance_time(orc* o, uint64_t now) {
+  if (now > o->clock) o->clock = now;
+  o->cur_pos = UINT32_MAX;
+  o->fire_due();
+  return CC_OK;
+}
+
+// ResourceManager.close :250-264 — iterates ResourceManager.sessions in HashMap order
+int orc_session_close(orc* o, uint64_t client) {
+  std::vector<std::pair<uint64_t, uint32_t>> ord;
+  for (auto& kv : o->inst_by_id) {
+    const Inst& in = o->inst[kv.second];
+    if (in.client == client)
+      ord.emplace_back(o->sessions_order.order_key(java_hash(CC_TAG_LONG, kv.first), o->inst_seq[kv.first]), kv.second);
+  }
+  std::sort(ord.begin(), ord.end());
+  uint8_t saved = o->cur_src;
+  o->cur_src = CC_EVSRC_CLOSE;
+  o->cur_pos = UINT32_MAX;
+  for (auto& p : ord) {
+    uint32_t islot = p.second;
+    Inst& in = o->inst[islot];
+    Resource& r = o->res[in.res];
+    if (r.exists) {
+      r.sessions.erase(in.client);
+      if (!o->sm_close(islot)) break;  // an exception aborts the fan-out (unpinned)
+    }
+    o->unregister_instance(islot);
+  }
+  o->cur_src = saved;
+  return CC_OK;
+}
+
+// ResourceManager.expire :238-247 calls StateMachine.expire, which none of the covered state machines
+// override; Copycat then closes the session [not vendored] -> close fan-out.
+int orc_session_expire(orc* o, uint64_t client) { return orc_session_close(o, client); }
+
+uint64_t orc_applied_index(orc* o) { return o->applied; }
+
+uint64_t orc_event_count(orc* o) { return o->events.size(); }
+void orc_events_read(orc* o, uint32_t* pos, uint32_t* target, uint8_t* code, uint8_t* src, uint8_t* tag, uint64_t* payload) {
+  for (size_t i = 0; i < o->events.size(); ++i) {
+    const Event& e = o->events[i];
+    pos[i] = e.pos; target[i] = e.target; code[i] = e.code; src[i] = e.src; tag[i] = e.tag; payload[i] = e.payload;
+  }
+}
+void orc_events_clear(orc* o) { o->events.clear(); }
+uint64_t orc_aux_count(orc* o) { return o->aux.size(); }
+void orc_aux_read(orc* o, uint32_t* pos, uint64_t* member) {
+  for (size_t i = 0; i < o->aux.size(); ++i) { pos[i] = o->aux[i].first; member[i] = o->aux[i].second; }
+}
+void orc_aux_clear(orc* o) { o->aux.clear(); }
+
+int orc_read_value_state(orc* o, uint32_t first, uint32_t count, uint8_t* tag, uint64_t* value, uint8_t* has_current) {
+  if ((uint64_t)first + count > o->max_res) return CC_ERR_INVALID;
+  for (uint32_t i = 0; i < count; ++i) {
+    const Resource& r = o->res[first + i];
+    bool live = r.exists && r.type == CC_RES_VALUE;
+    tag[i] = live ? r.v.value.tag : 0;
+    value[i] = live ? r.v.value.v : 0;
+    has_current[i] = live && r.v.has_current ? 1 : 0;
+  }
+  return CC_OK;
+}
+
+int64_t orc_map_size(orc* o, uint32_t res) {
+  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_MAP) return -1;
+  return (int64_t)o->res[res].m.m.size();
+}
+
+int64_t orc_map_entries(orc* o, uint32_t res, uint64_t cap, uint8_t* ktag, uint64_t* key, uint8_t* vtag, uint64_t* val,
+                        uint64_t* commit_index) {
+  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_MAP) return -1;
+  std::vector<std::pair<MapKey, MapEntry>> v(o->res[res].m.m.begin(), o->res[res].m.m.end());
+  std::sort(v.begin(), v.end(), [](const std::pair<MapKey, MapEntry>& x, const std::pair<MapKey, MapEntry>& y) {
+    return x.first.tag != y.first.tag ? x.first.tag < y.first.tag : x.first.k < y.first.k;
+  });
+  uint64_t n = std::min<uint64_t>(cap, v.size());
+  for (uint64_t i = 0; i < n; ++i) {
+    ktag[i] = v[i].first.tag; key[i] = v[i].first.k; vtag[i] = v[i].second.value.tag; val[i] = v[i].second.value.v;
+    if (commit_index) commit_index[i] = v[i].second.commit_index;
+  }
+  return (int64_t)n;
+}
+
+int64_t orc_lock_state(orc* o, uint32_t res, int64_t* holder, uint64_t* holder_index, uint8_t* holder_cleaned, uint64_t cap,
+                       uint32_t* queue_inst, uint64_t* queue_index) {
+  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_LOCK) return -1;
+  const LockSM& l = o->res[res].l;
+  *holder = l.held ? (int64_t)l.lock.inst : -1;
+  *holder_index = l.held ? l.lock.index : 0;
+  *holder_cleaned = l.held && l.lock.cleaned ? 1 : 0;
+  uint64_t n = std::min<uint64_t>(cap, l.queue.size());
+  for (uint64_t i = 0; i < n; ++i) { queue_inst[i] = l.queue[i].inst; queue_index[i] = l.queue[i].index; }
+  return (int64_t)l.queue.size();
+}
+
+int64_t orc_election_state(orc* o, uint32_t res, int64_t* leader, uint64_t* leader_index, uint64_t cap,
+                           uint32_t* listener_inst, uint64_t* listener_index) {
+  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_ELECTION) return -1;
+  const ElectionSM& e = o->res[res].e;
+  *leader = e.has_leader ? (int64_t)e.leader.inst : -1;
+  *leader_index = e.has_leader ? e.leader.index : 0;
+  uint64_t n = std::min<uint64_t>(cap, e.listeners.size());
+  for (uint64_t i = 0; i < n; ++i) { listener_inst[i] = e.listeners[i].second.inst; listener_index[i] = e.listeners[i].second.index; }
+  return (int64_t)e.listeners.size();
+}
+
+int64_t orc_group_members(orc* o, uint32_t res, uint64_t cap, uint64_t* ids) {
+  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_GROUP) return -1;
+  std::vector<uint64_t> v;
+  for (auto& kv : o->res[res].g.members) v.push_back(kv.first);
+  std::sort(v.begin(), v.end());
+  uint64_t n = std::min<uint64_t>(cap, v.size());
+  for (uint64_t i = 0; i < n; ++i) ids[i] = v[i];
+  return (int64_t)v.size();
+}
+
+uint64_t orc_pending_timers(orc* o) { return o->timers.size(); }
+
+// a14 — leader commit index: the quorum-th largest match index, gated by the current-term start and
+// monotonicity (Raft §5.3/§5.4.2; Copycat's LeaderState is not vendored: rule defined by this build).
+void orc_quorum_commit(const uint64_t* match, uint32_t replicas, uint64_t groups, const uint64_t* term_start,
+                       const uint64_t* commit_in, uint64_t* commit_out) {
+  const uint32_t quorum = replicas / 2 + 1;
+  std::vector<uint64_t> m(replicas);
+  for (uint64_t g = 0; g < groups; ++g) {
+    for (uint32_t r = 0; r < replicas; ++r) m[r] = match[(uint64_t)r * groups + g];
+    std::sort(m.begin(), m.end(), [](uint64_t x, uint64_t y) { return x > y; });
+    uint64_t n = m[quorum - 1];
+    commit_out[g] = (n >= term_start[g] && n > commit_in[g]) ? n : commit_in[g];
+  }
+}
+
+// a15 — expired iff now - last > timeout (signed difference)
+void orc_expire_sweep(const uint64_t* last, uint64_t sessions, uint64_t now, uint64_t timeout, uint64_t* bitmap,
+                      uint64_t* count) {
+  uint64_t words = (sessions + 63) / 64, c = 0;
+  for (uint64_t w = 0; w < words; ++w) bitmap[w] = 0;
+  for (uint64_t s = 0; s < sessions; ++s) {
+    int64_t d = (int64_t)(now - last[s]);
+    if (d > (int64_t)timeout) { bitmap[s / 64] |= 1ull << (s % 64); ++c; }
+  }
+  *count += c;
+}
+
+}  // extern "C"
