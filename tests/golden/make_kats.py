@@ -1,0 +1,383 @@
+#!/usr/bin/env python3
+"""Writes tests/golden/kats.json: known-answer tests for the commit-apply path.
+
+Two kinds of KAT, each citing where its expected answers come from:
+  * "reference": the assertions of the reference's own tests (TestNG, run against a real Copycat cluster),
+    transcribed as (committed command, expected result / event) sequences.  The client-side API call is
+    mapped to the command(s) it submits (e.g. DistributedAtomicLong.incrementAndGet -> Get + CompareAndSet,
+    DistributedAtomicLong.java:117-146).  Strings are interned to HANDLE ids (see "strings").
+  * "quirk": hand-derived from the reference source for behaviour SURVEY Appendix A lists (A1..A15).
+  * "defined": rules that live in the un-vendored Copycat jar (timer order, quorum, expiry) — the answer
+    is this engine's documented rule, i.e. "parity unpinned".
+
+Value encoding: ["NULL"] | ["LONG", n] | ["INT", n] | ["BOOL", b] | ["H", handle] | ["SET", [ids...]].
+Run: python tests/golden/make_kats.py  (deterministic; the JSON is committed)
+"""
+import json
+import os
+
+STRINGS = {}
+
+
+def S(s):
+    """Interned String handle."""
+    if s not in STRINGS:
+        STRINGS[s] = len(STRINGS) + 1
+    return ["H", STRINGS[s]]
+
+
+NULL = ["NULL"]
+
+
+def L(n):
+    return ["LONG", n]
+
+
+def I(n):
+    return ["INT", n]
+
+
+def B(b):
+    return ["BOOL", bool(b)]
+
+
+def SET(*ids):
+    return ["SET", sorted(ids)]
+
+
+class K:
+    def __init__(self, name, kind, source, mode="deferred"):
+        self.d = {"name": name, "kind": kind, "source": source, "timer_mode": mode,
+                  "resources": [], "instances": [], "steps": []}
+
+    def res(self, slot, rtype):
+        self.d["resources"].append([slot, rtype])
+        return self
+
+    def inst(self, slot, res, iid, client):
+        self.d["instances"].append([slot, res, iid, client])
+        return self
+
+    def c(self, inst, op, key=None, a=None, b=None, aux=0, expect=None, status="OK", events=(), time=None):
+        step = {"commit": {"inst": inst, "op": op}}
+        cm = step["commit"]
+        if key is not None:
+            cm["key"] = key
+        if a is not None:
+            cm["a"] = a
+        if b is not None:
+            cm["b"] = b
+        if aux:
+            cm["aux"] = aux
+        if time is not None:
+            cm["time"] = time
+        step["expect"] = {"status": status, "result": expect if expect is not None else NULL}
+        if events:
+            step["events"] = [list(e) for e in events]
+        self.d["steps"].append(step)
+        return self
+
+    def advance(self, now, events=()):
+        step = {"advance": now}
+        if events:
+            step["events"] = [list(e) for e in events]
+        self.d["steps"].append(step)
+        return self
+
+    def close(self, client, events=()):
+        step = {"close": client}
+        if events:
+            step["events"] = [list(e) for e in events]
+        self.d["steps"].append(step)
+        return self
+
+    def ctl(self, what, expect_status="OK", **kw):
+        step = {"control": dict(what=what, **kw), "expect": {"status": expect_status}}
+        self.d["steps"].append(step)
+        return self
+
+    def state(self, **kw):
+        self.d["steps"].append({"state": kw})
+        return self
+
+
+def kats():
+    out = []
+    MAPT = "collections/src/test/java/io/atomix/collections/DistributedMapTest.java"
+
+    def map_kat(name, lines):
+        return K(name, "reference", f"{MAPT}:{lines}").res(0, "MAP").inst(0, 0, 100, 1)
+
+    hw, hwa = S("Hello world!"), S("Hello world again!")
+    foo, bar = S("foo"), S("bar")
+    out.append(map_kat("map_put_get_remove", "41-66")
+               .c(0, "MAP_PUT", key=foo, a=hw)
+               .c(0, "MAP_GET", key=foo, expect=hw)
+               .c(0, "MAP_REMOVE", key=foo, expect=hw)
+               .c(0, "MAP_GET", key=foo, expect=NULL))
+    out.append(map_kat("map_put_if_absent", "72-90")
+               .c(0, "MAP_PUT", key=foo, a=hw)
+               .c(0, "MAP_PUTIFABSENT", key=foo, a=S("something else"), expect=hw)
+               .c(0, "MAP_PUTIFABSENT", key=bar, a=S("something"), expect=NULL))
+    # putIfAbsent(foo, v, 100 ms) at t=0; Thread.sleep(1000) (session keep-alives tick the log clock);
+    # put(bar) at t=1000; containsKey(foo) == false
+    out.append(map_kat("map_put_if_absent_ttl", "96-111")
+               .c(0, "MAP_PUTIFABSENT", key=foo, a=hw, aux=100, time=0)
+               .advance(1000)
+               .c(0, "MAP_PUT", key=bar, a=hwa, time=1000)
+               .c(0, "MAP_CONTAINSKEY", key=foo, expect=B(False), time=1000))
+    out.append(map_kat("map_get_or_default", "117-136")
+               .c(0, "MAP_PUT", key=foo, a=hw)
+               .c(0, "MAP_GETORDEFAULT", key=foo, a=S("something else"), expect=hw)
+               .c(0, "MAP_GETORDEFAULT", key=bar, a=S("something"), expect=S("something")))
+    out.append(map_kat("map_contains_key", "142-161")
+               .c(0, "MAP_CONTAINSKEY", key=foo, expect=B(False))
+               .c(0, "MAP_PUT", key=foo, a=hw, expect=NULL)
+               .c(0, "MAP_CONTAINSKEY", key=foo, expect=B(True)))
+    out.append(map_kat("map_contains_value", "167-186")
+               .c(0, "MAP_CONTAINSVALUE", a=hw, expect=B(False))
+               .c(0, "MAP_PUT", key=foo, a=hw, expect=NULL)
+               .c(0, "MAP_CONTAINSVALUE", a=hw, expect=B(True)))
+    out.append(map_kat("map_size", "192-220")
+               .c(0, "MAP_SIZE", expect=I(0))
+               .c(0, "MAP_PUT", key=foo, a=hw)
+               .c(0, "MAP_SIZE", expect=I(1))
+               .c(0, "MAP_PUT", key=bar, a=hwa)
+               .c(0, "MAP_SIZE", expect=I(2)))
+    out.append(map_kat("map_put_ttl", "226-253")
+               .c(0, "MAP_PUT", key=foo, a=hw, aux=1000, time=0)
+               .c(0, "MAP_GET", key=foo, expect=hw, time=0)
+               .advance(3000)
+               .c(0, "MAP_GET", key=foo, expect=NULL, time=3000)
+               .c(0, "MAP_SIZE", expect=I(0), time=3000))
+    out.append(map_kat("map_clear", "258-286")
+               .c(0, "MAP_PUT", key=foo, a=hw)
+               .c(0, "MAP_PUT", key=bar, a=hwa)
+               .c(0, "MAP_SIZE", expect=I(2))
+               .c(0, "MAP_ISEMPTY", expect=B(False))
+               .c(0, "MAP_CLEAR")
+               .c(0, "MAP_SIZE", expect=I(0))
+               .c(0, "MAP_ISEMPTY", expect=B(True)))
+
+    AV = "atomic/src/test/java/io/atomix/atomic/DistributedAtomicValueTest.java"
+    out.append(K("atomic_value_set_get", "reference", f"{AV}:40-51").res(0, "VALUE").inst(0, 0, 100, 1)
+               .c(0, "VALUE_SET", a=hw)
+               .c(0, "VALUE_GET", expect=hw)
+               .state(value=[0, hw, True]))
+
+    # DistributedAtomicLongTest: a.get() then op; the op is the client CAS loop (DistributedAtomicLong.java:117-146):
+    # getValue() -> Get (cache empty) -> null -> E' = 0; CompareAndSet(null, 0 + delta) succeeds (A4).
+    # The test never awaits (A17): these are its intended answers.
+    AL = "atomic/src/test/java/io/atomix/atomic/DistributedAtomicLongTest.java"
+    for name, lines, delta in [("increment_and_get", "44-46", 1), ("decrement_and_get", "51-53", -1),
+                               ("get_and_increment", "58-60", 1), ("get_and_decrement", "65-67", -1),
+                               ("add_and_get", "72-74", 10), ("get_and_add", "79-81", 10)]:
+        out.append(K(f"atomic_long_{name}", "reference", f"{AL}:{lines},84-105").res(0, "VALUE").inst(0, 0, 100, 1)
+                   .c(0, "VALUE_GET", expect=NULL)             # a.get() (null -> 0 on the client)
+                   .c(0, "VALUE_GET", expect=NULL)             # updateValue: getValue() with an empty cache
+                   .c(0, "VALUE_CAS", a=NULL, b=L(delta), expect=B(True))
+                   .state(value=[0, L(delta), True]))
+
+    LK = "coordination/src/test/java/io/atomix/coordination/DistributedLockTest.java"
+    # lock() submits Lock(-1) (DistributedLock.java:107-117); the grant is the "lock"(true) event
+    out.append(K("lock_unlock", "reference", f"{LK}:38-48").res(0, "LOCK").inst(0, 0, 100, 1)
+               .c(0, "LOCK_LOCK", aux=-1, events=[(0, "LOCK", B(True))])
+               .c(0, "LOCK_UNLOCK")
+               .state(lock=[0, None, []]))
+
+    EL = "coordination/src/test/java/io/atomix/coordination/DistributedLeaderElectionTest.java"
+    out.append(K("election_elect", "reference", f"{EL}:41-48").res(0, "ELECTION").inst(0, 0, 100, 1)
+               .c(0, "ELECT_LISTEN", events=[(0, "ELECT", L(1))]))  # epoch = index of the Listen commit
+    # two clients; client1 closes -> client2 elected with a strictly larger epoch
+    out.append(K("election_next_on_close", "reference", f"{EL}:53-80").res(0, "ELECTION")
+               .inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(0, "ELECT_LISTEN", events=[(0, "ELECT", L(1))])
+               .c(1, "ELECT_LISTEN")
+               .close(1, events=[(1, "ELECT", L(2))]))
+
+    GR = "coordination/src/test/java/io/atomix/coordination/DistributedMembershipGroupTest.java"
+    out.append(K("group_join", "reference", f"{GR}:42-65").res(0, "GROUP").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(1, "GROUP_JOIN", expect=SET(101))
+               .c(0, "GROUP_JOIN", expect=SET(100, 101), events=[(1, "JOIN", L(100))]))
+    out.append(K("group_leave", "reference", f"{GR}:70-91").res(0, "GROUP").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(1, "GROUP_JOIN", expect=SET(101))
+               .c(0, "GROUP_JOIN", expect=SET(100, 101), events=[(1, "JOIN", L(100))])
+               .c(1, "GROUP_LEAVE", events=[(0, "LEAVE", L(101))])
+               .state(members=[0, [100]]))
+    cb = S("counter::incrementAndGet")
+    out.append(K("group_remote_execute", "reference", f"{GR}:96-117").res(0, "GROUP").inst(0, 0, 100, 1)
+               .inst(1, 0, 101, 2)
+               .c(1, "GROUP_JOIN", expect=SET(101))
+               .c(0, "GROUP_JOIN", expect=SET(100, 101), events=[(1, "JOIN", L(100))])
+               .c(0, "GROUP_EXECUTE", key=L(100), a=cb, events=[(0, "EXECUTE", cb)])
+               .c(0, "GROUP_EXECUTE", key=L(101), a=cb, events=[(1, "EXECUTE", cb)]))
+
+    RT = "manager/src/test/java/io/atomix/AtomixReplicaTest.java"
+    test = S("test")
+    out.append(K("manager_create_concurrency", "reference", f"{RT}:154-168")
+               .ctl("create", key=test, type="VALUE", client=1, index=10, expect_instance=10)
+               .ctl("create", key=test, type="VALUE", client=2, index=11, expect_instance=11)
+               .c("@10", "VALUE_SET", a=hw)
+               .c("@11", "VALUE_GET", expect=hw))
+    out.append(K("manager_get_create_concurrency", "reference", f"{RT}:173-189")
+               .ctl("get", key=test, type="VALUE", client=1, index=10, expect_instance=10)
+               .ctl("create", key=test, type="VALUE", client=2, index=11, expect_instance=11)
+               .c("@10", "VALUE_SET", a=hw)
+               .c("@11", "VALUE_GET", expect=hw))
+    t1, t2 = S("test1"), S("test2")
+    out.append(K("manager_operate_many", "reference", f"{RT}:194-215")
+               .ctl("get", key=t1, type="VALUE", client=1, index=10, expect_instance=10)
+               .ctl("create", key=t1, type="VALUE", client=2, index=11, expect_instance=11)
+               .ctl("get", key=t2, type="VALUE", client=1, index=12, expect_instance=12)
+               .ctl("create", key=t2, type="VALUE", client=2, index=13, expect_instance=13)
+               .c("@10", "VALUE_SET", a=foo)
+               .c("@11", "VALUE_GET", expect=foo)
+               .c("@12", "VALUE_SET", a=bar)
+               .c("@13", "VALUE_GET", expect=bar)
+               .c("@10", "VALUE_GET", expect=foo)
+               .c("@12", "VALUE_GET", expect=bar))
+    out.append(K("manager_get_reuses_instance", "quirk", "manager/src/main/java/io/atomix/manager/ResourceManager.java:125-141")
+               .ctl("get", key=test, type="VALUE", client=1, index=10, expect_instance=10)
+               .ctl("get", key=test, type="VALUE", client=1, index=11, expect_instance=10)
+               .ctl("get", key=test, type="MAP", client=3, index=12, expect_status="TYPE_MISMATCH")
+               .ctl("exists", key=test, expect_bool=True)
+               .ctl("exists", key=S("nope"), expect_bool=False))
+
+    # ---- quirk KATs, hand-derived from the cited source lines ------------------------
+    MS = "collections/src/main/java/io/atomix/collections/state/MapState.java"
+    out.append(K("A1_replace_if_present_inverts_args", "quirk", f"{MS}:207-228; DistributedMap.java:653-654")
+               .res(0, "MAP").inst(0, 0, 100, 1)
+               .c(0, "MAP_PUT", key=foo, a=S("old"))
+               # client replace(foo, "old", "new") -> ReplaceIfPresent(value="old", replace="new"): compares "new"
+               .c(0, "MAP_REPLACEIFPRESENT", key=foo, a=S("old"), b=S("new"), expect=B(False))
+               .c(0, "MAP_REPLACEIFPRESENT", key=foo, a=S("X"), b=S("old"), expect=B(True))
+               .c(0, "MAP_GET", key=foo, expect=S("X")))
+    AVS = "atomic/src/main/java/io/atomix/atomic/state/AtomicValueState.java"
+    out.append(K("A2_atomic_ttl_not_serialized", "quirk", "atomic/.../AtomicValueCommands.java:125-133,181-191")
+               .res(0, "VALUE").inst(0, 0, 100, 1)
+               .c(0, "VALUE_SET", a=L(5), aux=100, time=0)
+               .advance(10_000)
+               .c(0, "VALUE_GET", expect=L(5), time=10_000))
+    ES = "coordination/src/main/java/io/atomix/coordination/state/LeaderElectionState.java"
+    out.append(K("A3_is_leader_epoch_zero", "quirk", f"{ES}:96-98; LeaderElectionCommands.java:99-123")
+               .res(0, "ELECTION").inst(0, 0, 100, 1)
+               .c(0, "ELECT_LISTEN", events=[(0, "ELECT", L(1))])
+               .c(0, "ELECT_ISLEADER", aux=1, expect=B(False)))
+    out.append(K("A4_first_cas_null_expect", "quirk", f"{AVS}:124")
+               .res(0, "VALUE").inst(0, 0, 100, 1)
+               .c(0, "VALUE_CAS", a=L(0), b=L(7), expect=B(False))
+               .c(0, "VALUE_CAS", a=NULL, b=L(7), expect=B(True))
+               .c(0, "VALUE_CAS", a=NULL, b=L(8), expect=B(False))
+               .c(0, "VALUE_GETANDSET", a=NULL, expect=L(7))
+               .c(0, "VALUE_GET", expect=NULL)
+               .state(value=[0, NULL, True]))
+    # A5: HashMap order: Long key 1 -> bucket 1, key 2 -> bucket 2 (cap 16)
+    out.append(K("A5_contains_value_npe_order", "quirk", f"{MS}:49-60")
+               .res(0, "MAP").inst(0, 0, 100, 1).res(64, "MAP").inst(1, 64, 101, 1)
+               .c(0, "MAP_PUT", key=L(1), a=S("x"))
+               .c(0, "MAP_PUT", key=L(2), a=NULL)
+               .c(0, "MAP_CONTAINSVALUE", a=S("x"), expect=B(True))
+               .c(0, "MAP_CONTAINSVALUE", a=S("y"), status="NULL_POINTER")
+               .c(1, "MAP_PUT", key=L(1), a=NULL)
+               .c(1, "MAP_PUT", key=L(2), a=S("x"))
+               .c(1, "MAP_CONTAINSVALUE", a=S("x"), status="NULL_POINTER"))
+    out.append(K("A6_null_value_is_present", "quirk", f"{MS}:115-133,38-44,65-72")
+               .res(0, "MAP").inst(0, 0, 100, 1)
+               .c(0, "MAP_PUT", key=foo, a=NULL)
+               .c(0, "MAP_PUTIFABSENT", key=foo, a=S("v"), expect=NULL)
+               .c(0, "MAP_CONTAINSKEY", key=foo, expect=B(True))
+               .c(0, "MAP_GET", key=foo, expect=NULL)
+               .c(0, "MAP_GETORDEFAULT", key=foo, a=S("d"), expect=NULL)
+               .c(0, "MAP_REMOVEIFPRESENT", key=foo, a=S("v"), expect=B(False))
+               .c(0, "MAP_REMOVEIFPRESENT", key=foo, a=NULL, expect=B(True))
+               .c(0, "MAP_SIZE", expect=I(0)))
+    LS = "coordination/src/main/java/io/atomix/coordination/state/LockState.java"
+    out.append(K("A7_trylock_timeout_is_silent", "quirk", f"{LS}:41-61")
+               .res(0, "LOCK").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(0, "LOCK_LOCK", aux=-1, events=[(0, "LOCK", B(True))], time=0)
+               .c(1, "LOCK_LOCK", aux=100, time=0)     # tryLock(100 ms): queued, timer armed
+               .c(1, "LOCK_LOCK", aux=0, events=[(1, "LOCK", B(False))], time=10)  # tryLock(): fails now
+               .advance(200)                              # the waiter's timer fires: no event
+               .c(0, "LOCK_UNLOCK", time=200)             # nobody queued: lock becomes free
+               .state(lock=[0, None, []]))
+    out.append(K("lock_fifo_handoff_and_not_holder", "quirk", f"{LS}:66-85")
+               .res(0, "LOCK").inst(0, 0, 100, 1).inst(1, 0, 101, 2).inst(2, 0, 102, 3)
+               .c(0, "LOCK_LOCK", aux=-1, events=[(0, "LOCK", B(True))])
+               .c(1, "LOCK_LOCK", aux=-1)
+               .c(2, "LOCK_LOCK", aux=5000)
+               .c(2, "LOCK_UNLOCK", status="ILLEGAL_STATE")
+               .c(0, "LOCK_UNLOCK", events=[(1, "LOCK", B(True))])
+               .c(1, "LOCK_UNLOCK", events=[(2, "LOCK", B(True))])
+               .state(lock=[0, 2, []]))
+    out.append(K("A9_leader_relisten_appended", "quirk", f"{ES}:57-66,71-91")
+               .res(0, "ELECTION").inst(0, 0, 100, 1)
+               .c(0, "ELECT_LISTEN", events=[(0, "ELECT", L(1))])
+               .c(0, "ELECT_LISTEN")
+               .c(0, "ELECT_UNLISTEN", events=[(0, "ELECT", L(2))]))
+    GS = "coordination/src/main/java/io/atomix/coordination/state/MembershipGroupState.java"
+    out.append(K("A10_close_publishes_leave_for_non_member", "quirk", f"{GS}:36-42")
+               .res(0, "GROUP").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(0, "GROUP_JOIN", expect=SET(100))
+               .close(2, events=[(0, "LEAVE", L(101))]))
+    out.append(K("A11_lock_survives_holder_close", "quirk", f"{LS}:33-100")
+               .res(0, "LOCK").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(0, "LOCK_LOCK", aux=-1, events=[(0, "LOCK", B(True))])
+               .c(1, "LOCK_LOCK", aux=-1)
+               .close(1)
+               .state(lock=[0, 0, [1]]))
+    out.append(K("A13_delete_resource_by_instance_id", "quirk", "manager/.../ResourceManager.java:212-235; InstanceClient.java:73-74")
+               .ctl("get", key=test, type="VALUE", client=1, index=10, expect_instance=10)
+               .ctl("get", key=test, type="VALUE", client=2, index=11, expect_instance=11)
+               .ctl("delete", resource=11, expect_status="UNKNOWN_RESOURCE")
+               .ctl("delete", resource=10, expect_status="OK")
+               .c("#0", "VALUE_GET", status="UNKNOWN_SESSION"))
+    out.append(K("A15_long_is_not_integer", "quirk", f"{AVS}:124")
+               .res(0, "VALUE").inst(0, 0, 100, 1)
+               .c(0, "VALUE_SET", a=L(1))
+               .c(0, "VALUE_CAS", a=I(1), b=L(2), expect=B(False))
+               .c(0, "VALUE_CAS", a=L(1), b=I(2), expect=B(True))
+               .c(0, "VALUE_CAS", a=I(2), b=B(True), expect=B(True))
+               .c(0, "VALUE_GET", expect=B(True)))
+    out.append(K("lock_delete_then_unlock_commit_closed", "quirk", f"{LS}:87-98; ResourceManagerCommit.java:79-83")
+               .res(0, "LOCK").inst(0, 0, 100, 1)
+               .c(0, "LOCK_LOCK", aux=-1, events=[(0, "LOCK", B(True))])
+               .c(0, "DELETE")
+               .c(0, "LOCK_UNLOCK", status="ILLEGAL_STATE")
+               .c(0, "DELETE", status="ILLEGAL_STATE"))
+    out.append(K("dispatch_errors", "quirk", "manager/.../ResourceManager.java:60-69; ResourceStateMachineExecutor.java:78")
+               .res(0, "VALUE").inst(0, 0, 100, 1).res(64, "GROUP").inst(1, 64, 101, 1)
+               .c(5, "VALUE_GET", status="UNKNOWN_SESSION")
+               .c(0, "MAP_PUT", key=foo, a=hw, status="UNKNOWN_OP")
+               .c(1, "GROUP_EXECUTE", key=L(999), a=cb, status="ILLEGAL_ARGUMENT")
+               .c(1, "GROUP_SCHEDULE", key=L(999), a=cb, aux=10, status="ILLEGAL_ARGUMENT"))
+    out.append(K("group_schedule_fires_on_clock", "defined", f"{GS}:86-103 (timer order: Copycat, unpinned)")
+               .res(0, "GROUP").inst(0, 0, 100, 1)
+               .c(0, "GROUP_JOIN", expect=SET(100), time=0)
+               .c(0, "GROUP_SCHEDULE", key=L(100), a=cb, aux=50, time=0)
+               .advance(49)
+               .advance(50, events=[(0, "EXECUTE", cb)]))
+    # timer order rule (A8): manager mode defers due timers to after the commit that advanced the clock
+    out.append(K("A8_timer_deferred_after_commit", "defined", "ResourceManagerStateMachineExecutor.java:104-109")
+               .res(0, "MAP").inst(0, 0, 100, 1)
+               .c(0, "MAP_PUT", key=foo, a=hw, aux=100, time=0)
+               .c(0, "MAP_GET", key=foo, expect=hw, time=100)
+               .c(0, "MAP_GET", key=foo, expect=NULL, time=100))
+    k = K("A8_timer_immediate_module_mode", "defined", "ResourceStateMachineExecutor.java:109-117", mode="immediate")
+    out.append(k.res(0, "MAP").inst(0, 0, 100, 1)
+               .c(0, "MAP_PUT", key=foo, a=hw, aux=100, time=0)
+               .c(0, "MAP_GET", key=foo, expect=NULL, time=100))
+    return out
+
+
+def main():
+    data = {"comment": __doc__.strip().splitlines()[0], "strings": None, "kats": [k.d for k in kats()]}
+    data["strings"] = STRINGS
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kats.json")
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=False)
+        f.write("\n")
+    print(f"wrote {len(data['kats'])} KATs to {path}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,275 @@
+"""Runs the KATs of tests/golden/kats.json against a backend (the CPU oracle or the GPU engine).
+
+Consecutive commit steps are applied as ONE batch (so a multi-row batch is what gets checked); control,
+clock and close steps flush the pending batch first.  Events are compared per step as sorted multisets of
+(target instance slot, code, tag, payload) — per-target order is what the reference fixes.
+"""
+import json
+import os
+
+import numpy as np
+
+from copycat_amd import abi
+from copycat_amd.batch import Batch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KAT_PATH = os.path.join(HERE, "golden", "kats.json")
+
+RES = {"VALUE": abi.CC_RES_VALUE, "MAP": abi.CC_RES_MAP, "LOCK": abi.CC_RES_LOCK, "ELECTION": abi.CC_RES_ELECTION,
+       "GROUP": abi.CC_RES_GROUP}
+TAG = {"NULL": abi.CC_TAG_NULL, "LONG": abi.CC_TAG_LONG, "INT": abi.CC_TAG_INT, "BOOL": abi.CC_TAG_BOOL,
+       "H": abi.CC_TAG_HANDLE, "SET": abi.CC_TAG_SET}
+EV = {"CHANGE": abi.CC_EV_CHANGE, "LOCK": abi.CC_EV_LOCK, "ELECT": abi.CC_EV_ELECT, "JOIN": abi.CC_EV_JOIN,
+      "LEAVE": abi.CC_EV_LEAVE, "EXECUTE": abi.CC_EV_EXECUTE}
+ST = {"OK": abi.CC_ST_OK, "UNKNOWN_SESSION": abi.CC_ST_UNKNOWN_SESSION, "UNKNOWN_OP": abi.CC_ST_UNKNOWN_OP,
+      "ILLEGAL_STATE": abi.CC_ST_ILLEGAL_STATE, "ILLEGAL_ARGUMENT": abi.CC_ST_ILLEGAL_ARGUMENT,
+      "NULL_POINTER": abi.CC_ST_NULL_POINTER, "TYPE_MISMATCH": abi.CC_ST_TYPE_MISMATCH,
+      "UNKNOWN_RESOURCE": abi.CC_ST_UNKNOWN_RESOURCE}
+
+
+def load():
+    with open(KAT_PATH) as f:
+        return json.load(f)
+
+
+def enc(v):
+    """JSON value -> (tag, payload)."""
+    t = TAG[v[0]]
+    if t == abi.CC_TAG_NULL:
+        return t, 0
+    if t == abi.CC_TAG_BOOL:
+        return t, int(bool(v[1]))
+    if t == abi.CC_TAG_SET:
+        return t, len(v[1])
+    return t, int(v[1]) & 0xFFFFFFFFFFFFFFFF
+
+
+def op_code(name):
+    return getattr(abi, f"CC_OP_{name}")
+
+
+def uses_only_value(kat):
+    if any(r[1] != "VALUE" for r in kat["resources"]):
+        return False
+    for s in kat["steps"]:
+        if "control" in s or "close" in s:
+            return False
+        if "commit" in s and not (s["commit"]["op"].startswith("VALUE_") or s["commit"]["op"] == "DELETE"):
+            if s["commit"]["op"] in ("VALUE_LISTEN", "VALUE_UNLISTEN"):
+                return False
+            return False
+    return True
+
+
+class KatRun:
+    """Drives one KAT through `backend` and asserts every expectation."""
+
+    def __init__(self, kat, backend):
+        self.kat = kat
+        self.B = backend
+        self.next_index = 1
+        self.clock = 0
+        self.pending = []  # (step, row fields)
+
+    def inst_slot(self, ref):
+        if isinstance(ref, int):
+            return ref
+        if ref.startswith("@"):
+            s = self.B.inst_slot_of(int(ref[1:]))
+            assert s >= 0, f"unknown instance id {ref}"
+            return s
+        if ref.startswith("#"):
+            return int(ref[1:])
+        raise ValueError(ref)
+
+    def run(self):
+        for r in self.kat["resources"]:
+            self.B.resource_create(r[0], RES[r[1]])
+        for i in self.kat["instances"]:
+            self.B.instance_open(*i)
+        for step in self.kat["steps"]:
+            if "commit" in step:
+                self.pending.append(step)
+                continue
+            self.flush()
+            if "advance" in step:
+                self.clock = max(self.clock, step["advance"])
+                evs = self.B.advance(step["advance"])
+                self.check_events(step, evs)
+            elif "close" in step:
+                evs = self.B.close(step["close"])
+                self.check_events(step, evs)
+            elif "control" in step:
+                self.control(step)
+            elif "state" in step:
+                self.check_state(step["state"])
+        self.flush()
+
+    def flush(self):
+        if not self.pending:
+            return
+        n = len(self.pending)
+        b = Batch(n)
+        for i, step in enumerate(self.pending):
+            c = step["commit"]
+            if "time" in c:
+                self.clock = max(self.clock, c["time"])
+            b.index[i] = self.next_index
+            self.next_index += 1
+            b.time[i] = self.clock
+            b.inst[i] = self.inst_slot(c["inst"]) if not (isinstance(c["inst"], str) and c["inst"].startswith("@")) \
+                else self.inst_slot(c["inst"])
+            b.op[i] = op_code(c["op"])
+            ta, pa = enc(c["a"]) if "a" in c else (0, 0)
+            tb, pb = enc(c["b"]) if "b" in c else (0, 0)
+            kt, kp = (0, 0)
+            if "key" in c:
+                t, kp = enc(c["key"])
+                kt = abi.KTAG_OF_TAG[t]
+            b.flags[i] = abi.cc_flags(ta, tb, kt)
+            b.key[i], b.a[i], b.b[i] = kp, pa, pb
+            b.aux[i] = c.get("aux", 0) & 0xFFFFFFFFFFFFFFFF
+        status, value, events, aux = self.B.apply(b)
+        for i, step in enumerate(self.pending):
+            exp = step["expect"]
+            name = f"{self.kat['name']} row {i} ({step['commit']['op']})"
+            assert abi.status_code(status[i]) == ST[exp["status"]], \
+                f"{name}: status {abi.status_code(status[i])} != {exp['status']}"
+            if exp["status"] == "OK":
+                et, ep = enc(exp["result"])
+                assert (abi.status_tag(status[i]), int(value[i])) == (et, ep), \
+                    f"{name}: result ({abi.status_tag(status[i])},{int(value[i])}) != {exp['result']}"
+                if et == abi.CC_TAG_SET:
+                    got = sorted(int(m) for p, m in aux if p == i)
+                    assert got == sorted(exp["result"][1]), f"{name}: set {got} != {exp['result'][1]}"
+            self.check_events(step, [e for e in events if e[0] == i], name)
+        self.pending = []
+
+    def check_events(self, step, evs, name=None):
+        name = name or f"{self.kat['name']} {list(step)[0]}"
+        want = sorted((self.inst_slot(t), EV[code], *enc(v)) for t, code, v in step.get("events", []))
+        got = sorted((int(e[1]), int(e[2]), int(e[3]), int(e[4])) for e in evs)
+        assert got == want, f"{name}: events {got} != {want}"
+
+    def control(self, step):
+        c = step["control"]
+        what = c["what"]
+        exp = step["expect"]["status"]
+        if what in ("get", "create"):
+            key = enc(c["key"])[1]
+            self.next_index = max(self.next_index, c["index"] + 1)
+            st, iid = self.B.manager(what, key, RES[c["type"]], c["client"], c["index"])
+            assert abi.status_code(st) == ST[exp], f"{self.kat['name']} {what}: status {st}"
+            if "expect_instance" in c:
+                assert iid == c["expect_instance"], f"{self.kat['name']} {what}: instance {iid}"
+        elif what == "delete":
+            st = self.B.delete_resource(c["resource"])
+            assert abi.status_code(st) == ST[exp], f"{self.kat['name']} delete: status {st}"
+        elif what == "exists":
+            assert self.B.resource_exists(enc(c["key"])[1]) == c["expect_bool"]
+        else:
+            raise ValueError(what)
+
+    def check_state(self, s):
+        if "value" in s:
+            res, v, cur = s["value"]
+            tag, val, has = self.B.value_state(res)
+            assert (tag, val, bool(has)) == (*enc(v), cur), f"{self.kat['name']} value state {(tag, val, has)}"
+        if "lock" in s:
+            res, holder, queue = s["lock"]
+            h, q = self.B.lock_state(res)
+            assert (h, q) == (holder, queue), f"{self.kat['name']} lock state {(h, q)}"
+        if "members" in s:
+            res, ids = s["members"]
+            assert self.B.group_members(res) == ids
+
+
+class OracleBackend:
+    def __init__(self, kat, max_resources=256, max_instances=64):
+        from oracle.oracle_py import Oracle
+
+        flags = abi.CC_CFG_TIMERS_DEFERRED if kat.get("timer_mode", "deferred") == "deferred" else 0
+        self.O = Oracle(max_resources, max_instances, flags)
+
+    def resource_create(self, slot, t):
+        self.O.resource_create(slot, t)
+
+    def instance_open(self, inst, res, iid, client):
+        self.O.instance_open(inst, res, iid, client)
+
+    def inst_slot_of(self, iid):
+        return self.O.inst_slot_of(iid)
+
+    def _events(self):
+        e = self.O.take_events()
+        return [(int(e["pos"][i]), int(e["target"][i]), int(e["code"][i]), int(e["tag"][i]), int(e["payload"][i]))
+                for i in range(len(e["pos"]))]
+
+    def apply(self, b):
+        s, v = self.O.apply(b)
+        evs = self._events()
+        pos, mem = self.O.take_aux()
+        return s, v, evs, list(zip(pos.tolist(), mem.tolist()))
+
+    def advance(self, now):
+        self.O.advance_time(now)
+        return self._events()
+
+    def close(self, client):
+        self.O.session_close(client)
+        return self._events()
+
+    def manager(self, what, key, t, client, index):
+        fn = self.O.get_resource if what == "get" else self.O.create_resource
+        st, iid, _ = fn(key, t, client, index)
+        return st, iid
+
+    def delete_resource(self, rid):
+        return self.O.delete_resource(rid)
+
+    def resource_exists(self, key):
+        return self.O.resource_exists(key)
+
+    def value_state(self, res):
+        t, v, c = self.O.value_state(res, 1)
+        return int(t[0]), int(v[0]), int(c[0])
+
+    def lock_state(self, res):
+        h, _, _, q = self.O.lock_state(res)
+        return (None if h < 0 else h), [x[0] for x in q]
+
+    def group_members(self, res):
+        return self.O.group_members(res)
+
+
+class EngineBackend:
+    """GPU engine backend (AtomicValue KATs: the GPU-applied subset of this build)."""
+
+    def __init__(self, kat, max_resources=256, max_instances=64):
+        from copycat_amd.engine import Engine
+
+        self.E = Engine(max_resources, max_instances, 4096)
+
+    def resource_create(self, slot, t):
+        self.E.resource_create(slot, t)
+
+    def instance_open(self, inst, res, iid, client):
+        self.E.instance_open(inst, res, iid, client)
+
+    def apply(self, b):
+        s, v = self.E.apply_host(b)
+        return s, v, [], []
+
+    def advance(self, now):
+        return []
+
+    def value_state(self, res):
+        t, v, c = self.E.value_state(res, 1)
+        return int(t[0]), int(v[0]), int(c[0])
+
+
+def all_kats():
+    return load()["kats"]
+
+
+__all__ = ["KatRun", "OracleBackend", "EngineBackend", "all_kats", "uses_only_value", "np"]
