@@ -9,28 +9,26 @@ namespace cc {
 
 // ---- geometry -----------------------------------------------------------------------------------------
 constexpr int kWave = 64;                 // CDNA wavefront
-constexpr int kResPerBucket = 64;         // one apply wave owns 64 resource slots (lane = slot % 64)
-constexpr int kBucketShift = 6;
-constexpr int kMaxBuckets = 4096;         // => max_resources <= 262144
-constexpr int kPartWaves = 4;             // partition workgroup = 4 waves
-constexpr int kPartThreads = kPartWaves * kWave;
-constexpr int kWaveTile = 4096;           // commits per wave per partition tile
-constexpr int kTile = kPartWaves * kWaveTile;  // 16384 commits per partition tile
+constexpr int kLaneRes = 64;              // an apply wave owns 64 resource slots (lane = slot % 64)
+constexpr int kApplyWaves = 4;            // apply workgroup = 4 waves = one super-bucket of 256 slots
+constexpr int kSbShift = 8;               // super-bucket = slot >> 8
+constexpr int kMaxSb = 512;               // => max_resources <= 131072 with 256-slot super-buckets
+constexpr int kPT = 1024;                 // partition workgroup threads (16 waves)
+constexpr int kPW = kPT / kWave;
+constexpr int kTile = 16384;              // commits per partition tile (one workgroup)
+constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a tile
 constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan (1024-thread WG)
+constexpr int kApplyPer = 8;              // staging records per apply thread per chunk (prefetch depth)
 constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 
 // device error bits (d_err)
 constexpr uint32_t kErrUnsupported = 1u;
 constexpr uint32_t kErrEvents = 2u;
 
-// staging record meta word: pos(32) | op(8) | flags(8) | lane(6)
-__host__ __device__ inline uint64_t pack_meta(uint32_t pos, uint32_t op, uint32_t flags, uint32_t lane) {
-  return (uint64_t)pos | ((uint64_t)(op & 0xFF) << 32) | ((uint64_t)(flags & 0xFF) << 40) | ((uint64_t)(lane & 63) << 48);
-}
-__host__ __device__ inline uint32_t meta_pos(uint64_t m) { return (uint32_t)m; }
-__host__ __device__ inline uint32_t meta_op(uint64_t m) { return (uint32_t)(m >> 32) & 0xFF; }
-__host__ __device__ inline uint32_t meta_flags(uint64_t m) { return (uint32_t)(m >> 40) & 0xFF; }
-__host__ __device__ inline uint32_t meta_lane(uint64_t m) { return (uint32_t)(m >> 48) & 63; }
+// staging record meta word (u32): op(8) | flags(8) | slot-within-super-bucket(<=10 bits) << 16
+__host__ __device__ inline uint32_t smeta_op(uint32_t m) { return m & 0xFF; }
+__host__ __device__ inline uint32_t smeta_flags(uint32_t m) { return (m >> 8) & 0xFF; }
+__host__ __device__ inline uint32_t smeta_slot(uint32_t m) { return m >> 16; }
 
 struct alignas(16) u64x2 {
   uint64_t x, y;

@@ -39,11 +39,11 @@ struct cc_engine {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t last_stream = nullptr;
-  uint32_t nb = 0, nbits = 0;
+  uint32_t sb = 0, sb_bits = 0;  // super-buckets of 256 slots
   uint64_t sub_batch = 0, max_tiles = 0;
   // host mirrors of the registry
-  std::vector<uint8_t> res_type;     // [nb*64]
-  std::vector<uint8_t> bucket_type;  // [nb] (a bucket holds one resource type)
+  std::vector<uint8_t> res_type;     // [sb*256]
+  std::vector<uint8_t> bucket_type;  // [slots/64] (a 64-slot bucket holds one resource type)
   std::vector<uint32_t> bucket_live; // live resources per bucket
   std::vector<uint32_t> inst_res;    // [max_inst]
   std::vector<uint64_t> inst_id, inst_client;
@@ -56,8 +56,11 @@ struct cc_engine {
   uint32_t* d_counts = nullptr;
   uint32_t* d_tot = nullptr;
   uint32_t* d_base = nullptr;
-  uint64_t* d_st_meta = nullptr;
+  uint32_t* d_st_meta = nullptr;
   u64x2* d_st_ab = nullptr;
+  uint32_t* d_spos = nullptr;
+  uint8_t* d_rst_status = nullptr;
+  uint64_t* d_rst_value = nullptr;
   uint32_t* d_err = nullptr;
   uint64_t applied = 0;
   bool applied_pending = false;
@@ -115,7 +118,8 @@ static void free_all(cc_engine* e) {
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
   e->ev_pool.clear();
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta, e->d_val_v, e->d_counts, e->d_tot,
-                  e->d_base,     e->d_st_meta,  e->d_st_ab,    e->d_err,   e->d_last_index};
+                  e->d_base,     e->d_st_meta,  e->d_st_ab,    e->d_err,   e->d_last_index,
+                  e->d_spos,     e->d_rst_status, e->d_rst_value};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -126,26 +130,28 @@ extern "C" const char* cc_last_error(void) { return g_err.c_str(); }
 
 extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if (!cfg || !out) return set_err(CC_ERR_INVALID, "null config");
-  if (cfg->max_resources == 0 || cfg->max_resources > (uint32_t)kMaxBuckets * kResPerBucket)
-    return set_err(CC_ERR_CAPACITY, "max_resources must be in [1, 262144]");
+  if (cfg->max_resources == 0 || cfg->max_resources > (uint32_t)kMaxSb << kSbShift)
+    return set_err(CC_ERR_CAPACITY, "max_resources must be in [1, 131072]");
   if (cfg->max_instances == 0 || cfg->max_batch == 0) return set_err(CC_ERR_INVALID, "max_instances/max_batch must be > 0");
   cc_engine* e = new cc_engine();
   e->cfg = *cfg;
   e->device = cfg->device;
   hipError_t he = hipSetDevice(e->device);
   if (he != hipSuccess) { delete e; return set_err(CC_ERR_HIP, "hipSetDevice", he); }
-  e->nb = (cfg->max_resources + kResPerBucket - 1) / kResPerBucket;
-  e->nbits = 0;
-  while ((1u << e->nbits) < e->nb) ++e->nbits;
-  e->sub_batch = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
-  e->sub_batch = std::min<uint64_t>(e->sub_batch, cfg->max_batch);
-  e->sub_batch = std::max<uint64_t>(e->sub_batch, 1);
-  if (e->sub_batch > 0xFFFFFFFFull) e->sub_batch = 0xFFFFFFFFull & ~(uint64_t)(kTile - 1);
-  e->max_tiles = (e->sub_batch + kTile - 1) / kTile;
-  const uint64_t slots = (uint64_t)e->nb * kResPerBucket;
+  e->sb = (cfg->max_resources + (1u << kSbShift) - 1) >> kSbShift;
+  e->sb_bits = 0;
+  while ((1u << e->sb_bits) < e->sb) ++e->sb_bits;
+  // sub-batch: a multiple of the partition tile (keeps every sub-batch start 16 KiB-aligned)
+  uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
+  sub = std::min<uint64_t>(sub, cfg->max_batch);
+  sub = (sub + kTile - 1) / kTile * kTile;
+  sub = std::min<uint64_t>(sub, (uint64_t)1 << 31);
+  e->sub_batch = sub;
+  e->max_tiles = sub / kTile;
+  const uint64_t slots = (uint64_t)e->sb << kSbShift;
   e->res_type.assign(slots, CC_RES_NONE);
-  e->bucket_type.assign(e->nb, CC_RES_NONE);
-  e->bucket_live.assign(e->nb, 0);
+  e->bucket_type.assign(slots / kLaneRes, CC_RES_NONE);
+  e->bucket_live.assign(slots / kLaneRes, 0);
   e->inst_res.assign(cfg->max_instances, kNoRes);
   e->inst_id.assign(cfg->max_instances, 0);
   e->inst_client.assign(cfg->max_instances, 0);
@@ -163,11 +169,14 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_res_type, slots);
   ALLOC(e->d_val_meta, sizeof(uint32_t) * slots);
   ALLOC(e->d_val_v, sizeof(uint64_t) * slots);
-  ALLOC(e->d_counts, sizeof(uint32_t) * e->max_tiles * e->nb);
-  ALLOC(e->d_tot, sizeof(uint32_t) * e->nb);
-  ALLOC(e->d_base, sizeof(uint32_t) * e->nb);
-  ALLOC(e->d_st_meta, sizeof(uint64_t) * e->sub_batch);
+  ALLOC(e->d_counts, sizeof(uint32_t) * e->max_tiles * e->sb);
+  ALLOC(e->d_tot, sizeof(uint32_t) * e->sb);
+  ALLOC(e->d_base, sizeof(uint32_t) * e->sb);
+  ALLOC(e->d_st_meta, sizeof(uint32_t) * e->sub_batch);
   ALLOC(e->d_st_ab, sizeof(u64x2) * e->sub_batch);
+  ALLOC(e->d_spos, sizeof(uint32_t) * e->sub_batch);
+  ALLOC(e->d_rst_status, e->sub_batch);
+  ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
   ALLOC(e->d_err, sizeof(uint32_t));
   ALLOC(e->d_last_index, sizeof(uint64_t));
 #undef ALLOC
@@ -234,7 +243,7 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");
   for (uint64_t s = first; s < end; ++s) {
     if (e->res_type[s] != CC_RES_NONE) return set_err(CC_ERR_INVALID, "resource slot already in use");
-    const uint32_t b = (uint32_t)(s / kResPerBucket);
+    const uint32_t b = (uint32_t)(s / kLaneRes);
     if (e->bucket_type[b] != CC_RES_NONE && e->bucket_type[b] != type)
       return set_err(CC_ERR_INVALID, "a 64-slot bucket holds one resource type (allocate slots per type in groups of 64)");
   }
@@ -242,7 +251,7 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   if (rc) return rc;
   for (uint64_t s = first; s < end; ++s) {
     e->res_type[s] = (uint8_t)type;
-    const uint32_t b = (uint32_t)(s / kResPerBucket);
+    const uint32_t b = (uint32_t)(s / kLaneRes);
     e->bucket_type[b] = (uint8_t)type;
     e->bucket_live[b]++;
   }
@@ -269,7 +278,7 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   if (rc) return rc;
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
   e->res_type[slot] = CC_RES_NONE;
-  const uint32_t b = slot / kResPerBucket;
+  const uint32_t b = slot / kLaneRes;
   if (--e->bucket_live[b] == 0) e->bucket_type[b] = CC_RES_NONE;
   HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
   HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
@@ -326,6 +335,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   hipStream_t st = stream ? (hipStream_t)stream : e->own_stream;
   if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
   e->last_stream = st;
+  if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15))
+    return set_err(CC_ERR_INVALID, "status must be 4-byte and value 16-byte aligned");
   for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
     const uint64_t hi = std::min(n, lo + e->sub_batch);
     PartArgs pa{};
@@ -335,18 +346,18 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.a = c->a;
     pa.b = c->b;
     pa.lo = lo;
-    pa.n = hi;
+    pa.hi = hi;
     pa.inst_res = e->d_inst_res;
     pa.max_inst = e->cfg.max_instances;
-    pa.nb = e->nb;
-    pa.nbits = e->nbits;
+    pa.sb = e->sb;
+    pa.sb_shift = kSbShift;
+    pa.sb_bits = e->sb_bits;
     pa.counts = e->d_counts;
     pa.tot = e->d_tot;
     pa.base = e->d_base;
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
-    pa.out_status = out->status;
-    pa.out_value = out->value;
+    pa.spos = e->d_spos;
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
     ValueArgs va{};
@@ -354,14 +365,24 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.st_ab = e->d_st_ab;
     va.base = e->d_base;
     va.tot = e->d_tot;
-    va.nb = e->nb;
+    va.sb = e->sb;
     va.val_meta = e->d_val_meta;
     va.val_v = e->d_val_v;
-    va.out_status = out->status + lo;
-    va.out_value = out->value + lo;
+    va.rst_status = e->d_rst_status;
+    va.rst_value = e->d_rst_value;
     va.err = e->d_err;
     va.mark = marker_of(e);
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
+    UnpermuteArgs ua{};
+    ua.spos = e->d_spos;
+    ua.lo = lo;
+    ua.hi = hi;
+    ua.rst_status = e->d_rst_status;
+    ua.rst_value = e->d_rst_value;
+    ua.out_status = out->status;
+    ua.out_value = out->value;
+    ua.mark = marker_of(e);
+    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
   }
   if (c->index) {  // the applied watermark = index of the batch's last entry
     HIPCHECK(hipMemcpyAsync(e->d_last_index, c->index + (n - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
@@ -452,7 +473,8 @@ extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count,
   return CC_OK;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_part_count", "k_part_scan", "k_part_base", "k_part_scatter", "k_apply_value"};
+static const char* kKernelNames[K_NUM] = {"k_part_count", "k_part_scan", "k_part_base", "k_part_scatter", "k_apply_value",
+                                          "k_unpermute"};
 
 extern "C" int cc_profile_enable(cc_engine* e, int on) {
   if (!e) return CC_ERR_INVALID;

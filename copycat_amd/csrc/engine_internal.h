@@ -5,7 +5,7 @@
 namespace cc {
 
 // Optional per-kernel timing (HIP events recorded on the launch stream around each kernel).
-enum KernelId { K_PART_COUNT = 0, K_PART_SCAN, K_PART_BASE, K_PART_SCATTER, K_APPLY_VALUE, K_NUM };
+enum KernelId { K_PART_COUNT = 0, K_PART_SCAN, K_PART_BASE, K_PART_SCATTER, K_APPLY_VALUE, K_UNPERMUTE, K_NUM };
 struct Marker {
   void (*fn)(void* ctx, int kernel, int begin, hipStream_t st);
   void* ctx;
@@ -14,41 +14,53 @@ struct Marker {
   }
 };
 
-// One sub-batch [lo, n) of a batch (absolute row indices; column and output pointers are whole-batch).
+// One sub-batch [lo, hi) of a batch (absolute row indices; column pointers are whole-batch; staging buffers
+// are indexed relative to lo).
 struct PartArgs {
   const uint32_t* inst;
   const uint8_t* op;
   const uint8_t* flags;
   const uint64_t* a;
   const uint64_t* b;
-  uint64_t lo, n;
+  uint64_t lo, hi;
   const uint32_t* inst_res;
   uint32_t max_inst;
-  uint32_t nb, nbits;
-  uint32_t* counts;  // [tiles][nb]
-  uint32_t* tot;     // [nb]
-  uint32_t* base;    // [nb]
-  uint64_t* st_meta;
+  uint32_t sb, sb_shift, sb_bits;  // super-buckets
+  uint32_t* counts;  // [tiles][sb]
+  uint32_t* tot;     // [sb]
+  uint32_t* base;    // [sb]
+  uint32_t* st_meta; // staging records [sub_batch]
   u64x2* st_ab;
-  uint8_t* out_status;
-  uint64_t* out_value;
+  uint32_t* spos;    // [sub_batch] staging position of commit lo+i (kNoRes: unknown session)
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
+size_t scatter_lds_bytes(uint32_t sb);
 
 struct ValueArgs {
-  const uint64_t* st_meta;
+  const uint32_t* st_meta;
   const u64x2* st_ab;
   const uint32_t* base;
   const uint32_t* tot;
-  uint32_t nb;
-  uint32_t* val_meta;   // [nb*64]
-  uint64_t* val_v;      // [nb*64]
-  uint8_t* out_status;  // offset to the sub-batch start
-  uint64_t* out_value;
+  uint32_t sb;
+  uint32_t* val_meta;    // [sb*256]
+  uint64_t* val_v;       // [sb*256]
+  uint8_t* rst_status;   // staged results [sub_batch]
+  uint64_t* rst_value;
   uint32_t* err;
   Marker mark;
 };
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
+
+struct UnpermuteArgs {
+  const uint32_t* spos;
+  uint64_t lo, hi;
+  const uint8_t* rst_status;
+  const uint64_t* rst_value;
+  uint8_t* out_status;  // whole-batch outputs
+  uint64_t* out_value;
+  Marker mark;
+};
+int launch_unpermute(const UnpermuteArgs& a, hipStream_t st);
 
 }  // namespace cc

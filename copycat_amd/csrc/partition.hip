@@ -1,18 +1,21 @@
-// partition.hip — stable group-by of a commit batch into per-bucket lists (bucket = resource slot / 64).
+// partition.hip — stable group-by of a commit batch into per-super-bucket lists (super-bucket = 256 resource
+// slots = one apply workgroup), written as contiguous runs.
 //
 // Why: the reference applies commits one at a time in log order on one thread (ResourceManager.java:56-72);
 // commits on DIFFERENT resources are independent (ResourceManager multiplexes isolated state machines,
 // ResourceManager.java:37-39) but commits on the SAME resource form a sequential chain.  The engine therefore
-// regroups a batch so that one wave owns 64 resources and sees exactly their commits, still in log order.
+// regroups a batch so that one workgroup owns 256 resources and sees exactly their commits, in log order.
 //
-// Pipeline per sub-batch (all kernels stream their inputs coalesced; no global atomics):
-//   k_part_count   : per 16384-commit tile, a histogram over buckets (LDS atomics) -> counts[tile][bucket]
-//   k_part_scan    : per 64-bucket stripe, exclusive prefix over tiles (in place) + bucket totals
-//   k_part_base    : exclusive scan of bucket totals -> bucket base offsets
-//   k_part_scatter : per tile, stable multisplit: each wave walks its 4096 commits in steps of 64, ranks
-//                    same-bucket lanes with ballots, and writes 24-byte staging records at
-//                    base[b] + tile_prefix[b] + wave_prefix[b] + rank.  Commits on unknown instances get
-//                    their UNKNOWN_SESSION status here (ResourceManager.java:60-69).
+// Pipeline per sub-batch [lo, hi) (no global atomics; every global access coalesced):
+//   k_part_count   : per 16384-commit tile, a histogram over super-buckets (LDS atomics) -> counts[tile][sb]
+//   k_part_scan    : per 64-super-bucket stripe, exclusive prefix over tiles (in place) + totals
+//   k_part_base    : exclusive scan of the totals -> super-bucket base offsets in the staging list
+//   k_part_scatter : per tile, 4 chunks of 4096 commits: a stable multisplit of the chunk in LDS (ballot
+//                    ranking inside a wave, per-wave prefix sums across the 16 waves), then the chunk is
+//                    written out super-bucket by super-bucket, so every staging run is contiguous (no
+//                    partial-line writes), plus spos[i] = staging position of commit i for k_unpermute.
+//   k_unpermute    : out[i] = result_staged[spos[i]] (coalesced in log order; unknown sessions get their
+//                    UNKNOWN_SESSION status here, ResourceManager.java:60-69).
 #include "common.h"
 #include "engine_internal.h"
 
@@ -23,25 +26,25 @@ __device__ inline uint32_t resolve(const uint32_t* __restrict__ inst_res, uint32
   return s < max_inst ? inst_res[s] : kNoRes;
 }
 
-__global__ __launch_bounds__(kPartThreads) void k_part_count(const uint32_t* __restrict__ inst, uint64_t lo, uint64_t n,
-                                                          const uint32_t* __restrict__ inst_res, uint32_t max_inst,
-                                                          uint32_t nb, uint32_t* __restrict__ counts) {
-  extern __shared__ uint32_t hist[];  // [nb]
-  for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) hist[b] = 0;
+__global__ __launch_bounds__(kPT) void k_part_count(const uint32_t* __restrict__ inst, uint64_t lo, uint64_t hi,
+                                                 const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
+                                                 uint32_t sb_shift, uint32_t* __restrict__ counts) {
+  extern __shared__ uint32_t hist[];  // [sb]
+  for (uint32_t b = threadIdx.x; b < sb; b += kPT) hist[b] = 0;
   __syncthreads();
   const uint64_t t0 = lo + (uint64_t)blockIdx.x * kTile;
-  const uint64_t t1 = t0 + kTile < n ? t0 + kTile : n;
-  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
+  const uint64_t t1 = t0 + kTile < hi ? t0 + kTile : hi;
+  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPT) {
     const uint32_t r = resolve(inst_res, max_inst, inst[i]);
-    if (r != kNoRes) atomicAdd(&hist[r >> kBucketShift], 1u);
+    if (r != kNoRes) atomicAdd(&hist[r >> sb_shift], 1u);
   }
   __syncthreads();
-  uint32_t* row = counts + (uint64_t)blockIdx.x * nb;
-  for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) row[b] = hist[b];
+  uint32_t* row = counts + (uint64_t)blockIdx.x * sb;
+  for (uint32_t b = threadIdx.x; b < sb; b += kPT) row[b] = hist[b];
 }
 
-// One 1024-thread workgroup per stripe of 64 buckets: 16 row groups x 64 bucket lanes.
-__global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ counts, uint32_t tiles, uint32_t nb,
+// One 1024-thread workgroup per stripe of 64 columns: 16 row groups x 64 column lanes.
+__global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ counts, uint32_t tiles, uint32_t cols,
                                                    uint32_t* __restrict__ tot) {
   __shared__ uint32_t part[kScanGroups][kWave];
   const uint32_t l = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -50,140 +53,249 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ count
   const uint32_t r0 = g * per;
   const uint32_t r1 = r0 + per < tiles ? r0 + per : tiles;
   uint32_t s = 0;
-  if (b < nb)
-    for (uint32_t t = r0; t < r1; ++t) s += counts[(uint64_t)t * nb + b];
+  if (b < cols)
+    for (uint32_t t = r0; t < r1; ++t) s += counts[(uint64_t)t * cols + b];
   part[g][l] = s;
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t q = 0; q < g; ++q) pre += part[q][l];
-  if (g == kScanGroups - 1 && b < nb) tot[b] = pre + s;
-  if (b < nb)
+  if (g == kScanGroups - 1 && b < cols) tot[b] = pre + s;
+  if (b < cols)
     for (uint32_t t = r0; t < r1; ++t) {
-      const uint64_t k = (uint64_t)t * nb + b;
+      const uint64_t k = (uint64_t)t * cols + b;
       const uint32_t c = counts[k];
       counts[k] = pre;
       pre += c;
     }
 }
 
-// Exclusive scan of nb (<= 4096) bucket totals in one 1024-thread workgroup.
-__global__ __launch_bounds__(1024) void k_part_base(const uint32_t* __restrict__ tot, uint32_t nb, uint32_t* __restrict__ base) {
-  __shared__ uint32_t wsum[16];
+// Exclusive scan of one value per thread of a block of up to 1024 threads; every thread must call it.
+// Returns the exclusive prefix of this thread and writes the block total to *total.
+__device__ inline uint32_t block_exscan(uint32_t v, uint32_t* wsum /*[16] LDS*/, uint32_t* total) {
   const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
-  uint32_t v[4], s = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t i = t * 4 + k;
-    v[k] = i < nb ? tot[i] : 0;
-    s += v[k];
-  }
-  // inclusive wave scan of s
-  uint32_t inc = s;
+  uint32_t inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(inc, d, 64);
     if (l >= (uint32_t)d) inc += y;
   }
+  __syncthreads();  // wsum may still be read by a previous call
   if (l == 63) wsum[w] = inc;
   __syncthreads();
-  uint32_t wpre = 0;
-  for (uint32_t q = 0; q < w; ++q) wpre += wsum[q];
-  uint32_t run = wpre + inc - s;
+  uint32_t wpre = 0, all = 0;
+  for (uint32_t q = 0; q < blockDim.x / 64; ++q) {
+    const uint32_t x = wsum[q];
+    if (q < w) wpre += x;
+    all += x;
+  }
+  *total = all;
+  return wpre + inc - v;
+}
+
+// Exclusive scan of the super-bucket totals (<= 4096, 4 per thread) -> base offsets.
+__global__ __launch_bounds__(1024) void k_part_base(const uint32_t* __restrict__ tot, uint32_t cols, uint32_t* __restrict__ base) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x;
+  uint32_t v[4], s = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t i = t * 4 + k;
-    if (i < nb) base[i] = run;
+    v[k] = i < cols ? tot[i] : 0;
+    s += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_exscan(s, wsum, &total);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = t * 4 + k;
+    if (i < cols) base[i] = run;
     run += v[k];
   }
 }
 
-__global__ __launch_bounds__(kPartThreads) void k_part_scatter(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
-                                                            const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
-                                                            const uint64_t* __restrict__ cb, uint64_t lo, uint64_t n,
-                                                            const uint32_t* __restrict__ inst_res, uint32_t max_inst,
-                                                            uint32_t nb, uint32_t nbits, const uint32_t* __restrict__ offs,
-                                                            const uint32_t* __restrict__ base, uint64_t* __restrict__ st_meta,
-                                                            u64x2* __restrict__ st_ab, uint8_t* __restrict__ out_status,
-                                                            uint64_t* __restrict__ out_value) {
-  extern __shared__ uint32_t woff_flat[];  // [kPartWaves][nb]
-  auto woff = [&](uint32_t q, uint32_t b) -> uint32_t& { return woff_flat[q * nb + b]; };
-  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
-  const uint64_t w0 = tile0 + (uint64_t)w * kWaveTile;
-  const uint64_t w1 = w0 + kWaveTile < n ? w0 + kWaveTile : n;
+size_t scatter_lds_bytes(uint32_t sb) {
+  return (size_t)kChunk * (16 + 4 + 2) + (size_t)kPW * sb * 4 + (size_t)4 * sb * 4 + 16 * 4;
+}
 
-  // phase 1: per-wave bucket counts of this wave's 4096-commit sub-tile
-  for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads)
-#pragma unroll
-    for (int q = 0; q < kPartWaves; ++q) woff(q, b) = 0;
-  __syncthreads();
-  for (uint64_t i = w0 + l; i < w1; i += kWave) {
-    const uint32_t r = resolve(inst_res, max_inst, inst[i]);
-    if (r != kNoRes) atomicAdd(&woff(w, r >> kBucketShift), 1u);
-  }
-  __syncthreads();
-  // phase 2: wave-level exclusive offsets = bucket base + tile prefix + earlier waves of this tile
-  const uint32_t* trow = offs + (uint64_t)blockIdx.x * nb;
-  for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) {
-    uint32_t run = base[b] + trow[b];
-#pragma unroll
-    for (int q = 0; q < kPartWaves; ++q) {
-      const uint32_t c = woff(q, b);
-      woff(q, b) = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  // phase 3: stable scatter, 64 commits per step, same-bucket lanes ranked by ballot
-  uint32_t* my = woff_flat + w * nb;
+// LDS layout (dynamic): rab[kChunk] u64x2 | rmeta[kChunk] u32 | rsb[kChunk] u16 | wc[kPW][sb] u32 |
+//                       toff, trun, ctot, kstart [sb] u32 | wsum[16] u32
+__global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                   const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
+                                                   const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
+                                                   const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
+                                                   uint32_t sb_shift, uint32_t sb_bits, const uint32_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ base, uint32_t* __restrict__ st_meta,
+                                                   u64x2* __restrict__ st_ab, uint32_t* __restrict__ spos) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  u64x2* rab = reinterpret_cast<u64x2*>(smem);
+  uint32_t* rmeta = reinterpret_cast<uint32_t*>(rab + kChunk);
+  uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + kChunk);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + kChunk);  // [kPW][sb]
+  uint32_t* toff = wc + kPW * sb;
+  uint32_t* trun = toff + sb;
+  uint32_t* ctot = trun + sb;
+  uint32_t* kstart = ctot + sb;
+  uint32_t* wsum = kstart + sb;
+
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t lt = lanemask_lt();
-  for (uint64_t s0 = w0; s0 < w1; s0 += kWave) {
-    const uint64_t i = s0 + l;
-    const bool in = i < w1;
-    const uint32_t r = in ? resolve(inst_res, max_inst, inst[i]) : kNoRes;
-    const bool live = r != kNoRes;
-    if (in && !live) {  // ResourceManagerException "unknown resource session" (ResourceManager.java:64-68)
-      out_status[i] = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
-      out_value[i] = 0;
+  const uint32_t rmask = (1u << sb_shift) - 1;
+  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
+  const uint32_t* trow = offs + (uint64_t)blockIdx.x * sb;
+  for (uint32_t k = t; k < sb; k += kPT) {
+    toff[k] = base[k] + trow[k];
+    trun[k] = 0;
+  }
+
+  constexpr int J = kChunk / kPT;  // commits per thread per chunk
+  for (uint32_t ch = 0; ch < kTile / kChunk; ++ch) {
+    const uint64_t cbase = tile0 + (uint64_t)ch * kChunk;
+    if (cbase >= hi) break;  // block-uniform
+    for (uint32_t k = t; k < kPW * sb; k += kPT) wc[k] = 0;
+    __syncthreads();
+    // 1. wave w ranks commits cbase + w*(64*J) + j*64 + l (log order = (w, j, l)) by super-bucket
+    uint32_t key[J], loc[J], meta[J];
+    u64x2 ab[J];
+    bool live[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      const bool in = i < hi;
+      const uint32_t r = in ? resolve(inst_res, max_inst, inst[i]) : kNoRes;
+      live[j] = r != kNoRes;
+      key[j] = live[j] ? (r >> sb_shift) : 0;
+      meta[j] = 0;
+      ab[j] = u64x2{0, 0};
+      if (in) {
+        if (!live[j]) spos[i - lo] = kNoRes;
+        meta[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8) | ((r & rmask) << 16);
+        ab[j].x = ca[i];
+        ab[j].y = cb[i];
+      }
+      uint64_t peers = ballot(live[j]);
+      for (uint32_t k = 0; k < sb_bits; ++k) {
+        const bool bit = (key[j] >> k) & 1u;
+        const uint64_t m = ballot(live[j] && bit);
+        peers &= bit ? m : ~m;
+      }
+      uint32_t b0 = 0;
+      if (live[j]) b0 = wc[w * sb + key[j]];
+      loc[j] = b0 + (uint32_t)__popcll(peers & lt);
+      if (live[j] && (peers & lt) == 0) wc[w * sb + key[j]] = b0 + (uint32_t)__popcll(peers);
     }
-    const uint32_t b = live ? (r >> kBucketShift) : 0;
-    uint64_t peers = ballot(live);
-    for (uint32_t k = 0; k < nbits; ++k) {
-      const bool bit = (b >> k) & 1u;
-      const uint64_t m = ballot(live && bit);
-      peers &= bit ? m : ~m;
+    __syncthreads();
+    // 2. per super-bucket: exclusive prefix over waves and chunk totals; then chunk-sorted starts
+    for (uint32_t k = t; k < sb; k += kPT) {
+      uint32_t run = 0;
+      for (uint32_t q = 0; q < kPW; ++q) {
+        const uint32_t c = wc[q * sb + k];
+        wc[q * sb + k] = run;
+        run += c;
+      }
+      ctot[k] = run;
     }
-    uint32_t dst = 0;
-    if (live) dst = my[b] + (uint32_t)__popcll(peers & lt);
-    if (live && (peers & lt) == 0) my[b] += (uint32_t)__popcll(peers);
-    if (live) {
-      st_meta[dst] = pack_meta((uint32_t)(i - lo), op[i], flags[i], r & (kResPerBucket - 1));
-      u64x2 ab;
-      ab.x = ca[i];
-      ab.y = cb[i];
-      st_ab[dst] = ab;
+    __syncthreads();
+    uint32_t nlive = 0;
+    for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform loop
+      const uint32_t k = k0 + t;
+      uint32_t part;
+      const uint32_t ex = block_exscan(k < sb ? ctot[k] : 0, wsum, &part);
+      if (k < sb) kstart[k] = nlive + ex;
+      nlive += part;
     }
+    __syncthreads();
+    // 3. place records in LDS in sorted order; remember each commit's staging position
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      if (!live[j]) continue;
+      const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      const uint32_t within = wc[w * sb + key[j]] + loc[j];
+      const uint32_t s = kstart[key[j]] + within;
+      rab[s] = ab[j];
+      rmeta[s] = meta[j];
+      rsb[s] = (uint16_t)key[j];
+      spos[i - lo] = toff[key[j]] + trun[key[j]] + within;
+    }
+    __syncthreads();
+    // 4. write the chunk out super-bucket by super-bucket (contiguous runs)
+    for (uint32_t s = t; s < nlive; s += kPT) {
+      const uint32_t k = rsb[s];
+      const uint32_t g = toff[k] + trun[k] + (s - kstart[k]);
+      st_meta[g] = rmeta[s];
+      st_ab[g] = rab[s];
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
+    __syncthreads();
+  }
+}
+
+// out[i] = staged result of commit i (4 commits per thread: 16 B spos loads, coalesced stores).
+__global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ spos, uint64_t n,
+                                                   const uint8_t* __restrict__ rst_status,
+                                                   const uint64_t* __restrict__ rst_value, uint8_t* __restrict__ out_status,
+                                                   uint64_t* __restrict__ out_value) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t quads = n / 4;
+  const uint8_t unk = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += stride) {
+    const uint4 p = reinterpret_cast<const uint4*>(spos)[q];
+    const uint32_t pp[4] = {p.x, p.y, p.z, p.w};
+    uint32_t sw = 0;
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint8_t s = unk;
+      v[k] = 0;
+      if (pp[k] != kNoRes) {
+        s = rst_status[pp[k]];
+        v[k] = rst_value[pp[k]];
+      }
+      sw |= (uint32_t)s << (8 * k);
+    }
+    reinterpret_cast<uint32_t*>(out_status)[q] = sw;
+    u64x2* ov = reinterpret_cast<u64x2*>(out_value) + 2 * q;
+    ov[0] = u64x2{v[0], v[1]};
+    ov[1] = u64x2{v[2], v[3]};
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const uint64_t i = quads * 4 + threadIdx.x;
+    const uint32_t p = spos[i];
+    out_status[i] = p != kNoRes ? rst_status[p] : unk;
+    out_value[i] = p != kNoRes ? rst_value[p] : 0;
   }
 }
 
 int launch_partition(const PartArgs& a, hipStream_t st) {
-  const uint32_t tiles = (uint32_t)((a.n - a.lo + kTile - 1) / kTile);
+  const uint32_t tiles = (uint32_t)((a.hi - a.lo + kTile - 1) / kTile);
   if (tiles == 0) return 0;
   a.mark(K_PART_COUNT, 1, st);
-  hipLaunchKernelGGL(k_part_count, dim3(tiles), dim3(kPartThreads), a.nb * sizeof(uint32_t), st, a.inst, a.lo, a.n,
-                     a.inst_res, a.max_inst, a.nb, a.counts);
+  hipLaunchKernelGGL(k_part_count, dim3(tiles), dim3(kPT), a.sb * sizeof(uint32_t), st, a.inst, a.lo, a.hi, a.inst_res,
+                     a.max_inst, a.sb, a.sb_shift, a.counts);
   a.mark(K_PART_COUNT, 0, st);
   a.mark(K_PART_SCAN, 1, st);
-  hipLaunchKernelGGL(k_part_scan, dim3((a.nb + kWave - 1) / kWave), dim3(1024), 0, st, a.counts, tiles, a.nb, a.tot);
+  hipLaunchKernelGGL(k_part_scan, dim3((a.sb + kWave - 1) / kWave), dim3(1024), 0, st, a.counts, tiles, a.sb, a.tot);
   a.mark(K_PART_SCAN, 0, st);
   a.mark(K_PART_BASE, 1, st);
-  hipLaunchKernelGGL(k_part_base, dim3(1), dim3(1024), 0, st, a.tot, a.nb, a.base);
+  hipLaunchKernelGGL(k_part_base, dim3(1), dim3(1024), 0, st, a.tot, a.sb, a.base);
   a.mark(K_PART_BASE, 0, st);
   a.mark(K_PART_SCATTER, 1, st);
-  hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(kPartThreads), kPartWaves * a.nb * sizeof(uint32_t), st, a.inst,
-                     a.op, a.flags, a.a, a.b, a.lo, a.n, a.inst_res, a.max_inst, a.nb, a.nbits, a.counts, a.base,
-                     a.st_meta, a.st_ab, a.out_status, a.out_value);
+  hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(kPT), scatter_lds_bytes(a.sb), st, a.inst, a.op, a.flags, a.a, a.b,
+                     a.lo, a.hi, a.inst_res, a.max_inst, a.sb, a.sb_shift, a.sb_bits, a.counts, a.base, a.st_meta, a.st_ab,
+                     a.spos);
   a.mark(K_PART_SCATTER, 0, st);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_unpermute(const UnpermuteArgs& a, hipStream_t st) {
+  const uint64_t n = a.hi - a.lo;
+  uint64_t grid = (n / 4 + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  a.mark(K_UNPERMUTE, 1, st);
+  hipLaunchKernelGGL(k_unpermute, dim3((uint32_t)grid), dim3(256), 0, st, a.spos, n, a.rst_status, a.rst_value,
+                     a.out_status + a.lo, a.out_value + a.lo);
+  a.mark(K_UNPERMUTE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

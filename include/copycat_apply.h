@@ -135,7 +135,7 @@ extern "C" {
 
 /* ---- engine configuration ------------------------------------------------------------------------ */
 typedef struct cc_config {
-  uint32_t max_resources;   /* resource slots (ResourceManager.resources)                      */
+  uint32_t max_resources;   /* resource slots (ResourceManager.resources), <= 131072            */
   uint32_t max_instances;   /* instance-session slots (ResourceManager.sessions)               */
   uint64_t max_batch;       /* max commits per cc_apply_batch call                               */
   uint64_t max_events;      /* capacity of the device event stream per batch                      */
@@ -217,6 +217,7 @@ int  cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t count, uint32
  * Apply n committed entries (device-resident columns) in log order.  Replaces the per-entry chain
  * ResourceManager.operateResource (ResourceManager.java:56-72) -> executors -> state machine method.
  * `events` may be NULL when no op in the batch publishes (then publishing ops fail with CC_ERR_UNSUPPORTED). */
+/* d_out->status must be 4-byte aligned and d_out->value 16-byte aligned (hipMalloc / torch allocations are). */
 int  cc_apply_batch(cc_engine* e, const cc_batch* d_cols, uint64_t n, const cc_results* d_out,
                     const cc_events* d_events, void* stream);
 /* Same with host columns/results: H2D, apply, D2H, sync (PCIe-inclusive path). */
@@ -230,8 +231,9 @@ int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* 
                          uint8_t* h_has_current);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
- * kernel ids: 0 k_part_count, 1 k_part_scan, 2 k_part_base, 3 k_part_scatter, 4 k_apply_value.           */
-#define CC_PROFILE_KERNELS 5
+ * kernel ids: 0 k_part_count, 1 k_part_scan, 2 k_part_base, 3 k_part_scatter, 4 k_apply_value,
+ * 5 k_unpermute.                                                                                          */
+#define CC_PROFILE_KERNELS 6
 int  cc_profile_enable(cc_engine* e, int on);
 int  cc_profile_reset(cc_engine* e);
 /* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */
