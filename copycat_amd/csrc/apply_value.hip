@@ -1,15 +1,12 @@
 // apply_value.hip — AtomicValueState apply (also DistributedAtomicLong, whose add is a client-side CAS loop).
 //
-// One 256-thread workgroup owns one super-bucket = 256 AtomicValueState instances, held in LDS for the whole
-// launch.  It walks the super-bucket's staging list (log order, built by partition.hip) in chunks of 2048
-// records, prefetching the next chunk into registers while it resolves the current one:
-//   1. a stable 2-bit multisplit of the chunk in LDS hands wave w exactly the records of its 64 slots;
-//   2. each wave resolves its records 64 at a time, IN LOG ORDER, with ballots:
-//        peers(j) = lanes whose record targets the same slot as lane j   (6 ballots over the slot bits)
-//        rank(j)  = popcount(peers(j) & lanes-below-j)                    (position in that chain)
-//      round k applies every record of rank k — all on distinct slots — as an LDS read-modify-write;
-//   3. the chunk's results are staged in LDS and written back contiguously (staging order); k_unpermute
-//      later returns them to log order.
+// One 256-thread workgroup owns one super-bucket = 256 AtomicValueState instances: thread t holds slot t's
+// state in registers for the whole launch.  It walks the super-bucket's staging list (log order, built by
+// partition.hip) in chunks of 2048 records, prefetching the next chunk into registers while it resolves the
+// current one: a stable counting sort of the chunk by slot (ballot ranking + per-slot prefix sums in LDS)
+// gives every slot its commits in log order, and each thread applies its slot's chain sequentially — the
+// same order the reference's single state-machine thread would (ResourceManager.java:56-72).  Results are
+// staged in LDS and written back contiguously in staging order; k_unpermute returns them to log order.
 //
 // Per-op semantics restate AtomicValueState (atomic/src/main/java/io/atomix/atomic/state/AtomicValueState.java):
 //   get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144, delete :146-157.
@@ -75,31 +72,36 @@ __device__ inline uint32_t value_apply(uint32_t op, uint32_t flags, uint64_t a, 
   }
 }
 
-constexpr int kAT = kApplyWaves * kWave;  // 256 threads
+constexpr int kAT = kApplyWaves * kWave;  // 256 threads = 256 slots of the super-bucket
 constexpr int kACh = kAT * kApplyPer;     // 2048 records per chunk
 constexpr int kSbSlots = kApplyWaves * kLaneRes;
+constexpr int kGroups = kApplyPer * kApplyWaves;  // (j, wave) groups of 64 records, in log order
 
+// One workgroup per super-bucket; thread t owns slot t (its AtomicValueState lives in two registers).
+// Per chunk of 2048 staging records (record c = j*256 + t, log order = (j, wave, lane)):
+//   1. a stable counting sort of the chunk by slot: ballot ranking inside each (j, wave) group, per-group
+//      per-slot counts in LDS (tagged with the chunk number, so the table is never cleared), each owner
+//      thread scans its slot's 32 group counts, a block scan gives each slot's run start;
+//   2. thread t walks its slot's run sequentially — the reference's one-commit-at-a-time order, per slot;
+//   3. results go back through LDS to staging order and out contiguously.
 __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
                                                     const uint32_t* __restrict__ base, const uint32_t* __restrict__ tot,
                                                     uint32_t* __restrict__ val_meta, uint64_t* __restrict__ val_v,
                                                     uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                     uint32_t* __restrict__ err_out) {
-  __shared__ uint32_t smeta[kSbSlots];
-  __shared__ uint64_t sv[kSbSlots];
-  __shared__ u64x2 lab[kACh];
-  __shared__ uint32_t lmeta[kACh];
-  __shared__ uint16_t lidx[kACh];
+  __shared__ u64x2 sab[kACh];
+  __shared__ uint32_t sm[kACh];
+  __shared__ uint16_t sidx[kACh];
   __shared__ uint64_t rval[kACh];
   __shared__ uint8_t rstat[kACh];
-  __shared__ uint32_t gcnt[kApplyPer][kApplyWaves][kApplyWaves];
-  __shared__ uint32_t kseg[kApplyWaves + 1];
+  __shared__ uint32_t gcnt[kGroups][kSbSlots];  // (chunk+1) << 12 | value (count, then prefix); else stale
+  __shared__ uint32_t sstart[kSbSlots];
+  __shared__ uint32_t wsum[kApplyWaves];
 
   const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t lt = lanemask_lt();
-  for (uint32_t q = t; q < kSbSlots; q += kAT) {
-    smeta[q] = val_meta[(uint64_t)s * kSbSlots + q];
-    sv[q] = val_v[(uint64_t)s * kSbSlots + q];
-  }
+  ValState st_reg{val_meta[(uint64_t)s * kSbSlots + t], val_v[(uint64_t)s * kSbSlots + t]};
+  for (uint32_t q = t; q < kGroups * kSbSlots; q += kAT) (&gcnt[0][0])[q] = 0;
   const uint32_t lo = base[s], cnt = tot[s];
   uint32_t err = 0;
 
@@ -115,98 +117,80 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
       ab[j] = st_ab[lo + c];
     }
   }
+  __syncthreads();
+  uint32_t chunk_tag = 0;
   for (uint32_t c0 = 0; c0 < cnt; c0 += kACh) {
+    chunk_tag += 1u << 12;
+    // 1a. rank inside each (j, wave) group by slot (8 ballots); group leaders publish counts
+    uint32_t rank[kApplyPer], slot[kApplyPer];
+#pragma unroll
+    for (int j = 0; j < kApplyPer; ++j) {
+      const bool live = c0 + j * kAT + t < cnt;
+      slot[j] = smeta_slot(m[j]) & (kSbSlots - 1);
+      uint64_t peers = ballot(live);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool bit = (slot[j] >> k) & 1u;
+        const uint64_t mk = ballot(live && bit);
+        peers &= bit ? mk : ~mk;
+      }
+      rank[j] = live ? (uint32_t)__popcll(peers & lt) : 0xFFFFFFFFu;
+      if (live && (peers & lt) == 0) gcnt[j * kApplyWaves + w][slot[j]] = chunk_tag | (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // 1b. owner of slot t: exclusive prefix over the 32 groups; run length
+    uint32_t run = 0;
+#pragma unroll 8
+    for (int g = 0; g < kGroups; ++g) {
+      const uint32_t v = gcnt[g][t];
+      const uint32_t c = (v & ~0xFFFu) == chunk_tag ? (v & 0xFFFu) : 0;
+      gcnt[g][t] = chunk_tag | run;  // prefix, tagged
+      run += c;
+    }
+    // 1c. block exclusive scan of the run lengths -> run starts
+    uint32_t inc = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    if (l == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t start = inc - run;
+    for (uint32_t q = 0; q < w; ++q) start += wsum[q];
+    sstart[t] = start;
+    __syncthreads();
+    // 1d. place records in slot order
+#pragma unroll
+    for (int j = 0; j < kApplyPer; ++j) {
+      if (rank[j] == 0xFFFFFFFFu) continue;
+      const uint32_t p = sstart[slot[j]] + (gcnt[j * kApplyWaves + w][slot[j]] & 0xFFFu) + rank[j];
+      sm[p] = m[j];
+      sab[p] = ab[j];
+      sidx[p] = (uint16_t)(j * kAT + t);
+    }
+    __syncthreads();
     // prefetch the next chunk while this one resolves
-    uint32_t nm[kApplyPer];
-    u64x2 nab[kApplyPer];
 #pragma unroll
     for (int j = 0; j < kApplyPer; ++j) {
       const uint32_t c = c0 + kACh + j * kAT + t;
-      nm[j] = 0;
-      nab[j] = u64x2{0, 0};
+      m[j] = 0;
+      ab[j] = u64x2{0, 0};
       if (c < cnt) {
-        nm[j] = st_meta[lo + c];
-        nab[j] = st_ab[lo + c];
+        m[j] = st_meta[lo + c];
+        ab[j] = st_ab[lo + c];
       }
     }
-    // 1. stable multisplit of the chunk (order c = j*256 + t) by owning wave = slot >> 6
-    uint32_t rank[kApplyPer], key[kApplyPer];
-    bool live[kApplyPer];
-#pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      live[j] = c0 + j * kAT + t < cnt;
-      key[j] = (smeta_slot(m[j]) >> 6) & (kApplyWaves - 1);
-      const uint64_t lv = ballot(live[j]);
-      const uint64_t b0 = ballot(live[j] && (key[j] & 1));
-      const uint64_t b1 = ballot(live[j] && (key[j] & 2));
-      const uint64_t mk0 = lv & ~b0 & ~b1, mk1 = b0 & ~b1, mk2 = b1 & ~b0, mk3 = b0 & b1;
-      const uint64_t mine = key[j] == 0 ? mk0 : key[j] == 1 ? mk1 : key[j] == 2 ? mk2 : mk3;
-      rank[j] = (uint32_t)__popcll(mine & lt);
-      if (l < kApplyWaves) {
-        const uint64_t mk = l == 0 ? mk0 : l == 1 ? mk1 : l == 2 ? mk2 : mk3;
-        gcnt[j][w][l] = (uint32_t)__popcll(mk);
-      }
-    }
-    __syncthreads();
-    if (t < kApplyWaves) {
-      uint32_t run = 0;
-      for (int j = 0; j < kApplyPer; ++j)
-        for (int q = 0; q < kApplyWaves; ++q) {
-          const uint32_t c = gcnt[j][q][t];
-          gcnt[j][q][t] = run;
-          run += c;
-        }
-      kseg[t + 1] = run;  // segment sizes, prefixed below
-    }
-    __syncthreads();
-    if (t == 0) {
-      kseg[0] = 0;
-      for (int k = 1; k <= kApplyWaves; ++k) kseg[k] += kseg[k - 1];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      if (!live[j]) continue;
-      const uint32_t p = kseg[key[j]] + gcnt[j][w][key[j]] + rank[j];
-      lmeta[p] = m[j];
-      lab[p] = ab[j];
-      lidx[p] = (uint16_t)(j * kAT + t);
-    }
-    __syncthreads();
-    // 2. wave w resolves its segment against its 64 slots, in log order
-    const uint32_t seg_lo = kseg[w], seg_hi = kseg[w + 1];
-    for (uint32_t q0 = seg_lo; q0 < seg_hi; q0 += kWave) {
-      const uint32_t q = q0 + l;
-      const bool lv = q < seg_hi;
-      const uint32_t mm = lv ? lmeta[q] : 0;
-      const u64x2 abv = lv ? lab[q] : u64x2{0, 0};
-      const uint32_t rr = smeta_slot(mm) & 63;
-      uint64_t peers = ballot(lv);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const bool bit = (rr >> k) & 1u;
-        const uint64_t mk = ballot(lv && bit);
-        peers &= bit ? mk : ~mk;
-      }
-      const uint32_t rk = (uint32_t)__popcll(peers & lt);
-      const uint32_t si = w * kLaneRes + rr;
-      uint32_t st = 0;
-      uint64_t rv = 0;
-      bool pending = lv;
-      for (uint32_t k = 0; ballot(pending) != 0; ++k) {
-        if (pending && rk == k) {
-          ValState vs{smeta[si], sv[si]};
-          st = value_apply(smeta_op(mm), smeta_flags(mm), abv.x, abv.y, vs, rv, err);
-          smeta[si] = vs.meta;
-          sv[si] = vs.v;
-          pending = false;
-        }
-      }
-      if (lv) {
-        const uint32_t c = lidx[q];
-        rstat[c] = (uint8_t)st;
-        rval[c] = rv;
-      }
+    // 2. thread t applies its slot's commits in log order, state in registers
+    for (uint32_t k = 0; k < run; ++k) {
+      const uint32_t p = start + k;
+      const uint32_t mm = sm[p];
+      const u64x2 abv = sab[p];
+      uint64_t rv;
+      const uint32_t stt = value_apply(smeta_op(mm), smeta_flags(mm), abv.x, abv.y, st_reg, rv, err);
+      const uint32_t ci = sidx[p];
+      rstat[ci] = (uint8_t)stt;
+      rval[ci] = rv;
     }
     __syncthreads();
     // 3. results back in staging order, contiguous
@@ -216,16 +200,9 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
       rst_value[lo + c0 + c] = rval[c];
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      m[j] = nm[j];
-      ab[j] = nab[j];
-    }
   }
-  for (uint32_t q = t; q < kSbSlots; q += kAT) {
-    val_meta[(uint64_t)s * kSbSlots + q] = smeta[q];
-    val_v[(uint64_t)s * kSbSlots + q] = sv[q];
-  }
+  val_meta[(uint64_t)s * kSbSlots + t] = st_reg.meta;
+  val_v[(uint64_t)s * kSbSlots + t] = st_reg.v;
   if (err) atomicOr(err_out, err);
 }
 

@@ -58,7 +58,9 @@ struct cc_engine {
   uint32_t* d_base = nullptr;
   uint32_t* d_st_meta = nullptr;
   u64x2* d_st_ab = nullptr;
-  uint32_t* d_spos = nullptr;
+  uint16_t* d_cpos = nullptr;
+  uint16_t* d_ckst = nullptr;
+  uint32_t* d_crun = nullptr;
   uint8_t* d_rst_status = nullptr;
   uint64_t* d_rst_value = nullptr;
   uint32_t* d_err = nullptr;
@@ -119,7 +121,7 @@ static void free_all(cc_engine* e) {
   e->ev_pool.clear();
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta, e->d_val_v, e->d_counts, e->d_tot,
                   e->d_base,     e->d_st_meta,  e->d_st_ab,    e->d_err,   e->d_last_index,
-                  e->d_spos,     e->d_rst_status, e->d_rst_value};
+                  e->d_cpos,     e->d_ckst,     e->d_crun,     e->d_rst_status, e->d_rst_value};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -145,7 +147,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
   sub = std::min<uint64_t>(sub, cfg->max_batch);
   sub = (sub + kTile - 1) / kTile * kTile;
-  sub = std::min<uint64_t>(sub, (uint64_t)1 << 31);
+  sub = std::min<uint64_t>(sub, (uint64_t)1 << 30);
   e->sub_batch = sub;
   e->max_tiles = sub / kTile;
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
@@ -174,7 +176,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_base, sizeof(uint32_t) * e->sb);
   ALLOC(e->d_st_meta, sizeof(uint32_t) * e->sub_batch);
   ALLOC(e->d_st_ab, sizeof(u64x2) * e->sub_batch);
-  ALLOC(e->d_spos, sizeof(uint32_t) * e->sub_batch);
+  ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
+  ALLOC(e->d_ckst, sizeof(uint16_t) * (e->sub_batch / kChunk) * (e->sb + 1));
+  ALLOC(e->d_crun, sizeof(uint32_t) * (e->sub_batch / kChunk) * e->sb);
   ALLOC(e->d_rst_status, e->sub_batch);
   ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
   ALLOC(e->d_err, sizeof(uint32_t));
@@ -335,8 +339,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   hipStream_t st = stream ? (hipStream_t)stream : e->own_stream;
   if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
   e->last_stream = st;
-  if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15))
-    return set_err(CC_ERR_INVALID, "status must be 4-byte and value 16-byte aligned");
+  if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15) || (((uintptr_t)c->inst) & 15))
+    return set_err(CC_ERR_INVALID, "inst and value must be 16-byte aligned, status 4-byte aligned");
   for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
     const uint64_t hi = std::min(n, lo + e->sub_batch);
     PartArgs pa{};
@@ -357,7 +361,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.base = e->d_base;
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
-    pa.spos = e->d_spos;
+    pa.cpos = e->d_cpos;
+    pa.ckst = e->d_ckst;
+    pa.crun = e->d_crun;
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
     ValueArgs va{};
@@ -374,7 +380,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.mark = marker_of(e);
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
     UnpermuteArgs ua{};
-    ua.spos = e->d_spos;
+    ua.cpos = e->d_cpos;
+    ua.ckst = e->d_ckst;
+    ua.crun = e->d_crun;
+    ua.sb = e->sb;
     ua.lo = lo;
     ua.hi = hi;
     ua.rst_status = e->d_rst_status;

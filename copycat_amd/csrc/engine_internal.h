@@ -31,7 +31,9 @@ struct PartArgs {
   uint32_t* base;    // [sb]
   uint32_t* st_meta; // staging records [sub_batch]
   u64x2* st_ab;
-  uint32_t* spos;    // [sub_batch] staging position of commit lo+i (kNoRes: unknown session)
+  uint16_t* cpos;    // [sub_batch] chunk-sorted position of commit lo+i (0xFFFF: unknown session)
+  uint16_t* ckst;    // [chunks][sb+1] chunk-sorted run starts (+ live count)
+  uint32_t* crun;    // [chunks][sb] staging position of each run
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
@@ -53,7 +55,10 @@ struct ValueArgs {
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
 
 struct UnpermuteArgs {
-  const uint32_t* spos;
+  const uint16_t* cpos;
+  const uint16_t* ckst;
+  const uint32_t* crun;
+  uint32_t sb;
   uint64_t lo, hi;
   const uint8_t* rst_status;
   const uint64_t* rst_value;

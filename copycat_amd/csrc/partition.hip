@@ -13,9 +13,9 @@
 //   k_part_scatter : per tile, 4 chunks of 4096 commits: a stable multisplit of the chunk in LDS (ballot
 //                    ranking inside a wave, per-wave prefix sums across the 16 waves), then the chunk is
 //                    written out super-bucket by super-bucket, so every staging run is contiguous (no
-//                    partial-line writes), plus spos[i] = staging position of commit i for k_unpermute.
-//   k_unpermute    : out[i] = result_staged[spos[i]] (coalesced in log order; unknown sessions get their
-//                    UNKNOWN_SESSION status here, ResourceManager.java:60-69).
+//                    partial-line writes), plus each commit's chunk-sorted position and per-chunk run tables.
+//   k_unpermute    : per chunk, reads the chunk's result runs contiguously into LDS and writes results in log
+//                    order (unknown sessions get their UNKNOWN_SESSION status here, ResourceManager.java:60-69).
 #include "common.h"
 #include "engine_internal.h"
 
@@ -32,9 +32,20 @@ __global__ __launch_bounds__(kPT) void k_part_count(const uint32_t* __restrict__
   extern __shared__ uint32_t hist[];  // [sb]
   for (uint32_t b = threadIdx.x; b < sb; b += kPT) hist[b] = 0;
   __syncthreads();
-  const uint64_t t0 = lo + (uint64_t)blockIdx.x * kTile;
+  const uint64_t t0 = lo + (uint64_t)blockIdx.x * kTile;  // multiple of 4 (tiles and sub-batches are)
   const uint64_t t1 = t0 + kTile < hi ? t0 + kTile : hi;
-  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPT) {
+  const uint64_t q1 = t1 / 4;
+#pragma unroll 4
+  for (uint64_t q = t0 / 4 + threadIdx.x; q < q1; q += kPT) {
+    const uint4 v = reinterpret_cast<const uint4*>(inst)[q];
+    const uint32_t r0 = resolve(inst_res, max_inst, v.x), r1 = resolve(inst_res, max_inst, v.y);
+    const uint32_t r2 = resolve(inst_res, max_inst, v.z), r3 = resolve(inst_res, max_inst, v.w);
+    if (r0 != kNoRes) atomicAdd(&hist[r0 >> sb_shift], 1u);
+    if (r1 != kNoRes) atomicAdd(&hist[r1 >> sb_shift], 1u);
+    if (r2 != kNoRes) atomicAdd(&hist[r2 >> sb_shift], 1u);
+    if (r3 != kNoRes) atomicAdd(&hist[r3 >> sb_shift], 1u);
+  }
+  for (uint64_t i = q1 * 4 + threadIdx.x; i < t1; i += kPT) {  // ragged tail (< 4 commits)
     const uint32_t r = resolve(inst_res, max_inst, inst[i]);
     if (r != kNoRes) atomicAdd(&hist[r >> sb_shift], 1u);
   }
@@ -53,14 +64,17 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ count
   const uint32_t r0 = g * per;
   const uint32_t r1 = r0 + per < tiles ? r0 + per : tiles;
   uint32_t s = 0;
-  if (b < cols)
+  if (b < cols) {
+#pragma unroll 8
     for (uint32_t t = r0; t < r1; ++t) s += counts[(uint64_t)t * cols + b];
+  }
   part[g][l] = s;
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t q = 0; q < g; ++q) pre += part[q][l];
   if (g == kScanGroups - 1 && b < cols) tot[b] = pre + s;
   if (b < cols)
+#pragma unroll 8
     for (uint32_t t = r0; t < r1; ++t) {
       const uint64_t k = (uint64_t)t * cols + b;
       const uint32_t c = counts[k];
@@ -119,13 +133,19 @@ size_t scatter_lds_bytes(uint32_t sb) {
 
 // LDS layout (dynamic): rab[kChunk] u64x2 | rmeta[kChunk] u32 | rsb[kChunk] u16 | wc[kPW][sb] u32 |
 //                       toff, trun, ctot, kstart [sb] u32 | wsum[16] u32
+//
+// Per chunk c (4096 commits) the kernel also records, for k_unpermute:
+//   cpos[i]           u16  chunk-sorted position of commit i (0xFFFF: unknown session)
+//   ckst[c][0..sb]    u16  chunk-sorted start of each super-bucket's run, ckst[c][sb] = live commits
+//   crun[c][0..sb-1]  u32  staging position of that run
 __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                    const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                    const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
                                                    const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
                                                    uint32_t sb_shift, uint32_t sb_bits, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ base, uint32_t* __restrict__ st_meta,
-                                                   u64x2* __restrict__ st_ab, uint32_t* __restrict__ spos) {
+                                                   u64x2* __restrict__ st_ab, uint16_t* __restrict__ cpos,
+                                                   uint16_t* __restrict__ ckst, uint32_t* __restrict__ crun) {
   extern __shared__ __align__(16) uint8_t smem[];
   u64x2* rab = reinterpret_cast<u64x2*>(smem);
   uint32_t* rmeta = reinterpret_cast<uint32_t*>(rab + kChunk);
@@ -148,30 +168,38 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
   }
 
   constexpr int J = kChunk / kPT;  // commits per thread per chunk
-  for (uint32_t ch = 0; ch < kTile / kChunk; ++ch) {
-    const uint64_t cbase = tile0 + (uint64_t)ch * kChunk;
-    if (cbase >= hi) break;  // block-uniform
-    for (uint32_t k = t; k < kPW * sb; k += kPT) wc[k] = 0;
-    __syncthreads();
-    // 1. wave w ranks commits cbase + w*(64*J) + j*64 + l (log order = (w, j, l)) by super-bucket
-    uint32_t key[J], loc[J], meta[J];
-    u64x2 ab[J];
-    bool live[J];
+  // commit (w, j, l) of chunk ch is cbase + w*(64*J) + j*64 + l: log order = (w, j, l)
+  uint32_t res[J], meta[J];
+  u64x2 ab[J];
+  auto load = [&](uint64_t cbase) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
-      const bool in = i < hi;
-      const uint32_t r = in ? resolve(inst_res, max_inst, inst[i]) : kNoRes;
-      live[j] = r != kNoRes;
-      key[j] = live[j] ? (r >> sb_shift) : 0;
+      res[j] = kNoRes;
       meta[j] = 0;
       ab[j] = u64x2{0, 0};
-      if (in) {
-        if (!live[j]) spos[i - lo] = kNoRes;
-        meta[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8) | ((r & rmask) << 16);
+      if (i < hi) {
+        res[j] = resolve(inst_res, max_inst, inst[i]);
+        meta[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
         ab[j].x = ca[i];
         ab[j].y = cb[i];
       }
+    }
+  };
+  load(tile0);
+  for (uint32_t ch = 0; ch < kTile / kChunk; ++ch) {
+    const uint64_t cbase = tile0 + (uint64_t)ch * kChunk;
+    if (cbase >= hi) break;  // block-uniform
+    const uint64_t cglob = (cbase - lo) / kChunk;
+    for (uint32_t k = t; k < kPW * sb; k += kPT) wc[k] = 0;
+    __syncthreads();
+    // 1. rank by super-bucket inside each wave (ballot match), per-wave running counts in LDS
+    uint32_t key[J], loc[J];
+    bool live[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      live[j] = res[j] != kNoRes;
+      key[j] = live[j] ? (res[j] >> sb_shift) : 0;
       uint64_t peers = ballot(live[j]);
       for (uint32_t k = 0; k < sb_bits; ++k) {
         const bool bit = (key[j] >> k) & 1u;
@@ -204,18 +232,27 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
       nlive += part;
     }
     __syncthreads();
-    // 3. place records in LDS in sorted order; remember each commit's staging position
+    // 3. place records in LDS in sorted order; per-commit chunk position; chunk tables
+    for (uint32_t k = t; k <= sb; k += kPT) {
+      ckst[cglob * (sb + 1) + k] = (uint16_t)(k < sb ? kstart[k] : nlive);
+      if (k < sb) crun[cglob * sb + k] = toff[k] + trun[k];
+    }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      if (!live[j]) continue;
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
-      const uint32_t within = wc[w * sb + key[j]] + loc[j];
-      const uint32_t s = kstart[key[j]] + within;
+      if (i >= hi) continue;
+      if (!live[j]) {
+        cpos[i - lo] = 0xFFFF;
+        continue;
+      }
+      const uint32_t s = kstart[key[j]] + wc[w * sb + key[j]] + loc[j];
       rab[s] = ab[j];
-      rmeta[s] = meta[j];
+      rmeta[s] = meta[j] | ((res[j] & rmask) << 16);
       rsb[s] = (uint16_t)key[j];
-      spos[i - lo] = toff[key[j]] + trun[key[j]] + within;
+      cpos[i - lo] = (uint16_t)s;
     }
+    // prefetch the next chunk while this one is written out
+    if (ch + 1 < kTile / kChunk && cbase + kChunk < hi) load(cbase + kChunk);
     __syncthreads();
     // 4. write the chunk out super-bucket by super-bucket (contiguous runs)
     for (uint32_t s = t; s < nlive; s += kPT) {
@@ -230,39 +267,62 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
   }
 }
 
-// out[i] = staged result of commit i (4 commits per thread: 16 B spos loads, coalesced stores).
-__global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ spos, uint64_t n,
-                                                   const uint8_t* __restrict__ rst_status,
-                                                   const uint64_t* __restrict__ rst_value, uint8_t* __restrict__ out_status,
-                                                   uint64_t* __restrict__ out_value) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t quads = n / 4;
+// One workgroup per 4096-commit chunk: gather the chunk's result runs (contiguous in staging order) into LDS,
+// then emit results in log order through the chunk positions — every global access coalesced.
+__global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ cpos, const uint16_t* __restrict__ ckst,
+                                                const uint32_t* __restrict__ crun, uint32_t sb, uint64_t n,
+                                                const uint8_t* __restrict__ rst_status,
+                                                const uint64_t* __restrict__ rst_value, uint8_t* __restrict__ out_status,
+                                                uint64_t* __restrict__ out_value) {
+  __shared__ uint64_t lv[kChunk];
+  __shared__ uint8_t ls[kChunk];
+  __shared__ uint16_t kst[kMaxSb + 1];
+  __shared__ uint32_t run[kMaxSb];
+  const uint32_t t = threadIdx.x;
+  const uint64_t c = blockIdx.x;
+  const uint64_t i0 = c * kChunk;
+  for (uint32_t k = t; k <= sb; k += kPT) {
+    kst[k] = ckst[c * (sb + 1) + k];
+    if (k < sb) run[k] = crun[c * sb + k];
+  }
+  __syncthreads();
+  const uint32_t nlive = kst[sb];
+  for (uint32_t s = t; s < nlive; s += kPT) {
+    // run of s: the last k with kst[k] <= s (empty runs share their start with the next run)
+    uint32_t a = 0, b = sb;  // invariant: kst[a] <= s < kst[b] (kst[sb] = nlive > s)
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (kst[m] <= s) a = m; else b = m;
+    }
+    const uint32_t g = run[a] + (s - kst[a]);
+    ls[s] = rst_status[g];
+    lv[s] = rst_value[g];
+  }
+  __syncthreads();
   const uint8_t unk = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += stride) {
-    const uint4 p = reinterpret_cast<const uint4*>(spos)[q];
-    const uint32_t pp[4] = {p.x, p.y, p.z, p.w};
+  const uint64_t i1 = i0 + kChunk < n ? i0 + kChunk : n;
+  if (i1 - i0 == (uint64_t)kChunk) {  // full chunk: 4 commits per thread, vector stores
+    const uint64_t q = i0 / 4 + t;
+    const uint2 pp = reinterpret_cast<const uint2*>(cpos)[q];
+    const uint16_t p[4] = {(uint16_t)(pp.x & 0xFFFF), (uint16_t)(pp.x >> 16), (uint16_t)(pp.y & 0xFFFF), (uint16_t)(pp.y >> 16)};
     uint32_t sw = 0;
     uint64_t v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      uint8_t s = unk;
-      v[k] = 0;
-      if (pp[k] != kNoRes) {
-        s = rst_status[pp[k]];
-        v[k] = rst_value[pp[k]];
-      }
-      sw |= (uint32_t)s << (8 * k);
+      const bool ok = p[k] != 0xFFFF;
+      sw |= (uint32_t)(ok ? ls[p[k]] : unk) << (8 * k);
+      v[k] = ok ? lv[p[k]] : 0;
     }
     reinterpret_cast<uint32_t*>(out_status)[q] = sw;
     u64x2* ov = reinterpret_cast<u64x2*>(out_value) + 2 * q;
     ov[0] = u64x2{v[0], v[1]};
     ov[1] = u64x2{v[2], v[3]};
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-    const uint64_t i = quads * 4 + threadIdx.x;
-    const uint32_t p = spos[i];
-    out_status[i] = p != kNoRes ? rst_status[p] : unk;
-    out_value[i] = p != kNoRes ? rst_value[p] : 0;
+  } else {
+    for (uint64_t i = i0 + t; i < i1; i += kPT) {
+      const uint16_t p = cpos[i];
+      out_status[i] = p != 0xFFFF ? ls[p] : unk;
+      out_value[i] = p != 0xFFFF ? lv[p] : 0;
+    }
   }
 }
 
@@ -282,19 +342,18 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   a.mark(K_PART_SCATTER, 1, st);
   hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(kPT), scatter_lds_bytes(a.sb), st, a.inst, a.op, a.flags, a.a, a.b,
                      a.lo, a.hi, a.inst_res, a.max_inst, a.sb, a.sb_shift, a.sb_bits, a.counts, a.base, a.st_meta, a.st_ab,
-                     a.spos);
+                     a.cpos, a.ckst, a.crun);
   a.mark(K_PART_SCATTER, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_unpermute(const UnpermuteArgs& a, hipStream_t st) {
   const uint64_t n = a.hi - a.lo;
-  uint64_t grid = (n / 4 + 255) / 256;
-  if (grid > 4096) grid = 4096;
-  if (grid < 1) grid = 1;
+  const uint64_t chunks = (n + kChunk - 1) / kChunk;
+  if (chunks == 0) return 0;
   a.mark(K_UNPERMUTE, 1, st);
-  hipLaunchKernelGGL(k_unpermute, dim3((uint32_t)grid), dim3(256), 0, st, a.spos, n, a.rst_status, a.rst_value,
-                     a.out_status + a.lo, a.out_value + a.lo);
+  hipLaunchKernelGGL(k_unpermute, dim3((uint32_t)chunks), dim3(kPT), 0, st, a.cpos, a.ckst, a.crun, a.sb, n, a.rst_status,
+                     a.rst_value, a.out_status + a.lo, a.out_value + a.lo);
   a.mark(K_UNPERMUTE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -51,6 +51,8 @@ def _assert_same(E, O, gs, gv, os_, ov, resources):
     (50_000, 1000, 5, 4, 0.5),        # half the rows on 4 hot slots; ragged bucket (1000 % 64 != 0)
     (200_000, 65536, 6, 0, 0.0),
     (300_001, 4096, 7, 16, 0.2),
+    (1_000_003, 256, 8, 1, 0.9),      # one slot takes 90% of the rows: 1800-long chains per chunk
+    (700_000, 131072, 9, 0, 0.0),     # max_resources: 512 super-buckets
 ])
 def test_value_random_parity(n, resources, seed, hot, p_hot):
     from copycat_amd.workload import value_random_stream
