@@ -23,65 +23,49 @@ struct ValState {
 };
 
 // Applies one committed AtomicValue op to the state; returns the status byte, result payload in rv.
+// Branch-free (selects only): a wave's lanes carry different ops, and a switch would run every case.
 __device__ inline uint32_t value_apply(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, ValState& s, uint64_t& rv,
                                        uint32_t& err) {
   const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
   const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
   const uint32_t tag = s.meta & 0xFF, cur = (s.meta >> 8) & 1;
+  const bool is_get = op == CC_OP_VALUE_GET;        // get :77-83   return current != null ? value : null
+  const bool is_set = op == CC_OP_VALUE_SET;        // set :114-118 value = v
+  const bool is_cas = op == CC_OP_VALUE_CAS;        // compareAndSet :123-133
+  const bool is_gas = op == CC_OP_VALUE_GETANDSET;  // getAndSet :138-144 result = old value
+  const bool is_del = op == CC_OP_DELETE;           // delete :146-157 (current != null) -> value = current = null
+  const bool is_lis = op == CC_OP_VALUE_LISTEN || op == CC_OP_VALUE_UNLISTEN;
+  // (value == null && expect == null) || (value != null && expect != null && value.equals(expect))
+  const bool eq = (tag == CC_TAG_NULL && ta == CC_TAG_NULL) || (tag != CC_TAG_NULL && tag == ta && s.v == pa);
+  const bool write = is_set || is_gas || (is_cas && eq);
+  const bool clear = is_del && cur;
+  // result
+  uint32_t rtag = CC_TAG_NULL;
   rv = 0;
-  switch (op) {
-    case CC_OP_VALUE_GET:  // return current != null ? value : null
-      if (cur) {
-        rv = s.v;
-        return CC_STATUS(CC_ST_OK, tag);
-      }
-      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-    case CC_OP_VALUE_SET:  // cleanCurrent(); value = v; setCurrent(commit)
-      s.meta = vmeta(ta, 1);
-      s.v = pa;
-      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-    case CC_OP_VALUE_CAS: {  // (value == null && expect == null) || (value != null && expect != null && value.equals(expect))
-      const bool eq = (tag == CC_TAG_NULL && ta == CC_TAG_NULL) ||
-                      (tag != CC_TAG_NULL && ta != CC_TAG_NULL && tag == ta && s.v == pa);
-      if (eq) {
-        s.meta = vmeta(tb, 1);
-        s.v = pb;
-      }
-      rv = eq ? 1 : 0;
-      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
-    }
-    case CC_OP_VALUE_GETANDSET: {  // result = value; value = v; setCurrent
-      rv = s.v;
-      const uint32_t rt = tag;
-      s.meta = vmeta(ta, 1);
-      s.v = pa;
-      return CC_STATUS(CC_ST_OK, rt);
-    }
-    case CC_OP_DELETE:  // if (current != null) { current = null; value = null; }
-      if (cur) {
-        s.meta = 0;
-        s.v = 0;
-      }
-      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-    case CC_OP_VALUE_LISTEN:
-    case CC_OP_VALUE_UNLISTEN:
-      err |= kErrUnsupported;
-      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-    default:  // IllegalStateException "unknown operation type" (ResourceStateMachineExecutor.java:78)
-      return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
-  }
+  if ((is_get && cur) || is_gas) { rtag = tag; rv = s.v; }
+  if (is_cas) { rtag = CC_TAG_BOOL; rv = eq ? 1 : 0; }
+  const bool known = is_get || is_set || is_cas || is_gas || is_del || is_lis;
+  if (is_lis) err |= kErrUnsupported;
+  // state
+  const uint32_t ntag = is_cas ? tb : ta;
+  const uint64_t nv = is_cas ? pb : pa;
+  s.meta = write ? vmeta(ntag, 1) : (clear ? 0u : s.meta);
+  s.v = write ? nv : (clear ? 0ull : s.v);
+  // IllegalStateException "unknown operation type" (ResourceStateMachineExecutor.java:78)
+  return known ? CC_STATUS(CC_ST_OK, rtag) : CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
 }
 
 constexpr int kAT = kApplyWaves * kWave;  // 256 threads = 256 slots of the super-bucket
 constexpr int kACh = kAT * kApplyPer;     // 2048 records per chunk
 constexpr int kSbSlots = kApplyWaves * kLaneRes;
-constexpr int kGroups = kApplyPer * kApplyWaves;  // (j, wave) groups of 64 records, in log order
+constexpr int kWaveRecs = kWave * kApplyPer;  // records of a chunk per wave (contiguous)
 
 // One workgroup per super-bucket; thread t owns slot t (its AtomicValueState lives in two registers).
-// Per chunk of 2048 staging records (record c = j*256 + t, log order = (j, wave, lane)):
-//   1. a stable counting sort of the chunk by slot: ballot ranking inside each (j, wave) group, per-group
-//      per-slot counts in LDS (tagged with the chunk number, so the table is never cleared), each owner
-//      thread scans its slot's 32 group counts, a block scan gives each slot's run start;
+// Per chunk of 2048 staging records (wave w holds records w*512 + j*64 + lane, so log order = (w, j, lane)):
+//   1. a stable counting sort of the chunk by slot: each wave ranks its records with LDS atomics with return
+//      on its own 256-counter table (same-address lanes resolve in lane order on gfx950, and the wave's
+//      instructions are in program order), the owner of each slot prefixes the 4 wave counts, a block scan
+//      gives each slot's run start;
 //   2. thread t walks its slot's run sequentially — the reference's one-commit-at-a-time order, per slot;
 //   3. results go back through LDS to staging order and out contiguously.
 __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
@@ -94,57 +78,53 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
   __shared__ uint16_t sidx[kACh];
   __shared__ uint64_t rval[kACh];
   __shared__ uint8_t rstat[kACh];
-  __shared__ uint32_t gcnt[kGroups][kSbSlots];  // (chunk+1) << 12 | value (count, then prefix); else stale
+  __shared__ uint32_t wcnt[kApplyWaves][kSbSlots];  // per-wave slot counts (zeroed after use)
+  __shared__ uint32_t wpre[kApplyWaves][kSbSlots];  // per-wave slot prefixes
   __shared__ uint32_t sstart[kSbSlots];
   __shared__ uint32_t wsum[kApplyWaves];
 
   const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
-  const uint64_t lt = lanemask_lt();
   ValState st_reg{val_meta[(uint64_t)s * kSbSlots + t], val_v[(uint64_t)s * kSbSlots + t]};
-  for (uint32_t q = t; q < kGroups * kSbSlots; q += kAT) (&gcnt[0][0])[q] = 0;
+#pragma unroll
+  for (int q = 0; q < kApplyWaves; ++q) wcnt[q][t] = 0;
   const uint32_t lo = base[s], cnt = tot[s];
   uint32_t err = 0;
 
-  uint32_t m[kApplyPer];
-  u64x2 ab[kApplyPer];
+  uint32_t m[kApplyPer], nm[kApplyPer];
+  u64x2 ab[kApplyPer], nab[kApplyPer];
+  auto load = [&](uint32_t c0, uint32_t (&mm)[kApplyPer], u64x2 (&aa)[kApplyPer]) {
 #pragma unroll
-  for (int j = 0; j < kApplyPer; ++j) {
-    const uint32_t c = j * kAT + t;
-    m[j] = 0;
-    ab[j] = u64x2{0, 0};
-    if (c < cnt) {
-      m[j] = st_meta[lo + c];
-      ab[j] = st_ab[lo + c];
+    for (int j = 0; j < kApplyPer; ++j) {
+      const uint32_t c = c0 + w * kWaveRecs + j * kWave + l;
+      mm[j] = 0;
+      aa[j] = u64x2{0, 0};
+      if (c < cnt) {
+        mm[j] = st_meta[lo + c];
+        aa[j] = st_ab[lo + c];
+      }
     }
-  }
-  __syncthreads();
-  uint32_t chunk_tag = 0;
+  };
+  load(0, m, ab);
+  lds_barrier();
   for (uint32_t c0 = 0; c0 < cnt; c0 += kACh) {
-    chunk_tag += 1u << 12;
-    // 1a. rank inside each (j, wave) group by slot (8 ballots); group leaders publish counts
+    // the next chunk's records stream in during this whole chunk
+    load(c0 + kACh, nm, nab);
+    // 1a. rank each record among the wave's earlier records of its slot
     uint32_t rank[kApplyPer], slot[kApplyPer];
 #pragma unroll
     for (int j = 0; j < kApplyPer; ++j) {
-      const bool live = c0 + j * kAT + t < cnt;
+      const bool live = c0 + w * kWaveRecs + j * kWave + l < cnt;
       slot[j] = smeta_slot(m[j]) & (kSbSlots - 1);
-      uint64_t peers = ballot(live);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool bit = (slot[j] >> k) & 1u;
-        const uint64_t mk = ballot(live && bit);
-        peers &= bit ? mk : ~mk;
-      }
-      rank[j] = live ? (uint32_t)__popcll(peers & lt) : 0xFFFFFFFFu;
-      if (live && (peers & lt) == 0) gcnt[j * kApplyWaves + w][slot[j]] = chunk_tag | (uint32_t)__popcll(peers);
+      rank[j] = live ? atomicAdd(&wcnt[w][slot[j]], 1u) : 0xFFFFFFFFu;
     }
-    __syncthreads();
-    // 1b. owner of slot t: exclusive prefix over the 32 groups; run length
+    lds_barrier();
+    // 1b. owner of slot t: prefix over the 4 waves; run length; reset the counters
     uint32_t run = 0;
-#pragma unroll 8
-    for (int g = 0; g < kGroups; ++g) {
-      const uint32_t v = gcnt[g][t];
-      const uint32_t c = (v & ~0xFFFu) == chunk_tag ? (v & 0xFFFu) : 0;
-      gcnt[g][t] = chunk_tag | run;  // prefix, tagged
+#pragma unroll
+    for (int q = 0; q < kApplyWaves; ++q) {
+      const uint32_t c = wcnt[q][t];
+      wpre[q][t] = run;
+      wcnt[q][t] = 0;
       run += c;
     }
     // 1c. block exclusive scan of the run lengths -> run starts
@@ -155,55 +135,85 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
       if (l >= (uint32_t)d) inc += y;
     }
     if (l == 63) wsum[w] = inc;
-    __syncthreads();
+    lds_barrier();
     uint32_t start = inc - run;
     for (uint32_t q = 0; q < w; ++q) start += wsum[q];
     sstart[t] = start;
-    __syncthreads();
+    lds_barrier();
     // 1d. place records in slot order
 #pragma unroll
     for (int j = 0; j < kApplyPer; ++j) {
       if (rank[j] == 0xFFFFFFFFu) continue;
-      const uint32_t p = sstart[slot[j]] + (gcnt[j * kApplyWaves + w][slot[j]] & 0xFFFu) + rank[j];
+      const uint32_t p = sstart[slot[j]] + wpre[w][slot[j]] + rank[j];
       sm[p] = m[j];
       sab[p] = ab[j];
-      sidx[p] = (uint16_t)(j * kAT + t);
+      sidx[p] = (uint16_t)(w * kWaveRecs + j * kWave + l);
     }
-    __syncthreads();
-    // prefetch the next chunk while this one resolves
-#pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      const uint32_t c = c0 + kACh + j * kAT + t;
-      m[j] = 0;
-      ab[j] = u64x2{0, 0};
-      if (c < cnt) {
-        m[j] = st_meta[lo + c];
-        ab[j] = st_ab[lo + c];
+    lds_barrier();
+    // 2. thread t applies its slot's commits in log order, state in registers (next record's LDS reads
+    //    are issued before the current one is applied)
+    if (run) {
+      uint32_t mm = sm[start];
+      u64x2 abv = sab[start];
+      uint32_t ci = sidx[start];
+      for (uint32_t k = 0; k < run; ++k) {
+        const uint32_t pn = k + 1 < run ? start + k + 1 : start + k;
+        const uint32_t mm2 = sm[pn];
+        const u64x2 abv2 = sab[pn];
+        const uint32_t ci2 = sidx[pn];
+        uint64_t rv;
+        const uint32_t stt = value_apply(smeta_op(mm), smeta_flags(mm), abv.x, abv.y, st_reg, rv, err);
+        rstat[ci] = (uint8_t)stt;
+        rval[ci] = rv;
+        mm = mm2;
+        abv = abv2;
+        ci = ci2;
       }
     }
-    // 2. thread t applies its slot's commits in log order, state in registers
-    for (uint32_t k = 0; k < run; ++k) {
-      const uint32_t p = start + k;
-      const uint32_t mm = sm[p];
-      const u64x2 abv = sab[p];
-      uint64_t rv;
-      const uint32_t stt = value_apply(smeta_op(mm), smeta_flags(mm), abv.x, abv.y, st_reg, rv, err);
-      const uint32_t ci = sidx[p];
-      rstat[ci] = (uint8_t)stt;
-      rval[ci] = rv;
-    }
-    __syncthreads();
+    lds_barrier();
     // 3. results back in staging order, contiguous
     const uint32_t nhere = cnt - c0 < (uint32_t)kACh ? cnt - c0 : (uint32_t)kACh;
     for (uint32_t c = t; c < nhere; c += kAT) {
       rst_status[lo + c0 + c] = rstat[c];
       rst_value[lo + c0 + c] = rval[c];
     }
-    __syncthreads();
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < kApplyPer; ++j) {
+      m[j] = nm[j];
+      ab[j] = nab[j];
+    }
   }
   val_meta[(uint64_t)s * kSbSlots + t] = st_reg.meta;
   val_v[(uint64_t)s * kSbSlots + t] = st_reg.v;
   if (err) atomicOr(err_out, err);
+}
+
+// Engine-start self-check of the hardware property the stable rankings rely on: LDS atomics with return
+// from one wave instruction that hit the same address are resolved in lane order.  *bad counts violations.
+__global__ __launch_bounds__(256) void k_selfcheck_lds_order(uint32_t* __restrict__ bad) {
+  __shared__ uint32_t tbl[256];
+  const uint32_t t = threadIdx.x, l = t & 63;
+  uint32_t x = 0x9E3779B9u ^ (t * 2654435761u) ^ (blockIdx.x * 40503u);
+  uint32_t v = 0;
+  for (uint32_t it = 0; it < 32; ++it) {
+    tbl[t] = 0;
+    lds_barrier();
+    x = x * 1664525u + 1013904223u;
+    const uint32_t key = ((x >> 8) & ((1u << (it & 3)) - 1)) + (t >> 6) * 64;
+    const uint32_t old = atomicAdd(&tbl[key], 1u);
+    for (uint32_t j = 0; j < 64; ++j) {  // uniform loop: every lane takes part in each shuffle
+      const uint32_t kj = __shfl(key, j, 64), oj = __shfl(old, j, 64);
+      if (j < l && kj == key && oj >= old) ++v;
+    }
+    lds_barrier();
+  }
+  if (v) atomicAdd(bad, v);
+}
+
+int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
+  hipLaunchKernelGGL(k_selfcheck_lds_order, dim3(64), dim3(256), 0, st, d_bad);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {

@@ -44,6 +44,15 @@ __device__ inline uint64_t lanemask_lt() {
 }
 __device__ inline uint64_t ballot(bool p) { return __ballot(p); }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global load and
+// store of the wave (s_waitcnt vmcnt(0)), which would kill the cross-chunk prefetches the streaming kernels
+// rely on; none of the engine's kernels exchanges global-memory data between threads of a workgroup.
+__device__ inline void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ---- ops registered per resource type (ResourceStateMachine.init + Copycat reflection configure) -----
 __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {
   if (op == CC_OP_DELETE) return type != CC_RES_NONE;

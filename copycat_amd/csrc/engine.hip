@@ -192,6 +192,19 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if ((he = hipMemset(e->d_val_v, 0, sizeof(uint64_t) * slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
+  // the stable rankings of k_part_scatter / k_apply_value need same-address LDS atomics of one wave
+  // instruction to resolve in lane order: verify on this device before trusting any result
+  if (launch_selfcheck(e->d_err, e->own_stream) != 0) return fail("selfcheck launch", hipGetLastError());
+  uint32_t bad = 0;
+  if ((he = hipMemcpyAsync(&bad, e->d_err, sizeof bad, hipMemcpyDeviceToHost, e->own_stream)) != hipSuccess ||
+      (he = hipStreamSynchronize(e->own_stream)) != hipSuccess)
+    return fail("selfcheck", he);
+  if (bad) {
+    free_all(e);
+    delete e;
+    return set_err(CC_ERR_STATE, "device self-check failed: LDS atomics are not lane-ordered on this device");
+  }
+  if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
   *out = e;
   return CC_OK;
 }
@@ -355,7 +368,6 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.max_inst = e->cfg.max_instances;
     pa.sb = e->sb;
     pa.sb_shift = kSbShift;
-    pa.sb_bits = e->sb_bits;
     pa.counts = e->d_counts;
     pa.tot = e->d_tot;
     pa.base = e->d_base;

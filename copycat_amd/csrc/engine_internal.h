@@ -25,7 +25,7 @@ struct PartArgs {
   uint64_t lo, hi;
   const uint32_t* inst_res;
   uint32_t max_inst;
-  uint32_t sb, sb_shift, sb_bits;  // super-buckets
+  uint32_t sb, sb_shift;  // super-buckets
   uint32_t* counts;  // [tiles][sb]
   uint32_t* tot;     // [sb]
   uint32_t* base;    // [sb]
@@ -53,6 +53,7 @@ struct ValueArgs {
   Marker mark;
 };
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
+int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct UnpermuteArgs {
   const uint16_t* cpos;

@@ -10,8 +10,8 @@
 //   k_part_count   : per 16384-commit tile, a histogram over super-buckets (LDS atomics) -> counts[tile][sb]
 //   k_part_scan    : per 64-super-bucket stripe, exclusive prefix over tiles (in place) + totals
 //   k_part_base    : exclusive scan of the totals -> super-bucket base offsets in the staging list
-//   k_part_scatter : per tile, 4 chunks of 4096 commits: a stable multisplit of the chunk in LDS (ballot
-//                    ranking inside a wave, per-wave prefix sums across the 16 waves), then the chunk is
+//   k_part_scatter : per tile, 4 chunks of 4096 commits: a stable multisplit of the chunk in LDS (ranking
+//                    inside a wave by LDS atomics, per-wave prefix sums across the 16 waves), then the chunk is
 //                    written out super-bucket by super-bucket, so every staging run is contiguous (no
 //                    partial-line writes), plus each commit's chunk-sorted position and per-chunk run tables.
 //   k_unpermute    : per chunk, reads the chunk's result runs contiguously into LDS and writes results in log
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(kPT) void k_part_count(const uint32_t* __restrict__
                                                  uint32_t sb_shift, uint32_t* __restrict__ counts) {
   extern __shared__ uint32_t hist[];  // [sb]
   for (uint32_t b = threadIdx.x; b < sb; b += kPT) hist[b] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint64_t t0 = lo + (uint64_t)blockIdx.x * kTile;  // multiple of 4 (tiles and sub-batches are)
   const uint64_t t1 = t0 + kTile < hi ? t0 + kTile : hi;
   const uint64_t q1 = t1 / 4;
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kPT) void k_part_count(const uint32_t* __restrict__
     const uint32_t r = resolve(inst_res, max_inst, inst[i]);
     if (r != kNoRes) atomicAdd(&hist[r >> sb_shift], 1u);
   }
-  __syncthreads();
+  lds_barrier();
   uint32_t* row = counts + (uint64_t)blockIdx.x * sb;
   for (uint32_t b = threadIdx.x; b < sb; b += kPT) row[b] = hist[b];
 }
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ count
     for (uint32_t t = r0; t < r1; ++t) s += counts[(uint64_t)t * cols + b];
   }
   part[g][l] = s;
-  __syncthreads();
+  lds_barrier();
   uint32_t pre = 0;
   for (uint32_t q = 0; q < g; ++q) pre += part[q][l];
   if (g == kScanGroups - 1 && b < cols) tot[b] = pre + s;
@@ -93,9 +93,9 @@ __device__ inline uint32_t block_exscan(uint32_t v, uint32_t* wsum /*[16] LDS*/,
     const uint32_t y = __shfl_up(inc, d, 64);
     if (l >= (uint32_t)d) inc += y;
   }
-  __syncthreads();  // wsum may still be read by a previous call
+  lds_barrier();  // wsum may still be read by a previous call
   if (l == 63) wsum[w] = inc;
-  __syncthreads();
+  lds_barrier();
   uint32_t wpre = 0, all = 0;
   for (uint32_t q = 0; q < blockDim.x / 64; ++q) {
     const uint32_t x = wsum[q];
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
                                                    const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                    const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
                                                    const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
-                                                   uint32_t sb_shift, uint32_t sb_bits, const uint32_t* __restrict__ offs,
+                                                   uint32_t sb_shift, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ base, uint32_t* __restrict__ st_meta,
                                                    u64x2* __restrict__ st_ab, uint16_t* __restrict__ cpos,
                                                    uint16_t* __restrict__ ckst, uint32_t* __restrict__ crun) {
@@ -158,7 +158,6 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
   uint32_t* wsum = kstart + sb;
 
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  const uint64_t lt = lanemask_lt();
   const uint32_t rmask = (1u << sb_shift) - 1;
   const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
   const uint32_t* trow = offs + (uint64_t)blockIdx.x * sb;
@@ -169,49 +168,52 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
 
   constexpr int J = kChunk / kPT;  // commits per thread per chunk
   // commit (w, j, l) of chunk ch is cbase + w*(64*J) + j*64 + l: log order = (w, j, l)
-  uint32_t res[J], meta[J];
-  u64x2 ab[J];
-  auto load = [&](uint64_t cbase) {
+  // Prefetch in two stages so no wave ever stalls on the instance->resource gather right after its load:
+  // raw columns of chunk c+1 are requested at the top of chunk c, their gathers after chunk c's ranking.
+  uint32_t res[J], meta[J], ninst[J], nmeta[J];
+  u64x2 ab[J], nab[J];
+  auto load_raw = [&](uint64_t cbase, uint32_t (&in)[J], uint32_t (&mt)[J], u64x2 (&aa)[J]) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
-      res[j] = kNoRes;
-      meta[j] = 0;
-      ab[j] = u64x2{0, 0};
+      in[j] = kNoRes;
+      mt[j] = 0;
+      aa[j] = u64x2{0, 0};
       if (i < hi) {
-        res[j] = resolve(inst_res, max_inst, inst[i]);
-        meta[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
-        ab[j].x = ca[i];
-        ab[j].y = cb[i];
+        in[j] = inst[i];
+        mt[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
+        aa[j].x = ca[i];
+        aa[j].y = cb[i];
       }
     }
   };
-  load(tile0);
+  auto gather = [&](const uint32_t (&in)[J], uint32_t (&rr)[J]) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) rr[j] = in[j] == kNoRes ? kNoRes : resolve(inst_res, max_inst, in[j]);
+  };
+  load_raw(tile0, ninst, meta, ab);
+  gather(ninst, res);
   for (uint32_t ch = 0; ch < kTile / kChunk; ++ch) {
     const uint64_t cbase = tile0 + (uint64_t)ch * kChunk;
     if (cbase >= hi) break;  // block-uniform
     const uint64_t cglob = (cbase - lo) / kChunk;
+    const bool more = ch + 1 < kTile / kChunk && cbase + kChunk < hi;
+    if (more) load_raw(cbase + kChunk, ninst, nmeta, nab);
     for (uint32_t k = t; k < kPW * sb; k += kPT) wc[k] = 0;
-    __syncthreads();
-    // 1. rank by super-bucket inside each wave (ballot match), per-wave running counts in LDS
+    lds_barrier();
+    // 1. rank by super-bucket inside each wave: the wave's own counter table, LDS atomics with return
+    //    (same-address lanes of one instruction resolve in lane order on gfx950 — checked at engine start)
     uint32_t key[J], loc[J];
     bool live[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       live[j] = res[j] != kNoRes;
       key[j] = live[j] ? (res[j] >> sb_shift) : 0;
-      uint64_t peers = ballot(live[j]);
-      for (uint32_t k = 0; k < sb_bits; ++k) {
-        const bool bit = (key[j] >> k) & 1u;
-        const uint64_t m = ballot(live[j] && bit);
-        peers &= bit ? m : ~m;
-      }
-      uint32_t b0 = 0;
-      if (live[j]) b0 = wc[w * sb + key[j]];
-      loc[j] = b0 + (uint32_t)__popcll(peers & lt);
-      if (live[j] && (peers & lt) == 0) wc[w * sb + key[j]] = b0 + (uint32_t)__popcll(peers);
+      loc[j] = live[j] ? atomicAdd(&wc[w * sb + key[j]], 1u) : 0;
     }
-    __syncthreads();
+    uint32_t nres[J];
+    if (more) gather(ninst, nres);
+    lds_barrier();
     // 2. per super-bucket: exclusive prefix over waves and chunk totals; then chunk-sorted starts
     for (uint32_t k = t; k < sb; k += kPT) {
       uint32_t run = 0;
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
       }
       ctot[k] = run;
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t nlive = 0;
     for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform loop
       const uint32_t k = k0 + t;
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
       if (k < sb) kstart[k] = nlive + ex;
       nlive += part;
     }
-    __syncthreads();
+    lds_barrier();
     // 3. place records in LDS in sorted order; per-commit chunk position; chunk tables
     for (uint32_t k = t; k <= sb; k += kPT) {
       ckst[cglob * (sb + 1) + k] = (uint16_t)(k < sb ? kstart[k] : nlive);
@@ -251,9 +253,7 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
       rsb[s] = (uint16_t)key[j];
       cpos[i - lo] = (uint16_t)s;
     }
-    // prefetch the next chunk while this one is written out
-    if (ch + 1 < kTile / kChunk && cbase + kChunk < hi) load(cbase + kChunk);
-    __syncthreads();
+    lds_barrier();
     // 4. write the chunk out super-bucket by super-bucket (contiguous runs)
     for (uint32_t s = t; s < nlive; s += kPT) {
       const uint32_t k = rsb[s];
@@ -261,9 +261,17 @@ __global__ __launch_bounds__(kPT) void k_part_scatter(const uint32_t* __restrict
       st_meta[g] = rmeta[s];
       st_ab[g] = rab[s];
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
-    __syncthreads();
+    lds_barrier();
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        res[j] = nres[j];
+        meta[j] = nmeta[j];
+        ab[j] = nab[j];
+      }
+    }
   }
 }
 
@@ -285,7 +293,7 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
     kst[k] = ckst[c * (sb + 1) + k];
     if (k < sb) run[k] = crun[c * sb + k];
   }
-  __syncthreads();
+  lds_barrier();
   const uint32_t nlive = kst[sb];
   for (uint32_t s = t; s < nlive; s += kPT) {
     // run of s: the last k with kst[k] <= s (empty runs share their start with the next run)
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
     ls[s] = rst_status[g];
     lv[s] = rst_value[g];
   }
-  __syncthreads();
+  lds_barrier();
   const uint8_t unk = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
   const uint64_t i1 = i0 + kChunk < n ? i0 + kChunk : n;
   if (i1 - i0 == (uint64_t)kChunk) {  // full chunk: 4 commits per thread, vector stores
@@ -341,7 +349,7 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   a.mark(K_PART_BASE, 0, st);
   a.mark(K_PART_SCATTER, 1, st);
   hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(kPT), scatter_lds_bytes(a.sb), st, a.inst, a.op, a.flags, a.a, a.b,
-                     a.lo, a.hi, a.inst_res, a.max_inst, a.sb, a.sb_shift, a.sb_bits, a.counts, a.base, a.st_meta, a.st_ab,
+                     a.lo, a.hi, a.inst_res, a.max_inst, a.sb, a.sb_shift, a.counts, a.base, a.st_meta, a.st_ab,
                      a.cpos, a.ckst, a.crun);
   a.mark(K_PART_SCATTER, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
