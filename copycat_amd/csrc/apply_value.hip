@@ -1,12 +1,12 @@
 // apply_value.hip — AtomicValueState apply (also DistributedAtomicLong, whose add is a client-side CAS loop).
 //
 // One 256-thread workgroup owns one super-bucket = 256 AtomicValueState instances: thread t holds slot t's
-// state in registers for the whole launch.  It walks the super-bucket's staging list (log order, built by
-// partition.hip) in chunks of 2048 records, prefetching the next chunk into registers while it resolves the
+// state in registers for the whole launch.  It walks the super-bucket's staging list (its run in every tile,
+// tile order = log order; built by partition.hip) in chunks of 2048 records, prefetching the next chunk into registers while it resolves the
 // current one: a stable counting sort of the chunk by slot (ballot ranking + per-slot prefix sums in LDS)
 // gives every slot its commits in log order, and each thread applies its slot's chain sequentially — the
 // same order the reference's single state-machine thread would (ResourceManager.java:56-72).  Results are
-// staged in LDS and written back contiguously in staging order; k_unpermute returns them to log order.
+// staged in LDS and written back to the records' staging positions; k_unpermute returns them to log order.
 //
 // Per-op semantics restate AtomicValueState (atomic/src/main/java/io/atomix/atomic/state/AtomicValueState.java):
 //   get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144, delete :146-157.
@@ -69,7 +69,7 @@ constexpr int kWaveRecs = kWave * kApplyPer;  // records of a chunk per wave (co
 //   2. thread t walks its slot's run sequentially — the reference's one-commit-at-a-time order, per slot;
 //   3. results go back through LDS to staging order and out contiguously.
 __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
-                                                    const uint32_t* __restrict__ base, const uint32_t* __restrict__ tot,
+                                                    const uint16_t* __restrict__ ttab, uint32_t tiles, uint32_t sb,
                                                     uint32_t* __restrict__ val_meta, uint64_t* __restrict__ val_v,
                                                     uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                     uint32_t* __restrict__ err_out) {
@@ -82,33 +82,75 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
   __shared__ uint32_t wpre[kApplyWaves][kSbSlots];  // per-wave slot prefixes
   __shared__ uint32_t sstart[kSbSlots];
   __shared__ uint32_t wsum[kApplyWaves];
+  __shared__ uint32_t rstart[kMaxTiles];     // staging position of this super-bucket's run in tile t
+  __shared__ uint32_t rpre[kMaxTiles + 1];   // records of this super-bucket before tile t
 
   const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
   ValState st_reg{val_meta[(uint64_t)s * kSbSlots + t], val_v[(uint64_t)s * kSbSlots + t]};
 #pragma unroll
   for (int q = 0; q < kApplyWaves; ++q) wcnt[q][t] = 0;
-  const uint32_t lo = base[s], cnt = tot[s];
+  // the super-bucket's list = its run in every tile, in tile order (tile-local layout of partition.hip)
+  {
+    constexpr int PT = kMaxTiles / kAT;  // tiles per thread
+    uint32_t len[PT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t tt = t * PT + k;
+      len[k] = 0;
+      if (tt < tiles) {
+        const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
+        const uint32_t b0 = row[s], b1 = row[s + 1];
+        rstart[tt] = tt * kTile + b0;
+        len[k] = b1 - b0;
+      }
+      sum += len[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    if (l == 63) wsum[w] = inc;
+    lds_barrier();
+    uint32_t run = inc - sum;
+    for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t tt = t * PT + k;
+      if (tt < tiles) rpre[tt] = run;
+      run += len[k];
+    }
+    if (t == kAT - 1) rpre[tiles] = run;
+    lds_barrier();
+  }
+  const uint32_t cnt = rpre[tiles];
   uint32_t err = 0;
 
-  uint32_t m[kApplyPer], nm[kApplyPer];
+  uint32_t m[kApplyPer], nm[kApplyPer], pos[kApplyPer], npos[kApplyPer];
   u64x2 ab[kApplyPer], nab[kApplyPer];
-  auto load = [&](uint32_t c0, uint32_t (&mm)[kApplyPer], u64x2 (&aa)[kApplyPer]) {
+  uint32_t cur = 0;  // this thread's run cursor (its records are visited in increasing order)
+  auto load = [&](uint32_t c0, uint32_t (&mm)[kApplyPer], u64x2 (&aa)[kApplyPer], uint32_t (&pp)[kApplyPer]) {
 #pragma unroll
     for (int j = 0; j < kApplyPer; ++j) {
       const uint32_t c = c0 + w * kWaveRecs + j * kWave + l;
       mm[j] = 0;
       aa[j] = u64x2{0, 0};
+      pp[j] = 0;
       if (c < cnt) {
-        mm[j] = st_meta[lo + c];
-        aa[j] = st_ab[lo + c];
+        while (rpre[cur + 1] <= c) ++cur;
+        const uint32_t g = rstart[cur] + (c - rpre[cur]);
+        pp[j] = g;
+        mm[j] = st_meta[g];
+        aa[j] = st_ab[g];
       }
     }
   };
-  load(0, m, ab);
+  load(0, m, ab, pos);
   lds_barrier();
   for (uint32_t c0 = 0; c0 < cnt; c0 += kACh) {
     // the next chunk's records stream in during this whole chunk
-    load(c0 + kACh, nm, nab);
+    load(c0 + kACh, nm, nab, npos);
     // 1a. rank each record among the wave's earlier records of its slot
     uint32_t rank[kApplyPer], slot[kApplyPer];
 #pragma unroll
@@ -171,17 +213,21 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
       }
     }
     lds_barrier();
-    // 3. results back in staging order, contiguous
-    const uint32_t nhere = cnt - c0 < (uint32_t)kACh ? cnt - c0 : (uint32_t)kACh;
-    for (uint32_t c = t; c < nhere; c += kAT) {
-      rst_status[lo + c0 + c] = rstat[c];
-      rst_value[lo + c0 + c] = rval[c];
+    // 3. results back to the records' staging positions (contiguous within each run)
+#pragma unroll
+    for (int j = 0; j < kApplyPer; ++j) {
+      const uint32_t ci = w * kWaveRecs + j * kWave + l;
+      if (c0 + ci < cnt) {
+        rst_status[pos[j]] = rstat[ci];
+        rst_value[pos[j]] = rval[ci];
+      }
     }
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < kApplyPer; ++j) {
       m[j] = nm[j];
       ab[j] = nab[j];
+      pos[j] = npos[j];
     }
   }
   val_meta[(uint64_t)s * kSbSlots + t] = st_reg.meta;
@@ -218,8 +264,8 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
 
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {
   a.mark(K_APPLY_VALUE, 1, st);
-  hipLaunchKernelGGL(k_apply_value, dim3(a.sb), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.base, a.tot, a.val_meta, a.val_v,
-                     a.rst_status, a.rst_value, a.err);
+  hipLaunchKernelGGL(k_apply_value, dim3(a.sb), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.val_meta,
+                     a.val_v, a.rst_status, a.rst_value, a.err);
   a.mark(K_APPLY_VALUE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

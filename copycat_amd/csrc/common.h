@@ -19,6 +19,7 @@ constexpr int kTile = 16384;              // commits per partition tile (one wor
 constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a tile
 constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan (1024-thread WG)
 constexpr int kApplyPer = 8;              // staging records per apply thread per chunk (prefetch depth)
+constexpr int kMaxTiles = 1024;           // tiles per sub-batch => sub-batch <= 16M commits
 constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 
 // device error bits (d_err)

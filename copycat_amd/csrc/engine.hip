@@ -53,14 +53,10 @@ struct cc_engine {
   uint32_t* d_val_meta = nullptr;
   uint64_t* d_val_v = nullptr;
   // workspace
-  uint32_t* d_counts = nullptr;
-  uint32_t* d_tot = nullptr;
-  uint32_t* d_base = nullptr;
   uint32_t* d_st_meta = nullptr;
   u64x2* d_st_ab = nullptr;
   uint16_t* d_cpos = nullptr;
-  uint16_t* d_ckst = nullptr;
-  uint32_t* d_crun = nullptr;
+  uint16_t* d_ttab = nullptr;
   uint8_t* d_rst_status = nullptr;
   uint64_t* d_rst_value = nullptr;
   uint32_t* d_err = nullptr;
@@ -119,9 +115,8 @@ static void free_all(cc_engine* e) {
   drain_profile(e);
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
   e->ev_pool.clear();
-  void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta, e->d_val_v, e->d_counts, e->d_tot,
-                  e->d_base,     e->d_st_meta,  e->d_st_ab,    e->d_err,   e->d_last_index,
-                  e->d_cpos,     e->d_ckst,     e->d_crun,     e->d_rst_status, e->d_rst_value};
+  void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta,   e->d_val_v,     e->d_st_meta, e->d_st_ab,
+                  e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -147,7 +142,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
   sub = std::min<uint64_t>(sub, cfg->max_batch);
   sub = (sub + kTile - 1) / kTile * kTile;
-  sub = std::min<uint64_t>(sub, (uint64_t)1 << 30);
+  sub = std::min<uint64_t>(sub, (uint64_t)kMaxTiles * kTile);
   e->sub_batch = sub;
   e->max_tiles = sub / kTile;
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
@@ -171,14 +166,10 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_res_type, slots);
   ALLOC(e->d_val_meta, sizeof(uint32_t) * slots);
   ALLOC(e->d_val_v, sizeof(uint64_t) * slots);
-  ALLOC(e->d_counts, sizeof(uint32_t) * e->max_tiles * e->sb);
-  ALLOC(e->d_tot, sizeof(uint32_t) * e->sb);
-  ALLOC(e->d_base, sizeof(uint32_t) * e->sb);
   ALLOC(e->d_st_meta, sizeof(uint32_t) * e->sub_batch);
   ALLOC(e->d_st_ab, sizeof(u64x2) * e->sub_batch);
   ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
-  ALLOC(e->d_ckst, sizeof(uint16_t) * (e->sub_batch / kChunk) * (e->sb + 1));
-  ALLOC(e->d_crun, sizeof(uint32_t) * (e->sub_batch / kChunk) * e->sb);
+  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sb + 1));
   ALLOC(e->d_rst_status, e->sub_batch);
   ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
   ALLOC(e->d_err, sizeof(uint32_t));
@@ -368,21 +359,17 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.max_inst = e->cfg.max_instances;
     pa.sb = e->sb;
     pa.sb_shift = kSbShift;
-    pa.counts = e->d_counts;
-    pa.tot = e->d_tot;
-    pa.base = e->d_base;
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
     pa.cpos = e->d_cpos;
-    pa.ckst = e->d_ckst;
-    pa.crun = e->d_crun;
+    pa.ttab = e->d_ttab;
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
     ValueArgs va{};
     va.st_meta = e->d_st_meta;
     va.st_ab = e->d_st_ab;
-    va.base = e->d_base;
-    va.tot = e->d_tot;
+    va.ttab = e->d_ttab;
+    va.tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
     va.sb = e->sb;
     va.val_meta = e->d_val_meta;
     va.val_v = e->d_val_v;
@@ -393,8 +380,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
     UnpermuteArgs ua{};
     ua.cpos = e->d_cpos;
-    ua.ckst = e->d_ckst;
-    ua.crun = e->d_crun;
+    ua.ttab = e->d_ttab;
     ua.sb = e->sb;
     ua.lo = lo;
     ua.hi = hi;
@@ -494,8 +480,7 @@ extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count,
   return CC_OK;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_part_count", "k_part_scan", "k_part_base", "k_part_scatter", "k_apply_value",
-                                          "k_unpermute"};
+static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute"};
 
 extern "C" int cc_profile_enable(cc_engine* e, int on) {
   if (!e) return CC_ERR_INVALID;

@@ -5,7 +5,7 @@
 namespace cc {
 
 // Optional per-kernel timing (HIP events recorded on the launch stream around each kernel).
-enum KernelId { K_PART_COUNT = 0, K_PART_SCAN, K_PART_BASE, K_PART_SCATTER, K_APPLY_VALUE, K_UNPERMUTE, K_NUM };
+enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_NUM };
 struct Marker {
   void (*fn)(void* ctx, int kernel, int begin, hipStream_t st);
   void* ctx;
@@ -26,24 +26,20 @@ struct PartArgs {
   const uint32_t* inst_res;
   uint32_t max_inst;
   uint32_t sb, sb_shift;  // super-buckets
-  uint32_t* counts;  // [tiles][sb]
-  uint32_t* tot;     // [sb]
-  uint32_t* base;    // [sb]
-  uint32_t* st_meta; // staging records [sub_batch]
+  uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
   u64x2* st_ab;
-  uint16_t* cpos;    // [sub_batch] chunk-sorted position of commit lo+i (0xFFFF: unknown session)
-  uint16_t* ckst;    // [chunks][sb+1] chunk-sorted run starts (+ live count)
-  uint32_t* crun;    // [chunks][sb] staging position of each run
+  uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
+  uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
-size_t scatter_lds_bytes(uint32_t sb);
+size_t tile_lds_bytes(uint32_t sb);
 
 struct ValueArgs {
   const uint32_t* st_meta;
   const u64x2* st_ab;
-  const uint32_t* base;
-  const uint32_t* tot;
+  const uint16_t* ttab;
+  uint32_t tiles;
   uint32_t sb;
   uint32_t* val_meta;    // [sb*256]
   uint64_t* val_v;       // [sb*256]
@@ -57,8 +53,7 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct UnpermuteArgs {
   const uint16_t* cpos;
-  const uint16_t* ckst;
-  const uint32_t* crun;
+  const uint16_t* ttab;
   uint32_t sb;
   uint64_t lo, hi;
   const uint8_t* rst_status;

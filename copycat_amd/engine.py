@@ -201,7 +201,7 @@ class Engine:
     def profile_read(self):
         """{kernel name: (total device ms, launches)} since the last profile() call (synchronizes)."""
         out = {}
-        for k in range(6):
+        for k in range(3):
             ms, n, name = C.c_double(), C.c_uint64(), C.c_char_p()
             _check(self.L.cc_profile_read(self.h, k, C.byref(ms), C.byref(n), C.byref(name)))
             out[name.value.decode()] = (ms.value, n.value)

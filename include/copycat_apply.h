@@ -142,8 +142,8 @@ typedef struct cc_config {
   uint64_t map_capacity;    /* total map entries across all CC_RES_MAP resources (0 = none)       */
   int32_t  device;          /* HIP device ordinal                                                  */
   uint32_t flags;           /* CC_CFG_* */
-  uint64_t sub_batch;       /* commits per internal sub-batch (0 = engine default; sized to keep the
-                               partition staging resident in the 256 MiB Infinity Cache)           */
+  uint64_t sub_batch;       /* commits per internal sub-batch (0 = default 16M; rounded up to a multiple
+                               of 16384, at most 16M)                                              */
   uint64_t reserved[4];
 } cc_config;
 
@@ -231,9 +231,8 @@ int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* 
                          uint8_t* h_has_current);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
- * kernel ids: 0 k_part_count, 1 k_part_scan, 2 k_part_base, 3 k_part_scatter, 4 k_apply_value,
- * 5 k_unpermute.                                                                                          */
-#define CC_PROFILE_KERNELS 6
+ * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute.                                              */
+#define CC_PROFILE_KERNELS 3
 int  cc_profile_enable(cc_engine* e, int on);
 int  cc_profile_reset(cc_engine* e);
 /* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */
