@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 
-ENGINE_SRCS = ["engine.hip", "partition.hip", "apply_value.hip", "quorum.hip"]
+ENGINE_SRCS = ["engine.hip", "partition.hip", "apply_value.hip", "apply_map.hip", "quorum.hip"]
 ENGINE_HDRS = ["common.h", "engine_internal.h"]
 ENGINE_SO = os.path.join(HERE, "libcopycat_apply.so")
 WORKLOAD_SO = os.path.join(HERE, "libcopycat_workload.so")
@@ -44,7 +44,7 @@ def build_engine(force=False):
 def build_workload(force=False):
     src = os.path.join(CSRC, "workload.cpp")
     if force or _stale(WORKLOAD_SO, [src]):
-        _run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "workload.cpp",
+        _run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread", "workload.cpp",
               "-o", WORKLOAD_SO])
     return WORKLOAD_SO
 

@@ -1,0 +1,472 @@
+// apply_map.hip — MapState apply (DistributedMap key operations) on a GPU open-addressing table.
+//
+// Table: 2^map_bits regions of 2048 entries in HBM.  A key (map slot, key tag, key payload) lives in the region
+// picked by the top bits of map_hash and is found by linear probing from the hash's low 11 bits.  Entry =
+// key u64 | word u32 (slot, key tag, USED, PRESENT, value tag) | value u64 | commit index u64 | insert index
+// u64 (the commit index that created the HashMap node: Java iteration order within a bucket).
+// A removed key keeps its entry (USED, not PRESENT) so that probe chains stay intact; entries of a deleted map
+// are marked DEAD.  A region is compacted (live entries re-inserted) when a launch finds it more than 3/4 used.
+//
+// One 256-thread workgroup owns one region for the whole launch: it loads the region into LDS, walks the
+// region's staged commits (its run in every partition tile, in log order) in chunks of 1024, and writes the
+// region back.  Per chunk:
+//   1. binding: commits that can create a node (put, putIfAbsent) find or claim their key's entry — rounds of
+//      LDS compare-and-swap; a claim is marked PENDING until the next round so no thread compares against a
+//      key that is not yet written;
+//   2. lookup: every other key op only finds its entry (a key that is unbound after step 1 is absent at that
+//      commit: nothing earlier in the log can have created it);
+//   3. a stable counting sort of the chunk by entry (LDS atomics with return, one wave at a time: lane order
+//      within a wave, wave order across waves = log order);
+//   4. each entry's commits are applied in log order by one thread (the reference's single state-machine
+//      thread, restricted to one key: different keys of a map are independent, MapState.java:32-289).
+//
+// Per-op semantics restate MapState (collections/src/main/java/io/atomix/collections/state/MapState.java):
+//   containsKey :38-44, get :65-72, getOrDefault :77-84, put :89-110, putIfAbsent :115-133, remove :138-154,
+//   removeIfPresent :159-178, replace :183-202, replaceIfPresent :207-228 (stores `value`, compares `replace`).
+// Not applied on the GPU (the batch fails with CC_ERR_UNSUPPORTED): containsValue/size/isEmpty/clear and
+// Delete (they read or reset a whole map), and put/putIfAbsent/replace/replaceIfPresent with ttl > 0 (timers).
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+constexpr int kMT = 256;                // threads per region workgroup
+constexpr int kMPer = 4;                // commits per thread per chunk
+constexpr int kMCh = kMT * kMPer;       // 1024 commits per chunk
+constexpr int kMEPer = kMapRegion / kMT;  // table entries per thread (8)
+constexpr uint32_t kNoEnt = 0xFFFFu;
+constexpr uint32_t kEntFull = 0xFFFEu;
+
+__device__ inline bool map_key_op(uint32_t op) { return op == 60 || (op >= 62 && op <= 69); }
+__device__ inline bool map_binds(uint32_t op) { return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT; }
+__device__ inline bool map_reads_ttl(uint32_t op) {
+  return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT;
+}
+
+// Applies one committed key op to an entry (w: word with PRESENT + value tag, v: value payload).
+// Returns the status byte; rv = result payload; `wrote` = the entry now holds this commit (commit index),
+// `created` = a new HashMap node was created (insert index).
+__device__ inline uint32_t map_apply(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t& w, uint64_t& v,
+                                     uint64_t& rv, bool& wrote, bool& created) {
+  const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
+  const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
+  const bool P = (w & kMwPresent) != 0;
+  const uint32_t T = P ? mw_vtag(w) : CC_TAG_NULL;
+  const uint64_t V = P ? v : 0;
+  auto store = [&](uint32_t tag, uint64_t x) {
+    w = (w & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    v = x;
+  };
+  auto erase = [&]() {
+    w &= ~(kMwPresent | kMwVtagMask);
+    v = 0;
+  };
+  wrote = created = false;
+  rv = 0;
+  switch (op) {
+    case CC_OP_MAP_CONTAINSKEY:
+      rv = P;
+      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+    case CC_OP_MAP_GET:  // a key mapped to null is present and returns null
+      rv = V;
+      return CC_STATUS(CC_ST_OK, T);
+    case CC_OP_MAP_GETORDEFAULT:
+      rv = P ? V : pa;
+      return CC_STATUS(CC_ST_OK, P ? T : ta);
+    case CC_OP_MAP_PUT:
+      rv = V;
+      store(ta, pa);
+      wrote = true;
+      created = !P;
+      return CC_STATUS(CC_ST_OK, T);
+    case CC_OP_MAP_PUTIFABSENT:
+      if (P) {
+        rv = V;
+        return CC_STATUS(CC_ST_OK, T);
+      }
+      store(ta, pa);
+      wrote = created = true;
+      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+    case CC_OP_MAP_REMOVE:
+      rv = V;
+      erase();
+      return CC_STATUS(CC_ST_OK, T);
+    case CC_OP_MAP_REMOVEIFPRESENT: {
+      // fail: absent, or stored null and value not null, or stored non-null and !stored.equals(value)
+      const bool fail = !P || (T == CC_TAG_NULL && ta != CC_TAG_NULL) || (T != CC_TAG_NULL && !(T == ta && V == pa));
+      if (!fail) erase();
+      rv = !fail;
+      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+    }
+    case CC_OP_MAP_REPLACE:
+      if (!P) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+      rv = V;
+      store(ta, pa);
+      wrote = true;
+      return CC_STATUS(CC_ST_OK, T);
+    case CC_OP_MAP_REPLACEIFPRESENT: {
+      const bool ok = P && ((T == CC_TAG_NULL && tb == CC_TAG_NULL) || (T != CC_TAG_NULL && T == tb && V == pb));
+      if (ok) {
+        store(ta, pa);
+        wrote = true;
+      }
+      rv = ok;
+      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+    }
+  }
+  return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
+}
+
+// Result of a commit that has no entry in the region: unknown op, an op not applied here, or a key op on a key
+// that is absent for the whole chunk.
+__device__ inline uint32_t map_orphan(uint32_t op, uint32_t meta, uint32_t flags, uint64_t a, uint64_t b, uint64_t& rv,
+                                      uint32_t& err) {
+  rv = 0;
+  if (!op_registered(CC_RES_MAP, op)) return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
+  if (!map_key_op(op) || (map_reads_ttl(op) && (meta & kMetaTtl))) {
+    err |= kErrUnsupported;
+    return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+  }
+  uint32_t w = kMwUsed;
+  uint64_t v = 0;
+  bool wrote, created;
+  return map_apply(op, flags, a, b, w, v, rv, wrote, created);
+}
+
+__device__ inline uint32_t map_ident_of(uint32_t res, uint32_t flags) { return mw_ident(res, CC_FLAG_KTAG(flags)); }
+
+__global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
+                                                  const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
+                                                  const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
+                                                  uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
+                                                  uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
+                                                  uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
+                                                  uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
+                                                  uint32_t* __restrict__ err_out) {
+  __shared__ uint64_t tkey[kMapRegion];
+  __shared__ uint32_t tword[kMapRegion];
+  __shared__ uint64_t tval[kMapRegion];
+  __shared__ uint64_t tci[kMapRegion];   // commit index of the entry's current value (MapState.Value.commit)
+  __shared__ uint64_t tins[kMapRegion];  // commit index that created the entry's HashMap node
+  __shared__ u64x2 rab[kMCh];          // chunk sorted by entry
+  __shared__ uint32_t rmeta[kMCh];
+  __shared__ uint32_t rpos[kMCh];      // staging position
+  __shared__ uint64_t ridx[kMCh];      // commit index
+  __shared__ uint32_t ecnt[kMapRegion + 1];  // commits per entry in the chunk -> run starts
+  __shared__ uint32_t rstart[kMaxTiles];
+  __shared__ uint32_t rpre[kMaxTiles + 1];
+  __shared__ uint32_t wsum[kMT / kWave];
+  __shared__ uint32_t flag[3];
+  __shared__ uint32_t used_total;
+
+  const uint32_t region = blockIdx.x, k = sb_val + region, t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint64_t tb = (uint64_t)region * kMapRegion;
+  uint32_t err = 0;
+
+  // ---- load the region; compact it when more than 3/4 of its entries are bound ----
+  if (t < 3) flag[t] = 0;
+  if (t == 0) used_total = 0;
+  for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
+  {
+    uint64_t ek[kMEPer], ev[kMEPer], eci[kMEPer], eins[kMEPer];
+    uint32_t ew[kMEPer], used = 0;
+#pragma unroll
+    for (int q = 0; q < kMEPer; ++q) {
+      const uint32_t e = q * kMT + t;
+      ek[q] = tbl_key[tb + e];
+      ew[q] = tbl_word[tb + e];
+      ev[q] = tbl_val[tb + e];
+      eci[q] = tbl_ci[tb + e];
+      eins[q] = tbl_ins[tb + e];
+      used += (ew[q] & kMwUsed) ? 1 : 0;
+    }
+    lds_barrier();
+    atomicAdd(&used_total, used);
+    lds_barrier();
+    const bool compact = used_total > kMapRegion * 3 / 4;  // block-uniform
+#pragma unroll
+    for (int q = 0; q < kMEPer; ++q) {
+      const uint32_t e = q * kMT + t;
+      tkey[e] = ek[q];
+      tword[e] = compact ? 0u : ew[q];
+      tval[e] = ev[q];
+      tci[e] = eci[q];
+      tins[e] = eins[q];
+    }
+    lds_barrier();
+    if (compact) {
+      // live keys are distinct: claim the first free slot of each probe chain (no key comparisons needed)
+#pragma unroll
+      for (int q = 0; q < kMEPer; ++q) {
+        if ((ew[q] & kMwPresent) && !(ew[q] & kMwDead)) {
+          const uint32_t res = ew[q] & kMwSlotMask, kt = (ew[q] >> 17) & 3;
+          uint32_t p = (uint32_t)map_hash(res, kt, ek[q]) & (kMapRegion - 1);
+          while (atomicCAS(&tword[p], 0u, ew[q]) != 0u) p = (p + 1) & (kMapRegion - 1);
+          tkey[p] = ek[q];
+          tval[p] = ev[q];
+          tci[p] = eci[q];
+          tins[p] = eins[q];
+        }
+      }
+      lds_barrier();
+    }
+  }
+
+  // ---- this region's list = its run in every partition tile, in tile order ----
+  {
+    constexpr int PT = kMaxTiles / kMT;
+    uint32_t len[PT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const uint32_t tt = t * PT + q;
+      len[q] = 0;
+      if (tt < tiles) {
+        const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
+        const uint32_t b0 = row[k], b1 = row[k + 1];
+        rstart[tt] = tt * kTile + b0;
+        len[q] = b1 - b0;
+      }
+      sum += len[q];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    if (l == 63) wsum[w] = inc;
+    lds_barrier();
+    uint32_t run = inc - sum;
+    for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const uint32_t tt = t * PT + q;
+      if (tt < tiles) rpre[tt] = run;
+      run += len[q];
+    }
+    if (t == kMT - 1) rpre[tiles] = run;
+    lds_barrier();
+  }
+  const uint32_t cnt = rpre[tiles];
+  uint32_t round = 0;  // resolution rounds (continues across chunks: flag[] is a 3-deep ring)
+
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kMCh) {
+    // ---- load this thread's commits: chunk order (w, j, l) = log order ----
+    uint32_t m[kMPer], res[kMPer], g[kMPer], ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
+    u64x2 ab[kMPer];
+    uint64_t key[kMPer], idx[kMPer];
+    bool keyop[kMPer];
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      const uint32_t c = c0 + w * (kWave * kMPer) + j * kWave + l;
+      ent[j] = kNoEnt;
+      keyop[j] = false;
+      g[j] = 0xFFFFFFFFu;
+      if (c < cnt) {
+        uint32_t lo = 0, hi = tiles;  // last tile with rpre <= c
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (rpre[mid] <= c) lo = mid; else hi = mid;
+        }
+        g[j] = rstart[lo] + (c - rpre[lo]);
+        m[j] = st_meta[g[j]];
+        ab[j] = st_ab[g[j]];
+        res[j] = st_res[g[j]];
+        key[j] = st_key[g[j]];
+        idx[j] = st_idx[g[j]];
+        const uint32_t op = smeta_op(m[j]);
+        keyop[j] = map_key_op(op) && !(map_reads_ttl(op) && (m[j] & kMetaTtl));
+        ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
+        p[j] = (uint32_t)map_hash(res[j], CC_FLAG_KTAG(smeta_flags(m[j])), key[j]) & (kMapRegion - 1);
+      }
+    }
+    // ---- 1. binding rounds (put / putIfAbsent) ----
+    bool pend[kMPer];
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) pend[j] = false;
+    for (;; ++round) {
+      bool again = false;
+#pragma unroll
+      for (int j = 0; j < kMPer; ++j) {
+        if (pend[j]) {  // claimed last round; its key is visible to everyone after that round's barrier
+          atomicAnd(&tword[ent[j]], ~kMwPending);
+          pend[j] = false;
+        }
+        if (!keyop[j] || ent[j] != kNoEnt || !map_binds(smeta_op(m[j]))) continue;
+        for (uint32_t steps = 0;; ++steps) {
+          if (steps == kMapRegion) {
+            ent[j] = kEntFull;
+            break;
+          }
+          uint32_t wv = tword[p[j]];
+          if (wv == 0u) {
+            wv = atomicCAS(&tword[p[j]], 0u, ident[j] | kMwPending);
+            if (wv == 0u) {
+              tkey[p[j]] = key[j];
+              tval[p[j]] = 0;
+              ent[j] = p[j];
+              pend[j] = true;
+              again = true;
+              break;
+            }
+          }
+          if (wv & kMwPending) {  // claimed this round by another commit: look again next round
+            again = true;
+            break;
+          }
+          if ((wv & kMwIdentMask) == ident[j] && tkey[p[j]] == key[j]) {
+            ent[j] = p[j];
+            break;
+          }
+          p[j] = (p[j] + 1) & (kMapRegion - 1);
+        }
+      }
+      if (again) flag[round % 3] = 1;
+      lds_barrier();
+      const bool go = flag[round % 3] != 0;
+      if (t == 0) flag[(round + 2) % 3] = 0;
+      if (!go) break;
+    }
+    ++round;
+    // ---- 2. lookup for the other key ops (nothing is pending now) ----
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      if (!keyop[j] || ent[j] != kNoEnt) continue;
+      for (uint32_t steps = 0; steps < kMapRegion; ++steps) {
+        const uint32_t wv = tword[p[j]];
+        if (wv == 0u) break;  // end of chain: absent
+        if ((wv & kMwIdentMask) == ident[j] && tkey[p[j]] == key[j]) {
+          ent[j] = p[j];
+          break;
+        }
+        p[j] = (p[j] + 1) & (kMapRegion - 1);
+      }
+    }
+    // commits without an entry are resolved now
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      if (g[j] == 0xFFFFFFFFu) continue;
+      if (ent[j] == kEntFull) {
+        err |= kErrCapacity;
+        ent[j] = kNoEnt;
+      }
+      if (ent[j] == kNoEnt || !keyop[j]) {
+        ent[j] = kNoEnt;
+        uint64_t rv;
+        const uint32_t s = map_orphan(smeta_op(m[j]), m[j], smeta_flags(m[j]), ab[j].x, ab[j].y, rv, err);
+        rst_status[g[j]] = (uint8_t)s;
+        rst_value[g[j]] = rv;
+      }
+    }
+    // ---- 3. stable counting sort by entry: one wave at a time keeps log order ----
+    for (uint32_t q = 0; q < kMT / kWave; ++q) {
+      if (w == q) {
+#pragma unroll
+        for (int j = 0; j < kMPer; ++j)
+          if (ent[j] != kNoEnt) rk[j] = atomicAdd(&ecnt[ent[j]], 1u);
+      }
+      lds_barrier();
+    }
+    {
+      uint32_t v[kMEPer], sum = 0;
+#pragma unroll
+      for (int q = 0; q < kMEPer; ++q) {
+        v[q] = ecnt[t * kMEPer + q];
+        sum += v[q];
+      }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      lds_barrier();
+      if (l == 63) wsum[w] = inc;
+      lds_barrier();
+      uint32_t run = inc - sum;
+      for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+      for (int q = 0; q < kMEPer; ++q) {
+        ecnt[t * kMEPer + q] = run;  // run start of entry
+        run += v[q];
+      }
+      if (t == kMT - 1) ecnt[kMapRegion] = run;
+      lds_barrier();
+    }
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      if (ent[j] == kNoEnt) continue;
+      const uint32_t s = ecnt[ent[j]] + rk[j];
+      rab[s] = ab[j];
+      rmeta[s] = m[j];
+      rpos[s] = g[j];
+      ridx[s] = idx[j];
+    }
+    lds_barrier();
+    // ---- 4. each entry's commits in log order, by the thread holding its first commit ----
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      if (ent[j] == kNoEnt || rk[j] != 0) continue;
+      const uint32_t e = ent[j];
+      const uint32_t s0 = ecnt[e], s1 = ecnt[e + 1];
+      uint32_t wv = tword[e];
+      uint64_t vv = tval[e], ci = 0, ins = 0;
+      bool any_w = false, any_c = false;
+      for (uint32_t s = s0; s < s1; ++s) {
+        const uint32_t mm = rmeta[s];
+        const u64x2 x = rab[s];
+        uint64_t rv;
+        bool wrote, created;
+        const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, wv, vv, rv, wrote, created);
+        rst_status[rpos[s]] = (uint8_t)st;
+        rst_value[rpos[s]] = rv;
+        if (wrote) { ci = ridx[s]; any_w = true; }
+        if (created) { ins = ridx[s]; any_c = true; }
+      }
+      tword[e] = wv;
+      tval[e] = vv;
+      if (any_w) tci[e] = ci;
+      if (any_c) tins[e] = ins;
+    }
+    lds_barrier();
+    for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
+    lds_barrier();
+  }
+
+  // ---- write the region back ----
+#pragma unroll
+  for (int q = 0; q < kMEPer; ++q) {
+    const uint32_t e = q * kMT + t;
+    tbl_key[tb + e] = tkey[e];
+    tbl_word[tb + e] = tword[e];
+    tbl_val[tb + e] = tval[e];
+    tbl_ci[tb + e] = tci[e];
+    tbl_ins[tb + e] = tins[e];
+  }
+  if (err) atomicOr(err_out, err);
+}
+
+// A deleted map: its entries become DEAD (never matched; reclaimed by the next compaction of their region).
+__global__ void k_map_drop(uint32_t* __restrict__ tbl_word, uint64_t entries, uint32_t slot) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= entries) return;
+  const uint32_t wv = tbl_word[e];
+  if ((wv & kMwUsed) && !(wv & kMwDead) && (wv & kMwSlotMask) == slot) tbl_word[e] = (wv & ~(kMwPresent | kMwVtagMask)) | kMwDead;
+}
+
+int launch_apply_map(const MapArgs& a, hipStream_t st) {
+  if (a.map_bits == 0 || a.tiles == 0) return 0;
+  a.mark(K_APPLY_MAP, 1, st);
+  hipLaunchKernelGGL(k_apply_map, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
+                     a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins, a.rst_status,
+                     a.rst_value, a.err);
+  a.mark(K_APPLY_MAP, 0, st);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st) {
+  hipLaunchKernelGGL(k_map_drop, dim3((uint32_t)((entries + 255) / 256)), dim3(256), 0, st, tbl_word, entries, slot);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cc

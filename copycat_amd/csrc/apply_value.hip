@@ -264,7 +264,7 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
 
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {
   a.mark(K_APPLY_VALUE, 1, st);
-  hipLaunchKernelGGL(k_apply_value, dim3(a.sb), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.val_meta,
+  hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.val_meta,
                      a.val_v, a.rst_status, a.rst_value, a.err);
   a.mark(K_APPLY_VALUE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

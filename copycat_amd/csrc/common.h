@@ -13,10 +13,14 @@ constexpr int kLaneRes = 64;              // an apply wave owns 64 resource slot
 constexpr int kApplyWaves = 4;            // apply workgroup = 4 waves = one super-bucket of 256 slots
 constexpr int kSbShift = 8;               // super-bucket = slot >> 8
 constexpr int kMaxSb = 512;               // => max_resources <= 131072 with 256-slot super-buckets
+constexpr int kMapRegion = 2048;          // map table entries per region (one map apply workgroup, LDS-resident)
+constexpr int kMaxMapSb = 1024;           // map regions => map_capacity <= 2M entries
+constexpr int kMaxSbTotal = kMaxSb + kMaxMapSb;
 constexpr int kPT = 1024;                 // partition workgroup threads (16 waves)
 constexpr int kPW = kPT / kWave;
 constexpr int kTile = 16384;              // commits per partition tile (one workgroup)
-constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a tile
+constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a tile (value-only engines)
+constexpr int kChunkMaps = 2048;          // ... when map commits (bigger records) share the partition
 constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan (1024-thread WG)
 constexpr int kApplyPer = 8;              // staging records per apply thread per chunk (prefetch depth)
 constexpr int kMaxTiles = 1024;           // tiles per sub-batch => sub-batch <= 16M commits
@@ -25,6 +29,7 @@ constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 // device error bits (d_err)
 constexpr uint32_t kErrUnsupported = 1u;
 constexpr uint32_t kErrEvents = 2u;
+constexpr uint32_t kErrCapacity = 4u;     // a map table region is full
 
 // staging record meta word (u32): op(8) | flags(8) | slot-within-super-bucket(<=10 bits) << 16
 __host__ __device__ inline uint32_t smeta_op(uint32_t m) { return m & 0xFF; }
@@ -69,7 +74,32 @@ __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {
 // ops this build applies on the GPU (others raise CC_ERR_UNSUPPORTED for the batch)
 __host__ __device__ inline bool op_on_gpu(uint32_t type, uint32_t op) {
   if (type == CC_RES_VALUE) return op == CC_OP_DELETE || (op >= 50 && op <= 53);
+  if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops; map-wide ops are next
   return false;
 }
+
+// Map key placement: (map slot, key tag, key) -> 64-bit hash; the top bits pick the table region (= map
+// super-bucket), the low bits the first probe inside it.  Shared by the partition and the map apply kernel.
+__host__ __device__ inline uint64_t map_hash(uint32_t res, uint32_t ktag, uint64_t key) {
+  uint64_t h = key ^ ((uint64_t)res << 32) ^ ((uint64_t)ktag << 61) ^ 0x9E3779B97F4A7C15ull;
+  h ^= h >> 30;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 31;
+  return h;
+}
+// map table entry word: slot(17) | ktag(2) << 17 | USED << 19 | PRESENT << 20 | vtag(3) << 21 | PENDING << 24 | DEAD << 25
+constexpr uint32_t kMwSlotMask = (1u << 17) - 1;
+constexpr uint32_t kMwUsed = 1u << 19;
+constexpr uint32_t kMwPresent = 1u << 20;
+constexpr uint32_t kMwVtagMask = 7u << 21;
+constexpr uint32_t kMwPending = 1u << 24;  // bound this round, key not yet visible (apply_map resolution)
+constexpr uint32_t kMwDead = 1u << 25;     // entry of a deleted map: never matches, reclaimed by compaction
+constexpr uint32_t kMwIdentMask = kMwSlotMask | (3u << 17) | kMwUsed | kMwDead;
+// staging meta: op | flags << 8 | slot low byte << 16 | (map records) ttl > 0 << 24
+constexpr uint32_t kMetaTtl = 1u << 24;
+__host__ __device__ inline uint32_t mw_ident(uint32_t res, uint32_t ktag) { return (res & kMwSlotMask) | ((ktag & 3) << 17) | kMwUsed; }
+__host__ __device__ inline uint32_t mw_vtag(uint32_t w) { return (w >> 21) & 7; }
 
 }  // namespace cc

@@ -39,7 +39,10 @@ struct cc_engine {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t last_stream = nullptr;
-  uint32_t sb = 0, sb_bits = 0;  // super-buckets of 256 slots
+  uint32_t sb = 0, sb_bits = 0;  // value super-buckets of 256 slots
+  uint32_t map_bits = 0;         // 2^map_bits map table regions follow them (0: no maps)
+  uint64_t map_entries = 0;
+  uint32_t sb_total() const { return sb + (map_bits ? 1u << map_bits : 0u); }
   uint64_t sub_batch = 0, max_tiles = 0;
   // host mirrors of the registry
   std::vector<uint8_t> res_type;     // [sb*256]
@@ -60,6 +63,15 @@ struct cc_engine {
   uint8_t* d_rst_status = nullptr;
   uint64_t* d_rst_value = nullptr;
   uint32_t* d_err = nullptr;
+  // map table (apply_map.hip) + map staging columns
+  uint64_t* d_tbl_key = nullptr;
+  uint32_t* d_tbl_word = nullptr;
+  uint64_t* d_tbl_val = nullptr;
+  uint64_t* d_tbl_ci = nullptr;
+  uint64_t* d_tbl_ins = nullptr;
+  uint32_t* d_st_res = nullptr;
+  uint64_t* d_st_key = nullptr;
+  uint64_t* d_st_idx = nullptr;
   uint64_t applied = 0;
   bool applied_pending = false;
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
@@ -116,7 +128,9 @@ static void free_all(cc_engine* e) {
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
   e->ev_pool.clear();
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta,   e->d_val_v,     e->d_st_meta, e->d_st_ab,
-                  e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value};
+                  e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
+                  e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_st_res,
+                  e->d_st_key,   e->d_st_idx};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -138,6 +152,15 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   e->sb = (cfg->max_resources + (1u << kSbShift) - 1) >> kSbShift;
   e->sb_bits = 0;
   while ((1u << e->sb_bits) < e->sb) ++e->sb_bits;
+  if (cfg->map_capacity) {  // regions of 2048 entries, load <= 1/2
+    if (cfg->map_capacity > (uint64_t)kMaxMapSb * kMapRegion / 2) {
+      delete e;
+      return set_err(CC_ERR_CAPACITY, "map_capacity must be <= 1048576");
+    }
+    e->map_bits = 1;
+    while (((uint64_t)kMapRegion << e->map_bits) < 2 * cfg->map_capacity) ++e->map_bits;
+    e->map_entries = (uint64_t)kMapRegion << e->map_bits;
+  }
   // sub-batch: a multiple of the partition tile (keeps every sub-batch start 16 KiB-aligned)
   uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
   sub = std::min<uint64_t>(sub, cfg->max_batch);
@@ -169,7 +192,17 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_st_meta, sizeof(uint32_t) * e->sub_batch);
   ALLOC(e->d_st_ab, sizeof(u64x2) * e->sub_batch);
   ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
-  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sb + 1));
+  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sb_total() + 1));
+  if (e->map_bits) {
+    ALLOC(e->d_tbl_key, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_tbl_word, sizeof(uint32_t) * e->map_entries);
+    ALLOC(e->d_tbl_val, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_tbl_ci, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_tbl_ins, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_st_res, sizeof(uint32_t) * e->sub_batch);
+    ALLOC(e->d_st_key, sizeof(uint64_t) * e->sub_batch);
+    ALLOC(e->d_st_idx, sizeof(uint64_t) * e->sub_batch);
+  }
   ALLOC(e->d_rst_status, e->sub_batch);
   ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
   ALLOC(e->d_err, sizeof(uint32_t));
@@ -182,6 +215,11 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if ((he = hipMemset(e->d_val_meta, 0, sizeof(uint32_t) * slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_val_v, 0, sizeof(uint64_t) * slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
+  if (e->map_bits) {  // word 0 = empty entry
+    if ((he = hipMemset(e->d_tbl_word, 0, sizeof(uint32_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_tbl_ci, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_tbl_ins, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
+  }
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
   // the stable rankings of k_part_scatter / k_apply_value need same-address LDS atomics of one wave
   // instruction to resolve in lane order: verify on this device before trusting any result
@@ -216,8 +254,11 @@ static int check_device_err(cc_engine* e) {
   HIPCHECK(hipMemcpy(&err, e->d_err, sizeof err, hipMemcpyDeviceToHost));
   if (err) {
     HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
+    if (err & kErrCapacity) return set_err(CC_ERR_CAPACITY, "a map table region is full (raise map_capacity)");
     if (err & kErrUnsupported)
-      return set_err(CC_ERR_UNSUPPORTED, "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten)");
+      return set_err(CC_ERR_UNSUPPORTED,
+                     "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten; map "
+                     "containsValue/size/isEmpty/clear/Delete; map ops with ttl > 0)");
     return set_err(CC_ERR_STATE, "device-side check failed");
   }
   return CC_OK;
@@ -245,8 +286,9 @@ static int quiesce(cc_engine* e) {
 }
 
 static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
-  if (type != CC_RES_VALUE)
-    return set_err(CC_ERR_UNSUPPORTED, "this build applies AtomicValue resources on the GPU; map/lock/election/group are not built yet");
+  if (type == CC_RES_MAP && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map resources need cc_config.map_capacity > 0");
+  if (type != CC_RES_VALUE && type != CC_RES_MAP)
+    return set_err(CC_ERR_UNSUPPORTED, "this build applies AtomicValue and Map resources on the GPU; lock/election/group are not built yet");
   const uint64_t end = (uint64_t)first + count;
   if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");
   for (uint64_t s = first; s < end; ++s) {
@@ -285,6 +327,11 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   int rc = quiesce(e);
   if (rc) return rc;
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
+  if (e->res_type[slot] == CC_RES_MAP) {  // MapState.delete :264-274 — the map's entries die with it
+    if (launch_map_drop_resource(e->d_tbl_word, e->map_entries, slot, e->own_stream))
+      return set_err(CC_ERR_HIP, "map drop launch", hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(e->own_stream));
+  }
   e->res_type[slot] = CC_RES_NONE;
   const uint32_t b = slot / kLaneRes;
   if (--e->bucket_live[b] == 0) e->bucket_type[b] = CC_RES_NONE;
@@ -345,22 +392,32 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   e->last_stream = st;
   if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15) || (((uintptr_t)c->inst) & 15))
     return set_err(CC_ERR_INVALID, "inst and value must be 16-byte aligned, status 4-byte aligned");
+  if (e->map_bits && !c->key) return set_err(CC_ERR_INVALID, "an engine with maps needs the key column");
   for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
     const uint64_t hi = std::min(n, lo + e->sub_batch);
+    const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
     PartArgs pa{};
     pa.inst = c->inst;
     pa.op = c->op;
     pa.flags = c->flags;
     pa.a = c->a;
     pa.b = c->b;
+    pa.key = c->key;
+    pa.index = c->index;
+    pa.aux = c->aux;
     pa.lo = lo;
     pa.hi = hi;
     pa.inst_res = e->d_inst_res;
+    pa.res_type = e->d_res_type;
     pa.max_inst = e->cfg.max_instances;
-    pa.sb = e->sb;
-    pa.sb_shift = kSbShift;
+    pa.sb = e->sb_total();
+    pa.sb_val = e->sb;
+    pa.map_bits = e->map_bits;
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
+    pa.st_res = e->d_st_res;
+    pa.st_key = e->d_st_key;
+    pa.st_idx = e->d_st_idx;
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
     pa.mark = marker_of(e);
@@ -369,8 +426,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.st_meta = e->d_st_meta;
     va.st_ab = e->d_st_ab;
     va.ttab = e->d_ttab;
-    va.tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
-    va.sb = e->sb;
+    va.tiles = tiles;
+    va.sb = e->sb_total();
+    va.sb_val = e->sb;
     va.val_meta = e->d_val_meta;
     va.val_v = e->d_val_v;
     va.rst_status = e->d_rst_status;
@@ -378,10 +436,33 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.err = e->d_err;
     va.mark = marker_of(e);
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
+    if (e->map_bits) {
+      MapArgs ma{};
+      ma.st_meta = e->d_st_meta;
+      ma.st_ab = e->d_st_ab;
+      ma.st_res = e->d_st_res;
+      ma.st_key = e->d_st_key;
+      ma.st_idx = e->d_st_idx;
+      ma.ttab = e->d_ttab;
+      ma.tiles = tiles;
+      ma.sb = e->sb_total();
+      ma.sb_val = e->sb;
+      ma.map_bits = e->map_bits;
+      ma.tbl_key = e->d_tbl_key;
+      ma.tbl_word = e->d_tbl_word;
+      ma.tbl_val = e->d_tbl_val;
+      ma.tbl_ci = e->d_tbl_ci;
+      ma.tbl_ins = e->d_tbl_ins;
+      ma.rst_status = e->d_rst_status;
+      ma.rst_value = e->d_rst_value;
+      ma.err = e->d_err;
+      ma.mark = marker_of(e);
+      if (launch_apply_map(ma, st)) return set_err(CC_ERR_HIP, "map apply launch", hipGetLastError());
+    }
     UnpermuteArgs ua{};
     ua.cpos = e->d_cpos;
     ua.ttab = e->d_ttab;
-    ua.sb = e->sb;
+    ua.sb = e->sb_total();
     ua.lo = lo;
     ua.hi = hi;
     ua.rst_status = e->d_rst_status;
@@ -480,7 +561,42 @@ extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count,
   return CC_OK;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute"};
+extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag,
+                                   uint64_t* h_key, uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index) {
+  if (!e || !count || slot >= e->cfg.max_resources || e->res_type[slot] != CC_RES_MAP)
+    return set_err(CC_ERR_INVALID, "not a map slot");
+  if (cap && (!h_key_tag || !h_key || !h_value_tag || !h_value)) return set_err(CC_ERR_INVALID, "null output");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  const uint64_t n = e->map_entries;
+  std::vector<uint64_t> key(n), val(n), ci(n);
+  std::vector<uint32_t> word(n);
+  HIPCHECK(hipMemcpy(key.data(), e->d_tbl_key, 8 * n, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(word.data(), e->d_tbl_word, 4 * n, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(val.data(), e->d_tbl_val, 8 * n, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(ci.data(), e->d_tbl_ci, 8 * n, hipMemcpyDeviceToHost));
+  static const uint8_t ktag_tag[4] = {CC_TAG_LONG, CC_TAG_INT, CC_TAG_BOOL, CC_TAG_HANDLE};
+  struct Row { uint8_t kt; uint64_t k; uint8_t vt; uint64_t v, ci; };
+  std::vector<Row> rows;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t w = word[i];
+    if ((w & kMwUsed) && (w & kMwPresent) && !(w & kMwDead) && (w & kMwSlotMask) == slot)
+      rows.push_back(Row{ktag_tag[(w >> 17) & 3], key[i], (uint8_t)mw_vtag(w), val[i], ci[i]});
+  }
+  std::sort(rows.begin(), rows.end(), [](const Row& x, const Row& y) { return x.kt != y.kt ? x.kt < y.kt : x.k < y.k; });
+  *count = rows.size();
+  const uint64_t m = std::min<uint64_t>(cap, rows.size());
+  for (uint64_t i = 0; i < m; ++i) {
+    h_key_tag[i] = rows[i].kt;
+    h_key[i] = rows[i].k;
+    h_value_tag[i] = rows[i].vt;
+    h_value[i] = rows[i].v;
+    if (h_commit_index) h_commit_index[i] = rows[i].ci;
+  }
+  return CC_OK;
+}
+
+static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map"};
 
 extern "C" int cc_profile_enable(cc_engine* e, int on) {
   if (!e) return CC_ERR_INVALID;

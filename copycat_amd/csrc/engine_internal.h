@@ -5,7 +5,7 @@
 namespace cc {
 
 // Optional per-kernel timing (HIP events recorded on the launch stream around each kernel).
-enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_NUM };
+enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_APPLY_MAP, K_NUM };
 struct Marker {
   void (*fn)(void* ctx, int kernel, int begin, hipStream_t st);
   void* ctx;
@@ -22,25 +22,35 @@ struct PartArgs {
   const uint8_t* flags;
   const uint64_t* a;
   const uint64_t* b;
+  const uint64_t* key;    // maps only
+  const uint64_t* index;  // maps only (commit index of map entries)
+  const uint64_t* aux;    // maps only (ttl > 0 is not applied on the GPU)
   uint64_t lo, hi;
   const uint32_t* inst_res;
+  const uint8_t* res_type;
   uint32_t max_inst;
-  uint32_t sb, sb_shift;  // super-buckets
+  uint32_t sb;        // super-buckets in total = sb_val + 2^map_bits (0 map bits: no maps)
+  uint32_t sb_val;
+  uint32_t map_bits;
   uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
   u64x2* st_ab;
+  uint32_t* st_res;   // map records: resource slot, key, log index
+  uint64_t* st_key;
+  uint64_t* st_idx;
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
-size_t tile_lds_bytes(uint32_t sb);
+size_t tile_lds_bytes(uint32_t sb, bool maps);
 
 struct ValueArgs {
   const uint32_t* st_meta;
   const u64x2* st_ab;
   const uint16_t* ttab;
   uint32_t tiles;
-  uint32_t sb;
+  uint32_t sb;           // total super-buckets (ttab row width - 1)
+  uint32_t sb_val;       // value super-buckets (the apply grid)
   uint32_t* val_meta;    // [sb*256]
   uint64_t* val_v;       // [sb*256]
   uint8_t* rst_status;   // staged results [sub_batch]
@@ -50,6 +60,30 @@ struct ValueArgs {
 };
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
+
+struct MapArgs {
+  const uint32_t* st_meta;
+  const u64x2* st_ab;
+  const uint32_t* st_res;
+  const uint64_t* st_key;
+  const uint64_t* st_idx;
+  const uint16_t* ttab;
+  uint32_t tiles;
+  uint32_t sb;  // total super-buckets (ttab row width - 1)
+  uint32_t sb_val;
+  uint32_t map_bits;
+  uint64_t* tbl_key;  // [2^map_bits * kMapRegion]
+  uint32_t* tbl_word;
+  uint64_t* tbl_val;
+  uint64_t* tbl_ci;
+  uint64_t* tbl_ins;
+  uint8_t* rst_status;
+  uint64_t* rst_value;
+  uint32_t* err;
+  Marker mark;
+};
+int launch_apply_map(const MapArgs& a, hipStream_t st);
+int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
 
 struct UnpermuteArgs {
   const uint16_t* cpos;

@@ -6,13 +6,17 @@
 // ResourceManager.java:37-39) but commits on the SAME resource form a sequential chain.  The engine therefore
 // regroups a batch so that one workgroup owns 256 resources and sees exactly their commits, in log order.
 //
+// Super-buckets: value resources by slot (slot >> 8, 256 slots each); map commits by hash(map, key) into
+// one of 2^map_bits table regions that follow them (a map's keys are independent chains).
+//
 // Layout: the sub-batch is cut into 16384-commit tiles; tile t owns staging positions [t*16384, (t+1)*16384)
 // and stores its live commits there sorted by super-bucket (stable, so log order within each run).  The run
 // of super-bucket k in tile t starts at ttab[t][k] (tile-local); ttab[t][sb] = live commits of the tile.
 // No global scan is needed: the apply workgroup of super-bucket k walks its run in every tile, in tile order.
 //
 //   k_part_tile  : per tile: (0) histogram of the tile over super-buckets -> tile-local run starts;
-//                  (1..4) 4 chunks of 4096 commits: a stable multisplit of the chunk in LDS (ranking inside a
+//                  (1..) chunks of 4096 commits (2048 when map commits share the batch): a stable multisplit of
+//                  the chunk in LDS (ranking inside a
 //                  wave by LDS atomics with return, per-wave prefix sums across the 16 waves), then the chunk is
 //                  written out run by run (contiguous stores), and each commit's tile-local position -> cpos.
 //   k_unpermute  : per tile: the tile's staged results are read contiguously into LDS and written back in log
@@ -50,32 +54,57 @@ __device__ inline uint32_t block_exscan(uint32_t v, uint32_t* wsum /*[16] LDS*/,
   return wpre + inc - v;
 }
 
-size_t tile_lds_bytes(uint32_t sb) {
-  return (size_t)kChunk * (16 + 4 + 2) + (size_t)kPW * sb * 4 + (size_t)4 * sb * 4 + 16 * 4;
+// Per-wave counters are packed u16 pairs (a wave ranks at most 256 commits of a chunk): wc[w][k/2].
+size_t tile_lds_bytes(uint32_t sb, bool maps) {
+  const size_t chunk = maps ? kChunkMaps : kChunk;
+  const size_t rec = 16 + 4 + 2 + (maps ? 4 + 8 + 8 : 0);
+  return chunk * rec + (size_t)kPW * ((sb + 1) / 2) * 4 + (size_t)4 * sb * 4 + 16 * 4;
 }
 
-// LDS layout (dynamic): rab[kChunk] u64x2 | rmeta[kChunk] u32 | rsb[kChunk] u16 | wc[kPW][sb] u32 |
-//                       toff, trun, ctot, kstart [sb] u32 | wsum[16] u32
+// Super-bucket of a commit: value resources by slot (slot >> 8); map commits by hash(map, key) into the map
+// regions that follow the value super-buckets.
+template <bool MAPS>
+__device__ inline uint32_t route(uint32_t r, uint32_t f, uint64_t key, const uint8_t* __restrict__ res_type, uint32_t sb_val,
+                                 uint32_t map_bits, bool& is_map) {
+  is_map = false;
+  if (MAPS && res_type[r] == CC_RES_MAP) {
+    is_map = true;
+    return sb_val + (uint32_t)(map_hash(r, CC_FLAG_KTAG(f), key) >> (64 - map_bits));
+  }
+  return r >> kSbShift;
+}
+
+// LDS layout (dynamic): rab[C] u64x2 | [MAPS: rkey[C] u64 | ridx[C] u64 | rres[C] u32] | rmeta[C] u32 |
+//                       rsb[C] u16 | wc[kPW][(sb+1)/2] u32 | toff, trun, ctot, kstart [sb] u32 | wsum[16] u32
+template <int J, bool MAPS>
 __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
-                                                const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
-                                                const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
-                                                uint32_t sb_shift, uint32_t* __restrict__ st_meta,
-                                                u64x2* __restrict__ st_ab, uint16_t* __restrict__ cpos,
+                                                const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
+                                                const uint64_t* __restrict__ cidx, const uint64_t* __restrict__ caux,
+                                                uint64_t lo, uint64_t hi,
+                                                const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
+                                                uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits,
+                                                uint32_t* __restrict__ st_meta, u64x2* __restrict__ st_ab,
+                                                uint32_t* __restrict__ st_res, uint64_t* __restrict__ st_key,
+                                                uint64_t* __restrict__ st_idx, uint16_t* __restrict__ cpos,
                                                 uint16_t* __restrict__ ttab) {
+  constexpr int C = J * kPT;  // commits per chunk
   extern __shared__ __align__(16) uint8_t smem[];
   u64x2* rab = reinterpret_cast<u64x2*>(smem);
-  uint32_t* rmeta = reinterpret_cast<uint32_t*>(rab + kChunk);
-  uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + kChunk);
-  uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + kChunk);  // [kPW][sb]
-  uint32_t* toff = wc + kPW * sb;
+  uint64_t* rkey = reinterpret_cast<uint64_t*>(rab + C);
+  uint64_t* ridx = rkey + (MAPS ? C : 0);
+  uint32_t* rres = reinterpret_cast<uint32_t*>(ridx + (MAPS ? C : 0));
+  uint32_t* rmeta = rres + (MAPS ? C : 0);
+  uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + C);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + C);  // [kPW][hw] packed u16 pairs
+  const uint32_t hw = (sb + 1) / 2;
+  uint32_t* toff = wc + kPW * hw;
   uint32_t* trun = toff + sb;
   uint32_t* ctot = trun + sb;
   uint32_t* kstart = ctot + sb;
   uint32_t* wsum = kstart + sb;
 
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  const uint32_t rmask = (1u << sb_shift) - 1;
   const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
   const uint64_t tile1 = tile0 + kTile < hi ? tile0 + kTile : hi;
   const uint32_t tbase = blockIdx.x * kTile;  // staging region of this tile (relative to lo)
@@ -83,49 +112,67 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   // 0. histogram of the whole tile -> tile-local run starts (ttab row)
   for (uint32_t k = t; k < sb; k += kPT) ctot[k] = 0;
   lds_barrier();
-  {
+  if (!MAPS) {
     const uint64_t q1 = tile1 / 4;
 #pragma unroll 4
     for (uint64_t q = tile0 / 4 + t; q < q1; q += kPT) {
       const uint4 v = reinterpret_cast<const uint4*>(inst)[q];
       const uint32_t r0 = resolve(inst_res, max_inst, v.x), r1 = resolve(inst_res, max_inst, v.y);
       const uint32_t r2 = resolve(inst_res, max_inst, v.z), r3 = resolve(inst_res, max_inst, v.w);
-      if (r0 != kNoRes) atomicAdd(&ctot[r0 >> sb_shift], 1u);
-      if (r1 != kNoRes) atomicAdd(&ctot[r1 >> sb_shift], 1u);
-      if (r2 != kNoRes) atomicAdd(&ctot[r2 >> sb_shift], 1u);
-      if (r3 != kNoRes) atomicAdd(&ctot[r3 >> sb_shift], 1u);
+      if (r0 != kNoRes) atomicAdd(&ctot[r0 >> kSbShift], 1u);
+      if (r1 != kNoRes) atomicAdd(&ctot[r1 >> kSbShift], 1u);
+      if (r2 != kNoRes) atomicAdd(&ctot[r2 >> kSbShift], 1u);
+      if (r3 != kNoRes) atomicAdd(&ctot[r3 >> kSbShift], 1u);
     }
     for (uint64_t i = q1 * 4 + t; i < tile1; i += kPT) {  // ragged tail (< 4 commits)
       const uint32_t r = resolve(inst_res, max_inst, inst[i]);
-      if (r != kNoRes) atomicAdd(&ctot[r >> sb_shift], 1u);
+      if (r != kNoRes) atomicAdd(&ctot[r >> kSbShift], 1u);
+    }
+  } else {
+#pragma unroll 4
+    for (uint64_t i = tile0 + t; i < tile1; i += kPT) {
+      const uint32_t r = resolve(inst_res, max_inst, inst[i]);
+      if (r == kNoRes) continue;
+      bool is_map;
+      const uint32_t f = res_type[r] == CC_RES_MAP ? flags[i] : 0;
+      const uint64_t key = res_type[r] == CC_RES_MAP ? ckey[i] : 0;
+      atomicAdd(&ctot[route<MAPS>(r, f, key, res_type, sb_val, map_bits, is_map)], 1u);
     }
   }
   lds_barrier();
   {
-    uint32_t total;
-    const uint32_t ex = block_exscan(t < sb ? ctot[t] : 0, wsum, &total);  // sb <= kPT
     uint16_t* row = ttab + (uint64_t)blockIdx.x * (sb + 1);
-    if (t < sb) {
-      toff[t] = ex;
-      trun[t] = 0;
-      row[t] = (uint16_t)ex;
+    uint32_t run = 0;
+    for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform
+      const uint32_t k = k0 + t;
+      uint32_t part;
+      const uint32_t ex = block_exscan(k < sb ? ctot[k] : 0, wsum, &part);
+      if (k < sb) {
+        toff[k] = run + ex;
+        trun[k] = 0;
+        row[k] = (uint16_t)(run + ex);
+      }
+      run += part;
     }
-    if (t == 0) row[sb] = (uint16_t)total;  // live commits of the tile (<= 16384)
+    if (t == 0) row[sb] = (uint16_t)run;  // live commits of the tile (<= 16384)
   }
 
-  constexpr int J = kChunk / kPT;  // commits per thread per chunk
   // commit (w, j, l) of a chunk is cbase + w*(64*J) + j*64 + l: log order = (w, j, l).
   // Prefetch in two stages so no wave stalls on the instance->resource gather right after its load:
   // raw columns of chunk c+1 are requested at the top of chunk c, their gathers after chunk c's ranking.
   uint32_t res[J], meta[J], ninst[J], nmeta[J];
   u64x2 ab[J], nab[J];
-  auto load_raw = [&](uint64_t cbase, uint32_t (&in)[J], uint32_t (&mt)[J], u64x2 (&aa)[J]) {
+  uint64_t key[J], idx[J], nkey[J], nidx[J];
+  auto load_raw = [&](uint64_t cbase, uint32_t (&in)[J], uint32_t (&mt)[J], u64x2 (&aa)[J], uint64_t (&kk)[J],
+                      uint64_t (&ii)[J]) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
       in[j] = kNoRes;
       mt[j] = 0;
       aa[j] = u64x2{0, 0};
+      kk[j] = 0;
+      ii[j] = 0;
       if (i < hi) {
         in[j] = inst[i];
         mt[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
@@ -134,47 +181,64 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       }
     }
   };
-  auto gather = [&](const uint32_t (&in)[J], uint32_t (&rr)[J]) {
+  // gathers: instance -> resource, and (maps only) the key, log index and ttl sign of map commits
+  auto gather = [&](uint64_t cbase, const uint32_t (&in)[J], uint32_t (&rr)[J], uint32_t (&mt)[J], uint64_t (&kk)[J],
+                    uint64_t (&ii)[J]) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) rr[j] = in[j] == kNoRes ? kNoRes : resolve(inst_res, max_inst, in[j]);
+    for (int j = 0; j < J; ++j) {
+      rr[j] = in[j] == kNoRes ? kNoRes : resolve(inst_res, max_inst, in[j]);
+      if (MAPS && rr[j] != kNoRes && res_type[rr[j]] == CC_RES_MAP) {
+        const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+        kk[j] = ckey[i];
+        ii[j] = cidx ? cidx[i] : 0;
+        if (caux && (int64_t)caux[i] > 0) mt[j] |= kMetaTtl;
+      }
+    }
   };
-  load_raw(tile0, ninst, meta, ab);
-  gather(ninst, res);
-  for (uint32_t ch = 0; ch < kTile / kChunk; ++ch) {
-    const uint64_t cbase = tile0 + (uint64_t)ch * kChunk;
+  load_raw(tile0, ninst, meta, ab, key, idx);
+  gather(tile0, ninst, res, meta, key, idx);
+  for (uint32_t ch = 0; ch < kTile / C; ++ch) {
+    const uint64_t cbase = tile0 + (uint64_t)ch * C;
     if (cbase >= hi) break;  // block-uniform
-    const bool more = ch + 1 < kTile / kChunk && cbase + kChunk < hi;
-    if (more) load_raw(cbase + kChunk, ninst, nmeta, nab);
-    for (uint32_t k = t; k < kPW * sb; k += kPT) wc[k] = 0;
+    const bool more = ch + 1 < kTile / C && cbase + C < hi;
+    if (more) load_raw(cbase + C, ninst, nmeta, nab, nkey, nidx);
+    for (uint32_t k = t; k < kPW * hw; k += kPT) wc[k] = 0;
     lds_barrier();
     // 1. rank by super-bucket inside each wave: the wave's own counter table, LDS atomics with return
     //    (same-address lanes of one instruction resolve in lane order on gfx950 — checked at engine start)
-    uint32_t key[J], loc[J];
-    bool live[J];
+    uint32_t sk[J], loc[J];
+    bool live[J], ismap[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       live[j] = res[j] != kNoRes;
-      key[j] = live[j] ? (res[j] >> sb_shift) : 0;
-      loc[j] = live[j] ? atomicAdd(&wc[w * sb + key[j]], 1u) : 0;
+      sk[j] = live[j] ? route<MAPS>(res[j], meta[j] >> 8, key[j], res_type, sb_val, map_bits, ismap[j]) : 0;
+      if (!live[j]) ismap[j] = false;
+      const uint32_t sh = 16 * (sk[j] & 1);
+      loc[j] = live[j] ? (atomicAdd(&wc[w * hw + (sk[j] >> 1)], 1u << sh) >> sh) & 0xFFFF : 0;
     }
     uint32_t nres[J];
-    if (more) gather(ninst, nres);
+    if (more) gather(cbase + C, ninst, nres, nmeta, nkey, nidx);
     lds_barrier();
-    // 2. per super-bucket: exclusive prefix over waves and chunk totals; then chunk-sorted starts
-    for (uint32_t k = t; k < sb; k += kPT) {
-      uint32_t run = 0;
+    // 2. per super-bucket: exclusive prefix over waves (packed halves) and chunk totals; chunk-sorted starts
+    for (uint32_t kw = t; kw < hw; kw += kPT) {
+      uint32_t r0 = 0, r1 = 0;
       for (uint32_t q = 0; q < kPW; ++q) {
-        const uint32_t c = wc[q * sb + k];
-        wc[q * sb + k] = run;
-        run += c;
+        const uint32_t c = wc[q * hw + kw];
+        wc[q * hw + kw] = r0 | (r1 << 16);
+        r0 += c & 0xFFFF;
+        r1 += c >> 16;
       }
-      ctot[k] = run;
+      ctot[2 * kw] = r0;
+      if (2 * kw + 1 < sb) ctot[2 * kw + 1] = r1;
     }
     lds_barrier();
-    uint32_t nlive;
-    {
-      const uint32_t ex = block_exscan(t < sb ? ctot[t] : 0, wsum, &nlive);
-      if (t < sb) kstart[t] = ex;
+    uint32_t nlive = 0;
+    for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform
+      const uint32_t k = k0 + t;
+      uint32_t part;
+      const uint32_t ex = block_exscan(k < sb ? ctot[k] : 0, wsum, &part);
+      if (k < sb) kstart[k] = nlive + ex;
+      nlive += part;
     }
     lds_barrier();
     // 3. place records in LDS in sorted order; per-commit tile-local position
@@ -186,12 +250,18 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
         cpos[i - lo] = 0xFFFF;
         continue;
       }
-      const uint32_t within = wc[w * sb + key[j]] + loc[j];
-      const uint32_t s = kstart[key[j]] + within;
+      const uint32_t pre = (wc[w * hw + (sk[j] >> 1)] >> (16 * (sk[j] & 1))) & 0xFFFF;
+      const uint32_t within = pre + loc[j];
+      const uint32_t s = kstart[sk[j]] + within;
       rab[s] = ab[j];
-      rmeta[s] = meta[j] | ((res[j] & rmask) << 16);
-      rsb[s] = (uint16_t)key[j];
-      cpos[i - lo] = (uint16_t)(toff[key[j]] + trun[key[j]] + within);
+      rmeta[s] = meta[j] | ((res[j] & ((1u << kSbShift) - 1)) << 16);
+      rsb[s] = (uint16_t)sk[j];
+      if (MAPS) {
+        rres[s] = res[j];
+        rkey[s] = key[j];
+        ridx[s] = idx[j];
+      }
+      cpos[i - lo] = (uint16_t)(toff[sk[j]] + trun[sk[j]] + within);
     }
     lds_barrier();
     // 4. write the chunk out run by run (contiguous)
@@ -200,6 +270,11 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
       st_meta[g] = rmeta[s];
       st_ab[g] = rab[s];
+      if (MAPS && k >= sb_val) {
+        st_res[g] = rres[s];
+        st_key[g] = rkey[s];
+        st_idx[g] = ridx[s];
+      }
     }
     lds_barrier();
     for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
@@ -209,6 +284,8 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
         res[j] = nres[j];
         meta[j] = nmeta[j];
         ab[j] = nab[j];
+        key[j] = nkey[j];
+        idx[j] = nidx[j];
       }
     }
   }
@@ -258,9 +335,16 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
 int launch_partition(const PartArgs& a, hipStream_t st) {
   const uint32_t tiles = (uint32_t)((a.hi - a.lo + kTile - 1) / kTile);
   if (tiles == 0) return 0;
+  const bool maps = a.map_bits != 0;
   a.mark(K_PART_TILE, 1, st);
-  hipLaunchKernelGGL(k_part_tile, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb), st, a.inst, a.op, a.flags, a.a, a.b, a.lo,
-                     a.hi, a.inst_res, a.max_inst, a.sb, a.sb_shift, a.st_meta, a.st_ab, a.cpos, a.ttab);
+  if (maps)
+    hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true), st, a.inst,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
+                       a.sb_val, a.map_bits, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+  else
+    hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false), st, a.inst,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
+                       a.sb_val, a.map_bits, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -2,8 +2,11 @@
 //
 // These are the benches' and tests' inputs, not part of the apply path.  Each generator writes SoA columns
 // in the layout of cc_batch (include/copycat_apply.h).
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/copycat_apply.h"
@@ -117,6 +120,130 @@ uint64_t wl_value_random(uint64_t n, uint32_t resources, uint32_t first_inst, ui
     a[i] = pa;
     b[i] = pb;
   }
+  return n;
+}
+
+// MapState parity stream (adversarial): every key op, all key and value tags, null values, hot keys, ops of
+// other resource types on a map (UNKNOWN_OP) and unknown instance slots.  Map m is instance slot first_inst + m.
+// aux (ttl) is 0 or negative (no timer); small value domains make the conditional ops hit.
+uint64_t wl_map_random(uint64_t n, uint32_t maps, uint32_t first_inst, uint32_t max_inst, uint32_t keys, uint64_t seed,
+                       uint32_t hot, uint32_t p_hot_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
+                       uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b, uint64_t* aux) {
+  SplitMix64 rng(seed);
+  static const uint8_t ops[] = {CC_OP_MAP_PUT, CC_OP_MAP_PUT, CC_OP_MAP_PUT, CC_OP_MAP_PUT, CC_OP_MAP_PUT,
+                                CC_OP_MAP_PUTIFABSENT, CC_OP_MAP_PUTIFABSENT, CC_OP_MAP_GET, CC_OP_MAP_GET, CC_OP_MAP_GET,
+                                CC_OP_MAP_GETORDEFAULT, CC_OP_MAP_CONTAINSKEY, CC_OP_MAP_REMOVE, CC_OP_MAP_REMOVE,
+                                CC_OP_MAP_REMOVEIFPRESENT, CC_OP_MAP_REMOVEIFPRESENT, CC_OP_MAP_REPLACE, CC_OP_MAP_REPLACE,
+                                CC_OP_MAP_REPLACEIFPRESENT, CC_OP_MAP_REPLACEIFPRESENT};
+  auto rand_val = [&](uint8_t& t, uint64_t& p) {
+    const uint64_t k = rng.below(16);
+    t = k < 3 ? CC_TAG_NULL : (k < 11 ? CC_TAG_LONG : (k < 13 ? CC_TAG_INT : (k < 15 ? CC_TAG_BOOL : CC_TAG_HANDLE)));
+    p = t == CC_TAG_BOOL ? rng.below(2) : rng.below(3);
+    if (t == CC_TAG_NULL) p = rng.next();  // non-canonical payload under NULL must be ignored
+    if (t == CC_TAG_LONG && rng.below(8) == 0) p = ~p;
+  };
+  for (uint64_t i = 0; i < n; ++i) {
+    const bool is_hot = hot && rng.below(1000000) < p_hot_ppm;
+    const uint32_t m = is_hot ? (uint32_t)rng.below(std::min(hot, maps)) : (uint32_t)rng.below(maps);
+    uint32_t kt = 0;
+    uint64_t kp;
+    if (is_hot) {
+      kp = rng.below(hot);
+    } else {
+      const uint64_t q = rng.below(16);
+      kt = q < 12 ? 0 : (q < 14 ? 1 : (q < 15 ? 2 : 3));  // LONG / INT / BOOL / HANDLE keys
+      kp = kt == 2 ? rng.below(2) : rng.below(keys);
+      if (kt == 0 && rng.below(4) == 0) kp = ~kp;  // negative longs (spread over the hash)
+    }
+    uint8_t o = ops[rng.below(sizeof ops)];
+    uint32_t s = first_inst + m;
+    const uint64_t k = rng.below(1000);
+    if (k < 3) s = max_inst + (uint32_t)rng.below(1000);  // unknown instance slot
+    else if (k < 6) o = (uint8_t)(50 + rng.below(4));     // an AtomicValue op on a map: UNKNOWN_OP
+    uint8_t ta, tb;
+    uint64_t pa, pb;
+    rand_val(ta, pa);
+    rand_val(tb, pb);
+    if (index) index[i] = index0 + i;
+    if (time) time[i] = (index0 + i) / 1024;
+    inst[i] = s;
+    op[i] = o;
+    flags[i] = CC_FLAGS(ta, tb, kt);
+    key[i] = kp;
+    a[i] = pa;
+    b[i] = pb;
+    if (aux) aux[i] = rng.below(4) == 0 ? (uint64_t)(-(int64_t)rng.below(3)) : 0;  // ttl <= 0: no timer
+  }
+  return n;
+}
+
+// Config 3 stream: DistributedMap put/get/remove (45/45/10) over `pairs` (power of two) distinct
+// (map, key) pairs spread over `maps` maps; pair rank ~ Zipf(s).  Rank r -> pair (r * 0x9E3779B1 + 0x7F4A7C15)
+// mod pairs (a bijection), pair -> map pair % maps (instance slot first_inst + map), key = mix64(pair) (Long).
+// Rows [row0, row0 + n) of the stream are written; any sub-range gives the same rows (chunks are seeded by
+// their 64K-row block), so the bench can generate and upload a 1e9-row stream block by block on `threads`.
+uint64_t wl_map_zipf(uint64_t row0, uint64_t n, uint32_t maps, uint32_t pairs, double s, uint32_t first_inst,
+                     uint64_t seed, uint32_t threads, uint64_t* index, uint64_t* time, uint32_t* inst, uint8_t* op,
+                     uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b) {
+  if (!pairs || (pairs & (pairs - 1)) || !maps) return 0;
+  // Walker alias table over the Zipf pmf
+  std::vector<double> pr(pairs);
+  double z = 0;
+  for (uint32_t r = 0; r < pairs; ++r) z += (pr[r] = 1.0 / std::pow((double)r + 1.0, s));
+  std::vector<uint32_t> alias(pairs), small, large;
+  std::vector<double> q(pairs);
+  for (uint32_t r = 0; r < pairs; ++r) {
+    q[r] = pr[r] / z * pairs;
+    (q[r] < 1.0 ? small : large).push_back(r);
+  }
+  while (!small.empty() && !large.empty()) {
+    const uint32_t l = small.back(), g = large.back();
+    small.pop_back();
+    alias[l] = g;
+    q[g] -= 1.0 - q[l];
+    if (q[g] < 1.0) {
+      large.pop_back();
+      small.push_back(g);
+    }
+  }
+  for (uint32_t r : large) q[r] = 1.0, alias[r] = r;
+  for (uint32_t r : small) q[r] = 1.0, alias[r] = r;
+  std::vector<uint32_t> qthr(pairs);
+  for (uint32_t r = 0; r < pairs; ++r) qthr[r] = (uint32_t)std::min(4294967295.0, q[r] * 4294967296.0);
+  constexpr uint64_t kBlock = 65536;
+  auto gen = [&](uint64_t blk0, uint64_t blk1) {
+    for (uint64_t blk = blk0; blk < blk1; ++blk) {
+      SplitMix64 rng(seed ^ (blk * 0xD1B54A32D192ED03ull));
+      const uint64_t r0 = blk * kBlock;
+      for (uint64_t rr = r0; rr < r0 + kBlock; ++rr) {
+        const uint64_t x = rng.next(), y = rng.next(), w = rng.next();
+        if (rr < row0 || rr >= row0 + n) continue;
+        uint32_t rank = (uint32_t)(((x & 0xFFFFFFFFull) * pairs) >> 32);
+        if ((uint32_t)(x >> 32) >= qthr[rank]) rank = alias[rank];
+        const uint32_t pair = (uint32_t)(rank * 0x9E3779B1u + 0x7F4A7C15u) & (pairs - 1);
+        SplitMix64 km(pair);
+        const uint64_t i = rr - row0;
+        const uint32_t u = (uint32_t)(y % 100);
+        if (index) index[i] = 1 + rr;
+        if (time) time[i] = (1 + rr) / 1024;
+        inst[i] = first_inst + pair % maps;
+        op[i] = u < 45 ? CC_OP_MAP_PUT : (u < 90 ? CC_OP_MAP_GET : CC_OP_MAP_REMOVE);
+        flags[i] = CC_FLAGS(u < 45 ? CC_TAG_LONG : CC_TAG_NULL, CC_TAG_NULL, 0);
+        key[i] = km.next();
+        a[i] = u < 45 ? w : 0;
+        b[i] = 0;
+      }
+    }
+  };
+  const uint64_t b0 = row0 / kBlock, b1 = (row0 + n + kBlock - 1) / kBlock;
+  const uint32_t nt = std::max<uint32_t>(1, std::min<uint64_t>(threads ? threads : 1, b1 - b0));
+  std::vector<std::thread> th;
+  const uint64_t per = (b1 - b0 + nt - 1) / nt;
+  for (uint32_t t = 0; t < nt; ++t) {
+    const uint64_t lo = b0 + t * per, hi = std::min(b1, lo + per);
+    if (lo < hi) th.emplace_back(gen, lo, hi);
+  }
+  for (auto& x : th) x.join();
   return n;
 }
 

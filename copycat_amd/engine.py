@@ -53,6 +53,7 @@ def lib():
             "cc_apply_batch_host": (i32, [P, P, u64, P]),
             "cc_applied_index": (i32, [P, P]),
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
+            "cc_read_map_entries": (i32, [P, u32, u64, P, P, P, P, P, P]),
             "cc_quorum_commit": (i32, [P, u32, u64, P, P, P, P]),
             "cc_expire_sweep": (i32, [P, u64, u64, u64, P, P, P]),
             "cc_profile_enable": (i32, [P, i32]),
@@ -201,7 +202,7 @@ class Engine:
     def profile_read(self):
         """{kernel name: (total device ms, launches)} since the last profile() call (synchronizes)."""
         out = {}
-        for k in range(3):
+        for k in range(abi.CC_PROFILE_KERNELS):
             ms, n, name = C.c_double(), C.c_uint64(), C.c_char_p()
             _check(self.L.cc_profile_read(self.h, k, C.byref(ms), C.byref(n), C.byref(name)))
             out[name.value.decode()] = (ms.value, n.value)
@@ -212,6 +213,17 @@ class Engine:
         tag, val, cur = np.zeros(count, np.uint8), np.zeros(count, np.uint64), np.zeros(count, np.uint8)
         _check(self.L.cc_read_value_state(self.h, first, count, _np(tag), _np(val), _np(cur)))
         return tag, val, cur
+
+    def map_entries(self, slot):
+        """MapState entries of one map slot sorted by (key tag, key): (key_tag, key, value_tag, value, commit_index)
+        — the same layout as the oracle's map_entries."""
+        n = C.c_uint64()
+        _check(self.L.cc_read_map_entries(self.h, slot, 0, C.byref(n), None, None, None, None, None))
+        m = n.value
+        kt, k, vt, v, ci = (np.zeros(m, np.uint8), np.zeros(m, np.uint64), np.zeros(m, np.uint8),
+                            np.zeros(m, np.uint64), np.zeros(m, np.uint64))
+        _check(self.L.cc_read_map_entries(self.h, slot, m, C.byref(n), _np(kt), _np(k), _np(vt), _np(v), _np(ci)))
+        return kt, k, vt, v, ci
 
 
 def quorum_commit(match, term_start, commit_in, commit_out, stream=None):

@@ -27,6 +27,10 @@ def lib():
         L.wl_atomic_long.argtypes = [u64, u32, u32, u64, u32, u32, u64] + [P] * 7
         L.wl_value_random.restype = u64
         L.wl_value_random.argtypes = [u64, u32, u32, u32, u64, u32, u32, u64] + [P] * 7
+        L.wl_map_random.restype = u64
+        L.wl_map_random.argtypes = [u64, u32, u32, u32, u32, u64, u32, u32, u64] + [P] * 9
+        L.wl_map_zipf.restype = u64
+        L.wl_map_zipf.argtypes = [u64, u64, u32, u32, C.c_double, u32, u64, u32] + [P] * 8
         _LIB = L
     return _LIB
 
@@ -54,6 +58,27 @@ def value_random_stream(n, resources, max_inst, first_inst=0, seed=1, hot=0, p_h
     return b
 
 
+def map_random_stream(n, maps, max_inst, keys=64, first_inst=0, seed=1, hot=0, p_hot=0.0, index0=1):
+    """Adversarial MapState stream for parity tests (every key op, all tags, null values, hot keys,
+    wrong-type ops, unknown sessions, ttl <= 0)."""
+    b = Batch(n)
+    lib().wl_map_random(n, maps, first_inst, max_inst, keys, seed, hot, int(p_hot * 1e6), index0, _p(b.index),
+                        _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.key), _p(b.a), _p(b.b), _p(b.aux))
+    return b
+
+
+SEED_C3 = 0xA700000 + 3
+
+
+def map_zipf_rows(row0, n, maps=4096, pairs=1 << 20, s=0.99, first_inst=0, seed=SEED_C3, threads=8, out=None):
+    """Config 3: rows [row0, row0+n) of the DistributedMap put/get/remove Zipf stream (see wl_map_zipf)."""
+    b = out if out is not None else Batch(n)
+    got = lib().wl_map_zipf(row0, n, maps, pairs, s, first_inst, seed, threads, _p(b.index), _p(b.time), _p(b.inst),
+                            _p(b.op), _p(b.flags), _p(b.key), _p(b.a), _p(b.b))
+    assert got == n
+    return b
+
+
 SEED_C4 = 0xA700000 + 4
 
 
@@ -78,4 +103,4 @@ def expiry_sessions(sessions, timeout=5000, now=10_000_000, seed=SEED_C4 + 1):
     return last, now, timeout
 
 
-__all__ = ["atomic_long_stream", "value_random_stream", "quorum_groups", "expiry_sessions", "abi"]
+__all__ = ["atomic_long_stream", "value_random_stream", "map_random_stream", "map_zipf_rows", "quorum_groups", "expiry_sessions", "abi"]

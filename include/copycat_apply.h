@@ -139,7 +139,8 @@ typedef struct cc_config {
   uint32_t max_instances;   /* instance-session slots (ResourceManager.sessions)               */
   uint64_t max_batch;       /* max commits per cc_apply_batch call                               */
   uint64_t max_events;      /* capacity of the device event stream per batch                      */
-  uint64_t map_capacity;    /* total map entries across all CC_RES_MAP resources (0 = none)       */
+  uint64_t map_capacity;    /* live map entries across all CC_RES_MAP resources (0 = no maps; at most
+                               1M: the table has 2^k regions of 2048 entries, >= 2 x map_capacity) */
   int32_t  device;          /* HIP device ordinal                                                  */
   uint32_t flags;           /* CC_CFG_* */
   uint64_t sub_batch;       /* commits per internal sub-batch (0 = default 16M; rounded up to a multiple
@@ -229,10 +230,14 @@ int  cc_applied_index(cc_engine* e, uint64_t* out);
 /* AtomicValueState {value, current != null} for slots [first, first+count) (AtomicValueState.java:34-35) */
 int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* h_tag, uint64_t* h_value,
                          uint8_t* h_has_current);
+/* MapState.map of one map slot (MapState.java:33): *count = live entries; the first min(cap, count), sorted
+ * by (key tag, key), go to the arrays (key tag as a CC_TAG_*; commit_index may be NULL).               */
+int  cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag, uint64_t* h_key,
+                         uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
- * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute.                                              */
-#define CC_PROFILE_KERNELS 3
+ * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute, 3 k_apply_map.                             */
+#define CC_PROFILE_KERNELS 4
 int  cc_profile_enable(cc_engine* e, int on);
 int  cc_profile_reset(cc_engine* e);
 /* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */

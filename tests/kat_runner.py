@@ -48,16 +48,27 @@ def op_code(name):
     return getattr(abi, f"CC_OP_{name}")
 
 
-def uses_only_value(kat):
-    if any(r[1] != "VALUE" for r in kat["resources"]):
+GPU_VALUE_OPS = {"VALUE_GET", "VALUE_SET", "VALUE_CAS", "VALUE_GETANDSET"}
+GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_GETORDEFAULT", "MAP_REMOVE",
+               "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT"}
+
+
+def gpu_eligible(kat):
+    """KATs whose every step this build applies on the GPU: AtomicValue get/set/CAS/getAndSet/Delete and Map key
+    ops without ttl, no registry control, clock or close steps."""
+    types = {r[1] for r in kat["resources"]}
+    if not types <= {"VALUE", "MAP"}:
         return False
     for s in kat["steps"]:
-        if "control" in s or "close" in s:
+        if "control" in s or "close" in s or "advance" in s:
             return False
-        if "commit" in s and not (s["commit"]["op"].startswith("VALUE_") or s["commit"]["op"] == "DELETE"):
-            if s["commit"]["op"] in ("VALUE_LISTEN", "VALUE_UNLISTEN"):
+        if "commit" in s:
+            c = s["commit"]
+            if c["op"] == "DELETE":
+                if types != {"VALUE"}:
+                    return False
+            elif c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS or c.get("aux", 0) > 0:
                 return False
-            return False
     return True
 
 
@@ -243,12 +254,12 @@ class OracleBackend:
 
 
 class EngineBackend:
-    """GPU engine backend (AtomicValue KATs: the GPU-applied subset of this build)."""
+    """GPU engine backend (the GPU-applied subset of this build: see gpu_eligible)."""
 
     def __init__(self, kat, max_resources=256, max_instances=64):
         from copycat_amd.engine import Engine
 
-        self.E = Engine(max_resources, max_instances, 4096)
+        self.E = Engine(max_resources, max_instances, 4096, map_capacity=4096)
 
     def resource_create(self, slot, t):
         self.E.resource_create(slot, t)
@@ -272,4 +283,4 @@ def all_kats():
     return load()["kats"]
 
 
-__all__ = ["KatRun", "OracleBackend", "EngineBackend", "all_kats", "uses_only_value", "np"]
+__all__ = ["KatRun", "OracleBackend", "EngineBackend", "all_kats", "gpu_eligible", "np"]

@@ -35,8 +35,6 @@ def test_constants_match_header():
     d = header_defines()
     assert len(d) > 60
     for name, v in d.items():
-        if name in ("CC_PROFILE_KERNELS",):
-            continue
         assert hasattr(abi, name), f"abi.py lacks {name}"
         assert getattr(abi, name) == v, name
 

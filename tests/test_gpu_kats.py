@@ -1,0 +1,20 @@
+"""The reference-pinned KATs (tests/golden/kats.json) on the GPU engine, for every KAT this build applies on
+the GPU (gpu_eligible): the same expectations the CPU oracle is pinned against in test_oracle_kats.py."""
+import pytest
+
+from tests.kat_runner import EngineBackend, KatRun, all_kats, gpu_eligible
+
+pytestmark = pytest.mark.gpu
+
+KATS = [k for k in all_kats() if gpu_eligible(k)]
+
+
+def test_gpu_kat_coverage():
+    names = {k["name"] for k in KATS}
+    assert {"map_put_get_remove", "map_put_if_absent", "A1_replace_if_present_inverts_args"} <= names
+    assert len(KATS) >= 8
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_kat_on_gpu(kat):
+    KatRun(kat, EngineBackend(kat)).run()

@@ -1,0 +1,198 @@
+"""GPU parity: MapState key operations on the MI355X vs the CPU oracle, through the C-ABI.
+
+Bar: bit-exact per-commit status/value, every map's final entries (key tag, key, value tag, value, commit
+index) and the applied index (integer path, no tolerance)."""
+import numpy as np
+import pytest
+
+from copycat_amd import abi
+from copycat_amd.batch import Batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engines(maps, max_inst, max_batch, map_capacity, sub_batch=0, first_slot=0):
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+
+    slots = first_slot + maps
+    E = Engine(slots, max_inst, max_batch, map_capacity=map_capacity, sub_batch=sub_batch)
+    O = Oracle(slots, max_inst)
+    E.resource_create_range(first_slot, maps, abi.CC_RES_MAP)
+    E.instance_open_range(first_slot, maps, first_slot, 1000, 7)
+    for m in range(first_slot, slots):
+        O.resource_create(m, abi.CC_RES_MAP)
+        O.instance_open(m, m, 1000 + m, 7)
+    return E, O
+
+
+def _apply_both(E, O, parts):
+    out = []
+    for part in parts:
+        s, v = E.apply_host(part)
+        s2, v2 = O.apply(part)
+        out.append((s, v, s2, v2))
+    return [np.concatenate([o[i] for o in out]) for i in range(4)]
+
+
+def _assert_rows(gs, gv, os_, ov):
+    bad = np.nonzero((gs != os_) | (gv != ov))[0]
+    assert len(bad) == 0, (f"{len(bad)} rows differ; first {bad[:5]}: gpu {gs[bad[:5]]},{gv[bad[:5]]} "
+                           f"oracle {os_[bad[:5]]},{ov[bad[:5]]}")
+
+
+def _assert_maps(E, O, slots):
+    for m in slots:
+        g, o = E.map_entries(m), O.map_entries(m)
+        for x, y, what in zip(g, o, ("key tag", "key", "value tag", "value", "commit index")):
+            assert np.array_equal(x, y), f"map {m}: {what} differs ({len(g[0])} vs {len(o[0])} entries)"
+    assert E.applied_index() == O.applied_index()
+
+
+@pytest.mark.parametrize("n,maps,keys,seed,hot,p_hot,cap", [
+    (1, 1, 4, 1, 0, 0.0, 1024),
+    (100, 3, 8, 2, 0, 0.0, 1024),
+    (10_000, 16, 64, 3, 0, 0.0, 8192),        # ~600 commits per map over ~150 keys: long same-key chains
+    (200_000, 64, 256, 4, 2, 0.3, 65536),     # 30% of rows on 2 keys of 2 maps
+    (500_001, 1000, 256, 5, 0, 0.0, 1 << 20),  # ragged sub-batch tail; 1024 regions
+    (300_000, 7, 4, 6, 1, 0.9, 1024),         # one key takes 90% of the rows
+])
+def test_map_random_parity(n, maps, keys, seed, hot, p_hot, cap):
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed, hot=hot, p_hot=p_hot)
+    E, O = _engines(maps, max_inst, n, cap)
+    _assert_rows(*_apply_both(E, O, [b]))
+    _assert_maps(E, O, range(maps))
+
+
+def test_map_multi_subbatch_and_batches():
+    """Table state carried across sub-batches inside one call and across calls."""
+    from copycat_amd.workload import map_random_stream
+
+    maps, max_inst, n = 40, 48, 150_000
+    b = map_random_stream(n, maps, max_inst, keys=128, seed=11, hot=4, p_hot=0.2)
+    E, O = _engines(maps, max_inst, n, 32768, sub_batch=16384 * 2)
+    parts = [b.slice(lo, hi) for lo, hi in [(0, 1), (1, 50_000), (50_000, 50_000), (50_000, n)]]
+    _assert_rows(*_apply_both(E, O, parts))
+    _assert_maps(E, O, range(maps))
+
+
+def test_maps_and_values_in_one_engine():
+    """AtomicValue and Map resources side by side: each commit goes to its own kernel, results interleave."""
+    from copycat_amd.engine import Engine
+    from copycat_amd.workload import map_random_stream, value_random_stream
+    from oracle.oracle_py import Oracle
+
+    V, M = 192, 64  # value slots [0, 192), map slots [192, 256)
+    slots, max_inst = V + M, V + M + 8
+    bv = value_random_stream(120_000, V, max_inst, seed=31, hot=4, p_hot=0.2)
+    bm = map_random_stream(100_000, M, max_inst, keys=64, first_inst=V, seed=32, hot=2, p_hot=0.2)
+    rng = np.random.default_rng(5)
+    order = rng.permutation(len(bv) + len(bm))
+    cols = {}
+    for name, _ in abi.BATCH_COLUMNS:
+        cols[name] = np.concatenate([getattr(bv, name), getattr(bm, name)])[order]
+    cols["index"] = np.arange(1, len(order) + 1, dtype=np.uint64)
+    b = Batch.from_columns(**cols)
+    E = Engine(slots, max_inst, len(b), map_capacity=65536)
+    O = Oracle(slots, max_inst)
+    E.resource_create_range(0, V, abi.CC_RES_VALUE)
+    E.resource_create_range(V, M, abi.CC_RES_MAP)
+    E.instance_open_range(0, slots, 0, 1000, 7)
+    for r in range(slots):
+        O.resource_create(r, abi.CC_RES_VALUE if r < V else abi.CC_RES_MAP)
+        O.instance_open(r, r, 1000 + r, 7)
+    _assert_rows(*_apply_both(E, O, [b]))
+    for x, y in zip(E.value_state(0, V), O.value_state(0, V)):
+        assert np.array_equal(x, y)
+    _assert_maps(E, O, range(V, slots))
+
+
+def _puts(keys, slot_inst, op=abi.CC_OP_MAP_PUT, index0=1):
+    n = len(keys)
+    return Batch.from_columns(index=np.arange(index0, index0 + n, dtype=np.uint64), inst=np.full(n, slot_inst),
+                              op=np.full(n, op, np.uint8),
+                              flags=np.full(n, abi.cc_flags(abi.CC_TAG_LONG, 0, 0), np.uint8),
+                              key=np.asarray(keys, np.uint64), a=np.asarray(keys, np.uint64) * np.uint64(3))
+
+
+def test_map_region_compaction():
+    """Removed keys keep their entries until a launch finds the region > 3/4 bound and compacts it: without
+    compaction the third batch would overflow the two 2048-entry regions."""
+    E, O = _engines(1, 4, 4000, 2048)
+    old = np.arange(3400, dtype=np.uint64) * np.uint64(7919) + np.uint64(11)
+    new = old + np.uint64(1 << 40)
+    b1 = _puts(old, 0)
+    b2 = _puts(old, 0, op=abi.CC_OP_MAP_REMOVE, index0=3401)
+    b3 = _puts(new, 0, index0=6801)
+    _assert_rows(*_apply_both(E, O, [b1, b2, b3]))
+    b4 = _puts(np.concatenate([old[:100], new[:100]]), 0, op=abi.CC_OP_MAP_GET, index0=10201)
+    _assert_rows(*_apply_both(E, O, [b4]))
+    _assert_maps(E, O, [0])
+
+
+def test_map_capacity_error():
+    from copycat_amd.engine import EngineError
+
+    E, _ = _engines(1, 4, 8192, 1024)  # 2 regions of 2048 entries
+    with pytest.raises(EngineError) as ei:
+        E.apply_host(_puts(np.arange(6000, dtype=np.uint64), 0))
+    assert ei.value.rc == abi.CC_ERR_CAPACITY
+
+
+@pytest.mark.parametrize("op,aux", [(abi.CC_OP_MAP_CONTAINSVALUE, 0), (abi.CC_OP_MAP_SIZE, 0),
+                                    (abi.CC_OP_MAP_ISEMPTY, 0), (abi.CC_OP_MAP_CLEAR, 0), (abi.CC_OP_DELETE, 0),
+                                    (abi.CC_OP_MAP_PUT, 5), (abi.CC_OP_MAP_REPLACE, 1)])
+def test_map_ops_not_on_gpu_fail_loudly(op, aux):
+    from copycat_amd.engine import EngineError
+
+    E, _ = _engines(2, 4, 16, 1024)
+    b = _puts([1, 2, 3], 1)
+    b.op[1] = op
+    b.aux[1] = aux
+    with pytest.raises(EngineError) as ei:
+        E.apply_host(b)
+    assert ei.value.rc == abi.CC_ERR_UNSUPPORTED
+
+
+def test_map_get_with_positive_aux_is_applied():
+    """ttl is read by put/putIfAbsent/replace/replaceIfPresent only: a get row whose aux column holds a
+    positive number is an ordinary get (MapCommands.java: Get carries no ttl)."""
+    E, O = _engines(1, 4, 16, 1024)
+    b = _puts([1, 2, 3], 0)
+    b.op[2] = abi.CC_OP_MAP_GET
+    b.key[2] = 1
+    b.aux[2] = 99
+    _assert_rows(*_apply_both(E, O, [b]))
+
+
+def test_map_resource_delete_drops_entries():
+    """ResourceManager.deleteResource -> MapState.delete (MapState.java:264-274): a map re-created in the
+    same slot starts empty; other maps keep their entries."""
+    E, O = _engines(2, 4, 64, 1024)
+    b = _puts(np.arange(20, dtype=np.uint64), 0)
+    b2 = _puts(np.arange(20, dtype=np.uint64), 1, index0=21)
+    _apply_both(E, O, [b, b2])
+    E.resource_delete(0)
+    E.resource_create(0, abi.CC_RES_MAP)
+    E.instance_open(0, 0, 5000, 7)
+    assert len(E.map_entries(0)[0]) == 0
+    g = _puts(np.arange(20, dtype=np.uint64), 0, op=abi.CC_OP_MAP_GET, index0=41)
+    s, v = E.apply_host(g)
+    assert (s == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_NULL)).all() and (v == 0).all()
+    g2 = _puts(np.arange(20, dtype=np.uint64), 1, op=abi.CC_OP_MAP_GET, index0=61)
+    s, v = E.apply_host(g2)
+    assert (s == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_LONG)).all() and (v == np.arange(20) * 3).all()
+
+
+def test_map_zipf_stream_parity():
+    """Config-3 stream (Zipf 0.99 put/get/remove over 1M (map, key) pairs, 4096 maps) at 2M rows."""
+    from copycat_amd.workload import map_zipf_rows
+
+    n, maps = 2_000_000, 4096
+    b = map_zipf_rows(0, n, maps=maps)
+    E, O = _engines(maps, maps, n, 1 << 20)
+    _assert_rows(*_apply_both(E, O, [b]))
+    _assert_maps(E, O, range(0, maps, 97))
