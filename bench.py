@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Bench: committed ops applied/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
-Workload (BASELINE.json configs[1]): a DistributedAtomicLong client-model stream —
+Default workload (BASELINE.json configs[1]): a DistributedAtomicLong client-model stream —
 Get(50) + CompareAndSet(52) of java.lang.Long values, ~10% stale CASes — of 100M committed entries over
 65,536 AtomicValueState resources per GPU.  A "step" = one cc_apply_batch over the whole 100M-entry batch
 with its columns already resident in HBM (state carries over from step to step, as a replica's would).
@@ -15,6 +15,10 @@ roofline: per-kernel device time from HIP events recorded on the launch stream o
 (cc_profile_*), dominant kernel, algorithmic bytes = 39 B/commit x commits per launch.
 cpu_baseline: the oracle (C++ restatement of the Java apply path, single thread) timed on this host
 over a bounded prefix of the same stream (rank 0, N=1 only).
+
+--workload c3 (BASELINE.json configs[2]): DistributedMap put/get/remove 45/45/10 over 1,048,576 (map, key)
+pairs in 4,096 MapState resources, pair rank ~ Zipf(0.99), 1e9 committed entries per step (generated block by
+block on the host, uploaded once); algorithmic bytes 34.6 B/commit.
 """
 import argparse
 import json
@@ -31,6 +35,7 @@ import torch  # noqa: E402
 
 METRIC = "committed ops applied/sec (1 and 8 GPUs) + % of HBM GB/s roofline"
 B_OP_C2 = 39  # index 8 + res 4 + op 1 + flags 1 + expect 8 + update 8 in, status 1 + value 8 out
+B_OP_C3 = 34.6  # put 30 in / get, remove 22 in; 9 out; weighted by the 45/45/10 mix
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -45,15 +50,44 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26):
+    """Config-3 stream generated block by block on the host and copied into HBM-resident columns.
+    Returns (host Batch of the first keep_host rows for the CPU baseline, DeviceBatch)."""
+    from copycat_amd.batch import Batch
+    from copycat_amd.engine import DeviceBatch
+    from copycat_amd.workload import SEED_C3, map_zipf_rows
+
+    names = ("index", "inst", "op", "flags", "key", "a", "b")
+    host = Batch(min(n, block))
+    dt = {"index": torch.int64, "inst": torch.int32, "op": torch.uint8, "flags": torch.uint8, "key": torch.int64,
+          "a": torch.int64, "b": torch.int64}
+    cols = {k: torch.empty(n, dtype=dt[k], device=dev) for k in names}
+    keep = None
+    threads = min(16, os.cpu_count() or 1)
+    for lo in range(0, n, block):
+        m = min(block, n - lo)
+        part = host if m == len(host) else Batch(m)
+        map_zipf_rows(lo, m, maps=maps, pairs=pairs, s=zipf, seed=SEED_C3 + rank, threads=threads, out=part)
+        if lo == 0:
+            keep = part.slice(0, min(keep_host, m))
+        for k in names:
+            src = torch.from_numpy(getattr(part, k).view(np.dtype(str(dt[k]).replace("torch.", ""))))
+            cols[k][lo:lo + m].copy_(src, non_blocking=False)
+    return keep, DeviceBatch(cols, n)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--commits", type=int, default=100_000_000)
-    ap.add_argument("--resources", type=int, default=65536)
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c2")
+    ap.add_argument("--commits", type=int, default=0, help="default: 100M (c2), 1e9 (c3)")
+    ap.add_argument("--resources", type=int, default=0, help="default: 65536 resources (c2), 4096 maps (c3)")
+    ap.add_argument("--pairs", type=int, default=1 << 20, help="c3: distinct (map, key) pairs")
+    ap.add_argument("--zipf", type=float, default=0.99, help="c3: Zipf exponent of the pair rank (0 = uniform)")
     ap.add_argument("--sub-batch", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=100_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=0, help="default: 100M (c2), 20M (c3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -75,16 +109,27 @@ def main():
     from copycat_amd.engine import DeviceBatch, Engine
     from copycat_amd.workload import SEED_C2, atomic_long_stream
 
-    n, R = args.commits, args.resources
+    c3 = args.workload == "c3"
+    n = args.commits or (1_000_000_000 if c3 else 100_000_000)
+    R = args.resources or (4096 if c3 else 65536)
+    cpu_sample = args.cpu_sample or (20_000_000 if c3 else 100_000_000)
+    B_OP = B_OP_C3 if c3 else B_OP_C2
     t_gen = time.time()
-    batch = atomic_long_stream(n, resources=R, seed=SEED_C2 + rank, index0=1)
+    if c3:
+        batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample))
+    else:
+        batch = atomic_long_stream(n, resources=R, seed=SEED_C2 + rank, index0=1)
+        db = DeviceBatch.upload(batch, device=dev, columns=("index", "inst", "op", "flags", "a", "b"))
     t_gen = time.time() - t_gen
-    db = DeviceBatch.upload(batch, device=dev, columns=("index", "inst", "op", "flags", "a", "b"))
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     value = torch.zeros(n, dtype=torch.int64, device=dev)
 
-    E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch)
-    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    if c3:
+        E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, map_capacity=args.pairs)
+        E.resource_create_range(0, R, abi.CC_RES_MAP)
+    else:
+        E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch)
+        E.resource_create_range(0, R, abi.CC_RES_VALUE)
     E.instance_open_range(0, R, 0, 1 + rank, 1 + rank)
     stream = torch.cuda.current_stream(dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
@@ -131,40 +176,46 @@ def main():
         ms_tot, launches = prof[dom]
         commits_per_launch = n * args.steps / max(launches, 1)
         avg_ms = ms_tot / max(launches, 1)
-        achieved = B_OP_C2 * commits_per_launch / (avg_ms * 1e-3) / 1e9
+        achieved = B_OP * commits_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
             "avg_launch_ms": round(avg_ms, 4), "launches": launches,
             "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
-            "pipeline_achieved_gbps": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9, 1),
-            "pipeline_frac": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "bytes_per_commit": B_OP,
+            "pipeline_achieved_gbps": round(B_OP * n / (ms_per_step * 1e-3) / 1e9, 1),
+            "pipeline_frac": round(B_OP * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         }
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle_py import Oracle
 
-        m = min(n, args.cpu_sample)
+        m = min(n, cpu_sample)
         sample = batch.slice(0, m)
         O = Oracle(R, R)
         for r in range(R):
-            O.resource_create(r, abi.CC_RES_VALUE)
+            O.resource_create(r, abi.CC_RES_MAP if c3 else abi.CC_RES_VALUE)
             O.instance_open(r, r, 1 + r, 1)
         tc = time.perf_counter()
         O.apply(sample)
         tc = time.perf_counter() - tc
         cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
-               "sample": f"first {m:,} commits of the same c2 stream, C++ restatement of the Java apply path "
-                         f"(oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+               "sample": f"first {m:,} commits of the same {args.workload} stream, C++ restatement of the Java apply "
+                         f"path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
 
+    if c3:
+        wl = (f"c3: DistributedMap put/get/remove 45/45/10, Zipf({args.zipf}) over {args.pairs:,} (map, key) pairs in "
+              f"{R:,} MapState resources, {n:,} committed entries per GPU")
+    else:
+        wl = ("c2: DistributedAtomicLong Get/CompareAndSet client-model stream, "
+              f"{n:,} committed entries over {R:,} AtomicValueState resources per GPU")
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value_ops, 1), "unit": "ops/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": "c2: DistributedAtomicLong Get/CompareAndSet client-model stream, "
-                                   f"{n:,} committed entries over {R:,} AtomicValueState resources per GPU",
+            "config": {"workload": wl,
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "ok_status_share": round(ok_share, 4),
                        "gen_s": round(t_gen, 2)},

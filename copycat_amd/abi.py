@@ -5,7 +5,7 @@ tests/test_abi.py checks every constant here against the #defines of the header,
 import ctypes as C
 
 CC_ABI_VERSION = 1
-CC_PROFILE_KERNELS = 4  # k_part_tile, k_apply_value, k_unpermute, k_apply_map
+CC_PROFILE_KERNELS = 5  # k_part_tile, k_apply_value, k_unpermute, k_apply_map, k_map_hot
 
 CC_OK = 0
 CC_ERR_INVALID = -1

@@ -17,8 +17,10 @@
 //      commit: nothing earlier in the log can have created it);
 //   3. a stable counting sort of the chunk by entry (LDS atomics with return, one wave at a time: lane order
 //      within a wave, wave order across waves = log order);
-//   4. each entry's commits are applied in log order by one thread (the reference's single state-machine
-//      thread, restricted to one key: different keys of a map are independent, MapState.java:32-289).
+//   4. each entry's commits are applied in log order (the reference's single state-machine thread, restricted
+//      to one key: different keys of a map are independent, MapState.java:32-289): a segmented scan of the
+//      commits' transformers (map_ops.h) gives every commit its pre-state at once; an entry whose run holds a
+//      value-comparing op (removeIfPresent/replaceIfPresent) is walked by one thread.
 //
 // Per-op semantics restate MapState (collections/src/main/java/io/atomix/collections/state/MapState.java):
 //   containsKey :38-44, get :65-72, getOrDefault :77-84, put :89-110, putIfAbsent :115-133, remove :138-154,
@@ -27,6 +29,7 @@
 // Delete (they read or reset a whole map), and put/putIfAbsent/replace/replaceIfPresent with ttl > 0 (timers).
 #include "common.h"
 #include "engine_internal.h"
+#include "map_ops.h"
 
 namespace cc {
 
@@ -36,102 +39,6 @@ constexpr int kMCh = kMT * kMPer;       // 1024 commits per chunk
 constexpr int kMEPer = kMapRegion / kMT;  // table entries per thread (8)
 constexpr uint32_t kNoEnt = 0xFFFFu;
 constexpr uint32_t kEntFull = 0xFFFEu;
-
-__device__ inline bool map_key_op(uint32_t op) { return op == 60 || (op >= 62 && op <= 69); }
-__device__ inline bool map_binds(uint32_t op) { return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT; }
-__device__ inline bool map_reads_ttl(uint32_t op) {
-  return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT;
-}
-
-// Applies one committed key op to an entry (w: word with PRESENT + value tag, v: value payload).
-// Returns the status byte; rv = result payload; `wrote` = the entry now holds this commit (commit index),
-// `created` = a new HashMap node was created (insert index).
-__device__ inline uint32_t map_apply(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t& w, uint64_t& v,
-                                     uint64_t& rv, bool& wrote, bool& created) {
-  const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
-  const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
-  const bool P = (w & kMwPresent) != 0;
-  const uint32_t T = P ? mw_vtag(w) : CC_TAG_NULL;
-  const uint64_t V = P ? v : 0;
-  auto store = [&](uint32_t tag, uint64_t x) {
-    w = (w & ~kMwVtagMask) | kMwPresent | (tag << 21);
-    v = x;
-  };
-  auto erase = [&]() {
-    w &= ~(kMwPresent | kMwVtagMask);
-    v = 0;
-  };
-  wrote = created = false;
-  rv = 0;
-  switch (op) {
-    case CC_OP_MAP_CONTAINSKEY:
-      rv = P;
-      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
-    case CC_OP_MAP_GET:  // a key mapped to null is present and returns null
-      rv = V;
-      return CC_STATUS(CC_ST_OK, T);
-    case CC_OP_MAP_GETORDEFAULT:
-      rv = P ? V : pa;
-      return CC_STATUS(CC_ST_OK, P ? T : ta);
-    case CC_OP_MAP_PUT:
-      rv = V;
-      store(ta, pa);
-      wrote = true;
-      created = !P;
-      return CC_STATUS(CC_ST_OK, T);
-    case CC_OP_MAP_PUTIFABSENT:
-      if (P) {
-        rv = V;
-        return CC_STATUS(CC_ST_OK, T);
-      }
-      store(ta, pa);
-      wrote = created = true;
-      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-    case CC_OP_MAP_REMOVE:
-      rv = V;
-      erase();
-      return CC_STATUS(CC_ST_OK, T);
-    case CC_OP_MAP_REMOVEIFPRESENT: {
-      // fail: absent, or stored null and value not null, or stored non-null and !stored.equals(value)
-      const bool fail = !P || (T == CC_TAG_NULL && ta != CC_TAG_NULL) || (T != CC_TAG_NULL && !(T == ta && V == pa));
-      if (!fail) erase();
-      rv = !fail;
-      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
-    }
-    case CC_OP_MAP_REPLACE:
-      if (!P) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-      rv = V;
-      store(ta, pa);
-      wrote = true;
-      return CC_STATUS(CC_ST_OK, T);
-    case CC_OP_MAP_REPLACEIFPRESENT: {
-      const bool ok = P && ((T == CC_TAG_NULL && tb == CC_TAG_NULL) || (T != CC_TAG_NULL && T == tb && V == pb));
-      if (ok) {
-        store(ta, pa);
-        wrote = true;
-      }
-      rv = ok;
-      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
-    }
-  }
-  return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
-}
-
-// Result of a commit that has no entry in the region: unknown op, an op not applied here, or a key op on a key
-// that is absent for the whole chunk.
-__device__ inline uint32_t map_orphan(uint32_t op, uint32_t meta, uint32_t flags, uint64_t a, uint64_t b, uint64_t& rv,
-                                      uint32_t& err) {
-  rv = 0;
-  if (!op_registered(CC_RES_MAP, op)) return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
-  if (!map_key_op(op) || (map_reads_ttl(op) && (meta & kMetaTtl))) {
-    err |= kErrUnsupported;
-    return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-  }
-  uint32_t w = kMwUsed;
-  uint64_t v = 0;
-  bool wrote, created;
-  return map_apply(op, flags, a, b, w, v, rv, wrote, created);
-}
 
 __device__ inline uint32_t map_ident_of(uint32_t res, uint32_t flags) { return mw_ident(res, CC_FLAG_KTAG(flags)); }
 
@@ -152,7 +59,11 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
   __shared__ uint32_t rmeta[kMCh];
   __shared__ uint32_t rpos[kMCh];      // staging position
   __shared__ uint64_t ridx[kMCh];      // commit index
+  __shared__ uint16_t rent[kMCh];      // entry
   __shared__ uint32_t ecnt[kMapRegion + 1];  // commits per entry in the chunk -> run starts
+  __shared__ uint32_t eflag[kMapRegion];     // the entry's run holds a value-comparing op
+  __shared__ Comp wcomp[kMT / kWave];
+  __shared__ uint32_t whead[kMT / kWave];
   __shared__ uint32_t rstart[kMaxTiles];
   __shared__ uint32_t rpre[kMaxTiles + 1];
   __shared__ uint32_t wsum[kMT / kWave];
@@ -167,6 +78,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
   if (t < 3) flag[t] = 0;
   if (t == 0) used_total = 0;
   for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
+  for (uint32_t q = t; q < kMapRegion; q += kMT) eflag[q] = 0;
   {
     uint64_t ek[kMEPer], ev[kMEPer], eci[kMEPer], eins[kMEPer];
     uint32_t ew[kMEPer], used = 0;
@@ -401,12 +313,103 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       rmeta[s] = m[j];
       rpos[s] = g[j];
       ridx[s] = idx[j];
+      rent[s] = (uint16_t)ent[j];
+      if (compares_value(m[j])) eflag[ent[j]] = 1;
     }
     lds_barrier();
-    // ---- 4. each entry's commits in log order, by the thread holding its first commit ----
+    // ---- 4. every run (one entry's commits, log order) at once: a segmented scan of the commits'
+    //         transformers gives each commit its entry's state before it (map_ops.h); runs holding a
+    //         value-comparing op are walked by one thread instead ----
+    {
+      const uint32_t total = ecnt[kMapRegion];
+      Comp el[kMPer];
+      bool hd[kMPer];
+      Comp c = comp_identity();
+      bool ch = false;
+#pragma unroll
+      for (int q = 0; q < kMPer; ++q) {
+        const uint32_t s = t * kMPer + q;
+        el[q] = comp_identity();
+        hd[q] = false;
+        if (s < total) {
+          const uint32_t e = rent[s];
+          hd[q] = s == ecnt[e];
+          el[q] = element(rmeta[s], s);
+        }
+        c = hd[q] ? el[q] : compose(c, el[q]);
+        ch |= hd[q];
+      }
+      // segmented inclusive scan of the thread aggregates across the wave, then across waves
+      Comp inc = c;
+      bool ih = ch;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const Comp o = comp_shfl_up(inc, d);
+        const bool oh = __shfl_up((int)ih, d, 64) != 0;
+        if (l >= (uint32_t)d) {
+          if (!ih) inc = compose(o, inc);
+          ih |= oh;
+        }
+      }
+      if (l == 63) {
+        wcomp[w] = inc;
+        whead[w] = ih;
+      }
+      lds_barrier();
+      Comp pre = comp_identity();  // exclusive prefix of this thread (within its run)
+      for (uint32_t q = 0; q < w; ++q) {
+        if (whead[q]) pre = wcomp[q];
+        else pre = compose(pre, wcomp[q]);
+      }
+      {
+        const Comp o = comp_shfl_up(inc, 1);
+        const bool oh = __shfl_up((int)ih, 1, 64) != 0;
+        if (l > 0) pre = oh ? o : compose(pre, o);
+      }
+      // walk this thread's commits from its prefix
+      uint32_t fe[kMPer], fw[kMPer];
+      uint64_t fv[kMPer], fci[kMPer], fins[kMPer];
+      bool fin[kMPer];
+      Comp cur = pre;
+#pragma unroll
+      for (int q = 0; q < kMPer; ++q) {
+        const uint32_t s = t * kMPer + q;
+        fin[q] = false;
+        if (s >= total) continue;
+        const uint32_t e = rent[s];
+        if (hd[q]) cur = comp_identity();
+        if (eflag[e]) continue;
+        const uint32_t mm = rmeta[s];
+        uint32_t sw;
+        uint64_t sv, sci, sins;
+        materialize_lds(cur, tword[e], tval[e], tci[e], tins[e], rmeta, rab, ridx, sw, sv, sci, sins);
+        uint64_t rv;
+        bool wrote, created;
+        const u64x2 x = rab[s];
+        const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, sw, sv, rv, wrote, created);
+        rst_status[rpos[s]] = (uint8_t)st;
+        rst_value[rpos[s]] = rv;
+        cur = compose(cur, el[q]);
+        if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
+          fin[q] = true;
+          fe[q] = e;
+          materialize_lds(cur, tword[e], tval[e], tci[e], tins[e], rmeta, rab, ridx, fw[q], fv[q], fci[q], fins[q]);
+        }
+      }
+      lds_barrier();  // every pre-state has been read
+#pragma unroll
+      for (int q = 0; q < kMPer; ++q) {
+        if (!fin[q]) continue;
+        tword[fe[q]] = fw[q];
+        tval[fe[q]] = fv[q];
+        tci[fe[q]] = fci[q];
+        tins[fe[q]] = fins[q];
+      }
+    }
+    // runs with a value-comparing op: sequentially, by the thread holding the run's first commit
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
-      if (ent[j] == kNoEnt || rk[j] != 0) continue;
+      if (ent[j] == kNoEnt || rk[j] != 0 || !eflag[ent[j]]) continue;
       const uint32_t e = ent[j];
       const uint32_t s0 = ecnt[e], s1 = ecnt[e + 1];
       uint32_t wv = tword[e];
@@ -430,6 +433,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
     }
     lds_barrier();
     for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
+    for (uint32_t q = t; q < kMapRegion; q += kMT) eflag[q] = 0;
     lds_barrier();
   }
 

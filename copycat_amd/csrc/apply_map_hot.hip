@@ -1,0 +1,474 @@
+// apply_map_hot.hip — hot map keys: a key that holds a large share of a batch (Zipf-skewed DistributedMap
+// traffic, SURVEY §7 hard part (b)) is applied by a scan over many workgroups instead of one region's chain.
+//
+// Per sub-batch:
+//   k_hot_detect : one workgroup samples 64K commits, counts (map, key tag, key) in LDS, and takes the (up to)
+//                  64 most frequent keys above ~0.1% of the sample; binds their table entries (apply_map.hip
+//                  layout) and publishes the hot set.  The partition routes every commit of a hot key to that
+//                  key's own bucket (log order, like any super-bucket).  Hot-ness only steers work: a commit is
+//                  applied identically by either path.
+//   k_hot_lists  : per hot key: its run in every tile -> list offsets; snapshot of the entry's state.
+//   k_hot_agg    : per piece of 4096 commits of a key's list: the piece's composite transformer (below).
+//   k_hot_apply  : per piece: carry = composite of all earlier pieces applied to the snapshot; the piece's
+//                  commits are then applied in log order from that state (results written to staging); the
+//                  last piece writes the entry back.
+//
+// Key ops as transformers of one entry's state (absent | present(value, node)):
+//   put(v)          absent -> present(v, new node)     present -> present(v, same node)
+//   putIfAbsent(v)  absent -> present(v, new node)     present -> unchanged
+//   remove          absent -> absent                   present -> absent
+//   replace(v)      absent -> absent                   present -> present(v, same node)
+//   containsKey, get, getOrDefault: identity
+// This family is closed under composition (each branch ends absent, unchanged, or present with a value and a
+// node taken from some commit), so a composite is two branch outcomes that reference staging records: the scan
+// is exact.  removeIfPresent/replaceIfPresent compare the stored value (MapState.java:159-178, 207-228) and are
+// outside the family: a hot key whose list holds one is applied sequentially (correct, slower).
+#include "common.h"
+#include "engine_internal.h"
+#include "map_ops.h"
+
+namespace cc {
+
+constexpr int kHT = 256;                   // threads per hot-scan workgroup
+constexpr int kHPer = kHotPiece / kHT;     // commits per thread per piece (16)
+constexpr int kDetT = 1024;
+constexpr int kDetSlots = 4096;
+constexpr uint32_t kDetSample = 65536;
+
+// ---------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ flags,
+                                                     const uint64_t* __restrict__ ckey, uint64_t lo, uint64_t hi,
+                                                     const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
+                                                     uint32_t max_inst, uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
+                                                     uint64_t* tbl_val, uint64_t* tbl_ci, uint64_t* tbl_ins,
+                                                     HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n) {
+  __shared__ uint64_t th64[kDetSlots];
+  __shared__ uint64_t tkey[kDetSlots];
+  __shared__ uint32_t tident[kDetSlots];
+  __shared__ uint32_t tcnt[kDetSlots];
+  __shared__ uint32_t cand[256];
+  __shared__ uint32_t sel[kHotMax];
+  __shared__ uint32_t ncand;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t q = t; q < kDetSlots; q += kDetT) {
+    th64[q] = 0;
+    tcnt[q] = 0;
+  }
+  if (t == 0) ncand = 0;
+  __syncthreads();
+  const uint64_t n = hi - lo;
+  const uint32_t S = (uint32_t)(n < kDetSample ? n : kDetSample);
+  const uint64_t stride = S ? n / S : 1;
+  for (uint32_t j = t; j < S; j += kDetT) {
+    const uint64_t i = lo + (uint64_t)j * stride;
+    const uint32_t s = inst[i];
+    const uint32_t r = s < max_inst ? inst_res[s] : kNoRes;
+    if (r == kNoRes || res_type[r] != CC_RES_MAP) continue;
+    const uint32_t kt = CC_FLAG_KTAG(flags[i]);
+    const uint64_t key = ckey[i];
+    const uint64_t h = map_hash(r, kt, key);
+    if (h == 0) continue;
+    uint32_t q = (uint32_t)h & (kDetSlots - 1);
+    for (int step = 0; step < 64; ++step, q = (q + 1) & (kDetSlots - 1)) {
+      const uint64_t old = atomicCAS((unsigned long long*)&th64[q], 0ull, (unsigned long long)h);
+      if (old == 0) {
+        tkey[q] = key;
+        tident[q] = mw_ident(r, kt);
+        atomicAdd(&tcnt[q], 1u);
+        break;
+      }
+      if (old == h) {
+        atomicAdd(&tcnt[q], 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t thresh = S / 1024 > 16 ? S / 1024 : 16;
+  for (uint32_t q = t; q < kDetSlots; q += kDetT) {
+    if (th64[q] != 0 && tcnt[q] >= thresh) {
+      const uint32_t k = atomicAdd(&ncand, 1u);
+      if (k < 256) cand[k] = q;
+    }
+  }
+  __syncthreads();
+  const uint32_t nc = ncand < 256 ? ncand : 256;
+  if (t < nc) {  // keep the kHotMax most frequent (ties: lower slot)
+    const uint32_t c = cand[t], cc = tcnt[c];
+    uint32_t rank = 0;
+    for (uint32_t u = 0; u < nc; ++u) {
+      const uint32_t o = cand[u], oc = tcnt[o];
+      rank += (oc > cc || (oc == cc && o < c)) ? 1 : 0;
+    }
+    if (rank < (uint32_t)kHotMax) sel[rank] = c;
+  }
+  __syncthreads();
+  if (t >= kWave) return;
+  // bind each hot key's table entry (the tables are idle between the sub-batch's kernels); one wave, new
+  // entries inserted one lane at a time so no two lanes race for a slot
+  const uint32_t nh = nc < (uint32_t)kHotMax ? nc : (uint32_t)kHotMax;
+  const uint32_t l = t;
+  bool valid = l < nh, found = false;
+  uint64_t h = 0, key = 0;
+  uint32_t ident = 0, pos = 0;
+  uint64_t base = 0;
+  if (valid) {
+    const uint32_t q = sel[l];
+    h = th64[q];
+    key = tkey[q];
+    ident = tident[q];
+    base = (h >> (64 - map_bits)) * kMapRegion;
+  }
+  auto probe = [&](bool insert) {
+    uint32_t p = (uint32_t)h & (kMapRegion - 1);
+    for (int step = 0; step < kMapRegion; ++step, p = (p + 1) & (kMapRegion - 1)) {
+      const uint32_t w = __hip_atomic_load(&tbl_word[base + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w == 0u) {
+        if (insert) {
+          __hip_atomic_store(&tbl_key[base + p], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&tbl_val[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&tbl_ci[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&tbl_ins[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&tbl_word[base + p], ident, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          found = true;
+          pos = (uint32_t)(base + p);
+        }
+        return;
+      }
+      if ((w & kMwIdentMask) == ident &&
+          __hip_atomic_load(&tbl_key[base + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key) {
+        found = true;
+        pos = (uint32_t)(base + p);
+        return;
+      }
+    }
+  };
+  if (valid) probe(false);
+  for (uint64_t need = ballot(valid && !found); need; need &= need - 1) {
+    const uint32_t leader = (uint32_t)__builtin_ctzll(need);
+    if (l == leader) probe(true);  // a full region leaves the key cold
+    __threadfence();
+  }
+  const bool ok = valid && found;
+  const uint64_t okm = ballot(ok);
+  if (ok) {
+    const uint32_t k = (uint32_t)__builtin_popcountll(okm & lanemask_lt());
+    hot[k] = HotKey{h, key, ident, pos};
+  }
+  if (l == 0) *hot_n = (uint32_t)__builtin_popcountll(okm);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+struct HotS0 {
+  uint64_t v, ci, ins;
+  uint32_t w;
+  uint32_t pad;
+};
+
+__global__ __launch_bounds__(kHT) void k_hot_lists(const uint16_t* __restrict__ ttab, uint32_t tiles, uint32_t sb,
+                                                  uint32_t sb_hot, const HotKey* __restrict__ hot,
+                                                  const uint32_t* __restrict__ hot_n, const uint64_t* __restrict__ tbl_val,
+                                                  const uint32_t* __restrict__ tbl_word, const uint64_t* __restrict__ tbl_ci,
+                                                  const uint64_t* __restrict__ tbl_ins, uint32_t* __restrict__ hot_rpre,
+                                                  uint32_t* __restrict__ hot_rstart, uint32_t* __restrict__ hot_len,
+                                                  uint32_t* __restrict__ hot_cond, HotS0* __restrict__ hot_s0) {
+  __shared__ uint32_t wsum[kHT / kWave];
+  const uint32_t h = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
+  if (h >= *hot_n) return;
+  const uint32_t k = sb_hot + h;
+  constexpr int PT = kMaxTiles / kHT;
+  uint32_t len[PT], st[PT], sum = 0;
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const uint32_t tt = t * PT + q;
+    len[q] = 0;
+    st[q] = 0;
+    if (tt < tiles) {
+      const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
+      const uint32_t b0 = row[k], b1 = row[k + 1];
+      st[q] = tt * kTile + b0;
+      len[q] = b1 - b0;
+    }
+    sum += len[q];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (l >= (uint32_t)d) inc += y;
+  }
+  if (l == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+  uint32_t* rpre = hot_rpre + (uint64_t)h * (kMaxTiles + 1);
+  uint32_t* rstart = hot_rstart + (uint64_t)h * kMaxTiles;
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const uint32_t tt = t * PT + q;
+    if (tt < tiles) {
+      rpre[tt] = run;
+      rstart[tt] = st[q];
+    }
+    run += len[q];
+  }
+  if (t == kHT - 1) {
+    rpre[tiles] = run;
+    hot_len[h] = run;
+  }
+  if (t == 0) {
+    hot_cond[h] = 0;
+    const uint32_t p = hot[h].pos;
+    hot_s0[h] = HotS0{tbl_val[p], tbl_ci[p], tbl_ins[p], tbl_word[p], 0};
+  }
+}
+
+// piece enumeration shared by k_hot_agg / k_hot_apply: item -> (hot key, piece)
+__device__ inline void hot_items(const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len, uint32_t* pfx,
+                                 uint32_t& nh) {
+  nh = *hot_n;
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (uint32_t h = 0; h < nh; ++h) {
+      pfx[h] = s;
+      s += (hot_len[h] + kHotPiece - 1) / kHotPiece;
+    }
+    pfx[nh] = s;
+  }
+  __syncthreads();
+}
+
+// staging positions of list positions [p0, p0 + cnt): walk the tile runs from the run holding p0
+struct ListCursor {
+  const uint32_t* rpre;
+  const uint32_t* rstart;
+  uint32_t tiles, tile, pos;
+  __device__ void seek(uint32_t p) {
+    uint32_t a = 0, b = tiles;  // last tile with rpre <= p
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (rpre[m] <= p) a = m; else b = m;
+    }
+    tile = a;
+    pos = p;
+  }
+  __device__ uint32_t next() {
+    while (pos >= rpre[tile + 1]) ++tile;
+    return rstart[tile] + (pos++ - rpre[tile]);
+  }
+};
+
+__global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ st_meta, const uint32_t* __restrict__ hot_n,
+                                                const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
+                                                const uint32_t* __restrict__ hot_rstart, uint32_t tiles,
+                                                Comp* __restrict__ agg, uint32_t* __restrict__ hot_cond) {
+  __shared__ uint32_t pfx[kHotMax + 1];
+  __shared__ Comp wtot[kHT / kWave];
+  uint32_t nh;
+  hot_items(hot_n, hot_len, pfx, nh);
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  for (uint32_t item = blockIdx.x; item < pfx[nh]; item += gridDim.x) {
+    uint32_t h = 0;
+    while (pfx[h + 1] <= item) ++h;
+    const uint32_t p = item - pfx[h], L = hot_len[h];
+    const uint32_t p0 = p * kHotPiece + t * kHPer;
+    ListCursor cur{hot_rpre + (uint64_t)h * (kMaxTiles + 1), hot_rstart + (uint64_t)h * kMaxTiles, tiles, 0, 0};
+    Comp c = comp_identity();
+    bool cond = false;
+    if (p0 < L) {
+      cur.seek(p0);
+      const uint32_t e = p0 + kHPer < L ? p0 + kHPer : L;
+      for (uint32_t q = p0; q < e; ++q) {
+        const uint32_t g = cur.next();
+        const uint32_t m = st_meta[g];
+        cond |= compares_value(m);
+        c = compose(c, element(m, g));
+      }
+    }
+    if (cond) atomicOr(&hot_cond[h], 1u);
+    c = wave_scan(c, l);
+    if (l == 63) wtot[w] = c;
+    __syncthreads();
+    if (t == 0) {
+      Comp a = wtot[0];
+      for (int q = 1; q < kHT / kWave; ++q) a = compose(a, wtot[q]);
+      agg[(uint64_t)h * kHotMaxPieces + p] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// materialize a branch outcome applied to the snapshot: map_apply state (word, value) + commit/insert index
+__device__ inline void materialize(const Comp& c, const HotS0& s0, const uint32_t* __restrict__ st_meta,
+                                   const u64x2* __restrict__ st_ab, const uint64_t* __restrict__ st_idx, uint32_t& w,
+                                   uint64_t& v, uint64_t& ci, uint64_t& ins) {
+  const bool present0 = (s0.w & kMwPresent) != 0;
+  const Br b = present0 ? c.P : c.A;
+  const uint32_t base = s0.w & ~(kMwPresent | kMwVtagMask);
+  if (b.kind == kBrKeep) {
+    w = s0.w;
+    v = s0.v;
+    ci = s0.ci;
+    ins = s0.ins;
+  } else if (b.kind == kBrAbsent) {
+    w = base;
+    v = 0;
+    ci = s0.ci;
+    ins = s0.ins;
+  } else {
+    const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(st_meta[b.v]));
+    w = base | kMwPresent | (tag << 21);
+    v = tag ? st_ab[b.v].x : 0;
+    ci = st_idx[b.v];
+    ins = b.n == kOrig ? s0.ins : st_idx[b.n];
+  }
+}
+
+// one commit of a hot key on state (w, v): result -> staging; tracks commit/insert index
+__device__ inline void hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t idx, uint32_t& w, uint64_t& v,
+                                uint64_t& ci, uint64_t& ins, uint8_t* __restrict__ rst_status,
+                                uint64_t* __restrict__ rst_value, uint32_t& err) {
+  const uint32_t op = smeta_op(m);
+  uint64_t rv;
+  uint32_t st;
+  if (!map_applied(m)) {
+    st = map_orphan(op, m, smeta_flags(m), x.x, x.y, rv, err);
+  } else {
+    bool wrote, created;
+    st = map_apply(op, smeta_flags(m), x.x, x.y, w, v, rv, wrote, created);
+    if (wrote) ci = idx;
+    if (created) ins = idx;
+  }
+  rst_status[g] = (uint8_t)st;
+  rst_value[g] = rv;
+}
+
+__global__ __launch_bounds__(kHT) void k_hot_apply(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
+                                                  const uint64_t* __restrict__ st_idx, const uint32_t* __restrict__ hot_n,
+                                                  const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_len,
+                                                  const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_rstart,
+                                                  uint32_t tiles, const Comp* __restrict__ agg,
+                                                  const uint32_t* __restrict__ hot_cond, const HotS0* __restrict__ hot_s0,
+                                                  uint64_t* __restrict__ tbl_val, uint32_t* __restrict__ tbl_word,
+                                                  uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
+                                                  uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
+                                                  uint32_t* __restrict__ err_out) {
+  __shared__ uint32_t pfx[kHotMax + 1];
+  __shared__ Comp wtot[kHT / kWave];
+  __shared__ Comp carry;
+  uint32_t nh;
+  hot_items(hot_n, hot_len, pfx, nh);
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  uint32_t err = 0;
+  for (uint32_t item = blockIdx.x; item < pfx[nh]; item += gridDim.x) {
+    uint32_t h = 0;
+    while (pfx[h + 1] <= item) ++h;
+    const uint32_t p = item - pfx[h], L = hot_len[h], P = pfx[h + 1] - pfx[h];
+    const HotS0 s0 = hot_s0[h];
+    const uint32_t pos = hot[h].pos;
+    ListCursor cur{hot_rpre + (uint64_t)h * (kMaxTiles + 1), hot_rstart + (uint64_t)h * kMaxTiles, tiles, 0, 0};
+    if (hot_cond[h]) {  // value-comparing ops on this key: its whole list, in order, on one thread
+      if (p == 0 && t == 0) {
+        uint32_t sw = s0.w;
+        uint64_t sv = s0.v, ci = s0.ci, ins = s0.ins;
+        cur.seek(0);
+        for (uint32_t q = 0; q < L; ++q) {
+          const uint32_t g = cur.next();
+          hot_step(g, st_meta[g], st_ab[g], st_idx[g], sw, sv, ci, ins, rst_status, rst_value, err);
+        }
+        tbl_word[pos] = sw;
+        tbl_val[pos] = sv;
+        tbl_ci[pos] = ci;
+        tbl_ins[pos] = ins;
+      }
+      continue;
+    }
+    // carry: the composite of pieces [0, p), folded in order by wave 0
+    if (w == 0) {
+      const uint32_t per = (p + 63) / 64;
+      Comp c = comp_identity();
+      for (uint32_t q = l * per; q < (l + 1) * per && q < p; ++q) c = compose(c, agg[(uint64_t)h * kHotMaxPieces + q]);
+      c = wave_scan(c, l);
+      if (l == 63) carry = c;
+    }
+    // this thread's commits and their composite
+    const uint32_t p0 = p * kHotPiece + t * kHPer;
+    const uint32_t e = p0 < L ? (p0 + kHPer < L ? p0 + kHPer : L) : p0;
+    uint32_t gs[kHPer], ms[kHPer];
+    Comp c = comp_identity();
+    if (p0 < L) cur.seek(p0);
+#pragma unroll
+    for (int q = 0; q < kHPer; ++q) {
+      gs[q] = 0;
+      ms[q] = 0;
+      if (p0 + q < e) {
+        gs[q] = cur.next();
+        ms[q] = st_meta[gs[q]];
+        c = compose(c, element(ms[q], gs[q]));
+      }
+    }
+    const Comp inc = wave_scan(c, l);
+    if (l == 63) wtot[w] = inc;
+    __syncthreads();
+    // exclusive prefix of this thread = carry . waves before . lanes before
+    Comp pre = carry;
+    for (uint32_t q = 0; q < w; ++q) pre = compose(pre, wtot[q]);
+    Comp lanes = comp_identity();
+    {
+      Comp o;
+      o.A.kind = __shfl_up(inc.A.kind, 1, 64);
+      o.A.v = __shfl_up(inc.A.v, 1, 64);
+      o.A.n = __shfl_up(inc.A.n, 1, 64);
+      o.P.kind = __shfl_up(inc.P.kind, 1, 64);
+      o.P.v = __shfl_up(inc.P.v, 1, 64);
+      o.P.n = __shfl_up(inc.P.n, 1, 64);
+      if (l > 0) lanes = o;
+    }
+    pre = compose(pre, lanes);
+    if (p0 < L) {
+      uint32_t sw;
+      uint64_t sv, ci, ins;
+      materialize(pre, s0, st_meta, st_ab, st_idx, sw, sv, ci, ins);
+#pragma unroll
+      for (int q = 0; q < kHPer; ++q)
+        if (p0 + q < e) hot_step(gs[q], ms[q], st_ab[gs[q]], st_idx[gs[q]], sw, sv, ci, ins, rst_status, rst_value, err);
+      if (p == P - 1 && e == L) {  // the key's last commit: write the entry back
+        tbl_word[pos] = sw;
+        tbl_val[pos] = sv;
+        tbl_ci[pos] = ci;
+        tbl_ins[pos] = ins;
+      }
+    }
+    __syncthreads();
+  }
+  if (err) atomicOr(err_out, err);
+}
+
+int launch_map_hot_detect(const HotArgs& a, hipStream_t st) {
+  if (a.hi <= a.lo) return 0;
+  hipLaunchKernelGGL(k_hot_detect, dim3(1), dim3(kDetT), 0, st, a.inst, a.flags, a.key, a.lo, a.hi, a.inst_res, a.res_type,
+                     a.max_inst, a.map_bits, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
+  if (a.tiles == 0) return 0;
+  const uint32_t sb_hot = a.sb_val + (1u << a.map_bits);
+  a.mark(K_MAP_HOT, 1, st);
+  hipLaunchKernelGGL(k_hot_lists, dim3(kHotMax), dim3(kHT), 0, st, a.ttab, a.tiles, a.sb, sb_hot, a.hot, a.hot_n, a.tbl_val,
+                     a.tbl_word, a.tbl_ci, a.tbl_ins, a.hot_rpre, a.hot_rstart, a.hot_len, a.hot_cond,
+                     reinterpret_cast<HotS0*>(a.hot_s0));
+  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.st_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
+                     a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond);
+  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.st_meta, a.st_ab, a.st_idx, a.hot_n, a.hot, a.hot_len,
+                     a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
+                     reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
+                     a.rst_value, a.err);
+  a.mark(K_MAP_HOT, 0, st);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t hot_agg_bytes() { return sizeof(Comp) * (size_t)kHotMax * kHotMaxPieces; }
+size_t hot_s0_bytes() { return sizeof(HotS0) * (size_t)kHotMax; }
+
+}  // namespace cc

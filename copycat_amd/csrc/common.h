@@ -29,7 +29,18 @@ constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 // device error bits (d_err)
 constexpr uint32_t kErrUnsupported = 1u;
 constexpr uint32_t kErrEvents = 2u;
-constexpr uint32_t kErrCapacity = 4u;     // a map table region is full
+constexpr uint32_t kErrCapacity = 4u;
+// hot map keys (apply_map_hot.hip): detected per sub-batch, applied by a multi-workgroup scan
+constexpr int kHotMax = 64;         // hot keys per sub-batch
+constexpr int kHotSlots = 256;      // LDS hash of the hot set in the partition kernel
+constexpr int kHotPiece = 4096;     // commits per scan piece (one workgroup)
+constexpr int kHotMaxPieces = (16 << 20) / kHotPiece;
+struct HotKey {
+  uint64_t h64;    // map_hash(slot, key tag, key)
+  uint64_t key;
+  uint32_t ident;  // mw_ident(slot, key tag)
+  uint32_t pos;    // table entry (region * 2048 + index)
+};     // a map table region is full
 
 // staging record meta word (u32): op(8) | flags(8) | slot-within-super-bucket(<=10 bits) << 16
 __host__ __device__ inline uint32_t smeta_op(uint32_t m) { return m & 0xFF; }

@@ -42,7 +42,7 @@ struct cc_engine {
   uint32_t sb = 0, sb_bits = 0;  // value super-buckets of 256 slots
   uint32_t map_bits = 0;         // 2^map_bits map table regions follow them (0: no maps)
   uint64_t map_entries = 0;
-  uint32_t sb_total() const { return sb + (map_bits ? 1u << map_bits : 0u); }
+  uint32_t sb_total() const { return sb + (map_bits ? (1u << map_bits) + kHotMax : 0u); }
   uint64_t sub_batch = 0, max_tiles = 0;
   // host mirrors of the registry
   std::vector<uint8_t> res_type;     // [sb*256]
@@ -72,6 +72,15 @@ struct cc_engine {
   uint32_t* d_st_res = nullptr;
   uint64_t* d_st_key = nullptr;
   uint64_t* d_st_idx = nullptr;
+  // hot map keys (apply_map_hot.hip)
+  HotKey* d_hot = nullptr;
+  uint32_t* d_hot_n = nullptr;
+  uint32_t* d_hot_rpre = nullptr;
+  uint32_t* d_hot_rstart = nullptr;
+  uint32_t* d_hot_len = nullptr;
+  uint32_t* d_hot_cond = nullptr;
+  void* d_hot_agg = nullptr;
+  void* d_hot_s0 = nullptr;
   uint64_t applied = 0;
   bool applied_pending = false;
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
@@ -130,7 +139,8 @@ static void free_all(cc_engine* e) {
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta,   e->d_val_v,     e->d_st_meta, e->d_st_ab,
                   e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
                   e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_st_res,
-                  e->d_st_key,   e->d_st_idx};
+                  e->d_st_key,   e->d_st_idx,   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
+                  e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -202,6 +212,14 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_st_res, sizeof(uint32_t) * e->sub_batch);
     ALLOC(e->d_st_key, sizeof(uint64_t) * e->sub_batch);
     ALLOC(e->d_st_idx, sizeof(uint64_t) * e->sub_batch);
+    ALLOC(e->d_hot, sizeof(HotKey) * kHotMax);
+    ALLOC(e->d_hot_n, sizeof(uint32_t));
+    ALLOC(e->d_hot_rpre, sizeof(uint32_t) * kHotMax * (kMaxTiles + 1));
+    ALLOC(e->d_hot_rstart, sizeof(uint32_t) * kHotMax * kMaxTiles);
+    ALLOC(e->d_hot_len, sizeof(uint32_t) * kHotMax);
+    ALLOC(e->d_hot_cond, sizeof(uint32_t) * kHotMax);
+    ALLOC(e->d_hot_agg, hot_agg_bytes());
+    ALLOC(e->d_hot_s0, hot_s0_bytes());
   }
   ALLOC(e->d_rst_status, e->sub_batch);
   ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
@@ -219,6 +237,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_tbl_word, 0, sizeof(uint32_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_ci, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_ins, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_hot_n, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
   }
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
   // the stable rankings of k_part_scatter / k_apply_value need same-address LDS atomics of one wave
@@ -396,6 +415,43 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
     const uint64_t hi = std::min(n, lo + e->sub_batch);
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
+    HotArgs ha{};
+    if (e->map_bits) {  // hot map keys of this sub-batch (routed to their own buckets by the partition)
+      ha.inst = c->inst;
+      ha.flags = c->flags;
+      ha.key = c->key;
+      ha.lo = lo;
+      ha.hi = hi;
+      ha.inst_res = e->d_inst_res;
+      ha.res_type = e->d_res_type;
+      ha.max_inst = e->cfg.max_instances;
+      ha.st_meta = e->d_st_meta;
+      ha.st_ab = e->d_st_ab;
+      ha.st_idx = e->d_st_idx;
+      ha.ttab = e->d_ttab;
+      ha.tiles = tiles;
+      ha.sb = e->sb_total();
+      ha.sb_val = e->sb;
+      ha.map_bits = e->map_bits;
+      ha.tbl_key = e->d_tbl_key;
+      ha.tbl_word = e->d_tbl_word;
+      ha.tbl_val = e->d_tbl_val;
+      ha.tbl_ci = e->d_tbl_ci;
+      ha.tbl_ins = e->d_tbl_ins;
+      ha.hot = e->d_hot;
+      ha.hot_n = e->d_hot_n;
+      ha.hot_rpre = e->d_hot_rpre;
+      ha.hot_rstart = e->d_hot_rstart;
+      ha.hot_len = e->d_hot_len;
+      ha.hot_cond = e->d_hot_cond;
+      ha.hot_agg = e->d_hot_agg;
+      ha.hot_s0 = e->d_hot_s0;
+      ha.rst_status = e->d_rst_status;
+      ha.rst_value = e->d_rst_value;
+      ha.err = e->d_err;
+      ha.mark = marker_of(e);
+      if (launch_map_hot_detect(ha, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError());
+    }
     PartArgs pa{};
     pa.inst = c->inst;
     pa.op = c->op;
@@ -413,6 +469,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.sb = e->sb_total();
     pa.sb_val = e->sb;
     pa.map_bits = e->map_bits;
+    pa.hot = e->d_hot;
+    pa.hot_n = e->d_hot_n;
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
     pa.st_res = e->d_st_res;
@@ -437,6 +495,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.mark = marker_of(e);
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
     if (e->map_bits) {
+      if (launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
       ma.st_meta = e->d_st_meta;
       ma.st_ab = e->d_st_ab;
@@ -596,7 +655,7 @@ extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, ui
   return CC_OK;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map"};
+static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map", "k_map_hot"};
 
 extern "C" int cc_profile_enable(cc_engine* e, int on) {
   if (!e) return CC_ERR_INVALID;

@@ -5,7 +5,7 @@
 namespace cc {
 
 // Optional per-kernel timing (HIP events recorded on the launch stream around each kernel).
-enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_APPLY_MAP, K_NUM };
+enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_APPLY_MAP, K_MAP_HOT, K_NUM };
 struct Marker {
   void (*fn)(void* ctx, int kernel, int begin, hipStream_t st);
   void* ctx;
@@ -32,6 +32,8 @@ struct PartArgs {
   uint32_t sb;        // super-buckets in total = sb_val + 2^map_bits (0 map bits: no maps)
   uint32_t sb_val;
   uint32_t map_bits;
+  const HotKey* hot;  // hot map keys of this sub-batch (maps only)
+  const uint32_t* hot_n;
   uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
   u64x2* st_ab;
   uint32_t* st_res;   // map records: resource slot, key, log index
@@ -84,6 +86,45 @@ struct MapArgs {
 };
 int launch_apply_map(const MapArgs& a, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
+
+constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
+struct HotArgs {
+  // detection (before the partition)
+  const uint32_t* inst;
+  const uint8_t* flags;
+  const uint64_t* key;
+  uint64_t lo, hi;
+  const uint32_t* inst_res;
+  const uint8_t* res_type;
+  uint32_t max_inst;
+  // scan (after the partition)
+  const uint32_t* st_meta;
+  const u64x2* st_ab;
+  const uint64_t* st_idx;
+  const uint16_t* ttab;
+  uint32_t tiles, sb, sb_val, map_bits;
+  uint64_t* tbl_key;
+  uint32_t* tbl_word;
+  uint64_t* tbl_val;
+  uint64_t* tbl_ci;
+  uint64_t* tbl_ins;
+  HotKey* hot;
+  uint32_t* hot_n;
+  uint32_t* hot_rpre;    // [kHotMax][kMaxTiles + 1]
+  uint32_t* hot_rstart;  // [kHotMax][kMaxTiles]
+  uint32_t* hot_len;     // [kHotMax]
+  uint32_t* hot_cond;    // [kHotMax]
+  void* hot_agg;         // [kHotMax][kHotMaxPieces] composites
+  void* hot_s0;          // [kHotMax] entry snapshots
+  uint8_t* rst_status;
+  uint64_t* rst_value;
+  uint32_t* err;
+  Marker mark;
+};
+int launch_map_hot_detect(const HotArgs& a, hipStream_t st);
+int launch_map_hot_apply(const HotArgs& a, hipStream_t st);
+size_t hot_agg_bytes();
+size_t hot_s0_bytes();
 
 struct UnpermuteArgs {
   const uint16_t* cpos;

@@ -54,28 +54,23 @@ __device__ inline uint32_t block_exscan(uint32_t v, uint32_t* wsum /*[16] LDS*/,
   return wpre + inc - v;
 }
 
-// Per-wave counters are packed u16 pairs (a wave ranks at most 256 commits of a chunk): wc[w][k/2].
+// Per-wave counters are packed u16 pairs (a wave ranks at most 256 commits of a chunk): wc[w][k/2]; the
+// per-super-bucket tile offsets, run fills, chunk totals and chunk starts are u16 (a tile holds 16384 commits).
 size_t tile_lds_bytes(uint32_t sb, bool maps) {
   const size_t chunk = maps ? kChunkMaps : kChunk;
   const size_t rec = 16 + 4 + 2 + (maps ? 4 + 8 + 8 : 0);
-  return chunk * rec + (size_t)kPW * ((sb + 1) / 2) * 4 + (size_t)4 * sb * 4 + 16 * 4;
-}
-
-// Super-bucket of a commit: value resources by slot (slot >> 8); map commits by hash(map, key) into the map
-// regions that follow the value super-buckets.
-template <bool MAPS>
-__device__ inline uint32_t route(uint32_t r, uint32_t f, uint64_t key, const uint8_t* __restrict__ res_type, uint32_t sb_val,
-                                 uint32_t map_bits, bool& is_map) {
-  is_map = false;
-  if (MAPS && res_type[r] == CC_RES_MAP) {
-    is_map = true;
-    return sb_val + (uint32_t)(map_hash(r, CC_FLAG_KTAG(f), key) >> (64 - map_bits));
-  }
-  return r >> kSbShift;
+  const size_t hw = (sb + 1) / 2;
+  const size_t hot = maps ? kHotSlots * 4 + kHotMax * (8 + 8 + 4) : 0;
+  return chunk * rec + (size_t)kPW * hw * 4 + 4 * (2 * hw) * 2 + 16 * 4 + hot;
 }
 
 // LDS layout (dynamic): rab[C] u64x2 | [MAPS: rkey[C] u64 | ridx[C] u64 | rres[C] u32] | rmeta[C] u32 |
-//                       rsb[C] u16 | wc[kPW][(sb+1)/2] u32 | toff, trun, ctot, kstart [sb] u32 | wsum[16] u32
+//   rsb[C] u16 | wc[kPW][hw] u32 | toff, trun, ctot, kstart [2hw] u16 | wsum[16] u32 |
+//   [MAPS: hot keys: hslot[kHotSlots] u32 | hh64[kHotMax] u64 | hkey[kHotMax] u64 | hident[kHotMax] u32]
+//
+// Super-bucket of a commit: value resources by slot (slot >> 8); map commits by hash(map, key tag, key) into
+// the map regions that follow the value super-buckets; commits of a hot key (apply_map_hot.hip) into that
+// key's own bucket after the regions.
 template <int J, bool MAPS>
 __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
@@ -84,6 +79,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
                                                 uint64_t lo, uint64_t hi,
                                                 const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
                                                 uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits,
+                                                const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n,
                                                 uint32_t* __restrict__ st_meta, u64x2* __restrict__ st_ab,
                                                 uint32_t* __restrict__ st_res, uint64_t* __restrict__ st_key,
                                                 uint64_t* __restrict__ st_idx, uint16_t* __restrict__ cpos,
@@ -98,11 +94,51 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + C);
   uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + C);  // [kPW][hw] packed u16 pairs
   const uint32_t hw = (sb + 1) / 2;
-  uint32_t* toff = wc + kPW * hw;
-  uint32_t* trun = toff + sb;
-  uint32_t* ctot = trun + sb;
-  uint32_t* kstart = ctot + sb;
-  uint32_t* wsum = kstart + sb;
+  uint16_t* toff = reinterpret_cast<uint16_t*>(wc + kPW * hw);
+  uint16_t* trun = toff + 2 * hw;
+  uint16_t* ctot = trun + 2 * hw;
+  uint16_t* kstart = ctot + 2 * hw;
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(kstart + 2 * hw);
+  uint32_t* ctot32 = reinterpret_cast<uint32_t*>(ctot);  // packed view for LDS atomics
+  uint32_t* hslot = wsum + 16;
+  uint64_t* hh64 = reinterpret_cast<uint64_t*>(hslot + (MAPS ? kHotSlots : 0));
+  uint64_t* hkey = hh64 + kHotMax;
+  uint32_t* hident = reinterpret_cast<uint32_t*>(hkey + kHotMax);
+
+  uint32_t nhot = 0;
+  if (MAPS) {
+    nhot = *hot_n;
+    for (uint32_t q = threadIdx.x; q < kHotSlots; q += kPT) hslot[q] = 0xFFFFFFFFu;
+    if (threadIdx.x < nhot) {
+      const HotKey hk = hot[threadIdx.x];
+      hh64[threadIdx.x] = hk.h64;
+      hkey[threadIdx.x] = hk.key;
+      hident[threadIdx.x] = hk.ident;
+    }
+    lds_barrier();
+    if (threadIdx.x < nhot) {
+      uint32_t q = (uint32_t)(hh64[threadIdx.x] >> 32) & (kHotSlots - 1);
+      while (atomicCAS(&hslot[q], 0xFFFFFFFFu, threadIdx.x) != 0xFFFFFFFFu) q = (q + 1) & (kHotSlots - 1);
+    }
+  }
+  const uint32_t sb_hot = sb_val + (MAPS ? (1u << map_bits) : 0u);
+  auto route = [&](uint32_t r, uint32_t f, uint64_t key) -> uint32_t {
+    if (MAPS && res_type[r] == CC_RES_MAP) {
+      const uint32_t kt = CC_FLAG_KTAG(f);
+      const uint64_t h = map_hash(r, kt, key);
+      if (nhot) {
+        const uint32_t id = mw_ident(r, kt);
+        for (uint32_t q = (uint32_t)(h >> 32) & (kHotSlots - 1);; q = (q + 1) & (kHotSlots - 1)) {
+          const uint32_t x = hslot[q];
+          if (x == 0xFFFFFFFFu) break;
+          if (hh64[x] == h && hident[x] == id && hkey[x] == key) return sb_hot + x;
+        }
+      }
+      return sb_val + (uint32_t)(h >> (64 - map_bits));
+    }
+    return r >> kSbShift;
+  };
+  auto hist_add = [&](uint32_t k) { atomicAdd(&ctot32[k >> 1], 1u << (16 * (k & 1))); };
 
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
@@ -110,7 +146,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   const uint32_t tbase = blockIdx.x * kTile;  // staging region of this tile (relative to lo)
 
   // 0. histogram of the whole tile -> tile-local run starts (ttab row)
-  for (uint32_t k = t; k < sb; k += kPT) ctot[k] = 0;
+  for (uint32_t k = t; k < hw; k += kPT) ctot32[k] = 0;
   lds_barrier();
   if (!MAPS) {
     const uint64_t q1 = tile1 / 4;
@@ -119,24 +155,22 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       const uint4 v = reinterpret_cast<const uint4*>(inst)[q];
       const uint32_t r0 = resolve(inst_res, max_inst, v.x), r1 = resolve(inst_res, max_inst, v.y);
       const uint32_t r2 = resolve(inst_res, max_inst, v.z), r3 = resolve(inst_res, max_inst, v.w);
-      if (r0 != kNoRes) atomicAdd(&ctot[r0 >> kSbShift], 1u);
-      if (r1 != kNoRes) atomicAdd(&ctot[r1 >> kSbShift], 1u);
-      if (r2 != kNoRes) atomicAdd(&ctot[r2 >> kSbShift], 1u);
-      if (r3 != kNoRes) atomicAdd(&ctot[r3 >> kSbShift], 1u);
+      if (r0 != kNoRes) hist_add(r0 >> kSbShift);
+      if (r1 != kNoRes) hist_add(r1 >> kSbShift);
+      if (r2 != kNoRes) hist_add(r2 >> kSbShift);
+      if (r3 != kNoRes) hist_add(r3 >> kSbShift);
     }
     for (uint64_t i = q1 * 4 + t; i < tile1; i += kPT) {  // ragged tail (< 4 commits)
       const uint32_t r = resolve(inst_res, max_inst, inst[i]);
-      if (r != kNoRes) atomicAdd(&ctot[r >> kSbShift], 1u);
+      if (r != kNoRes) hist_add(r >> kSbShift);
     }
   } else {
 #pragma unroll 4
     for (uint64_t i = tile0 + t; i < tile1; i += kPT) {
       const uint32_t r = resolve(inst_res, max_inst, inst[i]);
       if (r == kNoRes) continue;
-      bool is_map;
-      const uint32_t f = res_type[r] == CC_RES_MAP ? flags[i] : 0;
-      const uint64_t key = res_type[r] == CC_RES_MAP ? ckey[i] : 0;
-      atomicAdd(&ctot[route<MAPS>(r, f, key, res_type, sb_val, map_bits, is_map)], 1u);
+      const bool m = res_type[r] == CC_RES_MAP;
+      hist_add(route(r, m ? flags[i] : 0u, m ? ckey[i] : 0ull));
     }
   }
   lds_barrier();
@@ -207,12 +241,11 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
     // 1. rank by super-bucket inside each wave: the wave's own counter table, LDS atomics with return
     //    (same-address lanes of one instruction resolve in lane order on gfx950 — checked at engine start)
     uint32_t sk[J], loc[J];
-    bool live[J], ismap[J];
+    bool live[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       live[j] = res[j] != kNoRes;
-      sk[j] = live[j] ? route<MAPS>(res[j], meta[j] >> 8, key[j], res_type, sb_val, map_bits, ismap[j]) : 0;
-      if (!live[j]) ismap[j] = false;
+      sk[j] = live[j] ? route(res[j], (meta[j] >> 8) & 0xFF, key[j]) : 0;
       const uint32_t sh = 16 * (sk[j] & 1);
       loc[j] = live[j] ? (atomicAdd(&wc[w * hw + (sk[j] >> 1)], 1u << sh) >> sh) & 0xFFFF : 0;
     }
@@ -228,8 +261,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
         r0 += c & 0xFFFF;
         r1 += c >> 16;
       }
-      ctot[2 * kw] = r0;
-      if (2 * kw + 1 < sb) ctot[2 * kw + 1] = r1;
+      ctot32[kw] = r0 | (r1 << 16);
     }
     lds_barrier();
     uint32_t nlive = 0;
@@ -340,11 +372,11 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   if (maps)
     hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   else
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

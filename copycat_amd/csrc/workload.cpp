@@ -126,9 +126,11 @@ uint64_t wl_value_random(uint64_t n, uint32_t resources, uint32_t first_inst, ui
 // MapState parity stream (adversarial): every key op, all key and value tags, null values, hot keys, ops of
 // other resource types on a map (UNKNOWN_OP) and unknown instance slots.  Map m is instance slot first_inst + m.
 // aux (ttl) is 0 or negative (no timer); small value domains make the conditional ops hit.
+// value_compare_ops = 0 replaces removeIfPresent/replaceIfPresent by remove/replace.
 uint64_t wl_map_random(uint64_t n, uint32_t maps, uint32_t first_inst, uint32_t max_inst, uint32_t keys, uint64_t seed,
                        uint32_t hot, uint32_t p_hot_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
-                       uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b, uint64_t* aux) {
+                       uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b, uint64_t* aux,
+                       uint32_t value_compare_ops) {
   SplitMix64 rng(seed);
   static const uint8_t ops[] = {CC_OP_MAP_PUT, CC_OP_MAP_PUT, CC_OP_MAP_PUT, CC_OP_MAP_PUT, CC_OP_MAP_PUT,
                                 CC_OP_MAP_PUTIFABSENT, CC_OP_MAP_PUTIFABSENT, CC_OP_MAP_GET, CC_OP_MAP_GET, CC_OP_MAP_GET,
@@ -156,6 +158,8 @@ uint64_t wl_map_random(uint64_t n, uint32_t maps, uint32_t first_inst, uint32_t 
       if (kt == 0 && rng.below(4) == 0) kp = ~kp;  // negative longs (spread over the hash)
     }
     uint8_t o = ops[rng.below(sizeof ops)];
+    if (!value_compare_ops && (o == CC_OP_MAP_REMOVEIFPRESENT || o == CC_OP_MAP_REPLACEIFPRESENT))
+      o = o == CC_OP_MAP_REMOVEIFPRESENT ? CC_OP_MAP_REMOVE : CC_OP_MAP_REPLACE;
     uint32_t s = first_inst + m;
     const uint64_t k = rng.below(1000);
     if (k < 3) s = max_inst + (uint32_t)rng.below(1000);  // unknown instance slot

@@ -28,7 +28,7 @@ def lib():
         L.wl_value_random.restype = u64
         L.wl_value_random.argtypes = [u64, u32, u32, u32, u64, u32, u32, u64] + [P] * 7
         L.wl_map_random.restype = u64
-        L.wl_map_random.argtypes = [u64, u32, u32, u32, u32, u64, u32, u32, u64] + [P] * 9
+        L.wl_map_random.argtypes = [u64, u32, u32, u32, u32, u64, u32, u32, u64] + [P] * 9 + [u32]
         L.wl_map_zipf.restype = u64
         L.wl_map_zipf.argtypes = [u64, u64, u32, u32, C.c_double, u32, u64, u32] + [P] * 8
         _LIB = L
@@ -58,12 +58,15 @@ def value_random_stream(n, resources, max_inst, first_inst=0, seed=1, hot=0, p_h
     return b
 
 
-def map_random_stream(n, maps, max_inst, keys=64, first_inst=0, seed=1, hot=0, p_hot=0.0, index0=1):
+def map_random_stream(n, maps, max_inst, keys=64, first_inst=0, seed=1, hot=0, p_hot=0.0, index0=1,
+                      value_compare_ops=True):
     """Adversarial MapState stream for parity tests (every key op, all tags, null values, hot keys,
-    wrong-type ops, unknown sessions, ttl <= 0)."""
+    wrong-type ops, unknown sessions, ttl <= 0).  value_compare_ops=False swaps removeIfPresent /
+    replaceIfPresent for remove / replace (the hot-key scan family)."""
     b = Batch(n)
     lib().wl_map_random(n, maps, first_inst, max_inst, keys, seed, hot, int(p_hot * 1e6), index0, _p(b.index),
-                        _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.key), _p(b.a), _p(b.b), _p(b.aux))
+                        _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.key), _p(b.a), _p(b.b), _p(b.aux),
+                        1 if value_compare_ops else 0)
     return b
 
 

@@ -236,8 +236,9 @@ int  cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* co
                          uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
- * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute, 3 k_apply_map.                             */
-#define CC_PROFILE_KERNELS 4
+ * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute, 3 k_apply_map, 4 k_map_hot (hot-key lists +
+ * scan, apply_map_hot.hip).                                                                                 */
+#define CC_PROFILE_KERNELS 5
 int  cc_profile_enable(cc_engine* e, int on);
 int  cc_profile_reset(cc_engine* e);
 /* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */

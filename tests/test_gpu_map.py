@@ -67,6 +67,23 @@ def test_map_random_parity(n, maps, keys, seed, hot, p_hot, cap):
     _assert_maps(E, O, range(maps))
 
 
+@pytest.mark.parametrize("n,sub_batch,hot,p_hot,seed", [
+    (400_000, 65536, 8, 0.6, 41),    # 7 sub-batches; each hot key ~5K commits per sub-batch: 2 scan pieces
+    (2_000_000, 0, 8, 0.6, 42),      # one sub-batch: ~37 pieces per hot key (carry across many pieces)
+    (300_000, 0, 1, 0.97, 43),       # one key takes 97%: ~71 pieces
+])
+def test_map_hot_key_scan_parity(n, sub_batch, hot, p_hot, seed):
+    """Hot keys (detected per sub-batch) applied by the multi-workgroup scan: every key op except the
+    value-comparing ones, which force the sequential path (covered by test_map_random_parity)."""
+    from copycat_amd.workload import map_random_stream
+
+    maps, max_inst = 16, 24
+    b = map_random_stream(n, maps, max_inst, keys=64, seed=seed, hot=hot, p_hot=p_hot, value_compare_ops=False)
+    E, O = _engines(maps, max_inst, n, 8192, sub_batch=sub_batch)
+    _assert_rows(*_apply_both(E, O, [b]))
+    _assert_maps(E, O, range(maps))
+
+
 def test_map_multi_subbatch_and_batches():
     """Table state carried across sub-batches inside one call and across calls."""
     from copycat_amd.workload import map_random_stream
