@@ -19,6 +19,10 @@ over a bounded prefix of the same stream (rank 0, N=1 only).
 --workload c3 (BASELINE.json configs[2]): DistributedMap put/get/remove 45/45/10 over 1,048,576 (map, key)
 pairs in 4,096 MapState resources, pair rank ~ Zipf(0.99), 1e9 committed entries per step (generated block by
 block on the host, uploaded once); algorithmic bytes 34.6 B/commit.
+
+--workload c4 (BASELINE.json configs[3]): leader quorum commit index for 1,048,576 5-replica Raft groups plus
+the session expiry sweep over 1,048,576 sessions; a step = one aggregation + one sweep; value = (groups +
+sessions) / s; algorithmic bytes 64 B/group and 8.125 B/session.
 """
 import argparse
 import json
@@ -76,12 +80,102 @@ def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26):
     return keep, DeviceBatch(cols, n)
 
 
+def run_c4(args, dev, rank, world, dist):
+    """Config 4: quorum commit-index aggregation + session expiry sweep, inputs resident in HBM."""
+    from copycat_amd.engine import expire_sweep, quorum_commit
+    from copycat_amd.workload import expiry_sessions, quorum_groups
+
+    G = args.commits or (1 << 20)
+    S = G
+    match, ts, ci = quorum_groups(G, replicas=5, seed=0xA700000 + 4 + rank)
+    last, now, timeout = expiry_sessions(S, seed=0xA700000 + 5 + rank)
+
+    def dev_u64(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+
+    d_match, d_ts, d_ci, d_last = dev_u64(match), dev_u64(ts), dev_u64(ci), dev_u64(last)
+    d_out = torch.zeros(G, dtype=torch.int64, device=dev)
+    d_bm = torch.zeros((S + 63) // 64, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(k=None):
+        if k is not None:
+            ev[k][0].record(stream)
+        quorum_commit(d_match, d_ts, d_ci, d_out, stream=stream)
+        if k is not None:
+            ev[k][1].record(stream)
+        d_cnt.zero_()
+        expire_sweep(d_last, now, timeout, d_bm, d_cnt, stream=stream)
+        if k is not None:
+            ev[k][2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    q_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    x_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    q_gbps = 64 * G / (q_ms * 1e-3) / 1e9
+    x_gbps = 8.125 * S / (x_ms * 1e-3) / 1e9
+    dom = "k_quorum" if q_ms >= x_ms else "k_expire"
+    ach = q_gbps if dom == "k_quorum" else x_gbps
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.oracle_py import expire_sweep as ox
+        from oracle.oracle_py import quorum_commit as oq
+
+        tc = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - tc < 10 or reps == 0:
+            oq(match, ts, ci)
+            ox(last, now, timeout)
+            reps += 1
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(reps * (G + S) / tc, 1), "unit": "groups+sessions/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} x (quorum over {G:,} groups + sweep over {S:,} sessions), oracle/oracle.cpp, "
+                         f"1 thread, {cpu_model()}"}
+    if rank == 0:
+        ms = elapsed * 1e3 / args.steps
+        out = {
+            "metric": METRIC, "value": round((G + S) * args.steps * world / elapsed, 1), "unit": "groups+sessions/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"c4: quorum commit index for {G:,} 5-replica Raft groups + expiry sweep over "
+                                   f"{S:,} sessions per GPU", "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "per_kernel_ms": {"k_quorum": round(q_ms, 5), "k_expire": round(x_ms, 5)},
+                         "per_kernel_gbps": {"k_quorum": round(q_gbps, 1), "k_expire": round(x_gbps, 1)},
+                         "bytes_per_unit": {"group": 64, "session": 8.125}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("c2", "c3"), default="c2")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4"), default="c2")
     ap.add_argument("--commits", type=int, default=0, help="default: 100M (c2), 1e9 (c3)")
     ap.add_argument("--resources", type=int, default=0, help="default: 65536 resources (c2), 4096 maps (c3)")
     ap.add_argument("--pairs", type=int, default=1 << 20, help="c3: distinct (map, key) pairs")
@@ -108,6 +202,9 @@ def main():
     from copycat_amd import abi
     from copycat_amd.engine import DeviceBatch, Engine
     from copycat_amd.workload import SEED_C2, atomic_long_stream
+
+    if args.workload == "c4":
+        return run_c4(args, dev, rank, world, dist)
 
     c3 = args.workload == "c3"
     n = args.commits or (1_000_000_000 if c3 else 100_000_000)

@@ -5,7 +5,7 @@ tests/test_abi.py checks every constant here against the #defines of the header,
 import ctypes as C
 
 CC_ABI_VERSION = 1
-CC_PROFILE_KERNELS = 5  # k_part_tile, k_apply_value, k_unpermute, k_apply_map, k_map_hot
+CC_PROFILE_KERNELS = 7  # k_part_tile, k_apply_value, k_unpermute, k_apply_map, k_map_hot, k_apply_coord, k_events
 
 CC_OK = 0
 CC_ERR_INVALID = -1
@@ -73,12 +73,19 @@ CC_EV_ELECT = 3
 CC_EV_JOIN = 4
 CC_EV_LEAVE = 5
 CC_EV_EXECUTE = 6
+CC_EV_MEMBER = 7
 
 CC_EVSRC_COMMIT = 0
 CC_EVSRC_TIMER = 1
 CC_EVSRC_CLOSE = 2
+CC_EVSRC_RESULT = 3
 
 CC_CFG_TIMERS_DEFERRED = 1
+CC_CFG_VALUE_EVENTS = 2
+CC_LOCK_QUEUE = 64
+CC_ELECTION_LISTENERS = 64
+CC_GROUP_MEMBERS = 64
+CC_VALUE_LISTENERS = 64
 
 # ops each resource type registers (ResourceStateMachine.init + Copycat reflection `configure`)
 TYPE_OPS = {

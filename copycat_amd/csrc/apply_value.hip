@@ -70,6 +70,7 @@ constexpr int kWaveRecs = kWave * kApplyPer;  // records of a chunk per wave (co
 //   3. results go back through LDS to staging order and out contiguously.
 __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
                                                     const uint16_t* __restrict__ ttab, uint32_t tiles, uint32_t sb,
+                                                    const uint8_t* __restrict__ sb_kind,
                                                     uint32_t* __restrict__ val_meta, uint64_t* __restrict__ val_v,
                                                     uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                     uint32_t* __restrict__ err_out) {
@@ -86,6 +87,7 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
   __shared__ uint32_t rpre[kMaxTiles + 1];   // records of this super-bucket before tile t
 
   const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
+  if (sb_kind && sb_kind[s]) return;  // holds coordination resources / value events: k_apply_coord
   ValState st_reg{val_meta[(uint64_t)s * kSbSlots + t], val_v[(uint64_t)s * kSbSlots + t]};
 #pragma unroll
   for (int q = 0; q < kApplyWaves; ++q) wcnt[q][t] = 0;
@@ -264,7 +266,7 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
 
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {
   a.mark(K_APPLY_VALUE, 1, st);
-  hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.val_meta,
+  hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.sb_kind, a.val_meta,
                      a.val_v, a.rst_status, a.rst_value, a.err);
   a.mark(K_APPLY_VALUE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

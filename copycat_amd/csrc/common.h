@@ -86,6 +86,8 @@ __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {
 __host__ __device__ inline bool op_on_gpu(uint32_t type, uint32_t op) {
   if (type == CC_RES_VALUE) return op == CC_OP_DELETE || (op >= 50 && op <= 53);
   if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops; map-wide ops are next
+  if (type == CC_RES_LOCK || type == CC_RES_ELECTION) return op_registered(type, op);
+  if (type == CC_RES_GROUP) return op_registered(type, op) && op != CC_OP_GROUP_SCHEDULE;
   return false;
 }
 
@@ -108,6 +110,38 @@ constexpr uint32_t kMwVtagMask = 7u << 21;
 constexpr uint32_t kMwPending = 1u << 24;  // bound this round, key not yet visible (apply_map resolution)
 constexpr uint32_t kMwDead = 1u << 25;     // entry of a deleted map: never matches, reclaimed by compaction
 constexpr uint32_t kMwIdentMask = kMwSlotMask | (3u << 17) | kMwUsed | kMwDead;
+// coordination state blocks (apply_coord.hip): one per resource slot, fixed capacity
+struct CoordHdr {
+  uint32_t who;    // lock holder / election leader instance slot
+  uint32_t flags;  // kCoHeld (held / has leader) | kCoCleaned
+  uint64_t idx;    // holder / leader commit index
+  uint32_t head;   // lock waiter ring head
+  uint32_t n;      // waiters / listeners / members
+  uint64_t pad;
+};
+struct CoordEnt {
+  uint64_t x;     // lock waiter: timeout deadline (kNoDeadline: none); election listener / group member: instance id
+  uint64_t idx;   // commit index
+  uint32_t inst;  // instance slot
+  uint32_t pad;
+};
+constexpr uint32_t kCoHeld = 1u, kCoCleaned = 2u;
+constexpr uint64_t kNoDeadline = ~0ull;
+constexpr int kCoordCap = 64;  // CC_LOCK_QUEUE = CC_ELECTION_LISTENERS = CC_GROUP_MEMBERS = CC_VALUE_LISTENERS
+constexpr size_t kCoordBlock = sizeof(CoordHdr) + kCoordCap * sizeof(CoordEnt);
+// one event of the per-sub-batch arena (apply_coord.hip -> events.hip)
+struct EvRec {
+  uint32_t g;       // staging position of the commit
+  uint32_t target;  // instance slot
+  uint64_t payload;
+  uint16_t k;       // emission order within the commit
+  uint8_t code, tag, src, pad[3];
+};
+constexpr uint32_t kErrTime = 8u;  // the time column decreased inside a batch
+
+// extended staging (partition.hip) options
+constexpr uint32_t kExtValue = 1u;     // value records carry the extended columns (value events on the GPU)
+constexpr uint32_t kExtDeferred = 2u;  // manager-mode timer order
 // staging meta: op | flags << 8 | slot low byte << 16 | (map records) ttl > 0 << 24
 constexpr uint32_t kMetaTtl = 1u << 24;
 __host__ __device__ inline uint32_t mw_ident(uint32_t res, uint32_t ktag) { return (res & kMwSlotMask) | ((ktag & 3) << 17) | kMwUsed; }

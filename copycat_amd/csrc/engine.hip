@@ -46,8 +46,6 @@ struct cc_engine {
   uint64_t sub_batch = 0, max_tiles = 0;
   // host mirrors of the registry
   std::vector<uint8_t> res_type;     // [sb*256]
-  std::vector<uint8_t> bucket_type;  // [slots/64] (a 64-slot bucket holds one resource type)
-  std::vector<uint32_t> bucket_live; // live resources per bucket
   std::vector<uint32_t> inst_res;    // [max_inst]
   std::vector<uint64_t> inst_id, inst_client;
   // device registry + state
@@ -81,6 +79,22 @@ struct cc_engine {
   uint32_t* d_hot_cond = nullptr;
   void* d_hot_agg = nullptr;
   void* d_hot_s0 = nullptr;
+  // extended staging (maps / coordination / value events) + coordination + events
+  bool ext = false, coord_on = false;
+  std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
+  uint8_t* d_sb_kind = nullptr;
+  uint64_t* d_inst_id = nullptr;     // instance slot -> instance id (election listeners, group members)
+  uint8_t* d_coord = nullptr;        // [slots] coordination blocks
+  uint64_t* d_clock = nullptr;       // the engine's log clock (max time applied / advanced)
+  uint16_t* d_ev_cnt = nullptr;      // [sub_batch] events per staged commit
+  uint32_t* d_row_of = nullptr;      // [sub_batch]
+  uint32_t* d_ev_loc = nullptr;      // [sub_batch]
+  uint32_t* d_tile_sum = nullptr;    // [max_tiles]
+  uint64_t* d_tile_off = nullptr;    // [max_tiles]
+  EvRec* d_arena = nullptr;
+  unsigned long long* d_arena_n = nullptr;
+  unsigned long long* d_ev_total = nullptr;
+  uint64_t arena_cap = 0;
   uint64_t applied = 0;
   bool applied_pending = false;
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
@@ -140,11 +154,52 @@ static void free_all(cc_engine* e) {
                   e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
                   e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_st_res,
                   e->d_st_key,   e->d_st_idx,   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
-                  e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0};
+                  e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
+                  e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
+                  e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
+
+// Extended staging columns (maps, coordination, value events); with `coord`, the coordination blocks and the
+// event buffers.  Allocated on first need (engine creation or the first coordination resource).
+static int ensure_ext(cc_engine* e, bool coord) {
+  auto alloc = [&](void** p, size_t bytes) -> int {
+    if (*p) return CC_OK;
+    hipError_t x = hipMalloc(p, bytes);
+    if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc (extended staging)", x);
+    return CC_OK;
+  };
+  int rc = CC_OK;
+  if (!e->ext) {
+    if ((rc = alloc((void**)&e->d_st_res, sizeof(uint32_t) * e->sub_batch)) ||
+        (rc = alloc((void**)&e->d_st_key, sizeof(uint64_t) * e->sub_batch)) ||
+        (rc = alloc((void**)&e->d_st_idx, sizeof(uint64_t) * e->sub_batch)))
+      return rc;
+    e->ext = true;
+  }
+  if (coord && !e->coord_on) {
+    const uint64_t slots = (uint64_t)e->sb << kSbShift;
+    e->arena_cap = std::max<uint64_t>(e->cfg.max_events, 1);
+    if ((rc = alloc((void**)&e->d_coord, kCoordBlock * slots)) ||
+        (rc = alloc((void**)&e->d_ev_cnt, sizeof(uint16_t) * e->sub_batch)) ||
+        (rc = alloc((void**)&e->d_row_of, sizeof(uint32_t) * e->sub_batch)) ||
+        (rc = alloc((void**)&e->d_ev_loc, sizeof(uint32_t) * e->sub_batch)) ||
+        (rc = alloc((void**)&e->d_tile_sum, sizeof(uint32_t) * e->max_tiles)) ||
+        (rc = alloc((void**)&e->d_tile_off, sizeof(uint64_t) * e->max_tiles)) ||
+        (rc = alloc((void**)&e->d_arena, sizeof(EvRec) * e->arena_cap)) ||
+        (rc = alloc((void**)&e->d_arena_n, sizeof(unsigned long long))) ||
+        (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))))
+      return rc;
+    hipError_t x = hipMemset(e->d_coord, 0, kCoordBlock * slots);
+    if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
+    e->coord_on = true;
+  }
+  return CC_OK;
+}
+
+static bool is_coord(uint32_t type) { return type == CC_RES_LOCK || type == CC_RES_ELECTION || type == CC_RES_GROUP; }
 
 extern "C" int cc_abi_version(void) { return CC_ABI_VERSION; }
 extern "C" const char* cc_last_error(void) { return g_err.c_str(); }
@@ -180,8 +235,6 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   e->max_tiles = sub / kTile;
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
   e->res_type.assign(slots, CC_RES_NONE);
-  e->bucket_type.assign(slots / kLaneRes, CC_RES_NONE);
-  e->bucket_live.assign(slots / kLaneRes, 0);
   e->inst_res.assign(cfg->max_instances, kNoRes);
   e->inst_id.assign(cfg->max_instances, 0);
   e->inst_client.assign(cfg->max_instances, 0);
@@ -209,9 +262,6 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_tbl_val, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_tbl_ci, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_tbl_ins, sizeof(uint64_t) * e->map_entries);
-    ALLOC(e->d_st_res, sizeof(uint32_t) * e->sub_batch);
-    ALLOC(e->d_st_key, sizeof(uint64_t) * e->sub_batch);
-    ALLOC(e->d_st_idx, sizeof(uint64_t) * e->sub_batch);
     ALLOC(e->d_hot, sizeof(HotKey) * kHotMax);
     ALLOC(e->d_hot_n, sizeof(uint32_t));
     ALLOC(e->d_hot_rpre, sizeof(uint32_t) * kHotMax * (kMaxTiles + 1));
@@ -225,6 +275,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
   ALLOC(e->d_err, sizeof(uint32_t));
   ALLOC(e->d_last_index, sizeof(uint64_t));
+  ALLOC(e->d_sb_kind, e->sb);
+  ALLOC(e->d_inst_id, sizeof(uint64_t) * cfg->max_instances);
+  ALLOC(e->d_clock, sizeof(uint64_t));
 #undef ALLOC
   if ((he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", he);
   e->last_stream = e->own_stream;
@@ -233,6 +286,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if ((he = hipMemset(e->d_val_meta, 0, sizeof(uint32_t) * slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_val_v, 0, sizeof(uint64_t) * slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_sb_kind, 0, e->sb)) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_clock, 0, sizeof(uint64_t))) != hipSuccess) return fail("memset", he);
+  e->sb_kind.assign(e->sb, 0);
   if (e->map_bits) {  // word 0 = empty entry
     if ((he = hipMemset(e->d_tbl_word, 0, sizeof(uint32_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_ci, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
@@ -253,6 +309,14 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     return set_err(CC_ERR_STATE, "device self-check failed: LDS atomics are not lane-ordered on this device");
   }
   if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
+  if (e->map_bits || (cfg->flags & CC_CFG_VALUE_EVENTS)) {
+    int rc = ensure_ext(e, (cfg->flags & CC_CFG_VALUE_EVENTS) != 0);
+    if (rc) {
+      free_all(e);
+      delete e;
+      return rc;
+    }
+  }
   *out = e;
   return CC_OK;
 }
@@ -273,11 +337,15 @@ static int check_device_err(cc_engine* e) {
   HIPCHECK(hipMemcpy(&err, e->d_err, sizeof err, hipMemcpyDeviceToHost));
   if (err) {
     HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
-    if (err & kErrCapacity) return set_err(CC_ERR_CAPACITY, "a map table region is full (raise map_capacity)");
+    if (err & kErrTime) return set_err(CC_ERR_INVALID, "the time column must be non-decreasing within a batch");
+    if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
+    if (err & kErrCapacity)
+      return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, lock queue, listeners, members)");
     if (err & kErrUnsupported)
       return set_err(CC_ERR_UNSUPPORTED,
-                     "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten; map "
-                     "containsValue/size/isEmpty/clear/Delete; map ops with ttl > 0)");
+                     "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten without "
+                     "CC_CFG_VALUE_EVENTS; map containsValue/size/isEmpty/clear/Delete; map ops with ttl > 0; group "
+                     "schedule) or published events with no event stream");
     return set_err(CC_ERR_STATE, "device-side check failed");
   }
   return CC_OK;
@@ -306,25 +374,23 @@ static int quiesce(cc_engine* e) {
 
 static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
   if (type == CC_RES_MAP && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map resources need cc_config.map_capacity > 0");
-  if (type != CC_RES_VALUE && type != CC_RES_MAP)
-    return set_err(CC_ERR_UNSUPPORTED, "this build applies AtomicValue and Map resources on the GPU; lock/election/group are not built yet");
+  if (type < CC_RES_VALUE || type > CC_RES_GROUP) return set_err(CC_ERR_INVALID, "unknown resource type");
   const uint64_t end = (uint64_t)first + count;
   if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");
   for (uint64_t s = first; s < end; ++s) {
     if (e->res_type[s] != CC_RES_NONE) return set_err(CC_ERR_INVALID, "resource slot already in use");
-    const uint32_t b = (uint32_t)(s / kLaneRes);
-    if (e->bucket_type[b] != CC_RES_NONE && e->bucket_type[b] != type)
-      return set_err(CC_ERR_INVALID, "a 64-slot bucket holds one resource type (allocate slots per type in groups of 64)");
   }
   int rc = quiesce(e);
   if (rc) return rc;
+  const bool value_events = (e->cfg.flags & CC_CFG_VALUE_EVENTS) != 0;
+  if (is_coord(type) && (rc = ensure_ext(e, true))) return rc;
   for (uint64_t s = first; s < end; ++s) {
     e->res_type[s] = (uint8_t)type;
-    const uint32_t b = (uint32_t)(s / kLaneRes);
-    e->bucket_type[b] = (uint8_t)type;
-    e->bucket_live[b]++;
+    if (is_coord(type) || (type == CC_RES_VALUE && value_events)) e->sb_kind[s >> kSbShift] = 1;
   }
   HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
+  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)first * kCoordBlock, 0, kCoordBlock * (uint64_t)count));
   // fresh state: AtomicValueState() {value = null; current = null}
   HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
   HIPCHECK(hipMemset(e->d_val_v + first, 0, sizeof(uint64_t) * count));
@@ -352,8 +418,7 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
     HIPCHECK(hipStreamSynchronize(e->own_stream));
   }
   e->res_type[slot] = CC_RES_NONE;
-  const uint32_t b = slot / kLaneRes;
-  if (--e->bucket_live[b] == 0) e->bucket_type[b] = CC_RES_NONE;
+  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)slot * kCoordBlock, 0, kCoordBlock));
   HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
   HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(e->d_val_v + slot, 0, sizeof(uint64_t)));
@@ -383,6 +448,7 @@ static int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res
     e->inst_client[first + k] = client;
   }
   HIPCHECK(hipMemcpy(e->d_inst_res + first, e->inst_res.data() + first, sizeof(uint32_t) * count, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(e->d_inst_id + first, e->inst_id.data() + first, sizeof(uint64_t) * count, hipMemcpyHostToDevice));
   return CC_OK;
 }
 
@@ -399,7 +465,6 @@ extern "C" int cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t cou
 
 extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const cc_results* out, const cc_events* ev,
                               void* stream) {
-  (void)ev;
   if (!e || !c || !out) return set_err(CC_ERR_INVALID, "null argument");
   if (n == 0) return CC_OK;
   if (n > e->cfg.max_batch) return set_err(CC_ERR_CAPACITY, "batch larger than max_batch");
@@ -412,6 +477,12 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15) || (((uintptr_t)c->inst) & 15))
     return set_err(CC_ERR_INVALID, "inst and value must be 16-byte aligned, status 4-byte aligned");
   if (e->map_bits && !c->key) return set_err(CC_ERR_INVALID, "an engine with maps needs the key column");
+  if (ev && (!ev->pos || !ev->target || !ev->code || !ev->src || !ev->tag || !ev->payload || !ev->count))
+    return set_err(CC_ERR_INVALID, "event stream columns and count are required");
+  if (e->coord_on) {  // events of this batch start at 0; the log clock must not go backwards inside it
+    HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), st));
+    if (launch_time_check(c->time, n, e->d_clock, e->d_err, st)) return set_err(CC_ERR_HIP, "time check", hipGetLastError());
+  }
   for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
     const uint64_t hi = std::min(n, lo + e->sub_batch);
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
@@ -461,6 +532,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.key = c->key;
     pa.index = c->index;
     pa.aux = c->aux;
+    pa.time = c->time;
+    pa.clock_base = e->d_clock;
+    pa.ext_flags = ((e->cfg.flags & CC_CFG_VALUE_EVENTS) ? kExtValue : 0u) | ((e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? kExtDeferred : 0u);
+    pa.ext = e->ext;
     pa.lo = lo;
     pa.hi = hi;
     pa.inst_res = e->d_inst_res;
@@ -487,6 +562,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.tiles = tiles;
     va.sb = e->sb_total();
     va.sb_val = e->sb;
+    va.sb_kind = e->d_sb_kind;
     va.val_meta = e->d_val_meta;
     va.val_v = e->d_val_v;
     va.rst_status = e->d_rst_status;
@@ -518,6 +594,35 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.mark = marker_of(e);
       if (launch_apply_map(ma, st)) return set_err(CC_ERR_HIP, "map apply launch", hipGetLastError());
     }
+    if (e->coord_on) {
+      HIPCHECK(hipMemsetAsync(e->d_ev_cnt, 0, sizeof(uint16_t) * (hi - lo), st));
+      HIPCHECK(hipMemsetAsync(e->d_arena_n, 0, sizeof(unsigned long long), st));
+      CoordArgs ca{};
+      ca.st_meta = e->d_st_meta;
+      ca.st_ab = e->d_st_ab;
+      ca.st_res = e->d_st_res;
+      ca.st_key = e->d_st_key;
+      ca.st_idx = e->d_st_idx;
+      ca.ttab = e->d_ttab;
+      ca.tiles = tiles;
+      ca.sb = e->sb_total();
+      ca.sb_val = e->sb;
+      ca.sb_kind = e->d_sb_kind;
+      ca.res_type = e->d_res_type;
+      ca.inst_id = e->d_inst_id;
+      ca.coord = e->d_coord;
+      ca.val_meta = e->d_val_meta;
+      ca.val_v = e->d_val_v;
+      ca.rst_status = e->d_rst_status;
+      ca.rst_value = e->d_rst_value;
+      ca.ev_cnt = e->d_ev_cnt;
+      ca.arena = e->d_arena;
+      ca.arena_n = e->d_arena_n;
+      ca.arena_cap = e->arena_cap;
+      ca.err = e->d_err;
+      ca.mark = marker_of(e);
+      if (launch_apply_coord(ca, st)) return set_err(CC_ERR_HIP, "coordination apply launch", hipGetLastError());
+    }
     UnpermuteArgs ua{};
     ua.cpos = e->d_cpos;
     ua.ttab = e->d_ttab;
@@ -530,6 +635,38 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.out_value = out->value;
     ua.mark = marker_of(e);
     if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
+    if (e->coord_on) {
+      EventArgs ea{};
+      ea.cpos = e->d_cpos;
+      ea.lo = lo;
+      ea.hi = hi;
+      ea.tiles = tiles;
+      ea.ev_cnt = e->d_ev_cnt;
+      ea.row_of = e->d_row_of;
+      ea.ev_loc = e->d_ev_loc;
+      ea.tile_sum = e->d_tile_sum;
+      ea.tile_off = e->d_tile_off;
+      ea.ev_total = e->d_ev_total;
+      ea.arena = e->d_arena;
+      ea.arena_n = e->d_arena_n;
+      ea.arena_cap = e->arena_cap;
+      if (ev) {
+        ea.out_cap = ev->capacity;
+        ea.out_pos = ev->pos;
+        ea.out_target = ev->target;
+        ea.out_code = ev->code;
+        ea.out_src = ev->src;
+        ea.out_tag = ev->tag;
+        ea.out_payload = ev->payload;
+      }
+      ea.err = e->d_err;
+      ea.mark = marker_of(e);
+      if (launch_events(ea, st)) return set_err(CC_ERR_HIP, "events launch", hipGetLastError());
+    }
+  }
+  if (e->coord_on) {
+    if (ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    if (launch_clock_advance(c->time, n, 0, e->d_clock, st)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
   }
   if (c->index) {  // the applied watermark = index of the batch's last entry
     HIPCHECK(hipMemcpyAsync(e->d_last_index, c->index + (n - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
@@ -655,7 +792,85 @@ extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, ui
   return CC_OK;
 }
 
-static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map", "k_map_hot"};
+static int read_block(cc_engine* e, uint32_t slot, uint32_t type, CoordHdr& h, std::vector<CoordEnt>& ents, uint64_t* clock) {
+  if (!e || slot >= e->cfg.max_resources || e->res_type[slot] != type || !e->coord_on)
+    return set_err(CC_ERR_INVALID, "slot does not hold a resource of that type");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  std::vector<uint8_t> blk(kCoordBlock);
+  HIPCHECK(hipMemcpy(blk.data(), e->d_coord + (uint64_t)slot * kCoordBlock, kCoordBlock, hipMemcpyDeviceToHost));
+  memcpy(&h, blk.data(), sizeof h);
+  ents.resize(kCoordCap);
+  memcpy(ents.data(), blk.data() + sizeof(CoordHdr), sizeof(CoordEnt) * kCoordCap);
+  if (clock) HIPCHECK(hipMemcpy(clock, e->d_clock, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return CC_OK;
+}
+
+extern "C" int cc_read_lock_state(cc_engine* e, uint32_t slot, int64_t* holder, uint64_t* holder_index,
+                                  uint8_t* holder_cleaned, uint64_t cap, uint64_t* count, uint32_t* h_queue_inst,
+                                  uint64_t* h_queue_index) {
+  CoordHdr h;
+  std::vector<CoordEnt> q;
+  uint64_t clock = 0;
+  int rc = read_block(e, slot, CC_RES_LOCK, h, q, &clock);
+  if (rc) return rc;
+  const bool held = h.flags & kCoHeld;
+  if (holder) *holder = held ? (int64_t)h.who : -1;
+  if (holder_index) *holder_index = held ? h.idx : 0;
+  if (holder_cleaned) *holder_cleaned = held && (h.flags & kCoCleaned) ? 1 : 0;
+  uint64_t n = 0;
+  for (uint32_t i = 0; i < h.n; ++i) {  // timeouts due at the engine clock have fired (LockState.java:54-58)
+    const CoordEnt& x = q[(h.head + i) % kCoordCap];
+    if (x.x != kNoDeadline && x.x <= clock) continue;
+    if (n < cap) {
+      if (h_queue_inst) h_queue_inst[n] = x.inst;
+      if (h_queue_index) h_queue_index[n] = x.idx;
+    }
+    ++n;
+  }
+  if (count) *count = n;
+  return CC_OK;
+}
+
+extern "C" int cc_read_election_state(cc_engine* e, uint32_t slot, int64_t* leader, uint64_t* leader_index, uint64_t cap,
+                                      uint64_t* count, uint32_t* h_listener_inst, uint64_t* h_listener_index) {
+  CoordHdr h;
+  std::vector<CoordEnt> q;
+  int rc = read_block(e, slot, CC_RES_ELECTION, h, q, nullptr);
+  if (rc) return rc;
+  const bool has = h.flags & kCoHeld;
+  if (leader) *leader = has ? (int64_t)h.who : -1;
+  if (leader_index) *leader_index = has ? h.idx : 0;
+  for (uint32_t i = 0; i < h.n && i < cap; ++i) {
+    if (h_listener_inst) h_listener_inst[i] = q[i].inst;
+    if (h_listener_index) h_listener_index[i] = q[i].idx;
+  }
+  if (count) *count = h.n;
+  return CC_OK;
+}
+
+extern "C" int cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint64_t* h_ids) {
+  CoordHdr h;
+  std::vector<CoordEnt> q;
+  int rc = read_block(e, slot, CC_RES_GROUP, h, q, nullptr);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < h.n && i < cap; ++i)
+    if (h_ids) h_ids[i] = q[i].x;
+  if (count) *count = h.n;
+  return CC_OK;
+}
+
+extern "C" int cc_advance_time(cc_engine* e, uint64_t now) {
+  if (!e) return CC_ERR_INVALID;
+  int rc = quiesce(e);
+  if (rc) return rc;
+  if (launch_clock_advance(nullptr, 0, now, e->d_clock, e->own_stream)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(e->own_stream));
+  return CC_OK;
+}
+
+static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map", "k_map_hot",
+                                          "k_apply_coord", "k_events"};
 
 extern "C" int cc_profile_enable(cc_engine* e, int on) {
   if (!e) return CC_ERR_INVALID;

@@ -5,7 +5,7 @@
 namespace cc {
 
 // Optional per-kernel timing (HIP events recorded on the launch stream around each kernel).
-enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_APPLY_MAP, K_MAP_HOT, K_NUM };
+enum KernelId { K_PART_TILE = 0, K_APPLY_VALUE, K_UNPERMUTE, K_APPLY_MAP, K_MAP_HOT, K_APPLY_COORD, K_EVENTS, K_NUM };
 struct Marker {
   void (*fn)(void* ctx, int kernel, int begin, hipStream_t st);
   void* ctx;
@@ -24,7 +24,11 @@ struct PartArgs {
   const uint64_t* b;
   const uint64_t* key;    // maps only
   const uint64_t* index;  // maps only (commit index of map entries)
-  const uint64_t* aux;    // maps only (ttl > 0 is not applied on the GPU)
+  const uint64_t* aux;    // maps: ttl (> 0 not applied on the GPU); locks: timeout
+  const uint64_t* time;   // locks: log time (clock)
+  const uint64_t* clock_base;  // device: the engine clock before this batch
+  uint32_t ext_flags;     // kExtValue | kExtDeferred
+  bool ext;               // extended staging (maps / coordination / value events)
   uint64_t lo, hi;
   const uint32_t* inst_res;
   const uint8_t* res_type;
@@ -53,6 +57,7 @@ struct ValueArgs {
   uint32_t tiles;
   uint32_t sb;           // total super-buckets (ttab row width - 1)
   uint32_t sb_val;       // value super-buckets (the apply grid)
+  const uint8_t* sb_kind;  // non-zero: the super-bucket runs on k_apply_coord (may be null)
   uint32_t* val_meta;    // [sb*256]
   uint64_t* val_v;       // [sb*256]
   uint8_t* rst_status;   // staged results [sub_batch]
@@ -125,6 +130,58 @@ int launch_map_hot_detect(const HotArgs& a, hipStream_t st);
 int launch_map_hot_apply(const HotArgs& a, hipStream_t st);
 size_t hot_agg_bytes();
 size_t hot_s0_bytes();
+
+struct CoordArgs {
+  const uint32_t* st_meta;
+  const u64x2* st_ab;
+  const uint32_t* st_res;
+  const uint64_t* st_key;
+  const uint64_t* st_idx;
+  const uint16_t* ttab;
+  uint32_t tiles, sb, sb_val;
+  const uint8_t* sb_kind;
+  const uint8_t* res_type;
+  const uint64_t* inst_id;
+  uint8_t* coord;
+  uint32_t* val_meta;
+  uint64_t* val_v;
+  uint8_t* rst_status;
+  uint64_t* rst_value;
+  uint16_t* ev_cnt;
+  EvRec* arena;
+  unsigned long long* arena_n;
+  uint64_t arena_cap;
+  uint32_t* err;
+  Marker mark;
+};
+int launch_apply_coord(const CoordArgs& a, hipStream_t st);
+int launch_time_check(const uint64_t* time, uint64_t n, uint64_t* clock, uint32_t* err, hipStream_t st);
+int launch_clock_advance(const uint64_t* time, uint64_t n, uint64_t now, uint64_t* clock, hipStream_t st);
+
+struct EventArgs {
+  const uint16_t* cpos;
+  uint64_t lo, hi;
+  uint32_t tiles;
+  const uint16_t* ev_cnt;
+  uint32_t* row_of;
+  uint32_t* ev_loc;
+  uint32_t* tile_sum;
+  uint64_t* tile_off;
+  unsigned long long* ev_total;
+  const EvRec* arena;
+  const unsigned long long* arena_n;
+  uint64_t arena_cap;
+  uint64_t out_cap;
+  uint32_t* out_pos;
+  uint32_t* out_target;
+  uint8_t* out_code;
+  uint8_t* out_src;
+  uint8_t* out_tag;
+  uint64_t* out_payload;
+  uint32_t* err;
+  Marker mark;
+};
+int launch_events(const EventArgs& a, hipStream_t st);
 
 struct UnpermuteArgs {
   const uint16_t* cpos;

@@ -1,0 +1,128 @@
+// events.hip — the published events of a sub-batch, in the caller's order: by log row, then by the order in
+// which the commit published them (Session.publish order, ManagedResourceSession.java:64-71).
+//
+// apply_coord.hip leaves each commit's event count at its staging position (ev_cnt) and the events themselves,
+// tagged with (staging position, emission index), in an arena in whatever order workgroups finished.
+//   k_ev_rows    : per partition tile: the counts back in row order (through cpos), an exclusive scan inside
+//                  the tile, and row_of[staging position] = row for commits that published;
+//   k_ev_tiles   : one workgroup: exclusive scan of the tile totals on top of the events already written by
+//                  earlier sub-batches; capacity / no-stream checks;
+//   k_ev_scatter : every arena event to out[tile offset + row offset + emission index].
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+constexpr int kER = kPT;  // 1024 threads per tile
+constexpr int kERPer = kTile / kER;
+
+__global__ __launch_bounds__(kER) void k_ev_rows(const uint16_t* __restrict__ cpos, uint64_t n, const uint16_t* __restrict__ ev_cnt,
+                                                 uint32_t* __restrict__ row_of, uint32_t* __restrict__ ev_loc,
+                                                 uint32_t* __restrict__ tile_sum) {
+  __shared__ uint32_t wsum[kER / kWave];
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint64_t r0 = (uint64_t)blockIdx.x * kTile + (uint64_t)t * kERPer;
+  const uint32_t tbase = blockIdx.x * kTile;
+  uint32_t c[kERPer], sum = 0;
+#pragma unroll
+  for (int q = 0; q < kERPer; ++q) {
+    const uint64_t i = r0 + q;
+    c[q] = 0;
+    if (i < n) {
+      const uint16_t p = cpos[i];
+      if (p != 0xFFFF) {
+        c[q] = ev_cnt[tbase + p];
+        if (c[q]) row_of[tbase + p] = (uint32_t)i;
+      }
+    }
+    sum += c[q];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (l >= (uint32_t)d) inc += y;
+  }
+  if (l == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum, total = 0;
+  for (uint32_t q = 0; q < kER / kWave; ++q) {
+    if (q < w) run += wsum[q];
+    total += wsum[q];
+  }
+#pragma unroll
+  for (int q = 0; q < kERPer; ++q) {
+    const uint64_t i = r0 + q;
+    if (i < n) ev_loc[i] = run;
+    run += c[q];
+  }
+  if (t == 0) tile_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kER) void k_ev_tiles(const uint32_t* __restrict__ tile_sum, uint32_t tiles,
+                                                  unsigned long long* __restrict__ ev_total, uint64_t* __restrict__ tile_off,
+                                                  const unsigned long long* __restrict__ arena_n, uint64_t arena_cap,
+                                                  uint64_t out_cap, int has_out, uint32_t* __restrict__ err_out) {
+  __shared__ unsigned long long wsum[kER / kWave];
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  const unsigned long long base = *ev_total;
+  unsigned long long v = t < tiles ? tile_sum[t] : 0, inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(inc, d, 64);
+    if (l >= (uint32_t)d) inc += y;
+  }
+  if (l == 63) wsum[w] = inc;
+  __syncthreads();
+  unsigned long long run = inc - v, total = 0;
+  for (uint32_t q = 0; q < kER / kWave; ++q) {
+    if (q < w) run += wsum[q];
+    total += wsum[q];
+  }
+  if (t < tiles) tile_off[t] = base + run;
+  __syncthreads();
+  if (t == 0) {
+    *ev_total = base + total;
+    uint32_t err = 0;
+    if (*arena_n > arena_cap || (has_out && base + total > out_cap)) err |= kErrEvents;
+    if (!has_out && total) err |= kErrUnsupported;  // events published but no stream to publish them to
+    if (err) atomicOr(err_out, err);
+  }
+}
+
+__global__ void k_ev_scatter(const EvRec* __restrict__ arena, const unsigned long long* __restrict__ arena_n,
+                             uint64_t arena_cap, const uint32_t* __restrict__ row_of, const uint32_t* __restrict__ ev_loc,
+                             const uint64_t* __restrict__ tile_off, uint64_t lo, uint64_t out_cap, uint32_t* __restrict__ pos,
+                             uint32_t* __restrict__ target, uint8_t* __restrict__ code, uint8_t* __restrict__ src,
+                             uint8_t* __restrict__ tag, uint64_t* __restrict__ payload) {
+  const uint64_t ne = *arena_n < arena_cap ? *arena_n : arena_cap;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
+    const EvRec r = arena[e];
+    const uint32_t i = row_of[r.g];
+    const uint64_t dst = tile_off[i / kTile] + ev_loc[i] + r.k;
+    if (dst >= out_cap) continue;
+    pos[dst] = (uint32_t)(lo + i);
+    target[dst] = r.target;
+    code[dst] = r.code;
+    src[dst] = r.src;
+    tag[dst] = r.tag;
+    payload[dst] = r.payload;
+  }
+}
+
+int launch_events(const EventArgs& a, hipStream_t st) {
+  if (a.tiles == 0) return 0;
+  a.mark(K_EVENTS, 1, st);
+  hipLaunchKernelGGL(k_ev_rows, dim3(a.tiles), dim3(kER), 0, st, a.cpos, a.hi - a.lo, a.ev_cnt, a.row_of, a.ev_loc,
+                     a.tile_sum);
+  hipLaunchKernelGGL(k_ev_tiles, dim3(1), dim3(kER), 0, st, a.tile_sum, a.tiles, a.ev_total, a.tile_off, a.arena_n,
+                     a.arena_cap, a.out_cap, a.out_pos ? 1 : 0, a.err);
+  if (a.out_pos)
+    hipLaunchKernelGGL(k_ev_scatter, dim3(1024), dim3(256), 0, st, a.arena, a.arena_n, a.arena_cap, a.row_of, a.ev_loc,
+                       a.tile_off, a.lo, a.out_cap, a.out_pos, a.out_target, a.out_code, a.out_src, a.out_tag,
+                       a.out_payload);
+  a.mark(K_EVENTS, 0, st);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cc

@@ -64,19 +64,20 @@ size_t tile_lds_bytes(uint32_t sb, bool maps) {
   return chunk * rec + (size_t)kPW * hw * 4 + 4 * (2 * hw) * 2 + 16 * 4 + hot;
 }
 
-// LDS layout (dynamic): rab[C] u64x2 | [MAPS: rkey[C] u64 | ridx[C] u64 | rres[C] u32] | rmeta[C] u32 |
+// LDS layout (dynamic): rab[C] u64x2 | [EXT: rkey[C] u64 | ridx[C] u64 | rres[C] u32] | rmeta[C] u32 |
 //   rsb[C] u16 | wc[kPW][hw] u32 | toff, trun, ctot, kstart [2hw] u16 | wsum[16] u32 |
-//   [MAPS: hot keys: hslot[kHotSlots] u32 | hh64[kHotMax] u64 | hkey[kHotMax] u64 | hident[kHotMax] u32]
+//   [EXT: hot keys: hslot[kHotSlots] u32 | hh64[kHotMax] u64 | hkey[kHotMax] u64 | hident[kHotMax] u32]
 //
 // Super-bucket of a commit: value resources by slot (slot >> 8); map commits by hash(map, key tag, key) into
 // the map regions that follow the value super-buckets; commits of a hot key (apply_map_hot.hip) into that
 // key's own bucket after the regions.
-template <int J, bool MAPS>
+template <int J, bool EXT>
 __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                 const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
                                                 const uint64_t* __restrict__ cidx, const uint64_t* __restrict__ caux,
-                                                uint64_t lo, uint64_t hi,
+                                                const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ clock_base,
+                                                uint32_t ext_flags, uint64_t lo, uint64_t hi,
                                                 const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
                                                 uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits,
                                                 const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n,
@@ -88,9 +89,9 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   extern __shared__ __align__(16) uint8_t smem[];
   u64x2* rab = reinterpret_cast<u64x2*>(smem);
   uint64_t* rkey = reinterpret_cast<uint64_t*>(rab + C);
-  uint64_t* ridx = rkey + (MAPS ? C : 0);
-  uint32_t* rres = reinterpret_cast<uint32_t*>(ridx + (MAPS ? C : 0));
-  uint32_t* rmeta = rres + (MAPS ? C : 0);
+  uint64_t* ridx = rkey + (EXT ? C : 0);
+  uint32_t* rres = reinterpret_cast<uint32_t*>(ridx + (EXT ? C : 0));
+  uint32_t* rmeta = rres + (EXT ? C : 0);
   uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + C);
   uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + C);  // [kPW][hw] packed u16 pairs
   const uint32_t hw = (sb + 1) / 2;
@@ -101,12 +102,14 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   uint32_t* wsum = reinterpret_cast<uint32_t*>(kstart + 2 * hw);
   uint32_t* ctot32 = reinterpret_cast<uint32_t*>(ctot);  // packed view for LDS atomics
   uint32_t* hslot = wsum + 16;
-  uint64_t* hh64 = reinterpret_cast<uint64_t*>(hslot + (MAPS ? kHotSlots : 0));
+  uint64_t* hh64 = reinterpret_cast<uint64_t*>(hslot + (EXT ? kHotSlots : 0));
   uint64_t* hkey = hh64 + kHotMax;
   uint32_t* hident = reinterpret_cast<uint32_t*>(hkey + kHotMax);
 
   uint32_t nhot = 0;
-  if (MAPS) {
+  const uint64_t cbase0 = EXT && clock_base ? *clock_base : 0;
+  const bool value_ext = (ext_flags & kExtValue) != 0, deferred = (ext_flags & kExtDeferred) != 0;
+  if (EXT && map_bits) {
     nhot = *hot_n;
     for (uint32_t q = threadIdx.x; q < kHotSlots; q += kPT) hslot[q] = 0xFFFFFFFFu;
     if (threadIdx.x < nhot) {
@@ -121,9 +124,9 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       while (atomicCAS(&hslot[q], 0xFFFFFFFFu, threadIdx.x) != 0xFFFFFFFFu) q = (q + 1) & (kHotSlots - 1);
     }
   }
-  const uint32_t sb_hot = sb_val + (MAPS ? (1u << map_bits) : 0u);
+  const uint32_t sb_hot = sb_val + (EXT && map_bits ? (1u << map_bits) : 0u);
   auto route = [&](uint32_t r, uint32_t f, uint64_t key) -> uint32_t {
-    if (MAPS && res_type[r] == CC_RES_MAP) {
+    if (EXT && res_type[r] == CC_RES_MAP) {
       const uint32_t kt = CC_FLAG_KTAG(f);
       const uint64_t h = map_hash(r, kt, key);
       if (nhot) {
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   // 0. histogram of the whole tile -> tile-local run starts (ttab row)
   for (uint32_t k = t; k < hw; k += kPT) ctot32[k] = 0;
   lds_barrier();
-  if (!MAPS) {
+  if (!EXT) {
     const uint64_t q1 = tile1 / 4;
 #pragma unroll 4
     for (uint64_t q = tile0 / 4 + t; q < q1; q += kPT) {
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   // commit (w, j, l) of a chunk is cbase + w*(64*J) + j*64 + l: log order = (w, j, l).
   // Prefetch in two stages so no wave stalls on the instance->resource gather right after its load:
   // raw columns of chunk c+1 are requested at the top of chunk c, their gathers after chunk c's ranking.
-  uint32_t res[J], meta[J], ninst[J], nmeta[J];
+  uint32_t res[J], meta[J], ninst[J], nmeta[J], xs[J], nxs[J];
   u64x2 ab[J], nab[J];
   uint64_t key[J], idx[J], nkey[J], nidx[J];
   auto load_raw = [&](uint64_t cbase, uint32_t (&in)[J], uint32_t (&mt)[J], u64x2 (&aa)[J], uint64_t (&kk)[J],
@@ -215,22 +218,42 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       }
     }
   };
-  // gathers: instance -> resource, and (maps only) the key, log index and ttl sign of map commits
-  auto gather = [&](uint64_t cbase, const uint32_t (&in)[J], uint32_t (&rr)[J], uint32_t (&mt)[J], uint64_t (&kk)[J],
-                    uint64_t (&ii)[J]) {
+  // gathers: instance -> resource; with extended staging (maps, coordination, value events) the log index and
+  // per type: map key + ttl sign; lock (clock at which due timeouts fire, timeout) + clock; others the key.
+  // xs = the record's extended slot word: the map slot for map commits, the instance slot otherwise.
+  auto gather = [&](uint64_t cbase, const uint32_t (&in)[J], uint32_t (&rr)[J], uint32_t (&mt)[J], u64x2 (&aa)[J],
+                    uint64_t (&kk)[J], uint64_t (&ii)[J], uint32_t (&xx)[J]) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       rr[j] = in[j] == kNoRes ? kNoRes : resolve(inst_res, max_inst, in[j]);
-      if (MAPS && rr[j] != kNoRes && res_type[rr[j]] == CC_RES_MAP) {
+      xx[j] = in[j];
+      if (EXT && rr[j] != kNoRes) {
+        const uint32_t ty = res_type[rr[j]];
         const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
-        kk[j] = ckey[i];
-        ii[j] = cidx ? cidx[i] : 0;
-        if (caux && (int64_t)caux[i] > 0) mt[j] |= kMetaTtl;
+        if (ty == CC_RES_MAP) {
+          kk[j] = ckey[i];
+          ii[j] = cidx ? cidx[i] : 0;
+          xx[j] = rr[j];
+          if (caux && (int64_t)caux[i] > 0) mt[j] |= kMetaTtl;
+        } else if (ty != CC_RES_VALUE || value_ext) {
+          ii[j] = cidx ? cidx[i] : 0;
+          if (ty == CC_RES_LOCK) {  // deterministic log clock (time is non-decreasing within a batch)
+            const uint64_t ti = ctime ? ctime[i] : 0;
+            const uint64_t clk = ti > cbase0 ? ti : cbase0;
+            uint64_t prev = cbase0;
+            if (i > 0 && ctime) prev = ctime[i - 1] > cbase0 ? ctime[i - 1] : cbase0;
+            aa[j].x = deferred ? prev : clk;
+            aa[j].y = caux ? caux[i] : 0;
+            kk[j] = clk;
+          } else {
+            kk[j] = ckey ? ckey[i] : 0;
+          }
+        }
       }
     }
   };
   load_raw(tile0, ninst, meta, ab, key, idx);
-  gather(tile0, ninst, res, meta, key, idx);
+  gather(tile0, ninst, res, meta, ab, key, idx, xs);
   for (uint32_t ch = 0; ch < kTile / C; ++ch) {
     const uint64_t cbase = tile0 + (uint64_t)ch * C;
     if (cbase >= hi) break;  // block-uniform
@@ -250,7 +273,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       loc[j] = live[j] ? (atomicAdd(&wc[w * hw + (sk[j] >> 1)], 1u << sh) >> sh) & 0xFFFF : 0;
     }
     uint32_t nres[J];
-    if (more) gather(cbase + C, ninst, nres, nmeta, nkey, nidx);
+    if (more) gather(cbase + C, ninst, nres, nmeta, nab, nkey, nidx, nxs);
     lds_barrier();
     // 2. per super-bucket: exclusive prefix over waves (packed halves) and chunk totals; chunk-sorted starts
     for (uint32_t kw = t; kw < hw; kw += kPT) {
@@ -288,8 +311,8 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       rab[s] = ab[j];
       rmeta[s] = meta[j] | ((res[j] & ((1u << kSbShift) - 1)) << 16);
       rsb[s] = (uint16_t)sk[j];
-      if (MAPS) {
-        rres[s] = res[j];
+      if (EXT) {
+        rres[s] = xs[j];
         rkey[s] = key[j];
         ridx[s] = idx[j];
       }
@@ -302,7 +325,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
       st_meta[g] = rmeta[s];
       st_ab[g] = rab[s];
-      if (MAPS && k >= sb_val) {
+      if (EXT) {
         st_res[g] = rres[s];
         st_key[g] = rkey[s];
         st_idx[g] = ridx[s];
@@ -318,6 +341,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
         ab[j] = nab[j];
         key[j] = nkey[j];
         idx[j] = nidx[j];
+        xs[j] = nxs[j];
       }
     }
   }
@@ -367,15 +391,15 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
 int launch_partition(const PartArgs& a, hipStream_t st) {
   const uint32_t tiles = (uint32_t)((a.hi - a.lo + kTile - 1) / kTile);
   if (tiles == 0) return 0;
-  const bool maps = a.map_bits != 0;
+  const bool ext = a.ext;
   a.mark(K_PART_TILE, 1, st);
-  if (maps)
+  if (ext)
     hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
                        a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   else
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
                        a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

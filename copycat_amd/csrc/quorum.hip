@@ -131,7 +131,14 @@ __global__ __launch_bounds__(256) void k_expire(const uint64_t* __restrict__ las
       c += (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1);
     }
   }
-  if (l == 0 && c) atomicAdd(count, (unsigned long long)c);
+  // one counter update per workgroup: thousands of same-address atomics would serialize at the L2
+  __shared__ uint32_t wc[4];
+  if (l == 0) wc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
+    if (tot) atomicAdd(count, (unsigned long long)tot);
+  }
 }
 
 static int grid_for(uint64_t work, int per_block) {
@@ -170,7 +177,7 @@ extern "C" int cc_expire_sweep(const uint64_t* d_last, uint64_t sessions, uint64
   if (!d_last || !d_bitmap || !d_count || (((uintptr_t)d_last) & 15)) return CC_ERR_INVALID;
   if (sessions == 0) return CC_OK;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_expire, dim3(grid_for((sessions + 127) / 128, 4)), dim3(256), 0, st, d_last, sessions, now,
+  hipLaunchKernelGGL(k_expire, dim3(grid_for((sessions + 127) / 128, 16)), dim3(256), 0, st, d_last, sessions, now,
                      (int64_t)timeout, d_bitmap, (unsigned long long*)d_count);
   return hipGetLastError() == hipSuccess ? CC_OK : CC_ERR_HIP;
 }

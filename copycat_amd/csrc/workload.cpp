@@ -181,6 +181,92 @@ uint64_t wl_map_random(uint64_t n, uint32_t maps, uint32_t first_inst, uint32_t 
   return n;
 }
 
+// Coordination parity stream: resources [0, R) with types types[r] (CC_RES_LOCK / ELECTION / GROUP / VALUE),
+// each with K instances: instance slot r*K + k (instance id 1000 + slot, set up by the caller).  Ops per type:
+// lock/unlock with timeouts {-1, 0, 1..40 ms}; listen/unlisten/isLeader; join/leave/execute(member = an
+// instance id of that group, callback = handle); value get/set/CAS/getAndSet/listen/unlisten.  Rare Delete,
+// ops of other types (UNKNOWN_OP) and unknown instance slots.  Time = 1 + index / 8 ms (non-decreasing).
+uint64_t wl_coord_random(uint64_t n, uint32_t R, uint32_t K, const uint8_t* types, uint32_t max_inst, uint64_t seed,
+                         uint32_t p_delete_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
+                         uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b, uint64_t* aux) {
+  SplitMix64 rng(seed);
+  // client model for locks (so a waiter queue never exceeds K): a holder unlocks, a waiter sends unlock (fails:
+  // not the holder), anyone else locks.  Tracks LockState exactly, timeouts included (either timer order:
+  // the model removes a waiter once its deadline has passed, before the instance's next request).
+  struct Waiter { uint32_t k; uint64_t deadline; };
+  std::vector<int32_t> holder(R, -1);
+  std::vector<std::vector<Waiter>> queue(R);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t r = (uint32_t)rng.below(R), k = (uint32_t)rng.below(K);
+    const uint64_t now = 1 + (index0 + i) / 8;
+    uint32_t s = r * K + k;
+    uint8_t o = 0, ta = 0, tb = 0;
+    uint64_t pa = 0, pb = 0, ky = 0, ax = 0;
+    const uint64_t u = rng.below(100);
+    switch (types[r]) {
+      case CC_RES_LOCK: {
+        auto& q = queue[r];
+        // waiters whose timeout passed are gone (conservatively: strictly before now, both timer orders agree)
+        q.erase(std::remove_if(q.begin(), q.end(), [&](const Waiter& w) { return w.deadline + 1 < now; }), q.end());
+        const bool waiting = std::any_of(q.begin(), q.end(), [&](const Waiter& w) { return w.k == k; });
+        if (holder[r] == (int32_t)k || waiting || u < 10) {
+          o = CC_OP_LOCK_UNLOCK;
+          if (holder[r] == (int32_t)k) {
+            if (q.empty()) holder[r] = -1;
+            else { holder[r] = (int32_t)q.front().k; q.erase(q.begin()); }
+          }
+        } else {
+          o = CC_OP_LOCK_LOCK;
+          const uint64_t v = rng.below(10);
+          ax = v < 6 ? (uint64_t)-1 : (v < 8 ? 0 : 1 + rng.below(40));
+          if (holder[r] < 0) holder[r] = (int32_t)k;
+          else if (ax != 0) q.push_back(Waiter{k, ax == (uint64_t)-1 ? ~0ull - 2 : now + ax});
+        }
+        break;
+      }
+      case CC_RES_ELECTION:
+        o = u < 45 ? CC_OP_ELECT_LISTEN : (u < 90 ? CC_OP_ELECT_UNLISTEN : CC_OP_ELECT_ISLEADER);
+        break;
+      case CC_RES_GROUP:
+        o = u < 45 ? CC_OP_GROUP_JOIN : (u < 85 ? CC_OP_GROUP_LEAVE : CC_OP_GROUP_EXECUTE);
+        if (o == CC_OP_GROUP_EXECUTE) {
+          ky = 1000 + r * K + rng.below(K);  // a member id of this group (maybe not joined)
+          ta = CC_TAG_HANDLE;
+          pa = rng.below(100);
+        }
+        break;
+      default: {  // value
+        static const uint8_t vops[] = {CC_OP_VALUE_GET, CC_OP_VALUE_SET, CC_OP_VALUE_CAS, CC_OP_VALUE_GETANDSET,
+                                       CC_OP_VALUE_LISTEN, CC_OP_VALUE_UNLISTEN, CC_OP_VALUE_CAS};
+        o = vops[rng.below(sizeof vops)];
+        ta = rng.below(4) ? CC_TAG_LONG : CC_TAG_NULL;
+        tb = rng.below(4) ? CC_TAG_LONG : CC_TAG_NULL;
+        pa = rng.below(3);
+        pb = rng.below(3);
+      }
+    }
+    const uint64_t x = rng.below(1000000);
+    if (types[r] != CC_RES_LOCK) {  // locks stay on the client model (Delete on a lock: KATs)
+      if (x < p_delete_ppm) o = CC_OP_DELETE;
+      else if (x < p_delete_ppm + 2000) {  // possibly another type's op (never schedule: not applied on the GPU)
+        o = (uint8_t)(50 + rng.below(80));
+        if (o == CC_OP_GROUP_SCHEDULE) o = CC_OP_GROUP_LEAVE;
+      }
+      else if (x < p_delete_ppm + 4000) s = max_inst + (uint32_t)rng.below(100);  // unknown instance slot
+    }
+    if (index) index[i] = index0 + i;
+    if (time) time[i] = now;
+    inst[i] = s;
+    op[i] = o;
+    flags[i] = CC_FLAGS(ta, tb, 0);
+    key[i] = ky;
+    a[i] = pa;
+    b[i] = pb;
+    if (aux) aux[i] = ax;
+  }
+  return n;
+}
+
 // Config 3 stream: DistributedMap put/get/remove (45/45/10) over `pairs` (power of two) distinct
 // (map, key) pairs spread over `maps` maps; pair rank ~ Zipf(s).  Rank r -> pair (r * 0x9E3779B1 + 0x7F4A7C15)
 // mod pairs (a bijection), pair -> map pair % maps (instance slot first_inst + map), key = mix64(pair) (Long).

@@ -54,6 +54,10 @@ def lib():
             "cc_applied_index": (i32, [P, P]),
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
             "cc_read_map_entries": (i32, [P, u32, u64, P, P, P, P, P, P]),
+            "cc_read_lock_state": (i32, [P, u32, P, P, P, u64, P, P, P]),
+            "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
+            "cc_read_group_members": (i32, [P, u32, u64, P, P]),
+            "cc_advance_time": (i32, [P, u64]),
             "cc_quorum_commit": (i32, [P, u32, u64, P, P, P, P]),
             "cc_expire_sweep": (i32, [P, u64, u64, u64, P, P, P]),
             "cc_profile_enable": (i32, [P, i32]),
@@ -117,6 +121,30 @@ class DeviceBatch:
         return s
 
 
+class DeviceEvents:
+    """An event stream in HBM (cc_events): columns of `capacity` rows + a device row counter."""
+
+    def __init__(self, capacity, device="cuda"):
+        self.capacity = capacity
+        self.pos = torch.zeros(capacity, dtype=torch.int32, device=device)
+        self.target = torch.zeros(capacity, dtype=torch.int32, device=device)
+        self.code = torch.zeros(capacity, dtype=torch.uint8, device=device)
+        self.src = torch.zeros(capacity, dtype=torch.uint8, device=device)
+        self.tag = torch.zeros(capacity, dtype=torch.uint8, device=device)
+        self.payload = torch.zeros(capacity, dtype=torch.int64, device=device)
+        self.count = torch.zeros(1, dtype=torch.int64, device=device)
+
+    def struct(self):
+        return abi.cc_events(self.pos.data_ptr(), self.target.data_ptr(), self.code.data_ptr(), self.src.data_ptr(),
+                             self.tag.data_ptr(), self.payload.data_ptr(), self.capacity, self.count.data_ptr())
+
+    def host(self):
+        m = min(int(self.count.item()), self.capacity)
+        return {"pos": self.pos[:m].cpu().numpy().view(np.uint32), "target": self.target[:m].cpu().numpy().view(np.uint32),
+                "code": self.code[:m].cpu().numpy(), "src": self.src[:m].cpu().numpy(), "tag": self.tag[:m].cpu().numpy(),
+                "payload": self.payload[:m].cpu().numpy().view(np.uint64), "count": int(self.count.item())}
+
+
 class Engine:
     def __init__(self, max_resources, max_instances, max_batch, device=0, flags=abi.CC_CFG_TIMERS_DEFERRED,
                  sub_batch=0, max_events=0, map_capacity=0):
@@ -171,6 +199,25 @@ class Engine:
         r = abi.cc_results(status.data_ptr(), value.data_ptr())
         _check(self.L.cc_apply_batch(self.h, C.byref(s), db.n, C.byref(r), None, _stream_ptr(stream)))
 
+    def apply_events(self, db: DeviceBatch, status, value, events: "DeviceEvents", stream=None):
+        """apply() with an event stream (device tensors, see DeviceEvents)."""
+        s = db.struct()
+        r = abi.cc_results(status.data_ptr(), value.data_ptr())
+        ev = events.struct()
+        _check(self.L.cc_apply_batch(self.h, C.byref(s), db.n, C.byref(r), C.byref(ev), _stream_ptr(stream)))
+
+    def apply_host_events(self, b: Batch, capacity=None, device="cuda"):
+        """Host batch -> (status, value, events) through the device path with an event stream; events is a dict of
+        numpy columns (pos, target, code, src, tag, payload) in stream order (log row, then publish order)."""
+        n = len(b)
+        db = DeviceBatch.upload(b, device=device)
+        status = torch.zeros(n, dtype=torch.uint8, device=device)
+        value = torch.zeros(n, dtype=torch.int64, device=device)
+        evs = DeviceEvents(capacity if capacity is not None else max(4 * n, 1024), device=device)
+        self.apply_events(db, status, value, evs)
+        self.sync()
+        return status.cpu().numpy(), value.cpu().numpy().view(np.uint64), evs.host()
+
     def apply_host(self, b: Batch):
         """PCIe-inclusive path: host columns in, host results out (H2D + apply + D2H + sync)."""
         n = len(b)
@@ -213,6 +260,31 @@ class Engine:
         tag, val, cur = np.zeros(count, np.uint8), np.zeros(count, np.uint64), np.zeros(count, np.uint8)
         _check(self.L.cc_read_value_state(self.h, first, count, _np(tag), _np(val), _np(cur)))
         return tag, val, cur
+
+    def advance_time(self, now):
+        _check(self.L.cc_advance_time(self.h, now))
+
+    def lock_state(self, slot, cap=1024):
+        """(holder instance slot or -1, holder index, holder cleaned, [(waiter instance slot, index)])"""
+        h, hi, hc, n = C.c_int64(), C.c_uint64(), C.c_uint8(), C.c_uint64()
+        qi, qx = np.zeros(cap, np.uint32), np.zeros(cap, np.uint64)
+        _check(self.L.cc_read_lock_state(self.h, slot, C.byref(h), C.byref(hi), C.byref(hc), cap, C.byref(n), _np(qi),
+                                         _np(qx)))
+        m = min(n.value, cap)
+        return h.value, hi.value, hc.value, list(zip(qi[:m].tolist(), qx[:m].tolist()))
+
+    def election_state(self, slot, cap=1024):
+        """(leader instance slot or -1, leader index, [(listener instance slot, index)])"""
+        ld, li, n = C.c_int64(), C.c_uint64(), C.c_uint64()
+        qi, qx = np.zeros(cap, np.uint32), np.zeros(cap, np.uint64)
+        _check(self.L.cc_read_election_state(self.h, slot, C.byref(ld), C.byref(li), cap, C.byref(n), _np(qi), _np(qx)))
+        m = min(n.value, cap)
+        return ld.value, li.value, list(zip(qi[:m].tolist(), qx[:m].tolist()))
+
+    def group_members(self, slot, cap=4096):
+        ids, n = np.zeros(cap, np.uint64), C.c_uint64()
+        _check(self.L.cc_read_group_members(self.h, slot, cap, C.byref(n), _np(ids)))
+        return ids[:min(n.value, cap)].tolist()
 
     def map_entries(self, slot):
         """MapState entries of one map slot sorted by (key tag, key): (key_tag, key, value_tag, value, commit_index)

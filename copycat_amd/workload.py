@@ -29,6 +29,8 @@ def lib():
         L.wl_value_random.argtypes = [u64, u32, u32, u32, u64, u32, u32, u64] + [P] * 7
         L.wl_map_random.restype = u64
         L.wl_map_random.argtypes = [u64, u32, u32, u32, u32, u64, u32, u32, u64] + [P] * 9 + [u32]
+        L.wl_coord_random.restype = u64
+        L.wl_coord_random.argtypes = [u64, u32, u32, P, u32, u64, u32, u64] + [P] * 9
         L.wl_map_zipf.restype = u64
         L.wl_map_zipf.argtypes = [u64, u64, u32, u32, C.c_double, u32, u64, u32] + [P] * 8
         _LIB = L
@@ -67,6 +69,15 @@ def map_random_stream(n, maps, max_inst, keys=64, first_inst=0, seed=1, hot=0, p
     lib().wl_map_random(n, maps, first_inst, max_inst, keys, seed, hot, int(p_hot * 1e6), index0, _p(b.index),
                         _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.key), _p(b.a), _p(b.b), _p(b.aux),
                         1 if value_compare_ops else 0)
+    return b
+
+
+def coord_random_stream(n, types, K, max_inst, seed=1, p_delete=0.0005, index0=1):
+    """Coordination parity stream over resources with types[r]; resource r owns instance slots r*K + k."""
+    types = np.ascontiguousarray(types, np.uint8)
+    b = Batch(n)
+    lib().wl_coord_random(n, len(types), K, _p(types), max_inst, seed, int(p_delete * 1e6), index0, _p(b.index),
+                          _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.key), _p(b.a), _p(b.b), _p(b.aux))
     return b
 
 

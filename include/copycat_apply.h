@@ -127,11 +127,14 @@ extern "C" {
 #define CC_EV_JOIN     4  /* MembershipGroupState "join"(instance) :55 */
 #define CC_EV_LEAVE    5  /* MembershipGroupState "leave"(instance) :40,75 */
 #define CC_EV_EXECUTE  6  /* MembershipGroupState "execute"(callback) :95,115 */
+#define CC_EV_MEMBER   7  /* not an event: one row per member of a join's Set<Long> result (ascending ids,
+                             target = the joining instance, src CC_EVSRC_RESULT) MembershipGroupState.java:63 */
 
 /* event source */
 #define CC_EVSRC_COMMIT 0  /* published while applying commit `pos` */
 #define CC_EVSRC_TIMER  1  /* published by a timer that fired at commit `pos` */
 #define CC_EVSRC_CLOSE  2  /* published by a session close/expire fan-out */
+#define CC_EVSRC_RESULT 3  /* a variable-length result row (CC_EV_MEMBER) */
 
 /* ---- engine configuration ------------------------------------------------------------------------ */
 typedef struct cc_config {
@@ -150,6 +153,17 @@ typedef struct cc_config {
 
 #define CC_CFG_TIMERS_DEFERRED 1u  /* manager-mode timer order (A8): due timers fire after the commit
                                       that advanced time (ResourceManagerStateMachineExecutor.java:104-109) */
+#define CC_CFG_VALUE_EVENTS    2u  /* AtomicValue Listen/Unlisten + "change" events on the GPU (every value
+                                      resource then runs on the event-capable kernel)              */
+
+/* Coordination resources (lock / election / group) keep their variable-size state in fixed per-resource
+ * blocks: at most CC_LOCK_QUEUE waiters per lock, CC_ELECTION_LISTENERS listeners per election,
+ * CC_GROUP_MEMBERS members per group, CC_VALUE_LISTENERS listeners per value (CC_ERR_CAPACITY beyond).
+ * The time column must be non-decreasing within a batch when lock timeouts are used (Raft log time).   */
+#define CC_LOCK_QUEUE          64
+#define CC_ELECTION_LISTENERS  64
+#define CC_GROUP_MEMBERS       64
+#define CC_VALUE_LISTENERS     64
 
 /* ---- one batch of committed entries, SoA, log order ------------------------------------------------
  * Row i is InstanceCommand/InstanceQuery{instance, op} of log entry index[i]
@@ -202,7 +216,7 @@ void* cc_engine_stream(cc_engine* e);
  * New resource: ResourceManager.getResource/createResource new-key branch (ResourceManager.java:84-100,157-176);
  * the engine allocates state for `slot` (chosen by the host: resource id -> dense slot).       */
 int  cc_resource_create(cc_engine* e, uint32_t slot, uint32_t type);
-/* Bulk form: slots [first, first+count) all of `type`.  A 64-slot bucket (slot/64) holds one type. */
+/* Bulk form: slots [first, first+count) all of `type`. */
 int  cc_resource_create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type);
 /* ResourceManager.deleteResource (ResourceManager.java:212-235): delete() state, cancel timers,
  * and close every instance slot registered to the resource.                                   */
@@ -235,10 +249,24 @@ int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* 
 int  cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag, uint64_t* h_key,
                          uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index);
 
+/* LockState (LockState.java:33-36) after the timers due at the engine clock: holder instance slot (-1 none),
+ * its commit index and cleaned flag; *count = queued waiters, the first min(cap, count) to the arrays. */
+int  cc_read_lock_state(cc_engine* e, uint32_t slot, int64_t* holder, uint64_t* holder_index, uint8_t* holder_cleaned,
+                        uint64_t cap, uint64_t* count, uint32_t* h_queue_inst, uint64_t* h_queue_index);
+/* LeaderElectionState (LeaderElectionState.java:31-33): leader instance slot (-1 none) + index, listeners in
+ * insertion order. */
+int  cc_read_election_state(cc_engine* e, uint32_t slot, int64_t* leader, uint64_t* leader_index, uint64_t cap,
+                            uint64_t* count, uint32_t* h_listener_inst, uint64_t* h_listener_index);
+/* MembershipGroupState.members (MembershipGroupState.java:33): member instance ids, ascending. */
+int  cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint64_t* h_ids);
+/* Log time advanced without a commit (ResourceManagerStateMachineExecutor timers): due lock
+ * timeouts take effect (they publish nothing, LockState.java:54-58). */
+int  cc_advance_time(cc_engine* e, uint64_t now);
+
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
  * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute, 3 k_apply_map, 4 k_map_hot (hot-key lists +
- * scan, apply_map_hot.hip).                                                                                 */
-#define CC_PROFILE_KERNELS 5
+ * scan, apply_map_hot.hip), 5 k_apply_coord (coordination + value events), 6 k_events (event scan+scatter). */
+#define CC_PROFILE_KERNELS 7
 int  cc_profile_enable(cc_engine* e, int on);
 int  cc_profile_reset(cc_engine* e);
 /* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */

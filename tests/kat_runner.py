@@ -48,26 +48,31 @@ def op_code(name):
     return getattr(abi, f"CC_OP_{name}")
 
 
-GPU_VALUE_OPS = {"VALUE_GET", "VALUE_SET", "VALUE_CAS", "VALUE_GETANDSET"}
+GPU_VALUE_OPS = {"VALUE_GET", "VALUE_SET", "VALUE_CAS", "VALUE_GETANDSET", "VALUE_LISTEN", "VALUE_UNLISTEN"}
+GPU_COORD_OPS = {"LOCK_LOCK", "LOCK_UNLOCK", "ELECT_LISTEN", "ELECT_UNLISTEN", "ELECT_ISLEADER", "GROUP_JOIN",
+                 "GROUP_LEAVE", "GROUP_EXECUTE"}
 GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_GETORDEFAULT", "MAP_REMOVE",
                "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT"}
 
 
 def gpu_eligible(kat):
-    """KATs whose every step this build applies on the GPU: AtomicValue get/set/CAS/getAndSet/Delete and Map key
-    ops without ttl, no registry control, clock or close steps."""
+    """KATs whose every step this build applies on the GPU: AtomicValue ops (listeners with CC_CFG_VALUE_EVENTS),
+    Map key ops without ttl, lock / election / group ops except schedule, Delete on every type but maps, and
+    clock advances; no registry control or session-close steps (host control plane)."""
     types = {r[1] for r in kat["resources"]}
-    if not types <= {"VALUE", "MAP"}:
+    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP"}:
         return False
     for s in kat["steps"]:
-        if "control" in s or "close" in s or "advance" in s:
+        if "control" in s or "close" in s:
             return False
         if "commit" in s:
             c = s["commit"]
             if c["op"] == "DELETE":
-                if types != {"VALUE"}:
+                if "MAP" in types:
                     return False
-            elif c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS or c.get("aux", 0) > 0:
+            elif c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS:
+                return False
+            elif c["op"].startswith("MAP_") and c.get("aux", 0) > 0:
                 return False
     return True
 
@@ -254,29 +259,53 @@ class OracleBackend:
 
 
 class EngineBackend:
-    """GPU engine backend (the GPU-applied subset of this build: see gpu_eligible)."""
+    """GPU engine backend (the GPU-applied subset of this build: see gpu_eligible).  Batches go through the
+    device path with an event stream; join's member-set rows (CC_EV_MEMBER) are the aux results."""
 
     def __init__(self, kat, max_resources=256, max_instances=64):
         from copycat_amd.engine import Engine
 
-        self.E = Engine(max_resources, max_instances, 4096, map_capacity=4096)
+        flags = abi.CC_CFG_VALUE_EVENTS
+        if kat.get("timer_mode", "deferred") == "deferred":
+            flags |= abi.CC_CFG_TIMERS_DEFERRED
+        self.E = Engine(max_resources, max_instances, 4096, map_capacity=4096, flags=flags, max_events=1 << 16)
+        self.ids = {}
 
     def resource_create(self, slot, t):
         self.E.resource_create(slot, t)
 
     def instance_open(self, inst, res, iid, client):
         self.E.instance_open(inst, res, iid, client)
+        self.ids[iid] = inst
+
+    def inst_slot_of(self, iid):
+        return self.ids.get(iid, -1)
 
     def apply(self, b):
-        s, v = self.E.apply_host(b)
-        return s, v, [], []
+        s, v, ev = self.E.apply_host_events(b)
+        evs, aux = [], []
+        for i in range(len(ev["pos"])):
+            row = (int(ev["pos"][i]), int(ev["target"][i]), int(ev["code"][i]), int(ev["tag"][i]), int(ev["payload"][i]))
+            if row[2] == abi.CC_EV_MEMBER:
+                aux.append((row[0], row[4]))
+            else:
+                evs.append(row)
+        return s, v, evs, aux
 
     def advance(self, now):
+        self.E.advance_time(now)
         return []
 
     def value_state(self, res):
         t, v, c = self.E.value_state(res, 1)
         return int(t[0]), int(v[0]), int(c[0])
+
+    def lock_state(self, res):
+        h, _, _, q = self.E.lock_state(res)
+        return (None if h < 0 else h), [x[0] for x in q]
+
+    def group_members(self, res):
+        return self.E.group_members(res)
 
 
 def all_kats():

@@ -1,0 +1,175 @@
+"""GPU parity: LockState / LeaderElectionState / MembershipGroupState and AtomicValue listeners on the MI355X vs
+the CPU oracle, through the C-ABI device path with an event stream.
+
+Bar: bit-exact per-commit status/value; the published events (pos, src, target, code, tag, payload) as the
+same multiset per commit (each commit publishes at most one event per target, so this also fixes per-target
+order); join's member sets; final lock holders/queues, election leaders/listeners, group members and value
+state; the applied index."""
+import numpy as np
+import pytest
+
+from copycat_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+L, E_, G, V = abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP, abi.CC_RES_VALUE
+
+
+def _setup(types, K, flags, sub_batch=0, max_batch=1 << 20, max_events=1 << 22):
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+
+    R = len(types)
+    max_inst = R * K + 8
+    E = Engine(R, max_inst, max_batch, flags=flags, sub_batch=sub_batch, max_events=max_events)
+    O = Oracle(R, max_inst, flags & abi.CC_CFG_TIMERS_DEFERRED)
+    for r, t in enumerate(types):
+        E.resource_create(r, int(t))
+        O.resource_create(r, int(t))
+        for k in range(K):
+            E.instance_open(r * K + k, r, 1000 + r * K + k, 7 + k)
+            O.instance_open(r * K + k, r, 1000 + r * K + k, 7 + k)
+    return E, O, max_inst
+
+
+def _oracle_events(O):
+    e = O.take_events()
+    pos, mem = O.take_aux()
+    return e, pos, mem
+
+
+def _canon(pos, src, target, code, tag, payload):
+    rows = list(zip(pos.tolist(), src.tolist(), target.tolist(), code.tolist(), tag.tolist(), payload.tolist()))
+    return sorted(rows)
+
+
+def _check_batch(E, O, b):
+    s, v, ev = E.apply_host_events(b, capacity=max(8 * len(b), 1024))
+    s2, v2 = O.apply(b)
+    bad = np.nonzero((s != s2) | (v != v2))[0]
+    assert len(bad) == 0, (f"{len(bad)} rows differ; first {bad[:5]}: ops {b.op[bad[:5]]} gpu {s[bad[:5]]},{v[bad[:5]]} "
+                           f"oracle {s2[bad[:5]]},{v2[bad[:5]]}")
+    oe, apos, amem = _oracle_events(O)
+    member = ev["code"] == abi.CC_EV_MEMBER
+    got = _canon(*(ev[k][~member] for k in ("pos", "src", "target", "code", "tag", "payload")))
+    want = _canon(oe["pos"], oe["src"], oe["target"], oe["code"], oe["tag"], oe["payload"])
+    assert len(got) == len(want), f"{len(got)} events vs oracle {len(want)}"
+    assert got == want, next(((i, g, w) for i, (g, w) in enumerate(zip(got, want)) if g != w), None)
+    # join results: the member rows, per join, ascending ids (== the oracle's aux stream)
+    gm = list(zip(ev["pos"][member].tolist(), ev["payload"][member].tolist()))
+    assert gm == list(zip(apos.tolist(), amem.tolist()))
+    # the stream is ordered by log row
+    assert np.all(np.diff(ev["pos"].astype(np.int64)) >= 0)
+
+
+def _check_state(E, O, types):
+    for r, t in enumerate(types):
+        if t == L:
+            h, hi, hc, q = E.lock_state(r)
+            oh, ohi, ohc, oq = O.lock_state(r)
+            assert (h, hc, q) == (oh, ohc, oq), (r, (h, hc, q), (oh, ohc, oq))
+            if h >= 0:
+                assert hi == ohi
+        elif t == E_:
+            assert E.election_state(r) == O.election_state(r), r
+        elif t == G:
+            assert E.group_members(r) == O.group_members(r), r
+    vals = [r for r, t in enumerate(types) if t == V]
+    for r in vals:
+        assert tuple(int(x[0]) for x in E.value_state(r, 1)) == tuple(int(x[0]) for x in O.value_state(r, 1)), r
+    assert E.applied_index() == O.applied_index()
+
+
+FLAGS = abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_EVENTS
+
+
+@pytest.mark.parametrize("n,R,K,seed,flags", [
+    (1, 4, 2, 1, FLAGS),
+    (500, 8, 3, 2, FLAGS),
+    (20_000, 16, 6, 3, FLAGS),                                  # long per-resource chains
+    (20_000, 16, 6, 4, abi.CC_CFG_VALUE_EVENTS),                # module-mode timer order (A8)
+    (300_000, 1024, 4, 5, FLAGS),                               # many super-buckets; ragged tail
+    (200_000, 600, 8, 6, FLAGS),
+])
+def test_coord_random_parity(n, R, K, seed, flags):
+    from copycat_amd.workload import coord_random_stream
+
+    types = np.array([L, E_, G, V] * ((R + 3) // 4), np.uint8)[:R]
+    E, O, max_inst = _setup(types, K, flags)
+    b = coord_random_stream(n, types, K, max_inst, seed=seed)
+    _check_batch(E, O, b)
+    _check_state(E, O, types)
+
+
+def test_coord_sub_batches_batches_and_clock():
+    """State and the log clock carried across sub-batches and calls; advance_time expires lock waiters."""
+    from copycat_amd.workload import coord_random_stream
+
+    types = np.array([L, L, E_, G, V, L] * 20, np.uint8)
+    K = 5
+    E, O, max_inst = _setup(types, K, FLAGS, sub_batch=16384)
+    b = coord_random_stream(90_000, types, K, max_inst, seed=9)
+    for lo, hi in [(0, 1), (1, 30_000), (30_000, 30_000), (30_000, 90_000)]:
+        _check_batch(E, O, b.slice(lo, hi))
+    _check_state(E, O, types)
+    E.advance_time(int(b.time[-1]) + 1000)
+    O.advance_time(int(b.time[-1]) + 1000)
+    O.take_events()
+    _check_state(E, O, types)
+
+
+def _one(op, inst, aux=0, time=1, index=1, key=0, a=0, flags=0):
+    from copycat_amd.batch import Batch
+
+    return Batch.from_columns(index=[index], time=[time], inst=[inst], op=np.array([op], np.uint8),
+                              flags=np.array([flags], np.uint8), key=[key], a=[a], aux=[aux])
+
+
+def test_lock_queue_capacity_fails_loudly():
+    from copycat_amd.batch import Batch
+    from copycat_amd.engine import EngineError
+
+    K = abi.CC_LOCK_QUEUE + 2
+    E, O, max_inst = _setup(np.array([L], np.uint8), K, FLAGS)
+    n = K
+    b = Batch.from_columns(index=np.arange(1, n + 1), time=np.ones(n), inst=np.arange(n),
+                           op=np.full(n, abi.CC_OP_LOCK_LOCK, np.uint8), aux=np.full(n, 2**64 - 1, np.uint64))
+    with pytest.raises(EngineError) as ei:
+        E.apply_host_events(b)
+    assert ei.value.rc == abi.CC_ERR_CAPACITY
+
+
+def test_events_without_stream_and_schedule_fail_loudly():
+    from copycat_amd.engine import EngineError
+
+    E, O, _ = _setup(np.array([L, G], np.uint8), 2, FLAGS)
+    with pytest.raises(EngineError) as ei:  # the lock event has nowhere to go
+        E.apply_host(_one(abi.CC_OP_LOCK_LOCK, 0))
+    assert ei.value.rc == abi.CC_ERR_UNSUPPORTED
+    with pytest.raises(EngineError) as ei:
+        E.apply_host_events(_one(abi.CC_OP_GROUP_SCHEDULE, 2, aux=10, index=2))
+    assert ei.value.rc == abi.CC_ERR_UNSUPPORTED
+
+
+def test_time_must_not_decrease():
+    from copycat_amd.batch import Batch
+    from copycat_amd.engine import EngineError
+
+    E, O, _ = _setup(np.array([L], np.uint8), 2, FLAGS)
+    b = Batch.from_columns(index=[1, 2], time=[10, 5], inst=[0, 1], op=np.array([115, 115], np.uint8),
+                           aux=[5, 5])
+    with pytest.raises(EngineError) as ei:
+        E.apply_host_events(b)
+    assert ei.value.rc == abi.CC_ERR_INVALID
+
+
+def test_event_stream_capacity():
+    from copycat_amd.engine import EngineError
+    from copycat_amd.workload import coord_random_stream
+
+    types = np.array([G] * 8, np.uint8)
+    E, O, max_inst = _setup(types, 8, FLAGS)
+    b = coord_random_stream(5000, types, 8, max_inst, seed=12)
+    with pytest.raises(EngineError) as ei:
+        E.apply_host_events(b, capacity=100)
+    assert ei.value.rc == abi.CC_ERR_CAPACITY

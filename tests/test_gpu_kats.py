@@ -11,8 +11,10 @@ KATS = [k for k in all_kats() if gpu_eligible(k)]
 
 def test_gpu_kat_coverage():
     names = {k["name"] for k in KATS}
-    assert {"map_put_get_remove", "map_put_if_absent", "A1_replace_if_present_inverts_args"} <= names
-    assert len(KATS) >= 8
+    assert {"map_put_get_remove", "map_put_if_absent", "A1_replace_if_present_inverts_args", "lock_unlock",
+            "election_elect", "group_join", "group_leave", "A7_trylock_timeout_is_silent",
+            "lock_delete_then_unlock_commit_closed", "A9_leader_relisten_appended"} <= names
+    assert len(KATS) >= 25
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
