@@ -1,113 +1,103 @@
 // apply_value.hip — AtomicValueState apply (also DistributedAtomicLong, whose add is a client-side CAS loop).
 //
-// One 256-thread workgroup owns one super-bucket = 256 AtomicValueState instances: thread t holds slot t's
-// state in registers for the whole launch.  It walks the super-bucket's staging list (its run in every tile,
-// tile order = log order; built by partition.hip) in chunks of 2048 records, prefetching the next chunk into registers while it resolves the
-// current one: a stable counting sort of the chunk by slot (ballot ranking + per-slot prefix sums in LDS)
-// gives every slot its commits in log order, and each thread applies its slot's chain sequentially — the
-// same order the reference's single state-machine thread would (ResourceManager.java:56-72).  Results are
-// staged in LDS and written back to the records' staging positions; k_unpermute returns them to log order.
+// One 1024-thread workgroup owns one super-bucket = 256 AtomicValueState instances: thread t < 256 holds slot
+// t's state in registers for the whole launch.  The workgroup walks the super-bucket's staging list (its run
+// in every tile, tile order = log order; built by partition.hip) in chunks of 4096 records:
+//   1. all 16 waves load the chunk (the next chunk's loads are in flight while the current one is resolved)
+//      and sort it stably by slot: ranking inside each wave with LDS atomics with return (same-address lanes
+//      of one instruction resolve in lane order on gfx950 — checked at engine start), per-wave prefixes per
+//      slot, a scan over the 256 slots;
+//   2. threads 0..255 each apply their slot's commits sequentially, in log order — the same order the
+//      reference's single state-machine thread would (ResourceManager.java:56-72);
+//   3. results go back to the records' staging positions; k_unpermute returns them to log order.
 //
+// The partition encodes every value record for this walk (common.h value_encode): the op becomes flag bits
+// plus the precomputed status byte, the operands the canonical compare value and the canonical new value.
 // Per-op semantics restate AtomicValueState (atomic/src/main/java/io/atomix/atomic/state/AtomicValueState.java):
 //   get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144, delete :146-157.
 // `ttl` is never serialized for these commands (AtomicValueCommands.java:125-133,181-191,227-235),
-// so no TTL timer can exist.  Listen/Unlisten (:41-63) publish events: not applied by this build (flagged).
+// so no TTL timer can exist.  Listen/Unlisten (:41-63) publish events: applied by apply_coord.hip under
+// CC_CFG_VALUE_EVENTS, flagged as unsupported here.
 #include "common.h"
 #include "engine_internal.h"
 
 namespace cc {
 
-struct ValState {
-  uint32_t meta;  // tag | has_current << 8
-  uint64_t v;
-};
+constexpr int kVT = 1024;                  // threads per workgroup (16 waves)
+constexpr int kVW = kVT / kWave;
+constexpr int kVPer = 4;                   // records per thread per chunk
+constexpr int kVCh = kVT * kVPer;          // 4096 records per chunk
+constexpr int kVWaveRecs = kWave * kVPer;  // records of a chunk per wave (contiguous in log order)
+constexpr int kVSlots = 1 << kSbShift;     // 256 slots per super-bucket
+constexpr int kVPairs = kVSlots / 2;       // per-wave slot counters: packed u16 pairs
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 
-// Applies one committed AtomicValue op to the state; returns the status byte, result payload in rv.
-// Branch-free (selects only): a wave's lanes carry different ops, and a switch would run every case.
-__device__ inline uint32_t value_apply(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, ValState& s, uint64_t& rv,
-                                       uint32_t& err) {
-  const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
-  const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
-  const uint32_t tag = s.meta & 0xFF, cur = (s.meta >> 8) & 1;
-  const bool is_get = op == CC_OP_VALUE_GET;        // get :77-83   return current != null ? value : null
-  const bool is_set = op == CC_OP_VALUE_SET;        // set :114-118 value = v
-  const bool is_cas = op == CC_OP_VALUE_CAS;        // compareAndSet :123-133
-  const bool is_gas = op == CC_OP_VALUE_GETANDSET;  // getAndSet :138-144 result = old value
-  const bool is_del = op == CC_OP_DELETE;           // delete :146-157 (current != null) -> value = current = null
-  const bool is_lis = op == CC_OP_VALUE_LISTEN || op == CC_OP_VALUE_UNLISTEN;
-  // (value == null && expect == null) || (value != null && expect != null && value.equals(expect))
-  const bool eq = (tag == CC_TAG_NULL && ta == CC_TAG_NULL) || (tag != CC_TAG_NULL && tag == ta && s.v == pa);
-  const bool write = is_set || is_gas || (is_cas && eq);
-  const bool clear = is_del && cur;
-  // result
-  uint32_t rtag = CC_TAG_NULL;
-  rv = 0;
-  if ((is_get && cur) || is_gas) { rtag = tag; rv = s.v; }
-  if (is_cas) { rtag = CC_TAG_BOOL; rv = eq ? 1 : 0; }
-  const bool known = is_get || is_set || is_cas || is_gas || is_del || is_lis;
-  if (is_lis) err |= kErrUnsupported;
-  // state
-  const uint32_t ntag = is_cas ? tb : ta;
-  const uint64_t nv = is_cas ? pb : pa;
-  s.meta = write ? vmeta(ntag, 1) : (clear ? 0u : s.meta);
-  s.v = write ? nv : (clear ? 0ull : s.v);
-  // IllegalStateException "unknown operation type" (ResourceStateMachineExecutor.java:78)
-  return known ? CC_STATUS(CC_ST_OK, rtag) : CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
+// One step of a slot's chain.  State: ms = tag | has_current << 8, v = payload (0 when the tag is NULL: every
+// write stores a canonical payload and delete clears both, so current == null implies value == null, and get's
+// `current != null ? value : null` is the value itself).  Returns the status byte; rv = result payload.
+__device__ inline uint32_t value_walk(uint32_t m, uint64_t x, uint64_t y, uint32_t& ms, uint64_t& v, uint64_t& rv) {
+  const uint32_t tag = ms & 0xFFu;
+  // compareAndSet :124 (value == null && expect == null) || (value != null && value.equals(expect))
+  const bool eq = vrec_ctag(m) == tag && v == x;
+  const bool is_c = (m & kVrC) != 0, is_r = (m & kVrR) != 0, is_d = (m & kVrD) != 0;
+  const bool w = (m & kVrW) != 0 || (is_c && eq);
+  rv = is_r ? v : ((is_c && eq) ? 1ull : 0ull);
+  const uint32_t st = is_r ? (tag << 4) : (m & 0xFFu);
+  ms = w ? (vrec_ntag(m) | 0x100u) : (is_d ? 0u : ms);
+  v = w ? y : (is_d ? 0ull : v);
+  return st;
 }
 
-constexpr int kAT = kApplyWaves * kWave;  // 256 threads = 256 slots of the super-bucket
-constexpr int kACh = kAT * kApplyPer;     // 2048 records per chunk
-constexpr int kSbSlots = kApplyWaves * kLaneRes;
-constexpr int kWaveRecs = kWave * kApplyPer;  // records of a chunk per wave (contiguous)
+// Largest r in [0, tiles) with rpre[r] <= c (rpre non-decreasing, rpre[0] = 0): a two-round 64-ary search by
+// the whole wave (c is wave-uniform; every lane must be active).  Record c lies in run r when c < rpre[tiles].
+__device__ inline uint32_t find_run(const uint32_t* rpre, uint32_t tiles, uint32_t c) {
+  const uint32_t l = __lane_id();
+  const uint32_t step = (tiles + kWave - 1) / kWave;
+  uint32_t cand = l * step;
+  uint64_t b = __ballot(cand < tiles && rpre[cand] <= c);
+  const uint32_t base = (uint32_t)(63 - __clzll((long long)b)) * step;
+  cand = base + l;
+  b = __ballot(l < step && cand < tiles && rpre[cand] <= c);
+  return base + (uint32_t)(63 - __clzll((long long)b));
+}
 
-// One workgroup per super-bucket; thread t owns slot t (its AtomicValueState lives in two registers).
-// Per chunk of 2048 staging records (wave w holds records w*512 + j*64 + lane, so log order = (w, j, lane)):
-//   1. a stable counting sort of the chunk by slot: each wave ranks its records with LDS atomics with return
-//      on its own 256-counter table (same-address lanes resolve in lane order on gfx950, and the wave's
-//      instructions are in program order), the owner of each slot prefixes the 4 wave counts, a block scan
-//      gives each slot's run start;
-//   2. thread t walks its slot's run sequentially — the reference's one-commit-at-a-time order, per slot;
-//   3. results go back through LDS to staging order and out contiguously.
-__global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
+__global__ __launch_bounds__(kVT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
                                                     const uint16_t* __restrict__ ttab, uint32_t tiles, uint32_t sb,
                                                     const uint8_t* __restrict__ sb_kind,
                                                     uint32_t* __restrict__ val_meta, uint64_t* __restrict__ val_v,
                                                     uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                     uint32_t* __restrict__ err_out) {
-  __shared__ u64x2 sab[kACh];
-  __shared__ uint32_t sm[kACh];
-  __shared__ uint16_t sidx[kACh];
-  __shared__ uint64_t rval[kACh];
-  __shared__ uint8_t rstat[kACh];
-  __shared__ uint32_t wcnt[kApplyWaves][kSbSlots];  // per-wave slot counts (zeroed after use)
-  __shared__ uint32_t wpre[kApplyWaves][kSbSlots];  // per-wave slot prefixes
-  __shared__ uint32_t sstart[kSbSlots];
-  __shared__ uint32_t wsum[kApplyWaves];
-  __shared__ uint32_t rstart[kMaxTiles];     // staging position of this super-bucket's run in tile t
-  __shared__ uint32_t rpre[kMaxTiles + 1];   // records of this super-bucket before tile t
+  __shared__ u64x2 sab[kVCh];                  // the chunk sorted by slot
+  __shared__ uint32_t sm[kVCh];
+  __shared__ uint64_t rval[kVCh];              // results, sorted order
+  __shared__ uint8_t rstat[kVCh];
+  __shared__ uint32_t wcnt[kVW][kVPairs];      // per-wave slot counts -> per-wave exclusive prefixes (u16 pairs)
+  __shared__ uint32_t qsum[kVW / 2][kVPairs];  // counts of wave pairs
+  __shared__ uint32_t ctot[kVPairs];           // slot totals of the chunk (u16 pairs)
+  __shared__ uint32_t sstart[kVSlots];
+  __shared__ uint32_t wsum[kVW];
+  __shared__ uint32_t rstart[kMaxTiles];       // staging position of this super-bucket's run in tile t
+  __shared__ uint32_t rpre[kMaxTiles + 1];     // records of this super-bucket before tile t
 
   const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
   if (sb_kind && sb_kind[s]) return;  // holds coordination resources / value events: k_apply_coord
-  ValState st_reg{val_meta[(uint64_t)s * kSbSlots + t], val_v[(uint64_t)s * kSbSlots + t]};
-#pragma unroll
-  for (int q = 0; q < kApplyWaves; ++q) wcnt[q][t] = 0;
+  uint32_t ms = 0;
+  uint64_t sv = 0;
+  if (t < (uint32_t)kVSlots) {
+    ms = val_meta[(uint64_t)s * kVSlots + t];
+    sv = val_v[(uint64_t)s * kVSlots + t];
+  }
+  for (uint32_t k = t; k < (uint32_t)(kVW * kVPairs); k += kVT) (&wcnt[0][0])[k] = 0;
   // the super-bucket's list = its run in every tile, in tile order (tile-local layout of partition.hip)
   {
-    constexpr int PT = kMaxTiles / kAT;  // tiles per thread
-    uint32_t len[PT], sum = 0;
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t tt = t * PT + k;
-      len[k] = 0;
-      if (tt < tiles) {
-        const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
-        const uint32_t b0 = row[s], b1 = row[s + 1];
-        rstart[tt] = tt * kTile + b0;
-        len[k] = b1 - b0;
-      }
-      sum += len[k];
+    uint32_t len = 0;
+    if (t < tiles) {
+      const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
+      const uint32_t b0 = row[s], b1 = row[s + 1];
+      rstart[t] = t * kTile + b0;
+      len = b1 - b0;
     }
-    uint32_t inc = sum;
+    uint32_t inc = len;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(inc, d, 64);
@@ -115,125 +105,138 @@ __global__ __launch_bounds__(kAT) void k_apply_value(const uint32_t* __restrict_
     }
     if (l == 63) wsum[w] = inc;
     lds_barrier();
-    uint32_t run = inc - sum;
-    for (uint32_t q = 0; q < w; ++q) run += wsum[q];
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t tt = t * PT + k;
-      if (tt < tiles) rpre[tt] = run;
-      run += len[k];
+    uint32_t pre = inc - len, all = 0;
+    for (uint32_t q = 0; q < (uint32_t)kVW; ++q) {
+      const uint32_t x = wsum[q];
+      if (q < w) pre += x;
+      all += x;
     }
-    if (t == kAT - 1) rpre[tiles] = run;
+    if (t < tiles) rpre[t] = pre;
+    if (t == 0) rpre[tiles] = all;
     lds_barrier();
   }
   const uint32_t cnt = rpre[tiles];
   uint32_t err = 0;
 
-  uint32_t m[kApplyPer], nm[kApplyPer], pos[kApplyPer], npos[kApplyPer];
-  u64x2 ab[kApplyPer], nab[kApplyPer];
-  uint32_t cur = 0;  // this thread's run cursor (its records are visited in increasing order)
-  auto load = [&](uint32_t c0, uint32_t (&mm)[kApplyPer], u64x2 (&aa)[kApplyPer], uint32_t (&pp)[kApplyPer]) {
+  // thread (w, j, l) holds record c0 + w*256 + j*64 + l of a chunk: log order = (w, j, l)
+  uint32_t m[kVPer], nm[kVPer], g[kVPer], ng[kVPer];
+  u64x2 ab[kVPer], nab[kVPer];
+  auto load = [&](uint32_t c0, uint32_t (&mm)[kVPer], u64x2 (&aa)[kVPer], uint32_t (&gg)[kVPer]) {
 #pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      const uint32_t c = c0 + w * kWaveRecs + j * kWave + l;
+    for (int j = 0; j < kVPer; ++j) {
+      const uint32_t crow = c0 + w * kVWaveRecs + j * kWave, c = crow + l;
       mm[j] = 0;
       aa[j] = u64x2{0, 0};
-      pp[j] = 0;
-      if (c < cnt) {
-        while (rpre[cur + 1] <= c) ++cur;
-        const uint32_t g = rstart[cur] + (c - rpre[cur]);
-        pp[j] = g;
-        mm[j] = st_meta[g];
-        aa[j] = st_ab[g];
+      gg[j] = kNoPos;
+      if (crow < cnt) {  // wave-uniform
+        uint32_t r = find_run(rpre, tiles, crow);
+        if (c < cnt) {
+          while (rpre[r + 1] <= c) ++r;  // a lane is at most 63 records past its row's start
+          const uint32_t gp = rstart[r] + (c - rpre[r]);
+          gg[j] = gp;
+          mm[j] = st_meta[gp];
+          aa[j] = st_ab[gp];
+        }
       }
     }
   };
-  load(0, m, ab, pos);
-  lds_barrier();
-  for (uint32_t c0 = 0; c0 < cnt; c0 += kACh) {
+  load(0, m, ab, g);
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kVCh) {
     // the next chunk's records stream in during this whole chunk
-    load(c0 + kACh, nm, nab, npos);
+    load(c0 + kVCh, nm, nab, ng);
     // 1a. rank each record among the wave's earlier records of its slot
-    uint32_t rank[kApplyPer], slot[kApplyPer];
+    uint32_t rank[kVPer], slot[kVPer];
 #pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      const bool live = c0 + w * kWaveRecs + j * kWave + l < cnt;
-      slot[j] = smeta_slot(m[j]) & (kSbSlots - 1);
-      rank[j] = live ? atomicAdd(&wcnt[w][slot[j]], 1u) : 0xFFFFFFFFu;
+    for (int j = 0; j < kVPer; ++j) {
+      slot[j] = smeta_slot(m[j]) & (kVSlots - 1);
+      const uint32_t sh = 16 * (slot[j] & 1);
+      rank[j] = g[j] != kNoPos ? (atomicAdd(&wcnt[w][slot[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
     }
     lds_barrier();
-    // 1b. owner of slot t: prefix over the 4 waves; run length; reset the counters
-    uint32_t run = 0;
-#pragma unroll
-    for (int q = 0; q < kApplyWaves; ++q) {
-      const uint32_t c = wcnt[q][t];
-      wpre[q][t] = run;
-      wcnt[q][t] = 0;
-      run += c;
+    // 1b. exclusive prefixes over the 16 waves, per slot (thread = slot pair x wave pair; u16 halves never carry:
+    //     a chunk holds 4096 records)
+    {
+      const uint32_t pr = t & (kVPairs - 1), q = t >> 7;
+      const uint32_t c0v = wcnt[2 * q][pr], c1v = wcnt[2 * q + 1][pr];
+      qsum[q][pr] = c0v + c1v;
+      lds_barrier();
+      uint32_t base = 0;
+      for (uint32_t qq = 0; qq < q; ++qq) base += qsum[qq][pr];
+      wcnt[2 * q][pr] = base;
+      wcnt[2 * q + 1][pr] = base + c0v;
+      if (q == kVW / 2 - 1) ctot[pr] = base + c0v + c1v;
+      lds_barrier();
     }
-    // 1c. block exclusive scan of the run lengths -> run starts
-    uint32_t inc = run;
+    // 1c. run start of every slot (exclusive scan over the 256 slots by waves 0..3)
+    uint32_t run = 0, start = 0;
+    if (t < (uint32_t)kVSlots) {
+      run = (ctot[t >> 1] >> (16 * (t & 1))) & 0xFFFFu;
+      uint32_t inc = run;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(inc, d, 64);
-      if (l >= (uint32_t)d) inc += y;
-    }
-    if (l == 63) wsum[w] = inc;
-    lds_barrier();
-    uint32_t start = inc - run;
-    for (uint32_t q = 0; q < w; ++q) start += wsum[q];
-    sstart[t] = start;
-    lds_barrier();
-    // 1d. place records in slot order
-#pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      if (rank[j] == 0xFFFFFFFFu) continue;
-      const uint32_t p = sstart[slot[j]] + wpre[w][slot[j]] + rank[j];
-      sm[p] = m[j];
-      sab[p] = ab[j];
-      sidx[p] = (uint16_t)(w * kWaveRecs + j * kWave + l);
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      if (l == 63) wsum[w] = inc;
+      start = inc - run;
     }
     lds_barrier();
-    // 2. thread t applies its slot's commits in log order, state in registers (next record's LDS reads
+    if (t < (uint32_t)kVSlots) {
+      for (uint32_t q = 0; q < w; ++q) start += wsum[q];
+      sstart[t] = start;
+    }
+    lds_barrier();
+    // 1d. place records in slot order; p[j] = sorted position (results come back from there)
+    uint32_t p[kVPer];
+#pragma unroll
+    for (int j = 0; j < kVPer; ++j) {
+      p[j] = 0;
+      if (g[j] == kNoPos) continue;
+      const uint32_t sl = slot[j];
+      const uint32_t pre = (wcnt[w][sl >> 1] >> (16 * (sl & 1))) & 0xFFFFu;
+      p[j] = sstart[sl] + pre + rank[j];
+      sm[p[j]] = m[j];
+      sab[p[j]] = ab[j];
+    }
+    lds_barrier();
+    for (uint32_t k = t; k < (uint32_t)(kVW * kVPairs); k += kVT) (&wcnt[0][0])[k] = 0;
+    // 2. thread t applies its slot's commits in log order, state in registers (the next record's LDS reads
     //    are issued before the current one is applied)
-    if (run) {
+    if (t < (uint32_t)kVSlots && run) {
       uint32_t mm = sm[start];
-      u64x2 abv = sab[start];
-      uint32_t ci = sidx[start];
+      u64x2 xy = sab[start];
       for (uint32_t k = 0; k < run; ++k) {
         const uint32_t pn = k + 1 < run ? start + k + 1 : start + k;
         const uint32_t mm2 = sm[pn];
-        const u64x2 abv2 = sab[pn];
-        const uint32_t ci2 = sidx[pn];
+        const u64x2 xy2 = sab[pn];
         uint64_t rv;
-        const uint32_t stt = value_apply(smeta_op(mm), smeta_flags(mm), abv.x, abv.y, st_reg, rv, err);
-        rstat[ci] = (uint8_t)stt;
-        rval[ci] = rv;
+        const uint32_t stt = value_walk(mm, xy.x, xy.y, ms, sv, rv);
+        if (mm & kVrL) err |= kErrUnsupported;
+        rstat[start + k] = (uint8_t)stt;
+        rval[start + k] = rv;
         mm = mm2;
-        abv = abv2;
-        ci = ci2;
+        xy = xy2;
       }
     }
     lds_barrier();
     // 3. results back to the records' staging positions (contiguous within each run)
 #pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
-      const uint32_t ci = w * kWaveRecs + j * kWave + l;
-      if (c0 + ci < cnt) {
-        rst_status[pos[j]] = rstat[ci];
-        rst_value[pos[j]] = rval[ci];
-      }
+    for (int j = 0; j < kVPer; ++j) {
+      if (g[j] == kNoPos) continue;
+      rst_status[g[j]] = rstat[p[j]];
+      rst_value[g[j]] = rval[p[j]];
     }
-    lds_barrier();
 #pragma unroll
-    for (int j = 0; j < kApplyPer; ++j) {
+    for (int j = 0; j < kVPer; ++j) {
       m[j] = nm[j];
       ab[j] = nab[j];
-      pos[j] = npos[j];
+      g[j] = ng[j];
     }
   }
-  val_meta[(uint64_t)s * kSbSlots + t] = st_reg.meta;
-  val_v[(uint64_t)s * kSbSlots + t] = st_reg.v;
+  if (t < (uint32_t)kVSlots) {
+    val_meta[(uint64_t)s * kVSlots + t] = ms;
+    val_v[(uint64_t)s * kVSlots + t] = sv;
+  }
   if (err) atomicOr(err_out, err);
 }
 
@@ -266,8 +269,8 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
 
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {
   a.mark(K_APPLY_VALUE, 1, st);
-  hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kAT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.sb_kind, a.val_meta,
-                     a.val_v, a.rst_status, a.rst_value, a.err);
+  hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kVT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.sb_kind,
+                     a.val_meta, a.val_v, a.rst_status, a.rst_value, a.err);
   a.mark(K_APPLY_VALUE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -9,9 +9,7 @@ namespace cc {
 
 // ---- geometry -----------------------------------------------------------------------------------------
 constexpr int kWave = 64;                 // CDNA wavefront
-constexpr int kLaneRes = 64;              // an apply wave owns 64 resource slots (lane = slot % 64)
-constexpr int kApplyWaves = 4;            // apply workgroup = 4 waves = one super-bucket of 256 slots
-constexpr int kSbShift = 8;               // super-bucket = slot >> 8
+constexpr int kSbShift = 8;               // super-bucket = slot >> 8 (256 slots: one apply workgroup)
 constexpr int kMaxSb = 512;               // => max_resources <= 131072 with 256-slot super-buckets
 constexpr int kMapRegion = 2048;          // map table entries per region (one map apply workgroup, LDS-resident)
 constexpr int kMaxMapSb = 1024;           // map regions => map_capacity <= 2M entries
@@ -22,7 +20,6 @@ constexpr int kTile = 16384;              // commits per partition tile (one wor
 constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a tile (value-only engines)
 constexpr int kChunkMaps = 2048;          // ... when map commits (bigger records) share the partition
 constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan (1024-thread WG)
-constexpr int kApplyPer = 8;              // staging records per apply thread per chunk (prefetch depth)
 constexpr int kMaxTiles = 1024;           // tiles per sub-batch => sub-batch <= 16M commits
 constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 
@@ -53,6 +50,37 @@ struct alignas(16) u64x2 {
 
 // AtomicValueState per slot: meta = tag | (has_current << 8); value payload separately.
 __host__ __device__ inline uint32_t vmeta(uint32_t tag, uint32_t cur) { return (tag & 0xFF) | ((cur & 1) << 8); }
+
+// Value records staged for k_apply_value are encoded by the partition (value_encode): the walk then needs no
+// op decode and no tag canonicalisation.  meta = status byte of ops that do not return the current value
+// (bits 0..7) | W 8 | C 9 | R 10 | D 11 | L 12 | new tag 13..15 | slot-in-super-bucket 16..23 | compare tag
+// 24..26; operands = (canonical compare value, canonical new value).  Semantics: AtomicValueState.java
+// get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144, delete :146-157.
+constexpr uint32_t kVrW = 1u << 8;   // unconditional write: set, getAndSet
+constexpr uint32_t kVrC = 1u << 9;   // compareAndSet
+constexpr uint32_t kVrR = 1u << 10;  // returns the current value: get, getAndSet
+constexpr uint32_t kVrD = 1u << 11;  // delete
+constexpr uint32_t kVrL = 1u << 12;  // listen / unlisten: events, not applied by k_apply_value (flagged)
+__host__ __device__ inline uint32_t vrec_ntag(uint32_t m) { return (m >> 13) & 7u; }
+__host__ __device__ inline uint32_t vrec_ctag(uint32_t m) { return (m >> 24) & 7u; }
+__host__ __device__ inline void value_encode(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t& m, u64x2& xy) {
+  const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
+  const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
+  uint32_t bits, ntag = 0, ctag = 0;
+  uint64_t x = 0, y = 0;
+  switch (op) {
+    case CC_OP_VALUE_GET: bits = kVrR; break;
+    case CC_OP_VALUE_SET: bits = kVrW; ntag = ta; y = pa; break;
+    case CC_OP_VALUE_CAS: bits = kVrC | CC_STATUS(CC_ST_OK, CC_TAG_BOOL); ctag = ta; x = pa; ntag = tb; y = pb; break;
+    case CC_OP_VALUE_GETANDSET: bits = kVrW | kVrR; ntag = ta; y = pa; break;
+    case CC_OP_DELETE: bits = kVrD; break;
+    case CC_OP_VALUE_LISTEN:
+    case CC_OP_VALUE_UNLISTEN: bits = kVrL; break;
+    default: bits = CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);  // ResourceStateMachineExecutor.java:78
+  }
+  m = bits | (ntag << 13) | (ctag << 24);
+  xy = u64x2{x, y};
+}
 
 __device__ inline uint32_t lane_id() { return __lane_id(); }
 __device__ inline uint64_t lanemask_lt() {

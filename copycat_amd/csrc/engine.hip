@@ -48,6 +48,12 @@ struct cc_engine {
   std::vector<uint8_t> res_type;     // [sb*256]
   std::vector<uint32_t> inst_res;    // [max_inst]
   std::vector<uint64_t> inst_id, inst_client;
+  // java.util.HashMap iteration order of ResourceManager.sessions (ResourceManager.java:37): bucket index under
+  // the table capacity (starts at 16, doubles when the size passes 3/4 of it, never shrinks), then insertion
+  // order within the bucket.  Used to order the close fan-out (ResourceManager.java:250-264).
+  uint32_t sess_cap = 16, sess_thr = 12, sess_size = 0;
+  uint64_t sess_next = 0;
+  std::vector<uint64_t> inst_seq;
   // device registry + state
   uint32_t* d_inst_res = nullptr;
   uint8_t* d_res_type = nullptr;
@@ -238,6 +244,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   e->inst_res.assign(cfg->max_instances, kNoRes);
   e->inst_id.assign(cfg->max_instances, 0);
   e->inst_client.assign(cfg->max_instances, 0);
+  e->inst_seq.assign(cfg->max_instances, 0);
   auto fail = [&](const char* what, hipError_t x) {
     free_all(e);
     delete e;
@@ -426,6 +433,7 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   for (uint32_t i = 0; i < e->cfg.max_instances; ++i)
     if (e->inst_res[i] == slot) {
       e->inst_res[i] = kNoRes;
+      --e->sess_size;
       HIPCHECK(hipMemcpy(e->d_inst_res + i, &none, sizeof none, hipMemcpyHostToDevice));
     }
   return CC_OK;
@@ -446,6 +454,11 @@ static int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res
     e->inst_res[first + k] = (uint32_t)(res_first + k * res_stride);
     e->inst_id[first + k] = id_first + k;
     e->inst_client[first + k] = client;
+    e->inst_seq[first + k] = e->sess_next++;  // HashMap.putVal of a new key
+    if (++e->sess_size > e->sess_thr) {
+      e->sess_cap <<= 1;
+      e->sess_thr <<= 1;
+    }
   }
   HIPCHECK(hipMemcpy(e->d_inst_res + first, e->inst_res.data() + first, sizeof(uint32_t) * count, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(e->d_inst_id + first, e->inst_id.data() + first, sizeof(uint64_t) * count, hipMemcpyHostToDevice));
@@ -540,6 +553,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.hi = hi;
     pa.inst_res = e->d_inst_res;
     pa.res_type = e->d_res_type;
+    pa.sb_kind = e->d_sb_kind;
     pa.max_inst = e->cfg.max_instances;
     pa.sb = e->sb_total();
     pa.sb_val = e->sb;
@@ -738,6 +752,164 @@ extern "C" int cc_applied_index(cc_engine* e, uint64_t* out) {
   int rc = cc_sync(e);
   *out = e->applied;
   return rc;
+}
+
+// HashMap.hash of a java.lang.Long key: h = (int)(v ^ v >>> 32); h ^ h >>> 16
+static uint32_t java_long_hash(uint64_t v) {
+  const uint32_t h = (uint32_t)(v ^ (v >> 32));
+  return h ^ (h >> 16);
+}
+
+// ResourceManager.close(Session) for each client session of h_clients, in that order (ResourceManager.java:250-264).
+extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* d_events,
+                                 void* stream, uint64_t* h_closed) {
+  if (!e || (count && !h_clients)) return set_err(CC_ERR_INVALID, "null argument");
+  if (d_events && (!d_events->pos || !d_events->target || !d_events->code || !d_events->src || !d_events->tag ||
+                   !d_events->payload || !d_events->count))
+    return set_err(CC_ERR_INVALID, "event stream columns and count are required");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  hipStream_t st = stream ? (hipStream_t)stream : e->own_stream;
+  e->last_stream = st;
+  // the fan-out order: client order, then each client's instances in HashMap order of `sessions`
+  std::vector<std::pair<uint64_t, uint32_t>> by_client;  // (client rank, slot) candidates
+  {
+    std::vector<std::pair<uint64_t, uint64_t>> rank(count);  // (client, rank), sorted for lookup
+    for (uint64_t i = 0; i < count; ++i) rank[i] = {h_clients[i], i};
+    std::sort(rank.begin(), rank.end());
+    for (uint32_t i = 0; i < e->cfg.max_instances; ++i) {
+      if (e->inst_res[i] == kNoRes) continue;
+      auto it = std::lower_bound(rank.begin(), rank.end(), std::make_pair(e->inst_client[i], (uint64_t)0));
+      if (it != rank.end() && it->first == e->inst_client[i]) by_client.emplace_back(it->second, i);
+    }
+  }
+  struct Close { uint64_t crank, okey; uint32_t slot; };
+  std::vector<Close> order;
+  order.reserve(by_client.size());
+  for (auto& bc : by_client) {
+    const uint32_t i = bc.second;
+    const uint64_t okey = ((uint64_t)(java_long_hash(e->inst_id[i]) & (e->sess_cap - 1)) << 40) | e->inst_seq[i];
+    order.push_back(Close{bc.first, okey, i});
+  }
+  std::sort(order.begin(), order.end(), [](const Close& x, const Close& y) {
+    return x.crank != y.crank ? x.crank < y.crank : x.okey < y.okey;
+  });
+  const uint32_t m = (uint32_t)order.size();
+  if (h_closed) *h_closed = 0;
+  if (m == 0) {
+    if (d_events) HIPCHECK(hipMemsetAsync(d_events->count, 0, sizeof(uint64_t), st));
+    HIPCHECK(hipStreamSynchronize(st));
+    return CC_OK;
+  }
+  // positions grouped by resource (only state machines with a close handler: value, election, group)
+  std::vector<uint32_t> cinst(m), rlist, rstart, items;
+  std::vector<std::pair<uint32_t, uint32_t>> rp;
+  for (uint32_t p = 0; p < m; ++p) {
+    cinst[p] = order[p].slot;
+    const uint32_t r = e->inst_res[order[p].slot];
+    const uint8_t ty = e->res_type[r];
+    if (ty == CC_RES_VALUE || ty == CC_RES_ELECTION || ty == CC_RES_GROUP) rp.emplace_back(r, p);
+  }
+  std::sort(rp.begin(), rp.end());
+  for (size_t q = 0; q < rp.size(); ++q) {
+    if (q == 0 || rp[q].first != rp[q - 1].first) {
+      rlist.push_back(rp[q].first);
+      rstart.push_back((uint32_t)q);
+    }
+    items.push_back(rp[q].second);
+  }
+  rstart.push_back((uint32_t)rp.size());
+  const uint32_t nr = (uint32_t)rlist.size();
+  // device scratch: cinst | rlist | rstart | items | cnt | fail, off
+  const size_t n32 = (size_t)m + nr + (nr + 1) + items.size() + m + 1;
+  uint32_t* d32 = nullptr;
+  uint64_t* d_off = nullptr;
+  HIPCHECK(hipMalloc(&d32, sizeof(uint32_t) * n32));
+  if (hipMalloc(&d_off, sizeof(uint64_t) * (m + 1)) != hipSuccess) {
+    (void)hipFree(d32);
+    return set_err(CC_ERR_HIP, "hipMalloc close offsets");
+  }
+  std::vector<uint32_t> h32;
+  h32.reserve(n32);
+  h32.insert(h32.end(), cinst.begin(), cinst.end());
+  h32.insert(h32.end(), rlist.begin(), rlist.end());
+  h32.insert(h32.end(), rstart.begin(), rstart.end());
+  h32.insert(h32.end(), items.begin(), items.end());
+  h32.insert(h32.end(), (size_t)m, 0u);
+  h32.push_back(m);
+  CloseArgs ca{};
+  ca.cinst = d32;
+  ca.m = m;
+  ca.rlist = d32 + m;
+  ca.rstart = d32 + m + nr;
+  ca.items = d32 + m + nr + nr + 1;
+  ca.cnt = d32 + m + nr + nr + 1 + items.size();
+  ca.fail = ca.cnt + m;
+  ca.nr = nr;
+  ca.off = d_off;
+  ca.inst_res = e->d_inst_res;
+  ca.res_type = e->d_res_type;
+  ca.inst_id = e->d_inst_id;
+  ca.coord = e->coord_on ? e->d_coord : nullptr;
+  ca.arena = e->d_arena;
+  ca.arena_n = e->d_arena_n;
+  ca.arena_cap = e->coord_on ? e->arena_cap : 0;
+  ca.err = e->d_err;
+  unsigned long long zero_n = 0, *d_zero = nullptr;
+  if (!ca.arena_n) {  // no coordination state: no handler can publish; the scan still needs a counter
+    if (hipMalloc(&d_zero, sizeof zero_n) != hipSuccess) {
+      (void)hipFree(d32);
+      (void)hipFree(d_off);
+      return set_err(CC_ERR_HIP, "hipMalloc close counter");
+    }
+    ca.arena_n = d_zero;
+  }
+  if (d_events) {
+    ca.out_cap = d_events->capacity;
+    ca.out_pos = d_events->pos;
+    ca.out_target = d_events->target;
+    ca.out_code = d_events->code;
+    ca.out_src = d_events->src;
+    ca.out_tag = d_events->tag;
+    ca.out_payload = d_events->payload;
+    ca.out_count = d_events->count;
+  }
+  uint32_t stop = m;
+  hipError_t x = hipMemcpyAsync(d32, h32.data(), sizeof(uint32_t) * n32, hipMemcpyHostToDevice, st);
+  if (x == hipSuccess) x = hipMemsetAsync(ca.arena_n, 0, sizeof(unsigned long long), st);
+  if (x == hipSuccess && launch_close(ca, st)) x = hipGetLastError();
+  if (x == hipSuccess) x = hipMemcpyAsync(&stop, ca.fail, sizeof stop, hipMemcpyDeviceToHost, st);
+  if (x == hipSuccess) x = hipStreamSynchronize(st);
+  (void)hipFree(d32);
+  (void)hipFree(d_off);
+  if (d_zero) (void)hipFree(d_zero);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "session close", x);
+  // the host mirror of ResourceManager.sessions
+  for (uint32_t p = 0; p < stop && p < m; ++p) {
+    e->inst_res[cinst[p]] = kNoRes;
+    --e->sess_size;
+  }
+  if (h_closed) *h_closed = stop < m ? stop : m;
+  return check_device_err(e);
+}
+
+// Expired sessions from cc_expire_sweep's bitmap (bit s = client session id s), closed in ascending id order:
+// ResourceManager.expire (:238-247; no covered state machine overrides expire) then the close fan-out.
+extern "C" int cc_sessions_expire(cc_engine* e, const uint64_t* d_bitmap, uint64_t sessions, const cc_events* d_events,
+                                  void* stream, uint64_t* h_closed) {
+  if (!e || (sessions && !d_bitmap)) return set_err(CC_ERR_INVALID, "null argument");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  const uint64_t words = (sessions + 63) / 64;
+  std::vector<uint64_t> bm(words);
+  if (words) HIPCHECK(hipMemcpy(bm.data(), d_bitmap, sizeof(uint64_t) * words, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> clients;
+  for (uint64_t wi = 0; wi < words; ++wi)
+    for (uint64_t b = bm[wi]; b; b &= b - 1) {
+      const uint64_t sid = wi * 64 + (uint64_t)__builtin_ctzll(b);
+      if (sid < sessions) clients.push_back(sid);
+    }
+  return cc_sessions_close(e, clients.data(), clients.size(), d_events, stream, h_closed);
 }
 
 extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* h_tag, uint64_t* h_value,

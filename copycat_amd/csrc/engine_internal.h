@@ -32,6 +32,7 @@ struct PartArgs {
   uint64_t lo, hi;
   const uint32_t* inst_res;
   const uint8_t* res_type;
+  const uint8_t* sb_kind;  // value super-buckets run by k_apply_coord (their value records stay unencoded)
   uint32_t max_inst;
   uint32_t sb;        // super-buckets in total = sb_val + 2^map_bits (0 map bits: no maps)
   uint32_t sb_val;
@@ -48,7 +49,7 @@ struct PartArgs {
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
-size_t tile_lds_bytes(uint32_t sb, bool maps);
+size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk);
 
 struct ValueArgs {
   const uint32_t* st_meta;
@@ -182,6 +183,36 @@ struct EventArgs {
   Marker mark;
 };
 int launch_events(const EventArgs& a, hipStream_t st);
+
+// Session close / expire fan-out (close.hip): m closes in fan-out order, grouped by resource.
+struct CloseArgs {
+  const uint32_t* cinst;   // [m] instance slots in fan-out order
+  uint32_t m;
+  const uint32_t* rlist;   // [nr] resources with a close handler among them
+  const uint32_t* rstart;  // [nr + 1] -> items
+  const uint32_t* items;   // positions, grouped by resource, ascending
+  uint32_t nr;
+  uint32_t* inst_res;
+  const uint8_t* res_type;
+  const uint64_t* inst_id;
+  uint8_t* coord;          // null: no coordination blocks (then no state machine has a close handler)
+  uint32_t* fail;          // [1] first position whose close throws (init m)
+  uint32_t* cnt;           // [m] events per close (zeroed)
+  uint64_t* off;           // [m + 1]
+  EvRec* arena;
+  unsigned long long* arena_n;
+  uint64_t arena_cap;
+  uint64_t out_cap;
+  uint32_t* out_pos;
+  uint32_t* out_target;
+  uint8_t* out_code;
+  uint8_t* out_src;
+  uint8_t* out_tag;
+  uint64_t* out_payload;
+  uint64_t* out_count;
+  uint32_t* err;
+};
+int launch_close(const CloseArgs& a, hipStream_t st);
 
 struct UnpermuteArgs {
   const uint16_t* cpos;

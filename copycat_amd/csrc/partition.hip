@@ -24,6 +24,8 @@
 #include "common.h"
 #include "engine_internal.h"
 
+#include <cstdlib>
+
 namespace cc {
 
 // ResourceManager.operateResource dispatch (ResourceManager.java:60-62): instance slot -> resource slot.
@@ -56,8 +58,7 @@ __device__ inline uint32_t block_exscan(uint32_t v, uint32_t* wsum /*[16] LDS*/,
 
 // Per-wave counters are packed u16 pairs (a wave ranks at most 256 commits of a chunk): wc[w][k/2]; the
 // per-super-bucket tile offsets, run fills, chunk totals and chunk starts are u16 (a tile holds 16384 commits).
-size_t tile_lds_bytes(uint32_t sb, bool maps) {
-  const size_t chunk = maps ? kChunkMaps : kChunk;
+size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk) {
   const size_t rec = 16 + 4 + 2 + (maps ? 4 + 8 + 8 : 0);
   const size_t hw = (sb + 1) / 2;
   const size_t hot = maps ? kHotSlots * 4 + kHotMax * (8 + 8 + 4) : 0;
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
                                                 const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ clock_base,
                                                 uint32_t ext_flags, uint64_t lo, uint64_t hi,
                                                 const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
-                                                uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits,
+                                                const uint8_t* __restrict__ sb_kind, uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits,
                                                 const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n,
                                                 uint32_t* __restrict__ st_meta, u64x2* __restrict__ st_ab,
                                                 uint32_t* __restrict__ st_res, uint64_t* __restrict__ st_key,
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
 
   uint32_t nhot = 0;
   const uint64_t cbase0 = EXT && clock_base ? *clock_base : 0;
-  const bool value_ext = (ext_flags & kExtValue) != 0, deferred = (ext_flags & kExtDeferred) != 0;
+  const bool deferred = (ext_flags & kExtDeferred) != 0;
   if (EXT && map_bits) {
     nhot = *hot_n;
     for (uint32_t q = threadIdx.x; q < kHotSlots; q += kPT) hslot[q] = 0xFFFFFFFFu;
@@ -221,12 +222,14 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   // gathers: instance -> resource; with extended staging (maps, coordination, value events) the log index and
   // per type: map key + ttl sign; lock (clock at which due timeouts fire, timeout) + clock; others the key.
   // xs = the record's extended slot word: the map slot for map commits, the instance slot otherwise.
+  // Records for k_apply_value are encoded for its walk (common.h value_encode).
   auto gather = [&](uint64_t cbase, const uint32_t (&in)[J], uint32_t (&rr)[J], uint32_t (&mt)[J], u64x2 (&aa)[J],
                     uint64_t (&kk)[J], uint64_t (&ii)[J], uint32_t (&xx)[J]) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       rr[j] = in[j] == kNoRes ? kNoRes : resolve(inst_res, max_inst, in[j]);
       xx[j] = in[j];
+      if (!EXT && rr[j] != kNoRes) value_encode(mt[j] & 0xFF, (mt[j] >> 8) & 0xFF, aa[j].x, aa[j].y, mt[j], aa[j]);
       if (EXT && rr[j] != kNoRes) {
         const uint32_t ty = res_type[rr[j]];
         const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
@@ -235,7 +238,9 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
           ii[j] = cidx ? cidx[i] : 0;
           xx[j] = rr[j];
           if (caux && (int64_t)caux[i] > 0) mt[j] |= kMetaTtl;
-        } else if (ty != CC_RES_VALUE || value_ext) {
+        } else if (ty == CC_RES_VALUE && !sb_kind[rr[j] >> kSbShift]) {
+          value_encode(mt[j] & 0xFF, (mt[j] >> 8) & 0xFF, aa[j].x, aa[j].y, mt[j], aa[j]);
+        } else {
           ii[j] = cidx ? cidx[i] : 0;
           if (ty == CC_RES_LOCK) {  // deterministic log clock (time is non-decreasing within a batch)
             const uint64_t ti = ctime ? ctime[i] : 0;
@@ -394,12 +399,16 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   const bool ext = a.ext;
   a.mark(K_PART_TILE, 1, st);
   if (ext)
-    hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
+    hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
+                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+  else if (getenv("CC_PART_J2"))  // experiment knob: 2048-commit chunks (smaller LDS footprint)
+    hipLaunchKernelGGL((k_part_tile<2, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, 2 * kPT), st, a.inst,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
                        a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   else
-    hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.max_inst, a.sb,
+    hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, kChunk), st, a.inst,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
                        a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -263,6 +263,20 @@ int  cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* 
  * timeouts take effect (they publish nothing, LockState.java:54-58). */
 int  cc_advance_time(cc_engine* e, uint64_t now);
 
+/* ---- session close / expire fan-out (ResourceManager.close :250-264, expire :238-247) -------------------
+ * For each client session of h_clients, in order: every instance it owns, in java.util.HashMap iteration order of
+ * ResourceManager.sessions, is closed on its state machine (LeaderElectionState.close :35-52 hands leadership to the
+ * first listener, MembershipGroupState.close :36-42 publishes "leave", an AtomicValue listener is dropped; locks and
+ * maps have no close handler) and leaves the dispatch table: later commits on it get CC_ST_UNKNOWN_SESSION.  Events
+ * go to d_events (src CC_EVSRC_CLOSE, pos 0xFFFFFFFF) in fan-out order; *count is written.  A close that throws
+ * (an election leader already cleaned by delete) ends the fan-out there, as the reference's loop does:
+ * *h_closed = the instances closed.  Synchronous (control plane).                                              */
+int  cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* d_events, void* stream,
+                       uint64_t* h_closed);
+/* The expired set of cc_expire_sweep (bit s = client session id s, u64 words in HBM), closed in ascending id order. */
+int  cc_sessions_expire(cc_engine* e, const uint64_t* d_bitmap, uint64_t sessions, const cc_events* d_events, void* stream,
+                        uint64_t* h_closed);
+
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
  * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute, 3 k_apply_map, 4 k_map_hot (hot-key lists +
  * scan, apply_map_hot.hip), 5 k_apply_coord (coordination + value events), 6 k_events (event scan+scatter). */
