@@ -43,6 +43,20 @@ B_OP_C3 = 34.6  # put 30 in / get, remove 22 in; 9 out; weight
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def pmc_traffic(kernel, workload):
+    """HBM-side bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the same
+    bench command (scripts/pmc_traffic.py -> profiles/traffic_latest.json; counters cannot be read in-process)."""
+    p = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload", "c2") != workload:
+            return None
+        return d["kernels"][kernel]["bytes_per_launch"] / 1e9
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -276,7 +290,9 @@ def main():
         achieved = B_OP * commits_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, args.workload),
+            "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
+            "alg_gb_per_launch": round(B_OP * commits_per_launch / 1e9, 4),
             "avg_launch_ms": round(avg_ms, 4), "launches": launches,
             "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
             "bytes_per_commit": B_OP,
