@@ -5,7 +5,8 @@ tests/test_abi.py checks every constant here against the #defines of the header,
 import ctypes as C
 
 CC_ABI_VERSION = 1
-CC_PROFILE_KERNELS = 7  # k_part_tile, k_apply_value, k_unpermute, k_apply_map, k_map_hot, k_apply_coord, k_events
+CC_PROFILE_KERNELS = 7
+CC_PHASES = 8  # phase clocks per kernel of the diagnostics build (cc_debug_phases)
 
 CC_OK = 0
 CC_ERR_INVALID = -1

@@ -21,6 +21,7 @@ constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a t
 constexpr int kChunkMaps = 2048;          // ... when map commits (bigger records) share the partition
 constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan (1024-thread WG)
 constexpr int kMaxTiles = 1024;           // tiles per sub-batch => sub-batch <= 16M commits
+constexpr int kPersistGrid = 256;         // persistent tile loops: one 1024-thread workgroup per CU
 constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 
 // device error bits (d_err)
@@ -97,6 +98,20 @@ __device__ inline void lds_barrier() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
+// ---- optional in-kernel phase clocks (diagnostics build: -DCC_PHASE_TIMING, scripts/probes/phase_timing.py) --
+// Thread 0 of every workgroup accumulates s_memrealtime ticks (100 MHz) between phase marks; the sums are added to
+// a per-kernel __device__ array at the end and read back with cc_debug_phases.  Compiled out by default.
+constexpr int kPhases = 8;
+#ifdef CC_PHASE_TIMING
+#define PH_DECL uint64_t ph_last_ = wall_clock64(); uint64_t ph_acc_[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH(k) do { if (threadIdx.x == 0) { const uint64_t n_ = wall_clock64(); ph_acc_[k] += n_ - ph_last_; ph_last_ = n_; } } while (0)
+#define PH_FLUSH(buf) do { if (threadIdx.x == 0) for (int q_ = 0; q_ < kPhases; ++q_) atomicAdd(&(buf)[q_], (unsigned long long)ph_acc_[q_]); } while (0)
+#else
+#define PH_DECL
+#define PH(k) do { } while (0)
+#define PH_FLUSH(buf) do { } while (0)
+#endif
 
 // ---- ops registered per resource type (ResourceStateMachine.init + Copycat reflection configure) -----
 __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {

@@ -56,6 +56,8 @@ struct cc_engine {
   std::vector<uint64_t> inst_seq;
   // device registry + state
   uint32_t* d_inst_res = nullptr;
+  uint16_t* d_inst_res16 = nullptr;  // value-only fast path (< 65535 resources, <= 65536 instances)
+  uint16_t* d_res16 = nullptr;       // [sub_batch] resolved resource per commit (same path)
   uint8_t* d_res_type = nullptr;
   uint32_t* d_val_meta = nullptr;
   uint64_t* d_val_v = nullptr;
@@ -162,7 +164,7 @@ static void free_all(cc_engine* e) {
                   e->d_st_key,   e->d_st_idx,   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
-                  e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total};
+                  e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -256,11 +258,15 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if (x != hipSuccess) return fail("hipMalloc " #p, x); \
   } while (0)
   ALLOC(e->d_inst_res, sizeof(uint32_t) * cfg->max_instances);
+  if (cfg->max_resources < 0xFFFFu && cfg->max_instances <= 65536u) {
+    ALLOC(e->d_inst_res16, sizeof(uint16_t) * ((cfg->max_instances + 7) / 8 * 8));
+    ALLOC(e->d_res16, sizeof(uint16_t) * e->sub_batch);
+  }
   ALLOC(e->d_res_type, slots);
   ALLOC(e->d_val_meta, sizeof(uint32_t) * slots);
   ALLOC(e->d_val_v, sizeof(uint64_t) * slots);
-  ALLOC(e->d_st_meta, sizeof(uint32_t) * e->sub_batch);
-  ALLOC(e->d_st_ab, sizeof(u64x2) * e->sub_batch);
+  ALLOC(e->d_st_meta, sizeof(uint32_t) * (e->sub_batch + kPT));  // + dummy rows for unconditional stores
+  ALLOC(e->d_st_ab, sizeof(u64x2) * (e->sub_batch + kPT));
   ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
   ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sb_total() + 1));
   if (e->map_bits) {
@@ -278,8 +284,8 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_hot_agg, hot_agg_bytes());
     ALLOC(e->d_hot_s0, hot_s0_bytes());
   }
-  ALLOC(e->d_rst_status, e->sub_batch);
-  ALLOC(e->d_rst_value, sizeof(uint64_t) * e->sub_batch);
+  ALLOC(e->d_rst_status, e->sub_batch + 4 * kPT);  // + dummy rows for unconditional result stores
+  ALLOC(e->d_rst_value, sizeof(uint64_t) * (e->sub_batch + 4 * kPT));
   ALLOC(e->d_err, sizeof(uint32_t));
   ALLOC(e->d_last_index, sizeof(uint64_t));
   ALLOC(e->d_sb_kind, e->sb);
@@ -567,6 +573,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.st_idx = e->d_st_idx;
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
+    pa.dummy = e->sub_batch;
+    pa.inst_res16 = e->d_inst_res16;
+    pa.res16 = e->ext ? nullptr : e->d_res16;
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
     ValueArgs va{};
@@ -581,6 +590,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.val_v = e->d_val_v;
     va.rst_status = e->d_rst_status;
     va.rst_value = e->d_rst_value;
+    va.dummy = e->sub_batch;
     va.err = e->d_err;
     va.mark = marker_of(e);
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
@@ -647,6 +657,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.rst_value = e->d_rst_value;
     ua.out_status = out->status;
     ua.out_value = out->value;
+    ua.dummy_status = e->d_rst_status + e->sub_batch;
+    ua.dummy_value = e->d_rst_value + e->sub_batch;
     ua.mark = marker_of(e);
     if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
     if (e->coord_on) {
@@ -1059,6 +1071,14 @@ extern "C" int cc_profile_reset(cc_engine* e) {
     e->prof_n[k] = 0;
   }
   return CC_OK;
+}
+
+extern "C" int cc_debug_phases(cc_engine* e, int kernel, uint64_t* ticks) {
+  if (!e || !ticks || kernel < 0 || kernel >= K_NUM) return CC_ERR_INVALID;
+  HIPCHECK(hipSetDevice(e->device));
+  HIPCHECK(hipStreamSynchronize(e->last_stream));
+  const int rc = phase_read(kernel, ticks);
+  return rc == CC_OK ? CC_OK : set_err(rc, "phase clocks: not a CC_PHASE_TIMING build, or not instrumented kernel");
 }
 
 extern "C" int cc_profile_read(cc_engine* e, int kernel, double* total_ms, uint64_t* launches, const char** name) {

@@ -14,6 +14,9 @@ struct Marker {
   }
 };
 
+// Phase clocks of the diagnostics build (common.h PH_*): read and clear one kernel's sums (ticks of 10 ns).
+int phase_read(int kernel, uint64_t* out /*[kPhases]*/);
+
 // One sub-batch [lo, hi) of a batch (absolute row indices; column pointers are whole-batch; staging buffers
 // are indexed relative to lo).
 struct PartArgs {
@@ -46,9 +49,14 @@ struct PartArgs {
   uint64_t* st_idx;
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
+  uint64_t dummy;     // first of the kPT dummy staging rows after the staging area (= sub_batch)
+  uint16_t* inst_res16;  // value-only engines, < 65535 resources, <= 65536 instances: u16 copy of inst_res
+  uint16_t* res16;       // ... and the resolved resource of every commit of the sub-batch (null: not this path)
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
+int launch_tile_hist16(const PartArgs& a, uint32_t tiles, hipStream_t st);
+int launch_part_value(const PartArgs& a, uint32_t tiles, hipStream_t st);
 size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk);
 
 struct ValueArgs {
@@ -61,8 +69,9 @@ struct ValueArgs {
   const uint8_t* sb_kind;  // non-zero: the super-bucket runs on k_apply_coord (may be null)
   uint32_t* val_meta;    // [sb*256]
   uint64_t* val_v;       // [sb*256]
-  uint8_t* rst_status;   // staged results [sub_batch]
+  uint8_t* rst_status;   // staged results [sub_batch + kPT]
   uint64_t* rst_value;
+  uint64_t dummy;        // first of the dummy result rows after the staging area (= sub_batch)
   uint32_t* err;
   Marker mark;
 };
@@ -223,6 +232,8 @@ struct UnpermuteArgs {
   const uint64_t* rst_value;
   uint8_t* out_status;  // whole-batch outputs
   uint64_t* out_value;
+  uint8_t* dummy_status;  // 4 x kPT dummy result rows (after the staging area) for unconditional stores
+  uint64_t* dummy_value;
   Marker mark;
 };
 int launch_unpermute(const UnpermuteArgs& a, hipStream_t st);

@@ -28,6 +28,10 @@
 
 namespace cc {
 
+#ifdef CC_PHASE_TIMING
+__device__ unsigned long long g_ph_part[kPhases], g_ph_unperm[kPhases];  // g_ph_part: k_part_tile
+#endif
+
 // ResourceManager.operateResource dispatch (ResourceManager.java:60-62): instance slot -> resource slot.
 __device__ inline uint32_t resolve(const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t s) {
   return s < max_inst ? inst_res[s] : kNoRes;
@@ -54,6 +58,68 @@ __device__ inline uint32_t block_exscan(uint32_t v, uint32_t* wsum /*[16] LDS*/,
   }
   *total = all;
   return wpre + inc - v;
+}
+
+// Value-only engines: the tile histogram (tile-local run starts = the ttab row) in its own launch, so that the
+// partition workgroups start streaming their tile at once instead of reading it twice.  512 threads per tile,
+// 32 commits each (16-byte loads of the instance column, then the instance -> resource gathers).
+constexpr int kHT = 512;
+__global__ __launch_bounds__(kHT) void k_tile_hist(const uint32_t* __restrict__ inst, uint64_t lo, uint64_t hi,
+                                                   const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
+                                                   uint16_t* __restrict__ ttab) {
+  __shared__ uint32_t h[kMaxSb];
+  __shared__ uint32_t wsum[kHT / kWave];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t k = t; k < sb; k += kHT) h[k] = 0;
+  __syncthreads();
+  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
+  const uint64_t tile1 = tile0 + kTile < hi ? tile0 + kTile : hi;
+  const uint64_t q1 = tile1 / 4;
+  constexpr int kQ = kTile / 4 / kHT;  // uint4 groups per thread (8)
+  uint4 v[kQ];
+#pragma unroll
+  for (int k = 0; k < kQ; ++k) {
+    const uint64_t q = tile0 / 4 + t + (uint64_t)k * kHT;
+    v[k] = q < q1 ? reinterpret_cast<const uint4*>(inst)[q] : make_uint4(kNoRes, kNoRes, kNoRes, kNoRes);
+  }
+#pragma unroll
+  for (int k = 0; k < kQ; ++k) {
+    const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t r = resolve(inst_res, max_inst, x[e]);
+      if (r != kNoRes) atomicAdd(&h[r >> kSbShift], 1u);
+    }
+  }
+  for (uint64_t i = q1 * 4 + t; i < tile1; i += kHT) {  // ragged tail (< 4 commits)
+    if (i < tile0) continue;
+    const uint32_t r = resolve(inst_res, max_inst, inst[i]);
+    if (r != kNoRes) atomicAdd(&h[r >> kSbShift], 1u);
+  }
+  __syncthreads();
+  uint16_t* row = ttab + (uint64_t)blockIdx.x * (sb + 1);
+  uint32_t run = 0;
+  for (uint32_t k0 = 0; k0 < sb; k0 += kHT) {  // block-uniform; sb <= kMaxSb
+    const uint32_t k = k0 + t;
+    const uint32_t c = k < sb ? h[k] : 0;
+    uint32_t inc = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if ((t & 63) >= (uint32_t)d) inc += y;
+    }
+    __syncthreads();
+    if ((t & 63) == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+    for (uint32_t q = 0; q < kHT / kWave; ++q) {
+      pre += q < (t >> 6) ? wsum[q] : 0;
+      all += wsum[q];
+    }
+    if (k < sb) row[k] = (uint16_t)(run + pre + inc - c);
+    run += all;
+  }
+  if (t == 0) row[sb] = (uint16_t)run;  // live commits of the tile (<= 16384)
 }
 
 // Per-wave counters are packed u16 pairs (a wave ranks at most 256 commits of a chunk): wc[w][k/2]; the
@@ -107,6 +173,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   uint64_t* hkey = hh64 + kHotMax;
   uint32_t* hident = reinterpret_cast<uint32_t*>(hkey + kHotMax);
 
+  PH_DECL
   uint32_t nhot = 0;
   const uint64_t cbase0 = EXT && clock_base ? *clock_base : 0;
   const bool deferred = (ext_flags & kExtDeferred) != 0;
@@ -194,6 +261,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
     }
     if (t == 0) row[sb] = (uint16_t)run;  // live commits of the tile (<= 16384)
   }
+  PH(0);
 
   // commit (w, j, l) of a chunk is cbase + w*(64*J) + j*64 + l: log order = (w, j, l).
   // Prefetch in two stages so no wave stalls on the instance->resource gather right after its load:
@@ -266,6 +334,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
     if (more) load_raw(cbase + C, ninst, nmeta, nab, nkey, nidx);
     for (uint32_t k = t; k < kPW * hw; k += kPT) wc[k] = 0;
     lds_barrier();
+    PH(6);
     // 1. rank by super-bucket inside each wave: the wave's own counter table, LDS atomics with return
     //    (same-address lanes of one instruction resolve in lane order on gfx950 — checked at engine start)
     uint32_t sk[J], loc[J];
@@ -280,6 +349,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
     uint32_t nres[J];
     if (more) gather(cbase + C, ninst, nres, nmeta, nab, nkey, nidx, nxs);
     lds_barrier();
+    PH(1);
     // 2. per super-bucket: exclusive prefix over waves (packed halves) and chunk totals; chunk-sorted starts
     for (uint32_t kw = t; kw < hw; kw += kPT) {
       uint32_t r0 = 0, r1 = 0;
@@ -292,6 +362,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       ctot32[kw] = r0 | (r1 << 16);
     }
     lds_barrier();
+    PH(2);
     uint32_t nlive = 0;
     for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform
       const uint32_t k = k0 + t;
@@ -301,6 +372,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       nlive += part;
     }
     lds_barrier();
+    PH(3);
     // 3. place records in LDS in sorted order; per-commit tile-local position
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -324,6 +396,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       cpos[i - lo] = (uint16_t)(toff[sk[j]] + trun[sk[j]] + within);
     }
     lds_barrier();
+    PH(4);
     // 4. write the chunk out run by run (contiguous)
     for (uint32_t s = t; s < nlive; s += kPT) {
       const uint32_t k = rsb[s];
@@ -337,6 +410,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       }
     }
     lds_barrier();
+    PH(5);
     for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
     if (more) {
 #pragma unroll
@@ -350,47 +424,114 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       }
     }
   }
+#ifdef CC_PHASE_TIMING
+  if (!EXT) PH_FLUSH(g_ph_part);
+#endif
 }
 
-// One workgroup per tile: the tile's staged results (contiguous) -> LDS -> log order through cpos.
-__global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ cpos, const uint16_t* __restrict__ ttab,
-                                                uint32_t sb, uint64_t n, const uint8_t* __restrict__ rst_status,
+// Persistent over tiles (tile T = blockIdx.x + k * gridDim.x): the tile's staged results (contiguous, tile-local)
+// are in LDS while they are written back in log order through cpos; the NEXT tile's results and cpos are loaded
+// into registers (16-byte loads) during that scatter and moved to LDS at the top of the next iteration.
+constexpr int kUnVal = kTile / (2 * kPT);  // u64x2 value loads per thread per tile (8)
+constexpr int kUnPos = kTile / (4 * kPT);  // 4-commit cpos groups per thread per tile (4)
+__global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ cpos, uint32_t tiles, uint64_t n,
+                                                const uint8_t* __restrict__ rst_status,
                                                 const uint64_t* __restrict__ rst_value, uint8_t* __restrict__ out_status,
-                                                uint64_t* __restrict__ out_value) {
-  __shared__ uint64_t lv[kTile];
-  __shared__ uint8_t ls[kTile];
+                                                uint64_t* __restrict__ out_value, uint8_t* __restrict__ dummy_status,
+                                                uint64_t* __restrict__ dummy_value) {
+  __shared__ uint4 lv2[kTile / 2];
+  __shared__ uint4 ls4[kTile / 16];
+  PH_DECL
+  const uint64_t* lv = reinterpret_cast<const uint64_t*>(lv2);
+  const uint8_t* ls = reinterpret_cast<const uint8_t*>(ls4);
   const uint32_t t = threadIdx.x;
-  const uint64_t i0 = (uint64_t)blockIdx.x * kTile;
-  const uint32_t nlive = ttab[(uint64_t)blockIdx.x * (sb + 1) + sb];
-  for (uint32_t p = t; p < nlive; p += kPT) {
-    ls[p] = rst_status[i0 + p];
-    lv[p] = rst_value[i0 + p];
-  }
-  lds_barrier();
+  // Prefetch registers as named scalars (an array here is kept in scratch by the compiler, which would make
+  // every prefetch wait).  Staging buffers hold whole tiles (the sub-batch is a multiple of kTile): full-tile
+  // loads stay in bounds; the prefetch is unconditional (the last tile is re-read).
+  static_assert(kUnVal == 8 && kUnPos == 4, "unpermute prefetch registers");
+  uint4 rs, v0, v1, v2, v3, v4, v5, v6, v7;
+  uint2 p0, p1, p2, p3;
+  auto load = [&](uint32_t TT) {
+    const uint64_t i0 = (uint64_t)TT * kTile;
+    const uint4* sv = reinterpret_cast<const uint4*>(rst_value + i0) + t;
+    const uint2* sp = reinterpret_cast<const uint2*>(cpos + i0) + t;
+    rs = reinterpret_cast<const uint4*>(rst_status + i0)[t];
+    v0 = sv[0 * kPT]; v1 = sv[1 * kPT]; v2 = sv[2 * kPT]; v3 = sv[3 * kPT];
+    v4 = sv[4 * kPT]; v5 = sv[5 * kPT]; v6 = sv[6 * kPT]; v7 = sv[7 * kPT];
+    p0 = sp[0 * kPT]; p1 = sp[1 * kPT]; p2 = sp[2 * kPT]; p3 = sp[3 * kPT];
+  };
+  uint32_t T = blockIdx.x;
+  load(T < tiles ? T : tiles - 1);
   const uint8_t unk = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
-  const uint64_t i1 = i0 + kTile < n ? i0 + kTile : n;
-  const uint64_t q1 = i1 / 4;
-  for (uint64_t q = i0 / 4 + t; q < q1; q += kPT) {  // 4 commits per thread: vector loads/stores
-    const uint2 pp = reinterpret_cast<const uint2*>(cpos)[q];
-    const uint32_t p[4] = {pp.x & 0xFFFF, pp.x >> 16, pp.y & 0xFFFF, pp.y >> 16};
-    uint32_t sw = 0;
-    uint64_t v[4];
+  uint64_t tail_i = ~0ull, tail_v0 = 0, tail_v1 = 0, tail_v2 = 0;
+  uint32_t tail_sw = 0;
+  for (; T < tiles; T += gridDim.x) {
+    lds_barrier();  // the previous tile's scatter is done reading LDS
+    ls4[t] = rs;
+    lv2[t + 0 * kPT] = v0; lv2[t + 1 * kPT] = v1; lv2[t + 2 * kPT] = v2; lv2[t + 3 * kPT] = v3;
+    lv2[t + 4 * kPT] = v4; lv2[t + 5 * kPT] = v5; lv2[t + 6 * kPT] = v6; lv2[t + 7 * kPT] = v7;
+    const uint2 pp[kUnPos] = {p0, p1, p2, p3};
+    lds_barrier();
+    PH(0);
+    load(T + gridDim.x < tiles ? T + gridDim.x : tiles - 1);
+    const uint64_t i0 = (uint64_t)T * kTile;
+    // 4-commit groups wholly inside the batch go to the outputs; the others to the dummy rows (unconditional
+    // stores: see k_part_value), and the one group that straddles the batch end is written after the loop
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool ok = p[k] != 0xFFFF;
-      sw |= (uint32_t)(ok ? ls[p[k]] : unk) << (8 * k);
-      v[k] = ok ? lv[p[k]] : 0;
+    for (int k = 0; k < kUnPos; ++k) {
+      const uint64_t i = i0 + 4 * (uint64_t)(t + k * kPT);  // commits i .. i+3
+      const uint32_t p[4] = {pp[k].x & 0xFFFF, pp[k].x >> 16, pp[k].y & 0xFFFF, pp[k].y >> 16};
+      uint32_t sw = 0;
+      uint64_t v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = p[q] != 0xFFFF;
+        sw |= (uint32_t)(ok ? ls[p[q]] : unk) << (8 * q);
+        v[q] = ok ? lv[p[q]] : 0;
+      }
+      const bool in = i + 4 <= n;
+      uint32_t* os = in ? reinterpret_cast<uint32_t*>(out_status) + i / 4 : reinterpret_cast<uint32_t*>(dummy_status) + t;
+      u64x2* ov = in ? reinterpret_cast<u64x2*>(out_value) + i / 2 : reinterpret_cast<u64x2*>(dummy_value) + 2 * t;
+      *os = sw;
+      ov[0] = u64x2{v[0], v[1]};
+      ov[1] = u64x2{v[2], v[3]};
+      if (!in && i < n) {  // the straddling group (at most one in the grid): remember it for after the loop
+        tail_sw = sw;
+        tail_v0 = v[0];
+        tail_v1 = v[1];
+        tail_v2 = v[2];
+        tail_i = i;
+      }
     }
-    reinterpret_cast<uint32_t*>(out_status)[q] = sw;
-    u64x2* ov = reinterpret_cast<u64x2*>(out_value) + 2 * q;
-    ov[0] = u64x2{v[0], v[1]};
-    ov[1] = u64x2{v[2], v[3]};
+    PH(1);
   }
-  for (uint64_t i = q1 * 4 + t; i < i1; i += kPT) {
-    const uint32_t p = cpos[i];
-    out_status[i] = p != 0xFFFF ? ls[p] : unk;
-    out_value[i] = p != 0xFFFF ? lv[p] : 0;
+  if (tail_i != ~0ull) {  // commits tail_i .. n-1 (1 to 3 of them)
+    const uint64_t vv[3] = {tail_v0, tail_v1, tail_v2};
+    for (int q = 0; q < 3 && tail_i + q < n; ++q) {
+      out_status[tail_i + q] = (uint8_t)(tail_sw >> (8 * q));
+      out_value[tail_i + q] = vv[q];
+    }
   }
+  PH_FLUSH(g_ph_unperm);
+}
+
+int phase_read_value(uint64_t* out);
+int phase_read_partv(uint64_t* out);
+int phase_read(int kernel, uint64_t* out) {
+#ifdef CC_PHASE_TIMING
+  if (kernel == K_APPLY_VALUE) return phase_read_value(out);
+  if (kernel == K_PART_TILE && getenv("CC_PART_VALUE")) return phase_read_partv(out);  // the value partition
+  unsigned long long z[kPhases] = {};
+  if (kernel != K_UNPERMUTE && kernel != K_PART_TILE) return CC_ERR_INVALID;
+  const void* sym = kernel == K_PART_TILE ? HIP_SYMBOL(g_ph_part) : HIP_SYMBOL(g_ph_unperm);
+  if (hipMemcpyFromSymbol(out, sym, sizeof z) != hipSuccess || hipMemcpyToSymbol(sym, z, sizeof z) != hipSuccess)
+    return CC_ERR_HIP;
+  return CC_OK;
+#else
+  (void)kernel;
+  (void)out;
+  return CC_ERR_UNSUPPORTED;
+#endif
 }
 
 int launch_partition(const PartArgs& a, hipStream_t st) {
@@ -398,18 +539,23 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   if (tiles == 0) return 0;
   const bool ext = a.ext;
   a.mark(K_PART_TILE, 1, st);
-  if (ext)
-    hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
-  else if (getenv("CC_PART_J2"))  // experiment knob: 2048-commit chunks (smaller LDS footprint)
-    hipLaunchKernelGGL((k_part_tile<2, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, 2 * kPT), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
-  else
+  static const bool part_value = getenv("CC_PART_VALUE") != nullptr;  // experiment: persistent value partition
+  if (!ext && part_value) {  // tile histograms, then the persistent value partition (partition_value.hip)
+    if (a.res16) {
+      if (launch_tile_hist16(a, tiles, st)) return -1;
+    } else {
+      hipLaunchKernelGGL(k_tile_hist, dim3(tiles), dim3(kHT), 0, st, a.inst, a.lo, a.hi, a.inst_res, a.max_inst, a.sb, a.ttab);
+    }
+    if (launch_part_value(a, tiles, st)) return -1;
+  } else if (!ext) {
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, kChunk), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
                        a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+  } else {
+    hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst,
+                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
+                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+  }
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -419,8 +565,9 @@ int launch_unpermute(const UnpermuteArgs& a, hipStream_t st) {
   const uint64_t tiles = (n + kTile - 1) / kTile;
   if (tiles == 0) return 0;
   a.mark(K_UNPERMUTE, 1, st);
-  hipLaunchKernelGGL(k_unpermute, dim3((uint32_t)tiles), dim3(kPT), 0, st, a.cpos, a.ttab, a.sb, n, a.rst_status,
-                     a.rst_value, a.out_status + a.lo, a.out_value + a.lo);
+  const uint32_t grid = (uint32_t)(tiles < kPersistGrid ? tiles : kPersistGrid);
+  hipLaunchKernelGGL(k_unpermute, dim3(grid), dim3(kPT), 0, st, a.cpos, (uint32_t)tiles, n, a.rst_status, a.rst_value,
+                     a.out_status + a.lo, a.out_value + a.lo, a.dummy_status, a.dummy_value);
   a.mark(K_UNPERMUTE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

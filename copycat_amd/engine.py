@@ -20,7 +20,7 @@ from . import abi
 from .batch import Batch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_HERE, "libcopycat_apply.so")
+SO_PATH = os.environ.get("CC_ENGINE_SO") or os.path.join(_HERE, "libcopycat_apply.so")  # override: diagnostics builds
 _LIB = None
 
 

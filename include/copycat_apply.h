@@ -286,6 +286,12 @@ int  cc_profile_reset(cc_engine* e);
 /* Accumulated device time (ms) and launch count of one kernel since the last reset (synchronizes). */
 int  cc_profile_read(cc_engine* e, int kernel, double* total_ms, uint64_t* launches, const char** name);
 
+/* Diagnostics build only (-DCC_PHASE_TIMING; scripts/probes/phase_timing.py): per-phase s_memrealtime ticks
+ * (10 ns) summed over the workgroups of kernel `kernel` (0 k_part_tile, 1 k_apply_value, 2 k_unpermute) since
+ * the last read, CC_PHASES entries; CC_ERR_UNSUPPORTED in the product build. */
+#define CC_PHASES 8
+int cc_debug_phases(cc_engine* e, int kernel, uint64_t* ticks);
+
 /* ---- leader quorum commit index (Copycat leader [not vendored]) ------------------------
  * Per group g: N = the quorum-th largest of d_match[r*groups + g], r < replicas (r = 0 is the leader's
  * last log index), quorum = replicas/2 + 1; new = (N >= d_term_start[g] && N > d_commit_in[g]) ? N : d_commit_in[g]. */

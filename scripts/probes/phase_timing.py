@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Diagnostics: per-phase wall time inside k_part_tile / k_apply_value / k_unpermute on the c2 stream.
+
+  python scripts/probes/phase_timing.py --build        # here (CPU): hipcc the engine with -DCC_PHASE_TIMING
+  python scripts/probes/phase_timing.py [--commits N]  # GPU box: run c2 and print the phase table
+
+Thread 0 of every workgroup sums s_memrealtime ticks (10 ns) between phase marks (common.h PH_*); the table
+shows the sum over workgroups divided by the number of workgroups (= average time per workgroup per launch).
+"""
+import argparse
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+OUT = os.path.join(ROOT, "copycat_amd", "diag", "libcopycat_apply_phase.so")
+PHASES_PARTV = ["prologue", "rank", "scan(1 wave)", "place+issue", "write-out", "-", "-", "-"]  # CC_PART_VALUE=1
+PHASES = {
+    0: ["histogram+row", "rank+wait", "wave-prefix", "exscan", "place", "write-out", "top(clear,issue)", "-"],
+    1: ["setup", "rank+wait", "wave-prefix", "slot-scan", "place", "walk", "result-store", "-"],
+    2: ["load", "scatter", "-", "-", "-", "-", "-", "-"],
+}
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    from copycat_amd import build as b
+
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC",
+           "-shared", "-DCC_PHASE_TIMING", *b.ENGINE_SRCS, "-o", OUT]
+    subprocess.run(cmd, cwd=b.CSRC, check=True)
+    print(OUT)
+
+
+def run(args):
+    os.environ["CC_ENGINE_SO"] = OUT
+    sys.path.insert(0, ROOT)
+    import torch
+
+    from copycat_amd import abi
+    from copycat_amd.engine import DeviceBatch, Engine, lib
+    from copycat_amd.workload import SEED_C2, atomic_long_stream
+
+    n, R = args.commits, 65536
+    b = atomic_long_stream(n, resources=R, seed=SEED_C2, index0=1)
+    db = DeviceBatch.upload(b, device="cuda:0", columns=("index", "inst", "op", "flags", "a", "b"))
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    va = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    E = Engine(R, R, n, device=0, sub_batch=args.sub_batch)
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E.instance_open_range(0, R, 0, 1, 1)
+    L = lib()
+    L.cc_debug_phases.restype = C.c_int
+    L.cc_debug_phases.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    ticks = (C.c_uint64 * 8)()
+    E.apply(db, st, va)
+    E.sync()
+    for k in range(3):
+        L.cc_debug_phases(E.h, k, ticks)  # clear the warmup sums
+    E.profile(True)
+    for _ in range(args.steps):
+        E.apply(db, st, va)
+    E.sync()
+    prof = E.profile_read()
+    sub = args.sub_batch or (16 << 20)
+    launches = args.steps * ((n + sub - 1) // sub)
+    tiles = (n + 16383) // 16384
+    if os.environ.get("CC_PART_VALUE"):
+        PHASES[0] = PHASES_PARTV
+    wgs = {0: min(tiles, 256) * launches if os.environ.get("CC_PART_VALUE") else tiles * args.steps, 1: 256 * launches, 2: min(tiles, 256) * launches}
+    names = {0: "k_part_tile", 1: "k_apply_value", 2: "k_unpermute"}
+    for k in range(3):
+        rc = L.cc_debug_phases(E.h, k, ticks)
+        assert rc == 0, rc
+        tot = sum(ticks)
+        ms, nl = prof.get(names[k], (0.0, 0))
+        print(f"{names[k]}: {ms / max(nl, 1) * 1e3:.1f} us/launch, workgroups {wgs[k]}, "
+              f"per-WG mean {tot * 10e-3 / wgs[k]:.2f} us")
+        for q in range(8):
+            if ticks[q]:
+                print(f"   {PHASES[k][q]:18s} {ticks[q] * 10e-3 / wgs[k]:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--commits", type=int, default=100_000_000)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--sub-batch", type=int, default=0)
+    a = ap.parse_args()
+    build() if a.build else run(a)
