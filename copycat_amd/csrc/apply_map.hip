@@ -25,8 +25,9 @@
 // Per-op semantics restate MapState (collections/src/main/java/io/atomix/collections/state/MapState.java):
 //   containsKey :38-44, get :65-72, getOrDefault :77-84, put :89-110, putIfAbsent :115-133, remove :138-154,
 //   removeIfPresent :159-178, replace :183-202, replaceIfPresent :207-228 (stores `value`, compares `replace`).
-// Not applied on the GPU (the batch fails with CC_ERR_UNSUPPORTED): containsValue/size/isEmpty/clear and
-// Delete (they read or reset a whole map), and put/putIfAbsent/replace/replaceIfPresent with ttl > 0 (timers).
+// containsValue/size/isEmpty/clear and Delete read or reset a whole map: they are batch barriers applied by
+// map_wide.hip.  Not applied on the GPU (the batch fails with CC_ERR_UNSUPPORTED): put/putIfAbsent/replace/
+// replaceIfPresent with ttl > 0 (timers).
 #include "common.h"
 #include "engine_internal.h"
 #include "map_ops.h"
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
                                                   uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
+                                                  unsigned long long* __restrict__ dropped,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                   uint32_t* __restrict__ err_out) {
   __shared__ uint64_t tkey[kMapRegion];
@@ -110,6 +112,8 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       // live keys are distinct: claim the first free slot of each probe chain (no key comparisons needed)
 #pragma unroll
       for (int q = 0; q < kMEPer; ++q) {
+        // a bound key that is absent now is dropped: it still counts toward its map's peak-size bound
+        if ((ew[q] & kMwUsed) && !(ew[q] & (kMwPresent | kMwDead)) && dropped) atomicAdd(&dropped[ew[q] & kMwSlotMask], 1ull);
         if ((ew[q] & kMwPresent) && !(ew[q] & kMwDead)) {
           const uint32_t res = ew[q] & kMwSlotMask, kt = (ew[q] >> 17) & 3;
           uint32_t p = (uint32_t)map_hash(res, kt, ek[q]) & (kMapRegion - 1);
@@ -462,7 +466,8 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.map_bits == 0 || a.tiles == 0) return 0;
   a.mark(K_APPLY_MAP, 1, st);
   hipLaunchKernelGGL(k_apply_map, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
-                     a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins, a.rst_status,
+                     a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+                     (unsigned long long*)a.dropped, a.rst_status,
                      a.rst_value, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

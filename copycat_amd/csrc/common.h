@@ -181,6 +181,7 @@ struct EvRec {
   uint8_t code, tag, src, pad[3];
 };
 constexpr uint32_t kErrTime = 8u;  // the time column decreased inside a batch
+constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration order is undetermined (map_wide.hip)
 
 // extended staging (partition.hip) options
 constexpr uint32_t kExtValue = 1u;     // value records carry the extended columns (value events on the GPU)

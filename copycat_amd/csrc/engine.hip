@@ -81,6 +81,13 @@ struct cc_engine {
   // hot map keys (apply_map_hot.hip)
   HotKey* d_hot = nullptr;
   uint32_t* d_hot_n = nullptr;
+  // whole-map ops (map_wide.hip): barrier rows of the current batch, per-map peak-size bounds, scratch
+  uint32_t* d_bar = nullptr;       // [kBarCap]
+  uint32_t* d_bar_n = nullptr;
+  uint32_t* d_mw_peak = nullptr;   // [max_resources]
+  uint64_t* d_mw_drop = nullptr;   // [max_resources]
+  unsigned long long* d_mw_ctl = nullptr;  // [16]
+  std::vector<uint32_t> bars;
   uint32_t* d_hot_rpre = nullptr;
   uint32_t* d_hot_rstart = nullptr;
   uint32_t* d_hot_len = nullptr;
@@ -164,7 +171,8 @@ static void free_all(cc_engine* e) {
                   e->d_st_key,   e->d_st_idx,   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
-                  e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16};
+                  e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
+                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -277,6 +285,11 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_tbl_ins, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_hot, sizeof(HotKey) * kHotMax);
     ALLOC(e->d_hot_n, sizeof(uint32_t));
+    ALLOC(e->d_bar, sizeof(uint32_t) * kBarCap);
+    ALLOC(e->d_bar_n, sizeof(uint32_t));
+    ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
+    ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
+    ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
     ALLOC(e->d_hot_rpre, sizeof(uint32_t) * kHotMax * (kMaxTiles + 1));
     ALLOC(e->d_hot_rstart, sizeof(uint32_t) * kHotMax * kMaxTiles);
     ALLOC(e->d_hot_len, sizeof(uint32_t) * kHotMax);
@@ -307,6 +320,8 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_tbl_ci, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_ins, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_hot_n, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_mw_peak, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_mw_drop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
   }
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
   // the stable rankings of k_part_scatter / k_apply_value need same-address LDS atomics of one wave
@@ -351,13 +366,16 @@ static int check_device_err(cc_engine* e) {
   if (err) {
     HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
     if (err & kErrTime) return set_err(CC_ERR_INVALID, "the time column must be non-decreasing within a batch");
+    if (err & kErrMapOrder)
+      return set_err(CC_ERR_STATE, "map containsValue: the answer depends on java.util.HashMap iteration order and the "
+                                   "map's table capacity (peak size) is not determined exactly by the engine's bounds");
     if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
     if (err & kErrCapacity)
       return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, lock queue, listeners, members)");
     if (err & kErrUnsupported)
       return set_err(CC_ERR_UNSUPPORTED,
                      "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten without "
-                     "CC_CFG_VALUE_EVENTS; map containsValue/size/isEmpty/clear/Delete; map ops with ttl > 0; group "
+                     "CC_CFG_VALUE_EVENTS; map ops with ttl > 0; group "
                      "schedule) or published events with no event stream");
     return set_err(CC_ERR_STATE, "device-side check failed");
   }
@@ -404,6 +422,10 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
   if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)first * kCoordBlock, 0, kCoordBlock * (uint64_t)count));
+  if (type == CC_RES_MAP) {  // a new HashMap: capacity 16, no history
+    HIPCHECK(hipMemset(e->d_mw_peak + first, 0, sizeof(uint32_t) * count));
+    HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
+  }
   // fresh state: AtomicValueState() {value = null; current = null}
   HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
   HIPCHECK(hipMemset(e->d_val_v + first, 0, sizeof(uint64_t) * count));
@@ -502,8 +524,27 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), st));
     if (launch_time_check(c->time, n, e->d_clock, e->d_err, st)) return set_err(CC_ERR_HIP, "time check", hipGetLastError());
   }
-  for (uint64_t lo = 0; lo < n; lo += e->sub_batch) {
-    const uint64_t hi = std::min(n, lo + e->sub_batch);
+  // Whole-map ops are barriers (map_wide.hip): find them (one sync), then apply the rows between them as segments.
+  e->bars.clear();
+  if (e->map_bits) {
+    if (launch_map_barriers(c->inst, c->op, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar, e->d_bar_n,
+                            kBarCap, st))
+      return set_err(CC_ERR_HIP, "map barrier scan launch", hipGetLastError());
+    uint32_t nb = 0;
+    HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (nb > kBarCap) return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) in one batch than kBarCap");
+    if (nb) {
+      e->bars.resize(nb);
+      HIPCHECK(hipMemcpy(e->bars.data(), e->d_bar, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost));
+      std::sort(e->bars.begin(), e->bars.end());
+    }
+  }
+  for (size_t seg = 0; seg <= e->bars.size(); ++seg) {
+  const uint64_t seg_lo = seg == 0 ? 0 : (uint64_t)e->bars[seg - 1] + 1;
+  const uint64_t seg_hi = seg < e->bars.size() ? (uint64_t)e->bars[seg] : n;
+  for (uint64_t lo = seg_lo; lo < seg_hi; lo += e->sub_batch) {
+    const uint64_t hi = std::min(seg_hi, lo + e->sub_batch);
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
     HotArgs ha{};
     if (e->map_bits) {  // hot map keys of this sub-batch (routed to their own buckets by the partition)
@@ -612,6 +653,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.tbl_val = e->d_tbl_val;
       ma.tbl_ci = e->d_tbl_ci;
       ma.tbl_ins = e->d_tbl_ins;
+      ma.dropped = e->d_mw_drop;
       ma.rst_status = e->d_rst_status;
       ma.rst_value = e->d_rst_value;
       ma.err = e->d_err;
@@ -689,6 +731,36 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ea.mark = marker_of(e);
       if (launch_events(ea, st)) return set_err(CC_ERR_HIP, "events launch", hipGetLastError());
     }
+  }
+  if (seg < e->bars.size()) {  // the barrier row, against the table as it stands after the rows before it
+    const uint64_t row = seg_hi;
+    uint32_t in = 0, res = 0;
+    uint8_t op = 0, fl = 0;
+    uint64_t a = 0;
+    HIPCHECK(hipMemcpy(&in, c->inst + row, sizeof in, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&op, c->op + row, 1, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&fl, c->flags + row, 1, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&a, c->a + row, sizeof a, hipMemcpyDeviceToHost));
+    res = e->inst_res[in];
+    MapWideArgs mw{};
+    mw.slot = res;
+    mw.op = op;
+    mw.atag = CC_FLAG_TAG_A(fl);
+    mw.apay = a;
+    mw.row = row;
+    mw.tbl_word = e->d_tbl_word;
+    mw.tbl_key = e->d_tbl_key;
+    mw.tbl_val = e->d_tbl_val;
+    mw.tbl_ins = e->d_tbl_ins;
+    mw.entries = e->map_entries;
+    mw.peak_lo = e->d_mw_peak;
+    mw.dropped = e->d_mw_drop;
+    mw.ctl = e->d_mw_ctl;
+    mw.out_status = out->status;
+    mw.out_value = out->value;
+    mw.err = e->d_err;
+    if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError());
+  }
   }
   if (e->coord_on) {
     if (ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));

@@ -94,6 +94,7 @@ struct MapArgs {
   uint64_t* tbl_val;
   uint64_t* tbl_ci;
   uint64_t* tbl_ins;
+  uint64_t* dropped;  // [max_resources] compaction drops bound-but-absent entries: counted per map (map_wide.hip)
   uint8_t* rst_status;
   uint64_t* rst_value;
   uint32_t* err;
@@ -101,6 +102,29 @@ struct MapArgs {
 };
 int launch_apply_map(const MapArgs& a, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
+
+// Whole-map ops (containsValue / isEmpty / size / clear / Delete): barrier rows of a batch (map_wide.hip).
+constexpr uint32_t kBarCap = 1u << 16;  // barrier rows per batch
+int launch_map_barriers(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res,
+                        const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
+                        hipStream_t st);
+struct MapWideArgs {
+  uint32_t slot, op, atag;
+  uint64_t apay;
+  uint64_t row;  // absolute row of the barrier in the batch
+  uint32_t* tbl_word;
+  const uint64_t* tbl_key;
+  const uint64_t* tbl_val;
+  const uint64_t* tbl_ins;
+  uint64_t entries;
+  uint32_t* peak_lo;           // [max_resources] lower bound on the map's peak size
+  uint64_t* dropped;           // [max_resources] entries dropped by compaction / clear (upper-bound term)
+  unsigned long long* ctl;     // [C_N] scratch
+  uint8_t* out_status;
+  uint64_t* out_value;
+  uint32_t* err;
+};
+int launch_map_wide(const MapWideArgs& a, hipStream_t st);
 
 constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
 struct HotArgs {

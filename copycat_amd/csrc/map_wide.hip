@@ -1,0 +1,218 @@
+// map_wide.hip — MapState operations that read or reset a whole map: containsValue :49-60, isEmpty :244-250,
+// size :233-239, clear :255-261 and the map's DeleteCommand (ResourceStateMachine.java:34-40 -> MapState.delete
+// :264-274) (collections/src/main/java/io/atomix/collections/state/MapState.java).
+//
+// A map's keys are spread over every table region (apply_map.hip), so these ops cannot run inside the region
+// kernel.  They are *barriers*: cc_apply_batch finds them first (k_map_barriers), applies the rows between two
+// barriers as an ordinary segment (partition + region apply), then applies the barrier row against the table as
+// it stands at that log position:
+//   k_mw_count   every entry of the map: live size, bound entries, stored nulls, values equal to the operand;
+//   k_mw_order   containsValue only, when the answer depends on java.util.HashMap iteration order (the map
+//                stores a null AND a match: the first of them in iteration order decides NPE vs true, A5);
+//   k_mw_finish  the row's status/value, the map's peak-size bound; clear/Delete then drop the entries
+//                (k_map_drop, apply_map.hip).
+//
+// Iteration order (oracle/oracle.cpp JavaOrder): bucket = Java hash & (capacity - 1), then insertion order in
+// the bucket (= the commit index that created the node, tbl_ins).  The capacity is a function of the map's peak
+// size (HashMap.resize doubles it when ++size > 0.75 * capacity and never shrinks it).  The engine keeps a lower
+// bound on the peak (sizes seen at barriers) and an upper bound (bound entries + entries dropped by compaction or
+// clear: every key that was ever present owned one).  When the two bounds give different capacities and the
+// order matters, the batch fails with CC_ERR_STATE ("order undetermined") instead of guessing.
+#include <algorithm>
+
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+constexpr int kMwT = 256;
+
+__device__ inline bool map_wide_op(uint32_t op) {
+  return op == CC_OP_DELETE || op == CC_OP_MAP_CONTAINSVALUE || op == CC_OP_MAP_ISEMPTY || op == CC_OP_MAP_SIZE ||
+         op == CC_OP_MAP_CLEAR;
+}
+
+// Rows whose instance is open on a live map and whose op reads or resets the whole map.
+__global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                      uint64_t n, const uint32_t* __restrict__ inst_res,
+                                                      const uint8_t* __restrict__ res_type, uint32_t max_inst,
+                                                      uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
+  if (i >= n) return;
+  if (!map_wide_op(op[i])) return;
+  const uint32_t in = inst[i];
+  if (in >= max_inst) return;
+  const uint32_t r = inst_res[in];
+  if (r == kNoRes || res_type[r] != CC_RES_MAP) return;
+  const uint32_t k = atomicAdd(bar_n, 1u);
+  if (k < cap) bar[k] = (uint32_t)i;
+}
+
+// java.lang.{Long,Integer,Boolean}.hashCode spread by HashMap.hash (oracle java_hash; HANDLE as Long).
+__device__ inline uint32_t java_hash_dev(uint32_t ktag, uint64_t v) {
+  uint32_t h;
+  switch (ktag) {  // key tags: 0 LONG, 1 INT, 2 BOOL, 3 HANDLE
+    case 1: h = (uint32_t)v; break;
+    case 2: h = v ? 1231u : 1237u; break;
+    default: h = (uint32_t)(v ^ (v >> 32)); break;
+  }
+  return h ^ (h >> 16);
+}
+// HashMap capacity after the map's size peaked at p (16, doubled while p > 0.75 * capacity).
+__device__ inline uint64_t java_cap(uint64_t p) {
+  uint64_t cap = 16, thr = 12;
+  while (p > thr) {
+    cap <<= 1;
+    thr <<= 1;
+  }
+  return cap;
+}
+
+// ctl layout (u64): 0 present, 1 bound (used, not dead), 2 stored nulls, 3 matches, 4/5 min bucket of a
+// null / a match, 6/7 min insertion index of a null / a match inside that bucket, 8 capacity (0 = undetermined)
+enum { C_PRES = 0, C_USED, C_NULLS, C_MATCH, C_BN, C_BM, C_IN, C_IM, C_CAP, C_N };
+
+__global__ void k_mw_reset(unsigned long long* ctl) {
+  const int t = threadIdx.x;
+  if (t < C_N) ctl[t] = (t >= C_BN && t <= C_IM) ? ~0ull : 0ull;
+}
+
+__device__ inline unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+__global__ __launch_bounds__(kMwT) void k_mw_count(const uint32_t* __restrict__ word, const uint64_t* __restrict__ val,
+                                                  uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag,
+                                                  uint64_t apay, unsigned long long* __restrict__ ctl) {
+  unsigned long long pres = 0, used = 0, nulls = 0, match = 0;
+  for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
+    const uint32_t w = word[e];
+    if (!(w & kMwUsed) || (w & kMwDead) || (w & kMwSlotMask) != slot) continue;
+    ++used;
+    if (!(w & kMwPresent)) continue;
+    ++pres;
+    if (op == CC_OP_MAP_CONTAINSVALUE) {
+      const uint32_t vt = mw_vtag(w);
+      if (vt == CC_TAG_NULL) ++nulls;
+      else if (vt == atag && val[e] == apay) ++match;
+    }
+  }
+  pres = wave_sum(pres);
+  used = wave_sum(used);
+  nulls = wave_sum(nulls);
+  match = wave_sum(match);
+  if ((threadIdx.x & 63) == 0 && used) {
+    atomicAdd(&ctl[C_PRES], pres);
+    atomicAdd(&ctl[C_USED], used);
+    if (nulls) atomicAdd(&ctl[C_NULLS], nulls);
+    if (match) atomicAdd(&ctl[C_MATCH], match);
+  }
+}
+
+// pass 0: the capacity, then the first bucket holding a null / a match; pass 1: inside the common first bucket,
+// the first insertion of each.  Runs only for an order-dependent containsValue (all threads read the same ctl).
+__global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ word, const uint64_t* __restrict__ key,
+                                                  const uint64_t* __restrict__ val, const uint64_t* __restrict__ ins,
+                                                  uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag, uint64_t apay,
+                                                  const uint32_t* __restrict__ peak_lo, const unsigned long long* __restrict__ dropped,
+                                                  int pass, unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
+  if (op != CC_OP_MAP_CONTAINSVALUE || ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0) return;
+  const uint64_t lo = max((uint64_t)peak_lo[slot], (uint64_t)ctl[C_PRES]);
+  const uint64_t hi = ctl[C_USED] + dropped[slot];
+  const uint64_t cap = java_cap(lo);
+  if (java_cap(hi) != cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && pass == 0) atomicOr(err, kErrMapOrder);
+    return;
+  }
+  if (pass == 1 && ctl[C_BN] != ctl[C_BM]) return;  // decided by the buckets
+  for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
+    const uint32_t w = word[e];
+    if (!(w & kMwPresent) || (w & kMwDead) || (w & kMwSlotMask) != slot) continue;
+    const uint32_t vt = mw_vtag(w);
+    const bool isnull = vt == CC_TAG_NULL;
+    if (!isnull && !(vt == atag && val[e] == apay)) continue;
+    const uint64_t b = java_hash_dev((w >> 17) & 3, key[e]) & (cap - 1);
+    if (pass == 0) {
+      atomicMin(&ctl[isnull ? C_BN : C_BM], (unsigned long long)b);
+    } else if (b == ctl[C_BN]) {
+      atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ins[e]);
+    }
+  }
+  if (pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) ctl[C_CAP] = cap;
+}
+
+// The barrier row's result (MapState.java :49-60 / :233-239 / :244-250 / :255-261 / :264-274) and the map's
+// peak-size bounds.
+__global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsigned long long* __restrict__ ctl,
+                            uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped, uint8_t* __restrict__ out_status,
+                            uint64_t* __restrict__ out_value) {
+  if (threadIdx.x != 0) return;
+  const uint64_t pres = ctl[C_PRES];
+  uint32_t st = CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+  uint64_t v = 0;
+  switch (op) {
+    case CC_OP_MAP_SIZE:  // int
+      st = CC_STATUS(CC_ST_OK, CC_TAG_INT);
+      v = (uint64_t)(int64_t)(int32_t)(uint32_t)pres;
+      break;
+    case CC_OP_MAP_ISEMPTY:
+      st = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+      v = pres == 0;
+      break;
+    case CC_OP_MAP_CONTAINSVALUE: {
+      const uint64_t nulls = ctl[C_NULLS], match = ctl[C_MATCH];
+      bool npe;
+      if (nulls == 0 || match == 0) {
+        npe = nulls != 0;
+      } else {  // the first of (null, match) in HashMap iteration order
+        const uint64_t bn = ctl[C_BN], bm = ctl[C_BM];
+        npe = bn != bm ? bn < bm : ctl[C_IN] < ctl[C_IM];
+      }
+      if (npe) {
+        st = CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
+      } else {
+        st = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+        v = match != 0;
+      }
+      break;
+    }
+    default:  // clear / Delete: every entry is dropped; the keys they held count toward the peak bound
+      dropped[slot] += ctl[C_USED];
+      break;
+  }
+  if (pres > peak_lo[slot]) peak_lo[slot] = (uint32_t)min(pres, (uint64_t)0xFFFFFFFFu);
+  out_status[row] = (uint8_t)st;
+  out_value[row] = v;
+}
+
+int launch_map_barriers(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res,
+                        const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
+                        hipStream_t st) {
+  if (hipMemsetAsync(bar_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, n, inst_res,
+                     res_type, max_inst, bar, bar_n, cap);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (a.entries + kMwT - 1) / kMwT);
+  const uint32_t atag = a.atag, op = a.op;
+  const uint64_t apay = atag == CC_TAG_NULL ? 0 : a.apay;  // canonical NULL payload
+  hipLaunchKernelGGL(k_mw_reset, dim3(1), dim3(64), 0, st, a.ctl);
+  hipLaunchKernelGGL(k_mw_count, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_val, a.entries, a.slot, op, atag, apay, a.ctl);
+  if (op == CC_OP_MAP_CONTAINSVALUE) {
+    for (int pass = 0; pass < 2; ++pass)
+      hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.entries,
+                         a.slot, op, atag, apay, a.peak_lo, (const unsigned long long*)a.dropped, pass, a.ctl, a.err);
+  }
+  hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,
+                     (unsigned long long*)a.dropped, a.out_status,
+                     a.out_value);
+  if (hipGetLastError() != hipSuccess) return -1;
+  if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE) return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, st);
+  return 0;
+}
+
+}  // namespace cc

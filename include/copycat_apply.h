@@ -232,6 +232,11 @@ int  cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t count, uint32
  * Apply n committed entries (device-resident columns) in log order.  Replaces the per-entry chain
  * ResourceManager.operateResource (ResourceManager.java:56-72) -> executors -> state machine method.
  * `events` may be NULL when no op in the batch publishes (then publishing ops fail with CC_ERR_UNSUPPORTED). */
+/* Map containsValue/size/isEmpty/clear/Delete rows (MapState.java:49-60,233-274) read or reset a whole map: on
+ * an engine with maps the call first scans the batch for them (one host sync), then applies the rows between
+ * them as segments and each such row against the table as it stands at its log position.  A containsValue whose
+ * answer depends on java.util.HashMap iteration order when the map's table capacity is not determined exactly
+ * fails the batch with CC_ERR_STATE (see copycat_amd/csrc/map_wide.hip). */
 /* d_out->status must be 4-byte aligned and d_out->value 16-byte aligned (hipMalloc / torch allocations are). */
 int  cc_apply_batch(cc_engine* e, const cc_batch* d_cols, uint64_t n, const cc_results* d_out,
                     const cc_events* d_events, void* stream);

@@ -159,9 +159,7 @@ def test_map_capacity_error():
     assert ei.value.rc == abi.CC_ERR_CAPACITY
 
 
-@pytest.mark.parametrize("op,aux", [(abi.CC_OP_MAP_CONTAINSVALUE, 0), (abi.CC_OP_MAP_SIZE, 0),
-                                    (abi.CC_OP_MAP_ISEMPTY, 0), (abi.CC_OP_MAP_CLEAR, 0), (abi.CC_OP_DELETE, 0),
-                                    (abi.CC_OP_MAP_PUT, 5), (abi.CC_OP_MAP_REPLACE, 1)])
+@pytest.mark.parametrize("op,aux", [(abi.CC_OP_MAP_PUT, 5), (abi.CC_OP_MAP_REPLACE, 1)])
 def test_map_ops_not_on_gpu_fail_loudly(op, aux):
     from copycat_amd.engine import EngineError
 
@@ -213,3 +211,130 @@ def test_map_zipf_stream_parity():
     E, O = _engines(maps, maps, n, 1 << 20)
     _assert_rows(*_apply_both(E, O, [b]))
     _assert_maps(E, O, range(0, maps, 97))
+
+
+# ---- whole-map ops: containsValue / size / isEmpty / clear / Delete (MapState.java:49-60, 233-274) ----------
+
+_WIDE = np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_ISEMPTY, abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_CLEAR,
+                  abi.CC_OP_DELETE], np.uint8)
+
+
+def _with_barriers(b, rate, seed, ops=_WIDE, p=None):
+    """Turn a share of a key-op stream's rows into whole-map ops (operand a of containsValue: a small Long)."""
+    rng = np.random.default_rng(seed)
+    rows = np.nonzero(rng.random(len(b)) < rate)[0]
+    b.op[rows] = rng.choice(ops, size=len(rows), p=p)
+    cv = rows[b.op[rows] == abi.CC_OP_MAP_CONTAINSVALUE]
+    b.a[cv] = rng.integers(0, 3, len(cv)).astype(np.uint64)
+    b.flags[cv] = (b.flags[cv] & np.uint8(0xF8)) | np.uint8(abi.CC_TAG_LONG)
+    return rows
+
+
+def _no_null_values(b):
+    """Key ops store non-null values only: containsValue is then independent of HashMap iteration order."""
+    f = b.flags
+    ta, tb = f & 7, (f >> 3) & 7
+    f[ta == abi.CC_TAG_NULL] |= np.uint8(abi.CC_TAG_LONG)
+    f[tb == abi.CC_TAG_NULL] |= np.uint8(abi.CC_TAG_LONG << 3)
+
+
+@pytest.mark.parametrize("n,maps,keys,rate,sub_batch,hot,p_hot,seed", [
+    (2_000, 2, 16, 0.02, 0, 0, 0.0, 71),
+    (50_000, 8, 64, 0.002, 0, 0, 0.0, 72),
+    (200_000, 64, 256, 0.0005, 32768, 2, 0.3, 73),   # barriers inside and across sub-batches, hot keys
+])
+def test_map_wide_ops_parity(n, maps, keys, rate, sub_batch, hot, p_hot, seed):
+    """size/isEmpty/containsValue/clear/Delete rows split the batch into segments; each is applied against the
+    table exactly as it stands at its log position."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed, hot=hot, p_hot=p_hot)
+    _no_null_values(b)
+    rows = _with_barriers(b, rate, seed)
+    assert len(rows) > 0
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch)
+    gs, gv, os_, ov = _apply_both(E, O, [b])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    wide = gs[rows]
+    assert (wide == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_INT)).any()  # some size rows landed on live maps
+
+
+def test_map_contains_value_iteration_order():
+    """A map holding both null values and matches: containsValue NPEs iff a null comes first in
+    java.util.HashMap iteration order (A5, MapState.java:52).  Puts only, so the peak size (and with it the
+    table capacity) is exact."""
+    rng = np.random.default_rng(81)
+    E, O = _engines(3, 8, 4096, 8192)
+    idx = 1
+    seen_npe = seen_true = 0
+    for step in range(6):
+        k = rng.integers(0, 1 << 40, 150).astype(np.uint64)
+        b = _puts(k, int(step % 3), index0=idx)
+        tags = rng.choice([abi.CC_TAG_NULL, abi.CC_TAG_LONG, abi.CC_TAG_INT], size=len(k), p=[0.1, 0.6, 0.3])
+        b.flags[:] = tags.astype(np.uint8)
+        b.a[:] = rng.integers(0, 40, len(k)).astype(np.uint64)
+        b.key[::7] = (b.key[::7] & np.uint64(0x7FFFFFFF))  # Integer-sized keys in some rows
+        b.flags[::7] |= np.uint8(1 << 6)                  # ... with the Integer key tag
+        cv = np.arange(5, len(k), 5)
+        b.op[cv] = abi.CC_OP_MAP_CONTAINSVALUE
+        b.a[cv] = rng.integers(0, 40, len(cv)).astype(np.uint64)
+        gs, gv, os_, ov = _apply_both(E, O, [b])
+        _assert_rows(gs, gv, os_, ov)
+        seen_npe += int((gs[cv] == abi.cc_status(abi.CC_ST_NULL_POINTER, abi.CC_TAG_NULL)).sum())
+        seen_true += int(((gs[cv] == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_BOOL)) & (gv[cv] == 1)).sum())
+        idx += len(k)
+    assert seen_npe > 0 and seen_true > 0
+    _assert_maps(E, O, range(3))
+
+
+def test_map_contains_value_undetermined_capacity_fails_loudly():
+    """Peak 30 (capacity 64) is not observed by any barrier and 25 keys were removed since: the engine's bounds
+    (15 live .. 40 bound) straddle a resize, so an order-dependent containsValue fails with CC_ERR_STATE
+    instead of guessing.  A size barrier at the peak pins the capacity and the same query becomes exact."""
+    from copycat_amd.engine import EngineError
+
+    def stream(with_size):
+        keys = np.arange(30, dtype=np.uint64) * np.uint64(1 << 20) + np.uint64(5)
+        b1 = _puts(keys, 0)
+        b1.flags[::3] = np.uint8(abi.CC_TAG_NULL)  # some stored nulls
+        b1.a[:] = 7
+        parts = [b1]
+        if with_size:
+            parts.append(_puts([0], 0, op=abi.CC_OP_MAP_SIZE, index0=31))
+        parts.append(_puts(keys[:25], 0, op=abi.CC_OP_MAP_REMOVE, index0=40))
+        b3 = _puts(np.arange(10, dtype=np.uint64) + np.uint64(1 << 50), 0, index0=70)
+        b3.a[:] = 7
+        parts.append(b3)
+        q = _puts([0], 0, op=abi.CC_OP_MAP_CONTAINSVALUE, index0=90)
+        q.a[:] = 7
+        parts.append(q)
+        return parts
+
+    E, O = _engines(1, 4, 64, 1024)
+    parts = stream(False)
+    _apply_both(E, O, parts[:-1])
+    with pytest.raises(EngineError) as ei:
+        E.apply_host(parts[-1])
+    assert ei.value.rc == abi.CC_ERR_STATE
+    E, O = _engines(1, 4, 64, 1024)
+    _assert_rows(*_apply_both(E, O, stream(True)))
+    _assert_maps(E, O, [0])
+
+
+def test_map_clear_then_reuse_keys():
+    """clear / Delete drop every entry of one map (other maps keep theirs); the same keys are then re-put
+    as new HashMap nodes; size and isEmpty follow."""
+    E, O = _engines(2, 4, 256, 1024)
+    k = np.arange(40, dtype=np.uint64)
+    parts = [_puts(k, 0), _puts(k, 1, index0=41)]
+    for i, op in enumerate([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_CLEAR, abi.CC_OP_MAP_ISEMPTY, abi.CC_OP_MAP_SIZE]):
+        parts.append(_puts([0], 0, op=op, index0=100 + i))
+    parts.append(_puts(k[:10], 0, index0=200))
+    parts.append(_puts([0, 0], 0, op=abi.CC_OP_MAP_SIZE, index0=300))
+    parts.append(_puts([0], 1, op=abi.CC_OP_DELETE, index0=400))
+    parts.append(_puts([0, 0], 1, op=abi.CC_OP_MAP_ISEMPTY, index0=500))
+    one = Batch.from_columns(**{name: np.concatenate([getattr(x, name) for x in parts]) for name, _ in abi.BATCH_COLUMNS})
+    _assert_rows(*_apply_both(E, O, [one]))
+    _assert_maps(E, O, [0, 1])
