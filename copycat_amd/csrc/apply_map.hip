@@ -27,7 +27,7 @@
 //   removeIfPresent :159-178, replace :183-202, replaceIfPresent :207-228 (stores `value`, compares `replace`).
 // containsValue/size/isEmpty/clear and Delete read or reset a whole map: they are batch barriers applied by
 // map_wide.hip.  Not applied on the GPU (the batch fails with CC_ERR_UNSUPPORTED): put/putIfAbsent/replace/
-// replaceIfPresent with ttl > 0 (timers).
+// replaceIfPresent with ttl > 0 before the engine enters TTL mode (k_apply_map<true>: see below).
 #include "common.h"
 #include "engine_internal.h"
 #include "map_ops.h"
@@ -35,14 +35,18 @@
 namespace cc {
 
 constexpr int kMT = 256;                // threads per region workgroup
-constexpr int kMPer = 4;                // commits per thread per chunk
-constexpr int kMCh = kMT * kMPer;       // 1024 commits per chunk
 constexpr int kMEPer = kMapRegion / kMT;  // table entries per thread (8)
 constexpr uint32_t kNoEnt = 0xFFFFu;
 constexpr uint32_t kEntFull = 0xFFFEu;
 
 __device__ inline uint32_t map_ident_of(uint32_t res, uint32_t flags) { return mw_ident(res, CC_FLAG_KTAG(flags)); }
 
+// TTL: the map table has live TTL timers (MapState.java:91-93,119-121,189-192,218-220).  Every entry then carries
+// its timer's deadline (tbl_dl, 0 = none) and every run is walked sequentially: before each commit the entry
+// expires if its deadline is <= the clock at which the reference last fired timers (module mode: this commit's
+// clock; manager mode: the previous commit's, A8), and a commit that stores a value re-arms or cancels the timer.
+// The per-record clocks come from the input columns through map_row (staging position -> batch row).
+template <bool TTL>
 __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
                                                   const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
                                                   const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
@@ -50,8 +54,13 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
                                                   uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
                                                   unsigned long long* __restrict__ dropped,
+                                                  uint64_t* __restrict__ tbl_dl, const uint32_t* __restrict__ map_row,
+                                                  const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
+                                                  const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                   uint32_t* __restrict__ err_out) {
+  constexpr int kMPer = TTL ? 2 : 4;  // commits per thread per chunk (the TTL variant's LDS holds deadlines)
+  constexpr int kMCh = kMT * kMPer;
   __shared__ uint64_t tkey[kMapRegion];
   __shared__ uint32_t tword[kMapRegion];
   __shared__ uint64_t tval[kMapRegion];
@@ -62,6 +71,9 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
   __shared__ uint32_t rpos[kMCh];      // staging position
   __shared__ uint64_t ridx[kMCh];      // commit index
   __shared__ uint16_t rent[kMCh];      // entry
+  __shared__ uint64_t tdl[TTL ? kMapRegion : 1];  // timer deadline of the entry (0: none)
+  __shared__ uint64_t rfire[TTL ? kMCh : 1];      // clock of the last timer firing before the commit
+  __shared__ uint64_t rdl[TTL ? kMCh : 1];        // deadline the commit arms if it stores (0: none)
   __shared__ uint32_t ecnt[kMapRegion + 1];  // commits per entry in the chunk -> run starts
   __shared__ uint32_t eflag[kMapRegion];     // the entry's run holds a value-comparing op
   __shared__ Comp wcomp[kMT / kWave];
@@ -82,7 +94,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
   for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
   for (uint32_t q = t; q < kMapRegion; q += kMT) eflag[q] = 0;
   {
-    uint64_t ek[kMEPer], ev[kMEPer], eci[kMEPer], eins[kMEPer];
+    uint64_t ek[kMEPer], ev[kMEPer], eci[kMEPer], eins[kMEPer], edl[kMEPer];
     uint32_t ew[kMEPer], used = 0;
 #pragma unroll
     for (int q = 0; q < kMEPer; ++q) {
@@ -92,6 +104,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       ev[q] = tbl_val[tb + e];
       eci[q] = tbl_ci[tb + e];
       eins[q] = tbl_ins[tb + e];
+      edl[q] = TTL ? tbl_dl[tb + e] : 0;
       used += (ew[q] & kMwUsed) ? 1 : 0;
     }
     lds_barrier();
@@ -106,6 +119,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       tval[e] = ev[q];
       tci[e] = eci[q];
       tins[e] = eins[q];
+      if (TTL) tdl[e] = compact ? 0 : edl[q];
     }
     lds_barrier();
     if (compact) {
@@ -122,6 +136,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
           tval[p] = ev[q];
           tci[p] = eci[q];
           tins[p] = eins[q];
+          if (TTL) tdl[p] = edl[q];
         }
       }
       lds_barrier();
@@ -191,7 +206,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
         key[j] = st_key[g[j]];
         idx[j] = st_idx[g[j]];
         const uint32_t op = smeta_op(m[j]);
-        keyop[j] = map_key_op(op) && !(map_reads_ttl(op) && (m[j] & kMetaTtl));
+        keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
         ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
         p[j] = (uint32_t)map_hash(res[j], CC_FLAG_KTAG(smeta_flags(m[j])), key[j]) & (kMapRegion - 1);
       }
@@ -269,7 +284,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       if (ent[j] == kNoEnt || !keyop[j]) {
         ent[j] = kNoEnt;
         uint64_t rv;
-        const uint32_t s = map_orphan(smeta_op(m[j]), m[j], smeta_flags(m[j]), ab[j].x, ab[j].y, rv, err);
+        const uint32_t s = map_orphan(smeta_op(m[j]), TTL ? (m[j] & ~kMetaTtl) : m[j], smeta_flags(m[j]), ab[j].x, ab[j].y, rv, err);
         rst_status[g[j]] = (uint8_t)s;
         rst_value[g[j]] = rv;
       }
@@ -318,7 +333,19 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       rpos[s] = g[j];
       ridx[s] = idx[j];
       rent[s] = (uint16_t)ent[j];
-      if (compares_value(m[j])) eflag[ent[j]] = 1;
+      if (TTL) {
+        const uint64_t cb = clock_base ? *clock_base : 0;
+        const uint32_t row = map_row[g[j]];
+        const uint64_t ti = ctime ? max(ctime[row], cb) : cb;
+        const uint64_t tp = ctime && row > 0 ? max(ctime[row - 1], cb) : cb;
+        const uint32_t op = smeta_op(m[j]);
+        const int64_t ttl = caux && map_reads_ttl(op) ? (int64_t)caux[row] : 0;
+        rfire[s] = deferred ? tp : ti;
+        rdl[s] = ttl > 0 ? ti + (uint64_t)ttl : 0;
+        eflag[ent[j]] = 1;  // every run is walked in order
+      } else if (compares_value(m[j])) {
+        eflag[ent[j]] = 1;
+      }
     }
     lds_barrier();
     // ---- 4. every run (one entry's commits, log order) at once: a segmented scan of the commits'
@@ -417,14 +444,23 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       const uint32_t e = ent[j];
       const uint32_t s0 = ecnt[e], s1 = ecnt[e + 1];
       uint32_t wv = tword[e];
-      uint64_t vv = tval[e], ci = 0, ins = 0;
+      uint64_t vv = tval[e], ci = 0, ins = 0, dl = TTL ? tdl[e] : 0;
       bool any_w = false, any_c = false;
       for (uint32_t s = s0; s < s1; ++s) {
         const uint32_t mm = rmeta[s];
         const u64x2 x = rab[s];
         uint64_t rv;
         bool wrote, created;
+        if (TTL && dl && dl <= rfire[s]) {  // the timer fired: map.remove(key) (MapState.java:91-93)
+          wv &= ~(kMwPresent | kMwVtagMask);
+          vv = 0;
+          dl = 0;
+        }
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, wv, vv, rv, wrote, created);
+        if (TTL) {  // a stored commit cancels the old timer and arms its own; a removal cancels it
+          if (wrote) dl = rdl[s];
+          else if (!(wv & kMwPresent)) dl = 0;
+        }
         rst_status[rpos[s]] = (uint8_t)st;
         rst_value[rpos[s]] = rv;
         if (wrote) { ci = ridx[s]; any_w = true; }
@@ -432,6 +468,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       }
       tword[e] = wv;
       tval[e] = vv;
+      if (TTL) tdl[e] = dl;
       if (any_w) tci[e] = ci;
       if (any_c) tins[e] = ins;
     }
@@ -450,6 +487,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
     tbl_val[tb + e] = tval[e];
     tbl_ci[tb + e] = tci[e];
     tbl_ins[tb + e] = tins[e];
+    if (TTL) tbl_dl[tb + e] = tdl[e];
   }
   if (err) atomicOr(err_out, err);
 }
@@ -465,11 +503,31 @@ __global__ void k_map_drop(uint32_t* __restrict__ tbl_word, uint64_t entries, ui
 int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.map_bits == 0 || a.tiles == 0) return 0;
   a.mark(K_APPLY_MAP, 1, st);
-  hipLaunchKernelGGL(k_apply_map, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
-                     a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
-                     (unsigned long long*)a.dropped, a.rst_status,
-                     a.rst_value, a.err);
+  if (a.ttl)
+    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
+                       a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+                       (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
+                       a.rst_status, a.rst_value, a.err);
+  else
+    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
+                       a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+                       (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
+                       a.rst_status, a.rst_value, a.err);
   a.mark(K_APPLY_MAP, 0, st);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// staging position -> batch row for the map records of a sub-batch (the TTL variant reads each commit's clock)
+__global__ void k_map_rows(const uint16_t* __restrict__ cpos, uint64_t lo, uint64_t hi, uint32_t* __restrict__ map_row) {
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  const uint16_t c = cpos[i - lo];
+  if (c == 0xFFFF) return;
+  map_row[((i - lo) / kTile) * kTile + c] = (uint32_t)i;
+}
+
+int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* map_row, hipStream_t st) {
+  hipLaunchKernelGGL(k_map_rows, dim3((uint32_t)((hi - lo + 255) / 256)), dim3(256), 0, st, cpos, lo, hi, map_row);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

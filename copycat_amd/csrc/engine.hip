@@ -88,6 +88,11 @@ struct cc_engine {
   uint64_t* d_mw_drop = nullptr;   // [max_resources]
   unsigned long long* d_mw_ctl = nullptr;  // [16]
   std::vector<uint32_t> bars;
+  // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good
+  uint64_t* d_tbl_dl = nullptr;    // [map_entries] timer deadline per entry (0: none)
+  uint32_t* d_map_row = nullptr;   // [sub_batch] staging position -> batch row
+  uint32_t* d_ttl_seen = nullptr;
+  bool ttl_live = false;
   uint32_t* d_hot_rpre = nullptr;
   uint32_t* d_hot_rstart = nullptr;
   uint32_t* d_hot_len = nullptr;
@@ -172,7 +177,8 @@ static void free_all(cc_engine* e) {
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
-                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl};
+                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
+                  e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -290,6 +296,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
+    ALLOC(e->d_tbl_dl, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_map_row, sizeof(uint32_t) * e->sub_batch);
+    ALLOC(e->d_ttl_seen, sizeof(uint32_t));
     ALLOC(e->d_hot_rpre, sizeof(uint32_t) * kHotMax * (kMaxTiles + 1));
     ALLOC(e->d_hot_rstart, sizeof(uint32_t) * kHotMax * kMaxTiles);
     ALLOC(e->d_hot_len, sizeof(uint32_t) * kHotMax);
@@ -322,6 +331,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_hot_n, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_peak, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_drop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_tbl_dl, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
   }
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
   // the stable rankings of k_part_scatter / k_apply_value need same-address LDS atomics of one wave
@@ -375,7 +385,7 @@ static int check_device_err(cc_engine* e) {
     if (err & kErrUnsupported)
       return set_err(CC_ERR_UNSUPPORTED,
                      "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten without "
-                     "CC_CFG_VALUE_EVENTS; map ops with ttl > 0; group "
+                     "CC_CFG_VALUE_EVENTS; group "
                      "schedule) or published events with no event stream");
     return set_err(CC_ERR_STATE, "device-side check failed");
   }
@@ -520,19 +530,20 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if (e->map_bits && !c->key) return set_err(CC_ERR_INVALID, "an engine with maps needs the key column");
   if (ev && (!ev->pos || !ev->target || !ev->code || !ev->src || !ev->tag || !ev->payload || !ev->count))
     return set_err(CC_ERR_INVALID, "event stream columns and count are required");
-  if (e->coord_on) {  // events of this batch start at 0; the log clock must not go backwards inside it
-    HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), st));
-    if (launch_time_check(c->time, n, e->d_clock, e->d_err, st)) return set_err(CC_ERR_HIP, "time check", hipGetLastError());
-  }
   // Whole-map ops are barriers (map_wide.hip): find them (one sync), then apply the rows between them as segments.
   e->bars.clear();
+  uint64_t clock_before = 0;  // the engine clock before this batch (TTL mode and barrier rows need it on the host)
   if (e->map_bits) {
-    if (launch_map_barriers(c->inst, c->op, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar, e->d_bar_n,
-                            kBarCap, st))
+    HIPCHECK(hipMemsetAsync(e->d_ttl_seen, 0, sizeof(uint32_t), st));
+    if (launch_map_barriers(c->inst, c->op, c->aux, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar,
+                            e->d_bar_n, kBarCap, e->d_ttl_seen, st))
       return set_err(CC_ERR_HIP, "map barrier scan launch", hipGetLastError());
-    uint32_t nb = 0;
+    uint32_t nb = 0, ttl_seen = 0;
     HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+    if (ttl_seen) e->ttl_live = true;
     if (nb > kBarCap) return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) in one batch than kBarCap");
     if (nb) {
       e->bars.resize(nb);
@@ -540,14 +551,21 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       std::sort(e->bars.begin(), e->bars.end());
     }
   }
+  if (e->coord_on || e->ttl_live) {  // events of this batch start at 0; the log clock must not go backwards inside it
+    if (e->coord_on) HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), st));
+    if (launch_time_check(c->time, n, e->d_clock, e->d_err, st)) return set_err(CC_ERR_HIP, "time check", hipGetLastError());
+  }
   for (size_t seg = 0; seg <= e->bars.size(); ++seg) {
   const uint64_t seg_lo = seg == 0 ? 0 : (uint64_t)e->bars[seg - 1] + 1;
   const uint64_t seg_hi = seg < e->bars.size() ? (uint64_t)e->bars[seg] : n;
   for (uint64_t lo = seg_lo; lo < seg_hi; lo += e->sub_batch) {
     const uint64_t hi = std::min(seg_hi, lo + e->sub_batch);
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
+    if (e->map_bits && e->ttl_live) {  // TTL mode: every key goes through its region (timers are walked in order)
+      HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
+    }
     HotArgs ha{};
-    if (e->map_bits) {  // hot map keys of this sub-batch (routed to their own buckets by the partition)
+    if (e->map_bits && !e->ttl_live) {  // hot map keys of this sub-batch (routed to their own buckets by the partition)
       ha.inst = c->inst;
       ha.flags = c->flags;
       ha.key = c->key;
@@ -619,6 +637,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.res16 = e->ext ? nullptr : e->d_res16;
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
+    if (e->map_bits && e->ttl_live && launch_map_rows(e->d_cpos, lo, hi, e->d_map_row, st))
+      return set_err(CC_ERR_HIP, "map rows launch", hipGetLastError());
     ValueArgs va{};
     va.st_meta = e->d_st_meta;
     va.st_ab = e->d_st_ab;
@@ -636,7 +656,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.mark = marker_of(e);
     if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
     if (e->map_bits) {
-      if (launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
+      if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
       ma.st_meta = e->d_st_meta;
       ma.st_ab = e->d_st_ab;
@@ -654,6 +674,13 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.tbl_ci = e->d_tbl_ci;
       ma.tbl_ins = e->d_tbl_ins;
       ma.dropped = e->d_mw_drop;
+      ma.ttl = e->ttl_live;
+      ma.tbl_dl = e->d_tbl_dl;
+      ma.map_row = e->d_map_row;
+      ma.time = c->time;
+      ma.aux = c->aux;
+      ma.clock_base = e->d_clock;
+      ma.deferred = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) != 0;
       ma.rst_status = e->d_rst_status;
       ma.rst_value = e->d_rst_value;
       ma.err = e->d_err;
@@ -752,6 +779,17 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.tbl_key = e->d_tbl_key;
     mw.tbl_val = e->d_tbl_val;
     mw.tbl_ins = e->d_tbl_ins;
+    if (e->ttl_live) {  // the clock at which the reference last fired timers before this row (A8)
+      uint64_t t0 = clock_before, t1 = clock_before;
+      if (c->time) {
+        HIPCHECK(hipMemcpy(&t1, c->time + row, sizeof t1, hipMemcpyDeviceToHost));
+        if (row > 0) HIPCHECK(hipMemcpy(&t0, c->time + row - 1, sizeof t0, hipMemcpyDeviceToHost));
+        t0 = std::max(t0, clock_before);
+        t1 = std::max(t1, clock_before);
+      }
+      mw.tbl_dl = e->d_tbl_dl;
+      mw.fire_clock = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? t0 : t1;
+    }
     mw.entries = e->map_entries;
     mw.peak_lo = e->d_mw_peak;
     mw.dropped = e->d_mw_drop;
@@ -762,8 +800,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError());
   }
   }
-  if (e->coord_on) {
-    if (ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  if (e->coord_on && ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  if (e->coord_on || e->map_bits) {  // the log clock (timers: lock timeouts, map TTL)
     if (launch_clock_advance(c->time, n, 0, e->d_clock, st)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
   }
   if (c->index) {  // the applied watermark = index of the batch's last entry
@@ -1027,11 +1065,19 @@ extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, ui
   HIPCHECK(hipMemcpy(word.data(), e->d_tbl_word, 4 * n, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(val.data(), e->d_tbl_val, 8 * n, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(ci.data(), e->d_tbl_ci, 8 * n, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> dl;
+  uint64_t clock = 0;
+  if (e->ttl_live) {  // every timer due by the engine clock has fired (MapState TTL removal)
+    dl.resize(n);
+    HIPCHECK(hipMemcpy(dl.data(), e->d_tbl_dl, 8 * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&clock, e->d_clock, sizeof clock, hipMemcpyDeviceToHost));
+  }
   static const uint8_t ktag_tag[4] = {CC_TAG_LONG, CC_TAG_INT, CC_TAG_BOOL, CC_TAG_HANDLE};
   struct Row { uint8_t kt; uint64_t k; uint8_t vt; uint64_t v, ci; };
   std::vector<Row> rows;
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t w = word[i];
+    if (!dl.empty() && dl[i] && dl[i] <= clock) continue;
     if ((w & kMwUsed) && (w & kMwPresent) && !(w & kMwDead) && (w & kMwSlotMask) == slot)
       rows.push_back(Row{ktag_tag[(w >> 17) & 3], key[i], (uint8_t)mw_vtag(w), val[i], ci[i]});
   }

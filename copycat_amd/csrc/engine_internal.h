@@ -95,6 +95,13 @@ struct MapArgs {
   uint64_t* tbl_ci;
   uint64_t* tbl_ins;
   uint64_t* dropped;  // [max_resources] compaction drops bound-but-absent entries: counted per map (map_wide.hip)
+  bool ttl;           // TTL mode: entries carry timer deadlines (k_apply_map<true>)
+  uint64_t* tbl_dl;
+  const uint32_t* map_row;     // [sub_batch] staging position -> batch row (launch_map_rows)
+  const uint64_t* time;        // batch columns (absolute rows)
+  const uint64_t* aux;
+  const uint64_t* clock_base;  // device: the engine clock before this batch
+  bool deferred;               // manager-mode timer order (CC_CFG_TIMERS_DEFERRED)
   uint8_t* rst_status;
   uint64_t* rst_value;
   uint32_t* err;
@@ -102,12 +109,14 @@ struct MapArgs {
 };
 int launch_apply_map(const MapArgs& a, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
+int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* map_row, hipStream_t st);
 
 // Whole-map ops (containsValue / isEmpty / size / clear / Delete): barrier rows of a batch (map_wide.hip).
 constexpr uint32_t kBarCap = 1u << 16;  // barrier rows per batch
-int launch_map_barriers(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res,
+// Also flags (ttl_seen = 1) a map put/putIfAbsent/replace/replaceIfPresent row with ttl > 0.
+int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
-                        hipStream_t st);
+                        uint32_t* ttl_seen, hipStream_t st);
 struct MapWideArgs {
   uint32_t slot, op, atag;
   uint64_t apay;
@@ -116,6 +125,8 @@ struct MapWideArgs {
   const uint64_t* tbl_key;
   const uint64_t* tbl_val;
   const uint64_t* tbl_ins;
+  const uint64_t* tbl_dl;      // TTL mode: entry deadlines (null: no timers)
+  uint64_t fire_clock;         // entries with a deadline <= this clock have expired at the barrier row
   uint64_t entries;
   uint32_t* peak_lo;           // [max_resources] lower bound on the map's peak size
   uint64_t* dropped;           // [max_resources] entries dropped by compaction / clear (upper-bound term)

@@ -32,20 +32,44 @@ __device__ inline bool map_wide_op(uint32_t op) {
          op == CC_OP_MAP_CLEAR;
 }
 
-// Rows whose instance is open on a live map and whose op reads or resets the whole map.
+__device__ inline bool ttl_op(uint32_t op) {
+  return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT;
+}
+
+// Rows whose instance is open on a live map and whose op reads or resets the whole map; and whether any map row
+// arms a TTL timer (the engine then switches to TTL mode for good).
 __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
-                                                      uint64_t n, const uint32_t* __restrict__ inst_res,
+                                                      const uint64_t* __restrict__ aux, uint64_t n,
+                                                      const uint32_t* __restrict__ inst_res,
                                                       const uint8_t* __restrict__ res_type, uint32_t max_inst,
-                                                      uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap) {
+                                                      uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap,
+                                                      uint32_t* __restrict__ ttl_seen) {
   const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   if (i >= n) return;
-  if (!map_wide_op(op[i])) return;
+  const uint32_t o = op[i];
+  const bool wide = map_wide_op(o), ttl = aux && ttl_op(o);
+  if (!wide && !ttl) return;
+  if (ttl && (int64_t)aux[i] <= 0) {
+    if (!wide) return;
+  }
   const uint32_t in = inst[i];
   if (in >= max_inst) return;
   const uint32_t r = inst_res[in];
   if (r == kNoRes || res_type[r] != CC_RES_MAP) return;
+  if (!wide) {
+    *ttl_seen = 1u;
+    return;
+  }
   const uint32_t k = atomicAdd(bar_n, 1u);
   if (k < cap) bar[k] = (uint32_t)i;
+}
+
+// An entry is live at the barrier row: present, and no TTL timer of it has fired by then.
+__device__ inline bool live_at(uint32_t w, const uint64_t* __restrict__ dl, uint64_t e, uint64_t fire) {
+  if (!(w & kMwPresent)) return false;
+  if (!dl) return true;
+  const uint64_t d = dl[e];
+  return d == 0 || d > fire;
 }
 
 // java.lang.{Long,Integer,Boolean}.hashCode spread by HashMap.hash (oracle java_hash; HANDLE as Long).
@@ -84,14 +108,14 @@ __device__ inline unsigned long long wave_sum(unsigned long long x) {
 }
 
 __global__ __launch_bounds__(kMwT) void k_mw_count(const uint32_t* __restrict__ word, const uint64_t* __restrict__ val,
-                                                  uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag,
+                                                  const uint64_t* __restrict__ dl, uint64_t fire, uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag,
                                                   uint64_t apay, unsigned long long* __restrict__ ctl) {
   unsigned long long pres = 0, used = 0, nulls = 0, match = 0;
   for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
     const uint32_t w = word[e];
     if (!(w & kMwUsed) || (w & kMwDead) || (w & kMwSlotMask) != slot) continue;
     ++used;
-    if (!(w & kMwPresent)) continue;
+    if (!live_at(w, dl, e, fire)) continue;
     ++pres;
     if (op == CC_OP_MAP_CONTAINSVALUE) {
       const uint32_t vt = mw_vtag(w);
@@ -115,7 +139,7 @@ __global__ __launch_bounds__(kMwT) void k_mw_count(const uint32_t* __restrict__ 
 // the first insertion of each.  Runs only for an order-dependent containsValue (all threads read the same ctl).
 __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ word, const uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ val, const uint64_t* __restrict__ ins,
-                                                  uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag, uint64_t apay,
+                                                  const uint64_t* __restrict__ dl, uint64_t fire, uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag, uint64_t apay,
                                                   const uint32_t* __restrict__ peak_lo, const unsigned long long* __restrict__ dropped,
                                                   int pass, unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
   if (op != CC_OP_MAP_CONTAINSVALUE || ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0) return;
@@ -129,7 +153,7 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
   if (pass == 1 && ctl[C_BN] != ctl[C_BM]) return;  // decided by the buckets
   for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
     const uint32_t w = word[e];
-    if (!(w & kMwPresent) || (w & kMwDead) || (w & kMwSlotMask) != slot) continue;
+    if ((w & kMwDead) || (w & kMwSlotMask) != slot || !live_at(w, dl, e, fire)) continue;
     const uint32_t vt = mw_vtag(w);
     const bool isnull = vt == CC_TAG_NULL;
     if (!isnull && !(vt == atag && val[e] == apay)) continue;
@@ -187,12 +211,12 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
   out_value[row] = v;
 }
 
-int launch_map_barriers(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res,
+int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
-                        hipStream_t st) {
+                        uint32_t* ttl_seen, hipStream_t st) {
   if (hipMemsetAsync(bar_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
-  hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, n, inst_res,
-                     res_type, max_inst, bar, bar_n, cap);
+  hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
+                     res_type, max_inst, bar, bar_n, cap, ttl_seen);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -201,10 +225,12 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
   const uint32_t atag = a.atag, op = a.op;
   const uint64_t apay = atag == CC_TAG_NULL ? 0 : a.apay;  // canonical NULL payload
   hipLaunchKernelGGL(k_mw_reset, dim3(1), dim3(64), 0, st, a.ctl);
-  hipLaunchKernelGGL(k_mw_count, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_val, a.entries, a.slot, op, atag, apay, a.ctl);
+  hipLaunchKernelGGL(k_mw_count, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_val, a.tbl_dl, a.fire_clock, a.entries, a.slot, op,
+                     atag, apay, a.ctl);
   if (op == CC_OP_MAP_CONTAINSVALUE) {
     for (int pass = 0; pass < 2; ++pass)
-      hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.entries,
+      hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.tbl_dl,
+                         a.fire_clock, a.entries,
                          a.slot, op, atag, apay, a.peak_lo, (const unsigned long long*)a.dropped, pass, a.ctl, a.err);
   }
   hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,

@@ -52,13 +52,14 @@ GPU_VALUE_OPS = {"VALUE_GET", "VALUE_SET", "VALUE_CAS", "VALUE_GETANDSET", "VALU
 GPU_COORD_OPS = {"LOCK_LOCK", "LOCK_UNLOCK", "ELECT_LISTEN", "ELECT_UNLISTEN", "ELECT_ISLEADER", "GROUP_JOIN",
                  "GROUP_LEAVE", "GROUP_EXECUTE"}
 GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_GETORDEFAULT", "MAP_REMOVE",
-               "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT"}
+               "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT", "MAP_CONTAINSVALUE", "MAP_SIZE",
+               "MAP_ISEMPTY", "MAP_CLEAR"}
 
 
 def gpu_eligible(kat):
     """KATs whose every step this build applies on the GPU: AtomicValue ops (listeners with CC_CFG_VALUE_EVENTS),
-    Map key ops without ttl, lock / election / group ops except schedule, Delete on every type but maps, and
-    clock advances; no registry control or session-close steps (host control plane)."""
+    every Map op (TTL timers included), lock / election / group ops except schedule, Delete, and clock advances;
+    no registry control or session-close steps (host control plane)."""
     types = {r[1] for r in kat["resources"]}
     if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP"}:
         return False
@@ -67,12 +68,7 @@ def gpu_eligible(kat):
             return False
         if "commit" in s:
             c = s["commit"]
-            if c["op"] == "DELETE":
-                if "MAP" in types:
-                    return False
-            elif c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS:
-                return False
-            elif c["op"].startswith("MAP_") and c.get("aux", 0) > 0:
+            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS:
                 return False
     return True
 

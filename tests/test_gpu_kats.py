@@ -13,8 +13,10 @@ def test_gpu_kat_coverage():
     names = {k["name"] for k in KATS}
     assert {"map_put_get_remove", "map_put_if_absent", "A1_replace_if_present_inverts_args", "lock_unlock",
             "election_elect", "group_join", "group_leave", "A7_trylock_timeout_is_silent",
-            "lock_delete_then_unlock_commit_closed", "A9_leader_relisten_appended"} <= names
-    assert len(KATS) >= 25
+            "lock_delete_then_unlock_commit_closed", "A9_leader_relisten_appended", "map_contains_value", "map_size",
+            "map_clear", "map_put_ttl", "map_put_if_absent_ttl", "A5_contains_value_npe_order",
+            "A8_timer_deferred_after_commit", "A8_timer_immediate_module_mode"} <= names
+    assert len(KATS) >= 34
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])

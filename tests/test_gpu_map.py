@@ -11,13 +11,13 @@ from copycat_amd.batch import Batch
 pytestmark = pytest.mark.gpu
 
 
-def _engines(maps, max_inst, max_batch, map_capacity, sub_batch=0, first_slot=0):
+def _engines(maps, max_inst, max_batch, map_capacity, sub_batch=0, first_slot=0, flags=abi.CC_CFG_TIMERS_DEFERRED):
     from copycat_amd.engine import Engine
     from oracle.oracle_py import Oracle
 
     slots = first_slot + maps
-    E = Engine(slots, max_inst, max_batch, map_capacity=map_capacity, sub_batch=sub_batch)
-    O = Oracle(slots, max_inst)
+    E = Engine(slots, max_inst, max_batch, map_capacity=map_capacity, sub_batch=sub_batch, flags=flags)
+    O = Oracle(slots, max_inst, flags & abi.CC_CFG_TIMERS_DEFERRED)
     E.resource_create_range(first_slot, maps, abi.CC_RES_MAP)
     E.instance_open_range(first_slot, maps, first_slot, 1000, 7)
     for m in range(first_slot, slots):
@@ -157,19 +157,6 @@ def test_map_capacity_error():
     with pytest.raises(EngineError) as ei:
         E.apply_host(_puts(np.arange(6000, dtype=np.uint64), 0))
     assert ei.value.rc == abi.CC_ERR_CAPACITY
-
-
-@pytest.mark.parametrize("op,aux", [(abi.CC_OP_MAP_PUT, 5), (abi.CC_OP_MAP_REPLACE, 1)])
-def test_map_ops_not_on_gpu_fail_loudly(op, aux):
-    from copycat_amd.engine import EngineError
-
-    E, _ = _engines(2, 4, 16, 1024)
-    b = _puts([1, 2, 3], 1)
-    b.op[1] = op
-    b.aux[1] = aux
-    with pytest.raises(EngineError) as ei:
-        E.apply_host(b)
-    assert ei.value.rc == abi.CC_ERR_UNSUPPORTED
 
 
 def test_map_get_with_positive_aux_is_applied():
@@ -338,3 +325,57 @@ def test_map_clear_then_reuse_keys():
     one = Batch.from_columns(**{name: np.concatenate([getattr(x, name) for x in parts]) for name, _ in abi.BATCH_COLUMNS})
     _assert_rows(*_apply_both(E, O, [one]))
     _assert_maps(E, O, [0, 1])
+
+
+# ---- TTL timers: put/putIfAbsent/replace/replaceIfPresent with ttl > 0 (MapState.java:91-93,119-121,189-192,218-220)
+
+def _with_ttl(b, seed, p_ttl=0.4, max_ttl=300, step=8):
+    """Log time advances by one every `step` rows; a share of the ttl-reading rows arm timers of 1..max_ttl."""
+    rng = np.random.default_rng(seed)
+    n = len(b)
+    b.time[:] = np.arange(n, dtype=np.uint64) // np.uint64(step) + np.uint64(1000)
+    arm = rng.random(n) < p_ttl
+    b.aux[:] = np.where(arm, rng.integers(1, max_ttl, n), rng.choice([0, -5], n)).astype(np.int64).view(np.uint64)
+
+
+@pytest.mark.parametrize("flags", [abi.CC_CFG_TIMERS_DEFERRED, 0], ids=["manager", "module"])
+@pytest.mark.parametrize("n,maps,keys,sub_batch,seed", [
+    (3_000, 2, 16, 0, 91),
+    (120_000, 32, 128, 16384 * 2, 92),
+])
+def test_map_ttl_parity(flags, n, maps, keys, sub_batch, seed):
+    """Entries expire when the reference's timer fires (before the commit in module mode, after the commit that
+    advanced the clock in manager mode, A8); a later store re-arms or cancels; size sees only live entries;
+    state read back between batches and after advance_time excludes expired keys."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed)
+    _no_null_values(b)
+    _with_ttl(b, seed)
+    _with_barriers(b, 0.002, seed, ops=np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_ISEMPTY], np.uint8))
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch, flags=flags)
+    cut = n // 3
+    _assert_rows(*_apply_both(E, O, [b.slice(0, cut)]))
+    _assert_maps(E, O, range(maps))
+    _assert_rows(*_apply_both(E, O, [b.slice(cut, n)]))
+    _assert_maps(E, O, range(maps))
+    now = int(b.time[-1]) + 150
+    E.advance_time(now)
+    O.advance_time(now)
+    _assert_maps(E, O, range(maps))
+
+
+def test_map_ttl_expiry_boundary():
+    """A put with ttl 10 at time 100 expires at 110: in manager mode a get at time 110 still sees it (the timer
+    fires after that commit), in module mode it does not."""
+    for flags, expect in ((abi.CC_CFG_TIMERS_DEFERRED, abi.CC_TAG_LONG), (0, abi.CC_TAG_NULL)):
+        E, O = _engines(1, 4, 16, 1024, flags=flags)
+        b = _puts([7, 7, 7], 0)
+        b.op[1:] = abi.CC_OP_MAP_GET
+        b.time[:] = [100, 109, 110]
+        b.aux[0] = 10
+        gs, gv, os_, ov = _apply_both(E, O, [b])
+        _assert_rows(gs, gv, os_, ov)
+        assert gs[1] == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_LONG)
+        assert gs[2] == abi.cc_status(abi.CC_ST_OK, expect)
