@@ -7,8 +7,8 @@
 // A removed key keeps its entry (USED, not PRESENT) so that probe chains stay intact; entries of a deleted map
 // are marked DEAD.  A region is compacted (live entries re-inserted) when a launch finds it more than 3/4 used.
 //
-// One 256-thread workgroup owns one region for the whole launch: it loads the region into LDS, walks the
-// region's staged commits (its run in every partition tile, in log order) in chunks of 1024, and writes the
+// One 1024-thread workgroup (512 in TTL mode) owns one region for the whole launch: it loads the region into LDS, walks the
+// region's staged commits (its run in every partition tile, in log order) in chunks of 1024 (512), and writes the
 // region back.  Per chunk:
 //   1. binding: commits that can create a node (put, putIfAbsent) find or claim their key's entry — rounds of
 //      LDS compare-and-swap; a claim is marked PENDING until the next round so no thread compares against a
@@ -34,8 +34,6 @@
 
 namespace cc {
 
-constexpr int kMT = 256;                // threads per region workgroup
-constexpr int kMEPer = kMapRegion / kMT;  // table entries per thread (8)
 constexpr uint32_t kNoEnt = 0xFFFFu;
 constexpr uint32_t kEntFull = 0xFFFEu;
 
@@ -47,7 +45,7 @@ __device__ inline uint32_t map_ident_of(uint32_t res, uint32_t flags) { return m
 // clock; manager mode: the previous commit's, A8), and a commit that stores a value re-arms or cancels the timer.
 // The per-record clocks come from the input columns through map_row (staging position -> batch row).
 template <bool TTL>
-__global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
+__global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
                                                   const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
                                                   const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
@@ -59,8 +57,10 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                   uint32_t* __restrict__ err_out) {
-  constexpr int kMPer = TTL ? 2 : 4;  // commits per thread per chunk (the TTL variant's LDS holds deadlines)
-  constexpr int kMCh = kMT * kMPer;
+  constexpr int MT = TTL ? 512 : 1024;    // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
+  constexpr int MEPer = kMapRegion / MT;  // table entries per thread
+  constexpr int kMPer = 1;                // commits per thread per chunk
+  constexpr int kMCh = MT * kMPer;
   __shared__ uint64_t tkey[kMapRegion];
   __shared__ uint32_t tword[kMapRegion];
   __shared__ uint64_t tval[kMapRegion];
@@ -76,11 +76,11 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
   __shared__ uint64_t rdl[TTL ? kMCh : 1];        // deadline the commit arms if it stores (0: none)
   __shared__ uint32_t ecnt[kMapRegion + 1];  // commits per entry in the chunk -> run starts
   __shared__ uint32_t eflag[kMapRegion];     // the entry's run holds a value-comparing op
-  __shared__ Comp wcomp[kMT / kWave];
-  __shared__ uint32_t whead[kMT / kWave];
+  __shared__ Comp wcomp[MT / kWave];
+  __shared__ uint32_t whead[MT / kWave];
   __shared__ uint32_t rstart[kMaxTiles];
   __shared__ uint32_t rpre[kMaxTiles + 1];
-  __shared__ uint32_t wsum[kMT / kWave];
+  __shared__ uint32_t wsum[MT / kWave];
   __shared__ uint32_t flag[3];
   __shared__ uint32_t used_total;
 
@@ -91,14 +91,14 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
   // ---- load the region; compact it when more than 3/4 of its entries are bound ----
   if (t < 3) flag[t] = 0;
   if (t == 0) used_total = 0;
-  for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
-  for (uint32_t q = t; q < kMapRegion; q += kMT) eflag[q] = 0;
+  for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
+  for (uint32_t q = t; q < kMapRegion; q += MT) eflag[q] = 0;
   {
-    uint64_t ek[kMEPer], ev[kMEPer], eci[kMEPer], eins[kMEPer], edl[kMEPer];
-    uint32_t ew[kMEPer], used = 0;
+    uint64_t ek[MEPer], ev[MEPer], eci[MEPer], eins[MEPer], edl[MEPer];
+    uint32_t ew[MEPer], used = 0;
 #pragma unroll
-    for (int q = 0; q < kMEPer; ++q) {
-      const uint32_t e = q * kMT + t;
+    for (int q = 0; q < MEPer; ++q) {
+      const uint32_t e = q * MT + t;
       ek[q] = tbl_key[tb + e];
       ew[q] = tbl_word[tb + e];
       ev[q] = tbl_val[tb + e];
@@ -112,8 +112,8 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
     lds_barrier();
     const bool compact = used_total > kMapRegion * 3 / 4;  // block-uniform
 #pragma unroll
-    for (int q = 0; q < kMEPer; ++q) {
-      const uint32_t e = q * kMT + t;
+    for (int q = 0; q < MEPer; ++q) {
+      const uint32_t e = q * MT + t;
       tkey[e] = ek[q];
       tword[e] = compact ? 0u : ew[q];
       tval[e] = ev[q];
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
     if (compact) {
       // live keys are distinct: claim the first free slot of each probe chain (no key comparisons needed)
 #pragma unroll
-      for (int q = 0; q < kMEPer; ++q) {
+      for (int q = 0; q < MEPer; ++q) {
         // a bound key that is absent now is dropped: it still counts toward its map's peak-size bound
         if ((ew[q] & kMwUsed) && !(ew[q] & (kMwPresent | kMwDead)) && dropped) atomicAdd(&dropped[ew[q] & kMwSlotMask], 1ull);
         if ((ew[q] & kMwPresent) && !(ew[q] & kMwDead)) {
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
 
   // ---- this region's list = its run in every partition tile, in tile order ----
   {
-    constexpr int PT = kMaxTiles / kMT;
+    constexpr int PT = kMaxTiles / MT;
     uint32_t len[PT], sum = 0;
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       if (tt < tiles) rpre[tt] = run;
       run += len[q];
     }
-    if (t == kMT - 1) rpre[tiles] = run;
+    if (t == MT - 1) rpre[tiles] = run;
     lds_barrier();
   }
   const uint32_t cnt = rpre[tiles];
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       }
     }
     // ---- 3. stable counting sort by entry: one wave at a time keeps log order ----
-    for (uint32_t q = 0; q < kMT / kWave; ++q) {
+    for (uint32_t q = 0; q < MT / kWave; ++q) {
       if (w == q) {
 #pragma unroll
         for (int j = 0; j < kMPer; ++j)
@@ -299,10 +299,10 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       lds_barrier();
     }
     {
-      uint32_t v[kMEPer], sum = 0;
+      uint32_t v[MEPer], sum = 0;
 #pragma unroll
-      for (int q = 0; q < kMEPer; ++q) {
-        v[q] = ecnt[t * kMEPer + q];
+      for (int q = 0; q < MEPer; ++q) {
+        v[q] = ecnt[t * MEPer + q];
         sum += v[q];
       }
       uint32_t inc = sum;
@@ -317,11 +317,11 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       uint32_t run = inc - sum;
       for (uint32_t q = 0; q < w; ++q) run += wsum[q];
 #pragma unroll
-      for (int q = 0; q < kMEPer; ++q) {
-        ecnt[t * kMEPer + q] = run;  // run start of entry
+      for (int q = 0; q < MEPer; ++q) {
+        ecnt[t * MEPer + q] = run;  // run start of entry
         run += v[q];
       }
-      if (t == kMT - 1) ecnt[kMapRegion] = run;
+      if (t == MT - 1) ecnt[kMapRegion] = run;
       lds_barrier();
     }
 #pragma unroll
@@ -473,15 +473,15 @@ __global__ __launch_bounds__(kMT) void k_apply_map(const uint32_t* __restrict__ 
       if (any_c) tins[e] = ins;
     }
     lds_barrier();
-    for (uint32_t q = t; q <= kMapRegion; q += kMT) ecnt[q] = 0;
-    for (uint32_t q = t; q < kMapRegion; q += kMT) eflag[q] = 0;
+    for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
+    for (uint32_t q = t; q < kMapRegion; q += MT) eflag[q] = 0;
     lds_barrier();
   }
 
   // ---- write the region back ----
 #pragma unroll
-  for (int q = 0; q < kMEPer; ++q) {
-    const uint32_t e = q * kMT + t;
+  for (int q = 0; q < MEPer; ++q) {
+    const uint32_t e = q * MT + t;
     tbl_key[tb + e] = tkey[e];
     tbl_word[tb + e] = tword[e];
     tbl_val[tb + e] = tval[e];
@@ -504,12 +504,12 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.map_bits == 0 || a.tiles == 0) return 0;
   a.mark(K_APPLY_MAP, 1, st);
   if (a.ttl)
-    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
+    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
                        a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.err);
   else
-    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(kMT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
+    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(1024), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
                        a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.err);

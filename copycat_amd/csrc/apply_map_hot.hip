@@ -2,8 +2,9 @@
 // traffic, SURVEY §7 hard part (b)) is applied by a scan over many workgroups instead of one region's chain.
 //
 // Per sub-batch:
-//   k_hot_detect : one workgroup samples 64K commits, counts (map, key tag, key) in LDS, and takes the (up to)
-//                  64 most frequent keys above ~0.1% of the sample; binds their table entries (apply_map.hip
+//   k_hot_detect : one workgroup samples 64K commits (64 blocks of 1024 consecutive rows), counts (map, key tag,
+//                  key) in an LDS sketch, and takes the (up to) 64 most frequent keys above ~0.1% of the
+//                  sample; binds their table entries (apply_map.hip
 //                  layout) and publishes the hot set.  The partition routes every commit of a hot key to that
 //                  key's own bucket (log order, like any super-bucket).  Hot-ness only steers work: a commit is
 //                  applied identically by either path.
@@ -34,6 +35,8 @@ constexpr int kHPer = kHotPiece / kHT;     // commits per thread per piece (16)
 constexpr int kDetT = 1024;
 constexpr int kDetSlots = 4096;
 constexpr uint32_t kDetSample = 65536;
+constexpr uint32_t kDetBlk = 1024;  // consecutive rows per sample block
+constexpr int kDetProbe = 8;
 
 // ---------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ flags,
@@ -58,28 +61,44 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
   __syncthreads();
   const uint64_t n = hi - lo;
   const uint32_t S = (uint32_t)(n < kDetSample ? n : kDetSample);
-  const uint64_t stride = S ? n / S : 1;
-  for (uint32_t j = t; j < S; j += kDetT) {
-    const uint64_t i = lo + (uint64_t)j * stride;
-    const uint32_t s = inst[i];
-    const uint32_t r = s < max_inst ? inst_res[s] : kNoRes;
-    if (r == kNoRes || res_type[r] != CC_RES_MAP) continue;
-    const uint32_t kt = CC_FLAG_KTAG(flags[i]);
-    const uint64_t key = ckey[i];
-    const uint64_t h = map_hash(r, kt, key);
-    if (h == 0) continue;
-    uint32_t q = (uint32_t)h & (kDetSlots - 1);
-    for (int step = 0; step < 64; ++step, q = (q + 1) & (kDetSlots - 1)) {
-      const uint64_t old = atomicCAS((unsigned long long*)&th64[q], 0ull, (unsigned long long)h);
-      if (old == 0) {
-        tkey[q] = key;
-        tident[q] = mw_ident(r, kt);
-        atomicAdd(&tcnt[q], 1u);
-        break;
-      }
-      if (old == h) {
-        atomicAdd(&tcnt[q], 1u);
-        break;
+  // the sample: 64 blocks of 1024 consecutive rows spread evenly over the sub-batch (coalesced column loads;
+  // hot-ness only steers work, so any sample is correct), loads for 4 rows issued before their LDS updates
+  const uint64_t spacing = n > kDetSample ? n / (kDetSample / kDetBlk) : kDetBlk;
+  constexpr int U = 4;
+  for (uint32_t j0 = t; j0 < S; j0 += kDetT * U) {
+    uint32_t r[U], kt[U];
+    uint64_t key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = j0 + u * kDetT;
+      r[u] = kNoRes;
+      if (j >= S) continue;
+      const uint64_t i = lo + (uint64_t)(j / kDetBlk) * spacing + (j % kDetBlk);
+      const uint32_t sl = inst[i];
+      kt[u] = CC_FLAG_KTAG(flags[i]);
+      key[u] = ckey[i];
+      r[u] = sl < max_inst ? inst_res[sl] : kNoRes;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r[u] == kNoRes || res_type[r[u]] != CC_RES_MAP) continue;
+      const uint64_t h = map_hash(r[u], kt[u], key[u]);
+      if (h == 0) continue;
+      // short probes: a Zipf sample holds far more distinct cold keys than the sketch has slots; a hot key shows
+      // up early and often, so a sample that finds no slot within kDetProbe steps is dropped
+      uint32_t q = (uint32_t)h & (kDetSlots - 1);
+      for (int step = 0; step < kDetProbe; ++step, q = (q + 1) & (kDetSlots - 1)) {
+        const uint64_t old = atomicCAS((unsigned long long*)&th64[q], 0ull, (unsigned long long)h);
+        if (old == 0) {
+          tkey[q] = key[u];
+          tident[q] = mw_ident(r[u], kt[u]);
+          atomicAdd(&tcnt[q], 1u);
+          break;
+        }
+        if (old == h) {
+          atomicAdd(&tcnt[q], 1u);
+          break;
+        }
       }
     }
   }
