@@ -1174,6 +1174,132 @@ extern "C" int cc_advance_time(cc_engine* e, uint64_t now) {
 static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map", "k_map_hot",
                                           "k_apply_coord", "k_events"};
 
+// ---- snapshot / restore (restart without replaying the whole log) -------------------
+// Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
+// mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
+namespace {
+constexpr uint64_t kSnapMagic = 0x31304E5053434343ull;  // "CCCSPN01"
+struct SnapHdr {
+  uint64_t magic;
+  uint32_t abi, flags;  // flags: 1 coord blocks, 2 map TTL mode
+  uint32_t max_resources, max_instances, map_bits, sb;
+  uint64_t applied, sess_next;
+  uint32_t sess_cap, sess_thr, sess_size, pad;
+};
+struct Section {
+  void* dev;
+  void* host;
+  uint64_t bytes;
+};
+}  // namespace
+
+static std::vector<Section> snap_sections(cc_engine* e) {
+  const uint64_t slots = (uint64_t)e->sb << kSbShift, mi = e->cfg.max_instances, mr = e->cfg.max_resources;
+  std::vector<Section> v = {
+      {nullptr, e->res_type.data(), slots},
+      {nullptr, e->inst_res.data(), 4 * mi},
+      {nullptr, e->inst_id.data(), 8 * mi},
+      {nullptr, e->inst_client.data(), 8 * mi},
+      {nullptr, e->inst_seq.data(), 8 * mi},
+      {nullptr, e->sb_kind.data(), e->sb},
+      {e->d_inst_res, nullptr, 4 * mi},
+      {e->d_res_type, nullptr, slots},
+      {e->d_val_meta, nullptr, 4 * slots},
+      {e->d_val_v, nullptr, 8 * slots},
+      {e->d_sb_kind, nullptr, e->sb},
+      {e->d_inst_id, nullptr, 8 * mi},
+      {e->d_clock, nullptr, 8},
+  };
+  if (e->map_bits) {
+    const uint64_t n = e->map_entries;
+    v.push_back({e->d_tbl_key, nullptr, 8 * n});
+    v.push_back({e->d_tbl_word, nullptr, 4 * n});
+    v.push_back({e->d_tbl_val, nullptr, 8 * n});
+    v.push_back({e->d_tbl_ci, nullptr, 8 * n});
+    v.push_back({e->d_tbl_ins, nullptr, 8 * n});
+    v.push_back({e->d_tbl_dl, nullptr, 8 * n});
+    v.push_back({e->d_mw_peak, nullptr, 4 * mr});
+    v.push_back({e->d_mw_drop, nullptr, 8 * mr});
+  }
+  if (e->coord_on) v.push_back({e->d_coord, nullptr, kCoordBlock * slots});
+  return v;
+}
+
+extern "C" int cc_snapshot_size(cc_engine* e, uint64_t* bytes) {
+  if (!e || !bytes) return CC_ERR_INVALID;
+  uint64_t total = sizeof(SnapHdr);
+  for (const Section& x : snap_sections(e)) total += 8 + x.bytes;
+  *bytes = total;
+  return CC_OK;
+}
+
+extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
+  if (!e || !h_buf) return CC_ERR_INVALID;
+  int rc = cc_sync(e);  // results of every batch so far are final (and the applied watermark is current)
+  if (rc) return rc;
+  uint64_t need = 0;
+  cc_snapshot_size(e, &need);
+  if (cap < need) return set_err(CC_ERR_CAPACITY, "snapshot buffer smaller than cc_snapshot_size");
+  SnapHdr h{};
+  h.magic = kSnapMagic;
+  h.abi = CC_ABI_VERSION;
+  h.flags = (e->coord_on ? 1u : 0u) | (e->ttl_live ? 2u : 0u);
+  h.max_resources = e->cfg.max_resources;
+  h.max_instances = e->cfg.max_instances;
+  h.map_bits = e->map_bits;
+  h.sb = e->sb;
+  h.applied = e->applied;
+  h.sess_next = e->sess_next;
+  h.sess_cap = e->sess_cap;
+  h.sess_thr = e->sess_thr;
+  h.sess_size = e->sess_size;
+  uint8_t* p = (uint8_t*)h_buf;
+  memcpy(p, &h, sizeof h);
+  p += sizeof h;
+  for (const Section& x : snap_sections(e)) {
+    memcpy(p, &x.bytes, 8);
+    p += 8;
+    if (x.dev) HIPCHECK(hipMemcpy(p, x.dev, x.bytes, hipMemcpyDeviceToHost));
+    else memcpy(p, x.host, x.bytes);
+    p += x.bytes;
+  }
+  return CC_OK;
+}
+
+extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t size) {
+  if (!e || !h_buf || size < sizeof(SnapHdr)) return set_err(CC_ERR_INVALID, "snapshot too small");
+  SnapHdr h;
+  memcpy(&h, h_buf, sizeof h);
+  if (h.magic != kSnapMagic || h.abi != CC_ABI_VERSION) return set_err(CC_ERR_INVALID, "not a snapshot of this engine ABI");
+  if (h.max_resources != e->cfg.max_resources || h.max_instances != e->cfg.max_instances || h.map_bits != e->map_bits ||
+      h.sb != e->sb)
+    return set_err(CC_ERR_INVALID, "snapshot configuration (max_resources/max_instances/map_capacity) differs");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  if ((h.flags & 1u) && (rc = ensure_ext(e, true))) return rc;
+  e->ttl_live = (h.flags & 2u) != 0;
+  const uint8_t* p = (const uint8_t*)h_buf + sizeof h;
+  const uint8_t* end = (const uint8_t*)h_buf + size;
+  for (const Section& x : snap_sections(e)) {
+    uint64_t b = 0;
+    if (p + 8 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+    memcpy(&b, p, 8);
+    p += 8;
+    if (b != x.bytes || p + b > end) return set_err(CC_ERR_INVALID, "snapshot section size mismatch");
+    if (x.dev) HIPCHECK(hipMemcpy(x.dev, p, b, hipMemcpyHostToDevice));
+    else memcpy(x.host, p, b);
+    p += b;
+  }
+  e->applied = h.applied;
+  e->applied_pending = false;
+  e->sess_next = h.sess_next;
+  e->sess_cap = h.sess_cap;
+  e->sess_thr = h.sess_thr;
+  e->sess_size = h.sess_size;
+  HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
+  return CC_OK;
+}
+
 extern "C" int cc_profile_enable(cc_engine* e, int on) {
   if (!e) return CC_ERR_INVALID;
   e->prof_on = on != 0;

@@ -58,6 +58,9 @@ def lib():
             "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
             "cc_read_group_members": (i32, [P, u32, u64, P, P]),
             "cc_advance_time": (i32, [P, u64]),
+            "cc_snapshot_size": (i32, [P, P]),
+            "cc_snapshot_save": (i32, [P, P, u64]),
+            "cc_snapshot_restore": (i32, [P, P, u64]),
             "cc_quorum_commit": (i32, [P, u32, u64, P, P, P, P]),
             "cc_expire_sweep": (i32, [P, u64, u64, u64, P, P, P]),
             "cc_profile_enable": (i32, [P, i32]),
@@ -263,6 +266,19 @@ class Engine:
 
     def advance_time(self, now):
         _check(self.L.cc_advance_time(self.h, now))
+
+    def snapshot(self) -> bytes:
+        """The engine's whole state (device arrays + host registry mirrors) as bytes (cc_snapshot_save)."""
+        n = C.c_uint64()
+        _check(self.L.cc_snapshot_size(self.h, C.byref(n)))
+        buf = np.zeros(n.value, np.uint8)
+        _check(self.L.cc_snapshot_save(self.h, _np(buf), n.value))
+        return buf.tobytes()
+
+    def restore(self, snap: bytes):
+        """Load a snapshot into this engine (same max_resources / max_instances / map_capacity)."""
+        buf = np.frombuffer(snap, np.uint8).copy()
+        _check(self.L.cc_snapshot_restore(self.h, _np(buf), len(buf)))
 
     def lock_state(self, slot, cap=1024):
         """(holder instance slot or -1, holder index, holder cleaned, [(waiter instance slot, index)])"""

@@ -245,6 +245,14 @@ int  cc_apply_batch_host(cc_engine* e, const cc_batch* h_cols, uint64_t n, const
 /* Highest log index applied so far (the applied watermark; all-gathered across GPUs by the host). */
 int  cc_applied_index(cc_engine* e, uint64_t* out);
 
+/* ---- snapshot / restore ---------------------------------------------------------------------------
+ * Replaces recovery by full log replay (the reference replays Copycat's log, AbstractReplicaTest.java:82-84):
+ * the engine's whole device state plus its host registry mirrors, as one host buffer.  Save syncs first;
+ * restore needs an engine created with the same max_resources, max_instances and map_capacity. */
+int  cc_snapshot_size(cc_engine* e, uint64_t* bytes);
+int  cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap);
+int  cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t size);
+
 /* ---- state readback for parity checks ------------------------------------------------------------ */
 /* AtomicValueState {value, current != null} for slots [first, first+count) (AtomicValueState.java:34-35) */
 int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* h_tag, uint64_t* h_value,

@@ -1,0 +1,95 @@
+"""GPU snapshot / restore: a fresh engine restored from a snapshot taken mid-stream
+continues bit-exact against the CPU oracle that never stopped — AtomicValue, Map (TTL timers, whole-map ops)
+and coordination state (lock queues with timeouts, election listeners, group members, events)."""
+import numpy as np
+import pytest
+
+from copycat_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows_equal(a, b):
+    for x, y in zip(a, b):
+        bad = np.nonzero(x != y)[0]
+        assert len(bad) == 0, f"{len(bad)} rows differ, first {bad[:5]}"
+
+
+def test_snapshot_restore_values_and_maps():
+    from copycat_amd.engine import Engine
+    from copycat_amd.workload import map_random_stream, value_random_stream
+    from oracle.oracle_py import Oracle
+    from tests.test_gpu_map import _no_null_values, _with_barriers, _with_ttl
+
+    V, M = 256, 32
+    slots, max_inst = V + M, V + M + 8
+    bv = value_random_stream(60_000, V, max_inst, seed=101, hot=4, p_hot=0.2)
+    bm = map_random_stream(60_000, M, max_inst, keys=64, first_inst=V, seed=102)
+    _no_null_values(bm)
+    _with_ttl(bm, 103)
+    _with_barriers(bm, 0.002, 104, ops=np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_CONTAINSVALUE], np.uint8))
+    order = np.random.default_rng(7).permutation(len(bv) + len(bm))
+    from copycat_amd.batch import Batch
+    cols = {name: np.concatenate([getattr(bv, name), getattr(bm, name)])[order] for name, _ in abi.BATCH_COLUMNS}
+    cols["index"] = np.arange(1, len(order) + 1, dtype=np.uint64)
+    cols["time"] = np.sort(cols["time"])
+    b = Batch.from_columns(**cols)
+
+    def engine():
+        E = Engine(slots, max_inst, len(b), map_capacity=16384)
+        E.resource_create_range(0, V, abi.CC_RES_VALUE)
+        E.resource_create_range(V, M, abi.CC_RES_MAP)
+        E.instance_open_range(0, slots, 0, 1000, 7)
+        return E
+
+    E = engine()
+    O = Oracle(slots, max_inst)
+    for r in range(slots):
+        O.resource_create(r, abi.CC_RES_VALUE if r < V else abi.CC_RES_MAP)
+        O.instance_open(r, r, 1000 + r, 7)
+    cut = len(b) // 2
+    first = b.slice(0, cut)
+    _rows_equal(E.apply_host(first), O.apply(first))
+    snap = E.snapshot()
+    del E
+    E2 = Engine(slots, max_inst, len(b), map_capacity=16384)  # empty registry: everything comes from the snapshot
+    E2.restore(snap)
+    rest = b.slice(cut, len(b))
+    _rows_equal(E2.apply_host(rest), O.apply(rest))
+    for x, y in zip(E2.value_state(0, V), O.value_state(0, V)):
+        assert np.array_equal(x, y)
+    for m in range(V, slots):
+        for x, y in zip(E2.map_entries(m), O.map_entries(m)):
+            assert np.array_equal(x, y)
+    assert E2.applied_index() == O.applied_index()
+
+
+def test_snapshot_restore_coordination():
+    from copycat_amd.engine import Engine
+    from copycat_amd.workload import coord_random_stream
+    from tests.test_gpu_coord import E_, FLAGS, G, L, V, _check_batch, _check_state, _setup
+
+    types = np.array([L, E_, G, V] * 24, np.uint8)
+    K = 5
+    E, O, max_inst = _setup(types, K, FLAGS)
+    b = coord_random_stream(60_000, types, K, max_inst, seed=21)
+    _check_batch(E, O, b.slice(0, 30_000))
+    snap = E.snapshot()
+    del E
+    E2 = Engine(len(types), max_inst, 1 << 20, flags=FLAGS, max_events=1 << 22)
+    E2.restore(snap)
+    _check_state(E2, O, types)
+    _check_batch(E2, O, b.slice(30_000, 60_000))
+    _check_state(E2, O, types)
+
+
+def test_snapshot_rejects_other_configuration():
+    from copycat_amd.engine import Engine, EngineError
+
+    E = Engine(64, 64, 16)
+    snap = E.snapshot()
+    with pytest.raises(EngineError) as ei:
+        Engine(128, 64, 16).restore(snap)
+    assert ei.value.rc == abi.CC_ERR_INVALID
+    with pytest.raises(EngineError):
+        Engine(64, 64, 16).restore(snap[:100])
