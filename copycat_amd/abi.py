@@ -21,6 +21,7 @@ CC_RES_MAP = 2
 CC_RES_LOCK = 3
 CC_RES_ELECTION = 4
 CC_RES_GROUP = 5
+CC_RES_SET = 6
 
 CC_OP_DELETE = 1
 CC_OP_VALUE_GET = 50
@@ -42,6 +43,12 @@ CC_OP_MAP_REPLACEIFPRESENT = 69
 CC_OP_MAP_ISEMPTY = 70
 CC_OP_MAP_SIZE = 71
 CC_OP_MAP_CLEAR = 72
+CC_OP_SET_CONTAINS = 100
+CC_OP_SET_ADD = 101
+CC_OP_SET_REMOVE = 102
+CC_OP_SET_SIZE = 103
+CC_OP_SET_ISEMPTY = 104
+CC_OP_SET_CLEAR = 105
 CC_OP_ELECT_LISTEN = 110
 CC_OP_ELECT_UNLISTEN = 111
 CC_OP_ELECT_ISLEADER = 112
@@ -95,6 +102,7 @@ TYPE_OPS = {
     CC_RES_LOCK: {CC_OP_DELETE, 115, 116},
     CC_RES_ELECTION: {CC_OP_DELETE, 110, 111, 112},
     CC_RES_GROUP: {CC_OP_DELETE, 120, 121, 122, 123},
+    CC_RES_SET: {CC_OP_DELETE} | set(range(100, 106)),
 }
 # key tags of the flags column (keys are never null)
 KTAG_OF_TAG = {CC_TAG_LONG: 0, CC_TAG_INT: 1, CC_TAG_BOOL: 2, CC_TAG_HANDLE: 3}

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (r[u] == kNoRes || res_type[r[u]] != CC_RES_MAP) continue;
+      if (r[u] == kNoRes || !is_keyed(res_type[r[u]])) continue;
       const uint64_t h = map_hash(r[u], kt[u], key[u]);
       if (h == 0) continue;
       // short probes: a Zipf sample holds far more distinct cold keys than the sketch has slots; a hot key shows

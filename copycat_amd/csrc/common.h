@@ -122,13 +122,31 @@ __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {
     case CC_RES_LOCK: return op == 115 || op == 116;
     case CC_RES_ELECTION: return op >= 110 && op <= 112;
     case CC_RES_GROUP: return op >= 120 && op <= 123;
+    case CC_RES_SET: return op >= 100 && op <= 105;
   }
   return false;
+}
+// resources whose elements live in the map table (apply_map.hip): MapState and SetState
+__host__ __device__ inline bool is_keyed(uint32_t type) { return type == CC_RES_MAP || type == CC_RES_SET; }
+// SetState ops as the MapState key ops they behave like (the result is rewritten by k_set_results):
+// contains -> containsKey, add -> putIfAbsent(Boolean TRUE), remove -> remove; anything else -> 0 (unknown op)
+__host__ __device__ inline uint32_t set_as_map_op(uint32_t op) {
+  switch (op) {
+    case CC_OP_SET_CONTAINS: return CC_OP_MAP_CONTAINSKEY;
+    case CC_OP_SET_ADD: return CC_OP_MAP_PUTIFABSENT;
+    case CC_OP_SET_REMOVE: return CC_OP_MAP_REMOVE;
+    case CC_OP_SET_SIZE: return CC_OP_MAP_SIZE;
+    case CC_OP_SET_ISEMPTY: return CC_OP_MAP_ISEMPTY;
+    case CC_OP_SET_CLEAR: return CC_OP_MAP_CLEAR;
+    case CC_OP_DELETE: return CC_OP_DELETE;
+  }
+  return 0;
 }
 // ops this build applies on the GPU (others raise CC_ERR_UNSUPPORTED for the batch)
 __host__ __device__ inline bool op_on_gpu(uint32_t type, uint32_t op) {
   if (type == CC_RES_VALUE) return op == CC_OP_DELETE || (op >= 50 && op <= 53);
-  if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops; map-wide ops are next
+  if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops (whole-map ops: map_wide.hip)
+  if (type == CC_RES_SET) return op >= 100 && op <= 102;
   if (type == CC_RES_LOCK || type == CC_RES_ELECTION) return op_registered(type, op);
   if (type == CC_RES_GROUP) return op_registered(type, op) && op != CC_OP_GROUP_SCHEDULE;
   return false;

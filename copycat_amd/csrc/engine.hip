@@ -93,6 +93,7 @@ struct cc_engine {
   uint32_t* d_map_row = nullptr;   // [sub_batch] staging position -> batch row
   uint32_t* d_ttl_seen = nullptr;
   bool ttl_live = false;
+  bool has_sets = false;  // SetState resources share the map table (results rewritten by k_set_results)
   uint32_t* d_hot_rpre = nullptr;
   uint32_t* d_hot_rstart = nullptr;
   uint32_t* d_hot_len = nullptr;
@@ -414,8 +415,9 @@ static int quiesce(cc_engine* e) {
 }
 
 static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
-  if (type == CC_RES_MAP && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map resources need cc_config.map_capacity > 0");
-  if (type < CC_RES_VALUE || type > CC_RES_GROUP) return set_err(CC_ERR_INVALID, "unknown resource type");
+  if (is_keyed(type) && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map and set resources need cc_config.map_capacity > 0");
+  if (type < CC_RES_VALUE || type > CC_RES_SET) return set_err(CC_ERR_INVALID, "unknown resource type");
+  if (type == CC_RES_SET) e->has_sets = true;
   const uint64_t end = (uint64_t)first + count;
   if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");
   for (uint64_t s = first; s < end; ++s) {
@@ -432,7 +434,7 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
   if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)first * kCoordBlock, 0, kCoordBlock * (uint64_t)count));
-  if (type == CC_RES_MAP) {  // a new HashMap: capacity 16, no history
+  if (is_keyed(type)) {  // a new HashMap: capacity 16, no history
     HIPCHECK(hipMemset(e->d_mw_peak + first, 0, sizeof(uint32_t) * count));
     HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
   }
@@ -457,7 +459,7 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   int rc = quiesce(e);
   if (rc) return rc;
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
-  if (e->res_type[slot] == CC_RES_MAP) {  // MapState.delete :264-274 — the map's entries die with it
+  if (is_keyed(e->res_type[slot])) {  // MapState.delete :264-274 / SetState.delete :123-134 — entries die with it
     if (launch_map_drop_resource(e->d_tbl_word, e->map_entries, slot, e->own_stream))
       return set_err(CC_ERR_HIP, "map drop launch", hipGetLastError());
     HIPCHECK(hipStreamSynchronize(e->own_stream));
@@ -609,7 +611,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.b = c->b;
     pa.key = c->key;
     pa.index = c->index;
-    pa.aux = c->aux;
+    pa.aux = (e->coord_on || e->ttl_live) ? c->aux : nullptr;  // maps read ttl only in TTL mode (the scan saw none)
     pa.time = c->time;
     pa.clock_base = e->d_clock;
     pa.ext_flags = ((e->cfg.flags & CC_CFG_VALUE_EVENTS) ? kExtValue : 0u) | ((e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? kExtDeferred : 0u);
@@ -771,7 +773,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     res = e->inst_res[in];
     MapWideArgs mw{};
     mw.slot = res;
-    mw.op = op;
+    mw.op = e->res_type[res] == CC_RES_SET ? set_as_map_op(op) : op;
     mw.atag = CC_FLAG_TAG_A(fl);
     mw.apay = a;
     mw.row = row;
@@ -800,6 +802,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError());
   }
   }
+  if (e->has_sets && launch_set_results(c->inst, c->op, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, out->status,
+                                        out->value, st))
+    return set_err(CC_ERR_HIP, "set results launch", hipGetLastError());
   if (e->coord_on && ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   if (e->coord_on || e->map_bits) {  // the log clock (timers: lock timeouts, map TTL)
     if (launch_clock_advance(c->time, n, 0, e->d_clock, st)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
@@ -1053,8 +1058,8 @@ extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count,
 
 extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag,
                                    uint64_t* h_key, uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index) {
-  if (!e || !count || slot >= e->cfg.max_resources || e->res_type[slot] != CC_RES_MAP)
-    return set_err(CC_ERR_INVALID, "not a map slot");
+  if (!e || !count || slot >= e->cfg.max_resources || !is_keyed(e->res_type[slot]))
+    return set_err(CC_ERR_INVALID, "not a map or set slot");
   if (cap && (!h_key_tag || !h_key || !h_value_tag || !h_value)) return set_err(CC_ERR_INVALID, "null output");
   int rc = quiesce(e);
   if (rc) return rc;
@@ -1292,6 +1297,7 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   }
   e->applied = h.applied;
   e->applied_pending = false;
+  e->has_sets = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_SET) != e->res_type.end();
   e->sess_next = h.sess_next;
   e->sess_cap = h.sess_cap;
   e->sess_thr = h.sess_thr;

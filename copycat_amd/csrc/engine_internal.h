@@ -136,6 +136,9 @@ struct MapWideArgs {
   uint32_t* err;
 };
 int launch_map_wide(const MapWideArgs& a, hipStream_t st);
+// SetState result rewrite after the batch (map_wide.hip)
+int launch_set_results(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
+                       uint32_t max_inst, uint8_t* status, uint64_t* value, hipStream_t st);
 
 constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
 struct HotArgs {

@@ -32,8 +32,12 @@ __device__ inline bool map_wide_op(uint32_t op) {
          op == CC_OP_MAP_CLEAR;
 }
 
+__device__ inline bool set_wide_op(uint32_t op) {
+  return op == CC_OP_DELETE || op == CC_OP_SET_SIZE || op == CC_OP_SET_ISEMPTY || op == CC_OP_SET_CLEAR;
+}
 __device__ inline bool ttl_op(uint32_t op) {
-  return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT;
+  return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT ||
+         op == CC_OP_SET_ADD;
 }
 
 // Rows whose instance is open on a live map and whose op reads or resets the whole map; and whether any map row
@@ -47,7 +51,8 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   if (i >= n) return;
   const uint32_t o = op[i];
-  const bool wide = map_wide_op(o), ttl = aux && ttl_op(o);
+  bool wide = map_wide_op(o) || set_wide_op(o);
+  const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
   if (ttl && (int64_t)aux[i] <= 0) {
     if (!wide) return;
@@ -55,8 +60,14 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   const uint32_t in = inst[i];
   if (in >= max_inst) return;
   const uint32_t r = inst_res[in];
-  if (r == kNoRes || res_type[r] != CC_RES_MAP) return;
+  if (r == kNoRes) return;
+  const uint32_t ty = res_type[r];
+  if (ty == CC_RES_MAP) wide = map_wide_op(o);
+  else if (ty == CC_RES_SET) wide = set_wide_op(o);
+  else return;
   if (!wide) {
+    // not a barrier here: a row that arms a TTL timer on this map / set?
+    if (!aux || !(ty == CC_RES_MAP ? ttl_op(o) && o != CC_OP_SET_ADD : o == CC_OP_SET_ADD) || (int64_t)aux[i] <= 0) return;
     *ttl_seen = 1u;
     return;
   }
@@ -209,6 +220,33 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
   if (pres > peak_lo[slot]) peak_lo[slot] = (uint32_t)min(pres, (uint64_t)0xFFFFFFFFu);
   out_status[row] = (uint8_t)st;
   out_value[row] = v;
+}
+
+// SetState results (SetState.java:49-87): add returns false whatever happened; remove returns whether the element
+// was present (the map remove it ran as returned the stored Boolean TRUE, or null).
+__global__ __launch_bounds__(kMwT) void k_set_results(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                     uint64_t n, const uint32_t* __restrict__ inst_res,
+                                                     const uint8_t* __restrict__ res_type, uint32_t max_inst,
+                                                     uint8_t* __restrict__ status, uint64_t* __restrict__ value) {
+  const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t o = op[i];
+  if (o != CC_OP_SET_ADD && o != CC_OP_SET_REMOVE) return;
+  const uint32_t in = inst[i];
+  if (in >= max_inst) return;
+  const uint32_t r = inst_res[in];
+  if (r == kNoRes || res_type[r] != CC_RES_SET) return;
+  const uint8_t s = status[i];
+  if (CC_STATUS_CODE(s) != CC_ST_OK) return;
+  value[i] = o == CC_OP_SET_ADD ? 0ull : (CC_STATUS_TAG(s) != CC_TAG_NULL ? 1ull : 0ull);
+  status[i] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+}
+
+int launch_set_results(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
+                       uint32_t max_inst, uint8_t* status, uint64_t* value, hipStream_t st) {
+  hipLaunchKernelGGL(k_set_results, dim3((uint32_t)((n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, n, inst_res,
+                     res_type, max_inst, status, value);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,

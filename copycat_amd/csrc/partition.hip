@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
   }
   const uint32_t sb_hot = sb_val + (EXT && map_bits ? (1u << map_bits) : 0u);
   auto route = [&](uint32_t r, uint32_t f, uint64_t key) -> uint32_t {
-    if (EXT && res_type[r] == CC_RES_MAP) {
+    if (EXT && is_keyed(res_type[r])) {
       const uint32_t kt = CC_FLAG_KTAG(f);
       const uint64_t h = map_hash(r, kt, key);
       if (nhot) {
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
     for (uint64_t i = tile0 + t; i < tile1; i += kPT) {
       const uint32_t r = resolve(inst_res, max_inst, inst[i]);
       if (r == kNoRes) continue;
-      const bool m = res_type[r] == CC_RES_MAP;
+      const bool m = is_keyed(res_type[r]);
       hist_add(route(r, m ? flags[i] : 0u, m ? ckey[i] : 0ull));
     }
   }
@@ -301,7 +301,16 @@ __global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ 
       if (EXT && rr[j] != kNoRes) {
         const uint32_t ty = res_type[rr[j]];
         const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
-        if (ty == CC_RES_MAP) {
+        if (is_keyed(ty)) {
+          if (ty == CC_RES_SET) {  // a set element is a map key holding Boolean TRUE (SetState.java:49-66)
+            const uint32_t mop = set_as_map_op(mt[j] & 0xFF);
+            uint32_t fl = (mt[j] >> 8) & 0xFF;
+            if (mop == CC_OP_MAP_PUTIFABSENT) {
+              fl = (fl & ~7u) | CC_TAG_BOOL;
+              aa[j].x = 1;
+            }
+            mt[j] = (mt[j] & ~0xFFFFu) | mop | (fl << 8);
+          }
           kk[j] = ckey[i];
           ii[j] = cidx ? cidx[i] : 0;
           xx[j] = rr[j];

@@ -52,6 +52,7 @@ extern "C" {
 #define CC_RES_LOCK      3  /* LockState         coordination/.../state/LockState.java:33 */
 #define CC_RES_ELECTION  4  /* LeaderElectionState coordination/.../state/LeaderElectionState.java:31 */
 #define CC_RES_GROUP     5  /* MembershipGroupState coordination/.../state/MembershipGroupState.java:33 */
+#define CC_RES_SET       6  /* SetState          collections/.../state/SetState.java:32 (shares the map table) */
 
 /* ---- op codes = Catalyst @SerializeWith ids of the inner operation ------------- */
 #define CC_OP_DELETE            1   /* ResourceStateMachine.DeleteCommand (no wire id) ResourceStateMachine.java:53 */
@@ -77,6 +78,15 @@ extern "C" {
 #define CC_OP_MAP_SIZE          71  /* query */
 #define CC_OP_MAP_CLEAR         72
 /* LeaderElectionCommands.java:80-99 */
+/* SetState (collections/.../state/SetCommands.java:133-238): the element travels in the key column (key tag in
+ * CC_FLAGS), the ttl of Add in aux */
+#define CC_OP_SET_CONTAINS     100  /* query */
+#define CC_OP_SET_ADD          101
+#define CC_OP_SET_REMOVE       102
+#define CC_OP_SET_SIZE         103  /* query */
+#define CC_OP_SET_ISEMPTY      104  /* query */
+#define CC_OP_SET_CLEAR        105
+
 #define CC_OP_ELECT_LISTEN     110
 #define CC_OP_ELECT_UNLISTEN   111
 #define CC_OP_ELECT_ISLEADER   112  /* query */

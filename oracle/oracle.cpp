@@ -272,6 +272,7 @@ struct orc {
       case CC_RES_VALUE:  // AtomicValueState.delete :146-157 (timer is always null, A2)
         if (r.v.has_current) { r.v.has_current = false; r.v.value = TV(); }
         return CC_ST_OK;
+      case CC_RES_SET:  // SetState.delete :123-134 (same shape: cancel timers, clean, clear)
       case CC_RES_MAP: {  // MapState.delete :264-274
         for (auto& kv : r.m.m) if (kv.second.timer) cancel(kv.second.timer);
         for (size_t i = 0; i < r.m.m.size(); ++i) r.m.order.on_remove();
@@ -549,6 +550,45 @@ struct orc {
         }
         break;
       }
+      case CC_RES_SET: {  // SetState (collections/src/main/java/io/atomix/collections/state/SetState.java)
+        MapSM& s = r.m;  // element -> Value{commit, timer}; the stored value is a Boolean TRUE marker
+        MapKey k{ktag_to_tag(CC_FLAG_KTAG(c.flags)), c.key};
+        int64_t ttl = (int64_t)c.aux;
+        switch (c.op) {
+          case CC_OP_SET_CONTAINS:  // contains :38-44
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, s.m.count(k) ? 1 : 0));
+            return;
+          case CC_OP_SET_ADD: {  // add :49-66 — returns false whether or not the element was added
+            if (!s.m.count(k)) {
+              uint64_t timer = 0;
+              if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
+              MapEntry e; e.value = tv(CC_TAG_BOOL, 1); e.commit_index = c.index; e.timer = timer; e.seq = s.order.on_insert();
+              s.m.emplace(k, e);
+            }
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
+            return;
+          }
+          case CC_OP_SET_REMOVE: {  // remove :70-87
+            auto it = s.m.find(k);
+            if (it == s.m.end()) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 0)); return; }
+            if (it->second.timer) cancel(it->second.timer);
+            s.m.erase(it); s.order.on_remove();
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, 1));
+            return;
+          }
+          case CC_OP_SET_SIZE:  // size :92-98 (int)
+            ret(CC_ST_OK, tv(CC_TAG_INT, (uint64_t)(int64_t)(int32_t)s.m.size()));
+            return;
+          case CC_OP_SET_ISEMPTY:  // isEmpty :103-109
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, s.m.empty() ? 1 : 0));
+            return;
+          case CC_OP_SET_CLEAR:  // clear :114-120 -> delete()
+            sm_delete(in.res);
+            ret(CC_ST_OK, TV());
+            return;
+        }
+        break;
+      }
       case CC_RES_LOCK: {
         LockSM& s = r.l;
         switch (c.op) {
@@ -705,7 +745,7 @@ orc* orc_create(uint32_t max_resources, uint32_t max_instances, uint32_t flags) 
 void orc_destroy(orc* o) { delete o; }
 
 int orc_resource_create(orc* o, uint32_t slot, uint32_t type) {
-  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_GROUP || o->res[slot].exists) return CC_ERR_INVALID;
+  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_SET || o->res[slot].exists) return CC_ERR_INVALID;
   o->init_resource(slot, type, slot);
   return CC_OK;
 }
@@ -908,13 +948,13 @@ int orc_read_value_state(orc* o, uint32_t first, uint32_t count, uint8_t* tag, u
 }
 
 int64_t orc_map_size(orc* o, uint32_t res) {
-  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_MAP) return -1;
+  if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET)) return -1;
   return (int64_t)o->res[res].m.m.size();
 }
 
 int64_t orc_map_entries(orc* o, uint32_t res, uint64_t cap, uint8_t* ktag, uint64_t* key, uint8_t* vtag, uint64_t* val,
                         uint64_t* commit_index) {
-  if (res >= o->max_res || !o->res[res].exists || o->res[res].type != CC_RES_MAP) return -1;
+  if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET)) return -1;
   std::vector<std::pair<MapKey, MapEntry>> v(o->res[res].m.m.begin(), o->res[res].m.m.end());
   std::sort(v.begin(), v.end(), [](const std::pair<MapKey, MapEntry>& x, const std::pair<MapKey, MapEntry>& y) {
     return x.first.tag != y.first.tag ? x.first.tag < y.first.tag : x.first.k < y.first.k;

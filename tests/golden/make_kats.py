@@ -362,6 +362,29 @@ def kats():
                .c(0, "MAP_PUT", key=foo, a=hw, aux=100, time=0)
                .c(0, "MAP_GET", key=foo, expect=hw, time=100)
                .c(0, "MAP_GET", key=foo, expect=NULL, time=100))
+    SETT = "collections/src/test/java/io/atomix/collections/DistributedSetTest.java"
+    # two clients, one set: contains false, add, contains true (both), remove, contains false (both)
+    out.append(K("set_add_remove", "reference", f"{SETT}:42-58").res(0, "SET").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(0, "SET_CONTAINS", key=hw, expect=B(False))
+               .c(1, "SET_CONTAINS", key=hw, expect=B(False))
+               .c(0, "SET_ADD", key=hw, expect=B(False))  # SetState.add returns false even when it adds (:65)
+               .c(0, "SET_CONTAINS", key=hw, expect=B(True))
+               .c(1, "SET_CONTAINS", key=hw, expect=B(True))
+               .c(1, "SET_REMOVE", key=hw, expect=B(True))
+               .c(0, "SET_CONTAINS", key=hw, expect=B(False))
+               .c(1, "SET_CONTAINS", key=hw, expect=B(False)))
+    k = K("set_ttl_size_clear", "defined", "collections/src/main/java/io/atomix/collections/state/SetState.java:49-134")
+    out.append(k.res(0, "SET").inst(0, 0, 100, 1)
+               .c(0, "SET_ADD", key=foo, aux=100, expect=B(False), time=0)
+               .c(0, "SET_ADD", key=bar, expect=B(False), time=0)
+               .c(0, "SET_ADD", key=bar, expect=B(False), time=0)
+               .c(0, "SET_SIZE", expect=I(2), time=0)
+               .c(0, "SET_SIZE", expect=I(2), time=150)  # manager mode: the due timer fires after this commit (A8)
+               .c(0, "SET_CONTAINS", key=foo, expect=B(False), time=150)
+               .c(0, "SET_SIZE", expect=I(1), time=150)
+               .c(0, "SET_REMOVE", key=foo, expect=B(False), time=150)
+               .c(0, "SET_CLEAR", time=150)
+               .c(0, "SET_ISEMPTY", expect=B(True), time=150))
     k = K("A8_timer_immediate_module_mode", "defined", "ResourceStateMachineExecutor.java:109-117", mode="immediate")
     out.append(k.res(0, "MAP").inst(0, 0, 100, 1)
                .c(0, "MAP_PUT", key=foo, a=hw, aux=100, time=0)

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 KAT_PATH = os.path.join(HERE, "golden", "kats.json")
 
 RES = {"VALUE": abi.CC_RES_VALUE, "MAP": abi.CC_RES_MAP, "LOCK": abi.CC_RES_LOCK, "ELECTION": abi.CC_RES_ELECTION,
-       "GROUP": abi.CC_RES_GROUP}
+       "GROUP": abi.CC_RES_GROUP, "SET": abi.CC_RES_SET}
 TAG = {"NULL": abi.CC_TAG_NULL, "LONG": abi.CC_TAG_LONG, "INT": abi.CC_TAG_INT, "BOOL": abi.CC_TAG_BOOL,
        "H": abi.CC_TAG_HANDLE, "SET": abi.CC_TAG_SET}
 EV = {"CHANGE": abi.CC_EV_CHANGE, "LOCK": abi.CC_EV_LOCK, "ELECT": abi.CC_EV_ELECT, "JOIN": abi.CC_EV_JOIN,
@@ -54,6 +54,7 @@ GPU_COORD_OPS = {"LOCK_LOCK", "LOCK_UNLOCK", "ELECT_LISTEN", "ELECT_UNLISTEN", "
 GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_GETORDEFAULT", "MAP_REMOVE",
                "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT", "MAP_CONTAINSVALUE", "MAP_SIZE",
                "MAP_ISEMPTY", "MAP_CLEAR"}
+GPU_SET_OPS = {"SET_CONTAINS", "SET_ADD", "SET_REMOVE", "SET_SIZE", "SET_ISEMPTY", "SET_CLEAR"}
 
 
 def gpu_eligible(kat):
@@ -61,14 +62,14 @@ def gpu_eligible(kat):
     every Map op (TTL timers included), lock / election / group ops except schedule, Delete, and clock advances;
     no registry control or session-close steps (host control plane)."""
     types = {r[1] for r in kat["resources"]}
-    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP"}:
+    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET"}:
         return False
     for s in kat["steps"]:
         if "control" in s or "close" in s:
             return False
         if "commit" in s:
             c = s["commit"]
-            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS:
+            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS | GPU_SET_OPS:
                 return False
     return True
 
