@@ -504,6 +504,67 @@ int launch_time_check(const uint64_t* time, uint64_t n, uint64_t* clock, uint32_
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ---- MembershipGroupState.schedule (op 122) :86-103: a barrier row of the batch (engine.hip) --------------
+// The row's status against the group as it stands at that log position; *found tells the host to arm the timer.
+__global__ void k_group_schedule(const uint8_t* __restrict__ coord, uint32_t slot, uint64_t member, uint64_t row,
+                                 uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value, uint32_t* __restrict__ found) {
+  if (threadIdx.x != 0) return;
+  const uint8_t* blk = coord + (uint64_t)slot * kCoordBlock;
+  const CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
+  const CoordEnt* E = reinterpret_cast<const CoordEnt*>(blk + sizeof(CoordHdr));
+  uint32_t f = 0;
+  for (uint32_t q = 0; q < h.n && q < (uint32_t)kCoordCap; ++q) f |= E[q].x == member ? 1u : 0u;
+  out_status[row] = (uint8_t)(f ? CC_STATUS(CC_ST_OK, CC_TAG_NULL) : CC_STATUS(CC_ST_ILLEGAL_ARGUMENT, CC_TAG_NULL));
+  out_value[row] = 0;
+  *found = f;
+}
+
+// The timer fires (:92-98): publish "execute"(callback) to the member's instance if it is still in the group.
+__global__ void k_group_fire(const uint8_t* __restrict__ coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload,
+                             uint32_t pos, unsigned long long* __restrict__ ev_total, uint64_t cap,
+                             uint32_t* __restrict__ o_pos, uint32_t* __restrict__ o_target, uint8_t* __restrict__ o_code,
+                             uint8_t* __restrict__ o_src, uint8_t* __restrict__ o_tag, uint64_t* __restrict__ o_payload,
+                             uint32_t* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  const uint8_t* blk = coord + (uint64_t)slot * kCoordBlock;
+  const CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
+  const CoordEnt* E = reinterpret_cast<const CoordEnt*>(blk + sizeof(CoordHdr));
+  for (uint32_t q = 0; q < h.n && q < (uint32_t)kCoordCap; ++q) {
+    if (E[q].x != member) continue;
+    if (!o_pos) {
+      atomicOr(err, kErrUnsupported);  // an event with no stream to publish it to
+      return;
+    }
+    const unsigned long long k = *ev_total;
+    if (k >= cap) {
+      atomicOr(err, kErrEvents);
+      return;
+    }
+    o_pos[k] = pos;
+    o_target[k] = E[q].inst;
+    o_code[k] = CC_EV_EXECUTE;
+    o_src[k] = CC_EVSRC_TIMER;
+    o_tag[k] = (uint8_t)tag;
+    o_payload[k] = payload;
+    *ev_total = k + 1;
+    return;
+  }
+}
+
+int launch_group_schedule(const uint8_t* coord, uint32_t slot, uint64_t member, uint64_t row, uint8_t* out_status,
+                          uint64_t* out_value, uint32_t* found, hipStream_t st) {
+  hipLaunchKernelGGL(k_group_schedule, dim3(1), dim3(64), 0, st, coord, slot, member, row, out_status, out_value, found);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_group_fire(const uint8_t* coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
+                      unsigned long long* ev_total, const cc_events* ev, uint32_t* err, hipStream_t st) {
+  hipLaunchKernelGGL(k_group_fire, dim3(1), dim3(64), 0, st, coord, slot, member, tag, payload, pos, ev_total,
+                     ev ? ev->capacity : 0, ev ? ev->pos : nullptr, ev ? ev->target : nullptr, ev ? ev->code : nullptr,
+                     ev ? ev->src : nullptr, ev ? ev->tag : nullptr, ev ? ev->payload : nullptr, err);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_clock_advance(const uint64_t* time, uint64_t n, uint64_t now, uint64_t* clock, hipStream_t st) {
   hipLaunchKernelGGL(k_clock_advance, dim3(1), dim3(1), 0, st, time, n, now, clock);
   return hipGetLastError() == hipSuccess ? 0 : -1;

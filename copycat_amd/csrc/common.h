@@ -148,7 +148,7 @@ __host__ __device__ inline bool op_on_gpu(uint32_t type, uint32_t op) {
   if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops (whole-map ops: map_wide.hip)
   if (type == CC_RES_SET) return op >= 100 && op <= 102;
   if (type == CC_RES_LOCK || type == CC_RES_ELECTION) return op_registered(type, op);
-  if (type == CC_RES_GROUP) return op_registered(type, op) && op != CC_OP_GROUP_SCHEDULE;
+  if (type == CC_RES_GROUP) return op_registered(type, op);  // schedule rows are batch barriers (engine.hip)
   return false;
 }
 

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "common.h"
@@ -94,6 +95,15 @@ struct cc_engine {
   uint32_t* d_ttl_seen = nullptr;
   bool ttl_live = false;
   bool has_sets = false;  // SetState resources share the map table (results rewritten by k_set_results)
+  // MembershipGroupState.schedule timers (MembershipGroupState.java:86-103): armed by schedule barrier rows, fired
+  // at the batch boundary where the reference's fire_due runs (host-ordered by (deadline, id))
+  struct GroupTimer {
+    uint64_t deadline, id, member, payload;
+    uint32_t slot, tag;
+    uint64_t fire_b;  // boundary in the current batch (rows before it applied first); ~0: not in this batch
+  };
+  std::vector<GroupTimer> gtimers;
+  uint64_t gtimer_seq = 0;
   uint32_t* d_hot_rpre = nullptr;
   uint32_t* d_hot_rstart = nullptr;
   uint32_t* d_hot_len = nullptr;
@@ -292,14 +302,11 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_tbl_ins, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_hot, sizeof(HotKey) * kHotMax);
     ALLOC(e->d_hot_n, sizeof(uint32_t));
-    ALLOC(e->d_bar, sizeof(uint32_t) * kBarCap);
-    ALLOC(e->d_bar_n, sizeof(uint32_t));
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
     ALLOC(e->d_tbl_dl, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_map_row, sizeof(uint32_t) * e->sub_batch);
-    ALLOC(e->d_ttl_seen, sizeof(uint32_t));
     ALLOC(e->d_hot_rpre, sizeof(uint32_t) * kHotMax * (kMaxTiles + 1));
     ALLOC(e->d_hot_rstart, sizeof(uint32_t) * kHotMax * kMaxTiles);
     ALLOC(e->d_hot_len, sizeof(uint32_t) * kHotMax);
@@ -310,6 +317,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_rst_status, e->sub_batch + 4 * kPT);  // + dummy rows for unconditional result stores
   ALLOC(e->d_rst_value, sizeof(uint64_t) * (e->sub_batch + 4 * kPT));
   ALLOC(e->d_err, sizeof(uint32_t));
+  ALLOC(e->d_bar, sizeof(uint32_t) * kBarCap);
+  ALLOC(e->d_bar_n, sizeof(uint32_t));
+  ALLOC(e->d_ttl_seen, sizeof(uint32_t));
   ALLOC(e->d_last_index, sizeof(uint64_t));
   ALLOC(e->d_sb_kind, e->sb);
   ALLOC(e->d_inst_id, sizeof(uint64_t) * cfg->max_instances);
@@ -465,6 +475,10 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
     HIPCHECK(hipStreamSynchronize(e->own_stream));
   }
   e->res_type[slot] = CC_RES_NONE;
+  // ResourceManagerStateMachineExecutor.close cancels the resource's timers
+  e->gtimers.erase(std::remove_if(e->gtimers.begin(), e->gtimers.end(),
+                                  [slot](const cc_engine::GroupTimer& g) { return g.slot == slot; }),
+                   e->gtimers.end());
   if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)slot * kCoordBlock, 0, kCoordBlock));
   HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
   HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
@@ -535,7 +549,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   // Whole-map ops are barriers (map_wide.hip): find them (one sync), then apply the rows between them as segments.
   e->bars.clear();
   uint64_t clock_before = 0;  // the engine clock before this batch (TTL mode and barrier rows need it on the host)
-  if (e->map_bits) {
+  if (e->map_bits || e->coord_on) {
     HIPCHECK(hipMemsetAsync(e->d_ttl_seen, 0, sizeof(uint32_t), st));
     if (launch_map_barriers(c->inst, c->op, c->aux, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar,
                             e->d_bar_n, kBarCap, e->d_ttl_seen, st))
@@ -546,7 +560,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (ttl_seen) e->ttl_live = true;
-    if (nb > kBarCap) return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) in one batch than kBarCap");
+    if (nb > kBarCap)
+      return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) and group schedules in one batch than kBarCap");
     if (nb) {
       e->bars.resize(nb);
       HIPCHECK(hipMemcpy(e->bars.data(), e->d_bar, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost));
@@ -557,9 +572,53 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (e->coord_on) HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), st));
     if (launch_time_check(c->time, n, e->d_clock, e->d_err, st)) return set_err(CC_ERR_HIP, "time check", hipGetLastError());
   }
-  for (size_t seg = 0; seg <= e->bars.size(); ++seg) {
-  const uint64_t seg_lo = seg == 0 ? 0 : (uint64_t)e->bars[seg - 1] + 1;
-  const uint64_t seg_hi = seg < e->bars.size() ? (uint64_t)e->bars[seg] : n;
+  // Group timers: where each pending one fires in this batch (the clock at row r is max(clock_before, time[r])).
+  const bool deferred = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) != 0;
+  auto time_at = [&](uint64_t r, uint64_t& t) -> int {
+    t = clock_before;
+    if (c->time) {
+      HIPCHECK(hipMemcpy(&t, c->time + r, sizeof t, hipMemcpyDeviceToHost));
+      t = std::max(t, clock_before);
+    }
+    return CC_OK;
+  };
+  // first row r >= from whose clock reaches d -> the boundary the timer fires at (manager mode: after row r;
+  // module mode: before it, A8), or ~0 when no row of this batch reaches it
+  auto fire_boundary = [&](uint64_t d, uint64_t from, uint64_t& b) -> int {
+    b = ~0ull;
+    uint64_t lo_r = from, hi_r = n;  // search [lo_r, hi_r)
+    while (lo_r < hi_r) {
+      const uint64_t mid = (lo_r + hi_r) / 2;
+      uint64_t t = 0;
+      int rc = time_at(mid, t);
+      if (rc) return rc;
+      if (t >= d) hi_r = mid;
+      else lo_r = mid + 1;
+    }
+    if (lo_r < n) b = deferred ? lo_r + 1 : lo_r;
+    return CC_OK;
+  };
+  for (auto& gt : e->gtimers) {
+    int rc = fire_boundary(gt.deadline, 0, gt.fire_b);
+    if (rc) return rc;
+  }
+  uint64_t cur = 0;
+  size_t bi = 0;
+  for (;;) {
+  // the next thing in log order: a barrier row, or a group timer firing (timers first at the same boundary)
+  const uint64_t bar_b = bi < e->bars.size() ? (uint64_t)e->bars[bi] : ~0ull;
+  size_t tk = e->gtimers.size();
+  for (size_t q = 0; q < e->gtimers.size(); ++q) {
+    const auto& g = e->gtimers[q];
+    if (g.fire_b == ~0ull || g.fire_b < cur) continue;
+    if (tk == e->gtimers.size()) { tk = q; continue; }
+    const auto& b = e->gtimers[tk];
+    if (std::make_tuple(g.fire_b, g.deadline, g.id) < std::make_tuple(b.fire_b, b.deadline, b.id)) tk = q;
+  }
+  const uint64_t tim_b = tk < e->gtimers.size() ? e->gtimers[tk].fire_b : ~0ull;
+  const int action = (tim_b != ~0ull && tim_b <= bar_b) ? 2 : (bar_b != ~0ull ? 1 : 0);
+  const uint64_t seg_lo = cur;
+  const uint64_t seg_hi = action == 2 ? tim_b : (action == 1 ? bar_b : n);
   for (uint64_t lo = seg_lo; lo < seg_hi; lo += e->sub_batch) {
     const uint64_t hi = std::min(seg_hi, lo + e->sub_batch);
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
@@ -761,8 +820,20 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       if (launch_events(ea, st)) return set_err(CC_ERR_HIP, "events launch", hipGetLastError());
     }
   }
-  if (seg < e->bars.size()) {  // the barrier row, against the table as it stands after the rows before it
+  if (action == 2) {  // a group timer fires here (MembershipGroupState.java:92-98)
+    cc_engine::GroupTimer gt = e->gtimers[tk];
+    e->gtimers.erase(e->gtimers.begin() + (ptrdiff_t)tk);
+    const uint32_t pos = (uint32_t)(deferred ? seg_hi - 1 : seg_hi);
+    if (launch_group_fire(e->d_coord, gt.slot, gt.member, gt.tag, gt.payload, pos, e->d_ev_total, ev, e->d_err, st))
+      return set_err(CC_ERR_HIP, "group timer launch", hipGetLastError());
+    cur = seg_hi;
+    continue;
+  }
+  if (action == 0) break;
+  {  // the barrier row, against the state as it stands after the rows before it
     const uint64_t row = seg_hi;
+    cur = row + 1;
+    ++bi;
     uint32_t in = 0, res = 0;
     uint8_t op = 0, fl = 0;
     uint64_t a = 0;
@@ -771,6 +842,32 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemcpy(&fl, c->flags + row, 1, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(&a, c->a + row, sizeof a, hipMemcpyDeviceToHost));
     res = e->inst_res[in];
+    if (e->res_type[res] == CC_RES_GROUP) {  // schedule :86-103 (member = key, callback = a, delay = aux)
+      uint64_t member = 0, delay = 0;
+      HIPCHECK(hipMemcpy(&member, c->key + row, sizeof member, hipMemcpyDeviceToHost));
+      if (c->aux) HIPCHECK(hipMemcpy(&delay, c->aux + row, sizeof delay, hipMemcpyDeviceToHost));
+      if (launch_group_schedule(e->d_coord, res, member, row, out->status, out->value, e->d_ttl_seen, st))
+        return set_err(CC_ERR_HIP, "group schedule launch", hipGetLastError());
+      uint32_t found = 0;
+      HIPCHECK(hipMemcpyAsync(&found, e->d_ttl_seen, sizeof found, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (found) {
+        uint64_t now = 0;
+        int rc = time_at(row, now);
+        if (rc) return rc;
+        cc_engine::GroupTimer gt{};
+        gt.deadline = now + ((int64_t)delay > 0 ? delay : 0);
+        gt.id = ++e->gtimer_seq;
+        gt.member = member;
+        gt.tag = CC_FLAG_TAG_A(fl);
+        gt.payload = gt.tag == CC_TAG_NULL ? 0 : a;
+        gt.slot = res;
+        rc = fire_boundary(gt.deadline, deferred ? row : row + 1, gt.fire_b);
+        if (rc) return rc;
+        e->gtimers.push_back(gt);
+      }
+      continue;
+    }
     MapWideArgs mw{};
     mw.slot = res;
     mw.op = e->res_type[res] == CC_RES_SET ? set_as_map_op(op) : op;
@@ -1167,14 +1264,34 @@ extern "C" int cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, 
   return CC_OK;
 }
 
-extern "C" int cc_advance_time(cc_engine* e, uint64_t now) {
+extern "C" int cc_advance_time_events(cc_engine* e, uint64_t now, const cc_events* d_events) {
   if (!e) return CC_ERR_INVALID;
   int rc = quiesce(e);
   if (rc) return rc;
+  if (e->coord_on) {  // due group timers fire in (deadline, id) order; events at pos 0xFFFFFFFF (no commit)
+    HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), e->own_stream));
+    std::sort(e->gtimers.begin(), e->gtimers.end(), [](const cc_engine::GroupTimer& x, const cc_engine::GroupTimer& y) {
+      return x.deadline != y.deadline ? x.deadline < y.deadline : x.id < y.id;
+    });
+    uint64_t clk = 0;  // the reference fires everything due by max(clock, now)
+    HIPCHECK(hipMemcpy(&clk, e->d_clock, sizeof clk, hipMemcpyDeviceToHost));
+    const uint64_t thr = std::max(clk, now);
+    size_t k = 0;
+    for (; k < e->gtimers.size() && e->gtimers[k].deadline <= thr; ++k) {
+      const auto& gt = e->gtimers[k];
+      if (launch_group_fire(e->d_coord, gt.slot, gt.member, gt.tag, gt.payload, 0xFFFFFFFFu, e->d_ev_total, d_events, e->d_err,
+                            e->own_stream))
+        return set_err(CC_ERR_HIP, "group timer launch", hipGetLastError());
+    }
+    e->gtimers.erase(e->gtimers.begin(), e->gtimers.begin() + (ptrdiff_t)k);
+    if (d_events) HIPCHECK(hipMemcpyAsync(d_events->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, e->own_stream));
+  }
   if (launch_clock_advance(nullptr, 0, now, e->d_clock, e->own_stream)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
   HIPCHECK(hipStreamSynchronize(e->own_stream));
-  return CC_OK;
+  return check_device_err(e);
 }
+
+extern "C" int cc_advance_time(cc_engine* e, uint64_t now) { return cc_advance_time_events(e, now, nullptr); }
 
 static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unpermute", "k_apply_map", "k_map_hot",
                                           "k_apply_coord", "k_events"};
@@ -1232,7 +1349,7 @@ static std::vector<Section> snap_sections(cc_engine* e) {
 
 extern "C" int cc_snapshot_size(cc_engine* e, uint64_t* bytes) {
   if (!e || !bytes) return CC_ERR_INVALID;
-  uint64_t total = sizeof(SnapHdr);
+  uint64_t total = sizeof(SnapHdr) + 16 + e->gtimers.size() * sizeof(cc_engine::GroupTimer);
   for (const Section& x : snap_sections(e)) total += 8 + x.bytes;
   *bytes = total;
   return CC_OK;
@@ -1268,6 +1385,10 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
     else memcpy(p, x.host, x.bytes);
     p += x.bytes;
   }
+  const uint64_t ng = e->gtimers.size();  // pending MembershipGroup.schedule timers
+  memcpy(p, &ng, 8);
+  memcpy(p + 8, &e->gtimer_seq, 8);
+  if (ng) memcpy(p + 16, e->gtimers.data(), ng * sizeof(cc_engine::GroupTimer));
   return CC_OK;
 }
 
@@ -1295,6 +1416,14 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
     else memcpy(x.host, p, b);
     p += b;
   }
+  uint64_t ng = 0;
+  if (p + 16 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&ng, p, 8);
+  memcpy(&e->gtimer_seq, p + 8, 8);
+  p += 16;
+  if (p + ng * sizeof(cc_engine::GroupTimer) > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  e->gtimers.resize(ng);
+  if (ng) memcpy(e->gtimers.data(), p, ng * sizeof(cc_engine::GroupTimer));
   e->applied = h.applied;
   e->applied_pending = false;
   e->has_sets = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_SET) != e->res_type.end();

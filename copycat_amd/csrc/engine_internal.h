@@ -136,6 +136,11 @@ struct MapWideArgs {
   uint32_t* err;
 };
 int launch_map_wide(const MapWideArgs& a, hipStream_t st);
+// MembershipGroupState.schedule barrier rows and their timers (apply_coord.hip)
+int launch_group_schedule(const uint8_t* coord, uint32_t slot, uint64_t member, uint64_t row, uint8_t* out_status,
+                          uint64_t* out_value, uint32_t* found, hipStream_t st);
+int launch_group_fire(const uint8_t* coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
+                      unsigned long long* ev_total, const cc_events* ev, uint32_t* err, hipStream_t st);
 // SetState result rewrite after the batch (map_wide.hip)
 int launch_set_results(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
                        uint32_t max_inst, uint8_t* status, uint64_t* value, hipStream_t st);

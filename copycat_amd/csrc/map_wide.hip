@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   if (i >= n) return;
   const uint32_t o = op[i];
-  bool wide = map_wide_op(o) || set_wide_op(o);
+  bool wide = map_wide_op(o) || set_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
   if (ttl && (int64_t)aux[i] <= 0) {
@@ -64,7 +64,9 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   const uint32_t ty = res_type[r];
   if (ty == CC_RES_MAP) wide = map_wide_op(o);
   else if (ty == CC_RES_SET) wide = set_wide_op(o);
+  else if (ty == CC_RES_GROUP) wide = o == CC_OP_GROUP_SCHEDULE;  // MembershipGroupState.schedule: a timer
   else return;
+  if (ty == CC_RES_GROUP && !wide) return;
   if (!wide) {
     // not a barrier here: a row that arms a TTL timer on this map / set?
     if (!aux || !(ty == CC_RES_MAP ? ttl_op(o) && o != CC_OP_SET_ADD : o == CC_OP_SET_ADD) || (int64_t)aux[i] <= 0) return;

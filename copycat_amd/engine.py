@@ -58,6 +58,7 @@ def lib():
             "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
             "cc_read_group_members": (i32, [P, u32, u64, P, P]),
             "cc_advance_time": (i32, [P, u64]),
+            "cc_advance_time_events": (i32, [P, u64, P]),
             "cc_snapshot_size": (i32, [P, P]),
             "cc_snapshot_save": (i32, [P, P, u64]),
             "cc_snapshot_restore": (i32, [P, P, u64]),
@@ -266,6 +267,13 @@ class Engine:
 
     def advance_time(self, now):
         _check(self.L.cc_advance_time(self.h, now))
+
+    def advance_time_events(self, now, capacity=1024, device="cuda"):
+        """advance_time publishing the events of group timers that come due (see cc_advance_time_events)."""
+        evs = DeviceEvents(capacity, device=device)
+        ev = evs.struct()
+        _check(self.L.cc_advance_time_events(self.h, now, C.byref(ev)))
+        return evs.host()
 
     def snapshot(self) -> bytes:
         """The engine's whole state (device arrays + host registry mirrors) as bytes (cc_snapshot_save)."""

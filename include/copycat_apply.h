@@ -285,6 +285,10 @@ int  cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* 
 /* Log time advanced without a commit (ResourceManagerStateMachineExecutor timers): due lock
  * timeouts take effect (they publish nothing, LockState.java:54-58). */
 int  cc_advance_time(cc_engine* e, uint64_t now);
+/* Same, publishing the "execute" events of MembershipGroup.schedule timers that come due (pos 0xFFFFFFFF,
+ * src CC_EVSRC_TIMER) to d_events; *d_events->count is written.  cc_advance_time fails with CC_ERR_UNSUPPORTED
+ * when such an event is due and has no stream. */
+int  cc_advance_time_events(cc_engine* e, uint64_t now, const cc_events* d_events);
 
 /* ---- session close / expire fan-out (ResourceManager.close :250-264, expire :238-247) -------------------
  * For each client session of h_clients, in order: every instance it owns, in java.util.HashMap iteration order of

@@ -50,7 +50,7 @@ def op_code(name):
 
 GPU_VALUE_OPS = {"VALUE_GET", "VALUE_SET", "VALUE_CAS", "VALUE_GETANDSET", "VALUE_LISTEN", "VALUE_UNLISTEN"}
 GPU_COORD_OPS = {"LOCK_LOCK", "LOCK_UNLOCK", "ELECT_LISTEN", "ELECT_UNLISTEN", "ELECT_ISLEADER", "GROUP_JOIN",
-                 "GROUP_LEAVE", "GROUP_EXECUTE"}
+                 "GROUP_LEAVE", "GROUP_EXECUTE", "GROUP_SCHEDULE"}
 GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_GETORDEFAULT", "MAP_REMOVE",
                "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT", "MAP_CONTAINSVALUE", "MAP_SIZE",
                "MAP_ISEMPTY", "MAP_CLEAR"}
@@ -59,7 +59,7 @@ GPU_SET_OPS = {"SET_CONTAINS", "SET_ADD", "SET_REMOVE", "SET_SIZE", "SET_ISEMPTY
 
 def gpu_eligible(kat):
     """KATs whose every step this build applies on the GPU: AtomicValue ops (listeners with CC_CFG_VALUE_EVENTS),
-    every Map op (TTL timers included), lock / election / group ops except schedule, Delete, and clock advances;
+    every Map and Set op (TTL timers included), lock / election / group ops, Delete, and clock advances;
     no registry control or session-close steps (host control plane)."""
     types = {r[1] for r in kat["resources"]}
     if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET"}:
@@ -290,8 +290,9 @@ class EngineBackend:
         return s, v, evs, aux
 
     def advance(self, now):
-        self.E.advance_time(now)
-        return []
+        ev = self.E.advance_time_events(now)
+        return [(int(ev["pos"][i]), int(ev["target"][i]), int(ev["code"][i]), int(ev["tag"][i]), int(ev["payload"][i]))
+                for i in range(len(ev["pos"]))]
 
     def value_state(self, res):
         t, v, c = self.E.value_state(res, 1)

@@ -139,15 +139,12 @@ def test_lock_queue_capacity_fails_loudly():
     assert ei.value.rc == abi.CC_ERR_CAPACITY
 
 
-def test_events_without_stream_and_schedule_fail_loudly():
+def test_events_without_stream_fail_loudly():
     from copycat_amd.engine import EngineError
 
     E, O, _ = _setup(np.array([L, G], np.uint8), 2, FLAGS)
     with pytest.raises(EngineError) as ei:  # the lock event has nowhere to go
         E.apply_host(_one(abi.CC_OP_LOCK_LOCK, 0))
-    assert ei.value.rc == abi.CC_ERR_UNSUPPORTED
-    with pytest.raises(EngineError) as ei:
-        E.apply_host_events(_one(abi.CC_OP_GROUP_SCHEDULE, 2, aux=10, index=2))
     assert ei.value.rc == abi.CC_ERR_UNSUPPORTED
 
 
@@ -173,3 +170,39 @@ def test_event_stream_capacity():
     with pytest.raises(EngineError) as ei:
         E.apply_host_events(b, capacity=100)
     assert ei.value.rc == abi.CC_ERR_CAPACITY
+
+
+@pytest.mark.parametrize("flags", [FLAGS, abi.CC_CFG_VALUE_EVENTS], ids=["manager", "module"])
+def test_group_schedule_timers(flags):
+    """MembershipGroup.schedule (MembershipGroupState.java:86-103) as batch barriers: unknown member ->
+    IllegalArgumentException; otherwise a timer that publishes "execute"(callback) to the member, if it is still
+    in the group, at the commit where the reference's fire_due runs (A8: after the commit that advanced the clock
+    in manager mode, before it in module mode); timers carried across batches and fired by advance_time."""
+    from copycat_amd.workload import coord_random_stream
+
+    types = np.array([L, E_, G, V, G, G] * 8, np.uint8)
+    K = 5
+    E, O, max_inst = _setup(types, K, flags)
+    b = coord_random_stream(60_000, types, K, max_inst, seed=17)
+    rng = np.random.default_rng(17)
+    res_of = np.where(b.inst < max_inst, b.inst // K, 0)
+    grp = np.nonzero((types[np.minimum(res_of, len(types) - 1)] == G) & (b.inst < len(types) * K))[0]
+    rows = rng.choice(grp, size=300, replace=False)
+    b.op[rows] = abi.CC_OP_GROUP_SCHEDULE
+    g = res_of[rows]
+    member = 1000 + g * K + rng.integers(0, K + 2, len(rows))  # some ids are not instances of this group
+    b.key[rows] = member.astype(np.uint64)
+    b.flags[rows] = abi.cc_flags(abi.CC_TAG_HANDLE, 0, 0)
+    b.a[rows] = rng.integers(0, 1 << 20, len(rows)).astype(np.uint64)
+    b.aux[rows] = rng.integers(-5, 400, len(rows)).astype(np.int64).view(np.uint64)
+    for lo, hi in [(0, 20_000), (20_000, 20_001), (20_001, 60_000)]:
+        _check_batch(E, O, b.slice(lo, hi))
+    _check_state(E, O, types)
+    now = int(b.time[-1]) + 500
+    ev = E.advance_time_events(now, capacity=4096)
+    O.advance_time(now)
+    oe = O.take_events()
+    got = sorted(zip(ev["target"].tolist(), ev["code"].tolist(), ev["tag"].tolist(), ev["payload"].tolist()))
+    want = sorted(zip(oe["target"].tolist(), oe["code"].tolist(), oe["tag"].tolist(), oe["payload"].tolist()))
+    assert got == want
+    assert (ev["src"] == abi.CC_EVSRC_TIMER).all() and (ev["pos"] == 0xFFFFFFFF).all()
