@@ -22,6 +22,8 @@ CC_RES_LOCK = 3
 CC_RES_ELECTION = 4
 CC_RES_GROUP = 5
 CC_RES_SET = 6
+CC_RES_QUEUE = 7
+CC_QUEUE_CAP = 64
 
 CC_OP_DELETE = 1
 CC_OP_VALUE_GET = 50
@@ -43,6 +45,16 @@ CC_OP_MAP_REPLACEIFPRESENT = 69
 CC_OP_MAP_ISEMPTY = 70
 CC_OP_MAP_SIZE = 71
 CC_OP_MAP_CLEAR = 72
+CC_OP_QUEUE_CONTAINS = 90
+CC_OP_QUEUE_ADD = 91
+CC_OP_QUEUE_OFFER = 92
+CC_OP_QUEUE_PEEK = 93
+CC_OP_QUEUE_POLL = 94
+CC_OP_QUEUE_ELEMENT = 95
+CC_OP_QUEUE_REMOVE = 96
+CC_OP_QUEUE_SIZE = 97
+CC_OP_QUEUE_ISEMPTY = 98
+CC_OP_QUEUE_CLEAR = 99
 CC_OP_SET_CONTAINS = 100
 CC_OP_SET_ADD = 101
 CC_OP_SET_REMOVE = 102
@@ -74,6 +86,7 @@ CC_ST_ILLEGAL_ARGUMENT = 4
 CC_ST_NULL_POINTER = 5
 CC_ST_TYPE_MISMATCH = 6
 CC_ST_UNKNOWN_RESOURCE = 7
+CC_ST_NO_SUCH_ELEMENT = 8
 
 CC_EV_CHANGE = 1
 CC_EV_LOCK = 2
@@ -103,6 +116,7 @@ TYPE_OPS = {
     CC_RES_ELECTION: {CC_OP_DELETE, 110, 111, 112},
     CC_RES_GROUP: {CC_OP_DELETE, 120, 121, 122, 123},
     CC_RES_SET: {CC_OP_DELETE} | set(range(100, 106)),
+    CC_RES_QUEUE: {CC_OP_DELETE} | set(range(90, 100)),
 }
 # key tags of the flags column (keys are never null)
 KTAG_OF_TAG = {CC_TAG_LONG: 0, CC_TAG_INT: 1, CC_TAG_BOOL: 2, CC_TAG_HANDLE: 3}

@@ -242,6 +242,89 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
       ev(E[p].inst, CC_EV_EXECUTE, CC_FLAG_TAG_A(r.flags), r.a);
       return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
     }
+    case CC_RES_QUEUE: {  // QueueState.java:33-199: an ArrayDeque of (value tag in pad, payload in x), FIFO ring
+      const uint32_t ta = CC_FLAG_TAG_A(r.flags);
+      const uint64_t pa = ta ? r.a : 0;
+      auto at = [&](uint32_t i) -> CoordEnt& { return E[(h.head + i) % kCoordCap]; };
+      auto first_match = [&](uint32_t& pos) -> int {  // 1 match, 0 none, -1 NPE (a stored null's equals)
+        for (uint32_t i = 0; i < h.n; ++i) {
+          const CoordEnt& e = at(i);
+          if (e.pad == CC_TAG_NULL) return -1;
+          if (e.pad == ta && e.x == pa) {
+            pos = i;
+            return 1;
+          }
+        }
+        return 0;
+      };
+      auto pop = [&]() {
+        h.head = (h.head + 1) % kCoordCap;
+        --h.n;
+      };
+      switch (r.op) {
+        case CC_OP_DELETE:
+        case CC_OP_QUEUE_CLEAR:  // clear :184-190 / delete :191-199
+          h.n = 0;
+          h.head = 0;
+          return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+        case CC_OP_QUEUE_CONTAINS: {  // contains :36-46
+          uint32_t pos = 0;
+          const int m = first_match(pos);
+          if (m < 0) return CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
+          rv = m;
+          return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+        }
+        case CC_OP_QUEUE_ADD:    // add :51-59
+        case CC_OP_QUEUE_OFFER:  // offer :64-72 — both answer false
+          if (h.n == (uint32_t)kCoordCap) {
+            err |= kErrCapacity;
+          } else {
+            at(h.n) = CoordEnt{pa, r.idx, r.inst, ta};
+            ++h.n;
+          }
+          return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+        case CC_OP_QUEUE_PEEK:  // peek :77-87
+          if (!h.n) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+          rv = at(0).x;
+          return CC_STATUS(CC_ST_OK, at(0).pad);
+        case CC_OP_QUEUE_POLL: {  // poll :92-105
+          if (!h.n) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+          const CoordEnt e = at(0);
+          pop();
+          rv = e.x;
+          return CC_STATUS(CC_ST_OK, e.pad);
+        }
+        case CC_OP_QUEUE_ELEMENT:  // element :111-124 (throws when empty; the head stays)
+          if (!h.n) return CC_STATUS(CC_ST_NO_SUCH_ELEMENT, CC_TAG_NULL);
+          rv = at(0).x;
+          return CC_STATUS(CC_ST_OK, at(0).pad);
+        case CC_OP_QUEUE_REMOVE: {  // remove :130-157
+          if (ta != CC_TAG_NULL) {
+            uint32_t pos = 0;
+            const int m = first_match(pos);
+            if (m < 0) return CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
+            if (m) {
+              for (uint32_t i = pos; i + 1 < h.n; ++i) at(i) = at(i + 1);
+              --h.n;
+            }
+            rv = m;
+            return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+          }
+          if (!h.n) return CC_STATUS(CC_ST_NO_SUCH_ELEMENT, CC_TAG_NULL);  // ArrayDeque.remove()
+          const CoordEnt e = at(0);
+          pop();
+          rv = e.x;
+          return CC_STATUS(CC_ST_OK, e.pad);
+        }
+        case CC_OP_QUEUE_SIZE:  // size :162-168 (int)
+          rv = h.n;
+          return CC_STATUS(CC_ST_OK, CC_TAG_INT);
+        case CC_OP_QUEUE_ISEMPTY:  // isEmpty :173-179
+          rv = h.n == 0;
+          return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+      }
+      return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
+    }
     case CC_RES_VALUE: {
       const uint32_t ta = CC_FLAG_TAG_A(r.flags), tb = CC_FLAG_TAG_B(r.flags);
       const uint64_t pa = ta ? r.a : 0, pb = tb ? r.b : 0;

@@ -123,6 +123,7 @@ __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {
     case CC_RES_ELECTION: return op >= 110 && op <= 112;
     case CC_RES_GROUP: return op >= 120 && op <= 123;
     case CC_RES_SET: return op >= 100 && op <= 105;
+    case CC_RES_QUEUE: return op >= 90 && op <= 99;
   }
   return false;
 }
@@ -147,6 +148,7 @@ __host__ __device__ inline bool op_on_gpu(uint32_t type, uint32_t op) {
   if (type == CC_RES_VALUE) return op == CC_OP_DELETE || (op >= 50 && op <= 53);
   if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops (whole-map ops: map_wide.hip)
   if (type == CC_RES_SET) return op >= 100 && op <= 102;
+  if (type == CC_RES_QUEUE) return op_registered(type, op);
   if (type == CC_RES_LOCK || type == CC_RES_ELECTION) return op_registered(type, op);
   if (type == CC_RES_GROUP) return op_registered(type, op);  // schedule rows are batch barriers (engine.hip)
   return false;

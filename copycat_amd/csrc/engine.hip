@@ -232,7 +232,9 @@ static int ensure_ext(cc_engine* e, bool coord) {
   return CC_OK;
 }
 
-static bool is_coord(uint32_t type) { return type == CC_RES_LOCK || type == CC_RES_ELECTION || type == CC_RES_GROUP; }
+static bool is_coord(uint32_t type) {
+  return type == CC_RES_LOCK || type == CC_RES_ELECTION || type == CC_RES_GROUP || type == CC_RES_QUEUE;
+}
 
 extern "C" int cc_abi_version(void) { return CC_ABI_VERSION; }
 extern "C" const char* cc_last_error(void) { return g_err.c_str(); }
@@ -426,7 +428,7 @@ static int quiesce(cc_engine* e) {
 
 static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
   if (is_keyed(type) && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map and set resources need cc_config.map_capacity > 0");
-  if (type < CC_RES_VALUE || type > CC_RES_SET) return set_err(CC_ERR_INVALID, "unknown resource type");
+  if (type < CC_RES_VALUE || type > CC_RES_QUEUE) return set_err(CC_ERR_INVALID, "unknown resource type");
   if (type == CC_RES_SET) e->has_sets = true;
   const uint64_t end = (uint64_t)first + count;
   if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");

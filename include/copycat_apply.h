@@ -53,6 +53,8 @@ extern "C" {
 #define CC_RES_ELECTION  4  /* LeaderElectionState coordination/.../state/LeaderElectionState.java:31 */
 #define CC_RES_GROUP     5  /* MembershipGroupState coordination/.../state/MembershipGroupState.java:33 */
 #define CC_RES_SET       6  /* SetState          collections/.../state/SetState.java:32 (shares the map table) */
+#define CC_RES_QUEUE     7  /* QueueState        collections/.../state/QueueState.java:33 (a FIFO of CC_QUEUE_CAP) */
+#define CC_QUEUE_CAP    64
 
 /* ---- op codes = Catalyst @SerializeWith ids of the inner operation ------------- */
 #define CC_OP_DELETE            1   /* ResourceStateMachine.DeleteCommand (no wire id) ResourceStateMachine.java:53 */
@@ -78,6 +80,17 @@ extern "C" {
 #define CC_OP_MAP_SIZE          71  /* query */
 #define CC_OP_MAP_CLEAR         72
 /* LeaderElectionCommands.java:80-99 */
+/* QueueState (collections/.../state/QueueCommands.java:133-235): the element travels in operand a */
+#define CC_OP_QUEUE_CONTAINS   90  /* query */
+#define CC_OP_QUEUE_ADD        91
+#define CC_OP_QUEUE_OFFER      92
+#define CC_OP_QUEUE_PEEK       93  /* query */
+#define CC_OP_QUEUE_POLL       94
+#define CC_OP_QUEUE_ELEMENT    95
+#define CC_OP_QUEUE_REMOVE     96  /* a = element, or NULL: remove the head */
+#define CC_OP_QUEUE_SIZE       97  /* query */
+#define CC_OP_QUEUE_ISEMPTY    98  /* query */
+#define CC_OP_QUEUE_CLEAR      99
 /* SetState (collections/.../state/SetCommands.java:133-238): the element travels in the key column (key tag in
  * CC_FLAGS), the ttl of Add in aux */
 #define CC_OP_SET_CONTAINS     100  /* query */
@@ -125,6 +138,7 @@ extern "C" {
 #define CC_ST_NULL_POINTER     5  /* NullPointerException in MapState.containsValue MapState.java:52 */
 #define CC_ST_TYPE_MISMATCH    6  /* ResourceManagerException "inconsistent resource type" ResourceManager.java:120,181 */
 #define CC_ST_UNKNOWN_RESOURCE 7  /* ResourceManagerException "unknown resource" ResourceManager.java:216 */
+#define CC_ST_NO_SUCH_ELEMENT  8  /* NoSuchElementException of ArrayDeque.element/remove() QueueState.java:113,144 */
 #define CC_STATUS(code, tag)   ((uint8_t)(((code) & 15u) | (((tag) & 15u) << 4)))
 #define CC_STATUS_CODE(s)      ((s) & 15u)
 #define CC_STATUS_TAG(s)       (((s) >> 4) & 15u)

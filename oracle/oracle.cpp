@@ -127,6 +127,7 @@ struct Resource {
   LockSM l;
   ElectionSM e;
   GroupSM g;
+  std::deque<TV> q;  // QueueState.queue: ArrayDeque of commits, here their values (QueueState.java:33)
 };
 
 struct Inst {  // ResourceManager.SessionHolder + ManagedResourceSession
@@ -271,6 +272,9 @@ struct orc {
     switch (r.type) {
       case CC_RES_VALUE:  // AtomicValueState.delete :146-157 (timer is always null, A2)
         if (r.v.has_current) { r.v.has_current = false; r.v.value = TV(); }
+        return CC_ST_OK;
+      case CC_RES_QUEUE:  // QueueState.delete :191-199
+        r.q.clear();
         return CC_ST_OK;
       case CC_RES_SET:  // SetState.delete :123-134 (same shape: cancel timers, clean, clear)
       case CC_RES_MAP: {  // MapState.delete :264-274
@@ -550,6 +554,67 @@ struct orc {
         }
         break;
       }
+      case CC_RES_QUEUE: {  // QueueState (collections/src/main/java/io/atomix/collections/state/QueueState.java)
+        auto& q = r.q;
+        auto first_match = [&](size_t& at) -> int {  // 1 match, 0 none, -1 NPE (a stored null's equals)
+          for (size_t i = 0; i < q.size(); ++i) {
+            if (tv_null(q[i])) return -1;
+            if (tv_equals(q[i], a)) { at = i; return 1; }
+          }
+          return 0;
+        };
+        switch (c.op) {
+          case CC_OP_QUEUE_CONTAINS: {  // contains :36-46
+            size_t at = 0;
+            int m = first_match(at);
+            if (m < 0) ret(CC_ST_NULL_POINTER, TV());
+            else ret(CC_ST_OK, tv(CC_TAG_BOOL, m ? 1 : 0));
+            return;
+          }
+          case CC_OP_QUEUE_ADD:    // add :51-59 (returns false)
+          case CC_OP_QUEUE_OFFER:  // offer :64-72 (returns false)
+            q.push_back(a);
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
+            return;
+          case CC_OP_QUEUE_PEEK:  // peek :77-87
+            ret(CC_ST_OK, q.empty() ? TV() : q.front());
+            return;
+          case CC_OP_QUEUE_POLL:  // poll :92-105
+            if (q.empty()) { ret(CC_ST_OK, TV()); return; }
+            ret(CC_ST_OK, q.front());
+            q.pop_front();
+            return;
+          case CC_OP_QUEUE_ELEMENT:  // element :111-124 — ArrayDeque.element throws when empty; does not remove
+            if (q.empty()) { ret(CC_ST_NO_SUCH_ELEMENT, TV()); return; }
+            ret(CC_ST_OK, q.front());
+            return;
+          case CC_OP_QUEUE_REMOVE: {  // remove :130-157
+            if (!tv_null(a)) {
+              size_t at = 0;
+              int m = first_match(at);
+              if (m < 0) { ret(CC_ST_NULL_POINTER, TV()); return; }
+              if (m) q.erase(q.begin() + (std::ptrdiff_t)at);
+              ret(CC_ST_OK, tv(CC_TAG_BOOL, m ? 1 : 0));
+              return;
+            }
+            if (q.empty()) { ret(CC_ST_NO_SUCH_ELEMENT, TV()); return; }  // ArrayDeque.remove()
+            ret(CC_ST_OK, q.front());
+            q.pop_front();
+            return;
+          }
+          case CC_OP_QUEUE_SIZE:  // size :162-168 (int)
+            ret(CC_ST_OK, tv(CC_TAG_INT, (uint64_t)(int64_t)(int32_t)q.size()));
+            return;
+          case CC_OP_QUEUE_ISEMPTY:  // isEmpty :173-179
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, q.empty() ? 1 : 0));
+            return;
+          case CC_OP_QUEUE_CLEAR:  // clear :184-190 -> delete()
+            q.clear();
+            ret(CC_ST_OK, TV());
+            return;
+        }
+        break;
+      }
       case CC_RES_SET: {  // SetState (collections/src/main/java/io/atomix/collections/state/SetState.java)
         MapSM& s = r.m;  // element -> Value{commit, timer}; the stored value is a Boolean TRUE marker
         MapKey k{ktag_to_tag(CC_FLAG_KTAG(c.flags)), c.key};
@@ -745,7 +810,7 @@ orc* orc_create(uint32_t max_resources, uint32_t max_instances, uint32_t flags) 
 void orc_destroy(orc* o) { delete o; }
 
 int orc_resource_create(orc* o, uint32_t slot, uint32_t type) {
-  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_SET || o->res[slot].exists) return CC_ERR_INVALID;
+  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_QUEUE || o->res[slot].exists) return CC_ERR_INVALID;
   o->init_resource(slot, type, slot);
   return CC_OK;
 }

@@ -362,6 +362,51 @@ def kats():
                .c(0, "MAP_PUT", key=foo, a=hw, aux=100, time=0)
                .c(0, "MAP_GET", key=foo, expect=hw, time=100)
                .c(0, "MAP_GET", key=foo, expect=NULL, time=100))
+    QT = "collections/src/test/java/io/atomix/collections/DistributedQueueTest.java"
+
+    def queue_kat(name, lines):
+        return K(name, "reference", f"{QT}:{lines}").res(0, "QUEUE").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+
+    out.append(queue_kat("queue_offer_poll", "41-65")
+               .c(0, "QUEUE_OFFER", a=hw, expect=B(False))
+               .c(1, "QUEUE_SIZE", expect=I(1))
+               .c(1, "QUEUE_POLL", expect=hw)
+               .c(1, "QUEUE_ISEMPTY", expect=B(True)))
+    out.append(queue_kat("queue_offer_remove", "70-94")
+               .c(0, "QUEUE_OFFER", a=hw, expect=B(False))
+               .c(1, "QUEUE_SIZE", expect=I(1))
+               .c(1, "QUEUE_REMOVE", expect=hw)  # remove() with no element: the head (QueueState.java:143-152)
+               .c(1, "QUEUE_ISEMPTY", expect=B(True)))
+    out.append(queue_kat("queue_offer_peek", "99-123")
+               .c(0, "QUEUE_OFFER", a=hw, expect=B(False))
+               .c(1, "QUEUE_SIZE", expect=I(1))
+               .c(1, "QUEUE_PEEK", expect=hw)
+               .c(1, "QUEUE_ISEMPTY", expect=B(False)))
+    out.append(queue_kat("queue_offer_element", "128-152")
+               .c(0, "QUEUE_OFFER", a=hw, expect=B(False))
+               .c(1, "QUEUE_SIZE", expect=I(1))
+               .c(1, "QUEUE_ELEMENT", expect=hw)
+               .c(1, "QUEUE_ISEMPTY", expect=B(False)))
+    out.append(queue_kat("queue_add_remove", "158-176")
+               .c(0, "QUEUE_CONTAINS", a=hw, expect=B(False))
+               .c(1, "QUEUE_CONTAINS", a=hw, expect=B(False))
+               .c(0, "QUEUE_ADD", a=hw, expect=B(False))
+               .c(0, "QUEUE_CONTAINS", a=hw, expect=B(True))
+               .c(1, "QUEUE_CONTAINS", a=hw, expect=B(True))
+               .c(1, "QUEUE_REMOVE", a=hw, expect=B(True))
+               .c(0, "QUEUE_CONTAINS", a=hw, expect=B(False))
+               .c(1, "QUEUE_CONTAINS", a=hw, expect=B(False)))
+    k = K("queue_null_and_empty_quirks", "defined", "collections/src/main/java/io/atomix/collections/state/QueueState.java:36-157")
+    out.append(k.res(0, "QUEUE").inst(0, 0, 100, 1)
+               .c(0, "QUEUE_ELEMENT", status="NO_SUCH_ELEMENT")   # ArrayDeque.element on empty throws
+               .c(0, "QUEUE_REMOVE", status="NO_SUCH_ELEMENT")    # ArrayDeque.remove() on empty throws
+               .c(0, "QUEUE_POLL", expect=NULL)
+               .c(0, "QUEUE_ADD", a=NULL, expect=B(False))       # a null value is stored (the commit is the element)
+               .c(0, "QUEUE_ADD", a=foo, expect=B(False))
+               .c(0, "QUEUE_CONTAINS", a=foo, status="NULL_POINTER")  # the stored null's equals NPEs first
+               .c(0, "QUEUE_POLL", expect=NULL)
+               .c(0, "QUEUE_CONTAINS", a=foo, expect=B(True))
+               .c(0, "QUEUE_SIZE", expect=I(1)))
     SETT = "collections/src/test/java/io/atomix/collections/DistributedSetTest.java"
     # two clients, one set: contains false, add, contains true (both), remove, contains false (both)
     out.append(K("set_add_remove", "reference", f"{SETT}:42-58").res(0, "SET").inst(0, 0, 100, 1).inst(1, 0, 101, 2)

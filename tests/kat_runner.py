@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 KAT_PATH = os.path.join(HERE, "golden", "kats.json")
 
 RES = {"VALUE": abi.CC_RES_VALUE, "MAP": abi.CC_RES_MAP, "LOCK": abi.CC_RES_LOCK, "ELECTION": abi.CC_RES_ELECTION,
-       "GROUP": abi.CC_RES_GROUP, "SET": abi.CC_RES_SET}
+       "GROUP": abi.CC_RES_GROUP, "SET": abi.CC_RES_SET, "QUEUE": abi.CC_RES_QUEUE}
 TAG = {"NULL": abi.CC_TAG_NULL, "LONG": abi.CC_TAG_LONG, "INT": abi.CC_TAG_INT, "BOOL": abi.CC_TAG_BOOL,
        "H": abi.CC_TAG_HANDLE, "SET": abi.CC_TAG_SET}
 EV = {"CHANGE": abi.CC_EV_CHANGE, "LOCK": abi.CC_EV_LOCK, "ELECT": abi.CC_EV_ELECT, "JOIN": abi.CC_EV_JOIN,
@@ -24,7 +24,7 @@ EV = {"CHANGE": abi.CC_EV_CHANGE, "LOCK": abi.CC_EV_LOCK, "ELECT": abi.CC_EV_ELE
 ST = {"OK": abi.CC_ST_OK, "UNKNOWN_SESSION": abi.CC_ST_UNKNOWN_SESSION, "UNKNOWN_OP": abi.CC_ST_UNKNOWN_OP,
       "ILLEGAL_STATE": abi.CC_ST_ILLEGAL_STATE, "ILLEGAL_ARGUMENT": abi.CC_ST_ILLEGAL_ARGUMENT,
       "NULL_POINTER": abi.CC_ST_NULL_POINTER, "TYPE_MISMATCH": abi.CC_ST_TYPE_MISMATCH,
-      "UNKNOWN_RESOURCE": abi.CC_ST_UNKNOWN_RESOURCE}
+      "UNKNOWN_RESOURCE": abi.CC_ST_UNKNOWN_RESOURCE, "NO_SUCH_ELEMENT": abi.CC_ST_NO_SUCH_ELEMENT}
 
 
 def load():
@@ -55,6 +55,8 @@ GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_
                "MAP_REMOVEIFPRESENT", "MAP_REPLACE", "MAP_REPLACEIFPRESENT", "MAP_CONTAINSVALUE", "MAP_SIZE",
                "MAP_ISEMPTY", "MAP_CLEAR"}
 GPU_SET_OPS = {"SET_CONTAINS", "SET_ADD", "SET_REMOVE", "SET_SIZE", "SET_ISEMPTY", "SET_CLEAR"}
+GPU_QUEUE_OPS = {"QUEUE_CONTAINS", "QUEUE_ADD", "QUEUE_OFFER", "QUEUE_PEEK", "QUEUE_POLL", "QUEUE_ELEMENT", "QUEUE_REMOVE",
+                 "QUEUE_SIZE", "QUEUE_ISEMPTY", "QUEUE_CLEAR"}
 
 
 def gpu_eligible(kat):
@@ -62,14 +64,14 @@ def gpu_eligible(kat):
     every Map and Set op (TTL timers included), lock / election / group ops, Delete, and clock advances;
     no registry control or session-close steps (host control plane)."""
     types = {r[1] for r in kat["resources"]}
-    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET"}:
+    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET", "QUEUE"}:
         return False
     for s in kat["steps"]:
         if "control" in s or "close" in s:
             return False
         if "commit" in s:
             c = s["commit"]
-            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS | GPU_SET_OPS:
+            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS | GPU_SET_OPS | GPU_QUEUE_OPS:
                 return False
     return True
 
