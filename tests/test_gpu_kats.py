@@ -16,8 +16,9 @@ def test_gpu_kat_coverage():
             "lock_delete_then_unlock_commit_closed", "A9_leader_relisten_appended", "map_contains_value", "map_size",
             "map_clear", "map_put_ttl", "map_put_if_absent_ttl", "A5_contains_value_npe_order",
             "A8_timer_deferred_after_commit", "A8_timer_immediate_module_mode", "set_add_remove",
-            "set_ttl_size_clear"} <= names
-    assert len(KATS) >= 36
+            "set_ttl_size_clear", "group_schedule_fires_on_clock", "dispatch_errors", "queue_offer_poll",
+            "queue_add_remove", "queue_null_and_empty_quirks"} <= names
+    assert len(KATS) >= 44
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
