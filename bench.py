@@ -23,6 +23,11 @@ block on the host, uploaded once); algorithmic bytes 34.6 B/commit (SURVEY §8(d
 --workload c4 (BASELINE.json configs[3]): leader quorum commit index for 1,048,576 5-replica Raft groups plus
 the session expiry sweep over 1,048,576 sessions; a step = one aggregation + one sweep; value = (groups +
 sessions) / s; algorithmic bytes 64 B/group and 8.125 B/session.
+
+--workload c5: mixed coordination -- 32,768 resources per GPU (262,144 over 8), a third each LockState,
+LeaderElectionState and MembershipGroupState, one instance each; 100M committed lock/unlock (timeouts -1/0/>0),
+listen/unlisten/isLeader and join/leave entries per step from the parity-test generator, applied with the
+ordered event stream in HBM; algorithmic bytes 48 B/op (26 in, 9 out, ~1 event of 13 B).
 """
 import argparse
 import json
@@ -40,6 +45,7 @@ import torch  # noqa: E402
 METRIC = "committed ops applied/sec (1 and 8 GPUs) + % of HBM GB/s roofline"
 B_OP_C2 = 39  # index 8 + res 4 + op 1 + flags 1 + expect 8 + update 8 in, status 1 + value 8 out
 B_OP_C3 = 34.6  # put 30 in / get, remove 22 in; 9 out; weighted by the 45/45/10 mix
+B_OP_C5 = 48  # 26 in + 9 out + ~1 event x 13 B
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -184,12 +190,112 @@ def run_c4(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
+def run_c5(args, dev, rank, world, dist):
+    """Mixed coordination through cc_apply_batch with the event stream."""
+    from copycat_amd import abi
+    from copycat_amd.engine import DeviceBatch, DeviceEvents, Engine
+    from copycat_amd.workload import coord_random_stream
+
+    n = args.commits or 100_000_000
+    R = args.resources or 262_144 // 8  # SURVEY c5: 262,144 resources sharded res % 8 -> 32,768 per GPU
+    third = (R + 2) // 3  # type-major slots: locks, then elections, then groups
+    types = np.repeat(np.array([abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP], np.uint8), third)[:R]
+    t_gen = time.time()
+    batch = coord_random_stream(n, types, 1, R, seed=0xA700000 + 5 + rank)
+    db = DeviceBatch.upload(batch, device=dev)
+    t_gen = time.time() - t_gen
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    value = torch.zeros(n, dtype=torch.int64, device=dev)
+    evs = DeviceEvents(2 * n, device=dev)
+    flags = abi.CC_CFG_TIMERS_DEFERRED
+    E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
+    for k, t in enumerate((abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP)):
+        E.resource_create_range(k * third, min(third, R - k * third), int(t))
+    E.instance_open_range(0, R, 0, 1000, 1 + rank)
+    stream = torch.cuda.current_stream(dev)
+    wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
+    wm_local = db.cols["index"][n - 1:n].view(torch.int64)
+
+    def step():
+        E.apply_events(db, status, value, evs, stream=stream)
+        if dist is not None:
+            dist.all_gather_into_tensor(wm_all, wm_local)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if not args.no_profile:
+        E.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    E.sync()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = E.profile_read() if not args.no_profile else {}
+    n_events = int(evs.count.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    roofline = None
+    if prof:
+        dom = max(prof, key=lambda k: prof[k][0])
+        ms_tot, launches = prof[dom]
+        commits_per_launch = n * args.steps / max(launches, 1)
+        avg_ms = ms_tot / max(launches, 1)
+        achieved = B_OP_C5 * commits_per_launch / (avg_ms * 1e-3) / 1e9
+        roofline = {
+            "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c5"),
+            "alg_gb_per_launch": round(B_OP_C5 * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
+            "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
+            "bytes_per_commit": B_OP_C5,
+            "pipeline_frac": round(B_OP_C5 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        }
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.oracle_py import Oracle
+
+        m = min(n, args.cpu_sample or 10_000_000)
+        O = Oracle(R, R, flags)
+        for r in range(R):
+            O.resource_create(r, int(types[r]))
+            O.instance_open(r, r, 1000 + r, 1)
+        tc = time.perf_counter()
+        O.apply(batch.slice(0, m))
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+               "sample": f"first {m:,} commits of the same c5 stream (events included), C++ restatement of the Java "
+                         f"apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": f"c5: mixed coordination (lock / election / group, a third each) over {R:,} resources, "
+                                   f"{n:,} committed entries per GPU with the ordered event stream",
+                       "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
+                       "events_per_step": n_events, "gen_s": round(t_gen, 2)},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("c2", "c3", "c4"), default="c2")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2")
     ap.add_argument("--commits", type=int, default=0, help="default: 100M (c2), 1e9 (c3)")
     ap.add_argument("--resources", type=int, default=0, help="default: 65536 resources (c2), 4096 maps (c3)")
     ap.add_argument("--pairs", type=int, default=1 << 20, help="c3: distinct (map, key) pairs")
@@ -219,6 +325,8 @@ def main():
 
     if args.workload == "c4":
         return run_c4(args, dev, rank, world, dist)
+    if args.workload == "c5":
+        return run_c5(args, dev, rank, world, dist)
 
     c3 = args.workload == "c3"
     n = args.commits or (1_000_000_000 if c3 else 100_000_000)
