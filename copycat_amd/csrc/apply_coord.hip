@@ -29,8 +29,8 @@
 namespace cc {
 
 constexpr int kCT = 256;            // threads = slots per super-bucket
-constexpr int kCPer = 4;            // commits per thread per chunk
-constexpr int kCCh = kCT * kCPer;   // 1024
+constexpr int kCPer = 8;            // commits per thread per chunk (2048: fewer chunk barriers; 146 KB LDS)
+constexpr int kCCh = kCT * kCPer;   // 2048
 constexpr int kEvBuf = 2048;        // LDS event buffer per chunk
 
 struct Emitter {
