@@ -17,7 +17,10 @@ constexpr int kMaxSbTotal = kMaxSb + kMaxMapSb;
 constexpr int kPT = 1024;                 // partition workgroup threads (16 waves)
 constexpr int kPW = kPT / kWave;
 constexpr int kTile = 16384;              // commits per partition tile (one workgroup)
-constexpr int kChunk = 4096;              // commits per LDS-staged chunk of a tile (value-only engines)
+#ifndef CC_PART_CHUNK
+#define CC_PART_CHUNK 4096
+#endif
+constexpr int kChunk = CC_PART_CHUNK;              // commits per LDS-staged chunk of a tile (value-only engines)
 constexpr int kChunkMaps = 2048;          // ... when map commits (bigger records) share the partition
 constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan (1024-thread WG)
 constexpr int kMaxTiles = 1024;           // tiles per sub-batch => sub-batch <= 16M commits

@@ -138,8 +138,11 @@ size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk) {
 // Super-bucket of a commit: value resources by slot (slot >> 8); map commits by hash(map, key tag, key) into
 // the map regions that follow the value super-buckets; commits of a hot key (apply_map_hot.hip) into that
 // key's own bucket after the regions.
+#ifndef CC_PART_WPE
+#define CC_PART_WPE 4  // waves per SIMD one 1024-thread workgroup needs
+#endif
 template <int J, bool EXT>
-__global__ __launch_bounds__(kPT) void k_part_tile(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+__global__ __launch_bounds__(kPT, CC_PART_WPE) void k_part_tile(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                 const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
                                                 const uint64_t* __restrict__ cidx, const uint64_t* __restrict__ caux,
