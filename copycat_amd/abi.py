@@ -103,6 +103,7 @@ CC_EVSRC_RESULT = 3
 
 CC_CFG_TIMERS_DEFERRED = 1
 CC_CFG_VALUE_EVENTS = 2
+CC_CFG_VALUE_RETAINED = 4
 CC_LOCK_QUEUE = 64
 CC_ELECTION_LISTENERS = 64
 CC_GROUP_MEMBERS = 64

@@ -62,6 +62,8 @@ struct cc_engine {
   uint8_t* d_res_type = nullptr;
   uint32_t* d_val_meta = nullptr;
   uint64_t* d_val_v = nullptr;
+  uint64_t* d_val_live = nullptr;             // [slots] retained value commit index (CC_CFG_VALUE_RETAINED)
+  unsigned long long* d_val_wrow = nullptr;   // [slots] last writer row + 1 of the current batch
   // workspace
   uint32_t* d_st_meta = nullptr;
   u64x2* d_st_ab = nullptr;
@@ -189,7 +191,7 @@ static void free_all(cc_engine* e) {
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
-                  e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen};
+                  e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -292,6 +294,10 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_res_type, slots);
   ALLOC(e->d_val_meta, sizeof(uint32_t) * slots);
   ALLOC(e->d_val_v, sizeof(uint64_t) * slots);
+  if (cfg->flags & CC_CFG_VALUE_RETAINED) {
+    ALLOC(e->d_val_live, sizeof(uint64_t) * slots);
+    ALLOC(e->d_val_wrow, sizeof(unsigned long long) * slots);
+  }
   ALLOC(e->d_st_meta, sizeof(uint32_t) * (e->sub_batch + kPT));  // + dummy rows for unconditional stores
   ALLOC(e->d_st_ab, sizeof(u64x2) * (e->sub_batch + kPT));
   ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
@@ -333,6 +339,10 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if ((he = hipMemset(e->d_res_type, 0, slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_val_meta, 0, sizeof(uint32_t) * slots)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_val_v, 0, sizeof(uint64_t) * slots)) != hipSuccess) return fail("memset", he);
+  if (e->d_val_live) {
+    if ((he = hipMemset(e->d_val_live, 0, sizeof(uint64_t) * slots)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_val_wrow, 0, sizeof(unsigned long long) * slots)) != hipSuccess) return fail("memset", he);
+  }
   if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_sb_kind, 0, e->sb)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_clock, 0, sizeof(uint64_t))) != hipSuccess) return fail("memset", he);
@@ -453,6 +463,7 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   // fresh state: AtomicValueState() {value = null; current = null}
   HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
   HIPCHECK(hipMemset(e->d_val_v + first, 0, sizeof(uint64_t) * count));
+  if (e->d_val_live) HIPCHECK(hipMemset(e->d_val_live + first, 0, sizeof(uint64_t) * count));
   return CC_OK;
 }
 
@@ -485,6 +496,7 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
   HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(e->d_val_v + slot, 0, sizeof(uint64_t)));
+  if (e->d_val_live) HIPCHECK(hipMemset(e->d_val_live + slot, 0, sizeof(uint64_t)));
   const uint32_t none = kNoRes;
   for (uint32_t i = 0; i < e->cfg.max_instances; ++i)
     if (e->inst_res[i] == slot) {
@@ -904,6 +916,12 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if (e->has_sets && launch_set_results(c->inst, c->op, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, out->status,
                                         out->value, st))
     return set_err(CC_ERR_HIP, "set results launch", hipGetLastError());
+  if (e->d_val_live) {  // retained value commits (live.hip): after every value op of the batch has applied
+    if (!c->index) return set_err(CC_ERR_INVALID, "CC_CFG_VALUE_RETAINED needs the index column");
+    if (launch_value_live(c->inst, c->op, out->status, out->value, c->index, n, e->d_inst_res, e->d_res_type,
+                          e->cfg.max_instances, e->d_val_meta, e->cfg.max_resources, e->d_val_wrow, e->d_val_live, st))
+      return set_err(CC_ERR_HIP, "retained value launch", hipGetLastError());
+  }
   if (e->coord_on && ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   if (e->coord_on || e->map_bits) {  // the log clock (timers: lock timeouts, map TTL)
     if (launch_clock_advance(c->time, n, 0, e->d_clock, st)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
@@ -1155,6 +1173,15 @@ extern "C" int cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count,
   return CC_OK;
 }
 
+extern "C" int cc_read_value_retained(cc_engine* e, uint32_t first, uint32_t count, uint64_t* h_index) {
+  if (!e || !h_index || (uint64_t)first + count > e->cfg.max_resources) return set_err(CC_ERR_INVALID, "range");
+  if (!e->d_val_live) return set_err(CC_ERR_INVALID, "engine created without CC_CFG_VALUE_RETAINED");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  HIPCHECK(hipMemcpy(h_index, e->d_val_live + first, sizeof(uint64_t) * count, hipMemcpyDeviceToHost));
+  return CC_OK;
+}
+
 extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag,
                                    uint64_t* h_key, uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index) {
   if (!e || !count || slot >= e->cfg.max_resources || !is_keyed(e->res_type[slot]))
@@ -1334,6 +1361,7 @@ static std::vector<Section> snap_sections(cc_engine* e) {
       {e->d_inst_id, nullptr, 8 * mi},
       {e->d_clock, nullptr, 8},
   };
+  if (e->d_val_live) v.push_back({e->d_val_live, nullptr, 8 * slots});
   if (e->map_bits) {
     const uint64_t n = e->map_entries;
     v.push_back({e->d_tbl_key, nullptr, 8 * n});

@@ -142,6 +142,10 @@ int launch_group_schedule(const uint8_t* coord, uint32_t slot, uint64_t member, 
 int launch_group_fire(const uint8_t* coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
                       unsigned long long* ev_total, const cc_events* ev, uint32_t* err, hipStream_t st);
 // SetState result rewrite after the batch (map_wide.hip)
+int launch_value_live(const uint32_t* inst, const uint8_t* op, const uint8_t* status, const uint64_t* value,
+                      const uint64_t* index, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
+                      uint32_t max_inst, const uint32_t* val_meta, uint32_t slots, unsigned long long* wrow,
+                      uint64_t* live, hipStream_t st);
 int launch_set_results(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
                        uint32_t max_inst, uint8_t* status, uint64_t* value, hipStream_t st);
 

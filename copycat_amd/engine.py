@@ -53,6 +53,7 @@ def lib():
             "cc_apply_batch_host": (i32, [P, P, u64, P]),
             "cc_applied_index": (i32, [P, P]),
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
+            "cc_read_value_retained": (i32, [P, u32, u32, P]),
             "cc_read_map_entries": (i32, [P, u32, u64, P, P, P, P, P, P]),
             "cc_read_lock_state": (i32, [P, u32, P, P, P, u64, P, P, P]),
             "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
@@ -264,6 +265,13 @@ class Engine:
         tag, val, cur = np.zeros(count, np.uint8), np.zeros(count, np.uint64), np.zeros(count, np.uint8)
         _check(self.L.cc_read_value_state(self.h, first, count, _np(tag), _np(val), _np(cur)))
         return tag, val, cur
+
+    def value_retained(self, first=0, count=None):
+        """Per value slot, the log index of the commit AtomicValueState still retains (0 = none)."""
+        count = self.max_resources - first if count is None else count
+        idx = np.zeros(count, np.uint64)
+        _check(self.L.cc_read_value_retained(self.h, first, count, _np(idx)))
+        return idx
 
     def advance_time(self, now):
         _check(self.L.cc_advance_time(self.h, now))

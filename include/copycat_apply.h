@@ -177,6 +177,8 @@ typedef struct cc_config {
 
 #define CC_CFG_TIMERS_DEFERRED 1u  /* manager-mode timer order (A8): due timers fire after the commit
                                       that advanced time (ResourceManagerStateMachineExecutor.java:104-109) */
+#define CC_CFG_VALUE_RETAINED  4u  /* keep, per AtomicValue slot, the log index of the commit the state machine
+                                      still retains (`current`, never clean()ed): cc_read_value_retained  */
 #define CC_CFG_VALUE_EVENTS    2u  /* AtomicValue Listen/Unlisten + "change" events on the GPU (every value
                                       resource then runs on the event-capable kernel)              */
 
@@ -281,6 +283,9 @@ int  cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t size);
 /* AtomicValueState {value, current != null} for slots [first, first+count) (AtomicValueState.java:34-35) */
 int  cc_read_value_state(cc_engine* e, uint32_t first, uint32_t count, uint8_t* h_tag, uint64_t* h_value,
                          uint8_t* h_has_current);
+/* Log compaction (Commit.clean(), AtomicValueState.java:88-157): per value slot in [first, first+count), the
+ * index of the one commit still retained (`current`), 0 if none.  Needs CC_CFG_VALUE_RETAINED.          */
+int  cc_read_value_retained(cc_engine* e, uint32_t first, uint32_t count, uint64_t* h_index);
 /* MapState.map of one map slot (MapState.java:33): *count = live entries; the first min(cap, count), sorted
  * by (key tag, key), go to the arrays (key tag as a CC_TAG_*; commit_index may be NULL).               */
 int  cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag, uint64_t* h_key,

@@ -1012,6 +1012,16 @@ int orc_read_value_state(orc* o, uint32_t first, uint32_t count, uint8_t* tag, u
   return CC_OK;
 }
 
+// retained value commit (AtomicValueState.current, never clean()ed: :88-157), 0 if none
+int orc_read_value_retained(orc* o, uint32_t first, uint32_t count, uint64_t* index) {
+  if ((uint64_t)first + count > o->max_res) return CC_ERR_INVALID;
+  for (uint32_t i = 0; i < count; ++i) {
+    const Resource& r = o->res[first + i];
+    index[i] = r.exists && r.type == CC_RES_VALUE && r.v.has_current ? r.v.current.index : 0;
+  }
+  return CC_OK;
+}
+
 int64_t orc_map_size(orc* o, uint32_t res) {
   if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET)) return -1;
   return (int64_t)o->res[res].m.m.size();

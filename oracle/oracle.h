@@ -74,6 +74,7 @@ void orc_aux_read(orc* o, uint32_t* pos, uint64_t* member);
 void orc_aux_clear(orc* o);
 
 /* state readback */
+int  orc_read_value_retained(orc* o, uint32_t first, uint32_t count, uint64_t* index);
 int  orc_read_value_state(orc* o, uint32_t first, uint32_t count, uint8_t* tag, uint64_t* value,
                           uint8_t* has_current);
 int64_t orc_map_size(orc* o, uint32_t res);

@@ -56,6 +56,7 @@ def lib():
             "orc_aux_read": (None, [P, P, P]),
             "orc_aux_clear": (None, [P]),
             "orc_read_value_state": (i32, [P, u32, u32, P, P, P]),
+            "orc_read_value_retained": (i32, [P, u32, u32, P]),
             "orc_map_size": (i64, [P, u32]),
             "orc_map_entries": (i64, [P, u32, u64, P, P, P, P, P]),
             "orc_lock_state": (i64, [P, u32, P, P, P, u64, P, P]),
@@ -185,6 +186,12 @@ class Oracle:
         rc = self.L.orc_read_value_state(self.h, first, count, _p(tag), _p(val), _p(cur))
         assert rc == 0
         return tag, val, cur
+
+    def value_retained(self, first=0, count=None):
+        count = self.max_resources - first if count is None else count
+        idx = np.zeros(count, np.uint64)
+        assert self.L.orc_read_value_retained(self.h, first, count, _p(idx)) == 0
+        return idx
 
     def map_entries(self, res):
         n = self.L.orc_map_size(self.h, res)
