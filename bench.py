@@ -304,6 +304,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=0, help="default: 100M (c2), 20M (c3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--retained", action="store_true", help="c2: also keep the retained value commit per slot (CC_CFG_VALUE_RETAINED)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -347,7 +348,8 @@ def main():
         E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, map_capacity=args.pairs)
         E.resource_create_range(0, R, abi.CC_RES_MAP)
     else:
-        E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch)
+        E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch,
+                   flags=abi.CC_CFG_TIMERS_DEFERRED | (abi.CC_CFG_VALUE_RETAINED if args.retained else 0))
         E.resource_create_range(0, R, abi.CC_RES_VALUE)
     E.instance_open_range(0, R, 0, 1 + rank, 1 + rank)
     stream = torch.cuda.current_stream(dev)

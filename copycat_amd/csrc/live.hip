@@ -5,7 +5,8 @@
 // the time its successor applies, and delete() cleans `current` (:146-157).  So after a batch the retained
 // commit of a value slot is: none if the slot has no current (val_meta bit 8, cleared by Delete), else the
 // batch's last successful writer on that slot, else the retained commit from before the batch.
-//   k_live_mark : per row, atomicMax(row + 1) into wrow[slot] for successful writers (one pass, 7 B/row).
+//   k_live_mark : per row, atomicMax(row + 1) into wrow[slot] for successful writers (one pass, 7 B/row + the
+//                 inst_res / res_type gathers; CAS rows also read their 8 B result).
 //   k_live_fold : per value slot, resolve wrow against has_current and index[], then clear wrow.
 #include "engine_internal.h"
 
@@ -15,7 +16,11 @@ __global__ void k_live_mark(const uint32_t* __restrict__ inst, const uint8_t* __
                             const uint8_t* __restrict__ status, const uint64_t* __restrict__ value, uint64_t n,
                             const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
                             uint32_t max_inst, unsigned long long* __restrict__ wrow) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+  // Rows are walked from the end of the batch (grid-stride, descending) and a slot whose recorded row is already
+  // later is skipped with a plain load: wrow only grows, so a stale (cached) read can only under-state it and a skip
+  // is always safe.  After the first sweep nearly every slot holds a late row, so few rows reach the atomic.
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = n - 1 - k;
     const uint8_t o = op[i];
     if (o != CC_OP_VALUE_SET && o != CC_OP_VALUE_CAS && o != CC_OP_VALUE_GETANDSET) continue;
     if (CC_STATUS_CODE(status[i]) != CC_ST_OK) continue;
@@ -24,6 +29,7 @@ __global__ void k_live_mark(const uint32_t* __restrict__ inst, const uint8_t* __
     if (in >= max_inst) continue;
     const uint32_t s = inst_res[in];
     if (s == kNoRes || res_type[s] != CC_RES_VALUE) continue;
+    if (__builtin_nontemporal_load(&wrow[s]) > i) continue;
     atomicMax(&wrow[s], (unsigned long long)(i + 1));
   }
 }
