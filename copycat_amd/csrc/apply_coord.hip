@@ -87,6 +87,7 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
   auto ev = [&](uint32_t target, uint32_t code, uint32_t tag, uint64_t payload) {
     em.emit(r.g, nev++, target, code, CC_EVSRC_COMMIT, tag, payload);
   };
+  if (h.flags & kCoZombie) return CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
   if (!op_registered(type, r.op)) return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
   switch (type) {
     case CC_RES_LOCK: {

@@ -18,9 +18,9 @@
 //
 // engine.hip turns the closing client sessions into the ordered list of instance slots (client order, then the
 // Java HashMap order of ResourceManager.sessions) and groups the list positions by resource.  Then:
-//   k_close_check   : one thread per position: the first position whose close throws (an election whose
-//                     cleaned leader commit belongs to that instance — a cleaned leader can never be replaced,
-//                     so the pre-state decides); the reference's loop stops there;
+//   k_close_check   : one thread per position: per client, the first position whose close throws (an election
+//                     whose cleaned leader commit belongs to that instance — a cleaned leader can never be
+//                     replaced, so the pre-state decides); that client's ResourceManager.close loop stops there;
 //   k_close_apply   : one thread per resource: its closes in fan-out order, positions before the stop; events
 //                     to the arena tagged (position, emission index), per-position event counts;
 //   k_close_scan    : one workgroup: exclusive scan of the per-position counts, capacity checks;
@@ -33,29 +33,31 @@ namespace cc {
 
 __global__ void k_close_check(const uint32_t* __restrict__ cinst, uint32_t m, const uint32_t* __restrict__ inst_res,
                               const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ coord,
-                              uint32_t* __restrict__ fail) {
+                              const uint32_t* __restrict__ pcl, uint32_t* __restrict__ fail) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m || !coord) return;
   const uint32_t islot = cinst[p], r = inst_res[islot];
   if (r == kNoRes || res_type[r] != CC_RES_ELECTION) return;
   const CoordHdr h = *reinterpret_cast<const CoordHdr*>(coord + (uint64_t)r * kCoordBlock);
-  if ((h.flags & kCoHeld) && (h.flags & kCoCleaned) && h.who == islot) atomicMin(fail, p);
+  if (h.flags & kCoZombie) return;  // not in ResourceManager.resources: no close handler runs
+  if ((h.flags & kCoHeld) && (h.flags & kCoCleaned) && h.who == islot) atomicMin(&fail[pcl[p]], p);
 }
 
 __global__ void k_close_apply(const uint32_t* __restrict__ cinst, const uint32_t* __restrict__ rlist,
                               const uint32_t* __restrict__ rstart, const uint32_t* __restrict__ items, uint32_t nr,
-                              const uint32_t* __restrict__ fail, const uint8_t* __restrict__ res_type,
+                              const uint32_t* __restrict__ pcl, const uint32_t* __restrict__ fail,
+                              const uint8_t* __restrict__ res_type,
                               const uint64_t* __restrict__ inst_id, uint8_t* __restrict__ coord, uint32_t* __restrict__ cnt,
                               EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n, uint64_t arena_cap) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nr) return;
-  const uint32_t r = rlist[k], type = res_type[r], stop = *fail;
+  const uint32_t r = rlist[k], type = res_type[r];
   uint8_t* blk = coord + (uint64_t)r * kCoordBlock;
   CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
   CoordEnt* E = reinterpret_cast<CoordEnt*>(blk + sizeof(CoordHdr));
   for (uint32_t q = rstart[k]; q < rstart[k + 1]; ++q) {
     const uint32_t p = items[q];
-    if (p >= stop) break;  // positions ascend: the reference's loop ended before this close
+    if (p >= fail[pcl[p]]) continue;  // this client's ResourceManager.close loop ended before this close
     const uint32_t islot = cinst[p];
     const uint64_t iid = inst_id[islot];
     uint32_t nev = 0;
@@ -121,19 +123,19 @@ __global__ void k_close_apply(const uint32_t* __restrict__ cinst, const uint32_t
 
 // exclusive scan of cnt[0, min(m, stop)) -> off[0..m]; the event count; capacity checks
 constexpr int kCS = 1024;
-__global__ __launch_bounds__(kCS) void k_close_scan(const uint32_t* __restrict__ cnt, uint32_t m, const uint32_t* __restrict__ fail,
+__global__ __launch_bounds__(kCS) void k_close_scan(const uint32_t* __restrict__ cnt, uint32_t m,
+                                                    const uint32_t* __restrict__ pcl, const uint32_t* __restrict__ fail,
                                                     uint64_t* __restrict__ off, const unsigned long long* __restrict__ arena_n,
                                                     uint64_t arena_cap, uint64_t out_cap, int has_out,
                                                     uint64_t* __restrict__ out_count, uint32_t* __restrict__ err_out) {
   __shared__ unsigned long long wsum[kCS / kWave];
   __shared__ unsigned long long carry;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  const uint32_t lim = *fail < m ? *fail : m;
   if (t == 0) carry = 0;
   __syncthreads();
   for (uint32_t b = 0; b < m; b += kCS) {
     const uint32_t p = b + t;
-    const unsigned long long v = p < lim ? cnt[p] : 0ull;
+    const unsigned long long v = p < m && p < fail[pcl[p]] ? cnt[p] : 0ull;
     unsigned long long inc = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -180,25 +182,25 @@ __global__ void k_close_scatter(const EvRec* __restrict__ arena, const unsigned 
   }
 }
 
-__global__ void k_close_unreg(const uint32_t* __restrict__ cinst, uint32_t m, const uint32_t* __restrict__ fail,
-                              uint32_t* __restrict__ inst_res) {
+__global__ void k_close_unreg(const uint32_t* __restrict__ cinst, uint32_t m, const uint32_t* __restrict__ pcl,
+                              const uint32_t* __restrict__ fail, uint32_t* __restrict__ inst_res) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < m && p < *fail) inst_res[cinst[p]] = kNoRes;
+  if (p < m && p < fail[pcl[p]]) inst_res[cinst[p]] = kNoRes;
 }
 
 int launch_close(const CloseArgs& a, hipStream_t st) {
   if (a.m == 0) return 0;
   const uint32_t gm = (a.m + 255) / 256;
-  hipLaunchKernelGGL(k_close_check, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.inst_res, a.res_type, a.coord, a.fail);
+  hipLaunchKernelGGL(k_close_check, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.inst_res, a.res_type, a.coord, a.pcl, a.fail);
   if (a.nr && a.coord)
     hipLaunchKernelGGL(k_close_apply, dim3((a.nr + 63) / 64), dim3(64), 0, st, a.cinst, a.rlist, a.rstart, a.items, a.nr,
-                       a.fail, a.res_type, a.inst_id, a.coord, a.cnt, a.arena, a.arena_n, a.arena_cap);
-  hipLaunchKernelGGL(k_close_scan, dim3(1), dim3(kCS), 0, st, a.cnt, a.m, a.fail, a.off, a.arena_n, a.arena_cap, a.out_cap,
+                       a.pcl, a.fail, a.res_type, a.inst_id, a.coord, a.cnt, a.arena, a.arena_n, a.arena_cap);
+  hipLaunchKernelGGL(k_close_scan, dim3(1), dim3(kCS), 0, st, a.cnt, a.m, a.pcl, a.fail, a.off, a.arena_n, a.arena_cap, a.out_cap,
                      a.out_pos ? 1 : 0, a.out_count, a.err);
   if (a.out_pos)
     hipLaunchKernelGGL(k_close_scatter, dim3(256), dim3(256), 0, st, a.arena, a.arena_n, a.arena_cap, a.off, a.out_cap,
                        a.out_pos, a.out_target, a.out_code, a.out_src, a.out_tag, a.out_payload);
-  hipLaunchKernelGGL(k_close_unreg, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.fail, a.inst_res);
+  hipLaunchKernelGGL(k_close_unreg, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.pcl, a.fail, a.inst_res);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

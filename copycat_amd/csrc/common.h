@@ -192,6 +192,10 @@ struct CoordEnt {
   uint32_t pad;
 };
 constexpr uint32_t kCoHeld = 1u, kCoCleaned = 2u;
+// the resource was removed from ResourceManager.resources by a deleteResource whose delete() threw (a lock or
+// election whose holder commit was already cleaned): its instances stay registered and every commit on them hits
+// `resources.get(...) == null` -> NullPointerException (ResourceManager.java:62,71); close skips its handler
+constexpr uint32_t kCoZombie = 4u;
 constexpr uint64_t kNoDeadline = ~0ull;
 constexpr int kCoordCap = 64;  // CC_LOCK_QUEUE = CC_ELECTION_LISTENERS = CC_GROUP_MEMBERS = CC_VALUE_LISTENERS
 constexpr size_t kCoordBlock = sizeof(CoordHdr) + kCoordCap * sizeof(CoordEnt);

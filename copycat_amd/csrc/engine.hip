@@ -12,14 +12,13 @@
 #include <tuple>
 #include <vector>
 
-#include "common.h"
-#include "engine_internal.h"
+#include "engine_state.h"
 
 using namespace cc;
 
 static thread_local std::string g_err;
 
-static int set_err(int code, const char* what, hipError_t e = hipSuccess) {
+int cc::set_err(int code, const char* what, hipError_t e) {
   char buf[512];
   if (e != hipSuccess)
     snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
@@ -28,118 +27,6 @@ static int set_err(int code, const char* what, hipError_t e = hipSuccess) {
   g_err = buf;
   return code;
 }
-
-#define HIPCHECK(x)                                        \
-  do {                                                     \
-    hipError_t _e = (x);                                   \
-    if (_e != hipSuccess) return set_err(CC_ERR_HIP, #x, _e); \
-  } while (0)
-
-struct cc_engine {
-  cc_config cfg{};
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t last_stream = nullptr;
-  uint32_t sb = 0, sb_bits = 0;  // value super-buckets of 256 slots
-  uint32_t map_bits = 0;         // 2^map_bits map table regions follow them (0: no maps)
-  uint64_t map_entries = 0;
-  uint32_t sb_total() const { return sb + (map_bits ? (1u << map_bits) + kHotMax : 0u); }
-  uint64_t sub_batch = 0, max_tiles = 0;
-  // host mirrors of the registry
-  std::vector<uint8_t> res_type;     // [sb*256]
-  std::vector<uint32_t> inst_res;    // [max_inst]
-  std::vector<uint64_t> inst_id, inst_client;
-  // java.util.HashMap iteration order of ResourceManager.sessions (ResourceManager.java:37): bucket index under
-  // the table capacity (starts at 16, doubles when the size passes 3/4 of it, never shrinks), then insertion
-  // order within the bucket.  Used to order the close fan-out (ResourceManager.java:250-264).
-  uint32_t sess_cap = 16, sess_thr = 12, sess_size = 0;
-  uint64_t sess_next = 0;
-  std::vector<uint64_t> inst_seq;
-  // device registry + state
-  uint32_t* d_inst_res = nullptr;
-  uint16_t* d_inst_res16 = nullptr;  // value-only fast path (< 65535 resources, <= 65536 instances)
-  uint16_t* d_res16 = nullptr;       // [sub_batch] resolved resource per commit (same path)
-  uint8_t* d_res_type = nullptr;
-  uint32_t* d_val_meta = nullptr;
-  uint64_t* d_val_v = nullptr;
-  uint64_t* d_val_live = nullptr;             // [slots] retained value commit index (CC_CFG_VALUE_RETAINED)
-  unsigned long long* d_val_wrow = nullptr;   // [slots] last writer row + 1 of the current batch
-  // workspace
-  uint32_t* d_st_meta = nullptr;
-  u64x2* d_st_ab = nullptr;
-  uint16_t* d_cpos = nullptr;
-  uint16_t* d_ttab = nullptr;
-  uint8_t* d_rst_status = nullptr;
-  uint64_t* d_rst_value = nullptr;
-  uint32_t* d_err = nullptr;
-  // map table (apply_map.hip) + map staging columns
-  uint64_t* d_tbl_key = nullptr;
-  uint32_t* d_tbl_word = nullptr;
-  uint64_t* d_tbl_val = nullptr;
-  uint64_t* d_tbl_ci = nullptr;
-  uint64_t* d_tbl_ins = nullptr;
-  uint32_t* d_st_res = nullptr;
-  uint64_t* d_st_key = nullptr;
-  uint64_t* d_st_idx = nullptr;
-  // hot map keys (apply_map_hot.hip)
-  HotKey* d_hot = nullptr;
-  uint32_t* d_hot_n = nullptr;
-  // whole-map ops (map_wide.hip): barrier rows of the current batch, per-map peak-size bounds, scratch
-  uint32_t* d_bar = nullptr;       // [kBarCap]
-  uint32_t* d_bar_n = nullptr;
-  uint32_t* d_mw_peak = nullptr;   // [max_resources]
-  uint64_t* d_mw_drop = nullptr;   // [max_resources]
-  unsigned long long* d_mw_ctl = nullptr;  // [16]
-  std::vector<uint32_t> bars;
-  // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good
-  uint64_t* d_tbl_dl = nullptr;    // [map_entries] timer deadline per entry (0: none)
-  uint32_t* d_map_row = nullptr;   // [sub_batch] staging position -> batch row
-  uint32_t* d_ttl_seen = nullptr;
-  bool ttl_live = false;
-  bool has_sets = false;  // SetState resources share the map table (results rewritten by k_set_results)
-  // MembershipGroupState.schedule timers (MembershipGroupState.java:86-103): armed by schedule barrier rows, fired
-  // at the batch boundary where the reference's fire_due runs (host-ordered by (deadline, id))
-  struct GroupTimer {
-    uint64_t deadline, id, member, payload;
-    uint32_t slot, tag;
-    uint64_t fire_b;  // boundary in the current batch (rows before it applied first); ~0: not in this batch
-  };
-  std::vector<GroupTimer> gtimers;
-  uint64_t gtimer_seq = 0;
-  uint32_t* d_hot_rpre = nullptr;
-  uint32_t* d_hot_rstart = nullptr;
-  uint32_t* d_hot_len = nullptr;
-  uint32_t* d_hot_cond = nullptr;
-  void* d_hot_agg = nullptr;
-  void* d_hot_s0 = nullptr;
-  // extended staging (maps / coordination / value events) + coordination + events
-  bool ext = false, coord_on = false;
-  std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
-  uint8_t* d_sb_kind = nullptr;
-  uint64_t* d_inst_id = nullptr;     // instance slot -> instance id (election listeners, group members)
-  uint8_t* d_coord = nullptr;        // [slots] coordination blocks
-  uint64_t* d_clock = nullptr;       // the engine's log clock (max time applied / advanced)
-  uint16_t* d_ev_cnt = nullptr;      // [sub_batch] events per staged commit
-  uint32_t* d_row_of = nullptr;      // [sub_batch]
-  uint32_t* d_ev_loc = nullptr;      // [sub_batch]
-  uint32_t* d_tile_sum = nullptr;    // [max_tiles]
-  uint64_t* d_tile_off = nullptr;    // [max_tiles]
-  EvRec* d_arena = nullptr;
-  unsigned long long* d_arena_n = nullptr;
-  unsigned long long* d_ev_total = nullptr;
-  uint64_t arena_cap = 0;
-  uint64_t applied = 0;
-  bool applied_pending = false;
-  uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
-  // per-kernel profiling (cc_profile_enable)
-  bool prof_on = false;
-  std::vector<hipEvent_t> ev_pool;
-  struct Pending { int kernel; hipEvent_t a, b; };
-  std::vector<Pending> pending;
-  hipEvent_t open_ev[K_NUM] = {};
-  double prof_ms[K_NUM] = {};
-  uint64_t prof_n[K_NUM] = {};
-};
 
 static hipEvent_t take_event(cc_engine* e) {
   if (!e->ev_pool.empty()) {
@@ -276,6 +163,12 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   e->inst_id.assign(cfg->max_instances, 0);
   e->inst_client.assign(cfg->max_instances, 0);
   e->inst_seq.assign(cfg->max_instances, 0);
+  e->res_id.assign(slots, 0);
+  e->res_key.assign(slots, 0);
+  e->res_has_key.assign(slots, 0);
+  e->res_zombie.assign(slots, 0);
+  e->used_res.reset(cfg->max_resources);
+  e->used_inst.reset(cfg->max_instances);
   auto fail = [&](const char* what, hipError_t x) {
     free_all(e);
     delete e;
@@ -430,13 +323,13 @@ extern "C" int cc_sync(cc_engine* e) {
 
 // Registry updates are control-plane (the reference runs them as log commands too: ResourceManager.java:77-235);
 // the host orders them against batches, so they first drain the stream the last batch ran on.
-static int quiesce(cc_engine* e) {
+int cc::quiesce(cc_engine* e) {
   HIPCHECK(hipSetDevice(e->device));
   HIPCHECK(hipStreamSynchronize(e->last_stream));
   return CC_OK;
 }
 
-static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
+int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
   if (is_keyed(type) && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map and set resources need cc_config.map_capacity > 0");
   if (type < CC_RES_VALUE || type > CC_RES_QUEUE) return set_err(CC_ERR_INVALID, "unknown resource type");
   if (type == CC_RES_SET) e->has_sets = true;
@@ -452,6 +345,9 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   for (uint64_t s = first; s < end; ++s) {
     e->res_type[s] = (uint8_t)type;
     if (is_coord(type) || (type == CC_RES_VALUE && value_events)) e->sb_kind[s >> kSbShift] = 1;
+    e->res_has_key[s] = 0;
+    e->res_zombie[s] = 0;
+    e->used_res.set(s);
   }
   HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
@@ -467,18 +363,36 @@ static int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t t
   return CC_OK;
 }
 
+// Slot-level registration (the host picked the slot): the resource id is the slot number, as in the oracle's
+// orc_resource_create; such a resource has no key (get/create never find it).
+static int create_slots(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
+  int rc = create_range(e, first, count, type);
+  if (rc) return rc;
+  for (uint64_t s = first; s < (uint64_t)first + count; ++s) {
+    e->res_id[s] = s;
+    e->res_by_id[s] = (uint32_t)s;
+  }
+  return CC_OK;
+}
+
 extern "C" int cc_resource_create(cc_engine* e, uint32_t slot, uint32_t type) {
   if (!e) return CC_ERR_INVALID;
-  return create_range(e, slot, 1, type);
+  return create_slots(e, slot, 1, type);
 }
 
 extern "C" int cc_resource_create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
   if (!e) return CC_ERR_INVALID;
-  return create_range(e, first, count, type);
+  return create_slots(e, first, count, type);
 }
 
 extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   if (!e || slot >= e->cfg.max_resources || e->res_type[slot] == CC_RES_NONE) return set_err(CC_ERR_INVALID, "unknown resource slot");
+  if (e->res_zombie[slot]) return set_err(CC_ERR_INVALID, "resource slot was removed by a failed deleteResource");
+  return delete_slot(e, slot);
+}
+
+// ResourceManager.deleteResource after resource.stateMachine.delete() succeeded (ResourceManager.java:212-235).
+int cc::delete_slot(cc_engine* e, uint32_t slot) {
   int rc = quiesce(e);
   if (rc) return rc;
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
@@ -502,12 +416,21 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
     if (e->inst_res[i] == slot) {
       e->inst_res[i] = kNoRes;
       --e->sess_size;
+      e->inst_by_id.erase(e->inst_id[i]);
+      e->used_inst.clear(i);
       HIPCHECK(hipMemcpy(e->d_inst_res + i, &none, sizeof none, hipMemcpyHostToDevice));
     }
+  // ResourceManager.resources / keys / ResourceHolder.sessions
+  auto rit = e->res_by_id.find(e->res_id[slot]);
+  if (rit != e->res_by_id.end() && rit->second == slot) e->res_by_id.erase(rit);
+  if (e->res_has_key[slot]) e->keys.erase(e->res_key[slot]);
+  e->res_has_key[slot] = 0;
+  e->res_sessions.erase(e->res_sessions.lower_bound({slot, 0}), e->res_sessions.lower_bound({slot + 1, 0}));
+  e->used_res.clear(slot);
   return CC_OK;
 }
 
-static int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint32_t res_stride,
+int cc::open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint32_t res_stride,
                       uint64_t id_first, uint64_t client) {
   const uint64_t end = (uint64_t)first + count;
   if (end > e->cfg.max_instances) return set_err(CC_ERR_CAPACITY, "instance slot out of range");
@@ -515,6 +438,7 @@ static int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res
     const uint64_t r = (uint64_t)res_first + k * res_stride;
     if (r >= e->cfg.max_resources || e->res_type[r] == CC_RES_NONE) return set_err(CC_ERR_INVALID, "instance on unknown resource");
     if (e->inst_res[first + k] != kNoRes) return set_err(CC_ERR_INVALID, "instance slot already open");
+    if (e->inst_by_id.count(id_first + k)) return set_err(CC_ERR_INVALID, "instance id already open");
   }
   int rc = quiesce(e);
   if (rc) return rc;
@@ -523,6 +447,8 @@ static int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res
     e->inst_id[first + k] = id_first + k;
     e->inst_client[first + k] = client;
     e->inst_seq[first + k] = e->sess_next++;  // HashMap.putVal of a new key
+    e->inst_by_id[id_first + k] = (uint32_t)(first + k);
+    e->used_inst.set(first + k);
     if (++e->sess_size > e->sess_thr) {
       e->sess_cap <<= 1;
       e->sess_thr <<= 1;
@@ -558,6 +484,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15) || (((uintptr_t)c->inst) & 15))
     return set_err(CC_ERR_INVALID, "inst and value must be 16-byte aligned, status 4-byte aligned");
   if (e->map_bits && !c->key) return set_err(CC_ERR_INVALID, "an engine with maps needs the key column");
+  if (e->d_val_live && !c->index) return set_err(CC_ERR_INVALID, "CC_CFG_VALUE_RETAINED needs the index column");
   if (ev && (!ev->pos || !ev->target || !ev->code || !ev->src || !ev->tag || !ev->payload || !ev->count))
     return set_err(CC_ERR_INVALID, "event stream columns and count are required");
   // Whole-map ops are barriers (map_wide.hip): find them (one sync), then apply the rows between them as segments.
@@ -916,8 +843,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if (e->has_sets && launch_set_results(c->inst, c->op, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, out->status,
                                         out->value, st))
     return set_err(CC_ERR_HIP, "set results launch", hipGetLastError());
-  if (e->d_val_live) {  // retained value commits (live.hip): after every value op of the batch has applied
-    if (!c->index) return set_err(CC_ERR_INVALID, "CC_CFG_VALUE_RETAINED needs the index column");
+  // Retained value commits (live.hip): after every value op of the batch has applied.  The post-pass attributes
+  // each row through the END-of-batch inst_res / res_type / val_meta: correct because the registry cannot change
+  // inside a cc_apply_batch call (resource create/delete, instance open/close are host calls that quiesce the
+  // stream between batches; no op applied on the device rebinds an instance or retypes a slot).
+  if (e->d_val_live) {
     if (launch_value_live(c->inst, c->op, out->status, out->value, c->index, n, e->d_inst_res, e->d_res_type,
                           e->cfg.max_instances, e->d_val_meta, e->cfg.max_resources, e->d_val_wrow, e->d_val_live, st))
       return set_err(CC_ERR_HIP, "retained value launch", hipGetLastError());
@@ -1052,6 +982,8 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
     cinst[p] = order[p].slot;
     const uint32_t r = e->inst_res[order[p].slot];
     const uint8_t ty = e->res_type[r];
+    // a resource a failed deleteResource left behind is not in `resources` any more: no close handler (:253-257)
+    if (e->res_zombie[r]) continue;
     if (ty == CC_RES_VALUE || ty == CC_RES_ELECTION || ty == CC_RES_GROUP) rp.emplace_back(r, p);
   }
   std::sort(rp.begin(), rp.end());
@@ -1064,8 +996,12 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   }
   rstart.push_back((uint32_t)rp.size());
   const uint32_t nr = (uint32_t)rlist.size();
-  // device scratch: cinst | rlist | rstart | items | cnt | fail, off
-  const size_t n32 = (size_t)m + nr + (nr + 1) + items.size() + m + 1;
+  // client rank of every position (order is sorted by client rank first)
+  const uint32_t nc = (uint32_t)count;
+  std::vector<uint32_t> pcl(m);
+  for (uint32_t p = 0; p < m; ++p) pcl[p] = (uint32_t)order[p].crank;
+  // device scratch: cinst | rlist | rstart | items | cnt | pcl | fail[nc], off
+  const size_t n32 = (size_t)m + nr + (nr + 1) + items.size() + m + m + nc;
   uint32_t* d32 = nullptr;
   uint64_t* d_off = nullptr;
   HIPCHECK(hipMalloc(&d32, sizeof(uint32_t) * n32));
@@ -1080,7 +1016,8 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   h32.insert(h32.end(), rstart.begin(), rstart.end());
   h32.insert(h32.end(), items.begin(), items.end());
   h32.insert(h32.end(), (size_t)m, 0u);
-  h32.push_back(m);
+  h32.insert(h32.end(), pcl.begin(), pcl.end());
+  h32.insert(h32.end(), (size_t)nc, m);
   CloseArgs ca{};
   ca.cinst = d32;
   ca.m = m;
@@ -1088,7 +1025,8 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   ca.rstart = d32 + m + nr;
   ca.items = d32 + m + nr + nr + 1;
   ca.cnt = d32 + m + nr + nr + 1 + items.size();
-  ca.fail = ca.cnt + m;
+  ca.pcl = ca.cnt + m;
+  ca.fail = ca.cnt + m + m;
   ca.nr = nr;
   ca.off = d_off;
   ca.inst_res = e->d_inst_res;
@@ -1118,22 +1056,32 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
     ca.out_payload = d_events->payload;
     ca.out_count = d_events->count;
   }
-  uint32_t stop = m;
+  std::vector<uint32_t> fail(nc, m);
   hipError_t x = hipMemcpyAsync(d32, h32.data(), sizeof(uint32_t) * n32, hipMemcpyHostToDevice, st);
   if (x == hipSuccess) x = hipMemsetAsync(ca.arena_n, 0, sizeof(unsigned long long), st);
   if (x == hipSuccess && launch_close(ca, st)) x = hipGetLastError();
-  if (x == hipSuccess) x = hipMemcpyAsync(&stop, ca.fail, sizeof stop, hipMemcpyDeviceToHost, st);
+  if (x == hipSuccess) x = hipMemcpyAsync(fail.data(), ca.fail, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, st);
   if (x == hipSuccess) x = hipStreamSynchronize(st);
   (void)hipFree(d32);
   (void)hipFree(d_off);
   if (d_zero) (void)hipFree(d_zero);
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "session close", x);
-  // the host mirror of ResourceManager.sessions
-  for (uint32_t p = 0; p < stop && p < m; ++p) {
-    e->inst_res[cinst[p]] = kNoRes;
+  // the host mirrors of ResourceManager.sessions and ResourceHolder.sessions (:253-261); a close that threw has
+  // already removed its ResourceHolder.sessions entry but keeps its holder
+  uint64_t closed = 0;
+  for (uint32_t p = 0; p < m; ++p) {
+    const uint32_t stop = fail[pcl[p]];
+    if (p > stop) continue;  // after the close that threw: this client's loop had ended
+    const uint32_t i = cinst[p], r = e->inst_res[i];
+    if (!e->res_zombie[r]) e->res_sessions.erase({r, e->inst_client[i]});
+    if (p == stop) continue;
+    e->inst_res[i] = kNoRes;
     --e->sess_size;
+    e->inst_by_id.erase(e->inst_id[i]);
+    e->used_inst.clear(i);
+    ++closed;
   }
-  if (h_closed) *h_closed = stop < m ? stop : m;
+  if (h_closed) *h_closed = closed;
   return check_device_err(e);
 }
 
@@ -1329,10 +1277,11 @@ static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unp
 // Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
 // mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
 namespace {
-constexpr uint64_t kSnapMagic = 0x31304E5053434343ull;  // "CCCSPN01"
+constexpr uint64_t kSnapMagic = 0x32304E5053434343ull;  // "CCCSPN02"
+constexpr uint32_t kSnapRetained = 4u;                   // SnapHdr.flags: CC_CFG_VALUE_RETAINED section present
 struct SnapHdr {
   uint64_t magic;
-  uint32_t abi, flags;  // flags: 1 coord blocks, 2 map TTL mode
+  uint32_t abi, flags;  // flags: 1 coord blocks, 2 map TTL mode, 4 retained value commits
   uint32_t max_resources, max_instances, map_bits, sb;
   uint64_t applied, sess_next;
   uint32_t sess_cap, sess_thr, sess_size, pad;
@@ -1360,6 +1309,10 @@ static std::vector<Section> snap_sections(cc_engine* e) {
       {e->d_sb_kind, nullptr, e->sb},
       {e->d_inst_id, nullptr, 8 * mi},
       {e->d_clock, nullptr, 8},
+      {nullptr, e->res_id.data(), 8 * slots},
+      {nullptr, e->res_key.data(), 8 * slots},
+      {nullptr, e->res_has_key.data(), slots},
+      {nullptr, e->res_zombie.data(), slots},
   };
   if (e->d_val_live) v.push_back({e->d_val_live, nullptr, 8 * slots});
   if (e->map_bits) {
@@ -1379,7 +1332,8 @@ static std::vector<Section> snap_sections(cc_engine* e) {
 
 extern "C" int cc_snapshot_size(cc_engine* e, uint64_t* bytes) {
   if (!e || !bytes) return CC_ERR_INVALID;
-  uint64_t total = sizeof(SnapHdr) + 16 + e->gtimers.size() * sizeof(cc_engine::GroupTimer);
+  uint64_t total = sizeof(SnapHdr) + 16 + e->gtimers.size() * sizeof(cc_engine::GroupTimer) + 8 +
+                   e->res_sessions.size() * 24;
   for (const Section& x : snap_sections(e)) total += 8 + x.bytes;
   *bytes = total;
   return CC_OK;
@@ -1395,7 +1349,7 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
   SnapHdr h{};
   h.magic = kSnapMagic;
   h.abi = CC_ABI_VERSION;
-  h.flags = (e->coord_on ? 1u : 0u) | (e->ttl_live ? 2u : 0u);
+  h.flags = (e->coord_on ? 1u : 0u) | (e->ttl_live ? 2u : 0u) | (e->d_val_live ? kSnapRetained : 0u);
   h.max_resources = e->cfg.max_resources;
   h.max_instances = e->cfg.max_instances;
   h.map_bits = e->map_bits;
@@ -1419,6 +1373,15 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
   memcpy(p, &ng, 8);
   memcpy(p + 8, &e->gtimer_seq, 8);
   if (ng) memcpy(p + 16, e->gtimers.data(), ng * sizeof(cc_engine::GroupTimer));
+  p += 16 + ng * sizeof(cc_engine::GroupTimer);
+  const uint64_t ns = e->res_sessions.size();  // ResourceHolder.sessions: (slot, client, instance id) triples
+  memcpy(p, &ns, 8);
+  p += 8;
+  for (const auto& kv : e->res_sessions) {
+    const uint64_t t[3] = {kv.first.first, kv.first.second, kv.second};
+    memcpy(p, t, 24);
+    p += 24;
+  }
   return CC_OK;
 }
 
@@ -1430,6 +1393,8 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   if (h.max_resources != e->cfg.max_resources || h.max_instances != e->cfg.max_instances || h.map_bits != e->map_bits ||
       h.sb != e->sb)
     return set_err(CC_ERR_INVALID, "snapshot configuration (max_resources/max_instances/map_capacity) differs");
+  if (((h.flags & kSnapRetained) != 0) != (e->d_val_live != nullptr))  // the section lists would differ
+    return set_err(CC_ERR_INVALID, "snapshot and engine differ in CC_CFG_VALUE_RETAINED");
   int rc = quiesce(e);
   if (rc) return rc;
   if ((h.flags & 1u) && (rc = ensure_ext(e, true))) return rc;
@@ -1454,6 +1419,35 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   if (p + ng * sizeof(cc_engine::GroupTimer) > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
   e->gtimers.resize(ng);
   if (ng) memcpy(e->gtimers.data(), p, ng * sizeof(cc_engine::GroupTimer));
+  p += ng * sizeof(cc_engine::GroupTimer);
+  uint64_t ns = 0;
+  if (p + 8 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&ns, p, 8);
+  p += 8;
+  if (p + ns * 24 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  e->res_sessions.clear();
+  for (uint64_t i = 0; i < ns; ++i, p += 24) {
+    uint64_t t[3];
+    memcpy(t, p, 24);
+    e->res_sessions[{(uint32_t)t[0], t[1]}] = t[2];
+  }
+  // the control-plane maps and slot occupancy follow from the restored arrays
+  e->keys.clear();
+  e->res_by_id.clear();
+  e->inst_by_id.clear();
+  e->used_res.reset(e->cfg.max_resources);
+  e->used_inst.reset(e->cfg.max_instances);
+  for (uint32_t s = 0; s < e->cfg.max_resources; ++s) {
+    if (e->res_type[s] == CC_RES_NONE) continue;
+    e->used_res.set(s);
+    if (e->res_has_key[s]) e->keys[e->res_key[s]] = e->res_id[s];
+    if (!e->res_zombie[s]) e->res_by_id[e->res_id[s]] = s;
+  }
+  for (uint32_t i = 0; i < e->cfg.max_instances; ++i) {
+    if (e->inst_res[i] == kNoRes) continue;
+    e->used_inst.set(i);
+    e->inst_by_id[e->inst_id[i]] = i;
+  }
   e->applied = h.applied;
   e->applied_pending = false;
   e->has_sets = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_SET) != e->res_type.end();

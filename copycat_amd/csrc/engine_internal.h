@@ -252,7 +252,9 @@ struct CloseArgs {
   const uint8_t* res_type;
   const uint64_t* inst_id;
   uint8_t* coord;          // null: no coordination blocks (then no state machine has a close handler)
-  uint32_t* fail;          // [1] first position whose close throws (init m)
+  const uint32_t* pcl;     // [m] client rank of each position (positions are grouped by client, in client order)
+  uint32_t* fail;          // [clients] per client: first position whose close throws (init m); that client's
+                           // fan-out ends there (ResourceManager.close runs once per session), the others go on
   uint32_t* cnt;           // [m] events per close (zeroed)
   uint64_t* off;           // [m + 1]
   EvRec* arena;

@@ -1,0 +1,185 @@
+// engine_state.h — the engine handle (struct cc_engine) shared by the host-side translation units of
+// libcopycat_apply.so: engine.hip (lifecycle, registry, batched apply driver, readback, snapshots) and
+// manager.hip (the ResourceManager control plane, ResourceManager.java:77-264).  Host code only.
+#pragma once
+#include <map>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+// error reporting (cc_last_error) and the stream drain every registry update starts with
+int set_err(int code, const char* what, hipError_t e = hipSuccess);
+int quiesce(cc_engine* e);
+// registry primitives (engine.hip): resource slots [first, first+count) of `type`; instance slots first+k ->
+// resource res_first + k*res_stride, instance id id_first+k, owned by `client`; a successful deleteResource
+int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type);
+int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint32_t res_stride, uint64_t id_first,
+               uint64_t client);
+int delete_slot(cc_engine* e, uint32_t slot);
+
+// Occupancy bitmap of a slot space with lowest-free / highest-free search (control-plane allocation: rare, so a
+// word scan from a hint is enough).
+struct SlotBits {
+  std::vector<uint64_t> w;
+  uint64_t n = 0, lo = 0;  // lo: no free slot below it
+  void reset(uint64_t count) {
+    n = count;
+    w.assign((count + 63) / 64, 0);
+    lo = 0;
+  }
+  bool test(uint64_t s) const { return (w[s >> 6] >> (s & 63)) & 1; }
+  void set(uint64_t s) { w[s >> 6] |= 1ull << (s & 63); }
+  void clear(uint64_t s) {
+    w[s >> 6] &= ~(1ull << (s & 63));
+    if (s < lo) lo = s;
+  }
+  int64_t lowest() {  // lowest free slot, -1 if none
+    for (uint64_t i = lo >> 6; i < w.size(); ++i)
+      if (~w[i]) {
+        const uint64_t s = i * 64 + (uint64_t)__builtin_ctzll(~w[i]);
+        lo = i * 64;
+        return s < n ? (int64_t)s : -1;
+      }
+    lo = n;
+    return -1;
+  }
+  int64_t highest() {  // highest free slot, -1 if none
+    for (uint64_t i = w.size(); i-- > 0;) {
+      uint64_t f = ~w[i];
+      if (i == w.size() - 1 && (n & 63)) f &= (1ull << (n & 63)) - 1;
+      if (f) return (int64_t)(i * 64 + 63 - (uint64_t)__builtin_clzll(f));
+    }
+    return -1;
+  }
+};
+}  // namespace cc
+
+#define HIPCHECK(x)                                                \
+  do {                                                             \
+    hipError_t _e = (x);                                           \
+    if (_e != hipSuccess) return cc::set_err(CC_ERR_HIP, #x, _e);  \
+  } while (0)
+
+using namespace cc;  // internal header: the engine's host translation units all work in namespace cc
+
+struct cc_engine {
+  cc_config cfg{};
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t last_stream = nullptr;
+  uint32_t sb = 0, sb_bits = 0;  // value super-buckets of 256 slots
+  uint32_t map_bits = 0;         // 2^map_bits map table regions follow them (0: no maps)
+  uint64_t map_entries = 0;
+  uint32_t sb_total() const { return sb + (map_bits ? (1u << map_bits) + kHotMax : 0u); }
+  uint64_t sub_batch = 0, max_tiles = 0;
+  // host mirrors of the registry
+  std::vector<uint8_t> res_type;     // [sb*256]
+  std::vector<uint32_t> inst_res;    // [max_inst]
+  std::vector<uint64_t> inst_id, inst_client;
+  // java.util.HashMap iteration order of ResourceManager.sessions (ResourceManager.java:37): bucket index under
+  // the table capacity (starts at 16, doubles when the size passes 3/4 of it, never shrinks), then insertion
+  // order within the bucket.  Used to order the close fan-out (ResourceManager.java:250-264).
+  uint32_t sess_cap = 16, sess_thr = 12, sess_size = 0;
+  uint64_t sess_next = 0;
+  std::vector<uint64_t> inst_seq;
+  // ResourceManager control plane (manager.hip; ResourceManager.java:37-39,269-295).  Resource ids and instance ids
+  // are commit indices (:86-88,103,185); slots are the engine's dense handles for them.
+  std::unordered_map<uint64_t, uint64_t> keys;       // ResourceManager.keys: host-interned key -> resource id
+  std::unordered_map<uint64_t, uint32_t> res_by_id;  // ResourceManager.resources: resource id -> slot
+  std::unordered_map<uint64_t, uint32_t> inst_by_id; // ResourceManager.sessions: instance id -> instance slot
+  std::map<std::pair<uint32_t, uint64_t>, uint64_t> res_sessions;  // ResourceHolder.sessions: (slot, client) -> instance id
+  std::vector<uint64_t> res_id, res_key;  // [slots] resource id; key (when res_has_key)
+  std::vector<uint8_t> res_has_key;       // [slots] created through get/create (low-level slots have no key)
+  std::vector<uint8_t> res_zombie;        // [slots] removed from `resources` by a deleteResource whose delete() threw
+  cc::SlotBits used_res, used_inst;       // slot occupancy (allocation: values/maps low, coordination high; instances low)
+  // device registry + state
+  uint32_t* d_inst_res = nullptr;
+  uint16_t* d_inst_res16 = nullptr;  // value-only fast path (< 65535 resources, <= 65536 instances)
+  uint16_t* d_res16 = nullptr;       // [sub_batch] resolved resource per commit (same path)
+  uint8_t* d_res_type = nullptr;
+  uint32_t* d_val_meta = nullptr;
+  uint64_t* d_val_v = nullptr;
+  uint64_t* d_val_live = nullptr;             // [slots] retained value commit index (CC_CFG_VALUE_RETAINED)
+  unsigned long long* d_val_wrow = nullptr;   // [slots] last writer row + 1 of the current batch
+  // workspace
+  uint32_t* d_st_meta = nullptr;
+  u64x2* d_st_ab = nullptr;
+  uint16_t* d_cpos = nullptr;
+  uint16_t* d_ttab = nullptr;
+  uint8_t* d_rst_status = nullptr;
+  uint64_t* d_rst_value = nullptr;
+  uint32_t* d_err = nullptr;
+  // map table (apply_map.hip) + map staging columns
+  uint64_t* d_tbl_key = nullptr;
+  uint32_t* d_tbl_word = nullptr;
+  uint64_t* d_tbl_val = nullptr;
+  uint64_t* d_tbl_ci = nullptr;
+  uint64_t* d_tbl_ins = nullptr;
+  uint32_t* d_st_res = nullptr;
+  uint64_t* d_st_key = nullptr;
+  uint64_t* d_st_idx = nullptr;
+  // hot map keys (apply_map_hot.hip)
+  HotKey* d_hot = nullptr;
+  uint32_t* d_hot_n = nullptr;
+  // whole-map ops (map_wide.hip): barrier rows of the current batch, per-map peak-size bounds, scratch
+  uint32_t* d_bar = nullptr;       // [kBarCap]
+  uint32_t* d_bar_n = nullptr;
+  uint32_t* d_mw_peak = nullptr;   // [max_resources]
+  uint64_t* d_mw_drop = nullptr;   // [max_resources]
+  unsigned long long* d_mw_ctl = nullptr;  // [16]
+  std::vector<uint32_t> bars;
+  // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good
+  uint64_t* d_tbl_dl = nullptr;    // [map_entries] timer deadline per entry (0: none)
+  uint32_t* d_map_row = nullptr;   // [sub_batch] staging position -> batch row
+  uint32_t* d_ttl_seen = nullptr;
+  bool ttl_live = false;
+  bool has_sets = false;  // SetState resources share the map table (results rewritten by k_set_results)
+  // MembershipGroupState.schedule timers (MembershipGroupState.java:86-103): armed by schedule barrier rows, fired
+  // at the batch boundary where the reference's fire_due runs (host-ordered by (deadline, id))
+  struct GroupTimer {
+    uint64_t deadline, id, member, payload;
+    uint32_t slot, tag;
+    uint64_t fire_b;  // boundary in the current batch (rows before it applied first); ~0: not in this batch
+  };
+  std::vector<GroupTimer> gtimers;
+  uint64_t gtimer_seq = 0;
+  uint32_t* d_hot_rpre = nullptr;
+  uint32_t* d_hot_rstart = nullptr;
+  uint32_t* d_hot_len = nullptr;
+  uint32_t* d_hot_cond = nullptr;
+  void* d_hot_agg = nullptr;
+  void* d_hot_s0 = nullptr;
+  // extended staging (maps / coordination / value events) + coordination + events
+  bool ext = false, coord_on = false;
+  std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
+  uint8_t* d_sb_kind = nullptr;
+  uint64_t* d_inst_id = nullptr;     // instance slot -> instance id (election listeners, group members)
+  uint8_t* d_coord = nullptr;        // [slots] coordination blocks
+  uint64_t* d_clock = nullptr;       // the engine's log clock (max time applied / advanced)
+  uint16_t* d_ev_cnt = nullptr;      // [sub_batch] events per staged commit
+  uint32_t* d_row_of = nullptr;      // [sub_batch]
+  uint32_t* d_ev_loc = nullptr;      // [sub_batch]
+  uint32_t* d_tile_sum = nullptr;    // [max_tiles]
+  uint64_t* d_tile_off = nullptr;    // [max_tiles]
+  EvRec* d_arena = nullptr;
+  unsigned long long* d_arena_n = nullptr;
+  unsigned long long* d_ev_total = nullptr;
+  uint64_t arena_cap = 0;
+  uint64_t applied = 0;
+  bool applied_pending = false;
+  uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
+  // per-kernel profiling (cc_profile_enable)
+  bool prof_on = false;
+  std::vector<hipEvent_t> ev_pool;
+  struct Pending { int kernel; hipEvent_t a, b; };
+  std::vector<Pending> pending;
+  hipEvent_t open_ev[K_NUM] = {};
+  double prof_ms[K_NUM] = {};
+  uint64_t prof_n[K_NUM] = {};
+};

@@ -68,6 +68,15 @@ def lib():
             "cc_profile_enable": (i32, [P, i32]),
             "cc_profile_reset": (i32, [P]),
             "cc_profile_read": (i32, [P, i32, P, P, P]),
+            "cc_sessions_close": (i32, [P, P, u64, P, P, P]),
+            "cc_sessions_expire": (i32, [P, P, u64, P, P, P]),
+            "cc_get_resource": (i32, [P, u64, u32, u64, u64, P, P, P]),
+            "cc_create_resource": (i32, [P, u64, u32, u64, u64, P, P, P]),
+            "cc_resource_exists": (i32, [P, u64, P]),
+            "cc_delete_resource": (i32, [P, u64, P]),
+            "cc_instance_slot": (i32, [P, u64, P]),
+            "cc_resource_slot": (i32, [P, u64, P]),
+            "cc_debug_phases": (i32, [P, i32, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -196,6 +205,61 @@ class Engine:
 
     def instance_open_range(self, first, count, res_first, id_first, client):
         _check(self.L.cc_instance_open_range(self.h, first, count, res_first, id_first, client))
+
+    # ---- ResourceManager control commands (ResourceManager.java:77-235; manager.hip) ------------------------
+    def _ctl(self, fn, key, rtype, client, index):
+        iid, islot, st = C.c_uint64(), C.c_uint32(), C.c_uint8()
+        _check(fn(self.h, key, rtype, client, index, C.byref(iid), C.byref(islot), C.byref(st)))
+        return st.value, iid.value, islot.value
+
+    def get_resource(self, key, rtype, client, index):
+        """GetResource commit -> (status byte, instance id, instance slot)."""
+        return self._ctl(self.L.cc_get_resource, key, rtype, client, index)
+
+    def create_resource(self, key, rtype, client, index):
+        """CreateResource commit -> (status byte, instance id, instance slot)."""
+        return self._ctl(self.L.cc_create_resource, key, rtype, client, index)
+
+    def resource_exists(self, key):
+        out = C.c_uint8()
+        _check(self.L.cc_resource_exists(self.h, key, C.byref(out)))
+        return bool(out.value)
+
+    def delete_resource(self, resource_id):
+        """DeleteResource commit (by resource id) -> status byte."""
+        st = C.c_uint8()
+        _check(self.L.cc_delete_resource(self.h, resource_id, C.byref(st)))
+        return st.value
+
+    def instance_slot(self, instance_id):
+        out = C.c_int64()
+        _check(self.L.cc_instance_slot(self.h, instance_id, C.byref(out)))
+        return out.value
+
+    def resource_slot(self, resource_id):
+        out = C.c_int64()
+        _check(self.L.cc_resource_slot(self.h, resource_id, C.byref(out)))
+        return out.value
+
+    # ---- session close / expire fan-out (ResourceManager.java:237-264) -----------------------------------
+    def sessions_close(self, clients, capacity=1 << 16, device="cuda"):
+        """Close client sessions in order; returns (instances closed, events dict as DeviceEvents.host())."""
+        arr = np.ascontiguousarray(np.asarray(clients, dtype=np.uint64).reshape(-1))
+        evs = DeviceEvents(capacity, device=device)
+        ev = evs.struct()
+        closed = C.c_uint64()
+        _check(self.L.cc_sessions_close(self.h, _np(arr) if len(arr) else None, len(arr), C.byref(ev), None,
+                                        C.byref(closed)))
+        return closed.value, evs.host()
+
+    def sessions_expire(self, bitmap, sessions, capacity=1 << 16, device="cuda"):
+        """Close every client session whose bit is set in `bitmap` (a device u64 tensor, cc_expire_sweep's output),
+        in ascending id order; returns (instances closed, events)."""
+        evs = DeviceEvents(capacity, device=device)
+        ev = evs.struct()
+        closed = C.c_uint64()
+        _check(self.L.cc_sessions_expire(self.h, _dptr(bitmap), sessions, C.byref(ev), None, C.byref(closed)))
+        return closed.value, evs.host()
 
     # ---- the hot path ----------------------------------------------------------------------------------
     def apply(self, db: DeviceBatch, status, value, stream=None):

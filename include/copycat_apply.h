@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CC_ABI_VERSION 1
+#define CC_ABI_VERSION 2
 
 /* ---- return codes ------------------------------------------------------------------------------ */
 #define CC_OK               0
@@ -254,6 +254,31 @@ int  cc_instance_open(cc_engine* e, uint32_t inst, uint32_t res_slot, uint64_t i
 int  cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint64_t id_first,
                             uint64_t client_session);
 
+/* ---- ResourceManager control commands (ResourceManager.java:77-235) ------------------------------------
+ * GetResource / CreateResource / DeleteResource / ResourceExists commits, applied by the host between batches in log
+ * order (manager.hip).  `key` is the host-interned GetResource.key String, `client` = commit.session().id(),
+ * `index` = commit.index().  Resource ids and instance ids are commit indices; the engine picks the slots.
+ * *status = CC_STATUS(CC_ST_OK, CC_TAG_LONG) with *instance_id = the ManagedResourceSession id (the Long the reference
+ * returns) and *inst_slot = the instance slot its commits carry in cc_batch.inst; or CC_ST_TYPE_MISMATCH
+ * ("inconsistent resource type" :119-121,178-181).  Return codes: CC_ERR_CAPACITY when no slot is free.       */
+/* getResource :77-143 — a new key creates the resource (id = index); a client that already holds an instance of
+ * the resource gets that instance back (ResourceHolder.sessions :137-141) */
+int  cc_get_resource(cc_engine* e, uint64_t key, uint32_t type, uint64_t client, uint64_t index, uint64_t* instance_id,
+                     uint32_t* inst_slot, uint8_t* status);
+/* createResource :148-196 — always a new instance (id = index), not recorded in ResourceHolder.sessions */
+int  cc_create_resource(cc_engine* e, uint64_t key, uint32_t type, uint64_t client, uint64_t index, uint64_t* instance_id,
+                        uint32_t* inst_slot, uint8_t* status);
+/* resourceExists :201-207 */
+int  cc_resource_exists(cc_engine* e, uint64_t key, uint8_t* exists);
+/* deleteResource :212-235 by RESOURCE id (clients send their instance id, so only the creating instance matches,
+ * A13): *status = OK|BOOL (true), CC_ST_UNKNOWN_RESOURCE, or CC_ST_ILLEGAL_STATE when the state machine's delete()
+ * throws (a lock / election whose holder commit was already cleaned): the resource then leaves `resources` but its
+ * key and instances stay, and commits on those instances get CC_ST_NULL_POINTER (:62,71).                     */
+int  cc_delete_resource(cc_engine* e, uint64_t resource_id, uint8_t* status);
+/* id -> slot lookups of ResourceManager.sessions / resources (-1: none) */
+int  cc_instance_slot(cc_engine* e, uint64_t instance_id, int64_t* slot);
+int  cc_resource_slot(cc_engine* e, uint64_t resource_id, int64_t* slot);
+
 /* ---- the hot path --------------------------------------------------------------------------------
  * Apply n committed entries (device-resident columns) in log order.  Replaces the per-entry chain
  * ResourceManager.operateResource (ResourceManager.java:56-72) -> executors -> state machine method.
@@ -315,8 +340,9 @@ int  cc_advance_time_events(cc_engine* e, uint64_t now, const cc_events* d_event
  * first listener, MembershipGroupState.close :36-42 publishes "leave", an AtomicValue listener is dropped; locks and
  * maps have no close handler) and leaves the dispatch table: later commits on it get CC_ST_UNKNOWN_SESSION.  Events
  * go to d_events (src CC_EVSRC_CLOSE, pos 0xFFFFFFFF) in fan-out order; *count is written.  A close that throws
- * (an election leader already cleaned by delete) ends the fan-out there, as the reference's loop does:
- * *h_closed = the instances closed.  Synchronous (control plane).                                              */
+ * (an election leader already cleaned by delete) ends that client's fan-out there, as the reference's loop does
+ * (ResourceManager.close runs once per session; the remaining clients are closed): *h_closed = the instances closed.
+ * Synchronous (control plane).                                              */
 int  cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* d_events, void* stream,
                        uint64_t* h_closed);
 /* The expired set of cc_expire_sweep (bit s = client session id s, u64 words in HBM), closed in ascending id order. */

@@ -121,6 +121,9 @@ struct Resource {
   uint64_t id = 0;   // resource id (= creating commit index under the manager)
   uint64_t key = 0;  // interned key handle
   bool has_key = false;
+  // removed from ResourceManager.resources by a deleteResource whose delete() threw (:214-220): the instances that
+  // still name its id find `resources.get(id) == null` forever, so the slot is never handed out again
+  bool zombie = false;
   std::unordered_map<uint64_t, uint64_t> sessions;  // ResourceHolder.sessions: client session -> instance id
   ValueSM v;
   MapSM m;
@@ -249,7 +252,7 @@ struct orc {
     sessions_order.on_remove();
   }
   int alloc_res_slot() {
-    for (uint32_t s = 0; s < max_res; ++s) if (!res[s].exists) return (int)s;
+    for (uint32_t s = 0; s < max_res; ++s) if (!res[s].exists && !res[s].zombie) return (int)s;
     return -1;
   }
   int alloc_inst_slot() {
@@ -810,7 +813,8 @@ orc* orc_create(uint32_t max_resources, uint32_t max_instances, uint32_t flags) 
 void orc_destroy(orc* o) { delete o; }
 
 int orc_resource_create(orc* o, uint32_t slot, uint32_t type) {
-  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_QUEUE || o->res[slot].exists) return CC_ERR_INVALID;
+  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_QUEUE || o->res[slot].exists || o->res[slot].zombie)
+    return CC_ERR_INVALID;
   o->init_resource(slot, type, slot);
   return CC_OK;
 }
@@ -906,6 +910,7 @@ int orc_delete_resource(orc* o, uint64_t resource_id, uint8_t* status) {
     // delete() threw after resources.remove(): keys, timers and instance holders are left behind; a later
     // commit on such an instance hits `resources.get(...) == null` -> NullPointerException (:62,71).
     r.exists = false;
+    r.zombie = true;
     *status = st;
     return CC_OK;
   }

@@ -60,15 +60,12 @@ GPU_QUEUE_OPS = {"QUEUE_CONTAINS", "QUEUE_ADD", "QUEUE_OFFER", "QUEUE_PEEK", "QU
 
 
 def gpu_eligible(kat):
-    """KATs whose every step this build applies on the GPU: AtomicValue ops (listeners with CC_CFG_VALUE_EVENTS),
-    every Map and Set op (TTL timers included), lock / election / group ops, Delete, and clock advances;
-    no registry control or session-close steps (host control plane)."""
+    """KATs whose every step this build runs through the engine: every op of every covered state machine, Delete,
+    clock advances, session closes (the GPU close fan-out) and manager control commands (manager.hip)."""
     types = {r[1] for r in kat["resources"]}
     if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET", "QUEUE"}:
         return False
     for s in kat["steps"]:
-        if "control" in s or "close" in s:
-            return False
         if "commit" in s:
             c = s["commit"]
             if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS | GPU_SET_OPS | GPU_QUEUE_OPS:
@@ -278,7 +275,7 @@ class EngineBackend:
         self.ids[iid] = inst
 
     def inst_slot_of(self, iid):
-        return self.ids.get(iid, -1)
+        return self.E.instance_slot(iid)
 
     def apply(self, b):
         s, v, ev = self.E.apply_host_events(b)
@@ -291,10 +288,30 @@ class EngineBackend:
                 evs.append(row)
         return s, v, evs, aux
 
-    def advance(self, now):
-        ev = self.E.advance_time_events(now)
+    @staticmethod
+    def _rows(ev):
         return [(int(ev["pos"][i]), int(ev["target"][i]), int(ev["code"][i]), int(ev["tag"][i]), int(ev["payload"][i]))
                 for i in range(len(ev["pos"]))]
+
+    def advance(self, now):
+        return self._rows(self.E.advance_time_events(now))
+
+    def close(self, client):
+        _, ev = self.E.sessions_close([client])
+        return self._rows(ev)
+
+    def manager(self, what, key, t, client, index):
+        fn = self.E.get_resource if what == "get" else self.E.create_resource
+        st, iid, islot = fn(key, t, client, index)
+        if abi.status_code(st) == abi.CC_ST_OK:
+            self.ids[iid] = islot
+        return st, iid
+
+    def delete_resource(self, rid):
+        return self.E.delete_resource(rid)
+
+    def resource_exists(self, key):
+        return self.E.resource_exists(key)
 
     def value_state(self, res):
         t, v, c = self.E.value_state(res, 1)

@@ -60,6 +60,7 @@ def _check_batch(E, O, b):
     assert gm == list(zip(apos.tolist(), amem.tolist()))
     # the stream is ordered by log row
     assert np.all(np.diff(ev["pos"].astype(np.int64)) >= 0)
+    return s, v, ev
 
 
 def _check_state(E, O, types):

@@ -17,8 +17,12 @@ def test_gpu_kat_coverage():
             "map_clear", "map_put_ttl", "map_put_if_absent_ttl", "A5_contains_value_npe_order",
             "A8_timer_deferred_after_commit", "A8_timer_immediate_module_mode", "set_add_remove",
             "set_ttl_size_clear", "group_schedule_fires_on_clock", "dispatch_errors", "queue_offer_poll",
-            "queue_add_remove", "queue_null_and_empty_quirks"} <= names
-    assert len(KATS) >= 44
+            "queue_add_remove", "queue_null_and_empty_quirks",
+            # session close fan-out (close.hip) and the manager control plane (manager.hip)
+            "election_next_on_close", "A10_close_publishes_leave_for_non_member", "A11_lock_survives_holder_close",
+            "manager_create_concurrency", "manager_get_create_concurrency", "manager_operate_many",
+            "manager_get_reuses_instance", "A13_delete_resource_by_instance_id"} <= names
+    assert len(KATS) == len(all_kats())  # every reference-pinned KAT runs through the engine
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])

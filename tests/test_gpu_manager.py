@@ -1,0 +1,240 @@
+"""GPU-engine parity of the ResourceManager control plane (manager.hip: cc_get_resource / cc_create_resource /
+cc_resource_exists / cc_delete_resource) interleaved with commit batches and session closes, vs the oracle.
+
+Reference: ResourceManager.getResource :77-143, createResource :148-196, resourceExists :201-207, deleteResource
+:212-235, close :250-264 (manager/src/main/java/io/atomix/manager/ResourceManager.java).  Pinned rules: resource id =
+instance id = commit index; get reuses the client's instance (ResourceHolder.sessions), create always mints one and
+does not record it; a type mismatch is "inconsistent resource type"; delete looks the RESOURCE id up (clients send
+their instance id, A13); a delete() that throws leaves a resource whose instances NPE.
+
+Bar: every control result (status, instance id, instance slot) equal; every batch bit-exact (status, value, events
+per commit); final state of every live resource, matched by resource id."""
+import numpy as np
+import pytest
+
+from copycat_amd import abi
+from copycat_amd.batch import Batch
+
+pytestmark = pytest.mark.gpu
+
+V, M, S, Q = abi.CC_RES_VALUE, abi.CC_RES_MAP, abi.CC_RES_SET, abi.CC_RES_QUEUE
+L, E_, G = abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP
+TYPES = [V, M, S, Q, L, E_, G]
+FLAGS = abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_EVENTS
+LONG, NULL = abi.CC_TAG_LONG, abi.CC_TAG_NULL
+
+
+class Pair:
+    """The engine and the oracle driven with the same control commands and batches."""
+
+    def __init__(self, max_res=64, max_inst=256):
+        from copycat_amd.engine import Engine
+        from oracle.oracle_py import Oracle
+
+        self.E = Engine(max_res, max_inst, 1 << 14, flags=FLAGS, map_capacity=4096, max_events=1 << 16)
+        self.O = Oracle(max_res, max_inst, abi.CC_CFG_TIMERS_DEFERRED)
+        self.index = 1
+        self.inst = {}     # instance id -> (type, client, resource id)
+        self.rtype = {}    # resource id -> type (live resources)
+        self.key_rid = {}  # key -> resource id
+
+    def control(self, what, key=0, rtype=V, client=1, rid=0):
+        idx = self.index
+        self.index += 1
+        if what in ("get", "create"):
+            e = (self.E.get_resource if what == "get" else self.E.create_resource)(key, rtype, client, idx)
+            o = (self.O.get_resource if what == "get" else self.O.create_resource)(key, rtype, client, idx)
+            assert e[0] == o[0], (what, key, rtype, e, o)
+            if abi.status_code(e[0]) == abi.CC_ST_OK:
+                assert e[1:] == o[1:], (what, e, o)  # instance id, and the lowest-free instance slot
+                res = self.key_rid.setdefault(key, idx)  # a new key's resource id is this commit's index
+                self.inst[e[1]] = (rtype, client, res)
+                self.rtype[res] = rtype
+            return e
+        if what == "exists":
+            assert self.E.resource_exists(key) == self.O.resource_exists(key)
+            return None
+        if what == "delete":
+            e, o = self.E.delete_resource(rid), self.O.delete_resource(rid)
+            assert e == o, ("delete", rid, e, o)
+            if abi.status_code(e) in (abi.CC_ST_OK, abi.CC_ST_ILLEGAL_STATE):
+                self.rtype.pop(rid, None)
+                if abi.status_code(e) == abi.CC_ST_OK:  # a failed delete keeps the key and the instances
+                    self.inst = {i: t for i, t in self.inst.items() if t[2] != rid}
+                    self.key_rid = {k: r for k, r in self.key_rid.items() if r != rid}
+            return e
+        raise ValueError(what)
+
+    def close(self, client):
+        closed, ev = self.E.sessions_close([client], capacity=1 << 16)
+        self.O.session_close(client)
+        oe = self.O.take_events()
+        got = sorted(zip(ev["target"].tolist(), ev["code"].tolist(), ev["tag"].tolist(), ev["payload"].tolist()))
+        want = sorted(zip(oe["target"].tolist(), oe["code"].tolist(), oe["tag"].tolist(), oe["payload"].tolist()))
+        assert got == want
+        self.inst = {i: t for i, t in self.inst.items() if t[1] != client}
+
+    def batch(self, rows):
+        """rows: (instance id or None for an unknown session, op, flags, key, a, b, aux) -> checked batch."""
+        n = len(rows)
+        b = Batch(n)
+        for i, (iid, op, fl, key, a, bb, aux) in enumerate(rows):
+            slot = self.E.instance_slot(iid) if iid is not None else -1
+            b.index[i] = self.index
+            self.index += 1
+            b.time[i] = self.index // 4
+            b.inst[i] = slot if slot >= 0 else 1 << 20  # beyond the instance table: unknown session
+            b.op[i], b.flags[i], b.key[i], b.a[i], b.b[i], b.aux[i] = op, fl, key, a, bb, aux & 0xFFFFFFFFFFFFFFFF
+        s, v, ev = self.E.apply_host_events(b, capacity=1 << 14)
+        s2, v2 = self.O.apply(b)
+        bad = np.nonzero((s != s2) | (v != v2))[0]
+        assert len(bad) == 0, [(int(b.op[j]), int(s[j]), int(v[j]), int(s2[j]), int(v2[j])) for j in bad[:5]]
+        oe = self.O.take_events()
+        apos, amem = self.O.take_aux()
+        member = ev["code"] == abi.CC_EV_MEMBER
+        got = sorted(zip(*(ev[k][~member].tolist() for k in ("pos", "src", "target", "code", "tag", "payload"))))
+        want = sorted(zip(*(oe[k].tolist() for k in ("pos", "src", "target", "code", "tag", "payload"))))
+        assert got == want
+        assert list(zip(ev["pos"][member].tolist(), ev["payload"][member].tolist())) == \
+            list(zip(apos.tolist(), amem.tolist()))
+        return s, v
+
+    def check_state(self):
+        E, O = self.E, self.O
+        for rid, t in self.rtype.items():
+            es, os_ = E.resource_slot(rid), O.L.orc_res_slot_of(O.h, rid)
+            assert es >= 0 and os_ >= 0, rid
+            if t == V:
+                assert [int(x[0]) for x in E.value_state(es, 1)] == [int(x[0]) for x in O.value_state(os_, 1)]
+            elif t in (M, S):
+                got, want = E.map_entries(es), O.map_entries(os_)
+                for g, w in zip(got, want):
+                    assert np.array_equal(g, w), rid
+            elif t == L:
+                h, hi, hc, q = E.lock_state(es)
+                oh, ohi, ohc, oq = O.lock_state(os_)
+                assert (h, hc, q) == (oh, ohc, oq) and (h < 0 or hi == ohi)
+            elif t == E_:
+                assert E.election_state(es) == O.election_state(os_)
+            elif t == G:
+                assert E.group_members(es) == O.group_members(os_)
+
+
+def _rand_row(rng, t, iid, members):
+    """One random commit on an instance of type t: (iid, op, flags, key, a, b, aux)."""
+    u = rng.random()
+    small = int(rng.integers(0, 3))
+    fl = abi.cc_flags(LONG if rng.random() < 0.8 else NULL, LONG if rng.random() < 0.8 else NULL, 0)
+    if rng.random() < 0.01:
+        return (iid, abi.CC_OP_DELETE, 0, 0, 0, 0, 0)
+    if t == V:
+        op = [abi.CC_OP_VALUE_GET, abi.CC_OP_VALUE_SET, abi.CC_OP_VALUE_CAS, abi.CC_OP_VALUE_GETANDSET,
+              abi.CC_OP_VALUE_LISTEN, abi.CC_OP_VALUE_UNLISTEN][int(rng.integers(0, 6))]
+        return (iid, op, fl, 0, small, int(rng.integers(0, 3)), 0)
+    if t == M:
+        op = [abi.CC_OP_MAP_PUT, abi.CC_OP_MAP_GET, abi.CC_OP_MAP_REMOVE, abi.CC_OP_MAP_PUTIFABSENT,
+              abi.CC_OP_MAP_CONTAINSKEY, abi.CC_OP_MAP_REPLACE, abi.CC_OP_MAP_SIZE][int(rng.integers(0, 7))]
+        return (iid, op, abi.cc_flags(LONG, NULL, 0), int(rng.integers(0, 6)), small, 0, 0)
+    if t == S:
+        op = [abi.CC_OP_SET_ADD, abi.CC_OP_SET_CONTAINS, abi.CC_OP_SET_REMOVE, abi.CC_OP_SET_SIZE][int(rng.integers(0, 4))]
+        return (iid, op, 0, int(rng.integers(0, 6)), 0, 0, 0)
+    if t == Q:
+        op = [abi.CC_OP_QUEUE_OFFER, abi.CC_OP_QUEUE_POLL, abi.CC_OP_QUEUE_POLL, abi.CC_OP_QUEUE_PEEK,
+              abi.CC_OP_QUEUE_SIZE, abi.CC_OP_QUEUE_CONTAINS][int(rng.integers(0, 6))]
+        return (iid, op, abi.cc_flags(LONG, 0, 0), 0, small, 0, 0)
+    if t == L:
+        if u < 0.5:
+            return (iid, abi.CC_OP_LOCK_UNLOCK, 0, 0, 0, 0, 0)
+        return (iid, abi.CC_OP_LOCK_LOCK, 0, 0, 0, 0, 0 if u < 0.98 else -1)  # few waiters: queue cap 64
+    if t == E_:
+        op = [abi.CC_OP_ELECT_LISTEN, abi.CC_OP_ELECT_UNLISTEN, abi.CC_OP_ELECT_ISLEADER][int(rng.integers(0, 3))]
+        return (iid, op, 0, 0, 0, 0, 0)
+    op = [abi.CC_OP_GROUP_JOIN, abi.CC_OP_GROUP_LEAVE, abi.CC_OP_GROUP_EXECUTE][int(rng.integers(0, 3))]
+    mem = int(rng.choice(members)) if members else 0
+    return (iid, op, abi.cc_flags(abi.CC_TAG_HANDLE, 0, 0) if op == abi.CC_OP_GROUP_EXECUTE else 0, mem, 7, 0, 0)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_manager_random(seed):
+    rng = np.random.default_rng(seed)
+    P = Pair()
+    keys = list(range(100, 124))
+    key_type = {k: TYPES[k % len(TYPES)] for k in keys}
+    clients = [1, 2, 3, 4, 5]
+    for rnd in range(40):
+        for _ in range(int(rng.integers(1, 6))):
+            u = rng.random()
+            k = int(rng.choice(keys))
+            t = key_type[k] if rng.random() < 0.9 else TYPES[int(rng.integers(0, len(TYPES)))]
+            c = int(rng.choice(clients))
+            if u < 0.45:
+                P.control("get", k, t, c)
+            elif u < 0.7:
+                P.control("create", k, t, c)
+            elif u < 0.8:
+                P.control("exists", k)
+            elif u < 0.95 and (P.rtype or P.inst):
+                # by resource id, or (A13) by an instance id as the client would send it
+                pool = list(P.rtype) + list(P.inst)
+                P.control("delete", rid=int(rng.choice(pool)))
+            else:
+                P.close(c)
+        iids = list(P.inst)
+        if not iids:
+            continue
+        rows = []
+        for _ in range(int(rng.integers(1, 120))):
+            iid = int(rng.choice(iids))
+            t, _, rid = P.inst[iid]
+            members = [i for i, x in P.inst.items() if x[2] == rid]
+            rows.append(_rand_row(rng, t, iid, members) if rng.random() > 0.02 else (None, abi.CC_OP_VALUE_GET, 0, 0, 0, 0, 0))
+        P.batch(rows)
+        if rnd % 10 == 9:
+            P.check_state()
+    P.check_state()
+
+
+def test_manager_zombie_after_failed_delete():
+    """LockState.delete cleans the holder commit without nulling it (LockState.java:87-98): a DeleteCommand, then
+    deleteResource -> delete() cleans it again and throws "commit closed"; the resource leaves `resources` but its key
+    and instances stay: commits on the instance are NullPointerException, get of the key is a type mismatch."""
+    P = Pair()
+    st, iid, _ = P.control("get", 500, L, 1)
+    st2, iid2, _ = P.control("get", 500, L, 2)
+    P.batch([(iid, abi.CC_OP_LOCK_LOCK, 0, 0, 0, 0, -1), (iid2, abi.CC_OP_LOCK_LOCK, 0, 0, 0, 0, -1),
+             (iid, abi.CC_OP_DELETE, 0, 0, 0, 0, 0)])
+    assert abi.status_code(P.control("delete", rid=iid)) == abi.CC_ST_ILLEGAL_STATE
+    s, _ = P.batch([(iid, abi.CC_OP_LOCK_UNLOCK, 0, 0, 0, 0, 0), (iid2, abi.CC_OP_LOCK_LOCK, 0, 0, 0, 0, 0)])
+    assert [abi.status_code(x) for x in s] == [abi.CC_ST_NULL_POINTER] * 2
+    assert abi.status_code(P.control("get", 500, L, 3)[0]) == abi.CC_ST_TYPE_MISMATCH
+    P.control("exists", 500)
+    assert P.E.resource_exists(500)
+    P.close(1)
+    s, _ = P.batch([(iid, abi.CC_OP_LOCK_UNLOCK, 0, 0, 0, 0, 0), (iid2, abi.CC_OP_LOCK_UNLOCK, 0, 0, 0, 0, 0)])
+    assert [abi.status_code(x) for x in s] == [abi.CC_ST_UNKNOWN_SESSION, abi.CC_ST_NULL_POINTER]
+    assert abi.status_code(P.control("delete", rid=iid)) == abi.CC_ST_UNKNOWN_RESOURCE
+
+
+def test_manager_state_survives_snapshot():
+    """Keys, resource ids, per-client instances and zombies travel in cc_snapshot_save; a restored engine answers
+    get/create/delete exactly as the original would."""
+    from copycat_amd.engine import Engine
+
+    rng = np.random.default_rng(9)
+    P = Pair()
+    for k in range(10):
+        P.control("get", 200 + k, TYPES[k % len(TYPES)], 1 + k % 3)
+        P.control("create", 200 + k, TYPES[k % len(TYPES)], 2)
+    rows = []
+    for iid, (t, _, rid) in P.inst.items():
+        members = [i for i, x in P.inst.items() if x[2] == rid]
+        rows += [_rand_row(rng, t, iid, members) for _ in range(5)]
+    P.batch(rows)
+    snap = P.E.snapshot()
+    fresh = Engine(64, 256, 1 << 14, flags=FLAGS, map_capacity=4096, max_events=1 << 16)
+    fresh.restore(snap)
+    P.E = fresh
+    for k in range(12):
+        P.control("get", 200 + k, TYPES[k % len(TYPES)], 1 + k % 4)
+    P.control("delete", rid=next(iter(P.rtype)))
+    P.check_state()

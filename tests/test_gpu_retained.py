@@ -61,3 +61,78 @@ def test_value_retained_resource_delete():
     slot = int(np.nonzero(live)[0][0])
     E.resource_delete(slot)
     assert E.value_retained()[slot] == 0
+
+
+def _value_engine(R, flags, n=1 << 16):
+    from copycat_amd.engine import Engine
+
+    E = Engine(R, R + 8, n, flags=flags)
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E.instance_open_range(0, R, 0, 1000, 7)
+    return E
+
+
+def test_retained_batch_without_index_is_rejected_before_any_work():
+    """CC_CFG_VALUE_RETAINED needs the index column: the call fails before any kernel runs, so device state, the
+    applied watermark and the retained commits are untouched and a retry with the column applies the batch once."""
+    import torch
+
+    from copycat_amd.engine import DeviceBatch, EngineError
+    from copycat_amd.workload import value_random_stream
+    from oracle.oracle_py import Oracle
+
+    R = 128
+    E = _value_engine(R, abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_RETAINED)
+    b = value_random_stream(4000, R, R + 8, seed=31)
+    db = DeviceBatch.upload(b, device="cuda", columns=("inst", "op", "flags", "a", "b"))
+    st = torch.zeros(len(b), dtype=torch.uint8, device="cuda")
+    va = torch.zeros(len(b), dtype=torch.int64, device="cuda")
+    with pytest.raises(EngineError) as ei:
+        E.apply(db, st, va)
+    assert ei.value.rc == abi.CC_ERR_INVALID
+    tag, val, cur = E.value_state()
+    assert not tag.any() and not cur.any() and not E.value_retained().any() and E.applied_index() == 0
+    O = Oracle(R, R + 8)
+    for r in range(R):
+        O.resource_create(r, abi.CC_RES_VALUE)
+        O.instance_open(r, r, 1000 + r, 7)
+    s, v = E.apply_host(b)
+    s2, v2 = O.apply(b)
+    assert np.array_equal(s, s2) and np.array_equal(v, v2)
+    assert np.array_equal(E.value_retained(), O.value_retained())
+
+
+def test_retained_snapshot_roundtrip_and_config_check():
+    """The retained-commit section travels in the snapshot (SnapHdr flag), and a snapshot restores only into an engine
+    with the same CC_CFG_VALUE_RETAINED setting, rejected before anything is copied."""
+    from copycat_amd.engine import EngineError
+    from copycat_amd.workload import value_random_stream
+    from oracle.oracle_py import Oracle
+
+    R = 256
+    flags = abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_RETAINED
+    b = value_random_stream(20_000, R, R + 8, seed=33)
+    E = _value_engine(R, flags)
+    O = Oracle(R, R + 8)
+    for r in range(R):
+        O.resource_create(r, abi.CC_RES_VALUE)
+        O.instance_open(r, r, 1000 + r, 7)
+    E.apply_host(b.slice(0, 10_000))
+    O.apply(b.slice(0, 10_000))
+    snap = E.snapshot()
+    F = _value_engine(R, flags)
+    F.restore(snap)
+    assert np.array_equal(F.value_retained(), O.value_retained())
+    s, v = F.apply_host(b.slice(10_000, 20_000))
+    s2, v2 = O.apply(b.slice(10_000, 20_000))
+    assert np.array_equal(s, s2) and np.array_equal(v, v2)
+    assert np.array_equal(F.value_retained(), O.value_retained())
+    plain = _value_engine(R, abi.CC_CFG_TIMERS_DEFERRED)
+    before = plain.value_state()
+    with pytest.raises(EngineError) as ei:
+        plain.restore(snap)
+    assert ei.value.rc == abi.CC_ERR_INVALID
+    for x, y in zip(before, plain.value_state()):
+        assert np.array_equal(x, y)
+    with pytest.raises(EngineError):
+        _value_engine(R, flags).restore(plain.snapshot())
