@@ -3,18 +3,30 @@
 
 Default workload (BASELINE.json configs[1]): a DistributedAtomicLong client-model stream —
 Get(50) + CompareAndSet(52) of java.lang.Long values, ~10% stale CASes — of 100M committed entries over
-65,536 AtomicValueState resources per GPU.  A "step" = one cc_apply_batch over the whole 100M-entry batch
-with its columns already resident in HBM (state carries over from step to step, as a replica's would).
+65,536 AtomicValueState resources per GPU.  A "step" = one cc_apply_batch over one 100M-entry batch with its
+columns already resident in HBM.  Every step applies its OWN batch: the client model continues from the values the
+previous steps left (copycat_amd.workload.AtomicLongClients), so every timed step holds the stated ~10% stale CASes
+(the per-step CAS success share is reported), and the results of every step stay in HBM.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): resources shard by id (rank r owns global ids
-r, r+N, ...; weak scaling: every rank applies its own 100M-entry stream over its own 65,536 resources);
-after every batch the applied-index watermark is all-gathered over RCCL — the only
-cross-GPU exchange on this path.
+Parity at full size: the oracle applies step 0's 100M rows on the host (this is also the timed CPU baseline); the
+GPU's step-0 status/value columns and its value state after step 0 must match bit for bit ("parity" in the JSON
+line; any mismatch exits non-zero).
+
+Multi-GPU (`--gpus N`): without WORLD_SIZE in the environment bench.py starts N ranks itself
+(torch.distributed.run, one process per GPU, RCCL) before touching any GPU.  Rank r applies its share of ONE global
+log: the global resources r, r+N, ... (weak scaling: 100M rows over 65,536 resources per rank per step), rows
+carrying the global log indices (copycat_amd.workload.AtomicLongClients, copycat_amd.shard).  After every batch each
+rank writes its applied watermark into HBM (cc_applied_index_async) and the watermarks are all-gathered over RCCL
+(SURVEY §8(e)); c4/c5 also all-gather (OR) the session-expiry bitmap.  Nothing else crosses GPUs.
 
 roofline: per-kernel device time from HIP events recorded on the launch stream over the timed region
-(cc_profile_*), dominant kernel, algorithmic bytes = 39 B/commit x commits per launch.
-cpu_baseline: the oracle (C++ restatement of the Java apply path, single thread) timed on this host
-over a bounded prefix of the same stream (rank 0, N=1 only).
+(cc_profile_*).  The 39 algorithmic bytes per commit are split over the kernels that move
+them: the 30 input bytes to k_part_tile (which reads the input columns), the 9 result bytes to k_unpermute (which
+writes the result columns); `frac` is the dominant kernel's share over its own launch time, `pipeline_frac` all 39
+bytes over the whole step.
+cpu_baseline: the oracle (C++ restatement of the Java apply path, single thread, as the reference's single
+state-machine thread) over step 0's rows (rank 0, N=1 only); cpu_baseline_all_cores: the same rows sharded by
+resource over the box's CPU share, one oracle per thread.
 
 --workload c3 (BASELINE.json configs[2]): DistributedMap put/get/remove 45/45/10 over 1,048,576 (map, key)
 pairs in 4,096 MapState resources, pair rank ~ Zipf(0.99), 1e9 committed entries per step (generated block by
@@ -33,6 +45,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -116,6 +130,8 @@ def run_c4(args, dev, rank, world, dist):
     d_match, d_ts, d_ci, d_last = dev_u64(match), dev_u64(ts), dev_u64(ci), dev_u64(last)
     d_out = torch.zeros(G, dtype=torch.int64, device=dev)
     d_bm = torch.zeros((S + 63) // 64, dtype=torch.int64, device=dev)
+    # rank r sweeps the global sessions [r*S, (r+1)*S): the all-gather concatenates the global expired bitmap
+    bm_all = torch.zeros(world * d_bm.numel(), dtype=torch.int64, device=dev)
     d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
@@ -131,6 +147,8 @@ def run_c4(args, dev, rank, world, dist):
         expire_sweep(d_last, now, timeout, d_bm, d_cnt, stream=stream)
         if k is not None:
             ev[k][2].record(stream)
+        if dist is not None:  # the expired-session bitmap exchange (RCCL all-gather over xGMI)
+            dist.all_gather_into_tensor(bm_all, d_bm)
 
     for _ in range(args.warmup):
         step()
@@ -214,12 +232,26 @@ def run_c5(args, dev, rank, world, dist):
     E.instance_open_range(0, R, 0, 1000, 1 + rank)
     stream = torch.cuda.current_stream(dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
-    wm_local = db.cols["index"][n - 1:n].view(torch.int64)
+    wm_local = torch.zeros(1, dtype=torch.int64, device=dev)
+    # session / lease expiry after each batch: 65,536 client sessions, rank r sweeps the global
+    # sessions [r*S/world, (r+1)*S/world); the all-gather of the per-rank bitmaps is the global expired set
+    from copycat_amd.engine import expire_sweep
+
+    S_local = max(64, (65536 // world) // 64 * 64)
+    rng = np.random.default_rng(0xA700000 + 55 + rank)
+    now_s, timeout_s = 10_000_000, 5000
+    d_last = torch.from_numpy((now_s - rng.integers(0, 2 * timeout_s, S_local)).astype(np.int64)).to(dev)
+    d_bm = torch.zeros(S_local // 64, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    bm_all = torch.zeros(world * (S_local // 64), dtype=torch.int64, device=dev)
 
     def step():
         E.apply_events(db, status, value, evs, stream=stream)
-        if dist is not None:
+        E.applied_index_async(wm_local, stream=stream)
+        expire_sweep(d_last, now_s, timeout_s, d_bm, d_cnt, stream=stream)
+        if dist is not None:  # watermark, then expired-session bitmap (RCCL all-gathers over xGMI)
             dist.all_gather_into_tensor(wm_all, wm_local)
+            dist.all_gather_into_tensor(bm_all, d_bm)
 
     for _ in range(args.warmup):
         step()
@@ -282,7 +314,10 @@ def run_c5(args, dev, rank, world, dist):
             "config": {"workload": f"c5: mixed coordination (lock / election / group, a third each) over {R:,} resources, "
                                    f"{n:,} committed entries per GPU with the ordered event stream",
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
-                       "events_per_step": n_events, "gen_s": round(t_gen, 2)},
+                       "events_per_step": n_events, "gen_s": round(t_gen, 2),
+                       "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())],
+                       "expired_sessions_per_step": int(np.unpackbits(
+                           (bm_all if dist is not None else d_bm).cpu().numpy().view(np.uint8)).sum())},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -290,75 +325,273 @@ def run_c5(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2")
-    ap.add_argument("--commits", type=int, default=0, help="default: 100M (c2), 1e9 (c3)")
-    ap.add_argument("--resources", type=int, default=0, help="default: 65536 resources (c2), 4096 maps (c3)")
-    ap.add_argument("--pairs", type=int, default=1 << 20, help="c3: distinct (map, key) pairs")
-    ap.add_argument("--zipf", type=float, default=0.99, help="c3: Zipf exponent of the pair rank (0 = uniform)")
-    ap.add_argument("--sub-batch", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=0, help="default: 100M (c2), 20M (c3)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--retained", action="store_true", help="c2: also keep the retained value commit per slot (CC_CFG_VALUE_RETAINED)")
-    args = ap.parse_args()
+def cpu_threads():
+    """The box's CPU share for host work (the GPU box exposes far more CPUs than one GPU's share of 16)."""
+    return max(1, min(16, os.cpu_count() or 1))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+def cpu_all_cores(batch, R, rtype, threads, flags=None):
+    """The same rows sharded by resource over `threads` threads, one oracle (C++ restatement) per thread; ctypes
+    releases the GIL inside each apply.  Returns (ops/s, threads)."""
+    from concurrent.futures import ThreadPoolExecutor
 
     from copycat_amd import abi
+    from oracle.oracle_py import Oracle
+
+    own = (batch.inst % threads).astype(np.uint8)
+    order = np.argsort(own, kind="stable")
+    cuts = np.searchsorted(own[order], np.arange(threads + 1))
+    parts = []
+    for t in range(threads):
+        rows = order[cuts[t]:cuts[t + 1]]
+        sub = type(batch)(0)
+        for name in type(batch).__slots__:
+            setattr(sub, name, np.ascontiguousarray(getattr(batch, name)[rows]))
+        parts.append(sub)
+    oracles = []
+    for t in range(threads):
+        O = Oracle(R, R) if flags is None else Oracle(R, R, flags)
+        for r in range(t, R, threads):
+            O.resource_create(r, int(rtype[r]) if hasattr(rtype, "__len__") else rtype)
+            O.instance_open(r, r, 1000 + r, 1)
+        oracles.append(O)
+    with ThreadPoolExecutor(threads) as ex:
+        tc = time.perf_counter()
+        list(ex.map(lambda t: oracles[t].apply(parts[t]), range(threads)))
+        tc = time.perf_counter() - tc
+    return len(batch) / tc, threads
+
+
+def run_c2(args, dev, rank, world, dist):
+    """Config 2 (the headline): per-step client-model streams, full-size parity on step 0, CAS success shares."""
+    from copycat_amd import abi
+    from copycat_amd.batch import Batch
     from copycat_amd.engine import DeviceBatch, Engine
-    from copycat_amd.workload import SEED_C2, atomic_long_stream
+    from copycat_amd.workload import SEED_C2, AtomicLongClients
 
-    if args.workload == "c4":
-        return run_c4(args, dev, rank, world, dist)
-    if args.workload == "c5":
-        return run_c5(args, dev, rank, world, dist)
-
-    c3 = args.workload == "c3"
-    n = args.commits or (1_000_000_000 if c3 else 100_000_000)
-    R = args.resources or (4096 if c3 else 65536)
-    cpu_sample = args.cpu_sample or (20_000_000 if c3 else 100_000_000)
-    B_OP = B_OP_C3 if c3 else B_OP_C2
+    n = args.commits or 100_000_000
+    R = args.resources or 65536
+    cols = ("index", "inst", "op", "flags", "a", "b")
+    total_steps = args.warmup + args.steps
+    per_stream = n * (30 + 9)  # device bytes per step: columns + results
+    nstreams = max(1, min(total_steps, int(args.hbm_budget_gb * 1e9 // per_stream)))
     t_gen = time.time()
-    if c3:
-        batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample))
-    else:
-        batch = atomic_long_stream(n, resources=R, seed=SEED_C2 + rank, index0=1)
-        db = DeviceBatch.upload(batch, device=dev, columns=("index", "inst", "op", "flags", "a", "b"))
+    clients = AtomicLongClients(resources=R, seed=SEED_C2, rank=rank, world=world, threads=cpu_threads())
+    host = Batch(n)
+    streams, results = [], []
+    parity_ref = None
+    cpu = cpu_all = None
+    E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch,
+               flags=abi.CC_CFG_TIMERS_DEFERRED | (abi.CC_CFG_VALUE_RETAINED if args.retained else 0))
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    # local slot k = global resource rank + world*k; its instance id = that global id + 1
+    E.instance_open_range(0, R, 0, 1 + rank, 1 + rank)
+    for k in range(nstreams):
+        clients.next(n, out=host)
+        if k == 0 and rank == 0 and not args.no_parity:
+            from oracle.oracle_py import Oracle
+
+            O = Oracle(R, R)
+            for r in range(R):
+                O.resource_create(r, abi.CC_RES_VALUE)
+                O.instance_open(r, r, 1 + r, 1)
+            tc = time.perf_counter()
+            s_ref, v_ref = O.apply(host)  # step 0's rows from the fresh state: the parity reference
+            tc = time.perf_counter() - tc
+            parity_ref = (s_ref, v_ref, O.value_state())
+            if world == 1 and not args.no_cpu_baseline:
+                cpu = {"value": round(n / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+                       "sample": f"step 0's {n:,} commits of the same c2 stream (the parity reference), C++ restatement "
+                                 f"of the Java apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+                v_all, thr = cpu_all_cores(host, R, abi.CC_RES_VALUE, cpu_threads())
+                cpu_all = {"value": round(v_all, 1), "unit": "ops/s", "cores": thr, "kind": "port",
+                           "sample": f"the same {n:,} commits sharded by resource (slot % {thr}) over {thr} threads, "
+                                     f"one oracle each, {cpu_model()}"}
+            del O
+        streams.append(DeviceBatch.upload(host, device=dev, columns=cols))
+        results.append((torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.int64, device=dev)))
+    del host
+    t_gen = time.time() - t_gen
+    stream = torch.cuda.current_stream(dev)
+    wm_local = torch.zeros(1, dtype=torch.int64, device=dev)
+    wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
+
+    def step(k):
+        st, va = results[k % nstreams]
+        E.apply(streams[k % nstreams], st, va, stream=stream)
+        E.applied_index_async(wm_local, stream=stream)
+        if dist is not None:  # applied-index watermark exchange (RCCL all-gather over xGMI)
+            dist.all_gather_into_tensor(wm_all, wm_local)
+
+    state0 = None
+    for k in range(args.warmup):
+        step(k)
+        if k == 0:
+            torch.cuda.synchronize(dev)
+            state0 = E.value_state()  # the GPU's state after step 0 (parity vs the oracle's)
+    torch.cuda.synchronize(dev)
+    if not args.no_profile:
+        E.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total_steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    E.sync()  # surfaces device-side errors
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = E.profile_read() if not args.no_profile else {}
+
+    # watermarks: every rank's last applied global log index, as all-gathered after the last step; stream k of rank r
+    # holds the global indices k*n*world + 1 + r + i*world
+    watermarks = wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]
+    k_last = (total_steps - 1) % nstreams
+    wm_expect = [k_last * n * world + 1 + (n - 1) * world + r for r in range(world)]
+    if watermarks != wm_expect:
+        sys.stderr.write(f"watermark mismatch: all-gathered {watermarks}, expected {wm_expect}\n")
+        sys.exit(4)
+    # CAS success share of every timed step (the stated ~0.9 of the client model)
+    shares = []
+    for k in range(args.warmup, total_steps):
+        db, (st, va) = streams[k % nstreams], results[k % nstreams]
+        cas = db.cols["op"] == abi.CC_OP_VALUE_CAS
+        shares.append(float(((va == 1) & cas).sum().item()) / max(1, int(cas.sum().item())))
+    parity = None
+    if parity_ref is not None:
+        s_ref, v_ref, st_ref = parity_ref
+        st0, va0 = results[0]
+        s_gpu = st0.cpu().numpy()
+        v_gpu = va0.cpu().numpy().view(np.uint64)
+        mism = int(np.count_nonzero((s_gpu != s_ref) | (v_gpu != v_ref)))
+        smism = None
+        if state0 is not None:
+            smism = int(sum(np.count_nonzero(a != b) for a, b in zip(state0, st_ref)))
+        parity = {"rows": n, "mismatches": mism, "state_slots": R, "state_mismatches": smism,
+                  "checked": "step 0: per-commit status+value and the value state after it, GPU vs oracle/oracle.cpp"}
+    ms_per_step = elapsed * 1e3 / args.steps
+    roofline = roofline_split(prof, n, args.steps, ms_per_step)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": ("c2: DistributedAtomicLong Get/CompareAndSet client-model stream, "
+                                    f"{n:,} committed entries per step over {R:,} AtomicValueState resources per GPU, "
+                                    "a new client-model batch every step"),
+                       "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
+                       "sub_batch": args.sub_batch or "default(16M)", "resident_streams": nstreams,
+                       "cas_success_share": {"min": round(min(shares), 4), "mean": round(sum(shares) / len(shares), 4)},
+                       "watermarks": watermarks, "gen_s": round(t_gen, 2)},
+            "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all,
+        }
+        if args.e2e:
+            out["end_to_end"] = end_to_end_c2(E, clients, n, dev)
+        print(json.dumps(out), flush=True)
+    bad = parity is not None and (parity["mismatches"] or parity["state_mismatches"])
+    if dist is not None:
+        dist.destroy_process_group()
+    if bad:
+        sys.stderr.write(f"PARITY FAILURE: {parity}\n")
+        sys.exit(3)
+
+
+def end_to_end_c2(E, clients, n, dev):
+    """One more client-model step through the PCIe: pinned host columns -> H2D -> apply -> D2H results, synced."""
+    from copycat_amd.batch import Batch
+    from copycat_amd.engine import DeviceBatch
+
+    host = clients.next(n, out=Batch(n))
+    names = ("index", "inst", "op", "flags", "a", "b")
+    tdt = {"index": torch.int64, "inst": torch.int32, "op": torch.uint8, "flags": torch.uint8, "a": torch.int64,
+           "b": torch.int64}
+    pinned = {k: torch.from_numpy(getattr(host, k).view(np.dtype(str(tdt[k]).replace("torch.", "")))).pin_memory()
+              for k in names}
+    dcols = {k: torch.empty(n, dtype=tdt[k], device=dev) for k in names}
+    st, va = torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev)
+    hs, hv = torch.empty(n, dtype=torch.uint8).pin_memory(), torch.empty(n, dtype=torch.int64).pin_memory()
+    torch.cuda.synchronize(dev)
+    cs = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t0 = time.perf_counter()
+    ev[0].record(cs)
+    for k in names:
+        dcols[k].copy_(pinned[k], non_blocking=True)
+    ev[1].record(cs)
+    E.apply(DeviceBatch(dcols, n), st, va, stream=cs)
+    ev[2].record(cs)
+    hs.copy_(st, non_blocking=True)
+    hv.copy_(va, non_blocking=True)
+    ev[3].record(cs)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    h2d, app, d2h = (ev[i].elapsed_time(ev[i + 1]) for i in range(3))
+    return {"value": round(n / dt, 1), "unit": "ops/s", "ms": round(dt * 1e3, 3),
+            "ms_h2d": round(h2d, 3), "ms_apply": round(app, 3), "ms_d2h": round(d2h, 3),
+            "pcie_gbps": round((30 + 9) * n / ((h2d + d2h) * 1e-3) / 1e9, 1),
+            "path": "pinned host columns (30 B/commit) H2D + cc_apply_batch + D2H of status/value (9 B/commit), "
+                    "one synced step, PCIe-inclusive"}
+
+
+def roofline_split(prof, n, steps, ms_per_step):
+    """c2 roofline: the 39 algorithmic bytes per commit split over the kernels that move them (30 input bytes read by
+    k_part_tile, 9 result bytes written by k_unpermute); the dominant kernel's share over its own launch time."""
+    if not prof:
+        return None
+    share = {"k_part_tile": 30.0, "k_unpermute": 9.0}
+    dom = max(prof, key=lambda k: prof[k][0])
+    ms_tot, launches = prof[dom]
+    commits_per_launch = n * steps / max(launches, 1)
+    avg_ms = ms_tot / max(launches, 1)
+    b = share.get(dom, 0.0)
+    achieved = b * commits_per_launch / (avg_ms * 1e-3) / 1e9
+    per_kernel = {}
+    for k, (ms, nl) in prof.items():
+        if nl and k in share:
+            per_kernel[k] = round(share[k] * n * steps / (ms * 1e-3) / 1e9, 1)
+    return {
+        "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c2"),
+        "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
+        "alg_bytes_per_commit": {"total": B_OP_C2, **share, "k_apply_value": 0.0},
+        "alg_gb_per_launch": round(b * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
+        "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
+        "per_kernel_alg_gbps": per_kernel,
+        "pipeline_achieved_gbps": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9, 1),
+        "pipeline_frac": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+    }
+
+
+def run_c3(args, dev, rank, world, dist):
+    """Config 3: DistributedMap Zipf stream (1e9 rows, generated block by block and uploaded once)."""
+    from copycat_amd import abi
+    from copycat_amd.engine import Engine
+
+    n = args.commits or 1_000_000_000
+    R = args.resources or 4096
+    cpu_sample = args.cpu_sample or 20_000_000
+    t_gen = time.time()
+    batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample))
     t_gen = time.time() - t_gen
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     value = torch.zeros(n, dtype=torch.int64, device=dev)
-
-    if c3:
-        E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, map_capacity=args.pairs)
-        E.resource_create_range(0, R, abi.CC_RES_MAP)
-    else:
-        E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch,
-                   flags=abi.CC_CFG_TIMERS_DEFERRED | (abi.CC_CFG_VALUE_RETAINED if args.retained else 0))
-        E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, map_capacity=args.pairs)
+    E.resource_create_range(0, R, abi.CC_RES_MAP)
     E.instance_open_range(0, R, 0, 1 + rank, 1 + rank)
     stream = torch.cuda.current_stream(dev)
+    wm_local = torch.zeros(1, dtype=torch.int64, device=dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
-    wm_local = db.cols["index"][n - 1:n].view(torch.int64)
 
     def step():
         E.apply(db, status, value, stream=stream)
-        if dist is not None:  # applied-index watermark exchange (RCCL all-gather over xGMI)
+        E.applied_index_async(wm_local, stream=stream)
+        if dist is not None:
             dist.all_gather_into_tensor(wm_all, wm_local)
 
     for _ in range(args.warmup):
@@ -376,77 +609,130 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    E.sync()  # surfaces device-side errors
+    E.sync()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
     prof = E.profile_read() if not args.no_profile else {}
-    # sanity: the result columns are the real per-commit results (spot-check CAS success share on rank 0)
-    st_h = status[: min(n, 1_000_000)].cpu().numpy()
-    ok_share = float(np.mean(abi.status_code(st_h) == abi.CC_ST_OK))
-
-    total_commits = n * args.steps * world
-    value_ops = total_commits / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-
     roofline = None
     if prof:
         dom = max(prof, key=lambda k: prof[k][0])
         ms_tot, launches = prof[dom]
         commits_per_launch = n * args.steps / max(launches, 1)
         avg_ms = ms_tot / max(launches, 1)
-        achieved = B_OP * commits_per_launch / (avg_ms * 1e-3) / 1e9
+        achieved = B_OP_C3 * commits_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, args.workload),
-            "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
-            "alg_gb_per_launch": round(B_OP * commits_per_launch / 1e9, 4),
-            "avg_launch_ms": round(avg_ms, 4), "launches": launches,
-            "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
-            "bytes_per_commit": B_OP,
-            "pipeline_achieved_gbps": round(B_OP * n / (ms_per_step * 1e-3) / 1e9, 1),
-            "pipeline_frac": round(B_OP * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c3"),
+            "alg_gb_per_launch": round(B_OP_C3 * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
+            "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
+            "bytes_per_commit": B_OP_C3,
+            "pipeline_frac": round(B_OP_C3 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         }
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle_py import Oracle
 
         m = min(n, cpu_sample)
-        sample = batch.slice(0, m)
         O = Oracle(R, R)
         for r in range(R):
-            O.resource_create(r, abi.CC_RES_MAP if c3 else abi.CC_RES_VALUE)
+            O.resource_create(r, abi.CC_RES_MAP)
             O.instance_open(r, r, 1 + r, 1)
         tc = time.perf_counter()
-        O.apply(sample)
+        O.apply(batch.slice(0, m))
         tc = time.perf_counter() - tc
         cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
-               "sample": f"first {m:,} commits of the same {args.workload} stream, C++ restatement of the Java apply "
-                         f"path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
-
-    if c3:
-        wl = (f"c3: DistributedMap put/get/remove 45/45/10, Zipf({args.zipf}) over {args.pairs:,} (map, key) pairs in "
-              f"{R:,} MapState resources, {n:,} committed entries per GPU")
-    else:
-        wl = ("c2: DistributedAtomicLong Get/CompareAndSet client-model stream, "
-              f"{n:,} committed entries over {R:,} AtomicValueState resources per GPU")
+               "sample": f"first {m:,} commits of the same c3 stream, C++ restatement of the Java apply path "
+                         f"(oracle/oracle.cpp), 1 thread, {cpu_model()}"}
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value_ops, 1), "unit": "ops/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": wl,
+            "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": (f"c3: DistributedMap put/get/remove 45/45/10, Zipf({args.zipf}) over {args.pairs:,} "
+                                    f"(map, key) pairs in {R:,} MapState resources, {n:,} committed entries per GPU"),
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
-                       "sub_batch": args.sub_batch or "default(16M)", "ok_status_share": round(ok_share, 4),
-                       "gen_s": round(t_gen, 2)},
+                       "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),
+                       "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without WORLD_SIZE: start N ranks (torch.distributed.run, one process per GPU) as a child
+    process, before anything touches a GPU, and return its exit code; None when this process is already a rank or
+    runs alone."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    visible = torch.cuda.device_count()  # counts devices without initialising the GPU on this image
+    if visible < args.gpus:
+        sys.stderr.write(f"bench.py --gpus {args.gpus}: only {visible} GPU(s) visible on this node; "
+                         f"one rank per GPU is required\n")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2")
+    ap.add_argument("--commits", type=int, default=0, help="default: 100M (c2, c5), 1e9 (c3)")
+    ap.add_argument("--resources", type=int, default=0, help="default: 65536 resources (c2), 4096 maps (c3)")
+    ap.add_argument("--pairs", type=int, default=1 << 20, help="c3: distinct (map, key) pairs")
+    ap.add_argument("--zipf", type=float, default=0.99, help="c3: Zipf exponent of the pair rank (0 = uniform)")
+    ap.add_argument("--sub-batch", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=0, help="c3: 20M, c5: 10M (c2 uses step 0's rows)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="c2: skip the full-size oracle parity check of step 0")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="c2: also time one PCIe-inclusive step (pinned H2D + apply + D2H)")
+    ap.add_argument("--hbm-budget-gb", type=float, default=200.0,
+                    help="c2: HBM for resident per-step batches (more steps than fit replay the resident ones)")
+    ap.add_argument("--retained", action="store_true", help="c2: also keep the retained value commit per slot (CC_CFG_VALUE_RETAINED)")
+    args = ap.parse_args()
+
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}\n")
+        sys.exit(2)
+    if not torch.cuda.is_available():
+        sys.stderr.write("bench.py: no GPU visible (the engine runs on MI355X only)\n")
+        sys.exit(2)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    run = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload]
+    return run(args, dev, rank, world, dist)
 
 
 if __name__ == "__main__":

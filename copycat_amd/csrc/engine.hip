@@ -239,6 +239,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if ((he = hipMemset(e->d_err, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_sb_kind, 0, e->sb)) != hipSuccess) return fail("memset", he);
   if ((he = hipMemset(e->d_clock, 0, sizeof(uint64_t))) != hipSuccess) return fail("memset", he);
+  if ((he = hipMemset(e->d_last_index, 0, sizeof(uint64_t))) != hipSuccess) return fail("memset", he);
   e->sb_kind.assign(e->sb, 0);
   if (e->map_bits) {  // word 0 = empty entry
     if ((he = hipMemset(e->d_tbl_word, 0, sizeof(uint32_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
@@ -921,6 +922,17 @@ done:
   return rc;
 }
 
+extern "C" int cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* stream) {
+  if (!e || !d_out) return set_err(CC_ERR_INVALID, "null argument");
+  HIPCHECK(hipSetDevice(e->device));
+  hipStream_t st = stream ? (hipStream_t)stream : e->own_stream;
+  if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
+  e->last_stream = st;
+  // the device copy of the last batch's last index (kept up to date stream-ordered by cc_apply_batch)
+  HIPCHECK(hipMemcpyAsync(d_out, e->d_last_index, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  return CC_OK;
+}
+
 extern "C" int cc_applied_index(cc_engine* e, uint64_t* out) {
   if (!e || !out) return CC_ERR_INVALID;
   int rc = cc_sync(e);
@@ -1450,6 +1462,7 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   }
   e->applied = h.applied;
   e->applied_pending = false;
+  HIPCHECK(hipMemcpy(e->d_last_index, &e->applied, sizeof(uint64_t), hipMemcpyHostToDevice));
   e->has_sets = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_SET) != e->res_type.end();
   e->sess_next = h.sess_next;
   e->sess_cap = h.sess_cap;

@@ -82,6 +82,140 @@ uint64_t wl_atomic_long(uint64_t n, uint32_t resources, uint32_t first_inst, uin
   return i;
 }
 
+// Config 2 stream, one bench step of a run: the same client model as wl_atomic_long, continued from the model
+// state (state_tag/state_val per resource: the value every client's CAS expects, updated in place to the state after
+// the n emitted rows), generated on `threads` threads with the same rows for any thread count.
+// Every add ends with a CAS that succeeds, so the value an add's CASes expect is the resource's value before the
+// step plus the deltas of the earlier adds on it (a per-resource prefix sum):
+//   pass 1 (parallel over chunks of adds): add k draws (resource, delta, kind, stale offset) from a counter-based
+//           generator keyed by (seed, k); rows per chunk (fresh 1, cold 2, stale 3 rows per add); per-chunk
+//           per-resource delta sums;
+//   pass 2 (parallel over resources): the model state at the start of every chunk (exclusive prefix over chunks);
+//   pass 3 (parallel over chunks): walk the chunk's adds from that state and write its rows contiguously.
+// Row i gets log index index0 + i * index_stride (a rank's share of one global log: stride = world size) and log time
+// index / 1024.  Only emitted rows change the model (an add cut off at row n leaves the rest unapplied).
+uint64_t wl_atomic_long_step(uint64_t n, uint32_t resources, uint32_t first_inst, uint64_t seed, uint32_t p_cold_ppm,
+                             uint32_t p_stale_ppm, uint64_t index0, uint64_t index_stride, uint8_t* state_tag,
+                             int64_t* state_val, uint32_t threads, uint64_t* index, uint64_t* time, uint32_t* inst,
+                             uint8_t* op, uint8_t* flags, uint64_t* a, uint64_t* b) {
+  if (!resources || !n) return 0;
+  const uint32_t T = std::max<uint32_t>(1, threads);
+  const uint64_t R = resources;
+  struct Add { uint32_t r; int16_t delta; uint8_t kind; uint16_t stale; };  // kind: 0 fresh, 1 cold, 2 stale
+  auto draw = [&](uint64_t k) {
+    SplitMix64 g(seed ^ (k * 0xD1B54A32D192ED03ull) ^ 0x5DEECE66Dull);
+    Add x;
+    x.r = (uint32_t)g.below(resources);
+    x.delta = (int16_t)((int64_t)g.below(2001) - 1000);
+    const uint64_t u = g.below(1000000);
+    x.kind = u < p_stale_ppm ? 2 : (u < (uint64_t)p_stale_ppm + p_cold_ppm ? 1 : 0);
+    x.stale = (uint16_t)g.below(1000);
+    return x;
+  };
+  auto run = [&](auto&& fn, uint64_t count) {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < T; ++t) th.emplace_back([&, t] { for (uint64_t c = t; c < count; c += T) fn(c); });
+    for (auto& x : th) x.join();
+  };
+  // chunks: enough adds for n rows (every add emits at least one row; ~1.4 on average)
+  constexpr uint64_t kChunk = 1 << 20;
+  const double rows_per_add = 1.0 + (p_cold_ppm + 2.0 * p_stale_ppm) / 1e6;
+  uint64_t chunks = (uint64_t)((double)n / rows_per_add / kChunk) + 2;
+  std::vector<Add> adds;
+  std::vector<uint64_t> crow;
+  std::vector<int64_t> dsum;   // [chunks][R] per-chunk delta sums
+  std::vector<uint8_t> seen;   // [chunks][R]
+  for (uint64_t have = 0;;) {  // (re)draw with more chunks if the estimate fell short
+    adds.resize(chunks * kChunk);
+    crow.assign(chunks + 1, 0);
+    dsum.assign(chunks * R, 0);
+    seen.assign(chunks * R, 0);
+    run([&](uint64_t c) {
+      uint64_t rows = 0;
+      int64_t* ds = dsum.data() + c * R;
+      uint8_t* sn = seen.data() + c * R;
+      for (uint64_t k = c * kChunk; k < (c + 1) * kChunk; ++k) {
+        const Add x = adds[k] = draw(k);
+        rows += 1 + x.kind;
+        ds[x.r] = (int64_t)((uint64_t)ds[x.r] + (uint64_t)(int64_t)x.delta);
+        sn[x.r] = 1;
+      }
+      crow[c + 1] = rows;
+    }, chunks);
+    for (uint64_t c = 0; c < chunks; ++c) crow[c + 1] += crow[c];
+    if (crow[chunks] >= n) break;
+    have = chunks;
+    chunks = have * 2;
+  }
+  // pass 2: model state at the start of every chunk (in place: dsum/seen of chunk c become the prefix before c)
+  std::vector<uint8_t> tag0(state_tag, state_tag + R);
+  std::vector<int64_t> val0(state_val, state_val + R);
+  run([&](uint64_t t) {
+    for (uint64_t r = t; r < R; r += T) {
+      uint8_t tg = tag0[r];
+      int64_t v = val0[r];
+      for (uint64_t c = 0; c < chunks; ++c) {
+        const int64_t d = dsum[c * R + r];
+        const uint8_t s = seen[c * R + r];
+        dsum[c * R + r] = v;
+        seen[c * R + r] = tg;
+        if (s) {
+          v = (int64_t)((uint64_t)(tg == CC_TAG_NULL ? 0 : v) + (uint64_t)d);
+          tg = CC_TAG_LONG;
+        }
+      }
+    }
+  }, T);
+  // pass 3: rows, chunk by chunk from each chunk's start state; the chunk holding row n - 1 leaves the final state
+  run([&](uint64_t c) {
+    uint64_t i = crow[c];
+    if (i >= n) return;
+    std::vector<uint8_t> tg(seen.begin() + c * R, seen.begin() + (c + 1) * R);
+    std::vector<int64_t> vl(dsum.begin() + c * R, dsum.begin() + (c + 1) * R);
+    for (uint64_t k = c * kChunk; k < (c + 1) * kChunk && i < n; ++k) {
+      const Add& x = adds[k];
+      auto emit = [&](uint8_t o, uint8_t ta, uint64_t pa, uint8_t tb, uint64_t pb) {
+        if (i >= n) return false;
+        const uint64_t idx = index0 + i * index_stride;
+        if (index) index[i] = idx;
+        if (time) time[i] = idx / 1024;
+        inst[i] = first_inst + x.r;
+        op[i] = o;
+        flags[i] = CC_FLAGS(ta, tb, 0);
+        a[i] = pa;
+        b[i] = pb;
+        ++i;
+        return true;
+      };
+      uint8_t& t = tg[x.r];
+      int64_t& v = vl[x.r];
+      auto cas = [&](uint8_t et, int64_t ev) {
+        const int64_t upd = (int64_t)((uint64_t)(et == CC_TAG_NULL ? 0 : ev) + (uint64_t)(int64_t)x.delta);
+        if (!emit(CC_OP_VALUE_CAS, et, (uint64_t)ev, CC_TAG_LONG, (uint64_t)upd)) return;
+        if ((t == CC_TAG_NULL && et == CC_TAG_NULL) || (t != CC_TAG_NULL && et == t && ev == v)) {
+          t = CC_TAG_LONG;
+          v = upd;
+        }
+      };
+      if (x.kind == 2) {  // stale cache: CAS(stale) fails, Get, CAS(current)
+        cas(CC_TAG_LONG, (t == CC_TAG_NULL ? 0 : v) + 1 + (int64_t)x.stale);
+        emit(CC_OP_VALUE_GET, 0, 0, 0, 0);
+        cas(t, t == CC_TAG_NULL ? 0 : v);
+      } else if (x.kind == 1) {  // cold cache: Get, CAS(current)
+        emit(CC_OP_VALUE_GET, 0, 0, 0, 0);
+        cas(t, t == CC_TAG_NULL ? 0 : v);
+      } else {
+        cas(t, t == CC_TAG_NULL ? 0 : v);
+      }
+    }
+    if (crow[c + 1] >= n) {  // the last chunk with rows: its walk ends in the state after row n - 1
+      memcpy(state_tag, tg.data(), R);
+      memcpy(state_val, vl.data(), 8 * R);
+    }
+  }, chunks);
+  return n;
+}
+
 // Adversarial AtomicValue stream for parity tests: every op (Get/Set/CAS/GetAndSet/Delete), every value tag
 // (NULL/LONG/INT/BOOL/HANDLE) over a tiny value domain (so equals hits and misses), unknown instance slots,
 // ops of other resource types (UNKNOWN_OP), and a hot set of `hot` resources receiving p_hot_ppm of the rows

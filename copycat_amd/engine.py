@@ -52,6 +52,7 @@ def lib():
             "cc_apply_batch": (i32, [P, P, u64, P, P, P]),
             "cc_apply_batch_host": (i32, [P, P, u64, P]),
             "cc_applied_index": (i32, [P, P]),
+            "cc_applied_index_async": (i32, [P, P, P]),
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
             "cc_read_value_retained": (i32, [P, u32, u32, P]),
             "cc_read_map_entries": (i32, [P, u32, u64, P, P, P, P, P, P]),
@@ -309,6 +310,10 @@ class Engine:
         out = C.c_uint64()
         _check(self.L.cc_applied_index(self.h, C.byref(out)))
         return out.value
+
+    def applied_index_async(self, out, stream=None):
+        """Write the applied watermark into the device tensor `out` (one int64), stream-ordered, no host sync."""
+        _check(self.L.cc_applied_index_async(self.h, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
 
     # ---- per-kernel HIP-event timing ------------------------------------------------------------------
     def profile(self, on=True):

@@ -25,6 +25,8 @@ def lib():
         P, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
         L.wl_atomic_long.restype = u64
         L.wl_atomic_long.argtypes = [u64, u32, u32, u64, u32, u32, u64] + [P] * 7
+        L.wl_atomic_long_step.restype = u64
+        L.wl_atomic_long_step.argtypes = [u64, u32, u32, u64, u32, u32, u64, u64, P, P, u32] + [P] * 7
         L.wl_value_random.restype = u64
         L.wl_value_random.argtypes = [u64, u32, u32, u32, u64, u32, u32, u64] + [P] * 7
         L.wl_map_random.restype = u64
@@ -50,6 +52,36 @@ def atomic_long_stream(n, resources=65536, first_inst=0, seed=SEED_C2, p_cold=0.
     lib().wl_atomic_long(n, resources, first_inst, seed, int(p_cold * 1e6), int(p_stale * 1e6), index0,
                          _p(b.index), _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.a), _p(b.b))
     return b
+
+
+class AtomicLongClients:
+    """Config 2 client model carried across bench steps (DistributedAtomicLong.java:117-146): each step's stream
+    continues from the values the clients' CASes expect after the previous step, so the ~10% stale-CAS mix holds
+    in every step.  Rank `rank` of `world` generates its share of ONE global log: its resources are the global
+    resources rank + world*k (local slot k) and its rows carry the global log indices index0 + i*world + rank."""
+
+    def __init__(self, resources=65536, seed=SEED_C2, p_cold=0.2, p_stale=0.1, rank=0, world=1, threads=None):
+        self.R = resources
+        self.seed = seed
+        self.p_cold, self.p_stale = p_cold, p_stale
+        self.rank, self.world = rank, world
+        self.threads = threads or min(16, os.cpu_count() or 1)
+        self.tag = np.zeros(resources, np.uint8)
+        self.val = np.zeros(resources, np.int64)
+        self.next_global = 1  # global log index of the next step's first row (all ranks agree)
+        self.step = 0
+
+    def next(self, n, out=None):
+        """The next step's n rows (a Batch; `out` is reused when given)."""
+        b = out if out is not None else Batch(n)
+        got = lib().wl_atomic_long_step(n, self.R, 0, self.seed + 0x9E37 * self.step, int(self.p_cold * 1e6),
+                                        int(self.p_stale * 1e6), self.next_global + self.rank, self.world, _p(self.tag),
+                                        _p(self.val), self.threads, _p(b.index), _p(b.time), _p(b.inst), _p(b.op),
+                                        _p(b.flags), _p(b.a), _p(b.b))
+        assert got == n
+        self.next_global += n * self.world
+        self.step += 1
+        return b
 
 
 def value_random_stream(n, resources, max_inst, first_inst=0, seed=1, hot=0, p_hot=0.0, index0=1):
@@ -117,4 +149,4 @@ def expiry_sessions(sessions, timeout=5000, now=10_000_000, seed=SEED_C4 + 1):
     return last, now, timeout
 
 
-__all__ = ["atomic_long_stream", "value_random_stream", "map_random_stream", "map_zipf_rows", "quorum_groups", "expiry_sessions", "abi"]
+__all__ = ["atomic_long_stream", "AtomicLongClients", "value_random_stream", "map_random_stream", "map_zipf_rows", "quorum_groups", "expiry_sessions", "abi"]

@@ -295,6 +295,9 @@ int  cc_apply_batch(cc_engine* e, const cc_batch* d_cols, uint64_t n, const cc_r
 int  cc_apply_batch_host(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out);
 /* Highest log index applied so far (the applied watermark; all-gathered across GPUs by the host). */
 int  cc_applied_index(cc_engine* e, uint64_t* out);
+/* The same watermark written stream-ordered into device memory (u64 at d_out) without a host sync: what a rank feeds
+ * to the RCCL all-gather of applied watermarks after each batch. */
+int  cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* stream);
 
 /* ---- snapshot / restore ---------------------------------------------------------------------------
  * Replaces recovery by full log replay (the reference replays Copycat's log, AbstractReplicaTest.java:82-84):
