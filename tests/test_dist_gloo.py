@@ -90,3 +90,89 @@ def test_two_rank_shard_matches_single_replica(tmp_path, oracle_lib):
     for s in range(1000):
         full[s // 64] |= np.uint64(1 << (s % 64))
     assert np.array_equal(tags[0]["bm"], full)
+
+
+# ---- bench.py's multi-GPU c2 layout: each rank generates its share of ONE global log ------------------------------
+R2, N2 = 1024, 30_000
+
+
+def _c2_worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+
+    from copycat_amd.workload import AtomicLongClients
+    from oracle.oracle_py import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    clients = AtomicLongClients(resources=R2, rank=rank, world=world, threads=2)
+    O = Oracle(R2, R2)
+    for k in range(R2):  # local slot k = global resource rank + world*k
+        O.resource_create(k, abi.CC_RES_VALUE)
+        O.instance_open(k, k, 1 + rank + world * k, 1 + rank)
+    outs = []
+    for step in range(2):
+        b = clients.next(N2)
+        st, va = O.apply(b)
+        wm = torch.tensor([O.applied_index()], dtype=torch.int64)
+        allw = torch.zeros(world, dtype=torch.int64)
+        dist.all_gather_into_tensor(allw, wm)
+        outs.append((b, st, va, allw.tolist()))
+    np.savez(os.path.join(outdir, f"c2_r{rank}.npz"),
+             **{f"{c}{s}": getattr(outs[s][0], c) for s in range(2) for c in ("index", "inst", "op", "flags", "a", "b")},
+             **{f"st{s}": outs[s][1] for s in range(2)}, **{f"va{s}": outs[s][2] for s in range(2)},
+             **{f"wm{s}": np.array(outs[s][3]) for s in range(2)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_c2_is_a_split_of_one_global_log(tmp_path, oracle_lib):
+    """The per-rank c2 streams of bench.py --gpus N merge (by log index) into one gap-free global log over
+    world * R resources; shard.split_batch of that log by resource owner gives back each rank's stream; one replica
+    applying the global log returns exactly the merged per-rank results; all-gathered watermarks are the global log
+    positions each rank reached."""
+    from copycat_amd.batch import Batch
+    from oracle.oracle_py import Oracle
+
+    world, port = 2, _free_port()
+    mp.spawn(_c2_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    z = [np.load(tmp_path / f"c2_r{r}.npz") for r in range(world)]
+    G = Oracle(world * R2, world * R2)
+    for g in range(world * R2):
+        G.resource_create(g, abi.CC_RES_VALUE)
+        G.instance_open(g, g, 1 + g, 1 + g % world)
+    for s in range(2):
+        # merge: global row = local row i of rank r at log index s*N2*world + 1 + r + i*world; global slot = r + world*k
+        glog = Batch(world * N2)
+        for r in range(world):
+            idx = z[r][f"index{s}"]
+            assert np.array_equal(idx, s * N2 * world + 1 + r + np.arange(N2, dtype=np.uint64) * world)
+            pos = (idx - 1 - s * N2 * world).astype(np.int64)
+            glog.index[pos] = idx
+            glog.inst[pos] = r + world * z[r][f"inst{s}"]
+            for c in ("op", "flags", "a", "b"):
+                getattr(glog, c)[pos] = z[r][f"{c}{s}"]
+        assert np.array_equal(glog.index, s * N2 * world + 1 + np.arange(world * N2, dtype=np.uint64))
+        parts = shard.split_batch(glog, shard.inst_owner_table(np.arange(world * R2), world), world)
+        for r, (rows, part) in enumerate(parts):
+            assert np.array_equal(part.index, z[r][f"index{s}"])
+            assert np.array_equal(part.inst // world, z[r][f"inst{s}"])
+        st, va = G.apply(glog)
+        mst, mva = shard.merge_results(len(glog), [(rows, z[r][f"st{s}"], z[r][f"va{s}"]) for r, (rows, _) in enumerate(parts)])
+        assert np.array_equal(st, mst) and np.array_equal(va, mva)
+        assert z[0][f"wm{s}"].tolist() == z[1][f"wm{s}"].tolist() == [(s + 1) * N2 * world - 1 + r for r in range(world)]
+        cas = glog.op == abi.CC_OP_VALUE_CAS
+        assert 0.85 < float((va[cas] == 1).mean()) < 0.95  # the stated stale-CAS mix in every step
+
+
+def test_bench_gpus_flag_fails_fast_without_gpus():
+    """bench.py --gpus N launches N ranks itself; on a box with fewer GPUs it stops before any GPU work."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=dict(os.environ, CUDA_VISIBLE_DEVICES=""))
+    assert r.returncode == 2 and "GPU(s) visible" in r.stderr, (r.returncode, r.stderr[-400:])
