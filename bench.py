@@ -208,27 +208,71 @@ def run_c4(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
+def event_checksum(pos, target, code, tag, payload):
+    """Order-independent checksum of an event multiset: sum over events of a 64-bit mix of (row, target, code, tag,
+    payload) (wrapping), plus the count."""
+    with np.errstate(over="ignore"):
+        x = (np.asarray(pos, np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ (np.asarray(target, np.uint64) << np.uint64(20))
+        x ^= (np.asarray(code, np.uint64) << np.uint64(52)) ^ (np.asarray(tag, np.uint64) << np.uint64(58))
+        x ^= np.asarray(payload, np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(31)
+        x *= np.uint64(0x94D049BB133111EB)
+        return int(x.sum(dtype=np.uint64)), int(len(x))
+
+
 def run_c5(args, dev, rank, world, dist):
-    """Mixed coordination through cc_apply_batch with the event stream."""
+    """Mixed coordination through cc_apply_batch with the event stream; a new batch every step (the
+    lock client model continues, copycat_amd.workload.CoordClients); step 0 checked against the oracle in full."""
     from copycat_amd import abi
+    from copycat_amd.batch import Batch
     from copycat_amd.engine import DeviceBatch, DeviceEvents, Engine
-    from copycat_amd.workload import coord_random_stream
+    from copycat_amd.workload import CoordClients
 
     n = args.commits or 100_000_000
     R = args.resources or 262_144 // 8  # SURVEY c5: 262,144 resources sharded res % 8 -> 32,768 per GPU
-    third = (R + 2) // 3  # type-major slots: locks, then elections, then groups
-    types = np.repeat(np.array([abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP], np.uint8), third)[:R]
+    kinds = np.array([abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP], np.uint8)
+    if args.c5_layout == "grouped":  # slot ranges by type: locks, then elections, then groups
+        types = np.repeat(kinds, (R + 2) // 3)[:R]
+    else:  # resources created in turn (a lock, an election, a group, ...): slot r holds type r % 3
+        types = np.resize(kinds, R)
+    total_steps = args.warmup + args.steps
+    nstreams = max(1, min(total_steps, int(args.hbm_budget_gb * 1e9 // (n * 54))))
+    flags = abi.CC_CFG_TIMERS_DEFERRED
     t_gen = time.time()
-    batch = coord_random_stream(n, types, 1, R, seed=0xA700000 + 5 + rank)
-    db = DeviceBatch.upload(batch, device=dev)
+    clients = CoordClients(types, K=1, max_inst=R, seed=0xA700000 + 5 + rank)
+    host = Batch(n)
+    streams, parity_ref, cpu = [], None, None
+    for k in range(nstreams):
+        clients.next(n, out=host)
+        if k == 0 and rank == 0 and not args.no_parity:
+            from oracle.oracle_py import Oracle
+
+            O = Oracle(R, R, flags)
+            for r in range(R):
+                O.resource_create(r, int(types[r]))
+                O.instance_open(r, r, 1000 + r, 1 + rank)
+            tc = time.perf_counter()
+            s_ref, v_ref = O.apply(host)
+            tc = time.perf_counter() - tc
+            oe = O.take_events()
+            apos, amem = O.take_aux()
+            parity_ref = (s_ref, v_ref, event_checksum(oe["pos"], oe["target"], oe["code"], oe["tag"], oe["payload"]),
+                          event_checksum(apos, np.zeros_like(apos), np.full(len(apos), abi.CC_EV_MEMBER), np.full(len(apos), 1),
+                                         amem))
+            if world == 1 and not args.no_cpu_baseline:
+                cpu = {"value": round(n / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+                       "sample": f"step 0's {n:,} commits of the same c5 stream (events included; the parity reference), "
+                                 f"C++ restatement of the Java apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+            del O, oe
+        streams.append(DeviceBatch.upload(host, device=dev))
+    del host
     t_gen = time.time() - t_gen
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     value = torch.zeros(n, dtype=torch.int64, device=dev)
     evs = DeviceEvents(2 * n, device=dev)
-    flags = abi.CC_CFG_TIMERS_DEFERRED
     E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
-    for k, t in enumerate((abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP)):
-        E.resource_create_range(k * third, min(third, R - k * third), int(t))
+    for r in range(R):
+        E.resource_create(r, int(types[r]))
     E.instance_open_range(0, R, 0, 1000, 1 + rank)
     stream = torch.cuda.current_stream(dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
@@ -245,16 +289,20 @@ def run_c5(args, dev, rank, world, dist):
     d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     bm_all = torch.zeros(world * (S_local // 64), dtype=torch.int64, device=dev)
 
-    def step():
-        E.apply_events(db, status, value, evs, stream=stream)
+    def step(k):
+        E.apply_events(streams[k % nstreams], status, value, evs, stream=stream)
         E.applied_index_async(wm_local, stream=stream)
         expire_sweep(d_last, now_s, timeout_s, d_bm, d_cnt, stream=stream)
         if dist is not None:  # watermark, then expired-session bitmap (RCCL all-gathers over xGMI)
             dist.all_gather_into_tensor(wm_all, wm_local)
             dist.all_gather_into_tensor(bm_all, d_bm)
 
-    for _ in range(args.warmup):
-        step()
+    parity = None
+    for k in range(args.warmup):
+        step(k)
+        if k == 0 and parity_ref is not None:
+            E.sync()
+            parity = c5_parity(parity_ref, status, value, evs, abi)
     torch.cuda.synchronize(dev)
     if not args.no_profile:
         E.profile(True)
@@ -262,8 +310,8 @@ def run_c5(args, dev, rank, world, dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.warmup, total_steps):
+        step(k)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -273,6 +321,8 @@ def run_c5(args, dev, rank, world, dist):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if parity is None and parity_ref is not None and args.warmup == 0 and nstreams >= total_steps and total_steps == 1:
+        parity = c5_parity(parity_ref, status, value, evs, abi)
     prof = E.profile_read() if not args.no_profile else {}
     n_events = int(evs.count.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -291,38 +341,44 @@ def run_c5(args, dev, rank, world, dist):
             "bytes_per_commit": B_OP_C5,
             "pipeline_frac": round(B_OP_C5 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         }
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle.oracle_py import Oracle
-
-        m = min(n, args.cpu_sample or 10_000_000)
-        O = Oracle(R, R, flags)
-        for r in range(R):
-            O.resource_create(r, int(types[r]))
-            O.instance_open(r, r, 1000 + r, 1)
-        tc = time.perf_counter()
-        O.apply(batch.slice(0, m))
-        tc = time.perf_counter() - tc
-        cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
-               "sample": f"first {m:,} commits of the same c5 stream (events included), C++ restatement of the Java "
-                         f"apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": f"c5: mixed coordination (lock / election / group, a third each) over {R:,} resources, "
-                                   f"{n:,} committed entries per GPU with the ordered event stream",
+            "config": {"workload": f"c5: mixed coordination (lock / election / group, a third each, {args.c5_layout} slots) over {R:,} resources, "
+                                   f"{n:,} committed entries per GPU per step with the ordered event stream, a new "
+                                   f"client-model batch every step",
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
-                       "events_per_step": n_events, "gen_s": round(t_gen, 2),
+                       "resident_streams": nstreams, "events_last_step": n_events, "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())],
                        "expired_sessions_per_step": int(np.unpackbits(
                            (bm_all if dist is not None else d_bm).cpu().numpy().view(np.uint8)).sum())},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "parity": parity, "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    bad = parity is not None and (parity["mismatches"] or not parity["events_equal"])
     if dist is not None:
         dist.destroy_process_group()
+    if bad:
+        sys.stderr.write(f"PARITY FAILURE: {parity}\n")
+        sys.exit(3)
+
+
+def c5_parity(ref, status, value, evs, abi):
+    s_ref, v_ref, ev_ref, mem_ref = ref
+    s = status.cpu().numpy()
+    v = value.cpu().numpy().view(np.uint64)
+    ev = evs.host()
+    member = ev["code"] == abi.CC_EV_MEMBER
+    got = event_checksum(*(ev[k][~member] for k in ("pos", "target", "code", "tag", "payload")))
+    got_mem = event_checksum(ev["pos"][member], np.zeros(int(member.sum()), np.uint64),
+                             np.full(int(member.sum()), abi.CC_EV_MEMBER), np.full(int(member.sum()), 1),
+                             ev["payload"][member])
+    return {"rows": len(s), "mismatches": int(np.count_nonzero((s != s_ref) | (v != v_ref))),
+            "events": got[1], "events_equal": got == ev_ref and got_mem == mem_ref,
+            "checked": "step 0: per-commit status+value, and the event multiset (count + order-free 64-bit checksum of "
+                       "(row, target, code, tag, payload)) incl. join member sets, GPU vs oracle/oracle.cpp"}
 
 
 def cpu_threads():
@@ -707,6 +763,8 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="c2: also time one PCIe-inclusive step (pinned H2D + apply + D2H)")
     ap.add_argument("--hbm-budget-gb", type=float, default=200.0,
                     help="c2: HBM for resident per-step batches (more steps than fit replay the resident ones)")
+    ap.add_argument("--c5-layout", choices=("interleaved", "grouped"), default="interleaved",
+                    help="c5: resource types by slot: r %% 3 (created in turn) or in thirds")
     ap.add_argument("--retained", action="store_true", help="c2: also keep the retained value commit per slot (CC_CFG_VALUE_RETAINED)")
     args = ap.parse_args()
 

@@ -1,8 +1,8 @@
 // apply_coord.hip — coordination state machines (LockState, LeaderElectionState, MembershipGroupState) and
 // AtomicValue with listeners, with their published events.
 //
-// Same shape as apply_value.hip: one 256-thread workgroup per super-bucket (256 resource slots), thread t owns
-// slot t and applies that slot's commits in log order.  The super-buckets handled here are those holding a
+// Like apply_value.hip, one thread owns one resource slot and applies that slot's commits in log order; here a
+// workgroup owns a quarter super-bucket (64 slots, see k_apply_coord).  The super-buckets handled here are those holding a
 // coordination resource (or every value super-bucket with CC_CFG_VALUE_EVENTS); k_apply_value skips them.
 // State that has variable size in the reference lives in a fixed block per slot (common.h CoordHdr/CoordEnt):
 // the lock's waiter FIFO (ArrayDeque, LockState.java:35), the election's listener LinkedHashMap
@@ -28,32 +28,52 @@
 
 namespace cc {
 
-constexpr int kCT = 256;            // threads = slots per super-bucket
-constexpr int kCPer = 8;            // commits per thread per chunk (2048: fewer chunk barriers; 146 KB LDS)
-constexpr int kCCh = kCT * kCPer;   // 2048
-constexpr int kEvBuf = 2048;        // LDS event buffer per chunk
+#ifdef CC_PHASE_TIMING
+__device__ unsigned long long g_ph_coord[kPhases];
+int phase_read_coord(uint64_t* out) {
+  unsigned long long z[kPhases] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ph_coord), sizeof z) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_ph_coord), z, sizeof z) != hipSuccess)
+    return CC_ERR_HIP;
+  return CC_OK;
+}
+#endif
 
+
+typedef __attribute__((address_space(3))) EvRec LdsEv;
+// Events of the walking lane: its own region of the LDS buffer (no atomics between lanes), a running count in a
+// register; past the region's end straight to the sub-batch arena (one global atomic per event).
 struct Emitter {
-  EvRec* buf;
-  uint32_t* nbuf;
+  LdsEv* buf;        // this lane's region (typed: its accesses never turn into flat ones)
+  uint32_t cap;      // events per lane region
   EvRec* arena;
   unsigned long long* arena_n;
   uint64_t arena_cap;
-  __device__ void emit(uint32_t g, uint32_t k, uint32_t target, uint32_t code, uint32_t src, uint32_t tag,
+  __device__ void emit(uint32_t& n, uint32_t g, uint32_t k, uint32_t target, uint32_t code, uint32_t src, uint32_t tag,
                        uint64_t payload) const {
-    EvRec e;
-    e.g = g;
-    e.target = target;
-    e.payload = tag == CC_TAG_NULL ? 0 : payload;
-    e.k = (uint16_t)k;
-    e.code = (uint8_t)code;
-    e.tag = (uint8_t)tag;
-    e.src = (uint8_t)src;
-    e.pad[0] = e.pad[1] = e.pad[2] = 0;
-    const uint32_t q = atomicAdd(nbuf, 1u);
-    if (q < (uint32_t)kEvBuf) {
-      buf[q] = e;
-    } else {  // buffer full: straight to the arena
+#ifdef CC_DIAG_NO_EMIT  // diagnostics build only: events dropped
+    if (code != 0xFF) return;
+#endif
+    const uint64_t pl = tag == CC_TAG_NULL ? 0 : payload;
+    const uint32_t q = n++;
+    if (q < cap) {  // field by field: a struct copy through an address-space-typed pointer does not compile
+      buf[q].g = g;
+      buf[q].target = target;
+      buf[q].payload = pl;
+      buf[q].k = (uint16_t)k;
+      buf[q].code = (uint8_t)code;
+      buf[q].tag = (uint8_t)tag;
+      buf[q].src = (uint8_t)src;
+    } else {  // region full: straight to the arena
+      EvRec e;
+      e.g = g;
+      e.target = target;
+      e.payload = pl;
+      e.k = (uint16_t)k;
+      e.code = (uint8_t)code;
+      e.tag = (uint8_t)tag;
+      e.src = (uint8_t)src;
+      e.pad[0] = e.pad[1] = e.pad[2] = 0;
       const unsigned long long a = atomicAdd(arena_n, 1ull);
       if (a < arena_cap) arena[a] = e;
     }
@@ -62,17 +82,88 @@ struct Emitter {
 
 __device__ inline CoordEnt* ents(uint8_t* blk) { return reinterpret_cast<CoordEnt*>(blk + sizeof(CoordHdr)); }
 
+// A slot's entries during k_apply_coord: the first kECache physical entries live in LDS (copied in at kernel start,
+// back at the end), the rest stay in the global block.  Small lock queues / listener and member lists (the common
+// case) then never wait on global memory inside a slot's sequential walk.
+constexpr uint32_t kECache = 8;
+// Reads and writes select on the index, never on the pointer: each access keeps its address space (ds_read /
+// global_load), so an LDS hit does not wait behind the walk's outstanding global stores as a flat access would.
+typedef __attribute__((address_space(3))) CoordEnt LdsEnt;
+typedef __attribute__((address_space(1))) CoordEnt GlbEnt;
+struct Ents {
+  LdsEnt* lds;
+  GlbEnt* glb;
+  // (the global path uses nontemporal accesses: distinct instructions the compiler cannot merge with the LDS path
+  // into one flat access through a selected pointer)
+  __device__ CoordEnt get(uint32_t p) const {
+    CoordEnt e;
+    if (p < kECache) {
+      e.x = lds[p].x;
+      e.idx = lds[p].idx;
+      e.inst = lds[p].inst;
+      e.pad = lds[p].pad;
+      return e;
+    }
+    e.x = __builtin_nontemporal_load(&glb[p].x);
+    e.idx = __builtin_nontemporal_load(&glb[p].idx);
+    e.inst = __builtin_nontemporal_load(&glb[p].inst);
+    e.pad = __builtin_nontemporal_load(&glb[p].pad);
+    return e;
+  }
+  __device__ CoordEnt glb_get(uint32_t p) const {
+    CoordEnt e;
+    e.x = glb[p].x;
+    e.idx = glb[p].idx;
+    e.inst = glb[p].inst;
+    e.pad = glb[p].pad;
+    return e;
+  }
+  __device__ void glb_put(uint32_t p, const CoordEnt& v) const {
+    glb[p].x = v.x;
+    glb[p].idx = v.idx;
+    glb[p].inst = v.inst;
+    glb[p].pad = v.pad;
+  }
+  __device__ void put(uint32_t p, const CoordEnt& v) const {
+    if (p < kECache) {
+      lds[p].x = v.x;
+      lds[p].idx = v.idx;
+      lds[p].inst = v.inst;
+      lds[p].pad = v.pad;
+      return;
+    }
+    __builtin_nontemporal_store(v.x, &glb[p].x);
+    __builtin_nontemporal_store(v.idx, &glb[p].idx);
+    __builtin_nontemporal_store(v.inst, &glb[p].inst);
+    __builtin_nontemporal_store(v.pad, &glb[p].pad);
+  }
+  __device__ void load() const {  // kernel start: the slot's first kECache entries
+#pragma unroll
+    for (uint32_t q = 0; q < kECache; ++q) put(q, glb_get(q));
+  }
+  __device__ void store() const {  // kernel end
+#pragma unroll
+    for (uint32_t q = 0; q < kECache; ++q) glb_put(q, get(q));
+  }
+};
+
 // ---- LockState ----------------------------------------------------------------------------------------
-__device__ inline void lock_expire(CoordHdr& h, CoordEnt* q, uint64_t th) {  // silent timeouts (A7)
+__device__ inline void lock_expire(CoordHdr& h, const Ents& q, uint64_t th) {  // silent timeouts (A7)
   uint32_t kept = 0;
   for (uint32_t i = 0; i < h.n; ++i) {
-    const CoordEnt e = q[(h.head + i) % kCoordCap];
+    const CoordEnt e = q.get((h.head + i) % kCoordCap);
     if (e.x != kNoDeadline && e.x <= th) continue;
-    if (kept != i) q[(h.head + kept) % kCoordCap] = e;
+    if (kept != i) q.put((h.head + kept) % kCoordCap, e);
     ++kept;
   }
   h.n = kept;
+  if (!kept) h.head = 0;  // an empty ring restarts at entry 0 (kept in LDS by k_apply_coord)
 }
+
+template <uint32_t V>
+struct TypeC {
+  static constexpr uint32_t value = V;
+};
 
 // ---- one commit on a coordination / value slot -----------------------------------------------------------
 struct Rec {
@@ -80,12 +171,16 @@ struct Rec {
   uint64_t a, b, key, idx, iid;
 };
 
-__device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h, uint8_t* blk, uint32_t& vmeta_s,
-                                       uint64_t& vval, uint64_t& rv, uint32_t& nev, const Emitter& em, uint32_t& err) {
-  CoordEnt* E = ents(blk);
+// T != 0: the resource type is known at compile time (a wave whose slots all hold one type walks a specialised
+// copy with no code for the other types); T == 0: the runtime `type`.
+template <uint32_t T>
+__device__ inline uint32_t coord_apply(uint32_t type_rt, const Rec& r, CoordHdr& h, const Ents& E, uint32_t& vmeta_s,
+                                       uint64_t& vval, uint64_t& rv, uint32_t& nev, const Emitter& em, uint32_t& lane_n,
+                                       uint32_t& err) {
+  const uint32_t type = T ? T : type_rt;
   rv = 0;
   auto ev = [&](uint32_t target, uint32_t code, uint32_t tag, uint64_t payload) {
-    em.emit(r.g, nev++, target, code, CC_EVSRC_COMMIT, tag, payload);
+    em.emit(lane_n, r.g, nev++, target, code, CC_EVSRC_COMMIT, tag, payload);
   };
   if (h.flags & kCoZombie) return CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
   if (!op_registered(type, r.op)) return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
@@ -114,7 +209,7 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
         } else if (h.n == (uint32_t)kCoordCap) {
           err |= kErrCapacity;
         } else {
-          E[(h.head + h.n) % kCoordCap] = CoordEnt{timeout > 0 ? clk + (uint64_t)timeout : kNoDeadline, r.idx, r.inst, 0};
+          E.put((h.head + h.n) % kCoordCap, CoordEnt{timeout > 0 ? clk + (uint64_t)timeout : kNoDeadline, r.idx, r.inst, 0});
           ++h.n;
         }
         return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
@@ -126,9 +221,9 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
         if (h.n == 0) {
           h.flags = 0;
         } else {
-          const CoordEnt e = E[h.head];
+          const CoordEnt e = E.get(h.head);
           h.head = (h.head + 1) % kCoordCap;
-          --h.n;
+          if (!--h.n) h.head = 0;
           h.flags = kCoHeld;
           h.who = e.inst;
           h.idx = e.idx;
@@ -154,10 +249,10 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
           ev(r.inst, CC_EV_ELECT, CC_TAG_LONG, r.idx);
         } else {
           bool found = false;
-          for (uint32_t i = 0; i < h.n && !found; ++i) found = E[i].x == r.iid;
+          for (uint32_t i = 0; i < h.n && !found; ++i) found = E.get(i).x == r.iid;
           if (!found) {  // may be the leader's own session (A9)
             if (h.n == (uint32_t)kCoordCap) err |= kErrCapacity;
-            else E[h.n++] = CoordEnt{r.iid, r.idx, r.inst, 0};
+            else E.put(h.n++, CoordEnt{r.iid, r.idx, r.inst, 0});
           }
         }
         return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
@@ -167,8 +262,8 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
           if (h.flags & kCoCleaned) return CC_STATUS(CC_ST_ILLEGAL_STATE, CC_TAG_NULL);
           h.flags = 0;
           if (h.n) {
-            const CoordEnt e = E[0];
-            for (uint32_t i = 1; i < h.n; ++i) E[i - 1] = E[i];
+            const CoordEnt e = E.get(0);
+            for (uint32_t i = 1; i < h.n; ++i) E.put(i - 1, E.get(i));
             --h.n;
             h.flags = kCoHeld;
             h.who = e.inst;
@@ -177,8 +272,8 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
           }
         } else {
           for (uint32_t i = 0; i < h.n; ++i)
-            if (E[i].x == r.iid) {
-              for (uint32_t k = i + 1; k < h.n; ++k) E[k - 1] = E[k];
+            if (E.get(i).x == r.iid) {
+              for (uint32_t k = i + 1; k < h.n; ++k) E.put(k - 1, E.get(k));
               --h.n;
               break;
             }
@@ -190,6 +285,9 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
       return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
     }
     case CC_RES_GROUP: {
+#ifdef CC_DIAG_GROUP_NOP  // diagnostics build only (scripts/probes/phase_timing.py): the group walk without its work
+      if (r.op != 0xFF) { rv = 0; return CC_STATUS(CC_ST_OK, CC_TAG_NULL); }
+#endif
       if (r.op == CC_OP_DELETE) {
         h.n = 0;
         return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
@@ -203,53 +301,58 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
         uint32_t lo = 0, hi = h.n;
         while (lo < hi) {
           const uint32_t m = (lo + hi) >> 1;
-          if (E[m].x < id) lo = m + 1; else hi = m;
+          if (E.get(m).x < id) lo = m + 1; else hi = m;
         }
-        hit = lo < h.n && E[lo].x == id;
+        hit = lo < h.n && E.get(lo).x == id;
         return lo;
       };
+      // one search for every op (converged across the wave's lanes): join / leave look up the committing instance,
+      // execute the target member
       bool hit;
+      const uint32_t p = find(r.op == CC_OP_GROUP_EXECUTE ? r.key : r.iid, hit);
       if (r.op == CC_OP_GROUP_JOIN) {
-        const uint32_t p = find(r.iid, hit);
         if (hit) {
-          E[p].idx = r.idx;  // previous.clean()
-          E[p].inst = r.inst;
+          CoordEnt e = E.get(p);  // previous.clean()
+          e.idx = r.idx;
+          e.inst = r.inst;
+          E.put(p, e);
         } else if (h.n == (uint32_t)kCoordCap) {
           err |= kErrCapacity;
         } else {
-          for (uint32_t i = h.n; i > p; --i) E[i] = E[i - 1];
-          E[p] = CoordEnt{r.iid, r.idx, r.inst, 0};
+          for (uint32_t i = h.n; i > p; --i) E.put(i, E.get(i - 1));
+          E.put(p, CoordEnt{r.iid, r.idx, r.inst, 0});
           ++h.n;
-          for (uint32_t i = 0; i < h.n; ++i)
-            if (E[i].idx != r.idx) ev(E[i].inst, CC_EV_JOIN, CC_TAG_LONG, r.iid);
+          for (uint32_t i = 0; i < h.n; ++i) {
+            const CoordEnt e = E.get(i);
+            if (e.idx != r.idx) ev(e.inst, CC_EV_JOIN, CC_TAG_LONG, r.iid);
+          }
         }
         for (uint32_t i = 0; i < h.n; ++i)  // the returned Set<Long>, ascending
-          em.emit(r.g, nev++, r.inst, CC_EV_MEMBER, CC_EVSRC_RESULT, CC_TAG_LONG, E[i].x);
+          em.emit(lane_n, r.g, nev++, r.inst, CC_EV_MEMBER, CC_EVSRC_RESULT, CC_TAG_LONG, E.get(i).x);
         rv = h.n;
         return CC_STATUS(CC_ST_OK, CC_TAG_SET);
       }
       if (r.op == CC_OP_GROUP_LEAVE) {
-        const uint32_t p = find(r.iid, hit);
         if (hit) {
-          for (uint32_t i = p + 1; i < h.n; ++i) E[i - 1] = E[i];
+          for (uint32_t i = p + 1; i < h.n; ++i) E.put(i - 1, E.get(i));
           --h.n;
-          for (uint32_t i = 0; i < h.n; ++i) ev(E[i].inst, CC_EV_LEAVE, CC_TAG_LONG, r.iid);
+          for (uint32_t i = 0; i < h.n; ++i) ev(E.get(i).inst, CC_EV_LEAVE, CC_TAG_LONG, r.iid);
         }
         return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
       }
       // execute(member = key, callback = a)
-      const uint32_t p = find(r.key, hit);
       if (!hit) return CC_STATUS(CC_ST_ILLEGAL_ARGUMENT, CC_TAG_NULL);  // "unknown member"
-      ev(E[p].inst, CC_EV_EXECUTE, CC_FLAG_TAG_A(r.flags), r.a);
+      ev(E.get(p).inst, CC_EV_EXECUTE, CC_FLAG_TAG_A(r.flags), r.a);
       return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
     }
     case CC_RES_QUEUE: {  // QueueState.java:33-199: an ArrayDeque of (value tag in pad, payload in x), FIFO ring
       const uint32_t ta = CC_FLAG_TAG_A(r.flags);
       const uint64_t pa = ta ? r.a : 0;
-      auto at = [&](uint32_t i) -> CoordEnt& { return E[(h.head + i) % kCoordCap]; };
+      auto at = [&](uint32_t i) -> CoordEnt { return E.get((h.head + i) % kCoordCap); };
+      auto set_at = [&](uint32_t i, const CoordEnt& v) { E.put((h.head + i) % kCoordCap, v); };
       auto first_match = [&](uint32_t& pos) -> int {  // 1 match, 0 none, -1 NPE (a stored null's equals)
         for (uint32_t i = 0; i < h.n; ++i) {
-          const CoordEnt& e = at(i);
+          const CoordEnt e = at(i);
           if (e.pad == CC_TAG_NULL) return -1;
           if (e.pad == ta && e.x == pa) {
             pos = i;
@@ -260,7 +363,7 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
       };
       auto pop = [&]() {
         h.head = (h.head + 1) % kCoordCap;
-        --h.n;
+        if (!--h.n) h.head = 0;
       };
       switch (r.op) {
         case CC_OP_DELETE:
@@ -280,7 +383,7 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
           if (h.n == (uint32_t)kCoordCap) {
             err |= kErrCapacity;
           } else {
-            at(h.n) = CoordEnt{pa, r.idx, r.inst, ta};
+            set_at(h.n, CoordEnt{pa, r.idx, r.inst, ta});
             ++h.n;
           }
           return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
@@ -305,7 +408,7 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
             const int m = first_match(pos);
             if (m < 0) return CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
             if (m) {
-              for (uint32_t i = pos; i + 1 < h.n; ++i) at(i) = at(i + 1);
+              for (uint32_t i = pos; i + 1 < h.n; ++i) set_at(i, at(i + 1));
               --h.n;
             }
             rv = m;
@@ -352,18 +455,24 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
           break;
         case CC_OP_VALUE_LISTEN: {  // listeners.put(session, commit)
           bool found = false;
-          for (uint32_t i = 0; i < h.n; ++i)
-            if (E[i].inst == r.inst) { E[i].idx = r.idx; found = true; }
+          for (uint32_t i = 0; i < h.n; ++i) {
+            CoordEnt e = E.get(i);
+            if (e.inst == r.inst) {
+              e.idx = r.idx;
+              E.put(i, e);
+              found = true;
+            }
+          }
           if (!found) {
             if (h.n == (uint32_t)kCoordCap) err |= kErrCapacity;
-            else E[h.n++] = CoordEnt{0, r.idx, r.inst, 0};
+            else E.put(h.n++, CoordEnt{0, r.idx, r.inst, 0});
           }
           break;
         }
         case CC_OP_VALUE_UNLISTEN:
           for (uint32_t i = 0; i < h.n; ++i)
-            if (E[i].inst == r.inst) {
-              for (uint32_t k = i + 1; k < h.n; ++k) E[k - 1] = E[k];
+            if (E.get(i).inst == r.inst) {
+              for (uint32_t k = i + 1; k < h.n; ++k) E.put(k - 1, E.get(k));
               --h.n;
               break;
             }
@@ -375,7 +484,7 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
       if (write) {
         vmeta_s = vmeta(ntag, 1);
         vval = nv;
-        for (uint32_t i = 0; i < h.n; ++i) ev(E[i].inst, CC_EV_CHANGE, ntag, nv);  // change(value) :68-72
+        for (uint32_t i = 0; i < h.n; ++i) ev(E.get(i).inst, CC_EV_CHANGE, ntag, nv);  // change(value) :68-72
       }
       rv = rvv;
       return CC_STATUS(CC_ST_OK, rtag);
@@ -384,42 +493,62 @@ __device__ inline uint32_t coord_apply(uint32_t type, const Rec& r, CoordHdr& h,
   return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
 }
 
-__global__ __launch_bounds__(kCT) void k_apply_coord(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
-                                                    const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
-                                                    const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
-                                                    uint32_t tiles, uint32_t sb, const uint8_t* __restrict__ sb_kind,
-                                                    const uint8_t* __restrict__ res_type, const uint64_t* __restrict__ inst_id,
-                                                    uint8_t* __restrict__ coord, uint32_t* __restrict__ val_meta,
-                                                    uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
-                                                    uint64_t* __restrict__ rst_value, uint16_t* __restrict__ ev_cnt,
-                                                    EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n,
-                                                    uint64_t arena_cap, uint32_t* __restrict__ err_out) {
-  __shared__ u64x2 rab[kCCh];
-  __shared__ uint64_t rkey[kCCh];
-  __shared__ uint64_t ridx[kCCh];
-  __shared__ uint32_t rmeta[kCCh];
-  __shared__ uint32_t rins[kCCh];
-  __shared__ uint32_t rpos[kCCh];
-  __shared__ uint32_t scnt[kCT + 1];
+// One workgroup per quarter super-bucket (kQ = 64 slots): the four workgroups of a super-bucket each read its list
+// (the run in every tile, tile order = log order) and keep the commits of their own slots.  256 threads load a
+// 512-commit chunk (the next chunk's meta words are in flight during the walk), rank their own commits per slot
+// inside each wave (LDS atomics with return: lane order), one wave turns the per-wave counts into slot run starts,
+// the owners' records are gathered into LDS in slot order, and wave 0 (lane = slot) applies each slot's commits in
+// log order with its CoordHdr (and AtomicValueState) held in registers for the whole launch.  Small LDS
+// (~48 KB) so three workgroups share a CU and hide each other's gathers.
+constexpr int kQ = 64;                     // slots per workgroup
+constexpr int kQPerSb = (1 << kSbShift) / kQ;
+constexpr int kCT2 = 256;                  // threads per workgroup
+constexpr int kCW2 = kCT2 / kWave;
+constexpr int kCPer2 = 2;                  // commits per thread per chunk
+constexpr int kCCh2 = kCT2 * kCPer2;       // 512 commits of the super-bucket per chunk
+constexpr int kEvLane = 16;                // LDS event slots per walking lane per chunk
+
+__global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
+                                                     const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
+                                                     const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
+                                                     uint32_t tiles, uint32_t sb, uint32_t sbq_base,
+                                                     const uint8_t* __restrict__ sb_kind,
+                                                     const uint8_t* __restrict__ res_type, const uint64_t* __restrict__ inst_id,
+                                                     uint8_t* __restrict__ coord, uint32_t* __restrict__ val_meta,
+                                                     uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
+                                                     uint64_t* __restrict__ rst_value, uint16_t* __restrict__ ev_cnt,
+                                                     EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n,
+                                                     uint64_t arena_cap, uint32_t* __restrict__ err_out) {
+  __shared__ u64x2 rab[kCCh2];
+  __shared__ uint64_t rkey[kCCh2];
+  __shared__ uint64_t ridx[kCCh2];
+  __shared__ uint64_t riid[kCCh2];
+  __shared__ uint32_t rmeta[kCCh2];
+  __shared__ uint32_t rins[kCCh2];
+  __shared__ uint32_t rpos[kCCh2];
+  __shared__ uint64_t oval[kCCh2];           // the walk's results in slot order (written out by all threads)
+  __shared__ uint16_t oev[kCCh2];
+  __shared__ uint8_t ost[kCCh2];
+  __shared__ uint32_t wc[kCW2][kQ];          // per-wave slot counts -> per-wave exclusive prefixes
+  __shared__ uint32_t sstart[kQ + 1];
   __shared__ uint32_t rstart[kMaxTiles];
   __shared__ uint32_t rpre[kMaxTiles + 1];
-  __shared__ uint32_t wsum[kCT / kWave];
-  __shared__ EvRec evbuf[kEvBuf];
-  __shared__ uint32_t evn;
+  __shared__ uint32_t wsum[kCW2];
+  __shared__ EvRec evbuf[kQ * kEvLane];
+  __shared__ uint32_t evoff[kQ + 1];
+  __shared__ CoordEnt ecache[kQ * kECache];   // the walkers' first entries (Ents)
   __shared__ unsigned long long evbase;
 
-  const uint32_t s = blockIdx.x;
+  const uint32_t s = blockIdx.x / kQPerSb, q0 = (blockIdx.x % kQPerSb) * kQ;
   if (!sb_kind[s]) return;  // value-only super-bucket: k_apply_value
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  const uint32_t res = s * kCT + t, type = res_type[res];
+  PH_DECL
   uint32_t err = 0;
-  scnt[t] = 0;
-  if (t == 0) {
-    scnt[kCT] = 0;
-    evn = 0;
-  }
-  {  // this super-bucket's list = its run in every tile, in tile order
-    constexpr int PT = kMaxTiles / kCT;
+  for (uint32_t k = t; k < (uint32_t)(kCW2 * kQ); k += kCT2) (&wc[0][0])[k] = 0;
+  // the list: this quarter's own bucket when the partition made quarter buckets, else the super-bucket's (filtered)
+  const uint32_t bk = sbq_base ? sbq_base + blockIdx.x : s;
+  {  // the list = its run in every tile, in tile order
+    constexpr int PT = kMaxTiles / kCT2;
     uint32_t len[PT], sum = 0;
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
@@ -427,7 +556,7 @@ __global__ __launch_bounds__(kCT) void k_apply_coord(const uint32_t* __restrict_
       len[q] = 0;
       if (tt < tiles) {
         const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
-        const uint32_t b0 = row[s], b1 = row[s + 1];
+        const uint32_t b0 = row[bk], b1 = row[bk + 1];
         rstart[tt] = tt * kTile + b0;
         len[q] = b1 - b0;
       }
@@ -449,109 +578,187 @@ __global__ __launch_bounds__(kCT) void k_apply_coord(const uint32_t* __restrict_
       if (tt < tiles) rpre[tt] = run;
       run += len[q];
     }
-    if (t == kCT - 1) rpre[tiles] = run;
+    if (t == kCT2 - 1) rpre[tiles] = run;
     __syncthreads();
   }
   const uint32_t cnt = rpre[tiles];
-  const Emitter em{evbuf, &evn, arena, arena_n, arena_cap};
+  const Emitter em{(LdsEv*)(evbuf + l * kEvLane), kEvLane, arena, arena_n, arena_cap};
+  // the walker lanes (wave 0, lane = slot) keep their state machine's header in registers for the whole launch
+  const uint32_t res = s * (1u << kSbShift) + q0 + l;
   uint8_t* blk = coord + (uint64_t)res * kCoordBlock;
-
-  for (uint32_t c0 = 0; c0 < cnt; c0 += kCCh) {
-    uint32_t m[kCPer], g[kCPer], rk[kCPer];
+  uint32_t type = 0, vm = 0;
+  uint64_t vv = 0;
+  CoordHdr h{};
+  const Ents E{(LdsEnt*)(ecache + l * kECache), (GlbEnt*)ents(blk)};
+  bool uni_type = false;  // wave 0's slots all hold one resource type (wave-uniform)
+  if (w == 0) {
+    type = res_type[res];
+    h = *reinterpret_cast<const CoordHdr*>(blk);
+    if (type == CC_RES_VALUE) {
+      vm = val_meta[res];
+      vv = val_v[res];
+    }
+    E.load();
+    uni_type = __all(type == (uint32_t)__shfl(type, 0, 64)) != 0;
+  }
+  // staging position of list entry c (binary search over the tiles' prefix)
+  auto pos_of = [&](uint32_t c) -> uint32_t {
+    uint32_t lo = 0, hi = tiles;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rpre[mid] <= c) lo = mid; else hi = mid;
+    }
+    return rstart[lo] + (c - rpre[lo]);
+  };
+  uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu, m0 = 0, m1 = 0;
+  auto load_meta = [&](uint32_t c0) {
+    const uint32_t c_0 = c0 + w * (kWave * kCPer2) + l, c_1 = c_0 + kWave;
+    g0 = c_0 < cnt ? pos_of(c_0) : 0xFFFFFFFFu;
+    g1 = c_1 < cnt ? pos_of(c_1) : 0xFFFFFFFFu;
+    m0 = st_meta[g0 != 0xFFFFFFFFu ? g0 : 0];
+    m1 = st_meta[g1 != 0xFFFFFFFFu ? g1 : 0];
+  };
+  load_meta(0);
+  PH(0);
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kCCh2) {
+    // rank this workgroup's commits per slot inside each wave (log order = (wave, j, lane))
+    const uint32_t gg[kCPer2] = {g0, g1}, mm[kCPer2] = {m0, m1};
+    uint32_t sl[kCPer2], rk[kCPer2];
+    bool own[kCPer2];
 #pragma unroll
-    for (int j = 0; j < kCPer; ++j) {
-      const uint32_t c = c0 + w * (kWave * kCPer) + j * kWave + l;
-      g[j] = 0xFFFFFFFFu;
-      if (c < cnt) {
-        uint32_t lo = 0, hi = tiles;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (rpre[mid] <= c) lo = mid; else hi = mid;
-        }
-        g[j] = rstart[lo] + (c - rpre[lo]);
-        m[j] = st_meta[g[j]];
+    for (int j = 0; j < kCPer2; ++j) {
+      sl[j] = ((mm[j] >> 16) & 0xFFu) - q0;
+      own[j] = gg[j] != 0xFFFFFFFFu && sl[j] < (uint32_t)kQ;
+      rk[j] = own[j] ? atomicAdd(&wc[w][sl[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    PH(1);
+    if (w == 0) {  // lane = slot: exclusive prefixes over the waves, then the slot run starts
+      uint32_t acc = 0;
+#pragma unroll
+      for (int q = 0; q < kCW2; ++q) {
+        const uint32_t c = wc[q][l];
+        wc[q][l] = acc;
+        acc += c;
+      }
+      uint32_t inc = acc;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      sstart[l] = inc - acc;
+      if (l == 63) sstart[kQ] = inc;
+    }
+    __syncthreads();
+    PH(2);
+    // gather the owned records into LDS, in slot order
+    {
+      uint32_t p[kCPer2], in[kCPer2];
+      u64x2 ab[kCPer2];
+      uint64_t ky[kCPer2], ix[kCPer2];
+#pragma unroll
+      for (int j = 0; j < kCPer2; ++j) {
+        p[j] = own[j] ? sstart[sl[j]] + wc[w][sl[j]] + rk[j] : 0u;
+        const uint32_t gx = own[j] ? gg[j] : 0u;
+        ab[j] = st_ab[gx];
+        ky[j] = st_key[gx];
+        ix[j] = st_idx[gx];
+        in[j] = st_res[gx];
+      }
+      uint64_t id[kCPer2];
+#pragma unroll
+      for (int j = 0; j < kCPer2; ++j) id[j] = inst_id[own[j] ? in[j] : 0u];
+#pragma unroll
+      for (int j = 0; j < kCPer2; ++j) {
+        if (!own[j]) continue;
+        rab[p[j]] = ab[j];
+        rkey[p[j]] = ky[j];
+        ridx[p[j]] = ix[j];
+        riid[p[j]] = id[j];
+        rmeta[p[j]] = mm[j];
+        rins[p[j]] = in[j];
+        rpos[p[j]] = gg[j];
       }
     }
-    // stable counting sort by slot, one wave at a time (log order = (wave, j, lane))
-    for (uint32_t q = 0; q < kCT / kWave; ++q) {
-      if (w == q) {
-#pragma unroll
-        for (int j = 0; j < kCPer; ++j)
-          if (g[j] != 0xFFFFFFFFu) rk[j] = atomicAdd(&scnt[(m[j] >> 16) & 0xFF], 1u);
-      }
-      __syncthreads();
-    }
-    const uint32_t mine = scnt[t];
-    uint32_t inc = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(inc, d, 64);
-      if (l >= (uint32_t)d) inc += y;
-    }
-    if (l == 63) wsum[w] = inc;
+    load_meta(c0 + kCCh2);  // the next chunk's positions and meta words stream in during the walk
+    for (uint32_t k = t; k < (uint32_t)(kCW2 * kQ); k += kCT2) (&wc[0][0])[k] = 0;  // (read above, before the barrier)
     __syncthreads();
-    uint32_t start = inc - mine;
-    for (uint32_t q = 0; q < w; ++q) start += wsum[q];
-    __syncthreads();
-    scnt[t] = start;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kCPer; ++j) {
-      if (g[j] == 0xFFFFFFFFu) continue;
-      const uint32_t p = scnt[(m[j] >> 16) & 0xFF] + rk[j];
-      rab[p] = st_ab[g[j]];
-      rkey[p] = st_key[g[j]];
-      ridx[p] = st_idx[g[j]];
-      rmeta[p] = m[j];
-      rins[p] = st_res[g[j]];
-      rpos[p] = g[j];
-    }
-    __syncthreads();
-    // this slot's commits, in log order
-    if (mine) {
-      CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
-      uint32_t vm = 0;
-      uint64_t vv = 0;
-      if (type == CC_RES_VALUE) {
-        vm = val_meta[res];
-        vv = val_v[res];
-      }
-      for (uint32_t p = start; p < start + mine; ++p) {
-        const uint32_t mm = rmeta[p];
+    PH(3);
+    // the walk: lane l of wave 0 applies slot q0 + l's commits in log order
+    uint32_t lane_n = 0;  // events this lane published in this chunk
+    if (w == 0) {
+      const uint32_t b = sstart[l], e = sstart[l + 1];
+      auto walk = [&](auto tc) {
+      for (uint32_t p = b; p < e; ++p) {
+        const uint32_t mmr = rmeta[p];
         Rec r;
-        r.op = smeta_op(mm);
-        r.flags = smeta_flags(mm);
+        r.op = smeta_op(mmr);
+        r.flags = smeta_flags(mmr);
         r.inst = rins[p];
         r.g = rpos[p];
         r.a = rab[p].x;
         r.b = rab[p].y;
         r.key = rkey[p];
         r.idx = ridx[p];
-        r.iid = inst_id[r.inst];
+        r.iid = riid[p];
         uint64_t rv;
         uint32_t nev = 0;
-        const uint32_t st = coord_apply(type, r, h, blk, vm, vv, rv, nev, em, err);
-        rst_status[r.g] = (uint8_t)st;
-        rst_value[r.g] = rv;
-        ev_cnt[r.g] = (uint16_t)nev;
+        const uint32_t st = coord_apply<decltype(tc)::value>(type, r, h, E, vm, vv, rv, nev, em, lane_n, err);
+        ost[p] = (uint8_t)st;
+        oval[p] = rv;
+        oev[p] = (uint16_t)nev;
       }
-      *reinterpret_cast<CoordHdr*>(blk) = h;
-      if (type == CC_RES_VALUE) {
-        val_meta[res] = vm;
-        val_v[res] = vv;
+      };
+      if (!uni_type) walk(TypeC<0>{});
+      else if (type == CC_RES_LOCK) walk(TypeC<CC_RES_LOCK>{});
+      else if (type == CC_RES_ELECTION) walk(TypeC<CC_RES_ELECTION>{});
+      else if (type == CC_RES_GROUP) walk(TypeC<CC_RES_GROUP>{});
+      else if (type == CC_RES_VALUE) walk(TypeC<CC_RES_VALUE>{});
+      else walk(TypeC<0>{});
+      // this chunk's event regions: exclusive prefix of the lanes' (capped) counts, one arena reservation
+      const uint32_t mine = lane_n < (uint32_t)kEvLane ? lane_n : (uint32_t)kEvLane;
+      uint32_t inc = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      evoff[l] = inc - mine;
+      if (l == 63) {
+        evoff[kQ] = inc;
+        evbase = inc ? atomicAdd(arena_n, (unsigned long long)inc) : 0ull;
       }
     }
     __syncthreads();
-    // flush the chunk's events: one arena reservation per chunk
-    const uint32_t nb = evn < (uint32_t)kEvBuf ? evn : (uint32_t)kEvBuf;
-    if (t == 0) evbase = nb ? atomicAdd(arena_n, (unsigned long long)nb) : 0ull;
+    for (uint32_t p = t; p < sstart[kQ]; p += kCT2) {  // results to the records' staging positions
+      const uint32_t gp = rpos[p];
+      rst_status[gp] = ost[p];
+      rst_value[gp] = oval[p];
+      ev_cnt[gp] = oev[p];
+    }
+    PH(4);
+    // flush the chunk's events (their order in the arena is free: events.hip sorts by (row, emission index))
+    const uint32_t nb = evoff[kQ];
+    for (uint32_t q = t; q < nb; q += kCT2) {
+      uint32_t lo = 0, hi = kQ;  // lane whose region holds q: evoff[lo] <= q < evoff[lo + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (evoff[mid] <= q) lo = mid; else hi = mid;
+      }
+      if (evbase + q < arena_cap) arena[evbase + q] = evbuf[lo * kEvLane + (q - evoff[lo])];
+    }
     __syncthreads();
-    for (uint32_t q = t; q < nb; q += kCT)
-      if (evbase + q < arena_cap) arena[evbase + q] = evbuf[q];
-    __syncthreads();
-    scnt[t] = 0;
-    if (t == 0) evn = 0;
-    __syncthreads();
+    PH(5);
+  }
+  PH_FLUSH(g_ph_coord);
+  if (w == 0) {
+    E.store();
+    *reinterpret_cast<CoordHdr*>(blk) = h;
+    if (type == CC_RES_VALUE) {
+      val_meta[res] = vm;
+      val_v[res] = vv;
+    }
   }
   if (err) atomicOr(err_out, err);
 }
@@ -574,8 +781,8 @@ __global__ void k_clock_advance(const uint64_t* __restrict__ time, uint64_t n, u
 int launch_apply_coord(const CoordArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_APPLY_COORD, 1, st);
-  hipLaunchKernelGGL(k_apply_coord, dim3(a.sb_val), dim3(kCT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
-                     a.ttab, a.tiles, a.sb, a.sb_kind, a.res_type, a.inst_id, a.coord, a.val_meta, a.val_v, a.rst_status,
+  hipLaunchKernelGGL(k_apply_coord, dim3(a.sb_val * kQPerSb), dim3(kCT2), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
+                     a.ttab, a.tiles, a.sb, a.sbq_base, a.sb_kind, a.res_type, a.inst_id, a.coord, a.val_meta, a.val_v, a.rst_status,
                      a.rst_value, a.ev_cnt, a.arena, a.arena_n, a.arena_cap, a.err);
   a.mark(K_APPLY_COORD, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

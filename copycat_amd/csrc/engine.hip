@@ -117,6 +117,8 @@ static int ensure_ext(cc_engine* e, bool coord) {
     hipError_t x = hipMemset(e->d_coord, 0, kCoordBlock * slots);
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
+    // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
+    e->quarter = tile_lds_bytes(e->sbq_base() + 4 * e->sb, true, kChunkMaps) <= 160u * 1024u;
   }
   return CC_OK;
 }
@@ -194,7 +196,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_st_meta, sizeof(uint32_t) * (e->sub_batch + kPT));  // + dummy rows for unconditional stores
   ALLOC(e->d_st_ab, sizeof(u64x2) * (e->sub_batch + kPT));
   ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
-  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sb_total() + 1));
+  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sbq_base() + 4 * e->sb + 1));
   if (e->map_bits) {
     ALLOC(e->d_tbl_key, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_tbl_word, sizeof(uint32_t) * e->map_entries);
@@ -625,6 +627,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.max_inst = e->cfg.max_instances;
     pa.sb = e->sb_total();
     pa.sb_val = e->sb;
+    pa.sbq_base = e->quarter ? e->sbq_base() : 0u;
     pa.map_bits = e->map_bits;
     pa.hot = e->d_hot;
     pa.hot_n = e->d_hot_n;
@@ -703,6 +706,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.tiles = tiles;
       ca.sb = e->sb_total();
       ca.sb_val = e->sb;
+      ca.sbq_base = e->quarter ? e->sbq_base() : 0u;
       ca.sb_kind = e->d_sb_kind;
       ca.res_type = e->d_res_type;
       ca.inst_id = e->d_inst_id;

@@ -40,6 +40,7 @@ struct PartArgs {
   uint32_t sb;        // super-buckets in total = sb_val + 2^map_bits (0 map bits: no maps)
   uint32_t sb_val;
   uint32_t map_bits;
+  uint32_t sbq_base;  // non-zero: commits of super-buckets run by k_apply_coord go to quarter buckets sbq_base + slot/64
   const HotKey* hot;  // hot map keys of this sub-batch (maps only)
   const uint32_t* hot_n;
   uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
@@ -196,6 +197,7 @@ struct CoordArgs {
   const uint64_t* st_idx;
   const uint16_t* ttab;
   uint32_t tiles, sb, sb_val;
+  uint32_t sbq_base;       // non-zero: the quarter buckets of the partition (else each workgroup filters its quarter)
   const uint8_t* sb_kind;
   const uint8_t* res_type;
   const uint64_t* inst_id;

@@ -76,7 +76,11 @@ struct cc_engine {
   uint32_t sb = 0, sb_bits = 0;  // value super-buckets of 256 slots
   uint32_t map_bits = 0;         // 2^map_bits map table regions follow them (0: no maps)
   uint64_t map_entries = 0;
-  uint32_t sb_total() const { return sb + (map_bits ? (1u << map_bits) + kHotMax : 0u); }
+  // buckets of the partition: value super-buckets, map regions + hot keys, then (coordination on, when the partition's
+  // LDS allows) one bucket per quarter super-bucket (64 slots) for every super-bucket run by k_apply_coord
+  bool quarter = false;
+  uint32_t sbq_base() const { return sb + (map_bits ? (1u << map_bits) + kHotMax : 0u); }
+  uint32_t sb_total() const { return sbq_base() + (quarter ? 4 * sb : 0u); }
   uint64_t sub_batch = 0, max_tiles = 0;
   // host mirrors of the registry
   std::vector<uint8_t> res_type;     // [sb*256]

@@ -150,6 +150,7 @@ __global__ __launch_bounds__(kPT, CC_PART_WPE) void k_part_tile(const uint32_t* 
                                                 uint32_t ext_flags, uint64_t lo, uint64_t hi,
                                                 const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
                                                 const uint8_t* __restrict__ sb_kind, uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits,
+                                                uint32_t sbq_base,
                                                 const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n,
                                                 uint32_t* __restrict__ st_meta, u64x2* __restrict__ st_ab,
                                                 uint32_t* __restrict__ st_res, uint64_t* __restrict__ st_key,
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(kPT, CC_PART_WPE) void k_part_tile(const uint32_t* 
       }
       return sb_val + (uint32_t)(h >> (64 - map_bits));
     }
+    if (EXT && sbq_base && sb_kind[r >> kSbShift]) return sbq_base + (r >> 6);  // quarter bucket (k_apply_coord)
     return r >> kSbShift;
   };
   auto hist_add = [&](uint32_t k) { atomicAdd(&ctot32[k >> 1], 1u << (16 * (k & 1))); };
@@ -529,9 +531,11 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
 
 int phase_read_value(uint64_t* out);
 int phase_read_partv(uint64_t* out);
+int phase_read_coord(uint64_t* out);
 int phase_read(int kernel, uint64_t* out) {
 #ifdef CC_PHASE_TIMING
   if (kernel == K_APPLY_VALUE) return phase_read_value(out);
+  if (kernel == K_APPLY_COORD) return phase_read_coord(out);
   if (kernel == K_PART_TILE && getenv("CC_PART_VALUE")) return phase_read_partv(out);  // the value partition
   unsigned long long z[kPhases] = {};
   if (kernel != K_UNPERMUTE && kernel != K_PART_TILE) return CC_ERR_INVALID;
@@ -562,11 +566,11 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   } else if (!ext) {
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, kChunk), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+                       a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   } else {
     hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+                       a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   }
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -320,16 +320,28 @@ uint64_t wl_map_random(uint64_t n, uint32_t maps, uint32_t first_inst, uint32_t 
 // lock/unlock with timeouts {-1, 0, 1..40 ms}; listen/unlisten/isLeader; join/leave/execute(member = an
 // instance id of that group, callback = handle); value get/set/CAS/getAndSet/listen/unlisten.  Rare Delete,
 // ops of other types (UNKNOWN_OP) and unknown instance slots.  Time = 1 + index / 8 ms (non-decreasing).
-uint64_t wl_coord_random(uint64_t n, uint32_t R, uint32_t K, const uint8_t* types, uint32_t max_inst, uint64_t seed,
-                         uint32_t p_delete_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
-                         uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b, uint64_t* aux) {
+// The lock client model of wl_coord_random, kept across calls (a bench applies one step's stream after another).
+struct CoordModel {
+  struct Waiter { uint32_t k; uint64_t deadline; };
+  std::vector<int32_t> holder;
+  std::vector<std::vector<Waiter>> queue;
+  explicit CoordModel(uint32_t R) : holder(R, -1), queue(R) {}
+};
+void* wl_coord_model_new(uint32_t R) { return new CoordModel(R); }
+void wl_coord_model_free(void* m) { delete static_cast<CoordModel*>(m); }
+
+uint64_t wl_coord_random_model(void* model, uint64_t n, uint32_t R, uint32_t K, const uint8_t* types, uint32_t max_inst,
+                               uint64_t seed, uint32_t p_delete_ppm, uint64_t index0, uint64_t* index, uint64_t* time,
+                               uint32_t* inst, uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b,
+                               uint64_t* aux) {
   SplitMix64 rng(seed);
   // client model for locks (so a waiter queue never exceeds K): a holder unlocks, a waiter sends unlock (fails:
   // not the holder), anyone else locks.  Tracks LockState exactly, timeouts included (either timer order:
   // the model removes a waiter once its deadline has passed, before the instance's next request).
-  struct Waiter { uint32_t k; uint64_t deadline; };
-  std::vector<int32_t> holder(R, -1);
-  std::vector<std::vector<Waiter>> queue(R);
+  using Waiter = CoordModel::Waiter;
+  CoordModel& M = *static_cast<CoordModel*>(model);
+  std::vector<int32_t>& holder = M.holder;
+  std::vector<std::vector<Waiter>>& queue = M.queue;
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t r = (uint32_t)rng.below(R), k = (uint32_t)rng.below(K);
     const uint64_t now = 1 + (index0 + i) / 8;
@@ -399,6 +411,14 @@ uint64_t wl_coord_random(uint64_t n, uint32_t R, uint32_t K, const uint8_t* type
     if (aux) aux[i] = ax;
   }
   return n;
+}
+
+uint64_t wl_coord_random(uint64_t n, uint32_t R, uint32_t K, const uint8_t* types, uint32_t max_inst, uint64_t seed,
+                         uint32_t p_delete_ppm, uint64_t index0, uint64_t* index, uint64_t* time, uint32_t* inst,
+                         uint8_t* op, uint8_t* flags, uint64_t* key, uint64_t* a, uint64_t* b, uint64_t* aux) {
+  CoordModel m(R);
+  return wl_coord_random_model(&m, n, R, K, types, max_inst, seed, p_delete_ppm, index0, index, time, inst, op, flags, key,
+                               a, b, aux);
 }
 
 // Config 3 stream: DistributedMap put/get/remove (45/45/10) over `pairs` (power of two) distinct

@@ -33,6 +33,12 @@ def lib():
         L.wl_map_random.argtypes = [u64, u32, u32, u32, u32, u64, u32, u32, u64] + [P] * 9 + [u32]
         L.wl_coord_random.restype = u64
         L.wl_coord_random.argtypes = [u64, u32, u32, P, u32, u64, u32, u64] + [P] * 9
+        L.wl_coord_model_new.restype = P
+        L.wl_coord_model_new.argtypes = [u32]
+        L.wl_coord_model_free.restype = None
+        L.wl_coord_model_free.argtypes = [P]
+        L.wl_coord_random_model.restype = u64
+        L.wl_coord_random_model.argtypes = [P, u64, u32, u32, P, u32, u64, u32, u64] + [P] * 9
         L.wl_map_zipf.restype = u64
         L.wl_map_zipf.argtypes = [u64, u64, u32, u32, C.c_double, u32, u64, u32] + [P] * 8
         _LIB = L
@@ -113,6 +119,38 @@ def coord_random_stream(n, types, K, max_inst, seed=1, p_delete=0.0005, index0=1
     return b
 
 
+class CoordClients:
+    """The coordination stream of coord_random_stream continued across calls (the lock client model carries over), so
+    a bench applies one step's batch after another without replaying a stream on state it no longer matches."""
+
+    def __init__(self, types, K=1, max_inst=None, seed=1, p_delete=0.0005):
+        self.types = np.ascontiguousarray(types, np.uint8)
+        self.K = K
+        self.max_inst = max_inst if max_inst is not None else len(self.types) * K
+        self.seed = seed
+        self.p_delete = p_delete
+        self.index0 = 1
+        self.step = 0
+        self.h = lib().wl_coord_model_new(len(self.types))
+
+    def __del__(self):
+        try:
+            lib().wl_coord_model_free(self.h)
+        except Exception:
+            pass
+
+    def next(self, n, out=None):
+        b = out if out is not None else Batch(n)
+        got = lib().wl_coord_random_model(self.h, n, len(self.types), self.K, _p(self.types), self.max_inst,
+                                          self.seed + 0x51ED * self.step, int(self.p_delete * 1e6), self.index0,
+                                          _p(b.index), _p(b.time), _p(b.inst), _p(b.op), _p(b.flags), _p(b.key),
+                                          _p(b.a), _p(b.b), _p(b.aux))
+        assert got == n
+        self.index0 += n
+        self.step += 1
+        return b
+
+
 SEED_C3 = 0xA700000 + 3
 
 
@@ -149,4 +187,4 @@ def expiry_sessions(sessions, timeout=5000, now=10_000_000, seed=SEED_C4 + 1):
     return last, now, timeout
 
 
-__all__ = ["atomic_long_stream", "AtomicLongClients", "value_random_stream", "map_random_stream", "map_zipf_rows", "quorum_groups", "expiry_sessions", "abi"]
+__all__ = ["atomic_long_stream", "AtomicLongClients", "CoordClients", "value_random_stream", "map_random_stream", "map_zipf_rows", "quorum_groups", "expiry_sessions", "abi"]

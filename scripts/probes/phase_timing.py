@@ -20,6 +20,7 @@ PHASES = {
     0: ["histogram+row", "rank+wait", "wave-prefix", "exscan", "place", "write-out", "top(clear,issue)", "-"],
     1: ["setup", "rank+wait", "wave-prefix", "slot-scan", "place", "walk", "result-store", "-"],
     2: ["load", "scatter", "-", "-", "-", "-", "-", "-"],
+    5: ["setup", "rank+wait", "slot-scan", "gather", "walk", "event-flush", "-", "-"],
 }
 
 
@@ -29,7 +30,7 @@ def build():
 
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC",
-           "-shared", "-DCC_PHASE_TIMING", *b.ENGINE_SRCS, "-o", OUT]
+           "-shared", "-DCC_PHASE_TIMING", *os.environ.get("PHASE_DEFS", "").split(), *b.ENGINE_SRCS, "-o", OUT]
     subprocess.run(cmd, cwd=b.CSRC, check=True)
     print(OUT)
 
@@ -43,6 +44,8 @@ def run(args):
     from copycat_amd.engine import DeviceBatch, Engine, lib
     from copycat_amd.workload import SEED_C2, atomic_long_stream
 
+    if args.c5:
+        return run_c5(args)
     n, R = args.commits, 65536
     b = atomic_long_stream(n, resources=R, seed=SEED_C2, index0=1)
     db = DeviceBatch.upload(b, device="cuda:0", columns=("index", "inst", "op", "flags", "a", "b"))
@@ -83,11 +86,60 @@ def run(args):
                 print(f"   {PHASES[k][q]:18s} {ticks[q] * 10e-3 / wgs[k]:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
 
 
+def run_c5(args):
+    """The coordination kernel on bench.py's c5 stream (32,768 resources, a third each lock/election/group)."""
+    import numpy as np
+    import torch
+
+    from copycat_amd import abi
+    from copycat_amd.engine import DeviceBatch, DeviceEvents, Engine, lib
+    n, R = args.commits, 32768
+    kinds = {"L": abi.CC_RES_LOCK, "E": abi.CC_RES_ELECTION, "G": abi.CC_RES_GROUP}
+    tl = [kinds[c] for c in args.types]
+    types = np.resize(np.array(tl, np.uint8), R) if args.interleave else np.repeat(np.array(tl, np.uint8), (R + len(tl) - 1) // len(tl))[:R]
+    from copycat_amd.workload import CoordClients
+
+    clients = CoordClients(types, K=1, max_inst=R, seed=0xA700000 + 5)
+    dbs = [DeviceBatch.upload(clients.next(n), device="cuda:0") for _ in range(args.steps + 1)]
+    db = dbs[0]
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    va = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    evs = DeviceEvents(2 * n, device="cuda:0")
+    E = Engine(R, R, n, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=2 * n)
+    for r in range(R):
+        E.resource_create(r, int(types[r]))
+    E.instance_open_range(0, R, 0, 1000, 1)
+    L = lib()
+    ticks = (C.c_uint64 * 8)()
+    E.apply_events(db, st, va, evs)
+    E.sync()
+    L.cc_debug_phases(E.h, 5, ticks)
+    E.profile(True)
+    for k in range(args.steps):
+        E.apply_events(dbs[k + 1], st, va, evs)
+    E.sync()
+    prof = E.profile_read()
+    L.cc_debug_phases(E.h, 5, ticks)
+    sub = args.sub_batch or (16 << 20)
+    launches = args.steps * ((n + sub - 1) // sub)
+    wgs = (R // 256) * 4 * launches
+    tot = sum(ticks)
+    ms, nl = prof.get("k_apply_coord", (0.0, 0))
+    print(f"[{args.types}] k_apply_coord: {ms / max(nl, 1) * 1e3:.1f} us/launch, workgroups {wgs}, per-WG mean {tot * 10e-3 / wgs:.2f} us")
+    for q in range(8):
+        if ticks[q]:
+            print(f"   {PHASES[5][q]:18s} {ticks[q] * 10e-3 / wgs:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
+    print({k: round(v[0] / args.steps, 3) for k, v in prof.items()})
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--commits", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--sub-batch", type=int, default=0)
+    ap.add_argument("--c5", action="store_true", help="the coordination kernel on the c5 stream")
+    ap.add_argument("--interleave", action="store_true", help="--c5: slot r holds type r %% len(types)")
+    ap.add_argument("--types", default="LEG", help="--c5: resource types in thirds (L lock, E election, G group)")
     a = ap.parse_args()
     build() if a.build else run(a)
