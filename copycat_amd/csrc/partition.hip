@@ -556,6 +556,7 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   const bool ext = a.ext;
   a.mark(K_PART_TILE, 1, st);
   static const bool part_value = getenv("CC_PART_VALUE") != nullptr;  // experiment: persistent value partition
+  static const bool part_tile_v1 = getenv("CC_PART_V1") != nullptr;   // A/B: the previous value partition
   if (!ext && part_value) {  // tile histograms, then the persistent value partition (partition_value.hip)
     if (a.res16) {
       if (launch_tile_hist16(a, tiles, st)) return -1;
@@ -563,6 +564,8 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
       hipLaunchKernelGGL(k_tile_hist, dim3(tiles), dim3(kHT), 0, st, a.inst, a.lo, a.hi, a.inst_res, a.max_inst, a.sb, a.ttab);
     }
     if (launch_part_value(a, tiles, st)) return -1;
+  } else if (!ext && !part_tile_v1) {  // value-only engines: partition_value.hip k_part_v2
+    if (launch_part_v2(a, tiles, st)) return -1;
   } else if (!ext) {
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, kChunk), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,

@@ -256,6 +256,195 @@ __global__ __launch_bounds__(kPT) void k_part_value(const uint32_t* __restrict__
   PH_FLUSH(g_ph_partv);
 }
 
+// ---- k_part_v2: the default value-only partition (one 1024-thread workgroup per 16384-commit tile) ----------------
+// Differences from k_part_tile<4, false>: every thread loads the instance column of all 16 of its tile commits (the
+// chunk mapping (chunk, wave, j, lane)) and chunk 0's raw columns before anything waits, resolves the 16 instances
+// with one batch of gathers, builds the tile histogram from those registers and keeps the resolved resources for the
+// chunks (the instance column is read once and gathered once per commit); the 4 chunks are unrolled (their
+// registers stay registers); the per-chunk wave prefixes, chunk totals and run starts are one wave's work (no block
+// scan), so a chunk has 4 barriers.
+constexpr int kV2J = 4;                   // commits per thread per chunk
+constexpr int kV2C = kV2J * kPT;          // 4096 commits per chunk
+constexpr int kV2N = kTile / kV2C;        // 4 chunks per tile
+
+template <int KP>
+__global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
+                                                 const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
+                                                 const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
+                                                 uint32_t* __restrict__ st_meta, u64x2* __restrict__ st_ab,
+                                                 uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab) {
+  __shared__ uint4 rab[kV2C];                  // the chunk in sorted order: encoded operands
+  __shared__ uint32_t rmeta[kV2C];             //   meta word (value_encode | slot-in-super-bucket << 16)
+  __shared__ uint16_t rsb[kV2C];               //   super-bucket
+  __shared__ uint32_t wc[kPW][kMaxSb / 2];     // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
+  __shared__ uint32_t hist[kMaxSb / 2];        // tile histogram (packed u16 pairs)
+  __shared__ uint16_t tpos[kMaxSb];            // tile-local position of run k's next piece
+  __shared__ uint16_t kst[kMaxSb];             // chunk-sorted start of run k
+  __shared__ uint32_t nlive_s;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint32_t hw = (sb + 1) / 2;
+  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
+  const uint32_t tbase = blockIdx.x * kTile;  // staging region of this tile (relative to lo)
+  for (uint32_t k = t; k < hw; k += kPT) hist[k] = 0;
+  for (uint32_t k = t; k < (uint32_t)(kPW * (kMaxSb / 2)); k += kPT) (&wc[0][0])[k] = 0;
+  // commit (c, w, j, l) of the tile: tile0 + c*4096 + w*256 + j*64 + l (log order)
+  auto row_of = [&](int c, int j) -> uint64_t { return tile0 + (uint64_t)c * kV2C + (uint64_t)w * (kWave * kV2J) + (uint64_t)j * kWave + l; };
+  uint32_t r[kV2N][kV2J];
+#pragma unroll
+  for (int c = 0; c < kV2N; ++c)
+#pragma unroll
+    for (int j = 0; j < kV2J; ++j) {
+      const uint64_t i = row_of(c, j);
+      r[c][j] = i < hi ? inst[i] : kNoRes;
+    }
+  uint8_t ob[kV2J], fb[kV2J];
+  uint64_t av[kV2J], bv[kV2J];
+  auto load_raw = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < kV2J; ++j) {
+      const uint64_t i = row_of(c, j), ic = i < hi ? i : lo;
+      ob[j] = op[ic];
+      fb[j] = flags[ic];
+      av[j] = ca[ic];
+      bv[j] = cb[ic];
+    }
+  };
+  load_raw(0);
+#pragma unroll
+  for (int c = 0; c < kV2N; ++c)
+#pragma unroll
+    for (int j = 0; j < kV2J; ++j) r[c][j] = r[c][j] < max_inst ? inst_res[r[c][j]] : kNoRes;
+  lds_barrier();  // hist / wc zeroed
+#pragma unroll
+  for (int c = 0; c < kV2N; ++c)
+#pragma unroll
+    for (int j = 0; j < kV2J; ++j)
+      if (r[c][j] != kNoRes) {
+        const uint32_t k = r[c][j] >> kSbShift;
+        atomicAdd(&hist[k >> 1], 1u << (16 * (k & 1)));
+      }
+  lds_barrier();
+  if (w == 0) {  // tile-local run starts: one wave, lane l owns super-buckets [l*KP, l*KP + KP)
+    uint32_t cnt[KP], mine = 0;
+#pragma unroll
+    for (int e = 0; e < KP; ++e) {
+      const uint32_t k = l * KP + e;
+      cnt[e] = k < sb ? (hist[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : 0u;
+      mine += cnt[e];
+    }
+    uint32_t inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    uint32_t run = inc - mine;
+    uint16_t* row = ttab + (uint64_t)blockIdx.x * (sb + 1);
+#pragma unroll
+    for (int e = 0; e < KP; ++e) {
+      const uint32_t k = l * KP + e;
+      if (k < sb) {
+        tpos[k] = (uint16_t)run;
+        row[k] = (uint16_t)run;
+      }
+      run += cnt[e];
+    }
+    if (l == 63) row[sb] = (uint16_t)inc;  // live commits of the tile (<= 16384)
+  }
+  // (tpos is first read after the next barrier)
+#pragma unroll
+  for (int c = 0; c < kV2N; ++c) {
+    // encode and rank this chunk's records (registers: loaded one chunk ahead); then the next chunk's loads
+    uint32_t sk[kV2J], loc[kV2J], mt[kV2J];
+    uint4 xy4[kV2J];
+#pragma unroll
+    for (int j = 0; j < kV2J; ++j) {
+      const bool live = r[c][j] != kNoRes;
+      u64x2 xy;
+      value_encode(ob[j], fb[j], av[j], bv[j], mt[j], xy);
+      mt[j] |= (r[c][j] & ((1u << kSbShift) - 1)) << 16;
+      xy4[j] = make_uint4((uint32_t)xy.x, (uint32_t)(xy.x >> 32), (uint32_t)xy.y, (uint32_t)(xy.y >> 32));
+      sk[j] = live ? (r[c][j] >> kSbShift) : 0u;
+      const uint32_t sh = 16 * (sk[j] & 1);
+      loc[j] = live ? (atomicAdd(&wc[w][sk[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
+    }
+    if (c + 1 < kV2N) load_raw(c + 1);
+    lds_barrier();
+    if (w == 0) {  // per super-bucket: exclusive prefix over the waves (in place), chunk totals, chunk-sorted starts
+      uint32_t tot[KP];
+#pragma unroll
+      for (int e = 0; e < KP; e += 2) {
+        const uint32_t pr = (l * KP + e) / 2;
+        uint32_t acc = 0;
+        if (pr < hw) {
+#pragma unroll
+          for (int q = 0; q < kPW; ++q) {
+            const uint32_t x = wc[q][pr];
+            wc[q][pr] = acc;
+            acc += x;
+          }
+        }
+        tot[e] = acc & 0xFFFFu;
+        tot[e + 1] = acc >> 16;
+      }
+      uint32_t mine = 0;
+#pragma unroll
+      for (int e = 0; e < KP; ++e) mine += tot[e];
+      uint32_t inc = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      uint32_t ks = inc - mine;
+#pragma unroll
+      for (int e = 0; e < KP; ++e) {
+        const uint32_t k = l * KP + e;
+        if (k < sb) kst[k] = (uint16_t)ks;
+        ks += tot[e];
+      }
+      if (l == 63) nlive_s = inc;
+    }
+    lds_barrier();
+    // place the records in sorted order; every commit's tile-local position (0xFFFF: unknown instance)
+#pragma unroll
+    for (int j = 0; j < kV2J; ++j) {
+      const uint64_t i = row_of(c, j);
+      uint32_t cp = 0xFFFFu;
+      if (loc[j] != 0xFFFFu) {
+        const uint32_t k = sk[j];
+        const uint32_t pre = (wc[w][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        const uint32_t sp = kst[k] + pre + loc[j];
+        rab[sp] = xy4[j];
+        rmeta[sp] = mt[j];
+        rsb[sp] = (uint16_t)k;
+        cp = tpos[k] + pre + loc[j];
+      }
+      if (i < hi) cpos[i - lo] = (uint16_t)cp;
+    }
+    lds_barrier();
+    // write the chunk out run by run (contiguous); the next chunk's counters are cleared behind the reads
+    const uint32_t nl = nlive_s;
+    for (uint32_t sp = t; sp < nl; sp += kPT) {
+      const uint32_t k = rsb[sp];
+      const uint32_t g = tbase + tpos[k] + (sp - kst[k]);
+      st_meta[g] = rmeta[sp];
+      reinterpret_cast<uint4*>(st_ab)[g] = rab[sp];
+    }
+    for (uint32_t k = t; k < (uint32_t)(kPW * hw); k += kPT) wc[k / hw][k % hw] = 0;
+    lds_barrier();
+    if (w == 0) {  // run k's next piece starts after this chunk's records of k
+#pragma unroll
+      for (int e = 0; e < KP; ++e) {
+        const uint32_t k = l * KP + e;
+        if (k < sb) tpos[k] = (uint16_t)(tpos[k] + ((k + 1 < sb ? kst[k + 1] : nl) - kst[k]));
+      }
+    }
+    // (tpos is next read after the next chunk's first barrier)
+  }
+}
+
 // inst_res (u32, kNoRes = closed) -> a u16 copy for k_tile_hist16's LDS table (0xFFFF = closed), padded to 8.
 __global__ void k_res16_table(const uint32_t* __restrict__ inst_res, uint32_t n, uint32_t npad, uint16_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -337,6 +526,19 @@ int launch_tile_hist16(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   const uint32_t grid = tiles < (uint32_t)kPersistGrid ? tiles : (uint32_t)kPersistGrid;
   hipLaunchKernelGGL(k_tile_hist16, dim3(grid), dim3(kHT16), 0, st, a.inst, a.lo, a.hi, tiles, (const uint16_t*)a.inst_res16,
                      npad, a.sb, a.ttab, a.res16);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_part_v2(const PartArgs& a, uint32_t tiles, hipStream_t st) {
+  const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
+  if (a.sb > (uint32_t)kMaxSb) return -1;
+#define CC_LAUNCH(KP)                                                                                                 \
+  hipLaunchKernelGGL((k_part_v2<KP>), dim3(tiles), dim3(kPT), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,      \
+                     a.inst_res, a.max_inst, a.sb, a.st_meta, a.st_ab, a.cpos, a.ttab)
+  if (kp <= 2) CC_LAUNCH(2);
+  else if (kp <= 4) CC_LAUNCH(4);
+  else CC_LAUNCH(8);
+#undef CC_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
