@@ -63,6 +63,11 @@ B_OP_C5 = 48  # 26 in + 9 out + ~1 event x 13 B
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+# the kernels behind each cc_profile marker (the value-only partition is k_part_v2; engines with maps, coordination
+# or value events use k_part_tile)
+MARKER_KERNELS = {"k_part_tile": ("k_part_v2", "k_part_tile"), "k_events": ("k_ev_rows", "k_ev_scatter")}
+
+
 def pmc_traffic(kernel, workload):
     """HBM-side bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of the same
     bench command (scripts/pmc_traffic.py -> profiles/traffic_latest.json; counters cannot be read in-process)."""
@@ -72,7 +77,11 @@ def pmc_traffic(kernel, workload):
             d = json.load(f)
         if d.get("workload", "c2") != workload:
             return None
-        return d["kernels"][kernel]["bytes_per_launch"] / 1e9
+        ks = d["kernels"]
+        for name in MARKER_KERNELS.get(kernel, (kernel,)):
+            if name in ks:
+                return ks[name]["bytes_per_launch"] / 1e9
+        return None
     except (OSError, KeyError, ValueError):
         return None
 
