@@ -130,7 +130,17 @@ struct Resource {
   LockSM l;
   ElectionSM e;
   GroupSM g;
-  std::deque<TV> q;  // QueueState.queue: ArrayDeque of commits, here their values (QueueState.java:33)
+  // QueueState.queue: ArrayDeque of commits (QueueState.java:33): value, index, and whether element() already
+  // clean()ed the head commit it did not remove (:111-124)
+  struct QEnt {
+    TV v;
+    uint64_t idx = 0;
+    bool cleaned = false;
+  };
+  std::deque<QEnt> q;
+  // commits dropped without clean(): retained by the log for good (AtomicValueState.listen re-put :42,
+  // MembershipGroupState.close :37-38)
+  std::vector<uint64_t> leaked;
 };
 
 struct Inst {  // ResourceManager.SessionHolder + ManagedResourceSession
@@ -342,7 +352,11 @@ struct orc {
         return true;
       }
       case CC_RES_GROUP: {  // MembershipGroupState.close :36-42 — publishes leave even for non-members (A10)
-        r.g.members.erase(in.id);
+        auto mit = r.g.members.find(in.id);  // members.remove without clean(): the join commit is never released
+        if (mit != r.g.members.end()) {
+          r.leaked.push_back(mit->second.index);
+          r.g.members.erase(mit);
+        }
         for (auto& kv : r.g.members) publish(kv.second.inst, CC_EV_LEAVE, tv(CC_TAG_LONG, in.id));
         return true;
       }
@@ -416,7 +430,12 @@ struct orc {
           }
           case CC_OP_VALUE_LISTEN: {  // listen :41-49 (listeners.put(session, commit))
             bool found = false;
-            for (auto& p : s.listeners) if (p.first == c.inst) { p.second = c.index; found = true; }
+            for (auto& p : s.listeners)
+              if (p.first == c.inst) {  // listeners.put replaces the session's commit without clean()ing it
+                r.leaked.push_back(p.second);
+                p.second = c.index;
+                found = true;
+              }
             if (!found) s.listeners.emplace_back(c.inst, c.index);
             ret(CC_ST_OK, TV());
             return;
@@ -561,8 +580,8 @@ struct orc {
         auto& q = r.q;
         auto first_match = [&](size_t& at) -> int {  // 1 match, 0 none, -1 NPE (a stored null's equals)
           for (size_t i = 0; i < q.size(); ++i) {
-            if (tv_null(q[i])) return -1;
-            if (tv_equals(q[i], a)) { at = i; return 1; }
+            if (tv_null(q[i].v)) return -1;
+            if (tv_equals(q[i].v, a)) { at = i; return 1; }
           }
           return 0;
         };
@@ -576,20 +595,21 @@ struct orc {
           }
           case CC_OP_QUEUE_ADD:    // add :51-59 (returns false)
           case CC_OP_QUEUE_OFFER:  // offer :64-72 (returns false)
-            q.push_back(a);
+            q.push_back(Resource::QEnt{a, c.index, false});
             ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
             return;
           case CC_OP_QUEUE_PEEK:  // peek :77-87
-            ret(CC_ST_OK, q.empty() ? TV() : q.front());
+            ret(CC_ST_OK, q.empty() ? TV() : q.front().v);
             return;
           case CC_OP_QUEUE_POLL:  // poll :92-105
             if (q.empty()) { ret(CC_ST_OK, TV()); return; }
-            ret(CC_ST_OK, q.front());
+            ret(CC_ST_OK, q.front().v);
             q.pop_front();
             return;
           case CC_OP_QUEUE_ELEMENT:  // element :111-124 — ArrayDeque.element throws when empty; does not remove
             if (q.empty()) { ret(CC_ST_NO_SUCH_ELEMENT, TV()); return; }
-            ret(CC_ST_OK, q.front());
+            ret(CC_ST_OK, q.front().v);
+            q.front().cleaned = true;  // value.clean() on the head it leaves in place
             return;
           case CC_OP_QUEUE_REMOVE: {  // remove :130-157
             if (!tv_null(a)) {
@@ -601,7 +621,7 @@ struct orc {
               return;
             }
             if (q.empty()) { ret(CC_ST_NO_SUCH_ELEMENT, TV()); return; }  // ArrayDeque.remove()
-            ret(CC_ST_OK, q.front());
+            ret(CC_ST_OK, q.front().v);
             q.pop_front();
             return;
           }
@@ -1025,6 +1045,46 @@ int orc_read_value_retained(orc* o, uint32_t first, uint32_t count, uint64_t* in
     index[i] = r.exists && r.type == CC_RES_VALUE && r.v.has_current ? r.v.current.index : 0;
   }
   return CC_OK;
+}
+
+// Every commit the resource's state machine holds without having clean()ed it (the log cannot compact them), as
+// ascending log indices; -1: no resource in the slot.  AtomicValueState current :88-109 + listeners :41-63 (+ re-put
+// leaks); MapState / SetState entries' commits; LockState holder (unless delete() cleaned it) + waiters :41-98;
+// LeaderElectionState leader + listeners :35-108; MembershipGroupState members + close leaks :36-42 + pending
+// schedule commits :86-103; QueueState elements not clean()ed by element() :51-199.
+int64_t orc_read_retained(orc* o, uint32_t slot, uint64_t cap, uint64_t* out) {
+  if (slot >= o->max_res || !o->res[slot].exists) return -1;
+  const Resource& r = o->res[slot];
+  std::vector<uint64_t> v(r.leaked.begin(), r.leaked.end());
+  switch (r.type) {
+    case CC_RES_VALUE:
+      if (r.v.has_current) v.push_back(r.v.current.index);
+      for (auto& p : r.v.listeners) v.push_back(p.second);
+      break;
+    case CC_RES_MAP:
+    case CC_RES_SET:
+      for (auto& kv : r.m.m) v.push_back(kv.second.commit_index);
+      break;
+    case CC_RES_LOCK:
+      if (r.l.held && !r.l.lock.cleaned) v.push_back(r.l.lock.index);
+      for (auto& c : r.l.queue) v.push_back(c.index);
+      break;
+    case CC_RES_ELECTION:
+      if (r.e.has_leader && !r.e.leader.cleaned) v.push_back(r.e.leader.index);
+      for (auto& p : r.e.listeners) v.push_back(p.second.index);
+      break;
+    case CC_RES_GROUP:
+      for (auto& kv : r.g.members) v.push_back(kv.second.index);
+      for (auto& kv : o->timers)
+        if (kv.second.res == slot && kv.second.kind == T_GROUP_SCHEDULE) v.push_back(kv.second.commit_index);
+      break;
+    case CC_RES_QUEUE:
+      for (auto& e : r.q) if (!e.cleaned) v.push_back(e.idx);
+      break;
+  }
+  std::sort(v.begin(), v.end());
+  for (uint64_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return (int64_t)v.size();
 }
 
 int64_t orc_map_size(orc* o, uint32_t res) {

@@ -77,6 +77,7 @@ void orc_aux_clear(orc* o);
 int  orc_read_value_retained(orc* o, uint32_t first, uint32_t count, uint64_t* index);
 int  orc_read_value_state(orc* o, uint32_t first, uint32_t count, uint8_t* tag, uint64_t* value,
                           uint8_t* has_current);
+int64_t orc_read_retained(orc* o, uint32_t slot, uint64_t cap, uint64_t* out);
 int64_t orc_map_size(orc* o, uint32_t res);
 /* entries sorted by (key tag, key); returns count written (<= cap) or -1 */
 int64_t orc_map_entries(orc* o, uint32_t res, uint64_t cap, uint8_t* ktag, uint64_t* key, uint8_t* vtag,

@@ -58,6 +58,7 @@ def lib():
             "orc_read_value_state": (i32, [P, u32, u32, P, P, P]),
             "orc_read_value_retained": (i32, [P, u32, u32, P]),
             "orc_map_size": (i64, [P, u32]),
+            "orc_read_retained": (i64, [P, u32, u64, P]),
             "orc_map_entries": (i64, [P, u32, u64, P, P, P, P, P]),
             "orc_lock_state": (i64, [P, u32, P, P, P, u64, P, P]),
             "orc_election_state": (i64, [P, u32, P, P, u64, P, P]),
@@ -192,6 +193,12 @@ class Oracle:
         idx = np.zeros(count, np.uint64)
         assert self.L.orc_read_value_retained(self.h, first, count, _p(idx)) == 0
         return idx
+
+    def retained(self, slot, cap=1 << 16):
+        """Ascending log indices of every commit the slot's state machine still holds uncleaned (None: no resource)."""
+        out = np.zeros(cap, np.uint64)
+        n = self.L.orc_read_retained(self.h, slot, cap, _p(out))
+        return None if n < 0 else out[:min(n, cap)].tolist()
 
     def map_entries(self, res):
         n = self.L.orc_map_size(self.h, res)
