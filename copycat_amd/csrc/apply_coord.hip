@@ -49,6 +49,19 @@ struct Emitter {
   EvRec* arena;
   unsigned long long* arena_n;
   uint64_t arena_cap;
+  LeakRec* leak;     // the engine's leak log (commits dropped without clean())
+  unsigned long long* leak_n;
+  uint64_t leak_cap;
+  __device__ void leaked(uint32_t slot, uint64_t idx, uint32_t& err) const {
+    const unsigned long long a = atomicAdd(leak_n, 1ull);
+    if (a < leak_cap) {
+      leak[a].idx = idx;
+      leak[a].slot = slot;
+      leak[a].pad = 0;
+    } else {
+      err |= kErrCapacity;
+    }
+  }
   __device__ void emit(uint32_t& n, uint32_t g, uint32_t k, uint32_t target, uint32_t code, uint32_t src, uint32_t tag,
                        uint64_t payload) const {
 #ifdef CC_DIAG_NO_EMIT  // diagnostics build only: events dropped
@@ -174,9 +187,9 @@ struct Rec {
 // T != 0: the resource type is known at compile time (a wave whose slots all hold one type walks a specialised
 // copy with no code for the other types); T == 0: the runtime `type`.
 template <uint32_t T>
-__device__ inline uint32_t coord_apply(uint32_t type_rt, const Rec& r, CoordHdr& h, const Ents& E, uint32_t& vmeta_s,
-                                       uint64_t& vval, uint64_t& rv, uint32_t& nev, const Emitter& em, uint32_t& lane_n,
-                                       uint32_t& err) {
+__device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Rec& r, CoordHdr& h, const Ents& E,
+                                       uint32_t& vmeta_s, uint64_t& vval, uint64_t& rv, uint32_t& nev, const Emitter& em,
+                                       uint32_t& lane_n, uint32_t& err) {
   const uint32_t type = T ? T : type_rt;
   rv = 0;
   auto ev = [&](uint32_t target, uint32_t code, uint32_t tag, uint64_t payload) {
@@ -353,8 +366,9 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, const Rec& r, CoordHdr&
       auto first_match = [&](uint32_t& pos) -> int {  // 1 match, 0 none, -1 NPE (a stored null's equals)
         for (uint32_t i = 0; i < h.n; ++i) {
           const CoordEnt e = at(i);
-          if (e.pad == CC_TAG_NULL) return -1;
-          if (e.pad == ta && e.x == pa) {
+          const uint32_t et = e.pad & kQTagMask;
+          if (et == CC_TAG_NULL) return -1;
+          if (et == ta && e.x == pa) {
             pos = i;
             return 1;
           }
@@ -390,18 +404,24 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, const Rec& r, CoordHdr&
         case CC_OP_QUEUE_PEEK:  // peek :77-87
           if (!h.n) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
           rv = at(0).x;
-          return CC_STATUS(CC_ST_OK, at(0).pad);
+          return CC_STATUS(CC_ST_OK, at(0).pad & kQTagMask);
         case CC_OP_QUEUE_POLL: {  // poll :92-105
           if (!h.n) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
           const CoordEnt e = at(0);
           pop();
           rv = e.x;
-          return CC_STATUS(CC_ST_OK, e.pad);
+          return CC_STATUS(CC_ST_OK, e.pad & kQTagMask);
         }
         case CC_OP_QUEUE_ELEMENT:  // element :111-124 (throws when empty; the head stays)
           if (!h.n) return CC_STATUS(CC_ST_NO_SUCH_ELEMENT, CC_TAG_NULL);
-          rv = at(0).x;
-          return CC_STATUS(CC_ST_OK, at(0).pad);
+          {
+            CoordEnt e0 = at(0);
+            rv = e0.x;
+            const uint32_t tg = e0.pad & kQTagMask;
+            e0.pad |= kQCleaned;  // value.clean() on the head it leaves in place
+            set_at(0, e0);
+            return CC_STATUS(CC_ST_OK, tg);
+          }
         case CC_OP_QUEUE_REMOVE: {  // remove :130-157
           if (ta != CC_TAG_NULL) {
             uint32_t pos = 0;
@@ -418,7 +438,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, const Rec& r, CoordHdr&
           const CoordEnt e = at(0);
           pop();
           rv = e.x;
-          return CC_STATUS(CC_ST_OK, e.pad);
+          return CC_STATUS(CC_ST_OK, e.pad & kQTagMask);
         }
         case CC_OP_QUEUE_SIZE:  // size :162-168 (int)
           rv = h.n;
@@ -457,7 +477,8 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, const Rec& r, CoordHdr&
           bool found = false;
           for (uint32_t i = 0; i < h.n; ++i) {
             CoordEnt e = E.get(i);
-            if (e.inst == r.inst) {
+            if (e.inst == r.inst) {  // the replaced commit is never clean()ed: retained for good
+              em.leaked(slot, e.idx, err);
               e.idx = r.idx;
               E.put(i, e);
               found = true;
@@ -518,7 +539,9 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict
                                                      uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
                                                      uint64_t* __restrict__ rst_value, uint16_t* __restrict__ ev_cnt,
                                                      EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n,
-                                                     uint64_t arena_cap, uint32_t* __restrict__ err_out) {
+                                                     uint64_t arena_cap, LeakRec* __restrict__ leak,
+                                                     unsigned long long* __restrict__ leak_n, uint64_t leak_cap,
+                                                     uint32_t* __restrict__ err_out) {
   __shared__ u64x2 rab[kCCh2];
   __shared__ uint64_t rkey[kCCh2];
   __shared__ uint64_t ridx[kCCh2];
@@ -582,7 +605,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict
     __syncthreads();
   }
   const uint32_t cnt = rpre[tiles];
-  const Emitter em{(LdsEv*)(evbuf + l * kEvLane), kEvLane, arena, arena_n, arena_cap};
+  const Emitter em{(LdsEv*)(evbuf + l * kEvLane), kEvLane, arena, arena_n, arena_cap, leak, leak_n, leak_cap};
   // the walker lanes (wave 0, lane = slot) keep their state machine's header in registers for the whole launch
   const uint32_t res = s * (1u << kSbShift) + q0 + l;
   uint8_t* blk = coord + (uint64_t)res * kCoordBlock;
@@ -704,7 +727,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict
         r.iid = riid[p];
         uint64_t rv;
         uint32_t nev = 0;
-        const uint32_t st = coord_apply<decltype(tc)::value>(type, r, h, E, vm, vv, rv, nev, em, lane_n, err);
+        const uint32_t st = coord_apply<decltype(tc)::value>(type, res, r, h, E, vm, vv, rv, nev, em, lane_n, err);
         ost[p] = (uint8_t)st;
         oval[p] = rv;
         oev[p] = (uint16_t)nev;
@@ -783,7 +806,7 @@ int launch_apply_coord(const CoordArgs& a, hipStream_t st) {
   a.mark(K_APPLY_COORD, 1, st);
   hipLaunchKernelGGL(k_apply_coord, dim3(a.sb_val * kQPerSb), dim3(kCT2), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
                      a.ttab, a.tiles, a.sb, a.sbq_base, a.sb_kind, a.res_type, a.inst_id, a.coord, a.val_meta, a.val_v, a.rst_status,
-                     a.rst_value, a.ev_cnt, a.arena, a.arena_n, a.arena_cap, a.err);
+                     a.rst_value, a.ev_cnt, a.arena, a.arena_n, a.arena_cap, a.leak, a.leak_n, a.leak_cap, a.err);
   a.mark(K_APPLY_COORD, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

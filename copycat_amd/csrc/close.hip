@@ -48,7 +48,9 @@ __global__ void k_close_apply(const uint32_t* __restrict__ cinst, const uint32_t
                               const uint32_t* __restrict__ pcl, const uint32_t* __restrict__ fail,
                               const uint8_t* __restrict__ res_type,
                               const uint64_t* __restrict__ inst_id, uint8_t* __restrict__ coord, uint32_t* __restrict__ cnt,
-                              EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n, uint64_t arena_cap) {
+                              EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n, uint64_t arena_cap,
+                              LeakRec* __restrict__ leak, unsigned long long* __restrict__ leak_n, uint64_t leak_cap,
+                              uint32_t* __restrict__ err) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nr) return;
   const uint32_t r = rlist[k], type = res_type[r];
@@ -110,7 +112,15 @@ __global__ void k_close_apply(const uint32_t* __restrict__ cinst, const uint32_t
         const uint32_t mid = (lo + hi) >> 1;
         if (E[mid].x < iid) lo = mid + 1; else hi = mid;
       }
-      if (lo < h.n && E[lo].x == iid) {
+      if (lo < h.n && E[lo].x == iid) {  // members.remove without clean(): the join commit stays in the log
+        const unsigned long long a = atomicAdd(leak_n, 1ull);
+        if (a < leak_cap) {
+          leak[a].idx = E[lo].idx;
+          leak[a].slot = r;
+          leak[a].pad = 0;
+        } else {
+          atomicOr(err, kErrCapacity);
+        }
         for (uint32_t j = lo + 1; j < h.n; ++j) E[j - 1] = E[j];
         --h.n;
       }
@@ -194,7 +204,8 @@ int launch_close(const CloseArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_close_check, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.inst_res, a.res_type, a.coord, a.pcl, a.fail);
   if (a.nr && a.coord)
     hipLaunchKernelGGL(k_close_apply, dim3((a.nr + 63) / 64), dim3(64), 0, st, a.cinst, a.rlist, a.rstart, a.items, a.nr,
-                       a.pcl, a.fail, a.res_type, a.inst_id, a.coord, a.cnt, a.arena, a.arena_n, a.arena_cap);
+                       a.pcl, a.fail, a.res_type, a.inst_id, a.coord, a.cnt, a.arena, a.arena_n, a.arena_cap,
+                       a.leak, a.leak_n, a.leak_cap, a.err);
   hipLaunchKernelGGL(k_close_scan, dim3(1), dim3(kCS), 0, st, a.cnt, a.m, a.pcl, a.fail, a.off, a.arena_n, a.arena_cap, a.out_cap,
                      a.out_pos ? 1 : 0, a.out_count, a.err);
   if (a.out_pos)

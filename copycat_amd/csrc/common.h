@@ -197,6 +197,16 @@ constexpr uint32_t kCoHeld = 1u, kCoCleaned = 2u;
 // `resources.get(...) == null` -> NullPointerException (ResourceManager.java:62,71); close skips its handler
 constexpr uint32_t kCoZombie = 4u;
 constexpr uint64_t kNoDeadline = ~0ull;
+// QueueState entry (CoordEnt.pad = value tag | kQCleaned): element() clean()ed the head it leaves in place
+// (QueueState.java:111-124), so the log no longer retains that commit
+constexpr uint32_t kQCleaned = 0x100u, kQTagMask = 0xFFu;
+// a commit the state machine dropped without clean() (AtomicValueState.listen's listeners.put over an existing
+// session :41-49, MembershipGroupState.close's members.remove :36-42): the log retains it for good.  Appended to
+// the engine's leak log by the kernels, drained into the host's per-slot lists (cc_read_retained)
+struct LeakRec {
+  uint64_t idx;
+  uint32_t slot, pad;
+};
 constexpr int kCoordCap = 64;  // CC_LOCK_QUEUE = CC_ELECTION_LISTENERS = CC_GROUP_MEMBERS = CC_VALUE_LISTENERS
 constexpr size_t kCoordBlock = sizeof(CoordHdr) + kCoordCap * sizeof(CoordEnt);
 // one event of the per-sub-batch arena (apply_coord.hip -> events.hip)

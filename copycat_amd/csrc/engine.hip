@@ -78,11 +78,14 @@ static void free_all(cc_engine* e) {
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
-                  e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow};
+                  e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
+                  e->d_leak,     e->d_leak_n};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
+
+constexpr uint64_t kLeakCap = 1u << 20;  // leak log entries between drains (16 MiB)
 
 // Extended staging columns (maps, coordination, value events); with `coord`, the coordination blocks and the
 // event buffers.  Allocated on first need (engine creation or the first coordination resource).
@@ -112,9 +115,13 @@ static int ensure_ext(cc_engine* e, bool coord) {
         (rc = alloc((void**)&e->d_tile_off, sizeof(uint64_t) * e->max_tiles)) ||
         (rc = alloc((void**)&e->d_arena, sizeof(EvRec) * e->arena_cap)) ||
         (rc = alloc((void**)&e->d_arena_n, sizeof(unsigned long long))) ||
-        (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))))
+        (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))) ||
+        (rc = alloc((void**)&e->d_leak, sizeof(LeakRec) * kLeakCap)) ||
+        (rc = alloc((void**)&e->d_leak_n, sizeof(unsigned long long))))
       return rc;
+    e->leak_cap = kLeakCap;
     hipError_t x = hipMemset(e->d_coord, 0, kCoordBlock * slots);
+    if (x == hipSuccess) x = hipMemset(e->d_leak_n, 0, sizeof(unsigned long long));
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
     // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
@@ -394,10 +401,27 @@ extern "C" int cc_resource_delete(cc_engine* e, uint32_t slot) {
   return delete_slot(e, slot);
 }
 
+// The device leak log into the per-slot host lists (the engine is quiesced).  An overflow was already reported by
+// the batch that caused it (kErrCapacity); the entries past the log's end are lost.
+int cc::drain_leaks(cc_engine* e) {
+  if (!e->d_leak_n) return CC_OK;
+  unsigned long long n = 0;
+  HIPCHECK(hipMemcpy(&n, e->d_leak_n, sizeof n, hipMemcpyDeviceToHost));
+  if (!n) return CC_OK;
+  n = std::min<unsigned long long>(n, e->leak_cap);
+  std::vector<LeakRec> v(n);
+  HIPCHECK(hipMemcpy(v.data(), e->d_leak, sizeof(LeakRec) * n, hipMemcpyDeviceToHost));
+  for (const LeakRec& r : v) e->leaks[r.slot].push_back(r.idx);
+  HIPCHECK(hipMemset(e->d_leak_n, 0, sizeof(unsigned long long)));
+  return CC_OK;
+}
+
 // ResourceManager.deleteResource after resource.stateMachine.delete() succeeded (ResourceManager.java:212-235).
 int cc::delete_slot(cc_engine* e, uint32_t slot) {
   int rc = quiesce(e);
   if (rc) return rc;
+  if ((rc = drain_leaks(e))) return rc;
+  e->leaks.erase(slot);  // the per-slot view ends with the resource (its dropped commits stay in the log)
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
   if (is_keyed(e->res_type[slot])) {  // MapState.delete :264-274 / SetState.delete :123-134 — entries die with it
     if (launch_map_drop_resource(e->d_tbl_word, e->map_entries, slot, e->own_stream))
@@ -719,6 +743,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.arena = e->d_arena;
       ca.arena_n = e->d_arena_n;
       ca.arena_cap = e->arena_cap;
+      ca.leak = e->d_leak;
+      ca.leak_n = e->d_leak_n;
+      ca.leak_cap = e->leak_cap;
       ca.err = e->d_err;
       ca.mark = marker_of(e);
       if (launch_apply_coord(ca, st)) return set_err(CC_ERR_HIP, "coordination apply launch", hipGetLastError());
@@ -808,6 +835,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         gt.tag = CC_FLAG_TAG_A(fl);
         gt.payload = gt.tag == CC_TAG_NULL ? 0 : a;
         gt.slot = res;
+        if (c->index) HIPCHECK(hipMemcpy(&gt.idx, c->index + row, sizeof gt.idx, hipMemcpyDeviceToHost));
         rc = fire_boundary(gt.deadline, deferred ? row : row + 1, gt.fire_b);
         if (rc) return rc;
         e->gtimers.push_back(gt);
@@ -1053,6 +1081,9 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   ca.arena_n = e->d_arena_n;
   ca.arena_cap = e->coord_on ? e->arena_cap : 0;
   ca.err = e->d_err;
+  ca.leak = e->d_leak;
+  ca.leak_n = e->d_leak_n;
+  ca.leak_cap = e->leak_cap;
   unsigned long long zero_n = 0, *d_zero = nullptr;
   if (!ca.arena_n) {  // no coordination state: no handler can publish; the scan still needs a counter
     if (hipMalloc(&d_zero, sizeof zero_n) != hipSuccess) {
@@ -1257,6 +1288,77 @@ extern "C" int cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, 
   return CC_OK;
 }
 
+// Every commit the slot's state machine holds without having clean()ed it, ascending (the
+// oracle's orc_read_retained restates the same sites).
+extern "C" int cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint64_t* h_index) {
+  if (!e || !count || slot >= e->cfg.max_resources || e->res_type[slot] == CC_RES_NONE)
+    return set_err(CC_ERR_INVALID, "unknown resource slot");
+  if (cap && !h_index) return set_err(CC_ERR_INVALID, "null output");
+  const uint32_t type = e->res_type[slot];
+  if (type == CC_RES_VALUE && !e->d_val_live)
+    return set_err(CC_ERR_INVALID, "engine created without CC_CFG_VALUE_RETAINED");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  if ((rc = drain_leaks(e))) return rc;
+  std::vector<uint64_t> v;
+  auto it = e->leaks.find(slot);
+  if (it != e->leaks.end()) v = it->second;
+  CoordHdr h{};
+  std::vector<CoordEnt> q;
+  if (is_coord(type) || (type == CC_RES_VALUE && e->coord_on)) {
+    if ((rc = read_block(e, slot, type, h, q, nullptr))) return rc;
+  }
+  switch (type) {
+    case CC_RES_VALUE: {  // current (AtomicValueState.java:88-157) + listeners :41-63
+      uint64_t cur = 0;
+      HIPCHECK(hipMemcpy(&cur, e->d_val_live + slot, sizeof cur, hipMemcpyDeviceToHost));
+      if (cur) v.push_back(cur);
+      for (uint32_t i = 0; i < h.n; ++i) v.push_back(q[i].idx);
+      break;
+    }
+    case CC_RES_MAP:
+    case CC_RES_SET: {  // MapState / SetState: each entry's commit (removal and TTL expiry clean it)
+      uint64_t n = 0;
+      if ((rc = cc_read_map_entries(e, slot, 0, &n, nullptr, nullptr, nullptr, nullptr, nullptr))) return rc;
+      std::vector<uint8_t> kt(n), vt(n);
+      std::vector<uint64_t> k(n), val(n), ci(n);
+      if ((rc = cc_read_map_entries(e, slot, n, &n, kt.data(), k.data(), vt.data(), val.data(), ci.data()))) return rc;
+      v.insert(v.end(), ci.begin(), ci.end());
+      break;
+    }
+    case CC_RES_LOCK: {  // holder unless delete() cleaned it; waiters whose timeout has not fired (LockState :41-98)
+      uint64_t n = 0, held_idx = 0;
+      int64_t holder = -1;
+      uint8_t cleaned = 0;
+      if ((rc = cc_read_lock_state(e, slot, &holder, &held_idx, &cleaned, 0, &n, nullptr, nullptr))) return rc;
+      std::vector<uint64_t> wi(n);
+      if ((rc = cc_read_lock_state(e, slot, &holder, &held_idx, &cleaned, n, &n, nullptr, wi.data()))) return rc;
+      if (holder >= 0 && !cleaned) v.push_back(held_idx);
+      v.insert(v.end(), wi.begin(), wi.end());
+      break;
+    }
+    case CC_RES_ELECTION:  // leader unless delete() cleaned it + listeners (LeaderElectionState :35-108)
+      if ((h.flags & kCoHeld) && !(h.flags & kCoCleaned)) v.push_back(h.idx);
+      for (uint32_t i = 0; i < h.n; ++i) v.push_back(q[i].idx);
+      break;
+    case CC_RES_GROUP:  // members + pending schedule commits (MembershipGroupState :47-103)
+      for (uint32_t i = 0; i < h.n; ++i) v.push_back(q[i].idx);
+      for (const auto& g : e->gtimers)
+        if (g.slot == slot) v.push_back(g.idx);
+      break;
+    case CC_RES_QUEUE:  // elements, less the head element() clean()ed (QueueState :51-199)
+      for (uint32_t i = 0; i < h.n; ++i) {
+        const CoordEnt& x = q[(h.head + i) % kCoordCap];
+        if (!(x.pad & kQCleaned)) v.push_back(x.idx);
+      }
+      break;
+  }
+  std::sort(v.begin(), v.end());
+  *count = v.size();
+  for (uint64_t i = 0; i < v.size() && i < cap; ++i) h_index[i] = v[i];
+  return CC_OK;
+}
+
 extern "C" int cc_advance_time_events(cc_engine* e, uint64_t now, const cc_events* d_events) {
   if (!e) return CC_ERR_INVALID;
   int rc = quiesce(e);
@@ -1293,7 +1395,7 @@ static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unp
 // Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
 // mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
 namespace {
-constexpr uint64_t kSnapMagic = 0x32304E5053434343ull;  // "CCCSPN02"
+constexpr uint64_t kSnapMagic = 0x33304E5053434343ull;  // "CCCSPN03"
 constexpr uint32_t kSnapRetained = 4u;                   // SnapHdr.flags: CC_CFG_VALUE_RETAINED section present
 struct SnapHdr {
   uint64_t magic;
@@ -1346,10 +1448,19 @@ static std::vector<Section> snap_sections(cc_engine* e) {
   return v;
 }
 
+static uint64_t leak_entries(const cc_engine* e) {
+  uint64_t n = 0;
+  for (const auto& kv : e->leaks) n += kv.second.size();
+  return n;
+}
+
 extern "C" int cc_snapshot_size(cc_engine* e, uint64_t* bytes) {
   if (!e || !bytes) return CC_ERR_INVALID;
+  int rc = quiesce(e);  // the leak log's entries are counted from the host lists
+  if (rc) return rc;
+  if ((rc = drain_leaks(e))) return rc;
   uint64_t total = sizeof(SnapHdr) + 16 + e->gtimers.size() * sizeof(cc_engine::GroupTimer) + 8 +
-                   e->res_sessions.size() * 24;
+                   e->res_sessions.size() * 24 + 8 + leak_entries(e) * 16;
   for (const Section& x : snap_sections(e)) total += 8 + x.bytes;
   *bytes = total;
   return CC_OK;
@@ -1360,7 +1471,7 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
   int rc = cc_sync(e);  // results of every batch so far are final (and the applied watermark is current)
   if (rc) return rc;
   uint64_t need = 0;
-  cc_snapshot_size(e, &need);
+  if ((rc = cc_snapshot_size(e, &need))) return rc;
   if (cap < need) return set_err(CC_ERR_CAPACITY, "snapshot buffer smaller than cc_snapshot_size");
   SnapHdr h{};
   h.magic = kSnapMagic;
@@ -1398,6 +1509,15 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
     memcpy(p, t, 24);
     p += 24;
   }
+  const uint64_t nl = leak_entries(e);  // commits dropped without clean(): (slot, log index) pairs
+  memcpy(p, &nl, 8);
+  p += 8;
+  for (const auto& kv : e->leaks)
+    for (uint64_t idx : kv.second) {
+      const uint64_t t[2] = {kv.first, idx};
+      memcpy(p, t, 16);
+      p += 16;
+    }
   return CC_OK;
 }
 
@@ -1447,6 +1567,18 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
     memcpy(t, p, 24);
     e->res_sessions[{(uint32_t)t[0], t[1]}] = t[2];
   }
+  uint64_t nl = 0;
+  if (p + 8 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&nl, p, 8);
+  p += 8;
+  if (p + nl * 16 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  e->leaks.clear();
+  for (uint64_t i = 0; i < nl; ++i, p += 16) {
+    uint64_t t[2];
+    memcpy(t, p, 16);
+    e->leaks[(uint32_t)t[0]].push_back(t[1]);
+  }
+  if (e->d_leak_n) HIPCHECK(hipMemset(e->d_leak_n, 0, sizeof(unsigned long long)));
   // the control-plane maps and slot occupancy follow from the restored arrays
   e->keys.clear();
   e->res_by_id.clear();

@@ -211,6 +211,9 @@ struct CoordArgs {
   EvRec* arena;
   unsigned long long* arena_n;
   uint64_t arena_cap;
+  LeakRec* leak;           // leak log (LeakRec, common.h)
+  unsigned long long* leak_n;
+  uint64_t leak_cap;
   uint32_t* err;
   Marker mark;
 };
@@ -231,6 +234,9 @@ struct EventArgs {
   const EvRec* arena;
   const unsigned long long* arena_n;
   uint64_t arena_cap;
+  LeakRec* leak;           // leak log: a group member removed by close (its join commit is never clean()ed)
+  unsigned long long* leak_n;
+  uint64_t leak_cap;
   uint64_t out_cap;
   uint32_t* out_pos;
   uint32_t* out_target;
@@ -263,6 +269,9 @@ struct CloseArgs {
   EvRec* arena;
   unsigned long long* arena_n;
   uint64_t arena_cap;
+  LeakRec* leak;           // leak log: a group member removed by close (its join commit is never clean()ed)
+  unsigned long long* leak_n;
+  uint64_t leak_cap;
   uint64_t out_cap;
   uint32_t* out_pos;
   uint32_t* out_target;

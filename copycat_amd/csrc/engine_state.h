@@ -22,6 +22,7 @@ int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type);
 int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first, uint32_t res_stride, uint64_t id_first,
                uint64_t client);
 int delete_slot(cc_engine* e, uint32_t slot);
+int drain_leaks(cc_engine* e);  // the device leak log -> cc_engine::leaks
 
 // Occupancy bitmap of a slot space with lowest-free / highest-free search (control-plane allocation: rare, so a
 // word scan from a hint is enough).
@@ -150,6 +151,7 @@ struct cc_engine {
     uint64_t deadline, id, member, payload;
     uint32_t slot, tag;
     uint64_t fire_b;  // boundary in the current batch (rows before it applied first); ~0: not in this batch
+    uint64_t idx;     // the schedule commit's log index (retained until the timer fires, :86-103)
   };
   std::vector<GroupTimer> gtimers;
   uint64_t gtimer_seq = 0;
@@ -175,6 +177,11 @@ struct cc_engine {
   unsigned long long* d_arena_n = nullptr;
   unsigned long long* d_ev_total = nullptr;
   uint64_t arena_cap = 0;
+  // commits dropped without clean() (LeakRec, common.h): the kernels' device log, drained into per-slot host lists
+  LeakRec* d_leak = nullptr;
+  unsigned long long* d_leak_n = nullptr;
+  uint64_t leak_cap = 0;
+  std::map<uint32_t, std::vector<uint64_t>> leaks;  // ordered: snapshots are byte-deterministic
   uint64_t applied = 0;
   bool applied_pending = false;
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)

@@ -59,6 +59,7 @@ def lib():
             "cc_read_lock_state": (i32, [P, u32, P, P, P, u64, P, P, P]),
             "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
             "cc_read_group_members": (i32, [P, u32, u64, P, P]),
+            "cc_read_retained": (i32, [P, u32, u64, P, P]),
             "cc_advance_time": (i32, [P, u64]),
             "cc_advance_time_events": (i32, [P, u64, P]),
             "cc_snapshot_size": (i32, [P, P]),
@@ -386,6 +387,15 @@ class Engine:
         ids, n = np.zeros(cap, np.uint64), C.c_uint64()
         _check(self.L.cc_read_group_members(self.h, slot, cap, C.byref(n), _np(ids)))
         return ids[:min(n.value, cap)].tolist()
+
+    def retained(self, slot):
+        """Ascending log indices of every commit the slot's state machine still holds without having clean()ed it
+        (cc_read_retained) — the layout of the oracle's retained()."""
+        n = C.c_uint64()
+        _check(self.L.cc_read_retained(self.h, slot, 0, C.byref(n), None))
+        out = np.zeros(max(n.value, 1), np.uint64)
+        _check(self.L.cc_read_retained(self.h, slot, n.value, C.byref(n), _np(out)))
+        return out[:n.value].tolist()
 
     def map_entries(self, slot):
         """MapState entries of one map slot sorted by (key tag, key): (key_tag, key, value_tag, value, commit_index)

@@ -329,6 +329,16 @@ int  cc_read_election_state(cc_engine* e, uint32_t slot, int64_t* leader, uint64
                             uint64_t* count, uint32_t* h_listener_inst, uint64_t* h_listener_index);
 /* MembershipGroupState.members (MembershipGroupState.java:33): member instance ids, ascending. */
 int  cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint64_t* h_ids);
+/* Log compaction for every state machine (Commit.clean()): the log indices of every commit
+ * the slot's state machine still holds without having clean()ed it, ascending — *count of them, the first
+ * min(cap, count) to h_index.  Value: `current` + listeners (AtomicValueState.java:41-157, needs
+ * CC_CFG_VALUE_RETAINED); map / set: each entry's commit (MapState.java:279-287); lock: the holder unless
+ * delete() cleaned it + waiters (LockState.java:41-98); election: the leader unless cleaned + listeners
+ * (LeaderElectionState.java:35-108); group: members + pending schedule commits (MembershipGroupState.java:47-103);
+ * queue: elements less the head element() cleaned (QueueState.java:51-199).  Plus the commits those state
+ * machines drop without clean() — a listen that replaces a session's listener (AtomicValueState.java:41-49), a
+ * member removed by close (MembershipGroupState.java:36-42) — which the log can never compact.            */
+int  cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint64_t* h_index);
 /* Log time advanced without a commit (ResourceManagerStateMachineExecutor timers): due lock
  * timeouts take effect (they publish nothing, LockState.java:54-58). */
 int  cc_advance_time(cc_engine* e, uint64_t now);

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from copycat_amd import abi
+from copycat_amd.batch import Batch
 
 pytestmark = pytest.mark.gpu
 
@@ -136,3 +137,119 @@ def test_retained_snapshot_roundtrip_and_config_check():
         assert np.array_equal(x, y)
     with pytest.raises(EngineError):
         _value_engine(R, flags).restore(plain.snapshot())
+
+
+# ---- every state machine: cc_read_retained vs the oracle's retained() ---------------------------------------------
+def _retained_all(E, O, slots):
+    for r in slots:
+        got, want = E.retained(int(r)), O.retained(int(r))
+        assert got == want, (int(r), len(got), len(want), sorted(set(got) ^ set(want))[:8])
+
+
+def _with_schedules(b, types, K, max_inst, rng, count):
+    """MembershipGroup.schedule rows on group instances (retained until their timer fires, :86-103)."""
+    G = abi.CC_RES_GROUP
+    res_of = np.where(b.inst < max_inst, b.inst // K, 0)
+    grp = np.nonzero((types[np.minimum(res_of, len(types) - 1)] == G) & (b.inst < len(types) * K))[0]
+    rows = rng.choice(grp, size=min(count, len(grp)), replace=False)
+    b.op[rows] = abi.CC_OP_GROUP_SCHEDULE
+    b.key[rows] = (1000 + res_of[rows] * K + rng.integers(0, K, len(rows))).astype(np.uint64)
+    b.flags[rows] = abi.cc_flags(abi.CC_TAG_HANDLE, 0, 0)
+    b.a[rows] = rng.integers(0, 1 << 20, len(rows)).astype(np.uint64)
+    b.aux[rows] = rng.integers(1, 400, len(rows)).astype(np.uint64)
+    return b
+
+
+@pytest.mark.parametrize("n,R,K,seed", [(2_000, 16, 3, 31), (120_000, 512, 5, 32)])
+def test_retained_coordination_parity(n, R, K, seed):
+    """Locks (holder until delete() cleans it, waiters), elections (leader, listeners), groups (members, pending
+    schedule commits, members dropped by close: leaked for good), values with listeners (current + listeners +
+    re-listen leaks): every slot's retained set after each batch, after session closes, across a snapshot round
+    trip and after the schedule timers fire."""
+    from copycat_amd.engine import Engine
+    from copycat_amd.workload import coord_random_stream
+    from tests.test_gpu_coord import FLAGS, _check_batch, _setup
+
+    L, E_, G, V = abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP, abi.CC_RES_VALUE
+    types = np.array([L, E_, G, V] * ((R + 3) // 4), np.uint8)[:R]
+    flags = FLAGS | abi.CC_CFG_VALUE_RETAINED
+    E, O, max_inst = _setup(types, K, flags)
+    rng = np.random.default_rng(seed)
+    b = _with_schedules(coord_random_stream(n, types, K, max_inst, seed=seed), types, K, max_inst, rng, 40)
+    cuts = [0, n // 3, n // 3 + 1, n]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        _check_batch(E, O, b.slice(lo, hi))
+        _retained_all(E, O, range(R))
+    assert sum(len(O.retained(r)) for r in range(R)) > R // 2
+    vals = np.nonzero(types == V)[0]
+    if n >= 100_000:  # re-listen leaks: more retained value commits than current + one listener per instance
+        assert sum(len(O.retained(int(r))) for r in vals) > (K + 1) * len(vals)
+    # a close drops group members without clean() (leaked) and value listeners / election listeners (cleaned)
+    for client in (7, 8):
+        E.sessions_close([client], capacity=1 << 18)
+        O.session_close(client)
+        O.take_events()
+    _retained_all(E, O, range(R))
+    grps = np.nonzero(types == G)[0]
+    if n >= 100_000:  # members dropped by close stay retained (MembershipGroupState.close :36-42)
+        assert sum(len(O.retained(int(r))) - len(O.group_members(int(r))) for r in grps) > 0
+    # snapshot round trip: the leak lists and pending schedule commits travel with the state
+    E2 = Engine(R, max_inst, 1 << 20, flags=flags, max_events=1 << 22)
+    E2.restore(E.snapshot())
+    _retained_all(E2, O, range(R))
+    # the schedule timers fire: their commits are released
+    now = int(b.time[-1]) + 1000
+    E.advance_time_events(now, capacity=1 << 16)
+    O.advance_time(now)
+    O.take_events()
+    _retained_all(E, O, range(R))
+
+
+def test_retained_queue_parity():
+    """QueueState: every element's commit, less heads element() cleaned (QueueState.java:111-124); poll/remove/clear
+    release theirs."""
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+    from tests.test_gpu_queue import _stream
+
+    Q, n = 64, 40_000
+    E = Engine(Q, Q + 8, n, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=1 << 16)
+    O = Oracle(Q, Q + 8)
+    E.resource_create_range(0, Q, abi.CC_RES_QUEUE)
+    E.instance_open_range(0, Q, 0, 1000, 7)
+    for q in range(Q):
+        O.resource_create(q, abi.CC_RES_QUEUE)
+        O.instance_open(q, q, 1000 + q, 7)
+    b = _stream(n, Q, Q + 8, 41)
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        s, v = E.apply_host(b.slice(lo, hi))
+        s2, v2 = O.apply(b.slice(lo, hi))
+        assert np.array_equal(s, s2) and np.array_equal(v, v2)
+        _retained_all(E, O, range(Q))
+    # clear, add, add, element (cleans the head it leaves queued), poll (removes it), element, add
+    ops = [abi.CC_OP_QUEUE_CLEAR, abi.CC_OP_QUEUE_ADD, abi.CC_OP_QUEUE_ADD, abi.CC_OP_QUEUE_ELEMENT, abi.CC_OP_QUEUE_POLL,
+           abi.CC_OP_QUEUE_ELEMENT, abi.CC_OP_QUEUE_ADD]
+    idx0 = n + 1
+    k = Batch.from_columns(index=np.arange(idx0, idx0 + len(ops), dtype=np.uint64),
+                           time=np.full(len(ops), int(b.time[-1]), np.uint64), inst=np.zeros(len(ops), np.uint32),
+                           op=np.array(ops, np.uint8), flags=np.full(len(ops), abi.CC_TAG_LONG, np.uint8),
+                           a=np.arange(len(ops), dtype=np.uint64))
+    E.apply_host(k)
+    O.apply(k)
+    got = E.retained(0)
+    assert got == O.retained(0) == [idx0 + 6]  # the two heads element() touched are no longer retained
+
+
+def test_retained_map_parity():
+    """MapState: each live entry's commit (replaced / removed / expired entries are cleaned)."""
+    from copycat_amd.workload import map_random_stream
+    from tests.test_gpu_map import _engines
+
+    maps, n = 128, 60_000
+    E, O = _engines(maps, maps + 8, n, 1 << 16)
+    b = map_random_stream(n, maps, maps + 8, keys=32, seed=51)
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        s, v = E.apply_host(b.slice(lo, hi))
+        s2, v2 = O.apply(b.slice(lo, hi))
+        assert np.array_equal(s, s2) and np.array_equal(v, v2)
+        _retained_all(E, O, range(maps))
