@@ -23,6 +23,7 @@ CC_RES_ELECTION = 4
 CC_RES_GROUP = 5
 CC_RES_SET = 6
 CC_RES_QUEUE = 7
+CC_RES_MULTIMAP = 8
 CC_QUEUE_CAP = 64
 
 CC_OP_DELETE = 1
@@ -61,6 +62,16 @@ CC_OP_SET_REMOVE = 102
 CC_OP_SET_SIZE = 103
 CC_OP_SET_ISEMPTY = 104
 CC_OP_SET_CLEAR = 105
+CC_OP_MMAP_CONTAINSKEY = 75
+CC_OP_MMAP_CONTAINSENTRY = 76
+CC_OP_MMAP_CONTAINSVALUE = 77
+CC_OP_MMAP_PUT = 78
+CC_OP_MMAP_GET = 79
+CC_OP_MMAP_REMOVE = 80
+CC_OP_MMAP_REMOVEVALUE = 81
+CC_OP_MMAP_ISEMPTY = 82
+CC_OP_MMAP_SIZE = 83
+CC_OP_MMAP_CLEAR = 84
 CC_OP_ELECT_LISTEN = 110
 CC_OP_ELECT_UNLISTEN = 111
 CC_OP_ELECT_ISLEADER = 112
@@ -77,6 +88,7 @@ CC_TAG_INT = 2
 CC_TAG_BOOL = 3
 CC_TAG_HANDLE = 4
 CC_TAG_SET = 5
+CC_TAG_LIST = 6
 
 CC_ST_OK = 0
 CC_ST_UNKNOWN_SESSION = 1
@@ -118,6 +130,7 @@ TYPE_OPS = {
     CC_RES_GROUP: {CC_OP_DELETE, 120, 121, 122, 123},
     CC_RES_SET: {CC_OP_DELETE} | set(range(100, 106)),
     CC_RES_QUEUE: {CC_OP_DELETE} | set(range(90, 100)),
+    CC_RES_MULTIMAP: {CC_OP_DELETE, 75} | set(range(78, 85)),
 }
 # key tags of the flags column (keys are never null)
 KTAG_OF_TAG = {CC_TAG_LONG: 0, CC_TAG_INT: 1, CC_TAG_BOOL: 2, CC_TAG_HANDLE: 3}
@@ -126,6 +139,18 @@ TAG_OF_KTAG = {v: k for k, v in KTAG_OF_TAG.items()}
 
 def cc_flags(tag_a=0, tag_b=0, ktag=0):
     return (tag_a & 7) | ((tag_b & 7) << 3) | ((ktag & 3) << 6)
+
+
+def flag_tag_a(f):
+    return f & 7
+
+
+def flag_tag_b(f):
+    return (f >> 3) & 7
+
+
+def flag_ktag(f):
+    return (f >> 6) & 3
 
 
 def cc_status(code, tag):
@@ -183,6 +208,31 @@ class cc_events(C.Structure):
         ("capacity", C.c_uint64),
         ("count", C.c_void_p),
     ]
+
+
+# Catalyst wire format (include/copycat_apply.h "Catalyst wire format"; copycat_amd/csrc/wire.cpp)
+CC_WIRE_ID_BOOLEAN = 129
+CC_WIRE_ID_INTEGER = 132
+CC_WIRE_ID_LONG = 133
+CC_WIRE_ID_STRING = 136
+
+
+class cc_wire_codec(C.Structure):
+    _fields_ = [
+        ("big_endian", C.c_uint8),
+        ("utf8_presence_byte", C.c_uint8),
+        ("utf8_len_bytes", C.c_uint8),
+        ("reserved8", C.c_uint8),
+        ("id_bool", C.c_int32),
+        ("id_int", C.c_int32),
+        ("id_long", C.c_int32),
+        ("id_string", C.c_int32),
+        ("reserved", C.c_uint64 * 4),
+    ]
+
+
+class cc_wire_out(C.Structure):
+    _fields_ = [(name, C.c_void_p) for name in ("inst", "iid", "op", "flags", "key", "a", "b", "aux", "kind")]
 
 
 BATCH_COLUMNS = (

@@ -339,7 +339,8 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         const uint64_t ti = ctime ? max(ctime[row], cb) : cb;
         const uint64_t tp = ctime && row > 0 ? max(ctime[row - 1], cb) : cb;
         const uint32_t op = smeta_op(m[j]);
-        const int64_t ttl = caux && map_reads_ttl(op) ? (int64_t)caux[row] : 0;
+        // the partition marks the rows whose ttl arms a timer (a multimap Put's does not: A18)
+        const int64_t ttl = caux && map_reads_ttl(op) && (m[j] & kMetaTtl) ? (int64_t)caux[row] : 0;
         rfire[s] = deferred ? tp : ti;
         rdl[s] = ttl > 0 ? ti + (uint64_t)ttl : 0;
         eflag[ent[j]] = 1;  // every run is walked in order

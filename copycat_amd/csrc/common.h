@@ -127,11 +127,14 @@ __host__ __device__ inline bool op_registered(uint32_t type, uint32_t op) {
     case CC_RES_GROUP: return op >= 120 && op <= 123;
     case CC_RES_SET: return op >= 100 && op <= 105;
     case CC_RES_QUEUE: return op >= 90 && op <= 99;
+    case CC_RES_MULTIMAP: return op == 75 || (op >= 78 && op <= 84);  // MultiMapState.java:37-207 (no 76 / 77)
   }
   return false;
 }
 // resources whose elements live in the map table (apply_map.hip): MapState and SetState
-__host__ __device__ inline bool is_keyed(uint32_t type) { return type == CC_RES_MAP || type == CC_RES_SET; }
+__host__ __device__ inline bool is_keyed(uint32_t type) {
+  return type == CC_RES_MAP || type == CC_RES_SET || type == CC_RES_MULTIMAP;
+}
 // SetState ops as the MapState key ops they behave like (the result is rewritten by k_set_results):
 // contains -> containsKey, add -> putIfAbsent(Boolean TRUE), remove -> remove; anything else -> 0 (unknown op)
 __host__ __device__ inline uint32_t set_as_map_op(uint32_t op) {
@@ -146,11 +149,32 @@ __host__ __device__ inline uint32_t set_as_map_op(uint32_t op) {
   }
   return 0;
 }
+// MultiMapState ops as MapState key ops (MultiMapState.java:37-207; results rewritten by k_keyed_results).  The
+// state is the set of keys put (put registers the key's value map but never stores the value, :68-91), so a key
+// is a map entry holding Boolean TRUE: containsKey -> containsKey; put -> putIfAbsent(TRUE), no TTL (the timer's
+// callback throws before it changes anything, A18); get / size(key) / remove(key, value) change nothing ->
+// containsKey; remove(key) -> remove; removeValue and clear drop every key (:140-165, every value map is
+// empty) -> clear; anything else -> 0 (unknown op).
+__host__ __device__ inline uint32_t mmap_as_map_op(uint32_t op, uint32_t tag_a) {
+  switch (op) {
+    case CC_OP_MMAP_CONTAINSKEY: return CC_OP_MAP_CONTAINSKEY;
+    case CC_OP_MMAP_PUT: return CC_OP_MAP_PUTIFABSENT;
+    case CC_OP_MMAP_GET: return CC_OP_MAP_CONTAINSKEY;
+    case CC_OP_MMAP_SIZE: return CC_OP_MAP_CONTAINSKEY;
+    case CC_OP_MMAP_REMOVE: return tag_a != CC_TAG_NULL ? CC_OP_MAP_CONTAINSKEY : CC_OP_MAP_REMOVE;
+    case CC_OP_MMAP_REMOVEVALUE: return CC_OP_MAP_CLEAR;
+    case CC_OP_MMAP_ISEMPTY: return CC_OP_MAP_ISEMPTY;
+    case CC_OP_MMAP_CLEAR: return CC_OP_MAP_CLEAR;
+    case CC_OP_DELETE: return CC_OP_DELETE;
+  }
+  return 0;
+}
 // ops this build applies on the GPU (others raise CC_ERR_UNSUPPORTED for the batch)
 __host__ __device__ inline bool op_on_gpu(uint32_t type, uint32_t op) {
   if (type == CC_RES_VALUE) return op == CC_OP_DELETE || (op >= 50 && op <= 53);
   if (type == CC_RES_MAP) return op == 60 || (op >= 62 && op <= 69);  // key ops (whole-map ops: map_wide.hip)
   if (type == CC_RES_SET) return op >= 100 && op <= 102;
+  if (type == CC_RES_MULTIMAP) return op == 75 || (op >= 78 && op <= 80) || op == 83;
   if (type == CC_RES_QUEUE) return op_registered(type, op);
   if (type == CC_RES_LOCK || type == CC_RES_ELECTION) return op_registered(type, op);
   if (type == CC_RES_GROUP) return op_registered(type, op);  // schedule rows are batch barriers (engine.hip)

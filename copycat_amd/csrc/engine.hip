@@ -87,6 +87,27 @@ static void free_all(cc_engine* e) {
 
 constexpr uint64_t kLeakCap = 1u << 20;  // leak log entries between drains (16 MiB)
 
+// The leak log with room for `need` entries past those already drained (an empty log is reallocated).
+static int ensure_leak(cc_engine* e, uint64_t need) {
+  if (!e->d_leak_n) {
+    hipError_t x = hipMalloc(&e->d_leak_n, sizeof(unsigned long long));
+    if (x == hipSuccess) x = hipMemset(e->d_leak_n, 0, sizeof(unsigned long long));
+    if (x != hipSuccess) return set_err(CC_ERR_HIP, "leak log counter", x);
+  }
+  if (e->d_leak && e->leak_cap >= need) return CC_OK;
+  if (e->d_leak) {
+    int rc = drain_leaks(e);
+    if (rc) return rc;
+    (void)hipFree(e->d_leak);
+    e->d_leak = nullptr;
+  }
+  const uint64_t cap = std::max<uint64_t>(need, kLeakCap);
+  hipError_t x = hipMalloc(&e->d_leak, sizeof(LeakRec) * cap);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc leak log", x);
+  e->leak_cap = cap;
+  return CC_OK;
+}
+
 // Extended staging columns (maps, coordination, value events); with `coord`, the coordination blocks and the
 // event buffers.  Allocated on first need (engine creation or the first coordination resource).
 static int ensure_ext(cc_engine* e, bool coord) {
@@ -116,12 +137,9 @@ static int ensure_ext(cc_engine* e, bool coord) {
         (rc = alloc((void**)&e->d_arena, sizeof(EvRec) * e->arena_cap)) ||
         (rc = alloc((void**)&e->d_arena_n, sizeof(unsigned long long))) ||
         (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))) ||
-        (rc = alloc((void**)&e->d_leak, sizeof(LeakRec) * kLeakCap)) ||
-        (rc = alloc((void**)&e->d_leak_n, sizeof(unsigned long long))))
+        (rc = ensure_leak(e, kLeakCap)))
       return rc;
-    e->leak_cap = kLeakCap;
     hipError_t x = hipMemset(e->d_coord, 0, kCoordBlock * slots);
-    if (x == hipSuccess) x = hipMemset(e->d_leak_n, 0, sizeof(unsigned long long));
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
     // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
@@ -341,8 +359,13 @@ int cc::quiesce(cc_engine* e) {
 
 int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type) {
   if (is_keyed(type) && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map and set resources need cc_config.map_capacity > 0");
-  if (type < CC_RES_VALUE || type > CC_RES_QUEUE) return set_err(CC_ERR_INVALID, "unknown resource type");
+  if (type < CC_RES_VALUE || type > CC_RES_MULTIMAP) return set_err(CC_ERR_INVALID, "unknown resource type");
   if (type == CC_RES_SET) e->has_sets = true;
+  if (type == CC_RES_MULTIMAP) {
+    e->has_mmaps = true;
+    int rc = ensure_leak(e, kLeakCap);
+    if (rc) return rc;
+  }
   const uint64_t end = (uint64_t)first + count;
   if (end > e->cfg.max_resources) return set_err(CC_ERR_CAPACITY, "resource slot out of range");
   for (uint64_t s = first; s < end; ++s) {
@@ -528,6 +551,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (ttl_seen) e->ttl_live = true;
+    if (e->has_mmaps) {  // every multimap Put of this batch may land in the leak log: room for n more
+      int rc = drain_leaks(e);
+      if (!rc) rc = ensure_leak(e, n);
+      if (rc) return rc;
+    }
     if (nb > kBarCap)
       return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) and group schedules in one batch than kBarCap");
     if (nb) {
@@ -844,7 +872,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     }
     MapWideArgs mw{};
     mw.slot = res;
-    mw.op = e->res_type[res] == CC_RES_SET ? set_as_map_op(op) : op;
+    mw.op = e->res_type[res] == CC_RES_SET        ? set_as_map_op(op)
+            : e->res_type[res] == CC_RES_MULTIMAP ? mmap_as_map_op(op, CC_FLAG_TAG_A(fl))
+                                                  : op;
     mw.atag = CC_FLAG_TAG_A(fl);
     mw.apay = a;
     mw.row = row;
@@ -873,9 +903,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError());
   }
   }
-  if (e->has_sets && launch_set_results(c->inst, c->op, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, out->status,
-                                        out->value, st))
-    return set_err(CC_ERR_HIP, "set results launch", hipGetLastError());
+  if (e->has_sets || e->has_mmaps) {
+    KeyedResultArgs ka{c->inst,     c->op,          c->flags, c->index,     n,           e->d_inst_res, e->d_res_type,
+                       e->cfg.max_instances, out->status, out->value, e->d_leak, e->d_leak_n, e->leak_cap, e->d_err};
+    if (launch_keyed_results(ka, st)) return set_err(CC_ERR_HIP, "set / multimap results launch", hipGetLastError());
+  }
   // Retained value commits (live.hip): after every value op of the batch has applied.  The post-pass attributes
   // each row through the END-of-batch inst_res / res_type / val_meta: correct because the registry cannot change
   // inside a cc_apply_batch call (resource create/delete, instance open/close are host calls that quiesce the
@@ -1346,6 +1378,8 @@ extern "C" int cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint6
       for (const auto& g : e->gtimers)
         if (g.slot == slot) v.push_back(g.idx);
       break;
+    case CC_RES_MULTIMAP:  // every Put (MultiMapState.put :68-91 neither cleans nor closes it): the leak lists
+      break;
     case CC_RES_QUEUE:  // elements, less the head element() clean()ed (QueueState :51-199)
       for (uint32_t i = 0; i < h.n; ++i) {
         const CoordEnt& x = q[(h.head + i) % kCoordCap];
@@ -1600,6 +1634,8 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   e->applied_pending = false;
   HIPCHECK(hipMemcpy(e->d_last_index, &e->applied, sizeof(uint64_t), hipMemcpyHostToDevice));
   e->has_sets = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_SET) != e->res_type.end();
+  e->has_mmaps = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_MULTIMAP) != e->res_type.end();
+  if (e->has_mmaps && (rc = ensure_leak(e, kLeakCap))) return rc;
   e->sess_next = h.sess_next;
   e->sess_cap = h.sess_cap;
   e->sess_thr = h.sess_thr;

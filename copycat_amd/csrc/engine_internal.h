@@ -148,8 +148,24 @@ int launch_value_live(const uint32_t* inst, const uint8_t* op, const uint8_t* st
                       const uint64_t* index, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
                       uint32_t max_inst, const uint32_t* val_meta, uint32_t slots, unsigned long long* wrow,
                       uint64_t* live, hipStream_t st);
-int launch_set_results(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
-                       uint32_t max_inst, uint8_t* status, uint64_t* value, hipStream_t st);
+// set / multimap results of the map ops they ran as (map_wide.hip k_keyed_results)
+struct KeyedResultArgs {
+  const uint32_t* inst;
+  const uint8_t* op;
+  const uint8_t* flags;
+  const uint64_t* index;
+  uint64_t n;
+  const uint32_t* inst_res;
+  const uint8_t* res_type;
+  uint32_t max_inst;
+  uint8_t* status;
+  uint64_t* value;
+  LeakRec* leak;  // multimap Put commits (never cleaned)
+  unsigned long long* leak_n;
+  uint64_t leak_cap;
+  uint32_t* err;
+};
+int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st);
 
 constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
 struct HotArgs {

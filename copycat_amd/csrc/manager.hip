@@ -50,7 +50,7 @@ int open_instance(cc_engine* e, uint32_t rslot, uint64_t index, uint64_t client,
 
 // A new key: resource id = commit index, a fresh state machine of `type` (:84-100,155-176).
 int new_resource(cc_engine* e, uint64_t key, uint32_t type, uint64_t index, uint32_t* rslot) {
-  if (type < CC_RES_VALUE || type > CC_RES_QUEUE) return set_err(CC_ERR_INVALID, "unknown resource type");
+  if (type < CC_RES_VALUE || type > CC_RES_MULTIMAP) return set_err(CC_ERR_INVALID, "unknown resource type");
   if (e->res_by_id.count(index)) return set_err(CC_ERR_INVALID, "resource id (commit index) already in use");
   uint32_t s = 0;
   int rc = alloc_res_slot(e, type, &s);

@@ -35,6 +35,9 @@ __device__ inline bool map_wide_op(uint32_t op) {
 __device__ inline bool set_wide_op(uint32_t op) {
   return op == CC_OP_DELETE || op == CC_OP_SET_SIZE || op == CC_OP_SET_ISEMPTY || op == CC_OP_SET_CLEAR;
 }
+__device__ inline bool mmap_wide_op(uint32_t op) {  // MultiMapState.removeValue / isEmpty / clear / delete
+  return op == CC_OP_DELETE || op == CC_OP_MMAP_REMOVEVALUE || op == CC_OP_MMAP_ISEMPTY || op == CC_OP_MMAP_CLEAR;
+}
 __device__ inline bool ttl_op(uint32_t op) {
   return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT ||
          op == CC_OP_SET_ADD;
@@ -51,7 +54,7 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   if (i >= n) return;
   const uint32_t o = op[i];
-  bool wide = map_wide_op(o) || set_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
+  bool wide = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
   if (ttl && (int64_t)aux[i] <= 0) {
@@ -64,9 +67,10 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   const uint32_t ty = res_type[r];
   if (ty == CC_RES_MAP) wide = map_wide_op(o);
   else if (ty == CC_RES_SET) wide = set_wide_op(o);
+  else if (ty == CC_RES_MULTIMAP) wide = mmap_wide_op(o);  // (its Put arms no map TTL timer: A18)
   else if (ty == CC_RES_GROUP) wide = o == CC_OP_GROUP_SCHEDULE;  // MembershipGroupState.schedule: a timer
   else return;
-  if (ty == CC_RES_GROUP && !wide) return;
+  if ((ty == CC_RES_GROUP || ty == CC_RES_MULTIMAP) && !wide) return;
   if (!wide) {
     // not a barrier here: a row that arms a TTL timer on this map / set?
     if (!aux || !(ty == CC_RES_MAP ? ttl_op(o) && o != CC_OP_SET_ADD : o == CC_OP_SET_ADD) || (int64_t)aux[i] <= 0) return;
@@ -224,30 +228,58 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
   out_value[row] = v;
 }
 
-// SetState results (SetState.java:49-87): add returns false whatever happened; remove returns whether the element
-// was present (the map remove it ran as returned the stored Boolean TRUE, or null).
-__global__ __launch_bounds__(kMwT) void k_set_results(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
-                                                     uint64_t n, const uint32_t* __restrict__ inst_res,
-                                                     const uint8_t* __restrict__ res_type, uint32_t max_inst,
-                                                     uint8_t* __restrict__ status, uint64_t* __restrict__ value) {
+// Results of the set / multimap ops that ran as map ops.
+// SetState (SetState.java:49-87): add returns false whatever happened; remove returns whether the element was
+// present (the map remove it ran as returned the stored Boolean TRUE, or null).
+// MultiMapState (MultiMapState.java:48-183): put returns true (its value is never stored, so never "contained")
+// and its commit is never cleaned (-> the leak log); get and remove(key) return an empty collection;
+// remove(key, value) false; size(key) 0.
+__global__ __launch_bounds__(kMwT) void k_keyed_results(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                       const uint8_t* __restrict__ flags, const uint64_t* __restrict__ index,
+                                                       uint64_t n, const uint32_t* __restrict__ inst_res,
+                                                       const uint8_t* __restrict__ res_type, uint32_t max_inst,
+                                                       uint8_t* __restrict__ status, uint64_t* __restrict__ value,
+                                                       LeakRec* __restrict__ leak, unsigned long long* __restrict__ leak_n,
+                                                       uint64_t leak_cap, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   if (i >= n) return;
   const uint32_t o = op[i];
-  if (o != CC_OP_SET_ADD && o != CC_OP_SET_REMOVE) return;
+  const bool set_op = o == CC_OP_SET_ADD || o == CC_OP_SET_REMOVE;
+  const bool mm_op = o == CC_OP_MMAP_PUT || o == CC_OP_MMAP_GET || o == CC_OP_MMAP_REMOVE || o == CC_OP_MMAP_SIZE;
+  if (!set_op && !mm_op) return;
   const uint32_t in = inst[i];
   if (in >= max_inst) return;
   const uint32_t r = inst_res[in];
-  if (r == kNoRes || res_type[r] != CC_RES_SET) return;
+  if (r == kNoRes || res_type[r] != (set_op ? CC_RES_SET : CC_RES_MULTIMAP)) return;
   const uint8_t s = status[i];
   if (CC_STATUS_CODE(s) != CC_ST_OK) return;
-  value[i] = o == CC_OP_SET_ADD ? 0ull : (CC_STATUS_TAG(s) != CC_TAG_NULL ? 1ull : 0ull);
-  status[i] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+  uint32_t tag = CC_TAG_BOOL;
+  uint64_t v = 0;
+  if (set_op) {
+    v = o == CC_OP_SET_ADD ? 0ull : (CC_STATUS_TAG(s) != CC_TAG_NULL ? 1ull : 0ull);
+  } else if (o == CC_OP_MMAP_PUT) {
+    v = 1;
+    const unsigned long long a = atomicAdd(leak_n, 1ull);
+    if (a < leak_cap) {
+      leak[a].idx = index ? index[i] : 0;
+      leak[a].slot = r;
+      leak[a].pad = 0;
+    } else {
+      atomicOr(err, kErrCapacity);
+    }
+  } else if (o == CC_OP_MMAP_SIZE) {
+    tag = CC_TAG_INT;
+  } else if (o == CC_OP_MMAP_GET || CC_FLAG_TAG_A(flags[i]) == CC_TAG_NULL) {
+    tag = CC_TAG_LIST;  // an empty collection
+  }
+  value[i] = v;
+  status[i] = CC_STATUS(CC_ST_OK, tag);
 }
 
-int launch_set_results(const uint32_t* inst, const uint8_t* op, uint64_t n, const uint32_t* inst_res, const uint8_t* res_type,
-                       uint32_t max_inst, uint8_t* status, uint64_t* value, hipStream_t st) {
-  hipLaunchKernelGGL(k_set_results, dim3((uint32_t)((n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, n, inst_res,
-                     res_type, max_inst, status, value);
+int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_keyed_results, dim3((uint32_t)((a.n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, a.inst, a.op, a.flags,
+                     a.index, a.n, a.inst_res, a.res_type, a.max_inst, a.status, a.value, a.leak, a.leak_n, a.leak_cap,
+                     a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

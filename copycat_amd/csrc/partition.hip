@@ -315,11 +315,19 @@ __global__ __launch_bounds__(kPT, CC_PART_WPE) void k_part_tile(const uint32_t* 
               aa[j].x = 1;
             }
             mt[j] = (mt[j] & ~0xFFFFu) | mop | (fl << 8);
+          } else if (ty == CC_RES_MULTIMAP) {  // a multimap key is a map key holding Boolean TRUE
+            uint32_t fl = (mt[j] >> 8) & 0xFF;
+            const uint32_t mop = mmap_as_map_op(mt[j] & 0xFF, fl & 7u);
+            if (mop == CC_OP_MAP_PUTIFABSENT) {
+              fl = (fl & ~7u) | CC_TAG_BOOL;
+              aa[j].x = 1;
+            }
+            mt[j] = (mt[j] & ~0xFFFFu) | mop | (fl << 8);
           }
           kk[j] = ckey[i];
           ii[j] = cidx ? cidx[i] : 0;
           xx[j] = rr[j];
-          if (caux && (int64_t)caux[i] > 0) mt[j] |= kMetaTtl;
+          if (caux && (int64_t)caux[i] > 0 && ty != CC_RES_MULTIMAP) mt[j] |= kMetaTtl;
         } else if (ty == CC_RES_VALUE && !sb_kind[rr[j] >> kSbShift]) {
           value_encode(mt[j] & 0xFF, (mt[j] >> 8) & 0xFF, aa[j].x, aa[j].y, mt[j], aa[j]);
         } else {

@@ -79,6 +79,12 @@ def lib():
             "cc_instance_slot": (i32, [P, u64, P]),
             "cc_resource_slot": (i32, [P, u64, P]),
             "cc_debug_phases": (i32, [P, i32, P]),
+            "cc_wire_codec_default": (None, [P]),
+            "cc_wire_interner_create": (i32, [u64, P]),
+            "cc_wire_interner_destroy": (i32, [P]),
+            "cc_wire_intern": (i32, [P, P, u64, P]),
+            "cc_wire_lookup": (i32, [P, u64, P, u64, P]),
+            "cc_wire_decode": (i32, [P, P, P, P, P, u64, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -178,6 +184,7 @@ class Engine:
         _check(L.cc_engine_create(C.byref(cfg), C.byref(h)))
         self.h = h
         self.max_resources = max_resources
+        self.max_instances = max_instances
         self.device = device
         self.L = L
 

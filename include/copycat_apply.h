@@ -54,6 +54,7 @@ extern "C" {
 #define CC_RES_GROUP     5  /* MembershipGroupState coordination/.../state/MembershipGroupState.java:33 */
 #define CC_RES_SET       6  /* SetState          collections/.../state/SetState.java:32 (shares the map table) */
 #define CC_RES_QUEUE     7  /* QueueState        collections/.../state/QueueState.java:33 (a FIFO of CC_QUEUE_CAP) */
+#define CC_RES_MULTIMAP  8  /* MultiMapState     collections/.../state/MultiMapState.java:30 (shares the map table) */
 #define CC_QUEUE_CAP    64
 
 /* ---- op codes = Catalyst @SerializeWith ids of the inner operation ------------- */
@@ -99,6 +100,20 @@ extern "C" {
 #define CC_OP_SET_SIZE         103  /* query */
 #define CC_OP_SET_ISEMPTY      104  /* query */
 #define CC_OP_SET_CLEAR        105
+/* MultiMapState (collections/.../state/MultiMapCommands.java:205-441): the key travels in the key column (key tag
+ * in CC_FLAGS), the value in operand a, Put's ttl in aux.  ContainsEntry and ContainsValue have no handler in
+ * MultiMapState (unknown operation).  MultiMapState.put never stores its value (:76-82): the state is the set of
+ * keys put and not removed since; every Put commit stays retained (never cleaned or closed).               */
+#define CC_OP_MMAP_CONTAINSKEY   75  /* query */
+#define CC_OP_MMAP_CONTAINSENTRY 76  /* query (no handler) */
+#define CC_OP_MMAP_CONTAINSVALUE 77  /* query (no handler) */
+#define CC_OP_MMAP_PUT           78
+#define CC_OP_MMAP_GET           79  /* query */
+#define CC_OP_MMAP_REMOVE        80  /* a = value, or NULL: remove the key */
+#define CC_OP_MMAP_REMOVEVALUE   81  /* a = value */
+#define CC_OP_MMAP_ISEMPTY       82  /* query */
+#define CC_OP_MMAP_SIZE          83  /* query */
+#define CC_OP_MMAP_CLEAR         84
 
 #define CC_OP_ELECT_LISTEN     110
 #define CC_OP_ELECT_UNLISTEN   111
@@ -120,6 +135,7 @@ extern "C" {
 #define CC_TAG_HANDLE  4   /* host-interned object (String, Runnable callback ...) */
 #define CC_TAG_SET     5   /* result only: Set<Long> of MembershipGroupState.join; payload = member count,
                               members are written to the aux-result stream */
+#define CC_TAG_LIST    6   /* result only: a Collection (MultiMapState get / remove(key)); payload = element count */
 
 /* flags column: bits 0-2 tag(a), bits 3-5 tag(b), bits 6-7 key tag (keys are never null,
  * KeyCommand asserts notNull MapCommands.java:77): 0 LONG, 1 INT, 2 BOOL, 3 HANDLE.               */
@@ -388,6 +404,58 @@ int  cc_quorum_commit(const uint64_t* d_match, uint32_t replicas, uint64_t group
  * expires).  Bit s of d_bitmap (u64 words, LSB first) is set for expired sessions; *d_count (u64) += expired. */
 int  cc_expire_sweep(const uint64_t* d_last, uint64_t sessions, uint64_t now, uint64_t timeout,
                      uint64_t* d_bitmap, uint64_t* d_count, void* stream);
+
+/* ---- Catalyst wire format -> columns (copycat_amd/csrc/wire.cpp) ----------------------
+ * A committed resource entry is InstanceCommand / InstanceQuery (@SerializeWith 30 / 31): writeLong(instance id),
+ * then serializer.writeObject(operation) (InstanceOperation.java:60-69); the operation's @SerializeWith id is the
+ * CC_OP_* code and its fields follow its writeObject chain (wire.cpp kSchema cites each).  Manager entries
+ * (GetResource 35, CreateResource 36, DeleteResource 37, ResourceExists 38) decode to control rows.
+ * Catalyst (Serializer / Buffer) is not vendored: the identifier byte before a registered type id (0 null,
+ * 1..4 an id of 1..4 bytes, 5 a class name), the ids of Long / Integer / Boolean / String, byte order and the
+ * UTF-8 framing are cc_wire_codec fields; the defaults below are this engine's restatement of Catalyst 1.x
+ * (parity unpinned: set them from the deployment's serializer registry). */
+#define CC_WIRE_ID_BOOLEAN 129
+#define CC_WIRE_ID_INTEGER 132
+#define CC_WIRE_ID_LONG    133
+#define CC_WIRE_ID_STRING  136
+typedef struct cc_wire_codec {
+  uint8_t  big_endian;          /* Catalyst Buffer byte order (1: big-endian, Java's)                        */
+  uint8_t  utf8_presence_byte;  /* writeUTF8 writes a boolean "not null" byte before the length               */
+  uint8_t  utf8_len_bytes;      /* width of writeUTF8's length prefix                                        */
+  uint8_t  reserved8;
+  int32_t  id_bool, id_int, id_long, id_string;  /* registered serializer ids                                  */
+  uint64_t reserved[4];
+} cc_wire_codec;
+void cc_wire_codec_default(cc_wire_codec* c);
+/* String values and resource keys become CC_TAG_HANDLE handles through an interner (equal bytes, equal handle:
+ * Java String.equals); handles are first_handle, first_handle + 1, ... in order of first appearance. */
+typedef struct cc_wire_interner cc_wire_interner;
+int  cc_wire_interner_create(uint64_t first_handle, cc_wire_interner** out);
+int  cc_wire_interner_destroy(cc_wire_interner* in);
+int  cc_wire_intern(cc_wire_interner* in, const uint8_t* bytes, uint64_t len, uint64_t* handle);
+int  cc_wire_lookup(cc_wire_interner* in, uint64_t handle, uint8_t* buf, uint64_t cap, uint64_t* len);
+/* decoded rows (host memory, n each).  kind 0: a resource operation (inst = the instance slot of the instance
+ * id through the engine's session registry, max_instances when unknown -> CC_ST_UNKNOWN_SESSION when applied;
+ * iid = the instance id itself; op/flags/key/a/b/aux as cc_batch).  With e == NULL (no engine: host-only
+ * decoding) inst is not written and iid is required.  kind 35/36/38: get/create/exists with key = the key's handle, a = the
+ * CC_RES_* of the state machine class (CC_RES_NONE when not one this engine runs); kind 37: delete, b = the
+ * resource id.  index and time are the log entry's own (the caller's) and are not touched. */
+typedef struct cc_wire_out {
+  uint32_t* inst;   /* needs an engine */
+  uint64_t* iid;    /* optional with an engine */
+  uint8_t*  op;
+  uint8_t*  flags;
+  uint64_t* key;
+  uint64_t* a;
+  uint64_t* b;
+  uint64_t* aux;
+  uint8_t*  kind;
+} cc_wire_out;
+/* Entry i is buf[offsets[i], offsets[i+1]).  Fails (CC_ERR_INVALID, *bad_row = the entry) on a truncated or
+ * over-long entry, an unknown operation, a null key, or a value that is neither null, Long, Integer, Boolean
+ * nor String (user objects have no canonical tag); rows before *bad_row are decoded. */
+int  cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* in, const uint8_t* buf,
+                    const uint64_t* offsets, uint64_t n, const cc_wire_out* out, uint64_t* bad_row);
 
 #ifdef __cplusplus
 }

@@ -289,6 +289,7 @@ struct orc {
       case CC_RES_QUEUE:  // QueueState.delete :191-199
         r.q.clear();
         return CC_ST_OK;
+      case CC_RES_MULTIMAP:  // MultiMapState.delete :209-222 (its value maps are always empty: A18)
       case CC_RES_SET:  // SetState.delete :123-134 (same shape: cancel timers, clean, clear)
       case CC_RES_MAP: {  // MapState.delete :264-274
         for (auto& kv : r.m.m) if (kv.second.timer) cancel(kv.second.timer);
@@ -677,6 +678,52 @@ struct orc {
         }
         break;
       }
+      case CC_RES_MULTIMAP: {  // MultiMapState (collections/src/main/java/io/atomix/collections/state/MultiMapState.java)
+        // map: key -> LinkedHashMap<value, commit>; put registers the key's map but never stores the value into it
+        // (:70-82), so every value map stays empty and the state is the set of keys (A18).  Entries of r.m are those
+        // keys (value Boolean TRUE as a marker).
+        MapSM& s = r.m;
+        MapKey k{ktag_to_tag(CC_FLAG_KTAG(c.flags)), c.key};
+        switch (c.op) {
+          case CC_OP_MMAP_CONTAINSKEY:  // containsKey :37-43
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, s.m.count(k) ? 1 : 0));
+            return;
+          case CC_OP_MMAP_GET:  // get :48-63 — the key's (empty) value map -> an empty collection
+            ret(CC_ST_OK, tv(CC_TAG_LIST, 0));
+            return;
+          case CC_OP_MMAP_PUT: {  // put :68-91 — !values.containsKey(value) always holds: true, commit never cleaned;
+            // a ttl > 0 schedules keyValues.remove(value).clean(), which throws (remove returns null) and changes
+            // nothing (A18)
+            if (!s.m.count(k)) {
+              MapEntry e; e.value = tv(CC_TAG_BOOL, 1); e.commit_index = c.index; e.seq = s.order.on_insert();
+              s.m.emplace(k, e);
+            }
+            r.leaked.push_back(c.index);
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, 1));
+            return;
+          }
+          case CC_OP_MMAP_REMOVE:  // remove :96-135
+            if (!tv_null(a)) {  // values.remove(value) finds nothing: false, the key stays
+              ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
+              return;
+            }
+            if (s.m.erase(k)) s.order.on_remove();  // map.remove(key): its (empty) values as a collection
+            ret(CC_ST_OK, tv(CC_TAG_LIST, 0));
+            return;
+          case CC_OP_MMAP_REMOVEVALUE:  // removeValue :140-165 — no entry matches; every (empty) value map goes
+          case CC_OP_MMAP_CLEAR:        // clear :201-207 -> delete()
+            sm_delete(in.res);
+            ret(CC_ST_OK, TV());
+            return;
+          case CC_OP_MMAP_SIZE:  // size :170-185 — sums of empty value maps
+            ret(CC_ST_OK, tv(CC_TAG_INT, 0));
+            return;
+          case CC_OP_MMAP_ISEMPTY:  // isEmpty :190-196 — keys with empty value maps still count
+            ret(CC_ST_OK, tv(CC_TAG_BOOL, s.m.empty() ? 1 : 0));
+            return;
+        }
+        break;  // ContainsEntry / ContainsValue: no handler
+      }
       case CC_RES_LOCK: {
         LockSM& s = r.l;
         switch (c.op) {
@@ -833,7 +880,7 @@ orc* orc_create(uint32_t max_resources, uint32_t max_instances, uint32_t flags) 
 void orc_destroy(orc* o) { delete o; }
 
 int orc_resource_create(orc* o, uint32_t slot, uint32_t type) {
-  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_QUEUE || o->res[slot].exists || o->res[slot].zombie)
+  if (!o || slot >= o->max_res || type < CC_RES_VALUE || type > CC_RES_MULTIMAP || o->res[slot].exists || o->res[slot].zombie)
     return CC_ERR_INVALID;
   o->init_resource(slot, type, slot);
   return CC_OK;
@@ -1081,6 +1128,8 @@ int64_t orc_read_retained(orc* o, uint32_t slot, uint64_t cap, uint64_t* out) {
     case CC_RES_QUEUE:
       for (auto& e : r.q) if (!e.cleaned) v.push_back(e.idx);
       break;
+    case CC_RES_MULTIMAP:  // every Put (in `leaked`)
+      break;
   }
   std::sort(v.begin(), v.end());
   for (uint64_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
@@ -1088,13 +1137,13 @@ int64_t orc_read_retained(orc* o, uint32_t slot, uint64_t cap, uint64_t* out) {
 }
 
 int64_t orc_map_size(orc* o, uint32_t res) {
-  if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET)) return -1;
+  if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET && o->res[res].type != CC_RES_MULTIMAP)) return -1;
   return (int64_t)o->res[res].m.m.size();
 }
 
 int64_t orc_map_entries(orc* o, uint32_t res, uint64_t cap, uint8_t* ktag, uint64_t* key, uint8_t* vtag, uint64_t* val,
                         uint64_t* commit_index) {
-  if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET)) return -1;
+  if (res >= o->max_res || !o->res[res].exists || (o->res[res].type != CC_RES_MAP && o->res[res].type != CC_RES_SET && o->res[res].type != CC_RES_MULTIMAP)) return -1;
   std::vector<std::pair<MapKey, MapEntry>> v(o->res[res].m.m.begin(), o->res[res].m.m.end());
   std::sort(v.begin(), v.end(), [](const std::pair<MapKey, MapEntry>& x, const std::pair<MapKey, MapEntry>& y) {
     return x.first.tag != y.first.tag ? x.first.tag < y.first.tag : x.first.k < y.first.k;

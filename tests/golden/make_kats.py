@@ -10,7 +10,8 @@ Two kinds of KAT, each citing where its expected answers come from:
   * "defined": rules that live in the un-vendored Copycat jar (timer order, quorum, expiry) — the answer
     is this engine's documented rule, i.e. "parity unpinned".
 
-Value encoding: ["NULL"] | ["LONG", n] | ["INT", n] | ["BOOL", b] | ["H", handle] | ["SET", [ids...]].
+Value encoding: ["NULL"] | ["LONG", n] | ["INT", n] | ["BOOL", b] | ["H", handle] | ["SET", [ids...]]
+| ["LIST", [values...]].
 Run: python tests/golden/make_kats.py  (deterministic; the JSON is committed)
 """
 import json
@@ -43,6 +44,10 @@ def B(b):
 
 def SET(*ids):
     return ["SET", sorted(ids)]
+
+
+def LIST(*vals):
+    return ["LIST", list(vals)]
 
 
 class K:
@@ -434,6 +439,34 @@ def kats():
     out.append(k.res(0, "MAP").inst(0, 0, 100, 1)
                .c(0, "MAP_PUT", key=foo, a=hw, aux=100, time=0)
                .c(0, "MAP_GET", key=foo, expect=NULL, time=100))
+    # MultiMapState.put registers the key's value map but never stores the value (MultiMapState.java:70-82): every
+    # put answers true, get and size see empty value maps, remove(key, value) finds nothing, removeValue drops every
+    # key (all value maps are empty, :140-165), and a put's TTL timer throws before it changes anything (A18).
+    k = K("A18_multimap_put_never_stores", "quirk", "collections/src/main/java/io/atomix/collections/state/MultiMapState.java:37-222")
+    out.append(k.res(0, "MULTIMAP").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
+               .c(0, "MMAP_ISEMPTY", expect=B(True), time=0)
+               .c(0, "MMAP_PUT", key=foo, a=hw, expect=B(True), time=0)
+               .c(1, "MMAP_PUT", key=foo, a=hw, expect=B(True), time=0)   # the value is still not "contained"
+               .c(1, "MMAP_CONTAINSKEY", key=foo, expect=B(True), time=0)
+               .c(0, "MMAP_GET", key=foo, expect=LIST(), time=0)
+               .c(0, "MMAP_SIZE", key=foo, expect=I(0), time=0)
+               .c(0, "MMAP_ISEMPTY", expect=B(False), time=0)
+               .c(0, "MMAP_REMOVE", key=foo, a=hw, expect=B(False), time=0)
+               .c(0, "MMAP_CONTAINSKEY", key=foo, expect=B(True), time=0)
+               .c(0, "MMAP_CONTAINSENTRY", key=foo, a=hw, status="UNKNOWN_OP", time=0)  # no handler
+               .c(0, "MMAP_CONTAINSVALUE", a=hw, status="UNKNOWN_OP", time=0)
+               .c(1, "MMAP_REMOVE", key=foo, expect=LIST(), time=0)
+               .c(0, "MMAP_CONTAINSKEY", key=foo, expect=B(False), time=0)
+               .c(0, "MMAP_REMOVE", key=foo, expect=LIST(), time=0)          # absent key: EMPTY_LIST
+               .c(0, "MMAP_PUT", key=bar, a=hw, aux=50, expect=B(True), time=0)
+               .c(0, "MMAP_PUT", key=foo, a=NULL, expect=B(True), time=0)
+               .c(0, "MMAP_CONTAINSKEY", key=bar, expect=B(True), time=100)  # the TTL timer changed nothing
+               .c(0, "MMAP_CONTAINSKEY", key=bar, expect=B(True), time=100)
+               .c(1, "MMAP_REMOVEVALUE", a=foo, time=100)                     # drops every (empty) key
+               .c(0, "MMAP_ISEMPTY", expect=B(True), time=100)
+               .c(0, "MMAP_PUT", key=foo, a=bar, expect=B(True), time=100)
+               .c(0, "MMAP_CLEAR", time=100)
+               .c(0, "MMAP_CONTAINSKEY", key=foo, expect=B(False), time=100))
     return out
 
 

@@ -16,9 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 KAT_PATH = os.path.join(HERE, "golden", "kats.json")
 
 RES = {"VALUE": abi.CC_RES_VALUE, "MAP": abi.CC_RES_MAP, "LOCK": abi.CC_RES_LOCK, "ELECTION": abi.CC_RES_ELECTION,
-       "GROUP": abi.CC_RES_GROUP, "SET": abi.CC_RES_SET, "QUEUE": abi.CC_RES_QUEUE}
+       "GROUP": abi.CC_RES_GROUP, "SET": abi.CC_RES_SET, "QUEUE": abi.CC_RES_QUEUE,
+       "MULTIMAP": abi.CC_RES_MULTIMAP}
 TAG = {"NULL": abi.CC_TAG_NULL, "LONG": abi.CC_TAG_LONG, "INT": abi.CC_TAG_INT, "BOOL": abi.CC_TAG_BOOL,
-       "H": abi.CC_TAG_HANDLE, "SET": abi.CC_TAG_SET}
+       "H": abi.CC_TAG_HANDLE, "SET": abi.CC_TAG_SET, "LIST": abi.CC_TAG_LIST}
 EV = {"CHANGE": abi.CC_EV_CHANGE, "LOCK": abi.CC_EV_LOCK, "ELECT": abi.CC_EV_ELECT, "JOIN": abi.CC_EV_JOIN,
       "LEAVE": abi.CC_EV_LEAVE, "EXECUTE": abi.CC_EV_EXECUTE}
 ST = {"OK": abi.CC_ST_OK, "UNKNOWN_SESSION": abi.CC_ST_UNKNOWN_SESSION, "UNKNOWN_OP": abi.CC_ST_UNKNOWN_OP,
@@ -39,7 +40,7 @@ def enc(v):
         return t, 0
     if t == abi.CC_TAG_BOOL:
         return t, int(bool(v[1]))
-    if t == abi.CC_TAG_SET:
+    if t in (abi.CC_TAG_SET, abi.CC_TAG_LIST):
         return t, len(v[1])
     return t, int(v[1]) & 0xFFFFFFFFFFFFFFFF
 
@@ -57,18 +58,20 @@ GPU_MAP_OPS = {"MAP_CONTAINSKEY", "MAP_PUT", "MAP_PUTIFABSENT", "MAP_GET", "MAP_
 GPU_SET_OPS = {"SET_CONTAINS", "SET_ADD", "SET_REMOVE", "SET_SIZE", "SET_ISEMPTY", "SET_CLEAR"}
 GPU_QUEUE_OPS = {"QUEUE_CONTAINS", "QUEUE_ADD", "QUEUE_OFFER", "QUEUE_PEEK", "QUEUE_POLL", "QUEUE_ELEMENT", "QUEUE_REMOVE",
                  "QUEUE_SIZE", "QUEUE_ISEMPTY", "QUEUE_CLEAR"}
+GPU_MMAP_OPS = {"MMAP_CONTAINSKEY", "MMAP_CONTAINSENTRY", "MMAP_CONTAINSVALUE", "MMAP_PUT", "MMAP_GET", "MMAP_REMOVE",
+                "MMAP_REMOVEVALUE", "MMAP_ISEMPTY", "MMAP_SIZE", "MMAP_CLEAR"}
 
 
 def gpu_eligible(kat):
     """KATs whose every step this build runs through the engine: every op of every covered state machine, Delete,
     clock advances, session closes (the GPU close fan-out) and manager control commands (manager.hip)."""
     types = {r[1] for r in kat["resources"]}
-    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET", "QUEUE"}:
+    if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET", "QUEUE", "MULTIMAP"}:
         return False
     for s in kat["steps"]:
         if "commit" in s:
             c = s["commit"]
-            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS | GPU_SET_OPS | GPU_QUEUE_OPS:
+            if c["op"] != "DELETE" and c["op"] not in GPU_VALUE_OPS | GPU_MAP_OPS | GPU_COORD_OPS | GPU_SET_OPS | GPU_QUEUE_OPS | GPU_MMAP_OPS:
                 return False
     return True
 

@@ -21,7 +21,7 @@ def test_gpu_kat_coverage():
             # session close fan-out (close.hip) and the manager control plane (manager.hip)
             "election_next_on_close", "A10_close_publishes_leave_for_non_member", "A11_lock_survives_holder_close",
             "manager_create_concurrency", "manager_get_create_concurrency", "manager_operate_many",
-            "manager_get_reuses_instance", "A13_delete_resource_by_instance_id"} <= names
+            "manager_get_reuses_instance", "A13_delete_resource_by_instance_id", "A18_multimap_put_never_stores"} <= names
     assert len(KATS) == len(all_kats())  # every reference-pinned KAT runs through the engine
 
 
