@@ -34,6 +34,24 @@
 
 namespace cc {
 
+#ifdef CC_PHASE_TIMING
+__device__ unsigned long long g_ph_map[kPhases];
+int phase_read_map(uint64_t* out) {
+  unsigned long long z[kPhases] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ph_map), sizeof z) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_ph_map), z, sizeof z) != hipSuccess)
+    return CC_ERR_HIP;
+  return CC_OK;
+}
+#endif
+
+#ifndef CC_MAP_MT
+#define CC_MAP_MT 512  // threads of k_apply_map<false>
+#endif
+#ifndef CC_MAP_CHUNK
+#define CC_MAP_CHUNK 2048  // commits per chunk of k_apply_map<false> (CC_MAP_CHUNK / CC_MAP_MT per thread)
+#endif
+constexpr uint32_t kNoRef = 0xFFFFFFFFu;
 constexpr uint32_t kNoEnt = 0xFFFFu;
 constexpr uint32_t kEntFull = 0xFFFEu;
 
@@ -45,7 +63,7 @@ __device__ inline uint32_t map_ident_of(uint32_t res, uint32_t flags) { return m
 // clock; manager mode: the previous commit's, A8), and a commit that stores a value re-arms or cancels the timer.
 // The per-record clocks come from the input columns through map_row (staging position -> batch row).
 template <bool TTL>
-__global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
+__global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
                                                   const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
                                                   const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
@@ -57,19 +75,29 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
                                                   uint32_t* __restrict__ err_out) {
-  constexpr int MT = TTL ? 512 : 1024;    // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
+  constexpr int MT = TTL ? 512 : CC_MAP_MT;  // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
   constexpr int MEPer = kMapRegion / MT;  // table entries per thread
-  constexpr int kMPer = 1;                // commits per thread per chunk
+  constexpr int kMPer = TTL ? 1 : CC_MAP_CHUNK / CC_MAP_MT;  // commits per thread per chunk
   constexpr int kMCh = MT * kMPer;
   __shared__ uint64_t tkey[kMapRegion];
   __shared__ uint32_t tword[kMapRegion];
   __shared__ uint64_t tval[kMapRegion];
-  __shared__ uint64_t tci[kMapRegion];   // commit index of the entry's current value (MapState.Value.commit)
-  __shared__ uint64_t tins[kMapRegion];  // commit index that created the entry's HashMap node
-  __shared__ u64x2 rab[kMCh];          // chunk sorted by entry
-  __shared__ uint32_t rmeta[kMCh];
-  __shared__ uint32_t rpos[kMCh];      // staging position
-  __shared__ uint64_t ridx[kMCh];      // commit index
+  // The entry's commit index (MapState.Value.commit) and node-creating index stay in HBM (tbl_ci / tbl_ins): the
+  // kernel only records, per entry, the staging position of the commit that last rewrote them (kNoRef: none), and
+  // the write-back gathers those commits' log indices.
+  __shared__ uint32_t tcr[kMapRegion];
+  __shared__ uint32_t tir[kMapRegion];
+  // the chunk sorted by entry: rab u64x2 | rmeta u32 | rpos u32 (staging position: the commit index is read from
+  // the staging area only for the commits that end up in tbl_ci / tbl_ins); the same bytes hold the per-wave entry
+  // counts (u16, 2 per word) during the sort
+  constexpr int NW = MT / kWave;
+  constexpr int kRb = kMCh * 24 > NW * kMapRegion * 2 ? kMCh * 24 : NW * kMapRegion * 2;
+  static_assert(kMPer * kWave < 65536, "per-wave counts are u16");
+  __shared__ __align__(16) uint8_t rbuf[kRb];
+  u64x2* const rab = reinterpret_cast<u64x2*>(rbuf);
+  uint32_t* const rmeta = reinterpret_cast<uint32_t*>(rbuf + kMCh * 16);
+  uint32_t* const rpos = reinterpret_cast<uint32_t*>(rbuf + kMCh * 20);
+  uint32_t* const wtab = reinterpret_cast<uint32_t*>(rbuf);  // [NW][kMapRegion / 2]
   __shared__ uint16_t rent[kMCh];      // entry
   __shared__ uint64_t tdl[TTL ? kMapRegion : 1];  // timer deadline of the entry (0: none)
   __shared__ uint64_t rfire[TTL ? kMCh : 1];      // clock of the last timer firing before the commit
@@ -87,6 +115,7 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
   const uint32_t region = blockIdx.x, k = sb_val + region, t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t tb = (uint64_t)region * kMapRegion;
   uint32_t err = 0;
+  PH_DECL
 
   // ---- load the region; compact it when more than 3/4 of its entries are bound ----
   if (t < 3) flag[t] = 0;
@@ -94,7 +123,7 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
   for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
   for (uint32_t q = t; q < kMapRegion; q += MT) eflag[q] = 0;
   {
-    uint64_t ek[MEPer], ev[MEPer], eci[MEPer], eins[MEPer], edl[MEPer];
+    uint64_t ek[MEPer], ev[MEPer], edl[MEPer];
     uint32_t ew[MEPer], used = 0;
 #pragma unroll
     for (int q = 0; q < MEPer; ++q) {
@@ -102,8 +131,6 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
       ek[q] = tbl_key[tb + e];
       ew[q] = tbl_word[tb + e];
       ev[q] = tbl_val[tb + e];
-      eci[q] = tbl_ci[tb + e];
-      eins[q] = tbl_ins[tb + e];
       edl[q] = TTL ? tbl_dl[tb + e] : 0;
       used += (ew[q] & kMwUsed) ? 1 : 0;
     }
@@ -117,12 +144,20 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
       tkey[e] = ek[q];
       tword[e] = compact ? 0u : ew[q];
       tval[e] = ev[q];
-      tci[e] = eci[q];
-      tins[e] = eins[q];
+      tcr[e] = kNoRef;
+      tir[e] = kNoRef;
       if (TTL) tdl[e] = compact ? 0 : edl[q];
     }
     lds_barrier();
     if (compact) {
+      // the live entries' indices move with them (read all before any is written: __syncthreads orders HBM too)
+      uint64_t eci[MEPer], eins[MEPer];
+#pragma unroll
+      for (int q = 0; q < MEPer; ++q) {
+        eci[q] = tbl_ci[tb + q * MT + t];
+        eins[q] = tbl_ins[tb + q * MT + t];
+      }
+      __syncthreads();
       // live keys are distinct: claim the first free slot of each probe chain (no key comparisons needed)
 #pragma unroll
       for (int q = 0; q < MEPer; ++q) {
@@ -134,12 +169,12 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
           while (atomicCAS(&tword[p], 0u, ew[q]) != 0u) p = (p + 1) & (kMapRegion - 1);
           tkey[p] = ek[q];
           tval[p] = ev[q];
-          tci[p] = eci[q];
-          tins[p] = eins[q];
+          tbl_ci[tb + p] = eci[q];
+          tbl_ins[tb + p] = eins[q];
           if (TTL) tdl[p] = edl[q];
         }
       }
-      lds_barrier();
+      __syncthreads();
     }
   }
 
@@ -180,37 +215,59 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
   }
   const uint32_t cnt = rpre[tiles];
   uint32_t round = 0;  // resolution rounds (continues across chunks: flag[] is a 3-deep ring)
+  PH(0);
 
-  for (uint32_t c0 = 0; c0 < cnt; c0 += kMCh) {
-    // ---- load this thread's commits: chunk order (w, j, l) = log order ----
-    uint32_t m[kMPer], res[kMPer], g[kMPer], ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
-    u64x2 ab[kMPer];
-    uint64_t key[kMPer], idx[kMPer];
-    bool keyop[kMPer];
+  // the records of chunk c0 (this thread's: chunk order (w, j, l) = log order); the next chunk's are requested
+  // at the top of each chunk and land while it is applied
+  uint32_t nm[kMPer], nres[kMPer], ng[kMPer];
+  u64x2 nab[kMPer];
+  uint64_t nkey[kMPer];
+  auto load_chunk = [&](uint32_t c0) {
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       const uint32_t c = c0 + w * (kWave * kMPer) + j * kWave + l;
-      ent[j] = kNoEnt;
-      keyop[j] = false;
-      g[j] = 0xFFFFFFFFu;
+      ng[j] = 0xFFFFFFFFu;
       if (c < cnt) {
         uint32_t lo = 0, hi = tiles;  // last tile with rpre <= c
         while (hi - lo > 1) {
           const uint32_t mid = (lo + hi) >> 1;
           if (rpre[mid] <= c) lo = mid; else hi = mid;
         }
-        g[j] = rstart[lo] + (c - rpre[lo]);
-        m[j] = st_meta[g[j]];
-        ab[j] = st_ab[g[j]];
-        res[j] = st_res[g[j]];
-        key[j] = st_key[g[j]];
-        idx[j] = st_idx[g[j]];
+        ng[j] = rstart[lo] + (c - rpre[lo]);
+        nm[j] = st_meta[ng[j]];
+        nab[j] = st_ab[ng[j]];
+        nres[j] = st_res[ng[j]];
+        nkey[j] = st_key[ng[j]];
+      }
+    }
+  };
+  load_chunk(0);
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kMCh) {
+    uint32_t m[kMPer], res[kMPer], g[kMPer], ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
+    u64x2 ab[kMPer];
+    uint64_t key[kMPer];
+    bool keyop[kMPer];
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      g[j] = ng[j];
+      m[j] = nm[j];
+      ab[j] = nab[j];
+      res[j] = nres[j];
+      key[j] = nkey[j];
+    }
+    if (c0 + kMCh < cnt) load_chunk(c0 + kMCh);  // block-uniform
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      ent[j] = kNoEnt;
+      keyop[j] = false;
+      if (g[j] != 0xFFFFFFFFu) {
         const uint32_t op = smeta_op(m[j]);
         keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
         ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
         p[j] = (uint32_t)map_hash(res[j], CC_FLAG_KTAG(smeta_flags(m[j])), key[j]) & (kMapRegion - 1);
       }
     }
+    PH(1);
     // ---- 1. binding rounds (put / putIfAbsent) ----
     bool pend[kMPer];
 #pragma unroll
@@ -259,6 +316,7 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
       if (!go) break;
     }
     ++round;
+    PH(2);
     // ---- 2. lookup for the other key ops (nothing is pending now) ----
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
@@ -289,15 +347,37 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         rst_value[g[j]] = rv;
       }
     }
-    // ---- 3. stable counting sort by entry: one wave at a time keeps log order ----
-    for (uint32_t q = 0; q < MT / kWave; ++q) {
-      if (w == q) {
+    PH(3);
+    // ---- 3. stable counting sort by entry: per-wave counts (in-wave rank from LDS atomics with return: same-
+    //         address lanes of one instruction resolve in lane order, checked at engine start), totals per entry,
+    //         then a commit's run position = run start + its entry's count in earlier waves + its in-wave rank ----
+    for (uint32_t q = t; q < (uint32_t)(NW * kMapRegion / 2); q += MT) wtab[q] = 0;
+    lds_barrier();
 #pragma unroll
-        for (int j = 0; j < kMPer; ++j)
-          if (ent[j] != kNoEnt) rk[j] = atomicAdd(&ecnt[ent[j]], 1u);
+    for (int j = 0; j < kMPer; ++j)  // program order over j, lane order inside one instruction = log order
+      if (ent[j] != kNoEnt) {
+        const uint32_t sh = 16 * (ent[j] & 1);
+        rk[j] = (atomicAdd(&wtab[w * (kMapRegion / 2) + (ent[j] >> 1)], 1u << sh) >> sh) & 0xFFFFu;
       }
-      lds_barrier();
+    lds_barrier();
+    for (uint32_t e2 = t; e2 < (uint32_t)(kMapRegion / 2); e2 += MT) {  // totals of 2 entries
+      uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const uint32_t c = wtab[q * (kMapRegion / 2) + e2];
+        s0 += c & 0xFFFF;
+        s1 += c >> 16;
+      }
+      ecnt[2 * e2 + 0] = s0;
+      ecnt[2 * e2 + 1] = s1;
     }
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j)  // + the entry's commits in earlier waves (wave-uniform trip count)
+      if (ent[j] != kNoEnt) {
+        const uint32_t sh = 16 * (ent[j] & 1);
+        for (uint32_t q = 0; q < w; ++q) rk[j] += (wtab[q * (kMapRegion / 2) + (ent[j] >> 1)] >> sh) & 0xFFFFu;
+      }
+    lds_barrier();
     {
       uint32_t v[MEPer], sum = 0;
 #pragma unroll
@@ -331,7 +411,6 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
       rab[s] = ab[j];
       rmeta[s] = m[j];
       rpos[s] = g[j];
-      ridx[s] = idx[j];
       rent[s] = (uint16_t)ent[j];
       if (TTL) {
         const uint64_t cb = clock_base ? *clock_base : 0;
@@ -349,6 +428,7 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
       }
     }
     lds_barrier();
+    PH(4);
     // ---- 4. every run (one entry's commits, log order) at once: a segmented scan of the commits'
     //         transformers gives each commit its entry's state before it (map_ops.h); runs holding a
     //         value-comparing op are walked by one thread instead ----
@@ -399,8 +479,8 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         if (l > 0) pre = oh ? o : compose(pre, o);
       }
       // walk this thread's commits from its prefix
-      uint32_t fe[kMPer], fw[kMPer];
-      uint64_t fv[kMPer], fci[kMPer], fins[kMPer];
+      uint32_t fe[kMPer], fw[kMPer], fcr[kMPer], fir[kMPer];
+      uint64_t fv[kMPer];
       bool fin[kMPer];
       Comp cur = pre;
 #pragma unroll
@@ -412,9 +492,9 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         if (hd[q]) cur = comp_identity();
         if (eflag[e]) continue;
         const uint32_t mm = rmeta[s];
-        uint32_t sw;
-        uint64_t sv, sci, sins;
-        materialize_lds(cur, tword[e], tval[e], tci[e], tins[e], rmeta, rab, ridx, sw, sv, sci, sins);
+        uint32_t sw, svr, snr;
+        uint64_t sv;
+        materialize_ref(cur, tword[e], tval[e], rmeta, rab, sw, sv, svr, snr);
         uint64_t rv;
         bool wrote, created;
         const u64x2 x = rab[s];
@@ -425,7 +505,10 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
           fin[q] = true;
           fe[q] = e;
-          materialize_lds(cur, tword[e], tval[e], tci[e], tins[e], rmeta, rab, ridx, fw[q], fv[q], fci[q], fins[q]);
+          uint32_t vr, nr;
+          materialize_ref(cur, tword[e], tval[e], rmeta, rab, fw[q], fv[q], vr, nr);
+          fcr[q] = vr != kOrig ? rpos[vr] : kNoRef;  // the rewriting commit's staging position
+          fir[q] = nr != kOrig ? rpos[nr] : kNoRef;
         }
       }
       lds_barrier();  // every pre-state has been read
@@ -434,10 +517,11 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         if (!fin[q]) continue;
         tword[fe[q]] = fw[q];
         tval[fe[q]] = fv[q];
-        tci[fe[q]] = fci[q];
-        tins[fe[q]] = fins[q];
+        if (fcr[q] != kNoRef) tcr[fe[q]] = fcr[q];
+        if (fir[q] != kNoRef) tir[fe[q]] = fir[q];
       }
     }
+    PH(5);
     // runs with a value-comparing op: sequentially, by the thread holding the run's first commit
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
@@ -445,7 +529,8 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
       const uint32_t e = ent[j];
       const uint32_t s0 = ecnt[e], s1 = ecnt[e + 1];
       uint32_t wv = tword[e];
-      uint64_t vv = tval[e], ci = 0, ins = 0, dl = TTL ? tdl[e] : 0;
+      uint64_t vv = tval[e], dl = TTL ? tdl[e] : 0;
+      uint32_t ci = 0, ins = 0;
       bool any_w = false, any_c = false;
       for (uint32_t s = s0; s < s1; ++s) {
         const uint32_t mm = rmeta[s];
@@ -464,19 +549,20 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
         }
         rst_status[rpos[s]] = (uint8_t)st;
         rst_value[rpos[s]] = rv;
-        if (wrote) { ci = ridx[s]; any_w = true; }
-        if (created) { ins = ridx[s]; any_c = true; }
+        if (wrote) { ci = rpos[s]; any_w = true; }
+        if (created) { ins = rpos[s]; any_c = true; }
       }
       tword[e] = wv;
       tval[e] = vv;
       if (TTL) tdl[e] = dl;
-      if (any_w) tci[e] = ci;
-      if (any_c) tins[e] = ins;
+      if (any_w) tcr[e] = ci;
+      if (any_c) tir[e] = ins;
     }
     lds_barrier();
     for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
     for (uint32_t q = t; q < kMapRegion; q += MT) eflag[q] = 0;
     lds_barrier();
+    PH(6);
   }
 
   // ---- write the region back ----
@@ -486,10 +572,12 @@ __global__ __launch_bounds__(1024) void k_apply_map(const uint32_t* __restrict__
     tbl_key[tb + e] = tkey[e];
     tbl_word[tb + e] = tword[e];
     tbl_val[tb + e] = tval[e];
-    tbl_ci[tb + e] = tci[e];
-    tbl_ins[tb + e] = tins[e];
+    if (tcr[e] != kNoRef) tbl_ci[tb + e] = st_idx[tcr[e]];
+    if (tir[e] != kNoRef) tbl_ins[tb + e] = st_idx[tir[e]];
     if (TTL) tbl_dl[tb + e] = tdl[e];
   }
+  PH(7);
+  if (!TTL) PH_FLUSH(g_ph_map);
   if (err) atomicOr(err_out, err);
 }
 
@@ -510,7 +598,7 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
                        (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.err);
   else
-    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(1024), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
+    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
                        a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.err);

@@ -59,6 +59,7 @@ int launch_partition(const PartArgs& a, hipStream_t st);
 int launch_tile_hist16(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_value(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_v2(const PartArgs& a, uint32_t tiles, hipStream_t st);
+int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st);
 size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk);
 
 struct ValueArgs {

@@ -209,6 +209,27 @@ __device__ inline void materialize_lds(const Comp& c, uint32_t w0, uint64_t v0, 
   }
 }
 
+// The same, for a kernel that keeps the commit / insert indices in HBM: the (word, value) state and the chunk
+// records whose commit rewrote the commit index (vref) and created the node (nref); kOrig: unchanged.
+__device__ inline void materialize_ref(const Comp& c, uint32_t w0, uint64_t v0, const uint32_t* rmeta, const u64x2* rab,
+                                       uint32_t& w, uint64_t& v, uint32_t& vref, uint32_t& nref) {
+  const Br b = (w0 & kMwPresent) ? c.P : c.A;
+  vref = nref = kOrig;
+  if (b.kind == kBrKeep) {
+    w = w0;
+    v = v0;
+  } else if (b.kind == kBrAbsent) {
+    w = w0 & ~(kMwPresent | kMwVtagMask);
+    v = 0;
+  } else {
+    const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(rmeta[b.v]));
+    w = (w0 & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    v = tag ? rab[b.v].x : 0;
+    vref = b.v;
+    nref = b.n;
+  }
+}
+
 // in-order inclusive scan of one Comp per lane across a wave
 __device__ inline Comp wave_scan(Comp c, uint32_t l) {
 #pragma unroll

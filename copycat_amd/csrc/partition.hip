@@ -446,9 +446,7 @@ __global__ __launch_bounds__(kPT, CC_PART_WPE) void k_part_tile(const uint32_t* 
       }
     }
   }
-#ifdef CC_PHASE_TIMING
-  if (!EXT) PH_FLUSH(g_ph_part);
-#endif
+  PH_FLUSH(g_ph_part);
 }
 
 // Persistent over tiles (tile T = blockIdx.x + k * gridDim.x): the tile's staged results (contiguous, tile-local)
@@ -540,9 +538,13 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
 int phase_read_value(uint64_t* out);
 int phase_read_partv(uint64_t* out);
 int phase_read_coord(uint64_t* out);
+int phase_read_map(uint64_t* out);
+int phase_read_partx(uint64_t* out);
 int phase_read(int kernel, uint64_t* out) {
 #ifdef CC_PHASE_TIMING
   if (kernel == K_APPLY_VALUE) return phase_read_value(out);
+  if (kernel == K_APPLY_MAP) return phase_read_map(out);
+  if (kernel == K_PART_TILE && !getenv("CC_PART_EXT_V1") && getenv("CC_PART_EXT_PHASES")) return phase_read_partx(out);
   if (kernel == K_APPLY_COORD) return phase_read_coord(out);
   if (kernel == K_PART_TILE && getenv("CC_PART_VALUE")) return phase_read_partv(out);  // the value partition
   unsigned long long z[kPhases] = {};
@@ -565,6 +567,7 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   a.mark(K_PART_TILE, 1, st);
   static const bool part_value = getenv("CC_PART_VALUE") != nullptr;  // experiment: persistent value partition
   static const bool part_tile_v1 = getenv("CC_PART_V1") != nullptr;   // A/B: the previous value partition
+  static const bool part_ext_v1 = getenv("CC_PART_EXT_V1") != nullptr;  // A/B: k_part_tile<2, true>
   if (!ext && part_value) {  // tile histograms, then the persistent value partition (partition_value.hip)
     if (a.res16) {
       if (launch_tile_hist16(a, tiles, st)) return -1;
@@ -578,6 +581,8 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, kChunk), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
                        a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+  } else if (!part_ext_v1) {  // extended staging: partition_ext.hip k_part_ext
+    if (launch_part_ext(a, tiles, st)) return -1;
   } else {
     hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,

@@ -1,0 +1,396 @@
+// partition_ext.hip — the tile-local partition (partition.hip) for batches with extended staging: maps (keys routed
+// to their table region or to a hot key's bucket), coordination resources (quarter buckets) and value events.
+//
+// Same output as k_part_tile<J, true> (staging records per super-bucket run, ttab rows, cpos), restructured so no
+// wave waits on a chain of dependent gathers:
+//   (0) the tile's 16 commits per thread are resolved in one batch — instance column, instance -> resource,
+//       resource -> type, then the map commits' key / flags — and each commit's route (super-bucket) is kept in a
+//       register with its resource slot and type for the whole tile: the histogram comes from those registers and
+//       the chunks never recompute a route (no second map_hash or hot-key probe);
+//   (1..) chunks of 2048 commits (fully unrolled: the route registers are indexed at compile time); a chunk's raw
+//       columns are requested at the top of the previous chunk, and with the type already known every column
+//       the record needs (key, index, ttl / timeout, clock) is in that one batch of loads.
+// Ranking, the per-wave prefix, run starts, placement and the run-by-run write-out are those of k_part_tile.
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+#ifndef CC_PART_EXT_UNROLL
+#define CC_PART_EXT_UNROLL 0  // 1: the chunk loop fully unrolled (bigger code, fewer spills)
+#endif
+namespace {
+constexpr int kXJ = kChunkMaps / kPT;  // commits per thread per chunk (2)
+constexpr int kXCh = kTile / kChunkMaps;  // chunks per tile (8)
+constexpr int kXQ = kXJ * kXCh;        // commits per thread per tile (16)
+constexpr uint32_t kRpDead = 0xFFFFFFFFu;
+}  // namespace
+
+#ifdef CC_PHASE_TIMING
+__device__ unsigned long long g_ph_partx[kPhases];
+int phase_read_partx(uint64_t* out) {
+  unsigned long long z[kPhases] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ph_partx), sizeof z) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_ph_partx), z, sizeof z) != hipSuccess)
+    return CC_ERR_HIP;
+  return CC_OK;
+}
+#endif
+
+__global__ __launch_bounds__(kPT, 4) void k_part_ext(
+    const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op, const uint8_t* __restrict__ flags,
+    const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
+    const uint64_t* __restrict__ cidx, const uint64_t* __restrict__ caux, const uint64_t* __restrict__ ctime,
+    const uint64_t* __restrict__ clock_base, uint32_t ext_flags, uint64_t lo, uint64_t hi,
+    const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
+    uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits, uint32_t sbq_base,
+    const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
+    u64x2* __restrict__ st_ab, uint32_t* __restrict__ st_res, uint64_t* __restrict__ st_key,
+    uint64_t* __restrict__ st_idx, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab) {
+  constexpr int J = kXJ, C = kChunkMaps;
+  extern __shared__ __align__(16) uint8_t smem[];  // layout: partition.hip tile_lds_bytes(sb, true, kChunkMaps)
+  u64x2* rab = reinterpret_cast<u64x2*>(smem);
+  uint64_t* rkey = reinterpret_cast<uint64_t*>(rab + C);
+  uint64_t* ridx = rkey + C;
+  uint32_t* rres = reinterpret_cast<uint32_t*>(ridx + C);
+  uint32_t* rmeta = rres + C;
+  uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + C);
+  uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + C);  // [kPW][hw] packed u16 pairs
+  const uint32_t hw = (sb + 1) / 2;
+  uint16_t* toff = reinterpret_cast<uint16_t*>(wc + kPW * hw);
+  uint16_t* trun = toff + 2 * hw;
+  uint16_t* ctot = trun + 2 * hw;
+  uint16_t* kstart = ctot + 2 * hw;
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(kstart + 2 * hw);
+  uint32_t* ctot32 = reinterpret_cast<uint32_t*>(ctot);
+  uint32_t* hslot = wsum + 16;
+  uint64_t* hh64 = reinterpret_cast<uint64_t*>(hslot + kHotSlots);
+  uint64_t* hkey = hh64 + kHotMax;
+  uint32_t* hident = reinterpret_cast<uint32_t*>(hkey + kHotMax);
+
+  PH_DECL
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint64_t cbase0 = clock_base ? *clock_base : 0;
+  const bool deferred = (ext_flags & kExtDeferred) != 0;
+  uint32_t nhot = 0;
+  if (map_bits) {
+    nhot = *hot_n;
+    for (uint32_t q = t; q < kHotSlots; q += kPT) hslot[q] = 0xFFFFFFFFu;
+    if (t < nhot) {
+      const HotKey hk = hot[t];
+      hh64[t] = hk.h64;
+      hkey[t] = hk.key;
+      hident[t] = hk.ident;
+    }
+  }
+  for (uint32_t k = t; k < hw; k += kPT) ctot32[k] = 0;
+  lds_barrier();
+  if (t < nhot) {
+    uint32_t q = (uint32_t)(hh64[t] >> 32) & (kHotSlots - 1);
+    while (atomicCAS(&hslot[q], 0xFFFFFFFFu, t) != 0xFFFFFFFFu) q = (q + 1) & (kHotSlots - 1);
+  }
+  lds_barrier();
+  const uint32_t sb_hot = sb_val + (map_bits ? (1u << map_bits) : 0u);
+  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
+  const uint64_t tile1 = tile0 + kTile < hi ? tile0 + kTile : hi;
+  const uint32_t tbase = blockIdx.x * kTile;
+  auto row_of = [&](int q) -> uint64_t {  // commit q of this thread: chunk q / J, slot (w, q % J, l)
+    return tile0 + (uint64_t)(q / J) * C + (uint64_t)w * (kWave * J) + (uint64_t)(q % J) * kWave + l;
+  };
+
+  // ---- 0. route every commit of the tile (one batch of loads per stage), histogram from registers ----
+  uint32_t rp[kXQ];     // resource slot | super-bucket << 17; kRpDead: unknown session / past the batch
+  uint32_t tp[kXQ / 4]; // resource type, 4 per word
+#pragma unroll
+  for (int q = 0; q < kXQ / 4; ++q) tp[q] = 0;
+#pragma unroll
+  for (int hq = 0; hq < kXQ; hq += kXQ / 2) {  // two halves of 8 (register pressure)
+    constexpr int H = kXQ / 2;
+    uint32_t rr[H];
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      const uint64_t i = row_of(hq + u);
+      rr[u] = i < tile1 ? inst[i] : kNoRes;
+    }
+#pragma unroll
+    for (int u = 0; u < H; ++u) rr[u] = rr[u] < max_inst ? inst_res[rr[u]] : kNoRes;
+    uint32_t ty[H];
+#pragma unroll
+    for (int u = 0; u < H; ++u) ty[u] = rr[u] != kNoRes ? res_type[rr[u]] : 0u;
+    uint32_t fl[H];
+    uint64_t ky[H];
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      fl[u] = 0;
+      ky[u] = 0;
+      if (is_keyed(ty[u])) {
+        const uint64_t i = row_of(hq + u);
+        fl[u] = flags[i];
+        ky[u] = ckey[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      const int q = hq + u;
+      rp[q] = kRpDead;
+      if (rr[u] == kNoRes) continue;
+      const uint32_t r = rr[u];
+      uint32_t k;
+      if (is_keyed(ty[u])) {
+        const uint32_t kt = CC_FLAG_KTAG(fl[u]);
+        const uint64_t h = map_hash(r, kt, ky[u]);
+        k = sb_val + (uint32_t)(h >> (64 - map_bits));
+        if (nhot) {
+          const uint32_t id = mw_ident(r, kt);
+          for (uint32_t s = (uint32_t)(h >> 32) & (kHotSlots - 1);; s = (s + 1) & (kHotSlots - 1)) {
+            const uint32_t x = hslot[s];
+            if (x == 0xFFFFFFFFu) break;
+            if (hh64[x] == h && hident[x] == id && hkey[x] == ky[u]) {
+              k = sb_hot + x;
+              break;
+            }
+          }
+        }
+      } else if (sbq_base && sb_kind[r >> kSbShift]) {
+        k = sbq_base + (r >> 6);  // quarter bucket (k_apply_coord)
+      } else {
+        k = r >> kSbShift;
+      }
+      rp[q] = r | (k << 17);
+      tp[q / 4] |= ty[u] << (8 * (q % 4));
+      atomicAdd(&ctot32[k >> 1], 1u << (16 * (k & 1)));
+    }
+  }
+  lds_barrier();
+  {
+    uint16_t* row = ttab + (uint64_t)blockIdx.x * (sb + 1);
+    uint32_t run = 0;
+    for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform
+      const uint32_t k = k0 + t;
+      uint32_t inc = k < sb ? ctot[k] : 0, v = inc;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      lds_barrier();
+      if (l == 63) wsum[w] = inc;
+      lds_barrier();
+      uint32_t pre = 0, all = 0;
+      for (uint32_t q = 0; q < (uint32_t)kPW; ++q) {
+        const uint32_t x = wsum[q];
+        pre += q < w ? x : 0;
+        all += x;
+      }
+      if (k < sb) {
+        toff[k] = run + pre + inc - v;
+        trun[k] = 0;
+        row[k] = (uint16_t)(run + pre + inc - v);
+      }
+      run += all;
+    }
+    if (t == 0) row[sb] = (uint16_t)run;  // live commits of the tile (<= 16384)
+  }
+  PH(0);
+
+  // ---- chunks: raw columns of chunk ch + 1 requested at the top of chunk ch ----
+  uint32_t in[J], mt[J], nin[J], nmt[J];
+  u64x2 ab[J], nab[J];
+  uint64_t kk[J], ii[J], xa[J], nkk[J], nii[J], nxa[J];
+  // a lock record's raw columns ride in the slots it does not use: ab = (clock, clock of the commit before), kk
+  // unused, xa = timeout
+  // the route registers rotate by J per chunk: rp[0..J) = this chunk, rp[J..2J) = the next (compile-time indices
+  // in a rolled loop)
+  auto load_raw = [&](uint32_t ch, int qb, uint32_t (&in_)[J], uint32_t (&mt_)[J], u64x2 (&ab_)[J], uint64_t (&kk_)[J],
+                      uint64_t (&ii_)[J], uint64_t (&xa_)[J]) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int q = qb + j;
+      const uint64_t i = tile0 + (uint64_t)ch * C + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      in_[j] = kNoRes;
+      mt_[j] = 0;
+      ab_[j] = u64x2{0, 0};
+      kk_[j] = ii_[j] = xa_[j] = 0;
+      if (rp[q] == kRpDead) continue;
+      const uint32_t ty = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      in_[j] = inst[i];
+      mt_[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
+      if (ty == CC_RES_LOCK) {  // clock of this commit and of the one before it (deterministic log time)
+        ab_[j].x = ctime ? ctime[i] : 0;
+        ab_[j].y = ctime && i > 0 ? ctime[i - 1] : 0;
+        xa_[j] = caux ? caux[i] : 0;
+        ii_[j] = cidx ? cidx[i] : 0;
+        continue;
+      }
+      ab_[j].x = ca[i];
+      ab_[j].y = cb[i];
+      const bool val_walk = ty == CC_RES_VALUE && !sb_kind[(rp[q] & 0x1FFFFu) >> kSbShift];
+      if (val_walk) continue;  // k_apply_value records: the encoded operands only
+      ii_[j] = cidx ? cidx[i] : 0;
+      {
+        kk_[j] = ckey ? ckey[i] : 0;
+        if (is_keyed(ty)) xa_[j] = caux ? caux[i] : 0;
+      }
+    }
+  };
+  load_raw(0, 0, in, mt, ab, kk, ii, xa);
+#if CC_PART_EXT_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+  for (uint32_t ch = 0; ch < (uint32_t)kXCh; ++ch) {
+    const uint64_t cbase = tile0 + (uint64_t)ch * C;
+    if (cbase >= tile1) break;  // block-uniform
+    const bool more = ch + 1 < (uint32_t)kXCh && cbase + C < tile1;
+    if (more) load_raw(ch + 1, J, nin, nmt, nab, nkk, nii, nxa);
+    for (uint32_t k = t; k < kPW * hw; k += kPT) wc[k] = 0;
+    lds_barrier();
+    PH(6);
+    // the records of this chunk (compute only: every column arrived with the chunk's loads)
+    uint32_t sk[J], loc[J], res[J], meta[J], xs[J];
+    bool live[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int q = j;
+      live[j] = rp[q] != kRpDead;
+      res[j] = rp[q] & 0x1FFFFu;
+      sk[j] = live[j] ? rp[q] >> 17 : 0u;
+      meta[j] = mt[j];
+      xs[j] = in[j];
+      if (!live[j]) continue;
+      const uint32_t ty = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      if (is_keyed(ty)) {
+        if (ty == CC_RES_SET || ty == CC_RES_MULTIMAP) {  // an element / multimap key holds Boolean TRUE
+          uint32_t fl = (meta[j] >> 8) & 0xFF;
+          const uint32_t mop = ty == CC_RES_SET ? set_as_map_op(meta[j] & 0xFF) : mmap_as_map_op(meta[j] & 0xFF, fl & 7u);
+          if (mop == CC_OP_MAP_PUTIFABSENT) {
+            fl = (fl & ~7u) | CC_TAG_BOOL;
+            ab[j].x = 1;
+          }
+          meta[j] = (meta[j] & ~0xFFFFu) | mop | (fl << 8);
+        }
+        xs[j] = res[j];
+        if ((int64_t)xa[j] > 0 && ty != CC_RES_MULTIMAP) meta[j] |= kMetaTtl;
+      } else if (ty == CC_RES_VALUE && !sb_kind[res[j] >> kSbShift]) {
+        value_encode(meta[j] & 0xFF, (meta[j] >> 8) & 0xFF, ab[j].x, ab[j].y, meta[j], ab[j]);
+      } else if (ty == CC_RES_LOCK) {
+        const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+        const uint64_t clk = ab[j].x > cbase0 ? ab[j].x : cbase0;
+        const uint64_t prev = i > 0 && ctime ? (ab[j].y > cbase0 ? ab[j].y : cbase0) : cbase0;
+        ab[j].x = deferred ? prev : clk;
+        ab[j].y = xa[j];
+        kk[j] = clk;
+      }
+      const uint32_t sh = 16 * (sk[j] & 1);
+      loc[j] = (atomicAdd(&wc[w * hw + (sk[j] >> 1)], 1u << sh) >> sh) & 0xFFFF;
+    }
+    lds_barrier();
+    PH(1);
+    // per super-bucket: exclusive prefix over waves (packed halves) and chunk totals; chunk-sorted starts
+    for (uint32_t kw = t; kw < hw; kw += kPT) {
+      uint32_t r0 = 0, r1 = 0;
+      for (uint32_t q = 0; q < (uint32_t)kPW; ++q) {
+        const uint32_t c = wc[q * hw + kw];
+        wc[q * hw + kw] = r0 | (r1 << 16);
+        r0 += c & 0xFFFF;
+        r1 += c >> 16;
+      }
+      ctot32[kw] = r0 | (r1 << 16);
+    }
+    lds_barrier();
+    PH(2);
+    uint32_t nlive = 0;
+    for (uint32_t k0 = 0; k0 < sb; k0 += kPT) {  // block-uniform
+      const uint32_t k = k0 + t;
+      const uint32_t v = k < sb ? ctot[k] : 0;
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      lds_barrier();
+      if (l == 63) wsum[w] = inc;
+      lds_barrier();
+      uint32_t pre = 0, all = 0;
+      for (uint32_t q = 0; q < (uint32_t)kPW; ++q) {
+        const uint32_t x = wsum[q];
+        pre += q < w ? x : 0;
+        all += x;
+      }
+      if (k < sb) kstart[k] = nlive + pre + inc - v;
+      nlive += all;
+    }
+    lds_barrier();
+    PH(3);
+    // place records in LDS in sorted order; per-commit tile-local position (stored below)
+    uint32_t cp[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      cp[j] = 0xFFFF;
+      const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      if (i >= tile1 || !live[j]) continue;
+      const uint32_t pre = (wc[w * hw + (sk[j] >> 1)] >> (16 * (sk[j] & 1))) & 0xFFFF;
+      const uint32_t within = pre + loc[j];
+      const uint32_t s = kstart[sk[j]] + within;
+      rab[s] = ab[j];
+      rmeta[s] = meta[j] | ((res[j] & ((1u << kSbShift) - 1)) << 16);
+      rsb[s] = (uint16_t)sk[j];
+      rres[s] = xs[j];
+      rkey[s] = kk[j];
+      ridx[s] = ii[j];
+      cp[j] = toff[sk[j]] + trun[sk[j]] + within;
+    }
+    lds_barrier();
+    PH(4);
+    // The next chunk's columns are taken into the working registers HERE, before this chunk's stores: waiting for
+    // a load also waits for every memory op issued before it (one in-order counter), so the wait covers only the
+    // previous chunk's stores, long done, and not the ones below.
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        in[j] = nin[j];
+        mt[j] = nmt[j];
+        ab[j] = nab[j];
+        kk[j] = nkk[j];
+        ii[j] = nii[j];
+        xa[j] = nxa[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      if (i < tile1) cpos[i - lo] = (uint16_t)cp[j];
+    }
+    // write the chunk out run by run (contiguous)
+    for (uint32_t s = t; s < nlive; s += kPT) {
+      const uint32_t k = rsb[s];
+      const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
+      st_meta[g] = rmeta[s];
+      st_ab[g] = rab[s];
+      st_res[g] = rres[s];
+      st_key[g] = rkey[s];
+      st_idx[g] = ridx[s];
+    }
+    lds_barrier();
+    PH(5);
+    for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
+#pragma unroll
+    for (int q = 0; q + J < kXQ; ++q) rp[q] = rp[q + J];  // rotate to the next chunk
+    static_assert(J == 2, "type rotation packs 4 per word");
+#pragma unroll
+    for (int q = 0; q < kXQ / 4; ++q) tp[q] = (tp[q] >> 16) | (q + 1 < kXQ / 4 ? tp[q + 1] << 16 : 0u);
+  }
+  PH_FLUSH(g_ph_partx);
+}
+
+int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
+  hipLaunchKernelGGL(k_part_ext, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst, a.op,
+                     a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res,
+                     a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
+                     a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cc

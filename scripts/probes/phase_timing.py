@@ -21,6 +21,8 @@ PHASES = {
     1: ["setup", "rank+wait", "wave-prefix", "slot-scan", "place", "walk", "result-store", "-"],
     2: ["load", "scatter", "-", "-", "-", "-", "-", "-"],
     5: ["setup", "rank+wait", "slot-scan", "gather", "walk", "event-flush", "-", "-"],
+    3: ["region-load+list", "chunk-load", "binding", "lookup+orphans", "sort", "scan-apply", "cmp-runs+clear",
+        "write-back"],
 }
 
 
@@ -46,6 +48,8 @@ def run(args):
 
     if args.c5:
         return run_c5(args)
+    if args.c3:
+        return run_c3(args)
     n, R = args.commits, 65536
     b = atomic_long_stream(n, resources=R, seed=SEED_C2, index0=1)
     db = DeviceBatch.upload(b, device="cuda:0", columns=("index", "inst", "op", "flags", "a", "b"))
@@ -84,6 +88,50 @@ def run(args):
         for q in range(8):
             if ticks[q]:
                 print(f"   {PHASES[k][q]:18s} {ticks[q] * 10e-3 / wgs[k]:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
+
+
+def run_c3(args):
+    """The map path on bench.py's c3 stream (Zipf 0.99 over 1M (map, key) pairs in 4,096 maps)."""
+    import torch
+
+    from copycat_amd import abi
+    from copycat_amd.engine import DeviceBatch, Engine, lib
+    from copycat_amd.workload import map_zipf_rows
+
+    n, R = args.commits, 4096
+    db = DeviceBatch.upload(map_zipf_rows(0, n, maps=R, pairs=1 << 20, threads=8), device="cuda:0")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    va = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    E = Engine(R, R, n, device=0, sub_batch=args.sub_batch, map_capacity=1 << 20)
+    E.resource_create_range(0, R, abi.CC_RES_MAP)
+    E.instance_open_range(0, R, 0, 1, 1)
+    L = lib()
+    L.cc_debug_phases.restype = C.c_int
+    L.cc_debug_phases.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    ticks = (C.c_uint64 * 8)()
+    E.apply(db, st, va)
+    E.sync()
+    for k in (0, 3):
+        L.cc_debug_phases(E.h, k, ticks)
+    E.profile(True)
+    for _ in range(args.steps):
+        E.apply(db, st, va)
+    E.sync()
+    prof = E.profile_read()
+    sub = args.sub_batch or (16 << 20)
+    launches = args.steps * ((n + sub - 1) // sub)
+    tiles = (n + 16383) // 16384
+    wgs = {0: tiles * args.steps, 3: 1024 * launches}
+    names = {0: "k_part_tile", 3: "k_apply_map"}
+    for k in (0, 3):
+        assert L.cc_debug_phases(E.h, k, ticks) == 0
+        tot = sum(ticks)
+        ms, nl = prof.get(names[k], (0.0, 0))
+        print(f"{names[k]}: {ms / max(nl, 1) * 1e3:.1f} us/launch, workgroups {wgs[k]}, per-WG mean {tot * 10e-3 / wgs[k]:.2f} us")
+        for q in range(8):
+            if ticks[q]:
+                print(f"   {PHASES[k][q]:18s} {ticks[q] * 10e-3 / wgs[k]:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
+    print({k: round(v[0] / args.steps, 3) for k, v in prof.items()})
 
 
 def run_c5(args):
@@ -134,6 +182,7 @@ def run_c5(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
+    ap.add_argument("--c3", action="store_true")
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--commits", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=3)
