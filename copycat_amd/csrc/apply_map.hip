@@ -57,6 +57,74 @@ constexpr uint32_t kEntFull = 0xFFFEu;
 
 __device__ inline uint32_t map_ident_of(uint32_t res, uint32_t flags) { return mw_ident(res, CC_FLAG_KTAG(flags)); }
 
+// The run transformers of map_ops.h (Comp) packed into two words for the chunk scan: per branch (absent / present
+// before the run) kind bits 0-1 | value record bits 2-13 | node record bits 14-25 (kPkOrig: the input's node);
+// records are chunk slots (< 4095).  A scan step then moves 2 words between lanes instead of 6.
+struct PComp {
+  uint32_t A, P;
+};
+constexpr uint32_t kPkOrig = 0xFFFu;
+__device__ inline uint32_t pk_kind(uint32_t b) { return b & 3u; }
+__device__ inline uint32_t pk_v(uint32_t b) { return (b >> 2) & 0xFFFu; }
+__device__ inline uint32_t pk_n(uint32_t b) { return (b >> 14) & 0xFFFu; }
+__device__ inline uint32_t pk_br(uint32_t kind, uint32_t v, uint32_t n) { return kind | (v << 2) | (n << 14); }
+__device__ inline PComp pc_identity() { return PComp{pk_br(kBrAbsent, 0, 0), pk_br(kBrKeep, 0, 0)}; }
+__device__ inline uint32_t pc_apply_present(const PComp& g, uint32_t v, uint32_t n) {  // g on present(v, n)
+  const uint32_t k = pk_kind(g.P);
+  if (k == kBrKeep) return pk_br(kBrPresent, v, n);
+  if (k == kBrPresent) return pk_br(kBrPresent, pk_v(g.P), pk_n(g.P) == kPkOrig ? n : pk_n(g.P));
+  return pk_br(kBrAbsent, 0, 0);
+}
+__device__ inline PComp pc_compose(const PComp& f, const PComp& g) {  // f first, then g
+  PComp r;
+  r.A = pk_kind(f.A) == kBrAbsent ? g.A : pc_apply_present(g, pk_v(f.A), pk_n(f.A));
+  const uint32_t k = pk_kind(f.P);
+  r.P = k == kBrKeep ? g.P : (k == kBrPresent ? pc_apply_present(g, pk_v(f.P), pk_n(f.P)) : g.A);
+  return r;
+}
+__device__ inline PComp pc_element(uint32_t m, uint32_t s) {  // element() of map_ops.h, packed
+  PComp c = pc_identity();
+  if (!map_applied(m)) return c;
+  switch (smeta_op(m)) {
+    case CC_OP_MAP_PUT:
+      c.A = pk_br(kBrPresent, s, s);
+      c.P = pk_br(kBrPresent, s, kPkOrig);
+      break;
+    case CC_OP_MAP_PUTIFABSENT:
+      c.A = pk_br(kBrPresent, s, s);
+      break;
+    case CC_OP_MAP_REMOVE:
+      c.P = pk_br(kBrAbsent, 0, 0);
+      break;
+    case CC_OP_MAP_REPLACE:
+      c.P = pk_br(kBrPresent, s, kPkOrig);
+      break;
+  }
+  return c;
+}
+__device__ inline PComp pc_shfl_up(const PComp& c, int d) {
+  return PComp{(uint32_t)__shfl_up((int)c.A, d, 64), (uint32_t)__shfl_up((int)c.P, d, 64)};
+}
+// materialize_ref of map_ops.h for a packed composite (vref / nref: kOrig when unchanged)
+__device__ inline void pc_materialize(const PComp& c, uint32_t w0, uint64_t v0, const uint32_t* rmeta, const u64x2* rab,
+                                      uint32_t& w, uint64_t& v, uint32_t& vref, uint32_t& nref) {
+  const uint32_t b = (w0 & kMwPresent) ? c.P : c.A;
+  vref = nref = kOrig;
+  if (pk_kind(b) == kBrKeep) {
+    w = w0;
+    v = v0;
+  } else if (pk_kind(b) == kBrAbsent) {
+    w = w0 & ~(kMwPresent | kMwVtagMask);
+    v = 0;
+  } else {
+    const uint32_t rv = pk_v(b), tag = CC_FLAG_TAG_A(smeta_flags(rmeta[rv]));
+    w = (w0 & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    v = tag ? rab[rv].x : 0;
+    vref = rv;
+    nref = pk_n(b) == kPkOrig ? kOrig : pk_n(b);
+  }
+}
+
 // TTL: the map table has live TTL timers (MapState.java:91-93,119-121,189-192,218-220).  Every entry then carries
 // its timer's deadline (tbl_dl, 0 = none) and every run is walked sequentially: before each commit the entry
 // expires if its deadline is <= the clock at which the reference last fired timers (module mode: this commit's
@@ -99,12 +167,19 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
   uint32_t* const rpos = reinterpret_cast<uint32_t*>(rbuf + kMCh * 20);
   uint32_t* const wtab = reinterpret_cast<uint32_t*>(rbuf);  // [NW][kMapRegion / 2]
   __shared__ uint16_t rent[kMCh];      // entry
+  // results by chunk-list position (the commit's place in this region's list, c - c0): written to the staging
+  // result rows at the end of the chunk, run by run (a region's list is contiguous within each partition tile)
+  __shared__ uint16_t rci[kMCh];       // chunk-list position of the sorted record
+  __shared__ uint64_t resv[kMCh];
+  __shared__ uint8_t ress[kMCh];
   __shared__ uint64_t tdl[TTL ? kMapRegion : 1];  // timer deadline of the entry (0: none)
   __shared__ uint64_t rfire[TTL ? kMCh : 1];      // clock of the last timer firing before the commit
   __shared__ uint64_t rdl[TTL ? kMCh : 1];        // deadline the commit arms if it stores (0: none)
   __shared__ uint32_t ecnt[kMapRegion + 1];  // commits per entry in the chunk -> run starts
-  __shared__ uint32_t eflag[kMapRegion];     // the entry's run holds a value-comparing op
-  __shared__ Comp wcomp[MT / kWave];
+  __shared__ uint32_t eflag[kMapRegion / 32];  // bit e: the entry's run holds a value-comparing op
+  __shared__ uint16_t tmap[kMCh];              // the partition tile of each list position of the next chunk
+  __shared__ PComp wcomp[MT / kWave];
+  static_assert(kMCh < (int)kPkOrig, "packed composites address chunk slots in 12 bits");
   __shared__ uint32_t whead[MT / kWave];
   __shared__ uint32_t rstart[kMaxTiles];
   __shared__ uint32_t rpre[kMaxTiles + 1];
@@ -121,7 +196,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
   if (t < 3) flag[t] = 0;
   if (t == 0) used_total = 0;
   for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
-  for (uint32_t q = t; q < kMapRegion; q += MT) eflag[q] = 0;
+  for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = 0;
   {
     uint64_t ek[MEPer], ev[MEPer], edl[MEPer];
     uint32_t ew[MEPer], used = 0;
@@ -222,17 +297,26 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
   uint32_t nm[kMPer], nres[kMPer], ng[kMPer];
   u64x2 nab[kMPer];
   uint64_t nkey[kMPer];
+  // tmap for the chunk at c0: each tile writes its own positions (one search per thread, not one per commit)
+  auto build_map = [&](uint32_t c0) {
+    const uint32_t cend = c0 + kMCh < cnt ? c0 + kMCh : cnt;
+    uint32_t lo = 0, hi = tiles;  // last tile with rpre <= c0
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rpre[mid] <= c0) lo = mid; else hi = mid;
+    }
+    for (uint32_t tt = lo + t; tt < tiles && rpre[tt] < cend; tt += MT) {
+      const uint32_t a = rpre[tt] > c0 ? rpre[tt] : c0, b = rpre[tt + 1] < cend ? rpre[tt + 1] : cend;
+      for (uint32_t c = a; c < b; ++c) tmap[c - c0] = (uint16_t)tt;
+    }
+  };
   auto load_chunk = [&](uint32_t c0) {
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       const uint32_t c = c0 + w * (kWave * kMPer) + j * kWave + l;
       ng[j] = 0xFFFFFFFFu;
       if (c < cnt) {
-        uint32_t lo = 0, hi = tiles;  // last tile with rpre <= c
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (rpre[mid] <= c) lo = mid; else hi = mid;
-        }
+        const uint32_t lo = tmap[c - c0];
         ng[j] = rstart[lo] + (c - rpre[lo]);
         nm[j] = st_meta[ng[j]];
         nab[j] = st_ab[ng[j]];
@@ -241,12 +325,16 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
       }
     }
   };
+  build_map(0);
+  lds_barrier();
   load_chunk(0);
-  for (uint32_t c0 = 0; c0 < cnt; c0 += kMCh) {
-    uint32_t m[kMPer], res[kMPer], g[kMPer], ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
-    u64x2 ab[kMPer];
-    uint64_t key[kMPer];
-    bool keyop[kMPer];
+  uint32_t m[kMPer], res[kMPer], g[kMPer];
+  u64x2 ab[kMPer];
+  uint64_t key[kMPer];
+  // The working registers take a chunk's records at the END of the chunk before it, after all of that chunk's
+  // work and before its result stores: waiting for a load also waits for every memory op issued before it (one
+  // in-order counter), so the wait never covers stores issued just before it.
+  auto take = [&]() {
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       g[j] = ng[j];
@@ -255,7 +343,17 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
       res[j] = nres[j];
       key[j] = nkey[j];
     }
-    if (c0 + kMCh < cnt) load_chunk(c0 + kMCh);  // block-uniform
+  };
+  take();
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kMCh) {
+    uint32_t ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
+    bool keyop[kMPer];
+    const bool more = c0 + kMCh < cnt;  // block-uniform
+    if (more) {  // (every thread has read tmap for this chunk's loads: it issued them before the last barrier)
+      build_map(c0 + kMCh);
+      lds_barrier();
+      load_chunk(c0 + kMCh);
+    }
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       ent[j] = kNoEnt;
@@ -343,8 +441,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
         ent[j] = kNoEnt;
         uint64_t rv;
         const uint32_t s = map_orphan(smeta_op(m[j]), TTL ? (m[j] & ~kMetaTtl) : m[j], smeta_flags(m[j]), ab[j].x, ab[j].y, rv, err);
-        rst_status[g[j]] = (uint8_t)s;
-        rst_value[g[j]] = rv;
+        const uint32_t cx = w * (kWave * kMPer) + j * kWave + l;
+        ress[cx] = (uint8_t)s;
+        resv[cx] = rv;
       }
     }
     PH(3);
@@ -412,6 +511,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
       rmeta[s] = m[j];
       rpos[s] = g[j];
       rent[s] = (uint16_t)ent[j];
+      rci[s] = (uint16_t)(w * (kWave * kMPer) + j * kWave + l);
       if (TTL) {
         const uint64_t cb = clock_base ? *clock_base : 0;
         const uint32_t row = map_row[g[j]];
@@ -422,9 +522,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
         const int64_t ttl = caux && map_reads_ttl(op) && (m[j] & kMetaTtl) ? (int64_t)caux[row] : 0;
         rfire[s] = deferred ? tp : ti;
         rdl[s] = ttl > 0 ? ti + (uint64_t)ttl : 0;
-        eflag[ent[j]] = 1;  // every run is walked in order
+        atomicOr(&eflag[ent[j] >> 5], 1u << (ent[j] & 31));  // every run is walked in order
       } else if (compares_value(m[j])) {
-        eflag[ent[j]] = 1;
+        atomicOr(&eflag[ent[j] >> 5], 1u << (ent[j] & 31));
       }
     }
     lds_barrier();
@@ -434,32 +534,32 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
     //         value-comparing op are walked by one thread instead ----
     {
       const uint32_t total = ecnt[kMapRegion];
-      Comp el[kMPer];
+      PComp el[kMPer];
       bool hd[kMPer];
-      Comp c = comp_identity();
+      PComp c = pc_identity();
       bool ch = false;
 #pragma unroll
       for (int q = 0; q < kMPer; ++q) {
         const uint32_t s = t * kMPer + q;
-        el[q] = comp_identity();
+        el[q] = pc_identity();
         hd[q] = false;
         if (s < total) {
           const uint32_t e = rent[s];
           hd[q] = s == ecnt[e];
-          el[q] = element(rmeta[s], s);
+          el[q] = pc_element(rmeta[s], s);
         }
-        c = hd[q] ? el[q] : compose(c, el[q]);
+        c = hd[q] ? el[q] : pc_compose(c, el[q]);
         ch |= hd[q];
       }
       // segmented inclusive scan of the thread aggregates across the wave, then across waves
-      Comp inc = c;
+      PComp inc = c;
       bool ih = ch;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
-        const Comp o = comp_shfl_up(inc, d);
+        const PComp o = pc_shfl_up(inc, d);
         const bool oh = __shfl_up((int)ih, d, 64) != 0;
         if (l >= (uint32_t)d) {
-          if (!ih) inc = compose(o, inc);
+          if (!ih) inc = pc_compose(o, inc);
           ih |= oh;
         }
       }
@@ -468,45 +568,45 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
         whead[w] = ih;
       }
       lds_barrier();
-      Comp pre = comp_identity();  // exclusive prefix of this thread (within its run)
+      PComp pre = pc_identity();  // exclusive prefix of this thread (within its run)
       for (uint32_t q = 0; q < w; ++q) {
         if (whead[q]) pre = wcomp[q];
-        else pre = compose(pre, wcomp[q]);
+        else pre = pc_compose(pre, wcomp[q]);
       }
       {
-        const Comp o = comp_shfl_up(inc, 1);
+        const PComp o = pc_shfl_up(inc, 1);
         const bool oh = __shfl_up((int)ih, 1, 64) != 0;
-        if (l > 0) pre = oh ? o : compose(pre, o);
+        if (l > 0) pre = oh ? o : pc_compose(pre, o);
       }
       // walk this thread's commits from its prefix
       uint32_t fe[kMPer], fw[kMPer], fcr[kMPer], fir[kMPer];
       uint64_t fv[kMPer];
       bool fin[kMPer];
-      Comp cur = pre;
+      PComp cur = pre;
 #pragma unroll
       for (int q = 0; q < kMPer; ++q) {
         const uint32_t s = t * kMPer + q;
         fin[q] = false;
         if (s >= total) continue;
         const uint32_t e = rent[s];
-        if (hd[q]) cur = comp_identity();
-        if (eflag[e]) continue;
+        if (hd[q]) cur = pc_identity();
+        if ((eflag[e >> 5] >> (e & 31)) & 1u) continue;
         const uint32_t mm = rmeta[s];
         uint32_t sw, svr, snr;
         uint64_t sv;
-        materialize_ref(cur, tword[e], tval[e], rmeta, rab, sw, sv, svr, snr);
+        pc_materialize(cur, tword[e], tval[e], rmeta, rab, sw, sv, svr, snr);
         uint64_t rv;
         bool wrote, created;
         const u64x2 x = rab[s];
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, sw, sv, rv, wrote, created);
-        rst_status[rpos[s]] = (uint8_t)st;
-        rst_value[rpos[s]] = rv;
-        cur = compose(cur, el[q]);
+        ress[rci[s]] = (uint8_t)st;
+        resv[rci[s]] = rv;
+        cur = pc_compose(cur, el[q]);
         if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
           fin[q] = true;
           fe[q] = e;
           uint32_t vr, nr;
-          materialize_ref(cur, tword[e], tval[e], rmeta, rab, fw[q], fv[q], vr, nr);
+          pc_materialize(cur, tword[e], tval[e], rmeta, rab, fw[q], fv[q], vr, nr);
           fcr[q] = vr != kOrig ? rpos[vr] : kNoRef;  // the rewriting commit's staging position
           fir[q] = nr != kOrig ? rpos[nr] : kNoRef;
         }
@@ -525,7 +625,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
     // runs with a value-comparing op: sequentially, by the thread holding the run's first commit
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
-      if (ent[j] == kNoEnt || rk[j] != 0 || !eflag[ent[j]]) continue;
+      if (ent[j] == kNoEnt || rk[j] != 0 || !((eflag[ent[j] >> 5] >> (ent[j] & 31)) & 1u)) continue;
       const uint32_t e = ent[j];
       const uint32_t s0 = ecnt[e], s1 = ecnt[e + 1];
       uint32_t wv = tword[e];
@@ -547,8 +647,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
           if (wrote) dl = rdl[s];
           else if (!(wv & kMwPresent)) dl = 0;
         }
-        rst_status[rpos[s]] = (uint8_t)st;
-        rst_value[rpos[s]] = rv;
+        ress[rci[s]] = (uint8_t)st;
+        resv[rci[s]] = rv;
         if (wrote) { ci = rpos[s]; any_w = true; }
         if (created) { ins = rpos[s]; any_c = true; }
       }
@@ -559,8 +659,19 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
       if (any_c) tir[e] = ins;
     }
     lds_barrier();
+    uint32_t gs[kMPer];
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) gs[j] = g[j];
+    if (more) take();
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j)  // this thread's own commits: consecutive lanes -> consecutive staging rows
+      if (gs[j] != 0xFFFFFFFFu) {
+        const uint32_t cx = w * (kWave * kMPer) + j * kWave + l;
+        rst_status[gs[j]] = ress[cx];
+        rst_value[gs[j]] = resv[cx];
+      }
     for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
-    for (uint32_t q = t; q < kMapRegion; q += MT) eflag[q] = 0;
+    for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = 0;
     lds_barrier();
     PH(6);
   }

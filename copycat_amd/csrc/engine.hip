@@ -76,7 +76,7 @@ static void free_all(cc_engine* e) {
                   e->d_st_key,   e->d_st_idx,   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
-                  e->d_tile_off, e->d_arena,    e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
+                  e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n};
@@ -135,6 +135,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
         (rc = alloc((void**)&e->d_tile_sum, sizeof(uint32_t) * e->max_tiles)) ||
         (rc = alloc((void**)&e->d_tile_off, sizeof(uint64_t) * e->max_tiles)) ||
         (rc = alloc((void**)&e->d_arena, sizeof(EvRec) * e->arena_cap)) ||
+        (rc = alloc((void**)&e->d_ev_perm, sizeof(uint32_t) * e->arena_cap)) ||
         (rc = alloc((void**)&e->d_arena_n, sizeof(unsigned long long))) ||
         (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))) ||
         (rc = ensure_leak(e, kLeakCap)))
@@ -807,6 +808,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ea.arena = e->d_arena;
       ea.arena_n = e->d_arena_n;
       ea.arena_cap = e->arena_cap;
+      ea.perm = e->d_ev_perm;
       if (ev) {
         ea.out_cap = ev->capacity;
         ea.out_pos = ev->pos;

@@ -251,9 +251,7 @@ struct EventArgs {
   const EvRec* arena;
   const unsigned long long* arena_n;
   uint64_t arena_cap;
-  LeakRec* leak;           // leak log: a group member removed by close (its join commit is never clean()ed)
-  unsigned long long* leak_n;
-  uint64_t leak_cap;
+  uint32_t* perm;          // [arena_cap] output position - the sub-batch's first -> arena index
   uint64_t out_cap;
   uint32_t* out_pos;
   uint32_t* out_target;

@@ -175,6 +175,7 @@ struct cc_engine {
   uint32_t* d_tile_sum = nullptr;    // [max_tiles]
   uint64_t* d_tile_off = nullptr;    // [max_tiles]
   EvRec* d_arena = nullptr;
+  uint32_t* d_ev_perm = nullptr;     // [arena_cap] event output order -> arena index (events.hip)
   unsigned long long* d_arena_n = nullptr;
   unsigned long long* d_ev_total = nullptr;
   uint64_t arena_cap = 0;

@@ -7,7 +7,12 @@
 //                  the tile, and row_of[staging position] = row for commits that published;
 //   k_ev_tiles   : one workgroup: exclusive scan of the tile totals on top of the events already written by
 //                  earlier sub-batches; capacity / no-stream checks;
-//   k_ev_scatter : every arena event to out[tile offset + row offset + emission index].
+//   k_ev_perm    : every arena event's output position (tile offset + row offset + emission index) -> perm[];
+//   k_ev_out     : the output rows in order, each gathering its arena record: the six output columns are
+//                  written contiguously (scattered 1-byte stores to them were the cost of the old one-pass
+//                  scatter, k_ev_scatter, kept for A/B under CC_EV_SCATTER).
+#include <cstdlib>
+
 #include "common.h"
 #include "engine_internal.h"
 
@@ -110,6 +115,41 @@ __global__ void k_ev_scatter(const EvRec* __restrict__ arena, const unsigned lon
   }
 }
 
+__global__ void k_ev_perm(const EvRec* __restrict__ arena, const unsigned long long* __restrict__ arena_n,
+                          uint64_t arena_cap, const uint32_t* __restrict__ row_of, const uint32_t* __restrict__ ev_loc,
+                          const uint64_t* __restrict__ tile_off, uint32_t* __restrict__ perm) {
+  const uint64_t ne = *arena_n < arena_cap ? *arena_n : arena_cap;
+  const uint64_t base = tile_off[0];
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = arena[e].g;
+    const uint16_t k = arena[e].k;
+    const uint32_t i = row_of[g];
+    const uint64_t d = tile_off[i / kTile] + ev_loc[i] + k - base;
+    if (d < arena_cap) perm[d] = (uint32_t)e;  // (more events than the arena holds: the call fails, kErrEvents)
+  }
+}
+
+__global__ void k_ev_out(const EvRec* __restrict__ arena, const unsigned long long* __restrict__ arena_n,
+                         uint64_t arena_cap, const uint32_t* __restrict__ perm,
+                         const uint32_t* __restrict__ row_of, const uint64_t* __restrict__ tile_off,
+                         const unsigned long long* __restrict__ ev_total, uint64_t lo, uint64_t out_cap,
+                         uint32_t* __restrict__ pos, uint32_t* __restrict__ target, uint8_t* __restrict__ code,
+                         uint8_t* __restrict__ src, uint8_t* __restrict__ tag, uint64_t* __restrict__ payload) {
+  const uint64_t base = tile_off[0], end = *ev_total < out_cap ? *ev_total : out_cap;
+  const uint64_t ne = *arena_n < arena_cap ? *arena_n : arena_cap;
+  if (*arena_n > arena_cap) return;  // the arena overflowed: perm is incomplete and the call fails (kErrEvents)
+  for (uint64_t d = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; d < end; d += (uint64_t)gridDim.x * blockDim.x) {
+    if (d - base >= ne) break;
+    const EvRec r = arena[perm[d - base]];
+    pos[d] = (uint32_t)(lo + row_of[r.g]);
+    target[d] = r.target;
+    code[d] = r.code;
+    src[d] = r.src;
+    tag[d] = r.tag;
+    payload[d] = r.payload;
+  }
+}
+
 int launch_events(const EventArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_EVENTS, 1, st);
@@ -117,10 +157,17 @@ int launch_events(const EventArgs& a, hipStream_t st) {
                      a.tile_sum);
   hipLaunchKernelGGL(k_ev_tiles, dim3(1), dim3(kER), 0, st, a.tile_sum, a.tiles, a.ev_total, a.tile_off, a.arena_n,
                      a.arena_cap, a.out_cap, a.out_pos ? 1 : 0, a.err);
-  if (a.out_pos)
+  static const bool one_pass = getenv("CC_EV_SCATTER") != nullptr;
+  if (a.out_pos && (one_pass || !a.perm)) {
     hipLaunchKernelGGL(k_ev_scatter, dim3(1024), dim3(256), 0, st, a.arena, a.arena_n, a.arena_cap, a.row_of, a.ev_loc,
                        a.tile_off, a.lo, a.out_cap, a.out_pos, a.out_target, a.out_code, a.out_src, a.out_tag,
                        a.out_payload);
+  } else if (a.out_pos) {
+    hipLaunchKernelGGL(k_ev_perm, dim3(1024), dim3(256), 0, st, a.arena, a.arena_n, a.arena_cap, a.row_of, a.ev_loc,
+                       a.tile_off, a.perm);
+    hipLaunchKernelGGL(k_ev_out, dim3(2048), dim3(256), 0, st, a.arena, a.arena_n, a.arena_cap, a.perm, a.row_of, a.tile_off, a.ev_total, a.lo,
+                       a.out_cap, a.out_pos, a.out_target, a.out_code, a.out_src, a.out_tag, a.out_payload);
+  }
   a.mark(K_EVENTS, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
