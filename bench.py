@@ -242,7 +242,7 @@ def run_c5(args, dev, rank, world, dist):
     kinds = np.array([abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP], np.uint8)
     if args.c5_layout == "grouped":  # slot ranges by type: locks, then elections, then groups
         types = np.repeat(kinds, (R + 2) // 3)[:R]
-    else:  # resources created in turn (a lock, an election, a group, ...): slot r holds type r % 3
+    else:  # resources created in turn (a lock, an election, a group, ...): instance r's resource has type r % 3
         types = np.resize(kinds, R)
     total_steps = args.warmup + args.steps
     nstreams = max(1, min(total_steps, int(args.hbm_budget_gb * 1e9 // (n * 54))))
@@ -280,9 +280,14 @@ def run_c5(args, dev, rank, world, dist):
     value = torch.zeros(n, dtype=torch.int64, device=dev)
     evs = DeviceEvents(2 * n, device=dev)
     E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
-    for r in range(R):
-        E.resource_create(r, int(types[r]))
-    E.instance_open_range(0, R, 0, 1000, 1 + rank)
+    if args.c5_layout == "manager":  # through the product's ResourceManager (cc_create_resource): the allocator
+        for r in range(R):           # places each type in 64-slot groups of its own; instance r = the r-th create
+            st, iid, islot = E.create_resource(r + 1, int(types[r]), 1 + rank, 1000 + r)
+            assert abi.status_code(st) == abi.CC_ST_OK and iid == 1000 + r and islot == r, (st, iid, islot)
+    else:  # raw slots: resource r in slot r
+        for r in range(R):
+            E.resource_create(r, int(types[r]))
+        E.instance_open_range(0, R, 0, 1000, 1 + rank)
     stream = torch.cuda.current_stream(dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
     wm_local = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -772,7 +777,7 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="c2: also time one PCIe-inclusive step (pinned H2D + apply + D2H)")
     ap.add_argument("--hbm-budget-gb", type=float, default=200.0,
                     help="c2: HBM for resident per-step batches (more steps than fit replay the resident ones)")
-    ap.add_argument("--c5-layout", choices=("interleaved", "grouped"), default="interleaved",
+    ap.add_argument("--c5-layout", choices=("manager", "interleaved", "grouped"), default="manager",
                     help="c5: resource types by slot: r %% 3 (created in turn) or in thirds")
     ap.add_argument("--retained", action="store_true", help="c2: also keep the retained value commit per slot (CC_CFG_VALUE_RETAINED)")
     args = ap.parse_args()

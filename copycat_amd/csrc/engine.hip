@@ -444,6 +444,7 @@ int cc::drain_leaks(cc_engine* e) {
 int cc::delete_slot(cc_engine* e, uint32_t slot) {
   int rc = quiesce(e);
   if (rc) return rc;
+  const uint32_t old_type = e->res_type[slot];
   if ((rc = drain_leaks(e))) return rc;
   e->leaks.erase(slot);  // the per-slot view ends with the resource (its dropped commits stay in the log)
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
@@ -478,6 +479,7 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
   e->res_has_key[slot] = 0;
   e->res_sessions.erase(e->res_sessions.lower_bound({slot, 0}), e->res_sessions.lower_bound({slot + 1, 0}));
   e->used_res.clear(slot);
+  if (old_type < 16) e->open_grp[old_type].insert(slot >> 6);  // room again in its group (manager.hip)
   return CC_OK;
 }
 
@@ -1626,6 +1628,18 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
     e->used_res.set(s);
     if (e->res_has_key[s]) e->keys[e->res_key[s]] = e->res_id[s];
     if (!e->res_zombie[s]) e->res_by_id[e->res_id[s]] = s;
+  }
+  for (auto& og : e->open_grp) og.clear();  // groups of one coordination type with room (manager.hip)
+  for (uint32_t g = 0; g * 64 < e->cfg.max_resources; ++g) {
+    uint32_t type = CC_RES_NONE, used = 0;
+    bool mixed = false;
+    for (uint32_t s = g * 64; s < g * 64 + 64 && s < e->cfg.max_resources; ++s) {
+      if (e->res_type[s] == CC_RES_NONE && !e->used_res.test(s)) continue;
+      ++used;
+      if (type == CC_RES_NONE) type = e->res_type[s];
+      else if (type != e->res_type[s]) mixed = true;
+    }
+    if (!mixed && type != CC_RES_NONE && used < 64 && type < 16) e->open_grp[type].insert(g);
   }
   for (uint32_t i = 0; i < e->cfg.max_instances; ++i) {
     if (e->inst_res[i] == kNoRes) continue;

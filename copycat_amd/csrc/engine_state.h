@@ -103,6 +103,7 @@ struct cc_engine {
   std::vector<uint8_t> res_has_key;       // [slots] created through get/create (low-level slots have no key)
   std::vector<uint8_t> res_zombie;        // [slots] removed from `resources` by a deleteResource whose delete() threw
   cc::SlotBits used_res, used_inst;       // slot occupancy (allocation: values/maps low, coordination high; instances low)
+  std::set<uint32_t> open_grp[16];        // per coordination type: 64-slot groups holding only that type, with room
   // device registry + state
   uint32_t* d_inst_res = nullptr;
   uint16_t* d_inst_res16 = nullptr;  // value-only fast path (< 65535 resources, <= 65536 instances)

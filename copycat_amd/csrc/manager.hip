@@ -11,7 +11,9 @@
 // Ids are commit indices: a new key's resource id is the index of the commit that created it (:86-88,157-159), every
 // new instance's id is the index of its commit (:103,128,185).  Slots are the engine's dense handles: value, map and
 // set resources take the lowest free slot, coordination resources (lock, election, group, queue) the highest, so
-// value super-buckets stay on the value-only apply kernel.  Instances take the lowest free instance slot.
+// value super-buckets stay on the value-only apply kernel; and a coordination resource goes into a 64-slot group
+// (one k_apply_coord walking wave) that holds only its type, so the walk runs the type-specialised code
+// (apply_coord.hip TypeC) without divergence between types.  Instances take the lowest free instance slot.
 #include <algorithm>
 #include <cstring>
 
@@ -23,7 +25,33 @@ namespace {
 
 bool coord_type(uint32_t t) { return t == CC_RES_LOCK || t == CC_RES_ELECTION || t == CC_RES_GROUP || t == CC_RES_QUEUE; }
 
+// every used slot of 64-slot group g holds `type`
+bool group_holds_only(const cc_engine* e, uint32_t g, uint32_t type) {
+  for (uint32_t s = g * 64; s < g * 64 + 64 && s < e->cfg.max_resources; ++s)
+    if (e->used_res.test(s) && e->res_type[s] != type) return false;
+  return true;
+}
+
 int alloc_res_slot(cc_engine* e, uint32_t type, uint32_t* slot) {
+  if (coord_type(type)) {
+    auto& open = e->open_grp[type];
+    while (!open.empty()) {  // the highest group of this type with room
+      const uint32_t g = *open.rbegin();
+      const uint64_t word = e->used_res.w[g];
+      const uint64_t valid = (uint64_t)g * 64 + 64 <= e->cfg.max_resources ? ~0ull : (1ull << (e->cfg.max_resources & 63)) - 1;
+      if ((~word & valid) && group_holds_only(e, g, type)) {
+        *slot = g * 64 + 63 - (uint32_t)__builtin_clzll(~word & valid);
+        return CC_OK;
+      }
+      open.erase(g);
+    }
+    for (uint64_t g = e->cfg.max_resources / 64; g-- > 0;)  // else the highest empty group
+      if (e->used_res.w[g] == 0) {
+        open.insert((uint32_t)g);
+        *slot = (uint32_t)(g * 64 + 63);
+        return CC_OK;
+      }
+  }
   const int64_t s = coord_type(type) ? e->used_res.highest() : e->used_res.lowest();
   if (s < 0) return set_err(CC_ERR_CAPACITY, "no free resource slot (max_resources)");
   *slot = (uint32_t)s;

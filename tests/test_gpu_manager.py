@@ -238,3 +238,34 @@ def test_manager_state_survives_snapshot():
         P.control("get", 200 + k, TYPES[k % len(TYPES)], 1 + k % 4)
     P.control("delete", rid=next(iter(P.rtype)))
     P.check_state()
+
+
+def test_manager_groups_coordination_types():
+    """The allocator puts each coordination type in 64-slot groups of its own (one k_apply_coord walking wave runs
+    one type's specialised walk), values / maps from the bottom; deleted slots are reused within their group."""
+    from copycat_amd.engine import Engine
+
+    R = 1024
+    E = Engine(R, R, 1 << 12, map_capacity=1 << 12)
+    kinds = [abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP, abi.CC_RES_QUEUE, abi.CC_RES_VALUE, abi.CC_RES_MAP]
+    slots = {}
+    for r in range(600):
+        t = kinds[r % len(kinds)]
+        st, iid, _ = E.create_resource(r + 1, t, 7, 10 + r)
+        assert abi.status_code(st) == abi.CC_ST_OK
+        slots[iid] = (E.resource_slot(iid), t)
+    groups = {}
+    for s, t in slots.values():
+        if t in (abi.CC_RES_VALUE, abi.CC_RES_MAP):
+            assert s < 256, s  # value / map slots from the bottom
+        else:
+            groups.setdefault(s >> 6, set()).add(t)
+    assert all(len(ts) == 1 for ts in groups.values()), groups
+    # a freed lock slot is taken by the next lock, not by another type
+    lock_iid = next(i for i, (s, t) in slots.items() if t == abi.CC_RES_LOCK)
+    freed = slots[lock_iid][0]
+    assert abi.status_code(E.delete_resource(lock_iid)) == abi.CC_ST_OK
+    st, iid, _ = E.create_resource(5000, abi.CC_RES_ELECTION, 7, 5000)
+    assert E.resource_slot(iid) >> 6 != freed >> 6
+    st, iid, _ = E.create_resource(5001, abi.CC_RES_LOCK, 7, 5001)
+    assert E.resource_slot(iid) >> 6 == freed >> 6
