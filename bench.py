@@ -279,7 +279,9 @@ def run_c5(args, dev, rank, world, dist):
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     value = torch.zeros(n, dtype=torch.int64, device=dev)
     evs = DeviceEvents(2 * n, device=dev)
-    E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
+    # slot capacity with one spare super-bucket: each type's last 64-slot group is partly filled (32,768 / 3 is no
+    # multiple of 64), and without spare groups the allocator would have to mix types in a group (a divergent walk)
+    E = Engine(R + 256, R, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
     if args.c5_layout == "manager":  # through the product's ResourceManager (cc_create_resource): the allocator
         for r in range(R):           # places each type in 64-slot groups of its own; instance r = the r-th create
             st, iid, islot = E.create_resource(r + 1, int(types[r]), 1 + rank, 1000 + r)

@@ -29,6 +29,10 @@
 namespace cc {
 
 #ifdef CC_PHASE_TIMING
+__device__ unsigned long long g_wg_t[2 * 4096];  // last launch: per workgroup (start, end) wall clock
+int phase_read_coord_wg(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * 2 * 4096) == hipSuccess ? CC_OK : CC_ERR_HIP;
+}
 __device__ unsigned long long g_ph_coord[kPhases];
 int phase_read_coord(uint64_t* out) {
   unsigned long long z[kPhases] = {};
@@ -775,6 +779,12 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict
     PH(5);
   }
   PH_FLUSH(g_ph_coord);
+#ifdef CC_PHASE_TIMING
+  if (t == 0 && blockIdx.x < 4096) {
+    g_wg_t[2 * blockIdx.x] = ph_t0_;
+    g_wg_t[2 * blockIdx.x + 1] = wall_clock64();
+  }
+#endif
   if (w == 0) {
     E.store();
     *reinterpret_cast<CoordHdr*>(blk) = h;

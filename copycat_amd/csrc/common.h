@@ -107,7 +107,7 @@ __device__ inline void lds_barrier() {
 // a per-kernel __device__ array at the end and read back with cc_debug_phases.  Compiled out by default.
 constexpr int kPhases = 8;
 #ifdef CC_PHASE_TIMING
-#define PH_DECL uint64_t ph_last_ = wall_clock64(); uint64_t ph_acc_[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH_DECL uint64_t ph_last_ = wall_clock64(); const uint64_t ph_t0_ = ph_last_; uint64_t ph_acc_[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(k) do { if (threadIdx.x == 0) { const uint64_t n_ = wall_clock64(); ph_acc_[k] += n_ - ph_last_; ph_last_ = n_; } } while (0)
 #define PH_FLUSH(buf) do { if (threadIdx.x == 0) for (int q_ = 0; q_ < kPhases; ++q_) atomicAdd(&(buf)[q_], (unsigned long long)ph_acc_[q_]); } while (0)
 #else

@@ -1678,6 +1678,12 @@ extern "C" int cc_profile_reset(cc_engine* e) {
 }
 
 extern "C" int cc_debug_phases(cc_engine* e, int kernel, uint64_t* ticks) {
+#ifdef CC_PHASE_TIMING
+  if (e && ticks && kernel == 64) {  // diagnostics: k_apply_coord's per-workgroup (start, end), 2 x 4096 entries
+    HIPCHECK(hipStreamSynchronize(e->last_stream));
+    return phase_read_coord_wg(ticks);
+  }
+#endif
   if (!e || !ticks || kernel < 0 || kernel >= K_NUM) return CC_ERR_INVALID;
   HIPCHECK(hipSetDevice(e->device));
   HIPCHECK(hipStreamSynchronize(e->last_stream));

@@ -235,6 +235,7 @@ struct CoordArgs {
   Marker mark;
 };
 int launch_apply_coord(const CoordArgs& a, hipStream_t st);
+int phase_read_coord_wg(uint64_t* out);  // CC_PHASE_TIMING builds
 int launch_time_check(const uint64_t* time, uint64_t n, uint64_t* clock, uint32_t* err, hipStream_t st);
 int launch_clock_advance(const uint64_t* time, uint64_t n, uint64_t now, uint64_t* clock, hipStream_t st);
 

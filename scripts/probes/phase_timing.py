@@ -144,7 +144,15 @@ def run_c5(args):
     n, R = args.commits, 32768
     kinds = {"L": abi.CC_RES_LOCK, "E": abi.CC_RES_ELECTION, "G": abi.CC_RES_GROUP}
     tl = [kinds[c] for c in args.types]
-    types = np.resize(np.array(tl, np.uint8), R) if args.interleave else np.repeat(np.array(tl, np.uint8), (R + len(tl) - 1) // len(tl))[:R]
+    if args.manager:
+        args.interleave = True
+    if args.group64:  # the allocator's layout: 64-slot groups of one type, types in turn
+        types = np.repeat(np.resize(np.array(tl, np.uint8), R // 64), 64)
+    elif args.interleave:
+        types = np.resize(np.array(tl, np.uint8), R)
+    else:
+        types = np.repeat(np.array(tl, np.uint8), (R + len(tl) - 1) // len(tl))[:R]
+    types_in = types.copy()
     from copycat_amd.workload import CoordClients
 
     clients = CoordClients(types, K=1, max_inst=R, seed=0xA700000 + 5)
@@ -154,9 +162,16 @@ def run_c5(args):
     va = torch.zeros(n, dtype=torch.int64, device="cuda:0")
     evs = DeviceEvents(2 * n, device="cuda:0")
     E = Engine(R, R, n, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=2 * n)
-    for r in range(R):
-        E.resource_create(r, int(types[r]))
-    E.instance_open_range(0, R, 0, 1000, 1)
+    if args.manager:  # as bench.py c5: cc_create_resource in turn (the allocator's 64-slot groups)
+        for r in range(R):
+            E.create_resource(r + 1, int(types[r]), 1, 1000 + r)
+        types = np.zeros(R, np.uint8)  # the slot -> type table, for the per-WG report
+        for r in range(R):
+            types[E.resource_slot(1000 + r)] = tl[r % len(tl)] if args.interleave else types_in[r]
+    else:
+        for r in range(R):
+            E.resource_create(r, int(types[r]))
+        E.instance_open_range(0, R, 0, 1000, 1)
     L = lib()
     ticks = (C.c_uint64 * 8)()
     E.apply_events(db, st, va, evs)
@@ -178,6 +193,28 @@ def run_c5(args):
         if ticks[q]:
             print(f"   {PHASES[5][q]:18s} {ticks[q] * 10e-3 / wgs:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
     print({k: round(v[0] / args.steps, 3) for k, v in prof.items()})
+    wgt = (C.c_uint64 * 8192)()
+    if L.cc_debug_phases(E.h, 64, wgt) == 0:  # the last launch's workgroups: start skew and duration spread
+        import numpy as np
+
+        a = np.frombuffer(wgt, np.uint64).reshape(-1, 2)[: wgs // max(launches, 1)].astype(np.int64)
+        a = a[a[:, 0] > 0]
+        t0 = a[:, 0].min()
+        st, en = (a[:, 0] - t0) * 10e-3, (a[:, 1] - t0) * 10e-3
+        print(f"last launch, {len(a)} WGs: start skew p50 {np.percentile(st, 50):.1f} p90 {np.percentile(st, 90):.1f} "
+              f"max {st.max():.1f} us; duration p50 {np.percentile(en - st, 50):.1f} p90 {np.percentile(en - st, 90):.1f} "
+              f"max {(en - st).max():.1f} us; last end {en.max():.1f} us")
+        dur = en - st
+        order = np.argsort(-dur)[:12]
+        tn = {int(abi.CC_RES_LOCK): "L", int(abi.CC_RES_ELECTION): "E", int(abi.CC_RES_GROUP): "G"}
+        print("   slowest:", [(int(b), round(float(dur[b]), 1), tn.get(int(types[(b // 4) * 256 + (b % 4) * 64]), "?"))
+                              for b in order])
+        for k, nm in tn.items():
+            sel = np.array([types[(b // 4) * 256 + (b % 4) * 64] == k for b in range(len(a))])
+            if sel.any():
+                print(f"   {nm}: p50 {np.percentile(dur[sel], 50):.1f} max {dur[sel].max():.1f} us over {sel.sum()} WGs")
+        late = st > 50
+        print(f"   WGs starting > 50 us late: {late.sum()} (their blockIdx mod 8: {np.bincount(np.nonzero(late)[0] % 8, minlength=8).tolist()})")
 
 
 if __name__ == "__main__":
@@ -189,6 +226,8 @@ if __name__ == "__main__":
     ap.add_argument("--sub-batch", type=int, default=0)
     ap.add_argument("--c5", action="store_true", help="the coordination kernel on the c5 stream")
     ap.add_argument("--interleave", action="store_true", help="--c5: slot r holds type r %% len(types)")
+    ap.add_argument("--group64", action="store_true", help="--c5: 64-slot groups of one type, types in turn")
+    ap.add_argument("--manager", action="store_true", help="--c5: resources created through cc_create_resource in turn")
     ap.add_argument("--types", default="LEG", help="--c5: resource types in thirds (L lock, E election, G group)")
     a = ap.parse_args()
     build() if a.build else run(a)
