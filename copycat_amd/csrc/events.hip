@@ -21,25 +21,31 @@ namespace cc {
 constexpr int kER = kPT;  // 1024 threads per tile
 constexpr int kERPer = kTile / kER;
 
+// Per tile: thread t owns rows [16 t, 16 t + 16) (two 16-byte loads of cpos); a staged commit that published
+// gets row_of (its row) and ev_loc (the tile-relative offset of its first event), both at its staging position.
 __global__ __launch_bounds__(kER) void k_ev_rows(const uint16_t* __restrict__ cpos, uint64_t n, const uint16_t* __restrict__ ev_cnt,
                                                  uint32_t* __restrict__ row_of, uint32_t* __restrict__ ev_loc,
                                                  uint32_t* __restrict__ tile_sum) {
+  static_assert(kERPer == 16, "two uint4 of cpos per thread");
   __shared__ uint32_t wsum[kER / kWave];
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t r0 = (uint64_t)blockIdx.x * kTile + (uint64_t)t * kERPer;
   const uint32_t tbase = blockIdx.x * kTile;
+  uint32_t pp[kERPer];
+  {
+    // (cpos has a full tile for every tile of the sub-batch: the rows past n read as unknown sessions below)
+    const uint4 v0 = reinterpret_cast<const uint4*>(cpos + r0)[0], v1 = reinterpret_cast<const uint4*>(cpos + r0)[1];
+    const uint32_t ww[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      pp[2 * q] = ww[q] & 0xFFFF;
+      pp[2 * q + 1] = ww[q] >> 16;
+    }
+  }
   uint32_t c[kERPer], sum = 0;
 #pragma unroll
   for (int q = 0; q < kERPer; ++q) {
-    const uint64_t i = r0 + q;
-    c[q] = 0;
-    if (i < n) {
-      const uint16_t p = cpos[i];
-      if (p != 0xFFFF) {
-        c[q] = ev_cnt[tbase + p];
-        if (c[q]) row_of[tbase + p] = (uint32_t)i;
-      }
-    }
+    c[q] = r0 + q < n && pp[q] != 0xFFFF ? ev_cnt[tbase + pp[q]] : 0u;
     sum += c[q];
   }
   uint32_t inc = sum;
@@ -57,8 +63,10 @@ __global__ __launch_bounds__(kER) void k_ev_rows(const uint16_t* __restrict__ cp
   }
 #pragma unroll
   for (int q = 0; q < kERPer; ++q) {
-    const uint64_t i = r0 + q;
-    if (i < n) ev_loc[i] = run;
+    if (c[q]) {
+      row_of[tbase + pp[q]] = (uint32_t)(r0 + q);
+      ev_loc[tbase + pp[q]] = run;
+    }
     run += c[q];
   }
   if (t == 0) tile_sum[blockIdx.x] = total;
@@ -104,7 +112,7 @@ __global__ void k_ev_scatter(const EvRec* __restrict__ arena, const unsigned lon
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
     const EvRec r = arena[e];
     const uint32_t i = row_of[r.g];
-    const uint64_t dst = tile_off[i / kTile] + ev_loc[i] + r.k;
+    const uint64_t dst = tile_off[r.g / kTile] + ev_loc[r.g] + r.k;
     if (dst >= out_cap) continue;
     pos[dst] = (uint32_t)(lo + i);
     target[dst] = r.target;
@@ -123,8 +131,7 @@ __global__ void k_ev_perm(const EvRec* __restrict__ arena, const unsigned long l
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t g = arena[e].g;
     const uint16_t k = arena[e].k;
-    const uint32_t i = row_of[g];
-    const uint64_t d = tile_off[i / kTile] + ev_loc[i] + k - base;
+    const uint64_t d = tile_off[g / kTile] + ev_loc[g] + k - base;
     if (d < arena_cap) perm[d] = (uint32_t)e;  // (more events than the arena holds: the call fails, kErrEvents)
   }
 }
