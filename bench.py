@@ -65,7 +65,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 # the kernels behind each cc_profile marker (the value-only partition is k_part_v2; engines with maps, coordination
 # or value events use k_part_tile)
-MARKER_KERNELS = {"k_part_tile": ("k_part_v2", "k_part_tile"), "k_events": ("k_ev_rows", "k_ev_scatter")}
+# the kernels each profiling marker spans (their HBM traffic adds up); the first present partition kernel is the one
+MARKER_KERNELS = {"k_part_tile": ("k_part_ext", "k_part_v2", "k_part_tile"), "k_events": ("k_ev_rows", "k_ev_perm", "k_ev_out"),
+                  "k_map_hot": ("k_hot_detect", "k_hot_agg", "k_hot_lists", "k_hot_apply")}
+MARKER_SUM = {"k_events", "k_map_hot"}
 
 
 def pmc_traffic(kernel, workload):
@@ -75,13 +78,20 @@ def pmc_traffic(kernel, workload):
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload", "c2") != workload:
+        if "workloads" in d:
+            if workload not in d["workloads"]:
+                return None
+            ks = d["workloads"][workload]["kernels"]
+        else:
+            if d.get("workload", "c2") != workload:
+                return None
+            ks = d["kernels"]
+        names = [n for n in MARKER_KERNELS.get(kernel, (kernel,)) if n in ks]
+        if not names:
             return None
-        ks = d["kernels"]
-        for name in MARKER_KERNELS.get(kernel, (kernel,)):
-            if name in ks:
-                return ks[name]["bytes_per_launch"] / 1e9
-        return None
+        if kernel in MARKER_SUM:
+            return round(sum(ks[n]["bytes_per_launch"] for n in names) / 1e9, 4)
+        return round(ks[names[0]]["bytes_per_launch"] / 1e9, 4)
     except (OSError, KeyError, ValueError):
         return None
 

@@ -5,8 +5,10 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half
 streaming reads, so reads are doubled; WRITE_SIZE is taken as is.  Both counters are in KiB and count L2 misses
 (Infinity-Cache hits included), i.e. an upper bound on HBM bytes.
 
-Usage: pmc_traffic.py <gpurun_out/TAG> <out.json> [workload=c2]   (expects TAG/fetch and TAG/write from scripts/gpu_round.sh)
-bench.py reads profiles/traffic_latest.json (a copy of the newest out.json) to fill roofline.traffic.
+Usage: pmc_traffic.py <gpurun_out/TAG> <out.json> [workload=c2]   (expects TAG/fetch and TAG/write: scripts/gpu_round.sh,
+scripts/gpu_profile_wl.sh).  out.json keeps one entry per workload ("workloads": {"c2": ..., "c3": ..., "c5": ...}):
+the workload's entry is replaced, the others kept.  bench.py reads profiles/traffic_latest.json to fill
+roofline.traffic.
 """
 import collections
 import csv
@@ -33,8 +35,18 @@ def main(d, out, workload="c2"):
         fk, wk = f.get(k, 0.0), w.get(k, 0.0)
         res[k] = {"fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
                   "bytes_per_launch": round((2 * fk + wk) * 1024)}
-    json.dump({"source": d, "workload": workload, "correction": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> B), per launch", "kernels": res},
-              open(out, "w"), indent=1)
+    doc = {"correction": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> B), per launch", "workloads": {}}
+    try:
+        with open(out) as fh:
+            old = json.load(fh)
+        if "workloads" in old:
+            doc["workloads"] = old["workloads"]
+        elif "kernels" in old:  # the single-workload layout of round 1
+            doc["workloads"][old.get("workload", "c2")] = {"source": old.get("source"), "kernels": old["kernels"]}
+    except (OSError, ValueError):
+        pass
+    doc["workloads"][workload] = {"source": d, "kernels": res}
+    json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
