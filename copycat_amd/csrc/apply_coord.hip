@@ -533,9 +533,7 @@ constexpr int kCPer2 = 2;                  // commits per thread per chunk
 constexpr int kCCh2 = kCT2 * kCPer2;       // 512 commits of the super-bucket per chunk
 constexpr int kEvLane = 16;                // LDS event slots per walking lane per chunk
 
-__global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
-                                                     const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
-                                                     const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
+__global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
                                                      uint32_t tiles, uint32_t sb, uint32_t sbq_base,
                                                      const uint8_t* __restrict__ sb_kind,
                                                      const uint8_t* __restrict__ res_type, const uint64_t* __restrict__ inst_id,
@@ -642,8 +640,8 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict
     const uint32_t c_0 = c0 + w * (kWave * kCPer2) + l, c_1 = c_0 + kWave;
     g0 = c_0 < cnt ? pos_of(c_0) : 0xFFFFFFFFu;
     g1 = c_1 < cnt ? pos_of(c_1) : 0xFFFFFFFFu;
-    m0 = st_meta[g0 != 0xFFFFFFFFu ? g0 : 0];
-    m1 = st_meta[g1 != 0xFFFFFFFFu ? g1 : 0];
+    m0 = xr[g0 != 0xFFFFFFFFu ? g0 : 0].meta;
+    m1 = xr[g1 != 0xFFFFFFFFu ? g1 : 0].meta;
   };
   load_meta(0);
   PH(0);
@@ -688,10 +686,10 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const uint32_t* __restrict
       for (int j = 0; j < kCPer2; ++j) {
         p[j] = own[j] ? sstart[sl[j]] + wc[w][sl[j]] + rk[j] : 0u;
         const uint32_t gx = own[j] ? gg[j] : 0u;
-        ab[j] = st_ab[gx];
-        ky[j] = st_key[gx];
-        ix[j] = st_idx[gx];
-        in[j] = st_res[gx];
+        ab[j] = xr[gx].ab;
+        ky[j] = xr[gx].key;
+        ix[j] = xr[gx].idx;
+        in[j] = xr[gx].res;
       }
       uint64_t id[kCPer2];
 #pragma unroll
@@ -814,7 +812,7 @@ __global__ void k_clock_advance(const uint64_t* __restrict__ time, uint64_t n, u
 int launch_apply_coord(const CoordArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_APPLY_COORD, 1, st);
-  hipLaunchKernelGGL(k_apply_coord, dim3(a.sb_val * kQPerSb), dim3(kCT2), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx,
+  hipLaunchKernelGGL(k_apply_coord, dim3(a.sb_val * kQPerSb), dim3(kCT2), 0, st, a.xrec,
                      a.ttab, a.tiles, a.sb, a.sbq_base, a.sb_kind, a.res_type, a.inst_id, a.coord, a.val_meta, a.val_v, a.rst_status,
                      a.rst_value, a.ev_cnt, a.arena, a.arena_n, a.arena_cap, a.leak, a.leak_n, a.leak_cap, a.err);
   a.mark(K_APPLY_COORD, 0, st);

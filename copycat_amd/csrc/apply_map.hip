@@ -131,9 +131,7 @@ __device__ inline void pc_materialize(const PComp& c, uint32_t w0, uint64_t v0, 
 // clock; manager mode: the previous commit's, A8), and a commit that stores a value re-arms or cancels the timer.
 // The per-record clocks come from the input columns through map_row (staging position -> batch row).
 template <bool TTL>
-__global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
-                                                  const uint32_t* __restrict__ st_res, const uint64_t* __restrict__ st_key,
-                                                  const uint64_t* __restrict__ st_idx, const uint16_t* __restrict__ ttab,
+__global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
                                                   uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
@@ -318,10 +316,12 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
       if (c < cnt) {
         const uint32_t lo = tmap[c - c0];
         ng[j] = rstart[lo] + (c - rpre[lo]);
-        nm[j] = st_meta[ng[j]];
-        nab[j] = st_ab[ng[j]];
-        nres[j] = st_res[ng[j]];
-        nkey[j] = st_key[ng[j]];
+        const u64x2* rec = reinterpret_cast<const u64x2*>(xr + ng[j]);  // (the log index is read at write-back)
+        nab[j] = rec[0];
+        nkey[j] = rec[1].x;
+        const u64x2 mr = rec[2];
+        nm[j] = (uint32_t)mr.x;
+        nres[j] = (uint32_t)(mr.x >> 32);
       }
     }
   };
@@ -683,8 +683,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const uint32_t* __restr
     tbl_key[tb + e] = tkey[e];
     tbl_word[tb + e] = tword[e];
     tbl_val[tb + e] = tval[e];
-    if (tcr[e] != kNoRef) tbl_ci[tb + e] = st_idx[tcr[e]];
-    if (tir[e] != kNoRef) tbl_ins[tb + e] = st_idx[tir[e]];
+    if (tcr[e] != kNoRef) tbl_ci[tb + e] = xr[tcr[e]].idx;
+    if (tir[e] != kNoRef) tbl_ins[tb + e] = xr[tir[e]].idx;
     if (TTL) tbl_dl[tb + e] = tdl[e];
   }
   PH(7);
@@ -704,13 +704,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.map_bits == 0 || a.tiles == 0) return 0;
   a.mark(K_APPLY_MAP, 1, st);
   if (a.ttl)
-    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
-                       a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.err);
   else
-    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.st_meta, a.st_ab, a.st_res, a.st_key,
-                       a.st_idx, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.err);
   a.mark(K_APPLY_MAP, 0, st);

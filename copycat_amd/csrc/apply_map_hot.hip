@@ -277,7 +277,7 @@ struct ListCursor {
   }
 };
 
-__global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ st_meta, const uint32_t* __restrict__ hot_n,
+__global__ __launch_bounds__(kHT) void k_hot_agg(const XRec* __restrict__ xr, const uint32_t* __restrict__ hot_n,
                                                 const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
                                                 const uint32_t* __restrict__ hot_rstart, uint32_t tiles,
                                                 Comp* __restrict__ agg, uint32_t* __restrict__ hot_cond) {
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ st
       const uint32_t e = p0 + kHPer < L ? p0 + kHPer : L;
       for (uint32_t q = p0; q < e; ++q) {
         const uint32_t g = cur.next();
-        const uint32_t m = st_meta[g];
+        const uint32_t m = xr[g].meta;
         cond |= compares_value(m);
         c = compose(c, element(m, g));
       }
@@ -318,8 +318,7 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ st
 }
 
 // materialize a branch outcome applied to the snapshot: map_apply state (word, value) + commit/insert index
-__device__ inline void materialize(const Comp& c, const HotS0& s0, const uint32_t* __restrict__ st_meta,
-                                   const u64x2* __restrict__ st_ab, const uint64_t* __restrict__ st_idx, uint32_t& w,
+__device__ inline void materialize(const Comp& c, const HotS0& s0, const XRec* __restrict__ xr, uint32_t& w,
                                    uint64_t& v, uint64_t& ci, uint64_t& ins) {
   const bool present0 = (s0.w & kMwPresent) != 0;
   const Br b = present0 ? c.P : c.A;
@@ -335,11 +334,11 @@ __device__ inline void materialize(const Comp& c, const HotS0& s0, const uint32_
     ci = s0.ci;
     ins = s0.ins;
   } else {
-    const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(st_meta[b.v]));
+    const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(xr[b.v].meta));
     w = base | kMwPresent | (tag << 21);
-    v = tag ? st_ab[b.v].x : 0;
-    ci = st_idx[b.v];
-    ins = b.n == kOrig ? s0.ins : st_idx[b.n];
+    v = tag ? xr[b.v].ab.x : 0;
+    ci = xr[b.v].idx;
+    ins = b.n == kOrig ? s0.ins : xr[b.n].idx;
   }
 }
 
@@ -362,8 +361,7 @@ __device__ inline void hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t
   rst_value[g] = rv;
 }
 
-__global__ __launch_bounds__(kHT) void k_hot_apply(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
-                                                  const uint64_t* __restrict__ st_idx, const uint32_t* __restrict__ hot_n,
+__global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, const uint32_t* __restrict__ hot_n,
                                                   const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_len,
                                                   const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_rstart,
                                                   uint32_t tiles, const Comp* __restrict__ agg,
@@ -393,7 +391,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const uint32_t* __restrict__ 
         cur.seek(0);
         for (uint32_t q = 0; q < L; ++q) {
           const uint32_t g = cur.next();
-          hot_step(g, st_meta[g], st_ab[g], st_idx[g], sw, sv, ci, ins, rst_status, rst_value, err);
+          hot_step(g, xr[g].meta, xr[g].ab, xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, err);
         }
         tbl_word[pos] = sw;
         tbl_val[pos] = sv;
@@ -422,7 +420,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const uint32_t* __restrict__ 
       ms[q] = 0;
       if (p0 + q < e) {
         gs[q] = cur.next();
-        ms[q] = st_meta[gs[q]];
+        ms[q] = xr[gs[q]].meta;
         c = compose(c, element(ms[q], gs[q]));
       }
     }
@@ -447,10 +445,10 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const uint32_t* __restrict__ 
     if (p0 < L) {
       uint32_t sw;
       uint64_t sv, ci, ins;
-      materialize(pre, s0, st_meta, st_ab, st_idx, sw, sv, ci, ins);
+      materialize(pre, s0, xr, sw, sv, ci, ins);
 #pragma unroll
       for (int q = 0; q < kHPer; ++q)
-        if (p0 + q < e) hot_step(gs[q], ms[q], st_ab[gs[q]], st_idx[gs[q]], sw, sv, ci, ins, rst_status, rst_value, err);
+        if (p0 + q < e) hot_step(gs[q], ms[q], xr[gs[q]].ab, xr[gs[q]].idx, sw, sv, ci, ins, rst_status, rst_value, err);
       if (p == P - 1 && e == L) {  // the key's last commit: write the entry back
         tbl_word[pos] = sw;
         tbl_val[pos] = sv;
@@ -477,9 +475,9 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_lists, dim3(kHotMax), dim3(kHT), 0, st, a.ttab, a.tiles, a.sb, sb_hot, a.hot, a.hot_n, a.tbl_val,
                      a.tbl_word, a.tbl_ci, a.tbl_ins, a.hot_rpre, a.hot_rstart, a.hot_len, a.hot_cond,
                      reinterpret_cast<HotS0*>(a.hot_s0));
-  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.st_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
+  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.xrec, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
                      a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond);
-  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.st_meta, a.st_ab, a.st_idx, a.hot_n, a.hot, a.hot_len,
+  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.xrec, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
                      a.rst_value, a.err);

@@ -233,6 +233,19 @@ struct LeakRec {
 };
 constexpr int kCoordCap = 64;  // CC_LOCK_QUEUE = CC_ELECTION_LISTENERS = CC_GROUP_MEMBERS = CC_VALUE_LISTENERS
 constexpr size_t kCoordBlock = sizeof(CoordHdr) + kCoordCap * sizeof(CoordEnt);
+// One staged record of the extended partition (map, set, multimap, coordination and value-event commits), one
+// 48-byte record per staging position: a bucket's run is then one contiguous span per chunk (its cache lines are
+// written whole while they sit in L2) instead of five column spans.  Value commits for k_apply_value keep the
+// st_meta / st_ab columns.
+struct XRec {
+  u64x2 ab;       // operands (locks: the clock at which due timeouts fire, the timeout)
+  uint64_t key;   // map key / group member / lock clock
+  uint64_t idx;   // log index
+  uint32_t meta;  // staging meta word (op | flags << 8 | slot low byte << 16 | kMetaTtl)
+  uint32_t res;   // map commits: the map slot; others: the instance slot
+  uint64_t pad;
+};
+static_assert(sizeof(XRec) == 48, "XRec is three 16-byte words");
 // one event of the per-sub-batch arena (apply_coord.hip -> events.hip)
 struct EvRec {
   uint32_t g;       // staging position of the commit

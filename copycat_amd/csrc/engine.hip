@@ -72,8 +72,8 @@ static void free_all(cc_engine* e) {
   e->ev_pool.clear();
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta,   e->d_val_v,     e->d_st_meta, e->d_st_ab,
                   e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
-                  e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_st_res,
-                  e->d_st_key,   e->d_st_idx,   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
+                  e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_xrec,
+                  e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
@@ -119,10 +119,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
   };
   int rc = CC_OK;
   if (!e->ext) {
-    if ((rc = alloc((void**)&e->d_st_res, sizeof(uint32_t) * e->sub_batch)) ||
-        (rc = alloc((void**)&e->d_st_key, sizeof(uint64_t) * e->sub_batch)) ||
-        (rc = alloc((void**)&e->d_st_idx, sizeof(uint64_t) * e->sub_batch)))
-      return rc;
+    if ((rc = alloc((void**)&e->d_xrec, sizeof(XRec) * e->sub_batch))) return rc;
     e->ext = true;
   }
   if (coord && !e->coord_on) {
@@ -634,9 +631,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.inst_res = e->d_inst_res;
       ha.res_type = e->d_res_type;
       ha.max_inst = e->cfg.max_instances;
-      ha.st_meta = e->d_st_meta;
-      ha.st_ab = e->d_st_ab;
-      ha.st_idx = e->d_st_idx;
+      ha.xrec = e->d_xrec;
       ha.ttab = e->d_ttab;
       ha.tiles = tiles;
       ha.sb = e->sb_total();
@@ -688,9 +683,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.hot_n = e->d_hot_n;
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
-    pa.st_res = e->d_st_res;
-    pa.st_key = e->d_st_key;
-    pa.st_idx = e->d_st_idx;
+    pa.xrec = e->d_xrec;
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
     pa.dummy = e->sub_batch;
@@ -719,11 +712,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (e->map_bits) {
       if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
-      ma.st_meta = e->d_st_meta;
-      ma.st_ab = e->d_st_ab;
-      ma.st_res = e->d_st_res;
-      ma.st_key = e->d_st_key;
-      ma.st_idx = e->d_st_idx;
+      ma.xrec = e->d_xrec;
       ma.ttab = e->d_ttab;
       ma.tiles = tiles;
       ma.sb = e->sb_total();
@@ -752,11 +741,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       HIPCHECK(hipMemsetAsync(e->d_ev_cnt, 0, sizeof(uint16_t) * (hi - lo), st));
       HIPCHECK(hipMemsetAsync(e->d_arena_n, 0, sizeof(unsigned long long), st));
       CoordArgs ca{};
-      ca.st_meta = e->d_st_meta;
-      ca.st_ab = e->d_st_ab;
-      ca.st_res = e->d_st_res;
-      ca.st_key = e->d_st_key;
-      ca.st_idx = e->d_st_idx;
+      ca.xrec = e->d_xrec;
       ca.ttab = e->d_ttab;
       ca.tiles = tiles;
       ca.sb = e->sb_total();

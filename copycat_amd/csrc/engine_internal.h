@@ -45,9 +45,7 @@ struct PartArgs {
   const uint32_t* hot_n;
   uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
   u64x2* st_ab;
-  uint32_t* st_res;   // map records: resource slot, key, log index
-  uint64_t* st_key;
-  uint64_t* st_idx;
+  XRec* xrec;         // extended staging records (k_part_ext)
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
   uint64_t dummy;     // first of the kPT dummy staging rows after the staging area (= sub_batch)
@@ -82,11 +80,7 @@ int launch_apply_value(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct MapArgs {
-  const uint32_t* st_meta;
-  const u64x2* st_ab;
-  const uint32_t* st_res;
-  const uint64_t* st_key;
-  const uint64_t* st_idx;
+  const XRec* xrec;
   const uint16_t* ttab;
   uint32_t tiles;
   uint32_t sb;  // total super-buckets (ttab row width - 1)
@@ -179,9 +173,7 @@ struct HotArgs {
   const uint8_t* res_type;
   uint32_t max_inst;
   // scan (after the partition)
-  const uint32_t* st_meta;
-  const u64x2* st_ab;
-  const uint64_t* st_idx;
+  const XRec* xrec;
   const uint16_t* ttab;
   uint32_t tiles, sb, sb_val, map_bits;
   uint64_t* tbl_key;
@@ -208,11 +200,7 @@ size_t hot_agg_bytes();
 size_t hot_s0_bytes();
 
 struct CoordArgs {
-  const uint32_t* st_meta;
-  const u64x2* st_ab;
-  const uint32_t* st_res;
-  const uint64_t* st_key;
-  const uint64_t* st_idx;
+  const XRec* xrec;
   const uint16_t* ttab;
   uint32_t tiles, sb, sb_val;
   uint32_t sbq_base;       // non-zero: the quarter buckets of the partition (else each workgroup filters its quarter)

@@ -127,9 +127,7 @@ struct cc_engine {
   uint64_t* d_tbl_val = nullptr;
   uint64_t* d_tbl_ci = nullptr;
   uint64_t* d_tbl_ins = nullptr;
-  uint32_t* d_st_res = nullptr;
-  uint64_t* d_st_key = nullptr;
-  uint64_t* d_st_idx = nullptr;
+  XRec* d_xrec = nullptr;  // [sub_batch] extended staging records (partition_ext.hip)
   // hot map keys (apply_map_hot.hip)
   HotKey* d_hot = nullptr;
   uint32_t* d_hot_n = nullptr;

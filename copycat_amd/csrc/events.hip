@@ -28,6 +28,9 @@ __global__ __launch_bounds__(kER) void k_ev_rows(const uint16_t* __restrict__ cp
                                                  uint32_t* __restrict__ tile_sum) {
   static_assert(kERPer == 16, "two uint4 of cpos per thread");
   __shared__ uint32_t wsum[kER / kWave];
+  // the tile's row_of / ev_loc are assembled in LDS and written out whole (scattered 4-byte stores to HBM cost a
+  // partly written line each); positions of commits that published nothing carry stale values nobody reads
+  __shared__ uint32_t lrow[kTile], lloc[kTile];
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t r0 = (uint64_t)blockIdx.x * kTile + (uint64_t)t * kERPer;
   const uint32_t tbase = blockIdx.x * kTile;
@@ -64,12 +67,17 @@ __global__ __launch_bounds__(kER) void k_ev_rows(const uint16_t* __restrict__ cp
 #pragma unroll
   for (int q = 0; q < kERPer; ++q) {
     if (c[q]) {
-      row_of[tbase + pp[q]] = (uint32_t)(r0 + q);
-      ev_loc[tbase + pp[q]] = run;
+      lrow[pp[q]] = (uint32_t)(r0 + q);
+      lloc[pp[q]] = run;
     }
     run += c[q];
   }
   if (t == 0) tile_sum[blockIdx.x] = total;
+  __syncthreads();
+  for (uint32_t k = t; k < (uint32_t)kTile; k += kER) {
+    row_of[tbase + k] = lrow[k];
+    ev_loc[tbase + k] = lloc[k];
+  }
 }
 
 __global__ __launch_bounds__(kER) void k_ev_tiles(const uint32_t* __restrict__ tile_sum, uint32_t tiles,

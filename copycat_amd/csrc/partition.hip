@@ -544,7 +544,7 @@ int phase_read(int kernel, uint64_t* out) {
 #ifdef CC_PHASE_TIMING
   if (kernel == K_APPLY_VALUE) return phase_read_value(out);
   if (kernel == K_APPLY_MAP) return phase_read_map(out);
-  if (kernel == K_PART_TILE && !getenv("CC_PART_EXT_V1") && getenv("CC_PART_EXT_PHASES")) return phase_read_partx(out);
+  if (kernel == K_PART_TILE && getenv("CC_PART_EXT_PHASES")) return phase_read_partx(out);
   if (kernel == K_APPLY_COORD) return phase_read_coord(out);
   if (kernel == K_PART_TILE && getenv("CC_PART_VALUE")) return phase_read_partv(out);  // the value partition
   unsigned long long z[kPhases] = {};
@@ -567,7 +567,6 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   a.mark(K_PART_TILE, 1, st);
   static const bool part_value = getenv("CC_PART_VALUE") != nullptr;  // experiment: persistent value partition
   static const bool part_tile_v1 = getenv("CC_PART_V1") != nullptr;   // A/B: the previous value partition
-  static const bool part_ext_v1 = getenv("CC_PART_EXT_V1") != nullptr;  // A/B: k_part_tile<2, true>
   if (!ext && part_value) {  // tile histograms, then the persistent value partition (partition_value.hip)
     if (a.res16) {
       if (launch_tile_hist16(a, tiles, st)) return -1;
@@ -580,13 +579,9 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   } else if (!ext) {
     hipLaunchKernelGGL((k_part_tile<kChunk / kPT, false>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, false, kChunk), st, a.inst,
                        a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
-  } else if (!part_ext_v1) {  // extended staging: partition_ext.hip k_part_ext
+                       a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n, a.st_meta, a.st_ab, nullptr, nullptr, nullptr, a.cpos, a.ttab);
+  } else {  // extended staging: partition_ext.hip k_part_ext
     if (launch_part_ext(a, tiles, st)) return -1;
-  } else {
-    hipLaunchKernelGGL((k_part_tile<kChunkMaps / kPT, true>), dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst,
-                       a.op, a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res, a.res_type, a.sb_kind, a.max_inst, a.sb,
-                       a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n, a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
   }
   a.mark(K_PART_TILE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -45,8 +45,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
     uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits, uint32_t sbq_base,
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
-    u64x2* __restrict__ st_ab, uint32_t* __restrict__ st_res, uint64_t* __restrict__ st_key,
-    uint64_t* __restrict__ st_idx, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab) {
+    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab) {
   constexpr int J = kXJ, C = kChunkMaps;
   extern __shared__ __align__(16) uint8_t smem[];  // layout: partition.hip tile_lds_bytes(sb, true, kChunkMaps)
   u64x2* rab = reinterpret_cast<u64x2*>(smem);
@@ -363,15 +362,20 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
       if (i < tile1) cpos[i - lo] = (uint16_t)cp[j];
     }
-    // write the chunk out run by run (contiguous)
+    // write the chunk out run by run (contiguous): k_apply_value records as (meta, operands) columns, every other
+    // record as one 48-byte XRec
     for (uint32_t s = t; s < nlive; s += kPT) {
       const uint32_t k = rsb[s];
       const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
-      st_meta[g] = rmeta[s];
-      st_ab[g] = rab[s];
-      st_res[g] = rres[s];
-      st_key[g] = rkey[s];
-      st_idx[g] = ridx[s];
+      if (k < sb_val && !sb_kind[k]) {
+        st_meta[g] = rmeta[s];
+        st_ab[g] = rab[s];
+      } else {
+        u64x2* o = reinterpret_cast<u64x2*>(xrec + g);
+        o[0] = rab[s];
+        o[1] = u64x2{rkey[s], ridx[s]};
+        o[2] = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), 0};
+      }
     }
     lds_barrier();
     PH(5);
@@ -389,7 +393,7 @@ int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   hipLaunchKernelGGL(k_part_ext, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
-                     a.st_meta, a.st_ab, a.st_res, a.st_key, a.st_idx, a.cpos, a.ttab);
+                     a.st_meta, a.st_ab, a.xrec, a.cpos, a.ttab);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

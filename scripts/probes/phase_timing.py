@@ -38,7 +38,7 @@ def build():
 
 
 def run(args):
-    os.environ["CC_ENGINE_SO"] = OUT
+    os.environ["CC_ENGINE_SO"] = os.environ.get("PHASE_SO", OUT)
     sys.path.insert(0, ROOT)
     import torch
 
