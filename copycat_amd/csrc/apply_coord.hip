@@ -29,9 +29,9 @@
 namespace cc {
 
 #ifdef CC_PHASE_TIMING
-__device__ unsigned long long g_wg_t[2 * 4096];  // last launch: per workgroup (start, end) wall clock
+__device__ unsigned long long g_wg_t[4 * 4096];  // last launch: per workgroup (start, end) wall clock, records, events
 int phase_read_coord_wg(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * 2 * 4096) == hipSuccess ? CC_OK : CC_ERR_HIP;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * 4 * 4096) == hipSuccess ? CC_OK : CC_ERR_HIP;
 }
 __device__ unsigned long long g_ph_coord[kPhases];
 int phase_read_coord(uint64_t* out) {
@@ -615,7 +615,6 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   uint64_t vv = 0;
   CoordHdr h{};
   const Ents E{(LdsEnt*)(ecache + l * kECache), (GlbEnt*)ents(blk)};
-  bool uni_type = false;  // wave 0's slots all hold one resource type (wave-uniform)
   if (w == 0) {
     type = res_type[res];
     h = *reinterpret_cast<const CoordHdr*>(blk);
@@ -624,7 +623,6 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
       vv = val_v[res];
     }
     E.load();
-    uni_type = __all(type == (uint32_t)__shfl(type, 0, 64)) != 0;
   }
   // staging position of list entry c (binary search over the tiles' prefix)
   auto pos_of = [&](uint32_t c) -> uint32_t {
@@ -644,6 +642,10 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     m1 = xr[g1 != 0xFFFFFFFFu ? g1 : 0].meta;
   };
   load_meta(0);
+#ifdef CC_PHASE_TIMING
+  uint64_t ev_total_lane = 0;
+  if (t == 0 && blockIdx.x < 4096) g_wg_t[4 * blockIdx.x + 3] = 0;
+#endif
   PH(0);
   for (uint32_t c0 = 0; c0 < cnt; c0 += kCCh2) {
     // rank this workgroup's commits per slot inside each wave (log order = (wave, j, lane))
@@ -735,12 +737,26 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
         oev[p] = (uint16_t)nev;
       }
       };
-      if (!uni_type) walk(TypeC<0>{});
-      else if (type == CC_RES_LOCK) walk(TypeC<CC_RES_LOCK>{});
-      else if (type == CC_RES_ELECTION) walk(TypeC<CC_RES_ELECTION>{});
-      else if (type == CC_RES_GROUP) walk(TypeC<CC_RES_GROUP>{});
-      else if (type == CC_RES_VALUE) walk(TypeC<CC_RES_VALUE>{});
+      // type-specialised walk when every lane with commits in this chunk holds one type (wave-uniform).  Lanes
+      // without commits do not count: a 64-slot group the allocator has not filled keeps CC_RES_NONE slots, and
+      // requiring those to match sent the whole group down the generic walk (its workgroups ran 1.4-2.3x longer).
+      const uint64_t act = __ballot(b < e);
+      uint32_t wt = 0;
+      bool uni = false;
+      if (act) {
+        wt = (uint32_t)__shfl((int)type, __ffsll((long long)act) - 1, 64);
+        uni = __all(b >= e || type == wt) != 0;
+      }
+      if (!act) {
+      } else if (!uni) walk(TypeC<0>{});
+      else if (wt == CC_RES_LOCK) walk(TypeC<CC_RES_LOCK>{});
+      else if (wt == CC_RES_ELECTION) walk(TypeC<CC_RES_ELECTION>{});
+      else if (wt == CC_RES_GROUP) walk(TypeC<CC_RES_GROUP>{});
+      else if (wt == CC_RES_VALUE) walk(TypeC<CC_RES_VALUE>{});
       else walk(TypeC<0>{});
+#ifdef CC_PHASE_TIMING
+      ev_total_lane += lane_n;
+#endif
       // this chunk's event regions: exclusive prefix of the lanes' (capped) counts, one arena reservation
       const uint32_t mine = lane_n < (uint32_t)kEvLane ? lane_n : (uint32_t)kEvLane;
       uint32_t inc = mine;
@@ -779,9 +795,11 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   PH_FLUSH(g_ph_coord);
 #ifdef CC_PHASE_TIMING
   if (t == 0 && blockIdx.x < 4096) {
-    g_wg_t[2 * blockIdx.x] = ph_t0_;
-    g_wg_t[2 * blockIdx.x + 1] = wall_clock64();
+    g_wg_t[4 * blockIdx.x] = ph_t0_;
+    g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
+    g_wg_t[4 * blockIdx.x + 2] = cnt;
   }
+  if (w == 0 && blockIdx.x < 4096) atomicAdd(&g_wg_t[4 * blockIdx.x + 3], (unsigned long long)ev_total_lane);
 #endif
   if (w == 0) {
     E.store();

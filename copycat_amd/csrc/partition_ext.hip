@@ -363,18 +363,24 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       if (i < tile1) cpos[i - lo] = (uint16_t)cp[j];
     }
     // write the chunk out run by run (contiguous): k_apply_value records as (meta, operands) columns, every other
-    // record as one 48-byte XRec
-    for (uint32_t s = t; s < nlive; s += kPT) {
+    // record as one 48-byte XRec.  Lanes take consecutive 16-byte pieces (piece p = part p % 3 of sorted record
+    // p / 3), so a wave's store covers 1 KiB of a run contiguously; one lane per record (three stores at a 48-byte
+    // stride) left every piece its own partial-line write request (WRITE_SIZE 99 B per commit against 50).
+    for (uint32_t p = t; p < 3 * nlive; p += kPT) {
+      const uint32_t s = p / 3, part = p - 3 * s;
       const uint32_t k = rsb[s];
       const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
       if (k < sb_val && !sb_kind[k]) {
-        st_meta[g] = rmeta[s];
-        st_ab[g] = rab[s];
+        if (part == 0) {
+          st_meta[g] = rmeta[s];
+          st_ab[g] = rab[s];
+        }
       } else {
-        u64x2* o = reinterpret_cast<u64x2*>(xrec + g);
-        o[0] = rab[s];
-        o[1] = u64x2{rkey[s], ridx[s]};
-        o[2] = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), 0};
+        u64x2 v;
+        if (part == 0) v = rab[s];
+        else if (part == 1) v = u64x2{rkey[s], ridx[s]};
+        else v = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), 0};
+        reinterpret_cast<u64x2*>(xrec + g)[part] = v;
       }
     }
     lds_barrier();

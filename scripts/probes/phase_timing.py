@@ -134,6 +134,21 @@ def run_c3(args):
     print({k: round(v[0] / args.steps, 3) for k, v in prof.items()})
 
 
+PHASES_PARTX = ["route+hist+ttab", "rank", "wave-prefix", "run-start scan", "place", "write-out", "top(clear,issue)", "-"]
+
+
+def part_ext_report(L, E, ticks, n, steps, prof):
+    """k_part_ext's phases (CC_PART_EXT_PHASES=1): one workgroup per 16384-commit tile."""
+    assert L.cc_debug_phases(E.h, 0, ticks) == 0
+    wgs = (n + 16383) // 16384 * steps
+    tot = sum(ticks)
+    ms, nl = prof.get("k_part_tile", (0.0, 0))
+    print(f"k_part_ext: {ms / max(nl, 1) * 1e3:.1f} us/launch, workgroups {wgs}, per-WG mean {tot * 10e-3 / wgs:.2f} us")
+    for q in range(8):
+        if ticks[q]:
+            print(f"   {PHASES_PARTX[q]:18s} {ticks[q] * 10e-3 / wgs:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
+
+
 def run_c5(args):
     """The coordination kernel on bench.py's c5 stream (32,768 resources, a third each lock/election/group)."""
     import numpy as np
@@ -177,6 +192,8 @@ def run_c5(args):
     E.apply_events(db, st, va, evs)
     E.sync()
     L.cc_debug_phases(E.h, 5, ticks)
+    if os.environ.get("CC_PART_EXT_PHASES"):
+        L.cc_debug_phases(E.h, 0, ticks)
     E.profile(True)
     for k in range(args.steps):
         E.apply_events(dbs[k + 1], st, va, evs)
@@ -193,11 +210,13 @@ def run_c5(args):
         if ticks[q]:
             print(f"   {PHASES[5][q]:18s} {ticks[q] * 10e-3 / wgs:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
     print({k: round(v[0] / args.steps, 3) for k, v in prof.items()})
-    wgt = (C.c_uint64 * 8192)()
+    if os.environ.get("CC_PART_EXT_PHASES"):
+        part_ext_report(L, E, ticks, n, args.steps, prof)
+    wgt = (C.c_uint64 * 16384)()
     if L.cc_debug_phases(E.h, 64, wgt) == 0:  # the last launch's workgroups: start skew and duration spread
         import numpy as np
 
-        a = np.frombuffer(wgt, np.uint64).reshape(-1, 2)[: wgs // max(launches, 1)].astype(np.int64)
+        a = np.frombuffer(wgt, np.uint64).reshape(-1, 4)[: wgs // max(launches, 1)].astype(np.int64)
         a = a[a[:, 0] > 0]
         t0 = a[:, 0].min()
         st, en = (a[:, 0] - t0) * 10e-3, (a[:, 1] - t0) * 10e-3
@@ -207,8 +226,11 @@ def run_c5(args):
         dur = en - st
         order = np.argsort(-dur)[:12]
         tn = {int(abi.CC_RES_LOCK): "L", int(abi.CC_RES_ELECTION): "E", int(abi.CC_RES_GROUP): "G"}
-        print("   slowest:", [(int(b), round(float(dur[b]), 1), tn.get(int(types[(b // 4) * 256 + (b % 4) * 64]), "?"))
-                              for b in order])
+        print("   slowest (wg, us, type, records, events):",
+              [(int(b), round(float(dur[b]), 1), tn.get(int(types[(b // 4) * 256 + (b % 4) * 64]), "?"), int(a[b, 2]), int(a[b, 3]))
+               for b in order])
+        print(f"   records per WG: p50 {np.percentile(a[:, 2], 50):.0f} max {a[:, 2].max()}; events per WG: p50 "
+              f"{np.percentile(a[:, 3], 50):.0f} max {a[:, 3].max()}")
         for k, nm in tn.items():
             sel = np.array([types[(b // 4) * 256 + (b % 4) * 64] == k for b in range(len(a))])
             if sel.any():
