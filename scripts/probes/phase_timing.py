@@ -18,7 +18,8 @@ OUT = os.path.join(ROOT, "copycat_amd", "diag", "libcopycat_apply_phase.so")
 PHASES_PARTV = ["prologue", "rank", "scan(1 wave)", "place+issue", "write-out", "-", "-", "-"]  # CC_PART_VALUE=1
 PHASES = {
     0: ["histogram+row", "rank+wait", "wave-prefix", "exscan", "place", "write-out", "top(clear,issue)", "-"],
-    1: ["setup", "rank+wait", "wave-prefix", "slot-scan", "place", "walk", "result-store", "-"],
+    1: ["setup", "rank+wait", "wave-prefix", "slot-scan", "place", "walk", "result-store", "-"] if os.environ.get("CC_APPLY_V1") else
+       ["W walk", "W wait", "L result store", "L rank", "L barriers", "L clear+bases", "L place", "L load issue"],
     2: ["load", "scatter", "-", "-", "-", "-", "-", "-"],
     5: ["setup", "rank+wait", "slot-scan", "gather", "walk", "event-flush", "-", "-"],
     3: ["region-load+list", "chunk-load", "binding", "lookup+orphans", "sort", "scan-apply", "cmp-runs+clear",
