@@ -37,6 +37,7 @@ constexpr int kDetSlots = 4096;
 constexpr uint32_t kDetSample = 65536;
 constexpr uint32_t kDetBlk = 1024;  // consecutive rows per sample block
 constexpr int kDetProbe = 8;
+constexpr int kDetCand = 1024;      // candidate keys above the sample threshold
 
 // ---------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ flags,
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
   __shared__ uint64_t tkey[kDetSlots];
   __shared__ uint32_t tident[kDetSlots];
   __shared__ uint32_t tcnt[kDetSlots];
-  __shared__ uint32_t cand[256];
+  __shared__ uint32_t cand[kDetCand];
   __shared__ uint32_t sel[kHotMax];
   __shared__ uint32_t ncand;
   const uint32_t t = threadIdx.x;
@@ -62,9 +63,9 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
   const uint64_t n = hi - lo;
   const uint32_t S = (uint32_t)(n < kDetSample ? n : kDetSample);
   // the sample: 64 blocks of 1024 consecutive rows spread evenly over the sub-batch (coalesced column loads;
-  // hot-ness only steers work, so any sample is correct), loads for 4 rows issued before their LDS updates
+  // hot-ness only steers work, so any sample is correct), loads for 16 rows issued before their LDS updates
   const uint64_t spacing = n > kDetSample ? n / (kDetSample / kDetBlk) : kDetBlk;
-  constexpr int U = 4;
+  constexpr int U = 16;  // rows per thread whose dependent loads (instance, resource, type) are in flight together
   for (uint32_t j0 = t; j0 < S; j0 += kDetT * U) {
     uint32_t r[U], kt[U];
     uint64_t key[U];
@@ -103,15 +104,17 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
     }
   }
   __syncthreads();
-  const uint32_t thresh = S / 1024 > 16 ? S / 1024 : 16;
+  // hot: >= 1/4096 of the sample (Zipf 0.99 over 1M pairs: the ~280 heaviest keys).  Every key left in the regions
+  // then carries < 0.025% of the sub-batch, so no region's chain is more than a few times the average one.
+  const uint32_t thresh = S / 4096 > 16 ? S / 4096 : 16;
   for (uint32_t q = t; q < kDetSlots; q += kDetT) {
     if (th64[q] != 0 && tcnt[q] >= thresh) {
       const uint32_t k = atomicAdd(&ncand, 1u);
-      if (k < 256) cand[k] = q;
+      if (k < (uint32_t)kDetCand) cand[k] = q;
     }
   }
   __syncthreads();
-  const uint32_t nc = ncand < 256 ? ncand : 256;
+  const uint32_t nc = ncand < (uint32_t)kDetCand ? ncand : (uint32_t)kDetCand;
   if (t < nc) {  // keep the kHotMax most frequent (ties: lower slot)
     const uint32_t c = cand[t], cc = tcnt[c];
     uint32_t rank = 0;
@@ -122,23 +125,21 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
     if (rank < (uint32_t)kHotMax) sel[rank] = c;
   }
   __syncthreads();
-  if (t >= kWave) return;
-  // bind each hot key's table entry (the tables are idle between the sub-batch's kernels); one wave, new
-  // entries inserted one lane at a time so no two lanes race for a slot
+  // bind each hot key's table entry (the tables are idle between the sub-batch's kernels): every key looks itself
+  // up in parallel (thread = key); the keys not in the table yet (first sub-batches only) are inserted by one wave,
+  // one lane at a time, so no two keys race for a slot; then wave 0 compacts the bound keys in rank order
   const uint32_t nh = nc < (uint32_t)kHotMax ? nc : (uint32_t)kHotMax;
-  const uint32_t l = t;
-  bool valid = l < nh, found = false;
-  uint64_t h = 0, key = 0;
-  uint32_t ident = 0, pos = 0;
-  uint64_t base = 0;
+  uint64_t h = 0, key = 0, base = 0;
+  uint32_t ident = 0;
+  const bool valid = t < nh;
   if (valid) {
-    const uint32_t q = sel[l];
+    const uint32_t q = sel[t];
     h = th64[q];
     key = tkey[q];
     ident = tident[q];
     base = (h >> (64 - map_bits)) * kMapRegion;
   }
-  auto probe = [&](bool insert) {
+  auto probe = [&](bool insert, uint32_t& pos) -> bool {
     uint32_t p = (uint32_t)h & (kMapRegion - 1);
     for (int step = 0; step < kMapRegion; ++step, p = (p + 1) & (kMapRegion - 1)) {
       const uint32_t w = __hip_atomic_load(&tbl_word[base + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -149,32 +150,70 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
           __hip_atomic_store(&tbl_ci[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_ins[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_word[base + p], ident, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          found = true;
           pos = (uint32_t)(base + p);
+          return true;
         }
-        return;
+        return false;
       }
       if ((w & kMwIdentMask) == ident &&
           __hip_atomic_load(&tbl_key[base + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key) {
-        found = true;
         pos = (uint32_t)(base + p);
-        return;
+        return true;
       }
     }
+    return false;  // a full region leaves the key cold
   };
-  if (valid) probe(false);
-  for (uint64_t need = ballot(valid && !found); need; need &= need - 1) {
-    const uint32_t leader = (uint32_t)__builtin_ctzll(need);
-    if (l == leader) probe(true);  // a full region leaves the key cold
-    __threadfence();
+  uint32_t pos = 0;
+  const bool found = valid && probe(false, pos);
+  __shared__ uint32_t bpos[kHotMax];
+  __shared__ uint8_t bok[kHotMax];
+  __shared__ uint32_t nmiss;
+  if (t == 0) nmiss = 0;
+  __syncthreads();
+  if (valid) {
+    bpos[t] = pos;
+    bok[t] = found ? 1 : 0;
+    if (!found) atomicAdd(&nmiss, 1u);
   }
-  const bool ok = valid && found;
-  const uint64_t okm = ballot(ok);
-  if (ok) {
-    const uint32_t k = (uint32_t)__builtin_popcountll(okm & lanemask_lt());
-    hot[k] = HotKey{h, key, ident, pos};
+  __syncthreads();
+  if (nmiss && t >= kWave && t < 2 * kWave) {  // inserts: wave 1, one key at a time in rank order
+    for (uint32_t g0 = 0; g0 < nh; g0 += kWave) {
+      const uint32_t gi = g0 + (t - kWave);
+      const bool miss = gi < nh && !bok[gi];
+      for (uint64_t need = ballot(miss); need; need &= need - 1) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(need);
+        if (t - kWave == leader) {
+          const uint32_t q = sel[gi];
+          h = th64[q];
+          key = tkey[q];
+          ident = tident[q];
+          base = (h >> (64 - map_bits)) * kMapRegion;
+          uint32_t ip = 0;
+          if (probe(true, ip)) {
+            bpos[gi] = ip;
+            bok[gi] = 1;
+          }
+        }
+        __threadfence();
+      }
+    }
   }
-  if (l == 0) *hot_n = (uint32_t)__builtin_popcountll(okm);
+  __syncthreads();
+  if (t >= kWave) return;
+  const uint32_t l = t;
+  uint32_t nbound = 0;
+  for (uint32_t g0 = 0; g0 < nh; g0 += kWave) {
+    const uint32_t gi = g0 + l;
+    const bool ok = gi < nh && bok[gi];
+    const uint64_t okm = ballot(ok);
+    if (ok) {
+      const uint32_t q = sel[gi];
+      const uint32_t k = nbound + (uint32_t)__builtin_popcountll(okm & lanemask_lt());
+      hot[k] = HotKey{th64[q], tkey[q], tident[q], bpos[gi]};
+    }
+    nbound += (uint32_t)__builtin_popcountll(okm);
+  }
+  if (l == 0) *hot_n = nbound;
 }
 
 // ---------------------------------------------------------------------------------------------------------

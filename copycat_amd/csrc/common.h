@@ -32,8 +32,8 @@ constexpr uint32_t kErrUnsupported = 1u;
 constexpr uint32_t kErrEvents = 2u;
 constexpr uint32_t kErrCapacity = 4u;
 // hot map keys (apply_map_hot.hip): detected per sub-batch, applied by a multi-workgroup scan
-constexpr int kHotMax = 64;         // hot keys per sub-batch
-constexpr int kHotSlots = 256;      // LDS hash of the hot set in the partition kernel
+constexpr int kHotMax = 256;        // hot keys per sub-batch
+constexpr int kHotSlots = 1024;     // LDS hash of the hot set in the partition kernel
 constexpr int kHotPiece = 4096;     // commits per scan piece (one workgroup)
 constexpr int kHotMaxPieces = (16 << 20) / kHotPiece;
 struct HotKey {
