@@ -23,6 +23,8 @@
 // Lock timeouts: a waiter whose deadline (clock at lock + timeout) is <= the clock at which due timers fire
 // before a commit (the previous commit's clock in manager mode, this commit's in module mode, A8) is gone
 // before that commit is applied; they publish nothing, so applying them lazily per lock is exact.
+#include <cstddef>
+
 #include "common.h"
 #include "engine_internal.h"
 
@@ -45,6 +47,9 @@ int phase_read_coord(uint64_t* out) {
 
 
 typedef __attribute__((address_space(3))) EvRec LdsEv;
+static_assert(sizeof(EvRec) == 24 && offsetof(EvRec, payload) == 8 && offsetof(EvRec, k) == 16 &&
+                  offsetof(EvRec, code) == 18 && offsetof(EvRec, tag) == 19 && offsetof(EvRec, src) == 20,
+              "Emitter::emit packs EvRec as three u64 words");
 // Events of the walking lane: its own region of the LDS buffer (no atomics between lanes), a running count in a
 // register; past the region's end straight to the sub-batch arena (one global atomic per event).
 struct Emitter {
@@ -73,14 +78,13 @@ struct Emitter {
 #endif
     const uint64_t pl = tag == CC_TAG_NULL ? 0 : payload;
     const uint32_t q = n++;
-    if (q < cap) {  // field by field: a struct copy through an address-space-typed pointer does not compile
-      buf[q].g = g;
-      buf[q].target = target;
-      buf[q].payload = pl;
-      buf[q].k = (uint16_t)k;
-      buf[q].code = (uint8_t)code;
-      buf[q].tag = (uint8_t)tag;
-      buf[q].src = (uint8_t)src;
+    if (q < cap) {  // the record as three 8-byte LDS stores (EvRec layout: {g, target}, payload, {k, code, tag, src})
+      typedef __attribute__((address_space(3))) uint64_t LdsU64;
+      LdsU64* p = reinterpret_cast<LdsU64*>(buf + q);
+      p[0] = (uint64_t)g | ((uint64_t)target << 32);
+      p[1] = pl;
+      p[2] = (uint64_t)(k & 0xFFFFu) | ((uint64_t)(code & 0xFFu) << 16) | ((uint64_t)(tag & 0xFFu) << 24) |
+             ((uint64_t)(src & 0xFFu) << 32);
     } else {  // region full: straight to the arena
       EvRec e;
       e.g = g;
