@@ -69,6 +69,16 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MARKER_KERNELS = {"k_part_tile": ("k_part_ext", "k_part_v2", "k_part_tile"), "k_events": ("k_ev_rows", "k_ev_perm", "k_ev_out"),
                   "k_map_hot": ("k_hot_detect", "k_hot_agg", "k_hot_lists", "k_hot_apply")}
 MARKER_SUM = {"k_events", "k_map_hot"}
+# the rocprofv3 kernel name(s) behind a profiling marker, per workload (the marker names are the engine's
+# profile slots; the partition slot runs k_part_v2 on value-only engines and k_part_ext otherwise)
+TRACE_NAMES = {"k_part_tile": {"c2": "k_part_v2<4>", "c3": "k_part_ext", "c5": "k_part_ext"},
+               "k_apply_value": {"c2": "k_apply_value_ws"}, "k_apply_map": {"c3": "k_apply_map<false>"},
+               "k_map_hot": {"c3": "k_hot_detect + k_hot_lists + k_hot_agg + k_hot_apply"},
+               "k_events": {"c5": "k_ev_rows + k_ev_perm + k_ev_out"}}
+
+
+def trace_name(marker, workload):
+    return TRACE_NAMES.get(marker, {}).get(workload, marker)
 
 
 def pmc_traffic(kernel, workload):
@@ -360,7 +370,7 @@ def run_c5(args, dev, rank, world, dist):
         avg_ms = ms_tot / max(launches, 1)
         achieved = B_OP_C5 * commits_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {
-            "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c5"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c5"),
             "alg_gb_per_launch": round(B_OP_C5 * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
             "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
@@ -638,7 +648,7 @@ def roofline_split(prof, n, steps, ms_per_step):
         if nl and k in share:
             per_kernel[k] = round(share[k] * n * steps / (ms * 1e-3) / 1e9, 1)
     return {
-        "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c2"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c2"),
         "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
         "alg_bytes_per_commit": {"total": B_OP_C2, **share, "k_apply_value": 0.0},
@@ -706,7 +716,7 @@ def run_c3(args, dev, rank, world, dist):
         avg_ms = ms_tot / max(launches, 1)
         achieved = B_OP_C3 * commits_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {
-            "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c3"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c3"),
             "alg_gb_per_launch": round(B_OP_C3 * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
             "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
