@@ -46,14 +46,19 @@ int phase_read_coord(uint64_t* out) {
 #endif
 
 
-typedef __attribute__((address_space(3))) EvRec LdsEv;
+typedef __attribute__((address_space(3))) uint64_t LdsU64;
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
+// The walkers' LDS state (event buffers, cached entries) is laid out lane-minor: word w of item i of lane l sits at
+// [(i * words + w) * kLanes + l], so a wave's access to the same item of every lane covers consecutive banks.  (The
+// lane-major layout put lanes 192 or 384 bytes apart: 16- to 32-way bank conflicts on every access of the walk.)
+constexpr uint32_t kLanes = kWave;
 static_assert(sizeof(EvRec) == 24 && offsetof(EvRec, payload) == 8 && offsetof(EvRec, k) == 16 &&
                   offsetof(EvRec, code) == 18 && offsetof(EvRec, tag) == 19 && offsetof(EvRec, src) == 20,
               "Emitter::emit packs EvRec as three u64 words");
 // Events of the walking lane: its own region of the LDS buffer (no atomics between lanes), a running count in a
 // register; past the region's end straight to the sub-batch arena (one global atomic per event).
 struct Emitter {
-  LdsEv* buf;        // this lane's region (typed: its accesses never turn into flat ones)
+  LdsU64* buf;       // this lane's column of the event planes: word w of event q at buf[(q * 3 + w) * kLanes]
   uint32_t cap;      // events per lane region
   EvRec* arena;
   unsigned long long* arena_n;
@@ -79,12 +84,10 @@ struct Emitter {
     const uint64_t pl = tag == CC_TAG_NULL ? 0 : payload;
     const uint32_t q = n++;
     if (q < cap) {  // the record as three 8-byte LDS stores (EvRec layout: {g, target}, payload, {k, code, tag, src})
-      typedef __attribute__((address_space(3))) uint64_t LdsU64;
-      LdsU64* p = reinterpret_cast<LdsU64*>(buf + q);
-      p[0] = (uint64_t)g | ((uint64_t)target << 32);
-      p[1] = pl;
-      p[2] = (uint64_t)(k & 0xFFFFu) | ((uint64_t)(code & 0xFFu) << 16) | ((uint64_t)(tag & 0xFFu) << 24) |
-             ((uint64_t)(src & 0xFFu) << 32);
+      buf[(q * 3 + 0) * kLanes] = (uint64_t)g | ((uint64_t)target << 32);
+      buf[(q * 3 + 1) * kLanes] = pl;
+      buf[(q * 3 + 2) * kLanes] = (uint64_t)(k & 0xFFFFu) | ((uint64_t)(code & 0xFFu) << 16) |
+                                  ((uint64_t)(tag & 0xFFu) << 24) | ((uint64_t)(src & 0xFFu) << 32);
     } else {  // region full: straight to the arena
       EvRec e;
       e.g = g;
@@ -109,20 +112,22 @@ __device__ inline CoordEnt* ents(uint8_t* blk) { return reinterpret_cast<CoordEn
 constexpr uint32_t kECache = 8;
 // Reads and writes select on the index, never on the pointer: each access keeps its address space (ds_read /
 // global_load), so an LDS hit does not wait behind the walk's outstanding global stores as a flat access would.
-typedef __attribute__((address_space(3))) CoordEnt LdsEnt;
 typedef __attribute__((address_space(1))) CoordEnt GlbEnt;
 struct Ents {
-  LdsEnt* lds;
+  LdsU64* lx;    // this lane's column of the entry planes: entry p at [p * kLanes]
+  LdsU64* lidx;
+  LdsU32* linst;
+  LdsU32* lpad;
   GlbEnt* glb;
   // (the global path uses nontemporal accesses: distinct instructions the compiler cannot merge with the LDS path
   // into one flat access through a selected pointer)
   __device__ CoordEnt get(uint32_t p) const {
     CoordEnt e;
     if (p < kECache) {
-      e.x = lds[p].x;
-      e.idx = lds[p].idx;
-      e.inst = lds[p].inst;
-      e.pad = lds[p].pad;
+      e.x = lx[p * kLanes];
+      e.idx = lidx[p * kLanes];
+      e.inst = linst[p * kLanes];
+      e.pad = lpad[p * kLanes];
       return e;
     }
     e.x = __builtin_nontemporal_load(&glb[p].x);
@@ -147,10 +152,10 @@ struct Ents {
   }
   __device__ void put(uint32_t p, const CoordEnt& v) const {
     if (p < kECache) {
-      lds[p].x = v.x;
-      lds[p].idx = v.idx;
-      lds[p].inst = v.inst;
-      lds[p].pad = v.pad;
+      lx[p * kLanes] = v.x;
+      lidx[p * kLanes] = v.idx;
+      linst[p * kLanes] = v.inst;
+      lpad[p * kLanes] = v.pad;
       return;
     }
     __builtin_nontemporal_store(v.x, &glb[p].x);
@@ -563,9 +568,10 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   __shared__ uint32_t rstart[kMaxTiles];
   __shared__ uint32_t rpre[kMaxTiles + 1];
   __shared__ uint32_t wsum[kCW2];
-  __shared__ EvRec evbuf[kQ * kEvLane];
+  __shared__ uint64_t evp[kEvLane * 3 * kQ];    // the walkers' event buffers (lane-minor planes, see kLanes)
   __shared__ uint32_t evoff[kQ + 1];
-  __shared__ CoordEnt ecache[kQ * kECache];   // the walkers' first entries (Ents)
+  __shared__ uint64_t ecx[kECache * kQ], eci[kECache * kQ];  // the walkers' first entries (Ents), lane-minor
+  __shared__ uint32_t ecn[kECache * kQ], ecp[kECache * kQ];
   __shared__ unsigned long long evbase;
 
   const uint32_t s = blockIdx.x / kQPerSb, q0 = (blockIdx.x % kQPerSb) * kQ;
@@ -611,14 +617,15 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     __syncthreads();
   }
   const uint32_t cnt = rpre[tiles];
-  const Emitter em{(LdsEv*)(evbuf + l * kEvLane), kEvLane, arena, arena_n, arena_cap, leak, leak_n, leak_cap};
+  static_assert(kQ == (int)kLanes, "one walking lane per slot of the quarter bucket");
+  const Emitter em{(LdsU64*)(evp + l), kEvLane, arena, arena_n, arena_cap, leak, leak_n, leak_cap};
   // the walker lanes (wave 0, lane = slot) keep their state machine's header in registers for the whole launch
   const uint32_t res = s * (1u << kSbShift) + q0 + l;
   uint8_t* blk = coord + (uint64_t)res * kCoordBlock;
   uint32_t type = 0, vm = 0;
   uint64_t vv = 0;
   CoordHdr h{};
-  const Ents E{(LdsEnt*)(ecache + l * kECache), (GlbEnt*)ents(blk)};
+  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk)};
   if (w == 0) {
     type = res_type[res];
     h = *reinterpret_cast<const CoordHdr*>(blk);
@@ -791,7 +798,13 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
         const uint32_t mid = (lo + hi) >> 1;
         if (evoff[mid] <= q) lo = mid; else hi = mid;
       }
-      if (evbase + q < arena_cap) arena[evbase + q] = evbuf[lo * kEvLane + (q - evoff[lo])];
+      if (evbase + q < arena_cap) {
+        const uint32_t i = q - evoff[lo];
+        uint64_t* dst = reinterpret_cast<uint64_t*>(arena + evbase + q);
+        dst[0] = evp[(i * 3 + 0) * kQ + lo];
+        dst[1] = evp[(i * 3 + 1) * kQ + lo];
+        dst[2] = evp[(i * 3 + 2) * kQ + lo];
+      }
     }
     __syncthreads();
     PH(5);
