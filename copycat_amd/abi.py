@@ -175,7 +175,9 @@ class cc_config(C.Structure):
         ("device", C.c_int32),
         ("flags", C.c_uint32),
         ("sub_batch", C.c_uint64),
-        ("reserved", C.c_uint64 * 4),
+        ("coord_cap", C.c_uint32),
+        ("reserved32", C.c_uint32),
+        ("reserved", C.c_uint64 * 3),
     ]
 
 

@@ -119,6 +119,7 @@ struct Ents {
   LdsU32* linst;
   LdsU32* lpad;
   GlbEnt* glb;
+  uint32_t cap;  // entries of the block (cc_config.coord_cap, a power of two)
   // (the global path uses nontemporal accesses: distinct instructions the compiler cannot merge with the LDS path
   // into one flat access through a selected pointer)
   __device__ CoordEnt get(uint32_t p) const {
@@ -177,9 +178,9 @@ struct Ents {
 __device__ inline void lock_expire(CoordHdr& h, const Ents& q, uint64_t th) {  // silent timeouts (A7)
   uint32_t kept = 0;
   for (uint32_t i = 0; i < h.n; ++i) {
-    const CoordEnt e = q.get((h.head + i) % kCoordCap);
+    const CoordEnt e = q.get((h.head + i) & (q.cap - 1));
     if (e.x != kNoDeadline && e.x <= th) continue;
-    if (kept != i) q.put((h.head + kept) % kCoordCap, e);
+    if (kept != i) q.put((h.head + kept) & (q.cap - 1), e);
     ++kept;
   }
   h.n = kept;
@@ -232,10 +233,10 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
           ev(r.inst, CC_EV_LOCK, CC_TAG_BOOL, 1);
         } else if (timeout == 0) {
           ev(r.inst, CC_EV_LOCK, CC_TAG_BOOL, 0);
-        } else if (h.n == (uint32_t)kCoordCap) {
+        } else if (h.n == E.cap) {
           err |= kErrCapacity;
         } else {
-          E.put((h.head + h.n) % kCoordCap, CoordEnt{timeout > 0 ? clk + (uint64_t)timeout : kNoDeadline, r.idx, r.inst, 0});
+          E.put((h.head + h.n) & (E.cap - 1), CoordEnt{timeout > 0 ? clk + (uint64_t)timeout : kNoDeadline, r.idx, r.inst, 0});
           ++h.n;
         }
         return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
@@ -248,7 +249,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
           h.flags = 0;
         } else {
           const CoordEnt e = E.get(h.head);
-          h.head = (h.head + 1) % kCoordCap;
+          h.head = (h.head + 1) & (E.cap - 1);
           if (!--h.n) h.head = 0;
           h.flags = kCoHeld;
           h.who = e.inst;
@@ -277,7 +278,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
           bool found = false;
           for (uint32_t i = 0; i < h.n && !found; ++i) found = E.get(i).x == r.iid;
           if (!found) {  // may be the leader's own session (A9)
-            if (h.n == (uint32_t)kCoordCap) err |= kErrCapacity;
+            if (h.n == E.cap) err |= kErrCapacity;
             else E.put(h.n++, CoordEnt{r.iid, r.idx, r.inst, 0});
           }
         }
@@ -342,7 +343,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
           e.idx = r.idx;
           e.inst = r.inst;
           E.put(p, e);
-        } else if (h.n == (uint32_t)kCoordCap) {
+        } else if (h.n == E.cap) {
           err |= kErrCapacity;
         } else {
           for (uint32_t i = h.n; i > p; --i) E.put(i, E.get(i - 1));
@@ -374,8 +375,8 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
     case CC_RES_QUEUE: {  // QueueState.java:33-199: an ArrayDeque of (value tag in pad, payload in x), FIFO ring
       const uint32_t ta = CC_FLAG_TAG_A(r.flags);
       const uint64_t pa = ta ? r.a : 0;
-      auto at = [&](uint32_t i) -> CoordEnt { return E.get((h.head + i) % kCoordCap); };
-      auto set_at = [&](uint32_t i, const CoordEnt& v) { E.put((h.head + i) % kCoordCap, v); };
+      auto at = [&](uint32_t i) -> CoordEnt { return E.get((h.head + i) & (E.cap - 1)); };
+      auto set_at = [&](uint32_t i, const CoordEnt& v) { E.put((h.head + i) & (E.cap - 1), v); };
       auto first_match = [&](uint32_t& pos) -> int {  // 1 match, 0 none, -1 NPE (a stored null's equals)
         for (uint32_t i = 0; i < h.n; ++i) {
           const CoordEnt e = at(i);
@@ -389,7 +390,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         return 0;
       };
       auto pop = [&]() {
-        h.head = (h.head + 1) % kCoordCap;
+        h.head = (h.head + 1) & (E.cap - 1);
         if (!--h.n) h.head = 0;
       };
       switch (r.op) {
@@ -407,7 +408,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         }
         case CC_OP_QUEUE_ADD:    // add :51-59
         case CC_OP_QUEUE_OFFER:  // offer :64-72 — both answer false
-          if (h.n == (uint32_t)kCoordCap) {
+          if (h.n == E.cap) {
             err |= kErrCapacity;
           } else {
             set_at(h.n, CoordEnt{pa, r.idx, r.inst, ta});
@@ -498,7 +499,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
             }
           }
           if (!found) {
-            if (h.n == (uint32_t)kCoordCap) err |= kErrCapacity;
+            if (h.n == E.cap) err |= kErrCapacity;
             else E.put(h.n++, CoordEnt{0, r.idx, r.inst, 0});
           }
           break;
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
                                                      uint32_t tiles, uint32_t sb, uint32_t sbq_base,
                                                      const uint8_t* __restrict__ sb_kind,
                                                      const uint8_t* __restrict__ res_type, const uint64_t* __restrict__ inst_id,
-                                                     uint8_t* __restrict__ coord, uint32_t* __restrict__ val_meta,
+                                                     uint8_t* __restrict__ coord, uint32_t coord_cap, uint32_t* __restrict__ val_meta,
                                                      uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
                                                      uint64_t* __restrict__ rst_value, uint16_t* __restrict__ ev_cnt,
                                                      EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n,
@@ -621,11 +622,11 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   const Emitter em{(LdsU64*)(evp + l), kEvLane, arena, arena_n, arena_cap, leak, leak_n, leak_cap};
   // the walker lanes (wave 0, lane = slot) keep their state machine's header in registers for the whole launch
   const uint32_t res = s * (1u << kSbShift) + q0 + l;
-  uint8_t* blk = coord + (uint64_t)res * kCoordBlock;
+  uint8_t* blk = coord + (uint64_t)res * coord_block(coord_cap);
   uint32_t type = 0, vm = 0;
   uint64_t vv = 0;
   CoordHdr h{};
-  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk)};
+  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk), coord_cap};
   if (w == 0) {
     type = res_type[res];
     h = *reinterpret_cast<const CoordHdr*>(blk);
@@ -848,7 +849,7 @@ int launch_apply_coord(const CoordArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_APPLY_COORD, 1, st);
   hipLaunchKernelGGL(k_apply_coord, dim3(a.sb_val * kQPerSb), dim3(kCT2), 0, st, a.xrec,
-                     a.ttab, a.tiles, a.sb, a.sbq_base, a.sb_kind, a.res_type, a.inst_id, a.coord, a.val_meta, a.val_v, a.rst_status,
+                     a.ttab, a.tiles, a.sb, a.sbq_base, a.sb_kind, a.res_type, a.inst_id, a.coord, a.coord_cap, a.val_meta, a.val_v, a.rst_status,
                      a.rst_value, a.ev_cnt, a.arena, a.arena_n, a.arena_cap, a.leak, a.leak_n, a.leak_cap, a.err);
   a.mark(K_APPLY_COORD, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -863,30 +864,30 @@ int launch_time_check(const uint64_t* time, uint64_t n, uint64_t* clock, uint32_
 
 // ---- MembershipGroupState.schedule (op 122) :86-103: a barrier row of the batch (engine.hip) --------------
 // The row's status against the group as it stands at that log position; *found tells the host to arm the timer.
-__global__ void k_group_schedule(const uint8_t* __restrict__ coord, uint32_t slot, uint64_t member, uint64_t row,
+__global__ void k_group_schedule(const uint8_t* __restrict__ coord, uint32_t ccap, uint32_t slot, uint64_t member, uint64_t row,
                                  uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value, uint32_t* __restrict__ found) {
   if (threadIdx.x != 0) return;
-  const uint8_t* blk = coord + (uint64_t)slot * kCoordBlock;
+  const uint8_t* blk = coord + (uint64_t)slot * coord_block(ccap);
   const CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
   const CoordEnt* E = reinterpret_cast<const CoordEnt*>(blk + sizeof(CoordHdr));
   uint32_t f = 0;
-  for (uint32_t q = 0; q < h.n && q < (uint32_t)kCoordCap; ++q) f |= E[q].x == member ? 1u : 0u;
+  for (uint32_t q = 0; q < h.n && q < ccap; ++q) f |= E[q].x == member ? 1u : 0u;
   out_status[row] = (uint8_t)(f ? CC_STATUS(CC_ST_OK, CC_TAG_NULL) : CC_STATUS(CC_ST_ILLEGAL_ARGUMENT, CC_TAG_NULL));
   out_value[row] = 0;
   *found = f;
 }
 
 // The timer fires (:92-98): publish "execute"(callback) to the member's instance if it is still in the group.
-__global__ void k_group_fire(const uint8_t* __restrict__ coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload,
+__global__ void k_group_fire(const uint8_t* __restrict__ coord, uint32_t ccap, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload,
                              uint32_t pos, unsigned long long* __restrict__ ev_total, uint64_t cap,
                              uint32_t* __restrict__ o_pos, uint32_t* __restrict__ o_target, uint8_t* __restrict__ o_code,
                              uint8_t* __restrict__ o_src, uint8_t* __restrict__ o_tag, uint64_t* __restrict__ o_payload,
                              uint32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
-  const uint8_t* blk = coord + (uint64_t)slot * kCoordBlock;
+  const uint8_t* blk = coord + (uint64_t)slot * coord_block(ccap);
   const CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
   const CoordEnt* E = reinterpret_cast<const CoordEnt*>(blk + sizeof(CoordHdr));
-  for (uint32_t q = 0; q < h.n && q < (uint32_t)kCoordCap; ++q) {
+  for (uint32_t q = 0; q < h.n && q < ccap; ++q) {
     if (E[q].x != member) continue;
     if (!o_pos) {
       atomicOr(err, kErrUnsupported);  // an event with no stream to publish it to
@@ -908,15 +909,15 @@ __global__ void k_group_fire(const uint8_t* __restrict__ coord, uint32_t slot, u
   }
 }
 
-int launch_group_schedule(const uint8_t* coord, uint32_t slot, uint64_t member, uint64_t row, uint8_t* out_status,
+int launch_group_schedule(const uint8_t* coord, uint32_t ccap, uint32_t slot, uint64_t member, uint64_t row, uint8_t* out_status,
                           uint64_t* out_value, uint32_t* found, hipStream_t st) {
-  hipLaunchKernelGGL(k_group_schedule, dim3(1), dim3(64), 0, st, coord, slot, member, row, out_status, out_value, found);
+  hipLaunchKernelGGL(k_group_schedule, dim3(1), dim3(64), 0, st, coord, ccap, slot, member, row, out_status, out_value, found);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_group_fire(const uint8_t* coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
+int launch_group_fire(const uint8_t* coord, uint32_t ccap, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
                       unsigned long long* ev_total, const cc_events* ev, uint32_t* err, hipStream_t st) {
-  hipLaunchKernelGGL(k_group_fire, dim3(1), dim3(64), 0, st, coord, slot, member, tag, payload, pos, ev_total,
+  hipLaunchKernelGGL(k_group_fire, dim3(1), dim3(64), 0, st, coord, ccap, slot, member, tag, payload, pos, ev_total,
                      ev ? ev->capacity : 0, ev ? ev->pos : nullptr, ev ? ev->target : nullptr, ev ? ev->code : nullptr,
                      ev ? ev->src : nullptr, ev ? ev->tag : nullptr, ev ? ev->payload : nullptr, err);
   return hipGetLastError() == hipSuccess ? 0 : -1;

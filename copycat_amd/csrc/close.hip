@@ -32,13 +32,13 @@
 namespace cc {
 
 __global__ void k_close_check(const uint32_t* __restrict__ cinst, uint32_t m, const uint32_t* __restrict__ inst_res,
-                              const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ coord,
+                              const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ coord, uint32_t ccap,
                               const uint32_t* __restrict__ pcl, uint32_t* __restrict__ fail) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m || !coord) return;
   const uint32_t islot = cinst[p], r = inst_res[islot];
   if (r == kNoRes || res_type[r] != CC_RES_ELECTION) return;
-  const CoordHdr h = *reinterpret_cast<const CoordHdr*>(coord + (uint64_t)r * kCoordBlock);
+  const CoordHdr h = *reinterpret_cast<const CoordHdr*>(coord + (uint64_t)r * coord_block(ccap));
   if (h.flags & kCoZombie) return;  // not in ResourceManager.resources: no close handler runs
   if ((h.flags & kCoHeld) && (h.flags & kCoCleaned) && h.who == islot) atomicMin(&fail[pcl[p]], p);
 }
@@ -47,14 +47,15 @@ __global__ void k_close_apply(const uint32_t* __restrict__ cinst, const uint32_t
                               const uint32_t* __restrict__ rstart, const uint32_t* __restrict__ items, uint32_t nr,
                               const uint32_t* __restrict__ pcl, const uint32_t* __restrict__ fail,
                               const uint8_t* __restrict__ res_type,
-                              const uint64_t* __restrict__ inst_id, uint8_t* __restrict__ coord, uint32_t* __restrict__ cnt,
+                              const uint64_t* __restrict__ inst_id, uint8_t* __restrict__ coord, uint32_t ccap,
+                              uint32_t* __restrict__ cnt,
                               EvRec* __restrict__ arena, unsigned long long* __restrict__ arena_n, uint64_t arena_cap,
                               LeakRec* __restrict__ leak, unsigned long long* __restrict__ leak_n, uint64_t leak_cap,
                               uint32_t* __restrict__ err) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nr) return;
   const uint32_t r = rlist[k], type = res_type[r];
-  uint8_t* blk = coord + (uint64_t)r * kCoordBlock;
+  uint8_t* blk = coord + (uint64_t)r * coord_block(ccap);
   CoordHdr h = *reinterpret_cast<const CoordHdr*>(blk);
   CoordEnt* E = reinterpret_cast<CoordEnt*>(blk + sizeof(CoordHdr));
   for (uint32_t q = rstart[k]; q < rstart[k + 1]; ++q) {
@@ -201,10 +202,10 @@ __global__ void k_close_unreg(const uint32_t* __restrict__ cinst, uint32_t m, co
 int launch_close(const CloseArgs& a, hipStream_t st) {
   if (a.m == 0) return 0;
   const uint32_t gm = (a.m + 255) / 256;
-  hipLaunchKernelGGL(k_close_check, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.inst_res, a.res_type, a.coord, a.pcl, a.fail);
+  hipLaunchKernelGGL(k_close_check, dim3(gm), dim3(256), 0, st, a.cinst, a.m, a.inst_res, a.res_type, a.coord, a.coord_cap, a.pcl, a.fail);
   if (a.nr && a.coord)
     hipLaunchKernelGGL(k_close_apply, dim3((a.nr + 63) / 64), dim3(64), 0, st, a.cinst, a.rlist, a.rstart, a.items, a.nr,
-                       a.pcl, a.fail, a.res_type, a.inst_id, a.coord, a.cnt, a.arena, a.arena_n, a.arena_cap,
+                       a.pcl, a.fail, a.res_type, a.inst_id, a.coord, a.coord_cap, a.cnt, a.arena, a.arena_n, a.arena_cap,
                        a.leak, a.leak_n, a.leak_cap, a.err);
   hipLaunchKernelGGL(k_close_scan, dim3(1), dim3(kCS), 0, st, a.cnt, a.m, a.pcl, a.fail, a.off, a.arena_n, a.arena_cap, a.out_cap,
                      a.out_pos ? 1 : 0, a.out_count, a.err);

@@ -231,8 +231,11 @@ struct LeakRec {
   uint64_t idx;
   uint32_t slot, pad;
 };
-constexpr int kCoordCap = 64;  // CC_LOCK_QUEUE = CC_ELECTION_LISTENERS = CC_GROUP_MEMBERS = CC_VALUE_LISTENERS
-constexpr size_t kCoordBlock = sizeof(CoordHdr) + kCoordCap * sizeof(CoordEnt);
+// entries per coordination block = cc_config.coord_cap (a power of two; 0 = the default CC_LOCK_QUEUE =
+// CC_ELECTION_LISTENERS = CC_GROUP_MEMBERS = CC_VALUE_LISTENERS = CC_QUEUE_CAP = 64)
+constexpr uint32_t kCoordCapDefault = 64;
+constexpr uint32_t kCoordCapMax = 65536;
+__host__ __device__ inline size_t coord_block(uint32_t cap) { return sizeof(CoordHdr) + (size_t)cap * sizeof(CoordEnt); }
 // One staged record of the extended partition (map, set, multimap, coordination and value-event commits), one
 // 48-byte record per staging position: a bucket's run is then one contiguous span per chunk (its cache lines are
 // written whole while they sit in L2) instead of five column spans.  Value commits for k_apply_value keep the

@@ -125,7 +125,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
   if (coord && !e->coord_on) {
     const uint64_t slots = (uint64_t)e->sb << kSbShift;
     e->arena_cap = std::max<uint64_t>(e->cfg.max_events, 1);
-    if ((rc = alloc((void**)&e->d_coord, kCoordBlock * slots)) ||
+    if ((rc = alloc((void**)&e->d_coord, coord_block(e->coord_cap) * slots)) ||
         (rc = alloc((void**)&e->d_ev_cnt, sizeof(uint16_t) * e->sub_batch)) ||
         (rc = alloc((void**)&e->d_row_of, sizeof(uint32_t) * e->sub_batch)) ||
         (rc = alloc((void**)&e->d_ev_loc, sizeof(uint32_t) * e->sub_batch)) ||
@@ -137,7 +137,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
         (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))) ||
         (rc = ensure_leak(e, kLeakCap)))
       return rc;
-    hipError_t x = hipMemset(e->d_coord, 0, kCoordBlock * slots);
+    hipError_t x = hipMemset(e->d_coord, 0, coord_block(e->coord_cap) * slots);
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
     // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
@@ -158,8 +158,12 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if (cfg->max_resources == 0 || cfg->max_resources > (uint32_t)kMaxSb << kSbShift)
     return set_err(CC_ERR_CAPACITY, "max_resources must be in [1, 131072]");
   if (cfg->max_instances == 0 || cfg->max_batch == 0) return set_err(CC_ERR_INVALID, "max_instances/max_batch must be > 0");
+  const uint32_t ccap = cfg->coord_cap ? cfg->coord_cap : kCoordCapDefault;
+  if (ccap < kCoordCapDefault || ccap > kCoordCapMax || (ccap & (ccap - 1)))
+    return set_err(CC_ERR_INVALID, "coord_cap must be 0 or a power of two in [64, 65536]");
   cc_engine* e = new cc_engine();
   e->cfg = *cfg;
+  e->coord_cap = ccap;
   e->device = cfg->device;
   hipError_t he = hipSetDevice(e->device);
   if (he != hipSuccess) { delete e; return set_err(CC_ERR_HIP, "hipSetDevice", he); }
@@ -382,7 +386,7 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
   }
   HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
-  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)first * kCoordBlock, 0, kCoordBlock * (uint64_t)count));
+  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)first * coord_block(e->coord_cap), 0, coord_block(e->coord_cap) * (uint64_t)count));
   if (is_keyed(type)) {  // a new HashMap: capacity 16, no history
     HIPCHECK(hipMemset(e->d_mw_peak + first, 0, sizeof(uint32_t) * count));
     HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
@@ -455,7 +459,7 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
   e->gtimers.erase(std::remove_if(e->gtimers.begin(), e->gtimers.end(),
                                   [slot](const cc_engine::GroupTimer& g) { return g.slot == slot; }),
                    e->gtimers.end());
-  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)slot * kCoordBlock, 0, kCoordBlock));
+  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)slot * coord_block(e->coord_cap), 0, coord_block(e->coord_cap)));
   HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
   HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(e->d_val_v + slot, 0, sizeof(uint64_t)));
@@ -751,6 +755,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.res_type = e->d_res_type;
       ca.inst_id = e->d_inst_id;
       ca.coord = e->d_coord;
+      ca.coord_cap = e->coord_cap;
       ca.val_meta = e->d_val_meta;
       ca.val_v = e->d_val_v;
       ca.rst_status = e->d_rst_status;
@@ -814,7 +819,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     cc_engine::GroupTimer gt = e->gtimers[tk];
     e->gtimers.erase(e->gtimers.begin() + (ptrdiff_t)tk);
     const uint32_t pos = (uint32_t)(deferred ? seg_hi - 1 : seg_hi);
-    if (launch_group_fire(e->d_coord, gt.slot, gt.member, gt.tag, gt.payload, pos, e->d_ev_total, ev, e->d_err, st))
+    if (launch_group_fire(e->d_coord, e->coord_cap, gt.slot, gt.member, gt.tag, gt.payload, pos, e->d_ev_total, ev, e->d_err, st))
       return set_err(CC_ERR_HIP, "group timer launch", hipGetLastError());
     cur = seg_hi;
     continue;
@@ -836,7 +841,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       uint64_t member = 0, delay = 0;
       HIPCHECK(hipMemcpy(&member, c->key + row, sizeof member, hipMemcpyDeviceToHost));
       if (c->aux) HIPCHECK(hipMemcpy(&delay, c->aux + row, sizeof delay, hipMemcpyDeviceToHost));
-      if (launch_group_schedule(e->d_coord, res, member, row, out->status, out->value, e->d_ttl_seen, st))
+      if (launch_group_schedule(e->d_coord, e->coord_cap, res, member, row, out->status, out->value, e->d_ttl_seen, st))
         return set_err(CC_ERR_HIP, "group schedule launch", hipGetLastError());
       uint32_t found = 0;
       HIPCHECK(hipMemcpyAsync(&found, e->d_ttl_seen, sizeof found, hipMemcpyDeviceToHost, st));
@@ -1098,6 +1103,7 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   ca.res_type = e->d_res_type;
   ca.inst_id = e->d_inst_id;
   ca.coord = e->coord_on ? e->d_coord : nullptr;
+  ca.coord_cap = e->coord_cap;
   ca.arena = e->d_arena;
   ca.arena_n = e->d_arena_n;
   ca.arena_cap = e->coord_on ? e->arena_cap : 0;
@@ -1246,11 +1252,11 @@ static int read_block(cc_engine* e, uint32_t slot, uint32_t type, CoordHdr& h, s
     return set_err(CC_ERR_INVALID, "slot does not hold a resource of that type");
   int rc = quiesce(e);
   if (rc) return rc;
-  std::vector<uint8_t> blk(kCoordBlock);
-  HIPCHECK(hipMemcpy(blk.data(), e->d_coord + (uint64_t)slot * kCoordBlock, kCoordBlock, hipMemcpyDeviceToHost));
+  std::vector<uint8_t> blk(coord_block(e->coord_cap));
+  HIPCHECK(hipMemcpy(blk.data(), e->d_coord + (uint64_t)slot * coord_block(e->coord_cap), coord_block(e->coord_cap), hipMemcpyDeviceToHost));
   memcpy(&h, blk.data(), sizeof h);
-  ents.resize(kCoordCap);
-  memcpy(ents.data(), blk.data() + sizeof(CoordHdr), sizeof(CoordEnt) * kCoordCap);
+  ents.resize(e->coord_cap);
+  memcpy(ents.data(), blk.data() + sizeof(CoordHdr), sizeof(CoordEnt) * e->coord_cap);
   if (clock) HIPCHECK(hipMemcpy(clock, e->d_clock, sizeof(uint64_t), hipMemcpyDeviceToHost));
   return CC_OK;
 }
@@ -1269,7 +1275,7 @@ extern "C" int cc_read_lock_state(cc_engine* e, uint32_t slot, int64_t* holder, 
   if (holder_cleaned) *holder_cleaned = held && (h.flags & kCoCleaned) ? 1 : 0;
   uint64_t n = 0;
   for (uint32_t i = 0; i < h.n; ++i) {  // timeouts due at the engine clock have fired (LockState.java:54-58)
-    const CoordEnt& x = q[(h.head + i) % kCoordCap];
+    const CoordEnt& x = q[(h.head + i) & (e->coord_cap - 1)];
     if (x.x != kNoDeadline && x.x <= clock) continue;
     if (n < cap) {
       if (h_queue_inst) h_queue_inst[n] = x.inst;
@@ -1371,7 +1377,7 @@ extern "C" int cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint6
       break;
     case CC_RES_QUEUE:  // elements, less the head element() clean()ed (QueueState :51-199)
       for (uint32_t i = 0; i < h.n; ++i) {
-        const CoordEnt& x = q[(h.head + i) % kCoordCap];
+        const CoordEnt& x = q[(h.head + i) & (e->coord_cap - 1)];
         if (!(x.pad & kQCleaned)) v.push_back(x.idx);
       }
       break;
@@ -1397,7 +1403,7 @@ extern "C" int cc_advance_time_events(cc_engine* e, uint64_t now, const cc_event
     size_t k = 0;
     for (; k < e->gtimers.size() && e->gtimers[k].deadline <= thr; ++k) {
       const auto& gt = e->gtimers[k];
-      if (launch_group_fire(e->d_coord, gt.slot, gt.member, gt.tag, gt.payload, 0xFFFFFFFFu, e->d_ev_total, d_events, e->d_err,
+      if (launch_group_fire(e->d_coord, e->coord_cap, gt.slot, gt.member, gt.tag, gt.payload, 0xFFFFFFFFu, e->d_ev_total, d_events, e->d_err,
                             e->own_stream))
         return set_err(CC_ERR_HIP, "group timer launch", hipGetLastError());
     }
@@ -1425,7 +1431,7 @@ struct SnapHdr {
   uint32_t abi, flags;  // flags: 1 coord blocks, 2 map TTL mode, 4 retained value commits
   uint32_t max_resources, max_instances, map_bits, sb;
   uint64_t applied, sess_next;
-  uint32_t sess_cap, sess_thr, sess_size, pad;
+  uint32_t sess_cap, sess_thr, sess_size, coord_cap;
 };
 struct Section {
   void* dev;
@@ -1467,7 +1473,7 @@ static std::vector<Section> snap_sections(cc_engine* e) {
     v.push_back({e->d_mw_peak, nullptr, 4 * mr});
     v.push_back({e->d_mw_drop, nullptr, 8 * mr});
   }
-  if (e->coord_on) v.push_back({e->d_coord, nullptr, kCoordBlock * slots});
+  if (e->coord_on) v.push_back({e->d_coord, nullptr, coord_block(e->coord_cap) * slots});
   return v;
 }
 
@@ -1509,6 +1515,7 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
   h.sess_cap = e->sess_cap;
   h.sess_thr = e->sess_thr;
   h.sess_size = e->sess_size;
+  h.coord_cap = e->coord_cap;
   uint8_t* p = (uint8_t*)h_buf;
   memcpy(p, &h, sizeof h);
   p += sizeof h;
@@ -1550,8 +1557,8 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   memcpy(&h, h_buf, sizeof h);
   if (h.magic != kSnapMagic || h.abi != CC_ABI_VERSION) return set_err(CC_ERR_INVALID, "not a snapshot of this engine ABI");
   if (h.max_resources != e->cfg.max_resources || h.max_instances != e->cfg.max_instances || h.map_bits != e->map_bits ||
-      h.sb != e->sb)
-    return set_err(CC_ERR_INVALID, "snapshot configuration (max_resources/max_instances/map_capacity) differs");
+      h.sb != e->sb || h.coord_cap != e->coord_cap)
+    return set_err(CC_ERR_INVALID, "snapshot configuration (max_resources/max_instances/map_capacity/coord_cap) differs");
   if (((h.flags & kSnapRetained) != 0) != (e->d_val_live != nullptr))  // the section lists would differ
     return set_err(CC_ERR_INVALID, "snapshot and engine differ in CC_CFG_VALUE_RETAINED");
   int rc = quiesce(e);

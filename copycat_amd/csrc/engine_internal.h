@@ -134,9 +134,9 @@ struct MapWideArgs {
 };
 int launch_map_wide(const MapWideArgs& a, hipStream_t st);
 // MembershipGroupState.schedule barrier rows and their timers (apply_coord.hip)
-int launch_group_schedule(const uint8_t* coord, uint32_t slot, uint64_t member, uint64_t row, uint8_t* out_status,
+int launch_group_schedule(const uint8_t* coord, uint32_t ccap, uint32_t slot, uint64_t member, uint64_t row, uint8_t* out_status,
                           uint64_t* out_value, uint32_t* found, hipStream_t st);
-int launch_group_fire(const uint8_t* coord, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
+int launch_group_fire(const uint8_t* coord, uint32_t ccap, uint32_t slot, uint64_t member, uint32_t tag, uint64_t payload, uint32_t pos,
                       unsigned long long* ev_total, const cc_events* ev, uint32_t* err, hipStream_t st);
 // SetState result rewrite after the batch (map_wide.hip)
 int launch_value_live(const uint32_t* inst, const uint8_t* op, const uint8_t* status, const uint64_t* value,
@@ -208,6 +208,7 @@ struct CoordArgs {
   const uint8_t* res_type;
   const uint64_t* inst_id;
   uint8_t* coord;
+  uint32_t coord_cap;      // entries per coordination block (cc_config.coord_cap)
   uint32_t* val_meta;
   uint64_t* val_v;
   uint8_t* rst_status;
@@ -265,6 +266,7 @@ struct CloseArgs {
   const uint8_t* res_type;
   const uint64_t* inst_id;
   uint8_t* coord;          // null: no coordination blocks (then no state machine has a close handler)
+  uint32_t coord_cap;      // entries per coordination block
   const uint32_t* pcl;     // [m] client rank of each position (positions are grouped by client, in client order)
   uint32_t* fail;          // [clients] per client: first position whose close throws (init m); that client's
                            // fan-out ends there (ResourceManager.close runs once per session), the others go on

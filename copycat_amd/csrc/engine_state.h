@@ -70,6 +70,7 @@ struct SlotBits {
 using namespace cc;  // internal header: the engine's host translation units all work in namespace cc
 
 struct cc_engine {
+  uint32_t coord_cap = 64;  // entries per coordination block (cc_config.coord_cap, a power of two)
   cc_config cfg{};
   int device = 0;
   hipStream_t own_stream = nullptr;

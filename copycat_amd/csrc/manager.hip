@@ -179,10 +179,10 @@ extern "C" int cc_delete_resource(cc_engine* e, uint64_t resource_id, uint8_t* s
     int rc = quiesce(e);
     if (rc) return rc;
     CoordHdr h;
-    HIPCHECK(hipMemcpy(&h, e->d_coord + (uint64_t)slot * kCoordBlock, sizeof h, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&h, e->d_coord + (uint64_t)slot * coord_block(e->coord_cap), sizeof h, hipMemcpyDeviceToHost));
     if ((h.flags & kCoHeld) && (h.flags & kCoCleaned)) {  // LockState.delete :87-98 / LeaderElectionState.delete :100-108
       h.flags |= kCoZombie;
-      HIPCHECK(hipMemcpy(e->d_coord + (uint64_t)slot * kCoordBlock, &h, sizeof h, hipMemcpyHostToDevice));
+      HIPCHECK(hipMemcpy(e->d_coord + (uint64_t)slot * coord_block(e->coord_cap), &h, sizeof h, hipMemcpyHostToDevice));
       e->res_by_id.erase(it);
       e->res_zombie[slot] = 1;
       *status = CC_STATUS(CC_ST_ILLEGAL_STATE, CC_TAG_NULL);

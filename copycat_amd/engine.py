@@ -169,9 +169,10 @@ class DeviceEvents:
 
 class Engine:
     def __init__(self, max_resources, max_instances, max_batch, device=0, flags=abi.CC_CFG_TIMERS_DEFERRED,
-                 sub_batch=0, max_events=0, map_capacity=0):
+                 sub_batch=0, max_events=0, map_capacity=0, coord_cap=0):
         L = lib()
         cfg = abi.cc_config()
+        cfg.coord_cap = coord_cap  # entries per coordination resource (0 = 64)
         cfg.max_resources = max_resources
         cfg.max_instances = max_instances
         cfg.max_batch = max_batch

@@ -188,7 +188,12 @@ typedef struct cc_config {
   uint32_t flags;           /* CC_CFG_* */
   uint64_t sub_batch;       /* commits per internal sub-batch (0 = default 16M; rounded up to a multiple
                                of 16384, at most 16M)                                              */
-  uint64_t reserved[4];
+  uint32_t coord_cap;       /* entries per coordination resource: lock waiters, election listeners, group
+                               members, value listeners, queue elements (0 = 64 = CC_LOCK_QUEUE; else a power
+                               of two in [64, 65536]; CC_ERR_CAPACITY beyond).  Device memory per resource slot:
+                               32 + 24 x coord_cap bytes; entries past the first 8 are walked in global memory. */
+  uint32_t reserved32;
+  uint64_t reserved[3];
 } cc_config;
 
 #define CC_CFG_TIMERS_DEFERRED 1u  /* manager-mode timer order (A8): due timers fire after the commit
@@ -198,9 +203,10 @@ typedef struct cc_config {
 #define CC_CFG_VALUE_EVENTS    2u  /* AtomicValue Listen/Unlisten + "change" events on the GPU (every value
                                       resource then runs on the event-capable kernel)              */
 
-/* Coordination resources (lock / election / group) keep their variable-size state in fixed per-resource
- * blocks: at most CC_LOCK_QUEUE waiters per lock, CC_ELECTION_LISTENERS listeners per election,
- * CC_GROUP_MEMBERS members per group, CC_VALUE_LISTENERS listeners per value (CC_ERR_CAPACITY beyond).
+/* Coordination resources (lock / election / group / queue) keep their variable-size state in per-resource
+ * blocks of cc_config.coord_cap entries; the defaults (coord_cap = 0): at most CC_LOCK_QUEUE waiters per lock,
+ * CC_ELECTION_LISTENERS listeners per election, CC_GROUP_MEMBERS members per group, CC_VALUE_LISTENERS listeners per
+ * value, CC_QUEUE_CAP elements per queue (CC_ERR_CAPACITY beyond).
  * The time column must be non-decreasing within a batch when lock timeouts are used (Raft log time).   */
 #define CC_LOCK_QUEUE          64
 #define CC_ELECTION_LISTENERS  64

@@ -15,13 +15,13 @@ pytestmark = pytest.mark.gpu
 L, E_, G, V = abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP, abi.CC_RES_VALUE
 
 
-def _setup(types, K, flags, sub_batch=0, max_batch=1 << 20, max_events=1 << 22):
+def _setup(types, K, flags, sub_batch=0, max_batch=1 << 20, max_events=1 << 22, coord_cap=0):
     from copycat_amd.engine import Engine
     from oracle.oracle_py import Oracle
 
     R = len(types)
     max_inst = R * K + 8
-    E = Engine(R, max_inst, max_batch, flags=flags, sub_batch=sub_batch, max_events=max_events)
+    E = Engine(R, max_inst, max_batch, flags=flags, sub_batch=sub_batch, max_events=max_events, coord_cap=coord_cap)
     O = Oracle(R, max_inst, flags & abi.CC_CFG_TIMERS_DEFERRED)
     for r, t in enumerate(types):
         E.resource_create(r, int(t))
@@ -43,8 +43,8 @@ def _canon(pos, src, target, code, tag, payload):
     return sorted(rows)
 
 
-def _check_batch(E, O, b):
-    s, v, ev = E.apply_host_events(b, capacity=max(8 * len(b), 1024))
+def _check_batch(E, O, b, capacity=0):
+    s, v, ev = E.apply_host_events(b, capacity=capacity or max(8 * len(b), 1024))
     s2, v2 = O.apply(b)
     bad = np.nonzero((s != s2) | (v != v2))[0]
     assert len(bad) == 0, (f"{len(bad)} rows differ; first {bad[:5]}: ops {b.op[bad[:5]]} gpu {s[bad[:5]]},{v[bad[:5]]} "
@@ -138,6 +138,39 @@ def test_lock_queue_capacity_fails_loudly():
     with pytest.raises(EngineError) as ei:
         E.apply_host_events(b)
     assert ei.value.rc == abi.CC_ERR_CAPACITY
+
+
+@pytest.mark.parametrize("cap,K,n", [(256, 200, 30_000), (1024, 700, 20_000)])
+def test_large_coordination_blocks(cap, K, n):
+    """cc_config.coord_cap: locks with hundreds of waiters, elections with hundreds of listeners, groups with hundreds
+    of members (entries past the walkers' 8 LDS-cached ones live in global memory), bit-exact vs the oracle; the
+    capacity error moves with the configured cap."""
+    from copycat_amd.batch import Batch
+    from copycat_amd.engine import EngineError
+    from copycat_amd.workload import coord_random_stream
+
+    types = np.array([L, E_, G, L, E_, G, V], np.uint8)
+    E, O, max_inst = _setup(types, K, FLAGS, coord_cap=cap, max_events=1 << 25)
+    b = coord_random_stream(n, types, K, max_inst, seed=11 + cap)
+    _check_batch(E, O, b, capacity=1 << 25)
+    _check_state(E, O, types)
+    # a queue of waiters past the cap fails loudly
+    E2, O2, _ = _setup(np.array([L], np.uint8), cap + 2, FLAGS, coord_cap=cap)
+    m = cap + 2
+    b2 = Batch.from_columns(index=np.arange(1, m + 1), time=np.ones(m), inst=np.arange(m),
+                            op=np.full(m, abi.CC_OP_LOCK_LOCK, np.uint8), aux=np.full(m, 2**64 - 1, np.uint64))
+    with pytest.raises(EngineError) as ei:
+        E2.apply_host_events(b2)
+    assert ei.value.rc == abi.CC_ERR_CAPACITY
+
+
+def test_coord_cap_must_be_power_of_two():
+    from copycat_amd.engine import Engine, EngineError
+
+    for bad in (32, 100, 1 << 17):
+        with pytest.raises(EngineError) as ei:
+            Engine(8, 8, 1024, coord_cap=bad)
+        assert ei.value.rc == abi.CC_ERR_INVALID
 
 
 def test_events_without_stream_fail_loudly():
