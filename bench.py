@@ -150,13 +150,20 @@ def run_c4(args, dev, rank, world, dist):
 
     G = args.commits or (1 << 20)
     S = G
-    match, ts, ci = quorum_groups(G, replicas=5, seed=0xA700000 + 4 + rank)
-    last, now, timeout = expiry_sessions(S, seed=0xA700000 + 5 + rank)
+    # resident input sets used in turn, so each step reads inputs the previous steps have pushed out of the 256 MiB
+    # Infinity Cache (one set is 72 MB at 1M groups + 1M sessions: re-read every step it would be served on-die)
+    nsets = max(1, args.c4_sets)
 
     def dev_u64(a):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
 
-    d_match, d_ts, d_ci, d_last = dev_u64(match), dev_u64(ts), dev_u64(ci), dev_u64(last)
+    sets = []
+    for j in range(nsets):
+        match, ts, ci = quorum_groups(G, replicas=5, seed=0xA700000 + 4 + rank + 1000 * j)
+        last, now, timeout = expiry_sessions(S, seed=0xA700000 + 5 + rank + 1000 * j)
+        sets.append((dev_u64(match), dev_u64(ts), dev_u64(ci), dev_u64(last)))
+    match, ts, ci = quorum_groups(G, replicas=5, seed=0xA700000 + 4 + rank)  # set 0 on the host: the CPU baseline
+    last, now, timeout = expiry_sessions(S, seed=0xA700000 + 5 + rank)
     d_out = torch.zeros(G, dtype=torch.int64, device=dev)
     d_bm = torch.zeros((S + 63) // 64, dtype=torch.int64, device=dev)
     # rank r sweeps the global sessions [r*S, (r+1)*S): the all-gather concatenates the global expired bitmap
@@ -166,7 +173,11 @@ def run_c4(args, dev, rank, world, dist):
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
+    calls = [0]
+
     def step(k=None):
+        d_match, d_ts, d_ci, d_last = sets[calls[0] % nsets]
+        calls[0] += 1
         if k is not None:
             ev[k][0].record(stream)
         quorum_commit(d_match, d_ts, d_ci, d_out, stream=stream)
@@ -224,7 +235,10 @@ def run_c4(args, dev, rank, world, dist):
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": f"c4: quorum commit index for {G:,} 5-replica Raft groups + expiry sweep over "
-                                   f"{S:,} sessions per GPU", "parallelism": f"shard{world}"},
+                                   f"{S:,} sessions per GPU", "parallelism": f"shard{world}",
+                       "input_sets": nsets, "input_set_mb": round((64 + 8) * G / 1e6, 1),
+                       "note": "steps take the resident input sets in turn; with >= 4 sets a step's inputs are not in "
+                               "the 256 MiB Infinity Cache"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                          "per_kernel_ms": {"k_quorum": round(q_ms, 5), "k_expire": round(x_ms, 5)},
@@ -799,6 +813,7 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="c2: also time one PCIe-inclusive step (pinned H2D + apply + D2H)")
     ap.add_argument("--hbm-budget-gb", type=float, default=200.0,
                     help="c2: HBM for resident per-step batches (more steps than fit replay the resident ones)")
+    ap.add_argument("--c4-sets", type=int, default=6, help="c4: resident input sets used in turn (Infinity Cache)")
     ap.add_argument("--c5-layout", choices=("manager", "interleaved", "grouped"), default="manager",
                     help="c5: resource types by slot: r %% 3 (created in turn) or in thirds")
     ap.add_argument("--retained", action="store_true", help="c2: also keep the retained value commit per slot (CC_CFG_VALUE_RETAINED)")
