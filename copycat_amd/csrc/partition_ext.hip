@@ -16,6 +16,9 @@
 
 namespace cc {
 
+#ifndef CC_PART_EXT_UNCOND
+#define CC_PART_EXT_UNCOND 1  // every present column loaded for every row under the full wave mask (0: per-type loads)
+#endif
 #ifndef CC_PART_EXT_UNROLL
 #define CC_PART_EXT_UNROLL 0  // 1: the chunk loop fully unrolled (bigger code, fewer spills)
 #endif
@@ -202,6 +205,33 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   // in a rolled loop)
   auto load_raw = [&](uint32_t ch, int qb, uint32_t (&in_)[J], uint32_t (&mt_)[J], u64x2 (&ab_)[J], uint64_t (&kk_)[J],
                       uint64_t (&ii_)[J], uint64_t (&xa_)[J]) {
+#if CC_PART_EXT_UNCOND
+    // every column the batch has, for every row (loads under the wave's full mask: no per-type divergent loads),
+    // then the record's fields selected by type
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int q = qb + j;
+      const uint64_t i0 = tile0 + (uint64_t)ch * C + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      const uint64_t i = i0 < tile1 ? i0 : lo;
+      const uint32_t ty = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      const bool dead = rp[q] == kRpDead;
+      const uint32_t iv = inst[i];
+      const uint32_t mv = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
+      const uint64_t av = ca ? ca[i] : 0, bv = cb ? cb[i] : 0, kv = ckey ? ckey[i] : 0, xv = caux ? caux[i] : 0;
+      const uint64_t iv2 = cidx ? cidx[i] : 0;
+      const uint64_t t0 = ctime ? ctime[i] : 0, t1 = ctime && i > 0 ? ctime[i - 1] : 0;
+      in_[j] = dead ? kNoRes : iv;
+      mt_[j] = dead ? 0u : mv;
+      const bool lock = ty == CC_RES_LOCK;
+      const bool val_walk = ty == CC_RES_VALUE && !sb_kind[(rp[q] & 0x1FFFFu) >> kSbShift];
+      ab_[j].x = dead ? 0 : (lock ? t0 : av);
+      ab_[j].y = dead ? 0 : (lock ? t1 : bv);
+      xa_[j] = dead || val_walk ? 0 : ((lock || is_keyed(ty)) ? xv : 0);
+      ii_[j] = dead || val_walk ? 0 : iv2;
+      kk_[j] = dead || val_walk || lock ? 0 : kv;
+    }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int q = qb + j;
