@@ -268,45 +268,45 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         h.n = 0;
         return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
       }
-      if (r.op == CC_OP_ELECT_LISTEN) {
-        if (!(h.flags & kCoHeld)) {
-          h.flags = kCoHeld;
-          h.who = r.inst;
-          h.idx = r.idx;
-          ev(r.inst, CC_EV_ELECT, CC_TAG_LONG, r.idx);
-        } else {
-          bool found = false;
-          for (uint32_t i = 0; i < h.n && !found; ++i) found = E.get(i).x == r.iid;
-          if (!found) {  // may be the leader's own session (A9)
-            if (h.n == E.cap) err |= kErrCapacity;
-            else E.put(h.n++, CoordEnt{r.iid, r.idx, r.inst, 0});
-          }
+      // listen / unlisten as one straight-line step (shared listener search and shift; see the group step)
+      const bool listen = r.op == CC_OP_ELECT_LISTEN, unlisten = r.op == CC_OP_ELECT_UNLISTEN;
+      const bool held = (h.flags & kCoHeld) != 0, self = held && h.who == r.inst;
+      if (unlisten && self && (h.flags & kCoCleaned)) return CC_STATUS(CC_ST_ILLEGAL_STATE, CC_TAG_NULL);
+      // listen while someone leads: is the session already listening (may be the leader's own session, A9)?
+      // unlisten of a listener: its entry
+      const bool search = (listen && held) || (unlisten && !self);
+      uint32_t fi = h.n;
+      for (uint32_t i = 0; i < (search ? h.n : 0u); ++i)
+        if (E.get(i).x == r.iid) {
+          fi = i;
+          break;
         }
-        return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+      const bool found = fi < h.n;
+      if (listen && !held) {  // the first listener leads
+        h.flags = kCoHeld;
+        h.who = r.inst;
+        h.idx = r.idx;
+        ev(r.inst, CC_EV_ELECT, CC_TAG_LONG, r.idx);
       }
-      if (r.op == CC_OP_ELECT_UNLISTEN) {
-        if ((h.flags & kCoHeld) && h.who == r.inst) {
-          if (h.flags & kCoCleaned) return CC_STATUS(CC_ST_ILLEGAL_STATE, CC_TAG_NULL);
-          h.flags = 0;
-          if (h.n) {
-            const CoordEnt e = E.get(0);
-            for (uint32_t i = 1; i < h.n; ++i) E.put(i - 1, E.get(i));
-            --h.n;
-            h.flags = kCoHeld;
-            h.who = e.inst;
-            h.idx = e.idx;
-            ev(e.inst, CC_EV_ELECT, CC_TAG_LONG, e.idx);
-          }
-        } else {
-          for (uint32_t i = 0; i < h.n; ++i)
-            if (E.get(i).x == r.iid) {
-              for (uint32_t k = i + 1; k < h.n; ++k) E.put(k - 1, E.get(k));
-              --h.n;
-              break;
-            }
-        }
-        return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+      if (listen && held && !found) {
+        if (h.n == E.cap) err |= kErrCapacity;
+        else E.put(h.n++, CoordEnt{r.iid, r.idx, r.inst, 0});
       }
+      // the leader unlistens: the next listener (entry 0) leads; a listener unlistens: its entry goes
+      const bool promote = unlisten && self && h.n != 0;
+      if (unlisten && self) h.flags = 0;
+      const CoordEnt e0 = promote ? E.get(0) : CoordEnt{0, 0, 0, 0};
+      if (promote || (unlisten && !self && found)) {
+        for (uint32_t k = (promote ? 0u : fi) + 1; k < h.n; ++k) E.put(k - 1, E.get(k));
+        --h.n;
+      }
+      if (promote) {
+        h.flags = kCoHeld;
+        h.who = e0.inst;
+        h.idx = e0.idx;
+        ev(e0.inst, CC_EV_ELECT, CC_TAG_LONG, e0.idx);
+      }
+      if (listen || unlisten) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
       // isLeader
       rv = ((h.flags & kCoHeld) && h.who == r.inst && h.idx == 0) ? 1 : 0;
       return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
@@ -337,36 +337,42 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
       // execute the target member
       bool hit;
       const uint32_t p = find(r.op == CC_OP_GROUP_EXECUTE ? r.key : r.iid, hit);
-      if (r.op == CC_OP_GROUP_JOIN) {
-        if (hit) {
-          CoordEnt e = E.get(p);  // previous.clean()
-          e.idx = r.idx;
-          e.inst = r.inst;
-          E.put(p, e);
-        } else if (h.n == E.cap) {
-          err |= kErrCapacity;
-        } else {
-          for (uint32_t i = h.n; i > p; --i) E.put(i, E.get(i - 1));
-          E.put(p, CoordEnt{r.iid, r.idx, r.inst, 0});
-          ++h.n;
-          for (uint32_t i = 0; i < h.n; ++i) {
-            const CoordEnt e = E.get(i);
-            if (e.idx != r.idx) ev(e.inst, CC_EV_JOIN, CC_TAG_LONG, r.iid);
-          }
-        }
+      // One straight-line step for join / leave / execute: the lanes of a walking wave hold different ops, and three
+      // divergent paths cost the wave all three every step; here the entry shifts, the join / leave fan-out (one
+      // loop over the members as they stand after the update) and the result share their code.
+      const bool join = r.op == CC_OP_GROUP_JOIN, leave = r.op == CC_OP_GROUP_LEAVE;
+      const bool full = h.n == E.cap;
+      const bool ins = join && !hit && !full, rem = leave && hit;
+      if (join && !hit && full) err |= kErrCapacity;
+      if (join && hit) {  // previous.clean(): the member's commit is replaced
+        CoordEnt e = E.get(p);
+        e.idx = r.idx;
+        e.inst = r.inst;
+        E.put(p, e);
+      }
+      if (ins) {
+        for (uint32_t i = h.n; i > p; --i) E.put(i, E.get(i - 1));
+        E.put(p, CoordEnt{r.iid, r.idx, r.inst, 0});
+        ++h.n;
+      }
+      if (rem) {
+        for (uint32_t i = p + 1; i < h.n; ++i) E.put(i - 1, E.get(i));
+        --h.n;
+      }
+      // "join"(id) to every other member (:55) / "leave"(id) to every remaining member (:75)
+      const uint32_t fan = (ins || rem) ? h.n : 0u;
+      const uint32_t code = join ? CC_EV_JOIN : CC_EV_LEAVE;
+      for (uint32_t i = 0; i < fan; ++i) {
+        const CoordEnt e = E.get(i);
+        if (rem || e.idx != r.idx) ev(e.inst, code, CC_TAG_LONG, r.iid);
+      }
+      if (join) {
         for (uint32_t i = 0; i < h.n; ++i)  // the returned Set<Long>, ascending
           em.emit(lane_n, r.g, nev++, r.inst, CC_EV_MEMBER, CC_EVSRC_RESULT, CC_TAG_LONG, E.get(i).x);
         rv = h.n;
         return CC_STATUS(CC_ST_OK, CC_TAG_SET);
       }
-      if (r.op == CC_OP_GROUP_LEAVE) {
-        if (hit) {
-          for (uint32_t i = p + 1; i < h.n; ++i) E.put(i - 1, E.get(i));
-          --h.n;
-          for (uint32_t i = 0; i < h.n; ++i) ev(E.get(i).inst, CC_EV_LEAVE, CC_TAG_LONG, r.iid);
-        }
-        return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
-      }
+      if (leave) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
       // execute(member = key, callback = a)
       if (!hit) return CC_STATUS(CC_ST_ILLEGAL_ARGUMENT, CC_TAG_NULL);  // "unknown member"
       ev(E.get(p).inst, CC_EV_EXECUTE, CC_FLAG_TAG_A(r.flags), r.a);
