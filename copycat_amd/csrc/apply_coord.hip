@@ -106,9 +106,10 @@ struct Emitter {
 
 __device__ inline CoordEnt* ents(uint8_t* blk) { return reinterpret_cast<CoordEnt*>(blk + sizeof(CoordHdr)); }
 
-// A slot's entries during k_apply_coord: the first kECache physical entries live in LDS (copied in at kernel start,
-// back at the end), the rest stay in the global block.  Small lock queues / listener and member lists (the common
-// case) then never wait on global memory inside a slot's sequential walk.
+// A slot's entries during k_apply_coord: entry 0 lives in the walking lane's registers, entries 1..kECache-1 in LDS
+// (copied in at kernel start, back at the end), the rest stay in the global block.  Small lock queues / listener
+// and member lists (the common case) then never wait on global memory inside a slot's sequential walk, and a
+// one-entry list (a lock with one waiter, a group with one member) never waits on LDS either.
 constexpr uint32_t kECache = 8;
 // Reads and writes select on the index, never on the pointer: each access keeps its address space (ds_read /
 // global_load), so an LDS hit does not wait behind the walk's outstanding global stores as a flat access would.
@@ -120,9 +121,11 @@ struct Ents {
   LdsU32* lpad;
   GlbEnt* glb;
   uint32_t cap;  // entries of the block (cc_config.coord_cap, a power of two)
+  mutable CoordEnt r0;  // entry 0 (registers)
   // (the global path uses nontemporal accesses: distinct instructions the compiler cannot merge with the LDS path
   // into one flat access through a selected pointer)
   __device__ CoordEnt get(uint32_t p) const {
+    if (p == 0) return r0;
     CoordEnt e;
     if (p < kECache) {
       e.x = lx[p * kLanes];
@@ -152,6 +155,10 @@ struct Ents {
     glb[p].pad = v.pad;
   }
   __device__ void put(uint32_t p, const CoordEnt& v) const {
+    if (p == 0) {
+      r0 = v;
+      return;
+    }
     if (p < kECache) {
       lx[p * kLanes] = v.x;
       lidx[p * kLanes] = v.idx;
@@ -337,6 +344,9 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
       // execute the target member
       bool hit;
       const uint32_t p = find(r.op == CC_OP_GROUP_EXECUTE ? r.key : r.iid, hit);
+#ifdef CC_DIAG_G1  // diagnostics build only: the group step stops after the member search
+      if (r.op != 0xFF) { rv = p + hit; return CC_STATUS(CC_ST_OK, CC_TAG_NULL); }
+#endif
       // One straight-line step for join / leave / execute: the lanes of a walking wave hold different ops, and three
       // divergent paths cost the wave all three every step; here the entry shifts, the join / leave fan-out (one
       // loop over the members as they stand after the update) and the result share their code.
@@ -360,6 +370,9 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         --h.n;
       }
       // "join"(id) to every other member (:55) / "leave"(id) to every remaining member (:75)
+#ifdef CC_DIAG_G2  // diagnostics build only: the group step without its fan-out and result rows
+      if (r.op != 0xFF) { rv = h.n; return CC_STATUS(CC_ST_OK, CC_TAG_NULL); }
+#endif
       const uint32_t fan = (ins || rem) ? h.n : 0u;
       const uint32_t code = join ? CC_EV_JOIN : CC_EV_LEAVE;
       for (uint32_t i = 0; i < fan; ++i) {
@@ -632,7 +645,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   uint32_t type = 0, vm = 0;
   uint64_t vv = 0;
   CoordHdr h{};
-  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk), coord_cap};
+  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk), coord_cap, CoordEnt{0, 0, 0, 0}};
   if (w == 0) {
     type = res_type[res];
     h = *reinterpret_cast<const CoordHdr*>(blk);
@@ -651,13 +664,62 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     }
     return rstart[lo] + (c - rpre[lo]);
   };
-  uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu, m0 = 0, m1 = 0;
+  // the next chunk's records (whole XRec: position, meta, operands, key, index, instance) stream into registers
+  // during the walk; the instance-id gather is issued at the top of the chunk, ahead of the rank and scan
+  uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu, m0 = 0, m1 = 0, n0 = 0, n1 = 0;
+  u64x2 a0{0, 0}, a1{0, 0};
+  uint64_t k0 = 0, k1 = 0, x0 = 0, x1 = 0;
+  // Staging positions of the wave's two rows: one 64-ary search for the run of the wave's first record, then a
+  // 64-run window in the lanes (run start wS, first record wP, next run's first record wB): a row's records find
+  // their runs with ballots and two lane shuffles (k_apply_value_ws); a binary search per record was ten dependent
+  // LDS reads.  Many short or empty runs (the window does not cover the rows): the binary search.
+  auto rows_pos = [&](uint32_t cw, uint32_t& p0, uint32_t& p1) {
+    p0 = p1 = 0xFFFFFFFFu;
+    if (cw >= cnt) return;  // wave-uniform
+    const uint32_t step = (tiles + kWave - 1) / kWave;
+    uint32_t cand = l * step;
+    uint64_t bm = __ballot(cand < tiles && rpre[cand] <= cw);
+    const uint32_t base = (uint32_t)(63 - __clzll((long long)bm)) * step;
+    cand = base + l;
+    bm = __ballot(l < step && cand < tiles && rpre[cand] <= cw);
+    const uint32_t rrow = base + (uint32_t)(63 - __clzll((long long)bm));
+    const uint32_t kr = rrow + l;
+    const uint32_t wB = kr + 1 <= tiles ? rpre[kr + 1] : 0xFFFFFFFFu;
+    const uint32_t wS = kr < tiles ? rstart[kr] : 0u, wP = kr < tiles ? rpre[kr] : 0u;
+    const uint32_t lastc = cw + kWave * kCPer2 - 1 < cnt ? cw + kWave * kCPer2 - 1 : cnt - 1;
+    const bool win = (uint32_t)__shfl((int)wB, 63, 64) > lastc;
+#pragma unroll
+    for (int j = 0; j < kCPer2; ++j) {
+      const uint32_t crow = cw + j * kWave, c = crow + l;
+      uint32_t g = 0xFFFFFFFFu;
+      if (crow < cnt) {  // wave-uniform
+        if (win) {
+          uint32_t ri = (uint32_t)__popcll(__ballot(wB <= crow));
+          for (uint64_t mb = __ballot(wB > crow && wB <= crow + (kWave - 1)); mb; mb &= mb - 1)
+            ri += c >= (uint32_t)__builtin_amdgcn_readlane((int)wB, __ffsll((long long)mb) - 1) ? 1u : 0u;
+          const uint32_t rs_ = (uint32_t)__shfl((int)wS, (int)ri, 64), rp_ = (uint32_t)__shfl((int)wP, (int)ri, 64);
+          if (c < cnt) g = rs_ + (c - rp_);
+        } else if (c < cnt) {
+          g = pos_of(c);
+        }
+      }
+      (j == 0 ? p0 : p1) = g;
+    }
+  };
+  static_assert(kCPer2 == 2, "two rows per wave");
   auto load_meta = [&](uint32_t c0) {
-    const uint32_t c_0 = c0 + w * (kWave * kCPer2) + l, c_1 = c_0 + kWave;
-    g0 = c_0 < cnt ? pos_of(c_0) : 0xFFFFFFFFu;
-    g1 = c_1 < cnt ? pos_of(c_1) : 0xFFFFFFFFu;
-    m0 = xr[g0 != 0xFFFFFFFFu ? g0 : 0].meta;
-    m1 = xr[g1 != 0xFFFFFFFFu ? g1 : 0].meta;
+    rows_pos(c0 + w * (kWave * kCPer2), g0, g1);
+    const XRec* r0 = xr + (g0 != 0xFFFFFFFFu ? g0 : 0), *r1 = xr + (g1 != 0xFFFFFFFFu ? g1 : 0);
+    a0 = r0->ab;
+    k0 = r0->key;
+    x0 = r0->idx;
+    m0 = r0->meta;
+    n0 = r0->res;
+    a1 = r1->ab;
+    k1 = r1->key;
+    x1 = r1->idx;
+    m1 = r1->meta;
+    n1 = r1->res;
   };
   load_meta(0);
 #ifdef CC_PHASE_TIMING
@@ -668,15 +730,21 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   for (uint32_t c0 = 0; c0 < cnt; c0 += kCCh2) {
     // rank this workgroup's commits per slot inside each wave (log order = (wave, j, lane))
     const uint32_t gg[kCPer2] = {g0, g1}, mm[kCPer2] = {m0, m1};
+    const uint32_t in[kCPer2] = {n0, n1};
+    const u64x2 ab[kCPer2] = {a0, a1};
+    const uint64_t ky[kCPer2] = {k0, k1}, ix[kCPer2] = {x0, x1};
     uint32_t sl[kCPer2], rk[kCPer2];
     bool own[kCPer2];
+    uint64_t id[kCPer2];
 #pragma unroll
     for (int j = 0; j < kCPer2; ++j) {
       sl[j] = ((mm[j] >> 16) & 0xFFu) - q0;
       own[j] = gg[j] != 0xFFFFFFFFu && sl[j] < (uint32_t)kQ;
-      rk[j] = own[j] ? atomicAdd(&wc[w][sl[j]], 1u) : 0u;
+      id[j] = inst_id[own[j] ? in[j] : 0u];
     }
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kCPer2; ++j) rk[j] = own[j] ? atomicAdd(&wc[w][sl[j]], 1u) : 0u;
+    lds_barrier();
     PH(1);
     if (w == 0) {  // lane = slot: exclusive prefixes over the waves, then the slot run starts
       uint32_t acc = 0;
@@ -695,25 +763,13 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
       sstart[l] = inc - acc;
       if (l == 63) sstart[kQ] = inc;
     }
-    __syncthreads();
+    lds_barrier();
     PH(2);
     // gather the owned records into LDS, in slot order
     {
-      uint32_t p[kCPer2], in[kCPer2];
-      u64x2 ab[kCPer2];
-      uint64_t ky[kCPer2], ix[kCPer2];
+      uint32_t p[kCPer2];
 #pragma unroll
-      for (int j = 0; j < kCPer2; ++j) {
-        p[j] = own[j] ? sstart[sl[j]] + wc[w][sl[j]] + rk[j] : 0u;
-        const uint32_t gx = own[j] ? gg[j] : 0u;
-        ab[j] = xr[gx].ab;
-        ky[j] = xr[gx].key;
-        ix[j] = xr[gx].idx;
-        in[j] = xr[gx].res;
-      }
-      uint64_t id[kCPer2];
-#pragma unroll
-      for (int j = 0; j < kCPer2; ++j) id[j] = inst_id[own[j] ? in[j] : 0u];
+      for (int j = 0; j < kCPer2; ++j) p[j] = own[j] ? sstart[sl[j]] + wc[w][sl[j]] + rk[j] : 0u;
 #pragma unroll
       for (int j = 0; j < kCPer2; ++j) {
         if (!own[j]) continue;
@@ -726,9 +782,9 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
         rpos[p[j]] = gg[j];
       }
     }
-    load_meta(c0 + kCCh2);  // the next chunk's positions and meta words stream in during the walk
+    load_meta(c0 + kCCh2);  // the next chunk's records stream in during the walk
     for (uint32_t k = t; k < (uint32_t)(kCW2 * kQ); k += kCT2) (&wc[0][0])[k] = 0;  // (read above, before the barrier)
-    __syncthreads();
+    lds_barrier();  // LDS only: __syncthreads() would wait for the loads just issued
     PH(3);
     // the walk: lane l of wave 0 applies slot q0 + l's commits in log order
     uint32_t lane_n = 0;  // events this lane published in this chunk
@@ -789,7 +845,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
         evbase = inc ? atomicAdd(arena_n, (unsigned long long)inc) : 0ull;
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t p = t; p < sstart[kQ]; p += kCT2) {  // results to the records' staging positions
       const uint32_t gp = rpos[p];
       rst_status[gp] = ost[p];
@@ -813,7 +869,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
         dst[2] = evp[(i * 3 + 2) * kQ + lo];
       }
     }
-    __syncthreads();
+    lds_barrier();
     PH(5);
   }
   PH_FLUSH(g_ph_coord);
