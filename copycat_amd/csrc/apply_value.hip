@@ -598,17 +598,25 @@ __global__ __launch_bounds__(kVT) void k_apply_value_ws(const uint32_t* __restri
 
 // Engine-start self-check of the hardware property the stable rankings rely on: LDS atomics with return
 // from one wave instruction that hit the same address are resolved in lane order.  *bad counts violations.
-__global__ __launch_bounds__(256) void k_selfcheck_lds_order(uint32_t* __restrict__ bad) {
-  __shared__ uint32_t tbl[256];
-  const uint32_t t = threadIdx.x, l = t & 63;
+// Shaped like the kernels' rankings: 1024-thread workgroups (16 waves contending for the LDS at once), each wave
+// on its own counter row, packed u16 pair counters bumped by 1 << 16 * (key & 1) as well as plain counters, and
+// per-wave key sets from 1 to 256 distinct keys (the value apply's 256 slots, the partition's super-buckets).
+__global__ __launch_bounds__(1024) void k_selfcheck_lds_order(uint32_t* __restrict__ bad) {
+  __shared__ uint32_t tbl[16][256];
+  const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
   uint32_t x = 0x9E3779B9u ^ (t * 2654435761u) ^ (blockIdx.x * 40503u);
   uint32_t v = 0;
   for (uint32_t it = 0; it < 32; ++it) {
-    tbl[t] = 0;
+    for (uint32_t k = l; k < 256; k += 64) tbl[w][k] = 0;
     lds_barrier();
     x = x * 1664525u + 1013904223u;
-    const uint32_t key = ((x >> 8) & ((1u << (it & 3)) - 1)) + (t >> 6) * 64;
-    const uint32_t old = atomicAdd(&tbl[key], 1u);
+    const uint32_t nkeys = 1u << (it & 7);                      // 1 .. 128 keys, then (it & 8) the skewed form
+    uint32_t key = (x >> 8) & (nkeys * 2 - 1) & 255u;
+    if (it & 8) key = ((x >> 8) & 7u) == 0 ? (x >> 12) & 255u : 0u;  // one hot key plus a tail
+    const bool packed = (it & 16) != 0;
+    const uint32_t sh = packed ? 16 * (key & 1) : 0;
+    const uint32_t addr = packed ? key >> 1 : key;
+    const uint32_t old = (atomicAdd(&tbl[w][addr], 1u << sh) >> sh) & 0xFFFFu;
     for (uint32_t j = 0; j < 64; ++j) {  // uniform loop: every lane takes part in each shuffle
       const uint32_t kj = __shfl(key, j, 64), oj = __shfl(old, j, 64);
       if (j < l && kj == key && oj >= old) ++v;
@@ -619,7 +627,7 @@ __global__ __launch_bounds__(256) void k_selfcheck_lds_order(uint32_t* __restric
 }
 
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
-  hipLaunchKernelGGL(k_selfcheck_lds_order, dim3(64), dim3(256), 0, st, d_bad);
+  hipLaunchKernelGGL(k_selfcheck_lds_order, dim3(256), dim3(1024), 0, st, d_bad);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -546,7 +546,7 @@ int phase_read(int kernel, uint64_t* out) {
   if (kernel == K_APPLY_MAP) return phase_read_map(out);
   if (kernel == K_PART_TILE && getenv("CC_PART_EXT_PHASES")) return phase_read_partx(out);
   if (kernel == K_APPLY_COORD) return phase_read_coord(out);
-  if (kernel == K_PART_TILE && getenv("CC_PART_VALUE")) return phase_read_partv(out);  // the value partition
+  if (kernel == K_PART_TILE && (getenv("CC_PART_VALUE") || getenv("CC_PART_V2_PHASES"))) return phase_read_partv(out);
   unsigned long long z[kPhases] = {};
   if (kernel != K_UNPERMUTE && kernel != K_PART_TILE) return CC_ERR_INVALID;
   const void* sym = kernel == K_PART_TILE ? HIP_SYMBOL(g_ph_part) : HIP_SYMBOL(g_ph_unperm);

@@ -283,6 +283,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
   __shared__ uint16_t kst[kMaxSb];             // chunk-sorted start of run k
   __shared__ uint32_t nlive_s;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  PH_DECL
   const uint32_t hw = (sb + 1) / 2;
   const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
   const uint32_t tbase = blockIdx.x * kTile;  // staging region of this tile (relative to lo)
@@ -316,6 +317,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
 #pragma unroll
     for (int j = 0; j < kV2J; ++j) r[c][j] = r[c][j] < max_inst ? inst_res[r[c][j]] : kNoRes;
   lds_barrier();  // hist / wc zeroed
+  PH(0);
 #pragma unroll
   for (int c = 0; c < kV2N; ++c)
 #pragma unroll
@@ -352,6 +354,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
     }
     if (l == 63) row[sb] = (uint16_t)inc;  // live commits of the tile (<= 16384)
   }
+  PH(1);
   // (tpos is first read after the next barrier)
 #pragma unroll
   for (int c = 0; c < kV2N; ++c) {
@@ -369,8 +372,10 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
       const uint32_t sh = 16 * (sk[j] & 1);
       loc[j] = live ? (atomicAdd(&wc[w][sk[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
     }
+    PH(2);
     if (c + 1 < kV2N) load_raw(c + 1);
     lds_barrier();
+    PH(3);
     if (w == 0) {  // per super-bucket: exclusive prefix over the waves (in place), chunk totals, chunk-sorted starts
       uint32_t tot[KP];
 #pragma unroll
@@ -407,6 +412,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
       if (l == 63) nlive_s = inc;
     }
     lds_barrier();
+    PH(4);
     // place the records in sorted order; every commit's tile-local position (0xFFFF: unknown instance)
 #pragma unroll
     for (int j = 0; j < kV2J; ++j) {
@@ -424,6 +430,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
       if (i < hi) cpos[i - lo] = (uint16_t)cp;
     }
     lds_barrier();
+    PH(5);
     // write the chunk out run by run (contiguous); the next chunk's counters are cleared behind the reads
     const uint32_t nl = nlive_s;
     for (uint32_t sp = t; sp < nl; sp += kPT) {
@@ -434,6 +441,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
     }
     for (uint32_t k = t; k < (uint32_t)(kPW * hw); k += kPT) wc[k / hw][k % hw] = 0;
     lds_barrier();
+    PH(6);
     if (w == 0) {  // run k's next piece starts after this chunk's records of k
 #pragma unroll
       for (int e = 0; e < KP; ++e) {
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(kPT) void k_part_v2(const uint32_t* __restrict__ in
     }
     // (tpos is next read after the next chunk's first barrier)
   }
+  PH_FLUSH(g_ph_partv);
 }
 
 // inst_res (u32, kNoRes = closed) -> a u16 copy for k_tile_hist16's LDS table (0xFFFF = closed), padded to 8.

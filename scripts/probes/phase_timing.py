@@ -77,6 +77,9 @@ def run(args):
     tiles = (n + 16383) // 16384
     if os.environ.get("CC_PART_VALUE"):
         PHASES[0] = PHASES_PARTV
+    if os.environ.get("CC_PART_V2_PHASES"):  # k_part_v2 (one workgroup per tile)
+        PHASES[0] = ["prologue loads+gather", "histogram+row", "encode+rank", "issue next+barrier", "wave scan",
+                     "place+cpos", "write-out+clear", "-"]
     wgs = {0: min(tiles, 256) * launches if os.environ.get("CC_PART_VALUE") else tiles * args.steps, 1: 256 * launches, 2: min(tiles, 256) * launches}
     names = {0: "k_part_tile", 1: "k_apply_value", 2: "k_unpermute"}
     for k in range(3):
