@@ -44,6 +44,17 @@ def test_struct_layouts():
     assert C.sizeof(abi.cc_results) == 16
     assert C.sizeof(abi.cc_events) == 8 * 8
     assert C.sizeof(abi.cc_config) == 4 + 4 + 8 + 8 + 8 + 4 + 4 + 8 + 32
+    assert abi.cc_config.coord_cap.offset == 48 and abi.cc_config.reserved.offset == 56
+
+
+def test_config_fields_match_header():
+    """cc_config's field names and order in abi.py are the header's."""
+    import re
+
+    hdr = open(os.path.join(ROOT, "include", "copycat_apply.h")).read()
+    body = hdr[hdr.index("typedef struct cc_config {"):hdr.index("} cc_config;")]
+    names = re.findall(r"^\s*(?:u?int\d+_t)\s+(\w+)", body, re.M)
+    assert names == [f[0] for f in abi.cc_config._fields_]
 
 
 def test_engine_library_exports_every_declared_function():
