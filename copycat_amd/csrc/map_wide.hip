@@ -43,17 +43,11 @@ __device__ inline bool ttl_op(uint32_t op) {
          op == CC_OP_SET_ADD;
 }
 
-// Rows whose instance is open on a live map and whose op reads or resets the whole map; and whether any map row
-// arms a TTL timer (the engine then switches to TTL mode for good).
-__global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
-                                                      const uint64_t* __restrict__ aux, uint64_t n,
-                                                      const uint32_t* __restrict__ inst_res,
-                                                      const uint8_t* __restrict__ res_type, uint32_t max_inst,
-                                                      uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap,
-                                                      uint32_t* __restrict__ ttl_seen) {
-  const uint64_t i = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t o = op[i];
+// One candidate row (its op is whole-map / set / multimap / schedule, or may arm a TTL timer): resolve its resource.
+__device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* __restrict__ inst,
+                                       const uint64_t* __restrict__ aux, const uint32_t* __restrict__ inst_res,
+                                       const uint8_t* __restrict__ res_type, uint32_t max_inst, uint32_t* __restrict__ bar,
+                                       uint32_t* __restrict__ bar_n, uint32_t cap, uint32_t* __restrict__ ttl_seen) {
   bool wide = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
@@ -79,6 +73,45 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   }
   const uint32_t k = atomicAdd(bar_n, 1u);
   if (k < cap) bar[k] = (uint32_t)i;
+}
+
+// Rows whose instance is open on a live map and whose op reads or resets the whole map; and whether any map row
+// arms a TTL timer (the engine then switches to TTL mode for good).  Each thread scans 16 rows of the op column with one 16-byte load (a row per thread spent the
+// launch on issuing 64-byte loads: 2.2 ms per 1e9 rows); candidate rows (rare) are resolved one by one.
+constexpr int kMwRows = 16;
+__global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                      const uint64_t* __restrict__ aux, uint64_t n,
+                                                      const uint32_t* __restrict__ inst_res,
+                                                      const uint8_t* __restrict__ res_type, uint32_t max_inst,
+                                                      uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap,
+                                                      uint32_t* __restrict__ ttl_seen) {
+  const uint64_t g = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
+  const uint64_t i0 = g * kMwRows;
+  if (i0 >= n) return;
+  uint32_t wv[kMwRows / 4];
+  if (i0 + kMwRows <= n && (reinterpret_cast<uintptr_t>(op) & 15) == 0) {
+    const uint4 v = reinterpret_cast<const uint4*>(op)[g];
+    wv[0] = v.x;
+    wv[1] = v.y;
+    wv[2] = v.z;
+    wv[3] = v.w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < kMwRows / 4; ++q) {
+      wv[q] = 0;
+      for (int b = 0; b < 4; ++b) {
+        const uint64_t i = i0 + 4 * q + b;
+        if (i < n) wv[q] |= (uint32_t)op[i] << (8 * b);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kMwRows; ++q) {
+    const uint64_t i = i0 + q;
+    const uint32_t o = (wv[q / 4] >> (8 * (q % 4))) & 0xFFu;
+    const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
+    if (cand && i < n) map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen);
+  }
 }
 
 // An entry is live at the barrier row: present, and no TTL timer of it has fired by then.
@@ -287,7 +320,8 @@ int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t*
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
                         uint32_t* ttl_seen, hipStream_t st) {
   if (hipMemsetAsync(bar_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
-  hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((n + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
+  const uint64_t groups = (n + kMwRows - 1) / kMwRows;
+  hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((groups + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
                      res_type, max_inst, bar, bar_n, cap, ttl_seen);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
