@@ -40,10 +40,44 @@ constexpr int kDetProbe = 8;
 constexpr int kDetCand = 1024;      // candidate keys above the sample threshold
 
 // ---------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ flags,
-                                                     const uint64_t* __restrict__ ckey, uint64_t lo, uint64_t hi,
-                                                     const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type,
-                                                     uint32_t max_inst, uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
+// The sample: 64 blocks of 1024 consecutive rows spread evenly over the sub-batch (coalesced column loads; hot-ness
+// only steers work, so any sample is correct).  k_hot_sample resolves every sampled row (instance -> resource ->
+// type -> map hash) with one thread per row over 64 workgroups, so the dependent gathers overlap across the chip;
+// k_hot_detect then only counts the resolved keys (one workgroup, an LDS sketch).
+struct HotSamp {
+  uint64_t h64;    // map_hash (0: not a keyed commit)
+  uint64_t key;
+  uint32_t ident;  // mw_ident(slot, key tag)
+  uint32_t pad;
+};
+size_t hot_samp_bytes() { return sizeof(HotSamp) * kDetSample; }
+
+__global__ __launch_bounds__(kDetBlk) void k_hot_sample(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ flags,
+                                                       const uint64_t* __restrict__ ckey, uint64_t lo, uint64_t hi,
+                                                       const uint32_t* __restrict__ inst_res,
+                                                       const uint8_t* __restrict__ res_type, uint32_t max_inst,
+                                                       HotSamp* __restrict__ samp) {
+  const uint64_t n = hi - lo;
+  const uint32_t S = (uint32_t)(n < kDetSample ? n : kDetSample);
+  const uint32_t j = blockIdx.x * kDetBlk + threadIdx.x;
+  if (j >= S) return;
+  const uint64_t spacing = n > kDetSample ? n / (kDetSample / kDetBlk) : kDetBlk;
+  const uint64_t i = lo + (uint64_t)(j / kDetBlk) * spacing + (j % kDetBlk);
+  const uint32_t sl = inst[i];
+  const uint32_t kt = CC_FLAG_KTAG(flags[i]);
+  const uint64_t key = ckey[i];
+  const uint32_t r = sl < max_inst ? inst_res[sl] : kNoRes;
+  HotSamp x{0, key, 0, 0};
+  if (r != kNoRes && is_keyed(res_type[r])) {
+    x.h64 = map_hash(r, kt, key);
+    x.ident = mw_ident(r, kt);
+  }
+  samp[j] = x;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kDetT) void k_hot_detect(const HotSamp* __restrict__ samp, uint64_t lo, uint64_t hi,
+                                                     uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
                                                      uint64_t* tbl_val, uint64_t* tbl_ci, uint64_t* tbl_ins,
                                                      HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n) {
   __shared__ uint64_t th64[kDetSlots];
@@ -62,28 +96,18 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
   __syncthreads();
   const uint64_t n = hi - lo;
   const uint32_t S = (uint32_t)(n < kDetSample ? n : kDetSample);
-  // the sample: 64 blocks of 1024 consecutive rows spread evenly over the sub-batch (coalesced column loads;
-  // hot-ness only steers work, so any sample is correct), loads for 16 rows issued before their LDS updates
-  const uint64_t spacing = n > kDetSample ? n / (kDetSample / kDetBlk) : kDetBlk;
-  constexpr int U = 16;  // rows per thread whose dependent loads (instance, resource, type) are in flight together
+  // the resolved sample (k_hot_sample), 16 rows per thread in flight before their LDS updates
+  constexpr int U = 16;
   for (uint32_t j0 = t; j0 < S; j0 += kDetT * U) {
-    uint32_t r[U], kt[U];
-    uint64_t key[U];
+    HotSamp x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = j0 + u * kDetT;
-      r[u] = kNoRes;
-      if (j >= S) continue;
-      const uint64_t i = lo + (uint64_t)(j / kDetBlk) * spacing + (j % kDetBlk);
-      const uint32_t sl = inst[i];
-      kt[u] = CC_FLAG_KTAG(flags[i]);
-      key[u] = ckey[i];
-      r[u] = sl < max_inst ? inst_res[sl] : kNoRes;
+      x[u] = j < S ? samp[j] : HotSamp{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (r[u] == kNoRes || !is_keyed(res_type[r[u]])) continue;
-      const uint64_t h = map_hash(r[u], kt[u], key[u]);
+      const uint64_t h = x[u].h64;
       if (h == 0) continue;
       // short probes: a Zipf sample holds far more distinct cold keys than the sketch has slots; a hot key shows
       // up early and often, so a sample that finds no slot within kDetProbe steps is dropped
@@ -91,8 +115,8 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const uint32_t* __restrict
       for (int step = 0; step < kDetProbe; ++step, q = (q + 1) & (kDetSlots - 1)) {
         const uint64_t old = atomicCAS((unsigned long long*)&th64[q], 0ull, (unsigned long long)h);
         if (old == 0) {
-          tkey[q] = key[u];
-          tident[q] = mw_ident(r[u], kt[u]);
+          tkey[q] = x[u].key;
+          tident[q] = x[u].ident;
           atomicAdd(&tcnt[q], 1u);
           break;
         }
@@ -502,8 +526,13 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
 
 int launch_map_hot_detect(const HotArgs& a, hipStream_t st) {
   if (a.hi <= a.lo) return 0;
-  hipLaunchKernelGGL(k_hot_detect, dim3(1), dim3(kDetT), 0, st, a.inst, a.flags, a.key, a.lo, a.hi, a.inst_res, a.res_type,
-                     a.max_inst, a.map_bits, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n);
+  const uint64_t n = a.hi - a.lo;
+  const uint32_t S = (uint32_t)(n < kDetSample ? n : kDetSample);
+  HotSamp* samp = reinterpret_cast<HotSamp*>(a.hot_samp);
+  hipLaunchKernelGGL(k_hot_sample, dim3((S + kDetBlk - 1) / kDetBlk), dim3(kDetBlk), 0, st, a.inst, a.flags, a.key, a.lo, a.hi,
+                     a.inst_res, a.res_type, a.max_inst, samp);
+  hipLaunchKernelGGL(k_hot_detect, dim3(1), dim3(kDetT), 0, st, samp, a.lo, a.hi, a.map_bits, a.tbl_key, a.tbl_word,
+                     a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -74,7 +74,7 @@ static void free_all(cc_engine* e) {
                   e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
                   e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_xrec,
                   e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
-                  e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_sb_kind,    e->d_inst_id,
+                  e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_hot_samp, e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
@@ -243,6 +243,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_hot_cond, sizeof(uint32_t) * kHotMax);
     ALLOC(e->d_hot_agg, hot_agg_bytes());
     ALLOC(e->d_hot_s0, hot_s0_bytes());
+    ALLOC(e->d_hot_samp, hot_samp_bytes());
   }
   ALLOC(e->d_rst_status, e->sub_batch + 4 * kPT);  // + dummy rows for unconditional result stores
   ALLOC(e->d_rst_value, sizeof(uint64_t) * (e->sub_batch + 4 * kPT));
@@ -654,6 +655,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.hot_cond = e->d_hot_cond;
       ha.hot_agg = e->d_hot_agg;
       ha.hot_s0 = e->d_hot_s0;
+      ha.hot_samp = e->d_hot_samp;
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.err = e->d_err;

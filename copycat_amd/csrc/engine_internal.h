@@ -189,6 +189,7 @@ struct HotArgs {
   uint32_t* hot_cond;    // [kHotMax]
   void* hot_agg;         // [kHotMax][kHotMaxPieces] composites
   void* hot_s0;          // [kHotMax] entry snapshots
+  void* hot_samp;        // [65536] resolved detection sample (apply_map_hot.hip HotSamp)
   uint8_t* rst_status;
   uint64_t* rst_value;
   uint32_t* err;
@@ -198,6 +199,7 @@ int launch_map_hot_detect(const HotArgs& a, hipStream_t st);
 int launch_map_hot_apply(const HotArgs& a, hipStream_t st);
 size_t hot_agg_bytes();
 size_t hot_s0_bytes();
+size_t hot_samp_bytes();
 
 struct CoordArgs {
   const XRec* xrec;

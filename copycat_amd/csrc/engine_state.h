@@ -162,6 +162,7 @@ struct cc_engine {
   uint32_t* d_hot_cond = nullptr;
   void* d_hot_agg = nullptr;
   void* d_hot_s0 = nullptr;
+  void* d_hot_samp = nullptr;
   // extended staging (maps / coordination / value events) + coordination + events
   bool ext = false, coord_on = false;
   std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
