@@ -328,6 +328,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
   build_map(0);
   lds_barrier();
   load_chunk(0);
+  // every thread has read tmap for chunk 0 before the first chunk's build_map(c0 + kMCh) overwrites it (without
+  // this barrier a fast wave could rebuild tmap under a slow wave's chunk-0 lookups: wrong staging positions)
+  lds_barrier();
   uint32_t m[kMPer], res[kMPer], g[kMPer];
   u64x2 ab[kMPer];
   uint64_t key[kMPer];

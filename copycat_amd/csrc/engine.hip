@@ -12,6 +12,8 @@
 #include <tuple>
 #include <vector>
 
+#include <cstdlib>
+
 #include "engine_state.h"
 
 using namespace cc;
@@ -660,7 +662,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.rst_value = e->d_rst_value;
       ha.err = e->d_err;
       ha.mark = marker_of(e);
-      if (launch_map_hot_detect(ha, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError());
+      static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
+      if (no_hot) HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
+      else if (launch_map_hot_detect(ha, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError());
     }
     PartArgs pa{};
     pa.inst = c->inst;
