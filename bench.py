@@ -61,6 +61,7 @@ B_OP_C2 = 39  # index 8 + res 4 + op 1 + flags 1 + expect 8 + upd
 B_OP_C3 = 34.6  # put 30 in / get, remove 22 in; 9 out; weighted by the 45/45/10 mix
 B_OP_C5 = 48  # 26 in + 9 out + ~1 event x 13 B
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+RESULT_SENTINEL = 0xFF  # result prefill: status 0xFF (tag nibble 15) is never a legal status (copycat_amd.engine)
 
 
 # the kernels behind each cc_profile marker (the value-only partition is k_part_v2; engines with maps, coordination
@@ -193,6 +194,28 @@ def run_c4(args, dev, rank, world, dist):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    parity = None
+    if not args.no_parity:  # set 0 through both kernels (untimed) against the oracle: every group and every bit
+        from oracle.oracle_py import expire_sweep as ox
+        from oracle.oracle_py import quorum_commit as oq
+
+        d_match, d_ts, d_ci, d_last = sets[0]
+        d_out.fill_(-1)
+        d_bm.fill_(-1)
+        d_cnt.zero_()
+        quorum_commit(d_match, d_ts, d_ci, d_out, stream=stream)
+        expire_sweep(d_last, now, timeout, d_bm, d_cnt, stream=stream)
+        torch.cuda.synchronize(dev)
+        q_ref = oq(match, ts, ci)
+        b_ref, c_ref = ox(last, now, timeout)
+        q_gpu = d_out.cpu().numpy().view(np.uint64)
+        b_gpu = d_bm.cpu().numpy().view(np.uint64)
+        parity = {"groups": G, "group_mismatches": int(np.count_nonzero(q_gpu != q_ref)), "sessions": S,
+                  "bitmap_word_mismatches": int(np.count_nonzero(b_gpu != b_ref)),
+                  "expired": int(d_cnt.item()), "expired_ref": c_ref,
+                  "checked": "input set 0: new commit index of every group (output prefilled with -1) and every word of "
+                             "the expired-session bitmap (prefilled with all ones), GPU vs oracle/oracle.cpp"}
+    torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -244,23 +267,22 @@ def run_c4(args, dev, rank, world, dist):
                          "per_kernel_ms": {"k_quorum": round(q_ms, 5), "k_expire": round(x_ms, 5)},
                          "per_kernel_gbps": {"k_quorum": round(q_gbps, 1), "k_expire": round(x_gbps, 1)},
                          "bytes_per_unit": {"group": 64, "session": 8.125}},
-            "cpu_baseline": cpu,
+            "parity": parity, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if parity is not None and (parity["group_mismatches"] or parity["bitmap_word_mismatches"]
+                               or parity["expired"] != parity["expired_ref"]):
+        sys.stderr.write(f"PARITY FAILURE: {parity}\n")
+        sys.exit(3)
 
 
-def event_checksum(pos, target, code, tag, payload):
-    """Order-independent checksum of an event multiset: sum over events of a 64-bit mix of (row, target, code, tag,
-    payload) (wrapping), plus the count."""
-    with np.errstate(over="ignore"):
-        x = (np.asarray(pos, np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ (np.asarray(target, np.uint64) << np.uint64(20))
-        x ^= (np.asarray(code, np.uint64) << np.uint64(52)) ^ (np.asarray(tag, np.uint64) << np.uint64(58))
-        x ^= np.asarray(payload, np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
-        x ^= x >> np.uint64(31)
-        x *= np.uint64(0x94D049BB133111EB)
-        return int(x.sum(dtype=np.uint64)), int(len(x))
+def per_target(ev, keys=("pos", "target", "code", "tag", "payload", "src")):
+    """The event stream regrouped by target session, each target's events in stream (emission) order: the order a
+    client session observes (SURVEY A12 -- only per-target order is defined across sessions)."""
+    order = np.argsort(np.asarray(ev["target"]), kind="stable")
+    return {k: np.asarray(ev[k])[order] for k in keys}
 
 
 def run_c5(args, dev, rank, world, dist):
@@ -282,7 +304,24 @@ def run_c5(args, dev, rank, world, dist):
     nstreams = max(1, min(total_steps, int(args.hbm_budget_gb * 1e9 // (n * 54))))
     flags = abi.CC_CFG_TIMERS_DEFERRED
     t_gen = time.time()
-    clients = CoordClients(types, K=1, max_inst=R, seed=0xA700000 + 5 + rank)
+    # Session expiry: S_glob client sessions; rank r holds the keep-alives of sessions
+    # [r*S_local, (r+1)*S_local) and sweeps them; the all-gathered (OR-merged) bitmap is the global expired set, and
+    # every rank closes the instances IT hosts of every expired session (cc_sessions_expire, ResourceManager.expire
+    # :237-247).  Besides the R client instances (owned by the live sessions 1..world), every rank hosts V more
+    # instances that no commit addresses, owned by sessions spread over the whole id range: their sessions expire
+    # on whichever rank sweeps them, and only the merged bitmap closes them where they live.
+    S_local = max(64, (65536 // world) // 64 * 64)
+    S_glob = S_local * world
+    now_s, timeout_s = 10_000_000, 5000
+    last_glob = np.concatenate([now_s - np.random.default_rng(0xA700000 + 55 + r).integers(0, 2 * timeout_s, S_local)
+                                for r in range(world)]).astype(np.int64)
+    last_glob[:64] = now_s  # the sessions that own the client instances stay alive
+    V = 1024
+    victim_res = (np.arange(V, dtype=np.int64) * (R // V)) % R
+    victim_sess = (np.arange(V, dtype=np.int64) * 2654435761 + rank * 40503) % (S_glob - 64) + 64
+    expired_glob = (now_s - last_glob) > timeout_s
+    victims_expiring = int(expired_glob[victim_sess].sum())
+    clients = CoordClients(types, K=1, max_inst=R + V, seed=0xA700000 + 5 + rank)
     host = Batch(n)
     streams, parity_ref, cpu = [], None, None
     for k in range(nstreams):
@@ -290,18 +329,18 @@ def run_c5(args, dev, rank, world, dist):
         if k == 0 and rank == 0 and not args.no_parity:
             from oracle.oracle_py import Oracle
 
-            O = Oracle(R, R, flags)
+            O = Oracle(R, R + V, flags)
             for r in range(R):
                 O.resource_create(r, int(types[r]))
                 O.instance_open(r, r, 1000 + r, 1 + rank)
+            for j in range(V):
+                O.instance_open(R + j, int(victim_res[j]), 10_000_000 + j, int(victim_sess[j]))
             tc = time.perf_counter()
             s_ref, v_ref = O.apply(host)
             tc = time.perf_counter() - tc
             oe = O.take_events()
             apos, amem = O.take_aux()
-            parity_ref = (s_ref, v_ref, event_checksum(oe["pos"], oe["target"], oe["code"], oe["tag"], oe["payload"]),
-                          event_checksum(apos, np.zeros_like(apos), np.full(len(apos), abi.CC_EV_MEMBER), np.full(len(apos), 1),
-                                         amem))
+            parity_ref = (s_ref, v_ref, per_target(oe), (apos, amem))
             if world == 1 and not args.no_cpu_baseline:
                 cpu = {"value": round(n / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
                        "sample": f"step 0's {n:,} commits of the same c5 stream (events included; the parity reference), "
@@ -310,12 +349,12 @@ def run_c5(args, dev, rank, world, dist):
         streams.append(DeviceBatch.upload(host, device=dev))
     del host
     t_gen = time.time() - t_gen
-    status = torch.zeros(n, dtype=torch.uint8, device=dev)
-    value = torch.zeros(n, dtype=torch.int64, device=dev)
+    status = torch.full((n,), RESULT_SENTINEL, dtype=torch.uint8, device=dev)  # sentinel: unwritten rows show
+    value = torch.full((n,), -1, dtype=torch.int64, device=dev)
     evs = DeviceEvents(2 * n, device=dev)
     # slot capacity with one spare super-bucket: each type's last 64-slot group is partly filled (32,768 / 3 is no
     # multiple of 64), and without spare groups the allocator would have to mix types in a group (a divergent walk)
-    E = Engine(R + 256, R, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
+    E = Engine(R + 256, R + V, n, device=dev.index, sub_batch=args.sub_batch, flags=flags, max_events=2 * n)
     if args.c5_layout == "manager":  # through the product's ResourceManager (cc_create_resource): the allocator
         for r in range(R):           # places each type in 64-slot groups of its own; instance r = the r-th create
             st, iid, islot = E.create_resource(r + 1, int(types[r]), 1 + rank, 1000 + r)
@@ -324,20 +363,19 @@ def run_c5(args, dev, rank, world, dist):
         for r in range(R):
             E.resource_create(r, int(types[r]))
         E.instance_open_range(0, R, 0, 1000, 1 + rank)
+    for j in range(V):
+        E.instance_open(R + j, int(victim_res[j]), 10_000_000 + j, int(victim_sess[j]))
     stream = torch.cuda.current_stream(dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
     wm_local = torch.zeros(1, dtype=torch.int64, device=dev)
-    # session / lease expiry after each batch: 65,536 client sessions, rank r sweeps the global
-    # sessions [r*S/world, (r+1)*S/world); the all-gather of the per-rank bitmaps is the global expired set
     from copycat_amd.engine import expire_sweep
 
-    S_local = max(64, (65536 // world) // 64 * 64)
-    rng = np.random.default_rng(0xA700000 + 55 + rank)
-    now_s, timeout_s = 10_000_000, 5000
-    d_last = torch.from_numpy((now_s - rng.integers(0, 2 * timeout_s, S_local)).astype(np.int64)).to(dev)
+    d_last = torch.from_numpy(np.ascontiguousarray(last_glob[rank * S_local:(rank + 1) * S_local])).to(dev)
     d_bm = torch.zeros(S_local // 64, dtype=torch.int64, device=dev)
     d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     bm_all = torch.zeros(world * (S_local // 64), dtype=torch.int64, device=dev)
+    close_evs = DeviceEvents(1 << 16, device=dev)
+    closed_total = [0]
 
     def step(k):
         E.apply_events(streams[k % nstreams], status, value, evs, stream=stream)
@@ -346,6 +384,9 @@ def run_c5(args, dev, rank, world, dist):
         if dist is not None:  # watermark, then expired-session bitmap (RCCL all-gathers over xGMI)
             dist.all_gather_into_tensor(wm_all, wm_local)
             dist.all_gather_into_tensor(bm_all, d_bm)
+        # the expired sessions' instances on this rank leave (synchronous control plane, like the reference's expire)
+        closed, _ = E.sessions_expire(bm_all if dist is not None else d_bm, S_glob, events=close_evs)
+        closed_total[0] += closed
 
     parity = None
     for k in range(args.warmup):
@@ -403,11 +444,18 @@ def run_c5(args, dev, rank, world, dist):
                        "resident_streams": nstreams, "events_last_step": n_events, "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())],
                        "expired_sessions_per_step": int(np.unpackbits(
-                           (bm_all if dist is not None else d_bm).cpu().numpy().view(np.uint8)).sum())},
+                           (bm_all if dist is not None else d_bm).cpu().numpy().view(np.uint8)).sum()),
+                       "expiry": {"sessions": S_glob, "expired": int(expired_glob.sum()), "instances_closed": closed_total[0],
+                                  "instances_expected": victims_expiring,
+                                  "path": "per-rank cc_expire_sweep -> RCCL all-gather of the bitmaps -> "
+                                          "cc_sessions_expire on every rank, every step"}},
             "parity": parity, "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    bad = parity is not None and (parity["mismatches"] or not parity["events_equal"])
+    bad = parity is not None and (parity["mismatches"] or parity["unwritten"] or not parity["events_equal"])
+    if closed_total[0] != victims_expiring:
+        sys.stderr.write(f"EXPIRY FAILURE: closed {closed_total[0]} instances, expected {victims_expiring}\n")
+        bad = True
     if dist is not None:
         dist.destroy_process_group()
     if bad:
@@ -416,19 +464,28 @@ def run_c5(args, dev, rank, world, dist):
 
 
 def c5_parity(ref, status, value, evs, abi):
-    s_ref, v_ref, ev_ref, mem_ref = ref
+    s_ref, v_ref, ev_ref, (apos, amem) = ref
     s = status.cpu().numpy()
     v = value.cpu().numpy().view(np.uint64)
     ev = evs.host()
     member = ev["code"] == abi.CC_EV_MEMBER
-    got = event_checksum(*(ev[k][~member] for k in ("pos", "target", "code", "tag", "payload")))
-    got_mem = event_checksum(ev["pos"][member], np.zeros(int(member.sum()), np.uint64),
-                             np.full(int(member.sum()), abi.CC_EV_MEMBER), np.full(int(member.sum()), 1),
-                             ev["payload"][member])
+    got = per_target({k: ev[k][~member] for k in ("pos", "target", "code", "tag", "payload", "src")})
+    n_ev = len(got["pos"])
+    same_len = n_ev == len(ev_ref["pos"])
+    ev_bad = 0 if same_len else -1
+    if same_len:
+        d = np.zeros(n_ev, bool)
+        for k in got:
+            d |= got[k] != ev_ref[k]
+        ev_bad = int(np.count_nonzero(d))
+    mem_ok = np.array_equal(ev["pos"][member], apos) and np.array_equal(ev["payload"][member], amem)
     return {"rows": len(s), "mismatches": int(np.count_nonzero((s != s_ref) | (v != v_ref))),
-            "events": got[1], "events_equal": got == ev_ref and got_mem == mem_ref,
-            "checked": "step 0: per-commit status+value, and the event multiset (count + order-free 64-bit checksum of "
-                       "(row, target, code, tag, payload)) incl. join member sets, GPU vs oracle/oracle.cpp"}
+            "unwritten": int(np.count_nonzero(s == RESULT_SENTINEL)),
+            "events": n_ev, "events_ref": len(ev_ref["pos"]), "event_mismatches": ev_bad,
+            "events_equal": bool(same_len and ev_bad == 0 and mem_ok),
+            "checked": "step 0: per-commit status+value (results prefilled with the 0xFF sentinel status); every event "
+                       "per target session in emission order (row, target, code, tag, payload, src; SURVEY A12); "
+                       "join member sets in stream order; GPU vs oracle/oracle.cpp"}
 
 
 def cpu_threads():
@@ -515,7 +572,9 @@ def run_c2(args, dev, rank, world, dist):
                                      f"one oracle each, {cpu_model()}"}
             del O
         streams.append(DeviceBatch.upload(host, device=dev, columns=cols))
-        results.append((torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros(n, dtype=torch.int64, device=dev)))
+        # sentinel prefill (status 0xFF is no legal status): a row the kernels never write fails the step-0 parity
+        results.append((torch.full((n,), RESULT_SENTINEL, dtype=torch.uint8, device=dev),
+                        torch.full((n,), -1, dtype=torch.int64, device=dev)))
     del host
     t_gen = time.time() - t_gen
     stream = torch.cuda.current_stream(dev)
@@ -579,8 +638,10 @@ def run_c2(args, dev, rank, world, dist):
         smism = None
         if state0 is not None:
             smism = int(sum(np.count_nonzero(a != b) for a, b in zip(state0, st_ref)))
-        parity = {"rows": n, "mismatches": mism, "state_slots": R, "state_mismatches": smism,
-                  "checked": "step 0: per-commit status+value and the value state after it, GPU vs oracle/oracle.cpp"}
+        parity = {"rows": n, "mismatches": mism, "unwritten": int(np.count_nonzero(s_gpu == RESULT_SENTINEL)),
+                  "state_slots": R, "state_mismatches": smism,
+                  "checked": "step 0: per-commit status+value (results prefilled with the 0xFF sentinel status) and the "
+                             "value state after it, GPU vs oracle/oracle.cpp"}
     ms_per_step = elapsed * 1e3 / args.steps
     roofline = roofline_split(prof, n, args.steps, ms_per_step)
     if rank == 0:
@@ -597,10 +658,10 @@ def run_c2(args, dev, rank, world, dist):
                        "watermarks": watermarks, "gen_s": round(t_gen, 2)},
             "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all,
         }
-        if args.e2e:
+        if not args.no_e2e:  # the PCIe-inclusive figure beside the device-resident one (never `value`)
             out["end_to_end"] = end_to_end_c2(E, clients, n, dev)
         print(json.dumps(out), flush=True)
-    bad = parity is not None and (parity["mismatches"] or parity["state_mismatches"])
+    bad = parity is not None and (parity["mismatches"] or parity["unwritten"] or parity["state_mismatches"])
     if dist is not None:
         dist.destroy_process_group()
     if bad:
@@ -685,8 +746,8 @@ def run_c3(args, dev, rank, world, dist):
     t_gen = time.time()
     batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample))
     t_gen = time.time() - t_gen
-    status = torch.zeros(n, dtype=torch.uint8, device=dev)
-    value = torch.zeros(n, dtype=torch.int64, device=dev)
+    status = torch.full((n,), RESULT_SENTINEL, dtype=torch.uint8, device=dev)  # sentinel: unwritten rows show
+    value = torch.full((n,), -1, dtype=torch.int64, device=dev)
     E = Engine(R, R, n, device=dev.index, sub_batch=args.sub_batch, map_capacity=args.pairs)
     E.resource_create_range(0, R, abi.CC_RES_MAP)
     E.instance_open_range(0, R, 0, 1 + rank, 1 + rank)
@@ -700,8 +761,17 @@ def run_c3(args, dev, rank, world, dist):
         if dist is not None:
             dist.all_gather_into_tensor(wm_all, wm_local)
 
-    for _ in range(args.warmup):
+    m = min(n, cpu_sample)
+    gpu0 = None  # step 0's first m results (applied from the fresh state): the parity sample
+
+    def capture0():
+        torch.cuda.synchronize(dev)
+        return status[:m].cpu().numpy(), value[:m].cpu().numpy().view(np.uint64)
+
+    for k in range(args.warmup):
         step()
+        if k == 0:
+            gpu0 = capture0()
     torch.cuda.synchronize(dev)
     if not args.no_profile:
         E.profile(True)
@@ -716,6 +786,8 @@ def run_c3(args, dev, rank, world, dist):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     E.sync()
+    if gpu0 is None and args.steps == 1:  # no warmup: the one timed step is step 0
+        gpu0 = capture0()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -737,21 +809,28 @@ def run_c3(args, dev, rank, world, dist):
             "bytes_per_commit": B_OP_C3,
             "pipeline_frac": round(B_OP_C3 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         }
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    cpu = parity = None
+    if rank == 0 and (not args.no_parity or (world == 1 and not args.no_cpu_baseline)):
         from oracle.oracle_py import Oracle
 
-        m = min(n, cpu_sample)
         O = Oracle(R, R)
-        for r in range(R):
+        for r in range(R):  # the engine's registry (instance_open_range above)
             O.resource_create(r, abi.CC_RES_MAP)
-            O.instance_open(r, r, 1 + r, 1)
+            O.instance_open(r, r, 1 + rank + r, 1 + rank)
         tc = time.perf_counter()
-        O.apply(batch.slice(0, m))
+        s_ref, v_ref = O.apply(batch.slice(0, m))
         tc = time.perf_counter() - tc
-        cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
-               "sample": f"first {m:,} commits of the same c3 stream, C++ restatement of the Java apply path "
-                         f"(oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+                   "sample": f"first {m:,} commits of the same c3 stream (the parity sample), C++ restatement of the "
+                             f"Java apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
+        if not args.no_parity and gpu0 is not None:
+            s_gpu, v_gpu = gpu0
+            parity = {"rows": m, "mismatches": int(np.count_nonzero((s_gpu != s_ref) | (v_gpu != v_ref))),
+                      "unwritten": int(np.count_nonzero(s_gpu == RESULT_SENTINEL)),
+                      "checked": f"step 0: per-commit status+value of the first {m:,} rows (results prefilled with the "
+                                 f"0xFF sentinel status), GPU vs oracle/oracle.cpp"}
+        del O
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
@@ -762,11 +841,14 @@ def run_c3(args, dev, rank, world, dist):
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "parity": parity, "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if parity is not None and (parity["mismatches"] or parity["unwritten"]):
+        sys.stderr.write(f"PARITY FAILURE: {parity}\n")
+        sys.exit(3)
 
 
 def _free_port():
@@ -777,13 +859,36 @@ def _free_port():
     return p
 
 
+def count_gpus():
+    """GPUs this process may use, without any HIP / amdsmi call: the KFD topology nodes that have SIMDs
+    (/sys/class/kfd/kfd/topology/nodes/*/properties), narrowed by the *_VISIBLE_DEVICES lists the ROCm runtime honours."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0").strip() or 0) > 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if var in os.environ:
+            v = os.environ[var].strip()
+            n = min(n, len([x for x in v.split(",") if x.strip()]) if v else 0)
+    return n
+
+
 def launch_ranks(args):
     """`--gpus N` (N > 1) without WORLD_SIZE: start N ranks (torch.distributed.run, one process per GPU) as a child
     process, before anything touches a GPU, and return its exit code; None when this process is already a rank or
     runs alone."""
     if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
         return None
-    visible = torch.cuda.device_count()  # counts devices without initialising the GPU on this image
+    visible = count_gpus()  # no HIP call in the parent: the ranks are the first processes to touch a GPU
     if visible < args.gpus:
         sys.stderr.write(f"bench.py --gpus {args.gpus}: only {visible} GPU(s) visible on this node; "
                          f"one rank per GPU is required\n")
@@ -808,9 +913,12 @@ def main():
     ap.add_argument("--sub-batch", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=0, help="c3: 20M, c5: 10M (c2 uses step 0's rows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-parity", action="store_true", help="c2: skip the full-size oracle parity check of step 0")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the oracle parity check of step 0 (c2, c5: all rows; c3: the first --cpu-sample rows; "
+                         "c4: input set 0)")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--e2e", action="store_true", help="c2: also time one PCIe-inclusive step (pinned H2D + apply + D2H)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="c2: skip the PCIe-inclusive step (pinned H2D + apply + D2H) timed after the timed region")
     ap.add_argument("--hbm-budget-gb", type=float, default=200.0,
                     help="c2: HBM for resident per-step batches (more steps than fit replay the resident ones)")
     ap.add_argument("--c4-sets", type=int, default=6, help="c4: resident input sets used in turn (Infinity Cache)")

@@ -558,9 +558,15 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (ttl_seen) e->ttl_live = true;
-    if (e->has_mmaps) {  // every multimap Put of this batch may land in the leak log: room for n more
+    // The leak log (commits dropped without clean()) is drained before every batch of an engine that can add to it:
+    // every multimap put, and with value events every re-listen (AtomicValueState.listen :41-49) may land there, at
+    // most one entry per row, so the drained log gets room for n more; a coordination engine without value events
+    // adds entries only in the close fan-out (cc_sessions_close sizes the log for that itself) but is drained here
+    // too, so nothing accumulates across batches toward the log's end.
+    if (e->has_mmaps || e->coord_on) {
       int rc = drain_leaks(e);
-      if (!rc) rc = ensure_leak(e, n);
+      const bool may_leak = e->has_mmaps || (e->cfg.flags & CC_CFG_VALUE_EVENTS);
+      if (!rc && may_leak) rc = ensure_leak(e, n);
       if (rc) return rc;
     }
     if (nb > kBarCap)
@@ -956,6 +962,12 @@ extern "C" int cc_apply_batch_host(cc_engine* e, const cc_batch* h, uint64_t n, 
     rc = set_err(CC_ERR_HIP, "hipMalloc results");
     goto done;
   }
+  // sentinel prefill: status 0xFF is no legal status (tag nibble 15), so a row the kernels never wrote comes back
+  // as 0xFF instead of passing for a legal NULL result (status 0, value 0)
+  if (hipMemsetAsync(d_status, 0xFF, n, st) != hipSuccess || hipMemsetAsync(d_value, 0xA5, 8 * n, st) != hipSuccess) {
+    rc = set_err(CC_ERR_HIP, "result sentinel");
+    goto done;
+  }
   {
     cc_batch d{};
     d.index = (const uint64_t*)cols[0].dev;
@@ -1094,6 +1106,17 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   h32.insert(h32.end(), (size_t)m, 0u);
   h32.insert(h32.end(), pcl.begin(), pcl.end());
   h32.insert(h32.end(), (size_t)nc, m);
+  // every closed instance may drop one commit without clean() (a group member removed by close,
+  // MembershipGroupState.java:36-42; a value listener): the drained leak log gets room for m more
+  {
+    int rc2 = drain_leaks(e);
+    if (!rc2) rc2 = ensure_leak(e, m);
+    if (rc2) {
+      (void)hipFree(d32);
+      (void)hipFree(d_off);
+      return rc2;
+    }
+  }
   CloseArgs ca{};
   ca.cinst = d32;
   ca.m = m;
@@ -1557,6 +1580,12 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
   return CC_OK;
 }
 
+// Remaining bytes from p hold at least `count` records of `rec` bytes (no pointer arithmetic on the count: a corrupt
+// count cannot wrap the check).
+static bool snap_room(const uint8_t* p, const uint8_t* end, uint64_t count, uint64_t rec) {
+  return p <= end && count <= (uint64_t)(end - p) / rec;
+}
+
 extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t size) {
   if (!e || !h_buf || size < sizeof(SnapHdr)) return set_err(CC_ERR_INVALID, "snapshot too small");
   SnapHdr h;
@@ -1567,47 +1596,62 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
     return set_err(CC_ERR_INVALID, "snapshot configuration (max_resources/max_instances/map_capacity/coord_cap) differs");
   if (((h.flags & kSnapRetained) != 0) != (e->d_val_live != nullptr))  // the section lists would differ
     return set_err(CC_ERR_INVALID, "snapshot and engine differ in CC_CFG_VALUE_RETAINED");
+  if (e->coord_on && !(h.flags & 1u))  // the engine's coordination blocks have no section to come from
+    return set_err(CC_ERR_INVALID, "snapshot has no coordination state but the engine does");
+  const uint8_t* const base = (const uint8_t*)h_buf + sizeof h;
+  const uint8_t* const end = (const uint8_t*)h_buf + size;
+  // 1. validate the whole buffer before any engine state changes: a rejected snapshot leaves the engine as it was
+  std::vector<uint64_t> sizes;
+  for (const Section& x : snap_sections(e)) sizes.push_back(x.bytes);
+  if ((h.flags & 1u) && !e->coord_on) sizes.push_back(coord_block(e->coord_cap) * ((uint64_t)e->sb << kSbShift));
+  const uint8_t* p = base;
+  for (uint64_t want : sizes) {
+    uint64_t b = 0;
+    if (!snap_room(p, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+    memcpy(&b, p, 8);
+    p += 8;
+    if (b != want || !snap_room(p, end, b, 1)) return set_err(CC_ERR_INVALID, "snapshot section size mismatch");
+    p += b;
+  }
+  uint64_t ng = 0, ns = 0, nl = 0;
+  if (!snap_room(p, end, 2, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&ng, p, 8);
+  p += 16;
+  if (!snap_room(p, end, ng, sizeof(cc_engine::GroupTimer))) return set_err(CC_ERR_INVALID, "snapshot truncated (group timers)");
+  p += ng * sizeof(cc_engine::GroupTimer);
+  if (!snap_room(p, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&ns, p, 8);
+  p += 8;
+  if (!snap_room(p, end, ns, 24)) return set_err(CC_ERR_INVALID, "snapshot truncated (resource sessions)");
+  p += ns * 24;
+  if (!snap_room(p, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&nl, p, 8);
+  p += 8;
+  if (!snap_room(p, end, nl, 16)) return set_err(CC_ERR_INVALID, "snapshot truncated (leak lists)");
+  // 2. apply
   int rc = quiesce(e);
   if (rc) return rc;
   if ((h.flags & 1u) && (rc = ensure_ext(e, true))) return rc;
   e->ttl_live = (h.flags & 2u) != 0;
-  const uint8_t* p = (const uint8_t*)h_buf + sizeof h;
-  const uint8_t* end = (const uint8_t*)h_buf + size;
+  p = base;
   for (const Section& x : snap_sections(e)) {
-    uint64_t b = 0;
-    if (p + 8 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
-    memcpy(&b, p, 8);
     p += 8;
-    if (b != x.bytes || p + b > end) return set_err(CC_ERR_INVALID, "snapshot section size mismatch");
-    if (x.dev) HIPCHECK(hipMemcpy(x.dev, p, b, hipMemcpyHostToDevice));
-    else memcpy(x.host, p, b);
-    p += b;
+    if (x.dev) HIPCHECK(hipMemcpy(x.dev, p, x.bytes, hipMemcpyHostToDevice));
+    else memcpy(x.host, p, x.bytes);
+    p += x.bytes;
   }
-  uint64_t ng = 0;
-  if (p + 16 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
-  memcpy(&ng, p, 8);
   memcpy(&e->gtimer_seq, p + 8, 8);
   p += 16;
-  if (p + ng * sizeof(cc_engine::GroupTimer) > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
   e->gtimers.resize(ng);
   if (ng) memcpy(e->gtimers.data(), p, ng * sizeof(cc_engine::GroupTimer));
-  p += ng * sizeof(cc_engine::GroupTimer);
-  uint64_t ns = 0;
-  if (p + 8 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
-  memcpy(&ns, p, 8);
-  p += 8;
-  if (p + ns * 24 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  p += ng * sizeof(cc_engine::GroupTimer) + 8;
   e->res_sessions.clear();
   for (uint64_t i = 0; i < ns; ++i, p += 24) {
     uint64_t t[3];
     memcpy(t, p, 24);
     e->res_sessions[{(uint32_t)t[0], t[1]}] = t[2];
   }
-  uint64_t nl = 0;
-  if (p + 8 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
-  memcpy(&nl, p, 8);
   p += 8;
-  if (p + nl * 16 > end) return set_err(CC_ERR_INVALID, "snapshot truncated");
   e->leaks.clear();
   for (uint64_t i = 0; i < nl; ++i, p += 16) {
     uint64_t t[2];

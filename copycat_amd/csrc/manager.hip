@@ -76,6 +76,14 @@ int open_instance(cc_engine* e, uint32_t rslot, uint64_t index, uint64_t client,
   return CC_OK;
 }
 
+// open_instance for `index` will succeed: a free instance slot and an unused instance id.  Checked before a new key's
+// resource is registered, so a failed get / create leaves no keyed resource without an instance behind.
+int instance_room(cc_engine* e, uint64_t index) {
+  if (e->used_inst.lowest() < 0) return set_err(CC_ERR_CAPACITY, "no free instance slot (max_instances)");
+  if (e->inst_by_id.count(index)) return set_err(CC_ERR_INVALID, "instance id (commit index) already open");
+  return CC_OK;
+}
+
 // A new key: resource id = commit index, a fresh state machine of `type` (:84-100,155-176).
 int new_resource(cc_engine* e, uint64_t key, uint32_t type, uint64_t index, uint32_t* rslot) {
   if (type < CC_RES_VALUE || type > CC_RES_MULTIMAP) return set_err(CC_ERR_INVALID, "unknown resource type");
@@ -116,7 +124,7 @@ extern "C" int cc_get_resource(cc_engine* e, uint64_t key, uint32_t type, uint64
   auto kit = e->keys.find(key);
   if (kit == e->keys.end()) {  // :84-113
     uint32_t rs = 0;
-    if ((rc = new_resource(e, key, type, index, &rs))) return rc;
+    if ((rc = instance_room(e, index)) || (rc = new_resource(e, key, type, index, &rs))) return rc;
     if ((rc = open_instance(e, rs, index, client, instance_id, inst_slot))) return rc;
     e->res_sessions[{rs, client}] = index;
     return CC_OK;
@@ -148,7 +156,7 @@ extern "C" int cc_create_resource(cc_engine* e, uint64_t key, uint32_t type, uin
   uint32_t rs = 0;
   auto kit = e->keys.find(key);
   if (kit == e->keys.end()) {
-    if ((rc = new_resource(e, key, type, index, &rs))) return rc;
+    if ((rc = instance_room(e, index)) || (rc = new_resource(e, key, type, index, &rs))) return rc;
   } else if (!existing(e, kit->second, type, &rs)) {
     *status = CC_STATUS(CC_ST_TYPE_MISMATCH, CC_TAG_NULL);
     return CC_OK;

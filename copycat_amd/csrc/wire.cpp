@@ -382,7 +382,8 @@ extern "C" int cc_wire_lookup(cc_wire_interner* in, uint64_t handle, uint8_t* bu
 }
 
 extern "C" int cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* in, const uint8_t* buf,
-                              const uint64_t* offsets, uint64_t n, const cc_wire_out* out, uint64_t* bad_row) {
+                              uint64_t buf_len, const uint64_t* offsets, uint64_t n, const cc_wire_out* out,
+                              uint64_t* bad_row) {
   if (!in || !buf || !offsets || !out || !out->op || !out->flags || !out->key || !out->a || !out->b || !out->aux ||
       !out->kind || (e && !out->inst) || (!e && !out->iid))
     return set_err(CC_ERR_INVALID, "wire decode: null argument");
@@ -394,6 +395,10 @@ extern "C" int cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_
     if (offsets[i + 1] < offsets[i]) {
       if (bad_row) *bad_row = i;
       return set_err(CC_ERR_INVALID, "wire decode: offsets decrease");
+    }
+    if (offsets[i + 1] > buf_len) {  // never read past the caller's buffer
+      if (bad_row) *bad_row = i;
+      return set_err(CC_ERR_INVALID, "wire decode: entry ends past the buffer");
     }
     const int rc = decode_one(e, c, in, buf + offsets[i], buf + offsets[i + 1], i, out);
     if (rc) {

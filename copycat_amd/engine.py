@@ -24,6 +24,11 @@ SO_PATH = os.environ.get("CC_ENGINE_SO") or os.path.join(_HERE, "libcopycat_appl
 _LIB = None
 
 
+# Result prefill of the test / bench paths: status 0xFF has result tag nibble 15, which no commit can return
+# (tags 0..4), so a row the kernels never wrote is told apart from a legal NULL result (status 0, value 0).
+RESULT_SENTINEL = 0xFF
+
+
 class EngineError(RuntimeError):
     def __init__(self, rc, msg):
         super().__init__(f"cc error {rc}: {msg}")
@@ -84,7 +89,7 @@ def lib():
             "cc_wire_interner_destroy": (i32, [P]),
             "cc_wire_intern": (i32, [P, P, u64, P]),
             "cc_wire_lookup": (i32, [P, u64, P, u64, P]),
-            "cc_wire_decode": (i32, [P, P, P, P, P, u64, P, P]),
+            "cc_wire_decode": (i32, [P, P, P, P, u64, P, u64, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -262,14 +267,15 @@ class Engine:
                                         C.byref(closed)))
         return closed.value, evs.host()
 
-    def sessions_expire(self, bitmap, sessions, capacity=1 << 16, device="cuda"):
+    def sessions_expire(self, bitmap, sessions, capacity=1 << 16, device="cuda", events=None):
         """Close every client session whose bit is set in `bitmap` (a device u64 tensor, cc_expire_sweep's output),
-        in ascending id order; returns (instances closed, events)."""
-        evs = DeviceEvents(capacity, device=device)
+        in ascending id order; returns (instances closed, events).  With `events` (a DeviceEvents the caller keeps)
+        the close events stay in HBM and the second value is that DeviceEvents (no host copy)."""
+        evs = events if events is not None else DeviceEvents(capacity, device=device)
         ev = evs.struct()
         closed = C.c_uint64()
         _check(self.L.cc_sessions_expire(self.h, _dptr(bitmap), sessions, C.byref(ev), None, C.byref(closed)))
-        return closed.value, evs.host()
+        return closed.value, (evs if events is not None else evs.host())
 
     # ---- the hot path ----------------------------------------------------------------------------------
     def apply(self, db: DeviceBatch, status, value, stream=None):
@@ -292,6 +298,8 @@ class Engine:
         db = DeviceBatch.upload(b, device=device)
         status = torch.zeros(n, dtype=torch.uint8, device=device)
         value = torch.zeros(n, dtype=torch.int64, device=device)
+        status.fill_(RESULT_SENTINEL)  # a row no kernel writes stays 0xFF: never a legal status (see RESULT_SENTINEL)
+        value.fill_(-0x5A5A5A5A5A5A5A5B)
         evs = DeviceEvents(capacity if capacity is not None else max(4 * n, 1024), device=device)
         self.apply_events(db, status, value, evs)
         self.sync()

@@ -78,3 +78,11 @@ def allgather_expired(bitmap, device=None, group=None):
     dist.all_gather_into_tensor(out, t, group=group)
     words = out.view(world, -1).cpu().numpy().view(np.uint64)
     return np.bitwise_or.reduce(words, axis=0)
+
+
+def expired_sessions(bitmap, sessions):
+    """Session ids whose bit is set in an expired-session bitmap (u64 words, LSB first), ascending -- the order
+    cc_sessions_expire closes them in."""
+    words = np.ascontiguousarray(bitmap, np.uint64)
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:sessions]
+    return np.nonzero(bits)[0].tolist()

@@ -72,6 +72,8 @@ class WireDecoder:
         eh = self.engine.h if self.engine is not None else None
         buf = np.ascontiguousarray(buf, np.uint8)
         offsets = np.ascontiguousarray(offsets, np.uint64)
-        _check(lib().cc_wire_decode(eh, C.byref(self.codec), self.interner.h, _np(buf), _np(offsets), n,
+        if n and int(offsets[-1]) > buf.size:
+            raise ValueError(f"offsets end at {int(offsets[-1])} past the {buf.size}-byte buffer")
+        _check(lib().cc_wire_decode(eh, C.byref(self.codec), self.interner.h, _np(buf), buf.size, _np(offsets), n,
                                     C.byref(out), C.byref(bad)))
         return b, iid, kind

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CC_ABI_VERSION 2
+#define CC_ABI_VERSION 3
 
 /* ---- return codes ------------------------------------------------------------------------------ */
 #define CC_OK               0
@@ -457,10 +457,11 @@ typedef struct cc_wire_out {
   uint64_t* aux;
   uint8_t*  kind;
 } cc_wire_out;
-/* Entry i is buf[offsets[i], offsets[i+1]).  Fails (CC_ERR_INVALID, *bad_row = the entry) on a truncated or
+/* Entry i is buf[offsets[i], offsets[i+1]) of the buf_len-byte buffer (an entry that ends past buf_len fails with its
+ * row; ABI 3 added buf_len).  Fails (CC_ERR_INVALID, *bad_row = the entry) on a truncated or
  * over-long entry, an unknown operation, a null key, or a value that is neither null, Long, Integer, Boolean
  * nor String (user objects have no canonical tag); rows before *bad_row are decoded. */
-int  cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* in, const uint8_t* buf,
+int  cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* in, const uint8_t* buf, uint64_t buf_len,
                     const uint64_t* offsets, uint64_t n, const cc_wire_out* out, uint64_t* bad_row);
 
 #ifdef __cplusplus

@@ -176,3 +176,123 @@ def test_bench_gpus_flag_fails_fast_without_gpus():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=120, env=dict(os.environ, CUDA_VISIBLE_DEVICES=""))
     assert r.returncode == 2 and "GPU(s) visible" in r.stderr, (r.returncode, r.stderr[-400:])
+
+
+# ---- cross-shard session expiry: one client session owns instances on every rank ----------------------------------
+RX, KX, SX, NX = 96, 4, 40, 20_000  # coordination resources, instances per resource, client sessions, commits
+TYPES_X = np.resize(np.array([abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP], np.uint8), RX)
+
+
+def _client_of(slot):
+    """Owner session of instance slot r*KX + k: the KX instances of a resource belong to KX distinct sessions (a
+    client reaches a resource through one instance, ResourceManager.getResource :125-141), spread so that every
+    session owns instances on every rank."""
+    r, k = divmod(int(slot), KX)
+    return (r * 7 + k * 11) % SX
+
+
+def _expiry_last():
+    last = np.full(SX, 9_000, np.uint64)
+    last[np.arange(SX) % 3 == 1] = 1  # every third session is expired at now = 10_000, timeout = 5_000
+    return last
+
+
+def _open_x(O, rank=None, world=1):
+    for r in range(RX):
+        if rank is not None and shard.owner_of(r, world) != rank:
+            continue
+        O.resource_create(r, int(TYPES_X[r]))
+        for k in range(KX):
+            s = r * KX + k
+            O.instance_open(s, r, 1000 + s, _client_of(s))
+
+
+def _expire_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from copycat_amd.workload import coord_random_stream
+    from oracle.oracle_py import Oracle, expire_sweep
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = coord_random_stream(NX, TYPES_X, KX, RX * KX, seed=91)
+    own = shard.inst_owner_table(np.arange(RX * KX) // KX, world)
+    rows, part = shard.split_batch(b, own, world)[rank]
+    O = Oracle(RX, RX * KX)
+    _open_x(O, rank, world)
+    st, va = O.apply(part)
+    O.take_events()
+    O.take_aux()
+    # rank r sweeps the sessions s with s % world == r (the session's owner: it holds its keep-alives) ...
+    bm, _ = expire_sweep(_expiry_last(), now=10_000, timeout=5_000)
+    mine = np.zeros_like(bm)
+    for s in range(rank, SX, world):
+        mine[s // 64] |= bm[s // 64] & np.uint64(1 << (s % 64))
+    # ... and every rank closes the instances IT hosts of every expired session: the merged bitmap drives the fan-out
+    merged = shard.allgather_expired(mine)
+    expired = shard.expired_sessions(merged, SX)
+    for s in expired:
+        O.session_expire(s)
+    ev = O.take_events()
+    state = {}
+    for r in range(RX):
+        if shard.owner_of(r, world) == rank:
+            t = TYPES_X[r]
+            state[r] = (O.lock_state(r) if t == abi.CC_RES_LOCK else
+                        O.election_state(r) if t == abi.CC_RES_ELECTION else O.group_members(r))
+    np.savez(os.path.join(outdir, f"x_r{rank}.npz"), rows=rows, st=st, va=va, expired=np.array(expired),
+             state=np.array(repr(state)), **{f"ev_{k}": v for k, v in ev.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_session_expiry_fans_out_like_one_replica(tmp_path, oracle_lib):
+    """ResourceManager.expire (ResourceManager.java:237-247, close :250-264) for a client session that owns instances
+    on both ranks: the expired set is swept by the session's owner rank, OR-merged over the all-gather, and every rank
+    closes the instances it hosts.  The merged close events, regrouped per target session in emission order (A12),
+    and every resource's final state equal one replica expiring the same sessions."""
+    from copycat_amd.workload import coord_random_stream
+    from oracle.oracle_py import Oracle, expire_sweep
+
+    world, port = 2, _free_port()
+    mp.spawn(_expire_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    b = coord_random_stream(NX, TYPES_X, KX, RX * KX, seed=91)
+    O = Oracle(RX, RX * KX)
+    _open_x(O)
+    st1, va1 = O.apply(b)
+    O.take_events()
+    O.take_aux()
+    bm, _ = expire_sweep(_expiry_last(), now=10_000, timeout=5_000)
+    expired = shard.expired_sessions(bm, SX)
+    assert len(expired) == len(range(1, SX, 3))
+    for s in expired:
+        O.session_expire(s)
+    ev1 = O.take_events()
+    z = [np.load(tmp_path / f"x_r{r}.npz") for r in range(world)]
+    st, va = shard.merge_results(len(b), [(q["rows"], q["st"], q["va"]) for q in z])
+    assert np.array_equal(st, st1) and np.array_equal(va, va1)
+    for q in z:
+        assert q["expired"].tolist() == expired
+    keys = ("pos", "target", "code", "tag", "payload", "src")
+    merged = {k: np.concatenate([q[f"ev_{k}"] for q in z]) for k in keys}
+    assert len(merged["pos"]) == len(ev1["pos"]) > 0
+    assert np.all(merged["src"] == abi.CC_EVSRC_CLOSE)
+
+    def per_target(e):
+        o = np.argsort(e["target"], kind="stable")
+        return [np.asarray(e[k])[o] for k in keys]
+
+    for g, w in zip(per_target(merged), per_target(ev1)):
+        assert np.array_equal(g, w)
+    import ast
+
+    state = {}
+    for q in z:
+        state.update(ast.literal_eval(str(q["state"])))
+    for r in range(RX):
+        t = TYPES_X[r]
+        want = (O.lock_state(r) if t == abi.CC_RES_LOCK else
+                O.election_state(r) if t == abi.CC_RES_ELECTION else O.group_members(r))
+        assert state[r] == want, r

@@ -269,3 +269,20 @@ def test_manager_groups_coordination_types():
     assert E.resource_slot(iid) >> 6 != freed >> 6
     st, iid, _ = E.create_resource(5001, abi.CC_RES_LOCK, 7, 5001)
     assert E.resource_slot(iid) >> 6 == freed >> 6
+
+
+def test_manager_capacity_failure_registers_nothing():
+    """get / create of a NEW key when no instance slot is free fails with CC_ERR_CAPACITY and leaves no keyed resource
+    behind (a retry must not take the existing-key path a replica that never saw the failure would not take)."""
+    from copycat_amd.engine import Engine, EngineError
+
+    E = Engine(16, 2, 64)
+    st, iid, islot = E.get_resource(11, V, 1, 5)
+    assert abi.status_code(st) == abi.CC_ST_OK and iid == 5
+    st, iid, islot = E.create_resource(12, V, 1, 6)
+    assert abi.status_code(st) == abi.CC_ST_OK and iid == 6
+    for fn in (E.get_resource, E.create_resource):
+        with pytest.raises(EngineError) as ei:
+            fn(13, V, 1, 7)
+        assert ei.value.rc == abi.CC_ERR_CAPACITY
+        assert not E.resource_exists(13) and E.resource_slot(7) == -1

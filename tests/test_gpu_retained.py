@@ -253,3 +253,33 @@ def test_retained_map_parity():
         s2, v2 = O.apply(b.slice(lo, hi))
         assert np.array_equal(s, s2) and np.array_equal(v, v2)
         _retained_all(E, O, range(maps))
+
+
+def test_leak_log_drained_across_batches_without_multimaps():
+    """AtomicValueState.listen (AtomicValueState.java:41-49) replaces a session's listener with listeners.put and
+    never clean()s the replaced commit: it stays in the log for good (the engine's leak log, drained into the per-slot
+    retained lists).  More re-listens than the device log holds between drains (1,048,576) over several batches, on an
+    engine with value events and no multimaps, all apply, and every slot's retained commits equal the oracle's."""
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+
+    R, n, batches = 1024, 450_000, 3
+    flags = abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_EVENTS
+    E = Engine(R, R, n, flags=flags, max_events=4 * n)
+    O = Oracle(R, R, flags)
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E.instance_open_range(0, R, 0, 1000, 7)
+    for r in range(R):
+        O.resource_create(r, abi.CC_RES_VALUE)
+        O.instance_open(r, r, 1000 + r, 7)
+    for k in range(batches):
+        idx = np.arange(k * n + 1, (k + 1) * n + 1, dtype=np.uint64)
+        b = Batch.from_columns(index=idx, time=idx, inst=(idx % R).astype(np.uint32),
+                               op=np.full(n, abi.CC_OP_VALUE_LISTEN, np.uint8))
+        s, v, _ = E.apply_host_events(b)
+        s2, v2 = O.apply(b)
+        assert np.array_equal(s, s2) and np.array_equal(v, v2), k
+    assert batches * n - R > 1 << 20
+    for slot in list(range(0, R, 97)) + [R - 1]:
+        got, want = E.retained(slot), O.retained(slot, cap=1 << 12)
+        assert got == want and len(got) >= batches * n // R, slot

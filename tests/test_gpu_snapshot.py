@@ -93,3 +93,53 @@ def test_snapshot_rejects_other_configuration():
     assert ei.value.rc == abi.CC_ERR_INVALID
     with pytest.raises(EngineError):
         Engine(64, 64, 16).restore(snap[:100])
+
+
+def test_snapshot_corrupt_counts_rejected_before_any_state_changes():
+    """A snapshot whose trailing counts (group timers, resource sessions, leak lists) are corrupt -- huge values whose
+    byte size would wrap a pointer check -- or that is truncated anywhere is rejected with CC_ERR_INVALID, and the
+    engine keeps the state it had (the whole buffer is validated before anything is written)."""
+    import struct
+
+    from copycat_amd.engine import Engine, EngineError
+    from copycat_amd.workload import value_random_stream
+    from oracle.oracle_py import Oracle
+
+    R = 64
+    b = value_random_stream(3000, R, R + 8, seed=5)
+    E = Engine(R, R + 8, len(b))
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E.instance_open_range(0, R, 0, 1000, 7)
+    E.apply_host(b)
+    snap = bytearray(E.snapshot())
+    before = [x.copy() for x in E.value_state()]
+    # the trailer: ... ng(8) seq(8) [timers] ns(8) [24 B each] nl(8) [16 B each]; with no timers / sessions / leaks
+    # the last 32 bytes are ng, seq, ns, nl
+    F = Engine(R, R + 8, len(b))
+    F.resource_create_range(0, R, abi.CC_RES_VALUE)
+    F.instance_open_range(0, R, 0, 1000, 7)
+    F.apply_host(b.slice(0, 1000))
+    f_before = [x.copy() for x in F.value_state()]
+    for off in (32, 16, 8):  # ng, ns, nl
+        bad = bytearray(snap)
+        struct.pack_into("<Q", bad, len(bad) - off, (1 << 64) - 3)
+        with pytest.raises(EngineError) as ei:
+            F.restore(bytes(bad))
+        assert ei.value.rc == abi.CC_ERR_INVALID
+        for x, y in zip(F.value_state(), f_before):
+            assert np.array_equal(x, y)
+    for cut in (len(snap) - 1, len(snap) // 2, 200):
+        with pytest.raises(EngineError):
+            F.restore(bytes(snap[:cut]))
+        for x, y in zip(F.value_state(), f_before):
+            assert np.array_equal(x, y)
+    F.restore(bytes(snap))  # the intact snapshot still restores
+    for x, y in zip(F.value_state(), before):
+        assert np.array_equal(x, y)
+    O = Oracle(R, R + 8)
+    for r in range(R):
+        O.resource_create(r, abi.CC_RES_VALUE)
+        O.instance_open(r, r, 1000 + r, 7)
+    O.apply(b)
+    for x, y in zip(F.value_state(), O.value_state()):
+        assert np.array_equal(x, y)

@@ -166,3 +166,32 @@ def _carried(op):
         "GROUP_SCHEDULE": "key aux a", "GROUP_EXECUTE": "key a",
     }
     return set(table.get(op, "").split())
+
+
+def test_offsets_past_the_buffer_are_rejected():
+    """ABI 3: cc_wire_decode takes the buffer length and never reads past it; WireDecoder checks offsets[-1] first."""
+    import ctypes as C
+
+    from copycat_amd.engine import lib
+
+    meta, blob = _fixture()
+    offs = np.array(meta["offsets"], np.uint64)
+    d = _decoder()
+    with pytest.raises(ValueError):
+        d.decode(buf=blob[:-1], offsets=offs)
+    # the C check itself: a buffer length one short of the last entry's end fails with that entry's row
+    from copycat_amd.batch import Batch
+
+    n = len(offs) - 1
+    b = Batch(n)
+    iid = np.zeros(n, np.uint64)
+    kind = np.zeros(n, np.uint8)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    out = abi.cc_wire_out(inst=p(b.inst), iid=p(iid), op=p(b.op), flags=p(b.flags), key=p(b.key), a=p(b.a), b=p(b.b),
+                          aux=p(b.aux), kind=p(kind))
+    bad = C.c_uint64(0)
+    for s in meta["strings"]:
+        d.interner.intern(s)
+    rc = lib().cc_wire_decode(None, C.byref(d.codec), d.interner.h, p(blob), int(offs[-1]) - 1, p(offs), n,
+                              C.byref(out), C.byref(bad))
+    assert rc == abi.CC_ERR_INVALID and bad.value == n - 1
