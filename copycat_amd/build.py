@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 
-ENGINE_SRCS = ["engine.hip", "partition.hip", "partition_value.hip", "partition_ext.hip", "apply_value.hip", "apply_map.hip", "apply_map_hot.hip", "apply_coord.hip", "events.hip", "quorum.hip", "close.hip", "map_wide.hip", "live.hip", "manager.hip", "wire.cpp"]
+ENGINE_SRCS = ["engine.hip", "partition.hip", "partition_value.hip", "partition_ext.hip", "apply_value.hip", "value_path.hip", "apply_map.hip", "apply_map_hot.hip", "apply_coord.hip", "events.hip", "quorum.hip", "close.hip", "map_wide.hip", "live.hip", "manager.hip", "retained.hip", "wire.cpp"]
 ENGINE_HDRS = ["common.h", "engine_internal.h", "engine_state.h", "map_ops.h"]
 ENGINE_SO = os.path.join(HERE, "libcopycat_apply.so")
 WORKLOAD_SO = os.path.join(HERE, "libcopycat_workload.so")
@@ -36,8 +36,17 @@ def build_engine(force=False):
     deps = [os.path.join(CSRC, f) for f in ENGINE_SRCS + ENGINE_HDRS] + [os.path.join(ROOT, "include", "copycat_apply.h")]
     if force or _stale(ENGINE_SO, deps):
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-              *ENGINE_SRCS, "-o", ENGINE_SO])
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+        objdir = os.path.join(HERE, "build_obj")
+        os.makedirs(objdir, exist_ok=True)
+        objs = [os.path.join(objdir, os.path.splitext(f)[0] + ".o") for f in ENGINE_SRCS]
+        # one hipcc per translation unit, in parallel (every kernel is launched from the unit that defines it)
+        from concurrent.futures import ThreadPoolExecutor
+
+        jobs = max(1, min(len(ENGINE_SRCS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(lambda so: _run([hipcc, *flags, "-c", so[0], "-o", so[1]]), zip(ENGINE_SRCS, objs)))
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", ENGINE_SO])
     return ENGINE_SO
 
 

@@ -634,7 +634,9 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {
   static const bool v1 = getenv("CC_APPLY_V1") != nullptr;  // A/B: the phase-sequential walk
   a.mark(K_APPLY_VALUE, 1, st);
-  if (v1)
+  if (a.v3) {
+    if (launch_apply_value_v3(a, st)) return -1;
+  } else if (v1)
     hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kVT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.sb_kind,
                        a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy, a.err);
   else

@@ -188,6 +188,8 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   sub = std::min<uint64_t>(sub, (uint64_t)kMaxTiles * kTile);
   e->sub_batch = sub;
   e->max_tiles = sub / kTile;
+  e->value_v2 = getenv("CC_VALUE_V2") != nullptr;
+  e->v3_scatter = getenv("CC_V3_SCATTER") != nullptr;
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
   e->res_type.assign(slots, CC_RES_NONE);
   e->inst_res.assign(cfg->max_instances, kNoRes);
@@ -705,6 +707,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.dummy = e->sub_batch;
     pa.inst_res16 = e->d_inst_res16;
     pa.res16 = e->ext ? nullptr : e->d_res16;
+    const bool v3 = !e->ext && !e->value_v2;  // value-only engines: value_path.hip
+    pa.v3 = v3;
+    pa.v3_scatter = v3 && e->v3_scatter;
+    pa.out_status = out->status;
+    pa.out_value = out->value;
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
     if (e->map_bits && e->ttl_live && launch_map_rows(e->d_cpos, lo, hi, e->d_map_row, st))
@@ -713,7 +720,13 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.st_meta = e->d_st_meta;
     va.st_ab = e->d_st_ab;
     va.ttab = e->d_ttab;
-    va.tiles = tiles;
+    va.tiles = v3 ? (uint32_t)((hi - lo + kV3Tile - 1) / kV3Tile) : tiles;
+    va.v3 = v3;
+    va.v3_scatter = v3 && e->v3_scatter;
+    va.out_status = out->status;
+    va.out_value = out->value;
+    va.cb = c->b;
+    va.lo = lo;
     va.sb = e->sb_total();
     va.sb_val = e->sb;
     va.sb_kind = e->d_sb_kind;
@@ -795,8 +808,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.out_value = out->value;
     ua.dummy_status = e->d_rst_status + e->sub_batch;
     ua.dummy_value = e->d_rst_value + e->sub_batch;
+    ua.v3 = v3;
     ua.mark = marker_of(e);
-    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
+    if (!(v3 && e->v3_scatter) && launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
     if (e->coord_on) {
       EventArgs ea{};
       ea.cpos = e->d_cpos;
@@ -1414,6 +1428,60 @@ extern "C" int cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint6
   std::sort(v.begin(), v.end());
   *count = v.size();
   for (uint64_t i = 0; i < v.size() && i < cap; ++i) h_index[i] = v[i];
+  return CC_OK;
+}
+
+// Every slot's retained commits at once (the union of cc_read_retained over all resource slots) as a bitmap over
+// [first, first + count), built on the device (retained.hip); the compactor's per-batch feed.
+extern "C" int cc_retained_bitmap(cc_engine* e, uint64_t first, uint64_t count, uint64_t* d_bitmap, uint64_t* h_count) {
+  if (!e || (count && !d_bitmap) || ((uintptr_t)d_bitmap & 7)) return set_err(CC_ERR_INVALID, "null or misaligned bitmap");
+  if (count == 0) {
+    if (h_count) *h_count = 0;
+    return CC_OK;
+  }
+  const uint64_t slots = (uint64_t)e->sb << kSbShift;
+  bool values = false;
+  for (uint32_t s = 0; s < e->cfg.max_resources; ++s) values |= e->res_type[s] == CC_RES_VALUE;
+  if (values && !e->d_val_live) return set_err(CC_ERR_INVALID, "engine created without CC_CFG_VALUE_RETAINED");
+  int rc = quiesce(e);
+  if (rc) return rc;
+  if ((rc = drain_leaks(e))) return rc;
+  std::vector<uint64_t> host;  // pending MembershipGroup.schedule commits + commits dropped without clean()
+  for (const auto& g : e->gtimers)
+    if (g.idx >= first && g.idx - first < count) host.push_back(g.idx);
+  for (const auto& kv : e->leaks)
+    for (uint64_t i : kv.second)
+      if (i >= first && i - first < count) host.push_back(i);
+  uint64_t* d_list = nullptr;
+  unsigned long long* d_total = nullptr;
+  HIPCHECK(hipMalloc(&d_total, sizeof(unsigned long long) * (1 + host.size())));
+  d_list = reinterpret_cast<uint64_t*>(d_total + 1);
+  hipError_t x = host.empty() ? hipSuccess
+                              : hipMemcpyAsync(d_list, host.data(), 8 * host.size(), hipMemcpyHostToDevice, e->own_stream);
+  RetainedArgs ra{};
+  ra.res_type = e->d_res_type;
+  ra.slots = (uint32_t)std::min<uint64_t>(slots, e->cfg.max_resources);
+  ra.val_live = values ? e->d_val_live : nullptr;
+  ra.tbl_word = e->map_bits ? e->d_tbl_word : nullptr;
+  ra.tbl_ci = e->d_tbl_ci;
+  ra.tbl_dl = e->ttl_live ? e->d_tbl_dl : nullptr;
+  ra.entries = e->map_entries;
+  ra.coord = e->coord_on ? e->d_coord : nullptr;
+  ra.coord_cap = e->coord_cap;
+  ra.clock = e->d_clock;
+  ra.list = d_list;
+  ra.list_n = host.size();
+  ra.first = first;
+  ra.count = count;
+  ra.bitmap = d_bitmap;
+  ra.total = d_total;
+  if (x == hipSuccess && launch_retained(ra, e->own_stream)) x = hipGetLastError();
+  unsigned long long total = 0;
+  if (x == hipSuccess) x = hipMemcpyAsync(&total, d_total, sizeof total, hipMemcpyDeviceToHost, e->own_stream);
+  if (x == hipSuccess) x = hipStreamSynchronize(e->own_stream);
+  (void)hipFree(d_total);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "retained bitmap", x);
+  if (h_count) *h_count = total;
   return CC_OK;
 }
 

@@ -51,6 +51,10 @@ struct PartArgs {
   uint64_t dummy;     // first of the kPT dummy staging rows after the staging area (= sub_batch)
   uint16_t* inst_res16;  // value-only engines, < 65535 resources, <= 65536 instances: u16 copy of inst_res
   uint16_t* res16;       // ... and the resolved resource of every commit of the sub-batch (null: not this path)
+  bool v3;               // value-only pipeline of value_path.hip (8192-commit tiles, 16-byte records in st_ab)
+  bool v3_scatter;       //   ... results written straight to log order by the apply (no cpos / unpermute)
+  uint8_t* out_status;   //   ... the caller's result columns (whole batch; unknown-session rows)
+  uint64_t* out_value;
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
@@ -58,6 +62,7 @@ int launch_tile_hist16(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_value(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_v2(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st);
+int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st);
 size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk);
 
 struct ValueArgs {
@@ -74,9 +79,16 @@ struct ValueArgs {
   uint64_t* rst_value;
   uint64_t dummy;        // first of the dummy result rows after the staging area (= sub_batch)
   uint32_t* err;
+  bool v3;               // value_path.hip: 16-byte records, 8192-commit tiles
+  bool v3_scatter;       //   results straight to out_status / out_value at their log rows
+  const uint64_t* cb;    //   the batch's b column (escaped CAS updates) and the sub-batch's first row
+  uint64_t lo;
+  uint8_t* out_status;
+  uint64_t* out_value;
   Marker mark;
 };
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
+int launch_apply_value_v3(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct MapArgs {
@@ -303,8 +315,30 @@ struct UnpermuteArgs {
   uint64_t* out_value;
   uint8_t* dummy_status;  // 4 x kPT dummy result rows (after the staging area) for unconditional stores
   uint64_t* dummy_value;
+  bool v3;                // value_path.hip tiles (8192 commits)
   Marker mark;
 };
 int launch_unpermute(const UnpermuteArgs& a, hipStream_t st);
+
+// The bulk compaction view (retained.hip, cc_retained_bitmap): bit (i - first) of bitmap set iff log index i is held
+// by a state machine without clean().
+struct RetainedArgs {
+  const uint8_t* res_type;
+  uint32_t slots;
+  const uint64_t* val_live;  // null: no value resources
+  const uint32_t* tbl_word;  // null: no maps / sets
+  const uint64_t* tbl_ci;
+  const uint64_t* tbl_dl;    // null: no map timers
+  uint64_t entries;
+  const uint8_t* coord;      // null: no coordination blocks
+  uint32_t coord_cap;
+  const uint64_t* clock;
+  const uint64_t* list;      // host-known indices (pending schedules, leak lists), uploaded
+  uint64_t list_n;
+  uint64_t first, count;
+  uint64_t* bitmap;          // ceil(count / 64) words
+  unsigned long long* total; // null or: the retained indices in the range (popcount)
+};
+int launch_retained(const RetainedArgs& a, hipStream_t st);
 
 }  // namespace cc

@@ -452,33 +452,35 @@ __global__ __launch_bounds__(kPT, CC_PART_WPE) void k_part_tile(const uint32_t* 
 // Persistent over tiles (tile T = blockIdx.x + k * gridDim.x): the tile's staged results (contiguous, tile-local)
 // are in LDS while they are written back in log order through cpos; the NEXT tile's results and cpos are loaded
 // into registers (16-byte loads) during that scatter and moved to LDS at the top of the next iteration.
-constexpr int kUnVal = kTile / (2 * kPT);  // u64x2 value loads per thread per tile (8)
-constexpr int kUnPos = kTile / (4 * kPT);  // 4-commit cpos groups per thread per tile (4)
-__global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ cpos, uint32_t tiles, uint64_t n,
+// NT threads per workgroup, TL commits per tile: (1024, 16384) for the shared pipeline, (512, 8192) for value_path.hip.
+template <int NT, int TL>
+__global__ __launch_bounds__(NT) void k_unpermute(const uint16_t* __restrict__ cpos, uint32_t tiles, uint64_t n,
                                                 const uint8_t* __restrict__ rst_status,
                                                 const uint64_t* __restrict__ rst_value, uint8_t* __restrict__ out_status,
                                                 uint64_t* __restrict__ out_value, uint8_t* __restrict__ dummy_status,
                                                 uint64_t* __restrict__ dummy_value) {
-  __shared__ uint4 lv2[kTile / 2];
-  __shared__ uint4 ls4[kTile / 16];
+  constexpr int kUnVal = TL / (2 * NT);  // u64x2 value loads per thread per tile (8)
+  constexpr int kUnPos = TL / (4 * NT);  // 4-commit cpos groups per thread per tile (4)
+  __shared__ uint4 lv2[TL / 2];
+  __shared__ uint4 ls4[TL / 16];
   PH_DECL
   const uint64_t* lv = reinterpret_cast<const uint64_t*>(lv2);
   const uint8_t* ls = reinterpret_cast<const uint8_t*>(ls4);
   const uint32_t t = threadIdx.x;
   // Prefetch registers as named scalars (an array here is kept in scratch by the compiler, which would make
-  // every prefetch wait).  Staging buffers hold whole tiles (the sub-batch is a multiple of kTile): full-tile
+  // every prefetch wait).  Staging buffers hold whole tiles (the sub-batch is a multiple of TL): full-tile
   // loads stay in bounds; the prefetch is unconditional (the last tile is re-read).
   static_assert(kUnVal == 8 && kUnPos == 4, "unpermute prefetch registers");
   uint4 rs, v0, v1, v2, v3, v4, v5, v6, v7;
   uint2 p0, p1, p2, p3;
   auto load = [&](uint32_t TT) {
-    const uint64_t i0 = (uint64_t)TT * kTile;
+    const uint64_t i0 = (uint64_t)TT * TL;
     const uint4* sv = reinterpret_cast<const uint4*>(rst_value + i0) + t;
     const uint2* sp = reinterpret_cast<const uint2*>(cpos + i0) + t;
     rs = reinterpret_cast<const uint4*>(rst_status + i0)[t];
-    v0 = sv[0 * kPT]; v1 = sv[1 * kPT]; v2 = sv[2 * kPT]; v3 = sv[3 * kPT];
-    v4 = sv[4 * kPT]; v5 = sv[5 * kPT]; v6 = sv[6 * kPT]; v7 = sv[7 * kPT];
-    p0 = sp[0 * kPT]; p1 = sp[1 * kPT]; p2 = sp[2 * kPT]; p3 = sp[3 * kPT];
+    v0 = sv[0 * NT]; v1 = sv[1 * NT]; v2 = sv[2 * NT]; v3 = sv[3 * NT];
+    v4 = sv[4 * NT]; v5 = sv[5 * NT]; v6 = sv[6 * NT]; v7 = sv[7 * NT];
+    p0 = sp[0 * NT]; p1 = sp[1 * NT]; p2 = sp[2 * NT]; p3 = sp[3 * NT];
   };
   uint32_t T = blockIdx.x;
   load(T < tiles ? T : tiles - 1);
@@ -488,18 +490,18 @@ __global__ __launch_bounds__(kPT) void k_unpermute(const uint16_t* __restrict__ 
   for (; T < tiles; T += gridDim.x) {
     lds_barrier();  // the previous tile's scatter is done reading LDS
     ls4[t] = rs;
-    lv2[t + 0 * kPT] = v0; lv2[t + 1 * kPT] = v1; lv2[t + 2 * kPT] = v2; lv2[t + 3 * kPT] = v3;
-    lv2[t + 4 * kPT] = v4; lv2[t + 5 * kPT] = v5; lv2[t + 6 * kPT] = v6; lv2[t + 7 * kPT] = v7;
+    lv2[t + 0 * NT] = v0; lv2[t + 1 * NT] = v1; lv2[t + 2 * NT] = v2; lv2[t + 3 * NT] = v3;
+    lv2[t + 4 * NT] = v4; lv2[t + 5 * NT] = v5; lv2[t + 6 * NT] = v6; lv2[t + 7 * NT] = v7;
     const uint2 pp[kUnPos] = {p0, p1, p2, p3};
     lds_barrier();
     PH(0);
     load(T + gridDim.x < tiles ? T + gridDim.x : tiles - 1);
-    const uint64_t i0 = (uint64_t)T * kTile;
+    const uint64_t i0 = (uint64_t)T * TL;
     // 4-commit groups wholly inside the batch go to the outputs; the others to the dummy rows (unconditional
     // stores: see k_part_value), and the one group that straddles the batch end is written after the loop
 #pragma unroll
     for (int k = 0; k < kUnPos; ++k) {
-      const uint64_t i = i0 + 4 * (uint64_t)(t + k * kPT);  // commits i .. i+3
+      const uint64_t i = i0 + 4 * (uint64_t)(t + k * NT);  // commits i .. i+3
       const uint32_t p[4] = {pp[k].x & 0xFFFF, pp[k].x >> 16, pp[k].y & 0xFFFF, pp[k].y >> 16};
       uint32_t sw = 0;
       uint64_t v[4];
@@ -565,6 +567,11 @@ int launch_partition(const PartArgs& a, hipStream_t st) {
   if (tiles == 0) return 0;
   const bool ext = a.ext;
   a.mark(K_PART_TILE, 1, st);
+  if (!ext && a.v3) {  // value_path.hip: 8192-commit tiles
+    const int rc = launch_part_v3(a, (uint32_t)((a.hi - a.lo + kV3Tile - 1) / kV3Tile), st);
+    a.mark(K_PART_TILE, 0, st);
+    return rc;
+  }
   static const bool part_value = getenv("CC_PART_VALUE") != nullptr;  // experiment: persistent value partition
   static const bool part_tile_v1 = getenv("CC_PART_V1") != nullptr;   // A/B: the previous value partition
   if (!ext && part_value) {  // tile histograms, then the persistent value partition (partition_value.hip)
@@ -592,9 +599,16 @@ int launch_unpermute(const UnpermuteArgs& a, hipStream_t st) {
   const uint64_t tiles = (n + kTile - 1) / kTile;
   if (tiles == 0) return 0;
   a.mark(K_UNPERMUTE, 1, st);
-  const uint32_t grid = (uint32_t)(tiles < kPersistGrid ? tiles : kPersistGrid);
-  hipLaunchKernelGGL(k_unpermute, dim3(grid), dim3(kPT), 0, st, a.cpos, (uint32_t)tiles, n, a.rst_status, a.rst_value,
-                     a.out_status + a.lo, a.out_value + a.lo, a.dummy_status, a.dummy_value);
+  if (a.v3) {  // value_path.hip tiles: two 512-thread workgroups per CU
+    const uint64_t t3 = (n + kV3Tile - 1) / kV3Tile;
+    const uint32_t grid = (uint32_t)(t3 < 2 * kPersistGrid ? t3 : 2 * kPersistGrid);
+    hipLaunchKernelGGL((k_unpermute<512, kV3Tile>), dim3(grid), dim3(512), 0, st, a.cpos, (uint32_t)t3, n, a.rst_status,
+                       a.rst_value, a.out_status + a.lo, a.out_value + a.lo, a.dummy_status, a.dummy_value);
+  } else {
+    const uint32_t grid = (uint32_t)(tiles < kPersistGrid ? tiles : kPersistGrid);
+    hipLaunchKernelGGL((k_unpermute<kPT, kTile>), dim3(grid), dim3(kPT), 0, st, a.cpos, (uint32_t)tiles, n, a.rst_status,
+                       a.rst_value, a.out_status + a.lo, a.out_value + a.lo, a.dummy_status, a.dummy_value);
+  }
   a.mark(K_UNPERMUTE, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1,0 +1,646 @@
+// value_path.hip — the value-only engine pipeline (the c2 headline): k_part_v3 -> k_apply_value_v3 -> k_unpermute_v3.
+//
+// Same algorithm as partition_value.hip k_part_v2 + apply_value.hip k_apply_value_ws + partition.hip k_unpermute
+// (a stable group-by of the sub-batch by super-bucket = 256 AtomicValueState slots, then one walk per slot in log
+// order, then the results back to log order), with two changes aimed at HBM bytes and CU occupancy:
+//
+//  * one 16-byte staging record per commit instead of a 4-byte meta word + a 16-byte operand pair (20 B): the meta
+//    (slot, op class, the two value tags) shares the second word with the CAS update stored as a 46-bit difference
+//    from the expected value (a DistributedAtomicLong CAS loop updates by a small delta, DistributedAtomicLong.java
+//    :117-146).  A CAS whose difference does not fit keeps its row in the tile instead and the apply reads its update
+//    from the batch's b column (exact for every input; only the bytes moved differ);
+//  * 8192-commit tiles partitioned by 512-thread workgroups (two per CU: one workgroup's per-tile prologue -- the
+//    instance loads and the instance -> resource gathers -- overlaps the other's chunk loop) and unpermuted by
+//    512-thread workgroups.
+//
+// Reference semantics are AtomicValueState's (atomic/src/main/java/io/atomix/atomic/state/AtomicValueState.java):
+// get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144, delete :146-157; dispatch and unknown
+// sessions ResourceManager.operateResource :56-72 (UNKNOWN_SESSION rows are answered by the unpermute).
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+constexpr int kV3T = 512;                 // partition / unpermute workgroup threads
+constexpr int kV3W = kV3T / kWave;        // 8 waves
+constexpr int kV3J = 4;                   // commits per thread per chunk
+constexpr int kV3C = kV3J * kV3T;         // 2048 commits per chunk
+constexpr int kV3N = kV3Tile / kV3C;      // 4 chunks per tile
+static_assert(kV3N == 4, "k_part_v3 keeps 4 chunks x 4 commits per thread in registers");
+
+// ---- the 16-byte value record -------------------------------------------------------------------------------
+// w0 = the payload the op carries (CAS: canonical expected value; set / getAndSet: canonical new value; else 0)
+// w1 = meta (18 bits) | row (13 bits) << 18 | delta (33 bits) << 31
+//   meta: slot-in-super-bucket 0..7 | class 8..10 | compare tag 11..13 | new tag 14..16 | escaped 17
+//   row: the commit's row in its 8192-commit tile (results written straight to log order; escaped updates)
+//   delta (CAS): update - expected, two's complement; escaped (does not fit): the update is read from the b column
+enum : uint32_t { kC3Get = 0, kC3Set = 1, kC3Cas = 2, kC3Gas = 3, kC3Del = 4, kC3Lis = 5, kC3Unk = 6 };
+constexpr int kV3DeltaBits = 33;
+static_assert(kV3Tile <= (1 << 13), "the record's row field");
+
+// (The row, < 8192, is ORed into bits 18..30 of w1 where the partition places the record: v3_set_row.  Keeping it
+// out of the encode keeps k_part_v3 within 128 VGPRs.)
+__device__ inline uint4 v3_encode(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t slot) {
+  const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
+  const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
+  uint32_t cls = kC3Unk, ct = 0, nt = 0, esc = 0;
+  uint64_t w0 = 0, hi = 0;
+  if (op == CC_OP_VALUE_GET) {
+    cls = kC3Get;
+  } else if (op == CC_OP_VALUE_SET || op == CC_OP_VALUE_GETANDSET) {
+    cls = op == CC_OP_VALUE_SET ? kC3Set : kC3Gas;
+    nt = ta;
+    w0 = pa;
+  } else if (op == CC_OP_VALUE_CAS) {
+    cls = kC3Cas;
+    ct = ta;
+    nt = tb;
+    w0 = pa;
+    const uint64_t d = pb - pa;  // fits iff sign-extending its low 33 bits gives it back
+    esc = (uint64_t)(((int64_t)(d << (64 - kV3DeltaBits))) >> (64 - kV3DeltaBits)) == d ? 0u : 1u;
+    hi = esc ? 0ull : d;  // hi << 31 below keeps the low 33 bits
+  } else if (op == CC_OP_DELETE) {
+    cls = kC3Del;
+  } else if (op == CC_OP_VALUE_LISTEN || op == CC_OP_VALUE_UNLISTEN) {
+    cls = kC3Lis;
+  }
+  const uint64_t w1 = (uint64_t)(slot | (cls << 8) | (ct << 11) | (nt << 14) | (esc << 17)) | (hi << 31);
+  return make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+}
+__device__ inline uint32_t v3_slot(const uint4& r) { return r.z & 0xFFu; }
+__device__ inline uint4 v3_set_row(uint4 r, uint32_t row) {
+  r.z |= row << 18;
+  return r;
+}
+__device__ inline uint32_t v3_row(const uint4& r) { return (r.z >> 18) & (kV3Tile - 1); }
+
+// The record -> value_walk's form (common.h value_encode: meta word, canonical compare value x, canonical new
+// value y).  tile_row0 = the batch row of the record's tile start (escaped CAS updates are read from cb there).
+__device__ inline void v3_decode(const uint4& r, const uint64_t* __restrict__ cb, uint64_t tile_row0, uint32_t& m,
+                                 uint64_t& x, uint64_t& y) {
+  const uint32_t lo = r.z;
+  const uint32_t slot = lo & 0xFFu, cls = (lo >> 8) & 7u, ct = (lo >> 11) & 7u, nt = (lo >> 14) & 7u;
+  const uint64_t w0 = (uint64_t)r.x | ((uint64_t)r.y << 32);
+  const uint64_t w1 = (uint64_t)r.z | ((uint64_t)r.w << 32);
+  // class -> the walk's op bits (value_encode): get R, set W, CAS C + status OK|BOOL, getAndSet W|R, delete D,
+  // listen / unlisten L (not applied here: flagged), anything else the precomputed UNKNOWN_OP status
+  uint32_t bits = CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
+  bits = cls == kC3Get ? kVrR : bits;
+  bits = cls == kC3Set ? kVrW : bits;
+  bits = cls == kC3Cas ? (kVrC | CC_STATUS(CC_ST_OK, CC_TAG_BOOL)) : bits;
+  bits = cls == kC3Gas ? (kVrW | kVrR) : bits;
+  bits = cls == kC3Del ? kVrD : bits;
+  bits = cls == kC3Lis ? kVrL : bits;
+  m = bits | (nt << 13) | (slot << 16) | (ct << 24);
+  const bool cas = cls == kC3Cas;
+  x = cas ? w0 : 0;
+  y = (cls == kC3Set || cls == kC3Gas) ? w0 : 0;
+  if (cas) {
+    if ((lo >> 17) & 1u) y = nt ? cb[tile_row0 + ((lo >> 18) & (kV3Tile - 1))] : 0;  // escaped: from the b column
+    else y = w0 + (uint64_t)((int64_t)w1 >> 31);
+  }
+}
+
+// ---- k_part_v3: one 512-thread workgroup per 8192-commit tile -----------------------------------------------
+// As k_part_v2 (partition_value.hip): every thread loads the instance column of its 16 tile commits and chunk 0's raw
+// columns before anything waits, resolves the 16 instances with one batch of gathers, builds the tile histogram from
+// those registers and writes the tile's run starts (ttab row); then 4 chunks of 2048 commits: encode + rank inside
+// each wave (LDS atomics with return: same-address lanes of one instruction resolve in lane order, checked at engine
+// start), one wave takes the per-wave prefixes and chunk-sorted run starts, records are placed in LDS in sorted
+// order and written out run by run (contiguous 16-byte stores).  The input columns are read once: non-temporal loads.
+// SCATTER: the apply writes every result straight to its log row (no cpos, no unpermute); the partition answers the
+// unknown-session rows itself.
+template <int KP, bool SCATTER>
+__global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                    const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
+                                                    const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
+                                                    const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
+                                                    uint4* __restrict__ st_rec, uint16_t* __restrict__ cpos,
+                                                    uint16_t* __restrict__ ttab, uint8_t* __restrict__ out_status,
+                                                    uint64_t* __restrict__ out_value) {
+  __shared__ uint4 rab[kV3C];                  // the chunk in sorted order
+  __shared__ uint16_t rsb[kV3C];               //   super-bucket
+  __shared__ uint32_t wc[kV3W][kMaxSb / 2];    // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
+  __shared__ uint32_t hist[kMaxSb / 2];        // tile histogram (packed u16 pairs)
+  __shared__ uint16_t tpos[kMaxSb];            // tile-local position of run k's next piece
+  __shared__ uint16_t kst[kMaxSb];             // chunk-sorted start of run k
+  __shared__ uint32_t nlive_s;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint32_t hw = (sb + 1) / 2;
+  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kV3Tile;
+  const uint32_t tbase = blockIdx.x * kV3Tile;  // staging region of this tile (relative to lo)
+  for (uint32_t k = t; k < hw; k += kV3T) hist[k] = 0;
+  for (uint32_t k = t; k < (uint32_t)(kV3W * (kMaxSb / 2)); k += kV3T) (&wc[0][0])[k] = 0;
+  // commit (c, w, j, l) of the tile: row c*2048 + w*256 + j*64 + l (log order)
+  auto trow = [&](int c, int j) -> uint32_t { return (uint32_t)c * kV3C + w * (kWave * kV3J) + (uint32_t)j * kWave + l; };
+  const uint32_t nrow = (uint32_t)(hi - tile0 < (uint64_t)kV3Tile ? hi - tile0 : (uint64_t)kV3Tile);  // rows of this tile
+  uint32_t r[kV3N][kV3J];
+#pragma unroll
+  for (int c = 0; c < kV3N; ++c)
+#pragma unroll
+    for (int j = 0; j < kV3J; ++j) {
+      const uint32_t q = trow(c, j);
+      r[c][j] = q < nrow ? __builtin_nontemporal_load(inst + tile0 + q) : kNoRes;
+    }
+  uint8_t ob[kV3J], fb[kV3J];
+  uint64_t av[kV3J], bv[kV3J];
+  auto load_raw = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < kV3J; ++j) {
+      const uint32_t q = trow(c, j);
+      const uint64_t ic = q < nrow ? tile0 + q : lo;
+      ob[j] = __builtin_nontemporal_load(op + ic);
+      fb[j] = __builtin_nontemporal_load(flags + ic);
+      av[j] = __builtin_nontemporal_load(ca + ic);
+      bv[j] = __builtin_nontemporal_load(cb + ic);
+    }
+  };
+  load_raw(0);
+#pragma unroll
+  for (int c = 0; c < kV3N; ++c)
+#pragma unroll
+    for (int j = 0; j < kV3J; ++j) r[c][j] = r[c][j] < max_inst ? inst_res[r[c][j]] : kNoRes;
+  lds_barrier();  // hist / wc zeroed
+#pragma unroll
+  for (int c = 0; c < kV3N; ++c)
+#pragma unroll
+    for (int j = 0; j < kV3J; ++j)
+      if (r[c][j] != kNoRes) {
+        const uint32_t k = r[c][j] >> kSbShift;
+        atomicAdd(&hist[k >> 1], 1u << (16 * (k & 1)));
+      }
+  lds_barrier();
+  if (w == 0) {  // tile-local run starts: one wave, lane l owns super-buckets [l*KP, l*KP + KP)
+    uint32_t cnt[KP], mine = 0;
+#pragma unroll
+    for (int e = 0; e < KP; ++e) {
+      const uint32_t k = l * KP + e;
+      cnt[e] = k < sb ? (hist[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : 0u;
+      mine += cnt[e];
+    }
+    uint32_t inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    uint32_t run = inc - mine;
+    uint16_t* row = ttab + (uint64_t)blockIdx.x * (sb + 1);
+#pragma unroll
+    for (int e = 0; e < KP; ++e) {
+      const uint32_t k = l * KP + e;
+      if (k < sb) {
+        tpos[k] = (uint16_t)run;
+        row[k] = (uint16_t)run;
+      }
+      run += cnt[e];
+    }
+    if (l == 63) row[sb] = (uint16_t)inc;  // live commits of the tile (<= 8192)
+  }
+  // (tpos is first read after the next barrier; wave 0 wrote it before its first chunk barrier)
+#pragma unroll
+  for (int c = 0; c < kV3N; ++c) {
+    // encode and rank this chunk's records (registers: loaded one chunk ahead); then the next chunk's loads
+    uint32_t sk[kV3J], loc[kV3J];
+    uint4 rec[kV3J];
+#pragma unroll
+    for (int j = 0; j < kV3J; ++j) {
+      const bool live = r[c][j] != kNoRes;
+      rec[j] = v3_encode(ob[j], fb[j], av[j], bv[j], r[c][j] & ((1u << kSbShift) - 1));
+      sk[j] = live ? (r[c][j] >> kSbShift) : 0u;
+      const uint32_t sh = 16 * (sk[j] & 1);
+      loc[j] = live ? (atomicAdd(&wc[w][sk[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
+    }
+    if (c + 1 < kV3N) load_raw(c + 1);
+    lds_barrier();  // B1: the chunk's counters are complete
+    if (w == 0) {  // per super-bucket: exclusive prefix over the waves (in place), chunk totals, chunk-sorted starts
+      uint32_t tot[KP];
+#pragma unroll
+      for (int e = 0; e < KP; e += 2) {
+        const uint32_t pr = (l * KP + e) / 2;
+        uint32_t acc = 0;
+        if (pr < hw) {
+#pragma unroll
+          for (int q = 0; q < kV3W; ++q) {
+            const uint32_t x = wc[q][pr];
+            wc[q][pr] = acc;
+            acc += x;
+          }
+        }
+        tot[e] = acc & 0xFFFFu;
+        tot[e + 1] = acc >> 16;
+      }
+      uint32_t mine = 0;
+#pragma unroll
+      for (int e = 0; e < KP; ++e) mine += tot[e];
+      uint32_t inc = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      uint32_t ks = inc - mine;
+#pragma unroll
+      for (int e = 0; e < KP; ++e) {
+        const uint32_t k = l * KP + e;
+        if (k < sb) kst[k] = (uint16_t)ks;
+        ks += tot[e];
+      }
+      if (l == 63) nlive_s = inc;
+    }
+    lds_barrier();  // B2: prefixes, kst, nlive_s
+    // place the records in sorted order; every commit's tile-local position (0xFFFF: unknown instance)
+#pragma unroll
+    for (int j = 0; j < kV3J; ++j) {
+      const uint32_t q = trow(c, j);
+      uint32_t cp = 0xFFFFu;
+      if (loc[j] != 0xFFFFu) {
+        const uint32_t k = sk[j];
+        const uint32_t pre = (wc[w][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        const uint32_t sp = kst[k] + pre + loc[j];
+        rab[sp] = v3_set_row(rec[j], q);
+        rsb[sp] = (uint16_t)k;
+        cp = tpos[k] + pre + loc[j];
+      }
+      if (SCATTER) {
+        if (q < nrow && cp == 0xFFFFu) {  // unknown instance: ResourceManager.java:60-69
+          out_status[tile0 + q] = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
+          out_value[tile0 + q] = 0;
+        }
+      } else if (q < nrow) {
+        cpos[tbase + q] = (uint16_t)cp;
+      }
+    }
+    lds_barrier();  // B3: rab / rsb complete; every wave is done reading wc and tpos of this chunk
+    // write the chunk out run by run (contiguous); the next chunk's counters are cleared behind the reads
+    const uint32_t nl = nlive_s;
+    for (uint32_t sp = t; sp < nl; sp += kV3T) {
+      const uint32_t k = rsb[sp];
+      st_rec[tbase + tpos[k] + (sp - kst[k])] = rab[sp];
+    }
+    for (uint32_t k = t; k < (uint32_t)(kV3W * hw); k += kV3T) wc[k / hw][k % hw] = 0;
+    lds_barrier();  // B4: the write-out is done reading tpos / kst / rab; counters cleared
+    if (w == 0) {  // run k's next piece starts after this chunk's records of k
+#pragma unroll
+      for (int e = 0; e < KP; ++e) {
+        const uint32_t k = l * KP + e;
+        if (k < sb) tpos[k] = (uint16_t)(tpos[k] + ((k + 1 < sb ? kst[k + 1] : nl) - kst[k]));
+      }
+    }
+    // (tpos is next read after the next chunk's B1; kst and nlive_s are rewritten by wave 0 after B1 as well)
+  }
+}
+
+// ---- k_apply_value_v3: walker / loader waves (apply_value.hip k_apply_value_ws) over 16-byte records -----------
+// One 1024-thread workgroup per super-bucket: waves 0-3 walk (thread t = slot t, AtomicValueState in registers),
+// waves 4-15 load, decode, rank and place the next chunk (3072 records) into the other LDS buffer and store the
+// previous chunk's results.  The super-bucket's list is its run in every 8192-commit tile, in tile (= log) order.
+//
+// LDS hazards (the chunk pipeline; cf. the k_apply_map chunk-0 race):
+//   * buffer b is placed by the loaders during iteration i-1 and walked during iteration i; the one workgroup
+//     barrier per iteration separates the two, and the walkers' in-place results in b are read back by the loaders'
+//     store_results only in iteration i+1 (after the next barrier);
+//   * wcnt[b] / pbase are rewritten by `prepare` only after the loaders' arrival barrier (loader_barrier), which every
+//     loader wave reaches after its own ranking of the same chunk; wcnt[b^1] is cleared after that arrival barrier,
+//     and was last read (placement bases of the chunk before) before the previous workgroup barrier;
+//   * rstart / rpre (the run table) are written once, before the first workgroup barrier, and never rebuilt.
+constexpr int kWsLW = 12;
+constexpr int kWsPer = 4;
+constexpr int kWsCh = kWsLW * kWave * kWsPer;  // 3072 records per chunk
+constexpr int kAVT = 1024;
+constexpr int kAVW = kAVT / kWave;
+constexpr int kVSlots3 = 1 << kSbShift;
+constexpr int kVPairs3 = kVSlots3 / 2;
+constexpr uint32_t kNoPos3 = 0xFFFFFFFFu;
+
+__device__ inline uint32_t v3_value_walk(uint32_t m, uint64_t x, uint64_t y, uint32_t& ms, uint64_t& v, uint64_t& rv) {
+  const uint32_t tag = ms & 0xFFu;
+  // compareAndSet :124 (value == null && expect == null) || (value != null && value.equals(expect))
+  const bool eq = vrec_ctag(m) == tag && v == x;
+  const bool is_c = (m & kVrC) != 0, is_r = (m & kVrR) != 0, is_d = (m & kVrD) != 0;
+  const bool wr = (m & kVrW) != 0 || (is_c && eq);
+  rv = is_r ? v : ((is_c && eq) ? 1ull : 0ull);
+  const uint32_t st = is_r ? (tag << 4) : (m & 0xFFu);
+  ms = wr ? (vrec_ntag(m) | 0x100u) : (is_d ? 0u : ms);
+  v = wr ? y : (is_d ? 0ull : v);
+  return st;
+}
+
+// Largest r in [0, tiles) with rpre[r] <= c (two-round 64-ary search by the whole wave; tiles <= 4096).
+__device__ inline uint32_t v3_find_run(const uint32_t* rpre, uint32_t tiles, uint32_t c) {
+  const uint32_t l = __lane_id();
+  const uint32_t step = (tiles + kWave - 1) / kWave;
+  uint32_t cand = l * step;
+  uint64_t b = __ballot(cand < tiles && rpre[cand] <= c);
+  const uint32_t base = (uint32_t)(63 - __clzll((long long)b)) * step;
+  cand = base + l;
+  b = __ballot(l < step && cand < tiles && rpre[cand] <= c);
+  return base + (uint32_t)(63 - __clzll((long long)b));
+}
+
+__device__ inline void v3_loader_barrier(uint32_t* ctr, uint32_t target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (__lane_id() == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// SCATTER: results go straight to the caller's columns at the record's log row (out + lo + T*8192 + row).
+template <bool SCATTER>
+__global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict__ st_rec, const uint64_t* __restrict__ cb,
+                                                        uint64_t lo, const uint16_t* __restrict__ ttab, uint32_t tiles,
+                                                        uint32_t sb, uint32_t* __restrict__ val_meta,
+                                                        uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
+                                                        uint64_t* __restrict__ rst_value, uint64_t dummy,
+                                                        uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value,
+                                                        uint32_t* __restrict__ err_out) {
+  __shared__ u64x2 sab[2][kWsCh];               // chunk buffers sorted by slot; results in place (value -> .x)
+  __shared__ uint32_t sm[2][kWsCh];             //   meta words; results in place (status)
+  __shared__ uint32_t wcnt[2][kWsLW][kVPairs3];  // per-loader-wave slot counts (packed u16 pairs), double-buffered
+  __shared__ uint16_t pbase[kWsLW][kVSlots3];   // per loader wave: sorted position of its first record of each slot
+  __shared__ uint32_t sstart[2][kVSlots3 + 1];  // slot run starts of each buffer (+ total)
+  __shared__ uint32_t rstart[kV3MaxTiles];      // staging position of this super-bucket's run in tile r
+  __shared__ uint32_t rpre[kV3MaxTiles + 1];    // records of this super-bucket before tile r
+  __shared__ uint32_t wsum[kAVW];
+  __shared__ uint32_t lbar;
+
+  const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
+  const bool walker = w < 4;
+  const uint32_t lw = walker ? 0u : w - 4;
+  uint32_t ms = 0;
+  uint64_t sv = 0;
+  if (walker) {
+    ms = val_meta[(uint64_t)s * kVSlots3 + t];
+    sv = val_v[(uint64_t)s * kVSlots3 + t];
+  }
+  for (uint32_t k = t; k < (uint32_t)(2 * kWsLW * kVPairs3); k += kAVT) (&wcnt[0][0][0])[k] = 0;
+  if (t == 0) lbar = 0;
+  {  // the super-bucket's list = its run in every tile, in tile order; thread t owns tiles 2t, 2t+1
+    uint32_t len0 = 0, len1 = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t tt = 2 * t + q;
+      if (tt < tiles) {
+        const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
+        const uint32_t b0 = row[s], b1 = row[s + 1];
+        rstart[tt] = tt * kV3Tile + b0;
+        (q ? len1 : len0) = b1 - b0;
+      }
+    }
+    const uint32_t len = len0 + len1;
+    uint32_t inc = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    if (l == 63) wsum[w] = inc;
+    lds_barrier();
+    uint32_t pre = inc - len, all = 0;
+    for (uint32_t q = 0; q < (uint32_t)kAVW; ++q) {
+      const uint32_t x = wsum[q];
+      if (q < w) pre += x;
+      all += x;
+    }
+    if (2 * t < tiles) rpre[2 * t] = pre;
+    if (2 * t + 1 < tiles) rpre[2 * t + 1] = pre + len0;
+    if (t == 0) rpre[tiles] = all;
+    lds_barrier();
+  }
+  const uint32_t cnt = rpre[tiles];
+  const uint32_t nch = (cnt + kWsCh - 1) / kWsCh;
+  uint32_t err = 0;
+
+  // loader registers: the chunk to place next (rr, g; loaded one chunk ahead), the sorted / staging positions of the
+  // chunk being walked (pp, gp) and of the chunk before it (qp, gq: its results are stored during the walk)
+#define CC_J4(X) X(0) X(1) X(2) X(3)
+#define CC_DECL(J) uint32_t g##J = kNoPos3, pp##J = 0, gp##J = kNoPos3, qp##J = 0, gq##J = kNoPos3; uint4 rr##J = make_uint4(0, 0, 0, 0);
+  CC_J4(CC_DECL)
+#undef CC_DECL
+  // record c0 + lw*256 + j*64 + l of the list (log order = (loader wave, j, lane)); past the end: staging position 0.
+  // Staging position of list record c: the run r holding it gives rstart[r] + c - rpre[r]; one 64-ary search per wave
+  // and chunk finds the wave's first run, lane k then holds window run rrow + k, and rows find their runs with ballots.
+#define CC_LOAD1(J)                                                                               \
+  {                                                                                               \
+    const uint32_t crow = c0w + (J) * kWave, c = crow + l;                                        \
+    uint32_t gpos = 0;                                                                            \
+    if (crow < cnt) { /* wave-uniform */                                                          \
+      if (win) {                                                                                  \
+        uint32_t ri = (uint32_t)__popcll(__ballot(wB <= crow));                                   \
+        uint64_t mb = __ballot(wB > crow && wB <= crow + (kWave - 1));                            \
+        while (mb) {                                                                              \
+          const uint32_t bk = (uint32_t)__builtin_amdgcn_readlane((int)wB, __ffsll((long long)mb) - 1); \
+          ri += c >= bk ? 1u : 0u;                                                                \
+          mb &= mb - 1;                                                                           \
+        }                                                                                         \
+        const uint32_t rs_ = (uint32_t)__shfl((int)wS, (int)ri, 64);                              \
+        const uint32_t rp_ = (uint32_t)__shfl((int)wP, (int)ri, 64);                              \
+        if (c < cnt) gpos = rs_ + (c - rp_);                                                      \
+      } else {                                                                                    \
+        uint32_t r = v3_find_run(rpre, tiles, crow);                                              \
+        if (c < cnt) {                                                                            \
+          while (rpre[r + 1] <= c) ++r;                                                           \
+          gpos = rstart[r] + (c - rpre[r]);                                                       \
+        }                                                                                         \
+      }                                                                                           \
+    }                                                                                             \
+    g##J = c < cnt ? gpos : kNoPos3;                                                              \
+    rr##J = st_rec[gpos];                                                                         \
+  }
+#define CC_LOAD_CHUNK(C0)                                                                         \
+  {                                                                                               \
+    const uint32_t c0w = (C0) + lw * (kWave * kWsPer);                                            \
+    uint32_t wB = 0xFFFFFFFFu, wS = 0, wP = 0;                                                    \
+    bool win = false;                                                                             \
+    if (c0w < cnt) {                                                                              \
+      const uint32_t rrow = v3_find_run(rpre, tiles, c0w);                                        \
+      const uint32_t kr = rrow + l;                                                               \
+      wB = kr + 1 <= tiles ? rpre[kr + 1] : 0xFFFFFFFFu;                                          \
+      wS = kr < tiles ? rstart[kr] : 0u;                                                          \
+      wP = kr < tiles ? rpre[kr] : 0u;                                                            \
+      const uint32_t lastc = c0w + kWave * kWsPer - 1 < cnt ? c0w + kWave * kWsPer - 1 : cnt - 1; \
+      win = (uint32_t)__shfl((int)wB, 63, 64) > lastc;                                            \
+    }                                                                                             \
+    CC_J4(CC_LOAD1)                                                                               \
+  }
+  uint32_t bar_n = 0;  // loader-barrier arrivals expected so far
+  // rank / place the registers' chunk into buffer b (loaders only)
+  auto prepare = [&](uint32_t b) {
+    uint32_t rank[kWsPer], slot[kWsPer];
+    const uint4 rv4[kWsPer] = {rr0, rr1, rr2, rr3};
+    const uint32_t gv[kWsPer] = {g0, g1, g2, g3};
+#pragma unroll
+    for (int j = 0; j < kWsPer; ++j) {
+      slot[j] = v3_slot(rv4[j]);
+      const uint32_t sh = 16 * (slot[j] & 1);
+      rank[j] = gv[j] != kNoPos3 ? (atomicAdd(&wcnt[b][lw][slot[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
+    }
+    bar_n += kWsLW;
+    v3_loader_barrier(&lbar, bar_n);  // every loader wave has ranked this chunk into wcnt[b]
+    // the other counter buffer was last read before the previous workgroup barrier: clear it for the next chunk
+    for (uint32_t k = t - 4 * kWave; k < (uint32_t)(kWsLW * kVPairs3); k += kWsLW * kWave) (&wcnt[b ^ 1][0][0])[k] = 0;
+    // this wave's placement bases: lane l owns slots 4l..4l+3 (counter pairs 2l, 2l+1)
+    uint32_t a0 = 0, a1 = 0, p0 = 0, p1 = 0;
+#pragma unroll
+    for (int q = 0; q < kWsLW; ++q) {
+      const uint32_t c0v = wcnt[b][q][2 * l], c1v = wcnt[b][q][2 * l + 1];
+      if ((uint32_t)q == lw) {
+        p0 = a0;
+        p1 = a1;
+      }
+      a0 += c0v;
+      a1 += c1v;
+    }
+    const uint32_t r0 = a0 & 0xFFFFu, r1 = a0 >> 16, r2 = a1 & 0xFFFFu, r3 = a1 >> 16;
+    const uint32_t mine = r0 + r1 + r2 + r3;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    const uint32_t ex = inc - mine;
+    const uint32_t s0 = ex, s1 = ex + r0, s2 = s1 + r1, s3 = s2 + r2;
+    pbase[lw][4 * l] = (uint16_t)(s0 + (p0 & 0xFFFFu));
+    pbase[lw][4 * l + 1] = (uint16_t)(s1 + (p0 >> 16));
+    pbase[lw][4 * l + 2] = (uint16_t)(s2 + (p1 & 0xFFFFu));
+    pbase[lw][4 * l + 3] = (uint16_t)(s3 + (p1 >> 16));
+    if (lw == 0) {  // the walkers' run starts (read after the workgroup barrier)
+      sstart[b][4 * l] = s0;
+      sstart[b][4 * l + 1] = s1;
+      sstart[b][4 * l + 2] = s2;
+      sstart[b][4 * l + 3] = s3;
+      if (l == 63) sstart[b][kVSlots3] = inc;
+    }
+    // lanes read bases other lanes of this wave just wrote: LDS keeps one wave's accesses in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#define CC_PLACE1(J)                                                                \
+    {                                                                               \
+      pp##J = 0;                                                                    \
+      gp##J = SCATTER && g##J != kNoPos3 ? g##J / kV3Tile * kV3Tile + v3_row(rr##J) : g##J; \
+      if (g##J != kNoPos3) {                                                        \
+        uint32_t m_;                                                                \
+        uint64_t x_, y_;                                                            \
+        v3_decode(rr##J, cb, lo + (uint64_t)(g##J / kV3Tile) * kV3Tile, m_, x_, y_); \
+        pp##J = pbase[lw][slot[J]] + rank[J];                                       \
+        sm[b][pp##J] = m_;                                                          \
+        sab[b][pp##J] = u64x2{x_, y_};                                              \
+      }                                                                             \
+    }
+    CC_J4(CC_PLACE1)
+#undef CC_PLACE1
+  };
+  // the previous chunk's results (buffer b) back to the records' staging positions; unconditional stores
+  auto store_results = [&](uint32_t b) {
+#define CC_STORE1(J)                                                                \
+    {                                                                               \
+      const bool ok_ = gq##J != kNoPos3;                                            \
+      uint8_t* ds_ = SCATTER && ok_ ? out_status + lo + gq##J : rst_status + (ok_ ? (uint64_t)gq##J : dummy + t); \
+      uint64_t* dv_ = SCATTER && ok_ ? out_value + lo + gq##J : rst_value + (ok_ ? (uint64_t)gq##J : dummy + t); \
+      *ds_ = (uint8_t)sm[b][qp##J];                                                 \
+      *dv_ = sab[b][qp##J].x;                                                       \
+    }
+    CC_J4(CC_STORE1)
+#undef CC_STORE1
+  };
+
+  if (!walker) {
+    CC_LOAD_CHUNK(0)
+    prepare(0);
+    CC_LOAD_CHUNK(kWsCh)
+  }
+  lds_barrier();
+  for (uint32_t i = 0; i < nch; ++i) {
+    const uint32_t b = i & 1;
+    if (walker) {
+      const uint32_t start = sstart[b][t], run = sstart[b][t + 1] - start;
+      if (run) {
+        uint32_t mA[4], mB[4];
+        u64x2 xA[4], xB[4];
+        const uint32_t last = start + run - 1;
+        auto fetch = [&](uint32_t k0, uint32_t (&mm)[4], u64x2 (&xx)[4]) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t pq = start + k0 + q <= last ? start + k0 + q : last;
+            mm[q] = sm[b][pq];
+            xx[q] = sab[b][pq];
+          }
+        };
+        auto walk4 = [&](uint32_t k0, const uint32_t (&mm)[4], const u64x2 (&xx)[4]) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (k0 + q < run) {
+              uint64_t rv;
+              const uint32_t stt = v3_value_walk(mm[q], xx[q].x, xx[q].y, ms, sv, rv);
+              if (mm[q] & kVrL) err |= kErrUnsupported;
+              sm[b][start + k0 + q] = stt;
+              sab[b][start + k0 + q].x = rv;
+            }
+          }
+        };
+        fetch(0, mA, xA);
+        for (uint32_t k0 = 0; k0 < run; k0 += 8) {
+          fetch(k0 + 4, mB, xB);
+          walk4(k0, mA, xA);
+          if (k0 + 4 >= run) break;
+          fetch(k0 + 8, mA, xA);
+          walk4(k0 + 4, mB, xB);
+        }
+      }
+    } else {
+      store_results(b ^ 1);  // chunk i-1 (i = 0: the dummy rows)
+#define CC_SHIFT1(J) qp##J = pp##J; gq##J = gp##J;
+      CC_J4(CC_SHIFT1)
+#undef CC_SHIFT1
+      prepare(b ^ 1);        // chunk i+1 (past the end: no live records)
+      CC_LOAD_CHUNK((i + 2) * kWsCh)
+    }
+    lds_barrier();  // buffer hand-over: b walked (results in place), b^1 placed
+  }
+  if (!walker && nch) store_results((nch - 1) & 1);  // the last chunk (qp / gq since its walk)
+#undef CC_LOAD_CHUNK
+#undef CC_LOAD1
+#undef CC_J4
+  if (walker) {
+    val_meta[(uint64_t)s * kVSlots3 + t] = ms;
+    val_v[(uint64_t)s * kVSlots3 + t] = sv;
+  }
+  if (err) atomicOr(err_out, err);
+}
+
+int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
+  const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
+  if (a.sb > (uint32_t)kMaxSb || tiles > (uint32_t)kV3MaxTiles) return -1;
+#define CC_LAUNCH(KP, SC)                                                                                             \
+  hipLaunchKernelGGL((k_part_v3<KP, SC>), dim3(tiles), dim3(kV3T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi, \
+                     a.inst_res, a.max_inst, a.sb, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab, a.out_status,   \
+                     a.out_value)
+  if (a.v3_scatter) {
+    if (kp <= 2) CC_LAUNCH(2, true);
+    else if (kp <= 4) CC_LAUNCH(4, true);
+    else CC_LAUNCH(8, true);
+  } else {
+    if (kp <= 2) CC_LAUNCH(2, false);
+    else if (kp <= 4) CC_LAUNCH(4, false);
+    else CC_LAUNCH(8, false);
+  }
+#undef CC_LAUNCH
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
+  if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
+  if (a.v3_scatter)
+    hipLaunchKernelGGL(k_apply_value_v3<true>, dim3(a.sb_val), dim3(kAVT), 0, st, reinterpret_cast<const uint4*>(a.st_ab),
+                       a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy,
+                       a.out_status, a.out_value, a.err);
+  else
+    hipLaunchKernelGGL(k_apply_value_v3<false>, dim3(a.sb_val), dim3(kAVT), 0, st, reinterpret_cast<const uint4*>(a.st_ab),
+                       a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy,
+                       a.out_status, a.out_value, a.err);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cc

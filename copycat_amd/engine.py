@@ -65,6 +65,7 @@ def lib():
             "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
             "cc_read_group_members": (i32, [P, u32, u64, P, P]),
             "cc_read_retained": (i32, [P, u32, u64, P, P]),
+            "cc_retained_bitmap": (i32, [P, u64, u64, P, P]),
             "cc_advance_time": (i32, [P, u64]),
             "cc_advance_time_events": (i32, [P, u64, P]),
             "cc_snapshot_size": (i32, [P, P]),
@@ -412,6 +413,14 @@ class Engine:
         out = np.zeros(max(n.value, 1), np.uint64)
         _check(self.L.cc_read_retained(self.h, slot, n.value, C.byref(n), _np(out)))
         return out[:n.value].tolist()
+
+    def retained_bitmap(self, first, count, out=None, device="cuda"):
+        """cc_retained_bitmap: (device u64 bitmap over log indices [first, first + count), retained count)."""
+        words = (count + 63) // 64
+        bm = out if out is not None else torch.empty(max(words, 1), dtype=torch.int64, device=device)
+        n = C.c_uint64()
+        _check(self.L.cc_retained_bitmap(self.h, first, count, _dptr(bm), C.byref(n)))
+        return bm, n.value
 
     def map_entries(self, slot):
         """MapState entries of one map slot sorted by (key tag, key): (key_tag, key, value_tag, value, commit_index)

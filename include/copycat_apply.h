@@ -361,6 +361,13 @@ int  cc_read_group_members(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* 
  * machines drop without clean() — a listen that replaces a session's listener (AtomicValueState.java:41-49), a
  * member removed by close (MembershipGroupState.java:36-42) — which the log can never compact.            */
 int  cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint64_t* h_index);
+/* Bulk compaction feed: bit (i - first) of d_bitmap (ceil(count / 64) u64 words in HBM, LSB first) is set iff
+ * log index i in [first, first + count) is held by some resource's state machine without clean() -- the union over
+ * every live resource slot of cc_read_retained, built on the device in one pass (retained.hip).  *h_count (may be
+ * NULL) = the retained commits in the range.  A compactor calls it after a batch over (last compacted, commit index]:
+ * clear bits are compactable (Commit.clean(), ResourceManagerCommit.java:79-81); a bit that cleared since the
+ * previous call was released by a clean() in between.  Value resources need CC_CFG_VALUE_RETAINED.  Synchronous. */
+int  cc_retained_bitmap(cc_engine* e, uint64_t first, uint64_t count, uint64_t* d_bitmap, uint64_t* h_count);
 /* Log time advanced without a commit (ResourceManagerStateMachineExecutor timers): due lock
  * timeouts take effect (they publish nothing, LockState.java:54-58). */
 int  cc_advance_time(cc_engine* e, uint64_t now);

@@ -265,7 +265,7 @@ def test_leak_log_drained_across_batches_without_multimaps():
 
     R, n, batches = 1024, 450_000, 3
     flags = abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_EVENTS
-    E = Engine(R, R, n, flags=flags, max_events=4 * n)
+    E = Engine(R, R, n, flags=flags | abi.CC_CFG_VALUE_RETAINED, max_events=4 * n)
     O = Oracle(R, R, flags)
     E.resource_create_range(0, R, abi.CC_RES_VALUE)
     E.instance_open_range(0, R, 0, 1000, 7)
@@ -283,3 +283,97 @@ def test_leak_log_drained_across_batches_without_multimaps():
     for slot in list(range(0, R, 97)) + [R - 1]:
         got, want = E.retained(slot), O.retained(slot, cap=1 << 12)
         assert got == want and len(got) >= batches * n // R, slot
+
+
+# ---- the bulk compaction feed: cc_retained_bitmap == the union of every slot's cc_read_retained -----------------
+def _bitmap_indices(bm, first, count):
+    words = bm.cpu().numpy().view(np.uint64)[: (count + 63) // 64]
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:count]
+    return (np.nonzero(bits)[0].astype(np.uint64) + np.uint64(first)).tolist()
+
+
+def _oracle_union(O, slots):
+    out = set()
+    for r in slots:
+        got = O.retained(int(r), cap=1 << 16)
+        if got is not None:
+            out.update(got)
+    return out
+
+
+def test_retained_bitmap_coordination_32k_resources():
+    """Locks, elections, groups, values with listeners and queues over 32,768+ resources: after every batch, after a
+    session close and after the group timers fire, the device bitmap over the whole log range equals the union of the
+    oracle's per-slot retained sets (ResourceManagerCommit.clean :79-81 sites of every state machine); a sub-range and
+    the count agree too, and bits only clear between calls when a clean() released them."""
+    from copycat_amd.workload import coord_random_stream
+    from tests.test_gpu_coord import FLAGS, _check_batch, _setup
+
+    L_, E2, G, V, Q = abi.CC_RES_LOCK, abi.CC_RES_ELECTION, abi.CC_RES_GROUP, abi.CC_RES_VALUE, abi.CC_RES_QUEUE
+    R, K, n = 32_768 + 256, 2, 600_000
+    types = np.resize(np.array([L_, E2, G, V], np.uint8), R)
+    flags = FLAGS | abi.CC_CFG_VALUE_RETAINED
+    E, O, max_inst = _setup(types, K, flags, max_batch=n, max_events=1 << 23)
+    rng = np.random.default_rng(61)
+    b = _with_schedules(coord_random_stream(n, types, K, max_inst, seed=61), types, K, max_inst, rng, 200)
+    span = n + 1
+    prev = None
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        _check_batch(E, O, b.slice(lo, hi), capacity=8 * (hi - lo))
+        bm, cnt = E.retained_bitmap(1, span)
+        got = _bitmap_indices(bm, 1, span)
+        want = sorted(_oracle_union(O, range(R)))
+        assert cnt == len(got) and got == want, (cnt, len(got), len(want), sorted(set(got) ^ set(want))[:8])
+        assert len(want) > R // 2
+        if prev is not None:  # a commit of the first batch that is no longer retained was clean()ed in between
+            assert set(prev) - set(got) and not (set(got) - set(prev)) & set(range(1, n // 2 + 1))
+        prev = got
+    sub_first, sub_count = n // 3, 12_345
+    bm, cnt = E.retained_bitmap(sub_first, sub_count)
+    assert _bitmap_indices(bm, sub_first, sub_count) == [i for i in prev if sub_first <= i < sub_first + sub_count]
+    E.sessions_close([7], capacity=1 << 20)
+    O.session_close(7)
+    O.take_events()
+    bm, _ = E.retained_bitmap(1, span)
+    assert _bitmap_indices(bm, 1, span) == sorted(_oracle_union(O, range(R)))
+    now = int(b.time[-1]) + 1000
+    E.advance_time_events(now, capacity=1 << 16)
+    O.advance_time(now)
+    O.take_events()
+    bm, _ = E.retained_bitmap(1, span)
+    assert _bitmap_indices(bm, 1, span) == sorted(_oracle_union(O, range(R)))
+
+
+def test_retained_bitmap_maps_sets_multimaps_queues():
+    """Map and set entries (replace / remove / TTL expiry clean them), multimap puts (never cleaned, A18) and queue
+    elements in one engine: after each batch the bitmap equals the union of the oracle's per-slot retained sets."""
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+    from tests.test_gpu_multimap import _stream as keyed_stream
+    from tests.test_gpu_queue import _stream as queue_stream
+
+    M = 256
+    types = np.array([abi.CC_RES_MAP, abi.CC_RES_MULTIMAP, abi.CC_RES_SET] * M, np.uint8)
+    R = len(types) + M  # + M queues after the keyed resources
+    n = 60_000
+    E = Engine(R, R + 8, n, flags=abi.CC_CFG_TIMERS_DEFERRED, map_capacity=1 << 16, max_events=1 << 18)
+    O = Oracle(R, R + 8)
+    for r in range(R):
+        t = int(types[r]) if r < len(types) else abi.CC_RES_QUEUE
+        E.resource_create(r, t)
+        E.instance_open(r, r, 1000 + r, 7)
+        O.resource_create(r, t)
+        O.instance_open(r, r, 1000 + r, 7)
+    a = keyed_stream(n, types, 24, seed=71)
+    q = queue_stream(n, M, M + 8, 72)
+    q.inst[:] = np.where(q.inst < M, q.inst + len(types), R + 5)
+    q.index[:] = np.arange(n + 1, 2 * n + 1, dtype=np.uint64)
+    q.time[:] = int(a.time[-1]) + np.arange(n, dtype=np.uint64) // 8
+    for part in (a, q):
+        s, v = E.apply_host(part)
+        s2, v2 = O.apply(part)
+        assert np.array_equal(s, s2) and np.array_equal(v, v2)
+        bm, cnt = E.retained_bitmap(1, 2 * n)
+        got = _bitmap_indices(bm, 1, 2 * n)
+        want = sorted(_oracle_union(O, range(R)))
+        assert got == want and cnt == len(want) > M, (len(got), len(want), sorted(set(got) ^ set(want))[:8])

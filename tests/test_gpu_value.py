@@ -110,3 +110,56 @@ def test_device_resident_apply_matches_host_path():
     assert np.array_equal(va.view(torch.int64).cpu().numpy().view(np.uint64), v1)
     for x, y in zip(E1.value_state(), E2.value_state()):
         assert np.array_equal(x, y)
+
+
+def test_cas_update_deltas_at_the_record_boundary():
+    """value_path.hip stores a CAS update as a 46-bit difference from the expected value; a difference that does not
+    fit escapes to the batch's b column.  Chains of CASes that always succeed, with differences on both sides of the
+    46-bit boundary and across the i64 wrap, tag changes (Long -> Integer -> null) and expected NULLs, are bit-exact
+    against the oracle, with the value-only pipeline and with the previous one (CC_VALUE_V2)."""
+    import os
+
+    R, steps = 512, 48
+    deltas = [0, 1, -1, (1 << 45) - 1, -(1 << 45), 1 << 45, -(1 << 45) - 1, (1 << 63), (1 << 64) - 1, 12345678901234,
+              -(1 << 62), (1 << 46) + 3]
+    rng = np.random.default_rng(3)
+    cur = np.zeros(R, np.uint64)
+    ctag = np.zeros(R, np.uint8)
+    rows = []
+    for k in range(steps):
+        for r in rng.permutation(R):
+            d = deltas[(k + r) % len(deltas)] if k % 7 else int(rng.integers(0, 1 << 63))
+            ntag = abi.CC_TAG_LONG if (k + r) % 11 else (abi.CC_TAG_INT if (k + r) % 2 else abi.CC_TAG_NULL)
+            upd = (int(cur[r]) + d) % (1 << 64) if ntag != abi.CC_TAG_NULL else 0
+            if ntag == abi.CC_TAG_INT:
+                upd = upd & 0x7FFFFFFF
+            rows.append((r, abi.CC_OP_VALUE_CAS, int(ctag[r]) | (ntag << 3), int(cur[r]), upd))
+            cur[r], ctag[r] = upd, ntag
+            if (k + r) % 13 == 0:
+                rows.append((r, abi.CC_OP_VALUE_GET, 0, 0, 0))
+    n = len(rows)
+    arr = np.array(rows, dtype=object)
+    b = Batch.from_columns(index=np.arange(1, n + 1, dtype=np.uint64), time=np.arange(1, n + 1, dtype=np.uint64),
+                           inst=np.array(arr[:, 0], np.uint32), op=np.array(arr[:, 1], np.uint8),
+                           flags=np.array(arr[:, 2], np.uint8), a=np.array([int(x) for x in arr[:, 3]], np.uint64),
+                           b=np.array([int(x) for x in arr[:, 4]], np.uint64))
+    for v2 in (False, True):
+        if v2:
+            os.environ["CC_VALUE_V2"] = "1"
+        try:
+            E, O, gs, gv, os_, ov = _run_both(b, R, R, sub_batch=16384 * 2)
+        finally:
+            os.environ.pop("CC_VALUE_V2", None)
+        _assert_same(E, O, gs, gv, os_, ov, R)
+        cas = b.op == abi.CC_OP_VALUE_CAS
+        assert np.all(gv[cas] == 1)  # every CAS expected the value it found
+
+
+@pytest.mark.parametrize("n,sub", [(8191, 0), (8193, 0), (16384 * 3 + 8191, 16384), (100_001, 16384 * 2)])
+def test_value_ragged_tiles_and_sub_batches(n, sub):
+    """Batches that end inside an 8192-commit tile, and sub-batches of whole 16384-commit multiples."""
+    from copycat_amd.workload import atomic_long_stream
+
+    R = 4096
+    b = atomic_long_stream(n, resources=R)
+    _assert_same(*_run_both(b, R, R + 8, sub_batch=sub), R)
