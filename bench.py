@@ -363,8 +363,10 @@ def run_c5(args, dev, rank, world, dist):
         for r in range(R):
             E.resource_create(r, int(types[r]))
         E.instance_open_range(0, R, 0, 1000, 1 + rank)
-    for j in range(V):
-        E.instance_open(R + j, int(victim_res[j]), 10_000_000 + j, int(victim_sess[j]))
+    for j in range(V):  # (manager layout: resource r has id = its CreateResource commit's index 1000 + r)
+        rslot = E.resource_slot(1000 + int(victim_res[j])) if args.c5_layout == "manager" else int(victim_res[j])
+        assert rslot >= 0
+        E.instance_open(R + j, rslot, 10_000_000 + j, int(victim_sess[j]))
     stream = torch.cuda.current_stream(dev)
     wm_all = torch.zeros(world, dtype=torch.int64, device=dev)
     wm_local = torch.zeros(1, dtype=torch.int64, device=dev)

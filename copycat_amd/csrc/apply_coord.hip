@@ -551,24 +551,26 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
 // (the run in every tile, tile order = log order) and keep the commits of their own slots.  256 threads load a
 // 512-commit chunk (the next chunk's meta words are in flight during the walk), rank their own commits per slot
 // inside each wave (LDS atomics with return: lane order), one wave turns the per-wave counts into slot run starts,
-// the owners' records are gathered into LDS in slot order, and waves 0 and 1 walk: lane l < 32 of wave w applies
-// slot w*32 + l's commits in log order with its CoordHdr (and AtomicValueState) held in registers for the whole
-// launch.  (The walk is instruction-bound: two half-filled walking waves on two SIMDs finish a chunk in about half the
-// time one full wave does.)  Small LDS so two workgroups share a CU and hide each other's gathers.
+// the owners' records are gathered into LDS in slot order, and wave 0 (lane = slot) applies each slot's commits in
+// log order with its CoordHdr (and AtomicValueState) held in registers for the whole launch.  Small LDS
+// (~48 KB) so three workgroups share a CU and hide each other's gathers.
+// (Round 3 measured two 32-lane walking waves per workgroup instead of one: no change, 8.9 ms/step either way.  The
+// walk is bound by each lane's sequential chain -- about 2,700-4,500 cycles per step of a group / election slot,
+// phase clocks profiles/r03/c5_diag -- not by how many waves walk.)
 //
 // LDS hazards of the chunk loop (cf. the k_apply_map chunk-0 race): the run table (rstart / rpre) is
-// written once before the loop and only read after; the per-wave counters wc are read by the gather (their own wave's
-// row) and cleared by the same wave's lanes right after (in program order within the wave), before barrier 3; the
-// record planes (rab ... rpos) are written by the gather only after barrier 2 of the chunk, which every thread reaches
-// after the previous chunk's flush barrier (5), i.e. after the walk and the result stores stopped reading them.
+// written once before the loop and only read after (load_meta's rows_pos); the per-wave counters wc are read by the
+// gather (each wave reads its own row) and cleared right after by that same wave's lanes (k = t covers exactly row
+// w), in program order within the wave, before barrier 3; the record planes (rab ... rpos) are written by the gather
+// only after barrier 2 of a chunk, which every thread reaches after the previous chunk's final barrier, i.e. after
+// the walk and the result / event stores of that chunk stopped reading them.
 constexpr int kQ = 64;                     // slots per workgroup
 constexpr int kQPerSb = (1 << kSbShift) / kQ;
 constexpr int kCT2 = 256;                  // threads per workgroup
 constexpr int kCW2 = kCT2 / kWave;
 constexpr int kCPer2 = 2;                  // commits per thread per chunk
 constexpr int kCCh2 = kCT2 * kCPer2;       // 512 commits of the super-bucket per chunk
-constexpr int kEvLane = 16;                // LDS event slots per walking slot per chunk
-constexpr int kWalkLanes = 32;             // walking lanes per walking wave (waves 0 and 1)
+constexpr int kEvLane = 16;                // LDS event slots per walking lane per chunk
 
 __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
                                                      uint32_t tiles, uint32_t sb, uint32_t sbq_base,
@@ -597,11 +599,10 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   __shared__ uint32_t rpre[kMaxTiles + 1];
   __shared__ uint32_t wsum[kCW2];
   __shared__ uint64_t evp[kEvLane * 3 * kQ];    // the walkers' event buffers (lane-minor planes, see kLanes)
-  __shared__ uint32_t evoff[kQ + 1];        // per walking wave: exclusive prefix of its slots' event counts
-  __shared__ uint32_t evtot[2];
+  __shared__ uint32_t evoff[kQ + 1];
   __shared__ uint64_t ecx[kECache * kQ], eci[kECache * kQ];  // the walkers' first entries (Ents), lane-minor
   __shared__ uint32_t ecn[kECache * kQ], ecp[kECache * kQ];
-  __shared__ unsigned long long evbase[2];
+  __shared__ unsigned long long evbase;
 
   const uint32_t s = blockIdx.x / kQPerSb, q0 = (blockIdx.x % kQPerSb) * kQ;
   if (!sb_kind[s]) return;  // value-only super-bucket: k_apply_value
@@ -646,19 +647,16 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     __syncthreads();
   }
   const uint32_t cnt = rpre[tiles];
-  static_assert(kQ == (int)kLanes && kQ == 2 * kWalkLanes, "two walking waves of 32 lanes cover the quarter bucket");
-  // walking lane: waves 0 and 1, lanes 0..31; its slot ws (the LDS planes stay slot-minor with stride kLanes)
-  const bool walker = w < 2 && l < (uint32_t)kWalkLanes;
-  const uint32_t ws = w * kWalkLanes + (l & (kWalkLanes - 1));
-  const Emitter em{(LdsU64*)(evp + ws), kEvLane, arena, arena_n, arena_cap, leak, leak_n, leak_cap};
-  // the walker lanes keep their state machine's header in registers for the whole launch
-  const uint32_t res = s * (1u << kSbShift) + q0 + ws;
+  static_assert(kQ == (int)kLanes, "one walking lane per slot of the quarter bucket");
+  const Emitter em{(LdsU64*)(evp + l), kEvLane, arena, arena_n, arena_cap, leak, leak_n, leak_cap};
+  // the walker lanes (wave 0, lane = slot) keep their state machine's header in registers for the whole launch
+  const uint32_t res = s * (1u << kSbShift) + q0 + l;
   uint8_t* blk = coord + (uint64_t)res * coord_block(coord_cap);
   uint32_t type = 0, vm = 0;
   uint64_t vv = 0;
   CoordHdr h{};
-  const Ents E{(LdsU64*)(ecx + ws), (LdsU64*)(eci + ws), (LdsU32*)(ecn + ws), (LdsU32*)(ecp + ws), (GlbEnt*)ents(blk), coord_cap, CoordEnt{0, 0, 0, 0}};
-  if (walker) {
+  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk), coord_cap, CoordEnt{0, 0, 0, 0}};
+  if (w == 0) {
     type = res_type[res];
     h = *reinterpret_cast<const CoordHdr*>(blk);
     if (type == CC_RES_VALUE) {
@@ -798,10 +796,10 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     for (uint32_t k = t; k < (uint32_t)(kCW2 * kQ); k += kCT2) (&wc[0][0])[k] = 0;  // (read above, before the barrier)
     lds_barrier();  // LDS only: __syncthreads() would wait for the loads just issued
     PH(3);
-    // the walk: lane l < 32 of wave w < 2 applies slot q0 + w*32 + l's commits in log order
+    // the walk: lane l of wave 0 applies slot q0 + l's commits in log order
     uint32_t lane_n = 0;  // events this lane published in this chunk
-    if (w < 2) {
-      const uint32_t b = walker ? sstart[ws] : 0u, e = walker ? sstart[ws + 1] : 0u;
+    if (w == 0) {
+      const uint32_t b = sstart[l], e = sstart[l + 1];
       auto walk = [&](auto tc) {
       for (uint32_t p = b; p < e; ++p) {
         const uint32_t mmr = rmeta[p];
@@ -843,18 +841,18 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
 #ifdef CC_PHASE_TIMING
       ev_total_lane += lane_n;
 #endif
-      // this chunk's event regions of the wave: exclusive prefix of its lanes' (capped) counts, one arena reservation
-      const uint32_t mine = walker ? (lane_n < (uint32_t)kEvLane ? lane_n : (uint32_t)kEvLane) : 0u;
+      // this chunk's event regions: exclusive prefix of the lanes' (capped) counts, one arena reservation
+      const uint32_t mine = lane_n < (uint32_t)kEvLane ? lane_n : (uint32_t)kEvLane;
       uint32_t inc = mine;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(inc, d, 64);
         if (l >= (uint32_t)d) inc += y;
       }
-      if (walker) evoff[ws] = inc - mine;
+      evoff[l] = inc - mine;
       if (l == 63) {
-        evtot[w] = inc;
-        evbase[w] = inc ? atomicAdd(arena_n, (unsigned long long)inc) : 0ull;
+        evoff[kQ] = inc;
+        evbase = inc ? atomicAdd(arena_n, (unsigned long long)inc) : 0ull;
       }
     }
     lds_barrier();
@@ -865,19 +863,17 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
       ev_cnt[gp] = oev[p];
     }
     PH(4);
-    // flush the chunk's events (their order in the arena is free: events.hip sorts by (row, emission index)); walking
-    // wave w's events go to its own reservation evbase[w]
-    const uint32_t nb0 = evtot[0], nb = nb0 + evtot[1];
+    // flush the chunk's events (their order in the arena is free: events.hip sorts by (row, emission index))
+    const uint32_t nb = evoff[kQ];
     for (uint32_t q = t; q < nb; q += kCT2) {
-      const uint32_t ww = q < nb0 ? 0u : 1u, qq = q - (ww ? nb0 : 0u);
-      uint32_t lo = ww * kWalkLanes, hi = lo + kWalkLanes;  // slot whose region holds qq: evoff[lo] <= qq < next
+      uint32_t lo = 0, hi = kQ;  // lane whose region holds q: evoff[lo] <= q < evoff[lo + 1]
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (evoff[mid] <= qq) lo = mid; else hi = mid;
+        if (evoff[mid] <= q) lo = mid; else hi = mid;
       }
-      if (evbase[ww] + qq < arena_cap) {
-        const uint32_t i = qq - evoff[lo];
-        uint64_t* dst = reinterpret_cast<uint64_t*>(arena + evbase[ww] + qq);
+      if (evbase + q < arena_cap) {
+        const uint32_t i = q - evoff[lo];
+        uint64_t* dst = reinterpret_cast<uint64_t*>(arena + evbase + q);
         dst[0] = evp[(i * 3 + 0) * kQ + lo];
         dst[1] = evp[(i * 3 + 1) * kQ + lo];
         dst[2] = evp[(i * 3 + 2) * kQ + lo];
@@ -893,9 +889,9 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
     g_wg_t[4 * blockIdx.x + 2] = cnt;
   }
-  if (walker && blockIdx.x < 4096) atomicAdd(&g_wg_t[4 * blockIdx.x + 3], (unsigned long long)ev_total_lane);
+  if (w == 0 && blockIdx.x < 4096) atomicAdd(&g_wg_t[4 * blockIdx.x + 3], (unsigned long long)ev_total_lane);
 #endif
-  if (walker) {
+  if (w == 0) {
     E.store();
     *reinterpret_cast<CoordHdr*>(blk) = h;
     if (type == CC_RES_VALUE) {

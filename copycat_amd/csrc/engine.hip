@@ -189,7 +189,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   e->sub_batch = sub;
   e->max_tiles = sub / kTile;
   e->value_v2 = getenv("CC_VALUE_V2") != nullptr;
-  e->v3_scatter = getenv("CC_V3_SCATTER") != nullptr;
+
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
   e->res_type.assign(slots, CC_RES_NONE);
   e->inst_res.assign(cfg->max_instances, kNoRes);
@@ -709,9 +709,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.res16 = e->ext ? nullptr : e->d_res16;
     const bool v3 = !e->ext && !e->value_v2;  // value-only engines: value_path.hip
     pa.v3 = v3;
-    pa.v3_scatter = v3 && e->v3_scatter;
-    pa.out_status = out->status;
-    pa.out_value = out->value;
+
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
     if (e->map_bits && e->ttl_live && launch_map_rows(e->d_cpos, lo, hi, e->d_map_row, st))
@@ -722,9 +720,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.ttab = e->d_ttab;
     va.tiles = v3 ? (uint32_t)((hi - lo + kV3Tile - 1) / kV3Tile) : tiles;
     va.v3 = v3;
-    va.v3_scatter = v3 && e->v3_scatter;
-    va.out_status = out->status;
-    va.out_value = out->value;
+
     va.cb = c->b;
     va.lo = lo;
     va.sb = e->sb_total();
@@ -810,7 +806,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.dummy_value = e->d_rst_value + e->sub_batch;
     ua.v3 = v3;
     ua.mark = marker_of(e);
-    if (!(v3 && e->v3_scatter) && launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
+    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
     if (e->coord_on) {
       EventArgs ea{};
       ea.cpos = e->d_cpos;

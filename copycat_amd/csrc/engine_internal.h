@@ -52,9 +52,6 @@ struct PartArgs {
   uint16_t* inst_res16;  // value-only engines, < 65535 resources, <= 65536 instances: u16 copy of inst_res
   uint16_t* res16;       // ... and the resolved resource of every commit of the sub-batch (null: not this path)
   bool v3;               // value-only pipeline of value_path.hip (8192-commit tiles, 16-byte records in st_ab)
-  bool v3_scatter;       //   ... results written straight to log order by the apply (no cpos / unpermute)
-  uint8_t* out_status;   //   ... the caller's result columns (whole batch; unknown-session rows)
-  uint64_t* out_value;
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
@@ -80,11 +77,8 @@ struct ValueArgs {
   uint64_t dummy;        // first of the dummy result rows after the staging area (= sub_batch)
   uint32_t* err;
   bool v3;               // value_path.hip: 16-byte records, 8192-commit tiles
-  bool v3_scatter;       //   results straight to out_status / out_value at their log rows
   const uint64_t* cb;    //   the batch's b column (escaped CAS updates) and the sub-batch's first row
   uint64_t lo;
-  uint8_t* out_status;
-  uint64_t* out_value;
   Marker mark;
 };
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
@@ -255,7 +249,9 @@ struct EventArgs {
   const EvRec* arena;
   const unsigned long long* arena_n;
   uint64_t arena_cap;
-  uint32_t* perm;          // [arena_cap] output position - the sub-batch's first -> arena index
+  uint32_t* perm;          // [arena_cap] output position - the sub-batch's first -> arena index (CC_EV_V1)
+  EvRec* bucket;           // [arena_cap] the arena grouped by tile
+  uint32_t* ccnt;          // [ev_chunk_cap(arena_cap) * tiles] per (arena chunk, tile) counts -> bases
   uint64_t out_cap;
   uint32_t* out_pos;
   uint32_t* out_target;
@@ -267,6 +263,8 @@ struct EventArgs {
   Marker mark;
 };
 int launch_events(const EventArgs& a, hipStream_t st);
+constexpr uint64_t kEvChunk = 8192;  // arena events per bucketing workgroup (events.hip)
+inline uint64_t ev_chunk_cap(uint64_t arena_cap) { return (arena_cap + kEvChunk - 1) / kEvChunk; }
 
 // Session close / expire fan-out (close.hip): m closes in fan-out order, grouped by resource.
 struct CloseArgs {

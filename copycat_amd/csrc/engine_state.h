@@ -166,7 +166,7 @@ struct cc_engine {
   // extended staging (maps / coordination / value events) + coordination + events
   bool ext = false, coord_on = false;
   bool value_v2 = false;
-  bool v3_scatter = false;  // CC_V3_SCATTER=1 at creation: value_path.hip writes results straight to log order (A/B)  // CC_VALUE_V2=1 at creation: the value-only engine keeps the previous pipeline (A/B)
+  // CC_VALUE_V2=1 at creation: the value-only engine keeps the previous pipeline (A/B)
   std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
   uint8_t* d_sb_kind = nullptr;
   uint64_t* d_inst_id = nullptr;     // instance slot -> instance id (election listeners, group members)

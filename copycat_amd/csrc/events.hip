@@ -7,6 +7,16 @@
 //                  the tile, and row_of[staging position] = row for commits that published;
 //   k_ev_tiles   : one workgroup: exclusive scan of the tile totals on top of the events already written by
 //                  earlier sub-batches; capacity / no-stream checks;
+// Default order pass (round 3): the arena is bucketed by partition tile, and each tile's events are placed from LDS
+// tables, with no random gathers of per-row arrays:
+//   k_ev_count   : per tile, the events its commits published (ev_cnt over the tile's staging positions);
+//   k_ev_tiles   : (as above) the tiles' output offsets;
+//   k_ev_chist   : per arena chunk of kEvChunk events, events per tile (ccnt[chunk][tile]);
+//   k_ev_cscan   : per tile, the chunks' bucket bases (exclusive scan over chunks from the tile's offset);
+//   k_ev_place   : every arena event to its tile's bucket (order inside a bucket is free);
+//   k_ev_tile_out: per tile, the per-row event offsets rebuilt in LDS (cpos + ev_cnt), then each of the tile's events
+//                  written to its output row (tile offset + row offset + emission index).
+// The previous order pass (CC_EV_V1=1, A/B): k_ev_rows as above writes row_of / ev_loc per staging position;
 //   k_ev_perm    : every arena event's output position (tile offset + row offset + emission index) -> perm[];
 //   k_ev_out     : the output rows in order, each gathering its arena record: the six output columns are
 //                  written contiguously (scattered 1-byte stores to them were the cost of the old one-pass
@@ -165,9 +175,207 @@ __global__ void k_ev_out(const EvRec* __restrict__ arena, const unsigned long lo
   }
 }
 
+// ---- the tile-bucketed order pass ---------------------------------------------------------------------------
+constexpr int kEC = 256;  // threads of the counting / bucketing kernels
+
+// events per tile: ev_cnt summed over the tile's staging positions below the sub-batch's row count (memset per
+// sub-batch; positions without a staged commit hold 0)
+__global__ __launch_bounds__(kEC) void k_ev_count(const uint16_t* __restrict__ ev_cnt, uint64_t n, uint32_t* __restrict__ tile_sum) {
+  __shared__ uint32_t wsum[kEC / kWave];
+  const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t end = t0 + kTile < n ? t0 + kTile : n;
+  uint32_t s = 0;
+  for (uint64_t i = t0 + 8 * (uint64_t)t; i < end; i += 8 * kEC) {
+    if (i + 8 <= end) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ev_cnt + i);
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += (x[q] & 0xFFFFu) + (x[q] >> 16);
+    } else {
+      for (uint64_t k = i; k < end; ++k) s += ev_cnt[k];
+    }
+  }
+#pragma unroll
+  for (int d = 32; d; d >>= 1) s += __shfl_xor(s, d, 64);
+  if (l == 0) wsum[w] = s;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t tot = 0;
+    for (int q = 0; q < kEC / kWave; ++q) tot += wsum[q];
+    tile_sum[blockIdx.x] = tot;
+  }
+}
+
+// per arena chunk: events per tile
+__global__ __launch_bounds__(kEC) void k_ev_chist(const EvRec* __restrict__ arena, const unsigned long long* __restrict__ arena_n,
+                                                 uint64_t arena_cap, uint32_t tiles, uint32_t* __restrict__ ccnt) {
+  __shared__ uint32_t h[kMaxTiles];
+  const uint64_t ne = *arena_n < arena_cap ? *arena_n : arena_cap;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kEvChunk;
+  if (c0 >= ne) return;
+  for (uint32_t k = threadIdx.x; k < tiles; k += kEC) h[k] = 0;
+  __syncthreads();
+  const uint64_t c1 = c0 + kEvChunk < ne ? c0 + kEvChunk : ne;
+  for (uint64_t e = c0 + threadIdx.x; e < c1; e += kEC) atomicAdd(&h[arena[e].g / kTile], 1u);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < tiles; k += kEC) ccnt[(uint64_t)blockIdx.x * tiles + k] = h[k];
+}
+
+// per tile (one workgroup): the bucket base of each chunk's events of the tile (exclusive prefix over chunks, from the
+// tile's offset in the sub-batch's output); thread t owns a contiguous range of chunks
+__global__ __launch_bounds__(kEC) void k_ev_cscan(const unsigned long long* __restrict__ arena_n, uint64_t arena_cap,
+                                                 uint32_t tiles, const uint64_t* __restrict__ tile_off,
+                                                 uint32_t* __restrict__ ccnt) {
+  __shared__ uint32_t wsum[kEC / kWave];
+  const uint32_t T = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint64_t ne = *arena_n < arena_cap ? *arena_n : arena_cap;
+  const uint32_t chunks = (uint32_t)((ne + kEvChunk - 1) / kEvChunk);
+  const uint32_t per = (chunks + kEC - 1) / kEC, c0 = t * per, c1 = min(c0 + per, chunks);
+  uint32_t sum = 0;
+  for (uint32_t c = c0; c < c1; ++c) sum += ccnt[(uint64_t)c * tiles + T];
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (l >= (uint32_t)d) inc += y;
+  }
+  if (l == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = (uint32_t)(tile_off[T] - tile_off[0]) + inc - sum;
+  for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+  for (uint32_t c = c0; c < c1; ++c) {
+    uint32_t* p = ccnt + (uint64_t)c * tiles + T;
+    const uint32_t x = *p;
+    *p = run;
+    run += x;
+  }
+}
+
+// every event of the chunk to its tile's bucket (base of the (chunk, tile) piece + rank inside it)
+__global__ __launch_bounds__(kEC) void k_ev_place(const EvRec* __restrict__ arena, const unsigned long long* __restrict__ arena_n,
+                                                 uint64_t arena_cap, uint32_t tiles, const uint32_t* __restrict__ ccnt,
+                                                 EvRec* __restrict__ bucket) {
+  __shared__ uint32_t h[kMaxTiles];
+  const uint64_t ne = *arena_n < arena_cap ? *arena_n : arena_cap;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kEvChunk;
+  if (c0 >= ne) return;
+  for (uint32_t k = threadIdx.x; k < tiles; k += kEC) h[k] = ccnt[(uint64_t)blockIdx.x * tiles + k];
+  __syncthreads();
+  const uint64_t c1 = c0 + kEvChunk < ne ? c0 + kEvChunk : ne;
+  for (uint64_t e = c0 + threadIdx.x; e < c1; e += kEC) {
+    const EvRec r = arena[e];
+    const uint32_t d = atomicAdd(&h[r.g / kTile], 1u);
+    if (d < arena_cap) bucket[d] = r;
+  }
+}
+
+constexpr int kEvWin = 2048;  // output events assembled per window in k_ev_tile_out
+// per tile: the rows' event offsets in LDS, then the tile's events to their output rows, one window at a time
+__global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict__ cpos, uint64_t n, const uint16_t* __restrict__ ev_cnt,
+                                                    const uint32_t* __restrict__ tile_sum, const uint64_t* __restrict__ tile_off,
+                                                    const EvRec* __restrict__ bucket, const unsigned long long* __restrict__ arena_n,
+                                                    uint64_t arena_cap, uint64_t lo, uint64_t out_cap,
+                                                    uint32_t* __restrict__ pos, uint32_t* __restrict__ target,
+                                                    uint8_t* __restrict__ code, uint8_t* __restrict__ src,
+                                                    uint8_t* __restrict__ tag, uint64_t* __restrict__ payload) {
+  __shared__ uint32_t wsum[kER / kWave];
+  __shared__ uint16_t srow[kTile];  // staging position -> row in the tile
+  __shared__ uint32_t soff[kTile];  // staging position -> offset of its commit's first event in the tile's output
+  // one output window of kEvWin events, assembled in LDS so the six columns are written contiguously
+  __shared__ uint32_t wpos[kEvWin], wtgt[kEvWin], wcts[kEvWin];
+  __shared__ uint64_t wpay[kEvWin];
+  if (*arena_n > arena_cap) return;  // the arena overflowed: the call fails (kErrEvents)
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, T = blockIdx.x;
+  const uint64_t r0 = (uint64_t)T * kTile + (uint64_t)t * kERPer;
+  const uint32_t tbase = T * kTile;
+  uint32_t pp[kERPer];
+  {
+    const uint4 v0 = reinterpret_cast<const uint4*>(cpos + r0)[0], v1 = reinterpret_cast<const uint4*>(cpos + r0)[1];
+    const uint32_t ww[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      pp[2 * q] = ww[q] & 0xFFFF;
+      pp[2 * q + 1] = ww[q] >> 16;
+    }
+  }
+  uint32_t c[kERPer], sum = 0;
+#pragma unroll
+  for (int q = 0; q < kERPer; ++q) {
+    c[q] = r0 + q < n && pp[q] != 0xFFFF ? ev_cnt[tbase + pp[q]] : 0u;
+    sum += c[q];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (l >= (uint32_t)d) inc += y;
+  }
+  if (l == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+  for (int q = 0; q < kERPer; ++q) {
+    if (c[q]) {
+      srow[pp[q]] = (uint16_t)(t * kERPer + q);
+      soff[pp[q]] = run;
+    }
+    run += c[q];
+  }
+  __syncthreads();
+  const uint64_t toff = tile_off[T], b0 = toff - tile_off[0];
+  const uint32_t nev = tile_sum[T];
+  if (b0 + nev > arena_cap || toff + nev > out_cap) return;  // (the call fails: kErrEvents from k_ev_tiles)
+  for (uint32_t w0 = 0; w0 < nev; w0 += kEvWin) {  // block-uniform
+    const uint32_t wn = nev - w0 < (uint32_t)kEvWin ? nev - w0 : (uint32_t)kEvWin;
+    for (uint32_t i = t; i < nev; i += kER) {  // the tile's events (re-read per window from L2)
+      const EvRec r = bucket[b0 + i];
+      const uint32_t sp = r.g - tbase;
+      const uint32_t d = soff[sp] + r.k - w0;
+      if (d < wn) {
+        wpos[d] = (uint32_t)(lo + tbase + srow[sp]);
+        wtgt[d] = r.target;
+        wcts[d] = (uint32_t)r.code | ((uint32_t)r.src << 8) | ((uint32_t)r.tag << 16);
+        wpay[d] = r.payload;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < wn; i += kER) {
+      const uint64_t d = toff + w0 + i;
+      const uint32_t cts = wcts[i];
+      pos[d] = wpos[i];
+      target[d] = wtgt[i];
+      code[d] = (uint8_t)cts;
+      src[d] = (uint8_t)(cts >> 8);
+      tag[d] = (uint8_t)(cts >> 16);
+      payload[d] = wpay[i];
+    }
+    __syncthreads();
+  }
+}
+
 int launch_events(const EventArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_EVENTS, 1, st);
+  static const bool v1 = getenv("CC_EV_V1") != nullptr || getenv("CC_EV_SCATTER") != nullptr;
+  if (!v1 && a.bucket && a.ccnt) {
+    const uint32_t chunks = (uint32_t)ev_chunk_cap(a.arena_cap);
+    hipLaunchKernelGGL(k_ev_count, dim3(a.tiles), dim3(kEC), 0, st, a.ev_cnt, a.hi - a.lo, a.tile_sum);
+    hipLaunchKernelGGL(k_ev_tiles, dim3(1), dim3(kER), 0, st, a.tile_sum, a.tiles, a.ev_total, a.tile_off, a.arena_n,
+                       a.arena_cap, a.out_cap, a.out_pos ? 1 : 0, a.err);
+    if (a.out_pos) {
+      hipLaunchKernelGGL(k_ev_chist, dim3(chunks), dim3(kEC), 0, st, a.arena, a.arena_n, a.arena_cap, a.tiles, a.ccnt);
+      hipLaunchKernelGGL(k_ev_cscan, dim3(a.tiles), dim3(kEC), 0, st, a.arena_n, a.arena_cap, a.tiles, a.tile_off, a.ccnt);
+      hipLaunchKernelGGL(k_ev_place, dim3(chunks), dim3(kEC), 0, st, a.arena, a.arena_n, a.arena_cap, a.tiles, a.ccnt,
+                         a.bucket);
+      hipLaunchKernelGGL(k_ev_tile_out, dim3(a.tiles), dim3(kER), 0, st, a.cpos, a.hi - a.lo, a.ev_cnt, a.tile_sum,
+                         a.tile_off, a.bucket, a.arena_n, a.arena_cap, a.lo, a.out_cap, a.out_pos, a.out_target, a.out_code,
+                         a.out_src, a.out_tag, a.out_payload);
+    }
+    a.mark(K_EVENTS, 0, st);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   hipLaunchKernelGGL(k_ev_rows, dim3(a.tiles), dim3(kER), 0, st, a.cpos, a.hi - a.lo, a.ev_cnt, a.row_of, a.ev_loc,
                      a.tile_sum);
   hipLaunchKernelGGL(k_ev_tiles, dim3(1), dim3(kER), 0, st, a.tile_sum, a.tiles, a.ev_total, a.tile_off, a.arena_n,

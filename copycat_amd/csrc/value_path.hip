@@ -21,6 +21,17 @@
 
 namespace cc {
 
+#ifdef CC_PHASE_TIMING  // diagnostics build: phase clocks of k_part_v3 (g_ph_v3p) and k_apply_value_v3 (g_ph_v3a)
+__device__ unsigned long long g_ph_v3p[kPhases], g_ph_v3a[kPhases];
+int phase_read_v3(int kernel, uint64_t* out) {
+  unsigned long long z[kPhases] = {};
+  const void* sym = kernel == K_PART_TILE ? HIP_SYMBOL(g_ph_v3p) : HIP_SYMBOL(g_ph_v3a);
+  if (hipMemcpyFromSymbol(out, sym, sizeof z) != hipSuccess || hipMemcpyToSymbol(sym, z, sizeof z) != hipSuccess)
+    return CC_ERR_HIP;
+  return CC_OK;
+}
+#endif
+
 constexpr int kV3T = 512;                 // partition / unpermute workgroup threads
 constexpr int kV3W = kV3T / kWave;        // 8 waves
 constexpr int kV3J = 4;                   // commits per thread per chunk
@@ -32,7 +43,7 @@ static_assert(kV3N == 4, "k_part_v3 keeps 4 chunks x 4 commits per thread in reg
 // w0 = the payload the op carries (CAS: canonical expected value; set / getAndSet: canonical new value; else 0)
 // w1 = meta (18 bits) | row (13 bits) << 18 | delta (33 bits) << 31
 //   meta: slot-in-super-bucket 0..7 | class 8..10 | compare tag 11..13 | new tag 14..16 | escaped 17
-//   row: the commit's row in its 8192-commit tile (results written straight to log order; escaped updates)
+//   row: the commit's row in its 8192-commit tile (where an escaped CAS's update is read from)
 //   delta (CAS): update - expected, two's complement; escaped (does not fit): the update is read from the b column
 enum : uint32_t { kC3Get = 0, kC3Set = 1, kC3Cas = 2, kC3Gas = 3, kC3Del = 4, kC3Lis = 5, kC3Unk = 6 };
 constexpr int kV3DeltaBits = 33;
@@ -108,16 +119,13 @@ __device__ inline void v3_decode(const uint4& r, const uint64_t* __restrict__ cb
 // each wave (LDS atomics with return: same-address lanes of one instruction resolve in lane order, checked at engine
 // start), one wave takes the per-wave prefixes and chunk-sorted run starts, records are placed in LDS in sorted
 // order and written out run by run (contiguous 16-byte stores).  The input columns are read once: non-temporal loads.
-// SCATTER: the apply writes every result straight to its log row (no cpos, no unpermute); the partition answers the
-// unknown-session rows itself.
-template <int KP, bool SCATTER>
+template <int KP>
 __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                     const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                     const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
                                                     const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
                                                     uint4* __restrict__ st_rec, uint16_t* __restrict__ cpos,
-                                                    uint16_t* __restrict__ ttab, uint8_t* __restrict__ out_status,
-                                                    uint64_t* __restrict__ out_value) {
+                                                    uint16_t* __restrict__ ttab) {
   __shared__ uint4 rab[kV3C];                  // the chunk in sorted order
   __shared__ uint16_t rsb[kV3C];               //   super-bucket
   __shared__ uint32_t wc[kV3W][kMaxSb / 2];    // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
@@ -126,6 +134,7 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
   __shared__ uint16_t kst[kMaxSb];             // chunk-sorted start of run k
   __shared__ uint32_t nlive_s;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  PH_DECL
   const uint32_t hw = (sb + 1) / 2;
   const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kV3Tile;
   const uint32_t tbase = blockIdx.x * kV3Tile;  // staging region of this tile (relative to lo)
@@ -197,6 +206,7 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
     }
     if (l == 63) row[sb] = (uint16_t)inc;  // live commits of the tile (<= 8192)
   }
+  PH(0);
   // (tpos is first read after the next barrier; wave 0 wrote it before its first chunk barrier)
 #pragma unroll
   for (int c = 0; c < kV3N; ++c) {
@@ -212,6 +222,7 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
       loc[j] = live ? (atomicAdd(&wc[w][sk[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
     }
     if (c + 1 < kV3N) load_raw(c + 1);
+    PH(1);
     lds_barrier();  // B1: the chunk's counters are complete
     if (w == 0) {  // per super-bucket: exclusive prefix over the waves (in place), chunk totals, chunk-sorted starts
       uint32_t tot[KP];
@@ -248,6 +259,7 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
       }
       if (l == 63) nlive_s = inc;
     }
+    PH(2);
     lds_barrier();  // B2: prefixes, kst, nlive_s
     // place the records in sorted order; every commit's tile-local position (0xFFFF: unknown instance)
 #pragma unroll
@@ -262,15 +274,9 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
         rsb[sp] = (uint16_t)k;
         cp = tpos[k] + pre + loc[j];
       }
-      if (SCATTER) {
-        if (q < nrow && cp == 0xFFFFu) {  // unknown instance: ResourceManager.java:60-69
-          out_status[tile0 + q] = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
-          out_value[tile0 + q] = 0;
-        }
-      } else if (q < nrow) {
-        cpos[tbase + q] = (uint16_t)cp;
-      }
+      if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
     }
+    PH(3);
     lds_barrier();  // B3: rab / rsb complete; every wave is done reading wc and tpos of this chunk
     // write the chunk out run by run (contiguous); the next chunk's counters are cleared behind the reads
     const uint32_t nl = nlive_s;
@@ -279,6 +285,7 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
       st_rec[tbase + tpos[k] + (sp - kst[k])] = rab[sp];
     }
     for (uint32_t k = t; k < (uint32_t)(kV3W * hw); k += kV3T) wc[k / hw][k % hw] = 0;
+    PH(4);
     lds_barrier();  // B4: the write-out is done reading tpos / kst / rab; counters cleared
     if (w == 0) {  // run k's next piece starts after this chunk's records of k
 #pragma unroll
@@ -288,7 +295,9 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
       }
     }
     // (tpos is next read after the next chunk's B1; kst and nlive_s are rewritten by wave 0 after B1 as well)
+    PH(5);
   }
+  PH_FLUSH(g_ph_v3p);
 }
 
 // ---- k_apply_value_v3: walker / loader waves (apply_value.hip k_apply_value_ws) over 16-byte records -----------
@@ -345,17 +354,14 @@ __device__ inline void v3_loader_barrier(uint32_t* ctr, uint32_t target) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// SCATTER: results go straight to the caller's columns at the record's log row (out + lo + T*8192 + row).
-template <bool SCATTER>
 __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict__ st_rec, const uint64_t* __restrict__ cb,
                                                         uint64_t lo, const uint16_t* __restrict__ ttab, uint32_t tiles,
                                                         uint32_t sb, uint32_t* __restrict__ val_meta,
                                                         uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
                                                         uint64_t* __restrict__ rst_value, uint64_t dummy,
-                                                        uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value,
                                                         uint32_t* __restrict__ err_out) {
-  __shared__ u64x2 sab[2][kWsCh];               // chunk buffers sorted by slot; results in place (value -> .x)
-  __shared__ uint32_t sm[2][kWsCh];             //   meta words; results in place (status)
+  __shared__ u64x2 sab[2][kWsCh];               // chunk buffers sorted by slot; results in place {value, status}
+  __shared__ uint32_t sm[2][kWsCh];             //   meta words
   __shared__ uint32_t wcnt[2][kWsLW][kVPairs3];  // per-loader-wave slot counts (packed u16 pairs), double-buffered
   __shared__ uint16_t pbase[kWsLW][kVSlots3];   // per loader wave: sorted position of its first record of each slot
   __shared__ uint32_t sstart[2][kVSlots3 + 1];  // slot run starts of each buffer (+ total)
@@ -410,6 +416,20 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
   const uint32_t cnt = rpre[tiles];
   const uint32_t nch = (cnt + kWsCh - 1) / kWsCh;
   uint32_t err = 0;
+#ifdef CC_PHASE_TIMING
+  // thread 0 (walker): 0 walk, 1 wait; thread 256 (loader): 2 result store, 3 rank, 4 loader + workgroup barriers,
+  // 5 clear + placement bases, 6 decode + place, 7 load issue
+  uint64_t wph_last = wall_clock64(), wph[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto WPH = [&](int k) {
+    if (t == 0 || t == 4 * kWave) {
+      const uint64_t n_ = wall_clock64();
+      wph[k] += n_ - wph_last;
+      wph_last = n_;
+    }
+  };
+#else
+  auto WPH = [&](int) {};
+#endif
 
   // loader registers: the chunk to place next (rr, g; loaded one chunk ahead), the sorted / staging positions of the
   // chunk being walked (pp, gp) and of the chunk before it (qp, gq: its results are stored during the walk)
@@ -475,8 +495,10 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
       const uint32_t sh = 16 * (slot[j] & 1);
       rank[j] = gv[j] != kNoPos3 ? (atomicAdd(&wcnt[b][lw][slot[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
     }
+    WPH(3);
     bar_n += kWsLW;
     v3_loader_barrier(&lbar, bar_n);  // every loader wave has ranked this chunk into wcnt[b]
+    WPH(4);
     // the other counter buffer was last read before the previous workgroup barrier: clear it for the next chunk
     for (uint32_t k = t - 4 * kWave; k < (uint32_t)(kWsLW * kVPairs3); k += kWsLW * kWave) (&wcnt[b ^ 1][0][0])[k] = 0;
     // this wave's placement bases: lane l owns slots 4l..4l+3 (counter pairs 2l, 2l+1)
@@ -512,6 +534,7 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
       sstart[b][4 * l + 3] = s3;
       if (l == 63) sstart[b][kVSlots3] = inc;
     }
+    WPH(5);
     // lanes read bases other lanes of this wave just wrote: LDS keeps one wave's accesses in order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
@@ -519,7 +542,7 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
 #define CC_PLACE1(J)                                                                \
     {                                                                               \
       pp##J = 0;                                                                    \
-      gp##J = SCATTER && g##J != kNoPos3 ? g##J / kV3Tile * kV3Tile + v3_row(rr##J) : g##J; \
+      gp##J = g##J;                                                                 \
       if (g##J != kNoPos3) {                                                        \
         uint32_t m_;                                                                \
         uint64_t x_, y_;                                                            \
@@ -531,16 +554,16 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
     }
     CC_J4(CC_PLACE1)
 #undef CC_PLACE1
+    WPH(6);
   };
   // the previous chunk's results (buffer b) back to the records' staging positions; unconditional stores
   auto store_results = [&](uint32_t b) {
 #define CC_STORE1(J)                                                                \
     {                                                                               \
-      const bool ok_ = gq##J != kNoPos3;                                            \
-      uint8_t* ds_ = SCATTER && ok_ ? out_status + lo + gq##J : rst_status + (ok_ ? (uint64_t)gq##J : dummy + t); \
-      uint64_t* dv_ = SCATTER && ok_ ? out_value + lo + gq##J : rst_value + (ok_ ? (uint64_t)gq##J : dummy + t); \
-      *ds_ = (uint8_t)sm[b][qp##J];                                                 \
-      *dv_ = sab[b][qp##J].x;                                                       \
+      const uint64_t gx = gq##J != kNoPos3 ? (uint64_t)gq##J : dummy + t;           \
+      const u64x2 r_ = sab[b][qp##J];                                               \
+      rst_status[gx] = (uint8_t)r_.y;                                               \
+      rst_value[gx] = r_.x;                                                         \
     }
     CC_J4(CC_STORE1)
 #undef CC_STORE1
@@ -575,8 +598,10 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
               uint64_t rv;
               const uint32_t stt = v3_value_walk(mm[q], xx[q].x, xx[q].y, ms, sv, rv);
               if (mm[q] & kVrL) err |= kErrUnsupported;
-              sm[b][start + k0 + q] = stt;
-              sab[b][start + k0 + q].x = rv;
+              // the result over the record, one 16-byte LDS write: with 2 reads + 1 write per record, a group of 4
+              // records' reads plus the previous group's writes stay within the 15 outstanding LDS operations a
+              // wave can wait on precisely (two writes per record overflowed it and serialised the pipeline)
+              sab[b][start + k0 + q] = u64x2{rv, (uint64_t)stt};
             }
           }
         };
@@ -591,15 +616,23 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
       }
     } else {
       store_results(b ^ 1);  // chunk i-1 (i = 0: the dummy rows)
+      WPH(2);
 #define CC_SHIFT1(J) qp##J = pp##J; gq##J = gp##J;
       CC_J4(CC_SHIFT1)
 #undef CC_SHIFT1
       prepare(b ^ 1);        // chunk i+1 (past the end: no live records)
       CC_LOAD_CHUNK((i + 2) * kWsCh)
+      WPH(7);
     }
+    if (walker) WPH(0);
     lds_barrier();  // buffer hand-over: b walked (results in place), b^1 placed
+    WPH(walker ? 1 : 4);
   }
   if (!walker && nch) store_results((nch - 1) & 1);  // the last chunk (qp / gq since its walk)
+#ifdef CC_PHASE_TIMING
+  if (t == 0 || t == 4 * kWave)
+    for (int q = 0; q < kPhases; ++q) atomicAdd(&g_ph_v3a[q], (unsigned long long)wph[q]);
+#endif
 #undef CC_LOAD_CHUNK
 #undef CC_LOAD1
 #undef CC_J4
@@ -613,33 +646,20 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
   if (a.sb > (uint32_t)kMaxSb || tiles > (uint32_t)kV3MaxTiles) return -1;
-#define CC_LAUNCH(KP, SC)                                                                                             \
-  hipLaunchKernelGGL((k_part_v3<KP, SC>), dim3(tiles), dim3(kV3T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi, \
-                     a.inst_res, a.max_inst, a.sb, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab, a.out_status,   \
-                     a.out_value)
-  if (a.v3_scatter) {
-    if (kp <= 2) CC_LAUNCH(2, true);
-    else if (kp <= 4) CC_LAUNCH(4, true);
-    else CC_LAUNCH(8, true);
-  } else {
-    if (kp <= 2) CC_LAUNCH(2, false);
-    else if (kp <= 4) CC_LAUNCH(4, false);
-    else CC_LAUNCH(8, false);
-  }
+#define CC_LAUNCH(KP)                                                                                                 \
+  hipLaunchKernelGGL((k_part_v3<KP>), dim3(tiles), dim3(kV3T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,    \
+                     a.inst_res, a.max_inst, a.sb, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
+  if (kp <= 2) CC_LAUNCH(2);
+  else if (kp <= 4) CC_LAUNCH(4);
+  else CC_LAUNCH(8);
 #undef CC_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
   if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
-  if (a.v3_scatter)
-    hipLaunchKernelGGL(k_apply_value_v3<true>, dim3(a.sb_val), dim3(kAVT), 0, st, reinterpret_cast<const uint4*>(a.st_ab),
-                       a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy,
-                       a.out_status, a.out_value, a.err);
-  else
-    hipLaunchKernelGGL(k_apply_value_v3<false>, dim3(a.sb_val), dim3(kAVT), 0, st, reinterpret_cast<const uint4*>(a.st_ab),
-                       a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy,
-                       a.out_status, a.out_value, a.err);
+  hipLaunchKernelGGL(k_apply_value_v3, dim3(a.sb_val), dim3(kAVT), 0, st, reinterpret_cast<const uint4*>(a.st_ab), a.cb,
+                     a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

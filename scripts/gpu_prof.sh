@@ -1,0 +1,39 @@
+#!/bin/bash
+# Profile one workload: kernel trace + stats, then separate --pmc passes (HBM bytes, SQ instruction mix, LDS waits).
+# Big raw CSVs are summarised on the box and removed (gpurun copies back at most 64 MiB).
+# Usage (via gpurun): bash scripts/gpu_prof.sh TAG [bench args...]     e.g. gpu_prof.sh p_c2 --steps 2 --warmup 1
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+BA="--no-cpu-baseline --no-parity --no-e2e $@"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/kt -o run --output-format csv -- python3 $R/bench.py $BA > $R/$OUT/kt.log 2>&1 || { echo kt failed; tail -3 $R/$OUT/kt.log; exit 1; }
+tail -1 $R/$OUT/kt.log | cut -c1-300
+STATS=$(find $R/$OUT/kt -name "*kernel_stats.csv" | head -1)
+cp $STATS $R/$OUT/kernel_stats.csv
+find $R/$OUT/kt -name "*kernel_trace.csv" -delete
+i=0
+for CNT in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU" "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY"; do
+  i=$((i+1))
+  timeout -s KILL 240 rocprofv3 --pmc $CNT -d $R/$OUT/pmc$i -o run --output-format csv -- python3 $R/bench.py $BA > $R/$OUT/pmc$i.log 2>&1 || { echo "pmc $i ($CNT) failed"; tail -3 $R/$OUT/pmc$i.log; }
+  (cd $R && python3 scripts/pmc_kernel_summary.py $OUT/pmc$i > $OUT/pmc${i}_summary.txt 2>&1)
+  find $R/$OUT/pmc$i -name "*.csv" -delete
+done
+cd $R && python3 - <<'PY' > $OUT/kt_summary.txt
+import csv, sys
+rows = list(csv.DictReader(open("$OUT/kernel_stats.csv".replace("$OUT", sys.argv[1] if len(sys.argv) > 1 else "$OUT"))))
+PY
+python3 -c "
+import csv
+rows = list(csv.DictReader(open('$OUT/kernel_stats.csv')))
+print(f\"{'kernel':44s} {'calls':>6s} {'avg_us':>10s} {'total_ms':>10s}\")
+for r in rows:
+    n = r['Name'].split('(')[0].replace('void ', '').replace('cc::', '')
+    print(f\"{n[:44]:44s} {r['Calls']:>6s} {float(r['AverageNs'])/1e3:10.1f} {float(r['TotalDurationNs'])/1e6:10.3f}\")
+" > $OUT/kt_summary.txt
+head -25 $OUT/kt_summary.txt
+du -sh $OUT
+echo done

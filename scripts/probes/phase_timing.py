@@ -77,6 +77,10 @@ def run(args):
     tiles = (n + 16383) // 16384
     if os.environ.get("CC_PART_VALUE"):
         PHASES[0] = PHASES_PARTV
+    if os.environ.get("CC_V3_PHASES"):  # value_path.hip: k_part_v3 (two 512-thread workgroups per CU, 8192-commit tiles)
+        PHASES[0] = ["prologue loads+gather+hist", "encode+rank+issue", "B1+wave scan", "B2+place+cpos",
+                     "B3+write-out+clear", "B4+tpos", "-", "-"]
+        tiles = (n + 8191) // 8192
     if os.environ.get("CC_PART_V2_PHASES"):  # k_part_v2 (one workgroup per tile)
         PHASES[0] = ["prologue loads+gather", "histogram+row", "encode+rank", "issue next+barrier", "wave scan",
                      "place+cpos", "write-out+clear", "-"]
