@@ -67,15 +67,19 @@ RESULT_SENTINEL = 0xFF  # result prefill: status 0xFF (tag nibble 15) is never a
 # the kernels behind each cc_profile marker (the value-only partition is k_part_v2; engines with maps, coordination
 # or value events use k_part_tile)
 # the kernels each profiling marker spans (their HBM traffic adds up); the first present partition kernel is the one
-MARKER_KERNELS = {"k_part_tile": ("k_part_ext", "k_part_v2", "k_part_tile"), "k_events": ("k_ev_rows", "k_ev_perm", "k_ev_out"),
+MARKER_KERNELS = {"k_part_tile": ("k_part_v3", "k_part_ext", "k_part_v2", "k_part_tile"),
+                  "k_apply_value": ("k_apply_value_v3", "k_apply_value_ws", "k_apply_value"),
+                  "k_events": ("k_ev_count", "k_ev_tiles", "k_ev_chist", "k_ev_cscan", "k_ev_place", "k_ev_tile_out",
+                               "k_ev_rows", "k_ev_perm", "k_ev_out"),
                   "k_map_hot": ("k_hot_detect", "k_hot_agg", "k_hot_lists", "k_hot_apply")}
 MARKER_SUM = {"k_events", "k_map_hot"}
 # the rocprofv3 kernel name(s) behind a profiling marker, per workload (the marker names are the engine's
 # profile slots; the partition slot runs k_part_v2 on value-only engines and k_part_ext otherwise)
-TRACE_NAMES = {"k_part_tile": {"c2": "k_part_v2<4>", "c3": "k_part_ext", "c5": "k_part_ext"},
-               "k_apply_value": {"c2": "k_apply_value_ws"}, "k_apply_map": {"c3": "k_apply_map<false>"},
+TRACE_NAMES = {"k_part_tile": {"c2": "k_part_v3<4>", "c3": "k_part_ext", "c5": "k_part_ext"},
+               "k_apply_value": {"c2": "k_apply_value_v3"}, "k_apply_map": {"c3": "k_apply_map<false>"},
+               "k_unpermute": {"c2": "k_unpermute<512, 8192>", "c3": "k_unpermute<1024, 16384>", "c5": "k_unpermute<1024, 16384>"},
                "k_map_hot": {"c3": "k_hot_detect + k_hot_lists + k_hot_agg + k_hot_apply"},
-               "k_events": {"c5": "k_ev_rows + k_ev_perm + k_ev_out"}}
+               "k_events": {"c5": "k_ev_count + k_ev_tiles + k_ev_chist + k_ev_cscan + k_ev_place + k_ev_tile_out"}}
 
 
 def trace_name(marker, workload):
@@ -230,12 +234,28 @@ def run_c4(args, dev, rank, world, dist):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    q_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    x_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    # Per-kernel launch durations: each kernel alone, back to back over the resident input sets, between one event
+    # pair (an event pair around every ~15 us launch adds its own few us).  k_quorum moves 88% of the algorithmic
+    # bytes (64 B/group vs 8.125 B/session): it is the roofline kernel; k_expire is launch-latency bound (8.5 MB).
+    reps = 64
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record(stream)
+    for k in range(reps):
+        d_match, d_ts, d_ci, d_last = sets[k % nsets]
+        quorum_commit(d_match, d_ts, d_ci, d_out, stream=stream)
+    e1.record(stream)
+    for k in range(reps):
+        d_match, d_ts, d_ci, d_last = sets[k % nsets]
+        expire_sweep(d_last, now, timeout, d_bm, d_cnt, stream=stream)
+    e2.record(stream)
+    torch.cuda.synchronize(dev)
+    q_ms, x_ms = e0.elapsed_time(e1) / reps, e1.elapsed_time(e2) / reps
+    step_q_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    step_x_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
     q_gbps = 64 * G / (q_ms * 1e-3) / 1e9
     x_gbps = 8.125 * S / (x_ms * 1e-3) / 1e9
-    dom = "k_quorum" if q_ms >= x_ms else "k_expire"
-    ach = q_gbps if dom == "k_quorum" else x_gbps
+    dom = "k_quorum"
+    ach = q_gbps
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle_py import expire_sweep as ox
@@ -262,9 +282,14 @@ def run_c4(args, dev, rank, world, dist):
                        "input_sets": nsets, "input_set_mb": round((64 + 8) * G / 1e6, 1),
                        "note": "steps take the resident input sets in turn; with >= 4 sets a step's inputs are not in "
                                "the 256 MiB Infinity Cache"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+            "roofline": {"bound": "hbm", "kernel": dom, "trace_name": "k_quorum<5>", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": pmc_traffic("k_quorum", "c4"),
+                         "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
+                         "alg_gb_per_launch": round(64 * G / 1e9, 4), "avg_launch_ms": round(q_ms, 5),
+                         "timing": f"{reps} back-to-back launches of each kernel over the resident input sets, one event pair",
                          "per_kernel_ms": {"k_quorum": round(q_ms, 5), "k_expire": round(x_ms, 5)},
+                         "per_step_event_ms": {"k_quorum": round(step_q_ms, 5), "k_expire": round(step_x_ms, 5)},
                          "per_kernel_gbps": {"k_quorum": round(q_gbps, 1), "k_expire": round(x_gbps, 1)},
                          "bytes_per_unit": {"group": 64, "session": 8.125}},
             "parity": parity, "cpu_baseline": cpu,

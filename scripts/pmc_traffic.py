@@ -27,9 +27,24 @@ def per_kernel(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def per_kernel_summary(path, counter):
+    """scripts/gpu_prof.sh's on-box summary (scripts/pmc_kernel_summary.py output): kernel line, then counter lines."""
+    res, cur = {}, None
+    for line in open(path):
+        if not line.startswith(" "):
+            cur = line.strip().split("<")[0]
+        elif cur and line.split()[0] == counter:
+            res[cur] = float(line.split("avg=")[1])
+    return res
+
+
 def main(d, out, workload="c2"):
-    f = per_kernel(os.path.join(d, "fetch", "run_counter_collection.csv"))
-    w = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
+    if os.path.exists(os.path.join(d, "pmc1_summary.txt")):  # scripts/gpu_prof.sh layout
+        f = per_kernel_summary(os.path.join(d, "pmc1_summary.txt"), "FETCH_SIZE")
+        w = per_kernel_summary(os.path.join(d, "pmc2_summary.txt"), "WRITE_SIZE")
+    else:
+        f = per_kernel(os.path.join(d, "fetch", "run_counter_collection.csv"))
+        w = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
     res = {}
     for k in sorted(set(f) | set(w)):
         fk, wk = f.get(k, 0.0), w.get(k, 0.0)
