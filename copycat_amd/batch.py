@@ -40,7 +40,7 @@ class Batch:
     def slice(self, lo, hi):
         b = Batch(0)
         for name, _ in abi.BATCH_COLUMNS:
-            setattr(b, name, np.ascontiguousarray(getattr(self, name)[lo:hi]))
+            setattr(b, name, getattr(self, name)[lo:hi].copy())  # a copy: callers reuse the source buffer
         return b
 
     def columns(self):

@@ -300,6 +300,138 @@ __global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict_
   PH_FLUSH(g_ph_v3p);
 }
 
+// ---- k_part_v4: one persistent 1024-thread workgroup per CU, one pass per 8192-commit tile --------------------
+// Same output as k_part_v3 (the tile's records grouped by super-bucket in log order, its ttab row and cpos), but
+// the whole tile is ranked at once and placed into a 128 KiB LDS image of the tile's staging region, which is then
+// written out contiguously: every 128-byte line of the staging area is written whole by one instruction (k_part_v3
+// wrote each run piece per 2048-commit chunk, and lines shared by two pieces reached HBM as partial writes: 22.6 B
+// written per commit for 18).  Thread (w, j, l) holds commit w*512 + j*64 + l of the tile in registers (the
+// tile's rows are wave-contiguous, so per-wave lane-ordered counters give a stable rank); after the placement the
+// registers take the NEXT tile's loads, which are in flight while this tile's image is written out.
+// LDS hazards: each wave zeroes its own counter row at the top of a tile (its previous readers -- wave 0's scan and
+// the wave's own placement -- finished before the previous tile's B3); img / kst are rewritten only after the next
+// tile's B1 / B2, which every thread reaches after its own write-out reads.
+constexpr int kP4T = 1024;
+constexpr int kP4W = kP4T / kWave;    // 16 waves
+constexpr int kP4J = kV3Tile / kP4T;  // 8 commits per thread
+static_assert(kP4J == 8, "k_part_v4 keeps 8 commits per thread in registers");
+
+template <int KP>
+__global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                                                const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
+                                                const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
+                                                const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
+                                                uint32_t tiles, uint4* __restrict__ st_rec, uint16_t* __restrict__ cpos,
+                                                uint16_t* __restrict__ ttab) {
+  __shared__ uint4 img[kV3Tile];             // the tile's records in staging order
+  __shared__ uint32_t wc[kP4W][kMaxSb / 2];  // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
+  __shared__ uint16_t kst[kMaxSb + 1];       // tile-local run starts (+ live count)
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  const uint32_t hw = (sb + 1) / 2;
+  uint32_t T = blockIdx.x;
+  if (T >= tiles) return;
+  uint32_t ri[kP4J], ob[kP4J], fb[kP4J];
+  uint64_t av[kP4J], bv[kP4J];
+  auto rowq = [&](int j) -> uint32_t { return w * (kWave * kP4J) + (uint32_t)j * kWave + l; };
+  auto load = [&](uint32_t TT) {
+    const uint64_t t0 = lo + (uint64_t)TT * kV3Tile;
+    const uint32_t nr = (uint32_t)(hi - t0 < (uint64_t)kV3Tile ? hi - t0 : (uint64_t)kV3Tile);
+#pragma unroll
+    for (int j = 0; j < kP4J; ++j) {
+      const uint32_t q = rowq(j);
+      const uint64_t ic = t0 + (q < nr ? q : 0u);  // rows past the batch end re-read row 0 (ignored)
+      ri[j] = __builtin_nontemporal_load(inst + ic);
+      ob[j] = __builtin_nontemporal_load(op + ic);
+      fb[j] = __builtin_nontemporal_load(flags + ic);
+      av[j] = __builtin_nontemporal_load(ca + ic);
+      bv[j] = __builtin_nontemporal_load(cb + ic);
+    }
+  };
+  load(T);
+  for (;;) {
+    const uint64_t tile0 = lo + (uint64_t)T * kV3Tile;
+    const uint32_t tbase = T * kV3Tile;
+    const uint32_t nrow = (uint32_t)(hi - tile0 < (uint64_t)kV3Tile ? hi - tile0 : (uint64_t)kV3Tile);
+    for (uint32_t k = l; k < hw; k += kWave) wc[w][k] = 0;
+    uint32_t r[kP4J], loc[kP4J];
+#pragma unroll
+    for (int j = 0; j < kP4J; ++j) {  // instance -> resource (unconditional gathers, then the select)
+      const bool ok = rowq(j) < nrow && ri[j] < max_inst;
+      const uint32_t g = inst_res[ok ? ri[j] : 0u];
+      r[j] = ok ? g : kNoRes;
+    }
+#pragma unroll
+    for (int j = 0; j < kP4J; ++j) {
+      const uint32_t k = r[j] >> kSbShift, sh = 16 * (k & 1);
+      loc[j] = r[j] != kNoRes ? (atomicAdd(&wc[w][k >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
+    }
+    lds_barrier();  // B1: counters complete
+    if (w == 0) {   // per super-bucket: exclusive prefix over the waves (in place), totals, tile-local run starts
+      uint32_t tot[KP];
+#pragma unroll
+      for (int e = 0; e < KP; e += 2) {
+        const uint32_t pr = (l * KP + e) / 2;
+        uint32_t acc = 0;
+        if (pr < hw) {
+#pragma unroll
+          for (int q = 0; q < kP4W; ++q) {
+            const uint32_t x = wc[q][pr];
+            wc[q][pr] = acc;
+            acc += x;
+          }
+        }
+        tot[e] = acc & 0xFFFFu;
+        tot[e + 1] = acc >> 16;
+      }
+      uint32_t mine = 0;
+#pragma unroll
+      for (int e = 0; e < KP; ++e) mine += tot[e];
+      uint32_t inc = mine;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      uint32_t run = inc - mine;
+      uint16_t* row = ttab + (uint64_t)T * (sb + 1);
+#pragma unroll
+      for (int e = 0; e < KP; ++e) {
+        const uint32_t k = l * KP + e;
+        if (k < sb) {
+          kst[k] = (uint16_t)run;
+          row[k] = (uint16_t)run;
+        }
+        run += tot[e];
+      }
+      if (l == 63) {
+        kst[sb] = (uint16_t)inc;
+        row[sb] = (uint16_t)inc;
+      }
+    }
+    lds_barrier();  // B2: prefixes and run starts
+#pragma unroll
+    for (int j = 0; j < kP4J; ++j) {
+      const uint32_t q = rowq(j);
+      uint32_t cp = 0xFFFFu;
+      if (loc[j] != 0xFFFFu) {
+        const uint32_t k = r[j] >> kSbShift, sh = 16 * (k & 1);
+        const uint32_t sp = kst[k] + ((wc[w][k >> 1] >> sh) & 0xFFFFu) + loc[j];
+        img[sp] = v3_set_row(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << kSbShift) - 1)), q);
+        cp = sp;
+      }
+      if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
+    }
+    const uint32_t Tn = T + gridDim.x;
+    if (Tn < tiles) load(Tn);  // the raw registers are free: the next tile's loads fly during the write-out
+    lds_barrier();             // B3: the image is complete
+    // whole tile region, unconditionally (a fixed store count; rows past the live count are never read)
+#pragma unroll
+    for (int m = 0; m < kP4J; ++m) st_rec[tbase + t + m * kP4T] = img[t + m * kP4T];
+    if (Tn >= tiles) break;
+    T = Tn;
+  }
+}
+
 // ---- k_apply_value_v3: walker / loader waves (apply_value.hip k_apply_value_ws) over 16-byte records -----------
 // One 1024-thread workgroup per super-bucket: waves 0-3 walk (thread t = slot t, AtomicValueState in registers),
 // waves 4-15 load, decode, rank and place the next chunk (3072 records) into the other LDS buffer and store the
@@ -646,7 +778,19 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
   if (a.sb > (uint32_t)kMaxSb || tiles > (uint32_t)kV3MaxTiles) return -1;
-#define CC_LAUNCH(KP)                                                                                                 \
+  static const bool v3_part = getenv("CC_PART_V3") != nullptr;  // A/B: the chunked 512-thread partition
+  if (!v3_part) {
+    const uint32_t grid = tiles < (uint32_t)kPersistGrid ? tiles : (uint32_t)kPersistGrid;
+#define CC_LAUNCH4(KP)                                                                                                \
+  hipLaunchKernelGGL((k_part_v4<KP>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,     \
+                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
+    if (kp <= 2) CC_LAUNCH4(2);
+    else if (kp <= 4) CC_LAUNCH4(4);
+    else CC_LAUNCH4(8);
+#undef CC_LAUNCH4
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+#define CC_LAUNCH(KP)                                                                                               \
   hipLaunchKernelGGL((k_part_v3<KP>), dim3(tiles), dim3(kV3T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,    \
                      a.inst_res, a.max_inst, a.sb, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
   if (kp <= 2) CC_LAUNCH(2);
