@@ -227,7 +227,8 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_st_meta, sizeof(uint32_t) * (e->sub_batch + kPT));  // + dummy rows for unconditional stores
   ALLOC(e->d_st_ab, sizeof(u64x2) * (e->sub_batch + kPT));
   ALLOC(e->d_cpos, sizeof(uint16_t) * e->sub_batch);
-  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sbq_base() + 4 * e->sb + 1));
+  // (value-only engines: 2 tiles of 8192 per 16384 and 128-slot buckets -> 2 x (2 sb + 1) entries per 16384 commits)
+  ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sbq_base() + 4 * e->sb + 2));
   if (e->map_bits) {
     ALLOC(e->d_tbl_key, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_tbl_word, sizeof(uint32_t) * e->map_entries);

@@ -316,7 +316,7 @@ constexpr int kP4W = kP4T / kWave;    // 16 waves
 constexpr int kP4J = kV3Tile / kP4T;  // 8 commits per thread
 static_assert(kP4J == 8, "k_part_v4 keeps 8 commits per thread in registers");
 
-template <int KP>
+template <int KP, int KSB>
 __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                 const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
     }
 #pragma unroll
     for (int j = 0; j < kP4J; ++j) {
-      const uint32_t k = r[j] >> kSbShift, sh = 16 * (k & 1);
+      const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
       loc[j] = r[j] != kNoRes ? (atomicAdd(&wc[w][k >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
     }
     lds_barrier();  // B1: counters complete
@@ -414,9 +414,9 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
       const uint32_t q = rowq(j);
       uint32_t cp = 0xFFFFu;
       if (loc[j] != 0xFFFFu) {
-        const uint32_t k = r[j] >> kSbShift, sh = 16 * (k & 1);
+        const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
         const uint32_t sp = kst[k] + ((wc[w][k >> 1] >> sh) & 0xFFFFu) + loc[j];
-        img[sp] = v3_set_row(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << kSbShift) - 1)), q);
+        img[sp] = v3_set_row(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << KSB) - 1)), q);
         cp = sp;
       }
       if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
@@ -445,14 +445,25 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
 //     loader wave reaches after its own ranking of the same chunk; wcnt[b^1] is cleared after that arrival barrier,
 //     and was last read (placement bases of the chunk before) before the previous workgroup barrier;
 //   * rstart / rpre (the run table) are written once, before the first workgroup barrier, and never rebuilt.
-constexpr int kWsLW = 12;
 constexpr int kWsPer = 4;
-constexpr int kWsCh = kWsLW * kWave * kWsPer;  // 3072 records per chunk
-constexpr int kAVT = 1024;
-constexpr int kAVW = kAVT / kWave;
-constexpr int kVSlots3 = 1 << kSbShift;
-constexpr int kVPairs3 = kVSlots3 / 2;
 constexpr uint32_t kNoPos3 = 0xFFFFFFFFu;
+// NS slots per super-bucket: 256 (1024-thread workgroups: 4 walker + 12 loader waves, 3072-record chunks, one
+// workgroup per CU) or 128 (512-thread workgroups: 2 walker + 6 loader waves, 1536-record chunks, 79 KB of LDS: two
+// workgroups per CU, so one workgroup's per-chunk loader chain -- rank, arrival barrier, placement bases, placement
+// -- overlaps the other's; with one workgroup per CU that chain, not the bytes, bounded the launch: 0.60 ms/step
+// with contiguous loads and no walk at all, profiles/r03/diag1).
+template <int NS>
+struct V3A {
+  static constexpr int WW = NS / kWave;               // walker waves
+  static constexpr int LW = NS == 128 ? 6 : 12;       // loader waves
+  static constexpr int T = (WW + LW) * kWave;         // workgroup threads
+  static constexpr int W = T / kWave;
+  static constexpr int CH = LW * kWave * kWsPer;      // records per chunk
+  static constexpr int NP = NS / 2;                   // packed u16 counter pairs
+  static constexpr int SPL = NS / kWave;              // slots per loader lane in the placement bases
+  static constexpr int TPT = (kV3MaxTiles + T - 1) / T;  // run-table tiles per thread
+  static constexpr int MINW = NS == 128 ? 4 : 1;      // waves per SIMD asked of the register allocator
+};
 
 __device__ inline uint32_t v3_value_walk(uint32_t m, uint64_t x, uint64_t y, uint32_t& ms, uint64_t& v, uint64_t& rv) {
   const uint32_t tag = ms & 0xFFu;
@@ -486,25 +497,30 @@ __device__ inline void v3_loader_barrier(uint32_t* ctr, uint32_t target) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict__ st_rec, const uint64_t* __restrict__ cb,
+template <int NS>
+__global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(const uint4* __restrict__ st_rec, const uint64_t* __restrict__ cb,
                                                         uint64_t lo, const uint16_t* __restrict__ ttab, uint32_t tiles,
                                                         uint32_t sb, uint32_t* __restrict__ val_meta,
                                                         uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
                                                         uint64_t* __restrict__ rst_value, uint64_t dummy,
-                                                        uint32_t* __restrict__ err_out) {
+                                                        uint32_t* __restrict__ err_out, uint32_t diag) {
+  using P = V3A<NS>;
+  constexpr int kWsLW = P::LW, kWsCh = P::CH, kAVT = P::T, kAVW = P::W, kVSlots3 = NS, kVPairs3 = P::NP;
+  constexpr uint32_t kL0 = P::WW * kWave;       // first loader thread
   __shared__ u64x2 sab[2][kWsCh];               // chunk buffers sorted by slot; results in place {value, status}
   __shared__ uint32_t sm[2][kWsCh];             //   meta words
   __shared__ uint32_t wcnt[2][kWsLW][kVPairs3];  // per-loader-wave slot counts (packed u16 pairs), double-buffered
   __shared__ uint16_t pbase[kWsLW][kVSlots3];   // per loader wave: sorted position of its first record of each slot
   __shared__ uint32_t sstart[2][kVSlots3 + 1];  // slot run starts of each buffer (+ total)
-  __shared__ uint32_t rstart[kV3MaxTiles];      // staging position of this super-bucket's run in tile r
+  __shared__ uint16_t rb0[kV3MaxTiles];         // start of this super-bucket's run inside tile r
   __shared__ uint32_t rpre[kV3MaxTiles + 1];    // records of this super-bucket before tile r
   __shared__ uint32_t wsum[kAVW];
   __shared__ uint32_t lbar;
+  auto rstart = [&](uint32_t r) -> uint32_t { return r * kV3Tile + rb0[r]; };  // staging position of run r
 
   const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
-  const bool walker = w < 4;
-  const uint32_t lw = walker ? 0u : w - 4;
+  const bool walker = t < kL0;
+  const uint32_t lw = walker ? 0u : w - P::WW;
   uint32_t ms = 0;
   uint64_t sv = 0;
   if (walker) {
@@ -513,20 +529,21 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
   }
   for (uint32_t k = t; k < (uint32_t)(2 * kWsLW * kVPairs3); k += kAVT) (&wcnt[0][0][0])[k] = 0;
   if (t == 0) lbar = 0;
-  {  // the super-bucket's list = its run in every tile, in tile order; thread t owns tiles 2t, 2t+1
-    uint32_t len0 = 0, len1 = 0;
+  {  // the super-bucket's list = its run in every tile, in tile order; thread t owns tiles TPT*t .. TPT*t + TPT-1
+    uint32_t len[P::TPT], lsum = 0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint32_t tt = 2 * t + q;
+    for (int q = 0; q < P::TPT; ++q) {
+      const uint32_t tt = P::TPT * t + q;
+      len[q] = 0;
       if (tt < tiles) {
         const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
         const uint32_t b0 = row[s], b1 = row[s + 1];
-        rstart[tt] = tt * kV3Tile + b0;
-        (q ? len1 : len0) = b1 - b0;
+        rb0[tt] = (uint16_t)b0;
+        len[q] = b1 - b0;
       }
+      lsum += len[q];
     }
-    const uint32_t len = len0 + len1;
-    uint32_t inc = len;
+    uint32_t inc = lsum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(inc, d, 64);
@@ -534,14 +551,17 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
     }
     if (l == 63) wsum[w] = inc;
     lds_barrier();
-    uint32_t pre = inc - len, all = 0;
+    uint32_t pre = inc - lsum, all = 0;
     for (uint32_t q = 0; q < (uint32_t)kAVW; ++q) {
       const uint32_t x = wsum[q];
       if (q < w) pre += x;
       all += x;
     }
-    if (2 * t < tiles) rpre[2 * t] = pre;
-    if (2 * t + 1 < tiles) rpre[2 * t + 1] = pre + len0;
+#pragma unroll
+    for (int q = 0; q < P::TPT; ++q) {
+      if (P::TPT * t + q < tiles) rpre[P::TPT * t + q] = pre;
+      pre += len[q];
+    }
     if (t == 0) rpre[tiles] = all;
     lds_barrier();
   }
@@ -553,7 +573,7 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
   // 5 clear + placement bases, 6 decode + place, 7 load issue
   uint64_t wph_last = wall_clock64(), wph[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto WPH = [&](int k) {
-    if (t == 0 || t == 4 * kWave) {
+    if (t == 0 || t == kL0) {
       const uint64_t n_ = wall_clock64();
       wph[k] += n_ - wph_last;
       wph_last = n_;
@@ -592,10 +612,11 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
         uint32_t r = v3_find_run(rpre, tiles, crow);                                              \
         if (c < cnt) {                                                                            \
           while (rpre[r + 1] <= c) ++r;                                                           \
-          gpos = rstart[r] + (c - rpre[r]);                                                       \
+          gpos = rstart(r) + (c - rpre[r]);                                                       \
         }                                                                                         \
       }                                                                                           \
     }                                                                                             \
+    if (diag & 2u) gpos = c < cnt ? c : 0u; /* diagnostics: contiguous positions (wrong results) */ \
     g##J = c < cnt ? gpos : kNoPos3;                                                              \
     rr##J = st_rec[gpos];                                                                         \
   }
@@ -608,7 +629,7 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
       const uint32_t rrow = v3_find_run(rpre, tiles, c0w);                                        \
       const uint32_t kr = rrow + l;                                                               \
       wB = kr + 1 <= tiles ? rpre[kr + 1] : 0xFFFFFFFFu;                                          \
-      wS = kr < tiles ? rstart[kr] : 0u;                                                          \
+      wS = kr < tiles ? rstart(kr) : 0u;                                                          \
       wP = kr < tiles ? rpre[kr] : 0u;                                                            \
       const uint32_t lastc = c0w + kWave * kWsPer - 1 < cnt ? c0w + kWave * kWsPer - 1 : cnt - 1; \
       win = (uint32_t)__shfl((int)wB, 63, 64) > lastc;                                            \
@@ -632,40 +653,42 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
     v3_loader_barrier(&lbar, bar_n);  // every loader wave has ranked this chunk into wcnt[b]
     WPH(4);
     // the other counter buffer was last read before the previous workgroup barrier: clear it for the next chunk
-    for (uint32_t k = t - 4 * kWave; k < (uint32_t)(kWsLW * kVPairs3); k += kWsLW * kWave) (&wcnt[b ^ 1][0][0])[k] = 0;
-    // this wave's placement bases: lane l owns slots 4l..4l+3 (counter pairs 2l, 2l+1)
-    uint32_t a0 = 0, a1 = 0, p0 = 0, p1 = 0;
+    for (uint32_t k = t - kL0; k < (uint32_t)(kWsLW * kVPairs3); k += kWsLW * kWave) (&wcnt[b ^ 1][0][0])[k] = 0;
+    // this wave's placement bases: lane l owns slots SPL*l .. SPL*l + SPL-1 (counter pairs SPL/2*l ..)
+    constexpr int PPL = P::SPL / 2;
+    uint32_t acc[PPL], own[PPL];
+#pragma unroll
+    for (int e = 0; e < PPL; ++e) acc[e] = own[e] = 0;
 #pragma unroll
     for (int q = 0; q < kWsLW; ++q) {
-      const uint32_t c0v = wcnt[b][q][2 * l], c1v = wcnt[b][q][2 * l + 1];
-      if ((uint32_t)q == lw) {
-        p0 = a0;
-        p1 = a1;
+#pragma unroll
+      for (int e = 0; e < PPL; ++e) {
+        const uint32_t cv = wcnt[b][q][PPL * l + e];
+        if ((uint32_t)q == lw) own[e] = acc[e];
+        acc[e] += cv;
       }
-      a0 += c0v;
-      a1 += c1v;
     }
-    const uint32_t r0 = a0 & 0xFFFFu, r1 = a0 >> 16, r2 = a1 & 0xFFFFu, r3 = a1 >> 16;
-    const uint32_t mine = r0 + r1 + r2 + r3;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int e = 0; e < PPL; ++e) mine += (acc[e] & 0xFFFFu) + (acc[e] >> 16);
     uint32_t inc = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(inc, d, 64);
       if (l >= (uint32_t)d) inc += y;
     }
-    const uint32_t ex = inc - mine;
-    const uint32_t s0 = ex, s1 = ex + r0, s2 = s1 + r1, s3 = s2 + r2;
-    pbase[lw][4 * l] = (uint16_t)(s0 + (p0 & 0xFFFFu));
-    pbase[lw][4 * l + 1] = (uint16_t)(s1 + (p0 >> 16));
-    pbase[lw][4 * l + 2] = (uint16_t)(s2 + (p1 & 0xFFFFu));
-    pbase[lw][4 * l + 3] = (uint16_t)(s3 + (p1 >> 16));
-    if (lw == 0) {  // the walkers' run starts (read after the workgroup barrier)
-      sstart[b][4 * l] = s0;
-      sstart[b][4 * l + 1] = s1;
-      sstart[b][4 * l + 2] = s2;
-      sstart[b][4 * l + 3] = s3;
-      if (l == 63) sstart[b][kVSlots3] = inc;
+    uint32_t run = inc - mine;
+#pragma unroll
+    for (int e = 0; e < PPL; ++e) {
+      const uint32_t k = P::SPL * l + 2 * e;
+      pbase[lw][k] = (uint16_t)(run + (own[e] & 0xFFFFu));
+      if (lw == 0) sstart[b][k] = run;  // the walkers' run starts (read after the workgroup barrier)
+      run += acc[e] & 0xFFFFu;
+      pbase[lw][k + 1] = (uint16_t)(run + (own[e] >> 16));
+      if (lw == 0) sstart[b][k + 1] = run;
+      run += acc[e] >> 16;
     }
+    if (lw == 0 && l == 63) sstart[b][kVSlots3] = inc;
     WPH(5);
     // lanes read bases other lanes of this wave just wrote: LDS keeps one wave's accesses in order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -710,7 +733,7 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
   for (uint32_t i = 0; i < nch; ++i) {
     const uint32_t b = i & 1;
     if (walker) {
-      const uint32_t start = sstart[b][t], run = sstart[b][t + 1] - start;
+      const uint32_t start = sstart[b][t], run = (diag & 1u) ? 0u : sstart[b][t + 1] - start;
       if (run) {
         uint32_t mA[4], mB[4];
         u64x2 xA[4], xB[4];
@@ -762,7 +785,7 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
   }
   if (!walker && nch) store_results((nch - 1) & 1);  // the last chunk (qp / gq since its walk)
 #ifdef CC_PHASE_TIMING
-  if (t == 0 || t == 4 * kWave)
+  if (t == 0 || t == kL0)
     for (int q = 0; q < kPhases; ++q) atomicAdd(&g_ph_v3a[q], (unsigned long long)wph[q]);
 #endif
 #undef CC_LOAD_CHUNK
@@ -775,21 +798,39 @@ __global__ __launch_bounds__(kAVT) void k_apply_value_v3(const uint4* __restrict
   if (err) atomicOr(err_out, err);
 }
 
+// Slots per value super-bucket: 256 by default.  CC_V3_NS128=1 (A/B) selects 128-slot buckets (two 512-thread apply
+// workgroups per CU) when the partition's per-wave counters hold the doubled bucket count: measured slower on c2
+// (apply 0.91 -> 0.98, partition 0.88 -> 0.92 ms/step, profiles/r03/ab_ns128: the apply is bound by the loaders'
+// instruction and LDS throughput, not by the latency a second workgroup would hide, and 16-record runs over-fetch).
+uint32_t v3_slots_per_bucket(uint32_t sb) {
+  static const bool ns128 = getenv("CC_V3_NS128") != nullptr && getenv("CC_PART_V3") == nullptr;
+  return ns128 && 2 * sb <= (uint32_t)kMaxSb ? 128u : 256u;
+}
+
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
-  const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
   if (a.sb > (uint32_t)kMaxSb || tiles > (uint32_t)kV3MaxTiles) return -1;
   static const bool v3_part = getenv("CC_PART_V3") != nullptr;  // A/B: the chunked 512-thread partition
   if (!v3_part) {
     const uint32_t grid = tiles < (uint32_t)kPersistGrid ? tiles : (uint32_t)kPersistGrid;
-#define CC_LAUNCH4(KP)                                                                                                \
-  hipLaunchKernelGGL((k_part_v4<KP>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,     \
-                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
-    if (kp <= 2) CC_LAUNCH4(2);
-    else if (kp <= 4) CC_LAUNCH4(4);
-    else CC_LAUNCH4(8);
+    const bool half = v3_slots_per_bucket(a.sb) == 128;
+    const uint32_t nsb = half ? 2 * a.sb : a.sb;  // super-buckets (ttab row length - 1)
+    const uint32_t kp = (nsb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
+#define CC_LAUNCH4(KP, KSB)                                                                                           \
+  hipLaunchKernelGGL((k_part_v4<KP, KSB>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi, \
+                     a.inst_res, a.max_inst, nsb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
+    if (half) {
+      if (kp <= 2) CC_LAUNCH4(2, 7);
+      else if (kp <= 4) CC_LAUNCH4(4, 7);
+      else CC_LAUNCH4(8, 7);
+    } else {
+      if (kp <= 2) CC_LAUNCH4(2, 8);
+      else if (kp <= 4) CC_LAUNCH4(4, 8);
+      else CC_LAUNCH4(8, 8);
+    }
 #undef CC_LAUNCH4
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
+  const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
 #define CC_LAUNCH(KP)                                                                                               \
   hipLaunchKernelGGL((k_part_v3<KP>), dim3(tiles), dim3(kV3T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,    \
                      a.inst_res, a.max_inst, a.sb, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
@@ -802,8 +843,16 @@ int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
 
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
   if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
-  hipLaunchKernelGGL(k_apply_value_v3, dim3(a.sb_val), dim3(kAVT), 0, st, reinterpret_cast<const uint4*>(a.st_ab), a.cb,
-                     a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy, a.err);
+  static const uint32_t diag = getenv("CC_V3_DIAG") ? (uint32_t)atoi(getenv("CC_V3_DIAG")) : 0u;  // diagnostics only
+  const uint32_t ns = v3_slots_per_bucket(a.sb);
+  if (ns == 128)
+    hipLaunchKernelGGL(k_apply_value_v3<128>, dim3(a.sb * 2), dim3(V3A<128>::T), 0, st,
+                       reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb * 2, a.val_meta,
+                       a.val_v, a.rst_status, a.rst_value, a.dummy, a.err, diag);
+  else
+    hipLaunchKernelGGL(k_apply_value_v3<256>, dim3(a.sb_val), dim3(V3A<256>::T), 0, st,
+                       reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
+                       a.rst_status, a.rst_value, a.dummy, a.err, diag);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
