@@ -84,6 +84,16 @@ __device__ inline uint4 v3_set_row(uint4 r, uint32_t row) {
   return r;
 }
 __device__ inline uint32_t v3_row(const uint4& r) { return (r.z >> 18) & (kV3Tile - 1); }
+// k_part_v4 also stores an escaped CAS's row relative to the sub-batch start in its (unused) delta field (a reader
+// that does not know the record's tile can fetch the update from the b column; k_apply_value_v3 uses the tile row).
+__device__ inline uint4 v3_set_rows(uint4 r, uint32_t row, uint32_t rel) {
+  r.z |= row << 18;
+  if ((r.z >> 17) & 1u) {
+    r.z |= (rel & 1u) << 31;
+    r.w |= rel >> 1;
+  }
+  return r;
+}
 
 // The record -> value_walk's form (common.h value_encode: meta word, canonical compare value x, canonical new
 // value y).  tile_row0 = the batch row of the record's tile start (escaped CAS updates are read from cb there).
@@ -416,7 +426,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
       if (loc[j] != 0xFFFFu) {
         const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
         const uint32_t sp = kst[k] + ((wc[w][k >> 1] >> sh) & 0xFFFFu) + loc[j];
-        img[sp] = v3_set_row(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << KSB) - 1)), q);
+        img[sp] = v3_set_rows(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << KSB) - 1)), q, tbase + q);
         cp = sp;
       }
       if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
