@@ -217,6 +217,75 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
     em.emit(lane_n, r.g, nev++, target, code, CC_EVSRC_COMMIT, tag, payload);
   };
   if (h.flags & kCoZombie) return CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
+  // Small-state fast paths (type known at compile time, at most one entry, i.e. the whole list in the lane's
+  // register entry E.r0): the same updates and events as the general steps below, as straight-line selects with no
+  // search / shift / fan-out loops and no LDS or global entry accesses except writing entry 1 when the list grows to
+  // two.  The lanes of a walking wave hold different ops, and the general steps' loops made every lane pay every
+  // op's loop structure (2,700-4,500 cycles per step of a one-member group, profiles/r03/c5_diag).
+  if constexpr (T == CC_RES_GROUP) {
+    const bool join = r.op == CC_OP_GROUP_JOIN, leave = r.op == CC_OP_GROUP_LEAVE, exe = r.op == CC_OP_GROUP_EXECUTE;
+    if (h.n <= 1 && (join || leave || exe)) {  // MembershipGroupState.join :47-64, leave :69-81, execute :108-119
+      const uint64_t id = exe ? r.key : r.iid;
+      const CoordEnt e0 = E.r0;
+      const bool has = h.n != 0, hit = has && e0.x == id;
+      const bool ins = join && !hit, rem = leave && hit;  // (coord_cap >= 64: a one-entry list is never full)
+      const CoordEnt ne{r.iid, r.idx, r.inst, 0};
+      const bool after = has && e0.x < id;  // members stay sorted by instance id: the joiner after the member
+      CoordEnt n0 = e0;
+      if (join && hit) {  // previous.clean(): the member's commit is replaced
+        n0.idx = r.idx;
+        n0.inst = r.inst;
+      }
+      if (ins && !after) n0 = ne;
+      if (ins && has) E.put(1, after ? ne : e0);
+      E.r0 = n0;
+      h.n = ins ? h.n + 1u : (rem ? 0u : h.n);
+      // "join"(id) to every other member (:55); a leave leaves no member to tell (:75)
+      if (ins && has && e0.idx != r.idx) ev(e0.inst, CC_EV_JOIN, CC_TAG_LONG, r.iid);  // (as the general fan-out)
+      if (join) {  // the returned Set<Long>, ascending
+        em.emit(lane_n, r.g, nev++, r.inst, CC_EV_MEMBER, CC_EVSRC_RESULT, CC_TAG_LONG, n0.x);
+        if (h.n == 2) em.emit(lane_n, r.g, nev++, r.inst, CC_EV_MEMBER, CC_EVSRC_RESULT, CC_TAG_LONG, after ? ne.x : e0.x);
+        rv = h.n;
+        return CC_STATUS(CC_ST_OK, CC_TAG_SET);
+      }
+      if (leave) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+      if (!hit) return CC_STATUS(CC_ST_ILLEGAL_ARGUMENT, CC_TAG_NULL);  // "unknown member"
+      ev(e0.inst, CC_EV_EXECUTE, CC_FLAG_TAG_A(r.flags), r.a);
+      return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+    }
+  }
+  if constexpr (T == CC_RES_ELECTION) {
+    const bool listen = r.op == CC_OP_ELECT_LISTEN, unlisten = r.op == CC_OP_ELECT_UNLISTEN;
+    if (h.n <= 1 && (listen || unlisten || r.op == CC_OP_ELECT_ISLEADER)) {  // LeaderElectionState :57-98
+      const bool held = (h.flags & kCoHeld) != 0, self = held && h.who == r.inst;
+      if (unlisten && self && (h.flags & kCoCleaned)) return CC_STATUS(CC_ST_ILLEGAL_STATE, CC_TAG_NULL);
+      const CoordEnt e0 = E.r0;
+      const bool search = (listen && held) || (unlisten && !self);
+      const bool found = search && h.n != 0 && e0.x == r.iid;  // the session's listener entry (entry 0)
+      if (listen && !held) {  // the first listener leads
+        h.flags = kCoHeld;
+        h.who = r.inst;
+        h.idx = r.idx;
+        ev(r.inst, CC_EV_ELECT, CC_TAG_LONG, r.idx);
+      }
+      const bool add = listen && held && !found;  // (coord_cap >= 64: never full here)
+      const CoordEnt ne{r.iid, r.idx, r.inst, 0};
+      if (add && h.n == 1) E.put(1, ne);
+      if (add && h.n == 0) E.r0 = ne;
+      const bool promote = unlisten && self && h.n != 0;  // the leader unlistens: the next listener (entry 0) leads
+      if (unlisten && self) h.flags = 0;
+      h.n = add ? h.n + 1u : ((promote || (unlisten && !self && found)) ? 0u : h.n);
+      if (promote) {
+        h.flags = kCoHeld;
+        h.who = e0.inst;
+        h.idx = e0.idx;
+        ev(e0.inst, CC_EV_ELECT, CC_TAG_LONG, e0.idx);
+      }
+      if (listen || unlisten) return CC_STATUS(CC_ST_OK, CC_TAG_NULL);
+      rv = ((h.flags & kCoHeld) && h.who == r.inst && h.idx == 0) ? 1 : 0;  // isLeader (epoch 0, A3)
+      return CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+    }
+  }
   if (!op_registered(type, r.op)) return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
   switch (type) {
     case CC_RES_LOCK: {
