@@ -110,7 +110,7 @@ __device__ inline CoordEnt* ents(uint8_t* blk) { return reinterpret_cast<CoordEn
 // (copied in at kernel start, back at the end), the rest stay in the global block.  Small lock queues / listener
 // and member lists (the common case) then never wait on global memory inside a slot's sequential walk, and a
 // one-entry list (a lock with one waiter, a group with one member) never waits on LDS either.
-constexpr uint32_t kECache = 8;
+constexpr uint32_t kECache = 4;  // (4, not 8: k_apply_coord fits three workgroups per CU)
 // Reads and writes select on the index, never on the pointer: each access keeps its address space (ds_read /
 // global_load), so an LDS hit does not wait behind the walk's outstanding global stores as a flat access would.
 typedef __attribute__((address_space(1))) CoordEnt GlbEnt;
@@ -639,9 +639,9 @@ constexpr int kCT2 = 256;                  // threads per workgroup
 constexpr int kCW2 = kCT2 / kWave;
 constexpr int kCPer2 = 2;                  // commits per thread per chunk
 constexpr int kCCh2 = kCT2 * kCPer2;       // 512 commits of the super-bucket per chunk
-constexpr int kEvLane = 16;                // LDS event slots per walking lane per chunk
+constexpr int kEvLane = 8;                 // LDS event slots per walking lane per chunk (more: straight to the arena)
 
-__global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
+__global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
                                                      uint32_t tiles, uint32_t sb, uint32_t sbq_base,
                                                      const uint8_t* __restrict__ sb_kind,
                                                      const uint8_t* __restrict__ res_type, const uint64_t* __restrict__ inst_id,
@@ -659,12 +659,9 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
   __shared__ uint32_t rmeta[kCCh2];
   __shared__ uint32_t rins[kCCh2];
   __shared__ uint32_t rpos[kCCh2];
-  __shared__ uint64_t oval[kCCh2];           // the walk's results in slot order (written out by all threads)
-  __shared__ uint16_t oev[kCCh2];
-  __shared__ uint8_t ost[kCCh2];
   __shared__ uint32_t wc[kCW2][kQ];          // per-wave slot counts -> per-wave exclusive prefixes
   __shared__ uint32_t sstart[kQ + 1];
-  __shared__ uint32_t rstart[kMaxTiles];
+  __shared__ uint16_t rb0[kMaxTiles];        // run start inside tile r (staging position r * kTile + rb0[r])
   __shared__ uint32_t rpre[kMaxTiles + 1];
   __shared__ uint32_t wsum[kCW2];
   __shared__ uint64_t evp[kEvLane * 3 * kQ];    // the walkers' event buffers (lane-minor planes, see kLanes)
@@ -691,7 +688,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
       if (tt < tiles) {
         const uint16_t* row = ttab + (uint64_t)tt * (sb + 1);
         const uint32_t b0 = row[bk], b1 = row[bk + 1];
-        rstart[tt] = tt * kTile + b0;
+        rb0[tt] = (uint16_t)b0;
         len[q] = b1 - b0;
       }
       sum += len[q];
@@ -741,7 +738,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
       const uint32_t mid = (lo + hi) >> 1;
       if (rpre[mid] <= c) lo = mid; else hi = mid;
     }
-    return rstart[lo] + (c - rpre[lo]);
+    return lo * kTile + rb0[lo] + (c - rpre[lo]);
   };
   // the next chunk's records (whole XRec: position, meta, operands, key, index, instance) stream into registers
   // during the walk; the instance-id gather is issued at the top of the chunk, ahead of the rank and scan
@@ -764,7 +761,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     const uint32_t rrow = base + (uint32_t)(63 - __clzll((long long)bm));
     const uint32_t kr = rrow + l;
     const uint32_t wB = kr + 1 <= tiles ? rpre[kr + 1] : 0xFFFFFFFFu;
-    const uint32_t wS = kr < tiles ? rstart[kr] : 0u, wP = kr < tiles ? rpre[kr] : 0u;
+    const uint32_t wS = kr < tiles ? kr * kTile + rb0[kr] : 0u, wP = kr < tiles ? rpre[kr] : 0u;
     const uint32_t lastc = cw + kWave * kCPer2 - 1 < cnt ? cw + kWave * kCPer2 - 1 : cnt - 1;
     const bool win = (uint32_t)__shfl((int)wB, 63, 64) > lastc;
 #pragma unroll
@@ -885,9 +882,7 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
         uint64_t rv;
         uint32_t nev = 0;
         const uint32_t st = coord_apply<decltype(tc)::value>(type, res, r, h, E, vm, vv, rv, nev, em, lane_n, err);
-        ost[p] = (uint8_t)st;
-        oval[p] = rv;
-        oev[p] = (uint16_t)nev;
+        rab[p] = u64x2{rv, (uint64_t)(st & 0xFFu) | ((uint64_t)(nev & 0xFFFFu) << 8)};  // the result over the record
       }
       };
       // type-specialised walk when every lane with commits in this chunk holds one type (wave-uniform).  Lanes
@@ -927,9 +922,10 @@ __global__ __launch_bounds__(kCT2) void k_apply_coord(const XRec* __restrict__ x
     lds_barrier();
     for (uint32_t p = t; p < sstart[kQ]; p += kCT2) {  // results to the records' staging positions
       const uint32_t gp = rpos[p];
-      rst_status[gp] = ost[p];
-      rst_value[gp] = oval[p];
-      ev_cnt[gp] = oev[p];
+      const u64x2 o = rab[p];
+      rst_status[gp] = (uint8_t)o.y;
+      rst_value[gp] = o.x;
+      ev_cnt[gp] = (uint16_t)(o.y >> 8);
     }
     PH(4);
     // flush the chunk's events (their order in the arena is free: events.hip sorts by (row, emission index))

@@ -184,11 +184,12 @@ def run_c5(args):
     st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
     va = torch.zeros(n, dtype=torch.int64, device="cuda:0")
     evs = DeviceEvents(2 * n, device="cuda:0")
-    E = Engine(R, R, n, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=2 * n)
+    # (as bench.py c5: one spare super-bucket, so no 64-slot group has to mix types)
+    E = Engine(R + (256 if args.manager else 0), R, n, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=2 * n)
     if args.manager:  # as bench.py c5: cc_create_resource in turn (the allocator's 64-slot groups)
         for r in range(R):
             E.create_resource(r + 1, int(types[r]), 1, 1000 + r)
-        types = np.zeros(R, np.uint8)  # the slot -> type table, for the per-WG report
+        types = np.zeros(R + 256, np.uint8)  # the slot -> type table, for the per-WG report
         for r in range(R):
             types[E.resource_slot(1000 + r)] = tl[r % len(tl)] if args.interleave else types_in[r]
     else:
@@ -210,7 +211,7 @@ def run_c5(args):
     L.cc_debug_phases(E.h, 5, ticks)
     sub = args.sub_batch or (16 << 20)
     launches = args.steps * ((n + sub - 1) // sub)
-    wgs = (R // 256) * 4 * launches
+    wgs = ((R + (256 if args.manager else 0)) // 256) * 4 * launches
     tot = sum(ticks)
     ms, nl = prof.get("k_apply_coord", (0.0, 0))
     print(f"[{args.types}] k_apply_coord: {ms / max(nl, 1) * 1e3:.1f} us/launch, workgroups {wgs}, per-WG mean {tot * 10e-3 / wgs:.2f} us")
