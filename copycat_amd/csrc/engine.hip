@@ -81,7 +81,7 @@ static void free_all(cc_engine* e) {
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
-                  e->d_leak,     e->d_leak_n};
+                  e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -135,6 +135,8 @@ static int ensure_ext(cc_engine* e, bool coord) {
         (rc = alloc((void**)&e->d_tile_off, sizeof(uint64_t) * e->max_tiles)) ||
         (rc = alloc((void**)&e->d_arena, sizeof(EvRec) * e->arena_cap)) ||
         (rc = alloc((void**)&e->d_ev_perm, sizeof(uint32_t) * e->arena_cap)) ||
+        (rc = alloc((void**)&e->d_ev_bucket, sizeof(EvRec) * e->arena_cap)) ||
+        (rc = alloc((void**)&e->d_ev_ccnt, sizeof(uint32_t) * ev_chunk_cap(e->arena_cap) * e->max_tiles)) ||
         (rc = alloc((void**)&e->d_arena_n, sizeof(unsigned long long))) ||
         (rc = alloc((void**)&e->d_ev_total, sizeof(unsigned long long))) ||
         (rc = ensure_leak(e, kLeakCap)))
@@ -824,6 +826,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ea.arena_n = e->d_arena_n;
       ea.arena_cap = e->arena_cap;
       ea.perm = e->d_ev_perm;
+      ea.bucket = e->d_ev_bucket;  // the tile-bucketed order pass (CC_EV_V1=1: the gather pass)
+      ea.ccnt = e->d_ev_ccnt;
       if (ev) {
         ea.out_cap = ev->capacity;
         ea.out_pos = ev->pos;

@@ -178,6 +178,8 @@ struct cc_engine {
   uint32_t* d_tile_sum = nullptr;    // [max_tiles]
   uint64_t* d_tile_off = nullptr;    // [max_tiles]
   EvRec* d_arena = nullptr;
+  EvRec* d_ev_bucket = nullptr;      // [arena_cap] the arena grouped by partition tile (events.hip)
+  uint32_t* d_ev_ccnt = nullptr;     // [ev_chunk_cap(arena_cap) * max_tiles] per (arena chunk, tile) counts / bases
   uint32_t* d_ev_perm = nullptr;     // [arena_cap] event output order -> arena index (events.hip)
   unsigned long long* d_arena_n = nullptr;
   unsigned long long* d_ev_total = nullptr;
