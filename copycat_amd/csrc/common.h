@@ -265,6 +265,7 @@ constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration ord
 // extended staging (partition.hip) options
 constexpr uint32_t kExtValue = 1u;     // value records carry the extended columns (value events on the GPU)
 constexpr uint32_t kExtDeferred = 2u;  // manager-mode timer order
+constexpr uint32_t kExtTimeCheck = 4u; // the partition checks time[i] >= time[i-1] for its rows (kErrTime)
 // staging meta: op | flags << 8 | slot low byte << 16 | (map records) ttl > 0 << 24
 constexpr uint32_t kMetaTtl = 1u << 24;
 __host__ __device__ inline uint32_t mw_ident(uint32_t res, uint32_t ktag) { return (res & kMwSlotMask) | ((ktag & 3) << 17) | kMwUsed; }

@@ -584,7 +584,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   }
   if (e->coord_on || e->ttl_live) {  // events of this batch start at 0; the log clock must not go backwards inside it
     if (e->coord_on) HIPCHECK(hipMemsetAsync(e->d_ev_total, 0, sizeof(unsigned long long), st));
-    if (launch_time_check(c->time, n, e->d_clock, e->d_err, st)) return set_err(CC_ERR_HIP, "time check", hipGetLastError());
+    // (without barrier rows every row goes through k_part_ext, which checks it against the row before it)
+    if (!e->bars.empty() && launch_time_check(c->time, n, e->d_clock, e->d_err, st))
+      return set_err(CC_ERR_HIP, "time check", hipGetLastError());
   }
   // Group timers: where each pending one fires in this batch (the clock at row r is max(clock_before, time[r])).
   const bool deferred = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) != 0;
@@ -688,7 +690,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.aux = (e->coord_on || e->ttl_live) ? c->aux : nullptr;  // maps read ttl only in TTL mode (the scan saw none)
     pa.time = c->time;
     pa.clock_base = e->d_clock;
-    pa.ext_flags = ((e->cfg.flags & CC_CFG_VALUE_EVENTS) ? kExtValue : 0u) | ((e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? kExtDeferred : 0u);
+    pa.ext_flags = ((e->cfg.flags & CC_CFG_VALUE_EVENTS) ? kExtValue : 0u) | ((e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? kExtDeferred : 0u) |
+                   ((e->coord_on || e->ttl_live) && e->bars.empty() ? kExtTimeCheck : 0u);
+    pa.err = e->d_err;
     pa.ext = e->ext;
     pa.lo = lo;
     pa.hi = hi;

@@ -30,7 +30,8 @@ struct PartArgs {
   const uint64_t* aux;    // maps: ttl (> 0 not applied on the GPU); locks: timeout
   const uint64_t* time;   // locks: log time (clock)
   const uint64_t* clock_base;  // device: the engine clock before this batch
-  uint32_t ext_flags;     // kExtValue | kExtDeferred
+  uint32_t ext_flags;     // kExtValue | kExtDeferred | kExtTimeCheck
+  uint32_t* err;          // device error bits (kExtTimeCheck: kErrTime)
   bool ext;               // extended staging (maps / coordination / value events)
   uint64_t lo, hi;
   const uint32_t* inst_res;

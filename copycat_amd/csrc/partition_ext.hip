@@ -48,7 +48,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
     uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits, uint32_t sbq_base,
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
-    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab) {
+    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab,
+    uint32_t* __restrict__ err_out) {
   constexpr int J = kXJ, C = kChunkMaps;
   extern __shared__ __align__(16) uint8_t smem[];  // layout: partition.hip tile_lds_bytes(sb, true, kChunkMaps)
   u64x2* rab = reinterpret_cast<u64x2*>(smem);
@@ -74,6 +75,10 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t cbase0 = clock_base ? *clock_base : 0;
   const bool deferred = (ext_flags & kExtDeferred) != 0;
+  // the log clock must not go backwards (each row against the row before it; replaces k_time_check when the batch
+  // has no barrier rows, which are not partitioned)
+  const bool tcheck = ctime && (ext_flags & kExtTimeCheck);
+  uint32_t tbad = 0;
   uint32_t nhot = 0;
   if (map_bits) {
     nhot = *hot_n;
@@ -220,6 +225,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const uint64_t av = ca ? ca[i] : 0, bv = cb ? cb[i] : 0, kv = ckey ? ckey[i] : 0, xv = caux ? caux[i] : 0;
       const uint64_t iv2 = cidx ? cidx[i] : 0;
       const uint64_t t0 = ctime ? ctime[i] : 0, t1 = ctime && i > 0 ? ctime[i - 1] : 0;
+      tbad |= tcheck && i0 < tile1 && i0 > 0 && t0 < t1 ? 1u : 0u;
       in_[j] = dead ? kNoRes : iv;
       mt_[j] = dead ? 0u : mv;
       const bool lock = ty == CC_RES_LOCK;
@@ -423,13 +429,14 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     for (int q = 0; q < kXQ / 4; ++q) tp[q] = (tp[q] >> 16) | (q + 1 < kXQ / 4 ? tp[q + 1] << 16 : 0u);
   }
   PH_FLUSH(g_ph_partx);
+  if (tbad) atomicOr(err_out, kErrTime);
 }
 
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   hipLaunchKernelGGL(k_part_ext, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
-                     a.st_meta, a.st_ab, a.xrec, a.cpos, a.ttab);
+                     a.st_meta, a.st_ab, a.xrec, a.cpos, a.ttab, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
