@@ -64,19 +64,19 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 RESULT_SENTINEL = 0xFF  # result prefill: status 0xFF (tag nibble 15) is never a legal status (copycat_amd.engine)
 
 
-# the kernels behind each cc_profile marker (the value-only partition is k_part_v2; engines with maps, coordination
-# or value events use k_part_tile)
 # the kernels each profiling marker spans (their HBM traffic adds up); the first present partition kernel is the one
-MARKER_KERNELS = {"k_part_tile": ("k_part_v3", "k_part_ext", "k_part_v2", "k_part_tile"),
+# (value-only engines: k_part_v4, or k_part_v3 under CC_PART_V3; engines with maps, coordination or value events:
+# k_part_ext)
+MARKER_KERNELS = {"k_part_tile": ("k_part_v4", "k_part_v3", "k_part_ext", "k_part_v2", "k_part_tile"),
                   "k_apply_value": ("k_apply_value_v3", "k_apply_value_ws", "k_apply_value"),
                   "k_events": ("k_ev_count", "k_ev_tiles", "k_ev_chist", "k_ev_cscan", "k_ev_place", "k_ev_tile_out",
                                "k_ev_rows", "k_ev_perm", "k_ev_out"),
                   "k_map_hot": ("k_hot_detect", "k_hot_agg", "k_hot_lists", "k_hot_apply")}
 MARKER_SUM = {"k_events", "k_map_hot"}
 # the rocprofv3 kernel name(s) behind a profiling marker, per workload (the marker names are the engine's
-# profile slots; the partition slot runs k_part_v2 on value-only engines and k_part_ext otherwise)
-TRACE_NAMES = {"k_part_tile": {"c2": "k_part_v3<4>", "c3": "k_part_ext", "c5": "k_part_ext"},
-               "k_apply_value": {"c2": "k_apply_value_v3"}, "k_apply_map": {"c3": "k_apply_map<false>"},
+# profile slots; the partition slot runs k_part_v4 on value-only engines and k_part_ext otherwise)
+TRACE_NAMES = {"k_part_tile": {"c2": "k_part_v4<4, 8>", "c3": "k_part_ext", "c5": "k_part_ext"},
+               "k_apply_value": {"c2": "k_apply_value_v3<256>"}, "k_apply_map": {"c3": "k_apply_map<false>"},
                "k_unpermute": {"c2": "k_unpermute<512, 8192>", "c3": "k_unpermute<1024, 16384>", "c5": "k_unpermute<1024, 16384>"},
                "k_map_hot": {"c3": "k_hot_detect + k_hot_lists + k_hot_agg + k_hot_apply"},
                "k_events": {"c5": "k_ev_count + k_ev_tiles + k_ev_chist + k_ev_cscan + k_ev_place + k_ev_tile_out"}}

@@ -37,7 +37,9 @@ static hipEvent_t take_event(cc_engine* e) {
     return ev;
   }
   hipEvent_t ev = nullptr;
-  (void)hipEventCreate(&ev);
+  // timing-only markers: no system-scope fence (cache writeback + invalidate) when the event is recorded, which
+  // cost the timed c2 step ~0.15 ms (2.28 vs 2.13 ms with the markers off); elapsed times stay exact
+  if (hipEventCreateWithFlags(&ev, hipEventDisableSystemFence) != hipSuccess) (void)hipEventCreate(&ev);
   return ev;
 }
 
