@@ -734,8 +734,10 @@ def end_to_end_c2(E, clients, n, dev):
 
 
 def roofline_split(prof, n, steps, ms_per_step):
-    """c2 roofline: the 39 algorithmic bytes per commit split over the kernels that move them (30 input bytes read by
-    k_part_tile, 9 result bytes written by k_unpermute); the dominant kernel's share over its own launch time."""
+    """c2 roofline (the contract's definition): SURVEY §8(d)'s 39 algorithmic bytes per commit x the commits one launch
+    of the dominant kernel processes / that kernel's average launch time (HIP events around every launch of the timed
+    region).  Also reported: the bytes split over the kernels that move them at the interface (30 input bytes read
+    by the partition, 9 result bytes written by the unpermute) and the whole-pipeline fraction."""
     if not prof:
         return None
     share = {"k_part_tile": 30.0, "k_unpermute": 9.0}
@@ -743,7 +745,7 @@ def roofline_split(prof, n, steps, ms_per_step):
     ms_tot, launches = prof[dom]
     commits_per_launch = n * steps / max(launches, 1)
     avg_ms = ms_tot / max(launches, 1)
-    b = share.get(dom, 0.0)
+    b = B_OP_C2
     achieved = b * commits_per_launch / (avg_ms * 1e-3) / 1e9
     per_kernel = {}
     for k, (ms, nl) in prof.items():
@@ -753,7 +755,7 @@ def roofline_split(prof, n, steps, ms_per_step):
         "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c2"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c2"),
         "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
-        "alg_bytes_per_commit": {"total": B_OP_C2, **share, "k_apply_value": 0.0},
+        "alg_bytes_per_commit": B_OP_C2, "interface_split": {**share, "k_apply_value": 0.0},
         "alg_gb_per_launch": round(b * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
         "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
         "per_kernel_alg_gbps": per_kernel,
