@@ -45,13 +45,26 @@ static hipEvent_t take_event(cc_engine* e) {
 
 static void mark_fn(void* ctx, int k, int begin, hipStream_t st) {
   cc_engine* e = (cc_engine*)ctx;
+  // a value-only engine enqueues nothing between one kernel's end marker and the next kernel's begin marker inside a
+  // batch, so that end event doubles as the begin event (4 events per sub-batch instead of 6: each recorded event
+  // is a packet on the stream the timed step pays for)
+  if (begin && !e->ext && e->last_end && e->last_end_st == st) {
+    e->open_ev[k] = e->last_end;
+    e->open_shared[k] = true;
+    e->last_end = nullptr;
+    return;
+  }
   hipEvent_t ev = take_event(e);
   (void)hipEventRecord(ev, st);
   if (begin) {
     e->open_ev[k] = ev;
+    e->open_shared[k] = false;
+    e->last_end = nullptr;
   } else {
-    e->pending.push_back({k, e->open_ev[k], ev});
+    e->pending.push_back({k, e->open_ev[k], ev, e->open_shared[k]});
     e->open_ev[k] = nullptr;
+    e->last_end = ev;
+    e->last_end_st = st;
   }
 }
 
@@ -64,7 +77,7 @@ static void drain_profile(cc_engine* e) {
       e->prof_ms[p.kernel] += ms;
       e->prof_n[p.kernel] += 1;
     }
-    e->ev_pool.push_back(p.a);
+    if (!p.shared_a) e->ev_pool.push_back(p.a);  // (a shared begin event is an earlier entry's end event)
     e->ev_pool.push_back(p.b);
   }
   e->pending.clear();
@@ -537,6 +550,7 @@ extern "C" int cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t cou
 extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const cc_results* out, const cc_events* ev,
                               void* stream) {
   if (!e || !c || !out) return set_err(CC_ERR_INVALID, "null argument");
+  e->last_end = nullptr;  // (profiling markers: no begin marker is shared across calls)
   if (n == 0) return CC_OK;
   if (n > e->cfg.max_batch) return set_err(CC_ERR_CAPACITY, "batch larger than max_batch");
   if (!c->inst || !c->op || !c->flags || !c->a || !c->b || !out->status || !out->value)

@@ -195,7 +195,10 @@ struct cc_engine {
   // per-kernel profiling (cc_profile_enable)
   bool prof_on = false;
   std::vector<hipEvent_t> ev_pool;
-  struct Pending { int kernel; hipEvent_t a, b; };
+  struct Pending { int kernel; hipEvent_t a, b; bool shared_a; };  // shared_a: a is an earlier Pending's b
+  hipEvent_t last_end = nullptr;     // value-only engines: the last end marker, reused as the next begin marker
+  hipStream_t last_end_st = nullptr;
+  bool open_shared[K_NUM] = {};
   std::vector<Pending> pending;
   hipEvent_t open_ev[K_NUM] = {};
   double prof_ms[K_NUM] = {};
