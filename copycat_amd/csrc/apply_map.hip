@@ -140,7 +140,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
                                                   const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ rst_msz, uint32_t* __restrict__ err_out) {
   constexpr int MT = TTL ? 512 : CC_MAP_MT;  // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
   constexpr int MEPer = kMapRegion / MT;  // table entries per thread
   constexpr int kMPer = TTL ? 1 : CC_MAP_CHUNK / CC_MAP_MT;  // commits per thread per chunk
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
   __shared__ uint16_t rci[kMCh];       // chunk-list position of the sorted record
   __shared__ uint64_t resv[kMCh];
   __shared__ uint8_t ress[kMCh];
+  __shared__ int8_t resd[kMCh];  // the commit's change of its map's size (launch_map_size)
   __shared__ uint64_t tdl[TTL ? kMapRegion : 1];  // timer deadline of the entry (0: none)
   __shared__ uint64_t rfire[TTL ? kMCh : 1];      // clock of the last timer firing before the commit
   __shared__ uint64_t rdl[TTL ? kMCh : 1];        // deadline the commit arms if it stores (0: none)
@@ -447,6 +448,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         const uint32_t cx = w * (kWave * kMPer) + j * kWave + l;
         ress[cx] = (uint8_t)s;
         resv[cx] = rv;
+        resd[cx] = 0;
       }
     }
     PH(3);
@@ -601,9 +603,11 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         uint64_t rv;
         bool wrote, created;
         const u64x2 x = rab[s];
+        const int was = (sw & kMwPresent) != 0;
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, sw, sv, rv, wrote, created);
         ress[rci[s]] = (uint8_t)st;
         resv[rci[s]] = rv;
+        resd[rci[s]] = (int8_t)(((sw & kMwPresent) != 0) - was);
         cur = pc_compose(cur, el[q]);
         if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
           fin[q] = true;
@@ -640,6 +644,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         const u64x2 x = rab[s];
         uint64_t rv;
         bool wrote, created;
+        const int was = (wv & kMwPresent) != 0;
         if (TTL && dl && dl <= rfire[s]) {  // the timer fired: map.remove(key) (MapState.java:91-93)
           wv &= ~(kMwPresent | kMwVtagMask);
           vv = 0;
@@ -652,6 +657,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         }
         ress[rci[s]] = (uint8_t)st;
         resv[rci[s]] = rv;
+        resd[rci[s]] = (int8_t)(((wv & kMwPresent) != 0) - was);
         if (wrote) { ci = rpos[s]; any_w = true; }
         if (created) { ins = rpos[s]; any_c = true; }
       }
@@ -662,9 +668,12 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
       if (any_c) tir[e] = ins;
     }
     lds_barrier();
-    uint32_t gs[kMPer];
+    uint32_t gs[kMPer], rs[kMPer];
 #pragma unroll
-    for (int j = 0; j < kMPer; ++j) gs[j] = g[j];
+    for (int j = 0; j < kMPer; ++j) {
+      gs[j] = g[j];
+      rs[j] = res[j];
+    }
     if (more) take();
 #pragma unroll
     for (int j = 0; j < kMPer; ++j)  // this thread's own commits: consecutive lanes -> consecutive staging rows
@@ -672,6 +681,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         const uint32_t cx = w * (kWave * kMPer) + j * kWave + l;
         rst_status[gs[j]] = ress[cx];
         rst_value[gs[j]] = resv[cx];
+        rst_msz[gs[j]] = (rs[j] << 2) | (resd[cx] > 0 ? 1u : resd[cx] < 0 ? 2u : 0u);  // (launch_map_size)
       }
     for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
     for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = 0;
@@ -709,11 +719,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.ttl)
     hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
-                       a.rst_status, a.rst_value, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, a.err);
   else
     hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
-                       a.rst_status, a.rst_value, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -261,6 +261,11 @@ struct EvRec {
 };
 constexpr uint32_t kErrTime = 8u;  // the time column decreased inside a batch
 constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration order is undetermined (map_wide.hip)
+constexpr uint32_t kErrMapSize = 32u;   // a map's tracked size differs from its table at a barrier (internal check)
+// a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
+__device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
+  return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);
+}
 
 // extended staging (partition.hip) options
 constexpr uint32_t kExtValue = 1u;     // value records carry the extended columns (value events on the GPU)

@@ -96,7 +96,8 @@ static void free_all(cc_engine* e) {
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
-                  e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt};
+                  e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_msize,
+                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -257,6 +258,12 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
+    ALLOC(e->d_rst_msz, sizeof(uint32_t) * (e->sub_batch + 4 * kPT));
+    ALLOC(e->d_msize, sizeof(uint32_t) * cfg->max_resources);
+    ALLOC(e->d_mpcap, sizeof(uint32_t) * cfg->max_resources);
+    ALLOC(e->d_msz_tcnt, sizeof(uint32_t) * cfg->max_resources * e->max_tiles);  // [tile][map] counts
+    ALLOC(e->d_msz_list, sizeof(uint4) * kMszListCap);
+    ALLOC(e->d_msz_list_n, sizeof(uint32_t));
     ALLOC(e->d_tbl_dl, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_map_row, sizeof(uint32_t) * e->sub_batch);
     ALLOC(e->d_hot_rpre, sizeof(uint32_t) * kHotMax * (kMaxTiles + 1));
@@ -300,6 +307,8 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_hot_n, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_peak, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_drop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_msize, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_mpcap, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_dl, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
   }
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
@@ -348,6 +357,7 @@ static int check_device_err(cc_engine* e) {
     if (err & kErrMapOrder)
       return set_err(CC_ERR_STATE, "map containsValue: the answer depends on java.util.HashMap iteration order and the "
                                    "map's table capacity (peak size) is not determined exactly by the engine's bounds");
+    if (err & kErrMapSize) return set_err(CC_ERR_STATE, "internal check: a map's tracked size differs from its table");
     if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
     if (err & kErrCapacity)
       return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, lock queue, listeners, members)");
@@ -413,6 +423,8 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
   if (is_keyed(type)) {  // a new HashMap: capacity 16, no history
     HIPCHECK(hipMemset(e->d_mw_peak + first, 0, sizeof(uint32_t) * count));
     HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
+    HIPCHECK(hipMemset(e->d_msize + first, 0, sizeof(uint32_t) * count));
+    HIPCHECK(hipMemset(e->d_mpcap + first, 0, sizeof(uint32_t) * count));
   }
   // fresh state: AtomicValueState() {value = null; current = null}
   HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
@@ -546,6 +558,17 @@ extern "C" int cc_instance_open_range(cc_engine* e, uint32_t first, uint32_t cou
   if (!e) return CC_ERR_INVALID;
   return open_range(e, first, count, res_first, 1, id_first, client_session);
 }
+
+// Diagnostics (CC_DEBUG_SYNC=1): drain the stream after every launch of cc_apply_batch and name the launch whose
+// kernels failed.
+static const bool g_dbg_sync = getenv("CC_DEBUG_SYNC") != nullptr;
+#define DBG_SYNC(what)                                                                          \
+  do {                                                                                          \
+    if (g_dbg_sync) {                                                                           \
+      hipError_t _x = hipStreamSynchronize(st);                                                 \
+      if (_x != hipSuccess) return set_err(CC_ERR_HIP, "CC_DEBUG_SYNC after " what, _x);        \
+    }                                                                                           \
+  } while (0)
 
 extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const cc_results* out, const cc_events* ev,
                               void* stream) {
@@ -689,11 +712,12 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.hot_samp = e->d_hot_samp;
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
+      ha.rst_msz = e->d_rst_msz;
       ha.err = e->d_err;
       ha.mark = marker_of(e);
       static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
       if (no_hot) HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
-      else if (launch_map_hot_detect(ha, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError());
+      else if (launch_map_hot_detect(ha, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError()); DBG_SYNC("hot-key detect launch");
     }
     PartArgs pa{};
     pa.inst = c->inst;
@@ -734,7 +758,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.v3 = v3;
 
     pa.mark = marker_of(e);
-    if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError());
+    if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError()); DBG_SYNC("partition launch");
     if (e->map_bits && e->ttl_live && launch_map_rows(e->d_cpos, lo, hi, e->d_map_row, st))
       return set_err(CC_ERR_HIP, "map rows launch", hipGetLastError());
     ValueArgs va{};
@@ -756,7 +780,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.dummy = e->sub_batch;
     va.err = e->d_err;
     va.mark = marker_of(e);
-    if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError());
+    if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError()); DBG_SYNC("apply launch");
     if (e->map_bits) {
       if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
@@ -781,9 +805,29 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.deferred = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) != 0;
       ma.rst_status = e->d_rst_status;
       ma.rst_value = e->d_rst_value;
+      ma.rst_msz = e->d_rst_msz;
       ma.err = e->d_err;
       ma.mark = marker_of(e);
-      if (launch_apply_map(ma, st)) return set_err(CC_ERR_HIP, "map apply launch", hipGetLastError());
+      if (launch_apply_map(ma, st)) return set_err(CC_ERR_HIP, "map apply launch", hipGetLastError()); DBG_SYNC("map apply launch");
+      if (!e->ttl_live) {  // exact map sizes and HashMap capacities (containsValue's iteration order)
+        MapSizeArgs za{};
+        za.ttab = e->d_ttab;
+        za.cpos = e->d_cpos;
+        za.tiles = tiles;
+        za.rows = hi - lo;
+        za.sb = e->sb_total();
+        za.k0 = e->sb;
+        za.k1 = e->sbq_base();
+        za.rst_msz = e->d_rst_msz;
+        za.res_type = e->d_res_type;
+        za.max_resources = e->cfg.max_resources;
+        za.tcnt = e->d_msz_tcnt;
+        za.msize = e->d_msize;
+        za.mpcap = e->d_mpcap;
+        za.list = e->d_msz_list;
+        za.list_n = e->d_msz_list_n;
+        if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError()); DBG_SYNC("map size launch");
+      }
     }
     if (e->coord_on) {
       HIPCHECK(hipMemsetAsync(e->d_ev_cnt, 0, sizeof(uint16_t) * (hi - lo), st));
@@ -813,7 +857,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.leak_cap = e->leak_cap;
       ca.err = e->d_err;
       ca.mark = marker_of(e);
-      if (launch_apply_coord(ca, st)) return set_err(CC_ERR_HIP, "coordination apply launch", hipGetLastError());
+      if (launch_apply_coord(ca, st)) return set_err(CC_ERR_HIP, "coordination apply launch", hipGetLastError()); DBG_SYNC("coordination apply launch");
     }
     UnpermuteArgs ua{};
     ua.cpos = e->d_cpos;
@@ -829,7 +873,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.dummy_value = e->d_rst_value + e->sub_batch;
     ua.v3 = v3;
     ua.mark = marker_of(e);
-    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
+    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
     if (e->coord_on) {
       EventArgs ea{};
       ea.cpos = e->d_cpos;
@@ -859,7 +903,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       }
       ea.err = e->d_err;
       ea.mark = marker_of(e);
-      if (launch_events(ea, st)) return set_err(CC_ERR_HIP, "events launch", hipGetLastError());
+      if (launch_events(ea, st)) return set_err(CC_ERR_HIP, "events launch", hipGetLastError()); DBG_SYNC("events launch");
     }
   }
   if (action == 2) {  // a group timer fires here (MembershipGroupState.java:92-98)
@@ -883,7 +927,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemcpy(&op, c->op + row, 1, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(&fl, c->flags + row, 1, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(&a, c->a + row, sizeof a, hipMemcpyDeviceToHost));
-    res = e->inst_res[in];
+    // (k_map_barriers listed the row through the device registry; the host mirror must agree before its slot
+    // indexes any per-resource array)
+    if (row >= n || in >= e->cfg.max_instances || (res = e->inst_res[in]) >= e->cfg.max_resources ||
+        !(is_keyed(e->res_type[res]) || e->res_type[res] == CC_RES_GROUP))
+      return set_err(CC_ERR_STATE, "barrier row does not resolve to a map / set / multimap / group on the host registry");
     if (e->res_type[res] == CC_RES_GROUP) {  // schedule :86-103 (member = key, callback = a, delay = aux)
       uint64_t member = 0, delay = 0;
       HIPCHECK(hipMemcpy(&member, c->key + row, sizeof member, hipMemcpyDeviceToHost));
@@ -937,17 +985,19 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.entries = e->map_entries;
     mw.peak_lo = e->d_mw_peak;
     mw.dropped = e->d_mw_drop;
+    mw.msize = e->ttl_live ? nullptr : e->d_msize;
+    mw.mpcap = e->d_mpcap;
     mw.ctl = e->d_mw_ctl;
     mw.out_status = out->status;
     mw.out_value = out->value;
     mw.err = e->d_err;
-    if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError());
+    if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError()); DBG_SYNC("whole-map op launch");
   }
   }
   if (e->has_sets || e->has_mmaps) {
     KeyedResultArgs ka{c->inst,     c->op,          c->flags, c->index,     n,           e->d_inst_res, e->d_res_type,
                        e->cfg.max_instances, out->status, out->value, e->d_leak, e->d_leak_n, e->leak_cap, e->d_err};
-    if (launch_keyed_results(ka, st)) return set_err(CC_ERR_HIP, "set / multimap results launch", hipGetLastError());
+    if (launch_keyed_results(ka, st)) return set_err(CC_ERR_HIP, "set / multimap results launch", hipGetLastError()); DBG_SYNC("set / multimap results launch");
   }
   // Retained value commits (live.hip): after every value op of the batch has applied.  The post-pass attributes
   // each row through the END-of-batch inst_res / res_type / val_meta: correct because the registry cannot change
@@ -960,7 +1010,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   }
   if (e->coord_on && ev) HIPCHECK(hipMemcpyAsync(ev->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   if (e->coord_on || e->map_bits) {  // the log clock (timers: lock timeouts, map TTL)
-    if (launch_clock_advance(c->time, n, 0, e->d_clock, st)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
+    if (launch_clock_advance(c->time, n, 0, e->d_clock, st)) return set_err(CC_ERR_HIP, "clock", hipGetLastError()); DBG_SYNC("clock");
   }
   if (c->index) {  // the applied watermark = index of the batch's last entry
     HIPCHECK(hipMemcpyAsync(e->d_last_index, c->index + (n - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
@@ -1542,7 +1592,7 @@ static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unp
 // Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
 // mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
 namespace {
-constexpr uint64_t kSnapMagic = 0x33304E5053434343ull;  // "CCCSPN03"
+constexpr uint64_t kSnapMagic = 0x34304E5053434343ull;  // "CCCSPN04"
 constexpr uint32_t kSnapRetained = 4u;                   // SnapHdr.flags: CC_CFG_VALUE_RETAINED section present
 struct SnapHdr {
   uint64_t magic;
@@ -1590,6 +1640,8 @@ static std::vector<Section> snap_sections(cc_engine* e) {
     v.push_back({e->d_tbl_dl, nullptr, 8 * n});
     v.push_back({e->d_mw_peak, nullptr, 4 * mr});
     v.push_back({e->d_mw_drop, nullptr, 8 * mr});
+    v.push_back({e->d_msize, nullptr, 4 * mr});
+    v.push_back({e->d_mpcap, nullptr, 4 * mr});
   }
   if (e->coord_on) v.push_back({e->d_coord, nullptr, coord_block(e->coord_cap) * slots});
   return v;

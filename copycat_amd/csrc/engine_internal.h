@@ -108,10 +108,34 @@ struct MapArgs {
   bool deferred;               // manager-mode timer order (CC_CFG_TIMERS_DEFERRED)
   uint8_t* rst_status;
   uint64_t* rst_value;
+  uint32_t* rst_msz;           // [sub_batch] each commit's map and size change (msz_word), staging order
   uint32_t* err;
   Marker mark;
 };
 int launch_apply_map(const MapArgs& a, hipStream_t st);
+// Exact map sizes and HashMap capacities (map_wide.hip): after a sub-batch's map kernels, per (tile, map) insert /
+// remove counts from rst_msz, then per map a scan over its tiles (sizes at tile starts, capacity bounds per tile)
+// and an exact in-tile pass for the few tiles whose counts alone leave the capacity open.  Engines with maps
+// outside TTL mode.
+constexpr uint32_t kMpInexact = 1u << 31;  // mpcap flag: the capacity level is a lower bound only (list overflow)
+constexpr uint32_t kMszListCap = 1u << 18;  // (tile, map) pairs resolved exactly per sub-batch
+struct MapSizeArgs {
+  const uint16_t* ttab;
+  const uint16_t* cpos;
+  uint32_t tiles;
+  uint64_t rows;               // rows of the sub-batch
+  uint32_t sb;                 // ttab row width - 1
+  uint32_t k0, k1;             // the map and hot-key buckets [k0, k1)
+  const uint32_t* rst_msz;
+  const uint8_t* res_type;
+  uint32_t max_resources;
+  uint32_t* tcnt;              // [tiles][max_resources] (inserts | removes << 16) per (tile, map)
+  uint32_t* msize;             // [max_resources] live size at the sub-batch boundary
+  uint32_t* mpcap;             // [max_resources] log2(HashMap capacity / 16) of the peak size so far (| kMpInexact)
+  uint4* list;                 // [kMszListCap] (tile, map, size at the tile's start) pairs for the exact pass
+  uint32_t* list_n;
+};
+int launch_map_size(const MapSizeArgs& a, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
 int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* map_row, hipStream_t st);
 
@@ -134,6 +158,8 @@ struct MapWideArgs {
   uint64_t entries;
   uint32_t* peak_lo;           // [max_resources] lower bound on the map's peak size
   uint64_t* dropped;           // [max_resources] entries dropped by compaction / clear (upper-bound term)
+  uint32_t* msize;             // exact tracking (launch_map_size; null in TTL mode): the live size, and
+  const uint32_t* mpcap;       //   log2(capacity / 16) of the peak (in TTL mode a lower bound for the bounds above)
   unsigned long long* ctl;     // [C_N] scratch
   uint8_t* out_status;
   uint64_t* out_value;
@@ -199,6 +225,7 @@ struct HotArgs {
   void* hot_samp;        // [65536] resolved detection sample (apply_map_hot.hip HotSamp)
   uint8_t* rst_status;
   uint64_t* rst_value;
+  uint32_t* rst_msz;
   uint32_t* err;
   Marker mark;
 };

@@ -137,6 +137,13 @@ struct cc_engine {
   uint32_t* d_bar_n = nullptr;
   uint32_t* d_mw_peak = nullptr;   // [max_resources]
   uint64_t* d_mw_drop = nullptr;   // [max_resources]
+  // exact map sizes / HashMap capacities (map_wide.hip launch_map_size; not in TTL mode)
+  uint32_t* d_rst_msz = nullptr;   // [sub_batch + 4 kPT] each map commit's map and size change, staging order
+  uint32_t* d_msize = nullptr;     // [max_resources]
+  uint32_t* d_mpcap = nullptr;     // [max_resources]
+  uint32_t* d_msz_tcnt = nullptr;  // [max_tiles][max_resources]
+  uint4* d_msz_list = nullptr;     // [kMszListCap]
+  uint32_t* d_msz_list_n = nullptr;
   unsigned long long* d_mw_ctl = nullptr;  // [16]
   std::vector<uint32_t> bars;
   // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good

@@ -14,10 +14,14 @@
 //
 // Iteration order (oracle/oracle.cpp JavaOrder): bucket = Java hash & (capacity - 1), then insertion order in
 // the bucket (= the commit index that created the node, tbl_ins).  The capacity is a function of the map's peak
-// size (HashMap.resize doubles it when ++size > 0.75 * capacity and never shrinks it).  The engine keeps a lower
-// bound on the peak (sizes seen at barriers) and an upper bound (bound entries + entries dropped by compaction or
-// clear: every key that was ever present owned one).  When the two bounds give different capacities and the
-// order matters, the batch fails with CC_ERR_STATE ("order undetermined") instead of guessing.
+// size (HashMap.resize doubles it when ++size > 0.75 * capacity and never shrinks it; clear() keeps the table).
+// The engine tracks every map's size and capacity exactly (launch_map_size, after each sub-batch's map kernels:
+// per-commit size deltas -> per (tile, map) insert/remove counts -> per map the sizes at tile starts; a tile
+// whose counts straddle a resize threshold is replayed in log order).  In TTL mode (entries also leave when
+// their timers fire) the exact tracking stops and the engine falls back to bounds on the peak: lower = the
+// exact level reached before TTL mode and the sizes seen at barriers, upper = bound entries + entries dropped by
+// compaction or clear (every key that was ever present owned one).  Only there, when the two bounds give
+// different capacities and the order matters, the batch fails with CC_ERR_STATE instead of guessing.
 #include <algorithm>
 
 #include "common.h"
@@ -187,18 +191,33 @@ __global__ __launch_bounds__(kMwT) void k_mw_count(const uint32_t* __restrict__ 
 
 // pass 0: the capacity, then the first bucket holding a null / a match; pass 1: inside the common first bucket,
 // the first insertion of each.  Runs only for an order-dependent containsValue (all threads read the same ctl).
+// log2(HashMap capacity / 16) after the size peaked at p
+__device__ inline uint32_t cap_level(uint64_t p) {
+  uint32_t lv = 0;
+  for (uint64_t thr = 12; p > thr; thr <<= 1) ++lv;
+  return lv;
+}
+
 __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ word, const uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ val, const uint64_t* __restrict__ ins,
                                                   const uint64_t* __restrict__ dl, uint64_t fire, uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag, uint64_t apay,
                                                   const uint32_t* __restrict__ peak_lo, const unsigned long long* __restrict__ dropped,
+                                                  const uint32_t* __restrict__ mpcap, bool exact,
                                                   int pass, unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
   if (op != CC_OP_MAP_CONTAINSVALUE || ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0) return;
-  const uint64_t lo = max((uint64_t)peak_lo[slot], (uint64_t)ctl[C_PRES]);
-  const uint64_t hi = ctl[C_USED] + dropped[slot];
-  const uint64_t cap = java_cap(lo);
-  if (java_cap(hi) != cap) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && pass == 0) atomicOr(err, kErrMapOrder);
-    return;
+  const uint32_t mp = mpcap ? mpcap[slot] : 0u, lv = mp & ~kMpInexact;
+  uint64_t cap;
+  if (exact && !(mp & kMpInexact)) {
+    cap = 16ull << lv;  // the tracked peak's capacity (it covers the live size counted here)
+  } else {
+    // bounds: the level reached while tracking was exact means a peak above the previous level's threshold
+    const uint64_t lo = max(max((uint64_t)peak_lo[slot], (uint64_t)ctl[C_PRES]), lv ? (12ull << (lv - 1)) + 1 : 0ull);
+    const uint64_t hi = ctl[C_USED] + dropped[slot];
+    cap = java_cap(lo);
+    if (java_cap(hi) != cap) {
+      if (blockIdx.x == 0 && threadIdx.x == 0 && pass == 0) atomicOr(err, kErrMapOrder);
+      return;
+    }
   }
   if (pass == 1 && ctl[C_BN] != ctl[C_BM]) return;  // decided by the buckets
   for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
@@ -219,6 +238,16 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
 
 // The barrier row's result (MapState.java :49-60 / :233-239 / :244-250 / :255-261 / :264-274) and the map's
 // peak-size bounds.
+// Exact tracking (not in TTL mode): the tracked size must be what the table holds; clear / Delete empty the map.
+// (Its own launch: folded into k_mw_finish behind an `if (msize)`, hipcc 7.2 at -O3 lost the slot register on the
+// msize == null path of the clear / Delete case and k_mw_finish wrote dropped[] through a garbage index.)
+__global__ void k_mw_size(uint32_t slot, uint32_t op, const unsigned long long* __restrict__ ctl, uint32_t* __restrict__ msize,
+                          uint32_t* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  if (msize[slot] != ctl[C_PRES]) atomicOr(err, kErrMapSize);
+  if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE) msize[slot] = 0;
+}
+
 __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsigned long long* __restrict__ ctl,
                             uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped, uint8_t* __restrict__ out_status,
                             uint64_t* __restrict__ out_value) {
@@ -336,15 +365,184 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
   if (op == CC_OP_MAP_CONTAINSVALUE) {
     for (int pass = 0; pass < 2; ++pass)
       hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.tbl_dl,
-                         a.fire_clock, a.entries,
-                         a.slot, op, atag, apay, a.peak_lo, (const unsigned long long*)a.dropped, pass, a.ctl, a.err);
+                         a.fire_clock, a.entries, a.slot, op, atag, apay, a.peak_lo,
+                         (const unsigned long long*)a.dropped, a.mpcap, a.msize != nullptr, pass, a.ctl, a.err);
   }
+  if (a.msize) hipLaunchKernelGGL(k_mw_size, dim3(1), dim3(64), 0, st, a.slot, op, a.ctl, a.msize, a.err);
   hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,
-                     (unsigned long long*)a.dropped, a.out_status,
-                     a.out_value);
+                     (unsigned long long*)a.dropped, a.out_status, a.out_value);
   if (hipGetLastError() != hipSuccess) return -1;
   if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE) return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, st);
   return 0;
+}
+
+// ---- exact map sizes and capacities (MapState's java.util.HashMap: size, and the table capacity its peak size
+//      set, HashMap.putVal / resize) ----
+// k_apply_map / k_hot_apply write one word per map record (msz_word: the map slot and whether the commit inserted
+// or removed a key).  Then, per sub-batch:
+// 1. k_msize_count, one workgroup per partition tile: its map records' words (one coalesced span) counted per map
+//    in LDS (direct-indexed, 16384 maps per pass), the tile's row of tcnt written whole (coalesced, zeros included).
+// 2. k_msize_scan, one workgroup per 64 maps (lane = map, wave = a chunk of tiles): the size at every tile start (a
+//    prefix sum of inserts - removes in log order), per tile the capacity level bounds [level(max(size before, size
+//    after)), level(size before + inserts)], L = the highest lower bound (and the level so far).  Only a tile whose
+//    upper bound exceeds L can raise the capacity beyond L: it goes to the exact list.  Order-free: no serial walk.
+// 3. k_msize_exact, one workgroup per listed (tile, map): the tile's rows in log order (cpos), the map's size
+//    changes among them, the running maximum -> the tile's true peak -> atomicMax on the level.
+// Traffic per sub-batch: 4 B written + 4 B read per map record, 4 B x maps per tile (the counter rows, written and
+// read once); the exact pass reads a tile's cpos (32 KB) plus its gathers per listed pair.
+constexpr int kMszT = 1024;
+constexpr uint32_t kMszPass = 16384;  // maps counted per LDS pass (64 KB)
+
+__global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restrict__ ttab, uint32_t sb, uint32_t k0,
+                                                      uint32_t k1, const uint32_t* __restrict__ msz, uint32_t R,
+                                                      uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t cnt[kMszPass];
+  const uint32_t t = blockIdx.x;
+  const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
+  const uint32_t b0 = row[k0], b1 = row[k1];
+  const uint32_t* w = msz + (uint64_t)t * kTile;
+  uint32_t* out = tcnt + (uint64_t)t * R;
+  for (uint32_t base = 0; base < R; base += kMszPass) {
+    const uint32_t span = min(kMszPass, R - base);
+    for (uint32_t q = threadIdx.x; q < span; q += kMszT) cnt[q] = 0;
+    lds_barrier();
+    for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
+      const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
+      if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
+    }
+    lds_barrier();
+    for (uint32_t q = threadIdx.x; q < span; q += kMszT) out[base + q] = cnt[q];
+    lds_barrier();  // (the next pass clears cnt)
+  }
+}
+
+__device__ inline int32_t msz_net(uint32_t c) { return (int32_t)(c & 0xFFFFu) - (int32_t)(c >> 16); }
+
+constexpr int kMszScanW = 16;                         // waves per scan workgroup = tile chunks
+__global__ __launch_bounds__(kMszScanW * kWave) void k_msize_scan(const uint8_t* __restrict__ res_type, uint32_t R,
+                                                                 uint32_t tiles, const uint32_t* __restrict__ tcnt,
+                                                                 uint32_t* __restrict__ msize, uint32_t* __restrict__ mpcap,
+                                                                 uint4* __restrict__ list, uint32_t* __restrict__ list_n) {
+  __shared__ int32_t csum[kMszScanW][kWave];
+  __shared__ uint32_t clv[kMszScanW][kWave];
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, m = blockIdx.x * kWave + l;
+  const bool ok = m < R && is_keyed(res_type[m]);
+  const uint32_t per = (tiles + kMszScanW - 1) / kMszScanW, t0 = min(w * per, tiles), t1 = min(t0 + per, tiles);
+  // chunk w's tiles [t0, t1) in log order (row t of tcnt: coalesced over the lanes); three passes re-read the
+  // rows (16 KB per tile at 4096 maps: L2 / MALL-resident) instead of holding them in registers
+  const uint32_t* c = tcnt + m;
+  int32_t sum = 0;
+  if (ok) {
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; ++t) sum += msz_net(c[(uint64_t)t * R]);
+  }
+  csum[w][l] = sum;
+  lds_barrier();
+  const uint32_t s0 = ok ? msize[m] : 0u, mp = ok ? mpcap[m] : 0u;
+  int64_t start = s0;
+  for (uint32_t q = 0; q < w; ++q) start += csum[q][l];
+  // lower bounds: the highest level every tile's counts prove (with the level reached so far)
+  uint32_t lv = mp & ~kMpInexact;
+  if (ok) {
+    int64_t s = start;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t x = c[(uint64_t)t * R];
+      const int64_t fin = s + msz_net(x);
+      if (x) lv = max(lv, cap_level((uint64_t)max(s, fin)));
+      s = fin;
+    }
+  }
+  clv[w][l] = lv;
+  lds_barrier();
+  for (int q = 0; q < kMszScanW; ++q) lv = max(lv, clv[q][l]);
+  // tiles that may cross a resize threshold above lv: replayed by k_msize_exact
+  uint32_t inexact = 0;
+  if (ok) {
+    int64_t s = start;
+    const uint64_t hi_ok = 12ull << lv;  // level(p) <= lv  <=>  p <= 12 << lv
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t x = c[(uint64_t)t * R];
+      if ((uint64_t)(s + (x & 0xFFFFu)) > hi_ok) {
+        const uint32_t k = atomicAdd(list_n, 1u);
+        if (k < kMszListCap) list[k] = make_uint4(t, m, (uint32_t)s, 0u);
+        else inexact = kMpInexact;
+      }
+      s += msz_net(x);
+    }
+  }
+  lds_barrier();  // every lane read clv
+  clv[w][l] = inexact;
+  lds_barrier();
+  if (w == 0 && ok) {
+    for (int q = 0; q < kMszScanW; ++q) inexact |= clv[q][l];
+    int64_t total = 0;
+    for (int q = 0; q < kMszScanW; ++q) total += csum[q][l];
+    msize[m] = (uint32_t)((int64_t)s0 + total);
+    mpcap[m] = lv | inexact | (mp & kMpInexact);
+  }
+}
+
+__global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restrict__ ttab, const uint16_t* __restrict__ cpos,
+                                                      uint64_t rows, uint32_t sb, uint32_t k0, uint32_t k1,
+                                                      const uint32_t* __restrict__ msz, const uint4* __restrict__ list,
+                                                      const uint32_t* __restrict__ list_n, uint32_t* __restrict__ mpcap) {
+  constexpr int kPer = kTile / kMszT;
+  __shared__ int32_t wsum[kMszT / kWave], wmax[kMszT / kWave];
+  const uint32_t n = min(*list_n, kMszListCap), w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (uint32_t it = blockIdx.x; it < n; it += gridDim.x) {
+    const uint4 e = list[it];
+    const uint32_t t = e.x, m = e.y;
+    const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
+    const uint32_t b0 = row[k0], b1 = row[k1];
+    const uint64_t base = (uint64_t)t * kTile;
+    int32_t sum = 0, mx = 0;  // this thread's rows (consecutive, log order): net change, highest running value
+#pragma unroll 4
+    for (int j = 0; j < kPer; ++j) {
+      const uint64_t r = base + (uint64_t)threadIdx.x * kPer + j;
+      if (r >= rows) break;
+      const uint32_t p = cpos[r];
+      if (p < b0 || p >= b1) continue;  // unknown session (0xFFFF) or not a map record
+      const uint32_t x = msz[base + p];
+      if ((x >> 2) != m || !(x & 3u)) continue;
+      sum += (x & 3u) == 1u ? 1 : -1;
+      mx = max(mx, sum);
+    }
+    int32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t y = __shfl_up(inc, d, 64);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    int32_t best = inc - sum + mx;  // the highest running value inside this thread's rows, from the wave's start
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) best = max(best, __shfl_xor(best, d, 64));
+    if (l == 63) wsum[w] = inc;
+    if (l == 0) wmax[w] = best;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      int32_t run = 0, peak = 0;
+      for (int q = 0; q < kMszT / kWave; ++q) {
+        peak = max(peak, run + wmax[q]);
+        run += wsum[q];
+      }
+      atomicMax(&mpcap[m], cap_level((uint64_t)e.z + (uint64_t)peak));
+    }
+    lds_barrier();  // wsum / wmax are rewritten by the next item
+  }
+}
+
+int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
+  if (a.tiles == 0) return 0;
+  if (hipMemsetAsync(a.list_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.k1, a.rst_msz,
+                     a.max_resources, a.tcnt);
+  hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,
+                     a.res_type, a.max_resources, a.tiles, a.tcnt, a.msize, a.mpcap, a.list, a.list_n);
+  hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.rst_msz,
+                     a.list, a.list_n, a.mpcap);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace cc

@@ -276,38 +276,86 @@ def test_map_contains_value_iteration_order():
     _assert_maps(E, O, range(3))
 
 
-def test_map_contains_value_undetermined_capacity_fails_loudly():
-    """Peak 30 (capacity 64) is not observed by any barrier and 25 keys were removed since: the engine's bounds
-    (15 live .. 40 bound) straddle a resize, so an order-dependent containsValue fails with CC_ERR_STATE
-    instead of guessing.  A size barrier at the peak pins the capacity and the same query becomes exact."""
+def _peak_stream(with_size, ttl_row=False):
+    """Peak 30 (capacity 64) that no barrier observes, then 25 removes and 10 puts: the live size (15) and the
+    bound entries (40) straddle a resize, and the map holds both nulls and matches of the final query."""
+    keys = np.arange(30, dtype=np.uint64) * np.uint64(1 << 20) + np.uint64(5)
+    b1 = _puts(keys, 0)
+    b1.flags[::3] = np.uint8(abi.CC_TAG_NULL)  # some stored nulls
+    b1.a[:] = 7
+    if ttl_row:
+        b1.time[:] = 1
+        b1.aux[0] = 1 << 40  # a timer that never fires in the test: the engine enters TTL mode
+    parts = [b1]
+    if with_size:
+        parts.append(_puts([0], 0, op=abi.CC_OP_MAP_SIZE, index0=31))
+    parts.append(_puts(keys[:25], 0, op=abi.CC_OP_MAP_REMOVE, index0=40))
+    b3 = _puts(np.arange(10, dtype=np.uint64) + np.uint64(1 << 50), 0, index0=70)
+    b3.a[:] = 7
+    parts.append(b3)
+    q = _puts([0], 0, op=abi.CC_OP_MAP_CONTAINSVALUE, index0=90)
+    q.a[:] = 7
+    parts.append(q)
+    if ttl_row:
+        for p in parts[1:]:
+            p.time[:] = 2
+    return parts
+
+
+def test_map_contains_value_exact_capacity():
+    """The engine tracks every map's size and HashMap capacity exactly (launch_map_size): an order-dependent
+    containsValue after an unobserved peak is answered as the reference answers it, with or without a size
+    barrier at the peak, in one batch or over several (MapState.java:49-60)."""
+    for with_size in (False, True):
+        E, O = _engines(1, 4, 64, 1024)
+        _assert_rows(*_apply_both(E, O, _peak_stream(with_size)))
+        _assert_maps(E, O, [0])
+        parts = _peak_stream(with_size)
+        one = Batch.from_columns(**{name: np.concatenate([getattr(x, name) for x in parts]) for name, _ in abi.BATCH_COLUMNS})
+        E, O = _engines(1, 4, 128, 1024)
+        _assert_rows(*_apply_both(E, O, [one]))
+
+
+def test_map_contains_value_ttl_mode_bounds():
+    """In TTL mode (entries also leave when timers fire) exact tracking stops and the capacity comes from bounds:
+    the same undetermined case then fails with CC_ERR_STATE instead of guessing; a size barrier at the peak pins
+    it and the answer is exact again."""
     from copycat_amd.engine import EngineError
 
-    def stream(with_size):
-        keys = np.arange(30, dtype=np.uint64) * np.uint64(1 << 20) + np.uint64(5)
-        b1 = _puts(keys, 0)
-        b1.flags[::3] = np.uint8(abi.CC_TAG_NULL)  # some stored nulls
-        b1.a[:] = 7
-        parts = [b1]
-        if with_size:
-            parts.append(_puts([0], 0, op=abi.CC_OP_MAP_SIZE, index0=31))
-        parts.append(_puts(keys[:25], 0, op=abi.CC_OP_MAP_REMOVE, index0=40))
-        b3 = _puts(np.arange(10, dtype=np.uint64) + np.uint64(1 << 50), 0, index0=70)
-        b3.a[:] = 7
-        parts.append(b3)
-        q = _puts([0], 0, op=abi.CC_OP_MAP_CONTAINSVALUE, index0=90)
-        q.a[:] = 7
-        parts.append(q)
-        return parts
-
     E, O = _engines(1, 4, 64, 1024)
-    parts = stream(False)
+    parts = _peak_stream(False, ttl_row=True)
     _apply_both(E, O, parts[:-1])
     with pytest.raises(EngineError) as ei:
         E.apply_host(parts[-1])
     assert ei.value.rc == abi.CC_ERR_STATE
     E, O = _engines(1, 4, 64, 1024)
-    _assert_rows(*_apply_both(E, O, stream(True)))
+    _assert_rows(*_apply_both(E, O, _peak_stream(True, ttl_row=True)))
     _assert_maps(E, O, [0])
+
+
+@pytest.mark.parametrize("n,maps,keys,sub_batch,hot,p_hot,seed", [
+    (60_000, 3, 40, 0, 0, 0.0, 301),             # sizes oscillate around the 24 / 48 thresholds inside tiles
+    (400_000, 16, 48, 16384 * 3, 2, 0.3, 302),   # several sub-batches, hot keys (k_hot_apply deltas)
+    (300_000, 200, 30, 0, 0, 0.0, 303),          # many maps, few commits per map per tile
+])
+def test_map_contains_value_churn_parity(n, maps, keys, sub_batch, hot, p_hot, seed):
+    """Put / remove churn with stored nulls and containsValue / size barriers: every containsValue whose answer
+    depends on HashMap iteration order uses the exact tracked capacity; every size barrier checks the tracked size
+    against the table (the engine fails the batch on a difference)."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed, hot=hot, p_hot=p_hot)
+    rows = _with_barriers(b, 0.0015, seed, ops=np.array([abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_SIZE], np.uint8),
+                          p=[0.8, 0.2])
+    cut = n // 2
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch)
+    gs, gv, os_, ov = _apply_both(E, O, [b.slice(0, cut), b.slice(cut, n)])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    cv = rows[b.op[rows] == abi.CC_OP_MAP_CONTAINSVALUE]
+    npe = int((gs[cv] == abi.cc_status(abi.CC_ST_NULL_POINTER, abi.CC_TAG_NULL)).sum())
+    assert 0 < npe < len(cv)  # both outcomes occur
 
 
 def test_map_clear_then_reuse_keys():
