@@ -405,11 +405,11 @@ __device__ inline void materialize(const Comp& c, const HotS0& s0, const XRec* _
   }
 }
 
-// one commit of a hot key on state (w, v): result -> staging; tracks commit/insert index
-__device__ inline void hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t idx, uint32_t& w, uint64_t& v,
-                                uint64_t& ci, uint64_t& ins, uint8_t* __restrict__ rst_status,
-                                uint64_t* __restrict__ rst_value, uint32_t slot, uint32_t* __restrict__ rst_msz,
-                                uint32_t& err) {
+// one commit of a hot key on state (w, v): result -> staging; tracks commit/insert index; returns the commit's
+// size change (1 insert, 2 remove, 0 none: the 2-bit codes of hot_msz)
+__device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t idx, uint32_t& w, uint64_t& v,
+                                    uint64_t& ci, uint64_t& ins, uint8_t* __restrict__ rst_status,
+                                    uint64_t* __restrict__ rst_value, uint32_t& err) {
   const uint32_t op = smeta_op(m);
   const int was = (w & kMwPresent) != 0;
   uint64_t rv;
@@ -424,7 +424,7 @@ __device__ inline void hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t
   }
   rst_status[g] = (uint8_t)st;
   rst_value[g] = rv;
-  rst_msz[g] = msz_word(slot, was, (w & kMwPresent) != 0);  // the commit's change of its map's size
+  return msz_word(0, was, (w & kMwPresent) != 0);
 }
 
 __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, const uint32_t* __restrict__ hot_n,
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
                                                   uint64_t* __restrict__ tbl_val, uint32_t* __restrict__ tbl_word,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ rst_msz, uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ hot_msz, uint32_t* __restrict__ err_out) {
   __shared__ uint32_t pfx[kHotMax + 1];
   __shared__ Comp wtot[kHT / kWave];
   __shared__ Comp carry;
@@ -448,16 +448,24 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
     while (pfx[h + 1] <= item) ++h;
     const uint32_t p = item - pfx[h], L = hot_len[h], P = pfx[h + 1] - pfx[h];
     const HotS0 s0 = hot_s0[h];
-    const uint32_t pos = hot[h].pos, slot = hot[h].ident & kMwSlotMask;
+    const uint32_t pos = hot[h].pos;
+    // size-change codes of the key's list (launch_map_size): 2 bits per list position, 16 per word, word
+    // pfx[h] * kHT + position / 16 (a piece's kHPer = 16 positions per thread are one word)
+    uint32_t* const msz = hot_msz + (uint64_t)pfx[h] * kHT;
     ListCursor cur{hot_rpre + (uint64_t)h * (kMaxTiles + 1), hot_rstart + (uint64_t)h * kMaxTiles, tiles, 0, 0};
     if (hot_cond[h]) {  // value-comparing ops on this key: its whole list, in order, on one thread
       if (p == 0 && t == 0) {
         uint32_t sw = s0.w;
         uint64_t sv = s0.v, ci = s0.ci, ins = s0.ins;
         cur.seek(0);
+        uint32_t codes = 0;
         for (uint32_t q = 0; q < L; ++q) {
           const uint32_t g = cur.next();
-          hot_step(g, xr[g].meta, xr[g].ab, xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, slot, rst_msz, err);
+          codes |= hot_step(g, xr[g].meta, xr[g].ab, xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, err) << (2 * (q % 16));
+          if (q % 16 == 15 || q + 1 == L) {
+            msz[q / 16] = codes;
+            codes = 0;
+          }
         }
         tbl_word[pos] = sw;
         tbl_val[pos] = sv;
@@ -512,9 +520,12 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
       uint32_t sw;
       uint64_t sv, ci, ins;
       materialize(pre, s0, xr, sw, sv, ci, ins);
+      static_assert(kHPer == 16, "one 32-bit word of size-change codes per thread and piece");
+      uint32_t codes = 0;
 #pragma unroll
       for (int q = 0; q < kHPer; ++q)
-        if (p0 + q < e) hot_step(gs[q], ms[q], xr[gs[q]].ab, xr[gs[q]].idx, sw, sv, ci, ins, rst_status, rst_value, slot, rst_msz, err);
+        if (p0 + q < e) codes |= hot_step(gs[q], ms[q], xr[gs[q]].ab, xr[gs[q]].idx, sw, sv, ci, ins, rst_status, rst_value, err) << (2 * q);
+      msz[p0 / kHPer] = codes;  // (consecutive threads: consecutive words)
       if (p == P - 1 && e == L) {  // the key's last commit: write the entry back
         tbl_word[pos] = sw;
         tbl_val[pos] = sv;
@@ -551,7 +562,7 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.xrec, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
-                     a.rst_value, a.rst_msz, a.err);
+                     a.rst_value, a.hot_msz, a.err);
   a.mark(K_MAP_HOT, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -96,7 +96,7 @@ static void free_all(cc_engine* e) {
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
-                  e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_msize,
+                  e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -259,6 +259,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
     ALLOC(e->d_rst_msz, sizeof(uint32_t) * (e->sub_batch + 4 * kPT));
+    ALLOC(e->d_hot_msz, sizeof(uint32_t) * (kHotMaxPieces + kHotMax) * (kHotPiece / 16));
     ALLOC(e->d_msize, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mpcap, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_msz_tcnt, sizeof(uint32_t) * cfg->max_resources * e->max_tiles);  // [tile][map] counts
@@ -712,7 +713,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.hot_samp = e->d_hot_samp;
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
-      ha.rst_msz = e->d_rst_msz;
+      ha.hot_msz = e->d_hot_msz;
       ha.err = e->d_err;
       ha.mark = marker_of(e);
       static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
@@ -818,7 +819,13 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.sb = e->sb_total();
         za.k0 = e->sb;
         za.k1 = e->sbq_base();
+        za.sb_hot = e->sb + (1u << e->map_bits);
         za.rst_msz = e->d_rst_msz;
+        za.hot = e->d_hot;
+        za.hot_n = e->d_hot_n;
+        za.hot_len = e->d_hot_len;
+        za.hot_rpre = e->d_hot_rpre;
+        za.hot_msz = e->d_hot_msz;
         za.res_type = e->d_res_type;
         za.max_resources = e->cfg.max_resources;
         za.tcnt = e->d_msz_tcnt;

@@ -126,7 +126,13 @@ struct MapSizeArgs {
   uint64_t rows;               // rows of the sub-batch
   uint32_t sb;                 // ttab row width - 1
   uint32_t k0, k1;             // the map and hot-key buckets [k0, k1)
-  const uint32_t* rst_msz;
+  uint32_t sb_hot;             // the first hot-key bucket
+  const uint32_t* rst_msz;     // region records (k_apply_map)
+  const HotKey* hot;           // hot-key records (k_hot_apply): codes per hot list position
+  const uint32_t* hot_n;
+  const uint32_t* hot_len;
+  const uint32_t* hot_rpre;
+  const uint32_t* hot_msz;
   const uint8_t* res_type;
   uint32_t max_resources;
   uint32_t* tcnt;              // [tiles][max_resources] (inserts | removes << 16) per (tile, map)
@@ -225,7 +231,7 @@ struct HotArgs {
   void* hot_samp;        // [65536] resolved detection sample (apply_map_hot.hip HotSamp)
   uint8_t* rst_status;
   uint64_t* rst_value;
-  uint32_t* rst_msz;
+  uint32_t* hot_msz;     // [(kHotMaxPieces + kHotMax) * kHotPiece / 16] 2-bit size-change codes per list position
   uint32_t* err;
   Marker mark;
 };

@@ -138,7 +138,8 @@ struct cc_engine {
   uint32_t* d_mw_peak = nullptr;   // [max_resources]
   uint64_t* d_mw_drop = nullptr;   // [max_resources]
   // exact map sizes / HashMap capacities (map_wide.hip launch_map_size; not in TTL mode)
-  uint32_t* d_rst_msz = nullptr;   // [sub_batch + 4 kPT] each map commit's map and size change, staging order
+  uint32_t* d_rst_msz = nullptr;   // [sub_batch + 4 kPT] each region map commit's map and size change, staging order
+  uint32_t* d_hot_msz = nullptr;   // hot-key commits' size changes (HotArgs::hot_msz)
   uint32_t* d_msize = nullptr;     // [max_resources]
   uint32_t* d_mpcap = nullptr;     // [max_resources]
   uint32_t* d_msz_tcnt = nullptr;  // [max_tiles][max_resources]

@@ -378,10 +378,13 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
 
 // ---- exact map sizes and capacities (MapState's java.util.HashMap: size, and the table capacity its peak size
 //      set, HashMap.putVal / resize) ----
-// k_apply_map / k_hot_apply write one word per map record (msz_word: the map slot and whether the commit inserted
-// or removed a key).  Then, per sub-batch:
-// 1. k_msize_count, one workgroup per partition tile: its map records' words (one coalesced span) counted per map
-//    in LDS (direct-indexed, 16384 maps per pass), the tile's row of tcnt written whole (coalesced, zeros included).
+// k_apply_map writes one word per region record (msz_word: the map slot and whether the commit inserted or removed a
+// key); k_hot_apply writes 2-bit codes per position of each hot key's list, 16 per word (one coalesced word per
+// thread and piece: a word per commit at the hot commits' staging positions cost ~7 ms per c3 step in partial-line
+// writes).  Then, per sub-batch:
+// 1. k_msize_count, one workgroup per partition tile: the region records' words (one coalesced span) and each hot
+//    key's codes for its run in the tile (popcounts) counted per map in LDS (direct-indexed, 16384 maps per pass);
+//    the tile's row of tcnt written whole (coalesced, zeros included).
 // 2. k_msize_scan, one workgroup per 64 maps (lane = map, wave = a chunk of tiles): the size at every tile start (a
 //    prefix sum of inserts - removes in log order), per tile the capacity level bounds [level(max(size before, size
 //    after)), level(size before + inserts)], L = the highest lower bound (and the level so far).  Only a tile whose
@@ -393,13 +396,39 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
 constexpr int kMszT = 1024;
 constexpr uint32_t kMszPass = 16384;  // maps counted per LDS pass (64 KB)
 
+// hot-key list helpers: word of list position lp of key h (pfx: the keys' piece prefix, as k_hot_apply's)
+constexpr uint32_t kHotWords = kHotPiece / 16;  // code words per hot piece
+__device__ inline uint32_t hot_code(const uint32_t* __restrict__ hot_msz, const uint32_t* pfx, uint32_t h, uint32_t lp) {
+  return (hot_msz[(uint64_t)pfx[h] * kHotWords + lp / 16] >> (2 * (lp % 16))) & 3u;
+}
+__device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len, uint32_t* pfx,
+                               uint32_t& nh) {
+  nh = hot_n ? *hot_n : 0u;
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (uint32_t h = 0; h < nh; ++h) {
+      pfx[h] = s;
+      s += (hot_len[h] + kHotPiece - 1) / kHotPiece;
+    }
+    pfx[nh] = s;
+  }
+  lds_barrier();
+}
+
 __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restrict__ ttab, uint32_t sb, uint32_t k0,
-                                                      uint32_t k1, const uint32_t* __restrict__ msz, uint32_t R,
-                                                      uint32_t* __restrict__ tcnt) {
+                                                      uint32_t sb_hot, const uint32_t* __restrict__ msz,
+                                                      const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n,
+                                                      const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
+                                                      const uint32_t* __restrict__ hot_msz, uint32_t R,
+                                                      uint32_t* __restrict__ tcnt, uint32_t* __restrict__ list_n) {
   __shared__ uint32_t cnt[kMszPass];
-  const uint32_t t = blockIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *list_n = 0;  // (k_msize_scan, the next launch, appends to the list)
+  __shared__ uint32_t pfx[kHotMax + 1];
+  const uint32_t t = blockIdx.x, wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  uint32_t nh;
+  hot_pfx(hot_n, hot_len, pfx, nh);
   const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
-  const uint32_t b0 = row[k0], b1 = row[k1];
+  const uint32_t b0 = row[k0], b1 = row[sb_hot];
   const uint32_t* w = msz + (uint64_t)t * kTile;
   uint32_t* out = tcnt + (uint64_t)t * R;
   for (uint32_t base = 0; base < R; base += kMszPass) {
@@ -409,6 +438,27 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
       const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
       if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
+    }
+    for (uint32_t h = wv; h < nh; h += kMszT / kWave) {  // one wave per hot key: its run in this tile
+      const uint32_t m = (hot[h].ident & kMwSlotMask) - base;
+      const uint32_t* rp = hot_rpre + (uint64_t)h * (kMaxTiles + 1);
+      const uint32_t lp0 = rp[t], lp1 = rp[t + 1];
+      if (m >= span || lp0 >= lp1) continue;  // (wave-uniform)
+      uint32_t ins = 0, rem = 0;
+      for (uint32_t wd = lp0 / 16 + l; wd * 16 < lp1; wd += kWave) {
+        uint32_t x = hot_msz[(uint64_t)pfx[h] * kHotWords + wd];
+        const uint32_t a = wd * 16 < lp0 ? lp0 - wd * 16 : 0u, b = lp1 - wd * 16 < 16u ? lp1 - wd * 16 : 16u;
+        x &= (b == 16u ? ~0u : (1u << (2 * b)) - 1u) & ~((1u << (2 * a)) - 1u);  // positions [a, b) of the word
+        const uint32_t lo = x & 0x55555555u, hi = (x >> 1) & 0x55555555u;
+        ins += __popc(lo & ~hi);
+        rem += __popc(hi & ~lo);
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        ins += __shfl_xor(ins, d, 64);
+        rem += __shfl_xor(rem, d, 64);
+      }
+      if (l == 0 && (ins | rem)) atomicAdd(&cnt[m], ins | (rem << 16));
     }
     lds_barrier();
     for (uint32_t q = threadIdx.x; q < span; q += kMszT) out[base + q] = cnt[q];
@@ -485,28 +535,46 @@ __global__ __launch_bounds__(kMszScanW * kWave) void k_msize_scan(const uint8_t*
 }
 
 __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restrict__ ttab, const uint16_t* __restrict__ cpos,
-                                                      uint64_t rows, uint32_t sb, uint32_t k0, uint32_t k1,
-                                                      const uint32_t* __restrict__ msz, const uint4* __restrict__ list,
+                                                      uint64_t rows, uint32_t sb, uint32_t k0, uint32_t k1, uint32_t sb_hot,
+                                                      const uint32_t* __restrict__ msz, const HotKey* __restrict__ hot,
+                                                      const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len,
+                                                      const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_msz,
+                                                      const uint4* __restrict__ list,
                                                       const uint32_t* __restrict__ list_n, uint32_t* __restrict__ mpcap) {
   constexpr int kPer = kTile / kMszT;
   __shared__ int32_t wsum[kMszT / kWave], wmax[kMszT / kWave];
+  __shared__ uint32_t pfx[kHotMax + 1];
   const uint32_t n = min(*list_n, kMszListCap), w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  uint32_t nh;
+  hot_pfx(hot_n, hot_len, pfx, nh);
   for (uint32_t it = blockIdx.x; it < n; it += gridDim.x) {
     const uint4 e = list[it];
     const uint32_t t = e.x, m = e.y;
     const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
-    const uint32_t b0 = row[k0], b1 = row[k1];
+    const uint32_t b0 = row[k0], bh = row[sb_hot], b1 = row[k1];
     const uint64_t base = (uint64_t)t * kTile;
     int32_t sum = 0, mx = 0;  // this thread's rows (consecutive, log order): net change, highest running value
-#pragma unroll 4
     for (int j = 0; j < kPer; ++j) {
       const uint64_t r = base + (uint64_t)threadIdx.x * kPer + j;
       if (r >= rows) break;
       const uint32_t p = cpos[r];
       if (p < b0 || p >= b1) continue;  // unknown session (0xFFFF) or not a map record
-      const uint32_t x = msz[base + p];
-      if ((x >> 2) != m || !(x & 3u)) continue;
-      sum += (x & 3u) == 1u ? 1 : -1;
+      uint32_t code;
+      if (p < bh) {  // a region record
+        const uint32_t x = msz[base + p];
+        if ((x >> 2) != m) continue;
+        code = x & 3u;
+      } else {  // a hot key's record: its bucket (the last hot bucket starting at or before p), list position
+        uint32_t a = 0, b = nh;
+        while (b - a > 1) {
+          const uint32_t c = (a + b) >> 1;
+          if (row[sb_hot + c] <= p) a = c; else b = c;
+        }
+        if ((hot[a].ident & kMwSlotMask) != m) continue;
+        code = hot_code(hot_msz, pfx, a, hot_rpre[(uint64_t)a * (kMaxTiles + 1) + t] + (p - row[sb_hot + a]));
+      }
+      if (!code) continue;
+      sum += code == 1u ? 1 : -1;
       mx = max(mx, sum);
     }
     int32_t inc = sum;
@@ -535,13 +603,12 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
 
 int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
-  if (hipMemsetAsync(a.list_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
-  hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.k1, a.rst_msz,
-                     a.max_resources, a.tcnt);
+  hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.sb_hot, a.rst_msz, a.hot,
+                     a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n);
   hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,
                      a.res_type, a.max_resources, a.tiles, a.tcnt, a.msize, a.mpcap, a.list, a.list_n);
-  hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.rst_msz,
-                     a.list, a.list_n, a.mpcap);
+  hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.sb_hot,
+                     a.rst_msz, a.hot, a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.list, a.list_n, a.mpcap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
