@@ -27,6 +27,7 @@ constexpr int kXJ = kChunkMaps / kPT;  // commits per thread per chunk (2)
 constexpr int kXCh = kTile / kChunkMaps;  // chunks per tile (8)
 constexpr int kXQ = kXJ * kXCh;        // commits per thread per tile (16)
 constexpr uint32_t kRpDead = 0xFFFFFFFFu;
+constexpr uint32_t kTpWalk = 0x80u;  // type byte flag: a value commit of a super-bucket k_apply_value walks
 }  // namespace
 
 #ifdef CC_PHASE_TIMING
@@ -71,8 +72,12 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   uint64_t* hkey = hh64 + kHotMax;
   uint32_t* hident = reinterpret_cast<uint32_t*>(hkey + kHotMax);
 
+  // sb_kind in LDS: a global load whose value is used right away waits for every load issued before it (one
+  // in-order counter)
+  __shared__ uint8_t skind[kMaxSb];
   PH_DECL
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  for (uint32_t q = t; q < sb_val; q += kPT) skind[q] = sb_kind[q];
   const uint64_t cbase0 = clock_base ? *clock_base : 0;
   const bool deferred = (ext_flags & kExtDeferred) != 0;
   // the log clock must not go backwards (each row against the row before it; replaces k_time_check when the batch
@@ -107,7 +112,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 
   // ---- 0. route every commit of the tile (one batch of loads per stage), histogram from registers ----
   uint32_t rp[kXQ];     // resource slot | super-bucket << 17; kRpDead: unknown session / past the batch
-  uint32_t tp[kXQ / 4]; // resource type, 4 per word
+  uint32_t tp[kXQ / 4]; // resource type | kTpWalk (a k_apply_value record), 4 per word
 #pragma unroll
   for (int q = 0; q < kXQ / 4; ++q) tp[q] = 0;
 #pragma unroll
@@ -158,13 +163,14 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
             }
           }
         }
-      } else if (sbq_base && sb_kind[r >> kSbShift]) {
+      } else if (sbq_base && skind[r >> kSbShift]) {
         k = sbq_base + (r >> 6);  // quarter bucket (k_apply_coord)
       } else {
         k = r >> kSbShift;
       }
       rp[q] = r | (k << 17);
-      tp[q / 4] |= ty[u] << (8 * (q % 4));
+      const uint32_t vw = ty[u] == CC_RES_VALUE && !skind[r >> kSbShift] ? kTpWalk : 0u;
+      tp[q / 4] |= (ty[u] | vw) << (8 * (q % 4));
       atomicAdd(&ctot32[k >> 1], 1u << (16 * (k & 1)));
     }
   }
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const int q = qb + j;
       const uint64_t i0 = tile0 + (uint64_t)ch * C + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
       const uint64_t i = i0 < tile1 ? i0 : lo;
-      const uint32_t ty = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      const uint32_t tyb = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu, ty = tyb & ~kTpWalk;
       const bool dead = rp[q] == kRpDead;
       const uint32_t iv = inst[i];
       const uint32_t mv = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       in_[j] = dead ? kNoRes : iv;
       mt_[j] = dead ? 0u : mv;
       const bool lock = ty == CC_RES_LOCK;
-      const bool val_walk = ty == CC_RES_VALUE && !sb_kind[(rp[q] & 0x1FFFFu) >> kSbShift];
+      const bool val_walk = (tyb & kTpWalk) != 0;
       ab_[j].x = dead ? 0 : (lock ? t0 : av);
       ab_[j].y = dead ? 0 : (lock ? t1 : bv);
       xa_[j] = dead || val_walk ? 0 : ((lock || is_keyed(ty)) ? xv : 0);
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       ab_[j] = u64x2{0, 0};
       kk_[j] = ii_[j] = xa_[j] = 0;
       if (rp[q] == kRpDead) continue;
-      const uint32_t ty = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      const uint32_t tyb = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu, ty = tyb & ~kTpWalk;
       in_[j] = inst[i];
       mt_[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
       if (ty == CC_RES_LOCK) {  // clock of this commit and of the one before it (deterministic log time)
@@ -259,8 +265,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       }
       ab_[j].x = ca[i];
       ab_[j].y = cb[i];
-      const bool val_walk = ty == CC_RES_VALUE && !sb_kind[(rp[q] & 0x1FFFFu) >> kSbShift];
-      if (val_walk) continue;  // k_apply_value records: the encoded operands only
+      if (tyb & kTpWalk) continue;  // k_apply_value records: the encoded operands only
       ii_[j] = cidx ? cidx[i] : 0;
       {
         kk_[j] = ckey ? ckey[i] : 0;
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       meta[j] = mt[j];
       xs[j] = in[j];
       if (!live[j]) continue;
-      const uint32_t ty = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      const uint32_t tyb = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu, ty = tyb & ~kTpWalk;
       if (is_keyed(ty)) {
         if (ty == CC_RES_SET || ty == CC_RES_MULTIMAP) {  // an element / multimap key holds Boolean TRUE
           uint32_t fl = (meta[j] >> 8) & 0xFF;
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
         }
         xs[j] = res[j];
         if ((int64_t)xa[j] > 0 && ty != CC_RES_MULTIMAP) meta[j] |= kMetaTtl;
-      } else if (ty == CC_RES_VALUE && !sb_kind[res[j] >> kSbShift]) {
+      } else if (tyb & kTpWalk) {
         value_encode(meta[j] & 0xFF, (meta[j] >> 8) & 0xFF, ab[j].x, ab[j].y, meta[j], ab[j]);
       } else if (ty == CC_RES_LOCK) {
         const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const uint32_t s = p / 3, part = p - 3 * s;
       const uint32_t k = rsb[s];
       const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
-      if (k < sb_val && !sb_kind[k]) {
+      if (k < sb_val && !skind[k]) {
         if (part == 0) {
           st_meta[g] = rmeta[s];
           st_ab[g] = rab[s];
