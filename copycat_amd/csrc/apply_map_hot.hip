@@ -320,11 +320,13 @@ __device__ inline void hot_items(const uint32_t* __restrict__ hot_n, const uint3
   __syncthreads();
 }
 
-// staging positions of list positions [p0, p0 + cnt): walk the tile runs from the run holding p0
+// staging positions of list positions [p0, p0 + cnt): walk the tile runs from the run holding p0.  The key's run
+// table is an LDS copy (hot_runs_lds) and the current run's end and base stay in registers: read from HBM, the
+// binary search and one dependent load per position made every piece a chain of ~30 global round trips.
 struct ListCursor {
-  const uint32_t* rpre;
-  const uint32_t* rstart;
-  uint32_t tiles, tile, pos;
+  const uint32_t* rpre;    // [tiles + 1] list prefix per tile (LDS)
+  const uint32_t* rstart;  // [tiles] staging start of the key's run per tile (LDS)
+  uint32_t tiles, tile, pos, nxt, base;
   __device__ void seek(uint32_t p) {
     uint32_t a = 0, b = tiles;  // last tile with rpre <= p
     while (b - a > 1) {
@@ -333,12 +335,35 @@ struct ListCursor {
     }
     tile = a;
     pos = p;
+    nxt = rpre[a + 1];
+    base = rstart[a] - rpre[a];
   }
   __device__ uint32_t next() {
-    while (pos >= rpre[tile + 1]) ++tile;
-    return rstart[tile] + (pos++ - rpre[tile]);
+    while (pos >= nxt) {
+      ++tile;
+      nxt = rpre[tile + 1];
+      base = rstart[tile] - rpre[tile];
+    }
+    return base + pos++;
   }
 };
+// the item's key h (binary search over the piece prefix) and its run table copied into LDS (all threads; the
+// caller's previous item must be finished with the copy: a barrier at the top)
+__device__ inline uint32_t hot_item_key(const uint32_t* pfx, uint32_t nh, uint32_t item) {
+  uint32_t a = 0, b = nh;  // last key with pfx <= item
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (pfx[m] <= item) a = m; else b = m;
+  }
+  return a;
+}
+__device__ inline void hot_runs_lds(const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_rstart,
+                                    uint32_t h, uint32_t tiles, uint32_t* lrpre, uint32_t* lrst) {
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q <= tiles; q += blockDim.x) lrpre[q] = hot_rpre[(uint64_t)h * (kMaxTiles + 1) + q];
+  for (uint32_t q = threadIdx.x; q < tiles; q += blockDim.x) lrst[q] = hot_rstart[(uint64_t)h * kMaxTiles + q];
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(kHT) void k_hot_agg(const XRec* __restrict__ xr, const uint32_t* __restrict__ hot_n,
                                                 const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
@@ -346,15 +371,16 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const XRec* __restrict__ xr, co
                                                 Comp* __restrict__ agg, uint32_t* __restrict__ hot_cond) {
   __shared__ uint32_t pfx[kHotMax + 1];
   __shared__ Comp wtot[kHT / kWave];
+  __shared__ uint32_t lrpre[kMaxTiles + 1], lrst[kMaxTiles];
   uint32_t nh;
   hot_items(hot_n, hot_len, pfx, nh);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   for (uint32_t item = blockIdx.x; item < pfx[nh]; item += gridDim.x) {
-    uint32_t h = 0;
-    while (pfx[h + 1] <= item) ++h;
+    const uint32_t h = hot_item_key(pfx, nh, item);
+    hot_runs_lds(hot_rpre, hot_rstart, h, tiles, lrpre, lrst);
     const uint32_t p = item - pfx[h], L = hot_len[h];
     const uint32_t p0 = p * kHotPiece + t * kHPer;
-    ListCursor cur{hot_rpre + (uint64_t)h * (kMaxTiles + 1), hot_rstart + (uint64_t)h * kMaxTiles, tiles, 0, 0};
+    ListCursor cur{lrpre, lrst, tiles, 0, 0, 0, 0};
     Comp c = comp_identity();
     bool cond = false;
     if (p0 < L) {
@@ -439,20 +465,21 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
   __shared__ uint32_t pfx[kHotMax + 1];
   __shared__ Comp wtot[kHT / kWave];
   __shared__ Comp carry;
+  __shared__ uint32_t lrpre[kMaxTiles + 1], lrst[kMaxTiles];
   uint32_t nh;
   hot_items(hot_n, hot_len, pfx, nh);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   uint32_t err = 0;
   for (uint32_t item = blockIdx.x; item < pfx[nh]; item += gridDim.x) {
-    uint32_t h = 0;
-    while (pfx[h + 1] <= item) ++h;
+    const uint32_t h = hot_item_key(pfx, nh, item);
+    hot_runs_lds(hot_rpre, hot_rstart, h, tiles, lrpre, lrst);
     const uint32_t p = item - pfx[h], L = hot_len[h], P = pfx[h + 1] - pfx[h];
     const HotS0 s0 = hot_s0[h];
     const uint32_t pos = hot[h].pos;
     // size-change codes of the key's list (launch_map_size): 2 bits per list position, 16 per word, word
     // pfx[h] * kHT + position / 16 (a piece's kHPer = 16 positions per thread are one word)
     uint32_t* const msz = hot_msz + (uint64_t)pfx[h] * kHT;
-    ListCursor cur{hot_rpre + (uint64_t)h * (kMaxTiles + 1), hot_rstart + (uint64_t)h * kMaxTiles, tiles, 0, 0};
+    ListCursor cur{lrpre, lrst, tiles, 0, 0, 0, 0};
     if (hot_cond[h]) {  // value-comparing ops on this key: its whole list, in order, on one thread
       if (p == 0 && t == 0) {
         uint32_t sw = s0.w;

@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
   __shared__ uint32_t cnt[kMszPass];
   if (blockIdx.x == 0 && threadIdx.x == 0) *list_n = 0;  // (k_msize_scan, the next launch, appends to the list)
   __shared__ uint32_t pfx[kHotMax + 1];
-  const uint32_t t = blockIdx.x, wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x;
   uint32_t nh;
   hot_pfx(hot_n, hot_len, pfx, nh);
   const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
@@ -439,13 +439,13 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
       const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
       if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
     }
-    for (uint32_t h = wv; h < nh; h += kMszT / kWave) {  // one wave per hot key: its run in this tile
+    for (uint32_t h = threadIdx.x; h < nh; h += kMszT) {  // one thread per hot key: its run in this tile (a few words)
       const uint32_t m = (hot[h].ident & kMwSlotMask) - base;
       const uint32_t* rp = hot_rpre + (uint64_t)h * (kMaxTiles + 1);
       const uint32_t lp0 = rp[t], lp1 = rp[t + 1];
-      if (m >= span || lp0 >= lp1) continue;  // (wave-uniform)
+      if (m >= span || lp0 >= lp1) continue;
       uint32_t ins = 0, rem = 0;
-      for (uint32_t wd = lp0 / 16 + l; wd * 16 < lp1; wd += kWave) {
+      for (uint32_t wd = lp0 / 16; wd * 16 < lp1; ++wd) {
         uint32_t x = hot_msz[(uint64_t)pfx[h] * kHotWords + wd];
         const uint32_t a = wd * 16 < lp0 ? lp0 - wd * 16 : 0u, b = lp1 - wd * 16 < 16u ? lp1 - wd * 16 : 16u;
         x &= (b == 16u ? ~0u : (1u << (2 * b)) - 1u) & ~((1u << (2 * a)) - 1u);  // positions [a, b) of the word
@@ -453,12 +453,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
         ins += __popc(lo & ~hi);
         rem += __popc(hi & ~lo);
       }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        ins += __shfl_xor(ins, d, 64);
-        rem += __shfl_xor(rem, d, 64);
-      }
-      if (l == 0 && (ins | rem)) atomicAdd(&cnt[m], ins | (rem << 16));
+      if (ins | rem) atomicAdd(&cnt[m], ins | (rem << 16));
     }
     lds_barrier();
     for (uint32_t q = threadIdx.x; q < span; q += kMszT) out[base + q] = cnt[q];
@@ -544,6 +539,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
   constexpr int kPer = kTile / kMszT;
   __shared__ int32_t wsum[kMszT / kWave], wmax[kMszT / kWave];
   __shared__ uint32_t pfx[kHotMax + 1];
+  __shared__ uint32_t hb[kHotMax + 1], hslot[kHotMax], hlp[kHotMax];  // per item: the tile's hot runs (LDS lookups)
   const uint32_t n = min(*list_n, kMszListCap), w = threadIdx.x >> 6, l = threadIdx.x & 63;
   uint32_t nh;
   hot_pfx(hot_n, hot_len, pfx, nh);
@@ -553,6 +549,14 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
     const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
     const uint32_t b0 = row[k0], bh = row[sb_hot], b1 = row[k1];
     const uint64_t base = (uint64_t)t * kTile;
+    for (uint32_t h = threadIdx.x; h <= nh; h += kMszT) {
+      hb[h] = row[sb_hot + h];
+      if (h < nh) {
+        hslot[h] = hot[h].ident & kMwSlotMask;
+        hlp[h] = hot_rpre[(uint64_t)h * (kMaxTiles + 1) + t];
+      }
+    }
+    lds_barrier();
     int32_t sum = 0, mx = 0;  // this thread's rows (consecutive, log order): net change, highest running value
     for (int j = 0; j < kPer; ++j) {
       const uint64_t r = base + (uint64_t)threadIdx.x * kPer + j;
@@ -568,10 +572,10 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
         uint32_t a = 0, b = nh;
         while (b - a > 1) {
           const uint32_t c = (a + b) >> 1;
-          if (row[sb_hot + c] <= p) a = c; else b = c;
+          if (hb[c] <= p) a = c; else b = c;
         }
-        if ((hot[a].ident & kMwSlotMask) != m) continue;
-        code = hot_code(hot_msz, pfx, a, hot_rpre[(uint64_t)a * (kMaxTiles + 1) + t] + (p - row[sb_hot + a]));
+        if (hslot[a] != m) continue;
+        code = hot_code(hot_msz, pfx, a, hlp[a] + (p - hb[a]));
       }
       if (!code) continue;
       sum += code == 1u ? 1 : -1;
