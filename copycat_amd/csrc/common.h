@@ -12,7 +12,7 @@ constexpr int kWave = 64;                 // CDNA wavefront
 constexpr int kSbShift = 8;               // super-bucket = slot >> 8 (256 slots: one apply workgroup)
 constexpr int kMaxSb = 512;               // => max_resources <= 131072 with 256-slot super-buckets
 constexpr int kMapRegion = 2048;          // map table entries per region (one map apply workgroup, LDS-resident)
-constexpr int kMaxMapSb = 1024;           // map regions => map_capacity <= 2M entries
+constexpr int kMaxMapSb = 2048;           // map regions => map_capacity <= 2M live entries (load <= 1/2)
 constexpr int kMaxSbTotal = kMaxSb + kMaxMapSb;
 constexpr int kPT = 1024;                 // partition workgroup threads (16 waves)
 constexpr int kPW = kPT / kWave;

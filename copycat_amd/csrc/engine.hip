@@ -161,7 +161,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
     // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
-    e->quarter = tile_lds_bytes(e->sbq_base() + 4 * e->sb, true, kChunkMaps) <= 160u * 1024u;
+    e->quarter = part_ext_chunk(e->sbq_base() + 4 * e->sb) != 0;
   }
   return CC_OK;
 }
@@ -193,11 +193,15 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   if (cfg->map_capacity) {  // regions of 2048 entries, load <= 1/2
     if (cfg->map_capacity > (uint64_t)kMaxMapSb * kMapRegion / 2) {
       delete e;
-      return set_err(CC_ERR_CAPACITY, "map_capacity must be <= 1048576");
+      return set_err(CC_ERR_CAPACITY, "map_capacity must be <= 2097152");
     }
     e->map_bits = 1;
     while (((uint64_t)kMapRegion << e->map_bits) < 2 * cfg->map_capacity) ++e->map_bits;
     e->map_entries = (uint64_t)kMapRegion << e->map_bits;
+    if (part_ext_chunk(e->sbq_base()) == 0) {  // the extended partition's per-bucket LDS counters must fit
+      delete e;
+      return set_err(CC_ERR_CAPACITY, "map_capacity and max_resources together exceed the partition's bucket capacity");
+    }
   }
   // sub-batch: a multiple of the partition tile (keeps every sub-batch start 16 KiB-aligned)
   uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;

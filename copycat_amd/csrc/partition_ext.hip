@@ -23,9 +23,7 @@ namespace cc {
 #define CC_PART_EXT_UNROLL 0  // 1: the chunk loop fully unrolled (bigger code, fewer spills)
 #endif
 namespace {
-constexpr int kXJ = kChunkMaps / kPT;  // commits per thread per chunk (2)
-constexpr int kXCh = kTile / kChunkMaps;  // chunks per tile (8)
-constexpr int kXQ = kXJ * kXCh;        // commits per thread per tile (16)
+constexpr int kXQ = kTile / kPT;  // commits per thread per tile (16)
 constexpr uint32_t kRpDead = 0xFFFFFFFFu;
 constexpr uint32_t kTpWalk = 0x80u;  // type byte flag: a value commit of a super-bucket k_apply_value walks
 }  // namespace
@@ -41,6 +39,8 @@ int phase_read_partx(uint64_t* out) {
 }
 #endif
 
+// C: commits per LDS-staged chunk (2048; 1024 when the buckets' per-wave counters need the room: > 1024 map regions)
+template <int C>
 __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op, const uint8_t* __restrict__ flags,
     const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
@@ -51,8 +51,10 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
     u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab,
     uint32_t* __restrict__ err_out) {
-  constexpr int J = kXJ, C = kChunkMaps;
-  extern __shared__ __align__(16) uint8_t smem[];  // layout: partition.hip tile_lds_bytes(sb, true, kChunkMaps)
+  constexpr int J = C / kPT;       // commits per thread per chunk
+  constexpr int kXCh = kTile / C;  // chunks per tile
+  static_assert(J * kXCh == kXQ && (J == 1 || J == 2), "chunk geometry");
+  extern __shared__ __align__(16) uint8_t smem[];  // layout: partition.hip tile_lds_bytes(sb, true, C)
   u64x2* rab = reinterpret_cast<u64x2*>(smem);
   uint64_t* rkey = reinterpret_cast<uint64_t*>(rab + C);
   uint64_t* ridx = rkey + C;
@@ -429,16 +431,26 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
 #pragma unroll
     for (int q = 0; q + J < kXQ; ++q) rp[q] = rp[q + J];  // rotate to the next chunk
-    static_assert(J == 2, "type rotation packs 4 per word");
 #pragma unroll
-    for (int q = 0; q < kXQ / 4; ++q) tp[q] = (tp[q] >> 16) | (q + 1 < kXQ / 4 ? tp[q + 1] << 16 : 0u);
+    for (int q = 0; q < kXQ / 4; ++q) tp[q] = (tp[q] >> (8 * J)) | (q + 1 < kXQ / 4 ? tp[q + 1] << (32 - 8 * J) : 0u);
   }
   PH_FLUSH(g_ph_partx);
   if (tbad) atomicOr(err_out, kErrTime);
 }
 
+// chunk size of k_part_ext for sb buckets: 2048 while its LDS fits (plus the kernel's static 512 B), else 1024; 0: none
+size_t part_ext_chunk(uint32_t sb) {
+  constexpr size_t kLds = 160u * 1024u - kMaxSb;
+  if (tile_lds_bytes(sb, true, kChunkMaps) <= kLds) return kChunkMaps;
+  if (tile_lds_bytes(sb, true, kPT) <= kLds) return kPT;
+  return 0;
+}
+
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
-  hipLaunchKernelGGL(k_part_ext, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, kChunkMaps), st, a.inst, a.op,
+  const size_t c = part_ext_chunk(a.sb);
+  if (c == 0) return -1;
+  auto kern = c == (size_t)kChunkMaps ? k_part_ext<kChunkMaps> : k_part_ext<kPT>;
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
                      a.st_meta, a.st_ab, a.xrec, a.cpos, a.ttab, a.err);

@@ -183,7 +183,7 @@ typedef struct cc_config {
   uint64_t max_batch;       /* max commits per cc_apply_batch call                               */
   uint64_t max_events;      /* capacity of the device event stream per batch                      */
   uint64_t map_capacity;    /* live map entries across all CC_RES_MAP resources (0 = no maps; at most
-                               1M: the table has 2^k regions of 2048 entries, >= 2 x map_capacity) */
+                               2M: the table has 2^k regions of 2048 entries, >= 2 x map_capacity) */
   int32_t  device;          /* HIP device ordinal                                                  */
   uint32_t flags;           /* CC_CFG_* */
   uint64_t sub_batch;       /* commits per internal sub-batch (0 = default 16M; rounded up to a multiple

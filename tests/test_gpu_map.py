@@ -189,6 +189,24 @@ def test_map_resource_delete_drops_entries():
     assert (s == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_LONG)).all() and (v == np.arange(20) * 3).all()
 
 
+def test_map_capacity_2m_live_entries():
+    """map_capacity 2M (2048 table regions: the extended partition stages 1024-commit chunks so its per-bucket
+    counters fit the LDS): 1.5M distinct keys put over 512 maps, then a random key-op stream over them."""
+    from copycat_amd.workload import map_random_stream
+
+    maps, max_inst, n0 = 512, 520, 1_500_000
+    i = np.arange(n0, dtype=np.uint64)
+    b0 = Batch.from_columns(index=i + np.uint64(1), inst=(i % np.uint64(maps)).astype(np.uint32),
+                            op=np.full(n0, abi.CC_OP_MAP_PUT, np.uint8),
+                            flags=np.full(n0, abi.cc_flags(abi.CC_TAG_LONG, 0, 0), np.uint8),
+                            key=i // np.uint64(maps), a=i * np.uint64(7))
+    b1 = map_random_stream(400_000, maps, max_inst, keys=4096, seed=404, index0=n0 + 1)
+    E, O = _engines(maps, max_inst, n0, 2 << 20)
+    _assert_rows(*_apply_both(E, O, [b0, b1]))
+    _assert_maps(E, O, range(0, maps, 37))
+    assert sum(len(E.map_entries(m)[0]) for m in range(0, maps, 64)) > 1_500_000 // 64  # well past 1M live in all
+
+
 def test_map_zipf_stream_parity():
     """Config-3 stream (Zipf 0.99 put/get/remove over 1M (map, key) pairs, 4096 maps) at 2M rows."""
     from copycat_amd.workload import map_zipf_rows
