@@ -161,7 +161,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
     // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
-    e->quarter = part_ext_chunk(e->sbq_base() + 4 * e->sb) != 0;
+    e->quarter = part_ext_chunk(e->sbq_base() + 4 * e->sb, e->map_bits != 0) != 0;
   }
   return CC_OK;
 }
@@ -198,7 +198,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     e->map_bits = 1;
     while (((uint64_t)kMapRegion << e->map_bits) < 2 * cfg->map_capacity) ++e->map_bits;
     e->map_entries = (uint64_t)kMapRegion << e->map_bits;
-    if (part_ext_chunk(e->sbq_base()) == 0) {  // the extended partition's per-bucket LDS counters must fit
+    if (part_ext_chunk(e->sbq_base(), true) == 0) {  // the extended partition's per-bucket LDS counters must fit
       delete e;
       return set_err(CC_ERR_CAPACITY, "map_capacity and max_resources together exceed the partition's bucket capacity");
     }

@@ -62,7 +62,7 @@ int launch_part_v2(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st);
 size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk);
-size_t part_ext_chunk(uint32_t sb);  // k_part_ext's chunk for sb buckets (0: its LDS cannot hold them)
+size_t part_ext_chunk(uint32_t sb, bool maps);  // k_part_ext's chunk for sb buckets (0: its LDS cannot hold them)
 
 struct ValueArgs {
   const uint32_t* st_meta;

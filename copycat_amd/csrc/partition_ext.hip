@@ -11,6 +11,8 @@
 //       columns are requested at the top of the previous chunk, and with the type already known every column
 //       the record needs (key, index, ttl / timeout, clock) is in that one batch of loads.
 // Ranking, the per-wave prefix, run starts, placement and the run-by-run write-out are those of k_part_tile.
+#include <cstdlib>
+
 #include "common.h"
 #include "engine_internal.h"
 
@@ -438,16 +440,19 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   if (tbad) atomicOr(err_out, kErrTime);
 }
 
-// chunk size of k_part_ext for sb buckets: 2048 while its LDS fits (plus the kernel's static 512 B), else 1024; 0: none
-size_t part_ext_chunk(uint32_t sb) {
+// chunk size of k_part_ext for sb buckets: with maps 2048 while its LDS fits (plus the kernel's static 512 B), else
+// 1024; without maps 1024 (no scratch spills at J = 1: c5's partition 4.16 -> 3.98 ms per step; c3's is 1% slower
+// at 1024, profiles/r03/ab_chunk); 0: none fits
+size_t part_ext_chunk(uint32_t sb, bool maps) {
   constexpr size_t kLds = 160u * 1024u - kMaxSb;
-  if (tile_lds_bytes(sb, true, kChunkMaps) <= kLds) return kChunkMaps;
+  static const bool small = getenv("CC_PART_EXT_1024") != nullptr;  // A/B: 1024-commit chunks whenever they fit
+  if (maps && !small && tile_lds_bytes(sb, true, kChunkMaps) <= kLds) return kChunkMaps;
   if (tile_lds_bytes(sb, true, kPT) <= kLds) return kPT;
   return 0;
 }
 
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
-  const size_t c = part_ext_chunk(a.sb);
+  const size_t c = part_ext_chunk(a.sb, a.map_bits != 0);
   if (c == 0) return -1;
   auto kern = c == (size_t)kChunkMaps ? k_part_ext<kChunkMaps> : k_part_ext<kPT>;
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c), st, a.inst, a.op,
