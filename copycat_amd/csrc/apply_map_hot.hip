@@ -30,8 +30,11 @@
 
 namespace cc {
 
-constexpr int kHT = 256;                   // threads per hot-scan workgroup
-constexpr int kHPer = kHotPiece / kHT;     // commits per thread per piece (16)
+#ifndef CC_HOT_T
+#define CC_HOT_T 256
+#endif
+constexpr int kHT = CC_HOT_T;              // threads per hot-scan workgroup
+constexpr int kHPer = kHotPiece / kHT;     // commits per thread per piece (4)
 constexpr int kDetT = 1024;
 constexpr int kDetSlots = 4096;
 constexpr uint32_t kDetSample = 65536;
@@ -477,8 +480,8 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
     const HotS0 s0 = hot_s0[h];
     const uint32_t pos = hot[h].pos;
     // size-change codes of the key's list (launch_map_size): 2 bits per list position, 16 per word, word
-    // pfx[h] * kHT + position / 16 (a piece's kHPer = 16 positions per thread are one word)
-    uint32_t* const msz = hot_msz + (uint64_t)pfx[h] * kHT;
+    // pfx[h] * kHotPiece / 16 + position / 16 (a thread's kHPer positions of a piece are whole bytes of one word)
+    uint32_t* const msz = hot_msz + (uint64_t)pfx[h] * (kHotPiece / 16);
     ListCursor cur{lrpre, lrst, tiles, 0, 0, 0, 0};
     if (hot_cond[h]) {  // value-comparing ops on this key: its whole list, in order, on one thread
       if (p == 0 && t == 0) {
@@ -547,12 +550,15 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
       uint32_t sw;
       uint64_t sv, ci, ins;
       materialize(pre, s0, xr, sw, sv, ci, ins);
-      static_assert(kHPer == 16, "one 32-bit word of size-change codes per thread and piece");
+      static_assert(kHPer == 16 || kHPer == 8 || kHPer == 4, "size-change codes: whole bytes per thread and piece");
       uint32_t codes = 0;
 #pragma unroll
       for (int q = 0; q < kHPer; ++q)
         if (p0 + q < e) codes |= hot_step(gs[q], ms[q], xr[gs[q]].ab, xr[gs[q]].idx, sw, sv, ci, ins, rst_status, rst_value, err) << (2 * q);
-      msz[p0 / kHPer] = codes;  // (consecutive threads: consecutive words)
+      // (consecutive threads: consecutive words / halves / bytes of the code words, little-endian)
+      if (kHPer == 16) msz[p0 / 16] = codes;
+      else if (kHPer == 8) reinterpret_cast<uint16_t*>(msz)[p0 / 8] = (uint16_t)codes;
+      else reinterpret_cast<uint8_t*>(msz)[p0 / 4] = (uint8_t)codes;
       if (p == P - 1 && e == L) {  // the key's last commit: write the entry back
         tbl_word[pos] = sw;
         tbl_val[pos] = sv;

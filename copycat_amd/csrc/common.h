@@ -36,7 +36,10 @@ constexpr uint32_t kErrCapacity = 4u;
 // hot map keys (apply_map_hot.hip): detected per sub-batch, applied by a multi-workgroup scan
 constexpr int kHotMax = 256;        // hot keys per sub-batch
 constexpr int kHotSlots = 1024;     // LDS hash of the hot set in the partition kernel
-constexpr int kHotPiece = 4096;     // commits per scan piece (one workgroup)
+#ifndef CC_HOT_PIECE
+#define CC_HOT_PIECE 1024  // (4096: 16 commits per thread, ~48 KB of a wave's records in flight per step; 1024: the hot
+#endif                     //  path 32.0 -> 23.3 ms per c3 step, profiles/r03/ab_hp)
+constexpr int kHotPiece = CC_HOT_PIECE;  // commits per scan piece (one workgroup)
 constexpr int kHotMaxPieces = (16 << 20) / kHotPiece;
 struct HotKey {
   uint64_t h64;    // map_hash(slot, key tag, key)
