@@ -744,7 +744,7 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   // during the walk; the instance-id gather is issued at the top of the chunk, ahead of the rank and scan
   uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu, m0 = 0, m1 = 0, n0 = 0, n1 = 0;
   u64x2 a0{0, 0}, a1{0, 0};
-  uint64_t k0 = 0, k1 = 0, x0 = 0, x1 = 0;
+  uint64_t k0 = 0, k1 = 0, x0 = 0, x1 = 0, i0 = 0, i1 = 0;
   // Staging positions of the wave's two rows: one 64-ary search for the run of the wave's first record, then a
   // 64-run window in the lanes (run start wS, first record wP, next run's first record wB): a row's records find
   // their runs with ballots and two lane shuffles (k_apply_value_ws); a binary search per record was ten dependent
@@ -796,6 +796,8 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
     x1 = r1->idx;
     m1 = r1->meta;
     n1 = r1->res;
+    i0 = r0->pad;  // the instance id (k_part_ext writes it into the record on coordination engines)
+    i1 = r1->pad;
   };
   load_meta(0);
 #ifdef CC_PHASE_TIMING
@@ -808,15 +810,13 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
     const uint32_t gg[kCPer2] = {g0, g1}, mm[kCPer2] = {m0, m1};
     const uint32_t in[kCPer2] = {n0, n1};
     const u64x2 ab[kCPer2] = {a0, a1};
-    const uint64_t ky[kCPer2] = {k0, k1}, ix[kCPer2] = {x0, x1};
+    const uint64_t ky[kCPer2] = {k0, k1}, ix[kCPer2] = {x0, x1}, id[kCPer2] = {i0, i1};
     uint32_t sl[kCPer2], rk[kCPer2];
     bool own[kCPer2];
-    uint64_t id[kCPer2];
 #pragma unroll
     for (int j = 0; j < kCPer2; ++j) {
       sl[j] = ((mm[j] >> 16) & 0xFFu) - q0;
       own[j] = gg[j] != 0xFFFFFFFFu && sl[j] < (uint32_t)kQ;
-      id[j] = inst_id[own[j] ? in[j] : 0u];
     }
 #pragma unroll
     for (int j = 0; j < kCPer2; ++j) rk[j] = own[j] ? atomicAdd(&wc[w][sl[j]], 1u) : 0u;

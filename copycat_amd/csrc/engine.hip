@@ -161,7 +161,7 @@ static int ensure_ext(cc_engine* e, bool coord) {
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "memset coord", x);
     e->coord_on = true;
     // quarter buckets for k_apply_coord when the extended partition's LDS still fits with them
-    e->quarter = part_ext_chunk(e->sbq_base() + 4 * e->sb, e->map_bits != 0) != 0;
+    e->quarter = part_ext_chunk(e->sbq_base() + 4 * e->sb, e->map_bits != 0, true) != 0;
   }
   return CC_OK;
 }
@@ -198,7 +198,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     e->map_bits = 1;
     while (((uint64_t)kMapRegion << e->map_bits) < 2 * cfg->map_capacity) ++e->map_bits;
     e->map_entries = (uint64_t)kMapRegion << e->map_bits;
-    if (part_ext_chunk(e->sbq_base(), true) == 0) {  // the extended partition's per-bucket LDS counters must fit
+    if (part_ext_chunk(e->sbq_base(), true, false) == 0) {  // the extended partition's per-bucket LDS counters must fit
       delete e;
       return set_err(CC_ERR_CAPACITY, "map_capacity and max_resources together exceed the partition's bucket capacity");
     }
@@ -742,6 +742,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.lo = lo;
     pa.hi = hi;
     pa.inst_res = e->d_inst_res;
+    pa.inst_id = e->coord_on ? e->d_inst_id : nullptr;
     pa.res_type = e->d_res_type;
     pa.sb_kind = e->d_sb_kind;
     pa.max_inst = e->cfg.max_instances;

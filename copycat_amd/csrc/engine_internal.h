@@ -35,6 +35,7 @@ struct PartArgs {
   bool ext;               // extended staging (maps / coordination / value events)
   uint64_t lo, hi;
   const uint32_t* inst_res;
+  const uint64_t* inst_id;   // coordination engines: instance ids, carried in XRec.pad for k_apply_coord (else null)
   const uint8_t* res_type;
   const uint8_t* sb_kind;  // value super-buckets run by k_apply_coord (their value records stay unencoded)
   uint32_t max_inst;
@@ -61,8 +62,8 @@ int launch_part_value(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_v2(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st);
-size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk);
-size_t part_ext_chunk(uint32_t sb, bool maps);  // k_part_ext's chunk for sb buckets (0: its LDS cannot hold them)
+size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk, bool ids = false);  // ids: k_part_ext's instance-id plane
+size_t part_ext_chunk(uint32_t sb, bool maps, bool ids);  // k_part_ext's chunk for sb buckets (0: its LDS cannot hold them)
 
 struct ValueArgs {
   const uint32_t* st_meta;

@@ -124,11 +124,11 @@ __global__ __launch_bounds__(kHT) void k_tile_hist(const uint32_t* __restrict__ 
 
 // Per-wave counters are packed u16 pairs (a wave ranks at most 256 commits of a chunk): wc[w][k/2]; the
 // per-super-bucket tile offsets, run fills, chunk totals and chunk starts are u16 (a tile holds 16384 commits).
-size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk) {
+size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk, bool ids) {
   const size_t rec = 16 + 4 + 2 + (maps ? 4 + 8 + 8 : 0);
   const size_t hw = (sb + 1) / 2;
   const size_t hot = maps ? kHotSlots * 4 + kHotMax * (8 + 8 + 4) : 0;
-  return chunk * rec + (size_t)kPW * hw * 4 + 4 * (2 * hw) * 2 + 16 * 4 + hot;
+  return chunk * rec + (size_t)kPW * hw * 4 + 4 * (2 * hw) * 2 + 16 * 4 + hot + (maps && ids ? chunk * 8 : 0);
 }
 
 // LDS layout (dynamic): rab[C] u64x2 | [EXT: rkey[C] u64 | ridx[C] u64 | rres[C] u32] | rmeta[C] u32 |

@@ -42,13 +42,14 @@ int phase_read_partx(uint64_t* out) {
 #endif
 
 // C: commits per LDS-staged chunk (2048; 1024 when the buckets' per-wave counters need the room: > 1024 map regions)
-template <int C>
+// IDS: coordination engines (instance ids into XRec.pad; a compile-time switch, so map-only engines pay no registers)
+template <int C, bool IDS>
 __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op, const uint8_t* __restrict__ flags,
     const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
     const uint64_t* __restrict__ cidx, const uint64_t* __restrict__ caux, const uint64_t* __restrict__ ctime,
     const uint64_t* __restrict__ clock_base, uint32_t ext_flags, uint64_t lo, uint64_t hi,
-    const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
+    const uint64_t* __restrict__ inst_id, const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
     uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits, uint32_t sbq_base,
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
     u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab,
@@ -75,6 +76,9 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   uint64_t* hh64 = reinterpret_cast<uint64_t*>(hslot + kHotSlots);
   uint64_t* hkey = hh64 + kHotMax;
   uint32_t* hident = reinterpret_cast<uint32_t*>(hkey + kHotMax);
+  // coordination engines (inst_id): each record's instance id, written into XRec.pad so k_apply_coord gets it with the
+  // record instead of a dependent gather per chunk (tile_lds_bytes(..., ids) appends this plane)
+  uint64_t* rpad = reinterpret_cast<uint64_t*>(hident + kHotMax);
 
   // sb_kind in LDS: a global load whose value is used right away waits for every load issued before it (one
   // in-order counter)
@@ -278,6 +282,14 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     }
   };
   load_raw(0, 0, in, mt, ab, kk, ii, xa);
+  // instance ids of the working chunk's records: requested when its instance slots are taken into the working
+  // registers (here for chunk 0, at the take for the others), used at the next placement
+  uint64_t idv[J];
+  auto issue_ids = [&]() {
+#pragma unroll
+    for (int j = 0; j < J; ++j) idv[j] = IDS ? inst_id[in[j] < max_inst ? in[j] : 0u] : 0ull;
+  };
+  issue_ids();
 #if CC_PART_EXT_UNROLL
 #pragma unroll
 #else
@@ -384,6 +396,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       rres[s] = xs[j];
       rkey[s] = kk[j];
       ridx[s] = ii[j];
+      if (IDS) rpad[s] = idv[j];
       cp[j] = toff[sk[j]] + trun[sk[j]] + within;
     }
     lds_barrier();
@@ -401,6 +414,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
         ii[j] = nii[j];
         xa[j] = nxa[j];
       }
+      issue_ids();
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -424,7 +438,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
         u64x2 v;
         if (part == 0) v = rab[s];
         else if (part == 1) v = u64x2{rkey[s], ridx[s]};
-        else v = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), 0};
+        else v = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), IDS ? rpad[s] : 0ull};
         reinterpret_cast<u64x2*>(xrec + g)[part] = v;
       }
     }
@@ -443,20 +457,22 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 // chunk size of k_part_ext for sb buckets: with maps 2048 while its LDS fits (plus the kernel's static 512 B), else
 // 1024; without maps 1024 (no scratch spills at J = 1: c5's partition 4.16 -> 3.98 ms per step; c3's is 1% slower
 // at 1024, profiles/r03/ab_chunk); 0: none fits
-size_t part_ext_chunk(uint32_t sb, bool maps) {
+size_t part_ext_chunk(uint32_t sb, bool maps, bool ids) {
   constexpr size_t kLds = 160u * 1024u - kMaxSb;
   static const bool small = getenv("CC_PART_EXT_1024") != nullptr;  // A/B: 1024-commit chunks whenever they fit
-  if (maps && !small && tile_lds_bytes(sb, true, kChunkMaps) <= kLds) return kChunkMaps;
-  if (tile_lds_bytes(sb, true, kPT) <= kLds) return kPT;
+  if (maps && !small && tile_lds_bytes(sb, true, kChunkMaps, ids) <= kLds) return kChunkMaps;
+  if (tile_lds_bytes(sb, true, kPT, ids) <= kLds) return kPT;
   return 0;
 }
 
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
-  const size_t c = part_ext_chunk(a.sb, a.map_bits != 0);
+  const size_t c = part_ext_chunk(a.sb, a.map_bits != 0, a.inst_id != nullptr);
   if (c == 0) return -1;
-  auto kern = c == (size_t)kChunkMaps ? k_part_ext<kChunkMaps> : k_part_ext<kPT>;
-  hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c), st, a.inst, a.op,
-                     a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_res,
+  const bool ids = a.inst_id != nullptr;
+  auto kern = c == (size_t)kChunkMaps ? (ids ? k_part_ext<kChunkMaps, true> : k_part_ext<kChunkMaps, false>)
+                                      : (ids ? k_part_ext<kPT, true> : k_part_ext<kPT, false>);
+  hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c, a.inst_id != nullptr), st, a.inst, a.op,
+                     a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_id, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
                      a.st_meta, a.st_ab, a.xrec, a.cpos, a.ttab, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
