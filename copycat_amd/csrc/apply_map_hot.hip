@@ -79,10 +79,12 @@ __global__ __launch_bounds__(kDetBlk) void k_hot_sample(const uint32_t* __restri
 }
 
 // ---------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kDetT) void k_hot_detect(const HotSamp* __restrict__ samp, uint64_t lo, uint64_t hi,
-                                                     uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
-                                                     uint64_t* tbl_val, uint64_t* tbl_ci, uint64_t* tbl_ins,
-                                                     HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n) {
+// The hot keys of a batch: counted once per batch (k_hot_count, from k_hot_sample's rows spread over the whole batch:
+// correctness never depends on which keys are hot, and one batch's commits share their distribution), bound to their
+// table entries before every sub-batch (k_hot_bind: the tables change between sub-batches).  Per-sub-batch counting
+// cost ~95 us of one workgroup's LDS atomics each time (c3: 5.6 ms per step).
+__global__ __launch_bounds__(kDetT) void k_hot_count(const HotSamp* __restrict__ samp, uint64_t lo, uint64_t hi,
+                                                    HotKey* __restrict__ cand_out, uint32_t* __restrict__ cand_n) {
   __shared__ uint64_t th64[kDetSlots];
   __shared__ uint64_t tkey[kDetSlots];
   __shared__ uint32_t tident[kDetSlots];
@@ -152,6 +154,20 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const HotSamp* __restrict_
     if (rank < (uint32_t)kHotMax) sel[rank] = c;
   }
   __syncthreads();
+  const uint32_t nsel = nc < (uint32_t)kHotMax ? nc : (uint32_t)kHotMax;
+  if (t < nsel) {
+    const uint32_t q = sel[t];
+    cand_out[t] = HotKey{th64[q], tkey[q], tident[q], 0u};
+  }
+  if (t == 0) *cand_n = nsel;
+}
+
+__global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ cand, const uint32_t* __restrict__ cand_n,
+                                                   uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
+                                                   uint64_t* tbl_val, uint64_t* tbl_ci, uint64_t* tbl_ins,
+                                                   HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t nc = *cand_n;
   // bind each hot key's table entry (the tables are idle between the sub-batch's kernels): every key looks itself
   // up in parallel (thread = key); the keys not in the table yet (first sub-batches only) are inserted by one wave,
   // one lane at a time, so no two keys race for a slot; then wave 0 compacts the bound keys in rank order
@@ -160,10 +176,10 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const HotSamp* __restrict_
   uint32_t ident = 0;
   const bool valid = t < nh;
   if (valid) {
-    const uint32_t q = sel[t];
-    h = th64[q];
-    key = tkey[q];
-    ident = tident[q];
+    const HotKey c = cand[t];
+    h = c.h64;
+    key = c.key;
+    ident = c.ident;
     base = (h >> (64 - map_bits)) * kMapRegion;
   }
   auto probe = [&](bool insert, uint32_t& pos) -> bool {
@@ -210,10 +226,10 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const HotSamp* __restrict_
       for (uint64_t need = ballot(miss); need; need &= need - 1) {
         const uint32_t leader = (uint32_t)__builtin_ctzll(need);
         if (t - kWave == leader) {
-          const uint32_t q = sel[gi];
-          h = th64[q];
-          key = tkey[q];
-          ident = tident[q];
+          const HotKey c = cand[gi];
+          h = c.h64;
+          key = c.key;
+          ident = c.ident;
           base = (h >> (64 - map_bits)) * kMapRegion;
           uint32_t ip = 0;
           if (probe(true, ip)) {
@@ -234,9 +250,9 @@ __global__ __launch_bounds__(kDetT) void k_hot_detect(const HotSamp* __restrict_
     const bool ok = gi < nh && bok[gi];
     const uint64_t okm = ballot(ok);
     if (ok) {
-      const uint32_t q = sel[gi];
+      const HotKey c = cand[gi];
       const uint32_t k = nbound + (uint32_t)__builtin_popcountll(okm & lanemask_lt());
-      hot[k] = HotKey{th64[q], tkey[q], tident[q], bpos[gi]};
+      hot[k] = HotKey{c.h64, c.key, c.ident, bpos[gi]};
     }
     nbound += (uint32_t)__builtin_popcountll(okm);
   }
@@ -578,7 +594,12 @@ int launch_map_hot_detect(const HotArgs& a, hipStream_t st) {
   HotSamp* samp = reinterpret_cast<HotSamp*>(a.hot_samp);
   hipLaunchKernelGGL(k_hot_sample, dim3((S + kDetBlk - 1) / kDetBlk), dim3(kDetBlk), 0, st, a.inst, a.flags, a.key, a.lo, a.hi,
                      a.inst_res, a.res_type, a.max_inst, samp);
-  hipLaunchKernelGGL(k_hot_detect, dim3(1), dim3(kDetT), 0, st, samp, a.lo, a.hi, a.map_bits, a.tbl_key, a.tbl_word,
+  hipLaunchKernelGGL(k_hot_count, dim3(1), dim3(kDetT), 0, st, samp, a.lo, a.hi, a.hot_cand, a.hot_cand_n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_map_hot_bind(const HotArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_hot_bind, dim3(1), dim3(kDetT), 0, st, a.hot_cand, a.hot_cand_n, a.map_bits, a.tbl_key, a.tbl_word,
                      a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

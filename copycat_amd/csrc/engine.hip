@@ -90,7 +90,7 @@ static void free_all(cc_engine* e) {
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta,   e->d_val_v,     e->d_st_meta, e->d_st_ab,
                   e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
                   e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_xrec,
-                  e->d_hot,       e->d_hot_n,     e->d_hot_rpre,   e->d_hot_rstart,
+                  e->d_hot,       e->d_hot_n,     e->d_hot_cand,   e->d_hot_cand_n, e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_hot_samp, e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
@@ -259,6 +259,8 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_tbl_ins, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_hot, sizeof(HotKey) * kHotMax);
     ALLOC(e->d_hot_n, sizeof(uint32_t));
+    ALLOC(e->d_hot_cand, sizeof(HotKey) * kHotMax);
+    ALLOC(e->d_hot_cand_n, sizeof(uint32_t));
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
@@ -662,6 +664,21 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     int rc = fire_boundary(gt.deadline, 0, gt.fire_b);
     if (rc) return rc;
   }
+  if (e->map_bits && !e->ttl_live) {  // the batch's hot map keys (apply_map_hot.hip): counted once, bound per sub-batch
+    HotArgs hb{};
+    hb.inst = c->inst;
+    hb.flags = c->flags;
+    hb.key = c->key;
+    hb.lo = 0;
+    hb.hi = n;
+    hb.inst_res = e->d_inst_res;
+    hb.res_type = e->d_res_type;
+    hb.max_inst = e->cfg.max_instances;
+    hb.hot_samp = e->d_hot_samp;
+    hb.hot_cand = e->d_hot_cand;
+    hb.hot_cand_n = e->d_hot_cand_n;
+    if (launch_map_hot_detect(hb, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError());
+  }
   uint64_t cur = 0;
   size_t bi = 0;
   for (;;) {
@@ -715,6 +732,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.hot_agg = e->d_hot_agg;
       ha.hot_s0 = e->d_hot_s0;
       ha.hot_samp = e->d_hot_samp;
+      ha.hot_cand = e->d_hot_cand;
+      ha.hot_cand_n = e->d_hot_cand_n;
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.hot_msz = e->d_hot_msz;
@@ -722,7 +741,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.mark = marker_of(e);
       static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
       if (no_hot) HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
-      else if (launch_map_hot_detect(ha, st)) return set_err(CC_ERR_HIP, "hot-key detect launch", hipGetLastError()); DBG_SYNC("hot-key detect launch");
+      else if (launch_map_hot_bind(ha, st)) return set_err(CC_ERR_HIP, "hot-key bind launch", hipGetLastError()); DBG_SYNC("hot-key bind launch");
     }
     PartArgs pa{};
     pa.inst = c->inst;

@@ -224,6 +224,8 @@ struct HotArgs {
   uint64_t* tbl_ins;
   HotKey* hot;
   uint32_t* hot_n;
+  HotKey* hot_cand;      // [kHotMax] the batch's hot keys by rank (k_hot_count), bound per sub-batch (k_hot_bind)
+  uint32_t* hot_cand_n;
   uint32_t* hot_rpre;    // [kHotMax][kMaxTiles + 1]
   uint32_t* hot_rstart;  // [kHotMax][kMaxTiles]
   uint32_t* hot_len;     // [kHotMax]
@@ -237,7 +239,8 @@ struct HotArgs {
   uint32_t* err;
   Marker mark;
 };
-int launch_map_hot_detect(const HotArgs& a, hipStream_t st);
+int launch_map_hot_detect(const HotArgs& a, hipStream_t st);  // once per batch: sample + count (rows [lo, hi))
+int launch_map_hot_bind(const HotArgs& a, hipStream_t st);    // per sub-batch: the candidates' table entries
 int launch_map_hot_apply(const HotArgs& a, hipStream_t st);
 size_t hot_agg_bytes();
 size_t hot_s0_bytes();

@@ -132,6 +132,8 @@ struct cc_engine {
   // hot map keys (apply_map_hot.hip)
   HotKey* d_hot = nullptr;
   uint32_t* d_hot_n = nullptr;
+  HotKey* d_hot_cand = nullptr;      // [kHotMax] the batch's hot keys (counted once per batch)
+  uint32_t* d_hot_cand_n = nullptr;
   // whole-map ops (map_wide.hip): barrier rows of the current batch, per-map peak-size bounds, scratch
   uint32_t* d_bar = nullptr;       // [kBarCap]
   uint32_t* d_bar_n = nullptr;
