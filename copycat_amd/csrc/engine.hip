@@ -403,6 +403,7 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
   if (is_keyed(type) && !e->map_bits) return set_err(CC_ERR_CAPACITY, "map and set resources need cc_config.map_capacity > 0");
   if (type < CC_RES_VALUE || type > CC_RES_MULTIMAP) return set_err(CC_ERR_INVALID, "unknown resource type");
   if (type == CC_RES_SET) e->has_sets = true;
+  if (type == CC_RES_VALUE) e->has_values = true;
   if (type == CC_RES_MULTIMAP) {
     e->has_mmaps = true;
     int rc = ensure_leak(e, kLeakCap);
@@ -805,7 +806,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.dummy = e->sub_batch;
     va.err = e->d_err;
     va.mark = marker_of(e);
-    if (launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError()); DBG_SYNC("apply launch");
+    if ((e->has_values || !e->ext) && launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError()); DBG_SYNC("apply launch");
     if (e->map_bits) {
       if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
@@ -1864,6 +1865,7 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   e->applied_pending = false;
   HIPCHECK(hipMemcpy(e->d_last_index, &e->applied, sizeof(uint64_t), hipMemcpyHostToDevice));
   e->has_sets = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_SET) != e->res_type.end();
+  e->has_values = e->has_values || std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_VALUE) != e->res_type.end();
   e->has_mmaps = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_MULTIMAP) != e->res_type.end();
   if (e->has_mmaps && (rc = ensure_leak(e, kLeakCap))) return rc;
   e->sess_next = h.sess_next;

@@ -155,6 +155,7 @@ struct cc_engine {
   uint32_t* d_ttl_seen = nullptr;
   bool ttl_live = false;
   bool has_sets = false;
+  bool has_values = false;  // an AtomicValueState resource was ever created (else k_apply_value is not launched)
   bool has_mmaps = false;  // MultiMapState resources share the map table too (every Put lands in the leak log)  // SetState resources share the map table (results rewritten by k_set_results)
   // MembershipGroupState.schedule timers (MembershipGroupState.java:86-103): armed by schedule barrier rows, fired
   // at the batch boundary where the reference's fire_due runs (host-ordered by (deadline, id))
