@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_count(const HotSamp* __restrict__
   __syncthreads();
   // hot: >= 1/4096 of the sample (Zipf 0.99 over 1M pairs: the ~280 heaviest keys).  Every key left in the regions
   // then carries < 0.025% of the sub-batch, so no region's chain is more than a few times the average one.
-  const uint32_t thresh = S / 4096 > 16 ? S / 4096 : 16;
+  const uint32_t thresh = S / (16 * kHotMax) > 16 * 256 / kHotMax ? S / (16 * kHotMax) : 16 * 256 / kHotMax;
   for (uint32_t q = t; q < kDetSlots; q += kDetT) {
     if (th64[q] != 0 && tcnt[q] >= thresh) {
       const uint32_t k = atomicAdd(&ncand, 1u);

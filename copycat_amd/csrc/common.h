@@ -34,7 +34,10 @@ constexpr uint32_t kErrUnsupported = 1u;
 constexpr uint32_t kErrEvents = 2u;
 constexpr uint32_t kErrCapacity = 4u;
 // hot map keys (apply_map_hot.hip): detected per sub-batch, applied by a multi-workgroup scan
-constexpr int kHotMax = 256;        // hot keys per sub-batch
+#ifndef CC_HOT_MAX
+#define CC_HOT_MAX 256
+#endif
+constexpr int kHotMax = CC_HOT_MAX;  // hot keys per sub-batch
 constexpr int kHotSlots = 1024;     // LDS hash of the hot set in the partition kernel
 #ifndef CC_HOT_PIECE
 #define CC_HOT_PIECE 1024  // (4096: 16 commits per thread, ~48 KB of a wave's records in flight per step; 1024: the hot
