@@ -384,7 +384,8 @@ __device__ inline void hot_runs_lds(const uint32_t* __restrict__ hot_rpre, const
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kHT) void k_hot_agg(const XRec* __restrict__ xr, const uint32_t* __restrict__ hot_n,
+// (reads each hot commit's meta word from the compact copy k_part_ext writes, hot_meta, not from its 48-byte record)
+__global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ hot_meta, const uint32_t* __restrict__ hot_n,
                                                 const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
                                                 const uint32_t* __restrict__ hot_rstart, uint32_t tiles,
                                                 Comp* __restrict__ agg, uint32_t* __restrict__ hot_cond) {
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const XRec* __restrict__ xr, co
       const uint32_t e = p0 + kHPer < L ? p0 + kHPer : L;
       for (uint32_t q = p0; q < e; ++q) {
         const uint32_t g = cur.next();
-        const uint32_t m = xr[g].meta;
+        const uint32_t m = hot_meta[g];
         cond |= compares_value(m);
         c = compose(c, element(m, g));
       }
@@ -611,7 +612,7 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_lists, dim3(kHotMax), dim3(kHT), 0, st, a.ttab, a.tiles, a.sb, sb_hot, a.hot, a.hot_n, a.tbl_val,
                      a.tbl_word, a.tbl_ci, a.tbl_ins, a.hot_rpre, a.hot_rstart, a.hot_len, a.hot_cond,
                      reinterpret_cast<HotS0*>(a.hot_s0));
-  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.xrec, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
+  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.hot_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
                      a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond);
   hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.xrec, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,

@@ -90,7 +90,7 @@ static void free_all(cc_engine* e) {
   void* ptrs[] = {e->d_inst_res, e->d_res_type, e->d_val_meta,   e->d_val_v,     e->d_st_meta, e->d_st_ab,
                   e->d_err,      e->d_last_index, e->d_cpos,    e->d_ttab,      e->d_rst_status, e->d_rst_value,
                   e->d_tbl_key,  e->d_tbl_word, e->d_tbl_val,   e->d_tbl_ci,    e->d_tbl_ins,    e->d_xrec,
-                  e->d_hot,       e->d_hot_n,     e->d_hot_cand,   e->d_hot_cand_n, e->d_hot_rpre,   e->d_hot_rstart,
+                  e->d_hot,       e->d_hot_n,     e->d_hot_cand,   e->d_hot_cand_n, e->d_hot_meta, e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_hot_samp, e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
@@ -260,6 +260,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_hot, sizeof(HotKey) * kHotMax);
     ALLOC(e->d_hot_n, sizeof(uint32_t));
     ALLOC(e->d_hot_cand, sizeof(HotKey) * kHotMax);
+    ALLOC(e->d_hot_meta, sizeof(uint32_t) * e->sub_batch);
     ALLOC(e->d_hot_cand_n, sizeof(uint32_t));
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
@@ -735,6 +736,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.hot_samp = e->d_hot_samp;
       ha.hot_cand = e->d_hot_cand;
       ha.hot_cand_n = e->d_hot_cand_n;
+      ha.hot_meta = e->d_hot_meta;
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.hot_msz = e->d_hot_msz;
@@ -775,6 +777,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
     pa.xrec = e->d_xrec;
+    pa.hot_meta = e->d_hot_meta;
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
     pa.dummy = e->sub_batch;

@@ -48,6 +48,7 @@ struct PartArgs {
   uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
   u64x2* st_ab;
   XRec* xrec;         // extended staging records (k_part_ext)
+  uint32_t* hot_meta; // maps: the meta word of each hot-bucket record again, compact (k_hot_agg reads only these)
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
   uint64_t dummy;     // first of the kPT dummy staging rows after the staging area (= sub_batch)
@@ -225,6 +226,7 @@ struct HotArgs {
   HotKey* hot;
   uint32_t* hot_n;
   HotKey* hot_cand;      // [kHotMax] the batch's hot keys by rank (k_hot_count), bound per sub-batch (k_hot_bind)
+  const uint32_t* hot_meta;  // [sub_batch] meta word of each hot-bucket record (k_part_ext), read by k_hot_agg
   uint32_t* hot_cand_n;
   uint32_t* hot_rpre;    // [kHotMax][kMaxTiles + 1]
   uint32_t* hot_rstart;  // [kHotMax][kMaxTiles]

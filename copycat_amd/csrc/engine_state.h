@@ -133,6 +133,7 @@ struct cc_engine {
   HotKey* d_hot = nullptr;
   uint32_t* d_hot_n = nullptr;
   HotKey* d_hot_cand = nullptr;      // [kHotMax] the batch's hot keys (counted once per batch)
+  uint32_t* d_hot_meta = nullptr;    // [sub_batch] hot-bucket records' meta words (k_part_ext -> k_hot_agg)
   uint32_t* d_hot_cand_n = nullptr;
   // whole-map ops (map_wide.hip): barrier rows of the current batch, per-map peak-size bounds, scratch
   uint32_t* d_bar = nullptr;       // [kBarCap]

@@ -52,8 +52,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint64_t* __restrict__ inst_id, const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
     uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits, uint32_t sbq_base,
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
-    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint16_t* __restrict__ cpos, uint16_t* __restrict__ ttab,
-    uint32_t* __restrict__ err_out) {
+    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint32_t* __restrict__ hot_meta, uint16_t* __restrict__ cpos,
+    uint16_t* __restrict__ ttab, uint32_t* __restrict__ err_out) {
   constexpr int J = C / kPT;       // commits per thread per chunk
   constexpr int kXCh = kTile / C;  // chunks per tile
   static_assert(J * kXCh == kXQ && (J == 1 || J == 2), "chunk geometry");
@@ -436,6 +436,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
         }
       } else {
         u64x2 v;
+        if (part == 0 && hot_meta && k >= sb_hot && k < sb_hot + kHotMax) hot_meta[g] = rmeta[s];
         if (part == 0) v = rab[s];
         else if (part == 1) v = u64x2{rkey[s], ridx[s]};
         else v = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), IDS ? rpad[s] : 0ull};
@@ -474,7 +475,7 @@ int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c, a.inst_id != nullptr), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_id, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
-                     a.st_meta, a.st_ab, a.xrec, a.cpos, a.ttab, a.err);
+                     a.st_meta, a.st_ab, a.xrec, a.map_bits ? a.hot_meta : nullptr, a.cpos, a.ttab, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
