@@ -72,221 +72,9 @@ __device__ inline uint32_t find_run(const uint32_t* rpre, uint32_t tiles, uint32
   return base + (uint32_t)(63 - __clzll((long long)b));
 }
 
-__global__ __launch_bounds__(kVT) void k_apply_value(const uint32_t* __restrict__ st_meta, const u64x2* __restrict__ st_ab,
-                                                    const uint16_t* __restrict__ ttab, uint32_t tiles, uint32_t sb,
-                                                    const uint8_t* __restrict__ sb_kind,
-                                                    uint32_t* __restrict__ val_meta, uint64_t* __restrict__ val_v,
-                                                    uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                    uint64_t dummy, uint32_t* __restrict__ err_out) {
-  __shared__ u64x2 sab[kVCh];                  // the chunk sorted by slot
-  __shared__ uint32_t sm[kVCh];
-  __shared__ uint64_t rval[kVCh];              // results, sorted order
-  __shared__ uint8_t rstat[kVCh];
-  __shared__ uint32_t wcnt[kVW][kVPairs];      // per-wave slot counts -> per-wave exclusive prefixes (u16 pairs)
-  __shared__ uint32_t sstart[kVSlots + 1];   // run start of every slot in the sorted chunk (+ total)
-  __shared__ uint32_t wsum[kVW];
-  __shared__ uint32_t rstart[kMaxTiles];       // staging position of this super-bucket's run in tile t
-  __shared__ uint32_t rpre[kMaxTiles + 1];     // records of this super-bucket before tile t
-
-  const uint32_t s = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
-  if (sb_kind && sb_kind[s]) return;
-  PH_DECL  // holds coordination resources / value events: k_apply_coord
-  uint32_t ms = 0;
-  uint64_t sv = 0;
-  if (t < (uint32_t)kVSlots) {
-    ms = val_meta[(uint64_t)s * kVSlots + t];
-    sv = val_v[(uint64_t)s * kVSlots + t];
-  }
-  for (uint32_t k = t; k < (uint32_t)(kVW * kVPairs); k += kVT) (&wcnt[0][0])[k] = 0;
-  // the super-bucket's list = its run in every tile, in tile order (tile-local layout of partition.hip)
-  {
-    uint32_t len = 0;
-    if (t < tiles) {
-      const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
-      const uint32_t b0 = row[s], b1 = row[s + 1];
-      rstart[t] = t * kTile + b0;
-      len = b1 - b0;
-    }
-    uint32_t inc = len;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(inc, d, 64);
-      if (l >= (uint32_t)d) inc += y;
-    }
-    if (l == 63) wsum[w] = inc;
-    lds_barrier();
-    uint32_t pre = inc - len, all = 0;
-    for (uint32_t q = 0; q < (uint32_t)kVW; ++q) {
-      const uint32_t x = wsum[q];
-      if (q < w) pre += x;
-      all += x;
-    }
-    if (t < tiles) rpre[t] = pre;
-    if (t == 0) rpre[tiles] = all;
-    lds_barrier();
-  }
-  const uint32_t cnt = rpre[tiles];
-  uint32_t err = 0;
-
-  // thread (w, j, l) holds record c0 + w*256 + j*64 + l of a chunk: log order = (w, j, l).
-  // The chunk's records are loaded into registers one chunk ahead, right after the previous chunk was placed in
-  // LDS (the same registers: nothing is copied).  All global loads and stores of an iteration are unconditional
-  // (a record past the end loads staging position 0 and stores its result to the dummy rows after the staging
-  // area) so the compiler can count outstanding VMEM operations exactly and never waits on the prefetch early.
-  // Loop-carried record registers are named scalars (m0..m3, g0..g3, ab0..ab3): as arrays the compiler keeps them
-  // in scratch, and every prefetch would wait on its scratch spill.
-  static_assert(kVPer == 4, "record registers");
-#define CC_J4(X) X(0) X(1) X(2) X(3)
-#define CC_DECL(J) uint32_t m##J = 0, g##J = kNoPos; uint4 ab##J = make_uint4(0, 0, 0, 0);
-  CC_J4(CC_DECL)
-#undef CC_DECL
-#define CC_LOAD1(J)                                                                               \
-  {                                                                                               \
-    const uint32_t crow = c0l + w * kVWaveRecs + (J) * kWave, c = crow + l;                       \
-    uint32_t gp = 0;                                                                              \
-    if (crow < cnt) { /* wave-uniform; LDS only */                                                \
-      uint32_t r = find_run(rpre, tiles, crow);                                                   \
-      if (c < cnt) {                                                                              \
-        while (rpre[r + 1] <= c) ++r; /* a lane is at most 63 records past its row's start */    \
-        gp = rstart[r] + (c - rpre[r]);                                                           \
-      }                                                                                           \
-    }                                                                                             \
-    g##J = c < cnt ? gp : kNoPos;                                                                 \
-    m##J = st_meta[gp];                                                                           \
-    ab##J = reinterpret_cast<const uint4*>(st_ab)[gp];                                            \
-  }
-#define CC_VALUE_LOAD(C0) { const uint32_t c0l = (C0); CC_J4(CC_LOAD1) }
-  CC_VALUE_LOAD(0)
-  PH(0);
-  for (uint32_t c0 = 0; c0 < cnt; c0 += kVCh) {
-    // 1a. rank each record among the wave's earlier records of its slot
-    uint32_t rank[kVPer], slot[kVPer];
-    const uint32_t mv[kVPer] = {m0, m1, m2, m3}, gv[kVPer] = {g0, g1, g2, g3};
-#pragma unroll
-    for (int j = 0; j < kVPer; ++j) {
-      slot[j] = smeta_slot(mv[j]) & (kVSlots - 1);
-      const uint32_t sh = 16 * (slot[j] & 1);
-      rank[j] = gv[j] != kNoPos ? (atomicAdd(&wcnt[w][slot[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
-    }
-    lds_barrier();
-    PH(1);
-    // 1b+1c. one wave: per slot, exclusive prefixes over the 16 waves (in place) and the chunk total, then the run
-    //        start of every slot (exclusive scan over the 256 slots; lane l owns slots 4l..4l+3 = pairs 2l, 2l+1).
-    //        u16 halves never carry: a chunk holds 4096 records.
-    if (w == 0) {
-      uint32_t a0 = 0, a1 = 0;  // running per-pair sums (packed halves)
-#pragma unroll
-      for (int q = 0; q < kVW; ++q) {
-        const uint32_t c0v = wcnt[q][2 * l], c1v = wcnt[q][2 * l + 1];
-        wcnt[q][2 * l] = a0;
-        wcnt[q][2 * l + 1] = a1;
-        a0 += c0v;
-        a1 += c1v;
-      }
-      const uint32_t r0 = a0 & 0xFFFFu, r1 = a0 >> 16, r2 = a1 & 0xFFFFu, r3 = a1 >> 16;
-      const uint32_t mine = r0 + r1 + r2 + r3;
-      uint32_t inc = mine;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (l >= (uint32_t)d) inc += y;
-      }
-      const uint32_t ex = inc - mine;
-      sstart[4 * l] = ex;
-      sstart[4 * l + 1] = ex + r0;
-      sstart[4 * l + 2] = ex + r0 + r1;
-      sstart[4 * l + 3] = ex + r0 + r1 + r2;
-      if (l == 63) sstart[kVSlots] = inc;
-    }
-    lds_barrier();
-    PH(3);
-    uint32_t run = 0, start = 0;
-    if (t < (uint32_t)kVSlots) {
-      start = sstart[t];
-      run = sstart[t + 1] - start;
-    }
-    // 1d. place records in slot order; p[j] = sorted position (results come back from there)
-    uint32_t p[kVPer];
-    const uint32_t gs[kVPer] = {g0, g1, g2, g3};
-#define CC_PLACE1(J)                                                                \
-    {                                                                               \
-      p[J] = 0;                                                                     \
-      if (g##J != kNoPos) {                                                         \
-        const uint32_t sl = slot[J];                                                \
-        const uint32_t pre = (wcnt[w][sl >> 1] >> (16 * (sl & 1))) & 0xFFFFu;       \
-        p[J] = sstart[sl] + pre + rank[J];                                          \
-        sm[p[J]] = m##J;                                                            \
-        reinterpret_cast<uint4*>(sab)[p[J]] = ab##J;                                \
-      }                                                                             \
-    }
-    CC_J4(CC_PLACE1)
-#undef CC_PLACE1
-    // the next chunk streams in during the walk
-    CC_VALUE_LOAD(c0 + kVCh)
-    lds_barrier();
-    PH(4);
-    for (uint32_t k = t; k < (uint32_t)(kVW * kVPairs); k += kVT) (&wcnt[0][0])[k] = 0;
-    // 2. thread t applies its slot's commits in log order, state in registers
-    if (t < (uint32_t)kVSlots && run) {
-      // software pipeline: the LDS reads of the next 4 records are in flight while 4 are applied (ping-pong
-      // register sets, no register moves that would wait on them)
-      uint32_t mA[4], mB[4];
-      u64x2 xA[4], xB[4];
-      const uint32_t last = start + run - 1;
-      auto fetch = [&](uint32_t k0, uint32_t (&mm)[4], u64x2 (&xx)[4]) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t pq = start + k0 + q <= last ? start + k0 + q : last;
-          mm[q] = sm[pq];
-          xx[q] = sab[pq];
-        }
-      };
-      auto walk4 = [&](uint32_t k0, const uint32_t (&mm)[4], const u64x2 (&xx)[4]) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (k0 + q < run) {
-            uint64_t rv;
-            const uint32_t stt = value_walk(mm[q], xx[q].x, xx[q].y, ms, sv, rv);
-            if (mm[q] & kVrL) err |= kErrUnsupported;
-            rstat[start + k0 + q] = (uint8_t)stt;
-            rval[start + k0 + q] = rv;
-          }
-        }
-      };
-      fetch(0, mA, xA);
-      for (uint32_t k0 = 0; k0 < run; k0 += 8) {
-        fetch(k0 + 4, mB, xB);
-        walk4(k0, mA, xA);
-        if (k0 + 4 >= run) break;
-        fetch(k0 + 8, mA, xA);
-        walk4(k0 + 4, mB, xB);
-      }
-    }
-    lds_barrier();
-    PH(5);
-    // 3. results back to the records' staging positions (contiguous within each run); unconditional stores
-#pragma unroll
-    for (int j = 0; j < kVPer; ++j) {
-      const uint64_t gp = gs[j] != kNoPos ? (uint64_t)gs[j] : dummy + t;
-      rst_status[gp] = rstat[p[j]];
-      rst_value[gp] = rval[p[j]];
-    }
-    PH(6);
-  }
-#undef CC_VALUE_LOAD
-#undef CC_LOAD1
-#undef CC_J4
-  PH_FLUSH(g_ph_value);
-  if (t < (uint32_t)kVSlots) {
-    val_meta[(uint64_t)s * kVSlots + t] = ms;
-    val_v[(uint64_t)s * kVSlots + t] = sv;
-  }
-  if (err) atomicOr(err_out, err);
-}
-
 // ---- k_apply_value_ws: the same walk with the sort pipelined behind it (loader / walker waves) -------------------
-// k_apply_value runs its phases in turn: 12 of its 16 waves idle through the walk and the 4 walking waves idle
-// through the sort.  Here waves 0-3 only walk (thread t = slot t, state in registers) and waves 4-15 only load,
+// (Round 1's k_apply_value ran its phases in turn: 12 of its 16 waves idled through the walk and the 4 walking
+// waves through the sort.)  Here waves 0-3 only walk (thread t = slot t, state in registers) and waves 4-15 only load,
 // sort and store: while the walkers apply chunk i (3072 records) out of one LDS buffer, the loaders store chunk
 // i-1's results, rank / place chunk i+1 into the other buffer and issue chunk i+2's loads.  One workgroup barrier
 // per chunk hands the buffers over; the loaders' own rank -> place step synchronises the 12 loader waves through an
@@ -632,14 +420,10 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st) {
 }
 
 int launch_apply_value(const ValueArgs& a, hipStream_t st) {
-  static const bool v1 = getenv("CC_APPLY_V1") != nullptr;  // A/B: the phase-sequential walk
   a.mark(K_APPLY_VALUE, 1, st);
   if (a.v3) {
     if (launch_apply_value_v3(a, st)) return -1;
-  } else if (v1)
-    hipLaunchKernelGGL(k_apply_value, dim3(a.sb_val), dim3(kVT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb, a.sb_kind,
-                       a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy, a.err);
-  else
+  } else
     hipLaunchKernelGGL(k_apply_value_ws, dim3(a.sb_val), dim3(kVT), 0, st, a.st_meta, a.st_ab, a.ttab, a.tiles, a.sb,
                        a.sb_kind, a.val_meta, a.val_v, a.rst_status, a.rst_value, a.dummy, a.err);
   a.mark(K_APPLY_VALUE, 0, st);

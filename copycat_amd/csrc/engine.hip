@@ -93,7 +93,7 @@ static void free_all(cc_engine* e) {
                   e->d_hot,       e->d_hot_n,     e->d_hot_cand,   e->d_hot_cand_n, e->d_hot_meta, e->d_hot_rpre,   e->d_hot_rstart,
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_hot_samp, e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
-                  e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total, e->d_inst_res16, e->d_res16,
+                  e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total,
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
@@ -141,6 +141,11 @@ static int ensure_ext(cc_engine* e, bool coord) {
     e->ext = true;
   }
   if (coord && !e->coord_on) {
+    // coordination records carry their instance id (k_part_ext's id plane: 8 more LDS bytes per chunk commit), so the
+    // partition must still fit with it; checked before anything is allocated or switched on
+    if (part_ext_chunk(e->sbq_base(), e->map_bits != 0, true) == 0)
+      return set_err(CC_ERR_CAPACITY, "map_capacity and max_resources together leave no room in the partition for "
+                                      "coordination resources / value events");
     const uint64_t slots = (uint64_t)e->sb << kSbShift;
     e->arena_cap = std::max<uint64_t>(e->cfg.max_events, 1);
     if ((rc = alloc((void**)&e->d_coord, coord_block(e->coord_cap) * slots)) ||
@@ -198,7 +203,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     e->map_bits = 1;
     while (((uint64_t)kMapRegion << e->map_bits) < 2 * cfg->map_capacity) ++e->map_bits;
     e->map_entries = (uint64_t)kMapRegion << e->map_bits;
-    if (part_ext_chunk(e->sbq_base(), true, false) == 0) {  // the extended partition's per-bucket LDS counters must fit
+    // the extended partition's per-bucket LDS counters must fit (with the instance-id plane when value events turn
+    // the coordination path on from the start; a later coordination resource is checked in ensure_ext)
+    if (part_ext_chunk(e->sbq_base(), true, (cfg->flags & CC_CFG_VALUE_EVENTS) != 0) == 0) {
       delete e;
       return set_err(CC_ERR_CAPACITY, "map_capacity and max_resources together exceed the partition's bucket capacity");
     }
@@ -210,7 +217,6 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   sub = std::min<uint64_t>(sub, (uint64_t)kMaxTiles * kTile);
   e->sub_batch = sub;
   e->max_tiles = sub / kTile;
-  e->value_v2 = getenv("CC_VALUE_V2") != nullptr;
 
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
   e->res_type.assign(slots, CC_RES_NONE);
@@ -235,10 +241,6 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if (x != hipSuccess) return fail("hipMalloc " #p, x); \
   } while (0)
   ALLOC(e->d_inst_res, sizeof(uint32_t) * cfg->max_instances);
-  if (cfg->max_resources < 0xFFFFu && cfg->max_instances <= 65536u) {
-    ALLOC(e->d_inst_res16, sizeof(uint16_t) * ((cfg->max_instances + 7) / 8 * 8));
-    ALLOC(e->d_res16, sizeof(uint16_t) * e->sub_batch);
-  }
   ALLOC(e->d_res_type, slots);
   ALLOC(e->d_val_meta, sizeof(uint32_t) * slots);
   ALLOC(e->d_val_v, sizeof(uint64_t) * slots);
@@ -781,13 +783,16 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
     pa.dummy = e->sub_batch;
-    pa.inst_res16 = e->d_inst_res16;
-    pa.res16 = e->ext ? nullptr : e->d_res16;
-    const bool v3 = !e->ext && !e->value_v2;  // value-only engines: value_path.hip
+    const bool v3 = !e->ext;  // value-only engines: value_path.hip
     pa.v3 = v3;
 
     pa.mark = marker_of(e);
-    if (launch_partition(pa, st)) return set_err(CC_ERR_HIP, "partition launch", hipGetLastError()); DBG_SYNC("partition launch");
+    if (launch_partition(pa, st)) {
+      const hipError_t x = hipGetLastError();
+      if (x == hipSuccess) return set_err(CC_ERR_CAPACITY, "the partition's LDS cannot hold this engine's buckets");
+      return set_err(CC_ERR_HIP, "partition launch", x);
+    }
+    DBG_SYNC("partition launch");
     if (e->map_bits && e->ttl_live && launch_map_rows(e->d_cpos, lo, hi, e->d_map_row, st))
       return set_err(CC_ERR_HIP, "map rows launch", hipGetLastError());
     ValueArgs va{};
@@ -1227,8 +1232,9 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   h32.insert(h32.end(), pcl.begin(), pcl.end());
   h32.insert(h32.end(), (size_t)nc, m);
   // every closed instance may drop one commit without clean() (a group member removed by close,
-  // MembershipGroupState.java:36-42; a value listener): the drained leak log gets room for m more
-  {
+  // MembershipGroupState.java:36-42; a value listener): the drained leak log gets room for m more.  Only the
+  // coordination handlers (groups, elections, value listeners) can leak; other engines skip the drain.
+  if (e->coord_on) {
     int rc2 = drain_leaks(e);
     if (!rc2) rc2 = ensure_leak(e, m);
     if (rc2) {

@@ -52,15 +52,10 @@ struct PartArgs {
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
   uint64_t dummy;     // first of the kPT dummy staging rows after the staging area (= sub_batch)
-  uint16_t* inst_res16;  // value-only engines, < 65535 resources, <= 65536 instances: u16 copy of inst_res
-  uint16_t* res16;       // ... and the resolved resource of every commit of the sub-batch (null: not this path)
   bool v3;               // value-only pipeline of value_path.hip (8192-commit tiles, 16-byte records in st_ab)
   Marker mark;
 };
 int launch_partition(const PartArgs& a, hipStream_t st);
-int launch_tile_hist16(const PartArgs& a, uint32_t tiles, hipStream_t st);
-int launch_part_value(const PartArgs& a, uint32_t tiles, hipStream_t st);
-int launch_part_v2(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st);
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st);
 size_t tile_lds_bytes(uint32_t sb, bool maps, size_t chunk, bool ids = false);  // ids: k_part_ext's instance-id plane

@@ -107,8 +107,6 @@ struct cc_engine {
   std::set<uint32_t> open_grp[16];        // per coordination type: 64-slot groups holding only that type, with room
   // device registry + state
   uint32_t* d_inst_res = nullptr;
-  uint16_t* d_inst_res16 = nullptr;  // value-only fast path (< 65535 resources, <= 65536 instances)
-  uint16_t* d_res16 = nullptr;       // [sub_batch] resolved resource per commit (same path)
   uint8_t* d_res_type = nullptr;
   uint32_t* d_val_meta = nullptr;
   uint64_t* d_val_v = nullptr;
@@ -177,7 +175,6 @@ struct cc_engine {
   void* d_hot_samp = nullptr;
   // extended staging (maps / coordination / value events) + coordination + events
   bool ext = false, coord_on = false;
-  bool value_v2 = false;
   // CC_VALUE_V2=1 at creation: the value-only engine keeps the previous pipeline (A/B)
   std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
   uint8_t* d_sb_kind = nullptr;

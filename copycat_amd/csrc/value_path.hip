@@ -1,11 +1,11 @@
-// value_path.hip — the value-only engine pipeline (the c2 headline): k_part_v3 -> k_apply_value_v3 -> k_unpermute_v3.
+// value_path.hip — the value-only engine pipeline (the c2 headline): k_part_v4 -> k_apply_value_v3 -> k_unpermute.
 //
 // Same algorithm as partition_value.hip k_part_v2 + apply_value.hip k_apply_value_ws + partition.hip k_unpermute
 // (a stable group-by of the sub-batch by super-bucket = 256 AtomicValueState slots, then one walk per slot in log
 // order, then the results back to log order), with two changes aimed at HBM bytes and CU occupancy:
 //
 //  * one 16-byte staging record per commit instead of a 4-byte meta word + a 16-byte operand pair (20 B): the meta
-//    (slot, op class, the two value tags) shares the second word with the CAS update stored as a 46-bit difference
+//    (slot, op class, the two value tags) shares the second word with the CAS update stored as a 33-bit difference
 //    from the expected value (a DistributedAtomicLong CAS loop updates by a small delta, DistributedAtomicLong.java
 //    :117-146).  A CAS whose difference does not fit keeps its row in the tile instead and the apply reads its update
 //    from the batch's b column (exact for every input; only the bytes moved differ);
@@ -21,7 +21,7 @@
 
 namespace cc {
 
-#ifdef CC_PHASE_TIMING  // diagnostics build: phase clocks of k_part_v3 (g_ph_v3p) and k_apply_value_v3 (g_ph_v3a)
+#ifdef CC_PHASE_TIMING  // diagnostics build: phase clocks of k_part_v4 (g_ph_v3p) and k_apply_value_v3 (g_ph_v3a)
 __device__ unsigned long long g_ph_v3p[kPhases], g_ph_v3a[kPhases];
 int phase_read_v3(int kernel, uint64_t* out) {
   unsigned long long z[kPhases] = {};
@@ -32,12 +32,6 @@ int phase_read_v3(int kernel, uint64_t* out) {
 }
 #endif
 
-constexpr int kV3T = 512;                 // partition / unpermute workgroup threads
-constexpr int kV3W = kV3T / kWave;        // 8 waves
-constexpr int kV3J = 4;                   // commits per thread per chunk
-constexpr int kV3C = kV3J * kV3T;         // 2048 commits per chunk
-constexpr int kV3N = kV3Tile / kV3C;      // 4 chunks per tile
-static_assert(kV3N == 4, "k_part_v3 keeps 4 chunks x 4 commits per thread in registers");
 
 // ---- the 16-byte value record -------------------------------------------------------------------------------
 // w0 = the payload the op carries (CAS: canonical expected value; set / getAndSet: canonical new value; else 0)
@@ -50,7 +44,7 @@ constexpr int kV3DeltaBits = 33;
 static_assert(kV3Tile <= (1 << 13), "the record's row field");
 
 // (The row, < 8192, is ORed into bits 18..30 of w1 where the partition places the record: v3_set_row.  Keeping it
-// out of the encode keeps k_part_v3 within 128 VGPRs.)
+// out of the encode keeps the partition within its VGPR budget.)
 __device__ inline uint4 v3_encode(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t slot) {
   const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
   const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
@@ -122,196 +116,8 @@ __device__ inline void v3_decode(const uint4& r, const uint64_t* __restrict__ cb
   }
 }
 
-// ---- k_part_v3: one 512-thread workgroup per 8192-commit tile -----------------------------------------------
-// As k_part_v2 (partition_value.hip): every thread loads the instance column of its 16 tile commits and chunk 0's raw
-// columns before anything waits, resolves the 16 instances with one batch of gathers, builds the tile histogram from
-// those registers and writes the tile's run starts (ttab row); then 4 chunks of 2048 commits: encode + rank inside
-// each wave (LDS atomics with return: same-address lanes of one instruction resolve in lane order, checked at engine
-// start), one wave takes the per-wave prefixes and chunk-sorted run starts, records are placed in LDS in sorted
-// order and written out run by run (contiguous 16-byte stores).  The input columns are read once: non-temporal loads.
-template <int KP>
-__global__ __launch_bounds__(kV3T, 4) void k_part_v3(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
-                                                    const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
-                                                    const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
-                                                    const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
-                                                    uint4* __restrict__ st_rec, uint16_t* __restrict__ cpos,
-                                                    uint16_t* __restrict__ ttab) {
-  __shared__ uint4 rab[kV3C];                  // the chunk in sorted order
-  __shared__ uint16_t rsb[kV3C];               //   super-bucket
-  __shared__ uint32_t wc[kV3W][kMaxSb / 2];    // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
-  __shared__ uint32_t hist[kMaxSb / 2];        // tile histogram (packed u16 pairs)
-  __shared__ uint16_t tpos[kMaxSb];            // tile-local position of run k's next piece
-  __shared__ uint16_t kst[kMaxSb];             // chunk-sorted start of run k
-  __shared__ uint32_t nlive_s;
-  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  PH_DECL
-  const uint32_t hw = (sb + 1) / 2;
-  const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kV3Tile;
-  const uint32_t tbase = blockIdx.x * kV3Tile;  // staging region of this tile (relative to lo)
-  for (uint32_t k = t; k < hw; k += kV3T) hist[k] = 0;
-  for (uint32_t k = t; k < (uint32_t)(kV3W * (kMaxSb / 2)); k += kV3T) (&wc[0][0])[k] = 0;
-  // commit (c, w, j, l) of the tile: row c*2048 + w*256 + j*64 + l (log order)
-  auto trow = [&](int c, int j) -> uint32_t { return (uint32_t)c * kV3C + w * (kWave * kV3J) + (uint32_t)j * kWave + l; };
-  const uint32_t nrow = (uint32_t)(hi - tile0 < (uint64_t)kV3Tile ? hi - tile0 : (uint64_t)kV3Tile);  // rows of this tile
-  uint32_t r[kV3N][kV3J];
-#pragma unroll
-  for (int c = 0; c < kV3N; ++c)
-#pragma unroll
-    for (int j = 0; j < kV3J; ++j) {
-      const uint32_t q = trow(c, j);
-      r[c][j] = q < nrow ? __builtin_nontemporal_load(inst + tile0 + q) : kNoRes;
-    }
-  uint8_t ob[kV3J], fb[kV3J];
-  uint64_t av[kV3J], bv[kV3J];
-  auto load_raw = [&](int c) {
-#pragma unroll
-    for (int j = 0; j < kV3J; ++j) {
-      const uint32_t q = trow(c, j);
-      const uint64_t ic = q < nrow ? tile0 + q : lo;
-      ob[j] = __builtin_nontemporal_load(op + ic);
-      fb[j] = __builtin_nontemporal_load(flags + ic);
-      av[j] = __builtin_nontemporal_load(ca + ic);
-      bv[j] = __builtin_nontemporal_load(cb + ic);
-    }
-  };
-  load_raw(0);
-#pragma unroll
-  for (int c = 0; c < kV3N; ++c)
-#pragma unroll
-    for (int j = 0; j < kV3J; ++j) r[c][j] = r[c][j] < max_inst ? inst_res[r[c][j]] : kNoRes;
-  lds_barrier();  // hist / wc zeroed
-#pragma unroll
-  for (int c = 0; c < kV3N; ++c)
-#pragma unroll
-    for (int j = 0; j < kV3J; ++j)
-      if (r[c][j] != kNoRes) {
-        const uint32_t k = r[c][j] >> kSbShift;
-        atomicAdd(&hist[k >> 1], 1u << (16 * (k & 1)));
-      }
-  lds_barrier();
-  if (w == 0) {  // tile-local run starts: one wave, lane l owns super-buckets [l*KP, l*KP + KP)
-    uint32_t cnt[KP], mine = 0;
-#pragma unroll
-    for (int e = 0; e < KP; ++e) {
-      const uint32_t k = l * KP + e;
-      cnt[e] = k < sb ? (hist[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : 0u;
-      mine += cnt[e];
-    }
-    uint32_t inc = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(inc, d, 64);
-      if (l >= (uint32_t)d) inc += y;
-    }
-    uint32_t run = inc - mine;
-    uint16_t* row = ttab + (uint64_t)blockIdx.x * (sb + 1);
-#pragma unroll
-    for (int e = 0; e < KP; ++e) {
-      const uint32_t k = l * KP + e;
-      if (k < sb) {
-        tpos[k] = (uint16_t)run;
-        row[k] = (uint16_t)run;
-      }
-      run += cnt[e];
-    }
-    if (l == 63) row[sb] = (uint16_t)inc;  // live commits of the tile (<= 8192)
-  }
-  PH(0);
-  // (tpos is first read after the next barrier; wave 0 wrote it before its first chunk barrier)
-#pragma unroll
-  for (int c = 0; c < kV3N; ++c) {
-    // encode and rank this chunk's records (registers: loaded one chunk ahead); then the next chunk's loads
-    uint32_t sk[kV3J], loc[kV3J];
-    uint4 rec[kV3J];
-#pragma unroll
-    for (int j = 0; j < kV3J; ++j) {
-      const bool live = r[c][j] != kNoRes;
-      rec[j] = v3_encode(ob[j], fb[j], av[j], bv[j], r[c][j] & ((1u << kSbShift) - 1));
-      sk[j] = live ? (r[c][j] >> kSbShift) : 0u;
-      const uint32_t sh = 16 * (sk[j] & 1);
-      loc[j] = live ? (atomicAdd(&wc[w][sk[j] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
-    }
-    if (c + 1 < kV3N) load_raw(c + 1);
-    PH(1);
-    lds_barrier();  // B1: the chunk's counters are complete
-    if (w == 0) {  // per super-bucket: exclusive prefix over the waves (in place), chunk totals, chunk-sorted starts
-      uint32_t tot[KP];
-#pragma unroll
-      for (int e = 0; e < KP; e += 2) {
-        const uint32_t pr = (l * KP + e) / 2;
-        uint32_t acc = 0;
-        if (pr < hw) {
-#pragma unroll
-          for (int q = 0; q < kV3W; ++q) {
-            const uint32_t x = wc[q][pr];
-            wc[q][pr] = acc;
-            acc += x;
-          }
-        }
-        tot[e] = acc & 0xFFFFu;
-        tot[e + 1] = acc >> 16;
-      }
-      uint32_t mine = 0;
-#pragma unroll
-      for (int e = 0; e < KP; ++e) mine += tot[e];
-      uint32_t inc = mine;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (l >= (uint32_t)d) inc += y;
-      }
-      uint32_t ks = inc - mine;
-#pragma unroll
-      for (int e = 0; e < KP; ++e) {
-        const uint32_t k = l * KP + e;
-        if (k < sb) kst[k] = (uint16_t)ks;
-        ks += tot[e];
-      }
-      if (l == 63) nlive_s = inc;
-    }
-    PH(2);
-    lds_barrier();  // B2: prefixes, kst, nlive_s
-    // place the records in sorted order; every commit's tile-local position (0xFFFF: unknown instance)
-#pragma unroll
-    for (int j = 0; j < kV3J; ++j) {
-      const uint32_t q = trow(c, j);
-      uint32_t cp = 0xFFFFu;
-      if (loc[j] != 0xFFFFu) {
-        const uint32_t k = sk[j];
-        const uint32_t pre = (wc[w][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-        const uint32_t sp = kst[k] + pre + loc[j];
-        rab[sp] = v3_set_row(rec[j], q);
-        rsb[sp] = (uint16_t)k;
-        cp = tpos[k] + pre + loc[j];
-      }
-      if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
-    }
-    PH(3);
-    lds_barrier();  // B3: rab / rsb complete; every wave is done reading wc and tpos of this chunk
-    // write the chunk out run by run (contiguous); the next chunk's counters are cleared behind the reads
-    const uint32_t nl = nlive_s;
-    for (uint32_t sp = t; sp < nl; sp += kV3T) {
-      const uint32_t k = rsb[sp];
-      st_rec[tbase + tpos[k] + (sp - kst[k])] = rab[sp];
-    }
-    for (uint32_t k = t; k < (uint32_t)(kV3W * hw); k += kV3T) wc[k / hw][k % hw] = 0;
-    PH(4);
-    lds_barrier();  // B4: the write-out is done reading tpos / kst / rab; counters cleared
-    if (w == 0) {  // run k's next piece starts after this chunk's records of k
-#pragma unroll
-      for (int e = 0; e < KP; ++e) {
-        const uint32_t k = l * KP + e;
-        if (k < sb) tpos[k] = (uint16_t)(tpos[k] + ((k + 1 < sb ? kst[k + 1] : nl) - kst[k]));
-      }
-    }
-    // (tpos is next read after the next chunk's B1; kst and nlive_s are rewritten by wave 0 after B1 as well)
-    PH(5);
-  }
-  PH_FLUSH(g_ph_v3p);
-}
-
 // ---- k_part_v4: one persistent 1024-thread workgroup per CU, one pass per 8192-commit tile --------------------
-// Same output as k_part_v3 (the tile's records grouped by super-bucket in log order, its ttab row and cpos), but
+// Same output as the round-3 k_part_v3 (the tile's records grouped by super-bucket in log order, its ttab row and cpos), but
 // the whole tile is ranked at once and placed into a 128 KiB LDS image of the tile's staging region, which is then
 // written out contiguously: every 128-byte line of the staging area is written whole by one instruction (k_part_v3
 // wrote each run piece per 2048-commit chunk, and lines shared by two pieces reached HBM as partial writes: 22.6 B
@@ -513,8 +319,13 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
                                                         uint32_t sb, uint32_t* __restrict__ val_meta,
                                                         uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
                                                         uint64_t* __restrict__ rst_value, uint64_t dummy,
-                                                        uint32_t* __restrict__ err_out, uint32_t diag) {
+                                                        uint32_t* __restrict__ err_out) {
   using P = V3A<NS>;
+#ifdef CC_DIAG  // diagnostics build only (-DCC_DIAG=1: no walk, 2: contiguous positions -- wrong results by design)
+  constexpr uint32_t diag = CC_DIAG;
+#else
+  constexpr uint32_t diag = 0;
+#endif
   constexpr int kWsLW = P::LW, kWsCh = P::CH, kAVT = P::T, kAVW = P::W, kVSlots3 = NS, kVPairs3 = P::NP;
   constexpr uint32_t kL0 = P::WW * kWave;       // first loader thread
   __shared__ u64x2 sab[2][kWsCh];               // chunk buffers sorted by slot; results in place {value, status}
@@ -808,61 +619,28 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
   if (err) atomicOr(err_out, err);
 }
 
-// Slots per value super-bucket: 256 by default.  CC_V3_NS128=1 (A/B) selects 128-slot buckets (two 512-thread apply
-// workgroups per CU) when the partition's per-wave counters hold the doubled bucket count: measured slower on c2
-// (apply 0.91 -> 0.98, partition 0.88 -> 0.92 ms/step, profiles/r03/ab_ns128: the apply is bound by the loaders'
-// instruction and LDS throughput, not by the latency a second workgroup would hide, and 16-record runs over-fetch).
-uint32_t v3_slots_per_bucket(uint32_t sb) {
-  static const bool ns128 = getenv("CC_V3_NS128") != nullptr && getenv("CC_PART_V3") == nullptr;
-  return ns128 && 2 * sb <= (uint32_t)kMaxSb ? 128u : 256u;
-}
-
+// Slots per value super-bucket: 256.  (128-slot buckets -- two 512-thread apply workgroups per CU -- measured slower
+// on c2: apply 0.91 -> 0.98, partition 0.88 -> 0.92 ms/step, profiles/r03/ab_ns128: the apply is bound by the loaders'
+// instruction and LDS throughput, not by the latency a second workgroup would hide, and 16-record runs over-fetch.)
 int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   if (a.sb > (uint32_t)kMaxSb || tiles > (uint32_t)kV3MaxTiles) return -1;
-  static const bool v3_part = getenv("CC_PART_V3") != nullptr;  // A/B: the chunked 512-thread partition
-  if (!v3_part) {
-    const uint32_t grid = tiles < (uint32_t)kPersistGrid ? tiles : (uint32_t)kPersistGrid;
-    const bool half = v3_slots_per_bucket(a.sb) == 128;
-    const uint32_t nsb = half ? 2 * a.sb : a.sb;  // super-buckets (ttab row length - 1)
-    const uint32_t kp = (nsb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
-#define CC_LAUNCH4(KP, KSB)                                                                                           \
-  hipLaunchKernelGGL((k_part_v4<KP, KSB>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi, \
-                     a.inst_res, a.max_inst, nsb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
-    if (half) {
-      if (kp <= 2) CC_LAUNCH4(2, 7);
-      else if (kp <= 4) CC_LAUNCH4(4, 7);
-      else CC_LAUNCH4(8, 7);
-    } else {
-      if (kp <= 2) CC_LAUNCH4(2, 8);
-      else if (kp <= 4) CC_LAUNCH4(4, 8);
-      else CC_LAUNCH4(8, 8);
-    }
-#undef CC_LAUNCH4
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
+  const uint32_t grid = tiles < (uint32_t)kPersistGrid ? tiles : (uint32_t)kPersistGrid;
   const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
-#define CC_LAUNCH(KP)                                                                                               \
-  hipLaunchKernelGGL((k_part_v3<KP>), dim3(tiles), dim3(kV3T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,    \
-                     a.inst_res, a.max_inst, a.sb, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
-  if (kp <= 2) CC_LAUNCH(2);
-  else if (kp <= 4) CC_LAUNCH(4);
-  else CC_LAUNCH(8);
-#undef CC_LAUNCH
+#define CC_LAUNCH4(KP)                                                                                                 \
+  hipLaunchKernelGGL((k_part_v4<KP, 8>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,   \
+                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
+  if (kp <= 2) CC_LAUNCH4(2);
+  else if (kp <= 4) CC_LAUNCH4(4);
+  else CC_LAUNCH4(8);
+#undef CC_LAUNCH4
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
   if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
-  static const uint32_t diag = getenv("CC_V3_DIAG") ? (uint32_t)atoi(getenv("CC_V3_DIAG")) : 0u;  // diagnostics only
-  const uint32_t ns = v3_slots_per_bucket(a.sb);
-  if (ns == 128)
-    hipLaunchKernelGGL(k_apply_value_v3<128>, dim3(a.sb * 2), dim3(V3A<128>::T), 0, st,
-                       reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb * 2, a.val_meta,
-                       a.val_v, a.rst_status, a.rst_value, a.dummy, a.err, diag);
-  else
-    hipLaunchKernelGGL(k_apply_value_v3<256>, dim3(a.sb_val), dim3(V3A<256>::T), 0, st,
-                       reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
-                       a.rst_status, a.rst_value, a.dummy, a.err, diag);
+  hipLaunchKernelGGL(k_apply_value_v3<256>, dim3(a.sb_val), dim3(V3A<256>::T), 0, st,
+                     reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
+                     a.rst_status, a.rst_value, a.dummy, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -309,7 +309,7 @@ class Engine:
     def apply_host(self, b: Batch):
         """PCIe-inclusive path: host columns in, host results out (H2D + apply + D2H + sync)."""
         n = len(b)
-        status = np.zeros(n, np.uint8)
+        status = np.full(n, RESULT_SENTINEL, np.uint8)  # cc_apply_batch_host prefills too; a row never written stays 0xFF
         value = np.zeros(n, np.uint64)
         s = abi.cc_batch()
         for name, _ in abi.BATCH_COLUMNS:

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from copycat_amd import abi
+from copycat_amd.batch import Batch
 
 pytestmark = pytest.mark.gpu
 
@@ -240,3 +241,35 @@ def test_group_schedule_timers(flags):
     want = sorted(zip(oe["target"].tolist(), oe["code"].tolist(), oe["tag"].tolist(), oe["payload"].tolist()))
     assert got == want
     assert (ev["src"] == abi.CC_EVSRC_TIMER).all() and (ev["pos"] == 0xFFFFFFFF).all()
+
+
+def test_coordination_on_a_full_partition_fails_at_creation():
+    """A 2M-entry map engine over 100,000 resources fills k_part_ext's LDS counters without the coordination
+    instance-id plane (8 more bytes per chunk commit).  Creating a lock there must fail with CC_ERR_CAPACITY at
+    cc_resource_create (and leave the engine usable for its maps), not make every later cc_apply_batch fail; an engine
+    asking for value events at creation is refused the same way."""
+    from copycat_amd.engine import Engine, EngineError
+    from oracle.oracle_py import Oracle
+
+    R = 100_000
+    E = Engine(R, 64, 4096, map_capacity=2 * 1024 * 1024)
+    E.resource_create(0, abi.CC_RES_MAP)
+    with pytest.raises(EngineError) as ei:
+        E.resource_create(1, abi.CC_RES_LOCK)
+    assert ei.value.rc == abi.CC_ERR_CAPACITY
+    E.instance_open(0, 0, 100, 7)
+    O = Oracle(R, 64)
+    O.resource_create(0, abi.CC_RES_MAP)
+    O.instance_open(0, 0, 100, 7)
+    n = 64
+    b = Batch.from_columns(index=np.arange(1, n + 1, dtype=np.uint64), time=np.arange(1, n + 1, dtype=np.uint64),
+                           inst=np.zeros(n, np.uint32),
+                           op=np.where(np.arange(n) % 2 == 0, abi.CC_OP_MAP_PUT, abi.CC_OP_MAP_GET).astype(np.uint8),
+                           flags=np.full(n, abi.cc_flags(abi.CC_TAG_LONG, 0, 0), np.uint8),
+                           key=(np.arange(n, dtype=np.uint64) // 4), a=np.arange(n, dtype=np.uint64) * 3)
+    s, v = E.apply_host(b)
+    s2, v2 = O.apply(b)
+    assert np.array_equal(s, s2) and np.array_equal(v, v2)
+    with pytest.raises(EngineError) as ei:
+        Engine(R, 64, 4096, map_capacity=2 * 1024 * 1024, flags=abi.CC_CFG_VALUE_EVENTS)
+    assert ei.value.rc == abi.CC_ERR_CAPACITY

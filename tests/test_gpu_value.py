@@ -18,11 +18,11 @@ def _setup(E, O, resources, first_inst=0):
         O.instance_open(first_inst + r, r, 1000 + r, 7)
 
 
-def _run_both(b: Batch, resources, max_inst, sub_batch=0, split=None):
+def _run_both(b: Batch, resources, max_inst, sub_batch=0, split=None, map_capacity=0):
     from copycat_amd.engine import Engine
     from oracle.oracle_py import Oracle
 
-    E = Engine(resources, max_inst, max(len(b), 1), sub_batch=sub_batch)
+    E = Engine(resources, max_inst, max(len(b), 1), sub_batch=sub_batch, map_capacity=map_capacity)
     O = Oracle(resources, max_inst)
     _setup(E, O, resources)
     parts = [b] if split is None else [b.slice(lo, hi) for lo, hi in split]
@@ -112,16 +112,18 @@ def test_device_resident_apply_matches_host_path():
         assert np.array_equal(x, y)
 
 
-def test_cas_update_deltas_at_the_record_boundary():
-    """value_path.hip stores a CAS update as a 46-bit difference from the expected value; a difference that does not
-    fit escapes to the batch's b column.  Chains of CASes that always succeed, with differences on both sides of the
-    46-bit boundary and across the i64 wrap, tag changes (Long -> Integer -> null) and expected NULLs, are bit-exact
-    against the oracle, with the value-only pipeline and with the previous one (CC_VALUE_V2)."""
-    import os
-
+@pytest.mark.parametrize("map_capacity", [0, 1024])
+def test_cas_update_deltas_at_the_record_boundary(map_capacity):
+    """value_path.hip stores a CAS update as a 33-bit two's-complement difference from the expected value
+    (kV3DeltaBits); a difference that does not fit escapes: its row is kept and the update is read from the batch's b
+    column.  Chains of CASes that always succeed (AtomicValueState.compareAndSet :123-133), with differences on both
+    sides of the 33-bit boundary (2^32 - 1 and -2^32 fit; 2^32 and -2^32 - 1 escape) and across the i64 wrap, tag
+    changes (Long -> Integer -> null) and expected NULLs, are bit-exact against the oracle -- on the value-only
+    pipeline (k_part_v4 -> k_apply_value_v3) and, with map_capacity > 0, on the extended one (k_part_ext ->
+    k_apply_value_ws, which carries whole operands)."""
     R, steps = 512, 48
-    deltas = [0, 1, -1, (1 << 45) - 1, -(1 << 45), 1 << 45, -(1 << 45) - 1, (1 << 63), (1 << 64) - 1, 12345678901234,
-              -(1 << 62), (1 << 46) + 3]
+    deltas = [0, 1, -1, (1 << 32) - 1, -(1 << 32), 1 << 32, -(1 << 32) - 1, (1 << 32) + 1, -(1 << 32) + 1,
+              (1 << 31), -(1 << 31) - 1, (1 << 63), (1 << 64) - 1, 12345678901234, -(1 << 62), (1 << 46) + 3]
     rng = np.random.default_rng(3)
     cur = np.zeros(R, np.uint64)
     ctag = np.zeros(R, np.uint8)
@@ -143,16 +145,15 @@ def test_cas_update_deltas_at_the_record_boundary():
                            inst=np.array(arr[:, 0], np.uint32), op=np.array(arr[:, 1], np.uint8),
                            flags=np.array(arr[:, 2], np.uint8), a=np.array([int(x) for x in arr[:, 3]], np.uint64),
                            b=np.array([int(x) for x in arr[:, 4]], np.uint64))
-    for v2 in (False, True):
-        if v2:
-            os.environ["CC_VALUE_V2"] = "1"
-        try:
-            E, O, gs, gv, os_, ov = _run_both(b, R, R, sub_batch=16384 * 2)
-        finally:
-            os.environ.pop("CC_VALUE_V2", None)
-        _assert_same(E, O, gs, gv, os_, ov, R)
-        cas = b.op == abi.CC_OP_VALUE_CAS
-        assert np.all(gv[cas] == 1)  # every CAS expected the value it found
+    # both sides of the boundary occur among the Long -> Long CASes
+    ll = (b.op == abi.CC_OP_VALUE_CAS) & (b.flags == (abi.CC_TAG_LONG | (abi.CC_TAG_LONG << 3)))
+    dd = (b.b[ll] - b.a[ll]).view(np.int64)
+    for d in ((1 << 32) - 1, -(1 << 32), 1 << 32, -(1 << 32) - 1):
+        assert np.any(dd == d), d
+    E, O, gs, gv, os_, ov = _run_both(b, R, R, sub_batch=16384 * 2, map_capacity=map_capacity)
+    _assert_same(E, O, gs, gv, os_, ov, R)
+    cas = b.op == abi.CC_OP_VALUE_CAS
+    assert np.all(gv[cas] == 1)  # every CAS expected the value it found
 
 
 @pytest.mark.parametrize("n,sub", [(8191, 0), (8193, 0), (16384 * 3 + 8191, 16384), (100_001, 16384 * 2)])
