@@ -100,6 +100,8 @@ static void free_all(cc_engine* e) {
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (void*& p : e->hw_buf)
+    if (p) (void)hipFree(p), p = nullptr;
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
 
@@ -1057,70 +1059,6 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     e->applied_pending = true;
   }
   return CC_OK;
-}
-
-extern "C" int cc_apply_batch_host(cc_engine* e, const cc_batch* h, uint64_t n, const cc_results* hout) {
-  if (!e || !h || !hout) return set_err(CC_ERR_INVALID, "null argument");
-  if (n == 0) return CC_OK;
-  HIPCHECK(hipSetDevice(e->device));
-  struct Col {
-    const void* src;
-    size_t esz;
-    void* dev;
-  } cols[9] = {{h->index, 8, nullptr}, {h->time, 8, nullptr}, {h->inst, 4, nullptr}, {h->op, 1, nullptr}, {h->flags, 1, nullptr},
-               {h->key, 8, nullptr},   {h->a, 8, nullptr},    {h->b, 8, nullptr},    {h->aux, 8, nullptr}};
-  hipStream_t st = e->own_stream;
-  if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
-  e->last_stream = st;
-  int rc = CC_OK;
-  uint8_t* d_status = nullptr;
-  uint64_t* d_value = nullptr;
-  for (auto& col : cols) {
-    if (!col.src) continue;
-    if (hipMalloc(&col.dev, col.esz * n) != hipSuccess) { rc = set_err(CC_ERR_HIP, "hipMalloc column"); goto done; }
-    if (hipMemcpyAsync(col.dev, col.src, col.esz * n, hipMemcpyHostToDevice, st) != hipSuccess) {
-      rc = set_err(CC_ERR_HIP, "H2D");
-      goto done;
-    }
-  }
-  if (hipMalloc(&d_status, n) != hipSuccess || hipMalloc(&d_value, 8 * n) != hipSuccess) {
-    rc = set_err(CC_ERR_HIP, "hipMalloc results");
-    goto done;
-  }
-  // sentinel prefill: status 0xFF is no legal status (tag nibble 15), so a row the kernels never wrote comes back
-  // as 0xFF instead of passing for a legal NULL result (status 0, value 0)
-  if (hipMemsetAsync(d_status, 0xFF, n, st) != hipSuccess || hipMemsetAsync(d_value, 0xA5, 8 * n, st) != hipSuccess) {
-    rc = set_err(CC_ERR_HIP, "result sentinel");
-    goto done;
-  }
-  {
-    cc_batch d{};
-    d.index = (const uint64_t*)cols[0].dev;
-    d.time = (const uint64_t*)cols[1].dev;
-    d.inst = (const uint32_t*)cols[2].dev;
-    d.op = (const uint8_t*)cols[3].dev;
-    d.flags = (const uint8_t*)cols[4].dev;
-    d.key = (const uint64_t*)cols[5].dev;
-    d.a = (const uint64_t*)cols[6].dev;
-    d.b = (const uint64_t*)cols[7].dev;
-    d.aux = (const uint64_t*)cols[8].dev;
-    cc_results r{d_status, d_value};
-    rc = cc_apply_batch(e, &d, n, &r, nullptr, st);
-    if (rc) goto done;
-    if (hipMemcpyAsync(hout->status, d_status, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(hout->value, d_value, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess) {
-      rc = set_err(CC_ERR_HIP, "D2H");
-      goto done;
-    }
-    rc = cc_sync(e);
-  }
-done:
-  (void)hipStreamSynchronize(st);
-  for (auto& col : cols)
-    if (col.dev) (void)hipFree(col.dev);
-  if (d_status) (void)hipFree(d_status);
-  if (d_value) (void)hipFree(d_value);
-  return rc;
 }
 
 extern "C" int cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* stream) {

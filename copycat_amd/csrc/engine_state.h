@@ -175,7 +175,6 @@ struct cc_engine {
   void* d_hot_samp = nullptr;
   // extended staging (maps / coordination / value events) + coordination + events
   bool ext = false, coord_on = false;
-  // CC_VALUE_V2=1 at creation: the value-only engine keeps the previous pipeline (A/B)
   std::vector<uint8_t> sb_kind;      // [sb] 1: the super-bucket runs on k_apply_coord
   uint8_t* d_sb_kind = nullptr;
   uint64_t* d_inst_id = nullptr;     // instance slot -> instance id (election listeners, group members)
@@ -201,6 +200,9 @@ struct cc_engine {
   uint64_t applied = 0;
   bool applied_pending = false;
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
+  // device staging of the host-memory entry points (host_path.hip): grown on demand, kept between calls
+  void* hw_buf[24] = {};
+  size_t hw_cap[24] = {};
   // per-kernel profiling (cc_profile_enable)
   bool prof_on = false;
   std::vector<hipEvent_t> ev_pool;

@@ -1,0 +1,251 @@
+// host_path.hip — the host-memory entry points of the C-ABI (host code only).
+//
+// A JVM host (Panama FFM / JNI) hands the engine Java heap or off-heap host memory, not HBM
+// pointers.  These calls stage host columns into engine-owned device buffers (grown on demand and kept between
+// calls: no hipMalloc / hipFree per batch), run the device entry point, and copy results AND events back, so every
+// reference path that publishes -- Session.publish -> InstanceEvent{instance, msg}
+// (manager/src/main/java/io/atomix/manager/ManagedResourceSession.java:64-71,
+//  manager/src/main/java/io/atomix/resource/InstanceEvent.java:29-80) -- has a host-memory route:
+//   cc_apply_batch_host / cc_apply_batch_host_events   ResourceManager.operateResource per entry (:56-72)
+//   cc_sessions_close_host / cc_sessions_expire_host    ResourceManager.close / expire (:237-264)
+//   cc_advance_time_events_host                         timer callbacks (ResourceManagerStateMachineExecutor :104-116)
+//   cc_retained_bitmap_host                             the compaction feed (ResourceManagerCommit.clean :79-81)
+// plus a plain device-memory API (cc_device_alloc / cc_memcpy ...) for the stateless device calls
+// (cc_quorum_commit, cc_expire_sweep) and for hosts that keep columns resident.
+#include <algorithm>
+#include <cstring>
+
+#include "engine_state.h"
+
+namespace {
+
+enum HwSlot : int {
+  kHwCol = 0,  // 9 input columns
+  kHwStatus = 9,
+  kHwValue,
+  kHwEvPos,
+  kHwEvTarget,
+  kHwEvCode,
+  kHwEvSrc,
+  kHwEvTag,
+  kHwEvPayload,
+  kHwEvCount,
+  kHwBitmap,
+  kHwNum
+};
+static_assert(kHwNum <= 24, "cc_engine::hw_buf");
+
+// Device buffer `slot` with room for `bytes` (the previous contents are not kept).  The callers are synchronous, so
+// no launch of an earlier call still reads a buffer that is replaced here.
+int hw(cc_engine* e, int slot, size_t bytes, void** out) {
+  bytes = std::max<size_t>(bytes, 256);
+  if (e->hw_cap[slot] < bytes) {
+    if (e->hw_buf[slot]) (void)hipFree(e->hw_buf[slot]);
+    e->hw_buf[slot] = nullptr;
+    e->hw_cap[slot] = 0;
+    const size_t cap = std::max(bytes, e->hw_cap[slot] * 3 / 2);
+    hipError_t x = hipMalloc(&e->hw_buf[slot], cap);
+    if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc (host-path staging)", x);
+    e->hw_cap[slot] = cap;
+  }
+  *out = e->hw_buf[slot];
+  return CC_OK;
+}
+
+// Device event columns of `cap` rows mirroring the host cc_events `h` (null: no event stream).
+int hw_events(cc_engine* e, const cc_events* h, cc_events* d) {
+  std::memset(d, 0, sizeof *d);
+  if (!h) return CC_OK;
+  if (!h->count || (h->capacity && (!h->pos || !h->target || !h->code || !h->src || !h->tag || !h->payload)))
+    return set_err(CC_ERR_INVALID, "host event stream: null column or count");
+  const size_t c = std::max<uint64_t>(h->capacity, 1);
+  int rc;
+  void* p;
+  if ((rc = hw(e, kHwEvPos, 4 * c, &p))) return rc;
+  d->pos = (uint32_t*)p;
+  if ((rc = hw(e, kHwEvTarget, 4 * c, &p))) return rc;
+  d->target = (uint32_t*)p;
+  if ((rc = hw(e, kHwEvCode, c, &p))) return rc;
+  d->code = (uint8_t*)p;
+  if ((rc = hw(e, kHwEvSrc, c, &p))) return rc;
+  d->src = (uint8_t*)p;
+  if ((rc = hw(e, kHwEvTag, c, &p))) return rc;
+  d->tag = (uint8_t*)p;
+  if ((rc = hw(e, kHwEvPayload, 8 * c, &p))) return rc;
+  d->payload = (uint64_t*)p;
+  if ((rc = hw(e, kHwEvCount, 8, &p))) return rc;
+  d->count = (uint64_t*)p;
+  d->capacity = h->capacity;
+  HIPCHECK(hipMemsetAsync(d->count, 0, sizeof(uint64_t), e->own_stream));
+  return CC_OK;
+}
+
+// Events back to the host: *h->count = the events published (may exceed capacity: then the call fails with
+// CC_ERR_CAPACITY, and the first `capacity` rows are still copied).
+int hw_events_back(cc_engine* e, const cc_events* h, const cc_events* d) {
+  if (!h) return CC_OK;
+  hipStream_t st = e->own_stream;
+  uint64_t cnt = 0;
+  HIPCHECK(hipMemcpyAsync(&cnt, d->count, sizeof cnt, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  *h->count = cnt;
+  const uint64_t m = std::min<uint64_t>(cnt, h->capacity);
+  if (m) {
+    HIPCHECK(hipMemcpyAsync(h->pos, d->pos, 4 * m, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(h->target, d->target, 4 * m, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(h->code, d->code, m, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(h->src, d->src, m, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(h->tag, d->tag, m, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(h->payload, d->payload, 8 * m, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+  }
+  return cnt > h->capacity ? set_err(CC_ERR_CAPACITY, "more events than the host event stream holds") : CC_OK;
+}
+
+int apply_host(cc_engine* e, const cc_batch* h, uint64_t n, const cc_results* hout, const cc_events* hev) {
+  if (!e || !h || !hout || (n && (!hout->status || !hout->value))) return set_err(CC_ERR_INVALID, "null argument");
+  HIPCHECK(hipSetDevice(e->device));
+  hipStream_t st = e->own_stream;
+  if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
+  e->last_stream = st;
+  cc_events dev{};
+  int rc = hw_events(e, hev, &dev);
+  if (rc) return rc;
+  if (n == 0) {
+    if (hev) *hev->count = 0;
+    return CC_OK;
+  }
+  const void* src[9] = {h->index, h->time, h->inst, h->op, h->flags, h->key, h->a, h->b, h->aux};
+  const size_t esz[9] = {8, 8, 4, 1, 1, 8, 8, 8, 8};
+  void* dcol[9] = {};
+  for (int c = 0; c < 9; ++c) {
+    if (!src[c]) continue;
+    if ((rc = hw(e, kHwCol + c, esz[c] * n, &dcol[c]))) return rc;
+    HIPCHECK(hipMemcpyAsync(dcol[c], src[c], esz[c] * n, hipMemcpyHostToDevice, st));
+  }
+  void *d_status, *d_value;
+  if ((rc = hw(e, kHwStatus, n, &d_status)) || (rc = hw(e, kHwValue, 8 * n, &d_value))) return rc;
+  // sentinel prefill: status 0xFF is no legal status (tag nibble 15), so a row the kernels never wrote comes back as
+  // 0xFF instead of passing for a legal NULL result (status 0, value 0)
+  HIPCHECK(hipMemsetAsync(d_status, 0xFF, n, st));
+  HIPCHECK(hipMemsetAsync(d_value, 0xA5, 8 * n, st));
+  cc_batch d{};
+  d.index = (const uint64_t*)dcol[0];
+  d.time = (const uint64_t*)dcol[1];
+  d.inst = (const uint32_t*)dcol[2];
+  d.op = (const uint8_t*)dcol[3];
+  d.flags = (const uint8_t*)dcol[4];
+  d.key = (const uint64_t*)dcol[5];
+  d.a = (const uint64_t*)dcol[6];
+  d.b = (const uint64_t*)dcol[7];
+  d.aux = (const uint64_t*)dcol[8];
+  cc_results r{(uint8_t*)d_status, (uint64_t*)d_value};
+  rc = cc_apply_batch(e, &d, n, &r, hev ? &dev : nullptr, st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
+  HIPCHECK(hipMemcpyAsync(hout->status, d_status, n, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(hout->value, d_value, 8 * n, hipMemcpyDeviceToHost, st));
+  const int rs = cc_sync(e);  // device-side checks (capacity, unsupported ops, time order) after the D2H
+  const int re = hw_events_back(e, hev, &dev);
+  return rs ? rs : re;
+}
+
+}  // namespace
+
+extern "C" int cc_apply_batch_host(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out) {
+  return apply_host(e, h_cols, n, h_out, nullptr);
+}
+
+extern "C" int cc_apply_batch_host_events(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out,
+                                          const cc_events* h_events) {
+  if (!h_events) return set_err(CC_ERR_INVALID, "null event stream (use cc_apply_batch_host)");
+  return apply_host(e, h_cols, n, h_out, h_events);
+}
+
+extern "C" int cc_sessions_close_host(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* h_events,
+                                      uint64_t* h_closed) {
+  if (!e) return set_err(CC_ERR_INVALID, "null engine");
+  HIPCHECK(hipSetDevice(e->device));
+  cc_events dev{};
+  int rc = hw_events(e, h_events, &dev);
+  if (rc) return rc;
+  rc = cc_sessions_close(e, h_clients, count, h_events ? &dev : nullptr, e->own_stream, h_closed);
+  const int re = hw_events_back(e, h_events, &dev);
+  return rc ? rc : re;
+}
+
+extern "C" int cc_sessions_expire_host(cc_engine* e, const uint64_t* h_bitmap, uint64_t sessions, const cc_events* h_events,
+                                       uint64_t* h_closed) {
+  if (!e || (sessions && !h_bitmap)) return set_err(CC_ERR_INVALID, "null argument");
+  std::vector<uint64_t> clients;  // ascending client session ids, as cc_sessions_expire orders them
+  for (uint64_t wi = 0; wi < (sessions + 63) / 64; ++wi)
+    for (uint64_t b = h_bitmap[wi]; b; b &= b - 1) {
+      const uint64_t sid = wi * 64 + (uint64_t)__builtin_ctzll(b);
+      if (sid < sessions) clients.push_back(sid);
+    }
+  return cc_sessions_close_host(e, clients.data(), clients.size(), h_events, h_closed);
+}
+
+extern "C" int cc_advance_time_events_host(cc_engine* e, uint64_t now, const cc_events* h_events) {
+  if (!e) return set_err(CC_ERR_INVALID, "null engine");
+  HIPCHECK(hipSetDevice(e->device));
+  cc_events dev{};
+  int rc = hw_events(e, h_events, &dev);
+  if (rc) return rc;
+  rc = cc_advance_time_events(e, now, h_events ? &dev : nullptr);
+  const int re = hw_events_back(e, h_events, &dev);
+  return rc ? rc : re;
+}
+
+extern "C" int cc_retained_bitmap_host(cc_engine* e, uint64_t first, uint64_t count, uint64_t* h_bitmap, uint64_t* h_count) {
+  if (!e || (count && !h_bitmap)) return set_err(CC_ERR_INVALID, "null argument");
+  if (count == 0) {
+    if (h_count) *h_count = 0;
+    return CC_OK;
+  }
+  HIPCHECK(hipSetDevice(e->device));
+  const uint64_t words = (count + 63) / 64;
+  void* d = nullptr;
+  int rc = hw(e, kHwBitmap, 8 * words, &d);
+  if (rc) return rc;
+  if ((rc = cc_retained_bitmap(e, first, count, (uint64_t*)d, h_count))) return rc;
+  HIPCHECK(hipMemcpy(h_bitmap, d, 8 * words, hipMemcpyDeviceToHost));
+  return CC_OK;
+}
+
+// ---- plain device memory (for the stateless device calls and hosts that keep columns resident) ---------------
+extern "C" int cc_device_alloc(int device, uint64_t bytes, void** d_out) {
+  if (!d_out) return set_err(CC_ERR_INVALID, "null argument");
+  *d_out = nullptr;
+  HIPCHECK(hipSetDevice(device));
+  HIPCHECK(hipMalloc(d_out, std::max<uint64_t>(bytes, 1)));
+  return CC_OK;
+}
+
+extern "C" int cc_device_free(void* d_ptr) {
+  if (d_ptr) HIPCHECK(hipFree(d_ptr));
+  return CC_OK;
+}
+
+extern "C" int cc_memcpy(void* dst, const void* src, uint64_t bytes, int kind, void* stream) {
+  if (bytes == 0) return CC_OK;
+  if (!dst || !src) return set_err(CC_ERR_INVALID, "null argument");
+  const hipMemcpyKind k = kind == CC_MEMCPY_H2D ? hipMemcpyHostToDevice
+                          : kind == CC_MEMCPY_D2H ? hipMemcpyDeviceToHost
+                          : kind == CC_MEMCPY_D2D ? hipMemcpyDeviceToDevice
+                                                  : hipMemcpyDefault;
+  if (kind < CC_MEMCPY_H2D || kind > CC_MEMCPY_D2D) return set_err(CC_ERR_INVALID, "memcpy kind");
+  HIPCHECK(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
+  HIPCHECK(hipStreamSynchronize((hipStream_t)stream));
+  return CC_OK;
+}
+
+extern "C" int cc_memset(void* d_ptr, int byte, uint64_t bytes, void* stream) {
+  if (bytes == 0) return CC_OK;
+  if (!d_ptr) return set_err(CC_ERR_INVALID, "null argument");
+  HIPCHECK(hipMemsetAsync(d_ptr, byte, bytes, (hipStream_t)stream));
+  HIPCHECK(hipStreamSynchronize((hipStream_t)stream));
+  return CC_OK;
+}

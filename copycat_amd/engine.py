@@ -56,6 +56,15 @@ def lib():
             "cc_instance_open_range": (i32, [P, u32, u32, u32, u64, u64]),
             "cc_apply_batch": (i32, [P, P, u64, P, P, P]),
             "cc_apply_batch_host": (i32, [P, P, u64, P]),
+            "cc_apply_batch_host_events": (i32, [P, P, u64, P, P]),
+            "cc_sessions_close_host": (i32, [P, P, u64, P, P]),
+            "cc_sessions_expire_host": (i32, [P, P, u64, P, P]),
+            "cc_advance_time_events_host": (i32, [P, u64, P]),
+            "cc_retained_bitmap_host": (i32, [P, u64, u64, P, P]),
+            "cc_device_alloc": (i32, [i32, u64, P]),
+            "cc_device_free": (i32, [P]),
+            "cc_memcpy": (i32, [P, P, u64, i32, P]),
+            "cc_memset": (i32, [P, i32, u64, P]),
             "cc_applied_index": (i32, [P, P]),
             "cc_applied_index_async": (i32, [P, P, P]),
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),

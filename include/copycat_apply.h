@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CC_ABI_VERSION 3
+#define CC_ABI_VERSION 4
 
 /* ---- return codes ------------------------------------------------------------------------------ */
 #define CC_OK               0
@@ -313,8 +313,20 @@ int  cc_resource_slot(cc_engine* e, uint64_t resource_id, int64_t* slot);
 /* d_out->status must be 4-byte aligned and d_out->value 16-byte aligned (hipMalloc / torch allocations are). */
 int  cc_apply_batch(cc_engine* e, const cc_batch* d_cols, uint64_t n, const cc_results* d_out,
                     const cc_events* d_events, void* stream);
-/* Same with host columns/results: H2D, apply, D2H, sync (PCIe-inclusive path). */
+/* ---- host-memory entry points (copycat_amd/csrc/host_path.hip) -------------------------------------------------
+ * For a host that holds no device pointers (a JVM through Panama FFM / JNI): host columns in,
+ * host results and events out.  The engine stages them in device buffers it owns (grown on demand, kept between
+ * calls); every call is synchronous.  A host event stream is a cc_events whose column pointers AND `count` point to
+ * host memory: *count = the events published (when it exceeds `capacity` the call returns CC_ERR_CAPACITY after
+ * copying the first `capacity` rows).  Events reach the client as Session.publish -> InstanceEvent{instance, msg}
+ * (ManagedResourceSession.java:64-71, InstanceEvent.java:29-80): `target` is the instance slot whose session
+ * receives the event, rows in publish order (log row, then the state machine's publish order). */
+/* Host columns/results: H2D, apply, D2H, sync (PCIe-inclusive path).  Publishing ops fail with
+ * CC_ERR_UNSUPPORTED here: use cc_apply_batch_host_events. */
 int  cc_apply_batch_host(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out);
+/* The same with the event stream (lock grants, elections, joins / leaves, executes, value changes). */
+int  cc_apply_batch_host_events(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out,
+                                const cc_events* h_events);
 /* Highest log index applied so far (the applied watermark; all-gathered across GPUs by the host). */
 int  cc_applied_index(cc_engine* e, uint64_t* out);
 /* The same watermark written stream-ordered into device memory (u64 at d_out) without a host sync: what a rank feeds
@@ -368,6 +380,8 @@ int  cc_read_retained(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count
  * clear bits are compactable (Commit.clean(), ResourceManagerCommit.java:79-81); a bit that cleared since the
  * previous call was released by a clean() in between.  Value resources need CC_CFG_VALUE_RETAINED.  Synchronous. */
 int  cc_retained_bitmap(cc_engine* e, uint64_t first, uint64_t count, uint64_t* d_bitmap, uint64_t* h_count);
+/* The same bitmap into host memory (ceil(count / 64) u64 words). */
+int  cc_retained_bitmap_host(cc_engine* e, uint64_t first, uint64_t count, uint64_t* h_bitmap, uint64_t* h_count);
 /* Log time advanced without a commit (ResourceManagerStateMachineExecutor timers): due lock
  * timeouts take effect (they publish nothing, LockState.java:54-58). */
 int  cc_advance_time(cc_engine* e, uint64_t now);
@@ -375,6 +389,8 @@ int  cc_advance_time(cc_engine* e, uint64_t now);
  * src CC_EVSRC_TIMER) to d_events; *d_events->count is written.  cc_advance_time fails with CC_ERR_UNSUPPORTED
  * when such an event is due and has no stream. */
 int  cc_advance_time_events(cc_engine* e, uint64_t now, const cc_events* d_events);
+/* The same with a host event stream. */
+int  cc_advance_time_events_host(cc_engine* e, uint64_t now, const cc_events* h_events);
 
 /* ---- session close / expire fan-out (ResourceManager.close :250-264, expire :238-247) -------------------
  * For each client session of h_clients, in order: every instance it owns, in java.util.HashMap iteration order of
@@ -390,6 +406,11 @@ int  cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64_t count, 
 /* The expired set of cc_expire_sweep (bit s = client session id s, u64 words in HBM), closed in ascending id order. */
 int  cc_sessions_expire(cc_engine* e, const uint64_t* d_bitmap, uint64_t sessions, const cc_events* d_events, void* stream,
                         uint64_t* h_closed);
+/* Host-memory forms (see "host-memory entry points" above): events to a host cc_events (NULL: none may publish). */
+int  cc_sessions_close_host(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* h_events,
+                            uint64_t* h_closed);
+int  cc_sessions_expire_host(cc_engine* e, const uint64_t* h_bitmap, uint64_t sessions, const cc_events* h_events,
+                             uint64_t* h_closed);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every engine kernel) ----------
  * kernel ids: 0 k_part_tile, 1 k_apply_value, 2 k_unpermute, 3 k_apply_map, 4 k_map_hot (hot-key lists +
@@ -417,6 +438,16 @@ int  cc_quorum_commit(const uint64_t* d_match, uint32_t replicas, uint64_t group
  * expires).  Bit s of d_bitmap (u64 words, LSB first) is set for expired sessions; *d_count (u64) += expired. */
 int  cc_expire_sweep(const uint64_t* d_last, uint64_t sessions, uint64_t now, uint64_t timeout,
                      uint64_t* d_bitmap, uint64_t* d_count, void* stream);
+
+/* ---- plain device memory: for cc_quorum_commit / cc_expire_sweep and hosts that keep columns resident in HBM --------
+ * (hipMalloc / hipFree / hipMemcpy on the engine's HIP runtime; cc_memcpy and cc_memset synchronize `stream`) */
+#define CC_MEMCPY_H2D 1
+#define CC_MEMCPY_D2H 2
+#define CC_MEMCPY_D2D 3
+int  cc_device_alloc(int device, uint64_t bytes, void** d_out);
+int  cc_device_free(void* d_ptr);
+int  cc_memcpy(void* dst, const void* src, uint64_t bytes, int kind, void* stream);
+int  cc_memset(void* d_ptr, int byte, uint64_t bytes, void* stream);
 
 /* ---- Catalyst wire format -> columns (copycat_amd/csrc/wire.cpp) ----------------------
  * A committed resource entry is InstanceCommand / InstanceQuery (@SerializeWith 30 / 31): writeLong(instance id),
