@@ -119,6 +119,15 @@ class Handle:
         return f"Handle({self.h})"
 
 
+def java_string_hash(s):
+    """java.lang.String.hashCode: s[0]*31^(n-1) + ... + s[n-1] over the UTF-16 code units, as a Java int."""
+    b = s.encode("utf-16-le")
+    h = 0
+    for i in range(0, len(b), 2):
+        h = (31 * h + (b[i] | (b[i + 1] << 8))) & 0xFFFFFFFF
+    return h - (1 << 32) if h >> 31 else h
+
+
 class Interner:
     """Interns host objects (e.g. Java Strings) to HANDLE ids so `equals` is id equality."""
 

@@ -165,7 +165,8 @@ __global__ __launch_bounds__(kDetT) void k_hot_count(const HotSamp* __restrict__
 __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ cand, const uint32_t* __restrict__ cand_n,
                                                    uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
                                                    uint64_t* tbl_val, uint64_t* tbl_ci, uint64_t* tbl_ins,
-                                                   HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n) {
+                                                   HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n,
+                                                   const uint8_t* __restrict__ msmall) {
   const uint32_t t = threadIdx.x;
   const uint32_t nc = *cand_n;
   // bind each hot key's table entry (the tables are idle between the sub-batch's kernels): every key looks itself
@@ -206,8 +207,10 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
     }
     return false;  // a full region leaves the key cold
   };
+  // a map still in its small-table window is followed commit by commit through its regions (map_small.hip)
+  auto small_map = [&](uint32_t id) { return msmall != nullptr && msmall[id & kMwSlotMask] != 0; };
   uint32_t pos = 0;
-  const bool found = valid && probe(false, pos);
+  const bool found = valid && !small_map(ident) && probe(false, pos);
   __shared__ uint32_t bpos[kHotMax];
   __shared__ uint8_t bok[kHotMax];
   __shared__ uint32_t nmiss;
@@ -222,7 +225,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
   if (nmiss && t >= kWave && t < 2 * kWave) {  // inserts: wave 1, one key at a time in rank order
     for (uint32_t g0 = 0; g0 < nh; g0 += kWave) {
       const uint32_t gi = g0 + (t - kWave);
-      const bool miss = gi < nh && !bok[gi];
+      const bool miss = gi < nh && !bok[gi] && !small_map(cand[gi].ident);
       for (uint64_t need = ballot(miss); need; need &= need - 1) {
         const uint32_t leader = (uint32_t)__builtin_ctzll(need);
         if (t - kWave == leader) {
@@ -601,7 +604,7 @@ int launch_map_hot_detect(const HotArgs& a, hipStream_t st) {
 
 int launch_map_hot_bind(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_bind, dim3(1), dim3(kDetT), 0, st, a.hot_cand, a.hot_cand_n, a.map_bits, a.tbl_key, a.tbl_word,
-                     a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n);
+                     a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n, a.msmall);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

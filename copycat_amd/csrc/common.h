@@ -268,6 +268,46 @@ struct EvRec {
 constexpr uint32_t kErrTime = 8u;  // the time column decreased inside a batch
 constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration order is undetermined (map_wide.hip)
 constexpr uint32_t kErrMapSize = 32u;   // a map's tracked size differs from its table at a barrier (internal check)
+constexpr uint32_t kErrHandleHash = 64u;  // a HANDLE map key whose String.hashCode was never registered (cc_handle_hashes)
+
+// java.util.HashMap placement of a map key: hash(key) = h ^ (h >>> 16), h = key.hashCode() -- Long (int)(v ^ v >>> 32),
+// Integer v, Boolean 1231 / 1237, String (HANDLE) its registered String.hashCode (hh: sorted handles + hashes);
+// ok = false for an unregistered HANDLE.  Key tags: 0 LONG, 1 INT, 2 BOOL, 3 HANDLE.
+__device__ inline uint32_t java_key_hash(uint32_t ktag, uint64_t v, const uint64_t* __restrict__ hh_key,
+                                         const int32_t* __restrict__ hh_val, uint32_t hh_n, bool& ok) {
+  uint32_t h;
+  ok = true;
+  switch (ktag) {
+    case 1: h = (uint32_t)v; break;
+    case 2: h = v ? 1231u : 1237u; break;
+    case 3: {
+      uint32_t lo = 0, hi = hh_n;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (hh_key[mid] < v) lo = mid + 1; else hi = mid;
+      }
+      ok = lo < hh_n && hh_key[lo] == v;
+      h = ok ? (uint32_t)hh_val[lo] : 0u;
+      break;
+    }
+    default: h = (uint32_t)(v ^ (v >> 32)); break;
+  }
+  return h ^ (h >> 16);
+}
+
+// A map's java.util.HashMap while its table is small (capacity <= 64; map_small.hip): the live keys' hashes (a
+// multiset, <= 48 of them), the capacity level (capacity = 16 << lvl) and whether a bin was treeified.  Below capacity
+// 64 a bin that reaches 9 keys resizes the table early (HashMap.treeifyBin); at 64 it becomes a red-black tree bin,
+// whose iteration order the engine does not follow (kSmTree; tree_bins: the bins, mod 64, that became trees).
+constexpr uint32_t kSmKeys = 48;
+struct SmallMap {
+  uint32_t n, lvl, flags, pad;
+  uint64_t tree_bins;
+  uint32_t jh[kSmKeys];
+};
+constexpr uint32_t kSmIn = 1u;       // the table is still small (capacity <= 64): tracked key by key
+constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin while tracked
+constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (TTL mode: timers remove keys unseen)
 // a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
 __device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
   return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);

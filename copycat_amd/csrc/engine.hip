@@ -97,11 +97,14 @@ static void free_all(cc_engine* e) {
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
-                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n};
+                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
+                  e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
     if (p) (void)hipFree(p), p = nullptr;
+  if (e->d_hh_key) (void)hipFree(e->d_hh_key);
+  if (e->d_hh_val) (void)hipFree(e->d_hh_val);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
 
@@ -125,6 +128,22 @@ static int ensure_leak(cc_engine* e, uint64_t need) {
   hipError_t x = hipMalloc(&e->d_leak, sizeof(LeakRec) * cap);
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc leak log", x);
   e->leak_cap = cap;
+  return CC_OK;
+}
+
+// The small-map event buffers (map_small.hip): one event per map commit of a sub-batch at most, sorted by hipcub.
+static int ensure_small(cc_engine* e) {
+  if (e->d_sm_key) return CC_OK;
+  const uint64_t cap = e->sub_batch;
+  const size_t tb = std::max<size_t>(small_sort_temp_bytes((uint32_t)cap), 256);
+  hipError_t x = hipMalloc(&e->d_sm_key, 8 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->d_sm_key2, 8 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->d_sm_val, 4 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->d_sm_val2, 4 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->d_sm_seg, 4ull * (e->cfg.max_resources + 1));
+  if (x == hipSuccess) x = hipMalloc(&e->d_sm_temp, tb);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc small-map events", x);
+  e->sm_temp_bytes = tb;
   return CC_OK;
 }
 
@@ -225,7 +244,6 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   e->inst_res.assign(cfg->max_instances, kNoRes);
   e->inst_id.assign(cfg->max_instances, 0);
   e->inst_client.assign(cfg->max_instances, 0);
-  e->inst_seq.assign(cfg->max_instances, 0);
   e->res_id.assign(slots, 0);
   e->res_key.assign(slots, 0);
   e->res_has_key.assign(slots, 0);
@@ -268,7 +286,10 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_hot_cand_n, sizeof(uint32_t));
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
-    ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 16);
+    ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
+    ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
+    ALLOC(e->d_msmall, cfg->max_resources);
+    ALLOC(e->d_sm_ctl, sizeof(uint32_t) * 4);
     ALLOC(e->d_rst_msz, sizeof(uint32_t) * (e->sub_batch + 4 * kPT));
     ALLOC(e->d_hot_msz, sizeof(uint32_t) * (kHotMaxPieces + kHotMax) * (kHotPiece / 16));
     ALLOC(e->d_msize, sizeof(uint32_t) * cfg->max_resources);
@@ -321,6 +342,9 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_mw_drop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msize, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mpcap, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_msm, 0, sizeof(SmallMap) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_msmall, 0, cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_sm_ctl, 0, sizeof(uint32_t) * 4)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_dl, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
   }
   if ((he = hipDeviceSynchronize()) != hipSuccess) return fail("sync", he);
@@ -367,9 +391,13 @@ static int check_device_err(cc_engine* e) {
     HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
     if (err & kErrTime) return set_err(CC_ERR_INVALID, "the time column must be non-decreasing within a batch");
     if (err & kErrMapOrder)
-      return set_err(CC_ERR_STATE, "map containsValue: the answer depends on java.util.HashMap iteration order and the "
-                                   "map's table capacity (peak size) is not determined exactly by the engine's bounds");
+      return set_err(CC_ERR_STATE, "map containsValue: the answer depends on java.util.HashMap iteration order inside a "
+                                   "bin that may have been a red-black tree bin, or on a table capacity the engine's "
+                                   "bounds leave open (TTL mode)");
     if (err & kErrMapSize) return set_err(CC_ERR_STATE, "internal check: a map's tracked size differs from its table");
+    if (err & kErrHandleHash)
+      return set_err(CC_ERR_STATE, "a HANDLE map key's String.hashCode is not registered (cc_handle_hashes), or a "
+                                   "sub-batch spans more than 2^40 log indices");
     if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
     if (err & kErrCapacity)
       return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, lock queue, listeners, members)");
@@ -438,6 +466,13 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
     HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
     HIPCHECK(hipMemset(e->d_msize + first, 0, sizeof(uint32_t) * count));
     HIPCHECK(hipMemset(e->d_mpcap + first, 0, sizeof(uint32_t) * count));
+    // MapState's table followed key by key while small (map_small.hip); sets / multimaps have no order-dependent op
+    std::vector<SmallMap> sm(count);
+    const bool is_map = type == CC_RES_MAP;
+    for (auto& x : sm) x.flags = is_map ? (e->ttl_live ? kSmUnknown : kSmIn) : 0u;
+    HIPCHECK(hipMemcpy(e->d_msm + first, sm.data(), sizeof(SmallMap) * count, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemset(e->d_msmall + first, is_map && !e->ttl_live ? 1 : 0, count));
+    if (is_map && !e->ttl_live) e->small_live = true;
   }
   // fresh state: AtomicValueState() {value = null; current = null}
   HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
@@ -502,6 +537,7 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
       return set_err(CC_ERR_HIP, "map drop launch", hipGetLastError());
     HIPCHECK(hipStreamSynchronize(e->own_stream));
   }
+  if (e->map_bits) HIPCHECK(hipMemset(e->d_msmall + slot, 0, 1));  // no more small-map events for it
   e->res_type[slot] = CC_RES_NONE;
   // ResourceManagerStateMachineExecutor.close cancels the resource's timers
   e->gtimers.erase(std::remove_if(e->gtimers.begin(), e->gtimers.end(),
@@ -516,7 +552,7 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
   for (uint32_t i = 0; i < e->cfg.max_instances; ++i)
     if (e->inst_res[i] == slot) {
       e->inst_res[i] = kNoRes;
-      --e->sess_size;
+      e->sessions.remove((int64_t)e->inst_id[i]);
       e->inst_by_id.erase(e->inst_id[i]);
       e->used_inst.clear(i);
       HIPCHECK(hipMemcpy(e->d_inst_res + i, &none, sizeof none, hipMemcpyHostToDevice));
@@ -548,13 +584,9 @@ int cc::open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_fi
     e->inst_res[first + k] = (uint32_t)(res_first + k * res_stride);
     e->inst_id[first + k] = id_first + k;
     e->inst_client[first + k] = client;
-    e->inst_seq[first + k] = e->sess_next++;  // HashMap.putVal of a new key
+    e->sessions.put((int64_t)(id_first + k));  // sessions.put(instance id, holder): HashMap.putVal of a new key
     e->inst_by_id[id_first + k] = (uint32_t)(first + k);
     e->used_inst.set(first + k);
-    if (++e->sess_size > e->sess_thr) {
-      e->sess_cap <<= 1;
-      e->sess_thr <<= 1;
-    }
   }
   HIPCHECK(hipMemcpy(e->d_inst_res + first, e->inst_res.data() + first, sizeof(uint32_t) * count, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(e->d_inst_id + first, e->inst_id.data() + first, sizeof(uint64_t) * count, hipMemcpyHostToDevice));
@@ -614,7 +646,12 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
-    if (ttl_seen) e->ttl_live = true;
+    if (ttl_seen && !e->ttl_live) {  // TTL mode for good: the small maps' key sets stop being followed
+      e->ttl_live = true;
+      if (e->small_live && launch_small_ttl(e->d_msm, e->d_msmall, e->cfg.max_resources, st))
+        return set_err(CC_ERR_HIP, "small-map TTL launch", hipGetLastError());
+      e->small_live = false;
+    }
     // The leak log (commits dropped without clean()) is drained before every batch of an engine that can add to it:
     // every multimap put, and with value events every re-listen (AtomicValueState.listen :41-49) may land there, at
     // most one entry per row, so the drained log gets room for n more; a coordination engine without value events
@@ -744,6 +781,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.hot_msz = e->d_hot_msz;
+      ha.msmall = e->small_live ? e->d_msmall : nullptr;  // maps in their small window are not hot-routed
       ha.err = e->d_err;
       ha.mark = marker_of(e);
       static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
@@ -868,7 +906,47 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.mpcap = e->d_mpcap;
         za.list = e->d_msz_list;
         za.list_n = e->d_msz_list_n;
+        za.err = e->d_err;
+        if (e->small_live) {  // maps still in their small-table window: their insertions / removals (map_small.hip)
+          int rc = ensure_small(e);
+          if (rc) return rc;
+          if (!c->index) return set_err(CC_ERR_INVALID, "an engine with maps needs the index column (log order)");
+          za.msmall = e->d_msmall;
+          za.xrec = e->d_xrec;
+          za.idx0 = c->index + lo;
+          za.hh_key = e->d_hh_key;
+          za.hh_val = e->d_hh_val;
+          za.hh_n = e->hh_n;
+          za.ev_key = e->d_sm_key;
+          za.ev_val = e->d_sm_val;
+          za.ev_cap = (uint32_t)e->sub_batch;
+          za.sm_ctl = e->d_sm_ctl;
+        }
         if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError()); DBG_SYNC("map size launch");
+        if (e->small_live) {
+          uint32_t ctl[2] = {0, 0};
+          HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
+          HIPCHECK(hipStreamSynchronize(st));
+          SmallArgs sa{};
+          sa.ev_key = e->d_sm_key;
+          sa.ev_key2 = e->d_sm_key2;
+          sa.ev_val = e->d_sm_val;
+          sa.ev_val2 = e->d_sm_val2;
+          sa.cap = (uint32_t)e->sub_batch;
+          sa.temp = e->d_sm_temp;
+          sa.temp_bytes = e->sm_temp_bytes;
+          sa.ctl = e->d_sm_ctl;
+          sa.seg = e->d_sm_seg;
+          sa.nseg = e->d_sm_seg + e->cfg.max_resources;
+          sa.state = e->d_msm;
+          sa.msmall = e->d_msmall;
+          sa.mpcap = e->d_mpcap;
+          sa.max_resources = e->cfg.max_resources;
+          const int rs = launch_small_replay(sa, ctl[0], st);
+          if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "small-map replay launch", hipGetLastError())
+                                  : set_err(CC_ERR_STATE, "small-map events exceed their buffer");
+          if (ctl[0] == 0 && ctl[1] == 0) e->small_live = false;  // (ctl[1]: maps still small after the last replay)
+        }
       }
     }
     if (e->coord_on) {
@@ -1030,10 +1108,17 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.msize = e->ttl_live ? nullptr : e->d_msize;
     mw.mpcap = e->d_mpcap;
     mw.ctl = e->d_mw_ctl;
+    mw.small = e->res_type[res] == CC_RES_MAP ? e->d_msm : nullptr;
+    mw.hh_key = e->d_hh_key;
+    mw.hh_val = e->d_hh_val;
+    mw.hh_n = e->hh_n;
     mw.out_status = out->status;
     mw.out_value = out->value;
     mw.err = e->d_err;
     if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError()); DBG_SYNC("whole-map op launch");
+    if (e->res_type[res] == CC_RES_MAP && (mw.op == CC_OP_MAP_CLEAR || mw.op == CC_OP_DELETE) &&
+        launch_small_clear(e->d_msm, res, st))
+      return set_err(CC_ERR_HIP, "small-map clear launch", hipGetLastError());
   }
   }
   if (e->has_sets || e->has_mmaps) {
@@ -1061,6 +1146,46 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   return CC_OK;
 }
 
+// String.hashCode of HANDLE keys (java.util.HashMap bins of MapState, MapState.java:33,49-60): merged into the host
+// map, then the sorted (handle, hash) table is uploaded whole (control plane: rare, and small next to a batch).
+extern "C" int cc_handle_hashes(cc_engine* e, const uint64_t* h_handles, const int32_t* h_hashes, uint64_t count) {
+  if (!e || (count && (!h_handles || !h_hashes))) return set_err(CC_ERR_INVALID, "null argument");
+  if (count == 0) return CC_OK;
+  int rc = quiesce(e);
+  if (rc) return rc;
+  for (uint64_t i = 0; i < count; ++i) {
+    auto it = e->hh.find(h_handles[i]);
+    if (it != e->hh.end() && it->second != h_hashes[i])
+      return set_err(CC_ERR_INVALID, "a handle's String.hashCode cannot change (interned Strings are immutable)");
+    e->hh[h_handles[i]] = h_hashes[i];
+  }
+  const uint32_t n = (uint32_t)e->hh.size();
+  if (n > e->hh_cap) {
+    const uint32_t cap = std::max<uint32_t>(n, e->hh_cap * 2);
+    uint64_t* k = nullptr;
+    int32_t* v = nullptr;
+    HIPCHECK(hipMalloc(&k, 8ull * cap));
+    if (hipMalloc(&v, 4ull * cap) != hipSuccess) {
+      (void)hipFree(k);
+      return set_err(CC_ERR_HIP, "hipMalloc handle hashes");
+    }
+    if (e->d_hh_key) (void)hipFree(e->d_hh_key);
+    if (e->d_hh_val) (void)hipFree(e->d_hh_val);
+    e->d_hh_key = k;
+    e->d_hh_val = v;
+    e->hh_cap = cap;
+  }
+  std::vector<uint64_t> hk;
+  std::vector<int32_t> hv;
+  hk.reserve(n);
+  hv.reserve(n);
+  for (const auto& kv : e->hh) hk.push_back(kv.first), hv.push_back(kv.second);
+  HIPCHECK(hipMemcpy(e->d_hh_key, hk.data(), 8ull * n, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(e->d_hh_val, hv.data(), 4ull * n, hipMemcpyHostToDevice));
+  e->hh_n = n;
+  return CC_OK;
+}
+
 extern "C" int cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* stream) {
   if (!e || !d_out) return set_err(CC_ERR_INVALID, "null argument");
   HIPCHECK(hipSetDevice(e->device));
@@ -1080,10 +1205,6 @@ extern "C" int cc_applied_index(cc_engine* e, uint64_t* out) {
 }
 
 // HashMap.hash of a java.lang.Long key: h = (int)(v ^ v >>> 32); h ^ h >>> 16
-static uint32_t java_long_hash(uint64_t v) {
-  const uint32_t h = (uint32_t)(v ^ (v >> 32));
-  return h ^ (h >> 16);
-}
 
 // ResourceManager.close(Session) for each client session of h_clients, in that order (ResourceManager.java:250-264).
 extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* d_events,
@@ -1111,10 +1232,14 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   struct Close { uint64_t crank, okey; uint32_t slot; };
   std::vector<Close> order;
   order.reserve(by_client.size());
-  for (auto& bc : by_client) {
-    const uint32_t i = bc.second;
-    const uint64_t okey = ((uint64_t)(java_long_hash(e->inst_id[i]) & (e->sess_cap - 1)) << 40) | e->inst_seq[i];
-    order.push_back(Close{bc.first, okey, i});
+  {
+    std::unordered_map<uint64_t, uint64_t> pos;  // instance id -> position in sessions.values() iteration order
+    uint64_t q = 0;
+    e->sessions.for_each([&](int64_t id) { pos[(uint64_t)id] = q++; });
+    for (auto& bc : by_client) {
+      const uint32_t i = bc.second;
+      order.push_back(Close{bc.first, pos.at(e->inst_id[i]), i});
+    }
   }
   std::sort(order.begin(), order.end(), [](const Close& x, const Close& y) {
     return x.crank != y.crank ? x.crank < y.crank : x.okey < y.okey;
@@ -1243,7 +1368,7 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
     if (!e->res_zombie[r]) e->res_sessions.erase({r, e->inst_client[i]});
     if (p == stop) continue;
     e->inst_res[i] = kNoRes;
-    --e->sess_size;
+    e->sessions.remove((int64_t)e->inst_id[i]);
     e->inst_by_id.erase(e->inst_id[i]);
     e->used_inst.clear(i);
     ++closed;
@@ -1571,14 +1696,14 @@ static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unp
 // Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
 // mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
 namespace {
-constexpr uint64_t kSnapMagic = 0x34304E5053434343ull;  // "CCCSPN04"
+constexpr uint64_t kSnapMagic = 0x35304E5053434343ull;  // "CCCSPN05"
 constexpr uint32_t kSnapRetained = 4u;                   // SnapHdr.flags: CC_CFG_VALUE_RETAINED section present
 struct SnapHdr {
   uint64_t magic;
   uint32_t abi, flags;  // flags: 1 coord blocks, 2 map TTL mode, 4 retained value commits
   uint32_t max_resources, max_instances, map_bits, sb;
-  uint64_t applied, sess_next;
-  uint32_t sess_cap, sess_thr, sess_size, coord_cap;
+  uint64_t applied;
+  uint32_t coord_cap, pad;
 };
 struct Section {
   void* dev;
@@ -1594,7 +1719,6 @@ static std::vector<Section> snap_sections(cc_engine* e) {
       {nullptr, e->inst_res.data(), 4 * mi},
       {nullptr, e->inst_id.data(), 8 * mi},
       {nullptr, e->inst_client.data(), 8 * mi},
-      {nullptr, e->inst_seq.data(), 8 * mi},
       {nullptr, e->sb_kind.data(), e->sb},
       {e->d_inst_res, nullptr, 4 * mi},
       {e->d_res_type, nullptr, slots},
@@ -1621,6 +1745,8 @@ static std::vector<Section> snap_sections(cc_engine* e) {
     v.push_back({e->d_mw_drop, nullptr, 8 * mr});
     v.push_back({e->d_msize, nullptr, 4 * mr});
     v.push_back({e->d_mpcap, nullptr, 4 * mr});
+    v.push_back({e->d_msm, nullptr, sizeof(SmallMap) * mr});
+    v.push_back({e->d_msmall, nullptr, mr});
   }
   if (e->coord_on) v.push_back({e->d_coord, nullptr, coord_block(e->coord_cap) * slots});
   return v;
@@ -1637,8 +1763,10 @@ extern "C" int cc_snapshot_size(cc_engine* e, uint64_t* bytes) {
   int rc = quiesce(e);  // the leak log's entries are counted from the host lists
   if (rc) return rc;
   if ((rc = drain_leaks(e))) return rc;
+  std::vector<uint8_t> sess;
+  e->sessions.save(sess);
   uint64_t total = sizeof(SnapHdr) + 16 + e->gtimers.size() * sizeof(cc_engine::GroupTimer) + 8 +
-                   e->res_sessions.size() * 24 + 8 + leak_entries(e) * 16;
+                   e->res_sessions.size() * 24 + 8 + leak_entries(e) * 16 + 8 + sess.size() + 8 + e->hh.size() * 16;
   for (const Section& x : snap_sections(e)) total += 8 + x.bytes;
   *bytes = total;
   return CC_OK;
@@ -1660,10 +1788,6 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
   h.map_bits = e->map_bits;
   h.sb = e->sb;
   h.applied = e->applied;
-  h.sess_next = e->sess_next;
-  h.sess_cap = e->sess_cap;
-  h.sess_thr = e->sess_thr;
-  h.sess_size = e->sess_size;
   h.coord_cap = e->coord_cap;
   uint8_t* p = (uint8_t*)h_buf;
   memcpy(p, &h, sizeof h);
@@ -1697,6 +1821,20 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
       memcpy(p, t, 16);
       p += 16;
     }
+  std::vector<uint8_t> sess;  // ResourceManager.sessions' java.util.HashMap structure (close order)
+  e->sessions.save(sess);
+  const uint64_t sb = sess.size();
+  memcpy(p, &sb, 8);
+  memcpy(p + 8, sess.data(), sb);
+  p += 8 + sb;
+  const uint64_t nh = e->hh.size();  // String.hashCode of HANDLE keys: (handle, hash) pairs
+  memcpy(p, &nh, 8);
+  p += 8;
+  for (const auto& kv : e->hh) {
+    const uint64_t t[2] = {kv.first, (uint64_t)(uint32_t)kv.second};
+    memcpy(p, t, 16);
+    p += 16;
+  }
   return CC_OK;
 }
 
@@ -1748,6 +1886,19 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   memcpy(&nl, p, 8);
   p += 8;
   if (!snap_room(p, end, nl, 16)) return set_err(CC_ERR_INVALID, "snapshot truncated (leak lists)");
+  const uint8_t* tail = p + nl * 16;
+  uint64_t sbytes = 0, nh = 0;
+  cc::JavaLongHashMap sessions;
+  if (!snap_room(tail, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&sbytes, tail, 8);
+  tail += 8;
+  if (!snap_room(tail, end, sbytes, 1) || sessions.load(tail, sbytes) != sbytes)
+    return set_err(CC_ERR_INVALID, "snapshot: malformed sessions table");
+  tail += sbytes;
+  if (!snap_room(tail, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&nh, tail, 8);
+  tail += 8;
+  if (!snap_room(tail, end, nh, 16)) return set_err(CC_ERR_INVALID, "snapshot truncated (handle hashes)");
   // 2. apply
   int rc = quiesce(e);
   if (rc) return rc;
@@ -1815,10 +1966,20 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   e->has_values = e->has_values || std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_VALUE) != e->res_type.end();
   e->has_mmaps = std::find(e->res_type.begin(), e->res_type.end(), (uint8_t)CC_RES_MULTIMAP) != e->res_type.end();
   if (e->has_mmaps && (rc = ensure_leak(e, kLeakCap))) return rc;
-  e->sess_next = h.sess_next;
-  e->sess_cap = h.sess_cap;
-  e->sess_thr = h.sess_thr;
-  e->sess_size = h.sess_size;
+  e->sessions = std::move(sessions);
+  e->small_live = e->map_bits && !e->ttl_live;  // (the next sub-batch recounts the maps still small)
+  {
+    std::vector<uint64_t> hk(nh);
+    std::vector<int32_t> hv(nh);
+    for (uint64_t i = 0; i < nh; ++i, tail += 16) {
+      uint64_t t[2];
+      memcpy(t, tail, 16);
+      hk[i] = t[0];
+      hv[i] = (int32_t)(uint32_t)t[1];
+    }
+    e->hh.clear();
+    if (nh && (rc = cc_handle_hashes(e, hk.data(), hv.data(), nh))) return rc;
+  }
   HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
   return CC_OK;
 }

@@ -138,8 +138,38 @@ struct MapSizeArgs {
   uint32_t* mpcap;             // [max_resources] log2(HashMap capacity / 16) of the peak size so far (| kMpInexact)
   uint4* list;                 // [kMszListCap] (tile, map, size at the tile's start) pairs for the exact pass
   uint32_t* list_n;
+  // small maps (map_small.hip): events of the maps still in the window (null msmall: none is)
+  const uint8_t* msmall;       // [max_resources] 1: the map's table is small (capacity <= 64), followed key by key
+  const XRec* xrec;            // the sub-batch's staging records (log index, key, key tag)
+  const uint64_t* idx0;        // device: the log index of the sub-batch's first row
+  const uint64_t* hh_key;      // String.hashCode of HANDLE keys (cc_handle_hashes), sorted by handle
+  const int32_t* hh_val;
+  uint32_t hh_n;
+  uint64_t* ev_key;            // [ev_cap] map << 44 | (index - idx0) << 4 | code
+  uint32_t* ev_val;            // [ev_cap] the key's HashMap hash
+  uint32_t ev_cap;
+  uint32_t* sm_ctl;            // [0] events emitted
+  uint32_t* err;
 };
 int launch_map_size(const MapSizeArgs& a, hipStream_t st);
+struct SmallArgs {
+  uint64_t *ev_key, *ev_key2;  // events and their sorted copy
+  uint32_t *ev_val, *ev_val2;
+  uint32_t cap;
+  void* temp;                  // hipcub radix-sort scratch
+  size_t temp_bytes;
+  uint32_t* ctl;               // [0] events, [1] maps still in the window (after the replay)
+  uint32_t* seg;               // [max_resources] run starts
+  uint32_t* nseg;
+  SmallMap* state;             // [max_resources]
+  uint8_t* msmall;
+  uint32_t* mpcap;
+  uint32_t max_resources;
+};
+int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st);
+size_t small_sort_temp_bytes(uint32_t cap);
+int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st);
+int launch_small_ttl(SmallMap* state, uint8_t* msmall, uint32_t R, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
 int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* map_row, hipStream_t st);
 
@@ -165,6 +195,10 @@ struct MapWideArgs {
   uint32_t* msize;             // exact tracking (launch_map_size; null in TTL mode): the live size, and
   const uint32_t* mpcap;       //   log2(capacity / 16) of the peak (in TTL mode a lower bound for the bounds above)
   unsigned long long* ctl;     // [C_N] scratch
+  const SmallMap* small;       // [max_resources] the small-table state (early resizes, tree bins; map_small.hip)
+  const uint64_t* hh_key;      // String.hashCode of HANDLE keys (sorted by handle)
+  const int32_t* hh_val;
+  uint32_t hh_n;
   uint8_t* out_status;
   uint64_t* out_value;
   uint32_t* err;
@@ -220,6 +254,7 @@ struct HotArgs {
   uint64_t* tbl_ins;
   HotKey* hot;
   uint32_t* hot_n;
+  const uint8_t* msmall;  // [max_resources] maps in their small-table window (map_small.hip): never hot-routed
   HotKey* hot_cand;      // [kHotMax] the batch's hot keys by rank (k_hot_count), bound per sub-batch (k_hot_bind)
   const uint32_t* hot_meta;  // [sub_batch] meta word of each hot-bucket record (k_part_ext), read by k_hot_agg
   uint32_t* hot_cand_n;

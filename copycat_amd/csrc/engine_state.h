@@ -11,6 +11,7 @@
 
 #include "common.h"
 #include "engine_internal.h"
+#include "java_hashmap.h"
 
 namespace cc {
 // error reporting (cc_last_error) and the stream drain every registry update starts with
@@ -88,12 +89,15 @@ struct cc_engine {
   std::vector<uint8_t> res_type;     // [sb*256]
   std::vector<uint32_t> inst_res;    // [max_inst]
   std::vector<uint64_t> inst_id, inst_client;
-  // java.util.HashMap iteration order of ResourceManager.sessions (ResourceManager.java:37): bucket index under
-  // the table capacity (starts at 16, doubles when the size passes 3/4 of it, never shrinks), then insertion
-  // order within the bucket.  Used to order the close fan-out (ResourceManager.java:250-264).
-  uint32_t sess_cap = 16, sess_thr = 12, sess_size = 0;
-  uint64_t sess_next = 0;
-  std::vector<uint64_t> inst_seq;
+  // ResourceManager.sessions (ResourceManager.java:37, a java.util.HashMap<Long, SessionHolder> keyed by instance
+  // id): its iteration order orders the close / expire fan-out (ResourceManager.java:237-264; java_hashmap.h)
+  cc::JavaLongHashMap sessions;
+  // String.hashCode of HANDLE keys (host-interned Strings): java.util.HashMap's bins of MapState (containsValue
+  // order, MapState.java:49-60).  Host map + a sorted device copy (handle, hash) for the map kernels.
+  std::map<uint64_t, int32_t> hh;
+  uint64_t* d_hh_key = nullptr;
+  int32_t* d_hh_val = nullptr;
+  uint32_t hh_n = 0, hh_cap = 0;
   // ResourceManager control plane (manager.hip; ResourceManager.java:37-39,269-295).  Resource ids and instance ids
   // are commit indices (:86-88,103,185); slots are the engine's dense handles for them.
   std::unordered_map<uint64_t, uint64_t> keys;       // ResourceManager.keys: host-interned key -> resource id
@@ -146,6 +150,16 @@ struct cc_engine {
   uint32_t* d_msz_tcnt = nullptr;  // [max_tiles][max_resources]
   uint4* d_msz_list = nullptr;     // [kMszListCap]
   uint32_t* d_msz_list_n = nullptr;
+  // maps whose HashMap table is still small (capacity <= 64): early resizes and tree bins (map_small.hip)
+  SmallMap* d_msm = nullptr;       // [max_resources]
+  uint8_t* d_msmall = nullptr;     // [max_resources] 1: in the window
+  uint32_t* d_sm_ctl = nullptr;    // [4] events of the sub-batch, maps still in the window
+  uint64_t *d_sm_key = nullptr, *d_sm_key2 = nullptr;  // [sub_batch] events (allocated while a map is small)
+  uint32_t *d_sm_val = nullptr, *d_sm_val2 = nullptr;
+  uint32_t* d_sm_seg = nullptr;    // [max_resources + 1] run starts + count
+  void* d_sm_temp = nullptr;
+  size_t sm_temp_bytes = 0;
+  bool small_live = false;         // some map may still be in the window (the host then reads the event count)
   unsigned long long* d_mw_ctl = nullptr;  // [16]
   std::vector<uint32_t> bars;
   // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good

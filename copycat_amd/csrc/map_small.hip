@@ -1,0 +1,170 @@
+// map_small.hip — the java.util.HashMap of a map whose table is still small (capacity <= 64), followed key by key.
+//
+// MapState keeps its entries in a `new HashMap<>()` (collections/src/main/java/io/atomix/collections/state/
+// MapState.java:33), and containsValue (:49-60) walks map.values(): the answer (true, or the NullPointerException of
+// a stored null met first) depends on the table's capacity.  The size-driven resizes are tracked by
+// launch_map_size (map_wide.hip).  Below capacity 64 there is a second trigger: java.util.HashMap.putVal calls
+// treeifyBin when a new key makes its bin's chain 9 long, and treeifyBin RESIZES a table under MIN_TREEIFY_CAPACITY
+// (64) instead of treeifying -- at any size.  At capacity 64 the same bin becomes a red-black tree bin, whose
+// iteration order (root first, later keys linked after their tree parent) this engine does not follow: it records
+// which bins (mod 64) became trees, and an order-dependent containsValue deciding inside one of them fails with
+// CC_ERR_STATE instead of guessing.
+//
+// Per map in that window the engine keeps the live keys' hashes (at most 48: a table of 64 holds <= 48 keys) and
+// replays the map's insertions and removals in log order:
+//   1. launch_map_size's count kernel (k_msize_count) emits one event per region commit of a small map that inserted
+//      or removed a key: key (map << 44 | (log index - the sub-batch's first) << 4 | insert / remove), value = the
+//      key's HashMap hash (hot-key routing is off for small maps, k_hot_bind, so every such commit is a region one);
+//   2. a radix sort by that key puts each map's events in log order (hipcub);
+//   3. one wave per map replays them: lane i holds the i-th live hash; an insert counts its bin's keys with one
+//      ballot (>= 8 before it: treeifyBin -- a resize below 64, a tree bin at 64), appends, and resizes when the
+//      size passes 3/4 of the capacity; a removal drops one equal hash.  The map leaves the window when its capacity
+//      passes 64 (no early resize, and no untracked tree, can happen below a tree-free table of 128 ... see
+//      map_wide.hip k_mw_order for the check above 64).
+// The capacity level reached is merged into the tracked level (mpcap, atomicMax): the true capacity is the larger of
+// the size-driven one and the early one (after the window both grow by size alone).
+// Cost: nothing once every map has left the window (the host stops looking: no event, no sync); while some are in
+// it, one host read of the event count per sub-batch, a sort of the events and one short wave walk per map.
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+// event runs: the first event of each map's run (the sort put one map's events together, in log order)
+__global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __restrict__ ctl, uint32_t* __restrict__ seg,
+                            uint32_t* __restrict__ nseg) {
+  const uint32_t E = ctl[0];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x)
+    if (i == 0 || (key[i] >> 44) != (key[i - 1] >> 44)) seg[atomicAdd(nseg, 1u)] = i;
+}
+
+// One wave per run: the map's live hashes in lanes 0..n-1, its events in log order.
+__global__ __launch_bounds__(256) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                      const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
+                                                      const uint32_t* __restrict__ nseg, SmallMap* __restrict__ st,
+                                                      uint8_t* __restrict__ msmall, uint32_t* __restrict__ mpcap) {
+  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
+    const uint32_t start = seg[r];
+    const uint32_t m = (uint32_t)(key[start] >> 44);
+    SmallMap* s = st + m;
+    uint32_t n = s->n, lvl = s->lvl, flags = s->flags;
+    uint64_t tree = s->tree_bins;
+    if (!(flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
+    uint32_t h = l < n ? s->jh[l] : 0u;
+    bool live = l < n;
+    for (uint32_t i = start; i < E; ++i) {
+      const uint64_t k = key[i];
+      if ((uint32_t)(k >> 44) != m) break;
+      const uint32_t x = val[i];
+      if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
+        const uint32_t mask = (16u << lvl) - 1u;
+        const uint32_t in_bin = (uint32_t)__builtin_popcountll(__ballot(live && (h & mask) == (x & mask)));
+        if (in_bin >= 8u) {  // the chain reaches 9 nodes: treeifyBin
+          if (lvl < 2u) ++lvl;  // capacity < MIN_TREEIFY_CAPACITY: resize()
+          else flags |= kSmTree, tree |= 1ull << (x & 63u);
+        }
+        if (l == n) h = x, live = true;
+        ++n;
+        if (n > (12u << lvl)) ++lvl;  // ++size > threshold: resize()
+        if (lvl >= 3u) {              // capacity 128: out of the window
+          flags &= ~kSmIn;
+          break;
+        }
+      } else if ((k & 3u) == 2u) {  // a key removed: removeNode (one equal hash leaves the multiset)
+        const uint64_t eq = __ballot(live && h == x);
+        if (eq) {
+          const uint32_t at = (uint32_t)__builtin_ctzll(eq), last = n - 1;
+          const uint32_t moved = __shfl(h, (int)last, 64);
+          if (l == at) h = moved;
+          if (l == last) live = false;
+          --n;
+        }
+      }
+    }
+    if (flags & kSmIn) {
+      if (l < kSmKeys) s->jh[l] = live ? h : 0u;
+    }
+    if (l == 0) {
+      s->n = (flags & kSmIn) ? n : 0u;
+      s->lvl = lvl;
+      s->flags = flags;
+      s->tree_bins = tree;
+      msmall[m] = (flags & kSmIn) ? 1u : 0u;
+      atomicMax(&mpcap[m], lvl);
+    }
+  }
+}
+
+// maps still in the window (read by the host with the next sub-batch's event count)
+__global__ void k_small_count(const uint8_t* __restrict__ msmall, uint32_t R, uint32_t* __restrict__ ctl) {
+  uint32_t c = 0;
+  for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x) c += msmall[m];
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&ctl[1], c);
+}
+
+// MapState.delete (clear / Delete, :255-274): every key leaves; the table keeps its capacity; no tree bin is left
+__global__ void k_small_clear(SmallMap* __restrict__ st, uint32_t m) {
+  if (threadIdx.x == 0) {
+    st[m].n = 0;
+    st[m].flags &= ~kSmTree;
+    st[m].tree_bins = 0;
+  }
+}
+
+// TTL mode: timers remove keys without a commit, so the small maps' key sets are no longer known
+__global__ void k_small_ttl(SmallMap* __restrict__ st, uint8_t* __restrict__ msmall, uint32_t R) {
+  for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
+    if (msmall[m]) {
+      st[m].flags |= kSmUnknown;
+      msmall[m] = 0;
+    }
+}
+
+int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
+  if (E > a.cap) return -2;
+  if (E) {
+    size_t need = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, need, a.ev_key, a.ev_key2, a.ev_val, a.ev_val2, (int)E, 0, 64, st) !=
+        hipSuccess)
+      return -1;
+    if (need > a.temp_bytes) return -3;  // (sized for cap events at creation)
+    size_t tb = a.temp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(a.temp, tb, a.ev_key, a.ev_key2, a.ev_val, a.ev_val2, (int)E, 0, 64, st) !=
+        hipSuccess)
+      return -1;
+    if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (E + 255) / 256);
+    hipLaunchKernelGGL(k_small_seg, dim3(grid), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg);
+    hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ctl, a.seg, a.nseg, a.state,
+                       a.msmall, a.mpcap);
+  }
+  // the next sub-batch's counters: events 0, maps still small recounted
+  if (hipMemsetAsync(a.ctl, 0, 2 * sizeof(uint32_t), st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_small_count, dim3(std::min<uint32_t>(256, (a.max_resources + 255) / 256)), dim3(256), 0, st, a.msmall,
+                     a.max_resources, a.ctl);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t small_sort_temp_bytes(uint32_t cap) {
+  size_t need = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, need, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
+  return need;
+}
+
+int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st) {
+  hipLaunchKernelGGL(k_small_clear, dim3(1), dim3(64), 0, st, state, m);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_small_ttl(SmallMap* state, uint8_t* msmall, uint32_t R, hipStream_t st) {
+  hipLaunchKernelGGL(k_small_ttl, dim3(std::min<uint32_t>(256, (R + 255) / 256)), dim3(256), 0, st, state, msmall, R);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cc

@@ -126,16 +126,6 @@ __device__ inline bool live_at(uint32_t w, const uint64_t* __restrict__ dl, uint
   return d == 0 || d > fire;
 }
 
-// java.lang.{Long,Integer,Boolean}.hashCode spread by HashMap.hash (oracle java_hash; HANDLE as Long).
-__device__ inline uint32_t java_hash_dev(uint32_t ktag, uint64_t v) {
-  uint32_t h;
-  switch (ktag) {  // key tags: 0 LONG, 1 INT, 2 BOOL, 3 HANDLE
-    case 1: h = (uint32_t)v; break;
-    case 2: h = v ? 1231u : 1237u; break;
-    default: h = (uint32_t)(v ^ (v >> 32)); break;
-  }
-  return h ^ (h >> 16);
-}
 // HashMap capacity after the map's size peaked at p (16, doubled while p > 0.75 * capacity).
 __device__ inline uint64_t java_cap(uint64_t p) {
   uint64_t cap = 16, thr = 12;
@@ -148,11 +138,13 @@ __device__ inline uint64_t java_cap(uint64_t p) {
 
 // ctl layout (u64): 0 present, 1 bound (used, not dead), 2 stored nulls, 3 matches, 4/5 min bucket of a
 // null / a match, 6/7 min insertion index of a null / a match inside that bucket, 8 capacity (0 = undetermined)
-enum { C_PRES = 0, C_USED, C_NULLS, C_MATCH, C_BN, C_BM, C_IN, C_IM, C_CAP, C_N };
+// 9.. per capacity level L >= 3 (128 << (L - 3)): bound keys of the map whose hash is the deciding bucket's modulo
+// that capacity (a tree bin can have formed there only if >= 9 keys ever shared it)
+enum { C_PRES = 0, C_USED, C_NULLS, C_MATCH, C_BN, C_BM, C_IN, C_IM, C_CAP, C_TR0, C_N = C_TR0 + 32 };
 
 __global__ void k_mw_reset(unsigned long long* ctl) {
   const int t = threadIdx.x;
-  if (t < C_N) ctl[t] = (t >= C_BN && t <= C_IM) ? ~0ull : 0ull;
+  for (int q = t; q < C_N; q += blockDim.x) ctl[q] = (q >= C_BN && q <= C_IM) ? ~0ull : 0ull;
 }
 
 __device__ inline unsigned long long wave_sum(unsigned long long x) {
@@ -202,35 +194,55 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
                                                   const uint64_t* __restrict__ val, const uint64_t* __restrict__ ins,
                                                   const uint64_t* __restrict__ dl, uint64_t fire, uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag, uint64_t apay,
                                                   const uint32_t* __restrict__ peak_lo, const unsigned long long* __restrict__ dropped,
-                                                  const uint32_t* __restrict__ mpcap, bool exact,
-                                                  int pass, unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
+                                                  const uint32_t* __restrict__ mpcap, bool exact, const SmallMap* __restrict__ small,
+                                                  const uint64_t* __restrict__ hh_key, const int32_t* __restrict__ hh_val,
+                                                  uint32_t hh_n, int pass, unsigned long long* __restrict__ ctl,
+                                                  uint32_t* __restrict__ err) {
   if (op != CC_OP_MAP_CONTAINSVALUE || ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0) return;
   const uint32_t mp = mpcap ? mpcap[slot] : 0u, lv = mp & ~kMpInexact;
+  const uint32_t sflags = small ? small[slot].flags : 0u;
   uint64_t cap;
   if (exact && !(mp & kMpInexact)) {
-    cap = 16ull << lv;  // the tracked peak's capacity (it covers the live size counted here)
+    cap = 16ull << lv;  // the tracked capacity (size-driven resizes, and treeifyBin's below 64: map_small.hip)
   } else {
     // bounds: the level reached while tracking was exact means a peak above the previous level's threshold
     const uint64_t lo = max(max((uint64_t)peak_lo[slot], (uint64_t)ctl[C_PRES]), lv ? (12ull << (lv - 1)) + 1 : 0ull);
     const uint64_t hi = ctl[C_USED] + dropped[slot];
-    cap = java_cap(lo);
-    if (java_cap(hi) != cap) {
+    cap = max(java_cap(lo), 16ull << lv);
+    uint64_t cap_hi = java_cap(hi);
+    if ((sflags & kSmUnknown) && hi >= 9) cap_hi = max(cap_hi, 64ull);  // an untracked early resize (treeifyBin)
+    if (max(cap_hi, 16ull << lv) != cap) {
       if (blockIdx.x == 0 && threadIdx.x == 0 && pass == 0) atomicOr(err, kErrMapOrder);
       return;
     }
   }
   if (pass == 1 && ctl[C_BN] != ctl[C_BM]) return;  // decided by the buckets
+  const uint64_t bb = ctl[C_BN];                     // (pass 1: the bucket holding the first null and the first match)
   for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
     const uint32_t w = word[e];
-    if ((w & kMwDead) || (w & kMwSlotMask) != slot || !live_at(w, dl, e, fire)) continue;
+    if ((w & kMwDead) || !(w & kMwUsed) || (w & kMwSlotMask) != slot) continue;
+    const bool present = live_at(w, dl, e, fire);
     const uint32_t vt = mw_vtag(w);
     const bool isnull = vt == CC_TAG_NULL;
-    if (!isnull && !(vt == atag && val[e] == apay)) continue;
-    const uint64_t b = java_hash_dev((w >> 17) & 3, key[e]) & (cap - 1);
+    const bool cand = present && (isnull || (vt == atag && val[e] == apay));
+    if (pass == 0 && !cand) continue;
+    bool ok;
+    const uint32_t jh = java_key_hash((w >> 17) & 3, key[e], hh_key, hh_val, hh_n, ok);
+    if (!ok) {
+      atomicOr(err, kErrHandleHash);
+      continue;
+    }
+    const uint64_t b = jh & (cap - 1);
     if (pass == 0) {
       atomicMin(&ctl[isnull ? C_BN : C_BM], (unsigned long long)b);
-    } else if (b == ctl[C_BN]) {
-      atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ins[e]);
+    } else {
+      if (cand && b == bb) atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ins[e]);
+      // every key the map ever bound (present or not) that shares the deciding bin at a capacity >= 128: a tree bin
+      // there needs >= 9 of them (HashMap.treeifyBin, TREEIFY_THRESHOLD)
+      for (uint32_t L = 3; L <= lv && L - 3 < 32; ++L) {
+        const uint64_t mk = (16ull << L) - 1;
+        if ((jh & mk) == (bb & mk)) atomicAdd(&ctl[C_TR0 + (L - 3)], 1ull);
+      }
     }
   }
   if (pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) ctl[C_CAP] = cap;
@@ -250,7 +262,7 @@ __global__ void k_mw_size(uint32_t slot, uint32_t op, const unsigned long long* 
 
 __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsigned long long* __restrict__ ctl,
                             uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped, uint8_t* __restrict__ out_status,
-                            uint64_t* __restrict__ out_value) {
+                            uint64_t* __restrict__ out_value, const SmallMap* __restrict__ small, uint32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
   const uint64_t pres = ctl[C_PRES];
   uint32_t st = CC_STATUS(CC_ST_OK, CC_TAG_NULL);
@@ -272,6 +284,16 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
       } else {  // the first of (null, match) in HashMap iteration order
         const uint64_t bn = ctl[C_BN], bm = ctl[C_BM];
         npe = bn != bm ? bn < bm : ctl[C_IN] < ctl[C_IM];
+        if (bn == bm) {  // decided inside one bin: by insertion order, unless that bin was ever a tree bin
+          bool tree = false;
+          if (small) {
+            const SmallMap& sm = small[slot];
+            tree = ((sm.flags & kSmTree) && ((sm.tree_bins >> (bn & 63u)) & 1ull)) ||
+                   ((sm.flags & kSmUnknown) && ctl[C_USED] + dropped[slot] >= 9);
+          }
+          for (int q = 0; q < 32; ++q) tree |= ctl[C_TR0 + q] + dropped[slot] >= 9;
+          if (tree) atomicOr(err, kErrMapOrder);
+        }
       }
       if (npe) {
         st = CC_STATUS(CC_ST_NULL_POINTER, CC_TAG_NULL);
@@ -359,18 +381,19 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
   const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (a.entries + kMwT - 1) / kMwT);
   const uint32_t atag = a.atag, op = a.op;
   const uint64_t apay = atag == CC_TAG_NULL ? 0 : a.apay;  // canonical NULL payload
-  hipLaunchKernelGGL(k_mw_reset, dim3(1), dim3(64), 0, st, a.ctl);
+  hipLaunchKernelGGL(k_mw_reset, dim3(1), dim3(64), 0, st, a.ctl);  // (C_N <= 64 entries)
   hipLaunchKernelGGL(k_mw_count, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_val, a.tbl_dl, a.fire_clock, a.entries, a.slot, op,
                      atag, apay, a.ctl);
   if (op == CC_OP_MAP_CONTAINSVALUE) {
     for (int pass = 0; pass < 2; ++pass)
       hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.tbl_dl,
                          a.fire_clock, a.entries, a.slot, op, atag, apay, a.peak_lo,
-                         (const unsigned long long*)a.dropped, a.mpcap, a.msize != nullptr, pass, a.ctl, a.err);
+                         (const unsigned long long*)a.dropped, a.mpcap, a.msize != nullptr, a.small, a.hh_key, a.hh_val,
+                         a.hh_n, pass, a.ctl, a.err);
   }
   if (a.msize) hipLaunchKernelGGL(k_mw_size, dim3(1), dim3(64), 0, st, a.slot, op, a.ctl, a.msize, a.err);
   hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,
-                     (unsigned long long*)a.dropped, a.out_status, a.out_value);
+                     (unsigned long long*)a.dropped, a.out_status, a.out_value, a.small, a.err);
   if (hipGetLastError() != hipSuccess) return -1;
   if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE) return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, st);
   return 0;
@@ -415,12 +438,33 @@ __device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_
   lds_barrier();
 }
 
+// A small map's insertion / removal (map_small.hip): its log index, the key's HashMap hash.
+__device__ inline void small_event(uint32_t m, uint32_t code, const XRec& xr, uint64_t idx0, const uint64_t* __restrict__ hh_key,
+                                   const int32_t* __restrict__ hh_val, uint32_t hh_n, uint64_t* __restrict__ ev_key,
+                                   uint32_t* __restrict__ ev_val, uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
+                                   uint32_t* __restrict__ err) {
+  bool ok;
+  const uint32_t jh = java_key_hash(CC_FLAG_KTAG(smeta_flags(xr.meta)), xr.key, hh_key, hh_val, hh_n, ok);
+  const uint64_t d = xr.idx - idx0;
+  if (!ok || d >> 40) atomicOr(err, kErrHandleHash);  // an unregistered String key / a sub-batch spanning 2^40 indices
+  const uint32_t at = atomicAdd(sm_ctl, 1u);
+  if (at < ev_cap) {
+    ev_key[at] = ((uint64_t)m << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
+    ev_val[at] = jh;
+  }
+}
+
 __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restrict__ ttab, uint32_t sb, uint32_t k0,
                                                       uint32_t sb_hot, const uint32_t* __restrict__ msz,
                                                       const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n,
                                                       const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
                                                       const uint32_t* __restrict__ hot_msz, uint32_t R,
-                                                      uint32_t* __restrict__ tcnt, uint32_t* __restrict__ list_n) {
+                                                      uint32_t* __restrict__ tcnt, uint32_t* __restrict__ list_n,
+                                                      const uint8_t* __restrict__ msmall, const XRec* __restrict__ xrec,
+                                                      const uint64_t* __restrict__ idx0p, const uint64_t* __restrict__ hh_key,
+                                                      const int32_t* __restrict__ hh_val, uint32_t hh_n,
+                                                      uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val,
+                                                      uint32_t ev_cap, uint32_t* __restrict__ sm_ctl, uint32_t* __restrict__ err) {
   __shared__ uint32_t cnt[kMszPass];
   if (blockIdx.x == 0 && threadIdx.x == 0) *list_n = 0;  // (k_msize_scan, the next launch, appends to the list)
   __shared__ uint32_t pfx[kHotMax + 1];
@@ -438,6 +482,9 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
       const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
       if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
+      if (code && base == 0 && msmall && msmall[x >> 2])  // a map still in its small window (map_small.hip)
+        small_event(x >> 2, code, xrec[(uint64_t)t * kTile + p], *idx0p, hh_key, hh_val, hh_n, ev_key, ev_val, ev_cap,
+                    sm_ctl, err);
     }
     for (uint32_t h = threadIdx.x; h < nh; h += kMszT) {  // one thread per hot key: its run in this tile (a few words)
       const uint32_t m = (hot[h].ident & kMwSlotMask) - base;
@@ -608,7 +655,8 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
 int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.sb_hot, a.rst_msz, a.hot,
-                     a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n);
+                     a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n, a.msmall, a.xrec,
+                     a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_cap, a.sm_ctl, a.err);
   hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,
                      a.res_type, a.max_resources, a.tiles, a.tcnt, a.msize, a.mpcap, a.list, a.list_n);
   hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.sb_hot,

@@ -173,6 +173,7 @@ struct cc_wire_interner {
   std::unordered_map<std::string, uint64_t> ids;
   std::vector<std::string> strs;  // handle - first -> bytes
   uint64_t first;
+  std::vector<int32_t> hashes;    // handle - first -> java.lang.String.hashCode
 };
 
 using namespace cc;
@@ -193,12 +194,44 @@ bool read_utf8(Reader& r, const cc_wire_codec& c, std::string& s, bool& null) {
   return true;
 }
 
+// java.lang.String.hashCode of the String decoded from UTF-8 bytes: s[0]*31^(n-1) + ... + s[n-1] over its UTF-16
+// code units (a code point above U+FFFF is a surrogate pair; a malformed sequence decodes to U+FFFD, as Java's
+// UTF-8 decoder replaces it).
+int32_t java_string_hash(const std::string& s) {
+  uint32_t h = 0;
+  auto unit = [&](uint32_t u) { h = 31u * h + u; };
+  const uint8_t* p = (const uint8_t*)s.data();
+  const size_t n = s.size();
+  for (size_t i = 0; i < n;) {
+    const uint32_t b = p[i];
+    uint32_t cp = 0xFFFD, len = 1;
+    if (b < 0x80) cp = b;
+    else if ((b >> 5) == 6 && i + 1 < n && (p[i + 1] >> 6) == 2) cp = ((b & 0x1F) << 6) | (p[i + 1] & 0x3F), len = 2;
+    else if ((b >> 4) == 14 && i + 2 < n && (p[i + 1] >> 6) == 2 && (p[i + 2] >> 6) == 2)
+      cp = ((b & 0x0F) << 12) | ((p[i + 1] & 0x3F) << 6) | (p[i + 2] & 0x3F), len = 3;
+    else if ((b >> 3) == 30 && i + 3 < n && (p[i + 1] >> 6) == 2 && (p[i + 2] >> 6) == 2 && (p[i + 3] >> 6) == 2)
+      cp = ((b & 0x07) << 18) | ((p[i + 1] & 0x3F) << 12) | ((p[i + 2] & 0x3F) << 6) | (p[i + 3] & 0x3F), len = 4;
+    if ((len == 2 && cp < 0x80) || (len == 3 && (cp < 0x800 || (cp >= 0xD800 && cp < 0xE000))) ||
+        (len == 4 && (cp < 0x10000 || cp > 0x10FFFF)))
+      cp = 0xFFFD;  // overlong / surrogate / out of range
+    if (cp >= 0x10000) {
+      unit(0xD800 + ((cp - 0x10000) >> 10));
+      unit(0xDC00 + ((cp - 0x10000) & 0x3FF));
+    } else {
+      unit(cp);
+    }
+    i += len;
+  }
+  return (int32_t)h;
+}
+
 uint64_t intern(cc_wire_interner* in, const std::string& s) {
   auto it = in->ids.find(s);
   if (it != in->ids.end()) return it->second;
   const uint64_t h = in->next++;
   in->ids.emplace(s, h);
   in->strs.push_back(s);
+  in->hashes.push_back(java_string_hash(s));
   return h;
 }
 
@@ -372,6 +405,13 @@ extern "C" int cc_wire_intern(cc_wire_interner* in, const uint8_t* bytes, uint64
   return CC_OK;
 }
 
+extern "C" int cc_wire_string_hash(cc_wire_interner* in, uint64_t handle, int32_t* hash) {
+  if (!in || !hash || handle < in->first || handle - in->first >= in->hashes.size())
+    return set_err(CC_ERR_INVALID, "unknown handle");
+  *hash = in->hashes[handle - in->first];
+  return CC_OK;
+}
+
 extern "C" int cc_wire_lookup(cc_wire_interner* in, uint64_t handle, uint8_t* buf, uint64_t cap, uint64_t* len) {
   if (!in || !len || handle < in->first || handle - in->first >= in->strs.size())
     return set_err(CC_ERR_INVALID, "lookup: unknown handle");
@@ -405,6 +445,17 @@ extern "C" int cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_
       if (bad_row) *bad_row = i;
       return rc;
     }
+  }
+  if (e) {  // the String.hashCode of every String key decoded, for the engine's java.util.HashMap model
+    std::vector<uint64_t> hk;
+    std::vector<int32_t> hv;
+    for (uint64_t i = 0; i < n; ++i)
+      if (out->kind[i] == 0 && CC_FLAG_KTAG(out->flags[i]) == 3u && out->key[i] >= in->first &&
+          out->key[i] - in->first < in->hashes.size() && !e->hh.count(out->key[i])) {
+        hk.push_back(out->key[i]);
+        hv.push_back(in->hashes[out->key[i] - in->first]);
+      }
+    if (!hk.empty()) return cc_handle_hashes(e, hk.data(), hv.data(), hk.size());
   }
   return CC_OK;
 }

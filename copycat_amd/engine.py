@@ -99,6 +99,8 @@ def lib():
             "cc_wire_interner_destroy": (i32, [P]),
             "cc_wire_intern": (i32, [P, P, u64, P]),
             "cc_wire_lookup": (i32, [P, u64, P, u64, P]),
+            "cc_wire_string_hash": (i32, [P, u64, P]),
+            "cc_handle_hashes": (i32, [P, P, P, u64]),
             "cc_wire_decode": (i32, [P, P, P, P, u64, P, u64, P, P]),
         }
         for name, (res, args) in sig.items():
@@ -286,6 +288,18 @@ class Engine:
         closed = C.c_uint64()
         _check(self.L.cc_sessions_expire(self.h, _dptr(bitmap), sessions, C.byref(ev), None, C.byref(closed)))
         return closed.value, (evs if events is not None else evs.host())
+
+    def handle_strings(self, strings):
+        """Register the java.lang.String behind each HANDLE key ({handle: str}): its String.hashCode places the key in
+        MapState's java.util.HashMap (containsValue order, treeifyBin resizes; cc_handle_hashes)."""
+        from .batch import java_string_hash
+
+        items = sorted(strings.items())
+        if not items:
+            return
+        hk = np.array([h for h, _ in items], np.uint64)
+        hv = np.array([java_string_hash(x) for _, x in items], np.int32)
+        _check(self.L.cc_handle_hashes(self.h, _np(hk), _np(hv), len(items)))
 
     # ---- the hot path ----------------------------------------------------------------------------------
     def apply(self, db: DeviceBatch, status, value, stream=None):

@@ -301,6 +301,15 @@ int  cc_delete_resource(cc_engine* e, uint64_t resource_id, uint8_t* status);
 int  cc_instance_slot(cc_engine* e, uint64_t instance_id, int64_t* slot);
 int  cc_resource_slot(cc_engine* e, uint64_t resource_id, int64_t* slot);
 
+/* java.lang.String.hashCode of HANDLE keys.  A HANDLE key is a host-interned String (GetResource / DistributedMap keys
+ * are Strings); java.util.HashMap places it by String.hashCode, which the handle alone does not give.  Map resources
+ * need it to answer containsValue in the reference's iteration order (MapState.java:49-60 walks map.values()) and
+ * to follow the table's capacity exactly (HashMap.treeifyBin resizes a table below capacity 64 when one bin reaches 9
+ * keys).  cc_wire_decode registers the Strings it interns itself; a host that interns Strings on its own registers
+ * them here before the batch that uses them (a map operation that needs an unregistered key's hash fails the batch
+ * with CC_ERR_STATE).  Registering a handle again with another hash is CC_ERR_INVALID. */
+int  cc_handle_hashes(cc_engine* e, const uint64_t* h_handles, const int32_t* h_hashes, uint64_t count);
+
 /* ---- the hot path --------------------------------------------------------------------------------
  * Apply n committed entries (device-resident columns) in log order.  Replaces the per-entry chain
  * ResourceManager.operateResource (ResourceManager.java:56-72) -> executors -> state machine method.
@@ -478,6 +487,8 @@ int  cc_wire_interner_create(uint64_t first_handle, cc_wire_interner** out);
 int  cc_wire_interner_destroy(cc_wire_interner* in);
 int  cc_wire_intern(cc_wire_interner* in, const uint8_t* bytes, uint64_t len, uint64_t* handle);
 int  cc_wire_lookup(cc_wire_interner* in, uint64_t handle, uint8_t* buf, uint64_t cap, uint64_t* len);
+/* java.lang.String.hashCode of an interned String (its UTF-8 bytes decoded to UTF-16 code units). */
+int  cc_wire_string_hash(cc_wire_interner* in, uint64_t handle, int32_t* hash);
 /* decoded rows (host memory, n each).  kind 0: a resource operation (inst = the instance slot of the instance
  * id through the engine's session registry, max_instances when unknown -> CC_ST_UNKNOWN_SESSION when applied;
  * iid = the instance id itself; op/flags/key/a/b/aux as cc_batch).  With e == NULL (no engine: host-only

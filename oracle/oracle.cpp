@@ -33,32 +33,504 @@ inline uint8_t ktag_to_tag(uint8_t k) {
   return m[k & 3];
 }
 
-// ---- java.util.HashMap iteration order (for outputs that depend on it) -----------------------------
-// Order = (bucket index under the current table capacity, insertion order within the bucket).  The
-// table starts at 16, doubles when ++size > 0.75*cap (HashMap.putVal/resize), never shrinks; a resize
-// splits each bucket preserving relative order; re-putting an existing key keeps its node.  Tree bins
-// (>= 8 colliding keys) are not modelled.  hashCode: Long (int)(v^(v>>>32)); Integer v; Boolean
-// 1231/1237; HANDLE keys use the Long formula on the handle (documented assumption).
-inline uint32_t java_hash(uint8_t tag, uint64_t v) {
-  int32_t h;
+struct MapKey {
+  uint8_t tag;
+  uint64_t k;
+  bool operator==(const MapKey& o) const { return tag == o.tag && k == o.k; }
+};
+struct MapKeyHash {
+  size_t operator()(const MapKey& x) const { return (size_t)(x.k * 0x9E3779B97F4A7C15ull) ^ x.tag; }
+};
+// ---- java.util.HashMap, JDK 8 (the reference's CI JDK, .travis.yml: oraclejdk8) -------------------------------
+// java.util.HashMap is not in /root/reference (a JDK class).  Its published JDK 8 algorithm is restated here for the
+// outputs that depend on iteration order (MapState.containsValue :49-60 walks map.values(); ResourceManager.close
+// :250-264 walks sessions.values()): the bins, each bin's `next` chain, and the red-black tree bins --
+//   hash(key) = h ^ (h >>> 16), h = key.hashCode()  (Long: (int)(v ^ (v >>> 32)); Integer: v; Boolean: 1231 / 1237;
+//     String: s[0]*31^(n-1) + ... over its UTF-16 units -- a HANDLE key is a String registered with orc_handle_string);
+//   putVal: a new key is appended to its bin's chain; when the chain it joined then holds >= 9 nodes
+//     (binCount >= TREEIFY_THRESHOLD - 1), treeifyBin: capacity < 64 (MIN_TREEIFY_CAPACITY) -> resize(), else the
+//     bin becomes a tree (treeify, root moved to the front); a tree bin takes a new key through putTreeVal (linked
+//     after its tree parent in the chain, root moved to the front); then ++size > threshold -> resize();
+//   resize: capacity 16 (threshold 12) at the first put, then doubled; chains split into lo / hi keeping their order;
+//     tree bins split the same way and untreeify at <= 6 nodes (UNTREEIFY_THRESHOLD) or are re-treeified;
+//   removeNode(movable = true): chains unlink; tree bins unlink from the chain, untreeify when the tree is too small
+//     (root.right / root.left / root.left.left null), else the red-black delete, root moved to the front;
+//   iteration: bins in index order, each along `next`.
+// Tree order: hash (signed int compare), then compareTo for keys of one class, else the class names (tieBreakOrder:
+// java.lang.Boolean < Integer < Long < String).  Distinct keys of one class never compare equal, so
+// System.identityHashCode is never reached.
+struct JCtx {  // String contents of HANDLE keys (handle -> UTF-16 units), registered by the test harness
+  std::unordered_map<uint64_t, std::vector<uint16_t>> str;
+};
+inline int32_t java_hashcode(const JCtx& cx, uint8_t tag, uint64_t v) {
   switch (tag) {
-    case CC_TAG_INT: h = (int32_t)(uint32_t)v; break;
-    case CC_TAG_BOOL: h = v ? 1231 : 1237; break;
-    default: h = (int32_t)(uint32_t)(v ^ (v >> 32)); break;
+    case CC_TAG_INT: return (int32_t)(uint32_t)v;
+    case CC_TAG_BOOL: return v ? 1231 : 1237;
+    case CC_TAG_HANDLE: {
+      auto it = cx.str.find(v);
+      if (it != cx.str.end()) {
+        uint32_t h = 0;  // String.hashCode
+        for (uint16_t u : it->second) h = 31u * h + u;
+        return (int32_t)h;
+      }
+      break;  // an unregistered handle: hashed as a Long (the engine refuses to guess: CC_ERR_STATE)
+    }
+    default: break;
   }
-  uint32_t u = (uint32_t)h;
-  return u ^ (u >> 16);
+  return (int32_t)(uint32_t)(v ^ (v >> 32));
 }
-struct JavaOrder {
-  uint32_t cap = 16, thr = 12, size = 0;
-  uint64_t next_seq = 0;
-  uint64_t on_insert() {  // a NEW key
-    uint64_t s = next_seq++;
-    if (++size > thr) { cap <<= 1; thr <<= 1; }
-    return s;
+inline uint32_t java_spread(int32_t h) { return (uint32_t)h ^ ((uint32_t)h >> 16); }
+inline uint32_t java_hash(const JCtx& cx, uint8_t tag, uint64_t v) { return java_spread(java_hashcode(cx, tag, v)); }
+
+struct JHM {
+  static constexpr int kNil = -1;
+  struct Node {
+    uint32_t hash = 0;
+    MapKey key{};
+    int next = kNil, prev = kNil, parent = kNil, left = kNil, right = kNil;
+    bool tree = false, red = false;
+  };
+  std::vector<Node> nd;
+  std::vector<int> free_;
+  std::vector<int> tab;  // empty until the first put (HashMap() allocates lazily)
+  uint32_t size = 0, threshold = 0;
+  std::unordered_map<MapKey, int, MapKeyHash> where;  // key -> node (a lookup shortcut; order lives in nd / tab)
+
+  uint32_t capacity() const { return (uint32_t)tab.size(); }
+  static int cls_rank(uint8_t tag) {  // getClass().getName() order
+    return tag == CC_TAG_BOOL ? 0 : tag == CC_TAG_INT ? 1 : tag == CC_TAG_LONG ? 2 : 3;
   }
-  void on_remove() { --size; }
-  uint64_t order_key(uint32_t hash, uint64_t seq) const { return ((uint64_t)(hash & (cap - 1)) << 40) | seq; }
+  // dir of key k (hash h) against node p, as treeify / putTreeVal compute it for a key not in the tree
+  static int dir_of(const JCtx& cx, uint32_t h, const MapKey& k, const Node& p) {
+    const int32_t ph = (int32_t)p.hash, hh = (int32_t)h;
+    if (ph > hh) return -1;
+    if (ph < hh) return 1;
+    const MapKey& pk = p.key;
+    if (k.tag == pk.tag) {  // compareComparables: same class
+      int c = 0;
+      switch (k.tag) {
+        case CC_TAG_LONG: c = (int64_t)k.k < (int64_t)pk.k ? -1 : ((int64_t)k.k > (int64_t)pk.k ? 1 : 0); break;
+        case CC_TAG_INT: c = (int32_t)k.k < (int32_t)pk.k ? -1 : ((int32_t)k.k > (int32_t)pk.k ? 1 : 0); break;
+        case CC_TAG_BOOL: c = (k.k != 0) == (pk.k != 0) ? 0 : (k.k ? 1 : -1); break;
+        default: {  // String.compareTo (unregistered handles: by handle number)
+          auto a = cx.str.find(k.k), b = cx.str.find(pk.k);
+          if (a != cx.str.end() && b != cx.str.end()) {
+            const auto &x = a->second, &y = b->second;
+            const size_t n = std::min(x.size(), y.size());
+            for (size_t i = 0; i < n && !c; ++i) c = x[i] < y[i] ? -1 : (x[i] > y[i] ? 1 : 0);
+            if (!c) c = x.size() < y.size() ? -1 : (x.size() > y.size() ? 1 : 0);
+          } else {
+            c = k.k < pk.k ? -1 : (k.k > pk.k ? 1 : 0);
+          }
+        }
+      }
+      if (c) return c;
+    }
+    // tieBreakOrder: class names (equal keys of one class never get here)
+    return cls_rank(k.tag) <= cls_rank(pk.tag) ? -1 : 1;
+  }
+
+  int new_node(uint32_t h, const MapKey& k) {
+    int x;
+    if (!free_.empty()) { x = free_.back(); free_.pop_back(); nd[x] = Node(); }
+    else { x = (int)nd.size(); nd.emplace_back(); }
+    nd[x].hash = h;
+    nd[x].key = k;
+    return x;
+  }
+
+  // ---- red-black tree bins (HashMap.TreeNode) ----
+  int rotate_left(int root, int p) {
+    int r, pp, rl;
+    if (p != kNil && (r = nd[p].right) != kNil) {
+      if ((rl = nd[p].right = nd[r].left) != kNil) nd[rl].parent = p;
+      if ((pp = nd[r].parent = nd[p].parent) == kNil) { root = r; nd[r].red = false; }
+      else if (nd[pp].left == p) nd[pp].left = r;
+      else nd[pp].right = r;
+      nd[r].left = p;
+      nd[p].parent = r;
+    }
+    return root;
+  }
+  int rotate_right(int root, int p) {
+    int l, pp, lr;
+    if (p != kNil && (l = nd[p].left) != kNil) {
+      if ((lr = nd[p].left = nd[l].right) != kNil) nd[lr].parent = p;
+      if ((pp = nd[l].parent = nd[p].parent) == kNil) { root = l; nd[l].red = false; }
+      else if (nd[pp].right == p) nd[pp].right = l;
+      else nd[pp].left = l;
+      nd[l].right = p;
+      nd[p].parent = l;
+    }
+    return root;
+  }
+  int balance_insertion(int root, int x) {
+    nd[x].red = true;
+    for (int xp, xpp, xppl, xppr;;) {
+      if ((xp = nd[x].parent) == kNil) { nd[x].red = false; return x; }
+      else if (!nd[xp].red || (xpp = nd[xp].parent) == kNil) return root;
+      if (xp == (xppl = nd[xpp].left)) {
+        if ((xppr = nd[xpp].right) != kNil && nd[xppr].red) {
+          nd[xppr].red = false; nd[xp].red = false; nd[xpp].red = true; x = xpp;
+        } else {
+          if (x == nd[xp].right) {
+            root = rotate_left(root, x = xp);
+            xpp = (xp = nd[x].parent) == kNil ? kNil : nd[xp].parent;
+          }
+          if (xp != kNil) {
+            nd[xp].red = false;
+            if (xpp != kNil) { nd[xpp].red = true; root = rotate_right(root, xpp); }
+          }
+        }
+      } else {
+        if (xppl != kNil && nd[xppl].red) {
+          nd[xppl].red = false; nd[xp].red = false; nd[xpp].red = true; x = xpp;
+        } else {
+          if (x == nd[xp].left) {
+            root = rotate_right(root, x = xp);
+            xpp = (xp = nd[x].parent) == kNil ? kNil : nd[xp].parent;
+          }
+          if (xp != kNil) {
+            nd[xp].red = false;
+            if (xpp != kNil) { nd[xpp].red = true; root = rotate_left(root, xpp); }
+          }
+        }
+      }
+    }
+  }
+  int balance_deletion(int root, int x) {
+    for (int xp, xpl, xpr;;) {
+      if (x == kNil || x == root) return root;
+      else if ((xp = nd[x].parent) == kNil) { nd[x].red = false; return x; }
+      else if (nd[x].red) { nd[x].red = false; return root; }
+      else if ((xpl = nd[xp].left) == x) {
+        if ((xpr = nd[xp].right) != kNil && nd[xpr].red) {
+          nd[xpr].red = false; nd[xp].red = true;
+          root = rotate_left(root, xp);
+          xpr = (xp = nd[x].parent) == kNil ? kNil : nd[xp].right;
+        }
+        if (xpr == kNil) x = xp;
+        else {
+          int sl = nd[xpr].left, sr = nd[xpr].right;
+          if ((sr == kNil || !nd[sr].red) && (sl == kNil || !nd[sl].red)) {
+            nd[xpr].red = true; x = xp;
+          } else {
+            if (sr == kNil || !nd[sr].red) {
+              if (sl != kNil) nd[sl].red = false;
+              nd[xpr].red = true;
+              root = rotate_right(root, xpr);
+              xpr = (xp = nd[x].parent) == kNil ? kNil : nd[xp].right;
+            }
+            if (xpr != kNil) {
+              nd[xpr].red = (xp == kNil) ? false : nd[xp].red;
+              if ((sr = nd[xpr].right) != kNil) nd[sr].red = false;
+            }
+            if (xp != kNil) { nd[xp].red = false; root = rotate_left(root, xp); }
+            x = root;
+          }
+        }
+      } else {  // symmetric
+        if (xpl != kNil && nd[xpl].red) {
+          nd[xpl].red = false; nd[xp].red = true;
+          root = rotate_right(root, xp);
+          xpl = (xp = nd[x].parent) == kNil ? kNil : nd[xp].left;
+        }
+        if (xpl == kNil) x = xp;
+        else {
+          int sl = nd[xpl].left, sr = nd[xpl].right;
+          if ((sl == kNil || !nd[sl].red) && (sr == kNil || !nd[sr].red)) {
+            nd[xpl].red = true; x = xp;
+          } else {
+            if (sl == kNil || !nd[sl].red) {
+              if (sr != kNil) nd[sr].red = false;
+              nd[xpl].red = true;
+              root = rotate_left(root, xpl);
+              xpl = (xp = nd[x].parent) == kNil ? kNil : nd[xp].left;
+            }
+            if (xpl != kNil) {
+              nd[xpl].red = (xp == kNil) ? false : nd[xp].red;
+              if ((sl = nd[xpl].left) != kNil) nd[sl].red = false;
+            }
+            if (xp != kNil) { nd[xp].red = false; root = rotate_right(root, xp); }
+            x = root;
+          }
+        }
+      }
+    }
+  }
+  void move_root_to_front(int root) {
+    if (root == kNil || tab.empty()) return;
+    const uint32_t index = (capacity() - 1) & nd[root].hash;
+    const int first = tab[index];
+    if (root != first) {
+      int rn;
+      tab[index] = root;
+      const int rp = nd[root].prev;
+      if ((rn = nd[root].next) != kNil) nd[rn].prev = rp;
+      if (rp != kNil) nd[rp].next = rn;
+      if (first != kNil) nd[first].prev = root;
+      nd[root].next = first;
+      nd[root].prev = kNil;
+    }
+  }
+  int root_of(int p) const {
+    while (nd[p].parent != kNil) p = nd[p].parent;
+    return p;
+  }
+  // TreeNode.treeify from chain head `hd` (every node already a tree node, linked by next / prev)
+  void treeify(const JCtx& cx, int hd) {
+    int root = kNil;
+    for (int x = hd, next; x != kNil; x = next) {
+      next = nd[x].next;
+      nd[x].left = nd[x].right = kNil;
+      if (root == kNil) {
+        nd[x].parent = kNil;
+        nd[x].red = false;
+        root = x;
+      } else {
+        for (int p = root;;) {
+          const int dir = dir_of(cx, nd[x].hash, nd[x].key, nd[p]);
+          const int xp = p;
+          if ((p = (dir <= 0) ? nd[p].left : nd[p].right) == kNil) {
+            nd[x].parent = xp;
+            if (dir <= 0) nd[xp].left = x;
+            else nd[xp].right = x;
+            root = balance_insertion(root, x);
+            break;
+          }
+        }
+      }
+    }
+    move_root_to_front(root);
+  }
+  // TreeNode.untreeify: plain nodes, same chain order
+  int untreeify(int hd) {
+    for (int q = hd; q != kNil; q = nd[q].next) {
+      nd[q].tree = false;
+      nd[q].red = false;
+      nd[q].parent = nd[q].left = nd[q].right = nd[q].prev = kNil;
+    }
+    return hd;
+  }
+  void treeify_bin(const JCtx& cx, uint32_t h) {
+    const uint32_t n = capacity();
+    if (n < 64) {  // MIN_TREEIFY_CAPACITY
+      resize(cx);
+      return;
+    }
+    const uint32_t index = (n - 1) & h;
+    int e = tab[index];
+    if (e == kNil) return;
+    int tl = kNil;
+    for (; e != kNil; e = nd[e].next) {  // replacementTreeNode: chain order kept, prev links added
+      nd[e].tree = true;
+      nd[e].prev = tl;
+      tl = e;
+    }
+    treeify(cx, tab[index]);
+  }
+  // TreeNode.split on resize
+  void split(const JCtx& cx, std::vector<int>& ntab, int b, uint32_t index, uint32_t bit) {
+    int loHead = kNil, loTail = kNil, hiHead = kNil, hiTail = kNil;
+    int lc = 0, hc = 0;
+    for (int e = b, next; e != kNil; e = next) {
+      next = nd[e].next;
+      nd[e].next = kNil;
+      if ((nd[e].hash & bit) == 0) {
+        if ((nd[e].prev = loTail) == kNil) loHead = e;
+        else nd[loTail].next = e;
+        loTail = e;
+        ++lc;
+      } else {
+        if ((nd[e].prev = hiTail) == kNil) hiHead = e;
+        else nd[hiTail].next = e;
+        hiTail = e;
+        ++hc;
+      }
+    }
+    std::vector<int> saved;
+    saved.swap(tab);  // treeify / moveRootToFront work on the NEW table
+    tab.swap(ntab);
+    if (loHead != kNil) {
+      if (lc <= 6) tab[index] = untreeify(loHead);
+      else {
+        tab[index] = loHead;
+        if (hiHead != kNil) treeify(cx, loHead);
+      }
+    }
+    if (hiHead != kNil) {
+      if (hc <= 6) tab[index + bit] = untreeify(hiHead);
+      else {
+        tab[index + bit] = hiHead;
+        if (loHead != kNil) treeify(cx, hiHead);
+      }
+    }
+    tab.swap(ntab);
+    saved.swap(tab);
+  }
+  void resize(const JCtx& cx) {
+    const uint32_t oldCap = capacity();
+    uint32_t newCap, newThr;
+    if (oldCap > 0) { newCap = oldCap << 1; newThr = threshold << 1; }
+    else { newCap = 16; newThr = 12; }
+    threshold = newThr;
+    std::vector<int> ntab(newCap, kNil);
+    for (uint32_t j = 0; j < oldCap; ++j) {
+      const int e = tab[j];
+      if (e == kNil) continue;
+      if (nd[e].next == kNil) ntab[nd[e].hash & (newCap - 1)] = e;
+      else if (nd[e].tree) split(cx, ntab, e, j, oldCap);
+      else {  // preserve order
+        int loHead = kNil, loTail = kNil, hiHead = kNil, hiTail = kNil;
+        for (int q = e, next; q != kNil; q = next) {
+          next = nd[q].next;
+          if ((nd[q].hash & oldCap) == 0) {
+            if (loTail == kNil) loHead = q; else nd[loTail].next = q;
+            loTail = q;
+          } else {
+            if (hiTail == kNil) hiHead = q; else nd[hiTail].next = q;
+            hiTail = q;
+          }
+        }
+        if (loTail != kNil) { nd[loTail].next = kNil; ntab[j] = loHead; }
+        if (hiTail != kNil) { nd[hiTail].next = kNil; ntab[j + oldCap] = hiHead; }
+      }
+    }
+    tab.swap(ntab);
+  }
+  // putVal for a key NOT in the map (an existing key's put changes no structure)
+  void put_new(const JCtx& cx, const MapKey& k) {
+    if (where.count(k)) return;
+    const uint32_t h = java_hash(cx, k.tag, k.k);
+    if (tab.empty()) resize(cx);
+    const uint32_t i = (capacity() - 1) & h;
+    int p = tab[i];
+    if (p == kNil) {
+      tab[i] = where[k] = new_node(h, k);
+    } else if (nd[p].tree) {  // putTreeVal
+      const int root = nd[p].parent != kNil ? root_of(p) : p;
+      for (int q = root;;) {
+        const int dir = dir_of(cx, h, k, nd[q]);
+        const int xp = q;
+        if ((q = (dir <= 0) ? nd[q].left : nd[q].right) == kNil) {
+          const int xpn = nd[xp].next;
+          const int x = new_node(h, k);
+          where[k] = x;
+          nd[x].tree = true;
+          nd[x].next = xpn;
+          if (dir <= 0) nd[xp].left = x; else nd[xp].right = x;
+          nd[xp].next = x;
+          nd[x].parent = nd[x].prev = xp;
+          if (xpn != kNil) nd[xpn].prev = x;
+          move_root_to_front(balance_insertion(root, x));
+          break;
+        }
+      }
+    } else {
+      int binCount = 0;
+      while (nd[p].next != kNil) { p = nd[p].next; ++binCount; }
+      const int x = new_node(h, k);
+      where[k] = x;
+      nd[p].next = x;
+      if (binCount >= 7) treeify_bin(cx, h);  // TREEIFY_THRESHOLD - 1: the chain now holds >= 9 nodes
+    }
+    if (++size > threshold) resize(cx);
+  }
+  // removeNode(hash, key, null, false, movable = true) for a key in the map
+  void remove(const JCtx& cx, const MapKey& k) {
+    auto it = where.find(k);
+    if (it == where.end()) return;
+    const int node = it->second;
+    where.erase(it);
+    const uint32_t n = capacity();
+    const uint32_t index = (n - 1) & nd[node].hash;
+    if (nd[node].tree) {
+      remove_tree_node(node, index);
+    } else {
+      int p = tab[index];
+      if (p == node) tab[index] = nd[node].next;
+      else {
+        while (nd[p].next != node) p = nd[p].next;
+        nd[p].next = nd[node].next;
+      }
+    }
+    --size;
+    free_.push_back(node);
+  }
+  void remove_tree_node(int self, uint32_t index) {  // TreeNode.removeTreeNode(map, tab, movable = true)
+    int first = tab[index], root = first, rl;
+    const int succ = nd[self].next, pred = nd[self].prev;
+    if (pred == kNil) tab[index] = first = succ;
+    else nd[pred].next = succ;
+    if (succ != kNil) nd[succ].prev = pred;
+    if (first == kNil) return;
+    if (nd[root].parent != kNil) root = root_of(root);
+    if (root == kNil || nd[root].right == kNil || (rl = nd[root].left) == kNil || nd[rl].left == kNil) {
+      tab[index] = untreeify(first);  // too small
+      return;
+    }
+    int p = self, pl = nd[self].left, pr = nd[self].right, replacement;
+    if (pl != kNil && pr != kNil) {
+      int s = pr, sl;
+      while ((sl = nd[s].left) != kNil) s = sl;  // successor
+      const bool c = nd[s].red;
+      nd[s].red = nd[p].red;
+      nd[p].red = c;  // swap colors
+      const int sr = nd[s].right;
+      const int pp = nd[p].parent;
+      if (s == pr) {  // p was s's direct parent
+        nd[p].parent = s;
+        nd[s].right = p;
+      } else {
+        const int sp = nd[s].parent;
+        if ((nd[p].parent = sp) != kNil) {
+          if (s == nd[sp].left) nd[sp].left = p;
+          else nd[sp].right = p;
+        }
+        if ((nd[s].right = pr) != kNil) nd[pr].parent = s;
+      }
+      nd[p].left = kNil;
+      if ((nd[p].right = sr) != kNil) nd[sr].parent = p;
+      if ((nd[s].left = pl) != kNil) nd[pl].parent = s;
+      if ((nd[s].parent = pp) == kNil) root = s;
+      else if (p == nd[pp].left) nd[pp].left = s;
+      else nd[pp].right = s;
+      replacement = sr != kNil ? sr : p;
+    } else if (pl != kNil) replacement = pl;
+    else if (pr != kNil) replacement = pr;
+    else replacement = p;
+    if (replacement != p) {
+      const int pp = nd[replacement].parent = nd[p].parent;
+      if (pp == kNil) root = replacement;
+      else if (p == nd[pp].left) nd[pp].left = replacement;
+      else nd[pp].right = replacement;
+      nd[p].left = nd[p].right = nd[p].parent = kNil;
+    }
+    const int r = nd[p].red ? root : balance_deletion(root, replacement);
+    if (replacement == p) {  // detach
+      const int pp = nd[p].parent;
+      nd[p].parent = kNil;
+      if (pp != kNil) {
+        if (p == nd[pp].left) nd[pp].left = kNil;
+        else if (p == nd[pp].right) nd[pp].right = kNil;
+      }
+    }
+    move_root_to_front(r);
+  }
+  // MapState.delete (iterator.remove() on every entry): every bin empties, the table keeps its capacity
+  void clear() {
+    std::fill(tab.begin(), tab.end(), kNil);
+    nd.clear();
+    free_.clear();
+    where.clear();
+    size = 0;
+  }
+  // map.values() / keySet() iteration order
+  template <class F>
+  void for_each(F f) const {
+    for (int b : tab)
+      for (int q = b; q != kNil; q = nd[q].next) f(nd[q].key);
+  }
 };
 
 struct Commit {  // a retained commit: index + instance-session slot
@@ -75,24 +547,15 @@ struct ValueSM {
   std::vector<std::pair<uint32_t, uint64_t>> listeners;  // (instance slot, listen index); insertion order
 };
 
-struct MapKey {
-  uint8_t tag;
-  uint64_t k;
-  bool operator==(const MapKey& o) const { return tag == o.tag && k == o.k; }
-};
-struct MapKeyHash {
-  size_t operator()(const MapKey& x) const { return (size_t)(x.k * 0x9E3779B97F4A7C15ull) ^ x.tag; }
-};
 // MapState.Value{commit, timer} MapState.java:279-287
 struct MapEntry {
   TV value;
   uint64_t commit_index = 0;
   uint64_t timer = 0;  // 0 = none
-  uint64_t seq = 0;    // Java HashMap insertion order
 };
 struct MapSM {
   std::unordered_map<MapKey, MapEntry, MapKeyHash> m;
-  JavaOrder order;
+  JHM order;  // the java.util.HashMap structure (iteration order)
 };
 
 // LockState.java:33-36
@@ -174,8 +637,8 @@ struct orc {
   std::vector<Resource> res;
   std::vector<Inst> inst;
   std::unordered_map<uint64_t, uint32_t> inst_by_id;  // ResourceManager.sessions key -> slot
-  JavaOrder sessions_order;                            // HashMap order of ResourceManager.sessions
-  std::unordered_map<uint64_t, uint64_t> inst_seq;     // instance id -> insertion seq
+  JHM sessions_order;                                  // ResourceManager.sessions (HashMap<Long, ...>) structure
+  JCtx cx;                                             // String contents of HANDLE keys (java hashCode / compareTo)
   std::unordered_map<uint64_t, uint64_t> keys;         // ResourceManager.keys: key -> resource id
   std::unordered_map<uint64_t, uint32_t> res_by_id;    // ResourceManager.resources: id -> slot
   std::map<std::pair<uint64_t, uint64_t>, Timer> timers;  // (deadline, id) -> timer
@@ -224,7 +687,7 @@ struct orc {
       case T_MAP_TTL:          // MapState.java:91-93,119-121,218-220: map.remove(key).commit.clean()
       case T_MAP_REPLACE_TTL: {  // MapState.java:189-192: map.remove(key); commit.clean()
         auto it = r.m.m.find(t.key);
-        if (it != r.m.m.end()) { r.m.m.erase(it); r.m.order.on_remove(); }
+        if (it != r.m.m.end()) { r.m.m.erase(it); r.m.order.remove(cx, t.key); }
         break;
       }
       case T_LOCK_TIMEOUT: {   // LockState.java:54-58 (silent, A7)
@@ -251,15 +714,14 @@ struct orc {
     Inst& in = inst[slot];
     in.open = true; in.res = rslot; in.id = id; in.client = client;
     inst_by_id[id] = slot;
-    inst_seq[id] = sessions_order.on_insert();
+    sessions_order.put_new(cx, MapKey{CC_TAG_LONG, id});
   }
   void unregister_instance(uint32_t slot) {
     Inst& in = inst[slot];
     if (!in.open) return;
     in.open = false;
     inst_by_id.erase(in.id);
-    inst_seq.erase(in.id);
-    sessions_order.on_remove();
+    sessions_order.remove(cx, MapKey{CC_TAG_LONG, in.id});
   }
   int alloc_res_slot() {
     for (uint32_t s = 0; s < max_res; ++s) if (!res[s].exists && !res[s].zombie) return (int)s;
@@ -293,7 +755,7 @@ struct orc {
       case CC_RES_SET:  // SetState.delete :123-134 (same shape: cancel timers, clean, clear)
       case CC_RES_MAP: {  // MapState.delete :264-274
         for (auto& kv : r.m.m) if (kv.second.timer) cancel(kv.second.timer);
-        for (size_t i = 0; i < r.m.m.size(); ++i) r.m.order.on_remove();
+        r.m.order.clear();
         r.m.m.clear();
         return CC_ST_OK;
       }
@@ -460,16 +922,14 @@ struct orc {
             return;
           case CC_OP_MAP_CONTAINSVALUE: {  // containsValue :49-60 — iterates in HashMap order; a stored
             // null value NPEs on `.equals` before a later match is reached (A5).
-            std::vector<std::pair<uint64_t, const MapEntry*>> ord;
-            ord.reserve(s.m.size());
-            for (auto& kv : s.m)
-              ord.emplace_back(s.order.order_key(java_hash(kv.first.tag, kv.first.k), kv.second.seq), &kv.second);
-            std::sort(ord.begin(), ord.end(), [](const std::pair<uint64_t, const MapEntry*>& x,
-                                                 const std::pair<uint64_t, const MapEntry*>& y) { return x.first < y.first; });
-            for (auto& p : ord) {
-              if (tv_null(p.second->value)) { ret(CC_ST_NULL_POINTER, TV()); return; }
-              if (tv_equals(p.second->value, a)) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 1)); return; }
-            }
+            bool done = false;
+            s.order.for_each([&](const MapKey& key) {
+              if (done) return;
+              const MapEntry& e = s.m.at(key);
+              if (tv_null(e.value)) { ret(CC_ST_NULL_POINTER, TV()); done = true; }
+              else if (tv_equals(e.value, a)) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 1)); done = true; }
+            });
+            if (done) return;
             ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
             return;
           }
@@ -493,7 +953,7 @@ struct orc {
               it->second.value = a; it->second.commit_index = c.index; it->second.timer = timer;
               ret(CC_ST_OK, prev);
             } else {
-              MapEntry e; e.value = a; e.commit_index = c.index; e.timer = timer; e.seq = s.order.on_insert();
+              MapEntry e; e.value = a; e.commit_index = c.index; e.timer = timer; s.order.put_new(cx, k);
               s.m.emplace(k, e);
               ret(CC_ST_OK, TV());
             }
@@ -504,7 +964,7 @@ struct orc {
             if (it == s.m.end()) {
               uint64_t timer = 0;
               if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
-              MapEntry e; e.value = a; e.commit_index = c.index; e.timer = timer; e.seq = s.order.on_insert();
+              MapEntry e; e.value = a; e.commit_index = c.index; e.timer = timer; s.order.put_new(cx, k);
               s.m.emplace(k, e);
               ret(CC_ST_OK, TV());
             } else {
@@ -517,7 +977,7 @@ struct orc {
             if (it != s.m.end()) {
               if (it->second.timer) cancel(it->second.timer);
               TV prev = it->second.value;
-              s.m.erase(it); s.order.on_remove();
+              s.m.erase(it); s.order.remove(cx, k);
               ret(CC_ST_OK, prev);
             } else {
               ret(CC_ST_OK, TV());
@@ -530,7 +990,7 @@ struct orc {
                         (!tv_null(it->second.value) && !tv_equals(it->second.value, a));
             if (fail) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 0)); return; }
             if (it->second.timer) cancel(it->second.timer);
-            s.m.erase(it); s.order.on_remove();
+            s.m.erase(it); s.order.remove(cx, k);
             ret(CC_ST_OK, tv(CC_TAG_BOOL, 1));
             return;
           }
@@ -651,7 +1111,7 @@ struct orc {
             if (!s.m.count(k)) {
               uint64_t timer = 0;
               if (ttl > 0) { Timer t; t.res = in.res; t.kind = T_MAP_TTL; t.key = k; t.commit_index = c.index; timer = schedule((uint64_t)ttl, t); }
-              MapEntry e; e.value = tv(CC_TAG_BOOL, 1); e.commit_index = c.index; e.timer = timer; e.seq = s.order.on_insert();
+              MapEntry e; e.value = tv(CC_TAG_BOOL, 1); e.commit_index = c.index; e.timer = timer; s.order.put_new(cx, k);
               s.m.emplace(k, e);
             }
             ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
@@ -661,7 +1121,7 @@ struct orc {
             auto it = s.m.find(k);
             if (it == s.m.end()) { ret(CC_ST_OK, tv(CC_TAG_BOOL, 0)); return; }
             if (it->second.timer) cancel(it->second.timer);
-            s.m.erase(it); s.order.on_remove();
+            s.m.erase(it); s.order.remove(cx, k);
             ret(CC_ST_OK, tv(CC_TAG_BOOL, 1));
             return;
           }
@@ -695,7 +1155,7 @@ struct orc {
             // a ttl > 0 schedules keyValues.remove(value).clean(), which throws (remove returns null) and changes
             // nothing (A18)
             if (!s.m.count(k)) {
-              MapEntry e; e.value = tv(CC_TAG_BOOL, 1); e.commit_index = c.index; e.seq = s.order.on_insert();
+              MapEntry e; e.value = tv(CC_TAG_BOOL, 1); e.commit_index = c.index; s.order.put_new(cx, k);
               s.m.emplace(k, e);
             }
             r.leaked.push_back(c.index);
@@ -707,7 +1167,7 @@ struct orc {
               ret(CC_ST_OK, tv(CC_TAG_BOOL, 0));
               return;
             }
-            if (s.m.erase(k)) s.order.on_remove();  // map.remove(key): its (empty) values as a collection
+            if (s.m.erase(k)) s.order.remove(cx, k);  // map.remove(key): its (empty) values as a collection
             ret(CC_ST_OK, tv(CC_TAG_LIST, 0));
             return;
           case CC_OP_MMAP_REMOVEVALUE:  // removeValue :140-165 — no entry matches; every (empty) value map goes
@@ -1019,6 +1479,12 @@ int orc_apply(orc* o, const cc_batch* cols, uint64_t n, uint8_t* status, uint64_
   return CC_OK;
 }
 
+// A HANDLE key's String (UTF-16 units): its java hashCode and compareTo (java.util.HashMap bins and tree bins).
+int orc_handle_string(orc* o, uint64_t handle, const uint16_t* units, uint64_t n) {
+  o->cx.str[handle] = std::vector<uint16_t>(units, units + n);
+  return CC_OK;
+}
+
 int orc_advance_time(orc* o, uint64_t now) {
   if (now > o->clock) o->clock = now;
   o->cur_pos = UINT32_MAX;
@@ -1028,13 +1494,11 @@ int orc_advance_time(orc* o, uint64_t now) {
 
 // ResourceManager.close :250-264 — iterates ResourceManager.sessions in HashMap order
 int orc_session_close(orc* o, uint64_t client) {
-  std::vector<std::pair<uint64_t, uint32_t>> ord;
-  for (auto& kv : o->inst_by_id) {
-    const Inst& in = o->inst[kv.second];
-    if (in.client == client)
-      ord.emplace_back(o->sessions_order.order_key(java_hash(CC_TAG_LONG, kv.first), o->inst_seq[kv.first]), kv.second);
-  }
-  std::sort(ord.begin(), ord.end());
+  std::vector<std::pair<uint64_t, uint32_t>> ord;  // sessions.values() in HashMap iteration order
+  o->sessions_order.for_each([&](const MapKey& id) {
+    const uint32_t slot = o->inst_by_id.at(id.k);
+    if (o->inst[slot].client == client) ord.emplace_back(ord.size(), slot);
+  });
   uint8_t saved = o->cur_src;
   o->cur_src = CC_EVSRC_CLOSE;
   o->cur_pos = UINT32_MAX;

@@ -58,6 +58,9 @@ int  orc_res_slot_of(orc* o, uint64_t resource_id);  /* -1 if unknown */
 int  orc_apply(orc* o, const cc_batch* cols, uint64_t n, uint8_t* status, uint64_t* value);
 /* advance the deterministic clock (keep-alive ticks between batches) and fire due timers */
 int  orc_advance_time(orc* o, uint64_t now);
+/* The String behind a HANDLE key (UTF-16 code units): its hashCode / compareTo place it in java.util.HashMap's bins
+ * and tree bins (containsValue order).  Unregistered handles hash like a Long of the handle. */
+int  orc_handle_string(orc* o, uint64_t handle, const uint16_t* units, uint64_t n);
 /* ResourceManager.close / expire (ResourceManager.java:237-264) for a client session */
 int  orc_session_close(orc* o, uint64_t client_session);
 int  orc_session_expire(orc* o, uint64_t client_session);

@@ -46,6 +46,7 @@ def lib():
             "orc_res_slot_of": (i32, [P, u64]),
             "orc_apply": (i32, [P, P, u64, P, P]),
             "orc_advance_time": (i32, [P, u64]),
+            "orc_handle_string": (i32, [P, u64, P, u64]),
             "orc_session_close": (i32, [P, u64]),
             "orc_session_expire": (i32, [P, u64]),
             "orc_applied_index": (u64, [P]),
@@ -150,6 +151,11 @@ class Oracle:
         rc = self.L.orc_apply(self.h, C.byref(s), n, _p(status), _p(value))
         assert rc == 0, rc
         return status, value
+
+    def handle_string(self, handle, s):
+        """Register the java.lang.String behind HANDLE `handle` (its hashCode / compareTo order the HashMap bins)."""
+        u = np.frombuffer(s.encode("utf-16-le"), dtype=np.uint16).copy()
+        assert self.L.orc_handle_string(self.h, handle, _p(u) if len(u) else None, len(u)) == 0
 
     def advance_time(self, now):
         self.L.orc_advance_time(self.h, now)

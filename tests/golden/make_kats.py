@@ -200,6 +200,26 @@ def kats():
                .c(1, "ELECT_LISTEN")
                .close(1, events=[(1, "ELECT", L(2))]))
 
+    # ResourceManager.sessions is a java.util.HashMap<Long, SessionHolder> (ResourceManager.java:37); close() walks it
+    # (:250-264), so the instances of a closing client close in HashMap order.  Instance ids 5 + 16 i (i = 0..9) all
+    # hash to bin 5 at capacity 16 (Long.hashCode = the id; spread leaves ids < 2^16 alone); the 9th put makes the bin
+    # 9 long and treeifyBin resizes to 32 (capacity < 64): even i stay in bin 5, odd i move to bin 21, so the client's
+    # instances close in the order 0 2 4 6 8 1 3 5 7 9.  Instance 1 leads the election; 0, 2..9 and then instance 10
+    # (another client, id 1000) listen.  Closing 0 2 4 6 8 removes them as listeners (no event); closing 1 hands the
+    # lead to the first listener left, 3 (its listen is commit 4), then 3 -> 5 -> 7 -> 9 -> 10
+    # (LeaderElectionState.close :35-52).  (Insertion order would close 0 1 2 3 ...: 2, 3, .. 10 elected in turn.)
+    kat = K("A12_close_order_treeify_resize", "quirk", "manager/src/main/java/io/atomix/manager/ResourceManager.java:37,250-264")
+    kat.res(0, "ELECTION")
+    for i in range(10):
+        kat.inst(i, 0, 5 + 16 * i, 7)
+    kat.inst(10, 0, 1000, 8)
+    kat.c(1, "ELECT_LISTEN", events=[(1, "ELECT", L(1))])
+    for i in [0, 2, 3, 4, 5, 6, 7, 8, 9, 10]:
+        kat.c(i, "ELECT_LISTEN")
+    kat.close(7, events=[(3, "ELECT", L(4)), (5, "ELECT", L(6)), (7, "ELECT", L(8)), (9, "ELECT", L(10)),
+                         (10, "ELECT", L(11))])
+    out.append(kat)
+
     GR = "coordination/src/test/java/io/atomix/coordination/DistributedMembershipGroupTest.java"
     out.append(K("group_join", "reference", f"{GR}:42-65").res(0, "GROUP").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
                .c(1, "GROUP_JOIN", expect=SET(101))
@@ -286,6 +306,42 @@ def kats():
                .c(1, "MAP_PUT", key=L(1), a=NULL)
                .c(1, "MAP_PUT", key=L(2), a=S("x"))
                .c(1, "MAP_CONTAINSVALUE", a=S("x"), status="NULL_POINTER"))
+    # java.util.HashMap (JDK 8, the reference CI's JDK) iteration order, hand-derived from putVal / treeifyBin /
+    # resize / treeify / moveRootToFront.  Long.hashCode(k) = (int)(k ^ k >>> 32); HashMap.hash spreads it as
+    # h ^ (h >>> 16).  Keys k_i = i * 2^20 + 5: h = i * 2^20 + 5, spread = h ^ (i * 2^4), so at capacity 16 every k_i
+    # is in bin 5; at capacity 32 the even i stay in bin 5 and the odd i go to bin 21.  The 9th put appends the bin's
+    # 9th node (binCount 7 >= TREEIFY_THRESHOLD - 1) and treeifyBin RESIZES (capacity 16 < MIN_TREEIFY_CAPACITY 64),
+    # although size 9 <= threshold 12: iteration is then k0 k2 k4 k6 k8 | k1 k3 k5 k7.  With k1 -> null and
+    # k2 -> 7, containsValue(7) meets k2 first: true (a model that resizes on size alone stays at 16 and NPEs on k1).
+    kA = [L(i * (1 << 20) + 5) for i in range(9)]
+    kat = K("A5_contains_value_treeify_resize", "quirk", f"{MS}:49-60").res(0, "MAP").inst(0, 0, 100, 1)
+    for i, k in enumerate(kA):
+        kat.c(0, "MAP_PUT", key=k, a=NULL if i == 1 else L(7) if i == 2 else L(100 + i))
+    kat.c(0, "MAP_CONTAINSVALUE", a=L(7), expect=B(True))
+    kat.c(0, "MAP_CONTAINSVALUE", a=L(8), status="NULL_POINTER")  # bin 5 holds no 8: bin 21's k1 (null) NPEs
+    kat.c(0, "MAP_CONTAINSVALUE", a=L(107), status="NULL_POINTER")  # k7 (107) is in bin 21 after k1 (null)
+    kat.c(0, "MAP_CONTAINSVALUE", a=L(106), expect=B(True))         # k6 (106) is in bin 5, before bin 21
+    out.append(kat)
+    # String keys hash by String.hashCode ("a" 97 -> bin 1, "b" 98 -> bin 2), not by their interned handle: "b" is
+    # interned first (handle order b < a), yet "a" comes first in iteration.
+    sb, sa = S("b"), S("a")
+    out.append(K("A5_contains_value_string_hash_order", "quirk", f"{MS}:49-60").res(0, "MAP").inst(0, 0, 100, 1)
+               .c(0, "MAP_PUT", key=sb, a=NULL)
+               .c(0, "MAP_PUT", key=sa, a=L(7))
+               .c(0, "MAP_CONTAINSVALUE", a=L(7), expect=B(True))
+               .c(0, "MAP_CONTAINSVALUE", a=L(8), status="NULL_POINTER"))
+    # A tree bin: keys k_i = i * 2^22 + 5 (spread = h ^ (i * 2^6): bin 5 at every capacity <= 64).  The 9th put
+    # resizes 16 -> 32, the 10th 32 -> 64 (treeifyBin below 64), the 11th treeifies bin 5 (capacity 64): treeify
+    # inserts k0..k10 into a red-black tree in chain order (ascending hash), whose root is k3, and moveRootToFront
+    # links k3 first: iteration k3 k0 k1 k2 k4 .. k10.  With k0 -> null and k3 -> 7: containsValue(7) is true.
+    kT = [L(i * (1 << 22) + 5) for i in range(11)]
+    kat = K("A5_contains_value_tree_bin_order", "quirk", f"{MS}:49-60").res(0, "MAP").inst(0, 0, 100, 1)
+    for i, k in enumerate(kT):
+        kat.c(0, "MAP_PUT", key=k, a=NULL if i == 0 else L(7) if i == 3 else L(100 + i))
+    kat.c(0, "MAP_CONTAINSVALUE", a=L(7), expect=B(True))
+    kat.c(0, "MAP_CONTAINSVALUE", a=L(8), status="NULL_POINTER")
+    kat.d["gpu"] = "refuses"  # the engine does not order tree bins: an order-dependent answer fails (CC_ERR_STATE)
+    out.append(kat)
     out.append(K("A6_null_value_is_present", "quirk", f"{MS}:115-133,38-44,65-72")
                .res(0, "MAP").inst(0, 0, 100, 1)
                .c(0, "MAP_PUT", key=foo, a=NULL)

@@ -65,6 +65,8 @@ GPU_MMAP_OPS = {"MMAP_CONTAINSKEY", "MMAP_CONTAINSENTRY", "MMAP_CONTAINSVALUE", 
 def gpu_eligible(kat):
     """KATs whose every step this build runs through the engine: every op of every covered state machine, Delete,
     clock advances, session closes (the GPU close fan-out) and manager control commands (manager.hip)."""
+    if kat.get("gpu") == "refuses":  # the engine fails such a batch loudly (test_gpu_kats.py checks that)
+        return False
     types = {r[1] for r in kat["resources"]}
     if not types <= {"VALUE", "MAP", "LOCK", "ELECTION", "GROUP", "SET", "QUEUE", "MULTIMAP"}:
         return False
@@ -98,6 +100,8 @@ class KatRun:
         raise ValueError(ref)
 
     def run(self):
+        # the Strings behind HANDLE ids: java.util.HashMap places a String key by String.hashCode
+        self.B.handle_strings({h: s for s, h in load()["strings"].items()})
         for r in self.kat["resources"]:
             self.B.resource_create(r[0], RES[r[1]])
         for i in self.kat["instances"]:
@@ -206,6 +210,10 @@ class OracleBackend:
         flags = abi.CC_CFG_TIMERS_DEFERRED if kat.get("timer_mode", "deferred") == "deferred" else 0
         self.O = Oracle(max_resources, max_instances, flags)
 
+    def handle_strings(self, strings):
+        for h, x in strings.items():
+            self.O.handle_string(h, x)
+
     def resource_create(self, slot, t):
         self.O.resource_create(slot, t)
 
@@ -269,6 +277,9 @@ class EngineBackend:
             flags |= abi.CC_CFG_TIMERS_DEFERRED
         self.E = Engine(max_resources, max_instances, 4096, map_capacity=4096, flags=flags, max_events=1 << 16)
         self.ids = {}
+
+    def handle_strings(self, strings):
+        self.E.handle_strings(strings)
 
     def resource_create(self, slot, t):
         self.E.resource_create(slot, t)

@@ -7,6 +7,7 @@ from tests.kat_runner import EngineBackend, KatRun, all_kats, gpu_eligible
 pytestmark = pytest.mark.gpu
 
 KATS = [k for k in all_kats() if gpu_eligible(k)]
+REFUSED = [k for k in all_kats() if k.get("gpu") == "refuses"]
 
 
 def test_gpu_kat_coverage():
@@ -22,9 +23,24 @@ def test_gpu_kat_coverage():
             "election_next_on_close", "A10_close_publishes_leave_for_non_member", "A11_lock_survives_holder_close",
             "manager_create_concurrency", "manager_get_create_concurrency", "manager_operate_many",
             "manager_get_reuses_instance", "A13_delete_resource_by_instance_id", "A18_multimap_put_never_stores"} <= names
-    assert len(KATS) == len(all_kats())  # every reference-pinned KAT runs through the engine
+    # every KAT runs through the engine; the ones it refuses (a containsValue decided inside a java.util.HashMap tree
+    # bin) must fail loudly: test_kat_refused_on_gpu
+    assert len(KATS) + len(REFUSED) == len(all_kats())
+    assert {"A5_contains_value_treeify_resize", "A5_contains_value_string_hash_order"} <= names
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
 def test_kat_on_gpu(kat):
     KatRun(kat, EngineBackend(kat)).run()
+
+
+@pytest.mark.parametrize("kat", REFUSED, ids=[k["name"] for k in REFUSED])
+def test_kat_refused_on_gpu(kat):
+    """A containsValue whose answer is decided inside a bin that became a red-black tree (HashMap.treeifyBin at
+    capacity >= 64) fails the batch with CC_ERR_STATE: the engine does not follow tree-bin order, and never guesses."""
+    from copycat_amd import abi
+    from copycat_amd.engine import EngineError
+
+    with pytest.raises(EngineError) as ei:
+        KatRun(kat, EngineBackend(kat)).run()
+    assert ei.value.rc == abi.CC_ERR_STATE

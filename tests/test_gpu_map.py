@@ -23,6 +23,9 @@ def _engines(maps, max_inst, max_batch, map_capacity, sub_batch=0, first_slot=0,
     for m in range(first_slot, slots):
         O.resource_create(m, abi.CC_RES_MAP)
         O.instance_open(m, m, 1000 + m, 7)
+    from tests.handles import register_key_strings
+
+    register_key_strings(E, O)  # String keys: java.util.HashMap places them by String.hashCode
     return E, O
 
 
@@ -121,6 +124,9 @@ def test_maps_and_values_in_one_engine():
     for r in range(slots):
         O.resource_create(r, abi.CC_RES_VALUE if r < V else abi.CC_RES_MAP)
         O.instance_open(r, r, 1000 + r, 7)
+    from tests.handles import register_key_strings
+
+    register_key_strings(E, O)
     _assert_rows(*_apply_both(E, O, [b]))
     for x, y in zip(E.value_state(0, V), O.value_state(0, V)):
         assert np.array_equal(x, y)
@@ -351,19 +357,26 @@ def test_map_contains_value_ttl_mode_bounds():
     _assert_maps(E, O, [0])
 
 
+@pytest.mark.parametrize("clustered", [False, True], ids=["spread", "clustered"])
 @pytest.mark.parametrize("n,maps,keys,sub_batch,hot,p_hot,seed", [
     (60_000, 3, 40, 0, 0, 0.0, 301),             # sizes oscillate around the 24 / 48 thresholds inside tiles
     (400_000, 16, 48, 16384 * 3, 2, 0.3, 302),   # several sub-batches, hot keys (k_hot_apply deltas)
     (300_000, 200, 30, 0, 0, 0.0, 303),          # many maps, few commits per map per tile
 ])
-def test_map_contains_value_churn_parity(n, maps, keys, sub_batch, hot, p_hot, seed):
+def test_map_contains_value_churn_parity(n, maps, keys, sub_batch, hot, p_hot, seed, clustered):
     """Put / remove churn with stored nulls and containsValue / size barriers: every containsValue whose answer
     depends on HashMap iteration order uses the exact tracked capacity; every size barrier checks the tracked size
-    against the table (the engine fails the batch on a difference)."""
+    against the table (the engine fails the batch on a difference).  Clustered: the Long keys are i * 2^20 + c
+    (i < 32), so up to 16 of a map's keys share a bin below capacity 64 -- treeifyBin resizes the table early
+    (java.util.HashMap, MapState.java:33,49-60) -- but never more than 8 share a bin of 64 (no tree bin)."""
     from copycat_amd.workload import map_random_stream
 
     max_inst = maps + 8
     b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed, hot=hot, p_hot=p_hot)
+    if clustered:
+        lk = (b.flags >> 6) == 0  # Long keys
+        c = (b.inst.astype(np.uint64) % np.uint64(3)) + np.uint64(5)
+        b.key[lk] = ((b.key[lk] & np.uint64(31)) << np.uint64(20)) + c[lk]
     rows = _with_barriers(b, 0.0015, seed, ops=np.array([abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_SIZE], np.uint8),
                           p=[0.8, 0.2])
     cut = n // 2

@@ -42,11 +42,14 @@ def test_snapshot_restore_values_and_maps():
         E.instance_open_range(0, slots, 0, 1000, 7)
         return E
 
+    from tests.handles import register_key_strings
+
     E = engine()
     O = Oracle(slots, max_inst)
     for r in range(slots):
         O.resource_create(r, abi.CC_RES_VALUE if r < V else abi.CC_RES_MAP)
         O.instance_open(r, r, 1000 + r, 7)
+    register_key_strings(E, O)  # (the restored engine gets them from the snapshot)
     cut = len(b) // 2
     first = b.slice(0, cut)
     _rows_equal(E.apply_host(first), O.apply(first))
