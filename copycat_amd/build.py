@@ -50,6 +50,22 @@ def build_engine(force=False):
     return ENGINE_SO
 
 
+def build_variant(out_path, defines, tag):
+    """A diagnostics / A-B build of the engine with extra -D flags (object files under build_obj/<tag>)."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"] + [f"-D{d}" for d in defines]
+    objdir = os.path.join(HERE, "build_obj", tag)
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.splitext(f)[0] + ".o") for f in ENGINE_SRCS]
+    from concurrent.futures import ThreadPoolExecutor
+
+    jobs = max(1, min(len(ENGINE_SRCS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda so: _run([hipcc, *flags, "-c", so[0], "-o", so[1]]), zip(ENGINE_SRCS, objs)))
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out_path])
+    return out_path
+
+
 def build_workload(force=False):
     src = os.path.join(CSRC, "workload.cpp")
     if force or _stale(WORKLOAD_SO, [src]):

@@ -308,6 +308,10 @@ struct SmallMap {
 constexpr uint32_t kSmIn = 1u;       // the table is still small (capacity <= 64): tracked key by key
 constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin while tracked
 constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (TTL mode: timers remove keys unseen)
+// per-map flags of the batch (cc_engine::d_msmall): bit 0 the table is small (events followed key by key), bit 1 the
+// batch asks the map's size / isEmpty (events followed for the in-stream answers); either keeps the map's keys out of
+// hot-key routing, so every such commit is a region record
+constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
 // a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
 __device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
   return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);

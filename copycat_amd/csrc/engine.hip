@@ -98,7 +98,8 @@ static void free_all(cc_engine* e) {
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
-                  e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp};
+                  e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp,
+                  e->d_szq,      e->d_szq_n};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -636,16 +637,49 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   // Whole-map ops are barriers (map_wide.hip): find them (one sync), then apply the rows between them as segments.
   e->bars.clear();
   uint64_t clock_before = 0;  // the engine clock before this batch (TTL mode and barrier rows need it on the host)
+  e->szq_n = 0;
   if (e->map_bits || e->coord_on) {
-    HIPCHECK(hipMemsetAsync(e->d_ttl_seen, 0, sizeof(uint32_t), st));
-    if (launch_map_barriers(c->inst, c->op, c->aux, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar,
-                            e->d_bar_n, kBarCap, e->d_ttl_seen, st))
-      return set_err(CC_ERR_HIP, "map barrier scan launch", hipGetLastError());
     uint32_t nb = 0, ttl_seen = 0;
-    HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    // Outside TTL mode map size / isEmpty rows are answered in the stream (listed in szq, their maps flagged); a batch
+    // that turns TTL mode on (or lists more than szq holds) is scanned again with them as barriers (or a larger list).
+    bool inline_size = e->map_bits && !e->ttl_live;
+    for (int pass = 0;; ++pass) {
+      if (inline_size && !e->d_szq) {
+        e->szq_cap = 1u << 20;
+        HIPCHECK(hipMalloc(&e->d_szq, sizeof(uint32_t) * e->szq_cap));
+        HIPCHECK(hipMalloc(&e->d_szq_n, sizeof(uint32_t)));
+      }
+      if (e->szq_flagged) {
+        if (launch_mflag_clear(e->d_msmall, e->cfg.max_resources, st)) return set_err(CC_ERR_HIP, "map flags", hipGetLastError());
+        e->szq_flagged = false;
+      }
+      HIPCHECK(hipMemsetAsync(e->d_ttl_seen, 0, sizeof(uint32_t), st));
+      if (launch_map_barriers(c->inst, c->op, c->aux, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar,
+                              e->d_bar_n, kBarCap, e->d_ttl_seen, inline_size ? e->d_szq : nullptr,
+                              inline_size ? e->d_szq_n : nullptr, e->szq_cap, e->d_msmall, st))
+        return set_err(CC_ERR_HIP, "map barrier scan launch", hipGetLastError());
+      uint32_t qn = 0;
+      HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
+      if (inline_size) HIPCHECK(hipMemcpyAsync(&qn, e->d_szq_n, sizeof qn, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (!inline_size) break;
+      e->szq_flagged = qn > 0;
+      if (ttl_seen || pass > 1) {  // this batch turns TTL mode on: size / isEmpty become barriers again
+        inline_size = false;
+        continue;
+      }
+      if (qn > e->szq_cap) {  // a larger list, then the same scan again
+        HIPCHECK(hipFree(e->d_szq));
+        e->d_szq = nullptr;
+        e->szq_cap = qn;
+        HIPCHECK(hipMalloc(&e->d_szq, sizeof(uint32_t) * e->szq_cap));
+        continue;
+      }
+      e->szq_n = qn;
+      break;
+    }
     if (ttl_seen && !e->ttl_live) {  // TTL mode for good: the small maps' key sets stop being followed
       e->ttl_live = true;
       if (e->small_live && launch_small_ttl(e->d_msm, e->d_msmall, e->cfg.max_resources, st))
@@ -742,6 +776,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   for (uint64_t lo = seg_lo; lo < seg_hi; lo += e->sub_batch) {
     const uint64_t hi = std::min(seg_hi, lo + e->sub_batch);
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
+    SizeArgs sz{};       // this sub-batch's size / isEmpty rows (map_small.hip)
+    bool sized = false;  // the event pipeline ran (its counters are reset after the answers)
+    uint32_t sized_events = 0;
     if (e->map_bits && e->ttl_live) {  // TTL mode: every key goes through its region (timers are walked in order)
       HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
     }
@@ -781,7 +818,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.hot_msz = e->d_hot_msz;
-      ha.msmall = e->small_live ? e->d_msmall : nullptr;  // maps in their small window are not hot-routed
+      ha.msmall = (e->small_live || e->szq_n) ? e->d_msmall : nullptr;  // small / size-queried maps: not hot-routed
       ha.err = e->d_err;
       ha.mark = marker_of(e);
       static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
@@ -825,6 +862,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.dummy = e->sub_batch;
     const bool v3 = !e->ext;  // value-only engines: value_path.hip
     pa.v3 = v3;
+    pa.out_status = out->status;
+    pa.out_value = out->value;
 
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) {
@@ -852,6 +891,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.rst_status = e->d_rst_status;
     va.rst_value = e->d_rst_value;
     va.dummy = e->sub_batch;
+    va.out_status = out->status;
+    va.out_value = out->value;
     va.err = e->d_err;
     va.mark = marker_of(e);
     if ((e->has_values || !e->ext) && launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError()); DBG_SYNC("apply launch");
@@ -907,7 +948,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.list = e->d_msz_list;
         za.list_n = e->d_msz_list_n;
         za.err = e->d_err;
-        if (e->small_live) {  // maps still in their small-table window: their insertions / removals (map_small.hip)
+        if (e->small_live || e->szq_n) {  // small-window / size-queried maps: their insertions / removals (map_small.hip)
           int rc = ensure_small(e);
           if (rc) return rc;
           if (!c->index) return set_err(CC_ERR_INVALID, "an engine with maps needs the index column (log order)");
@@ -923,7 +964,29 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           za.sm_ctl = e->d_sm_ctl;
         }
         if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError()); DBG_SYNC("map size launch");
-        if (e->small_live) {
+        if (e->szq_n) {  // this sub-batch's size / isEmpty rows join the events
+          sz.szq = e->d_szq;
+          sz.szq_n = e->szq_n;
+          sz.lo = lo;
+          sz.hi = hi;
+          sz.inst = c->inst;
+          sz.op = c->op;
+          sz.index = c->index;
+          sz.inst_res = e->d_inst_res;
+          sz.ev_key = e->d_sm_key;
+          sz.ev_val = e->d_sm_val;
+          sz.cap = (uint32_t)e->sub_batch;
+          sz.ctl = e->d_sm_ctl;
+          sz.sorted_key = e->d_sm_key2;
+          sz.sorted_val = e->d_sm_val2;
+          sz.seg = e->d_sm_seg;
+          sz.nseg = e->d_sm_seg + e->cfg.max_resources;
+          sz.msize = e->d_msize;
+          sz.out_status = out->status;
+          sz.out_value = out->value;
+          if (launch_size_emit(sz, st)) return set_err(CC_ERR_HIP, "size query launch", hipGetLastError());
+        }
+        if (e->small_live || e->szq_n) {
           uint32_t ctl[2] = {0, 0};
           HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
           HIPCHECK(hipStreamSynchronize(st));
@@ -945,7 +1008,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           const int rs = launch_small_replay(sa, ctl[0], st);
           if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "small-map replay launch", hipGetLastError())
                                   : set_err(CC_ERR_STATE, "small-map events exceed their buffer");
-          if (ctl[0] == 0 && ctl[1] == 0) e->small_live = false;  // (ctl[1]: maps still small after the last replay)
+          if (e->small_live && ctl[0] == 0 && ctl[1] == 0) e->small_live = false;  // (ctl[1]: maps small after the last replay)
+          sized = true;
+          sized_events = ctl[0];
         }
       }
     }
@@ -993,7 +1058,16 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.dummy_value = e->d_rst_value + e->sub_batch;
     ua.v3 = v3;
     ua.mark = marker_of(e);
-    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
+    if (!(v3 && kValueDirect) && launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
+    if (sized) {  // size / isEmpty answers over the unpermute's placeholders; then the next sub-batch's counters
+      if (e->szq_n && sized_events && launch_size_answer(sz, st))
+        return set_err(CC_ERR_HIP, "size answer launch", hipGetLastError());
+      SmallArgs sf{};
+      sf.ctl = e->d_sm_ctl;
+      sf.msmall = e->d_msmall;
+      sf.max_resources = e->cfg.max_resources;
+      if (launch_small_finish(sf, st)) return set_err(CC_ERR_HIP, "small-map counters", hipGetLastError());
+    }
     if (e->coord_on) {
       EventArgs ea{};
       ea.cpos = e->d_cpos;
@@ -1799,6 +1873,22 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
     else memcpy(p, x.host, x.bytes);
     p += x.bytes;
   }
+  {
+    std::vector<uint8_t> sess;  // ResourceManager.sessions' java.util.HashMap structure (close order)
+    e->sessions.save(sess);
+    const uint64_t sb = sess.size();
+    memcpy(p, &sb, 8);
+    memcpy(p + 8, sess.data(), sb);
+    p += 8 + sb;
+    const uint64_t nh = e->hh.size();  // String.hashCode of HANDLE keys: (handle, hash) pairs
+    memcpy(p, &nh, 8);
+    p += 8;
+    for (const auto& kv : e->hh) {
+      const uint64_t t[2] = {kv.first, (uint64_t)(uint32_t)kv.second};
+      memcpy(p, t, 16);
+      p += 16;
+    }
+  }
   const uint64_t ng = e->gtimers.size();  // pending MembershipGroup.schedule timers
   memcpy(p, &ng, 8);
   memcpy(p + 8, &e->gtimer_seq, 8);
@@ -1821,20 +1911,6 @@ extern "C" int cc_snapshot_save(cc_engine* e, void* h_buf, uint64_t cap) {
       memcpy(p, t, 16);
       p += 16;
     }
-  std::vector<uint8_t> sess;  // ResourceManager.sessions' java.util.HashMap structure (close order)
-  e->sessions.save(sess);
-  const uint64_t sb = sess.size();
-  memcpy(p, &sb, 8);
-  memcpy(p + 8, sess.data(), sb);
-  p += 8 + sb;
-  const uint64_t nh = e->hh.size();  // String.hashCode of HANDLE keys: (handle, hash) pairs
-  memcpy(p, &nh, 8);
-  p += 8;
-  for (const auto& kv : e->hh) {
-    const uint64_t t[2] = {kv.first, (uint64_t)(uint32_t)kv.second};
-    memcpy(p, t, 16);
-    p += 16;
-  }
   return CC_OK;
 }
 
@@ -1871,6 +1947,20 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
     if (b != want || !snap_room(p, end, b, 1)) return set_err(CC_ERR_INVALID, "snapshot section size mismatch");
     p += b;
   }
+  uint64_t sbytes = 0, nh = 0;
+  cc::JavaLongHashMap sessions;
+  if (!snap_room(p, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&sbytes, p, 8);
+  p += 8;
+  if (!snap_room(p, end, sbytes, 1) || sessions.load(p, sbytes) != sbytes)
+    return set_err(CC_ERR_INVALID, "snapshot: malformed sessions table");
+  p += sbytes;
+  if (!snap_room(p, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
+  memcpy(&nh, p, 8);
+  p += 8;
+  if (!snap_room(p, end, nh, 16)) return set_err(CC_ERR_INVALID, "snapshot truncated (handle hashes)");
+  const uint8_t* const hh_at = p;
+  p += nh * 16;
   uint64_t ng = 0, ns = 0, nl = 0;
   if (!snap_room(p, end, 2, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
   memcpy(&ng, p, 8);
@@ -1886,19 +1976,6 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   memcpy(&nl, p, 8);
   p += 8;
   if (!snap_room(p, end, nl, 16)) return set_err(CC_ERR_INVALID, "snapshot truncated (leak lists)");
-  const uint8_t* tail = p + nl * 16;
-  uint64_t sbytes = 0, nh = 0;
-  cc::JavaLongHashMap sessions;
-  if (!snap_room(tail, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
-  memcpy(&sbytes, tail, 8);
-  tail += 8;
-  if (!snap_room(tail, end, sbytes, 1) || sessions.load(tail, sbytes) != sbytes)
-    return set_err(CC_ERR_INVALID, "snapshot: malformed sessions table");
-  tail += sbytes;
-  if (!snap_room(tail, end, 1, 8)) return set_err(CC_ERR_INVALID, "snapshot truncated");
-  memcpy(&nh, tail, 8);
-  tail += 8;
-  if (!snap_room(tail, end, nh, 16)) return set_err(CC_ERR_INVALID, "snapshot truncated (handle hashes)");
   // 2. apply
   int rc = quiesce(e);
   if (rc) return rc;
@@ -1911,6 +1988,7 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
     else memcpy(x.host, p, x.bytes);
     p += x.bytes;
   }
+  p = hh_at + nh * 16;  // (the sessions table and handle hashes were parsed above)
   memcpy(&e->gtimer_seq, p + 8, 8);
   p += 16;
   e->gtimers.resize(ng);
@@ -1971,9 +2049,10 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   {
     std::vector<uint64_t> hk(nh);
     std::vector<int32_t> hv(nh);
-    for (uint64_t i = 0; i < nh; ++i, tail += 16) {
+    const uint8_t* q = hh_at;
+    for (uint64_t i = 0; i < nh; ++i, q += 16) {
       uint64_t t[2];
-      memcpy(t, tail, 16);
+      memcpy(t, q, 16);
       hk[i] = t[0];
       hv[i] = (int32_t)(uint32_t)t[1];
     }

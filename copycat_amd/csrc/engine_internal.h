@@ -32,6 +32,8 @@ struct PartArgs {
   const uint64_t* clock_base;  // device: the engine clock before this batch
   uint32_t ext_flags;     // kExtValue | kExtDeferred | kExtTimeCheck
   uint32_t* err;          // device error bits (kExtTimeCheck: kErrTime)
+  uint8_t* out_status;    // value-only engines (kValueDirect): the batch's result columns; rows of unknown
+  uint64_t* out_value;    //   instances are answered by the partition (UNKNOWN_SESSION)
   bool ext;               // extended staging (maps / coordination / value events)
   uint64_t lo, hi;
   const uint32_t* inst_res;
@@ -78,8 +80,16 @@ struct ValueArgs {
   bool v3;               // value_path.hip: 16-byte records, 8192-commit tiles
   const uint64_t* cb;    //   the batch's b column (escaped CAS updates) and the sub-batch's first row
   uint64_t lo;
+  uint8_t* out_status;   //   kValueDirect: results straight to the batch's rows (absolute), else to rst_*
+  uint64_t* out_value;
   Marker mark;
 };
+// Value-only engines: the apply stores every result at its log row (k_apply_value_v3), so no unpermute runs.
+#ifndef CC_VALUE_UNPERMUTE
+constexpr bool kValueDirect = true;
+#else
+constexpr bool kValueDirect = false;  // A/B build: results in staging order, then k_unpermute
+#endif
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
@@ -166,7 +176,33 @@ struct SmallArgs {
   uint32_t* mpcap;
   uint32_t max_resources;
 };
-int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st);
+int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st);  // sort, runs, replay (E events)
+int launch_small_finish(const SmallArgs& a, hipStream_t st);              // counters for the next sub-batch
+// size / isEmpty rows of the sub-batch [lo, hi): emitted into the event buffer before the sort (query entries), then
+// answered from the sorted buffer after the unpermute (the row's staged result is a placeholder)
+struct SizeArgs {
+  const uint32_t* szq;          // the batch's size / isEmpty rows (unordered)
+  uint32_t szq_n;
+  uint64_t lo, hi;              // the sub-batch's rows
+  const uint32_t* inst;         // batch columns
+  const uint8_t* op;
+  const uint64_t* index;
+  const uint32_t* inst_res;
+  uint64_t* ev_key;
+  uint32_t* ev_val;
+  uint32_t cap;
+  uint32_t* ctl;                // [0] the event count
+  const uint64_t* sorted_key;   // after the sort
+  const uint32_t* sorted_val;
+  const uint32_t* seg;
+  const uint32_t* nseg;
+  const uint32_t* msize;        // [max_resources] live sizes at the sub-batch end (exact tracking)
+  uint8_t* out_status;          // the batch's result columns (absolute rows)
+  uint64_t* out_value;
+};
+int launch_size_emit(const SizeArgs& a, hipStream_t st);
+int launch_size_answer(const SizeArgs& a, hipStream_t st);
+int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st);
 size_t small_sort_temp_bytes(uint32_t cap);
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st);
 int launch_small_ttl(SmallMap* state, uint8_t* msmall, uint32_t R, hipStream_t st);
@@ -176,9 +212,12 @@ int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* ma
 // Whole-map ops (containsValue / isEmpty / size / clear / Delete): barrier rows of a batch (map_wide.hip).
 constexpr uint32_t kBarCap = 1u << 16;  // barrier rows per batch
 // Also flags (ttl_seen = 1) a map put/putIfAbsent/replace/replaceIfPresent row with ttl > 0.
+// Outside TTL mode map size / isEmpty rows are not barriers: they are listed in szq (rows) and their maps flagged
+// (kMfSize in mflag), then answered in the stream (map_small.hip launch_size_answer).
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
-                        uint32_t* ttl_seen, hipStream_t st);
+                        uint32_t* ttl_seen, uint32_t* szq, uint32_t* szq_n, uint32_t szq_cap, uint8_t* mflag,
+                        hipStream_t st);
 struct MapWideArgs {
   uint32_t slot, op, atag;
   uint64_t apay;

@@ -160,6 +160,12 @@ struct cc_engine {
   void* d_sm_temp = nullptr;
   size_t sm_temp_bytes = 0;
   bool small_live = false;         // some map may still be in the window (the host then reads the event count)
+  // map size / isEmpty rows answered in the stream (outside TTL mode; map_small.hip k_size_answer)
+  uint32_t* d_szq = nullptr;       // [szq_cap] the batch's size / isEmpty rows
+  uint32_t* d_szq_n = nullptr;
+  uint32_t szq_cap = 0;
+  uint32_t szq_n = 0;              // this batch's
+  bool szq_flagged = false;        // maps carry kMfSize from the last batch (cleared before the next scan)
   unsigned long long* d_mw_ctl = nullptr;  // [16]
   std::vector<uint32_t> bars;
   // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good

@@ -59,6 +59,7 @@ __global__ __launch_bounds__(256) void k_small_replay(const uint64_t* __restrict
     for (uint32_t i = start; i < E; ++i) {
       const uint64_t k = key[i];
       if ((uint32_t)(k >> 44) != m) break;
+      if (k & 8u) continue;  // a size / isEmpty query (k_size_answer)
       const uint32_t x = val[i];
       if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
         const uint32_t mask = (16u << lvl) - 1u;
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void k_small_replay(const uint64_t* __restrict
       s->lvl = lvl;
       s->flags = flags;
       s->tree_bins = tree;
-      msmall[m] = (flags & kSmIn) ? 1u : 0u;
+      msmall[m] = (uint8_t)((msmall[m] & ~kMfSmall) | ((flags & kSmIn) ? kMfSmall : 0u));
       atomicMax(&mpcap[m], lvl);
     }
   }
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void k_small_replay(const uint64_t* __restrict
 // maps still in the window (read by the host with the next sub-batch's event count)
 __global__ void k_small_count(const uint8_t* __restrict__ msmall, uint32_t R, uint32_t* __restrict__ ctl) {
   uint32_t c = 0;
-  for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x) c += msmall[m];
+  for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x) c += msmall[m] & kMfSmall;
   for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(&ctl[1], c);
 }
@@ -119,10 +120,112 @@ __global__ void k_small_clear(SmallMap* __restrict__ st, uint32_t m) {
 // TTL mode: timers remove keys without a commit, so the small maps' key sets are no longer known
 __global__ void k_small_ttl(SmallMap* __restrict__ st, uint8_t* __restrict__ msmall, uint32_t R) {
   for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
-    if (msmall[m]) {
+    if (msmall[m] & kMfSmall) {
       st[m].flags |= kSmUnknown;
-      msmall[m] = 0;
+      msmall[m] &= (uint8_t)~kMfSmall;
     }
+}
+
+// ---- map size / isEmpty in the stream (MapState.size :233-239, isEmpty :244-250), outside TTL mode ---------------
+// The size at a row is the size at the sub-batch's end (the exact tracking, msize) minus the map's net insertions of
+// the sub-batch, plus those before the row.  The map's insertions / removals are the events k_msize_count emits for
+// flagged maps; the queries join them in the same buffer (key bit 3, after the commit whose index they carry: a
+// query takes the index of the command before it), so the radix sort puts each map's events and queries in log order.
+__global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, uint64_t lo, uint64_t hi,
+                            const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                            const uint64_t* __restrict__ index, const uint32_t* __restrict__ inst_res,
+                            uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val, uint32_t cap,
+                            uint32_t* __restrict__ ctl) {
+  const uint64_t idx0 = index[lo];
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < szq_n; q += gridDim.x * blockDim.x) {
+    const uint32_t row = szq[q];
+    if (row < lo || row >= hi) continue;
+    const uint32_t m = inst_res[inst[row]];  // (listed by the barrier scan on a live map: the registry is fixed in a batch)
+    const uint64_t d = (index[row] - idx0) & ((1ull << 40) - 1);
+    const uint32_t at = atomicAdd(ctl, 1u);
+    if (at < cap) {
+      ev_key[at] = ((uint64_t)m << 44) | (d << 4) | 8u | (op[row] == CC_OP_MAP_ISEMPTY ? 4u : 0u);
+      ev_val[at] = row;
+    }
+  }
+}
+
+// One wave per map run of the sorted buffer: the run's net change, then a wave-wide running count; each query row
+// gets the size before it (events with its index come first: a query follows the command whose index it carries).
+__global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                     const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
+                                                     const uint32_t* __restrict__ nseg, const uint32_t* __restrict__ msize,
+                                                     uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value) {
+  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
+    const uint32_t start = seg[r];
+    const uint32_t m = (uint32_t)(key[start] >> 44);
+    int32_t net = 0;
+    bool queries = false;
+    uint32_t end = start;
+    for (uint32_t b = start;; b += kWave) {  // pass 1: the run's end, net change, and whether it holds a query
+      const uint32_t i = b + l;
+      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
+      const uint64_t k = in ? key[i] : 0;
+      const int32_t dlt = !in || (k & 8u) ? 0 : ((k & 3u) == 1u ? 1 : ((k & 3u) == 2u ? -1 : 0));
+      int32_t sum = dlt;
+      for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+      net += sum;
+      queries |= __ballot(in && (k & 8u)) != 0;
+      const uint64_t inb = __ballot(in);
+      end = b + (uint32_t)__builtin_popcountll(inb);
+      if (inb != ~0ull) break;
+    }
+    if (!queries) continue;
+    int32_t size = (int32_t)msize[m] - net;  // at the sub-batch's start
+    for (uint32_t b = start; b < end; b += kWave) {  // pass 2: running size, answers
+      const uint32_t i = b + l;
+      const bool in = i < end;
+      const uint64_t k = in ? key[i] : 0;
+      const int32_t dlt = !in || (k & 8u) ? 0 : ((k & 3u) == 1u ? 1 : ((k & 3u) == 2u ? -1 : 0));
+      int32_t inc = dlt;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      if (in && (k & 8u)) {
+        const int32_t at = size + inc;  // (a query's own delta is 0: inc counts the events before it)
+        const uint32_t row = val[i];
+        if (k & 4u) {  // isEmpty
+          out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+          out_value[row] = at == 0 ? 1ull : 0ull;
+        } else {  // size: an int
+          out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_INT);
+          out_value[row] = (uint64_t)(int64_t)at;
+        }
+      }
+      size += __shfl(inc, 63, 64);
+    }
+  }
+}
+
+__global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
+  for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
+    mflag[m] &= (uint8_t)~kMfSize;
+}
+
+int launch_size_emit(const SizeArgs& a, hipStream_t st) {
+  if (a.szq_n == 0) return 0;
+  hipLaunchKernelGGL(k_size_emit, dim3(std::min<uint32_t>(1024, (a.szq_n + 255) / 256)), dim3(256), 0, st, a.szq, a.szq_n,
+                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.cap, a.ctl);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_size_answer(const SizeArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_size_answer, dim3(256), dim3(256), 0, st, a.sorted_key, a.sorted_val, a.ctl, a.seg, a.nseg,
+                     a.msize, a.out_status, a.out_value);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st) {
+  hipLaunchKernelGGL(k_mflag_clear, dim3(std::min<uint32_t>(256, (R + 255) / 256)), dim3(256), 0, st, mflag, R);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
@@ -143,7 +246,11 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
     hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ctl, a.seg, a.nseg, a.state,
                        a.msmall, a.mpcap);
   }
-  // the next sub-batch's counters: events 0, maps still small recounted
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the next sub-batch's counters (after the size answers read this one's): events 0, maps still small recounted
+int launch_small_finish(const SmallArgs& a, hipStream_t st) {
   if (hipMemsetAsync(a.ctl, 0, 2 * sizeof(uint32_t), st) != hipSuccess) return -1;
   hipLaunchKernelGGL(k_small_count, dim3(std::min<uint32_t>(256, (a.max_resources + 255) / 256)), dim3(256), 0, st, a.msmall,
                      a.max_resources, a.ctl);

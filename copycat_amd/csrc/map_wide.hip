@@ -51,7 +51,9 @@ __device__ inline bool ttl_op(uint32_t op) {
 __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* __restrict__ inst,
                                        const uint64_t* __restrict__ aux, const uint32_t* __restrict__ inst_res,
                                        const uint8_t* __restrict__ res_type, uint32_t max_inst, uint32_t* __restrict__ bar,
-                                       uint32_t* __restrict__ bar_n, uint32_t cap, uint32_t* __restrict__ ttl_seen) {
+                                       uint32_t* __restrict__ bar_n, uint32_t cap, uint32_t* __restrict__ ttl_seen,
+                                       uint32_t* __restrict__ szq, uint32_t* __restrict__ szq_n, uint32_t szq_cap,
+                                       uint8_t* __restrict__ mflag) {
   bool wide = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
@@ -69,6 +71,14 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
   else if (ty == CC_RES_GROUP) wide = o == CC_OP_GROUP_SCHEDULE;  // MembershipGroupState.schedule: a timer
   else return;
   if ((ty == CC_RES_GROUP || ty == CC_RES_MULTIMAP) && !wide) return;
+  if (szq && ty == CC_RES_MAP && (o == CC_OP_MAP_SIZE || o == CC_OP_MAP_ISEMPTY)) {
+    // MapState.size / isEmpty (:233-250) outside TTL mode: an ordinary row, answered from the exact size tracking
+    // (k_size_answer); its map's insertions and removals of the batch are followed (mflag bit 1)
+    const uint32_t k = atomicAdd(szq_n, 1u);
+    if (k < szq_cap) szq[k] = (uint32_t)i;
+    if (!(mflag[r] & kMfSize)) mflag[r] |= kMfSize;  // (a benign race: every writer stores the same bit set)
+    return;
+  }
   if (!wide) {
     // not a barrier here: a row that arms a TTL timer on this map / set?
     if (!aux || !(ty == CC_RES_MAP ? ttl_op(o) && o != CC_OP_SET_ADD : o == CC_OP_SET_ADD) || (int64_t)aux[i] <= 0) return;
@@ -88,7 +98,9 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
                                                       const uint32_t* __restrict__ inst_res,
                                                       const uint8_t* __restrict__ res_type, uint32_t max_inst,
                                                       uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap,
-                                                      uint32_t* __restrict__ ttl_seen) {
+                                                      uint32_t* __restrict__ ttl_seen, uint32_t* __restrict__ szq,
+                                                      uint32_t* __restrict__ szq_n, uint32_t szq_cap,
+                                                      uint8_t* __restrict__ mflag) {
   const uint64_t g = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   const uint64_t i0 = g * kMwRows;
   if (i0 >= n) return;
@@ -114,7 +126,8 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
     const uint64_t i = i0 + q;
     const uint32_t o = (wv[q / 4] >> (8 * (q % 4))) & 0xFFu;
     const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
-    if (cand && i < n) map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen);
+    if (cand && i < n)
+      map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag);
   }
 }
 
@@ -369,11 +382,13 @@ int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st) {
 
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
-                        uint32_t* ttl_seen, hipStream_t st) {
+                        uint32_t* ttl_seen, uint32_t* szq, uint32_t* szq_n, uint32_t szq_cap, uint8_t* mflag,
+                        hipStream_t st) {
   if (hipMemsetAsync(bar_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (szq_n && hipMemsetAsync(szq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   const uint64_t groups = (n + kMwRows - 1) / kMwRows;
   hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((groups + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
-                     res_type, max_inst, bar, bar_n, cap, ttl_seen);
+                     res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -482,7 +497,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
       const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
       if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
-      if (code && base == 0 && msmall && msmall[x >> 2])  // a map still in its small window (map_small.hip)
+      if (code && base == 0 && msmall && msmall[x >> 2])  // small-window or size-queried map (map_small.hip)
         small_event(x >> 2, code, xrec[(uint64_t)t * kTile + p], *idx0p, hh_key, hh_val, hh_n, ev_key, ev_val, ev_cap,
                     sm_ctl, err);
     }

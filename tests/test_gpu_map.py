@@ -367,8 +367,9 @@ def test_map_contains_value_churn_parity(n, maps, keys, sub_batch, hot, p_hot, s
     """Put / remove churn with stored nulls and containsValue / size barriers: every containsValue whose answer
     depends on HashMap iteration order uses the exact tracked capacity; every size barrier checks the tracked size
     against the table (the engine fails the batch on a difference).  Clustered: the Long keys are i * 2^20 + c
-    (i < 32), so up to 16 of a map's keys share a bin below capacity 64 -- treeifyBin resizes the table early
-    (java.util.HashMap, MapState.java:33,49-60) -- but never more than 8 share a bin of 64 (no tree bin)."""
+    (i < 16), so all 16 of a map's Long keys share a bin of 16 and 8 a bin of 32 -- with the Integer keys that
+    join them treeifyBin resizes the table early (java.util.HashMap, MapState.java:33,49-60) -- while a bin of 64
+    holds 4 of them (no tree bin)."""
     from copycat_amd.workload import map_random_stream
 
     max_inst = maps + 8
@@ -376,7 +377,7 @@ def test_map_contains_value_churn_parity(n, maps, keys, sub_batch, hot, p_hot, s
     if clustered:
         lk = (b.flags >> 6) == 0  # Long keys
         c = (b.inst.astype(np.uint64) % np.uint64(3)) + np.uint64(5)
-        b.key[lk] = ((b.key[lk] & np.uint64(31)) << np.uint64(20)) + c[lk]
+        b.key[lk] = ((b.key[lk] & np.uint64(15)) << np.uint64(20)) + c[lk]
     rows = _with_barriers(b, 0.0015, seed, ops=np.array([abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_SIZE], np.uint8),
                           p=[0.8, 0.2])
     cut = n // 2

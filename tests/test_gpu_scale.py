@@ -36,6 +36,27 @@ def test_c3_zipf_20m_rows():
     _assert_maps(E, O, sorted(set(range(0, maps, 257)) | set(int(h) for h in hot)))
 
 
+def test_c3_zipf_with_1pct_size_rows_20m():
+    """MapState.size / isEmpty (:233-250) as ordinary rows: 1% of a 20M-row Zipf map stream (200,000 of them, three
+    times the whole-map barrier list's 65,536) are size / isEmpty.  They are answered in the stream from the exact size
+    tracking -- no barrier, no host sync per row, no CC_ERR_CAPACITY -- bit-exact against the oracle, across
+    sub-batches (16,384 x 128 rows each)."""
+    from tests.test_gpu_map import _apply_both, _assert_maps, _assert_rows, _engines
+    from copycat_amd.workload import map_zipf_rows
+
+    n, maps, pairs = 20_000_000, 4096, 1 << 20
+    b = map_zipf_rows(0, n, maps=maps, pairs=pairs, threads=8)
+    rng = np.random.default_rng(77)
+    rows = np.nonzero(rng.random(n) < 0.01)[0]
+    b.op[rows] = rng.choice(np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_ISEMPTY], np.uint8), size=len(rows))
+    E, O = _engines(maps, maps, n, pairs, sub_batch=16384 * 128)
+    gs, gv, os_, ov = _apply_both(E, O, [b.slice(0, n // 2), b.slice(n // 2, n)])
+    _assert_rows(gs, gv, os_, ov)
+    sz = rows[b.op[rows] == abi.CC_OP_MAP_SIZE]
+    assert len(rows) > 3 * 65536 and len(np.unique(gv[sz])) > 100  # the sizes grow through the stream
+    _assert_maps(E, O, sorted(set(range(0, maps, 257))))
+
+
 def test_c5_mixed_coordination_10m_rows():
     from copycat_amd.engine import Engine
     from copycat_amd.workload import coord_random_stream

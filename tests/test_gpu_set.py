@@ -60,6 +60,9 @@ def _mixed(flags, ttl, n=80_000, seed=61, sub_batch=0):
     for r in range(slots):
         O.resource_create(r, abi.CC_RES_MAP if r < M else abi.CC_RES_SET)
         O.instance_open(r, r, 1000 + r, 7)
+    from tests.handles import register_key_strings
+
+    register_key_strings(E, O)
     return E, O, b, slots
 
 
