@@ -21,9 +21,10 @@ rank writes its applied watermark into HBM (cc_applied_index_async) and the wate
 
 roofline: per-kernel device time from HIP events recorded on the launch stream over the timed region
 (cc_profile_*).  The 39 algorithmic bytes per commit are split over the kernels that move
-them: the 30 input bytes to k_part_tile (which reads the input columns), the 9 result bytes to k_unpermute (which
-writes the result columns); `frac` is the dominant kernel's share over its own launch time, `pipeline_frac` all 39
-bytes over the whole step.
+them: the 30 input bytes to k_part_tile (which reads the input columns), the 9 result bytes to the kernel that writes
+the result columns (k_apply_value_v3, which stores every result at its log row on value-only engines; k_unpermute
+elsewhere); `frac` is the dominant kernel's share over its own launch time, `pipeline_frac` all 39 bytes over the
+whole step.
 cpu_baseline: the oracle (C++ restatement of the Java apply path, single thread, as the reference's single
 state-machine thread) over step 0's rows (rank 0, N=1 only); cpu_baseline_all_cores: the same rows sharded by
 resource over the box's CPU share, one oracle per thread.
@@ -65,10 +66,9 @@ RESULT_SENTINEL = 0xFF  # result prefill: status 0xFF (tag nibble 15) is never a
 
 
 # the kernels each profiling marker spans (their HBM traffic adds up); the first present partition kernel is the one
-# (value-only engines: k_part_v4, or k_part_v3 under CC_PART_V3; engines with maps, coordination or value events:
-# k_part_ext)
-MARKER_KERNELS = {"k_part_tile": ("k_part_v4", "k_part_v3", "k_part_ext", "k_part_v2", "k_part_tile"),
-                  "k_apply_value": ("k_apply_value_v3", "k_apply_value_ws", "k_apply_value"),
+# (value-only engines: k_part_v4; engines with maps, coordination or value events: k_part_ext)
+MARKER_KERNELS = {"k_part_tile": ("k_part_v4", "k_part_ext"),
+                  "k_apply_value": ("k_apply_value_v3", "k_apply_value_ws"),
                   "k_events": ("k_ev_count", "k_ev_tiles", "k_ev_chist", "k_ev_cscan", "k_ev_place", "k_ev_tile_out",
                                "k_ev_rows", "k_ev_perm", "k_ev_out"),
                   "k_map_hot": ("k_hot_detect", "k_hot_agg", "k_hot_lists", "k_hot_apply")}
@@ -737,10 +737,13 @@ def roofline_split(prof, n, steps, ms_per_step):
     """c2 roofline (the contract's definition): SURVEY §8(d)'s 39 algorithmic bytes per commit x the commits one launch
     of the dominant kernel processes / that kernel's average launch time (HIP events around every launch of the timed
     region).  Also reported: the bytes split over the kernels that move them at the interface (30 input bytes read
-    by the partition, 9 result bytes written by the unpermute) and the whole-pipeline fraction."""
+    by the partition, 9 result bytes written by the kernel that stores the results) and the whole-pipeline fraction."""
     if not prof:
         return None
-    share = {"k_part_tile": 30.0, "k_unpermute": 9.0}
+    # value-only engines store results at their log rows from the apply (no unpermute launch); an A/B build with the
+    # unpermute (-DCC_VALUE_UNPERMUTE) writes them there
+    writer = "k_unpermute" if prof.get("k_unpermute", (0, 0))[1] else "k_apply_value"
+    share = {"k_part_tile": 30.0, writer: 9.0}
     dom = max(prof, key=lambda k: prof[k][0])
     ms_tot, launches = prof[dom]
     commits_per_launch = n * steps / max(launches, 1)
@@ -755,7 +758,7 @@ def roofline_split(prof, n, steps, ms_per_step):
         "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c2"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c2"),
         "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
-        "alg_bytes_per_commit": B_OP_C2, "interface_split": {**share, "k_apply_value": 0.0},
+        "alg_bytes_per_commit": B_OP_C2, "interface_split": share,
         "alg_gb_per_launch": round(b * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
         "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
         "per_kernel_alg_gbps": per_kernel,
