@@ -862,8 +862,6 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.dummy = e->sub_batch;
     const bool v3 = !e->ext;  // value-only engines: value_path.hip
     pa.v3 = v3;
-    pa.out_status = out->status;
-    pa.out_value = out->value;
 
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) {
@@ -891,8 +889,6 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.rst_status = e->d_rst_status;
     va.rst_value = e->d_rst_value;
     va.dummy = e->sub_batch;
-    va.out_status = out->status;
-    va.out_value = out->value;
     va.err = e->d_err;
     va.mark = marker_of(e);
     if ((e->has_values || !e->ext) && launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError()); DBG_SYNC("apply launch");
@@ -1058,7 +1054,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.dummy_value = e->d_rst_value + e->sub_batch;
     ua.v3 = v3;
     ua.mark = marker_of(e);
-    if (!(v3 && kValueDirect) && launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
+    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
     if (sized) {  // size / isEmpty answers over the unpermute's placeholders; then the next sub-batch's counters
       if (e->szq_n && sized_events && launch_size_answer(sz, st))
         return set_err(CC_ERR_HIP, "size answer launch", hipGetLastError());

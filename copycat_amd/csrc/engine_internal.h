@@ -32,8 +32,6 @@ struct PartArgs {
   const uint64_t* clock_base;  // device: the engine clock before this batch
   uint32_t ext_flags;     // kExtValue | kExtDeferred | kExtTimeCheck
   uint32_t* err;          // device error bits (kExtTimeCheck: kErrTime)
-  uint8_t* out_status;    // value-only engines (kValueDirect): the batch's result columns; rows of unknown
-  uint64_t* out_value;    //   instances are answered by the partition (UNKNOWN_SESSION)
   bool ext;               // extended staging (maps / coordination / value events)
   uint64_t lo, hi;
   const uint32_t* inst_res;
@@ -80,16 +78,8 @@ struct ValueArgs {
   bool v3;               // value_path.hip: 16-byte records, 8192-commit tiles
   const uint64_t* cb;    //   the batch's b column (escaped CAS updates) and the sub-batch's first row
   uint64_t lo;
-  uint8_t* out_status;   //   kValueDirect: results straight to the batch's rows (absolute), else to rst_*
-  uint64_t* out_value;
   Marker mark;
 };
-// Value-only engines: the apply stores every result at its log row (k_apply_value_v3), so no unpermute runs.
-#ifndef CC_VALUE_UNPERMUTE
-constexpr bool kValueDirect = true;
-#else
-constexpr bool kValueDirect = false;  // A/B build: results in staging order, then k_unpermute
-#endif
 int launch_apply_value(const ValueArgs& a, hipStream_t st);
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);

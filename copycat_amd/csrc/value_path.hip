@@ -138,8 +138,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
                                                 const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
                                                 const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
                                                 uint32_t tiles, uint4* __restrict__ st_rec, uint16_t* __restrict__ cpos,
-                                                uint16_t* __restrict__ ttab, uint8_t* __restrict__ out_status,
-                                                uint64_t* __restrict__ out_value) {
+                                                uint16_t* __restrict__ ttab) {
   __shared__ uint4 img[kV3Tile];             // the tile's records in staging order
   __shared__ uint32_t wc[kP4W][kMaxSb / 2];  // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
   __shared__ uint16_t kst[kMaxSb + 1];       // tile-local run starts (+ live count)
@@ -236,16 +235,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
         img[sp] = v3_set_rows(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << KSB) - 1)), q, tbase + q);
         cp = sp;
       }
-      if (kValueDirect) {
-        // sessions.get(instanceId) == null: ResourceManagerException "unknown resource session"
-        // (ResourceManager.java:60-62); the row is not staged, its result is written here
-        if (q < nrow && loc[j] == 0xFFFFu) {
-          out_status[tile0 + q] = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
-          out_value[tile0 + q] = 0;
-        }
-      } else if (q < nrow) {
-        cpos[tbase + q] = (uint16_t)cp;
-      }
+      if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
     }
     const uint32_t Tn = T + gridDim.x;
     if (Tn < tiles) load(Tn);  // the raw registers are free: the next tile's loads fly during the write-out
@@ -329,8 +319,7 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
                                                         uint32_t sb, uint32_t* __restrict__ val_meta,
                                                         uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
                                                         uint64_t* __restrict__ rst_value, uint64_t dummy,
-                                                        uint32_t* __restrict__ err_out, uint8_t* __restrict__ out_status,
-                                                        uint64_t* __restrict__ out_value) {
+                                                        uint32_t* __restrict__ err_out) {
   using P = V3A<NS>;
 #ifdef CC_DIAG  // diagnostics build only (-DCC_DIAG=1: no walk, 2: contiguous positions -- wrong results by design)
   constexpr uint32_t diag = CC_DIAG;
@@ -529,7 +518,7 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
 #define CC_PLACE1(J)                                                                \
     {                                                                               \
       pp##J = 0;                                                                    \
-      gp##J = kValueDirect && g##J != kNoPos3 ? (g##J & ~(uint32_t)(kV3Tile - 1)) | v3_row(rr##J) : g##J; \
+      gp##J = g##J;                                                                 \
       if (g##J != kNoPos3) {                                                        \
         uint32_t m_;                                                                \
         uint64_t x_, y_;                                                            \
@@ -544,17 +533,13 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
     WPH(6);
   };
   // the previous chunk's results (buffer b) back to the records' staging positions; unconditional stores
-  // kValueDirect: gq is the record's row in the sub-batch; the result goes straight to the batch's result columns
-  // (out_* = the sub-batch's first row), rows past the list to the staging area's dummy rows
-  uint8_t* const st_to = kValueDirect ? out_status : rst_status;
-  uint64_t* const va_to = kValueDirect ? out_value : rst_value;
   auto store_results = [&](uint32_t b) {
 #define CC_STORE1(J)                                                                \
     {                                                                               \
-      const bool ok_ = gq##J != kNoPos3;                                            \
+      const uint64_t gx = gq##J != kNoPos3 ? (uint64_t)gq##J : dummy + t;           \
       const u64x2 r_ = sab[b][qp##J];                                               \
-      (ok_ ? st_to : rst_status + dummy)[ok_ ? (uint64_t)gq##J : t] = (uint8_t)r_.y; \
-      (ok_ ? va_to : rst_value + dummy)[ok_ ? (uint64_t)gq##J : t] = r_.x;          \
+      rst_status[gx] = (uint8_t)r_.y;                                               \
+      rst_value[gx] = r_.x;                                                         \
     }
     CC_J4(CC_STORE1)
 #undef CC_STORE1
@@ -643,8 +628,7 @@ int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
 #define CC_LAUNCH4(KP)                                                                                                 \
   hipLaunchKernelGGL((k_part_v4<KP, 8>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,   \
-                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab,         \
-                     a.out_status, a.out_value)
+                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
   if (kp <= 2) CC_LAUNCH4(2);
   else if (kp <= 4) CC_LAUNCH4(4);
   else CC_LAUNCH4(8);
@@ -656,7 +640,7 @@ int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
   if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
   hipLaunchKernelGGL(k_apply_value_v3<256>, dim3(a.sb_val), dim3(V3A<256>::T), 0, st,
                      reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
-                     a.rst_status, a.rst_value, a.dummy, a.err, a.out_status + a.lo, a.out_value + a.lo);
+                     a.rst_status, a.rst_value, a.dummy, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
