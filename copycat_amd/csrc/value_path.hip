@@ -146,6 +146,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
   const uint32_t hw = (sb + 1) / 2;
   uint32_t T = blockIdx.x;
   if (T >= tiles) return;
+  PH_DECL
   uint32_t ri[kP4J], ob[kP4J], fb[kP4J];
   uint64_t av[kP4J], bv[kP4J];
   auto rowq = [&](int j) -> uint32_t { return w * (kWave * kP4J) + (uint32_t)j * kWave + l; };
@@ -181,7 +182,9 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
       const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
       loc[j] = r[j] != kNoRes ? (atomicAdd(&wc[w][k >> 1], 1u << sh) >> sh) & 0xFFFFu : 0xFFFFu;
     }
+    PH(0);
     lds_barrier();  // B1: counters complete
+    PH(1);
     if (w == 0) {   // per super-bucket: exclusive prefix over the waves (in place), totals, tile-local run starts
       uint32_t tot[KP];
 #pragma unroll
@@ -224,7 +227,9 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
         row[sb] = (uint16_t)inc;
       }
     }
+    PH(2);
     lds_barrier();  // B2: prefixes and run starts
+    PH(3);
 #pragma unroll
     for (int j = 0; j < kP4J; ++j) {
       const uint32_t q = rowq(j);
@@ -239,13 +244,19 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
     }
     const uint32_t Tn = T + gridDim.x;
     if (Tn < tiles) load(Tn);  // the raw registers are free: the next tile's loads fly during the write-out
+    PH(4);
     lds_barrier();             // B3: the image is complete
+    PH(5);
     // whole tile region, unconditionally (a fixed store count; rows past the live count are never read)
 #pragma unroll
     for (int m = 0; m < kP4J; ++m) st_rec[tbase + t + m * kP4T] = img[t + m * kP4T];
+    PH(6);
     if (Tn >= tiles) break;
     T = Tn;
   }
+#ifdef CC_PHASE_TIMING
+  PH_FLUSH(g_ph_v3p);
+#endif
 }
 
 // ---- k_apply_value_v3: walker / loader waves (apply_value.hip k_apply_value_ws) over 16-byte records -----------

@@ -15,11 +15,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 OUT = os.path.join(ROOT, "copycat_amd", "diag", "libcopycat_apply_phase.so")
-PHASES_PARTV = ["prologue", "rank", "scan(1 wave)", "place+issue", "write-out", "-", "-", "-"]  # CC_PART_VALUE=1
 PHASES = {
     0: ["histogram+row", "rank+wait", "wave-prefix", "exscan", "place", "write-out", "top(clear,issue)", "-"],
-    1: ["setup", "rank+wait", "wave-prefix", "slot-scan", "place", "walk", "result-store", "-"] if os.environ.get("CC_APPLY_V1") else
-       ["W walk", "W wait", "L result store", "L rank", "L barriers", "L clear+bases", "L place", "L load issue"],
+    1: ["W walk", "W wait", "L result store", "L rank", "L barriers", "L clear+bases", "L place", "L load issue"],
     2: ["load", "scatter", "-", "-", "-", "-", "-", "-"],
     5: ["setup", "rank+wait", "slot-scan", "gather", "walk", "event-flush", "-", "-"],
     3: ["region-load+list", "chunk-load", "binding", "lookup+orphans", "sort", "scan-apply", "cmp-runs+clear",
@@ -75,16 +73,11 @@ def run(args):
     sub = args.sub_batch or (16 << 20)
     launches = args.steps * ((n + sub - 1) // sub)
     tiles = (n + 16383) // 16384
-    if os.environ.get("CC_PART_VALUE"):
-        PHASES[0] = PHASES_PARTV
-    if os.environ.get("CC_V3_PHASES"):  # value_path.hip: k_part_v3 (two 512-thread workgroups per CU, 8192-commit tiles)
-        PHASES[0] = ["prologue loads+gather+hist", "encode+rank+issue", "B1+wave scan", "B2+place+cpos",
-                     "B3+write-out+clear", "B4+tpos", "-", "-"]
+    if os.environ.get("CC_V3_PHASES"):  # value_path.hip: k_part_v4 (one 1024-thread workgroup per CU, 8192-commit tiles)
+        PHASES[0] = ["loads wait+gather+rank", "B1", "wave-0 scan", "B2", "place+cpos+issue next",
+                     "B3", "write-out", "-"]
         tiles = (n + 8191) // 8192
-    if os.environ.get("CC_PART_V2_PHASES"):  # k_part_v2 (one workgroup per tile)
-        PHASES[0] = ["prologue loads+gather", "histogram+row", "encode+rank", "issue next+barrier", "wave scan",
-                     "place+cpos", "write-out+clear", "-"]
-    wgs = {0: min(tiles, 256) * launches if os.environ.get("CC_PART_VALUE") else tiles * args.steps, 1: 256 * launches, 2: min(tiles, 256) * launches}
+    wgs = {0: tiles * args.steps, 1: 256 * launches, 2: min(tiles, 256) * launches}
     names = {0: "k_part_tile", 1: "k_apply_value", 2: "k_unpermute"}
     for k in range(3):
         rc = L.cc_debug_phases(E.h, k, ticks)
