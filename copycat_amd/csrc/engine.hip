@@ -99,7 +99,7 @@ static void free_all(cc_engine* e) {
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
                   e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp,
-                  e->d_szq,      e->d_szq_n};
+                  e->d_szq,      e->d_szq_n,    e->d_bar_rows, e->d_fb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -699,10 +699,24 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     }
     if (nb > kBarCap)
       return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) and group schedules in one batch than kBarCap");
-    if (nb) {
+    if (nb) {  // the barrier rows in log order, then their columns in one gather (one copy back, not one per field)
       e->bars.resize(nb);
       HIPCHECK(hipMemcpy(e->bars.data(), e->d_bar, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost));
       std::sort(e->bars.begin(), e->bars.end());
+      if (nb > e->bar_rows_cap) {
+        if (e->d_bar_rows) HIPCHECK(hipFree(e->d_bar_rows));
+        e->d_bar_rows = nullptr;
+        e->bar_rows_cap = 0;
+        HIPCHECK(hipMalloc(&e->d_bar_rows, sizeof(BarRow) * nb));
+        e->bar_rows_cap = nb;
+      }
+      HIPCHECK(hipMemcpyAsync(e->d_bar, e->bars.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, st));
+      if (launch_bar_fields(e->d_bar, nb, c->inst, c->op, c->flags, c->a, c->key, c->aux, c->index, c->time,
+                            e->d_bar_rows, st))
+        return set_err(CC_ERR_HIP, "barrier rows gather launch", hipGetLastError());
+      e->bar_rows.resize(nb);
+      HIPCHECK(hipMemcpyAsync(e->bar_rows.data(), e->d_bar_rows, sizeof(BarRow) * nb, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
     }
   }
   if (e->coord_on || e->ttl_live) {  // events of this batch start at 0; the log clock must not go backwards inside it
@@ -711,35 +725,51 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (!e->bars.empty() && launch_time_check(c->time, n, e->d_clock, e->d_err, st))
       return set_err(CC_ERR_HIP, "time check", hipGetLastError());
   }
-  // Group timers: where each pending one fires in this batch (the clock at row r is max(clock_before, time[r])).
+  // Group timers: where each pending one fires in this batch, and where the timer of each schedule row of the batch
+  // would (the clock at row r is max(clock_before, time[r])): the first row r >= from whose clock reaches the deadline
+  // -> the boundary the timer fires at (manager mode: after row r; module mode: before it, A8), or ~0 when no row of
+  // this batch reaches it.  One device search for all of them (k_fire_bounds).
   const bool deferred = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) != 0;
-  auto time_at = [&](uint64_t r, uint64_t& t) -> int {
-    t = clock_before;
-    if (c->time) {
-      HIPCHECK(hipMemcpy(&t, c->time + r, sizeof t, hipMemcpyDeviceToHost));
-      t = std::max(t, clock_before);
+  auto clock_at = [&](const BarRow& br) { return c->time ? std::max(br.t_row, clock_before) : clock_before; };
+  std::vector<uint64_t> sched_dl(e->bars.size(), 0), sched_fb(e->bars.size(), ~0ull);  // per barrier (schedule rows)
+  {
+    std::vector<uint64_t> dl, from;
+    std::vector<uint32_t> who;  // < gtimers.size(): a pending timer; else gtimers.size() + barrier index
+    for (size_t q = 0; q < e->gtimers.size(); ++q) {
+      dl.push_back(e->gtimers[q].deadline);
+      from.push_back(0);
+      who.push_back((uint32_t)q);
     }
-    return CC_OK;
-  };
-  // first row r >= from whose clock reaches d -> the boundary the timer fires at (manager mode: after row r;
-  // module mode: before it, A8), or ~0 when no row of this batch reaches it
-  auto fire_boundary = [&](uint64_t d, uint64_t from, uint64_t& b) -> int {
-    b = ~0ull;
-    uint64_t lo_r = from, hi_r = n;  // search [lo_r, hi_r)
-    while (lo_r < hi_r) {
-      const uint64_t mid = (lo_r + hi_r) / 2;
-      uint64_t t = 0;
-      int rc = time_at(mid, t);
-      if (rc) return rc;
-      if (t >= d) hi_r = mid;
-      else lo_r = mid + 1;
+    for (size_t k = 0; k < e->bars.size(); ++k) {
+      const BarRow& br = e->bar_rows[k];
+      if (br.op != CC_OP_GROUP_SCHEDULE) continue;
+      const uint64_t delay = c->aux ? br.aux : 0;
+      sched_dl[k] = clock_at(br) + ((int64_t)delay > 0 ? delay : 0);  // schedule :86-103
+      dl.push_back(sched_dl[k]);
+      from.push_back(deferred ? e->bars[k] : (uint64_t)e->bars[k] + 1);
+      who.push_back((uint32_t)(e->gtimers.size() + k));
     }
-    if (lo_r < n) b = deferred ? lo_r + 1 : lo_r;
-    return CC_OK;
-  };
-  for (auto& gt : e->gtimers) {
-    int rc = fire_boundary(gt.deadline, 0, gt.fire_b);
-    if (rc) return rc;
+    const uint32_t m = (uint32_t)dl.size();
+    if (m) {
+      if (m > e->fb_cap) {
+        if (e->d_fb) HIPCHECK(hipFree(e->d_fb));
+        e->d_fb = nullptr;
+        e->fb_cap = 0;
+        HIPCHECK(hipMalloc(&e->d_fb, sizeof(uint64_t) * 3 * m));
+        e->fb_cap = m;
+      }
+      std::vector<uint64_t> res(m);
+      HIPCHECK(hipMemcpyAsync(e->d_fb, dl.data(), 8ull * m, hipMemcpyHostToDevice, st));
+      HIPCHECK(hipMemcpyAsync(e->d_fb + m, from.data(), 8ull * m, hipMemcpyHostToDevice, st));
+      if (launch_fire_bounds(c->time, n, clock_before, e->d_fb, e->d_fb + m, m, deferred, e->d_fb + 2 * m, st))
+        return set_err(CC_ERR_HIP, "timer bounds launch", hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(res.data(), e->d_fb + 2 * m, 8ull * m, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      for (uint32_t i = 0; i < m; ++i) {
+        if (who[i] < e->gtimers.size()) e->gtimers[who[i]].fire_b = res[i];
+        else sched_fb[who[i] - e->gtimers.size()] = res[i];
+      }
+    }
   }
   if (e->map_bits && !e->ttl_live) {  // the batch's hot map keys (apply_map_hot.hip): counted once, bound per sub-batch
     HotArgs hb{};
@@ -1108,43 +1138,36 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if (action == 0) break;
   {  // the barrier row, against the state as it stands after the rows before it
     const uint64_t row = seg_hi;
+    const BarRow& br = e->bar_rows[bi];
+    const size_t bk = bi;
     cur = row + 1;
     ++bi;
-    uint32_t in = 0, res = 0;
-    uint8_t op = 0, fl = 0;
-    uint64_t a = 0;
-    HIPCHECK(hipMemcpy(&in, c->inst + row, sizeof in, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(&op, c->op + row, 1, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(&fl, c->flags + row, 1, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(&a, c->a + row, sizeof a, hipMemcpyDeviceToHost));
+    uint32_t res = 0;
+    const uint32_t in = br.inst;
+    const uint8_t op = br.op, fl = br.flags;
+    const uint64_t a = br.a;
     // (k_map_barriers listed the row through the device registry; the host mirror must agree before its slot
     // indexes any per-resource array)
     if (row >= n || in >= e->cfg.max_instances || (res = e->inst_res[in]) >= e->cfg.max_resources ||
         !(is_keyed(e->res_type[res]) || e->res_type[res] == CC_RES_GROUP))
       return set_err(CC_ERR_STATE, "barrier row does not resolve to a map / set / multimap / group on the host registry");
     if (e->res_type[res] == CC_RES_GROUP) {  // schedule :86-103 (member = key, callback = a, delay = aux)
-      uint64_t member = 0, delay = 0;
-      HIPCHECK(hipMemcpy(&member, c->key + row, sizeof member, hipMemcpyDeviceToHost));
-      if (c->aux) HIPCHECK(hipMemcpy(&delay, c->aux + row, sizeof delay, hipMemcpyDeviceToHost));
+      const uint64_t member = br.key;
       if (launch_group_schedule(e->d_coord, e->coord_cap, res, member, row, out->status, out->value, e->d_ttl_seen, st))
         return set_err(CC_ERR_HIP, "group schedule launch", hipGetLastError());
       uint32_t found = 0;
       HIPCHECK(hipMemcpyAsync(&found, e->d_ttl_seen, sizeof found, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
       if (found) {
-        uint64_t now = 0;
-        int rc = time_at(row, now);
-        if (rc) return rc;
         cc_engine::GroupTimer gt{};
-        gt.deadline = now + ((int64_t)delay > 0 ? delay : 0);
+        gt.deadline = sched_dl[bk];
         gt.id = ++e->gtimer_seq;
         gt.member = member;
         gt.tag = CC_FLAG_TAG_A(fl);
         gt.payload = gt.tag == CC_TAG_NULL ? 0 : a;
         gt.slot = res;
-        if (c->index) HIPCHECK(hipMemcpy(&gt.idx, c->index + row, sizeof gt.idx, hipMemcpyDeviceToHost));
-        rc = fire_boundary(gt.deadline, deferred ? row : row + 1, gt.fire_b);
-        if (rc) return rc;
+        gt.idx = br.idx;
+        gt.fire_b = sched_fb[bk];
         e->gtimers.push_back(gt);
       }
       continue;
@@ -1164,10 +1187,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (e->ttl_live) {  // the clock at which the reference last fired timers before this row (A8)
       uint64_t t0 = clock_before, t1 = clock_before;
       if (c->time) {
-        HIPCHECK(hipMemcpy(&t1, c->time + row, sizeof t1, hipMemcpyDeviceToHost));
-        if (row > 0) HIPCHECK(hipMemcpy(&t0, c->time + row - 1, sizeof t0, hipMemcpyDeviceToHost));
-        t0 = std::max(t0, clock_before);
-        t1 = std::max(t1, clock_before);
+        t1 = std::max(br.t_row, clock_before);
+        if (row > 0) t0 = std::max(br.t_prev, clock_before);
       }
       mw.tbl_dl = e->d_tbl_dl;
       mw.fire_clock = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? t0 : t1;

@@ -402,6 +402,24 @@ struct CloseArgs {
 };
 int launch_close(const CloseArgs& a, hipStream_t st);
 
+// One barrier row's columns, gathered on the device at the start of a batch (k_bar_fields): the host walks the
+// batch's barrier rows from these instead of one blocking copy per field per row.
+struct BarRow {
+  uint64_t a, key, aux, idx;
+  uint64_t t_prev, t_row;  // time[row - 1], time[row] (0 without a time column / at row 0)
+  uint32_t inst;
+  uint8_t op, flags, pad0, pad1;
+  uint32_t pad2, pad3;
+};
+static_assert(sizeof(BarRow) == 64, "BarRow");
+int launch_bar_fields(const uint32_t* rows, uint32_t nb, const uint32_t* inst, const uint8_t* op, const uint8_t* flags,
+                      const uint64_t* a, const uint64_t* key, const uint64_t* aux, const uint64_t* index,
+                      const uint64_t* time, BarRow* out, hipStream_t st);
+// Group-timer fire boundaries, one device binary search per timer over the batch's time column: the first row r >=
+// from[i] whose clock max(clock_before, time[r]) reaches deadline[i] -> r (+1 when timers are deferred), or ~0.
+int launch_fire_bounds(const uint64_t* time, uint64_t n, uint64_t clock_before, const uint64_t* deadline,
+                       const uint64_t* from, uint32_t m, bool deferred, uint64_t* out, hipStream_t st);
+
 struct UnpermuteArgs {
   const uint16_t* cpos;
   const uint16_t* ttab;

@@ -139,6 +139,11 @@ struct cc_engine {
   uint32_t* d_hot_cand_n = nullptr;
   // whole-map ops (map_wide.hip): barrier rows of the current batch, per-map peak-size bounds, scratch
   uint32_t* d_bar = nullptr;       // [kBarCap]
+  BarRow* d_bar_rows = nullptr;    // [bar_rows_cap] the batch's barrier rows' columns (k_bar_fields)
+  uint32_t bar_rows_cap = 0;
+  std::vector<BarRow> bar_rows;    // host copy, in row order (= bars)
+  uint64_t* d_fb = nullptr;        // [3 * fb_cap] group-timer fire-bound search: deadlines, search starts, results
+  uint32_t fb_cap = 0;
   uint32_t* d_bar_n = nullptr;
   uint32_t* d_mw_peak = nullptr;   // [max_resources]
   uint64_t* d_mw_drop = nullptr;   // [max_resources]

@@ -131,6 +131,63 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
   }
 }
 
+// The barrier rows' columns in one launch (the host then reads them with one copy per batch).
+__global__ void k_bar_fields(const uint32_t* __restrict__ rows, uint32_t nb, const uint32_t* __restrict__ inst,
+                             const uint8_t* __restrict__ op, const uint8_t* __restrict__ flags,
+                             const uint64_t* __restrict__ a, const uint64_t* __restrict__ key,
+                             const uint64_t* __restrict__ aux, const uint64_t* __restrict__ index,
+                             const uint64_t* __restrict__ time, BarRow* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  const uint32_t r = rows[i];
+  BarRow b{};
+  b.inst = inst[r];
+  b.op = op[r];
+  b.flags = flags[r];
+  b.a = a[r];
+  b.key = key ? key[r] : 0;
+  b.aux = aux ? aux[r] : 0;
+  b.idx = index ? index[r] : 0;
+  b.t_row = time ? time[r] : 0;
+  b.t_prev = time && r > 0 ? time[r - 1] : 0;
+  out[i] = b;
+}
+
+int launch_bar_fields(const uint32_t* rows, uint32_t nb, const uint32_t* inst, const uint8_t* op, const uint8_t* flags,
+                      const uint64_t* a, const uint64_t* key, const uint64_t* aux, const uint64_t* index,
+                      const uint64_t* time, BarRow* out, hipStream_t st) {
+  if (nb == 0) return 0;
+  hipLaunchKernelGGL(k_bar_fields, dim3((nb + 255) / 256), dim3(256), 0, st, rows, nb, inst, op, flags, a, key, aux, index,
+                     time, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The clock at row r is max(clock_before, time[r]) (non-decreasing: k_time_check / k_part_ext fail a batch whose
+// time column goes backwards), so the first row reaching a deadline is a binary search.
+__global__ void k_fire_bounds(const uint64_t* __restrict__ time, uint64_t n, uint64_t clock_before,
+                              const uint64_t* __restrict__ deadline, const uint64_t* __restrict__ from, uint32_t m,
+                              bool deferred, uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t d = deadline[i];
+  uint64_t lo = from[i], hi = n;  // search [lo, hi)
+  while (lo < hi) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    const uint64_t t = time ? (time[mid] > clock_before ? time[mid] : clock_before) : clock_before;
+    if (t >= d) hi = mid;
+    else lo = mid + 1;
+  }
+  out[i] = lo < n ? (deferred ? lo + 1 : lo) : ~0ull;
+}
+
+int launch_fire_bounds(const uint64_t* time, uint64_t n, uint64_t clock_before, const uint64_t* deadline,
+                       const uint64_t* from, uint32_t m, bool deferred, uint64_t* out, hipStream_t st) {
+  if (m == 0) return 0;
+  hipLaunchKernelGGL(k_fire_bounds, dim3((m + 255) / 256), dim3(256), 0, st, time, n, clock_before, deadline, from, m,
+                     deferred, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // An entry is live at the barrier row: present, and no TTL timer of it has fired by then.
 __device__ inline bool live_at(uint32_t w, const uint64_t* __restrict__ dl, uint64_t e, uint64_t fire) {
   if (!(w & kMwPresent)) return false;
