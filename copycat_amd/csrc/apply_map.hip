@@ -140,7 +140,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
                                                   const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ rst_msz, uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ rst_msz, TtlEmit te, uint32_t* __restrict__ err_out) {
   constexpr int MT = TTL ? 512 : CC_MAP_MT;  // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
   constexpr int MEPer = kMapRegion / MT;  // table entries per thread
   constexpr int kMPer = TTL ? 1 : CC_MAP_CHUNK / CC_MAP_MT;  // commits per thread per chunk
@@ -644,12 +644,14 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         const u64x2 x = rab[s];
         uint64_t rv;
         bool wrote, created;
-        const int was = (wv & kMwPresent) != 0;
         if (TTL && dl && dl <= rfire[s]) {  // the timer fired: map.remove(key) (MapState.java:91-93)
+          // (its size event, if this sub-batch owns the boundary it fired at: common.h TtlEmit)
+          if ((wv & kMwPresent) && te.ev_key) ttl_expiry_event(te, clock_base ? *clock_base : 0, wv, tkey[e], dl, err);
           wv &= ~(kMwPresent | kMwVtagMask);
           vv = 0;
           dl = 0;
         }
+        const int was = (wv & kMwPresent) != 0;  // (after the expiry: the commit's own change)
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, wv, vv, rv, wrote, created);
         if (TTL) {  // a stored commit cancels the old timer and arms its own; a removal cancels it
           if (wrote) dl = rdl[s];
@@ -719,11 +721,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.ttl)
     hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
-                       a.rst_status, a.rst_value, a.rst_msz, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, a.err);
   else
     hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
-                       a.rst_status, a.rst_value, a.rst_msz, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -307,7 +307,7 @@ struct SmallMap {
 };
 constexpr uint32_t kSmIn = 1u;       // the table is still small (capacity <= 64): tracked key by key
 constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin while tracked
-constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (TTL mode: timers remove keys unseen)
+constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (snapshots of round-4 engines before TTL-mode tracking)
 // per-map flags of the batch (cc_engine::d_msmall): bit 0 the table is small (events followed key by key), bit 1 the
 // batch asks the map's size / isEmpty (events followed for the in-stream answers); either keeps the map's keys out of
 // hot-key routing, so every such commit is a region record
@@ -315,6 +315,66 @@ constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
 // a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
 __device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
   return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);
+}
+
+// log2(HashMap capacity / 16) after the size peaked at p (resize doubles the table when ++size > 0.75 capacity)
+__host__ __device__ inline uint32_t cap_level(uint64_t p) {
+  uint32_t lv = 0;
+  for (uint64_t thr = 12; p > thr; thr <<= 1) ++lv;
+  return lv;
+}
+
+// ---- TTL mode: map timers as size events (map_small.hip) -------------------------------------------------------
+// In TTL mode a map's size also drops when a timer fires (MapState.java:91-93: the scheduled map.remove(key)), with no
+// commit.  Every expiry becomes an event at the boundary where the reference fires it: the first row of the batch
+// whose clock max(clock_before, time[r]) reaches the deadline, before that row (module mode) or after it (manager
+// mode, deferred: boundary r + 1).  Events are keyed map << 44 | position << 4 | code, position 2 * (row
+// - lo) + 1 for a commit of row `row`, 2 * (b - lo) for boundary b (before row b), code 1 insert / 2 remove, so a
+// radix sort puts each map's commits and expiries in log order.  A sub-batch [lo, hi) owns the boundaries [bl, bh]:
+// bh = hi, bl = lo at the batch start and after a barrier row, lo + 1 after another sub-batch (which owned lo).
+struct TtlEmit {
+  const uint64_t* time;   // the batch's time column (null: the clock is clock_before throughout)
+  uint64_t n;             // rows in the batch
+  uint64_t lo, bl, bh;
+  uint64_t adv;           // cc_advance_time: every timer due in (clock_before, adv] fires, at position 0 (0: a batch)
+  uint32_t deferred;
+  const uint64_t* hh_key;  // String.hashCode of HANDLE keys (java_key_hash)
+  const int32_t* hh_val;
+  uint32_t hh_n;
+  uint64_t* ev_key;        // the event buffer shared with launch_map_size's emission (SmallArgs::ev_key / ev_val)
+  uint32_t* ev_val;
+  uint32_t ev_cap;
+  uint32_t* ctl;           // ctl[0]: events appended
+};
+
+// One expiry of entry (word w, key) whose timer has deadline d, if the sub-batch owns its firing boundary.
+__device__ inline void ttl_expiry_event(const TtlEmit& t, uint64_t cb, uint32_t w, uint64_t key, uint64_t d,
+                                        uint32_t& err) {
+  if (d <= cb) return;  // fired by the end of an earlier batch (or cc_advance_time)
+  uint64_t pos = 0;
+  if (t.adv) {
+    if (d > t.adv) return;
+  } else {
+    uint64_t a = 0, b = t.n;  // the first row whose clock reaches d
+    while (a < b) {
+      const uint64_t mid = a + (b - a) / 2;
+      const uint64_t c = t.time ? (t.time[mid] > cb ? t.time[mid] : cb) : cb;
+      if (c >= d) b = mid;
+      else a = mid + 1;
+    }
+    if (a >= t.n) return;  // not due in this batch
+    const uint64_t bd = t.deferred ? a + 1 : a;
+    if (bd < t.bl || bd > t.bh) return;
+    pos = bd > t.lo ? 2 * (bd - t.lo) : 0;  // (a boundary before the sub-batch's first row: before all of it)
+  }
+  bool ok;
+  const uint32_t jh = java_key_hash((w >> 17) & 3, key, t.hh_key, t.hh_val, t.hh_n, ok);
+  if (!ok) err |= kErrHandleHash;
+  const uint32_t at = atomicAdd(t.ctl, 1u);
+  if (at < t.ev_cap) {
+    t.ev_key[at] = ((uint64_t)(w & kMwSlotMask) << 44) | ((pos & ((1ull << 40) - 1)) << 4) | 2u;
+    t.ev_val[at] = jh;
+  }
 }
 
 // extended staging (partition.hip) options

@@ -132,19 +132,32 @@ static int ensure_leak(cc_engine* e, uint64_t need) {
   return CC_OK;
 }
 
-// The small-map event buffers (map_small.hip): one event per map commit of a sub-batch at most, sorted by hipcub.
+// The map event buffers (map_small.hip), sorted by hipcub: one event per map commit of a sub-batch at most; in TTL
+// mode also one per expiry (at most one per commit that sees its key's timer fired, plus one per table entry).
+static uint64_t small_cap_needed(const cc_engine* e) {
+  return e->ttl_live ? 2 * e->sub_batch + e->map_entries : e->sub_batch;
+}
 static int ensure_small(cc_engine* e) {
-  if (e->d_sm_key) return CC_OK;
-  const uint64_t cap = e->sub_batch;
+  const uint64_t cap = small_cap_needed(e);
+  if (e->d_sm_key && e->sm_cap >= cap) return CC_OK;
+  if (cap > 0xFFFFFFFFull) return set_err(CC_ERR_CAPACITY, "map event buffer beyond 2^32 entries");
+  if (e->d_sm_key) {  // grown (TTL mode): the counters keep their buffer, the events are rebuilt per sub-batch
+    void* ps[] = {e->d_sm_key, e->d_sm_key2, e->d_sm_val, e->d_sm_val2, e->d_sm_temp};
+    for (void* p : ps) (void)hipFree(p);
+    e->d_sm_key = e->d_sm_key2 = nullptr;
+    e->d_sm_val = e->d_sm_val2 = nullptr;
+    e->d_sm_temp = nullptr;
+  }
   const size_t tb = std::max<size_t>(small_sort_temp_bytes((uint32_t)cap), 256);
   hipError_t x = hipMalloc(&e->d_sm_key, 8 * cap);
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_key2, 8 * cap);
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_val, 4 * cap);
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_val2, 4 * cap);
-  if (x == hipSuccess) x = hipMalloc(&e->d_sm_seg, 4ull * (e->cfg.max_resources + 1));
+  if (x == hipSuccess && !e->d_sm_seg) x = hipMalloc(&e->d_sm_seg, 4ull * (e->cfg.max_resources + 1));
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_temp, tb);
-  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc small-map events", x);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events", x);
   e->sm_temp_bytes = tb;
+  e->sm_cap = cap;
   return CC_OK;
 }
 
@@ -470,9 +483,9 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
     // MapState's table followed key by key while small (map_small.hip); sets / multimaps have no order-dependent op
     std::vector<SmallMap> sm(count);
     const bool is_map = type == CC_RES_MAP;
-    for (auto& x : sm) x.flags = is_map ? (e->ttl_live ? kSmUnknown : kSmIn) : 0u;
+    for (auto& x : sm) x.flags = is_map ? kSmIn : 0u;  // (TTL mode too: its commit + expiry events are replayed)
     HIPCHECK(hipMemcpy(e->d_msm + first, sm.data(), sizeof(SmallMap) * count, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemset(e->d_msmall + first, is_map && !e->ttl_live ? 1 : 0, count));
+    HIPCHECK(hipMemset(e->d_msmall + first, is_map ? 1 : 0, count));
     if (is_map && !e->ttl_live) e->small_live = true;
   }
   // fresh state: AtomicValueState() {value = null; current = null}
@@ -616,6 +629,67 @@ static const bool g_dbg_sync = getenv("CC_DEBUG_SYNC") != nullptr;
     }                                                                                           \
   } while (0)
 
+// TTL mode: the map events appended so far (commits, expiries) -> every map's size and capacity, the small maps' key
+// sets (map_small.hip: sort, runs, k_small_replay + k_ttl_replay), then the counters for the next round.
+static int ttl_replay(cc_engine* e, hipStream_t st) {
+  uint32_t ctl[2] = {0, 0};
+  HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  SmallArgs sa{};
+  sa.ev_key = e->d_sm_key;
+  sa.ev_key2 = e->d_sm_key2;
+  sa.ev_val = e->d_sm_val;
+  sa.ev_val2 = e->d_sm_val2;
+  sa.cap = (uint32_t)e->sm_cap;
+  sa.temp = e->d_sm_temp;
+  sa.temp_bytes = e->sm_temp_bytes;
+  sa.ctl = e->d_sm_ctl;
+  sa.seg = e->d_sm_seg;
+  sa.nseg = e->d_sm_seg + e->cfg.max_resources;
+  sa.state = e->d_msm;
+  sa.msmall = e->d_msmall;
+  sa.mpcap = e->d_mpcap;
+  sa.max_resources = e->cfg.max_resources;
+  sa.msize = e->d_msize;
+  const int rs = launch_small_replay(sa, ctl[0], st);
+  if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "TTL map events launch", hipGetLastError())
+                          : set_err(CC_ERR_STATE, "TTL map events exceed their buffer");
+  if (launch_small_finish(sa, st)) return set_err(CC_ERR_HIP, "map event counters", hipGetLastError());
+  return CC_OK;
+}
+
+static TtlEmit ttl_emit_args(const cc_engine* e, const uint64_t* time, uint64_t n, uint64_t lo, uint64_t bl, uint64_t bh,
+                             uint64_t adv) {
+  TtlEmit t{};
+  t.time = time;
+  t.n = n;
+  t.lo = lo;
+  t.bl = bl;
+  t.bh = bh;
+  t.adv = adv;
+  t.deferred = (e->cfg.flags & CC_CFG_TIMERS_DEFERRED) ? 1u : 0u;
+  t.hh_key = e->d_hh_key;
+  t.hh_val = e->d_hh_val;
+  t.hh_n = e->hh_n;
+  t.ev_key = e->d_sm_key;
+  t.ev_val = e->d_sm_val;
+  t.ev_cap = (uint32_t)e->sm_cap;
+  t.ctl = e->d_sm_ctl;
+  return t;
+}
+
+// TTL mode: the expiries of the boundaries [bl, bh] that no sub-batch owned (before a barrier row, at the batch end),
+// or every timer due by `adv` (cc_advance_time), as size events.
+static int ttl_flush(cc_engine* e, const uint64_t* time, uint64_t n, uint64_t bl, uint64_t bh, uint64_t adv,
+                     hipStream_t st) {
+  int rc = ensure_small(e);
+  if (rc) return rc;
+  const TtlEmit te = ttl_emit_args(e, time, n, bl, bl, bh, adv);
+  if (launch_ttl_scan(te, e->d_clock, e->d_tbl_word, e->d_tbl_key, e->d_tbl_dl, e->map_entries, e->d_err, st))
+    return set_err(CC_ERR_HIP, "TTL scan launch", hipGetLastError());
+  return ttl_replay(e, st);
+}
+
 extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const cc_results* out, const cc_events* ev,
                               void* stream) {
   if (!e || !c || !out) return set_err(CC_ERR_INVALID, "null argument");
@@ -680,11 +754,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       e->szq_n = qn;
       break;
     }
-    if (ttl_seen && !e->ttl_live) {  // TTL mode for good: the small maps' key sets stop being followed
+    if (ttl_seen && !e->ttl_live) {  // TTL mode for good: sizes and capacities from commit + expiry events
       e->ttl_live = true;
-      if (e->small_live && launch_small_ttl(e->d_msm, e->d_msmall, e->cfg.max_resources, st))
-        return set_err(CC_ERR_HIP, "small-map TTL launch", hipGetLastError());
-      e->small_live = false;
+      e->small_live = false;  // (every map's events are replayed in TTL mode, the small ones' key sets included)
     }
     // The leak log (commits dropped without clean()) is drained before every batch of an engine that can add to it:
     // every multimap put, and with value events every re-listen (AtomicValueState.listen :41-49) may land there, at
@@ -788,6 +860,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   }
   uint64_t cur = 0;
   size_t bi = 0;
+  uint64_t own_lo = 0;  // TTL mode: the first timer-firing boundary no sub-batch has owned yet (common.h TtlEmit)
   for (;;) {
   // the next thing in log order: a barrier row, or a group timer firing (timers first at the same boundary)
   const uint64_t bar_b = bi < e->bars.size() ? (uint64_t)e->bars[bi] : ~0ull;
@@ -949,8 +1022,55 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.rst_msz = e->d_rst_msz;
       ma.err = e->d_err;
       ma.mark = marker_of(e);
+      TtlEmit te{};
+      if (e->ttl_live) {  // this sub-batch owns the timer-firing boundaries [own_lo, hi] (common.h TtlEmit)
+        int rc = ensure_small(e);
+        if (rc) return rc;
+        te = ttl_emit_args(e, c->time, n, lo, own_lo, hi, 0);
+        ma.ttl_emit = te;
+      }
       if (launch_apply_map(ma, st)) return set_err(CC_ERR_HIP, "map apply launch", hipGetLastError()); DBG_SYNC("map apply launch");
-      if (!e->ttl_live) {  // exact map sizes and HashMap capacities (containsValue's iteration order)
+      if (e->ttl_live) {  // exact sizes and capacities in TTL mode: the sub-batch's commits and expiries as events
+        if (launch_ttl_scan(te, e->d_clock, e->d_tbl_word, e->d_tbl_key, e->d_tbl_dl, e->map_entries, e->d_err, st))
+          return set_err(CC_ERR_HIP, "TTL scan launch", hipGetLastError());
+        MapSizeArgs za{};
+        za.ttab = e->d_ttab;
+        za.cpos = e->d_cpos;
+        za.tiles = tiles;
+        za.rows = hi - lo;
+        za.sb = e->sb_total();
+        za.k0 = e->sb;
+        za.k1 = e->sbq_base();
+        za.sb_hot = e->sb + (1u << e->map_bits);
+        za.rst_msz = e->d_rst_msz;
+        za.hot = e->d_hot;
+        za.hot_n = e->d_hot_n;  // (0: no hot keys in TTL mode)
+        za.hot_len = e->d_hot_len;
+        za.hot_rpre = e->d_hot_rpre;
+        za.hot_msz = e->d_hot_msz;
+        za.res_type = e->d_res_type;
+        za.max_resources = e->cfg.max_resources;
+        za.tcnt = e->d_msz_tcnt;
+        za.msize = e->d_msize;
+        za.mpcap = e->d_mpcap;
+        za.list = e->d_msz_list;
+        za.list_n = e->d_msz_list_n;
+        za.xrec = e->d_xrec;
+        za.hh_key = e->d_hh_key;
+        za.hh_val = e->d_hh_val;
+        za.hh_n = e->hh_n;
+        za.ev_key = e->d_sm_key;
+        za.ev_val = e->d_sm_val;
+        za.ev_cap = (uint32_t)e->sm_cap;
+        za.sm_ctl = e->d_sm_ctl;
+        za.map_row = e->d_map_row;
+        za.lo = lo;
+        za.err = e->d_err;
+        if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError());
+        own_lo = hi + 1;
+        int rc = ttl_replay(e, st);
+        if (rc) return rc;
+      } else {  // exact map sizes and HashMap capacities (containsValue's iteration order)
         MapSizeArgs za{};
         za.ttab = e->d_ttab;
         za.cpos = e->d_cpos;
@@ -986,7 +1106,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           za.hh_n = e->hh_n;
           za.ev_key = e->d_sm_key;
           za.ev_val = e->d_sm_val;
-          za.ev_cap = (uint32_t)e->sub_batch;
+          za.ev_cap = (uint32_t)e->sm_cap;
           za.sm_ctl = e->d_sm_ctl;
         }
         if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError()); DBG_SYNC("map size launch");
@@ -1001,7 +1121,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sz.inst_res = e->d_inst_res;
           sz.ev_key = e->d_sm_key;
           sz.ev_val = e->d_sm_val;
-          sz.cap = (uint32_t)e->sub_batch;
+          sz.cap = (uint32_t)e->sm_cap;
           sz.ctl = e->d_sm_ctl;
           sz.sorted_key = e->d_sm_key2;
           sz.sorted_val = e->d_sm_val2;
@@ -1021,7 +1141,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.ev_key2 = e->d_sm_key2;
           sa.ev_val = e->d_sm_val;
           sa.ev_val2 = e->d_sm_val2;
-          sa.cap = (uint32_t)e->sub_batch;
+          sa.cap = (uint32_t)e->sm_cap;
           sa.temp = e->d_sm_temp;
           sa.temp_bytes = e->sm_temp_bytes;
           sa.ctl = e->d_sm_ctl;
@@ -1135,13 +1255,26 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     cur = seg_hi;
     continue;
   }
-  if (action == 0) break;
+  if (action == 0) {
+    if (e->map_bits && e->ttl_live && own_lo <= n) {  // the boundaries after the last sub-batch (manager mode: row n)
+      int rc = ttl_flush(e, c->time, n, own_lo, n, 0, st);
+      if (rc) return rc;
+    }
+    break;
+  }
   {  // the barrier row, against the state as it stands after the rows before it
     const uint64_t row = seg_hi;
     const BarRow& br = e->bar_rows[bi];
     const size_t bk = bi;
     cur = row + 1;
     ++bi;
+    if (e->map_bits && e->ttl_live) {  // the timers that fire up to this row's boundary, as size events (TtlEmit)
+      if (own_lo <= row) {
+        int rc = ttl_flush(e, c->time, n, own_lo, row, 0, st);
+        if (rc) return rc;
+      }
+      own_lo = row + 1;
+    }
     uint32_t res = 0;
     const uint32_t in = br.inst;
     const uint8_t op = br.op, fl = br.flags;
@@ -1196,7 +1329,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.entries = e->map_entries;
     mw.peak_lo = e->d_mw_peak;
     mw.dropped = e->d_mw_drop;
-    mw.msize = e->ttl_live ? nullptr : e->d_msize;
+    mw.msize = e->d_msize;  // exact in both modes (TTL mode: commit + expiry events, map_small.hip)
     mw.mpcap = e->d_mpcap;
     mw.ctl = e->d_mw_ctl;
     mw.small = e->res_type[res] == CC_RES_MAP ? e->d_msm : nullptr;
@@ -1772,6 +1905,14 @@ extern "C" int cc_advance_time_events(cc_engine* e, uint64_t now, const cc_event
     }
     e->gtimers.erase(e->gtimers.begin(), e->gtimers.begin() + (ptrdiff_t)k);
     if (d_events) HIPCHECK(hipMemcpyAsync(d_events->count, e->d_ev_total, sizeof(uint64_t), hipMemcpyDeviceToDevice, e->own_stream));
+  }
+  if (e->map_bits && e->ttl_live) {  // map timers due by the new clock fire: their keys leave (sizes, small maps)
+    uint64_t clk = 0;
+    HIPCHECK(hipMemcpy(&clk, e->d_clock, sizeof clk, hipMemcpyDeviceToHost));
+    if (now > clk) {
+      rc = ttl_flush(e, nullptr, 0, 0, 0, now, e->own_stream);
+      if (rc) return rc;
+    }
   }
   if (launch_clock_advance(nullptr, 0, now, e->d_clock, e->own_stream)) return set_err(CC_ERR_HIP, "clock", hipGetLastError());
   HIPCHECK(hipStreamSynchronize(e->own_stream));

@@ -107,6 +107,7 @@ struct MapArgs {
   uint8_t* rst_status;
   uint64_t* rst_value;
   uint32_t* rst_msz;           // [sub_batch] each commit's map and size change (msz_word), staging order
+  TtlEmit ttl_emit;            // TTL mode: expiries the walk sees (a commit after its key's timer fired), as events
   uint32_t* err;
   Marker mark;
 };
@@ -149,6 +150,8 @@ struct MapSizeArgs {
   uint32_t* ev_val;            // [ev_cap] the key's HashMap hash
   uint32_t ev_cap;
   uint32_t* sm_ctl;            // [0] events emitted
+  const uint32_t* map_row;     // TTL mode: every map's commits emitted, positioned by batch row (common.h TtlEmit)
+  uint64_t lo;                 //   (the sub-batch's first row)
   uint32_t* err;
 };
 int launch_map_size(const MapSizeArgs& a, hipStream_t st);
@@ -165,7 +168,11 @@ struct SmallArgs {
   uint8_t* msmall;
   uint32_t* mpcap;
   uint32_t max_resources;
+  uint32_t* msize;             // TTL mode: every map's size / capacity from its events (k_ttl_replay); else null
 };
+// TTL mode: the table entries whose timers fire at a boundary the sub-batch owns -> expiry events (common.h TtlEmit)
+int launch_ttl_scan(const TtlEmit& t, const uint64_t* clock_base, const uint32_t* word, const uint64_t* key,
+                    const uint64_t* dl, uint64_t entries, uint32_t* err, hipStream_t st);
 int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st);  // sort, runs, replay (E events)
 int launch_small_finish(const SmallArgs& a, hipStream_t st);              // counters for the next sub-batch
 // size / isEmpty rows of the sub-batch [lo, hi): emitted into the event buffer before the sort (query entries), then
@@ -195,7 +202,6 @@ int launch_size_answer(const SizeArgs& a, hipStream_t st);
 int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st);
 size_t small_sort_temp_bytes(uint32_t cap);
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st);
-int launch_small_ttl(SmallMap* state, uint8_t* msmall, uint32_t R, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
 int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* map_row, hipStream_t st);
 

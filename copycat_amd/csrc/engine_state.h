@@ -159,11 +159,12 @@ struct cc_engine {
   SmallMap* d_msm = nullptr;       // [max_resources]
   uint8_t* d_msmall = nullptr;     // [max_resources] 1: in the window
   uint32_t* d_sm_ctl = nullptr;    // [4] events of the sub-batch, maps still in the window
-  uint64_t *d_sm_key = nullptr, *d_sm_key2 = nullptr;  // [sub_batch] events (allocated while a map is small)
+  uint64_t *d_sm_key = nullptr, *d_sm_key2 = nullptr;  // [sm_cap] map events (small / size-queried maps; TTL mode: all)
   uint32_t *d_sm_val = nullptr, *d_sm_val2 = nullptr;
   uint32_t* d_sm_seg = nullptr;    // [max_resources + 1] run starts + count
   void* d_sm_temp = nullptr;
   size_t sm_temp_bytes = 0;
+  uint64_t sm_cap = 0;             // events the buffers hold (engine.hip small_cap_needed)
   bool small_live = false;         // some map may still be in the window (the host then reads the event count)
   // map size / isEmpty rows answered in the stream (outside TTL mode; map_small.hip k_size_answer)
   uint32_t* d_szq = nullptr;       // [szq_cap] the batch's size / isEmpty rows

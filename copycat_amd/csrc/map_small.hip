@@ -25,6 +25,11 @@
 // the size-driven one and the early one (after the window both grow by size alone).
 // Cost: nothing once every map has left the window (the host stops looking: no event, no sync); while some are in
 // it, one host read of the event count per sub-batch, a sort of the events and one short wave walk per map.
+//
+// TTL mode (common.h TtlEmit): timers remove keys with no commit, so there every map's commits AND expiries are events
+// (an expiry positioned at the boundary where the reference fires the timer, A8), and after the sort k_ttl_replay
+// walks each map's run for its size and peak (capacity) while k_small_replay follows the small maps' key sets as
+// above: sizes, capacities and small tables stay exact in both modes.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -100,6 +105,70 @@ __global__ __launch_bounds__(256) void k_small_replay(const uint64_t* __restrict
   }
 }
 
+// ---- TTL mode: exact sizes and capacities with timers (common.h TtlEmit) ------------------------------------
+// Every table entry whose timer fires at a boundary this sub-batch owns (or, for cc_advance_time, by the new clock)
+// and was not seen expiring by a commit of the sub-batch (k_apply_map<true> emits those itself): an expiry event.  An
+// entry that expired is still in the table (its key is bound, lazily absent) until a commit or a compaction drops it;
+// the boundary ownership keeps every expiry to one event.
+__global__ void k_ttl_scan(TtlEmit t, const uint64_t* __restrict__ clock_base, const uint32_t* __restrict__ word,
+                           const uint64_t* __restrict__ key, const uint64_t* __restrict__ dl, uint64_t entries,
+                           uint32_t* __restrict__ err_out) {
+  const uint64_t cb = *clock_base;
+  uint32_t err = 0;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t d = dl[e];
+    if (!d) continue;
+    const uint32_t w = word[e];
+    if (!(w & kMwUsed) || (w & kMwDead) || !(w & kMwPresent)) continue;
+    ttl_expiry_event(t, cb, w, key[e], d, err);
+  }
+  if (err) atomicOr(err_out, err);
+}
+
+// One wave per map run of the sorted events: the size at the run's start (msize), the running size over its commits
+// and expiries in log order, its peak -> the capacity level (HashMap.resize never shrinks), the size at the end.
+__global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ ctl,
+                                                    const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
+                                                    uint32_t* __restrict__ msize, uint32_t* __restrict__ mpcap) {
+  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
+    const uint32_t start = seg[r];
+    const uint32_t m = (uint32_t)(key[start] >> 44);
+    int64_t size = msize[m], peak = size;
+    for (uint32_t b = start;; b += kWave) {
+      const uint32_t i = b + l;
+      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
+      const uint64_t k = in ? key[i] : 0;
+      const int32_t dlt = !in || (k & 8u) ? 0 : ((k & 3u) == 1u ? 1 : ((k & 3u) == 2u ? -1 : 0));
+      int32_t inc = dlt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      int32_t mx = inc;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+      peak = max(peak, size + mx);
+      size += __shfl(inc, 63, 64);
+      if (__ballot(in) != ~0ull) break;
+    }
+    if (l == 0) {
+      msize[m] = (uint32_t)max<int64_t>(size, 0);
+      atomicMax(&mpcap[m], cap_level((uint64_t)max<int64_t>(peak, 0)));
+    }
+  }
+}
+
+int launch_ttl_scan(const TtlEmit& t, const uint64_t* clock_base, const uint32_t* word, const uint64_t* key,
+                    const uint64_t* dl, uint64_t entries, uint32_t* err, hipStream_t st) {
+  if (entries == 0) return 0;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (entries + 255) / 256);
+  hipLaunchKernelGGL(k_ttl_scan, dim3(grid), dim3(256), 0, st, t, clock_base, word, key, dl, entries, err);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // maps still in the window (read by the host with the next sub-batch's event count)
 __global__ void k_small_count(const uint8_t* __restrict__ msmall, uint32_t R, uint32_t* __restrict__ ctl) {
   uint32_t c = 0;
@@ -115,15 +184,6 @@ __global__ void k_small_clear(SmallMap* __restrict__ st, uint32_t m) {
     st[m].flags &= ~kSmTree;
     st[m].tree_bins = 0;
   }
-}
-
-// TTL mode: timers remove keys without a commit, so the small maps' key sets are no longer known
-__global__ void k_small_ttl(SmallMap* __restrict__ st, uint8_t* __restrict__ msmall, uint32_t R) {
-  for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
-    if (msmall[m] & kMfSmall) {
-      st[m].flags |= kSmUnknown;
-      msmall[m] &= (uint8_t)~kMfSmall;
-    }
 }
 
 // ---- map size / isEmpty in the stream (MapState.size :233-239, isEmpty :244-250), outside TTL mode ---------------
@@ -245,6 +305,8 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
     hipLaunchKernelGGL(k_small_seg, dim3(grid), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg);
     hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ctl, a.seg, a.nseg, a.state,
                        a.msmall, a.mpcap);
+    if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
+      hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -269,9 +331,5 @@ int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_small_ttl(SmallMap* state, uint8_t* msmall, uint32_t R, hipStream_t st) {
-  hipLaunchKernelGGL(k_small_ttl, dim3(std::min<uint32_t>(256, (R + 255) / 256)), dim3(256), 0, st, state, msmall, R);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 }  // namespace cc

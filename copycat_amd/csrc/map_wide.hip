@@ -18,10 +18,10 @@
 // The engine tracks every map's size and capacity exactly (launch_map_size, after each sub-batch's map kernels:
 // per-commit size deltas -> per (tile, map) insert/remove counts -> per map the sizes at tile starts; a tile
 // whose counts straddle a resize threshold is replayed in log order).  In TTL mode (entries also leave when
-// their timers fire) the exact tracking stops and the engine falls back to bounds on the peak: lower = the
-// exact level reached before TTL mode and the sizes seen at barriers, upper = bound entries + entries dropped by
-// compaction or clear (every key that was ever present owned one).  Only there, when the two bounds give
-// different capacities and the order matters, the batch fails with CC_ERR_STATE instead of guessing.
+// their timers fire) the sub-batch's commits and timer expiries become events in log order and are replayed per
+// map instead (map_small.hip k_ttl_replay, common.h TtlEmit).  The peak-size bounds below (lower = sizes seen at
+// barriers, upper = bound entries + entries dropped by compaction or clear) remain only for a capacity marked
+// inexact (kMpInexact: the exact list overflowed), where a straddling order-dependent answer fails with CC_ERR_STATE.
 #include <algorithm>
 
 #include "common.h"
@@ -253,12 +253,6 @@ __global__ __launch_bounds__(kMwT) void k_mw_count(const uint32_t* __restrict__ 
 
 // pass 0: the capacity, then the first bucket holding a null / a match; pass 1: inside the common first bucket,
 // the first insertion of each.  Runs only for an order-dependent containsValue (all threads read the same ctl).
-// log2(HashMap capacity / 16) after the size peaked at p
-__device__ inline uint32_t cap_level(uint64_t p) {
-  uint32_t lv = 0;
-  for (uint64_t thr = 12; p > thr; thr <<= 1) ++lv;
-  return lv;
-}
 
 __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ word, const uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ val, const uint64_t* __restrict__ ins,
@@ -510,14 +504,14 @@ __device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_
   lds_barrier();
 }
 
-// A small map's insertion / removal (map_small.hip): its log index, the key's HashMap hash.
-__device__ inline void small_event(uint32_t m, uint32_t code, const XRec& xr, uint64_t idx0, const uint64_t* __restrict__ hh_key,
-                                   const int32_t* __restrict__ hh_val, uint32_t hh_n, uint64_t* __restrict__ ev_key,
-                                   uint32_t* __restrict__ ev_val, uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
-                                   uint32_t* __restrict__ err) {
+// A map commit's insertion / removal as an event (map_small.hip): its position (the log index's offset in the
+// sub-batch, or in TTL mode 2 * row offset + 1: common.h TtlEmit) and the key's HashMap hash.
+__device__ inline void map_event(uint32_t m, uint32_t code, uint64_t d, const XRec& xr, const uint64_t* __restrict__ hh_key,
+                                 const int32_t* __restrict__ hh_val, uint32_t hh_n, uint64_t* __restrict__ ev_key,
+                                 uint32_t* __restrict__ ev_val, uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
+                                 uint32_t* __restrict__ err) {
   bool ok;
   const uint32_t jh = java_key_hash(CC_FLAG_KTAG(smeta_flags(xr.meta)), xr.key, hh_key, hh_val, hh_n, ok);
-  const uint64_t d = xr.idx - idx0;
   if (!ok || d >> 40) atomicOr(err, kErrHandleHash);  // an unregistered String key / a sub-batch spanning 2^40 indices
   const uint32_t at = atomicAdd(sm_ctl, 1u);
   if (at < ev_cap) {
@@ -536,7 +530,9 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
                                                       const uint64_t* __restrict__ idx0p, const uint64_t* __restrict__ hh_key,
                                                       const int32_t* __restrict__ hh_val, uint32_t hh_n,
                                                       uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val,
-                                                      uint32_t ev_cap, uint32_t* __restrict__ sm_ctl, uint32_t* __restrict__ err) {
+                                                      uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
+                                                      const uint32_t* __restrict__ map_row, uint64_t lo,
+                                                      uint32_t* __restrict__ err) {
   __shared__ uint32_t cnt[kMszPass];
   if (blockIdx.x == 0 && threadIdx.x == 0) *list_n = 0;  // (k_msize_scan, the next launch, appends to the list)
   __shared__ uint32_t pfx[kHotMax + 1];
@@ -554,9 +550,15 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
       const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
       if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
-      if (code && base == 0 && msmall && msmall[x >> 2])  // small-window or size-queried map (map_small.hip)
-        small_event(x >> 2, code, xrec[(uint64_t)t * kTile + p], *idx0p, hh_key, hh_val, hh_n, ev_key, ev_val, ev_cap,
-                    sm_ctl, err);
+      if (code && base == 0) {
+        const uint64_t g = (uint64_t)t * kTile + p;
+        if (map_row)  // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip)
+          map_event(x >> 2, code, 2 * ((uint64_t)map_row[g] - lo) + 1, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val,
+                    ev_cap, sm_ctl, err);
+        else if (msmall && msmall[x >> 2])  // small-window or size-queried map (map_small.hip)
+          map_event(x >> 2, code, xrec[g].idx - *idx0p, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_cap, sm_ctl,
+                    err);
+      }
     }
     for (uint32_t h = threadIdx.x; h < nh; h += kMszT) {  // one thread per hot key: its run in this tile (a few words)
       const uint32_t m = (hot[h].ident & kMwSlotMask) - base;
@@ -728,7 +730,9 @@ int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.sb_hot, a.rst_msz, a.hot,
                      a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n, a.msmall, a.xrec,
-                     a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_cap, a.sm_ctl, a.err);
+                     a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_cap, a.sm_ctl, a.map_row, a.lo,
+                     a.err);
+  if (a.map_row) return hipGetLastError() == hipSuccess ? 0 : -1;  // TTL mode: sizes from the events (k_ttl_replay)
   hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,
                      a.res_type, a.max_resources, a.tiles, a.tcnt, a.msize, a.mpcap, a.list, a.list_n);
   hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.sb_hot,

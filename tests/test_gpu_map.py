@@ -340,21 +340,54 @@ def test_map_contains_value_exact_capacity():
         _assert_rows(*_apply_both(E, O, [one]))
 
 
-def test_map_contains_value_ttl_mode_bounds():
-    """In TTL mode (entries also leave when timers fire) exact tracking stops and the capacity comes from bounds:
-    the same undetermined case then fails with CC_ERR_STATE instead of guessing; a size barrier at the peak pins
-    it and the answer is exact again."""
-    from copycat_amd.engine import EngineError
+def test_map_contains_value_ttl_mode_exact():
+    """In TTL mode (entries also leave when timers fire) sizes and capacities stay exact: commits and expiries are
+    replayed as events in log order (map_small.hip, common.h TtlEmit), so the order-dependent containsValue after an
+    unobserved peak is answered as the reference answers it, with or without a size barrier at the peak."""
+    for with_size in (False, True):
+        E, O = _engines(1, 4, 64, 1024)
+        _assert_rows(*_apply_both(E, O, _peak_stream(with_size, ttl_row=True)))
+        _assert_maps(E, O, [0])
 
-    E, O = _engines(1, 4, 64, 1024)
-    parts = _peak_stream(False, ttl_row=True)
-    _apply_both(E, O, parts[:-1])
-    with pytest.raises(EngineError) as ei:
-        E.apply_host(parts[-1])
-    assert ei.value.rc == abi.CC_ERR_STATE
-    E, O = _engines(1, 4, 64, 1024)
-    _assert_rows(*_apply_both(E, O, _peak_stream(True, ttl_row=True)))
-    _assert_maps(E, O, [0])
+
+@pytest.mark.parametrize("flags", [abi.CC_CFG_TIMERS_DEFERRED, 0], ids=["manager", "module"])
+@pytest.mark.parametrize("n,maps,keys,sub_batch,seed,clustered", [
+    (40_000, 3, 40, 0, 401, False),             # sizes oscillate around the 24 / 48 thresholds; timers fire mid-batch
+    (200_000, 12, 48, 16384 * 2, 402, True),    # several sub-batches; clustered keys: treeifyBin's early resizes
+])
+def test_map_contains_value_ttl_churn_parity(flags, n, maps, keys, sub_batch, seed, clustered):
+    """TTL mode with stored nulls: put / remove churn where a share of the stores arm timers that fire inside the
+    batch (module and manager order, A8), containsValue / size barriers, two batches, cc_advance_time, then a third
+    batch of containsValue rows.  Every answer -- the order-dependent containsValue included -- matches the oracle
+    (no CC_ERR_STATE), and every barrier checks the tracked size against the table."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed)
+    if clustered:
+        lk = (b.flags >> 6) == 0  # Long keys
+        c = (b.inst.astype(np.uint64) % np.uint64(3)) + np.uint64(5)
+        b.key[lk] = ((b.key[lk] & np.uint64(15)) << np.uint64(20)) + c[lk]
+    _with_ttl(b, seed, p_ttl=0.3, max_ttl=120, step=4)
+    rows = _with_barriers(b, 0.002, seed, ops=np.array([abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_SIZE], np.uint8),
+                          p=[0.8, 0.2])
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch, flags=flags)
+    cut = n // 2
+    gs, gv, os_, ov = _apply_both(E, O, [b.slice(0, cut), b.slice(cut, n)])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    cv = rows[b.op[rows] == abi.CC_OP_MAP_CONTAINSVALUE]
+    npe = int((gs[cv] == abi.cc_status(abi.CC_ST_NULL_POINTER, abi.CC_TAG_NULL)).sum())
+    assert 0 < npe < len(cv)  # both outcomes occur
+    now = int(b.time[-1]) + 60  # some timers fire without a commit
+    E.advance_time(now)
+    O.advance_time(now)
+    _assert_maps(E, O, range(maps))
+    q = _puts(np.zeros(maps * 4, np.uint64), 0, op=abi.CC_OP_MAP_CONTAINSVALUE, index0=int(b.index[-1]) + 1)
+    q.inst[:] = np.repeat(np.arange(maps, dtype=np.uint32), 4)
+    q.a[:] = np.tile(np.arange(4, dtype=np.uint64), maps)
+    q.time[:] = now + 1
+    _assert_rows(*_apply_both(E, O, [q]))
 
 
 @pytest.mark.parametrize("clustered", [False, True], ids=["spread", "clustered"])
