@@ -1456,13 +1456,23 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
   struct Close { uint64_t crank, okey; uint32_t slot; };
   std::vector<Close> order;
   order.reserve(by_client.size());
-  {
-    std::unordered_map<uint64_t, uint64_t> pos;  // instance id -> position in sessions.values() iteration order
+  if (!by_client.empty()) {  // the closing instances' positions in sessions.values() iteration order
+    std::vector<std::pair<uint64_t, uint64_t>> pos;  // (instance id, position), only the closing instances'
+    pos.reserve(by_client.size());
+    for (auto& bc : by_client) pos.emplace_back(e->inst_id[bc.second], ~0ull);
+    std::sort(pos.begin(), pos.end());
     uint64_t q = 0;
-    e->sessions.for_each([&](int64_t id) { pos[(uint64_t)id] = q++; });
+    e->sessions.for_each([&](int64_t id) {
+      auto it = std::lower_bound(pos.begin(), pos.end(), std::make_pair((uint64_t)id, (uint64_t)0));
+      if (it != pos.end() && it->first == (uint64_t)id) it->second = q;
+      ++q;
+    });
     for (auto& bc : by_client) {
       const uint32_t i = bc.second;
-      order.push_back(Close{bc.first, pos.at(e->inst_id[i]), i});
+      auto it = std::lower_bound(pos.begin(), pos.end(), std::make_pair(e->inst_id[i], (uint64_t)0));
+      if (it == pos.end() || it->first != e->inst_id[i] || it->second == ~0ull)
+        return set_err(CC_ERR_STATE, "an open instance is missing from the sessions map");
+      order.push_back(Close{bc.first, it->second, i});
     }
   }
   std::sort(order.begin(), order.end(), [](const Close& x, const Close& y) {
