@@ -118,7 +118,7 @@ __device__ inline void pc_materialize(const PComp& c, uint32_t w0, uint64_t v0, 
     v = 0;
   } else {
     const uint32_t rv = pk_v(b), tag = CC_FLAG_TAG_A(smeta_flags(rmeta[rv]));
-    w = (w0 & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    w = (w0 & ~(kMwVtagMask | kMwUnseen)) | kMwPresent | (tag << 21);
     v = tag ? rab[rv].x : 0;
     vref = rv;
     nref = pk_n(b) == kPkOrig ? kOrig : pk_n(b);
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
                                                   uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
-                                                  unsigned long long* __restrict__ dropped,
+                                                  unsigned long long* __restrict__ dropped, unsigned long long* __restrict__ tdrop,
                                                   uint64_t* __restrict__ tbl_dl, const uint32_t* __restrict__ map_row,
                                                   const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
@@ -236,7 +236,10 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
 #pragma unroll
       for (int q = 0; q < MEPer; ++q) {
         // a bound key that is absent now is dropped: it still counts toward its map's peak-size bound
-        if ((ew[q] & kMwUsed) && !(ew[q] & (kMwPresent | kMwDead)) && dropped) atomicAdd(&dropped[ew[q] & kMwSlotMask], 1ull);
+        if ((ew[q] & kMwUsed) && !(ew[q] & (kMwPresent | kMwDead | kMwUnseen)) && dropped) {
+          atomicAdd(&dropped[ew[q] & kMwSlotMask], 1ull);
+          atomicAdd(&tdrop[ew[q] & kMwSlotMask], 1ull);
+        }
         if ((ew[q] & kMwPresent) && !(ew[q] & kMwDead)) {
           const uint32_t res = ew[q] & kMwSlotMask, kt = (ew[q] >> 17) & 3;
           uint32_t p = (uint32_t)map_hash(res, kt, ek[q]) & (kMapRegion - 1);
@@ -720,11 +723,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   a.mark(K_APPLY_MAP, 1, st);
   if (a.ttl)
     hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
-                       (unsigned long long*)a.dropped, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
+                       (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, a.err);
   else
     hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
-                       (unsigned long long*)a.dropped, nullptr, nullptr, nullptr, nullptr, nullptr, false,
+                       (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;

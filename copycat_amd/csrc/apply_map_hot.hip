@@ -170,8 +170,9 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
   const uint32_t t = threadIdx.x;
   const uint32_t nc = *cand_n;
   // bind each hot key's table entry (the tables are idle between the sub-batch's kernels): every key looks itself
-  // up in parallel (thread = key); the keys not in the table yet (first sub-batches only) are inserted by one wave,
-  // one lane at a time, so no two keys race for a slot; then wave 0 compacts the bound keys in rank order
+  // up in parallel (thread = key); the keys not in the table yet are inserted by one wave, one lane at a time, so no
+  // two keys race for a slot, as UNSEEN placeholders (a candidate counted over the whole batch may never occur in
+  // this sub-batch: such an entry is no key the map held, kMwUnseen); then wave 0 compacts the bound keys in rank order
   const uint32_t nh = nc < (uint32_t)kHotMax ? nc : (uint32_t)kHotMax;
   uint64_t h = 0, key = 0, base = 0;
   uint32_t ident = 0;
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
           __hip_atomic_store(&tbl_val[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_ci[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_ins[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&tbl_word[base + p], ident, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&tbl_word[base + p], ident | kMwUnseen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           pos = (uint32_t)(base + p);
           return true;
         }
@@ -447,7 +448,7 @@ __device__ inline void materialize(const Comp& c, const HotS0& s0, const XRec* _
     ins = s0.ins;
   } else {
     const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(xr[b.v].meta));
-    w = base | kMwPresent | (tag << 21);
+    w = (base & ~kMwUnseen) | kMwPresent | (tag << 21);
     v = tag ? xr[b.v].ab.x : 0;
     ci = xr[b.v].idx;
     ins = b.n == kOrig ? s0.ins : xr[b.n].idx;

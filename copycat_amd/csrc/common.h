@@ -200,13 +200,17 @@ __host__ __device__ inline uint64_t map_hash(uint32_t res, uint32_t ktag, uint64
   h ^= h >> 31;
   return h;
 }
-// map table entry word: slot(17) | ktag(2) << 17 | USED << 19 | PRESENT << 20 | vtag(3) << 21 | PENDING << 24 | DEAD << 25
+// map table entry word: slot(17) | ktag(2) << 17 | USED << 19 | PRESENT << 20 | vtag(3) << 21 | PENDING << 24 | DEAD << 25 |
+// UNSEEN << 26
 constexpr uint32_t kMwSlotMask = (1u << 17) - 1;
 constexpr uint32_t kMwUsed = 1u << 19;
 constexpr uint32_t kMwPresent = 1u << 20;
 constexpr uint32_t kMwVtagMask = 7u << 21;
 constexpr uint32_t kMwPending = 1u << 24;  // bound this round, key not yet visible (apply_map resolution)
 constexpr uint32_t kMwDead = 1u << 25;     // entry of a deleted map: never matches, reclaimed by compaction
+// an entry k_hot_bind inserted for a hot-key candidate that no commit has stored into yet: not a key the map ever
+// held (left out of the bound-key counts and compaction drops that bound tree bins, map_wide.hip); cleared by a store
+constexpr uint32_t kMwUnseen = 1u << 26;
 constexpr uint32_t kMwIdentMask = kMwSlotMask | (3u << 17) | kMwUsed | kMwDead;
 // coordination state blocks (apply_coord.hip): one per resource slot, fixed capacity
 struct CoordHdr {

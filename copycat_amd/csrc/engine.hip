@@ -94,7 +94,7 @@ static void free_all(cc_engine* e) {
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_hot_samp, e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total,
-                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,
+                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,    e->d_mw_tdrop,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
@@ -300,6 +300,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_hot_cand_n, sizeof(uint32_t));
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
+    ALLOC(e->d_mw_tdrop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
     ALLOC(e->d_msmall, cfg->max_resources);
@@ -354,6 +355,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_hot_n, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_peak, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_drop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_mw_tdrop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msize, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mpcap, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msm, 0, sizeof(SmallMap) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
@@ -478,6 +480,7 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
   if (is_keyed(type)) {  // a new HashMap: capacity 16, no history
     HIPCHECK(hipMemset(e->d_mw_peak + first, 0, sizeof(uint32_t) * count));
     HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
+    HIPCHECK(hipMemset(e->d_mw_tdrop + first, 0, sizeof(uint64_t) * count));
     HIPCHECK(hipMemset(e->d_msize + first, 0, sizeof(uint32_t) * count));
     HIPCHECK(hipMemset(e->d_mpcap + first, 0, sizeof(uint32_t) * count));
     // MapState's table followed key by key while small (map_small.hip); sets / multimaps have no order-dependent op
@@ -1010,6 +1013,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.tbl_ci = e->d_tbl_ci;
       ma.tbl_ins = e->d_tbl_ins;
       ma.dropped = e->d_mw_drop;
+      ma.tdrop = e->d_mw_tdrop;
       ma.ttl = e->ttl_live;
       ma.tbl_dl = e->d_tbl_dl;
       ma.map_row = e->d_map_row;
@@ -1329,6 +1333,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.entries = e->map_entries;
     mw.peak_lo = e->d_mw_peak;
     mw.dropped = e->d_mw_drop;
+    mw.tdrop = e->d_mw_tdrop;
     mw.msize = e->d_msize;  // exact in both modes (TTL mode: commit + expiry events, map_small.hip)
     mw.mpcap = e->d_mpcap;
     mw.ctl = e->d_mw_ctl;
@@ -1938,7 +1943,7 @@ static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unp
 // Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
 // mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
 namespace {
-constexpr uint64_t kSnapMagic = 0x35304E5053434343ull;  // "CCCSPN05"
+constexpr uint64_t kSnapMagic = 0x36304E5053434343ull;  // "CCCSPN06"
 constexpr uint32_t kSnapRetained = 4u;                   // SnapHdr.flags: CC_CFG_VALUE_RETAINED section present
 struct SnapHdr {
   uint64_t magic;
@@ -1985,6 +1990,7 @@ static std::vector<Section> snap_sections(cc_engine* e) {
     v.push_back({e->d_tbl_dl, nullptr, 8 * n});
     v.push_back({e->d_mw_peak, nullptr, 4 * mr});
     v.push_back({e->d_mw_drop, nullptr, 8 * mr});
+    v.push_back({e->d_mw_tdrop, nullptr, 8 * mr});
     v.push_back({e->d_msize, nullptr, 4 * mr});
     v.push_back({e->d_mpcap, nullptr, 4 * mr});
     v.push_back({e->d_msm, nullptr, sizeof(SmallMap) * mr});

@@ -97,6 +97,7 @@ struct MapArgs {
   uint64_t* tbl_ci;
   uint64_t* tbl_ins;
   uint64_t* dropped;  // [max_resources] compaction drops bound-but-absent entries: counted per map (map_wide.hip)
+  uint64_t* tdrop;    // [max_resources] the same drops since the map's last clear / Delete (tree-bin test)
   bool ttl;           // TTL mode: entries carry timer deadlines (k_apply_map<true>)
   uint64_t* tbl_dl;
   const uint32_t* map_row;     // [sub_batch] staging position -> batch row (launch_map_rows)
@@ -227,6 +228,7 @@ struct MapWideArgs {
   uint64_t entries;
   uint32_t* peak_lo;           // [max_resources] lower bound on the map's peak size
   uint64_t* dropped;           // [max_resources] entries dropped by compaction / clear (upper-bound term)
+  uint64_t* tdrop;             // [max_resources] entries compacted away since the last clear (tree-bin test)
   uint32_t* msize;             // exact tracking (launch_map_size; null in TTL mode): the live size, and
   const uint32_t* mpcap;       //   log2(capacity / 16) of the peak (in TTL mode a lower bound for the bounds above)
   unsigned long long* ctl;     // [C_N] scratch

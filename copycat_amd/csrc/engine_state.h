@@ -147,6 +147,7 @@ struct cc_engine {
   uint32_t* d_bar_n = nullptr;
   uint32_t* d_mw_peak = nullptr;   // [max_resources]
   uint64_t* d_mw_drop = nullptr;   // [max_resources]
+  uint64_t* d_mw_tdrop = nullptr;  // [max_resources] keys compacted away since the map's last clear (tree-bin test)
   // exact map sizes / HashMap capacities (map_wide.hip launch_map_size; not in TTL mode)
   uint32_t* d_rst_msz = nullptr;   // [sub_batch + 4 kPT] each region map commit's map and size change, staging order
   uint32_t* d_hot_msz = nullptr;   // hot-key commits' size changes (HotArgs::hot_msz)

@@ -24,7 +24,7 @@ __device__ inline uint32_t map_apply(uint32_t op, uint32_t flags, uint64_t a, ui
   const uint32_t T = P ? mw_vtag(w) : CC_TAG_NULL;
   const uint64_t V = P ? v : 0;
   auto store = [&](uint32_t tag, uint64_t x) {
-    w = (w & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    w = (w & ~(kMwVtagMask | kMwUnseen)) | kMwPresent | (tag << 21);
     v = x;
   };
   auto erase = [&]() {
@@ -204,7 +204,7 @@ __device__ inline void materialize_lds(const Comp& c, uint32_t w0, uint64_t v0, 
     ins = ins0;
   } else {
     const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(rmeta[b.v]));
-    w = (w0 & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    w = (w0 & ~(kMwVtagMask | kMwUnseen)) | kMwPresent | (tag << 21);
     v = tag ? rab[b.v].x : 0;
     ci = ridx[b.v];
     ins = b.n == kOrig ? ins0 : ridx[b.n];
@@ -225,7 +225,7 @@ __device__ inline void materialize_ref(const Comp& c, uint32_t w0, uint64_t v0, 
     v = 0;
   } else {
     const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(rmeta[b.v]));
-    w = (w0 & ~kMwVtagMask) | kMwPresent | (tag << 21);
+    w = (w0 & ~(kMwVtagMask | kMwUnseen)) | kMwPresent | (tag << 21);
     v = tag ? rab[b.v].x : 0;
     vref = b.v;
     nref = b.n;

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kMwT) void k_mw_count(const uint32_t* __restrict__ 
   for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
     const uint32_t w = word[e];
     if (!(w & kMwUsed) || (w & kMwDead) || (w & kMwSlotMask) != slot) continue;
-    ++used;
+    if (!(w & kMwUnseen)) ++used;  // (a hot-key placeholder no commit stored into is no key the map ever held)
     if (!live_at(w, dl, e, fire)) continue;
     ++pres;
     if (op == CC_OP_MAP_CONTAINSVALUE) {
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
   const uint64_t bb = ctl[C_BN];                     // (pass 1: the bucket holding the first null and the first match)
   for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * kMwT) {
     const uint32_t w = word[e];
-    if ((w & kMwDead) || !(w & kMwUsed) || (w & kMwSlotMask) != slot) continue;
+    if ((w & kMwDead) || !(w & kMwUsed) || (w & kMwUnseen) || (w & kMwSlotMask) != slot) continue;
     const bool present = live_at(w, dl, e, fire);
     const uint32_t vt = mw_vtag(w);
     const bool isnull = vt == CC_TAG_NULL;
@@ -325,7 +325,8 @@ __global__ void k_mw_size(uint32_t slot, uint32_t op, const unsigned long long* 
 }
 
 __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsigned long long* __restrict__ ctl,
-                            uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped, uint8_t* __restrict__ out_status,
+                            uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped,
+                            unsigned long long* __restrict__ tdrop, uint8_t* __restrict__ out_status,
                             uint64_t* __restrict__ out_value, const SmallMap* __restrict__ small, uint32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
   const uint64_t pres = ctl[C_PRES];
@@ -350,12 +351,14 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
         npe = bn != bm ? bn < bm : ctl[C_IN] < ctl[C_IM];
         if (bn == bm) {  // decided inside one bin: by insertion order, unless that bin was ever a tree bin
           bool tree = false;
+          // (a tree bin needs 9 keys in the bin at once since the last clear, which wipes every bin: the bin's
+          // bound keys plus the keys compacted away since that clear bound them)
           if (small) {
             const SmallMap& sm = small[slot];
             tree = ((sm.flags & kSmTree) && ((sm.tree_bins >> (bn & 63u)) & 1ull)) ||
-                   ((sm.flags & kSmUnknown) && ctl[C_USED] + dropped[slot] >= 9);
+                   ((sm.flags & kSmUnknown) && ctl[C_USED] + tdrop[slot] >= 9);
           }
-          for (int q = 0; q < 32; ++q) tree |= ctl[C_TR0 + q] + dropped[slot] >= 9;
+          for (int q = 0; q < 32; ++q) tree |= ctl[C_TR0 + q] + tdrop[slot] >= 9;
           if (tree) atomicOr(err, kErrMapOrder);
         }
       }
@@ -367,8 +370,9 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
       }
       break;
     }
-    default:  // clear / Delete: every entry is dropped; the keys they held count toward the peak bound
+    default:  // clear / Delete: every entry is dropped; the keys they held count toward the peak bound; no bin is left
       dropped[slot] += ctl[C_USED];
+      tdrop[slot] = 0;
       break;
   }
   if (pres > peak_lo[slot]) peak_lo[slot] = (uint32_t)min(pres, (uint64_t)0xFFFFFFFFu);
@@ -459,7 +463,7 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
   }
   if (a.msize) hipLaunchKernelGGL(k_mw_size, dim3(1), dim3(64), 0, st, a.slot, op, a.ctl, a.msize, a.err);
   hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,
-                     (unsigned long long*)a.dropped, a.out_status, a.out_value, a.small, a.err);
+                     (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, a.out_status, a.out_value, a.small, a.err);
   if (hipGetLastError() != hipSuccess) return -1;
   if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE) return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, st);
   return 0;

@@ -423,6 +423,29 @@ def test_map_contains_value_churn_parity(n, maps, keys, sub_batch, hot, p_hot, s
     assert 0 < npe < len(cv)  # both outcomes occur
 
 
+def test_map_hot_placeholders_after_clear_then_ttl():
+    """Hot-key candidates are counted once per batch and bound before every sub-batch, so after a clear / Delete
+    barrier a sub-batch binds entries for keys its map no longer holds.  Those are placeholders (kMwUnseen): no key
+    the map ever held, left out of the bound-key counts behind the tree-bin test.  Clears and containsValue rows
+    mid-batch with hot keys over several sub-batches, then a batch that switches to TTL mode with more containsValue
+    rows: every answer and every map's entries match the oracle."""
+    from copycat_amd.workload import map_random_stream
+
+    maps, n = 4, 120_000
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=64, seed=71, hot=2, p_hot=0.5)
+    _with_barriers(b, 0.0015, 71, ops=np.array([abi.CC_OP_MAP_CLEAR, abi.CC_OP_MAP_CONTAINSVALUE], np.uint8), p=[0.3, 0.7])
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=16384 * 2)
+    _assert_rows(*_apply_both(E, O, [b]))
+    _assert_maps(E, O, range(maps))
+    b2 = map_random_stream(40_000, maps, max_inst, keys=64, seed=72, hot=2, p_hot=0.5, index0=int(b.index[-1]) + 1)
+    _with_ttl(b2, 72, p_ttl=0.2, max_ttl=200, step=4)
+    b2.time[:] += np.uint64(int(b.time.max()))
+    _with_barriers(b2, 0.002, 72, ops=np.array([abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_SIZE], np.uint8), p=[0.8, 0.2])
+    _assert_rows(*_apply_both(E, O, [b2]))
+    _assert_maps(E, O, range(maps))
+
+
 def test_map_clear_then_reuse_keys():
     """clear / Delete drop every entry of one map (other maps keep theirs); the same keys are then re-put
     as new HashMap nodes; size and isEmpty follow."""
