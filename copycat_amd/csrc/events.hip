@@ -271,6 +271,7 @@ __global__ __launch_bounds__(kEC) void k_ev_place(const EvRec* __restrict__ aren
 }
 
 constexpr int kEvWin = 2048;  // output events assembled per window in k_ev_tile_out
+constexpr int kEvMaxWin = 16;  // more windows than this in one tile: events stored straight to their rows
 // per tile: the rows' event offsets in LDS, then the tile's events to their output rows, one window at a time
 __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict__ cpos, uint64_t n, const uint16_t* __restrict__ ev_cnt,
                                                     const uint32_t* __restrict__ tile_sum, const uint64_t* __restrict__ tile_off,
@@ -327,6 +328,23 @@ __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict_
   const uint64_t toff = tile_off[T], b0 = toff - tile_off[0];
   const uint32_t nev = tile_sum[T];
   if (b0 + nev > arena_cap || toff + nev > out_cap) return;  // (the call fails: kErrEvents from k_ev_tiles)
+  // Each window re-reads the tile's event list (from L2): nev^2 / kEvWin record reads per tile.  A tile whose fan-out
+  // makes that more than kEvMaxWin windows (group / election bursts) writes each event straight to its output row
+  // instead: scattered stores, linear in nev.
+  if (nev > (uint32_t)(kEvWin * kEvMaxWin)) {
+    for (uint32_t i = t; i < nev; i += kER) {
+      const EvRec r = bucket[b0 + i];
+      const uint32_t sp = r.g - tbase;
+      const uint64_t d = toff + soff[sp] + r.k;
+      pos[d] = (uint32_t)(lo + tbase + srow[sp]);
+      target[d] = r.target;
+      code[d] = (uint8_t)r.code;
+      src[d] = (uint8_t)r.src;
+      tag[d] = (uint8_t)r.tag;
+      payload[d] = r.payload;
+    }
+    return;
+  }
   for (uint32_t w0 = 0; w0 < nev; w0 += kEvWin) {  // block-uniform
     const uint32_t wn = nev - w0 < (uint32_t)kEvWin ? nev - w0 : (uint32_t)kEvWin;
     for (uint32_t i = t; i < nev; i += kER) {  // the tile's events (re-read per window from L2)

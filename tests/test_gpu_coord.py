@@ -85,6 +85,21 @@ def _check_state(E, O, types):
 FLAGS = abi.CC_CFG_TIMERS_DEFERRED | abi.CC_CFG_VALUE_EVENTS
 
 
+def test_coord_event_fanout_burst():
+    """Groups and elections of 300 members in one partition tile: join / leave and leadership changes fan out to
+    every member, hundreds of thousands of events in the tile (k_ev_tile_out writes such a tile's events straight
+    to their rows instead of re-reading its list per 2,048-event window).  Events per commit vs the oracle."""
+    from copycat_amd.workload import coord_random_stream
+
+    types = np.array([G, G, E_, V], np.uint8)
+    K = 300
+    E, O, max_inst = _setup(types, K, FLAGS, coord_cap=512, max_events=1 << 23)
+    b = coord_random_stream(8000, types, K, max_inst, seed=17)
+    s, v, ev = _check_batch(E, O, b, capacity=1 << 23)
+    assert len(ev["pos"]) > 16 * 2048  # past the windowed path's limit in that tile
+    _check_state(E, O, types)
+
+
 @pytest.mark.parametrize("n,R,K,seed,flags", [
     (1, 4, 2, 1, FLAGS),
     (500, 8, 3, 2, FLAGS),
