@@ -348,7 +348,7 @@ def run_c5(args, dev, rank, world, dist):
     victims_expiring = int(expired_glob[victim_sess].sum())
     clients = CoordClients(types, K=1, max_inst=R + V, seed=0xA700000 + 5 + rank)
     host = Batch(n)
-    streams, parity_ref, cpu = [], None, None
+    streams, parity_ref, cpu, cpu_all = [], None, None, None
     for k in range(nstreams):
         clients.next(n, out=host)
         if k == 0 and rank == 0 and not args.no_parity:
@@ -371,6 +371,11 @@ def run_c5(args, dev, rank, world, dist):
                        "sample": f"step 0's {n:,} commits of the same c5 stream (events included; the parity reference), "
                                  f"C++ restatement of the Java apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
             del O, oe
+            if world == 1 and not args.no_cpu_baseline:
+                v_all, thr = cpu_all_cores(host, R, types, cpu_threads(), flags)
+                cpu_all = {"value": round(v_all, 1), "unit": "ops/s", "cores": thr, "kind": "port",
+                           "sample": f"the same {n:,} commits (events included) sharded by resource (slot % {thr}) over "
+                                     f"{thr} threads, one oracle each, {cpu_model()}"}
         streams.append(DeviceBatch.upload(host, device=dev))
     del host
     t_gen = time.time() - t_gen
@@ -476,7 +481,7 @@ def run_c5(args, dev, rank, world, dist):
                                   "instances_expected": victims_expiring,
                                   "path": "per-rank cc_expire_sweep -> RCCL all-gather of the bitmaps -> "
                                           "cc_sessions_expire on every rank, every step"}},
-            "parity": parity, "roofline": roofline, "cpu_baseline": cpu,
+            "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all,
         }
         print(json.dumps(out), flush=True)
     bad = parity is not None and (parity["mismatches"] or parity["unwritten"] or not parity["events_equal"])
@@ -550,6 +555,78 @@ def cpu_all_cores(batch, R, rtype, threads, flags=None):
         list(ex.map(lambda t: oracles[t].apply(parts[t]), range(threads)))
         tc = time.perf_counter() - tc
     return len(batch) / tc, threads
+
+
+def c3_full_gate(n, R, args, rank, status0, value0, gpu_tab, block=1 << 26):
+    """c3 step 0 in full: the same stream regenerated block by block and applied by one oracle (oracle/oracle.cpp) per
+    host thread, sharded by map (map r on oracle r % threads: one map's rows stay in log order on one oracle); every
+    row's status + value against the GPU's step-0 results, then every map's entries after step 0 against the GPU
+    table read right after step 0.  The oracles' apply time over the whole step is the all-cores CPU baseline."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from copycat_amd import abi
+    from copycat_amd.batch import Batch
+    from copycat_amd.workload import SEED_C3, map_zipf_rows
+    from oracle.oracle_py import Oracle
+
+    threads = cpu_threads()
+    oracles = []
+    for t in range(threads):
+        O = Oracle(R, R)
+        for r in range(t, R, threads):  # (the engine's registry: instance r = map r, id 1 + rank + r)
+            O.resource_create(r, abi.CC_RES_MAP)
+            O.instance_open(r, r, 1 + rank + r, 1 + rank)
+        oracles.append(O)
+    mism = unwritten = 0
+    t_apply = 0.0
+    host = Batch(min(n, block))
+    with ThreadPoolExecutor(threads) as ex:
+        for lo in range(0, n, block):
+            m = min(block, n - lo)
+            b = host if m == len(host) else Batch(m)
+            map_zipf_rows(lo, m, maps=R, pairs=args.pairs, s=args.zipf, seed=SEED_C3 + rank, threads=threads, out=b)
+            own = (b.inst % threads).astype(np.uint16)
+            order = np.argsort(own, kind="stable")
+            cuts = np.searchsorted(own[order], np.arange(threads + 1))
+            subs = []
+            for t in range(threads):
+                rows = order[cuts[t]:cuts[t + 1]]
+                part = Batch(0)
+                for name in Batch.__slots__:
+                    setattr(part, name, np.ascontiguousarray(getattr(b, name)[rows]))
+                subs.append(part)
+            tc = time.perf_counter()
+            res = list(ex.map(lambda t: oracles[t].apply(subs[t]), range(threads)))
+            t_apply += time.perf_counter() - tc
+            s_ref = np.empty(m, np.uint8)
+            v_ref = np.empty(m, np.uint64)
+            for t in range(threads):
+                rows = order[cuts[t]:cuts[t + 1]]
+                s_ref[rows] = res[t][0]
+                v_ref[rows] = res[t][1]
+            s_gpu = status0[lo:lo + m].cpu().numpy()
+            v_gpu = value0[lo:lo + m].cpu().numpy().view(np.uint64)
+            mism += int(np.count_nonzero((s_gpu != s_ref) | (v_gpu != v_ref)))
+            unwritten += int(np.count_nonzero(s_gpu == RESULT_SENTINEL))
+            del subs, res
+    sl, kt, k, vt, v, ci = gpu_tab
+    bounds = np.searchsorted(sl, np.arange(R + 1))
+    maps_bad, entries = 0, 0
+    for r in range(R):
+        a, z = bounds[r], bounds[r + 1]
+        want = oracles[r % threads].map_entries(r)
+        got = (kt[a:z], k[a:z], vt[a:z], v[a:z], ci[a:z])
+        entries += int(z - a)
+        maps_bad += 0 if all(np.array_equal(x, y) for x, y in zip(got, want)) else 1
+    parity = {"rows": n, "mismatches": mism, "unwritten": unwritten, "maps": R, "map_entries": entries,
+              "maps_mismatched": maps_bad,
+              "checked": f"step 0 in full: per-commit status+value of all {n:,} rows (results prefilled with the 0xFF "
+                         f"sentinel status) and every map's entries (key, value, commit index) after step 0, GPU vs "
+                         f"{threads} oracle/oracle.cpp instances sharded by map"}
+    cpu_all = {"value": round(n / t_apply, 1), "unit": "ops/s", "cores": threads, "kind": "port",
+               "sample": f"the whole step-0 stream ({n:,} commits) sharded by map (slot % {threads}) over {threads} "
+                         f"threads, one oracle each (apply time only; Zipf-hot maps load their shard), {cpu_model()}"}
+    return parity, cpu_all
 
 
 def run_c2(args, dev, rank, world, dist):
@@ -794,15 +871,16 @@ def run_c3(args, dev, rank, world, dist):
             dist.all_gather_into_tensor(wm_all, wm_local)
 
     m = min(n, cpu_sample)
-    gpu0 = None  # step 0's first m results (applied from the fresh state): the parity sample
+    gpu0 = None  # step 0's results (applied from the fresh state) and the map table right after it: the parity gate
 
     def capture0():
         torch.cuda.synchronize(dev)
-        return status[:m].cpu().numpy(), value[:m].cpu().numpy().view(np.uint64)
+        return status.clone(), value.clone(), E.map_table()
 
+    gate = rank == 0 and not args.no_parity
     for k in range(args.warmup):
         step()
-        if k == 0:
+        if k == 0 and gate:
             gpu0 = capture0()
     torch.cuda.synchronize(dev)
     if not args.no_profile:
@@ -818,7 +896,7 @@ def run_c3(args, dev, rank, world, dist):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     E.sync()
-    if gpu0 is None and args.steps == 1:  # no warmup: the one timed step is step 0
+    if gpu0 is None and gate and args.warmup == 0 and args.steps == 1:  # the one timed step is step 0
         gpu0 = capture0()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -841,7 +919,7 @@ def run_c3(args, dev, rank, world, dist):
             "bytes_per_commit": B_OP_C3,
             "pipeline_frac": round(B_OP_C3 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         }
-    cpu = parity = None
+    cpu = parity = cpu_all = None
     if rank == 0 and (not args.no_parity or (world == 1 and not args.no_cpu_baseline)):
         from oracle.oracle_py import Oracle
 
@@ -850,19 +928,18 @@ def run_c3(args, dev, rank, world, dist):
             O.resource_create(r, abi.CC_RES_MAP)
             O.instance_open(r, r, 1 + rank + r, 1 + rank)
         tc = time.perf_counter()
-        s_ref, v_ref = O.apply(batch.slice(0, m))
+        O.apply(batch.slice(0, m))
         tc = time.perf_counter() - tc
         if world == 1 and not args.no_cpu_baseline:
             cpu = {"value": round(m / tc, 1), "unit": "ops/s", "cores": 1, "kind": "port",
-                   "sample": f"first {m:,} commits of the same c3 stream (the parity sample), C++ restatement of the "
-                             f"Java apply path (oracle/oracle.cpp), 1 thread, {cpu_model()}"}
-        if not args.no_parity and gpu0 is not None:
-            s_gpu, v_gpu = gpu0
-            parity = {"rows": m, "mismatches": int(np.count_nonzero((s_gpu != s_ref) | (v_gpu != v_ref))),
-                      "unwritten": int(np.count_nonzero(s_gpu == RESULT_SENTINEL)),
-                      "checked": f"step 0: per-commit status+value of the first {m:,} rows (results prefilled with the "
-                                 f"0xFF sentinel status), GPU vs oracle/oracle.cpp"}
+                   "sample": f"first {m:,} commits of the same c3 stream, C++ restatement of the Java apply path "
+                             f"(oracle/oracle.cpp), 1 thread, {cpu_model()}"}
         del O
+        if not args.no_parity and gpu0 is not None:
+            parity, cpu_all = c3_full_gate(n, R, args, rank, *gpu0)
+            if world > 1 or args.no_cpu_baseline:
+                cpu_all = None
+        gpu0 = None
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
@@ -873,12 +950,12 @@ def run_c3(args, dev, rank, world, dist):
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]},
-            "parity": parity, "roofline": roofline, "cpu_baseline": cpu,
+            "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
-    if parity is not None and (parity["mismatches"] or parity["unwritten"]):
+    if parity is not None and (parity["mismatches"] or parity["unwritten"] or parity.get("maps_mismatched")):
         sys.stderr.write(f"PARITY FAILURE: {parity}\n")
         sys.exit(3)
 

@@ -1661,11 +1661,17 @@ extern "C" int cc_read_value_retained(cc_engine* e, uint32_t first, uint32_t cou
   return CC_OK;
 }
 
-extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag,
-                                   uint64_t* h_key, uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index) {
-  if (!e || !count || slot >= e->cfg.max_resources || !is_keyed(e->res_type[slot]))
-    return set_err(CC_ERR_INVALID, "not a map or set slot");
-  if (cap && (!h_key_tag || !h_key || !h_value_tag || !h_value)) return set_err(CC_ERR_INVALID, "null output");
+// The live entries of one map / set slot (all slots: ~0u), sorted by (slot, key tag, key).
+namespace {
+struct MapRow {
+  uint32_t slot;
+  uint8_t kt;
+  uint64_t k;
+  uint8_t vt;
+  uint64_t v, ci;
+};
+}  // namespace
+static int read_map_rows(cc_engine* e, uint32_t slot, std::vector<MapRow>& rows) {
   int rc = quiesce(e);
   if (rc) return rc;
   const uint64_t n = e->map_entries;
@@ -1683,18 +1689,52 @@ extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, ui
     HIPCHECK(hipMemcpy(&clock, e->d_clock, sizeof clock, hipMemcpyDeviceToHost));
   }
   static const uint8_t ktag_tag[4] = {CC_TAG_LONG, CC_TAG_INT, CC_TAG_BOOL, CC_TAG_HANDLE};
-  struct Row { uint8_t kt; uint64_t k; uint8_t vt; uint64_t v, ci; };
-  std::vector<Row> rows;
+  rows.clear();
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t w = word[i];
     if (!dl.empty() && dl[i] && dl[i] <= clock) continue;
-    if ((w & kMwUsed) && (w & kMwPresent) && !(w & kMwDead) && (w & kMwSlotMask) == slot)
-      rows.push_back(Row{ktag_tag[(w >> 17) & 3], key[i], (uint8_t)mw_vtag(w), val[i], ci[i]});
+    const uint32_t s = w & kMwSlotMask;
+    if ((w & kMwUsed) && (w & kMwPresent) && !(w & kMwDead) && (slot == ~0u || s == slot))
+      rows.push_back(MapRow{s, ktag_tag[(w >> 17) & 3], key[i], (uint8_t)mw_vtag(w), val[i], ci[i]});
   }
-  std::sort(rows.begin(), rows.end(), [](const Row& x, const Row& y) { return x.kt != y.kt ? x.kt < y.kt : x.k < y.k; });
+  std::sort(rows.begin(), rows.end(), [](const MapRow& x, const MapRow& y) {
+    return x.slot != y.slot ? x.slot < y.slot : (x.kt != y.kt ? x.kt < y.kt : x.k < y.k);
+  });
+  return CC_OK;
+}
+
+extern "C" int cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag,
+                                   uint64_t* h_key, uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index) {
+  if (!e || !count || slot >= e->cfg.max_resources || !is_keyed(e->res_type[slot]))
+    return set_err(CC_ERR_INVALID, "not a map or set slot");
+  if (cap && (!h_key_tag || !h_key || !h_value_tag || !h_value)) return set_err(CC_ERR_INVALID, "null output");
+  std::vector<MapRow> rows;
+  int rc = read_map_rows(e, slot, rows);
+  if (rc) return rc;
   *count = rows.size();
   const uint64_t m = std::min<uint64_t>(cap, rows.size());
   for (uint64_t i = 0; i < m; ++i) {
+    h_key_tag[i] = rows[i].kt;
+    h_key[i] = rows[i].k;
+    h_value_tag[i] = rows[i].vt;
+    h_value[i] = rows[i].v;
+    if (h_commit_index) h_commit_index[i] = rows[i].ci;
+  }
+  return CC_OK;
+}
+
+extern "C" int cc_read_map_table(cc_engine* e, uint64_t cap, uint64_t* count, uint32_t* h_slot, uint8_t* h_key_tag,
+                                 uint64_t* h_key, uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index) {
+  if (!e || !count) return set_err(CC_ERR_INVALID, "null argument");
+  if (!e->map_bits) return set_err(CC_ERR_INVALID, "engine without maps");
+  if (cap && (!h_slot || !h_key_tag || !h_key || !h_value_tag || !h_value)) return set_err(CC_ERR_INVALID, "null output");
+  std::vector<MapRow> rows;
+  int rc = read_map_rows(e, ~0u, rows);
+  if (rc) return rc;
+  *count = rows.size();
+  const uint64_t m = std::min<uint64_t>(cap, rows.size());
+  for (uint64_t i = 0; i < m; ++i) {
+    h_slot[i] = rows[i].slot;
     h_key_tag[i] = rows[i].kt;
     h_key[i] = rows[i].k;
     h_value_tag[i] = rows[i].vt;

@@ -70,6 +70,7 @@ def lib():
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
             "cc_read_value_retained": (i32, [P, u32, u32, P]),
             "cc_read_map_entries": (i32, [P, u32, u64, P, P, P, P, P, P]),
+            "cc_read_map_table": (i32, [P, u64, P, P, P, P, P, P, P]),
             "cc_read_lock_state": (i32, [P, u32, P, P, P, u64, P, P, P]),
             "cc_read_election_state": (i32, [P, u32, P, P, u64, P, P, P]),
             "cc_read_group_members": (i32, [P, u32, u64, P, P]),
@@ -455,6 +456,17 @@ class Engine:
                             np.zeros(m, np.uint64), np.zeros(m, np.uint64))
         _check(self.L.cc_read_map_entries(self.h, slot, m, C.byref(n), _np(kt), _np(k), _np(vt), _np(v), _np(ci)))
         return kt, k, vt, v, ci
+
+    def map_table(self):
+        """Every map / set slot's entries in one table pass, sorted by (slot, key tag, key):
+        (slot, key_tag, key, value_tag, value, commit_index)."""
+        n = C.c_uint64()
+        _check(self.L.cc_read_map_table(self.h, 0, C.byref(n), None, None, None, None, None, None))
+        m = n.value
+        sl, kt, k, vt, v, ci = (np.zeros(m, np.uint32), np.zeros(m, np.uint8), np.zeros(m, np.uint64),
+                                np.zeros(m, np.uint8), np.zeros(m, np.uint64), np.zeros(m, np.uint64))
+        _check(self.L.cc_read_map_table(self.h, m, C.byref(n), _np(sl), _np(kt), _np(k), _np(vt), _np(v), _np(ci)))
+        return sl, kt, k, vt, v, ci
 
 
 def quorum_commit(match, term_start, commit_in, commit_out, stream=None):

@@ -361,6 +361,10 @@ int  cc_read_value_retained(cc_engine* e, uint32_t first, uint32_t count, uint64
  * by (key tag, key), go to the arrays (key tag as a CC_TAG_*; commit_index may be NULL).               */
 int  cc_read_map_entries(cc_engine* e, uint32_t slot, uint64_t cap, uint64_t* count, uint8_t* h_key_tag, uint64_t* h_key,
                          uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index);
+/* Every map / set slot's live entries in one pass over the table (bulk form of cc_read_map_entries): *count =
+ * entries; the first min(cap, count), sorted by (slot, key tag, key), go to the arrays.                      */
+int  cc_read_map_table(cc_engine* e, uint64_t cap, uint64_t* count, uint32_t* h_slot, uint8_t* h_key_tag, uint64_t* h_key,
+                       uint8_t* h_value_tag, uint64_t* h_value, uint64_t* h_commit_index);
 
 /* LockState (LockState.java:33-36) after the timers due at the engine clock: holder instance slot (-1 none),
  * its commit index and cleaned flag; *count = queued waiters, the first min(cap, count) to the arrays. */
