@@ -442,9 +442,70 @@ extern "C" int cc_sync(cc_engine* e) {
 
 // Registry updates are control-plane (the reference runs them as log commands too: ResourceManager.java:77-235);
 // the host orders them against batches, so they first drain the stream the last batch ran on.
-int cc::quiesce(cc_engine* e) {
+int cc::sync_streams(cc_engine* e) {
   HIPCHECK(hipSetDevice(e->device));
   HIPCHECK(hipStreamSynchronize(e->last_stream));
+  return CC_OK;
+}
+
+int cc::quiesce(cc_engine* e) {
+  int rc = sync_streams(e);
+  if (rc) return rc;
+  return e->dev_dirty() ? dev_flush(e) : CC_OK;
+}
+
+// queued registry writes (cc_engine::dev_pend): fills and copies per destination array, coalesced when contiguous
+static void dev_fill(cc_engine* e, void* base, uint64_t off, int val, uint64_t bytes) {
+  if (!bytes) return;
+  auto& v = e->dev_pend[base];
+  uint8_t* dst = (uint8_t*)base + off;
+  if (!v.empty() && v.back().fill == val && v.back().dst + v.back().bytes == dst) {
+    v.back().bytes += bytes;
+    return;
+  }
+  v.push_back(cc_engine::DevWrite{dst, bytes, val, {}});
+}
+static void dev_copy(cc_engine* e, void* base, uint64_t off, const void* src, uint64_t bytes) {
+  if (!bytes) return;
+  auto& v = e->dev_pend[base];
+  uint8_t* dst = (uint8_t*)base + off;
+  const uint8_t* s = (const uint8_t*)src;
+  if (!v.empty() && v.back().fill < 0 && v.back().dst + v.back().bytes == dst) {
+    v.back().data.insert(v.back().data.end(), s, s + bytes);
+    v.back().bytes += bytes;
+    return;
+  }
+  v.push_back(cc_engine::DevWrite{dst, bytes, -1, std::vector<uint8_t>(s, s + bytes)});
+}
+static void mark_dirty(uint64_t& lo, uint64_t& hi, uint64_t a, uint64_t b) {
+  lo = std::min(lo, a);
+  hi = std::max(hi, b);
+}
+
+int cc::dev_flush(cc_engine* e) {
+  for (auto& kv : e->dev_pend)
+    for (auto& w : kv.second) {
+      if (w.fill >= 0) HIPCHECK(hipMemset(w.dst, w.fill, w.bytes));
+      else HIPCHECK(hipMemcpy(w.dst, w.data.data(), w.bytes, hipMemcpyHostToDevice));
+    }
+  e->dev_pend.clear();
+  if (e->res_dirty_hi) {
+    HIPCHECK(hipMemcpy(e->d_res_type + e->res_dirty_lo, e->res_type.data() + e->res_dirty_lo,
+                       e->res_dirty_hi - e->res_dirty_lo, hipMemcpyHostToDevice));
+    e->res_dirty_lo = ~0ull;
+    e->res_dirty_hi = 0;
+  }
+  if (e->inst_dirty_hi) {
+    const uint64_t lo = e->inst_dirty_lo, n = e->inst_dirty_hi - lo;
+    HIPCHECK(hipMemcpy(e->d_inst_res + lo, e->inst_res.data() + lo, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(e->d_inst_id + lo, e->inst_id.data() + lo, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
+    e->inst_dirty_lo = ~0ull;
+    e->inst_dirty_hi = 0;
+  }
+  if (e->sb_kind_dirty) {
+    HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
+    e->sb_kind_dirty = false;
+  }
   return CC_OK;
 }
 
@@ -463,7 +524,7 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
   for (uint64_t s = first; s < end; ++s) {
     if (e->res_type[s] != CC_RES_NONE) return set_err(CC_ERR_INVALID, "resource slot already in use");
   }
-  int rc = quiesce(e);
+  int rc = sync_streams(e);  // (its device writes are queued: dev_flush before the next device work)
   if (rc) return rc;
   const bool value_events = (e->cfg.flags & CC_CFG_VALUE_EVENTS) != 0;
   if (is_coord(type) && (rc = ensure_ext(e, true))) return rc;
@@ -474,27 +535,28 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
     e->res_zombie[s] = 0;
     e->used_res.set(s);
   }
-  HIPCHECK(hipMemcpy(e->d_res_type + first, e->res_type.data() + first, count, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemcpy(e->d_sb_kind, e->sb_kind.data(), e->sb, hipMemcpyHostToDevice));
-  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)first * coord_block(e->coord_cap), 0, coord_block(e->coord_cap) * (uint64_t)count));
+  mark_dirty(e->res_dirty_lo, e->res_dirty_hi, first, end);
+  e->sb_kind_dirty = true;
+  if (e->coord_on)
+    dev_fill(e, e->d_coord, (uint64_t)first * coord_block(e->coord_cap), 0, coord_block(e->coord_cap) * (uint64_t)count);
   if (is_keyed(type)) {  // a new HashMap: capacity 16, no history
-    HIPCHECK(hipMemset(e->d_mw_peak + first, 0, sizeof(uint32_t) * count));
-    HIPCHECK(hipMemset(e->d_mw_drop + first, 0, sizeof(uint64_t) * count));
-    HIPCHECK(hipMemset(e->d_mw_tdrop + first, 0, sizeof(uint64_t) * count));
-    HIPCHECK(hipMemset(e->d_msize + first, 0, sizeof(uint32_t) * count));
-    HIPCHECK(hipMemset(e->d_mpcap + first, 0, sizeof(uint32_t) * count));
+    dev_fill(e, e->d_mw_peak, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
+    dev_fill(e, e->d_mw_drop, sizeof(uint64_t) * first, 0, sizeof(uint64_t) * count);
+    dev_fill(e, e->d_mw_tdrop, sizeof(uint64_t) * first, 0, sizeof(uint64_t) * count);
+    dev_fill(e, e->d_msize, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
+    dev_fill(e, e->d_mpcap, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
     // MapState's table followed key by key while small (map_small.hip); sets / multimaps have no order-dependent op
     std::vector<SmallMap> sm(count);
     const bool is_map = type == CC_RES_MAP;
     for (auto& x : sm) x.flags = is_map ? kSmIn : 0u;  // (TTL mode too: its commit + expiry events are replayed)
-    HIPCHECK(hipMemcpy(e->d_msm + first, sm.data(), sizeof(SmallMap) * count, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemset(e->d_msmall + first, is_map ? 1 : 0, count));
+    dev_copy(e, e->d_msm, sizeof(SmallMap) * first, sm.data(), sizeof(SmallMap) * count);
+    dev_fill(e, e->d_msmall, first, is_map ? 1 : 0, count);
     if (is_map && !e->ttl_live) e->small_live = true;
   }
   // fresh state: AtomicValueState() {value = null; current = null}
-  HIPCHECK(hipMemset(e->d_val_meta + first, 0, sizeof(uint32_t) * count));
-  HIPCHECK(hipMemset(e->d_val_v + first, 0, sizeof(uint64_t) * count));
-  if (e->d_val_live) HIPCHECK(hipMemset(e->d_val_live + first, 0, sizeof(uint64_t) * count));
+  dev_fill(e, e->d_val_meta, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
+  dev_fill(e, e->d_val_v, sizeof(uint64_t) * first, 0, sizeof(uint64_t) * count);
+  if (e->d_val_live) dev_fill(e, e->d_val_live, sizeof(uint64_t) * first, 0, sizeof(uint64_t) * count);
   return CC_OK;
 }
 
@@ -543,7 +605,7 @@ int cc::drain_leaks(cc_engine* e) {
 
 // ResourceManager.deleteResource after resource.stateMachine.delete() succeeded (ResourceManager.java:212-235).
 int cc::delete_slot(cc_engine* e, uint32_t slot) {
-  int rc = quiesce(e);
+  int rc = sync_streams(e);  // (its device writes are queued: dev_flush before the next device work)
   if (rc) return rc;
   const uint32_t old_type = e->res_type[slot];
   if ((rc = drain_leaks(e))) return rc;
@@ -554,25 +616,24 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
       return set_err(CC_ERR_HIP, "map drop launch", hipGetLastError());
     HIPCHECK(hipStreamSynchronize(e->own_stream));
   }
-  if (e->map_bits) HIPCHECK(hipMemset(e->d_msmall + slot, 0, 1));  // no more small-map events for it
+  if (e->map_bits) dev_fill(e, e->d_msmall, slot, 0, 1);  // no more small-map events for it
   e->res_type[slot] = CC_RES_NONE;
   // ResourceManagerStateMachineExecutor.close cancels the resource's timers
   e->gtimers.erase(std::remove_if(e->gtimers.begin(), e->gtimers.end(),
                                   [slot](const cc_engine::GroupTimer& g) { return g.slot == slot; }),
                    e->gtimers.end());
-  if (e->coord_on) HIPCHECK(hipMemset(e->d_coord + (uint64_t)slot * coord_block(e->coord_cap), 0, coord_block(e->coord_cap)));
-  HIPCHECK(hipMemcpy(e->d_res_type + slot, e->res_type.data() + slot, 1, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemset(e->d_val_meta + slot, 0, sizeof(uint32_t)));
-  HIPCHECK(hipMemset(e->d_val_v + slot, 0, sizeof(uint64_t)));
-  if (e->d_val_live) HIPCHECK(hipMemset(e->d_val_live + slot, 0, sizeof(uint64_t)));
-  const uint32_t none = kNoRes;
+  if (e->coord_on) dev_fill(e, e->d_coord, (uint64_t)slot * coord_block(e->coord_cap), 0, coord_block(e->coord_cap));
+  mark_dirty(e->res_dirty_lo, e->res_dirty_hi, slot, slot + 1);
+  dev_fill(e, e->d_val_meta, sizeof(uint32_t) * slot, 0, sizeof(uint32_t));
+  dev_fill(e, e->d_val_v, sizeof(uint64_t) * slot, 0, sizeof(uint64_t));
+  if (e->d_val_live) dev_fill(e, e->d_val_live, sizeof(uint64_t) * slot, 0, sizeof(uint64_t));
   for (uint32_t i = 0; i < e->cfg.max_instances; ++i)
     if (e->inst_res[i] == slot) {
       e->inst_res[i] = kNoRes;
       e->sessions.remove((int64_t)e->inst_id[i]);
       e->inst_by_id.erase(e->inst_id[i]);
       e->used_inst.clear(i);
-      HIPCHECK(hipMemcpy(e->d_inst_res + i, &none, sizeof none, hipMemcpyHostToDevice));
+      mark_dirty(e->inst_dirty_lo, e->inst_dirty_hi, i, i + 1);
     }
   // ResourceManager.resources / keys / ResourceHolder.sessions
   auto rit = e->res_by_id.find(e->res_id[slot]);
@@ -595,7 +656,7 @@ int cc::open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_fi
     if (e->inst_res[first + k] != kNoRes) return set_err(CC_ERR_INVALID, "instance slot already open");
     if (e->inst_by_id.count(id_first + k)) return set_err(CC_ERR_INVALID, "instance id already open");
   }
-  int rc = quiesce(e);
+  int rc = sync_streams(e);  // (its device writes are queued: dev_flush before the next device work)
   if (rc) return rc;
   for (uint64_t k = 0; k < count; ++k) {
     e->inst_res[first + k] = (uint32_t)(res_first + k * res_stride);
@@ -605,8 +666,7 @@ int cc::open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_fi
     e->inst_by_id[id_first + k] = (uint32_t)(first + k);
     e->used_inst.set(first + k);
   }
-  HIPCHECK(hipMemcpy(e->d_inst_res + first, e->inst_res.data() + first, sizeof(uint32_t) * count, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemcpy(e->d_inst_id + first, e->inst_id.data() + first, sizeof(uint64_t) * count, hipMemcpyHostToDevice));
+  mark_dirty(e->inst_dirty_lo, e->inst_dirty_hi, first, end);
   return CC_OK;
 }
 
@@ -704,6 +764,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   HIPCHECK(hipSetDevice(e->device));
   hipStream_t st = stream ? (hipStream_t)stream : e->own_stream;
   if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
+  if (e->dev_dirty()) {  // registry writes queued by the control plane since the last device work
+    int rc = quiesce(e);
+    if (rc) return rc;
+  }
   e->last_stream = st;
   if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15) || (((uintptr_t)c->inst) & 15))
     return set_err(CC_ERR_INVALID, "inst and value must be 16-byte aligned, status 4-byte aligned");

@@ -16,7 +16,9 @@
 namespace cc {
 // error reporting (cc_last_error) and the stream drain every registry update starts with
 int set_err(int code, const char* what, hipError_t e = hipSuccess);
-int quiesce(cc_engine* e);
+int quiesce(cc_engine* e);      // drains the streams, then applies the queued registry writes (dev_flush)
+int sync_streams(cc_engine* e);  // drains the streams only (control-plane updates that queue their device writes)
+int dev_flush(cc_engine* e);
 // registry primitives (engine.hip): resource slots [first, first+count) of `type`; instance slots first+k ->
 // resource res_first + k*res_stride, instance id id_first+k, owned by `client`; a successful deleteResource
 int create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type);
@@ -109,6 +111,19 @@ struct cc_engine {
   std::vector<uint8_t> res_zombie;        // [slots] removed from `resources` by a deleteResource whose delete() threw
   cc::SlotBits used_res, used_inst;       // slot occupancy (allocation: values/maps low, coordination high; instances low)
   std::set<uint32_t> open_grp[16];        // per coordination type: 64-slot groups holding only that type, with room
+  // Control-plane registry writes queued for the next device work (engine.hip dev_flush): a run of creates / opens
+  // coalesces into one copy or fill per array instead of ~10 blocking copies per call.  Mirrored arrays (res_type,
+  // sb_kind, inst_res + inst_id) upload their dirty host range; the others queue fills / copies per array, in order.
+  struct DevWrite {
+    uint8_t* dst;
+    uint64_t bytes;
+    int fill;                   // byte value, or -1: copy `data`
+    std::vector<uint8_t> data;
+  };
+  std::map<const void*, std::vector<DevWrite>> dev_pend;
+  uint64_t res_dirty_lo = ~0ull, res_dirty_hi = 0, inst_dirty_lo = ~0ull, inst_dirty_hi = 0;
+  bool sb_kind_dirty = false;
+  bool dev_dirty() const { return !dev_pend.empty() || res_dirty_hi || inst_dirty_hi || sb_kind_dirty; }
   // device registry + state
   uint32_t* d_inst_res = nullptr;
   uint8_t* d_res_type = nullptr;

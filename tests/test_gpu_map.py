@@ -70,6 +70,27 @@ def test_map_random_parity(n, maps, keys, seed, hot, p_hot, cap):
     _assert_maps(E, O, range(maps))
 
 
+def test_map_table_bulk_readback():
+    """cc_read_map_table (every map's entries in one table pass, sorted by slot, key tag, key) equals the per-map
+    readback and the oracle's maps."""
+    from copycat_amd.workload import map_random_stream
+
+    maps = 37
+    b = map_random_stream(60_000, maps, maps + 8, keys=64, seed=81, hot=2, p_hot=0.3)
+    E, O = _engines(maps, maps + 8, len(b), 65536)
+    _assert_rows(*_apply_both(E, O, [b]))
+    sl, kt, k, vt, v, ci = E.map_table()
+    assert np.all(np.diff(sl.astype(np.int64)) >= 0)
+    bounds = np.searchsorted(sl, np.arange(maps + 1))
+    for m in range(maps):
+        a, z = bounds[m], bounds[m + 1]
+        one = E.map_entries(m)
+        for x, y in zip((kt[a:z], k[a:z], vt[a:z], v[a:z], ci[a:z]), one):
+            assert np.array_equal(x, y), m
+        for x, y in zip(one, O.map_entries(m)):
+            assert np.array_equal(x, y), m
+
+
 @pytest.mark.parametrize("n,sub_batch,hot,p_hot,seed", [
     (400_000, 65536, 8, 0.6, 41),    # 7 sub-batches; each hot key ~5K commits per sub-batch: 2 scan pieces
     (2_000_000, 0, 8, 0.6, 42),      # one sub-batch: ~37 pieces per hot key (carry across many pieces)
