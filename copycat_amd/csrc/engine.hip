@@ -836,8 +836,22 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       if (!rc && may_leak) rc = ensure_leak(e, n);
       if (rc) return rc;
     }
-    if (nb > kBarCap)
-      return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/size/isEmpty/clear/Delete) and group schedules in one batch than kBarCap");
+    if (nb > kBarCap) {
+      // More barrier rows than one listing holds: the batch runs as two consecutive batches (a batch boundary is a
+      // point of the log like any other: timers due by its clock have fired there in both timer orders, A8).  With an
+      // event stream the halves' events would need one output: that case still fails.
+      if (ev || n < 2)
+        return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/clear/Delete, size/isEmpty in TTL mode) and group "
+                                        "schedules in one batch with an event stream than kBarCap");
+      const uint64_t h = n / 2;
+      auto shift = [h](const auto* p) { return p ? p + h : p; };
+      const cc_batch c2{shift(c->index), shift(c->time), shift(c->inst), shift(c->op), shift(c->flags), shift(c->key),
+                        shift(c->a), shift(c->b), shift(c->aux)};
+      const cc_results o2{out->status + h, out->value + h};
+      int rc = cc_apply_batch(e, c, h, out, nullptr, stream);
+      if (!rc) rc = cc_apply_batch(e, &c2, n - h, &o2, nullptr, stream);
+      return rc;
+    }
     if (nb) {  // the barrier rows in log order, then their columns in one gather (one copy back, not one per field)
       e->bars.resize(nb);
       HIPCHECK(hipMemcpy(e->bars.data(), e->d_bar, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost));

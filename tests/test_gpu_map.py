@@ -467,6 +467,23 @@ def test_map_hot_placeholders_after_clear_then_ttl():
     _assert_maps(E, O, range(maps))
 
 
+def test_map_more_barrier_rows_than_one_listing():
+    """More containsValue / clear rows in one batch than one barrier listing holds (kBarCap = 65,536): the engine
+    applies the batch as consecutive halves (no CC_ERR_CAPACITY), every row as the oracle answers it."""
+    from copycat_amd.workload import map_random_stream
+
+    maps, n = 2, 150_000
+    b = map_random_stream(n, maps, maps + 8, keys=16, seed=91)
+    rng = np.random.default_rng(91)
+    rows = np.sort(rng.choice(n, 70_000, replace=False))
+    b.op[rows] = np.where(rng.random(len(rows)) < 0.98, abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_CLEAR).astype(np.uint8)
+    b.a[rows] = rng.integers(0, 3, len(rows)).astype(np.uint64)
+    b.flags[rows] = np.uint8(abi.cc_flags(abi.CC_TAG_LONG, 0, 0))
+    E, O = _engines(maps, maps + 8, n, 4096)
+    _assert_rows(*_apply_both(E, O, [b]))
+    _assert_maps(E, O, range(maps))
+
+
 def test_map_clear_then_reuse_keys():
     """clear / Delete drop every entry of one map (other maps keep theirs); the same keys are then re-put
     as new HashMap nodes; size and isEmpty follow."""
