@@ -131,7 +131,8 @@ __device__ inline void pc_materialize(const PComp& c, uint32_t w0, uint64_t v0, 
 // clock; manager mode: the previous commit's, A8), and a commit that stores a value re-arms or cancels the timer.
 // The per-record clocks come from the input columns through map_row (staging position -> batch row).
 template <bool TTL>
-__global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
+__global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict__ xr, const uint64_t* __restrict__ cb, uint64_t row0,
+                                                  const uint16_t* __restrict__ ttab,
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
                                                   uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
@@ -321,11 +322,13 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const XRec* __restrict_
         const uint32_t lo = tmap[c - c0];
         ng[j] = rstart[lo] + (c - rpre[lo]);
         const u64x2* rec = reinterpret_cast<const u64x2*>(xr + ng[j]);  // (the log index is read at write-back)
-        nab[j] = rec[0];
-        nkey[j] = rec[1].x;
-        const u64x2 mr = rec[2];
-        nm[j] = (uint32_t)mr.x;
-        nres[j] = (uint32_t)(mr.x >> 32);
+        const u64x2 r0 = rec[0], r1 = rec[1];  // (a, key), (idx, meta | rr << 32)
+        nkey[j] = r0.y;
+        nm[j] = (uint32_t)r1.y;
+        nres[j] = (uint32_t)(r1.y >> 32) & kMwSlotMask;
+        nab[j] = u64x2{r0.x, 0ull};
+        if (smeta_op(nm[j]) == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(nm[j])) != CC_TAG_NULL)
+          nab[j].y = cb[row0 + (uint64_t)(ng[j] / kTile) * kTile + ((uint32_t)(r1.y >> 32) >> 17)];  // (mrec_ab)
       }
     }
   };
@@ -722,11 +725,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.map_bits == 0 || a.tiles == 0) return 0;
   a.mark(K_APPLY_MAP, 1, st);
   if (a.ttl)
-    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, a.err);
   else
-    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.xrec, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.err);
   a.mark(K_APPLY_MAP, 0, st);

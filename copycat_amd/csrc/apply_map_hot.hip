@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ ho
 }
 
 // materialize a branch outcome applied to the snapshot: map_apply state (word, value) + commit/insert index
-__device__ inline void materialize(const Comp& c, const HotS0& s0, const XRec* __restrict__ xr, uint32_t& w,
+__device__ inline void materialize(const Comp& c, const HotS0& s0, const MRec* __restrict__ xr, uint32_t& w,
                                    uint64_t& v, uint64_t& ci, uint64_t& ins) {
   const bool present0 = (s0.w & kMwPresent) != 0;
   const Br b = present0 ? c.P : c.A;
@@ -449,7 +449,7 @@ __device__ inline void materialize(const Comp& c, const HotS0& s0, const XRec* _
   } else {
     const uint32_t tag = CC_FLAG_TAG_A(smeta_flags(xr[b.v].meta));
     w = (base & ~kMwUnseen) | kMwPresent | (tag << 21);
-    v = tag ? xr[b.v].ab.x : 0;
+    v = tag ? xr[b.v].a : 0;
     ci = xr[b.v].idx;
     ins = b.n == kOrig ? s0.ins : xr[b.n].idx;
   }
@@ -477,7 +477,8 @@ __device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint
   return msz_word(0, was, (w & kMwPresent) != 0);
 }
 
-__global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, const uint32_t* __restrict__ hot_n,
+__global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, const uint64_t* __restrict__ cb, uint64_t row0,
+                                                  const uint32_t* __restrict__ hot_n,
                                                   const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_len,
                                                   const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_rstart,
                                                   uint32_t tiles, const Comp* __restrict__ agg,
@@ -512,7 +513,8 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
         uint32_t codes = 0;
         for (uint32_t q = 0; q < L; ++q) {
           const uint32_t g = cur.next();
-          codes |= hot_step(g, xr[g].meta, xr[g].ab, xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, err) << (2 * (q % 16));
+          codes |= hot_step(g, xr[g].meta, mrec_ab(xr[g], cb, row0, g), xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, err)
+                   << (2 * (q % 16));
           if (q % 16 == 15 || q + 1 == L) {
             msz[q / 16] = codes;
             codes = 0;
@@ -575,7 +577,9 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const XRec* __restrict__ xr, 
       uint32_t codes = 0;
 #pragma unroll
       for (int q = 0; q < kHPer; ++q)
-        if (p0 + q < e) codes |= hot_step(gs[q], ms[q], xr[gs[q]].ab, xr[gs[q]].idx, sw, sv, ci, ins, rst_status, rst_value, err) << (2 * q);
+        if (p0 + q < e)
+          codes |= hot_step(gs[q], ms[q], mrec_ab(xr[gs[q]], cb, row0, gs[q]), xr[gs[q]].idx, sw, sv, ci, ins, rst_status,
+                            rst_value, err) << (2 * q);
       // (consecutive threads: consecutive words / halves / bytes of the code words, little-endian)
       if (kHPer == 16) msz[p0 / 16] = codes;
       else if (kHPer == 8) reinterpret_cast<uint16_t*>(msz)[p0 / 8] = (uint16_t)codes;
@@ -618,7 +622,7 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
                      reinterpret_cast<HotS0*>(a.hot_s0));
   hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.hot_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
                      a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond);
-  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.xrec, a.hot_n, a.hot, a.hot_len,
+  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.mrec, a.cb, a.lo, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
                      a.rst_value, a.hot_msz, a.err);

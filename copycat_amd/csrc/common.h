@@ -261,6 +261,17 @@ struct XRec {
   uint64_t pad;
 };
 static_assert(sizeof(XRec) == 48, "XRec is three 16-byte words");
+// One staged map / set / multimap record (k_part_ext -> k_apply_map, k_hot_*, launch_map_size): 32 bytes.  The b
+// operand is read only by replaceIfPresent (its compare value, MapState.java:207-228): from the batch's b column, by
+// the record's row in its partition tile (rr >> 17), instead of 8 more bytes in every record.
+struct MRec {
+  uint64_t a;     // value operand
+  uint64_t key;
+  uint64_t idx;   // log index
+  uint32_t meta;  // op | flags << 8 | slot low byte << 16 | kMetaTtl
+  uint32_t rr;    // map slot | row in the partition tile << 17
+};
+static_assert(sizeof(MRec) == 32, "MRec is two 16-byte words");
 // one event of the per-sub-batch arena (apply_coord.hip -> events.hip)
 struct EvRec {
   uint32_t g;       // staging position of the commit
@@ -319,6 +330,13 @@ constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
 // a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
 __device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
   return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);
+}
+
+// a map record's operands: (a, b), b gathered from the batch's b column for the one op that reads it (see MRec)
+__device__ inline u64x2 mrec_ab(const MRec& r, const uint64_t* __restrict__ cb, uint64_t lo, uint32_t g) {
+  const uint32_t fl = smeta_flags(r.meta);
+  const bool needs_b = smeta_op(r.meta) == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(fl) != CC_TAG_NULL;
+  return u64x2{r.a, needs_b ? cb[lo + (uint64_t)(g / kTile) * kTile + (r.rr >> 17)] : 0ull};
 }
 
 // log2(HashMap capacity / 16) after the size peaked at p (resize doubles the table when ++size > 0.75 capacity)

@@ -99,7 +99,7 @@ static void free_all(cc_engine* e) {
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
                   e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp,
-                  e->d_szq,      e->d_szq_n,    e->d_bar_rows, e->d_fb};
+                  e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -289,6 +289,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_ttab, sizeof(uint16_t) * e->max_tiles * (e->sbq_base() + 4 * e->sb + 2));
   if (e->map_bits) {
     ALLOC(e->d_tbl_key, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_mrec, sizeof(MRec) * e->sub_batch);
     ALLOC(e->d_tbl_word, sizeof(uint32_t) * e->map_entries);
     ALLOC(e->d_tbl_val, sizeof(uint64_t) * e->map_entries);
     ALLOC(e->d_tbl_ci, sizeof(uint64_t) * e->map_entries);
@@ -976,7 +977,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.inst_res = e->d_inst_res;
       ha.res_type = e->d_res_type;
       ha.max_inst = e->cfg.max_instances;
-      ha.xrec = e->d_xrec;
+      ha.mrec = e->d_mrec;
+      ha.cb = c->b;
       ha.ttab = e->d_ttab;
       ha.tiles = tiles;
       ha.sb = e->sb_total();
@@ -1040,6 +1042,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.st_meta = e->d_st_meta;
     pa.st_ab = e->d_st_ab;
     pa.xrec = e->d_xrec;
+    pa.mrec = e->d_mrec;
     pa.hot_meta = e->d_hot_meta;
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
@@ -1079,7 +1082,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (e->map_bits) {
       if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
-      ma.xrec = e->d_xrec;
+      ma.mrec = e->d_mrec;
+      ma.cb = c->b;
+      ma.lo = lo;
       ma.ttab = e->d_ttab;
       ma.tiles = tiles;
       ma.sb = e->sb_total();
@@ -1137,7 +1142,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.mpcap = e->d_mpcap;
         za.list = e->d_msz_list;
         za.list_n = e->d_msz_list_n;
-        za.xrec = e->d_xrec;
+        za.mrec = e->d_mrec;
         za.hh_key = e->d_hh_key;
         za.hh_val = e->d_hh_val;
         za.hh_n = e->hh_n;
@@ -1181,7 +1186,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           if (rc) return rc;
           if (!c->index) return set_err(CC_ERR_INVALID, "an engine with maps needs the index column (log order)");
           za.msmall = e->d_msmall;
-          za.xrec = e->d_xrec;
+          za.mrec = e->d_mrec;
           za.idx0 = c->index + lo;
           za.hh_key = e->d_hh_key;
           za.hh_val = e->d_hh_val;

@@ -47,7 +47,8 @@ struct PartArgs {
   const uint32_t* hot_n;
   uint32_t* st_meta;  // staging records [sub_batch], tile-local layout
   u64x2* st_ab;
-  XRec* xrec;         // extended staging records (k_part_ext)
+  XRec* xrec;         // extended staging records (k_part_ext): coordination and value-event commits
+  MRec* mrec;         // map / set / multimap commits' 32-byte records (same staging positions)
   uint32_t* hot_meta; // maps: the meta word of each hot-bucket record again, compact (k_hot_agg reads only these)
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
@@ -85,7 +86,9 @@ int launch_apply_value_v3(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct MapArgs {
-  const XRec* xrec;
+  const MRec* mrec;
+  const uint64_t* cb;  // the batch's b column (replaceIfPresent's compare value, mrec_ab)
+  uint64_t lo;         // the sub-batch's first row
   const uint16_t* ttab;
   uint32_t tiles;
   uint32_t sb;  // total super-buckets (ttab row width - 1)
@@ -142,7 +145,7 @@ struct MapSizeArgs {
   uint32_t* list_n;
   // small maps (map_small.hip): events of the maps still in the window (null msmall: none is)
   const uint8_t* msmall;       // [max_resources] 1: the map's table is small (capacity <= 64), followed key by key
-  const XRec* xrec;            // the sub-batch's staging records (log index, key, key tag)
+  const MRec* mrec;            // the sub-batch's map records (log index, key, key tag)
   const uint64_t* idx0;        // device: the log index of the sub-batch's first row
   const uint64_t* hh_key;      // String.hashCode of HANDLE keys (cc_handle_hashes), sorted by handle
   const int32_t* hh_val;
@@ -281,7 +284,8 @@ struct HotArgs {
   const uint8_t* res_type;
   uint32_t max_inst;
   // scan (after the partition)
-  const XRec* xrec;
+  const MRec* mrec;
+  const uint64_t* cb;  // the batch's b column (mrec_ab)
   const uint16_t* ttab;
   uint32_t tiles, sb, sb_val, map_bits;
   uint64_t* tbl_key;

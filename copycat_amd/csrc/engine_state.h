@@ -146,6 +146,7 @@ struct cc_engine {
   uint64_t* d_tbl_ci = nullptr;
   uint64_t* d_tbl_ins = nullptr;
   XRec* d_xrec = nullptr;  // [sub_batch] extended staging records (partition_ext.hip)
+  MRec* d_mrec = nullptr;  // [sub_batch] map / set / multimap records (same staging positions; maps only)
   // hot map keys (apply_map_hot.hip)
   HotKey* d_hot = nullptr;
   uint32_t* d_hot_n = nullptr;

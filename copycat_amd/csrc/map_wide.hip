@@ -510,7 +510,7 @@ __device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_
 
 // A map commit's insertion / removal as an event (map_small.hip): its position (the log index's offset in the
 // sub-batch, or in TTL mode 2 * row offset + 1: common.h TtlEmit) and the key's HashMap hash.
-__device__ inline void map_event(uint32_t m, uint32_t code, uint64_t d, const XRec& xr, const uint64_t* __restrict__ hh_key,
+__device__ inline void map_event(uint32_t m, uint32_t code, uint64_t d, const MRec& xr, const uint64_t* __restrict__ hh_key,
                                  const int32_t* __restrict__ hh_val, uint32_t hh_n, uint64_t* __restrict__ ev_key,
                                  uint32_t* __restrict__ ev_val, uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
                                  uint32_t* __restrict__ err) {
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
                                                       const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
                                                       const uint32_t* __restrict__ hot_msz, uint32_t R,
                                                       uint32_t* __restrict__ tcnt, uint32_t* __restrict__ list_n,
-                                                      const uint8_t* __restrict__ msmall, const XRec* __restrict__ xrec,
+                                                      const uint8_t* __restrict__ msmall, const MRec* __restrict__ xrec,
                                                       const uint64_t* __restrict__ idx0p, const uint64_t* __restrict__ hh_key,
                                                       const int32_t* __restrict__ hh_val, uint32_t hh_n,
                                                       uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val,
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
 int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.sb_hot, a.rst_msz, a.hot,
-                     a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n, a.msmall, a.xrec,
+                     a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n, a.msmall, a.mrec,
                      a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_cap, a.sm_ctl, a.map_row, a.lo,
                      a.err);
   if (a.map_row) return hipGetLastError() == hipSuccess ? 0 : -1;  // TTL mode: sizes from the events (k_ttl_replay)

@@ -52,7 +52,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint64_t* __restrict__ inst_id, const uint32_t* __restrict__ inst_res, const uint8_t* __restrict__ res_type, const uint8_t* __restrict__ sb_kind,
     uint32_t max_inst, uint32_t sb, uint32_t sb_val, uint32_t map_bits, uint32_t sbq_base,
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
-    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, uint32_t* __restrict__ hot_meta, uint16_t* __restrict__ cpos,
+    u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, MRec* __restrict__ mrec, uint32_t* __restrict__ hot_meta,
+    uint16_t* __restrict__ cpos,
     uint16_t* __restrict__ ttab, uint32_t* __restrict__ err_out) {
   constexpr int J = C / kPT;       // commits per thread per chunk
   constexpr int kXCh = kTile / C;  // chunks per tile
@@ -326,7 +327,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
           }
           meta[j] = (meta[j] & ~0xFFFFu) | mop | (fl << 8);
         }
-        xs[j] = res[j];
+        // map slot | row in the tile << 17 (MRec.rr: replaceIfPresent's b is read from the batch by row)
+        xs[j] = res[j] | ((uint32_t)(w * (kWave * J) + j * kWave + l + ch * C) << 17);
         if ((int64_t)xa[j] > 0 && ty != CC_RES_MULTIMAP) meta[j] |= kMetaTtl;
       } else if (tyb & kTpWalk) {
         value_encode(meta[j] & 0xFF, (meta[j] >> 8) & 0xFF, ab[j].x, ab[j].y, meta[j], ab[j]);
@@ -421,10 +423,12 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
       if (i < tile1) cpos[i - lo] = (uint16_t)cp[j];
     }
-    // write the chunk out run by run (contiguous): k_apply_value records as (meta, operands) columns, every other
-    // record as one 48-byte XRec.  Lanes take consecutive 16-byte pieces (piece p = part p % 3 of sorted record
-    // p / 3), so a wave's store covers 1 KiB of a run contiguously; one lane per record (three stores at a 48-byte
-    // stride) left every piece its own partial-line write request (WRITE_SIZE 99 B per commit against 50).
+    // write the chunk out run by run (contiguous): k_apply_value records as (meta, operands) columns, map records as
+    // one 32-byte MRec (2 pieces), every other record as one 48-byte XRec.  Lanes take consecutive 16-byte pieces
+    // (piece p = part p % 3 of sorted record p / 3), so a wave's store covers a run contiguously; one lane per record
+    // (three stores at a 48-byte stride) left every piece its own partial-line write request (WRITE_SIZE 99 B per
+    // commit against 50).
+    const uint32_t map_lim = sb_hot + (map_bits ? (uint32_t)kHotMax : 0u);  // map regions + hot-key buckets
     for (uint32_t p = t; p < 3 * nlive; p += kPT) {
       const uint32_t s = p / 3, part = p - 3 * s;
       const uint32_t k = rsb[s];
@@ -434,9 +438,13 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
           st_meta[g] = rmeta[s];
           st_ab[g] = rab[s];
         }
+      } else if (k >= sb_val && k < map_lim) {
+        if (part == 2) continue;
+        if (part == 0 && hot_meta && k >= sb_hot) hot_meta[g] = rmeta[s];
+        const u64x2 v = part == 0 ? u64x2{rab[s].x, rkey[s]} : u64x2{ridx[s], (uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32)};
+        reinterpret_cast<u64x2*>(mrec + g)[part] = v;
       } else {
         u64x2 v;
-        if (part == 0 && hot_meta && k >= sb_hot && k < sb_hot + kHotMax) hot_meta[g] = rmeta[s];
         if (part == 0) v = rab[s];
         else if (part == 1) v = u64x2{rkey[s], ridx[s]};
         else v = u64x2{(uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32), IDS ? rpad[s] : 0ull};
@@ -475,7 +483,7 @@ int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c, a.inst_id != nullptr), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_id, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
-                     a.st_meta, a.st_ab, a.xrec, a.map_bits ? a.hot_meta : nullptr, a.cpos, a.ttab, a.err);
+                     a.st_meta, a.st_ab, a.xrec, a.mrec, a.map_bits ? a.hot_meta : nullptr, a.cpos, a.ttab, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
