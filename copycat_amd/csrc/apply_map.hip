@@ -326,9 +326,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         nkey[j] = r0.y;
         nm[j] = (uint32_t)r1.y;
         nres[j] = (uint32_t)(r1.y >> 32) & kMwSlotMask;
-        nab[j] = u64x2{r0.x, 0ull};
-        if (smeta_op(nm[j]) == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(nm[j])) != CC_TAG_NULL)
-          nab[j].y = cb[row0 + (uint64_t)(ng[j] / kTile) * kTile + ((uint32_t)(r1.y >> 32) >> 17)];  // (mrec_ab)
+        // .y = the commit's batch row for now: replaceIfPresent's b is gathered at the top of the chunk that applies
+        // it (mrec_ab; a gather here would wait for this record's load before the chunk in flight goes on)
+        nab[j] = u64x2{r0.x, (uint64_t)(ng[j] / kTile) * kTile + ((uint32_t)(r1.y >> 32) >> 17)};
       }
     }
   };
@@ -370,6 +370,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       keyop[j] = false;
       if (g[j] != 0xFFFFFFFFu) {
         const uint32_t op = smeta_op(m[j]);
+        const uint64_t brow = ab[j].y;
+        ab[j].y = 0;
+        if (op == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(m[j])) != CC_TAG_NULL) ab[j].y = cb[row0 + brow];
         keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
         ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
         p[j] = (uint32_t)map_hash(res[j], CC_FLAG_KTAG(smeta_flags(m[j])), key[j]) & (kMapRegion - 1);

@@ -332,14 +332,7 @@ __global__ __launch_bounds__(kHT) void k_hot_lists(const uint16_t* __restrict__ 
 __device__ inline void hot_items(const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len, uint32_t* pfx,
                                  uint32_t& nh) {
   nh = *hot_n;
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
-    for (uint32_t h = 0; h < nh; ++h) {
-      pfx[h] = s;
-      s += (hot_len[h] + kHotPiece - 1) / kHotPiece;
-    }
-    pfx[nh] = s;
-  }
+  hot_piece_prefix(hot_len, nh, pfx);
   __syncthreads();
 }
 

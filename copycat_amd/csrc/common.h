@@ -264,6 +264,37 @@ static_assert(sizeof(XRec) == 48, "XRec is three 16-byte words");
 // One staged map / set / multimap record (k_part_ext -> k_apply_map, k_hot_*, launch_map_size): 32 bytes.  The b
 // operand is read only by replaceIfPresent (its compare value, MapState.java:207-228): from the batch's b column, by
 // the record's row in its partition tile (rr >> 17), instead of 8 more bytes in every record.
+// pfx[h] = scan pieces of the hot keys before h, for h <= nh (hot_len: each key's list length).  Wave 0 does it, 4 keys
+// per lane with their loads in flight together, and a wave scan: one thread walking the keys waited for each load in
+// turn (~256 dependent global round trips at the top of every workgroup of the hot / size kernels).  The caller
+// synchronises the workgroup before reading pfx.
+__device__ inline void hot_piece_prefix(const uint32_t* __restrict__ hot_len, uint32_t nh, uint32_t* pfx) {
+  constexpr int PL = (kHotMax + kWave - 1) / kWave;
+  if (threadIdx.x >= (uint32_t)kWave) return;
+  const uint32_t l = threadIdx.x;
+  uint32_t c[PL], sum = 0;
+#pragma unroll
+  for (int q = 0; q < PL; ++q) {
+    const uint32_t h = l * PL + q;
+    c[q] = h < nh ? (hot_len[h] + kHotPiece - 1) / kHotPiece : 0u;
+    sum += c[q];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, kWave);
+    if (l >= (uint32_t)d) inc += y;
+  }
+  uint32_t run = inc - sum;
+#pragma unroll
+  for (int q = 0; q < PL; ++q) {
+    const uint32_t h = l * PL + q;
+    if (h <= nh) pfx[h] = run;
+    run += c[q];
+  }
+  if (l == kWave - 1 && nh == (uint32_t)(PL * kWave)) pfx[nh] = inc;
+}
+
 struct MRec {
   uint64_t a;     // value operand
   uint64_t key;

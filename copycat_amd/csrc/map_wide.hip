@@ -497,14 +497,7 @@ __device__ inline uint32_t hot_code(const uint32_t* __restrict__ hot_msz, const 
 __device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len, uint32_t* pfx,
                                uint32_t& nh) {
   nh = hot_n ? *hot_n : 0u;
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
-    for (uint32_t h = 0; h < nh; ++h) {
-      pfx[h] = s;
-      s += (hot_len[h] + kHotPiece - 1) / kHotPiece;
-    }
-    pfx[nh] = s;
-  }
+  hot_piece_prefix(hot_len, nh, pfx);
   lds_barrier();
 }
 
