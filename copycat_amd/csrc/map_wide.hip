@@ -533,9 +533,48 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
   __shared__ uint32_t cnt[kMszPass];
   if (blockIdx.x == 0 && threadIdx.x == 0) *list_n = 0;  // (k_msize_scan, the next launch, appends to the list)
   __shared__ uint32_t pfx[kHotMax + 1];
+  // each hot key's run in this tile (list positions [hl0, hl1)) and the prefix of its 2-bit code words (wpfx): the
+  // words are then shared out over all threads (one thread per key walked the heaviest key's ~70 words per tile as
+  // a chain of dependent global loads)
+  __shared__ uint32_t hl0[kHotMax], hl1[kHotMax], hsl[kHotMax], wpfx[kHotMax + 1];
   const uint32_t t = blockIdx.x;
   uint32_t nh;
   hot_pfx(hot_n, hot_len, pfx, nh);
+  if (threadIdx.x < kWave) {
+    constexpr int PL = (kHotMax + kWave - 1) / kWave;
+    const uint32_t l = threadIdx.x;
+    uint32_t c[PL], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+      const uint32_t h = l * PL + q;
+      c[q] = 0;
+      if (h < nh) {
+        const uint32_t* rp = hot_rpre + (uint64_t)h * (kMaxTiles + 1);
+        const uint32_t a = rp[t], b = rp[t + 1];
+        hl0[h] = a;
+        hl1[h] = b;
+        hsl[h] = hot[h].ident & kMwSlotMask;
+        c[q] = a < b ? (b - 1) / 16 - a / 16 + 1 : 0u;
+      }
+      sum += c[q];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, kWave);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    uint32_t run = inc - sum;
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+      const uint32_t h = l * PL + q;
+      if (h < nh) wpfx[h] = run;
+      run += c[q];
+    }
+    if (l == kWave - 1) wpfx[kHotMax] = inc;  // all words of the tile
+  }
+  lds_barrier();
+  const uint32_t nwords = wpfx[kHotMax];
   const uint16_t* row = ttab + (uint64_t)t * (sb + 1);
   const uint32_t b0 = row[k0], b1 = row[sb_hot];
   const uint32_t* w = msz + (uint64_t)t * kTile;
@@ -557,20 +596,20 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
                     err);
       }
     }
-    for (uint32_t h = threadIdx.x; h < nh; h += kMszT) {  // one thread per hot key: its run in this tile (a few words)
-      const uint32_t m = (hot[h].ident & kMwSlotMask) - base;
-      const uint32_t* rp = hot_rpre + (uint64_t)h * (kMaxTiles + 1);
-      const uint32_t lp0 = rp[t], lp1 = rp[t + 1];
-      if (m >= span || lp0 >= lp1) continue;
-      uint32_t ins = 0, rem = 0;
-      for (uint32_t wd = lp0 / 16; wd * 16 < lp1; ++wd) {
-        uint32_t x = hot_msz[(uint64_t)pfx[h] * kHotWords + wd];
-        const uint32_t a = wd * 16 < lp0 ? lp0 - wd * 16 : 0u, b = lp1 - wd * 16 < 16u ? lp1 - wd * 16 : 16u;
-        x &= (b == 16u ? ~0u : (1u << (2 * b)) - 1u) & ~((1u << (2 * a)) - 1u);  // positions [a, b) of the word
-        const uint32_t lo = x & 0x55555555u, hi = (x >> 1) & 0x55555555u;
-        ins += __popc(lo & ~hi);
-        rem += __popc(hi & ~lo);
+    for (uint32_t i = threadIdx.x; i < nwords; i += kMszT) {  // one code word (16 list positions) per thread
+      uint32_t h = 0, hb = nh;  // the last key whose words start at or before i (keys without words are skipped)
+      while (hb - h > 1) {
+        const uint32_t c = (h + hb) >> 1;
+        if (wpfx[c] <= i) h = c; else hb = c;
       }
+      const uint32_t m = hsl[h] - base;
+      if (m >= span) continue;
+      const uint32_t lp0 = hl0[h], lp1 = hl1[h], wd = lp0 / 16 + (i - wpfx[h]);
+      uint32_t x = hot_msz[(uint64_t)pfx[h] * kHotWords + wd];
+      const uint32_t a = wd * 16 < lp0 ? lp0 - wd * 16 : 0u, b = lp1 - wd * 16 < 16u ? lp1 - wd * 16 : 16u;
+      x &= (b == 16u ? ~0u : (1u << (2 * b)) - 1u) & ~((1u << (2 * a)) - 1u);  // positions [a, b) of the word
+      const uint32_t lo = x & 0x55555555u, hi = (x >> 1) & 0x55555555u;
+      const uint32_t ins = __popc(lo & ~hi), rem = __popc(hi & ~lo);
       if (ins | rem) atomicAdd(&cnt[m], ins | (rem << 16));
     }
     lds_barrier();

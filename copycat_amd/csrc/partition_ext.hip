@@ -21,6 +21,10 @@ namespace cc {
 #ifndef CC_PART_EXT_UNCOND
 #define CC_PART_EXT_UNCOND 1  // every present column loaded for every row under the full wave mask (0: per-type loads)
 #endif
+#ifndef CC_PART_EXT_LATE
+#define CC_PART_EXT_LATE 1  // the next chunk's columns loaded into the working registers after the placement (0: at
+                            // the top of the chunk, into a second register set)
+#endif
 #ifndef CC_PART_EXT_UNROLL
 #define CC_PART_EXT_UNROLL 0  // 1: the chunk loop fully unrolled (bigger code, fewer spills)
 #endif
@@ -43,7 +47,8 @@ int phase_read_partx(uint64_t* out) {
 
 // C: commits per LDS-staged chunk (2048; 1024 when the buckets' per-wave counters need the room: > 1024 map regions)
 // IDS: coordination engines (instance ids into XRec.pad; a compile-time switch, so map-only engines pay no registers)
-template <int C, bool IDS>
+// TCK: the batch's clock column is checked (kExtTimeCheck; its two clocks per row ride with the chunk's loads)
+template <int C, bool IDS, bool TCK>
 __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op, const uint8_t* __restrict__ flags,
     const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb, const uint64_t* __restrict__ ckey,
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   const bool deferred = (ext_flags & kExtDeferred) != 0;
   // the log clock must not go backwards (each row against the row before it; replaces k_time_check when the batch
   // has no barrier rows, which are not partitioned)
-  const bool tcheck = ctime && (ext_flags & kExtTimeCheck);
+  const bool tcheck = TCK && ctime && (ext_flags & kExtTimeCheck);
   uint32_t tbad = 0;
   uint32_t nhot = 0;
   if (map_bits) {
@@ -125,8 +130,11 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 #pragma unroll
   for (int q = 0; q < kXQ / 4; ++q) tp[q] = 0;
 #pragma unroll
-  for (int hq = 0; hq < kXQ; hq += kXQ / 2) {  // two halves of 8 (register pressure)
-    constexpr int H = kXQ / 2;
+#ifndef CC_PART_EXT_ROUTE_SPLIT
+#define CC_PART_EXT_ROUTE_SPLIT 2  // route stages in two halves of 8 rows (1: all 16 at once, measured no faster)
+#endif
+  for (int hq = 0; hq < kXQ; hq += kXQ / CC_PART_EXT_ROUTE_SPLIT) {
+    constexpr int H = kXQ / CC_PART_EXT_ROUTE_SPLIT;
     uint32_t rr[H];
 #pragma unroll
     for (int u = 0; u < H; ++u) {
@@ -216,40 +224,50 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   PH(0);
 
   // ---- chunks: raw columns of chunk ch + 1 requested at the top of chunk ch ----
-  uint32_t in[J], mt[J], nin[J], nmt[J];
-  u64x2 ab[J], nab[J];
-  uint64_t kk[J], ii[J], xa[J], nkk[J], nii[J], nxa[J];
+  uint32_t in[J], mt[J], fl[J];
+  u64x2 ab[J];
+  uint64_t kk[J], ii[J], xa[J], t0v[J], t1v[J];
+#if !CC_PART_EXT_LATE
+  uint32_t nin[J], nmt[J], nfl[J];
+  u64x2 nab[J];
+  uint64_t nkk[J], nii[J], nxa[J], nt0[J], nt1[J];
+#endif
   // a lock record's raw columns ride in the slots it does not use: ab = (clock, clock of the commit before), kk
   // unused, xa = timeout
   // the route registers rotate by J per chunk: rp[0..J) = this chunk, rp[J..2J) = the next (compile-time indices
   // in a rolled loop)
-  auto load_raw = [&](uint32_t ch, int qb, uint32_t (&in_)[J], uint32_t (&mt_)[J], u64x2 (&ab_)[J], uint64_t (&kk_)[J],
-                      uint64_t (&ii_)[J], uint64_t (&xa_)[J]) {
+  // Raw loads only: a select or an ALU op on a loaded value makes the wave wait for that load right there (one
+  // in-order counter), i.e. for the whole next chunk's columns at the top of this chunk.  So op and flags stay in
+  // two registers until the take, a lock's clocks arrive in ab by address (ctime instead of ca / cb), and the
+  // fields a dead row or a type does not use keep whatever was loaded (nothing reads them: placement skips dead
+  // rows, the record's fields are picked by type at use).
+  auto load_raw = [&](uint32_t ch, int qb, uint32_t (&in_)[J], uint32_t (&mt_)[J], uint32_t (&fl_)[J], u64x2 (&ab_)[J],
+                      uint64_t (&kk_)[J], uint64_t (&ii_)[J], uint64_t (&xa_)[J], uint64_t (&t0_)[J], uint64_t (&t1_)[J]) {
 #if CC_PART_EXT_UNCOND
-    // every column the batch has, for every row (loads under the wave's full mask: no per-type divergent loads),
-    // then the record's fields selected by type
+    // every column the batch has, for every row (loads under the wave's full mask: no per-type divergent loads)
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int q = qb + j;
       const uint64_t i0 = tile0 + (uint64_t)ch * C + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
       const uint64_t i = i0 < tile1 ? i0 : lo;
-      const uint32_t tyb = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu, ty = tyb & ~kTpWalk;
-      const bool dead = rp[q] == kRpDead;
-      const uint32_t iv = inst[i];
-      const uint32_t mv = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
-      const uint64_t av = ca ? ca[i] : 0, bv = cb ? cb[i] : 0, kv = ckey ? ckey[i] : 0, xv = caux ? caux[i] : 0;
-      const uint64_t iv2 = cidx ? cidx[i] : 0;
-      const uint64_t t0 = ctime ? ctime[i] : 0, t1 = ctime && i > 0 ? ctime[i - 1] : 0;
-      tbad |= tcheck && i0 < tile1 && i0 > 0 && t0 < t1 ? 1u : 0u;
-      in_[j] = dead ? kNoRes : iv;
-      mt_[j] = dead ? 0u : mv;
+      const uint32_t ty = ((tp[q / 4] >> (8 * (q % 4))) & 0xFFu) & ~kTpWalk;
       const bool lock = ty == CC_RES_LOCK;
-      const bool val_walk = (tyb & kTpWalk) != 0;
-      ab_[j].x = dead ? 0 : (lock ? t0 : av);
-      ab_[j].y = dead ? 0 : (lock ? t1 : bv);
-      xa_[j] = dead || val_walk ? 0 : ((lock || is_keyed(ty)) ? xv : 0);
-      ii_[j] = dead || val_walk ? 0 : iv2;
-      kk_[j] = dead || val_walk || lock ? 0 : kv;
+      in_[j] = inst[i];
+      mt_[j] = op[i];
+      fl_[j] = flags[i];
+      const uint64_t* pa = lock ? (ctime ? ctime + i : nullptr) : (ca ? ca + i : nullptr);
+      const uint64_t* pb = lock ? (ctime && i > 0 ? ctime + (i - 1) : nullptr) : (cb ? cb + i : nullptr);
+      uint64_t av = 0, bv = 0;
+      if (pa) av = *pa;
+      if (pb) bv = *pb;
+      ab_[j] = u64x2{av, bv};
+      kk_[j] = ckey ? ckey[i] : 0;
+      xa_[j] = caux ? caux[i] : 0;
+      ii_[j] = cidx ? cidx[i] : 0;
+      if (TCK) {  // compared at the take (kErrTime)
+        t0_[j] = ctime ? ctime[i] : 0;
+        t1_[j] = ctime ? ctime[i > 0 ? i - 1 : i] : 0;
+      }
     }
     return;
 #endif
@@ -259,12 +277,14 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const uint64_t i = tile0 + (uint64_t)ch * C + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
       in_[j] = kNoRes;
       mt_[j] = 0;
+      fl_[j] = 0;
       ab_[j] = u64x2{0, 0};
       kk_[j] = ii_[j] = xa_[j] = 0;
       if (rp[q] == kRpDead) continue;
       const uint32_t tyb = (tp[q / 4] >> (8 * (q % 4))) & 0xFFu, ty = tyb & ~kTpWalk;
       in_[j] = inst[i];
-      mt_[j] = (uint32_t)op[i] | ((uint32_t)flags[i] << 8);
+      mt_[j] = op[i];
+      fl_[j] = flags[i];
       if (ty == CC_RES_LOCK) {  // clock of this commit and of the one before it (deterministic log time)
         ab_[j].x = ctime ? ctime[i] : 0;
         ab_[j].y = ctime && i > 0 ? ctime[i - 1] : 0;
@@ -282,15 +302,29 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       }
     }
   };
-  load_raw(0, 0, in, mt, ab, kk, ii, xa);
+  load_raw(0, 0, in, mt, fl, ab, kk, ii, xa, t0v, t1v);
+  // the clock check of a chunk's rows (TCK), at its take
+  auto tcheck_rows = [&](uint32_t ch, const uint64_t (&a_)[J], const uint64_t (&b_)[J]) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint64_t i0 = tile0 + (uint64_t)ch * C + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
+      tbad |= tcheck && i0 < tile1 && i0 > 0 && a_[j] < b_[j] ? 1u : 0u;
+    }
+  };
   // instance ids of the working chunk's records: requested when its instance slots are taken into the working
-  // registers (here for chunk 0, at the take for the others), used at the next placement
+  // registers (here for chunk 0, at the take for the others; CC_PART_EXT_LATE: at the top of the chunk), used at
+  // the placement
   uint64_t idv[J];
   auto issue_ids = [&]() {
 #pragma unroll
     for (int j = 0; j < J; ++j) idv[j] = IDS ? inst_id[in[j] < max_inst ? in[j] : 0u] : 0ull;
   };
+#if !CC_PART_EXT_LATE
+#pragma unroll
+  for (int j = 0; j < J; ++j) mt[j] |= fl[j] << 8;
+  if (TCK) tcheck_rows(0, t0v, t1v);
   issue_ids();
+#endif
 #if CC_PART_EXT_UNROLL
 #pragma unroll
 #else
@@ -300,10 +334,19 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const uint64_t cbase = tile0 + (uint64_t)ch * C;
     if (cbase >= tile1) break;  // block-uniform
     const bool more = ch + 1 < (uint32_t)kXCh && cbase + C < tile1;
-    if (more) load_raw(ch + 1, J, nin, nmt, nab, nkk, nii, nxa);
+#if !CC_PART_EXT_LATE
+    if (more) load_raw(ch + 1, J, nin, nmt, nfl, nab, nkk, nii, nxa, nt0, nt1);
+#endif
     for (uint32_t k = t; k < kPW * hw; k += kPT) wc[k] = 0;
     lds_barrier();
     PH(6);
+#if CC_PART_EXT_LATE
+    // this chunk's columns (loaded before the loop, or after the previous chunk's placement)
+#pragma unroll
+    for (int j = 0; j < J; ++j) mt[j] |= fl[j] << 8;
+    if (TCK) tcheck_rows(ch, t0v, t1v);
+    issue_ids();
+#endif
     // the records of this chunk (compute only: every column arrived with the chunk's loads)
     uint32_t sk[J], loc[J], res[J], meta[J], xs[J];
     bool live[J];
@@ -406,18 +449,25 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     // The next chunk's columns are taken into the working registers HERE, before this chunk's stores: waiting for
     // a load also waits for every memory op issued before it (one in-order counter), so the wait covers only the
     // previous chunk's stores, long done, and not the ones below.
+#if CC_PART_EXT_LATE
+    // the working registers are free (the chunk's records are in LDS): the next chunk's columns fly during the
+    // write-out below (its stores are issued after these loads, so waiting for the loads never waits for them)
+    if (more) load_raw(ch + 1, J, in, mt, fl, ab, kk, ii, xa, t0v, t1v);
+#else
     if (more) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         in[j] = nin[j];
-        mt[j] = nmt[j];
+        mt[j] = nmt[j] | (nfl[j] << 8);
         ab[j] = nab[j];
         kk[j] = nkk[j];
         ii[j] = nii[j];
         xa[j] = nxa[j];
       }
       issue_ids();
+      if (TCK) tcheck_rows(ch + 1, nt0, nt1);
     }
+#endif
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const uint64_t i = cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l;
@@ -477,9 +527,12 @@ size_t part_ext_chunk(uint32_t sb, bool maps, bool ids) {
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   const size_t c = part_ext_chunk(a.sb, a.map_bits != 0, a.inst_id != nullptr);
   if (c == 0) return -1;
-  const bool ids = a.inst_id != nullptr;
-  auto kern = c == (size_t)kChunkMaps ? (ids ? k_part_ext<kChunkMaps, true> : k_part_ext<kChunkMaps, false>)
-                                      : (ids ? k_part_ext<kPT, true> : k_part_ext<kPT, false>);
+  const bool ids = a.inst_id != nullptr, tck = a.time && (a.ext_flags & kExtTimeCheck);
+  auto kern = c == (size_t)kChunkMaps
+                  ? (ids ? (tck ? k_part_ext<kChunkMaps, true, true> : k_part_ext<kChunkMaps, true, false>)
+                         : (tck ? k_part_ext<kChunkMaps, false, true> : k_part_ext<kChunkMaps, false, false>))
+                  : (ids ? (tck ? k_part_ext<kPT, true, true> : k_part_ext<kPT, true, false>)
+                         : (tck ? k_part_ext<kPT, false, true> : k_part_ext<kPT, false, false>));
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c, a.inst_id != nullptr), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_id, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
