@@ -295,11 +295,13 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   uint32_t round = 0;  // resolution rounds (continues across chunks: flag[] is a 3-deep ring)
   PH(0);
 
-  // the records of chunk c0 (this thread's: chunk order (w, j, l) = log order); the next chunk's are requested
-  // at the top of each chunk and land while it is applied
-  uint32_t nm[kMPer], nres[kMPer], ng[kMPer];
-  u64x2 nab[kMPer];
-  uint64_t nkey[kMPer];
+  // The working registers: the records of chunk c0 (this thread's: chunk order (w, j, l) = log order).  The next
+  // chunk's are loaded into the same registers once this chunk's records sit sorted in LDS (after the placement),
+  // and land while the chunk is applied.  They are stored as loaded (res = the raw MRec.rr word, ab.y unused) and
+  // decoded at the top of their chunk: an op on a loaded value waits for the load right there (one in-order counter).
+  uint32_t m[kMPer], res[kMPer], g[kMPer];
+  u64x2 ab[kMPer];
+  uint64_t key[kMPer];
   // tmap for the chunk at c0: each tile writes its own positions (one search per thread, not one per commit)
   auto build_map = [&](uint32_t c0) {
     const uint32_t cend = c0 + kMCh < cnt ? c0 + kMCh : cnt;
@@ -317,18 +319,16 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       const uint32_t c = c0 + w * (kWave * kMPer) + j * kWave + l;
-      ng[j] = 0xFFFFFFFFu;
+      g[j] = 0xFFFFFFFFu;
       if (c < cnt) {
         const uint32_t lo = tmap[c - c0];
-        ng[j] = rstart[lo] + (c - rpre[lo]);
-        const u64x2* rec = reinterpret_cast<const u64x2*>(xr + ng[j]);  // (the log index is read at write-back)
+        g[j] = rstart[lo] + (c - rpre[lo]);
+        const u64x2* rec = reinterpret_cast<const u64x2*>(xr + g[j]);  // (the log index is read at write-back)
         const u64x2 r0 = rec[0], r1 = rec[1];  // (a, key), (idx, meta | rr << 32)
-        nkey[j] = r0.y;
-        nm[j] = (uint32_t)r1.y;
-        nres[j] = (uint32_t)(r1.y >> 32) & kMwSlotMask;
-        // .y = the commit's batch row for now: replaceIfPresent's b is gathered at the top of the chunk that applies
-        // it (mrec_ab; a gather here would wait for this record's load before the chunk in flight goes on)
-        nab[j] = u64x2{r0.x, (uint64_t)(ng[j] / kTile) * kTile + ((uint32_t)(r1.y >> 32) >> 17)};
+        key[j] = r0.y;
+        m[j] = (uint32_t)r1.y;
+        res[j] = (uint32_t)(r1.y >> 32);
+        ab[j].x = r0.x;
       }
     }
   };
@@ -338,39 +338,19 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   // every thread has read tmap for chunk 0 before the first chunk's build_map(c0 + kMCh) overwrites it (without
   // this barrier a fast wave could rebuild tmap under a slow wave's chunk-0 lookups: wrong staging positions)
   lds_barrier();
-  uint32_t m[kMPer], res[kMPer], g[kMPer];
-  u64x2 ab[kMPer];
-  uint64_t key[kMPer];
-  // The working registers take a chunk's records at the END of the chunk before it, after all of that chunk's
-  // work and before its result stores: waiting for a load also waits for every memory op issued before it (one
-  // in-order counter), so the wait never covers stores issued just before it.
-  auto take = [&]() {
-#pragma unroll
-    for (int j = 0; j < kMPer; ++j) {
-      g[j] = ng[j];
-      m[j] = nm[j];
-      ab[j] = nab[j];
-      res[j] = nres[j];
-      key[j] = nkey[j];
-    }
-  };
-  take();
   for (uint32_t c0 = 0; c0 < cnt; c0 += kMCh) {
     uint32_t ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
     bool keyop[kMPer];
     const bool more = c0 + kMCh < cnt;  // block-uniform
-    if (more) {  // (every thread has read tmap for this chunk's loads: it issued them before the last barrier)
-      build_map(c0 + kMCh);
-      lds_barrier();
-      load_chunk(c0 + kMCh);
-    }
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       ent[j] = kNoEnt;
       keyop[j] = false;
       if (g[j] != 0xFFFFFFFFu) {
         const uint32_t op = smeta_op(m[j]);
-        const uint64_t brow = ab[j].y;
+        const uint32_t rr = res[j];  // MRec.rr: map slot | row in the tile << 17
+        res[j] = rr & kMwSlotMask;
+        const uint64_t brow = (uint64_t)(g[j] / kTile) * kTile + (rr >> 17);  // (mrec_ab)
         ab[j].y = 0;
         if (op == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(m[j])) != CC_TAG_NULL) ab[j].y = cb[row0 + brow];
         keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
@@ -543,6 +523,15 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     }
     lds_barrier();
     PH(4);
+    // the chunk's records are in LDS now: the working registers are free for the next chunk (its tmap here, its
+    // loads after the scan's first barrier, which orders the tmap writes before them)
+    uint32_t gs[kMPer], rs[kMPer];
+#pragma unroll
+    for (int j = 0; j < kMPer; ++j) {
+      gs[j] = g[j];
+      rs[j] = res[j];
+    }
+    if (more) build_map(c0 + kMCh);
     // ---- 4. every run (one entry's commits, log order) at once: a segmented scan of the commits'
     //         transformers gives each commit its entry's state before it (map_ops.h); runs holding a
     //         value-comparing op are walked by one thread instead ----
@@ -582,6 +571,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         whead[w] = ih;
       }
       lds_barrier();
+      if (more) load_chunk(c0 + kMCh);
       PComp pre = pc_identity();  // exclusive prefix of this thread (within its run)
       for (uint32_t q = 0; q < w; ++q) {
         if (whead[q]) pre = wcomp[q];
@@ -679,13 +669,6 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       if (any_c) tir[e] = ins;
     }
     lds_barrier();
-    uint32_t gs[kMPer], rs[kMPer];
-#pragma unroll
-    for (int j = 0; j < kMPer; ++j) {
-      gs[j] = g[j];
-      rs[j] = res[j];
-    }
-    if (more) take();
 #pragma unroll
     for (int j = 0; j < kMPer; ++j)  // this thread's own commits: consecutive lanes -> consecutive staging rows
       if (gs[j] != 0xFFFFFFFFu) {
