@@ -115,10 +115,9 @@ constexpr uint32_t kECache = 4;  // (4, not 8: k_apply_coord fits three workgrou
 // global_load), so an LDS hit does not wait behind the walk's outstanding global stores as a flat access would.
 typedef __attribute__((address_space(1))) CoordEnt GlbEnt;
 struct Ents {
-  LdsU64* lx;    // this lane's column of the entry planes: entry p at [p * kLanes]
-  LdsU64* lidx;
-  LdsU32* linst;
-  LdsU32* lpad;
+  // this lane's column of the entry planes (one pointer: three planes per entry, lane-minor): entry p's x at
+  // [(3p) * kLanes], idx at [(3p + 1) * kLanes], inst | pad << 32 at [(3p + 2) * kLanes]
+  LdsU64* lc;
   GlbEnt* glb;
   uint32_t cap;  // entries of the block (cc_config.coord_cap, a power of two)
   mutable CoordEnt r0;  // entry 0 (registers)
@@ -128,10 +127,11 @@ struct Ents {
     if (p == 0) return r0;
     CoordEnt e;
     if (p < kECache) {
-      e.x = lx[p * kLanes];
-      e.idx = lidx[p * kLanes];
-      e.inst = linst[p * kLanes];
-      e.pad = lpad[p * kLanes];
+      e.x = lc[(3 * p) * kLanes];
+      e.idx = lc[(3 * p + 1) * kLanes];
+      const uint64_t ip = lc[(3 * p + 2) * kLanes];
+      e.inst = (uint32_t)ip;
+      e.pad = (uint32_t)(ip >> 32);
       return e;
     }
     e.x = __builtin_nontemporal_load(&glb[p].x);
@@ -160,10 +160,9 @@ struct Ents {
       return;
     }
     if (p < kECache) {
-      lx[p * kLanes] = v.x;
-      lidx[p * kLanes] = v.idx;
-      linst[p * kLanes] = v.inst;
-      lpad[p * kLanes] = v.pad;
+      lc[(3 * p) * kLanes] = v.x;
+      lc[(3 * p + 1) * kLanes] = v.idx;
+      lc[(3 * p + 2) * kLanes] = (uint64_t)v.inst | ((uint64_t)v.pad << 32);
       return;
     }
     __builtin_nontemporal_store(v.x, &glb[p].x);
@@ -666,8 +665,7 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   __shared__ uint32_t wsum[kCW2];
   __shared__ uint64_t evp[kEvLane * 3 * kQ];    // the walkers' event buffers (lane-minor planes, see kLanes)
   __shared__ uint32_t evoff[kQ + 1];
-  __shared__ uint64_t ecx[kECache * kQ], eci[kECache * kQ];  // the walkers' first entries (Ents), lane-minor
-  __shared__ uint32_t ecn[kECache * kQ], ecp[kECache * kQ];
+  __shared__ uint64_t ecache[3 * kECache * kQ];  // the walkers' first entries (Ents), lane-minor
   __shared__ unsigned long long evbase;
 
   const uint32_t s = blockIdx.x / kQPerSb, q0 = (blockIdx.x % kQPerSb) * kQ;
@@ -721,10 +719,17 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   uint32_t type = 0, vm = 0;
   uint64_t vv = 0;
   CoordHdr h{};
-  const Ents E{(LdsU64*)(ecx + l), (LdsU64*)(eci + l), (LdsU32*)(ecn + l), (LdsU32*)(ecp + l), (GlbEnt*)ents(blk), coord_cap, CoordEnt{0, 0, 0, 0}};
+  const Ents E{(LdsU64*)(ecache + l), (GlbEnt*)ents(blk), coord_cap, CoordEnt{0, 0, 0, 0}};
   if (w == 0) {
     type = res_type[res];
-    h = *reinterpret_cast<const CoordHdr*>(blk);
+    {  // (CoordHdr.pad is neither read nor written: two registers less across the walk)
+      const CoordHdr* hp = reinterpret_cast<const CoordHdr*>(blk);
+      h.who = hp->who;
+      h.flags = hp->flags;
+      h.idx = hp->idx;
+      h.head = hp->head;
+      h.n = hp->n;
+    }
     if (type == CC_RES_VALUE) {
       vm = val_meta[res];
       vv = val_v[res];
@@ -743,7 +748,7 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   // the next chunk's records (whole XRec: position, meta, operands, key, index, instance) stream into registers
   // during the walk; the instance-id gather is issued at the top of the chunk, ahead of the rank and scan
   uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu, m0 = 0, m1 = 0, n0 = 0, n1 = 0;
-  u64x2 a0{0, 0}, a1{0, 0};
+  uint64_t a0x = 0, a0y = 0, a1x = 0, a1y = 0;  // the operand pairs as four words (a u64x2 pair lived in scratch)
   uint64_t k0 = 0, k1 = 0, x0 = 0, x1 = 0, i0 = 0, i1 = 0;
   // Staging positions of the wave's two rows: one 64-ary search for the run of the wave's first record, then a
   // 64-run window in the lanes (run start wS, first record wP, next run's first record wB): a row's records find
@@ -786,12 +791,14 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   auto load_meta = [&](uint32_t c0) {
     rows_pos(c0 + w * (kWave * kCPer2), g0, g1);
     const XRec* r0 = xr + (g0 != 0xFFFFFFFFu ? g0 : 0), *r1 = xr + (g1 != 0xFFFFFFFFu ? g1 : 0);
-    a0 = r0->ab;
+    a0x = r0->ab.x;
+    a0y = r0->ab.y;
     k0 = r0->key;
     x0 = r0->idx;
     m0 = r0->meta;
     n0 = r0->res;
-    a1 = r1->ab;
+    a1x = r1->ab.x;
+    a1y = r1->ab.y;
     k1 = r1->key;
     x1 = r1->idx;
     m1 = r1->meta;
@@ -807,10 +814,9 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   PH(0);
   for (uint32_t c0 = 0; c0 < cnt; c0 += kCCh2) {
     // rank this workgroup's commits per slot inside each wave (log order = (wave, j, lane))
+    // (the two rows stay in named registers: an array of the 16-byte operand pairs, indexed in the gather, was
+    // promoted to scratch, and each prefetched pair was stored there right after its load, i.e. waited for)
     const uint32_t gg[kCPer2] = {g0, g1}, mm[kCPer2] = {m0, m1};
-    const uint32_t in[kCPer2] = {n0, n1};
-    const u64x2 ab[kCPer2] = {a0, a1};
-    const uint64_t ky[kCPer2] = {k0, k1}, ix[kCPer2] = {x0, x1}, id[kCPer2] = {i0, i1};
     uint32_t sl[kCPer2], rk[kCPer2];
     bool own[kCPer2];
 #pragma unroll
@@ -846,17 +852,18 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
       uint32_t p[kCPer2];
 #pragma unroll
       for (int j = 0; j < kCPer2; ++j) p[j] = own[j] ? sstart[sl[j]] + wc[w][sl[j]] + rk[j] : 0u;
-#pragma unroll
-      for (int j = 0; j < kCPer2; ++j) {
-        if (!own[j]) continue;
-        rab[p[j]] = ab[j];
-        rkey[p[j]] = ky[j];
-        ridx[p[j]] = ix[j];
-        riid[p[j]] = id[j];
-        rmeta[p[j]] = mm[j];
-        rins[p[j]] = in[j];
-        rpos[p[j]] = gg[j];
-      }
+      auto put = [&](uint32_t pj, const u64x2& abj, uint64_t kyj, uint64_t ixj, uint64_t idj, uint32_t mmj, uint32_t inj,
+                     uint32_t ggj) {
+        rab[pj] = abj;
+        rkey[pj] = kyj;
+        ridx[pj] = ixj;
+        riid[pj] = idj;
+        rmeta[pj] = mmj;
+        rins[pj] = inj;
+        rpos[pj] = ggj;
+      };
+      if (own[0]) put(p[0], u64x2{a0x, a0y}, k0, x0, i0, m0, n0, g0);
+      if (own[1]) put(p[1], u64x2{a1x, a1y}, k1, x1, i1, m1, n1, g1);
     }
     load_meta(c0 + kCCh2);  // the next chunk's records stream in during the walk
     for (uint32_t k = t; k < (uint32_t)(kCW2 * kQ); k += kCT2) (&wc[0][0])[k] = 0;  // (read above, before the barrier)
@@ -958,7 +965,12 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
 #endif
   if (w == 0) {
     E.store();
-    *reinterpret_cast<CoordHdr*>(blk) = h;
+    CoordHdr* hp = reinterpret_cast<CoordHdr*>((uintptr_t)E.glb - sizeof(CoordHdr));  // (= blk)
+    hp->who = h.who;
+    hp->flags = h.flags;
+    hp->idx = h.idx;
+    hp->head = h.head;
+    hp->n = h.n;
     if (type == CC_RES_VALUE) {
       val_meta[res] = vm;
       val_v[res] = vv;

@@ -424,10 +424,15 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ ho
 }
 
 // materialize a branch outcome applied to the snapshot: map_apply state (word, value) + commit/insert index
-__device__ inline void materialize(const Comp& c, const HotS0& s0, const MRec* __restrict__ xr, uint32_t& w,
+// (the snapshot as four words, not a HotS0 reference: the struct was kept in scratch, and its store there waited
+// for its load at the top of every item)
+__device__ inline void materialize(const Comp& c, const HotS0 s0, const MRec* __restrict__ xr, uint32_t& w,
                                    uint64_t& v, uint64_t& ci, uint64_t& ins) {
   const bool present0 = (s0.w & kMwPresent) != 0;
-  const Br b = present0 ? c.P : c.A;
+  Br b;
+  b.kind = present0 ? c.P.kind : c.A.kind;
+  b.v = present0 ? c.P.v : c.A.v;
+  b.n = present0 ? c.P.n : c.A.n;
   const uint32_t base = s0.w & ~(kMwPresent | kMwVtagMask);
   if (b.kind == kBrKeep) {
     w = s0.w;
