@@ -312,7 +312,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     }
   };
   // instance ids of the working chunk's records: requested when its instance slots are taken into the working
-  // registers (here for chunk 0, at the take for the others; CC_PART_EXT_LATE: at the top of the chunk), used at
+  // registers (here for chunk 0, at the take for the others; CC_PART_EXT_LATE: after the previous chunk's write-out,
+  // whose stores were issued after the loads they wait for, so that wait never covers them), used at
   // the placement
   uint64_t idv[J];
   auto issue_ids = [&]() {
@@ -323,8 +324,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 #pragma unroll
   for (int j = 0; j < J; ++j) mt[j] |= fl[j] << 8;
   if (TCK) tcheck_rows(0, t0v, t1v);
-  issue_ids();
 #endif
+  issue_ids();
 #if CC_PART_EXT_UNROLL
 #pragma unroll
 #else
@@ -345,7 +346,6 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 #pragma unroll
     for (int j = 0; j < J; ++j) mt[j] |= fl[j] << 8;
     if (TCK) tcheck_rows(ch, t0v, t1v);
-    issue_ids();
 #endif
     // the records of this chunk (compute only: every column arrived with the chunk's loads)
     uint32_t sk[J], loc[J], res[J], meta[J], xs[J];
@@ -501,6 +501,9 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
         reinterpret_cast<u64x2*>(xrec + g)[part] = v;
       }
     }
+#if CC_PART_EXT_LATE
+    if (more) issue_ids();  // the next chunk's instance ids (its instance column arrived during the write-out)
+#endif
     lds_barrier();
     PH(5);
     for (uint32_t k = t; k < sb; k += kPT) trun[k] += ctot[k];
