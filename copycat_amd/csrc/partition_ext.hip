@@ -256,7 +256,8 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       mt_[j] = op[i];
       fl_[j] = flags[i];
       const uint64_t* pa = lock ? (ctime ? ctime + i : nullptr) : (ca ? ca + i : nullptr);
-      const uint64_t* pb = lock ? (ctime && i > 0 ? ctime + (i - 1) : nullptr) : (cb ? cb + i : nullptr);
+      // (a keyed record's b is not staged: MRec drops it, and replaceIfPresent reads it from the batch by row)
+      const uint64_t* pb = lock ? (ctime && i > 0 ? ctime + (i - 1) : nullptr) : (cb && !is_keyed(ty) ? cb + i : nullptr);
       uint64_t av = 0, bv = 0;
       if (pa) av = *pa;
       if (pb) bv = *pb;
