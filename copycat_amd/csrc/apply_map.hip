@@ -342,6 +342,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     uint32_t ent[kMPer], rk[kMPer], ident[kMPer], p[kMPer];
     bool keyop[kMPer];
     const bool more = c0 + kMCh < cnt;  // block-uniform
+    // the sort's per-wave counters (wtab aliases the chunk records of rbuf, free since the previous chunk's final
+    // barrier); the binding rounds below always pass at least one barrier before the sort's atomics
+    for (uint32_t q = t; q < (uint32_t)(NW * kMapRegion / 2); q += MT) wtab[q] = 0;
 #pragma unroll
     for (int j = 0; j < kMPer; ++j) {
       ent[j] = kNoEnt;
@@ -444,8 +447,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     // ---- 3. stable counting sort by entry: per-wave counts (in-wave rank from LDS atomics with return: same-
     //         address lanes of one instruction resolve in lane order, checked at engine start), totals per entry,
     //         then a commit's run position = run start + its entry's count in earlier waves + its in-wave rank ----
-    for (uint32_t q = t; q < (uint32_t)(NW * kMapRegion / 2); q += MT) wtab[q] = 0;
-    lds_barrier();
+    // (wtab was zeroed at the top of the chunk: the binding rounds' barrier orders that before these atomics)
 #pragma unroll
     for (int j = 0; j < kMPer; ++j)  // program order over j, lane order inside one instruction = log order
       if (ent[j] != kNoEnt) {
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         const uint32_t y = __shfl_up(inc, d, 64);
         if (l >= (uint32_t)d) inc += y;
       }
-      lds_barrier();
+      // (no barrier before this write: wsum's last readers are the previous chunk's, many barriers ago)
       if (l == 63) wsum[w] = inc;
       lds_barrier();
       uint32_t run = inc - sum;
