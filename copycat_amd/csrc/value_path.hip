@@ -147,22 +147,58 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
   uint32_t T = blockIdx.x;
   if (T >= tiles) return;
   PH_DECL
-  uint32_t ri[kP4J], ob[kP4J], fb[kP4J];
+  // of2[j / 2] >> 16 * (j % 2) = op | flags << 8 of row j (two rows per register).  A full tile's op and flags columns arrive as 4-row words (opw / flw: lane l of
+  // wave w holds rows w*512 + i*256 + 4l .. +3), one load instruction per 256 rows instead of one per 64 (the 16
+  // byte loads per thread were issue-bound in the address unit: 19.4 -> 15.1 us per tile without them), and are
+  // spread to the rank layout (row w*512 + j*64 + l) by lane shuffles at the top of the tile; a partial tile or an
+  // unaligned column loads bytes.
+  uint32_t ri[kP4J], of2[kP4J / 2], opw[2], flw[2];
   uint64_t av[kP4J], bv[kP4J];
+  bool wide = false;
+  const bool opfl_al = ((((uintptr_t)op) | ((uintptr_t)flags) | (uintptr_t)lo) & 3u) == 0;
   auto rowq = [&](int j) -> uint32_t { return w * (kWave * kP4J) + (uint32_t)j * kWave + l; };
   auto load = [&](uint32_t TT) {
     const uint64_t t0 = lo + (uint64_t)TT * kV3Tile;
     const uint32_t nr = (uint32_t)(hi - t0 < (uint64_t)kV3Tile ? hi - t0 : (uint64_t)kV3Tile);
+    wide = opfl_al && nr == (uint32_t)kV3Tile;  // block-uniform
+    if (wide) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint64_t ic = t0 + w * (kWave * kP4J) + (uint32_t)i * (4 * kWave) + 4u * l;
+        opw[i] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(op + ic));
+        flw[i] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(flags + ic));
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kP4J; ++j) {
       const uint32_t q = rowq(j);
       const uint64_t ic = t0 + (q < nr ? q : 0u);  // rows past the batch end re-read row 0 (ignored)
       ri[j] = __builtin_nontemporal_load(inst + ic);
-      ob[j] = __builtin_nontemporal_load(op + ic);
-      fb[j] = __builtin_nontemporal_load(flags + ic);
+#ifdef CC_DIAG_NO_OPFL  // diagnostics build only: op / flags not loaded (wrong results; the byte loads' issue cost)
+      if (j % 2 == 0) of2[j / 2] = 0x11321132u;
+#else
+      if (!wide) {
+        const uint32_t v = (uint32_t)__builtin_nontemporal_load(op + ic) | ((uint32_t)__builtin_nontemporal_load(flags + ic) << 8);
+        of2[j / 2] = j % 2 ? (of2[j / 2] | (v << 16)) : v;
+      }
+#endif
       av[j] = __builtin_nontemporal_load(ca + ic);
       bv[j] = __builtin_nontemporal_load(cb + ic);
     }
+  };
+  // (at the top of a tile: the words landed with the instance column the gathers there wait for)
+  auto unpack = [&]() {
+#ifndef CC_DIAG_NO_OPFL
+    if (!wide) return;
+#pragma unroll
+    for (int j = 0; j < kP4J; ++j) {
+      const int src = (j % 4) * 16 + (int)(l >> 2);
+      const uint32_t sh = 8u * (l & 3u);
+      const uint32_t o = ((uint32_t)__shfl((int)opw[j / 4], src, kWave) >> sh) & 0xFFu;
+      const uint32_t f = ((uint32_t)__shfl((int)flw[j / 4], src, kWave) >> sh) & 0xFFu;
+      of2[j / 2] = j % 2 ? (of2[j / 2] | ((o | (f << 8)) << 16)) : (o | (f << 8));
+    }
+#endif
   };
   load(T);
   for (;;) {
@@ -177,6 +213,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
       const uint32_t g = inst_res[ok ? ri[j] : 0u];
       r[j] = ok ? g : kNoRes;
     }
+    unpack();  // (while the gathers fly)
 #pragma unroll
     for (int j = 0; j < kP4J; ++j) {
       const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
@@ -237,7 +274,8 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
       if (loc[j] != 0xFFFFu) {
         const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
         const uint32_t sp = kst[k] + ((wc[w][k >> 1] >> sh) & 0xFFFFu) + loc[j];
-        img[sp] = v3_set_rows(v3_encode(ob[j], fb[j], av[j], bv[j], r[j] & ((1u << KSB) - 1)), q, tbase + q);
+        const uint32_t ofj = of2[j / 2] >> (16 * (j % 2));
+        img[sp] = v3_set_rows(v3_encode(ofj & 0xFFu, (ofj >> 8) & 0xFFu, av[j], bv[j], r[j] & ((1u << KSB) - 1)), q, tbase + q);
         cp = sp;
       }
       if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
