@@ -270,8 +270,9 @@ __global__ __launch_bounds__(kEC) void k_ev_place(const EvRec* __restrict__ aren
   }
 }
 
-constexpr int kEvWin = 2048;  // output events assembled per window in k_ev_tile_out
-constexpr int kEvMaxWin = 16;  // more windows than this in one tile: events stored straight to their rows
+constexpr int kEvWin = 4096;   // output events assembled per window in k_ev_tile_out
+constexpr int kEvMaxWin = 15;  // more windows than this in one tile: events stored straight to their rows (and the
+                               // windowed path's row offsets stay below 65,536: u16)
 // per tile: the rows' event offsets in LDS, then the tile's events to their output rows, one window at a time
 __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict__ cpos, uint64_t n, const uint16_t* __restrict__ ev_cnt,
                                                     const uint32_t* __restrict__ tile_sum, const uint64_t* __restrict__ tile_off,
@@ -281,13 +282,23 @@ __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict_
                                                     uint8_t* __restrict__ code, uint8_t* __restrict__ src,
                                                     uint8_t* __restrict__ tag, uint64_t* __restrict__ payload) {
   __shared__ uint32_t wsum[kER / kWave];
-  __shared__ uint16_t srow[kTile];  // staging position -> row in the tile
-  __shared__ uint32_t soff[kTile];  // staging position -> offset of its commit's first event in the tile's output
-  // one output window of kEvWin events, assembled in LDS so the six columns are written contiguously
-  __shared__ uint32_t wpos[kEvWin], wtgt[kEvWin], wcts[kEvWin];
-  __shared__ uint64_t wpay[kEvWin];
+  __shared__ uint16_t srow[kTile];    // staging position -> row in the tile
+  __shared__ uint16_t soff16[kTile];  // staging position -> offset of its commit's first event in the tile's output
+  // one output window of kEvWin events, assembled in LDS so the six columns are written contiguously; a tile past
+  // kEvMaxWin windows keeps its (u32) row offsets in the same bytes instead (16-bit offsets and 4,096-event windows:
+  // c5's ~6K events per tile take two windows, each re-reading the tile's list, where 2,048-event windows took three)
+  __shared__ __align__(16) uint8_t wbuf[kEvWin * 20];
+  static_assert(kEvWin * 20 >= kTile * 4, "the direct path's u32 offsets fit the window bytes");
+  static_assert(kEvWin * kEvMaxWin < 65536, "windowed offsets are u16");
+  uint32_t* const wpos = reinterpret_cast<uint32_t*>(wbuf);
+  uint32_t* const wtgt = wpos + kEvWin;
+  uint32_t* const wcts = wtgt + kEvWin;
+  uint64_t* const wpay = reinterpret_cast<uint64_t*>(wcts + kEvWin);
+  uint32_t* const soff32 = reinterpret_cast<uint32_t*>(wbuf);
   if (*arena_n > arena_cap) return;  // the arena overflowed: the call fails (kErrEvents)
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, T = blockIdx.x;
+  const uint32_t nev = tile_sum[T];
+  const bool direct = nev > (uint32_t)(kEvWin * kEvMaxWin);  // block-uniform
   const uint64_t r0 = (uint64_t)T * kTile + (uint64_t)t * kERPer;
   const uint32_t tbase = T * kTile;
   uint32_t pp[kERPer];
@@ -320,22 +331,22 @@ __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict_
   for (int q = 0; q < kERPer; ++q) {
     if (c[q]) {
       srow[pp[q]] = (uint16_t)(t * kERPer + q);
-      soff[pp[q]] = run;
+      if (direct) soff32[pp[q]] = run;
+      else soff16[pp[q]] = (uint16_t)run;
     }
     run += c[q];
   }
   __syncthreads();
   const uint64_t toff = tile_off[T], b0 = toff - tile_off[0];
-  const uint32_t nev = tile_sum[T];
   if (b0 + nev > arena_cap || toff + nev > out_cap) return;  // (the call fails: kErrEvents from k_ev_tiles)
   // Each window re-reads the tile's event list (from L2): nev^2 / kEvWin record reads per tile.  A tile whose fan-out
   // makes that more than kEvMaxWin windows (group / election bursts) writes each event straight to its output row
   // instead: scattered stores, linear in nev.
-  if (nev > (uint32_t)(kEvWin * kEvMaxWin)) {
+  if (direct) {
     for (uint32_t i = t; i < nev; i += kER) {
       const EvRec r = bucket[b0 + i];
       const uint32_t sp = r.g - tbase;
-      const uint64_t d = toff + soff[sp] + r.k;
+      const uint64_t d = toff + soff32[sp] + r.k;
       pos[d] = (uint32_t)(lo + tbase + srow[sp]);
       target[d] = r.target;
       code[d] = (uint8_t)r.code;
@@ -350,7 +361,7 @@ __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict_
     for (uint32_t i = t; i < nev; i += kER) {  // the tile's events (re-read per window from L2)
       const EvRec r = bucket[b0 + i];
       const uint32_t sp = r.g - tbase;
-      const uint32_t d = soff[sp] + r.k - w0;
+      const uint32_t d = soff16[sp] + r.k - w0;
       if (d < wn) {
         wpos[d] = (uint32_t)(lo + tbase + srow[sp]);
         wtgt[d] = r.target;
