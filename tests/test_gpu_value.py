@@ -164,3 +164,38 @@ def test_value_ragged_tiles_and_sub_batches(n, sub):
     R = 4096
     b = atomic_long_stream(n, resources=R)
     _assert_same(*_run_both(b, R, R + 8, sub_batch=sub), R)
+
+
+@pytest.mark.parametrize("offset", [1, 2, 4])
+def test_value_partition_byte_columns_at_any_alignment(offset):
+    """k_part_v4 loads a full tile's op / flags columns as 4-row words when both column pointers are 4-byte aligned,
+    and byte by byte otherwise (and for a partial tile): the same results from op / flags columns that start 1, 2
+    or 4 bytes into their buffers, against the host path on aligned columns (itself checked against the oracle)."""
+    import torch
+
+    from copycat_amd.engine import DeviceBatch, Engine
+    from copycat_amd.workload import atomic_long_stream
+
+    R = 65536
+    b = atomic_long_stream(100_003, resources=R, seed=17)  # 12 full 8192-row tiles and a partial one
+    E1 = Engine(R, R, len(b))
+    E1.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E1.instance_open_range(0, R, 0, 1000, 7)
+    s1, v1 = E1.apply_host(b)
+    E2 = Engine(R, R, len(b))
+    E2.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E2.instance_open_range(0, R, 0, 1000, 7)
+    db = DeviceBatch.upload(b)
+    for name in ("op", "flags"):
+        buf = torch.zeros(len(b) + offset, dtype=torch.uint8, device="cuda")
+        buf[offset:] = db.cols[name]
+        db.cols[name] = buf[offset:]
+        assert db.cols[name].data_ptr() % 4 == offset % 4
+    st = torch.full((len(b),), 0xFF, dtype=torch.uint8, device="cuda")
+    va = torch.zeros(len(b), dtype=torch.int64, device="cuda")
+    E2.apply(db, st, va)
+    E2.sync()
+    assert np.array_equal(st.cpu().numpy(), s1)
+    assert np.array_equal(va.cpu().numpy().view(np.uint64), v1)
+    for x, y in zip(E1.value_state(), E2.value_state()):
+        assert np.array_equal(x, y)
