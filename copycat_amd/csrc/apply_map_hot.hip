@@ -9,7 +9,8 @@
 //                  key's own bucket (log order, like any super-bucket).  Hot-ness only steers work: a commit is
 //                  applied identically by either path.
 //   k_hot_lists  : per hot key: its run in every tile -> list offsets; snapshot of the entry's state.
-//   k_hot_agg    : per piece of 4096 commits of a key's list: the piece's composite transformer (below).
+//   k_hot_agg    : per piece of kHotPiece commits of a key's list: the piece's composite transformer (below).
+//   k_hot_carry  : per hot key: the pieces' composites -> their exclusive prefixes (in place).
 //   k_hot_apply  : per piece: carry = composite of all earlier pieces applied to the snapshot; the piece's
 //                  commits are then applied in log order from that state (results written to staging); the
 //                  last piece writes the entry back.
@@ -423,6 +424,38 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ ho
   }
 }
 
+// Each hot key's piece composites -> their exclusive prefixes, in place (one workgroup per key): k_hot_apply then
+// reads the composite of pieces [0, p) with one load.  (It folded them itself, wave 0 walking up to p / 64 dependent
+// loads per lane for every piece: O(P^2) over a key of P pieces, ~18 loads per lane for the hottest key's last ones.)
+__global__ __launch_bounds__(kHT) void k_hot_carry(const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len,
+                                                  Comp* __restrict__ agg) {
+  __shared__ uint32_t pfx[kHotMax + 1];
+  __shared__ Comp wtot[kHT / kWave];
+  uint32_t nh;
+  hot_items(hot_n, hot_len, pfx, nh);
+  const uint32_t h = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63;
+  if (h >= nh) return;  // block-uniform
+  const uint32_t P = pfx[h + 1] - pfx[h];
+  Comp* const a = agg + (uint64_t)h * kHotMaxPieces;
+  const uint32_t per = (P + kHT - 1) / kHT, q0 = min(t * per, P), q1 = min(q0 + per, P);
+  Comp c = comp_identity();
+  for (uint32_t q = q0; q < q1; ++q) c = compose(c, a[q]);
+  const Comp inc = wave_scan(c, l);
+  if (l == 63) wtot[w] = inc;
+  __syncthreads();
+  Comp run = comp_identity();  // pieces before this thread's: waves before, then lanes before
+  for (uint32_t q = 0; q < w; ++q) run = compose(run, wtot[q]);
+  {
+    const Comp o = comp_shfl_up(inc, 1);
+    if (l > 0) run = compose(run, o);
+  }
+  for (uint32_t q = q0; q < q1; ++q) {
+    const Comp x = a[q];
+    a[q] = run;
+    run = compose(run, x);
+  }
+}
+
 // materialize a branch outcome applied to the snapshot: map_apply state (word, value) + commit/insert index
 // (the snapshot as four words, not a HotS0 reference: the struct was kept in scratch, and its store there waited
 // for its load at the top of every item)
@@ -525,14 +558,8 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
       }
       continue;
     }
-    // carry: the composite of pieces [0, p), folded in order by wave 0
-    if (w == 0) {
-      const uint32_t per = (p + 63) / 64;
-      Comp c = comp_identity();
-      for (uint32_t q = l * per; q < (l + 1) * per && q < p; ++q) c = compose(c, agg[(uint64_t)h * kHotMaxPieces + q]);
-      c = wave_scan(c, l);
-      if (l == 63) carry = c;
-    }
+    // carry: the composite of pieces [0, p) (k_hot_carry's exclusive prefix)
+    if (t == 0) carry = agg[(uint64_t)h * kHotMaxPieces + p];
     // this thread's commits and their composite
     const uint32_t p0 = p * kHotPiece + t * kHPer;
     const uint32_t e = p0 < L ? (p0 + kHPer < L ? p0 + kHPer : L) : p0;
@@ -620,6 +647,7 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
                      reinterpret_cast<HotS0*>(a.hot_s0));
   hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.hot_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
                      a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond);
+  hipLaunchKernelGGL(k_hot_carry, dim3(kHotMax), dim3(kHT), 0, st, a.hot_n, a.hot_len, reinterpret_cast<Comp*>(a.hot_agg));
   hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.mrec, a.cb, a.lo, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
