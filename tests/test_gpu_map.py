@@ -94,6 +94,7 @@ def test_map_table_bulk_readback():
 @pytest.mark.parametrize("n,sub_batch,hot,p_hot,seed", [
     (400_000, 65536, 8, 0.6, 41),    # 7 sub-batches; each hot key ~5K commits per sub-batch: 2 scan pieces
     (2_000_000, 0, 8, 0.6, 42),      # one sub-batch: ~37 pieces per hot key (carry across many pieces)
+    (6_000_000, 0, 1, 0.9, 43),      # one key takes 90%: ~5,300 pieces in one sub-batch (k_hot_carry's long scan)
     (300_000, 0, 1, 0.97, 43),       # one key takes 97%: ~71 pieces
 ])
 def test_map_hot_key_scan_parity(n, sub_batch, hot, p_hot, seed):
