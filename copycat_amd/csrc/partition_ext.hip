@@ -529,12 +529,14 @@ size_t part_ext_chunk(uint32_t sb, bool maps, bool ids) {
 }
 
 int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
-  const size_t c = part_ext_chunk(a.sb, a.map_bits != 0, a.inst_id != nullptr);
-  if (c == 0) return -1;
   const bool ids = a.inst_id != nullptr, tck = a.time && (a.ext_flags & kExtTimeCheck);
+  // (with the clock check, 2048-commit chunks spill at the 128-VGPR cap -- 52-64 B per lane -- and a spill reload waits
+  // behind the next chunk's loads: such engines stage 1,024-commit chunks, which need no scratch)
+  size_t c = part_ext_chunk(a.sb, a.map_bits != 0, ids);
+  if (c == (size_t)kChunkMaps && tck) c = kPT;
+  if (c == 0) return -1;
   auto kern = c == (size_t)kChunkMaps
-                  ? (ids ? (tck ? k_part_ext<kChunkMaps, true, true> : k_part_ext<kChunkMaps, true, false>)
-                         : (tck ? k_part_ext<kChunkMaps, false, true> : k_part_ext<kChunkMaps, false, false>))
+                  ? (ids ? k_part_ext<kChunkMaps, true, false> : k_part_ext<kChunkMaps, false, false>)
                   : (ids ? (tck ? k_part_ext<kPT, true, true> : k_part_ext<kPT, true, false>)
                          : (tck ? k_part_ext<kPT, false, true> : k_part_ext<kPT, false, false>));
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c, a.inst_id != nullptr), st, a.inst, a.op,
