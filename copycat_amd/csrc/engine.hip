@@ -628,14 +628,22 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
   dev_fill(e, e->d_val_meta, sizeof(uint32_t) * slot, 0, sizeof(uint32_t));
   dev_fill(e, e->d_val_v, sizeof(uint64_t) * slot, 0, sizeof(uint64_t));
   if (e->d_val_live) dev_fill(e, e->d_val_live, sizeof(uint64_t) * slot, 0, sizeof(uint64_t));
-  for (uint32_t i = 0; i < e->cfg.max_instances; ++i)
-    if (e->inst_res[i] == slot) {
-      e->inst_res[i] = kNoRes;
-      e->sessions.remove((int64_t)e->inst_id[i]);
-      e->inst_by_id.erase(e->inst_id[i]);
-      e->used_inst.clear(i);
-      mark_dirty(e->inst_dirty_lo, e->inst_dirty_hi, i, i + 1);
-    }
+  // :223-229 walks sessions.entrySet() and iterator.remove()s every holder of the resource: removed in that
+  // iteration order (the red-black deletes of a tree bin depend on it)
+  std::vector<uint32_t> gone;
+  e->sessions.for_each([&](int64_t id) {
+    auto it = e->inst_by_id.find((uint64_t)id);
+    if (it != e->inst_by_id.end() && e->inst_res[it->second] == slot) gone.push_back(it->second);
+  });
+  for (uint32_t i = 0; i < e->cfg.max_instances; ++i)  // (every holder is registered in sessions; kept as a guard)
+    if (e->inst_res[i] == slot && std::find(gone.begin(), gone.end(), i) == gone.end()) gone.push_back(i);
+  for (uint32_t i : gone) {
+    e->inst_res[i] = kNoRes;
+    e->sessions.remove((int64_t)e->inst_id[i], /*movable=*/false);  // iterator.remove()
+    e->inst_by_id.erase(e->inst_id[i]);
+    e->used_inst.clear(i);
+    mark_dirty(e->inst_dirty_lo, e->inst_dirty_hi, i, i + 1);
+  }
   // ResourceManager.resources / keys / ResourceHolder.sessions
   auto rit = e->res_by_id.find(e->res_id[slot]);
   if (rit != e->res_by_id.end() && rit->second == slot) e->res_by_id.erase(rit);
@@ -1007,7 +1015,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.msmall = (e->small_live || e->szq_n) ? e->d_msmall : nullptr;  // small / size-queried maps: not hot-routed
       ha.err = e->d_err;
       ha.mark = marker_of(e);
-      static const bool no_hot = getenv("CC_NO_HOT") != nullptr;  // diagnostics: every key through its region
+      static const bool no_hot = diag_env("CC_NO_HOT");  // diagnostics: every key through its region
       if (no_hot) HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
       else if (launch_map_hot_bind(ha, st)) return set_err(CC_ERR_HIP, "hot-key bind launch", hipGetLastError()); DBG_SYNC("hot-key bind launch");
     }
@@ -1690,7 +1698,7 @@ extern "C" int cc_sessions_close(cc_engine* e, const uint64_t* h_clients, uint64
     if (!e->res_zombie[r]) e->res_sessions.erase({r, e->inst_client[i]});
     if (p == stop) continue;
     e->inst_res[i] = kNoRes;
-    e->sessions.remove((int64_t)e->inst_id[i]);
+    e->sessions.remove((int64_t)e->inst_id[i], /*movable=*/false);  // iterator.remove()
     e->inst_by_id.erase(e->inst_id[i]);
     e->used_inst.clear(i);
     ++closed;

@@ -1,6 +1,19 @@
 // engine_internal.h — launch-parameter structs shared by the engine's translation units.
 #pragma once
+#include <cstdlib>
+
 #include "common.h"
+
+// A/B and diagnostics switches read from the environment (CC_NO_HOT, CC_EV_V1, CC_EV_SCATTER, CC_PART_EXT_1024) exist
+// only in -DCC_DIAG builds (copycat_amd/build.py build_variant); the product library never takes an untested path.
+inline bool diag_env(const char* name) {
+#ifdef CC_DIAG
+  return getenv(name) != nullptr;
+#else
+  (void)name;
+  return false;
+#endif
+}
 
 namespace cc {
 

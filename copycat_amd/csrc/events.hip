@@ -387,7 +387,7 @@ __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict_
 int launch_events(const EventArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_EVENTS, 1, st);
-  static const bool v1 = getenv("CC_EV_V1") != nullptr || getenv("CC_EV_SCATTER") != nullptr;
+  static const bool v1 = diag_env("CC_EV_V1") || diag_env("CC_EV_SCATTER");
   if (!v1 && a.bucket && a.ccnt) {
     const uint32_t chunks = (uint32_t)ev_chunk_cap(a.arena_cap);
     hipLaunchKernelGGL(k_ev_count, dim3(a.tiles), dim3(kEC), 0, st, a.ev_cnt, a.hi - a.lo, a.tile_sum);
@@ -409,7 +409,7 @@ int launch_events(const EventArgs& a, hipStream_t st) {
                      a.tile_sum);
   hipLaunchKernelGGL(k_ev_tiles, dim3(1), dim3(kER), 0, st, a.tile_sum, a.tiles, a.ev_total, a.tile_off, a.arena_n,
                      a.arena_cap, a.out_cap, a.out_pos ? 1 : 0, a.err);
-  static const bool one_pass = getenv("CC_EV_SCATTER") != nullptr;
+  static const bool one_pass = diag_env("CC_EV_SCATTER");
   if (a.out_pos && (one_pass || !a.perm)) {
     hipLaunchKernelGGL(k_ev_scatter, dim3(1024), dim3(256), 0, st, a.arena, a.arena_n, a.arena_cap, a.row_of, a.ev_loc,
                        a.tile_off, a.lo, a.out_cap, a.out_pos, a.out_target, a.out_code, a.out_src, a.out_tag,

@@ -40,10 +40,10 @@ static_assert(kHwNum <= 24, "cc_engine::hw_buf");
 int hw(cc_engine* e, int slot, size_t bytes, void** out) {
   bytes = std::max<size_t>(bytes, 256);
   if (e->hw_cap[slot] < bytes) {
+    const size_t cap = std::max(bytes, e->hw_cap[slot] * 3 / 2);  // grow by half: no free + malloc per call
     if (e->hw_buf[slot]) (void)hipFree(e->hw_buf[slot]);
     e->hw_buf[slot] = nullptr;
     e->hw_cap[slot] = 0;
-    const size_t cap = std::max(bytes, e->hw_cap[slot] * 3 / 2);
     hipError_t x = hipMalloc(&e->hw_buf[slot], cap);
     if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc (host-path staging)", x);
     e->hw_cap[slot] = cap;

@@ -22,12 +22,14 @@ namespace cc {
 class JavaLongHashMap {
  public:
   static constexpr int kNil = -1;
-  struct Node {
+  struct Node {  // no implicit padding: snapshots of equal states are equal byte for byte
     uint32_t hash;
+    uint32_t pad0;
     int64_t key;
     int32_t next, prev, parent, left, right;
     uint8_t tree, red, pad[2];
   };
+  static_assert(sizeof(Node) == 40, "Node must have no implicit padding");
 
   static uint32_t spread(int64_t v) {
     const uint32_t h = (uint32_t)((uint64_t)v ^ ((uint64_t)v >> 32));
@@ -74,14 +76,18 @@ class JavaLongHashMap {
     if (++size_ > threshold_) resize();
   }
 
-  void remove(int64_t k) {  // removeNode(hash, key, null, false, movable = true)
+  // removeNode(hash, key, null, false, movable).  ResourceManager only ever removes through its entry-set iterator
+  // (deleteResource :223-229, close :251-263), and HashIterator.remove calls removeNode(..., movable = false): a tree
+  // bin then loses the node from its chain and its red-black links, but is neither untreeified when small nor has its
+  // root moved to the front.
+  void remove(int64_t k, bool movable) {
     auto it = where_.find(k);
     if (it == where_.end()) return;
     const int node = it->second;
     where_.erase(it);
     const uint32_t index = (capacity() - 1) & nd_[node].hash;
     if (nd_[node].tree) {
-      remove_tree_node(node, index);
+      remove_tree_node(node, index, movable);
     } else {
       int p = tab_[index];
       if (p == node) tab_[index] = nd_[node].next;
@@ -130,10 +136,25 @@ class JavaLongHashMap {
     std::memcpy(tab_.data(), p + 20, 4ull * hd[2]);
     std::memcpy(nd_.data(), p + 20 + 4ull * hd[2], sizeof(Node) * (size_t)hd[3]);
     std::memcpy(free_.data(), p + 20 + 4ull * hd[2] + sizeof(Node) * hd[3], 4ull * hd[4]);
-    where_.clear();
+    // the blob is untrusted: every table slot and node link must name a node (or kNil), the table must be a power
+    // of two, and no chain may be longer than the pool (a cycle would loop the rebuild below forever)
+    const int64_t nn = (int64_t)nd_.size();
+    auto ok = [nn](int32_t x) { return x == kNil || (x >= 0 && x < nn); };
+    if (!tab_.empty() && (tab_.size() & (tab_.size() - 1))) return 0;
     for (int b : tab_)
-      for (int q = b; q != kNil; q = nd_[q].next) where_[nd_[q].key] = q;
-    return where_.size() == size_ ? need : 0;
+      if (!ok(b)) return 0;
+    for (const Node& q : nd_)
+      if (!ok(q.next) || !ok(q.prev) || !ok(q.parent) || !ok(q.left) || !ok(q.right)) return 0;
+    for (int f : free_)
+      if (f < 0 || f >= nn) return 0;
+    where_.clear();
+    size_t walked = 0;
+    for (int b : tab_)
+      for (int q = b; q != kNil; q = nd_[q].next) {
+        if (++walked > nd_.size()) return 0;
+        where_[nd_[q].key] = q;
+      }
+    return where_.size() == size_ && walked == size_ ? need : 0;
   }
 
  private:
@@ -147,7 +168,7 @@ class JavaLongHashMap {
     int x;
     if (!free_.empty()) x = free_.back(), free_.pop_back();
     else x = (int)nd_.size(), nd_.emplace_back();
-    nd_[x] = Node{h, k, kNil, kNil, kNil, kNil, kNil, 0, 0, {0, 0}};
+    nd_[x] = Node{h, 0, k, kNil, kNil, kNil, kNil, kNil, 0, 0, {0, 0}};
     return x;
   }
   static int dir_of(uint32_t h, int64_t k, const Node& p) {  // hash (signed), then Long.compareTo
@@ -396,7 +417,7 @@ class JavaLongHashMap {
     }
     tab_.swap(ntab);
   }
-  void remove_tree_node(int self, uint32_t index) {  // TreeNode.removeTreeNode(map, tab, movable = true)
+  void remove_tree_node(int self, uint32_t index, bool movable) {  // TreeNode.removeTreeNode(map, tab, movable)
     int first = tab_[index], root = first, rl;
     const int succ = nd_[self].next, pred = nd_[self].prev;
     if (pred == kNil) tab_[index] = first = succ;
@@ -404,7 +425,7 @@ class JavaLongHashMap {
     if (succ != kNil) nd_[succ].prev = pred;
     if (first == kNil) return;
     if (nd_[root].parent != kNil) root = root_of(root);
-    if (nd_[root].right == kNil || (rl = nd_[root].left) == kNil || nd_[rl].left == kNil) {
+    if (movable && (nd_[root].right == kNil || (rl = nd_[root].left) == kNil || nd_[rl].left == kNil)) {
       tab_[index] = untreeify(first);  // too small
       return;
     }
@@ -447,7 +468,7 @@ class JavaLongHashMap {
         else if (p == nd_[pp].right) nd_[pp].right = kNil;
       }
     }
-    to_front(r);
+    if (movable) to_front(r);
   }
 };
 

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 // at 1024, profiles/r03/ab_chunk); 0: none fits
 size_t part_ext_chunk(uint32_t sb, bool maps, bool ids) {
   constexpr size_t kLds = 160u * 1024u - kMaxSb;
-  static const bool small = getenv("CC_PART_EXT_1024") != nullptr;  // A/B: 1024-commit chunks whenever they fit
+  static const bool small = diag_env("CC_PART_EXT_1024");  // A/B: 1024-commit chunks whenever they fit
   if (maps && !small && tile_lds_bytes(sb, true, kChunkMaps, ids) <= kLds) return kChunkMaps;
   if (tile_lds_bytes(sb, true, kPT, ids) <= kLds) return kPT;
   return 0;

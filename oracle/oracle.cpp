@@ -436,8 +436,9 @@ struct JHM {
     }
     if (++size > threshold) resize(cx);
   }
-  // removeNode(hash, key, null, false, movable = true) for a key in the map
-  void remove(const JCtx& cx, const MapKey& k) {
+  // removeNode(hash, key, null, false, movable) for a key in the map: map.remove(key) passes movable = true,
+  // an iterator's remove() movable = false (no untreeify when small, no moveRootToFront)
+  void remove(const JCtx& cx, const MapKey& k, bool movable = true) {
     auto it = where.find(k);
     if (it == where.end()) return;
     const int node = it->second;
@@ -445,7 +446,7 @@ struct JHM {
     const uint32_t n = capacity();
     const uint32_t index = (n - 1) & nd[node].hash;
     if (nd[node].tree) {
-      remove_tree_node(node, index);
+      remove_tree_node(node, index, movable);
     } else {
       int p = tab[index];
       if (p == node) tab[index] = nd[node].next;
@@ -457,7 +458,7 @@ struct JHM {
     --size;
     free_.push_back(node);
   }
-  void remove_tree_node(int self, uint32_t index) {  // TreeNode.removeTreeNode(map, tab, movable = true)
+  void remove_tree_node(int self, uint32_t index, bool movable) {  // TreeNode.removeTreeNode(map, tab, movable)
     int first = tab[index], root = first, rl;
     const int succ = nd[self].next, pred = nd[self].prev;
     if (pred == kNil) tab[index] = first = succ;
@@ -465,7 +466,7 @@ struct JHM {
     if (succ != kNil) nd[succ].prev = pred;
     if (first == kNil) return;
     if (nd[root].parent != kNil) root = root_of(root);
-    if (root == kNil || nd[root].right == kNil || (rl = nd[root].left) == kNil || nd[rl].left == kNil) {
+    if (root == kNil || (movable && (nd[root].right == kNil || (rl = nd[root].left) == kNil || nd[rl].left == kNil))) {
       tab[index] = untreeify(first);  // too small
       return;
     }
@@ -515,7 +516,7 @@ struct JHM {
         else if (p == nd[pp].right) nd[pp].right = kNil;
       }
     }
-    move_root_to_front(r);
+    if (movable) move_root_to_front(r);
   }
   // MapState.delete (iterator.remove() on every entry): every bin empties, the table keeps its capacity
   void clear() {
@@ -721,7 +722,8 @@ struct orc {
     if (!in.open) return;
     in.open = false;
     inst_by_id.erase(in.id);
-    sessions_order.remove(cx, MapKey{CC_TAG_LONG, in.id});
+    // ResourceManager removes holders only through sessions.entrySet().iterator().remove() (:227, :261)
+    sessions_order.remove(cx, MapKey{CC_TAG_LONG, in.id}, /*movable=*/false);
   }
   int alloc_res_slot() {
     for (uint32_t s = 0; s < max_res; ++s) if (!res[s].exists && !res[s].zombie) return (int)s;
@@ -1443,8 +1445,13 @@ int orc_delete_resource(orc* o, uint64_t resource_id, uint8_t* status) {
   }
   o->cancel_resource_timers(slot);   // resource.executor.close()
   if (r.has_key) o->keys.erase(r.key);
-  for (uint32_t i = 0; i < o->max_inst; ++i)
-    if (o->inst[i].open && o->inst[i].res == slot) o->unregister_instance(i);
+  // :223-229: every holder of the resource, iterator.remove()d in sessions' HashMap iteration order
+  std::vector<uint32_t> gone;
+  o->sessions_order.for_each([&](const MapKey& id) {
+    const uint32_t i = o->inst_by_id.at(id.k);
+    if (o->inst[i].open && o->inst[i].res == slot) gone.push_back(i);
+  });
+  for (uint32_t i : gone) o->unregister_instance(i);
   r.exists = false;
   *status = CC_STATUS_CODE(st) == CC_ST_OK ? CC_STATUS(CC_ST_OK, CC_TAG_BOOL) : st;
   return CC_OK;

@@ -220,6 +220,31 @@ def kats():
                          (10, "ELECT", L(11))])
     out.append(kat)
 
+    # ResourceManager removes holders only through sessions.entrySet().iterator().remove() (deleteResource :223-229,
+    # close :251-263), and JDK 8's HashIterator.remove calls removeNode(..., movable = false): a tree bin loses the node
+    # but is neither untreeified when small nor has its root moved to the bin's front.  Instance ids 5 + 64 i
+    # (i = 0..10) share bin 5: the 9th and 10th puts resize 16 -> 32 -> 64 (treeifyBin below capacity 64), the 11th
+    # treeifies the bin.  Closing client 7 (8 of the 11) leaves a 3-node tree {261, 389, 517} whose chain order is
+    # 389, 261, 517 (movable = true would untreeify it, or move its root 261 to the front).  709 then joins the bin.
+    # Listens are commits 646..656 (ids in order) and 710 (709).  Close 7 walks 197 5 69 133 325 453 581 645: the lead
+    # goes 5 -> 69 (647) -> 133 (648) -> 261 (650).  Close 8 walks 389 then 261: 389 leaves the listeners, 261 hands
+    # the lead to 517 (654) (261 first would elect 389 (652) and then 517).  Close 9 walks 517 709: 709 (710) leads.
+    kat = K("A12_close_after_tree_bin_removal", "quirk",
+            "manager/src/main/java/io/atomix/manager/ResourceManager.java:37,223-229,250-264")
+    tree_el = S("tree-bin-election")
+    ph1 = [(5, 7), (69, 7), (133, 7), (197, 7), (261, 8), (325, 7), (389, 8), (453, 7), (517, 9), (581, 7), (645, 7)]
+    for iid, client in ph1:
+        kat.ctl("create", key=tree_el, type="ELECTION", client=client, index=iid, expect_instance=iid)
+    kat.c("@5", "ELECT_LISTEN", events=[("@5", "ELECT", L(646))])
+    for iid, _ in ph1[1:]:
+        kat.c(f"@{iid}", "ELECT_LISTEN")
+    kat.close(7, events=[("@69", "ELECT", L(647)), ("@133", "ELECT", L(648)), ("@261", "ELECT", L(650))])
+    kat.ctl("create", key=tree_el, type="ELECTION", client=9, index=709, expect_instance=709)
+    kat.c("@709", "ELECT_LISTEN")
+    kat.close(8, events=[("@517", "ELECT", L(654))])
+    kat.close(9, events=[("@709", "ELECT", L(710))])
+    out.append(kat)
+
     GR = "coordination/src/test/java/io/atomix/coordination/DistributedMembershipGroupTest.java"
     out.append(K("group_join", "reference", f"{GR}:42-65").res(0, "GROUP").inst(0, 0, 100, 1).inst(1, 0, 101, 2)
                .c(1, "GROUP_JOIN", expect=SET(101))

@@ -87,12 +87,15 @@ class KatRun:
         self.next_index = 1
         self.clock = 0
         self.pending = []  # (step, row fields)
+        self.slot_of_id = {}  # instance id -> slot, kept after the instance closes (event targets name it)
 
     def inst_slot(self, ref):
         if isinstance(ref, int):
             return ref
         if ref.startswith("@"):
             s = self.B.inst_slot_of(int(ref[1:]))
+            if s < 0:
+                s = self.slot_of_id.get(int(ref[1:]), -1)
             assert s >= 0, f"unknown instance id {ref}"
             return s
         if ref.startswith("#"):
@@ -181,6 +184,8 @@ class KatRun:
             assert abi.status_code(st) == ST[exp], f"{self.kat['name']} {what}: status {st}"
             if "expect_instance" in c:
                 assert iid == c["expect_instance"], f"{self.kat['name']} {what}: instance {iid}"
+            if abi.status_code(st) == abi.CC_ST_OK:
+                self.slot_of_id[iid] = self.B.inst_slot_of(iid)
         elif what == "delete":
             st = self.B.delete_resource(c["resource"])
             assert abi.status_code(st) == ST[exp], f"{self.kat['name']} delete: status {st}"
