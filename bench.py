@@ -19,12 +19,11 @@ carrying the global log indices (copycat_amd.workload.AtomicLongClients, copycat
 rank writes its applied watermark into HBM (cc_applied_index_async) and the watermarks are all-gathered over RCCL
 (SURVEY §8(e)); c4/c5 also all-gather (OR) the session-expiry bitmap.  Nothing else crosses GPUs.
 
-roofline: per-kernel device time from HIP events recorded on the launch stream over the timed region
-(cc_profile_*).  The 39 algorithmic bytes per commit are split over the kernels that move
-them: the 30 input bytes to k_part_tile (which reads the input columns), the 9 result bytes to the kernel that writes
-the result columns (k_apply_value_v3, which stores every result at its log row on value-only engines; k_unpermute
-elsewhere); `frac` is the dominant kernel's share over its own launch time, `pipeline_frac` all 39 bytes over the
-whole step.
+roofline: the WHOLE step -- SURVEY §8(d)'s algorithmic bytes per commit (c2 39, c3 34.6, c5 48; c4 64 per group +
+8.125 per session) x the commits of one step / the step time, against 8 TB/s; `traffic` = the measured HBM bytes of
+the same step from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/traffic_latest.json).  Sub-fields:
+the dominant kernel's own figure (HIP events recorded on the launch stream around every launch of the timed region,
+cc_profile_*) and every profiled kernel's time per step.
 cpu_baseline: the oracle (C++ restatement of the Java apply path, single thread, as the reference's single
 state-machine thread) over step 0's rows (rank 0, N=1 only); cpu_baseline_all_cores: the same rows sharded by
 resource over the box's CPU share, one oracle per thread.
@@ -109,6 +108,52 @@ def pmc_traffic(kernel, workload):
         return round(ks[names[0]]["bytes_per_launch"] / 1e9, 4)
     except (OSError, KeyError, ValueError):
         return None
+
+
+def pmc_step_traffic(workload):
+    """Measured HBM-side bytes per commit of the WHOLE step: every engine kernel's (2 x FETCH_SIZE + WRITE_SIZE) per
+    launch x its launches, over the commits the profiled bench command applied (scripts/pmc_traffic.py with the
+    command's commit count -> profiles/traffic_latest.json "bytes_per_commit_total")."""
+    p = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["workloads"][workload]["bytes_per_commit_total"]
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
+def roofline_step(prof, workload, n, steps, ms_per_step, b_op, extra=None):
+    """The roofline of the whole step (round-4 verdict: `frac` is the step's, not one kernel's): SURVEY §8(d)'s
+    algorithmic bytes per commit x the commits of one step / the step time, against the 8 TB/s HBM peak.  `traffic`
+    is the measured HBM bytes of the same step from the committed PMC passes (null without them).  The dominant
+    kernel's own figure (HIP events around every launch of the timed region, on the launch stream) and every profiled
+    kernel's time per step are kept as sub-fields."""
+    achieved = b_op * n / (ms_per_step * 1e-3) / 1e9
+    tr = pmc_step_traffic(workload)
+    out = {"bound": "hbm", "scope": "whole step (every kernel and launch gap of cc_apply_batch over one step's batch)",
+           "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+           "traffic": round(tr * n / 1e9, 3) if tr else None,
+           "traffic_unit": "GB per step (HBM-side, 2 x FETCH_SIZE + WRITE_SIZE summed over every kernel, "
+                           "profiles/traffic_latest.json)",
+           "traffic_bytes_per_commit": round(tr, 1) if tr else None, "alg_bytes_per_commit": b_op,
+           "alg_gb_per_step": round(b_op * n / 1e9, 4)}
+    if prof:
+        dom = max(prof, key=lambda k: prof[k][0])
+        ms_tot, launches = prof[dom]
+        commits_per_launch = n * steps / max(launches, 1)
+        avg_ms = ms_tot / max(launches, 1)
+        k_ach = b_op * commits_per_launch / (avg_ms * 1e-3) / 1e9
+        out["dominant_kernel"] = {
+            "kernel": dom, "trace_name": trace_name(dom, workload), "avg_launch_ms": round(avg_ms, 4),
+            "launches": launches, "commits_per_launch": round(commits_per_launch),
+            "achieved": round(k_ach, 1), "frac": round(k_ach / HBM_PEAK_GBPS, 4),
+            "traffic": pmc_traffic(dom, workload), "traffic_unit": "GB per launch",
+            "note": "all of the step's algorithmic bytes charged to this kernel's launch time (an upper bound on its "
+                    "own fraction; the whole-step figure above is the honest one)"}
+        out["per_kernel_ms_per_step"] = {k: round(v[0] / steps, 4) for k, v in prof.items()}
+    if extra:
+        out.update(extra)
+    return out
 
 
 def cpu_model():
@@ -273,6 +318,9 @@ def run_c4(args, dev, rank, world, dist):
                          f"1 thread, {cpu_model()}"}
     if rank == 0:
         ms = elapsed * 1e3 / args.steps
+        step_gbps = (64 * G + 8.125 * S) / (ms * 1e-3) / 1e9
+        qt, xt = pmc_traffic("k_quorum", "c4"), pmc_traffic("k_expire", "c4")
+        c4_traffic = round(qt + xt, 4) if qt is not None and xt is not None else None
         out = {
             "metric": METRIC, "value": round((G + S) * args.steps * world / elapsed, 1), "unit": "groups+sessions/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
@@ -282,16 +330,22 @@ def run_c4(args, dev, rank, world, dist):
                        "input_sets": nsets, "input_set_mb": round((64 + 8) * G / 1e6, 1),
                        "note": "steps take the resident input sets in turn; with >= 4 sets a step's inputs are not in "
                                "the 256 MiB Infinity Cache"},
-            "roofline": {"bound": "hbm", "kernel": dom, "trace_name": "k_quorum<5>", "achieved": round(ach, 1),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "traffic": pmc_traffic("k_quorum", "c4"),
-                         "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
-                         "alg_gb_per_launch": round(64 * G / 1e9, 4), "avg_launch_ms": round(q_ms, 5),
+            "roofline": {"bound": "hbm", "scope": "whole step (one quorum aggregation + one expiry sweep + the RCCL "
+                                                   "exchanges)",
+                         "achieved": round(step_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
+                         "traffic": c4_traffic, "traffic_unit": "GB per step (k_quorum + k_expire, 2 x FETCH_SIZE + "
+                                                                "WRITE_SIZE, profiles/traffic_latest.json)",
+                         "alg_gb_per_step": round((64 * G + 8.125 * S) / 1e9, 4),
+                         "bytes_per_unit": {"group": 64, "session": 8.125},
+                         "dominant_kernel": {"kernel": dom, "trace_name": "k_quorum<5>", "achieved": round(ach, 1),
+                                             "frac": round(ach / HBM_PEAK_GBPS, 4), "avg_launch_ms": round(q_ms, 5),
+                                             "traffic": pmc_traffic("k_quorum", "c4"), "traffic_unit": "GB per launch",
+                                             "alg_gb_per_launch": round(64 * G / 1e9, 4)},
                          "timing": f"{reps} back-to-back launches of each kernel over the resident input sets, one event pair",
                          "per_kernel_ms": {"k_quorum": round(q_ms, 5), "k_expire": round(x_ms, 5)},
                          "per_step_event_ms": {"k_quorum": round(step_q_ms, 5), "k_expire": round(step_x_ms, 5)},
-                         "per_kernel_gbps": {"k_quorum": round(q_gbps, 1), "k_expire": round(x_gbps, 1)},
-                         "bytes_per_unit": {"group": 64, "session": 8.125}},
+                         "per_kernel_gbps": {"k_quorum": round(q_gbps, 1), "k_expire": round(x_gbps, 1)}},
             "parity": parity, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -449,21 +503,7 @@ def run_c5(args, dev, rank, world, dist):
     prof = E.profile_read() if not args.no_profile else {}
     n_events = int(evs.count.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    roofline = None
-    if prof:
-        dom = max(prof, key=lambda k: prof[k][0])
-        ms_tot, launches = prof[dom]
-        commits_per_launch = n * args.steps / max(launches, 1)
-        avg_ms = ms_tot / max(launches, 1)
-        achieved = B_OP_C5 * commits_per_launch / (avg_ms * 1e-3) / 1e9
-        roofline = {
-            "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c5"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c5"),
-            "alg_gb_per_launch": round(B_OP_C5 * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
-            "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
-            "bytes_per_commit": B_OP_C5,
-            "pipeline_frac": round(B_OP_C5 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        }
+    roofline = roofline_step(prof, "c5", n, args.steps, ms_per_step, B_OP_C5)
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(n * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
@@ -762,6 +802,8 @@ def run_c2(args, dev, rank, world, dist):
                        "watermarks": watermarks, "gen_s": round(t_gen, 2)},
             "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all,
         }
+        if not args.no_split and world == 1:  # one global log reaching 8 engines, split on this host
+            out["global_log_split"] = global_log_split(n, 8, cpu_threads())
         if not args.no_e2e:  # the PCIe-inclusive figure beside the device-resident one (never `value`)
             out["end_to_end"] = end_to_end_c2(E, clients, n, dev)
             out["end_to_end_pipelined"] = end_to_end_c2_pipelined(E, clients, n, dev)
@@ -772,6 +814,54 @@ def run_c2(args, dev, rank, world, dist):
     if bad:
         sys.stderr.write(f"PARITY FAILURE: {parity}\n")
         sys.exit(3)
+
+
+def global_log_split(n, world, threads, reps=3):
+    """The host half of the multi-GPU drop-in: one global c2 log of n rows over world x 65,536 resources
+    (ResourceManager multiplexes every resource in one log, ResourceManager.java:37-39) split by owner into `world`
+    per-rank batches (cc_split_batch, every column, log order kept per rank), and the per-rank results merged back
+    (cc_merge_results).  Staging buffers allocated once and reused; best of `reps` after a warm-up call."""
+    import ctypes as C
+
+    from copycat_amd import abi, shard
+    from copycat_amd.batch import Batch
+    from copycat_amd.engine import _check, _np, lib
+    from copycat_amd.workload import atomic_long_stream
+
+    R = 65536 * world
+    b = atomic_long_stream(n, R)
+    tab = (np.arange(R) % world).astype(np.uint8)
+    counts = shard.split_counts(b, tab, world, threads)
+    subs = [Batch(int(c)) for c in counts]
+    outs = (abi.cc_batch_out * world)()
+    for r in range(world):
+        for name in Batch.__slots__:
+            setattr(outs[r], name, _np(getattr(subs[r], name)))
+    cols = abi.cc_batch(**{name: _np(getattr(b, name)) for name in Batch.__slots__})
+    cap = counts.copy()
+    ts = []
+    for it in range(reps + 1):
+        t0 = time.perf_counter()
+        _check(lib().cc_split_batch(C.byref(cols), n, _np(tab), R, world, threads, outs, _np(cap), _np(counts), None))
+        ts.append(time.perf_counter() - t0)
+    pr = (abi.cc_results * world)()
+    keep = [(np.full(int(c), r, np.uint8), subs[r].index) for r, c in enumerate(counts)]
+    for r, (st, va) in enumerate(keep):
+        pr[r].status, pr[r].value = _np(st), _np(va)
+    st, va = np.empty(n, np.uint8), np.empty(n, np.uint64)
+    out = abi.cc_results(_np(st), _np(va))
+    tm = []
+    for it in range(reps + 1):
+        t0 = time.perf_counter()
+        _check(lib().cc_merge_results(_np(b.inst), n, _np(tab), R, world, threads, pr, C.byref(out)))
+        tm.append(time.perf_counter() - t0)
+    ok = bool(np.array_equal(va, b.index) and np.array_equal(st, tab[b.inst]))
+    s, m = min(ts[1:]), min(tm[1:])
+    return {"split_rows_per_s": round(n / s, 1), "split_ms": round(s * 1e3, 2), "merge_rows_per_s": round(n / m, 1),
+            "merge_ms": round(m * 1e3, 2), "rows": n, "ranks": world, "threads": threads, "cpu": cpu_model(),
+            "round_trip_ok": ok, "bytes_per_row": 54,
+            "path": "one global c2 log over 8 x 65,536 resources -> cc_split_batch (every column, stable per rank) -> "
+                    "cc_merge_results of per-rank status/value back to log order; host memory, best of 3 after a warm-up"}
 
 
 def end_to_end_c2(E, clients, n, dev):
@@ -852,37 +942,17 @@ def end_to_end_c2_pipelined(E, clients, n, dev, chunk=1 << 24):
 
 
 def roofline_split(prof, n, steps, ms_per_step):
-    """c2 roofline (the contract's definition): SURVEY §8(d)'s 39 algorithmic bytes per commit x the commits one launch
-    of the dominant kernel processes / that kernel's average launch time (HIP events around every launch of the timed
-    region).  Also reported: the bytes split over the kernels that move them at the interface (30 input bytes read
-    by the partition, 9 result bytes written by the kernel that stores the results) and the whole-pipeline fraction."""
-    if not prof:
-        return None
-    # value-only engines store results at their log rows from the apply (no unpermute launch); an A/B build with the
-    # unpermute (-DCC_VALUE_UNPERMUTE) writes them there
-    writer = "k_unpermute" if prof.get("k_unpermute", (0, 0))[1] else "k_apply_value"
-    share = {"k_part_tile": 30.0, writer: 9.0}
-    dom = max(prof, key=lambda k: prof[k][0])
-    ms_tot, launches = prof[dom]
-    commits_per_launch = n * steps / max(launches, 1)
-    avg_ms = ms_tot / max(launches, 1)
-    b = B_OP_C2
-    achieved = b * commits_per_launch / (avg_ms * 1e-3) / 1e9
-    per_kernel = {}
-    for k, (ms, nl) in prof.items():
-        if nl and k in share:
-            per_kernel[k] = round(share[k] * n * steps / (ms * 1e-3) / 1e9, 1)
-    return {
-        "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c2"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c2"),
-        "traffic_unit": "GB per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_latest.json)",
-        "alg_bytes_per_commit": B_OP_C2, "interface_split": share,
-        "alg_gb_per_launch": round(b * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
-        "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / steps, 4) for k, v in prof.items()},
-        "per_kernel_alg_gbps": per_kernel,
-        "pipeline_achieved_gbps": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9, 1),
-        "pipeline_frac": round(B_OP_C2 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-    }
+    """c2 roofline: the whole step's (roofline_step), plus the split of the 39 algorithmic bytes over the kernels that
+    move them at the interface (30 input bytes read by the partition, 9 result bytes written by the kernel that stores
+    the results) with each one's rate over its own launch time."""
+    extra = None
+    if prof:
+        writer = "k_unpermute" if prof.get("k_unpermute", (0, 0))[1] else "k_apply_value"
+        share = {"k_part_tile": 30.0, writer: 9.0}
+        per_kernel = {k: round(share[k] * n * steps / (ms * 1e-3) / 1e9, 1) for k, (ms, nl) in prof.items()
+                      if nl and k in share}
+        extra = {"interface_split": share, "per_kernel_alg_gbps": per_kernel}
+    return roofline_step(prof, "c2", n, steps, ms_per_step, B_OP_C2, extra)
 
 
 def run_c3(args, dev, rank, world, dist):
@@ -945,21 +1015,7 @@ def run_c3(args, dev, rank, world, dist):
         elapsed = float(t.item())
     prof = E.profile_read() if not args.no_profile else {}
     ms_per_step = elapsed * 1e3 / args.steps
-    roofline = None
-    if prof:
-        dom = max(prof, key=lambda k: prof[k][0])
-        ms_tot, launches = prof[dom]
-        commits_per_launch = n * args.steps / max(launches, 1)
-        avg_ms = ms_tot / max(launches, 1)
-        achieved = B_OP_C3 * commits_per_launch / (avg_ms * 1e-3) / 1e9
-        roofline = {
-            "bound": "hbm", "kernel": dom, "trace_name": trace_name(dom, "c3"), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(dom, "c3"),
-            "alg_gb_per_launch": round(B_OP_C3 * commits_per_launch / 1e9, 4), "avg_launch_ms": round(avg_ms, 4),
-            "launches": launches, "per_kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in prof.items()},
-            "bytes_per_commit": B_OP_C3,
-            "pipeline_frac": round(B_OP_C3 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        }
+    roofline = roofline_step(prof, "c3", n, args.steps, ms_per_step, B_OP_C3)
     cpu = parity = cpu_all = None
     if rank == 0 and (not args.no_parity or (world == 1 and not args.no_cpu_baseline)):
         from oracle.oracle_py import Oracle
@@ -1067,6 +1123,8 @@ def main():
                     help="skip the oracle parity check of step 0 (c2, c5: all rows; c3: the first --cpu-sample rows; "
                          "c4: input set 0)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-split", action="store_true",
+                    help="c2: skip the single-global-log split leg (cc_split_batch / cc_merge_results on the host cores)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="c2: skip the PCIe-inclusive step (pinned H2D + apply + D2H) timed after the timed region")
     ap.add_argument("--hbm-budget-gb", type=float, default=200.0,

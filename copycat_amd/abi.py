@@ -4,7 +4,7 @@ tests/test_abi.py checks every constant here against the #defines of the header,
 """
 import ctypes as C
 
-CC_ABI_VERSION = 4
+CC_ABI_VERSION = 5
 CC_MEMCPY_H2D, CC_MEMCPY_D2H, CC_MEMCPY_D2D = 1, 2, 3
 CC_PROFILE_KERNELS = 7
 CC_PHASES = 8  # phase clocks per kernel of the diagnostics build (cc_debug_phases)
@@ -194,6 +194,10 @@ class cc_batch(C.Structure):
         ("b", C.c_void_p),
         ("aux", C.c_void_p),
     ]
+
+
+class cc_batch_out(C.Structure):
+    _fields_ = cc_batch._fields_
 
 
 class cc_results(C.Structure):

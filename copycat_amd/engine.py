@@ -103,6 +103,8 @@ def lib():
             "cc_wire_string_hash": (i32, [P, u64, P]),
             "cc_handle_hashes": (i32, [P, P, P, u64]),
             "cc_wire_decode": (i32, [P, P, P, P, u64, P, u64, P, P]),
+            "cc_split_batch": (i32, [P, u64, P, u32, u32, u32, P, P, P, P]),
+            "cc_merge_results": (i32, [P, u64, P, u32, u32, u32, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

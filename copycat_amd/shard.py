@@ -7,8 +7,12 @@ commits WITHIN a resource matters, and a stable split keeps it.  The only exchan
   * the session-expiry result (OR of per-rank bitmaps),
 both tiny and all-gathered over RCCL (torch.distributed "nccl" on ROCm) once per batch.
 """
+import ctypes as C
+import os
+
 import numpy as np
 
+from . import abi
 from .batch import Batch
 
 NO_OWNER = -1
@@ -26,18 +30,81 @@ def inst_owner_table(inst_res, world):
     return own.astype(np.int32)
 
 
-def split_batch(b: Batch, inst_owner, world):
-    """Stable split of a batch into per-rank batches.  Returns [(rows, Batch)] indexed by rank."""
-    inst = b.inst.astype(np.int64)
-    own = np.where(inst < len(inst_owner), np.asarray(inst_owner)[np.minimum(inst, len(inst_owner) - 1)], 0)
+def _threads(threads):
+    if threads:
+        return int(threads)
+    n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def _rank_table(inst_owner, world):
+    t = np.ascontiguousarray(inst_owner)
+    if world > 256:
+        raise ValueError("world must be <= 256")
+    if t.dtype != np.uint8:
+        if len(t) and (t.min() < 0 or t.max() >= world):
+            raise ValueError("inst_owner names a rank outside [0, world)")
+        t = t.astype(np.uint8)
+    return t
+
+
+def split_counts(b: Batch, inst_owner, world, threads=0):
+    """Rows per rank of a stable split (cc_split_batch with no outputs)."""
+    from .engine import _check, _np, lib
+
+    tab = _rank_table(inst_owner, world)
+    counts = np.zeros(world, np.uint64)
+    cols = abi.cc_batch(**{name: _np(getattr(b, name)) for name in Batch.__slots__})
+    _check(lib().cc_split_batch(C.byref(cols), len(b), _np(tab), len(tab), world, _threads(threads), None, None,
+                                _np(counts), None))
+    return counts
+
+
+def split_batch(b: Batch, inst_owner, world, threads=0, rows=True):
+    """Stable split of one global log's batch into per-rank batches (native, multi-threaded: cc_split_batch).
+
+    Returns [(rows, Batch)] indexed by rank; rows[r] are the rank's rows of `b` in log order (None if rows=False:
+    merge_by_owner does not need them).  Rows whose instance slot is beyond the owner table go to rank 0."""
+    from .engine import _check, _np, lib
+
+    tab = _rank_table(inst_owner, world)
+    counts = split_counts(b, tab, world, threads)
     parts = []
+    outs = (abi.cc_batch_out * world)()
+    rowp = (C.c_void_p * world)()
     for r in range(world):
-        rows = np.nonzero(own == r)[0]
-        sub = Batch(0)
+        sub = Batch(int(counts[r]))
+        ridx = np.empty(int(counts[r]), np.uint64) if rows else None
         for name in Batch.__slots__:
-            setattr(sub, name, np.ascontiguousarray(getattr(b, name)[rows]))
-        parts.append((rows, sub))
+            setattr(outs[r], name, _np(getattr(sub, name)))
+        rowp[r] = _np(ridx) if rows else None
+        parts.append((ridx, sub))
+    cap = counts.copy()
+    cols = abi.cc_batch(**{name: _np(getattr(b, name)) for name in Batch.__slots__})
+    _check(lib().cc_split_batch(C.byref(cols), len(b), _np(tab), len(tab), world, _threads(threads), outs, _np(cap),
+                                _np(counts), rowp if rows else None))
     return parts
+
+
+def merge_by_owner(inst, inst_owner, world, parts, threads=0):
+    """parts[r] = (status, value) of rank r, in its split order -> (status[n], value[n]) in log order
+    (cc_merge_results: the split's owner walk backwards, no row ids needed)."""
+    from .engine import _check, _np, lib
+
+    tab = _rank_table(inst_owner, world)
+    inst = np.ascontiguousarray(inst, np.uint32)
+    n = len(inst)
+    status = np.empty(n, np.uint8)
+    value = np.empty(n, np.uint64)
+    pr = (abi.cc_results * world)()
+    keep = []
+    for r, (s, v) in enumerate(parts):
+        s, v = np.ascontiguousarray(s, np.uint8), np.ascontiguousarray(v, np.uint64)
+        keep.append((s, v))
+        pr[r].status, pr[r].value = _np(s), _np(v)
+    out = abi.cc_results(_np(status), _np(value))
+    _check(lib().cc_merge_results(_np(inst), n, _np(tab), len(tab), world, _threads(threads), pr, C.byref(out)))
+    return status, value
 
 
 def merge_results(n, parts):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CC_ABI_VERSION 4
+#define CC_ABI_VERSION 5
 
 /* ---- return codes ------------------------------------------------------------------------------ */
 #define CC_OK               0
@@ -516,6 +516,37 @@ typedef struct cc_wire_out {
  * nor String (user objects have no canonical tag); rows before *bad_row are decoded. */
 int  cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* in, const uint8_t* buf, uint64_t buf_len,
                     const uint64_t* offsets, uint64_t n, const cc_wire_out* out, uint64_t* bad_row);
+
+/* ---- one global log, many engines (ABI 5; copycat_amd/csrc/split.cpp) -----------------------------
+ * The reference multiplexes every resource in one Raft log (ResourceManager.java:37-39,56-72); with one engine per
+ * GPU the host splits each committed batch by the rank that owns the row's resource, and merges the per-rank results
+ * back into log order.  Host memory only: no engine and no GPU is involved.
+ *
+ * cc_split_batch: stable split of rows [0, n) of `in` (host columns; inst is required, any other column may be NULL
+ * and then stays NULL).  rank_of_inst[s] (s < n_inst) is the rank owning instance slot s; a row whose inst >= n_inst
+ * goes to rank 0 (whose engine answers UNKNOWN_SESSION).  counts[r] = rows of rank r.  With outs == NULL only the
+ * counts are computed.  Otherwise outs[r] receives rank r's rows in log order: every column present in `in` must be
+ * non-NULL in outs[r], with room for out_cap[r] rows; if counts[r] > out_cap[r] for any r the call returns
+ * CC_ERR_CAPACITY with `counts` filled and nothing written.  rows (optional, world pointers, each optional) receives
+ * each output row's row in `in`.  threads: worker threads (0 = hardware concurrency). */
+typedef struct cc_batch_out {
+  uint64_t* index;
+  uint64_t* time;
+  uint32_t* inst;
+  uint8_t*  op;
+  uint8_t*  flags;
+  uint64_t* key;
+  uint64_t* a;
+  uint64_t* b;
+  uint64_t* aux;
+} cc_batch_out;
+int  cc_split_batch(const cc_batch* in, uint64_t n, const uint8_t* rank_of_inst, uint32_t n_inst, uint32_t world,
+                    uint32_t threads, const cc_batch_out* outs, const uint64_t* out_cap, uint64_t* counts,
+                    uint64_t* const* rows);
+/* cc_merge_results: the inverse for the result columns.  Row i of `out` (n rows) takes the next unread row of
+ * parts[rank_of(inst[i])] (the same inst column and table the split used). */
+int  cc_merge_results(const uint32_t* inst, uint64_t n, const uint8_t* rank_of_inst, uint32_t n_inst, uint32_t world,
+                      uint32_t threads, const cc_results* parts, const cc_results* out);
 
 #ifdef __cplusplus
 }
