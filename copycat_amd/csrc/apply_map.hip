@@ -130,13 +130,21 @@ __device__ inline void pc_materialize(const PComp& c, uint32_t w0, uint64_t v0, 
 // expires if its deadline is <= the clock at which the reference last fired timers (module mode: this commit's
 // clock; manager mode: the previous commit's, A8), and a commit that stores a value re-arms or cancels the timer.
 // The per-record clocks come from the input columns through map_row (staging position -> batch row).
+// a node created in entry e by this launch (LDS bitmaps: once -> tc1, twice or more -> tc2 as well)
+__device__ inline void claim_mark(uint32_t* tc1, uint32_t* tc2, uint32_t e) {
+  const uint32_t bit = 1u << (e & 31);
+  if (atomicOr(&tc1[e >> 5], bit) & bit) atomicOr(&tc2[e >> 5], bit);
+}
+
 template <bool TTL>
 __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict__ xr, const uint64_t* __restrict__ cb, uint64_t row0,
                                                   const uint16_t* __restrict__ ttab,
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
                                                   uint32_t* __restrict__ tbl_word, uint64_t* __restrict__ tbl_val,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
-                                                  unsigned long long* __restrict__ dropped, unsigned long long* __restrict__ tdrop,
+                                                  uint64_t* __restrict__ tbl_claim, const uint64_t* __restrict__ idx0p,
+                                                  unsigned long long* __restrict__ dropped, const uint64_t* __restrict__ cgen,
+                                                  CsetEnt* __restrict__ cset, uint64_t cset_mask, uint32_t* __restrict__ cset_full,
                                                   uint64_t* __restrict__ tbl_dl, const uint32_t* __restrict__ map_row,
                                                   const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
@@ -177,6 +185,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   __shared__ uint64_t rdl[TTL ? kMCh : 1];        // deadline the commit arms if it stores (0: none)
   __shared__ uint32_t ecnt[kMapRegion + 1];  // commits per entry in the chunk -> run starts
   __shared__ uint32_t eflag[kMapRegion / 32];  // bit e: the entry's run holds a value-comparing op
+  // the entry's claim (tbl_claim, the tree-bin test of map_wide.hip): bound by this launch (free at its load), and
+  // how many nodes this launch created in it (one: its claim is that commit's index; more: the sub-batch's first)
+  __shared__ uint32_t tnew[kMapRegion / 32], tc1[kMapRegion / 32], tc2[kMapRegion / 32];
   __shared__ uint16_t tmap[kMCh];              // the partition tile of each list position of the next chunk
   __shared__ PComp wcomp[MT / kWave];
   static_assert(kMCh < (int)kPkOrig, "packed composites address chunk slots in 12 bits");
@@ -196,7 +207,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   if (t < 3) flag[t] = 0;
   if (t == 0) used_total = 0;
   for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
-  for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = 0;
+  for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = tnew[q] = tc1[q] = tc2[q] = 0;
   {
     uint64_t ek[MEPer], ev[MEPer], edl[MEPer];
     uint32_t ew[MEPer], used = 0;
@@ -226,11 +237,12 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     lds_barrier();
     if (compact) {
       // the live entries' indices move with them (read all before any is written: __syncthreads orders HBM too)
-      uint64_t eci[MEPer], eins[MEPer];
+      uint64_t eci[MEPer], eins[MEPer], ecl[MEPer];
 #pragma unroll
       for (int q = 0; q < MEPer; ++q) {
         eci[q] = tbl_ci[tb + q * MT + t];
         eins[q] = tbl_ins[tb + q * MT + t];
+        ecl[q] = tbl_claim[tb + q * MT + t];
       }
       __syncthreads();
       // live keys are distinct: claim the first free slot of each probe chain (no key comparisons needed)
@@ -239,7 +251,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         // a bound key that is absent now is dropped: it still counts toward its map's peak-size bound
         if ((ew[q] & kMwUsed) && !(ew[q] & (kMwPresent | kMwDead | kMwUnseen)) && dropped) {
           atomicAdd(&dropped[ew[q] & kMwSlotMask], 1ull);
-          atomicAdd(&tdrop[ew[q] & kMwSlotMask], 1ull);
+          // the key leaves the table: kept in the compacted-key set of its map (the tree-bin test, map_wide.hip)
+          const uint32_t ds = ew[q] & kMwSlotMask;
+          cset_insert(cset, cset_mask, cset_full, ds, (ew[q] >> 17) & 3u, ek[q], cgen[ds], ecl[q]);
         }
         if ((ew[q] & kMwPresent) && !(ew[q] & kMwDead)) {
           const uint32_t res = ew[q] & kMwSlotMask, kt = (ew[q] >> 17) & 3;
@@ -249,10 +263,16 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           tval[p] = ev[q];
           tbl_ci[tb + p] = eci[q];
           tbl_ins[tb + p] = eins[q];
+          tbl_claim[tb + p] = ecl[q];
           if (TTL) tdl[p] = edl[q];
         }
       }
       __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < MEPer; ++q) {  // entries free at the load (after compaction): a claim by this launch
+      const uint32_t e = q * MT + t;
+      if (tword[e] == 0u) atomicOr(&tnew[e >> 5], 1u << (e & 31));
     }
   }
 
@@ -609,6 +629,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         ress[rci[s]] = (uint8_t)st;
         resv[rci[s]] = rv;
         resd[rci[s]] = (int8_t)(((sw & kMwPresent) != 0) - was);
+        if ((sw & kMwPresent) && !was) claim_mark(tc1, tc2, e);
         cur = pc_compose(cur, el[q]);
         if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
           fin[q] = true;
@@ -661,6 +682,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         ress[rci[s]] = (uint8_t)st;
         resv[rci[s]] = rv;
         resd[rci[s]] = (int8_t)(((wv & kMwPresent) != 0) - was);
+        if ((wv & kMwPresent) && !was) claim_mark(tc1, tc2, e);
         if (wrote) { ci = rpos[s]; any_w = true; }
         if (created) { ins = rpos[s]; any_c = true; }
       }
@@ -694,6 +716,10 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     tbl_val[tb + e] = tval[e];
     if (tcr[e] != kNoRef) tbl_ci[tb + e] = xr[tcr[e]].idx;
     if (tir[e] != kNoRef) tbl_ins[tb + e] = xr[tir[e]].idx;
+    if (((tnew[e >> 5] >> (e & 31)) & 1u) && (tword[e] & kMwUsed)) {  // bound by this launch: its claim
+      const bool one = ((tc1[e >> 5] >> (e & 31)) & 1u) && !((tc2[e >> 5] >> (e & 31)) & 1u) && tir[e] != kNoRef;
+      tbl_claim[tb + e] = one ? xr[tir[e]].idx : *idx0p;
+    }
     if (TTL) tbl_dl[tb + e] = tdl[e];
   }
   PH(7);
@@ -701,9 +727,11 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   if (err) atomicOr(err_out, err);
 }
 
-// A deleted map: its entries become DEAD (never matched; reclaimed by the next compaction of their region).
-__global__ void k_map_drop(uint32_t* __restrict__ tbl_word, uint64_t entries, uint32_t slot) {
+// A deleted / cleared map: its entries become DEAD (never matched; reclaimed by the next compaction of their region),
+// and its generation moves on (the keys compacted away before no longer count toward its tree-bin test).
+__global__ void k_map_drop(uint32_t* __restrict__ tbl_word, uint64_t entries, uint32_t slot, uint64_t* __restrict__ cgen) {
   const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0 && cgen) ++cgen[slot];
   if (e >= entries) return;
   const uint32_t wv = tbl_word[e];
   if ((wv & kMwUsed) && !(wv & kMwDead) && (wv & kMwSlotMask) == slot) tbl_word[e] = (wv & ~(kMwPresent | kMwVtagMask)) | kMwDead;
@@ -714,11 +742,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   a.mark(K_APPLY_MAP, 1, st);
   if (a.ttl)
     hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
-                       (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
+                       a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, a.err);
   else
     hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
-                       (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, nullptr, nullptr, nullptr, nullptr, nullptr, false,
+                       a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -738,8 +766,8 @@ int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* ma
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st) {
-  hipLaunchKernelGGL(k_map_drop, dim3((uint32_t)((entries + 255) / 256)), dim3(256), 0, st, tbl_word, entries, slot);
+int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, uint64_t* cgen, hipStream_t st) {
+  hipLaunchKernelGGL(k_map_drop, dim3((uint32_t)((entries + 255) / 256)), dim3(256), 0, st, tbl_word, entries, slot, cgen);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

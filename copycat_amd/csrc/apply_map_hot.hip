@@ -166,6 +166,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_count(const HotSamp* __restrict__
 __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ cand, const uint32_t* __restrict__ cand_n,
                                                    uint32_t map_bits, uint64_t* tbl_key, uint32_t* tbl_word,
                                                    uint64_t* tbl_val, uint64_t* tbl_ci, uint64_t* tbl_ins,
+                                                   uint64_t* tbl_claim, const uint64_t* __restrict__ idx0p,
                                                    HotKey* __restrict__ hot, uint32_t* __restrict__ hot_n,
                                                    const uint8_t* __restrict__ msmall) {
   const uint32_t t = threadIdx.x;
@@ -195,6 +196,8 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
           __hip_atomic_store(&tbl_val[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_ci[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_ins[base + p], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // its claim (the tree-bin test, map_wide.hip): no later than this sub-batch's first commit
+          __hip_atomic_store(&tbl_claim[base + p], (uint64_t)*idx0p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&tbl_word[base + p], ident | kMwUnseen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           pos = (uint32_t)(base + p);
           return true;
@@ -634,7 +637,7 @@ int launch_map_hot_detect(const HotArgs& a, hipStream_t st) {
 
 int launch_map_hot_bind(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_bind, dim3(1), dim3(kDetT), 0, st, a.hot_cand, a.hot_cand_n, a.map_bits, a.tbl_key, a.tbl_word,
-                     a.tbl_val, a.tbl_ci, a.tbl_ins, a.hot, a.hot_n, a.msmall);
+                     a.tbl_val, a.tbl_ci, a.tbl_ins, a.tbl_claim, a.idx0, a.hot, a.hot_n, a.msmall);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -341,19 +341,89 @@ __device__ inline uint32_t java_key_hash(uint32_t ktag, uint64_t v, const uint64
   return h ^ (h >> 16);
 }
 
-// A map's java.util.HashMap while its table is small (capacity <= 64; map_small.hip): the live keys' hashes (a
-// multiset, <= 48 of them), the capacity level (capacity = 16 << lvl) and whether a bin was treeified.  Below capacity
-// 64 a bin that reaches 9 keys resizes the table early (HashMap.treeifyBin); at 64 it becomes a red-black tree bin,
-// whose iteration order the engine does not follow (kSmTree; tree_bins: the bins, mod 64, that became trees).
-constexpr uint32_t kSmKeys = 48;
+// Keys compacted away from the map table (apply_map.hip: a region more than 3/4 bound re-inserts its present entries
+// and drops the bound-but-absent ones), kept per (map, generation) in a device hash set with the log index at which
+// the key's entry was first bound (its claim: tbl_claim).  A tree bin (capacity >= 128) needs 9 keys in one bin at
+// once; the engine's test for "the deciding bin of an order-dependent containsValue may have been a tree bin" counts,
+// per capacity level L, the distinct keys the map bound in that bin at level L's bin width before its table grew past
+// L, since its last clear: the bound entries of the table plus this set's keys that are not bound now
+// (map_wide.hip k_mw_order / k_mw_cset).  A clear / Delete bumps the map's generation (its old keys no longer count).
+// meta: occupied << 31 | (generation & 0xFFF) << 19 | key tag << 17 | slot.
+struct CsetEnt {
+  uint64_t key;
+  unsigned long long claim;  // the earliest claim of the key's entries that were compacted away
+  uint32_t meta;
+  uint32_t pad;
+};
+__device__ inline uint32_t cset_meta(uint32_t slot, uint32_t kt, uint64_t gen) {
+  return 0x80000000u | ((uint32_t)(gen & 0xFFFu) << 19) | ((kt & 3u) << 17) | (slot & kMwSlotMask);
+}
+// (a key is inserted by the one workgroup compacting its region; a reader racing an insert of another key of the
+// same map may miss a dedupe and add a duplicate: that only over-counts, toward refusing)
+__device__ inline void cset_insert(CsetEnt* __restrict__ set, uint64_t mask, uint32_t* __restrict__ full, uint32_t slot,
+                                   uint32_t kt, uint64_t key, uint64_t gen, uint64_t claim) {
+  const uint32_t meta = cset_meta(slot, kt, gen);
+  uint64_t p = (map_hash(slot, kt, key) ^ (gen * 0x9E3779B97F4A7C15ull)) & mask;
+  for (int step = 0; step < 128; ++step, p = (p + 1) & mask) {
+    uint32_t m = __atomic_load_n(&set[p].meta, __ATOMIC_RELAXED);
+    if (m == 0u) {
+      m = atomicCAS(&set[p].meta, 0u, meta);
+      if (m == 0u) {
+        set[p].key = key;
+        set[p].claim = claim;  // (one key is compacted by one workgroup at a time: no racing dedupe of it)
+        return;
+      }
+    }
+    if (m == meta && set[p].key == key) {
+      atomicMin(&set[p].claim, (unsigned long long)claim);
+      return;
+    }
+  }
+  atomicOr(full, 1u);  // (the set is full: every later order-dependent test above capacity 64 refuses)
+}
+// A map's capacity-level timeline (cc_engine::d_lvl_at, kLvlSlots per map): the log index of the commit whose
+// insertion grew its HashMap table to level L (capacity 16 << L), ~0 while not reached (0 for level 0).  A key counts
+// toward level L's tree-bin test only if its entry was claimed before the table left level L (lvl_at[L + 1]).
+constexpr uint32_t kLvlSlots = 32;
+__device__ inline void lvl_reached(unsigned long long* __restrict__ lvl_at, uint32_t m, uint32_t from, uint32_t to,
+                                   uint64_t idx) {
+  for (uint32_t L = from + 1; L <= to && L < kLvlSlots; ++L) atomicMin(&lvl_at[(uint64_t)m * kLvlSlots + L], (unsigned long long)idx);
+}
+// Is the key bound in the map table now (an entry of its map and tag, not dead)?  Probes its region from the key's
+// first slot until an empty entry (map_hash: the top map_bits bits pick the region).
+__device__ inline bool tbl_bound(const uint32_t* __restrict__ word, const uint64_t* __restrict__ tkey, uint32_t map_bits,
+                                 uint32_t slot, uint32_t kt, uint64_t key) {
+  const uint64_t h = map_hash(slot, kt, key);
+  const uint64_t base = (h >> (64 - map_bits)) * (uint64_t)kMapRegion;
+  const uint32_t ident = (slot & kMwSlotMask) | ((kt & 3u) << 17) | kMwUsed;  // (mw_ident)
+  uint32_t p = (uint32_t)h & (kMapRegion - 1);
+  for (int step = 0; step < kMapRegion; ++step, p = (p + 1) & (kMapRegion - 1)) {
+    const uint32_t w = word[base + p];
+    if (w == 0u) return false;
+    if ((w & kMwIdentMask) == ident && tkey[base + p] == key) return true;
+  }
+  return false;
+}
+
+// A map's java.util.HashMap while its table is small (capacity <= 64; map_small.hip, small_jhm.h): the nodes of the
+// live keys (their hashes, chain and red-black tree links, at most 49 at once), the bin heads, the capacity level
+// (capacity = 16 << lvl) and the bins (mod 64) that became tree bins since the last clear.  Below capacity 64 a bin
+// that reaches 9 keys resizes the table early (HashMap.treeifyBin); at 64 it becomes a red-black tree bin, followed
+// node for node here; after the window (capacity 128) such a bin's order is no longer followed (tree_bins, sticky).
+constexpr uint32_t kSmNodes = 64;
 struct SmallMap {
   uint32_t n, lvl, flags, pad;
   uint64_t tree_bins;
-  uint32_t jh[kSmKeys];
+  uint64_t used;            // node pool occupancy
+  uint32_t jh[kSmNodes];    // node: the key's HashMap hash
+  uint8_t nx[kSmNodes], pv[kSmNodes], pa[kSmNodes], lf[kSmNodes], rt[kSmNodes];  // links: node + 1 (0 = null)
+  uint8_t nb[kSmNodes];     // bit 0 TreeNode, bit 1 red
+  uint8_t tab[64];          // bin heads: node + 1 (0 = null)
 };
-constexpr uint32_t kSmIn = 1u;       // the table is still small (capacity <= 64): tracked key by key
-constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin while tracked
-constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (snapshots of round-4 engines before TTL-mode tracking)
+constexpr uint32_t kSmIn = 1u;       // the table is still small (capacity <= 64): followed node for node
+constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin since the last clear
+constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (kept for the snapshot format; never set now)
+constexpr uint32_t kSmAmbig = 8u;    // two live keys with one hash (or a key the model does not hold): order unknown
 // per-map flags of the batch (cc_engine::d_msmall): bit 0 the table is small (events followed key by key), bit 1 the
 // batch asks the map's size / isEmpty (events followed for the in-stream answers); either keeps the map's keys out of
 // hot-key routing, so every such commit is a region record

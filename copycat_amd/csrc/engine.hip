@@ -94,7 +94,7 @@ static void free_all(cc_engine* e) {
                   e->d_hot_len,  e->d_hot_cond, e->d_hot_agg,   e->d_hot_s0,    e->d_hot_samp, e->d_sb_kind,    e->d_inst_id,
                   e->d_coord,    e->d_clock,    e->d_ev_cnt,    e->d_row_of,    e->d_ev_loc,     e->d_tile_sum,
                   e->d_tile_off, e->d_arena,    e->d_ev_perm,   e->d_arena_n,   e->d_ev_total,
-                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,    e->d_mw_tdrop,
+                  e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,    e->d_mw_cgen, e->d_cset, e->d_cset_full, e->d_tbl_claim, e->d_lvl_at, e->d_half_count,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
@@ -301,7 +301,12 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_hot_cand_n, sizeof(uint32_t));
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
-    ALLOC(e->d_mw_tdrop, sizeof(uint64_t) * cfg->max_resources);
+    ALLOC(e->d_mw_cgen, sizeof(uint64_t) * cfg->max_resources);
+    e->cset_mask = std::max<uint64_t>(4096, e->map_entries) - 1;  // (map_entries is a power of two)
+    ALLOC(e->d_cset, sizeof(CsetEnt) * (e->cset_mask + 1));
+    ALLOC(e->d_cset_full, sizeof(uint32_t));
+    ALLOC(e->d_tbl_claim, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_lvl_at, sizeof(unsigned long long) * kLvlSlots * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
     ALLOC(e->d_msmall, cfg->max_resources);
@@ -356,7 +361,12 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_hot_n, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_peak, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mw_drop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
-    if ((he = hipMemset(e->d_mw_tdrop, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_mw_cgen, 0, sizeof(uint64_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_cset, 0, sizeof(CsetEnt) * (e->cset_mask + 1))) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_cset_full, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_tbl_claim, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_lvl_at, 0xFF, sizeof(unsigned long long) * kLvlSlots * cfg->max_resources)) != hipSuccess)
+      return fail("memset", he);
     if ((he = hipMemset(e->d_msize, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mpcap, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msm, 0, sizeof(SmallMap) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
@@ -543,9 +553,15 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
   if (is_keyed(type)) {  // a new HashMap: capacity 16, no history
     dev_fill(e, e->d_mw_peak, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
     dev_fill(e, e->d_mw_drop, sizeof(uint64_t) * first, 0, sizeof(uint64_t) * count);
-    dev_fill(e, e->d_mw_tdrop, sizeof(uint64_t) * first, 0, sizeof(uint64_t) * count);
+    // (d_mw_cgen is not reset: a reused slot must not see the compacted keys of the map deleted from it, whose delete
+    // bumped the generation)
     dev_fill(e, e->d_msize, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
     dev_fill(e, e->d_mpcap, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
+    {  // the capacity-level timeline: level 0 from the start, none of the others reached
+      std::vector<unsigned long long> la((size_t)kLvlSlots * count, ~0ull);
+      for (uint32_t k = 0; k < count; ++k) la[(size_t)k * kLvlSlots] = 0;
+      dev_copy(e, e->d_lvl_at, sizeof(unsigned long long) * kLvlSlots * first, la.data(), sizeof(unsigned long long) * la.size());
+    }
     // MapState's table followed key by key while small (map_small.hip); sets / multimaps have no order-dependent op
     std::vector<SmallMap> sm(count);
     const bool is_map = type == CC_RES_MAP;
@@ -613,7 +629,7 @@ int cc::delete_slot(cc_engine* e, uint32_t slot) {
   e->leaks.erase(slot);  // the per-slot view ends with the resource (its dropped commits stay in the log)
   // ResourceManager.deleteResource: delete() the state, close the executor, drop every instance of the resource.
   if (is_keyed(e->res_type[slot])) {  // MapState.delete :264-274 / SetState.delete :123-134 — entries die with it
-    if (launch_map_drop_resource(e->d_tbl_word, e->map_entries, slot, e->own_stream))
+    if (launch_map_drop_resource(e->d_tbl_word, e->map_entries, slot, e->d_mw_cgen, e->own_stream))
       return set_err(CC_ERR_HIP, "map drop launch", hipGetLastError());
     HIPCHECK(hipStreamSynchronize(e->own_stream));
   }
@@ -703,7 +719,7 @@ static const bool g_dbg_sync = getenv("CC_DEBUG_SYNC") != nullptr;
 
 // TTL mode: the map events appended so far (commits, expiries) -> every map's size and capacity, the small maps' key
 // sets (map_small.hip: sort, runs, k_small_replay + k_ttl_replay), then the counters for the next round.
-static int ttl_replay(cc_engine* e, hipStream_t st) {
+static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = nullptr, uint64_t lo = 0) {
   uint32_t ctl[2] = {0, 0};
   HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
@@ -723,6 +739,9 @@ static int ttl_replay(cc_engine* e, hipStream_t st) {
   sa.mpcap = e->d_mpcap;
   sa.max_resources = e->cfg.max_resources;
   sa.msize = e->d_msize;
+  sa.lvl_at = e->d_lvl_at;
+  sa.index = index;  // (null for the expiry-only flushes: they grow no table)
+  sa.lo = lo;
   const int rs = launch_small_replay(sa, ctl[0], st);
   if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "TTL map events launch", hipGetLastError())
                           : set_err(CC_ERR_STATE, "TTL map events exceed their buffer");
@@ -781,6 +800,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   if ((((uintptr_t)out->status) & 3) || (((uintptr_t)out->value) & 15) || (((uintptr_t)c->inst) & 15))
     return set_err(CC_ERR_INVALID, "inst and value must be 16-byte aligned, status 4-byte aligned");
   if (e->map_bits && !c->key) return set_err(CC_ERR_INVALID, "an engine with maps needs the key column");
+  if (e->map_bits && !c->index)  // (log order of map events and the entries' claims: the tree-bin test, map_wide.hip)
+    return set_err(CC_ERR_INVALID, "an engine with maps needs the index column");
   if (e->d_val_live && !c->index) return set_err(CC_ERR_INVALID, "CC_CFG_VALUE_RETAINED needs the index column");
   if (ev && (!ev->pos || !ev->target || !ev->code || !ev->src || !ev->tag || !ev->payload || !ev->count))
     return set_err(CC_ERR_INVALID, "event stream columns and count are required");
@@ -848,18 +869,34 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (nb > kBarCap) {
       // More barrier rows than one listing holds: the batch runs as two consecutive batches (a batch boundary is a
       // point of the log like any other: timers due by its clock have fired there in both timer orders, A8).  With an
-      // event stream the halves' events would need one output: that case still fails.
-      if (ev || n < 2)
-        return set_err(CC_ERR_CAPACITY, "more whole-map ops (containsValue/clear/Delete, size/isEmpty in TTL mode) and group "
-                                        "schedules in one batch with an event stream than kBarCap");
+      // event stream the second half's events are appended after the first's, their rows moved by h.
+      if (n < 2)
+        return set_err(CC_ERR_CAPACITY, "more whole-map ops and group schedules in one row than kBarCap");
       const uint64_t h = n / 2;
       auto shift = [h](const auto* p) { return p ? p + h : p; };
       const cc_batch c2{shift(c->index), shift(c->time), shift(c->inst), shift(c->op), shift(c->flags), shift(c->key),
                         shift(c->a), shift(c->b), shift(c->aux)};
       const cc_results o2{out->status + h, out->value + h};
-      int rc = cc_apply_batch(e, c, h, out, nullptr, stream);
-      if (!rc) rc = cc_apply_batch(e, &c2, n - h, &o2, nullptr, stream);
-      return rc;
+      int rc = cc_apply_batch(e, c, h, out, ev, stream);
+      if (rc || !ev || !e->coord_on) return rc ? rc : cc_apply_batch(e, &c2, n - h, &o2, ev, stream);
+      uint64_t n1 = 0, n2 = 0;
+      HIPCHECK(hipMemcpyAsync(&n1, ev->count, sizeof n1, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (n1 > ev->capacity) return set_err(CC_ERR_CAPACITY, "event stream capacity exceeded");
+      if (!e->d_half_count) HIPCHECK(hipMalloc(&e->d_half_count, sizeof(uint64_t)));
+      cc_events ev2 = *ev;
+      ev2.pos += n1, ev2.target += n1, ev2.code += n1, ev2.src += n1, ev2.tag += n1, ev2.payload += n1;
+      ev2.capacity -= n1;
+      ev2.count = e->d_half_count;
+      if ((rc = cc_apply_batch(e, &c2, n - h, &o2, &ev2, stream))) return rc;
+      HIPCHECK(hipMemcpyAsync(&n2, e->d_half_count, sizeof n2, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (launch_ev_shift(ev2.pos, std::min(n2, ev2.capacity), (uint32_t)h, st))
+        return set_err(CC_ERR_HIP, "event row shift launch", hipGetLastError());
+      const uint64_t total = n1 + n2;
+      HIPCHECK(hipMemcpyAsync(ev->count, &total, sizeof total, hipMemcpyHostToDevice, st));
+      HIPCHECK(hipStreamSynchronize(st));  // (total is a host local)
+      return CC_OK;
     }
     if (nb) {  // the barrier rows in log order, then their columns in one gather (one copy back, not one per field)
       e->bars.resize(nb);
@@ -997,6 +1034,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.tbl_val = e->d_tbl_val;
       ha.tbl_ci = e->d_tbl_ci;
       ha.tbl_ins = e->d_tbl_ins;
+      ha.tbl_claim = e->d_tbl_claim;
+      ha.idx0 = c->index ? c->index + lo : nullptr;
       ha.hot = e->d_hot;
       ha.hot_n = e->d_hot_n;
       ha.hot_rpre = e->d_hot_rpre;
@@ -1103,8 +1142,13 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ma.tbl_val = e->d_tbl_val;
       ma.tbl_ci = e->d_tbl_ci;
       ma.tbl_ins = e->d_tbl_ins;
+      ma.tbl_claim = e->d_tbl_claim;
+      ma.idx0 = c->index ? c->index + lo : nullptr;
       ma.dropped = e->d_mw_drop;
-      ma.tdrop = e->d_mw_tdrop;
+      ma.cgen = e->d_mw_cgen;
+      ma.cset = e->d_cset;
+      ma.cset_mask = e->cset_mask;
+      ma.cset_full = e->d_cset_full;
       ma.ttl = e->ttl_live;
       ma.tbl_dl = e->d_tbl_dl;
       ma.map_row = e->d_map_row;
@@ -1160,10 +1204,12 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.sm_ctl = e->d_sm_ctl;
         za.map_row = e->d_map_row;
         za.lo = lo;
+        za.lvl_at = e->d_lvl_at;
+        za.index = c->index;
         za.err = e->d_err;
         if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError());
         own_lo = hi + 1;
-        int rc = ttl_replay(e, st);
+        int rc = ttl_replay(e, st, c->index, lo);
         if (rc) return rc;
       } else {  // exact map sizes and HashMap capacities (containsValue's iteration order)
         MapSizeArgs za{};
@@ -1189,6 +1235,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.list = e->d_msz_list;
         za.list_n = e->d_msz_list_n;
         za.err = e->d_err;
+        za.lvl_at = e->d_lvl_at;
+        za.index = c->index;
+        za.lo = lo;
         if (e->small_live || e->szq_n) {  // small-window / size-queried maps: their insertions / removals (map_small.hip)
           int rc = ensure_small(e);
           if (rc) return rc;
@@ -1246,6 +1295,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.msmall = e->d_msmall;
           sa.mpcap = e->d_mpcap;
           sa.max_resources = e->cfg.max_resources;
+          sa.lvl_at = e->d_lvl_at;
+          sa.idx0 = c->index + lo;
           const int rs = launch_small_replay(sa, ctl[0], st);
           if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "small-map replay launch", hipGetLastError())
                                   : set_err(CC_ERR_STATE, "small-map events exceed their buffer");
@@ -1412,6 +1463,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.tbl_key = e->d_tbl_key;
     mw.tbl_val = e->d_tbl_val;
     mw.tbl_ins = e->d_tbl_ins;
+    mw.tbl_claim = e->d_tbl_claim;
+    mw.lvl_at = e->d_lvl_at;
     if (e->ttl_live) {  // the clock at which the reference last fired timers before this row (A8)
       uint64_t t0 = clock_before, t1 = clock_before;
       if (c->time) {
@@ -1424,7 +1477,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.entries = e->map_entries;
     mw.peak_lo = e->d_mw_peak;
     mw.dropped = e->d_mw_drop;
-    mw.tdrop = e->d_mw_tdrop;
+    mw.cgen = e->d_mw_cgen;
+    mw.cset = e->d_cset;
+    mw.cset_n = e->cset_mask + 1;
+    mw.cset_full = e->d_cset_full;
+    mw.map_bits = e->map_bits;
     mw.msize = e->d_msize;  // exact in both modes (TTL mode: commit + expiry events, map_small.hip)
     mw.mpcap = e->d_mpcap;
     mw.ctl = e->d_mw_ctl;
@@ -2121,7 +2178,11 @@ static std::vector<Section> snap_sections(cc_engine* e) {
     v.push_back({e->d_tbl_dl, nullptr, 8 * n});
     v.push_back({e->d_mw_peak, nullptr, 4 * mr});
     v.push_back({e->d_mw_drop, nullptr, 8 * mr});
-    v.push_back({e->d_mw_tdrop, nullptr, 8 * mr});
+    v.push_back({e->d_mw_cgen, nullptr, 8 * mr});
+    v.push_back({e->d_cset, nullptr, sizeof(CsetEnt) * (e->cset_mask + 1)});
+    v.push_back({e->d_cset_full, nullptr, 4});
+    v.push_back({e->d_tbl_claim, nullptr, 8 * n});
+    v.push_back({e->d_lvl_at, nullptr, 8ull * kLvlSlots * mr});
     v.push_back({e->d_msize, nullptr, 4 * mr});
     v.push_back({e->d_mpcap, nullptr, 4 * mr});
     v.push_back({e->d_msm, nullptr, sizeof(SmallMap) * mr});

@@ -112,8 +112,13 @@ struct MapArgs {
   uint64_t* tbl_val;
   uint64_t* tbl_ci;
   uint64_t* tbl_ins;
+  uint64_t* tbl_claim;        // [entries] log index at which the entry was first bound (tree-bin test, map_wide.hip)
+  const uint64_t* idx0;       // device: the sub-batch's first log index (index column + lo)
   uint64_t* dropped;  // [max_resources] compaction drops bound-but-absent entries: counted per map (map_wide.hip)
-  uint64_t* tdrop;    // [max_resources] the same drops since the map's last clear / Delete (tree-bin test)
+  const uint64_t* cgen; // [max_resources] map generations (bumped by clear / Delete)
+  CsetEnt* cset;        // the compacted keys (common.h CsetEnt): each drop is inserted
+  uint64_t cset_mask;
+  uint32_t* cset_full;
   bool ttl;           // TTL mode: entries carry timer deadlines (k_apply_map<true>)
   uint64_t* tbl_dl;
   const uint32_t* map_row;     // [sub_batch] staging position -> batch row (launch_map_rows)
@@ -169,6 +174,8 @@ struct MapSizeArgs {
   uint32_t* sm_ctl;            // [0] events emitted
   const uint32_t* map_row;     // TTL mode: every map's commits emitted, positioned by batch row (common.h TtlEmit)
   uint64_t lo;                 //   (the sub-batch's first row)
+  unsigned long long* lvl_at;  // the capacity-level timeline (k_msize_exact records each resize's log index)
+  const uint64_t* index;       // the batch's index column (absolute rows)
   uint32_t* err;
 };
 int launch_map_size(const MapSizeArgs& a, hipStream_t st);
@@ -186,6 +193,12 @@ struct SmallArgs {
   uint32_t* mpcap;
   uint32_t max_resources;
   uint32_t* msize;             // TTL mode: every map's size / capacity from its events (k_ttl_replay); else null
+  // the capacity-level timeline (common.h lvl_reached): an event's log index is idx0 + its offset, or in TTL mode
+  // (positions by row, common.h TtlEmit) the index column at row lo + (position - 1) / 2
+  unsigned long long* lvl_at;  // [max_resources * kLvlSlots] (null: not recorded)
+  const uint64_t* idx0;
+  const uint64_t* index;
+  uint64_t lo;
 };
 // TTL mode: the table entries whose timers fire at a boundary the sub-batch owns -> expiry events (common.h TtlEmit)
 int launch_ttl_scan(const TtlEmit& t, const uint64_t* clock_base, const uint32_t* word, const uint64_t* key,
@@ -219,7 +232,7 @@ int launch_size_answer(const SizeArgs& a, hipStream_t st);
 int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st);
 size_t small_sort_temp_bytes(uint32_t cap);
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st);
-int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, hipStream_t st);
+int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, uint64_t* cgen, hipStream_t st);
 int launch_map_rows(const uint16_t* cpos, uint64_t lo, uint64_t hi, uint32_t* map_row, hipStream_t st);
 
 // Whole-map ops (containsValue / isEmpty / size / clear / Delete): barrier rows of a batch (map_wide.hip).
@@ -239,12 +252,18 @@ struct MapWideArgs {
   const uint64_t* tbl_key;
   const uint64_t* tbl_val;
   const uint64_t* tbl_ins;
+  const uint64_t* tbl_claim;   // first-bound log index of each entry, and each map's capacity-level timeline: a key
+  const unsigned long long* lvl_at;  // counts at level L only if bound before the table left L (common.h)
   const uint64_t* tbl_dl;      // TTL mode: entry deadlines (null: no timers)
   uint64_t fire_clock;         // entries with a deadline <= this clock have expired at the barrier row
   uint64_t entries;
   uint32_t* peak_lo;           // [max_resources] lower bound on the map's peak size
   uint64_t* dropped;           // [max_resources] entries dropped by compaction / clear (upper-bound term)
-  uint64_t* tdrop;             // [max_resources] entries compacted away since the last clear (tree-bin test)
+  uint64_t* cgen;              // [max_resources] map generations: clear / Delete bump them
+  const CsetEnt* cset;         // keys compacted away from the table (tree-bin test: k_mw_cset)
+  uint64_t cset_n;
+  const uint32_t* cset_full;
+  uint32_t map_bits;
   uint32_t* msize;             // exact tracking (launch_map_size; null in TTL mode): the live size, and
   const uint32_t* mpcap;       //   log2(capacity / 16) of the peak (in TTL mode a lower bound for the bounds above)
   unsigned long long* ctl;     // [C_N] scratch
@@ -306,6 +325,8 @@ struct HotArgs {
   uint64_t* tbl_val;
   uint64_t* tbl_ci;
   uint64_t* tbl_ins;
+  uint64_t* tbl_claim;    // [entries] first-bound log index of each entry (k_hot_bind claims with idx0)
+  const uint64_t* idx0;   // device: the sub-batch's first log index
   HotKey* hot;
   uint32_t* hot_n;
   const uint8_t* msmall;  // [max_resources] maps in their small-table window (map_small.hip): never hot-routed
@@ -388,6 +409,7 @@ struct EventArgs {
   Marker mark;
 };
 int launch_events(const EventArgs& a, hipStream_t st);
+int launch_ev_shift(uint32_t* pos, uint64_t n, uint32_t by, hipStream_t st);
 constexpr uint64_t kEvChunk = 8192;  // arena events per bucketing workgroup (events.hip)
 inline uint64_t ev_chunk_cap(uint64_t arena_cap) { return (arena_cap + kEvChunk - 1) / kEvChunk; }
 

@@ -163,7 +163,13 @@ struct cc_engine {
   uint32_t* d_bar_n = nullptr;
   uint32_t* d_mw_peak = nullptr;   // [max_resources]
   uint64_t* d_mw_drop = nullptr;   // [max_resources]
-  uint64_t* d_mw_tdrop = nullptr;  // [max_resources] keys compacted away since the map's last clear (tree-bin test)
+  uint64_t* d_mw_cgen = nullptr;   // [max_resources] the map's generation: bumped by clear / Delete (compacted-key set)
+  CsetEnt* d_cset = nullptr;       // keys compacted away from the table, per (map, generation) (common.h CsetEnt)
+  uint64_t cset_mask = 0;          // set entries - 1
+  uint32_t* d_cset_full = nullptr; // the set overflowed
+  uint64_t* d_tbl_claim = nullptr; // [map_entries] log index at which each entry was first bound
+  unsigned long long* d_lvl_at = nullptr;
+  uint64_t* d_half_count = nullptr;  // a batch applied as two calls (kBarCap): the second call's event count  // [max_resources * kLvlSlots] capacity-level timeline (common.h)
   // exact map sizes / HashMap capacities (map_wide.hip launch_map_size; not in TTL mode)
   uint32_t* d_rst_msz = nullptr;   // [sub_batch + 4 kPT] each region map commit's map and size change, staging order
   uint32_t* d_hot_msz = nullptr;   // hot-key commits' size changes (HotArgs::hot_msz)

@@ -384,6 +384,18 @@ __global__ __launch_bounds__(kER) void k_ev_tile_out(const uint16_t* __restrict_
   }
 }
 
+// Events of a batch applied as two calls (more barrier rows than one listing holds, engine.hip): the second call's
+// rows start at h, so its events' rows move by h.
+__global__ void k_ev_shift(uint32_t* __restrict__ pos, uint64_t n, uint32_t by) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) pos[i] += by;
+}
+
+int launch_ev_shift(uint32_t* pos, uint64_t n, uint32_t by, hipStream_t st) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_ev_shift, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, pos, n, by);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_events(const EventArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   a.mark(K_EVENTS, 1, st);

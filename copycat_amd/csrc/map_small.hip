@@ -6,25 +6,22 @@
 // launch_map_size (map_wide.hip).  Below capacity 64 there is a second trigger: java.util.HashMap.putVal calls
 // treeifyBin when a new key makes its bin's chain 9 long, and treeifyBin RESIZES a table under MIN_TREEIFY_CAPACITY
 // (64) instead of treeifying -- at any size.  At capacity 64 the same bin becomes a red-black tree bin, whose
-// iteration order (root first, later keys linked after their tree parent) this engine does not follow: it records
-// which bins (mod 64) became trees, and an order-dependent containsValue deciding inside one of them fails with
-// CC_ERR_STATE instead of guessing.
+// iteration order (root first, later keys linked after their tree parent) the engine follows here node for node.
 //
-// Per map in that window the engine keeps the live keys' hashes (at most 48: a table of 64 holds <= 48 keys) and
-// replays the map's insertions and removals in log order:
+// Per map in that window the engine keeps the map's HashMap node for node (small_jhm.h: at most 49 nodes) and
+// replays its insertions and removals in log order:
 //   1. launch_map_size's count kernel (k_msize_count) emits one event per region commit of a small map that inserted
 //      or removed a key: key (map << 44 | (log index - the sub-batch's first) << 4 | insert / remove), value = the
 //      key's HashMap hash (hot-key routing is off for small maps, k_hot_bind, so every such commit is a region one);
 //   2. a radix sort by that key puts each map's events in log order (hipcub);
-//   3. one wave per map replays them: lane i holds the i-th live hash; an insert counts its bin's keys with one
-//      ballot (>= 8 before it: treeifyBin -- a resize below 64, a tree bin at 64), appends, and resizes when the
-//      size passes 3/4 of the capacity; a removal drops one equal hash.  The map leaves the window when its capacity
-//      passes 64 (no early resize, and no untracked tree, can happen below a tree-free table of 128 ... see
-//      map_wide.hip k_mw_order for the check above 64).
+//   3. one thread per map replays them on an LDS copy of its HashMap: putVal (a chain of 9 calls treeifyBin: a
+//      resize below 64, a red-black tree bin at 64), resize, removeNode.  The map leaves the window when its capacity
+//      passes 64; a bin that was a tree bin there keeps its mark (tree_bins; see map_wide.hip k_mw_order for the
+//      checks above 64).  Inside the window an order-dependent containsValue reads a bin's chain from this model.
 // The capacity level reached is merged into the tracked level (mpcap, atomicMax): the true capacity is the larger of
 // the size-driven one and the early one (after the window both grow by size alone).
 // Cost: nothing once every map has left the window (the host stops looking: no event, no sync); while some are in
-// it, one host read of the event count per sub-batch, a sort of the events and one short wave walk per map.
+// it, one host read of the event count per sub-batch, a sort of the events and one short serial walk per map.
 //
 // TTL mode (common.h TtlEmit): timers remove keys with no commit, so there every map's commits AND expiries are events
 // (an expiry positioned at the boundary where the reference fires the timer, A8), and after the sort k_ttl_replay
@@ -34,6 +31,7 @@
 
 #include "common.h"
 #include "engine_internal.h"
+#include "small_jhm.h"
 
 namespace cc {
 
@@ -45,63 +43,58 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
     if (i == 0 || (key[i] >> 44) != (key[i - 1] >> 44)) seg[atomicAdd(nseg, 1u)] = i;
 }
 
-// One wave per run: the map's live hashes in lanes 0..n-1, its events in log order.
-__global__ __launch_bounds__(256) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                      const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
-                                                      const uint32_t* __restrict__ nseg, SmallMap* __restrict__ st,
-                                                      uint8_t* __restrict__ msmall, uint32_t* __restrict__ mpcap) {
-  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
-  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
-  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
+// One thread per run: the map's java.util.HashMap copied into LDS (small_jhm.h: node pool, chains, tree links),
+// its events applied in log order (putVal of a new key, removeNode), the state written back.  A map whose table
+// passes 64 leaves the window (its later events are not followed).
+constexpr int kSrT = 64;                                               // runs per workgroup
+constexpr int kSrStride = (int)((sizeof(SmallMap) + 8) / 8) | 1;       // u64 words per run's copy (odd: fewer bank conflicts)
+__global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                       const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
+                                                       const uint32_t* __restrict__ nseg, SmallMap* __restrict__ st,
+                                                       uint8_t* __restrict__ msmall, uint32_t* __restrict__ mpcap,
+                                                       unsigned long long* __restrict__ lvl_at, const uint64_t* __restrict__ idx0,
+                                                       const uint64_t* __restrict__ index, uint64_t lo, bool ttl) {
+  __shared__ uint64_t lds[kSrT * kSrStride];
+  static_assert(sizeof(SmallMap) % 8 == 0, "SmallMap copies are u64 words");
+  constexpr uint32_t W = sizeof(SmallMap) / 8;
+  SmallMap& lm = *reinterpret_cast<SmallMap*>(lds + threadIdx.x * kSrStride);
+  const uint32_t E = ctl[0], ns = *nseg;
+  for (uint32_t r = blockIdx.x * kSrT + threadIdx.x; r < ns; r += gridDim.x * kSrT) {
     const uint32_t start = seg[r];
     const uint32_t m = (uint32_t)(key[start] >> 44);
     SmallMap* s = st + m;
-    uint32_t n = s->n, lvl = s->lvl, flags = s->flags;
-    uint64_t tree = s->tree_bins;
-    if (!(flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
-    uint32_t h = l < n ? s->jh[l] : 0u;
-    bool live = l < n;
+    if (!(s->flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(s);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&lm);
+    for (uint32_t q = 0; q < W; ++q) dst[q] = src[q];
+    SmallJhm j(lm);
     for (uint32_t i = start; i < E; ++i) {
       const uint64_t k = key[i];
       if ((uint32_t)(k >> 44) != m) break;
       if (k & 8u) continue;  // a size / isEmpty query (k_size_answer)
       const uint32_t x = val[i];
       if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
-        const uint32_t mask = (16u << lvl) - 1u;
-        const uint32_t in_bin = (uint32_t)__builtin_popcountll(__ballot(live && (h & mask) == (x & mask)));
-        if (in_bin >= 8u) {  // the chain reaches 9 nodes: treeifyBin
-          if (lvl < 2u) ++lvl;  // capacity < MIN_TREEIFY_CAPACITY: resize()
-          else flags |= kSmTree, tree |= 1ull << (x & 63u);
+        const uint32_t lv0 = lm.lvl;
+        const bool stay = j.put(x);
+        if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
+          const uint64_t d = (k >> 4) & ((1ull << 40) - 1);
+          // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
+          if (ttl ? index != nullptr : idx0 != nullptr)
+            lvl_reached(lvl_at, m, lv0, lm.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
         }
-        if (l == n) h = x, live = true;
-        ++n;
-        if (n > (12u << lvl)) ++lvl;  // ++size > threshold: resize()
-        if (lvl >= 3u) {              // capacity 128: out of the window
-          flags &= ~kSmIn;
-          break;
-        }
-      } else if ((k & 3u) == 2u) {  // a key removed: removeNode (one equal hash leaves the multiset)
-        const uint64_t eq = __ballot(live && h == x);
-        if (eq) {
-          const uint32_t at = (uint32_t)__builtin_ctzll(eq), last = n - 1;
-          const uint32_t moved = __shfl(h, (int)last, 64);
-          if (l == at) h = moved;
-          if (l == last) live = false;
-          --n;
-        }
+        if (!stay) break;  // the table passed 64: out of the window
+      } else if ((k & 3u) == 2u) {  // a key removed: removeNode
+        j.remove(x);
       }
     }
-    if (flags & kSmIn) {
-      if (l < kSmKeys) s->jh[l] = live ? h : 0u;
+    if (!(lm.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
+      lm.n = 0;
+      lm.used = 0;
     }
-    if (l == 0) {
-      s->n = (flags & kSmIn) ? n : 0u;
-      s->lvl = lvl;
-      s->flags = flags;
-      s->tree_bins = tree;
-      msmall[m] = (uint8_t)((msmall[m] & ~kMfSmall) | ((flags & kSmIn) ? kMfSmall : 0u));
-      atomicMax(&mpcap[m], lvl);
-    }
+    uint64_t* back = reinterpret_cast<uint64_t*>(s);
+    for (uint32_t q = 0; q < W; ++q) back[q] = dst[q];
+    msmall[m] = (uint8_t)((msmall[m] & ~kMfSmall) | ((lm.flags & kSmIn) ? kMfSmall : 0u));
+    atomicMax(&mpcap[m], lm.lvl);
   }
 }
 
@@ -129,7 +122,9 @@ __global__ void k_ttl_scan(TtlEmit t, const uint64_t* __restrict__ clock_base, c
 // and expiries in log order, its peak -> the capacity level (HashMap.resize never shrinks), the size at the end.
 __global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ ctl,
                                                     const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
-                                                    uint32_t* __restrict__ msize, uint32_t* __restrict__ mpcap) {
+                                                    uint32_t* __restrict__ msize, uint32_t* __restrict__ mpcap,
+                                                    unsigned long long* __restrict__ lvl_at, const uint64_t* __restrict__ index,
+                                                    uint64_t lo) {
   const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
   const uint32_t waves = gridDim.x * (blockDim.x / kWave);
   for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
@@ -150,6 +145,11 @@ __global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__
       int32_t mx = inc;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+      if (lvl_at && index && dlt > 0 && size + inc > peak) {  // a commit growing the table (common.h timeline)
+        const uint64_t d = (k >> 4) & ((1ull << 40) - 1);  // (commits sit at odd positions 2 (row - lo) + 1)
+        lvl_reached(lvl_at, m, cap_level((uint64_t)max<int64_t>(peak, 0)), cap_level((uint64_t)(size + inc)),
+                    index[lo + (d - 1) / 2]);
+      }
       peak = max(peak, size + mx);
       size += __shfl(inc, 63, 64);
       if (__ballot(in) != ~0ull) break;
@@ -179,10 +179,14 @@ __global__ void k_small_count(const uint8_t* __restrict__ msmall, uint32_t R, ui
 
 // MapState.delete (clear / Delete, :255-274): every key leaves; the table keeps its capacity; no tree bin is left
 __global__ void k_small_clear(SmallMap* __restrict__ st, uint32_t m) {
-  if (threadIdx.x == 0) {
-    st[m].n = 0;
-    st[m].flags &= ~kSmTree;
-    st[m].tree_bins = 0;
+  SmallMap& s = st[m];
+  const uint32_t t = threadIdx.x;
+  s.tab[t] = 0;  // (64 threads: one bin head each)
+  if (t == 0) {
+    s.n = 0;
+    s.used = 0;
+    s.flags &= ~(kSmTree | kSmAmbig);
+    s.tree_bins = 0;
   }
 }
 
@@ -303,10 +307,11 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
     if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (E + 255) / 256);
     hipLaunchKernelGGL(k_small_seg, dim3(grid), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg);
-    hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ctl, a.seg, a.nseg, a.state,
-                       a.msmall, a.mpcap);
+    hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(kSrT), 0, st, a.ev_key2, a.ev_val2, a.ctl, a.seg, a.nseg, a.state,
+                       a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
-      hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap);
+      hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap,
+                         a.lvl_at, a.index, a.lo);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "engine_internal.h"
+#include "small_jhm.h"
 
 namespace cc {
 
@@ -212,6 +213,12 @@ __device__ inline uint64_t java_cap(uint64_t p) {
 // that capacity (a tree bin can have formed there only if >= 9 keys ever shared it)
 enum { C_PRES = 0, C_USED, C_NULLS, C_MATCH, C_BN, C_BM, C_IN, C_IM, C_CAP, C_TR0, C_N = C_TR0 + 32 };
 
+// the log index at which map `slot`'s table left level L (grew to L + 1; ~0 while it has not): a key whose entry was
+// claimed later never shared a bin of that width with the others
+__device__ inline uint64_t lvl_left(const unsigned long long* __restrict__ lvl_at, uint32_t slot, uint32_t L) {
+  return L + 1 < kLvlSlots ? (uint64_t)lvl_at[(uint64_t)slot * kLvlSlots + L + 1] : ~0ull;
+}
+
 __global__ void k_mw_reset(unsigned long long* ctl) {
   const int t = threadIdx.x;
   for (int q = t; q < C_N; q += blockDim.x) ctl[q] = (q >= C_BN && q <= C_IM) ? ~0ull : 0ull;
@@ -260,8 +267,9 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
                                                   const uint32_t* __restrict__ peak_lo, const unsigned long long* __restrict__ dropped,
                                                   const uint32_t* __restrict__ mpcap, bool exact, const SmallMap* __restrict__ small,
                                                   const uint64_t* __restrict__ hh_key, const int32_t* __restrict__ hh_val,
-                                                  uint32_t hh_n, int pass, unsigned long long* __restrict__ ctl,
-                                                  uint32_t* __restrict__ err) {
+                                                  uint32_t hh_n, int pass, const uint64_t* __restrict__ claim,
+                                                  const unsigned long long* __restrict__ lvl_at,
+                                                  unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
   if (op != CC_OP_MAP_CONTAINSVALUE || ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0) return;
   const uint32_t mp = mpcap ? mpcap[slot] : 0u, lv = mp & ~kMpInexact;
   const uint32_t sflags = small ? small[slot].flags : 0u;
@@ -300,16 +308,70 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
     if (pass == 0) {
       atomicMin(&ctl[isnull ? C_BN : C_BM], (unsigned long long)b);
     } else {
-      if (cand && b == bb) atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ins[e]);
-      // every key the map ever bound (present or not) that shares the deciding bin at a capacity >= 128: a tree bin
-      // there needs >= 9 of them (HashMap.treeifyBin, TREEIFY_THRESHOLD)
+      if (cand && b == bb) {
+        // the order inside the bin: creation order (tbl_ins) for a list bin; a small map's bin chain from its HashMap
+        // model (small_jhm.h), tree bins included
+        uint64_t ord = ins[e];
+        if (sflags & kSmIn) {
+          bool dup;
+          ord = small_chain_pos(small[slot], jh, dup);
+          if (dup || (16ull << small[slot].lvl) != cap) atomicOr(err, kErrMapOrder);
+        }
+        atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ord);
+      }
+      // every key the map bound since its last clear (present or not) that shares the deciding bin at a capacity
+      // >= 128 and was bound before the table grew past that capacity: a tree bin there needs >= 9 of them at once
+      // (HashMap.treeifyBin, TREEIFY_THRESHOLD)
       for (uint32_t L = 3; L <= lv && L - 3 < 32; ++L) {
         const uint64_t mk = (16ull << L) - 1;
-        if ((jh & mk) == (bb & mk)) atomicAdd(&ctl[C_TR0 + (L - 3)], 1ull);
+        if ((jh & mk) == (bb & mk) && claim[e] <= lvl_left(lvl_at, slot, L)) atomicAdd(&ctl[C_TR0 + (L - 3)], 1ull);
       }
     }
   }
   if (pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) ctl[C_CAP] = cap;
+}
+
+// The deciding bin's keys that the map bound since its last clear and that compaction dropped since (the set of
+// common.h CsetEnt; a key bound again now was counted among the table's entries by k_mw_order pass 1): added to the
+// per-level counts of the tree-bin test.  Runs only for an order-dependent containsValue decided inside one bin of a
+// table above 64 (all threads read the same ctl).  A set that overflowed counts as 9 (refuse).
+__global__ __launch_bounds__(kMwT) void k_mw_cset(const CsetEnt* __restrict__ set, uint64_t n, const uint32_t* __restrict__ full,
+                                                 const uint64_t* __restrict__ cgen, uint32_t slot,
+                                                 const uint32_t* __restrict__ word, const uint64_t* __restrict__ tkey,
+                                                 uint32_t map_bits, const uint32_t* __restrict__ mpcap,
+                                                 const SmallMap* __restrict__ small, const uint64_t* __restrict__ hh_key,
+                                                 const int32_t* __restrict__ hh_val, uint32_t hh_n,
+                                                 const unsigned long long* __restrict__ lvl_at,
+                                                 unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
+  if (ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0 || ctl[C_BN] != ctl[C_BM]) return;
+  if (small && (small[slot].flags & kSmIn)) return;  // (a small table's order is its model's)
+  const uint32_t lv = mpcap ? (mpcap[slot] & ~kMpInexact) : 0u;
+  if (lv < 3) return;
+  if (*full) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctl[C_TR0], 9ull);
+    return;
+  }
+  const uint64_t bb = ctl[C_BN], gen = cgen[slot];
+  const uint32_t want = cset_meta(slot, 0, gen) & ~(3u << 17);
+  for (uint64_t e = (uint64_t)blockIdx.x * kMwT + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kMwT) {
+    const uint32_t m = set[e].meta;
+    if ((m & ~(3u << 17)) != want) continue;  // another map / generation, or an empty entry
+    const uint32_t kt = (m >> 17) & 3u;
+    const uint64_t k = set[e].key;
+    bool ok;
+    const uint32_t jh = java_key_hash(kt, k, hh_key, hh_val, hh_n, ok);
+    if (!ok) {
+      atomicOr(err, kErrHandleHash);
+      continue;
+    }
+    if ((jh & 127u) != (bb & 127u)) continue;  // not in the bin even at 128 (bins only split further above)
+    if (tbl_bound(word, tkey, map_bits, slot, kt, k)) continue;  // counted among the bound entries
+    const uint64_t cl = set[e].claim;
+    for (uint32_t L = 3; L <= lv && L - 3 < 32; ++L) {
+      const uint64_t mk = (16ull << L) - 1;
+      if ((jh & mk) == (bb & mk) && cl <= lvl_left(lvl_at, slot, L)) atomicAdd(&ctl[C_TR0 + (L - 3)], 1ull);
+    }
+  }
 }
 
 // The barrier row's result (MapState.java :49-60 / :233-239 / :244-250 / :255-261 / :264-274) and the map's
@@ -326,7 +388,7 @@ __global__ void k_mw_size(uint32_t slot, uint32_t op, const unsigned long long* 
 
 __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsigned long long* __restrict__ ctl,
                             uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped,
-                            unsigned long long* __restrict__ tdrop, uint8_t* __restrict__ out_status,
+                            uint8_t* __restrict__ out_status,
                             uint64_t* __restrict__ out_value, const SmallMap* __restrict__ small, uint32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
   const uint64_t pres = ctl[C_PRES];
@@ -349,16 +411,20 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
       } else {  // the first of (null, match) in HashMap iteration order
         const uint64_t bn = ctl[C_BN], bm = ctl[C_BM];
         npe = bn != bm ? bn < bm : ctl[C_IN] < ctl[C_IM];
-        if (bn == bm) {  // decided inside one bin: by insertion order, unless that bin was ever a tree bin
+        if (bn == bm) {  // decided inside one bin: by the bin's chain order
           bool tree = false;
-          // (a tree bin needs 9 keys in the bin at once since the last clear, which wipes every bin: the bin's
-          // bound keys plus the keys compacted away since that clear bound them)
           if (small) {
             const SmallMap& sm = small[slot];
-            tree = ((sm.flags & kSmTree) && ((sm.tree_bins >> (bn & 63u)) & 1ull)) ||
-                   ((sm.flags & kSmUnknown) && ctl[C_USED] + tdrop[slot] >= 9);
+            if (sm.flags & kSmIn) {
+              tree = (sm.flags & kSmAmbig) != 0;  // the chain read from the map's HashMap model (k_mw_order)
+            } else {  // a bin that was a tree bin while the table was small (mod 64)
+              tree = ((sm.flags & kSmTree) && ((sm.tree_bins >> (bn & 63u)) & 1ull)) || (sm.flags & kSmUnknown);
+            }
           }
-          for (int q = 0; q < 32; ++q) tree |= ctl[C_TR0 + q] + tdrop[slot] >= 9;
+          // above capacity 64: creation order unless the bin could have been a tree bin, which needs 9 keys in it at
+          // once since the last clear (that wipes every bin); the bin's distinct keys since then are at most its
+          // bound keys plus the keys compacted away (k_mw_order pass 1, k_mw_cset)
+          for (int q = 0; q < 32; ++q) tree |= ctl[C_TR0 + q] >= 9;
           if (tree) atomicOr(err, kErrMapOrder);
         }
       }
@@ -371,8 +437,7 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
       break;
     }
     default:  // clear / Delete: every entry is dropped; the keys they held count toward the peak bound; no bin is left
-      dropped[slot] += ctl[C_USED];
-      tdrop[slot] = 0;
+      dropped[slot] += ctl[C_USED];  // (k_map_drop moves the map's generation on: its compacted keys stop counting)
       break;
   }
   if (pres > peak_lo[slot]) peak_lo[slot] = (uint32_t)min(pres, (uint64_t)0xFFFFFFFFu);
@@ -459,13 +524,19 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
       hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.tbl_dl,
                          a.fire_clock, a.entries, a.slot, op, atag, apay, a.peak_lo,
                          (const unsigned long long*)a.dropped, a.mpcap, a.msize != nullptr, a.small, a.hh_key, a.hh_val,
-                         a.hh_n, pass, a.ctl, a.err);
+                         a.hh_n, pass, a.tbl_claim, a.lvl_at, a.ctl, a.err);
+    if (a.cset) {
+      const uint32_t cg = (uint32_t)std::min<uint64_t>(2048, (a.cset_n + kMwT - 1) / kMwT);
+      hipLaunchKernelGGL(k_mw_cset, dim3(cg), dim3(kMwT), 0, st, a.cset, a.cset_n, a.cset_full, a.cgen, a.slot, a.tbl_word,
+                         a.tbl_key, a.map_bits, a.mpcap, a.small, a.hh_key, a.hh_val, a.hh_n, a.lvl_at, a.ctl, a.err);
+    }
   }
   if (a.msize) hipLaunchKernelGGL(k_mw_size, dim3(1), dim3(64), 0, st, a.slot, op, a.ctl, a.msize, a.err);
   hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,
-                     (unsigned long long*)a.dropped, (unsigned long long*)a.tdrop, a.out_status, a.out_value, a.small, a.err);
+                     (unsigned long long*)a.dropped, a.out_status, a.out_value, a.small, a.err);
   if (hipGetLastError() != hipSuccess) return -1;
-  if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE) return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, st);
+  if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE)
+    return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, a.cgen, st);
   return 0;
 }
 
@@ -658,20 +729,24 @@ __global__ __launch_bounds__(kMszScanW * kWave) void k_msize_scan(const uint8_t*
   clv[w][l] = lv;
   lds_barrier();
   for (int q = 0; q < kMszScanW; ++q) lv = max(lv, clv[q][l]);
-  // tiles that may cross a resize threshold above lv: replayed by k_msize_exact
+  // tiles that may cross a resize threshold above the level proven before them: replayed by k_msize_exact, which
+  // also records where each resize happened (the capacity-level timeline of the tree-bin test, common.h)
   uint32_t inexact = 0;
   if (ok) {
     int64_t s = start;
-    const uint64_t hi_ok = 12ull << lv;  // level(p) <= lv  <=>  p <= 12 << lv
+    uint32_t lr = mp & ~kMpInexact;  // the level proven at this chunk's start: before the sub-batch, and earlier chunks
+    for (uint32_t q = 0; q < w; ++q) lr = max(lr, clv[q][l]);
 #pragma unroll 8
     for (uint32_t t = t0; t < t1; ++t) {
       const uint32_t x = c[(uint64_t)t * R];
-      if ((uint64_t)(s + (x & 0xFFFFu)) > hi_ok) {
+      if ((uint64_t)(s + (x & 0xFFFFu)) > (12ull << lr)) {  // level(p) <= lr  <=>  p <= 12 << lr
         const uint32_t k = atomicAdd(list_n, 1u);
         if (k < kMszListCap) list[k] = make_uint4(t, m, (uint32_t)s, 0u);
         else inexact = kMpInexact;
       }
-      s += msz_net(x);
+      const int64_t fin = s + msz_net(x);
+      if (x) lr = max(lr, cap_level((uint64_t)max(s, fin)));
+      s = fin;
     }
   }
   lds_barrier();  // every lane read clv
@@ -692,7 +767,9 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
                                                       const uint32_t* __restrict__ hot_n, const uint32_t* __restrict__ hot_len,
                                                       const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_msz,
                                                       const uint4* __restrict__ list,
-                                                      const uint32_t* __restrict__ list_n, uint32_t* __restrict__ mpcap) {
+                                                      const uint32_t* __restrict__ list_n, uint32_t* __restrict__ mpcap,
+                                                      unsigned long long* __restrict__ lvl_at, const uint64_t* __restrict__ index,
+                                                      uint64_t lo) {
   constexpr int kPer = kTile / kMszT;
   __shared__ int32_t wsum[kMszT / kWave], wmax[kMszT / kWave];
   __shared__ uint32_t pfx[kHotMax + 1];
@@ -714,16 +791,16 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
       }
     }
     lds_barrier();
-    int32_t sum = 0, mx = 0;  // this thread's rows (consecutive, log order): net change, highest running value
-    for (int j = 0; j < kPer; ++j) {
-      const uint64_t r = base + (uint64_t)threadIdx.x * kPer + j;
-      if (r >= rows) break;
+    // the size change of this thread's j-th row (consecutive rows, log order): +1 insert, -1 removal, 0 other
+    auto delta = [&](int j, uint64_t& r) -> int32_t {
+      r = base + (uint64_t)threadIdx.x * kPer + j;
+      if (r >= rows) return 0;
       const uint32_t p = cpos[r];
-      if (p < b0 || p >= b1) continue;  // unknown session (0xFFFF) or not a map record
+      if (p < b0 || p >= b1) return 0;  // unknown session (0xFFFF) or not a map record
       uint32_t code;
       if (p < bh) {  // a region record
         const uint32_t x = msz[base + p];
-        if ((x >> 2) != m) continue;
+        if ((x >> 2) != m) return 0;
         code = x & 3u;
       } else {  // a hot key's record: its bucket (the last hot bucket starting at or before p), list position
         uint32_t a = 0, b = nh;
@@ -731,11 +808,15 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
           const uint32_t c = (a + b) >> 1;
           if (hb[c] <= p) a = c; else b = c;
         }
-        if (hslot[a] != m) continue;
+        if (hslot[a] != m) return 0;
         code = hot_code(hot_msz, pfx, a, hlp[a] + (p - hb[a]));
       }
-      if (!code) continue;
-      sum += code == 1u ? 1 : -1;
+      return code == 1u ? 1 : code == 2u ? -1 : 0;
+    };
+    int32_t sum = 0, mx = 0;  // this thread's rows: net change, highest running value
+    for (int j = 0; j < kPer; ++j) {
+      uint64_t r;
+      sum += delta(j, r);
       mx = max(mx, sum);
     }
     int32_t inc = sum;
@@ -758,6 +839,20 @@ __global__ __launch_bounds__(kMszT) void k_msize_exact(const uint16_t* __restric
       }
       atomicMax(&mpcap[m], cap_level((uint64_t)e.z + (uint64_t)peak));
     }
+    if (lvl_at && index && mx > 0) {  // rows that raise the running peak: the log index of each resize (timeline)
+      int64_t sz = (int64_t)e.z + (inc - sum);  // this thread's start size
+      for (uint32_t q = 0; q < w; ++q) sz += wsum[q];
+      int64_t pk = sz;
+      for (int j = 0; j < kPer; ++j) {
+        uint64_t r;
+        sz += delta(j, r);
+        if (sz > pk) {
+          if (cap_level((uint64_t)sz) > cap_level((uint64_t)max<int64_t>(pk, 0)))
+            lvl_reached(lvl_at, m, cap_level((uint64_t)max<int64_t>(pk, 0)), cap_level((uint64_t)sz), index[lo + r]);
+          pk = sz;
+        }
+      }
+    }
     lds_barrier();  // wsum / wmax are rewritten by the next item
   }
 }
@@ -772,7 +867,8 @@ int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,
                      a.res_type, a.max_resources, a.tiles, a.tcnt, a.msize, a.mpcap, a.list, a.list_n);
   hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.sb_hot,
-                     a.rst_msz, a.hot, a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.list, a.list_n, a.mpcap);
+                     a.rst_msz, a.hot, a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.list, a.list_n, a.mpcap, a.lvl_at,
+                     a.index, a.lo);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1,0 +1,433 @@
+// small_jhm.h — java.util.HashMap (JDK 8) of a map whose table is still small (capacity <= 64), node for node, on
+// the device.  MapState keeps its entries in a `new HashMap<>()` (collections/src/main/java/io/atomix/collections/
+// state/MapState.java:33) and containsValue (:49-60) walks map.values(): when a stored null and a match share a bin
+// the first of them in the bin's chain decides (NullPointerException or true).  A list bin's chain is its
+// nodes in creation order, but at capacity 64 a bin whose chain reaches 9 nodes becomes a red-black tree bin
+// (HashMap.treeifyBin), whose chain order is the tree's: the root first (moveRootToFront), each later node linked
+// after its tree parent (putTreeVal), nodes unlinked by removeTreeNode, the bin turned back into a list (untreeify)
+// when a removal leaves the tree too small.  The engine follows all of that here, so an order-dependent
+// containsValue on a small map is answered exactly, tree bins included.
+//
+// The structure restates the published JDK 8 algorithm (java.util.HashMap is a JDK class, not part of
+// /root/reference; the oracle's JHM, oracle/oracle.cpp, is the CPU restatement it is checked against):
+//   put:    putVal — an empty bin takes the node; a tree bin putTreeVal (by hash as a signed int: the keys' own
+//           compareTo is needed only for equal hashes); a list bin appends, and a chain of >= 9 calls treeifyBin
+//           (resize() below capacity 64, else treeify); then ++size > threshold resizes;
+//   remove: removeNode(movable = true) — MapState.remove / removeIfPresent and the TTL timer call map.remove(key);
+//   resize: lists split in order (a tree bin exists only at 64, and a table of 128 leaves this window).
+// Keys are known by their HashMap hash only (the events of map_small.hip): two live keys with one hash make the
+// map's order unknown to the engine (kSmAmbig; an order-dependent answer then fails with CC_ERR_STATE).
+#pragma once
+#include "common.h"
+
+namespace cc {
+
+struct SmallJhm {
+  SmallMap& s;
+  __device__ explicit SmallJhm(SmallMap& m) : s(m) {}
+
+  __device__ uint32_t cap() const { return 16u << s.lvl; }
+  __device__ bool tree(uint32_t x) const { return s.nb[x - 1] & 1u; }
+  __device__ bool red(uint32_t x) const { return x && (s.nb[x - 1] & 2u); }
+  __device__ void set_red(uint32_t x, bool r) { s.nb[x - 1] = (uint8_t)((s.nb[x - 1] & ~2u) | (r ? 2u : 0u)); }
+  // links are node + 1 (0: null)
+  __device__ uint32_t next(uint32_t x) const { return s.nx[x - 1]; }
+  __device__ uint32_t prev(uint32_t x) const { return s.pv[x - 1]; }
+  __device__ uint32_t par(uint32_t x) const { return s.pa[x - 1]; }
+  __device__ uint32_t left(uint32_t x) const { return s.lf[x - 1]; }
+  __device__ uint32_t right(uint32_t x) const { return s.rt[x - 1]; }
+  __device__ void set_next(uint32_t x, uint32_t v) { s.nx[x - 1] = (uint8_t)v; }
+  __device__ void set_prev(uint32_t x, uint32_t v) { s.pv[x - 1] = (uint8_t)v; }
+  __device__ void set_par(uint32_t x, uint32_t v) { s.pa[x - 1] = (uint8_t)v; }
+  __device__ void set_left(uint32_t x, uint32_t v) { s.lf[x - 1] = (uint8_t)v; }
+  __device__ void set_right(uint32_t x, uint32_t v) { s.rt[x - 1] = (uint8_t)v; }
+  __device__ uint32_t hash(uint32_t x) const { return s.jh[x - 1]; }
+
+  __device__ uint32_t alloc(uint32_t h) {
+    const uint64_t free = ~s.used;
+    if (!free) {
+      s.flags |= kSmAmbig;  // (cannot happen: a table of 64 holds at most 49 nodes for a moment)
+      return 0;
+    }
+    const uint32_t i = (uint32_t)__builtin_ctzll(free);
+    s.used |= 1ull << i;
+    s.jh[i] = h;
+    s.nx[i] = s.pv[i] = s.pa[i] = s.lf[i] = s.rt[i] = 0;
+    s.nb[i] = 0;
+    return i + 1;
+  }
+  __device__ void release(uint32_t x) { s.used &= ~(1ull << (x - 1)); }
+
+  // putTreeVal's direction: the hash as a signed int (an equal hash needs the keys' compareTo: unknown here)
+  __device__ int dir_of(uint32_t h, uint32_t p) {
+    const int32_t ph = (int32_t)hash(p), hh = (int32_t)h;
+    if (ph > hh) return -1;
+    if (ph < hh) return 1;
+    s.flags |= kSmAmbig;
+    return 1;
+  }
+  __device__ uint32_t root_of(uint32_t p) const {
+    while (par(p)) p = par(p);
+    return p;
+  }
+  __device__ uint32_t rotate_left(uint32_t root, uint32_t p) {
+    uint32_t r, pp, rl;
+    if (p && (r = right(p))) {
+      rl = left(r);
+      set_right(p, rl);
+      if (rl) set_par(rl, p);
+      pp = par(p);
+      set_par(r, pp);
+      if (!pp) root = r, set_red(r, false);
+      else if (left(pp) == p) set_left(pp, r);
+      else set_right(pp, r);
+      set_left(r, p);
+      set_par(p, r);
+    }
+    return root;
+  }
+  __device__ uint32_t rotate_right(uint32_t root, uint32_t p) {
+    uint32_t l, pp, lr;
+    if (p && (l = left(p))) {
+      lr = right(l);
+      set_left(p, lr);
+      if (lr) set_par(lr, p);
+      pp = par(p);
+      set_par(l, pp);
+      if (!pp) root = l, set_red(l, false);
+      else if (right(pp) == p) set_right(pp, l);
+      else set_left(pp, l);
+      set_right(l, p);
+      set_par(p, l);
+    }
+    return root;
+  }
+  __device__ uint32_t balance_insertion(uint32_t root, uint32_t x) {
+    set_red(x, true);
+    for (uint32_t xp, xpp, xppl, xppr;;) {
+      if (!(xp = par(x))) {
+        set_red(x, false);
+        return x;
+      }
+      if (!red(xp) || !(xpp = par(xp))) return root;
+      if (xp == (xppl = left(xpp))) {
+        if ((xppr = right(xpp)) && red(xppr)) {
+          set_red(xppr, false), set_red(xp, false), set_red(xpp, true), x = xpp;
+        } else {
+          if (x == right(xp)) {
+            root = rotate_left(root, x = xp);
+            xpp = (xp = par(x)) ? par(xp) : 0;
+          }
+          if (xp) {
+            set_red(xp, false);
+            if (xpp) set_red(xpp, true), root = rotate_right(root, xpp);
+          }
+        }
+      } else {
+        if (xppl && red(xppl)) {
+          set_red(xppl, false), set_red(xp, false), set_red(xpp, true), x = xpp;
+        } else {
+          if (x == left(xp)) {
+            root = rotate_right(root, x = xp);
+            xpp = (xp = par(x)) ? par(xp) : 0;
+          }
+          if (xp) {
+            set_red(xp, false);
+            if (xpp) set_red(xpp, true), root = rotate_left(root, xpp);
+          }
+        }
+      }
+    }
+  }
+  __device__ uint32_t balance_deletion(uint32_t root, uint32_t x) {
+    for (uint32_t xp, xpl, xpr;;) {
+      if (!x || x == root) return root;
+      if (!(xp = par(x))) {
+        set_red(x, false);
+        return x;
+      }
+      if (red(x)) {
+        set_red(x, false);
+        return root;
+      }
+      if ((xpl = left(xp)) == x) {
+        if (red(xpr = right(xp))) {
+          set_red(xpr, false), set_red(xp, true);
+          root = rotate_left(root, xp);
+          xpr = (xp = par(x)) ? right(xp) : 0;
+        }
+        if (!xpr) {
+          x = xp;
+        } else {
+          uint32_t sl = left(xpr), sr = right(xpr);
+          if (!red(sr) && !red(sl)) {
+            set_red(xpr, true), x = xp;
+          } else {
+            if (!red(sr)) {
+              if (sl) set_red(sl, false);
+              set_red(xpr, true);
+              root = rotate_right(root, xpr);
+              xpr = (xp = par(x)) ? right(xp) : 0;
+            }
+            if (xpr) {
+              set_red(xpr, xp ? red(xp) : false);
+              if ((sr = right(xpr))) set_red(sr, false);
+            }
+            if (xp) set_red(xp, false), root = rotate_left(root, xp);
+            x = root;
+          }
+        }
+      } else {
+        if (red(xpl)) {
+          set_red(xpl, false), set_red(xp, true);
+          root = rotate_right(root, xp);
+          xpl = (xp = par(x)) ? left(xp) : 0;
+        }
+        if (!xpl) {
+          x = xp;
+        } else {
+          uint32_t sl = left(xpl), sr = right(xpl);
+          if (!red(sl) && !red(sr)) {
+            set_red(xpl, true), x = xp;
+          } else {
+            if (!red(sl)) {
+              if (sr) set_red(sr, false);
+              set_red(xpl, true);
+              root = rotate_left(root, xpl);
+              xpl = (xp = par(x)) ? left(xp) : 0;
+            }
+            if (xpl) {
+              set_red(xpl, xp ? red(xp) : false);
+              if ((sl = left(xpl))) set_red(sl, false);
+            }
+            if (xp) set_red(xp, false), root = rotate_right(root, xp);
+            x = root;
+          }
+        }
+      }
+    }
+  }
+  __device__ void to_front(uint32_t root) {  // moveRootToFront
+    if (!root) return;
+    const uint32_t index = (cap() - 1) & hash(root);
+    const uint32_t first = s.tab[index];
+    if (root == first) return;
+    s.tab[index] = (uint8_t)root;
+    const uint32_t rp = prev(root), rn = next(root);
+    if (rn) set_prev(rn, rp);
+    if (rp) set_next(rp, rn);
+    if (first) set_prev(first, root);
+    set_next(root, first);
+    set_prev(root, 0);
+  }
+  __device__ void treeify(uint32_t hd) {
+    uint32_t root = 0;
+    for (uint32_t x = hd, nxt; x; x = nxt) {
+      nxt = next(x);
+      set_left(x, 0), set_right(x, 0);
+      if (!root) {
+        set_par(x, 0), set_red(x, false), root = x;
+        continue;
+      }
+      for (uint32_t p = root;;) {
+        const int dir = dir_of(hash(x), p);
+        const uint32_t xp = p;
+        if (!(p = dir <= 0 ? left(p) : right(p))) {
+          set_par(x, xp);
+          if (dir <= 0) set_left(xp, x);
+          else set_right(xp, x);
+          root = balance_insertion(root, x);
+          break;
+        }
+      }
+    }
+    to_front(root);
+  }
+  __device__ uint32_t untreeify(uint32_t hd) {
+    for (uint32_t q = hd; q; q = next(q)) {
+      s.nb[q - 1] = 0;
+      set_par(q, 0), set_left(q, 0), set_right(q, 0), set_prev(q, 0);
+    }
+    return hd;
+  }
+  // resize (the window holds list bins only below 64, where nothing is a tree): chains split in order; a table of
+  // 128 leaves the window (returns false)
+  __device__ bool resize() {
+    const uint32_t old = cap();
+    if (s.lvl + 1 >= 3u) {
+      ++s.lvl;
+      s.flags &= ~kSmIn;
+      return false;
+    }
+    ++s.lvl;
+    // in place: bins [old, 2 old) are unused at the old capacity, and bin j splits into j and j + old only
+    for (uint32_t j = 0; j < old; ++j) {
+      uint32_t lo = 0, lot = 0, hi = 0, hit = 0;
+      for (uint32_t q = s.tab[j], nxt; q; q = nxt) {
+        nxt = next(q);
+        set_next(q, 0);
+        if ((hash(q) & old) == 0) {
+          if (lot) set_next(lot, q); else lo = q;
+          lot = q;
+        } else {
+          if (hit) set_next(hit, q); else hi = q;
+          hit = q;
+        }
+      }
+      s.tab[j] = (uint8_t)lo;
+      s.tab[j + old] = (uint8_t)hi;
+    }
+    return true;
+  }
+  __device__ bool treeify_bin(uint32_t h) {
+    if (cap() < 64) return resize();  // MIN_TREEIFY_CAPACITY: resize instead
+    const uint32_t index = (cap() - 1) & h;
+    uint32_t tl = 0;
+    for (uint32_t q = s.tab[index]; q; q = next(q)) s.nb[q - 1] |= 1u, set_prev(q, tl), tl = q;
+    if (s.tab[index]) treeify(s.tab[index]);
+    s.flags |= kSmTree;
+    s.tree_bins |= 1ull << (index & 63u);
+    return true;
+  }
+  // putVal of a new key (an existing key's put changes no structure); false: the map left the window
+  __device__ bool put(uint32_t h) {
+    const uint32_t i = (cap() - 1) & h;
+    uint32_t p = s.tab[i];
+    if (!p) {
+      const uint32_t x = alloc(h);
+      s.tab[i] = (uint8_t)x;
+    } else if (tree(p)) {  // putTreeVal: linked after its tree parent, then the root moves to the front
+      const uint32_t root = root_of(p);
+      for (uint32_t q = root;;) {
+        const int dir = dir_of(h, q);
+        const uint32_t xp = q;
+        if (!(q = dir <= 0 ? left(q) : right(q))) {
+          const uint32_t xpn = next(xp), x = alloc(h);
+          if (!x) return true;
+          s.nb[x - 1] = 1u;
+          set_next(x, xpn);
+          if (dir <= 0) set_left(xp, x);
+          else set_right(xp, x);
+          set_next(xp, x);
+          set_par(x, xp), set_prev(x, xp);
+          if (xpn) set_prev(xpn, x);
+          to_front(balance_insertion(root, x));
+          break;
+        }
+      }
+    } else {
+      uint32_t bin = 0;
+      while (next(p)) p = next(p), ++bin;
+      const uint32_t x = alloc(h);
+      set_next(p, x);
+      if (bin >= 7u && !treeify_bin(h)) return false;  // the chain now holds >= 9 nodes
+    }
+    if (++s.n > (12u << s.lvl)) return resize();  // ++size > threshold
+    return true;
+  }
+  __device__ void remove_tree_node(uint32_t self, uint32_t index) {  // TreeNode.removeTreeNode(map, tab, movable = true)
+    uint32_t first = s.tab[index], root = first, rl;
+    const uint32_t succ = next(self), pred = prev(self);
+    if (!pred) s.tab[index] = (uint8_t)(first = succ);
+    else set_next(pred, succ);
+    if (succ) set_prev(succ, pred);
+    if (!first) return;
+    if (par(root)) root = root_of(root);
+    if (!right(root) || !(rl = left(root)) || !left(rl)) {
+      s.tab[index] = (uint8_t)untreeify(first);  // too small
+      return;
+    }
+    const uint32_t p = self, pl = left(p), pr = right(p);
+    uint32_t replacement;
+    if (pl && pr) {
+      uint32_t sx = pr, sl;
+      while ((sl = left(sx))) sx = sl;  // successor
+      const bool c = red(sx);
+      set_red(sx, red(p));
+      set_red(p, c);
+      const uint32_t sr = right(sx), pp = par(p);
+      if (sx == pr) {
+        set_par(p, sx);
+        set_right(sx, p);
+      } else {
+        const uint32_t sp = par(sx);
+        set_par(p, sp);
+        if (sp) {
+          if (sx == left(sp)) set_left(sp, p);
+          else set_right(sp, p);
+        }
+        set_right(sx, pr);
+        if (pr) set_par(pr, sx);
+      }
+      set_left(p, 0);
+      set_right(p, sr);
+      if (sr) set_par(sr, p);
+      set_left(sx, pl);
+      if (pl) set_par(pl, sx);
+      set_par(sx, pp);
+      if (!pp) root = sx;
+      else if (p == left(pp)) set_left(pp, sx);
+      else set_right(pp, sx);
+      replacement = sr ? sr : p;
+    } else {
+      replacement = pl ? pl : (pr ? pr : p);
+    }
+    if (replacement != p) {
+      const uint32_t pp = par(p);
+      set_par(replacement, pp);
+      if (!pp) root = replacement;
+      else if (p == left(pp)) set_left(pp, replacement);
+      else set_right(pp, replacement);
+      set_left(p, 0), set_right(p, 0), set_par(p, 0);
+    }
+    const uint32_t r = red(p) ? root : balance_deletion(root, replacement);
+    if (replacement == p) {  // detach
+      const uint32_t pp = par(p);
+      set_par(p, 0);
+      if (pp) {
+        if (p == left(pp)) set_left(pp, 0);
+        else if (p == right(pp)) set_right(pp, 0);
+      }
+    }
+    to_front(r);
+  }
+  // removeNode(movable = true) of the live key with hash h
+  __device__ void remove(uint32_t h) {
+    const uint32_t index = (cap() - 1) & h;
+    uint32_t node = 0, prv = 0, pp = 0;
+    for (uint32_t q = s.tab[index]; q; pp = q, q = next(q))
+      if (hash(q) == h) {
+        if (node) {  // two live keys with one hash: which one left is unknown here
+          s.flags |= kSmAmbig;
+          break;
+        }
+        node = q, prv = pp;
+      }
+    if (!node) {
+      s.flags |= kSmAmbig;  // (a removal of a key this model does not hold: its order is no longer known)
+      return;
+    }
+    if (tree(node)) remove_tree_node(node, index);
+    else if (!prv) s.tab[index] = (uint8_t)next(node);
+    else set_next(prv, next(node));
+    release(node);
+    --s.n;
+  }
+};
+
+// The position of the live key with hash h in its bin's chain (iteration order inside the bin); dup: another live
+// key of the bin has the same hash (the order between the two is unknown here).
+__device__ inline uint32_t small_chain_pos(const SmallMap& s, uint32_t h, bool& dup) {
+  const uint32_t index = ((16u << s.lvl) - 1u) & h;
+  uint32_t pos = 0, found = ~0u, steps = 0;
+  dup = false;
+  for (uint32_t q = s.tab[index]; q && steps < kSmNodes; q = s.nx[q - 1], ++steps, ++pos)
+    if (s.jh[q - 1] == h) {
+      if (found != ~0u) dup = true;
+      else found = pos;
+    }
+  if (found == ~0u) dup = true;  // (not in the model: unknown)
+  return found;
+}
+
+}  // namespace cc

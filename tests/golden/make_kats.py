@@ -16,6 +16,10 @@ Run: python tests/golden/make_kats.py  (deterministic; the JSON is committed)
 """
 import json
 import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from java_hashmap import MapStateModel  # noqa: E402  (tests/java_hashmap.py)
 
 STRINGS = {}
 
@@ -365,8 +369,49 @@ def kats():
         kat.c(0, "MAP_PUT", key=k, a=NULL if i == 0 else L(7) if i == 3 else L(100 + i))
     kat.c(0, "MAP_CONTAINSVALUE", a=L(7), expect=B(True))
     kat.c(0, "MAP_CONTAINSVALUE", a=L(8), status="NULL_POINTER")
-    kat.d["gpu"] = "refuses"  # the engine does not order tree bins: an order-dependent answer fails (CC_ERR_STATE)
     out.append(kat)
+
+    # More tree bins, with the expected answers computed by tests/java_hashmap.py (an independent Python restatement of
+    # the JDK 8 HashMap, cross-checked against the oracle's JHM by tests/test_oracle_hashmap.py): every value is
+    # queried, so each answer pins the chain order of its key against the null's.
+    def tree_kat(name, ops, refuses=False):
+        kat = K(name, "quirk", f"{MS}:49-60,89-110,138-154").res(0, "MAP").inst(0, 0, 100, 1)
+        model = MapStateModel()
+        for op in ops:
+            if op[0] == "put":
+                prev = model.put((1, op[1]), op[2])
+                kat.c(0, "MAP_PUT", key=L(op[1]), a=NULL if op[2] is None else L(op[2]),
+                      expect=NULL if prev is None else L(prev))
+            elif op[0] == "remove":
+                prev = model.remove((1, op[1]))
+                kat.c(0, "MAP_REMOVE", key=L(op[1]), expect=NULL if prev is None else L(prev))
+            else:  # query every stored value and one absent value
+                for v in sorted({x for x in model.vals.values() if x is not None}) + [999_999]:
+                    r = model.contains_value(v)
+                    if r == "NPE":
+                        kat.c(0, "MAP_CONTAINSVALUE", a=L(v), status="NULL_POINTER")
+                    else:
+                        kat.c(0, "MAP_CONTAINSVALUE", a=L(v), expect=B(r))
+        if refuses:
+            kat.d["gpu"] = "refuses"
+        out.append(kat)
+
+    kt = [i * (1 << 22) + 5 for i in range(16)]  # one bin (5) at every capacity <= 64
+    # putTreeVal after the treeify (keys 11..13 linked after their tree parents), the null in the middle
+    tree_kat("A5_tree_bin_put_after_treeify",
+             [("put", k, None if i == 5 else 200 + i) for i, k in enumerate(kt[:14])] + [("query",)])
+    # removeTreeNode (the root among them), then removals until the tree is too small and turns back into a list
+    tree_kat("A5_tree_bin_remove_and_untreeify",
+             [("put", k, None if i == 9 else 300 + i) for i, k in enumerate(kt[:13])] + [("query",)] +
+             [("remove", kt[i]) for i in (3, 0, 7)] + [("query",)] +
+             [("remove", kt[i]) for i in (1, 2, 4, 5, 6, 8)] + [("query",)] +
+             [("put", kt[13], 413), ("put", kt[3], 403)] + [("query",)])
+    # the tree bin's table grows past 64 (49 keys): its halves split off the tree order at 128, which the engine no
+    # longer follows -- an order-dependent answer inside that bin fails loudly there
+    others = [k for k in range(3000, 3200) if k % 64 != 5][:40]
+    tree_kat("A5_tree_bin_leaves_small_window",
+             [("put", k, None if i == 0 else 500 + i) for i, k in enumerate(kt[:11])] +
+             [("put", k, 600 + j) for j, k in enumerate(others)] + [("query",)], refuses=True)
     out.append(K("A6_null_value_is_present", "quirk", f"{MS}:115-133,38-44,65-72")
                .res(0, "MAP").inst(0, 0, 100, 1)
                .c(0, "MAP_PUT", key=foo, a=NULL)
