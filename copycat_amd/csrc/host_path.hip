@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include <unordered_map>
+
 #include "engine_state.h"
 
 namespace {
@@ -162,6 +164,150 @@ extern "C" int cc_apply_batch_host_events(cc_engine* e, const cc_batch* h_cols, 
                                           const cc_events* h_events) {
   if (!h_events) return set_err(CC_ERR_INVALID, "null event stream (use cc_apply_batch_host)");
   return apply_host(e, h_cols, n, h_out, h_events);
+}
+
+// ---- a batch applied up to the first commit the engine cannot hold (ABI 5) ------------------------------------------
+// Java's collections are unbounded (LockState's ArrayDeque, LeaderElectionState's LinkedHashMap, MembershipGroupState's
+// HashMap, QueueState, AtomicValueState's listeners: LockState.java:35, ...); the engine's coordination blocks hold
+// coord_cap entries.  cc_apply_batch fails such a batch after applying it (CC_ERR_CAPACITY).  This call instead applies
+// exactly the rows before the first commit that would overflow a collection and reports them: *applied = that row
+// (n when every row applied), the state is the one after rows [0, *applied), and the row itself and every row after
+// it are not applied (their results are not written), so the host can act (a larger engine from a snapshot, or the
+// commit failed) and resume at that row.
+//   1. Rows that can add an entry (lock with a timeout != 0, election listen, group join, value listen, queue
+//      add / offer) are counted per resource on the host (the registry mirror); a resource whose current entries
+//      plus those rows fit its block cannot overflow, and if every one fits the batch is applied as one call.
+//   2. Otherwise the rows before the first one that could overflow (running count > room) go as one call, and that
+//      row alone: if it overflows, its resource block, the clock, the applied index and the pending group timers
+//      are restored (the engine skips the entry it cannot hold, so nothing else moved) and the call stops there.
+// Other fixed capacities (a full map table region, max_events) still fail the call after applying it.
+namespace {
+
+bool adds_entry(uint8_t type, uint8_t op, uint64_t aux) {
+  switch (type) {
+    case CC_RES_LOCK: return op == CC_OP_LOCK_LOCK && aux != 0;  // tryLock() (timeout 0) never queues
+    case CC_RES_ELECTION: return op == CC_OP_ELECT_LISTEN;
+    case CC_RES_GROUP: return op == CC_OP_GROUP_JOIN;
+    case CC_RES_VALUE: return op == CC_OP_VALUE_LISTEN;
+    case CC_RES_QUEUE: return op == CC_OP_QUEUE_ADD || op == CC_OP_QUEUE_OFFER;
+    default: return false;
+  }
+}
+
+// apply host rows [lo, hi) appending to the host event stream `hev` (rows shifted to batch positions); *ev_n = events
+// so far
+int apply_part(cc_engine* e, const cc_batch* h, uint64_t lo, uint64_t hi, const cc_results* hout, const cc_events* hev,
+               uint64_t* ev_n) {
+  auto sh = [lo](const auto* p) { return p ? p + lo : p; };
+  const cc_batch part{sh(h->index), sh(h->time), sh(h->inst), sh(h->op), sh(h->flags), sh(h->key), sh(h->a), sh(h->b),
+                      sh(h->aux)};
+  const cc_results o{hout->status + lo, hout->value + lo};
+  if (!hev) return apply_host(e, &part, hi - lo, &o, nullptr);
+  uint64_t cnt = 0;
+  cc_events v = *hev;
+  const uint64_t k = std::min(*ev_n, hev->capacity);
+  v.pos += k, v.target += k, v.code += k, v.src += k, v.tag += k, v.payload += k;
+  v.capacity -= k;
+  v.count = &cnt;
+  const int rc = apply_host(e, &part, hi - lo, &o, &v);
+  for (uint64_t i = 0; i < std::min(cnt, v.capacity); ++i) v.pos[i] += (uint32_t)lo;
+  *ev_n += cnt;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint64_t n, const cc_results* hout,
+                                          const cc_events* hev, uint64_t* h_applied) {
+  if (!e || !h || !hout || !h_applied || (n && (!h->inst || !h->op))) return set_err(CC_ERR_INVALID, "null argument");
+  if (hev && (!hev->count || (hev->capacity && (!hev->pos || !hev->target || !hev->code || !hev->src || !hev->tag ||
+                                                !hev->payload))))
+    return set_err(CC_ERR_INVALID, "host event stream: null column or count");
+  *h_applied = 0;
+  uint64_t ev_n = 0;
+  auto finish = [&](int rc) {
+    if (hev) *hev->count = ev_n;
+    return rc;
+  };
+  const uint32_t max_inst = e->cfg.max_instances;
+  auto res_of = [&](uint64_t i) -> uint32_t {
+    const uint32_t in = h->inst[i];
+    return in < max_inst ? e->inst_res[in] : kNoRes;
+  };
+  const uint32_t cap = e->coord_cap;
+  const size_t blk = coord_block(cap);
+  auto adds = [&](uint64_t i, uint32_t r) {
+    return r != kNoRes && r < e->res_type.size() && adds_entry(e->res_type[r], h->op[i], h->aux ? h->aux[i] : 0);
+  };
+  auto entries = [&](uint32_t r, uint32_t* out) -> int {  // the block's current entry count (CoordHdr.n)
+    CoordHdr hd{};
+    HIPCHECK(hipMemcpy(&hd, e->d_coord + (uint64_t)r * blk, sizeof hd, hipMemcpyDeviceToHost));
+    *out = hd.n;
+    return CC_OK;
+  };
+  uint64_t pos = 0;
+  while (pos < n) {
+    // the first row at or after pos that could overflow its resource's block (none: the rest applies as one call)
+    uint64_t stop = n;
+    if (e->coord_on) {
+      std::unordered_map<uint32_t, uint64_t> cnt;
+      for (uint64_t i = pos; i < n; ++i) {
+        const uint32_t r = res_of(i);
+        if (adds(i, r)) ++cnt[r];
+      }
+      std::unordered_map<uint32_t, int64_t> room;  // resources that may overflow: entries they can still take
+      for (auto& kv : cnt) {
+        uint32_t cur = 0;
+        int rc = entries(kv.first, &cur);
+        if (rc) return finish(rc);
+        if (cur + kv.second > cap) room[kv.first] = (int64_t)cap - (int64_t)cur;
+      }
+      if (!room.empty())
+        for (uint64_t i = pos; i < n; ++i) {
+          const uint32_t r = res_of(i);
+          auto it = room.find(r);
+          if (it != room.end() && adds(i, r) && --it->second < 0) {
+            stop = i;
+            break;
+          }
+        }
+    }
+    if (stop > pos) {
+      const int rc = apply_part(e, h, pos, stop, hout, hev, &ev_n);
+      if (rc) return finish(rc);
+      pos = stop;
+      *h_applied = pos;
+      continue;
+    }
+    // row `pos` alone: its resource's block, the clock, the applied index and the group timers are saved first
+    const uint32_t r = res_of(pos);
+    std::vector<uint8_t> saved(blk);
+    uint64_t clock = 0, last = 0;
+    HIPCHECK(hipMemcpy(saved.data(), e->d_coord + (uint64_t)r * blk, blk, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&clock, e->d_clock, sizeof clock, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&last, e->d_last_index, sizeof last, hipMemcpyDeviceToHost));
+    const bool pending = e->applied_pending;
+    const auto gtimers = e->gtimers;
+    const uint64_t ev0 = ev_n;
+    const uint8_t st0 = hout->status[pos];
+    const uint64_t va0 = hout->value[pos];
+    const int rc = apply_part(e, h, pos, pos + 1, hout, hev, &ev_n);
+    if (rc == CC_ERR_CAPACITY) {
+      hout->status[pos] = st0;  // (the row is not applied: its result row keeps what the caller had there)
+      hout->value[pos] = va0;
+      HIPCHECK(hipMemcpy(e->d_coord + (uint64_t)r * blk, saved.data(), blk, hipMemcpyHostToDevice));
+      HIPCHECK(hipMemcpy(e->d_clock, &clock, sizeof clock, hipMemcpyHostToDevice));
+      HIPCHECK(hipMemcpy(e->d_last_index, &last, sizeof last, hipMemcpyHostToDevice));
+      e->applied_pending = pending;
+      e->gtimers = gtimers;
+      ev_n = ev0;
+      return finish(set_err(CC_ERR_CAPACITY, "a coordination collection is full (coord_cap): *applied rows were applied"));
+    }
+    if (rc) return finish(rc);
+    pos += 1;
+    *h_applied = pos;
+  }
+  return finish(CC_OK);
 }
 
 extern "C" int cc_sessions_close_host(cc_engine* e, const uint64_t* h_clients, uint64_t count, const cc_events* h_events,

@@ -104,6 +104,7 @@ def lib():
             "cc_handle_hashes": (i32, [P, P, P, u64]),
             "cc_wire_decode": (i32, [P, P, P, P, u64, P, u64, P, P]),
             "cc_split_batch": (i32, [P, u64, P, u32, u32, u32, P, P, P, P]),
+            "cc_apply_batch_host_prefix": (i32, [P, P, u64, P, P, P]),
             "cc_merge_results": (i32, [P, u64, P, u32, u32, u32, P, P]),
         }
         for name, (res, args) in sig.items():
@@ -343,6 +344,30 @@ class Engine:
         r = abi.cc_results(status.ctypes.data, value.ctypes.data)
         _check(self.L.cc_apply_batch_host(self.h, C.byref(s), n, C.byref(r)))
         return status, value
+
+    def apply_host_prefix(self, b: Batch, capacity=None):
+        """cc_apply_batch_host_prefix: rows applied up to the first commit a full coordination collection cannot hold.
+        Returns (applied, status, value, events): `applied` = rows applied (len(b) on success; the engine state is the
+        one after exactly those rows), events as apply_host_events returns them (numpy columns)."""
+        n = len(b)
+        status = np.full(n, RESULT_SENTINEL, np.uint8)
+        value = np.zeros(n, np.uint64)
+        s = abi.cc_batch()
+        for name, _ in abi.BATCH_COLUMNS:
+            setattr(s, name, getattr(b, name).ctypes.data)
+        r = abi.cc_results(status.ctypes.data, value.ctypes.data)
+        cap = capacity if capacity is not None else max(4 * n, 1024)
+        cols = {"pos": np.zeros(cap, np.uint32), "target": np.zeros(cap, np.uint32), "code": np.zeros(cap, np.uint8),
+                "src": np.zeros(cap, np.uint8), "tag": np.zeros(cap, np.uint8), "payload": np.zeros(cap, np.uint64)}
+        count = np.zeros(1, np.uint64)
+        ev = abi.cc_events(*(cols[k].ctypes.data for k in ("pos", "target", "code", "src", "tag", "payload")), cap,
+                           count.ctypes.data)
+        applied = C.c_uint64()
+        rc = self.L.cc_apply_batch_host_prefix(self.h, C.byref(s), n, C.byref(r), C.byref(ev), C.byref(applied))
+        if rc not in (abi.CC_OK, abi.CC_ERR_CAPACITY) or (rc == abi.CC_ERR_CAPACITY and applied.value >= n):
+            _check(rc)
+        m = int(min(count[0], cap))
+        return applied.value, status, value, {k: v[:m] for k, v in cols.items()}
 
     def sync(self):
         _check(self.L.cc_sync(self.h))

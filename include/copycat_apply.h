@@ -517,6 +517,17 @@ typedef struct cc_wire_out {
 int  cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* in, const uint8_t* buf, uint64_t buf_len,
                     const uint64_t* offsets, uint64_t n, const cc_wire_out* out, uint64_t* bad_row);
 
+/* ---- a batch applied up to the first commit the engine cannot hold (ABI 5; copycat_amd/csrc/host_path.hip) ----
+ * Java's coordination collections are unbounded; the engine's hold cc_config.coord_cap entries.  Like
+ * cc_apply_batch_host_events (h_events may be NULL), but a row that would add an entry to a full lock queue / listener
+ * list / member set / queue is not applied: the call returns CC_ERR_CAPACITY with *h_applied = that row, the engine
+ * state is exactly the state after rows [0, *h_applied), the events of those rows are in h_events, and rows from
+ * *h_applied on are not applied (their result rows keep what the caller put there).  The host resumes at that row
+ * (e.g. on an engine with a larger coord_cap restored from a snapshot, or treating the commit as failed).  On success
+ * *h_applied = n.  Other fixed capacities (a map table region, max_events) fail the call as cc_apply_batch does. */
+int  cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out,
+                                const cc_events* h_events, uint64_t* h_applied);
+
 /* ---- one global log, many engines (ABI 5; copycat_amd/csrc/split.cpp) -----------------------------
  * The reference multiplexes every resource in one Raft log (ResourceManager.java:37-39,56-72); with one engine per
  * GPU the host splits each committed batch by the rank that owns the row's resource, and merges the per-rank results

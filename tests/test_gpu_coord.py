@@ -326,3 +326,64 @@ def test_more_barrier_rows_than_one_listing_with_events():
     s, v, ev = _check_batch(E, O, b, capacity=4 * n)
     assert ev["pos"].max() >= n // 2  # events of the second call, at their own rows
     _check_state(E, O, [L] * locks)
+
+
+def test_prefix_apply_stops_before_a_full_lock_queue_and_resumes():
+    """cc_apply_batch_host_prefix (ABI 5): a lock queue of coord_cap (64) waiters; the 65th waiter's row is not applied
+    -- the call returns CC_ERR_CAPACITY with applied = that row and the engine in exactly the oracle's state after the
+    rows before it (results, events, lock queues) -- and the host resumes after it (here: the commit failed) to
+    oracle-equal state.  Other locks' traffic runs through the same batch."""
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+
+    R, K = 4, 80  # lock 0 gets 66 lockers; locks 1..3 random traffic
+    max_inst = R * K + 8
+    E = Engine(R, max_inst, 1 << 16, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=1 << 16)
+    O = Oracle(R, max_inst, abi.CC_CFG_TIMERS_DEFERRED)
+    for r in range(R):
+        E.resource_create(r, L)
+        O.resource_create(r, L)
+        for k in range(K):
+            E.instance_open(r * K + k, r, 1000 + r * K + k, 7 + r * K + k)
+            O.instance_open(r * K + k, r, 1000 + r * K + k, 7 + r * K + k)
+    rng = np.random.default_rng(5)
+    rows = [(0, abi.CC_OP_LOCK_LOCK, -1)] + [(k, abi.CC_OP_LOCK_LOCK, -1) for k in range(1, 66)]
+    rows += [(0, abi.CC_OP_LOCK_UNLOCK, 0), (66, abi.CC_OP_LOCK_LOCK, -1), (1, abi.CC_OP_LOCK_UNLOCK, 0)]
+    mixed = []
+    for _ in range(400):  # other locks, interleaved
+        r = int(rng.integers(1, R))
+        k = int(rng.integers(0, 20))
+        mixed.append((r * K + k, abi.CC_OP_LOCK_LOCK if rng.random() < 0.5 else abi.CC_OP_LOCK_UNLOCK,
+                      int(rng.choice([-1, 0, 50]))))
+    allrows = []
+    for i, x in enumerate(rows):
+        allrows.append(x)
+        allrows.extend(mixed[i * 5:(i + 1) * 5])
+    n = len(allrows)
+    b = Batch(n)
+    b.index[:] = np.arange(1, n + 1, dtype=np.uint64)
+    b.time[:] = np.arange(n, dtype=np.uint64)
+    b.inst[:] = [x[0] for x in allrows]
+    b.op[:] = [x[1] for x in allrows]
+    b.aux[:] = np.array([x[2] for x in allrows], np.int64).view(np.uint64)
+    stop = allrows.index((65, abi.CC_OP_LOCK_LOCK, -1))
+    applied, s, v, ev = E.apply_host_prefix(b)
+    assert applied == stop
+    s2, v2 = O.apply(b.slice(0, stop))
+    assert np.array_equal(s[:stop], s2) and np.array_equal(v[:stop], v2)
+    assert np.all(s[stop:] == 0xFF)  # not applied: the rows keep the caller's prefill
+    oe, _, _ = _oracle_events(O)
+    got = _canon(*(ev[k] for k in ("pos", "src", "target", "code", "tag", "payload")))
+    assert got == _canon(oe["pos"], oe["src"], oe["target"], oe["code"], oe["tag"], oe["payload"])
+    _check_state(E, O, [L] * R)
+    assert E.applied_index() == O.applied_index() == stop
+    # resume after the commit the engine could not hold (the host failed it)
+    rest = b.slice(stop + 1, n)
+    applied2, s3, v3, ev3 = E.apply_host_prefix(rest)
+    assert applied2 == len(rest)
+    s4, v4 = O.apply(rest)
+    assert np.array_equal(s3, s4) and np.array_equal(v3, v4)
+    oe = O.take_events()
+    got = _canon(*(ev3[k] for k in ("pos", "src", "target", "code", "tag", "payload")))
+    assert got == _canon(oe["pos"], oe["src"], oe["target"], oe["code"], oe["tag"], oe["payload"])
+    _check_state(E, O, [L] * R)
