@@ -253,7 +253,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           atomicAdd(&dropped[ew[q] & kMwSlotMask], 1ull);
           // the key leaves the table: kept in the compacted-key set of its map (the tree-bin test, map_wide.hip)
           const uint32_t ds = ew[q] & kMwSlotMask;
-          cset_insert(cset, cset_mask, cset_full, ds, (ew[q] >> 17) & 3u, ek[q], cgen[ds], ecl[q]);
+          cset_insert(cset, cset_mask, cset_full, ds, (ew[q] >> 17) & 3u, ek[q], cgen, ecl[q]);
         }
         if ((ew[q] & kMwPresent) && !(ew[q] & kMwDead)) {
           const uint32_t res = ew[q] & kMwSlotMask, kt = (ew[q] >> 17) & 3;

@@ -1,6 +1,7 @@
 // common.h — shared device/host definitions of the MI355X commit-apply engine (gfx950, wave64).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/copycat_apply.h"
@@ -360,12 +361,23 @@ __device__ inline uint32_t cset_meta(uint32_t slot, uint32_t kt, uint64_t gen) {
 }
 // (a key is inserted by the one workgroup compacting its region; a reader racing an insert of another key of the
 // same map may miss a dedupe and add a duplicate: that only over-counts, toward refusing)
+// An entry of a generation its map has left (a clear / Delete since: k_map_drop) is stale and taken over.
 __device__ inline void cset_insert(CsetEnt* __restrict__ set, uint64_t mask, uint32_t* __restrict__ full, uint32_t slot,
-                                   uint32_t kt, uint64_t key, uint64_t gen, uint64_t claim) {
+                                   uint32_t kt, uint64_t key, const uint64_t* __restrict__ cgen, uint64_t claim) {
+  const uint64_t gen = cgen[slot];
   const uint32_t meta = cset_meta(slot, kt, gen);
   uint64_t p = (map_hash(slot, kt, key) ^ (gen * 0x9E3779B97F4A7C15ull)) & mask;
   for (int step = 0; step < 128; ++step, p = (p + 1) & mask) {
     uint32_t m = __atomic_load_n(&set[p].meta, __ATOMIC_RELAXED);
+    if (m != 0u && m != meta && ((m >> 19) & 0xFFFu) != (uint32_t)(cgen[m & kMwSlotMask] & 0xFFFu)) {
+      const uint32_t was = atomicCAS(&set[p].meta, m, meta);  // a stale entry: reused
+      if (was == m) {
+        set[p].key = key;
+        set[p].claim = claim;
+        return;
+      }
+      m = was;
+    }
     if (m == 0u) {
       m = atomicCAS(&set[p].meta, 0u, meta);
       if (m == 0u) {
@@ -389,20 +401,20 @@ __device__ inline void lvl_reached(unsigned long long* __restrict__ lvl_at, uint
                                    uint64_t idx) {
   for (uint32_t L = from + 1; L <= to && L < kLvlSlots; ++L) atomicMin(&lvl_at[(uint64_t)m * kLvlSlots + L], (unsigned long long)idx);
 }
-// Is the key bound in the map table now (an entry of its map and tag, not dead)?  Probes its region from the key's
-// first slot until an empty entry (map_hash: the top map_bits bits pick the region).
-__device__ inline bool tbl_bound(const uint32_t* __restrict__ word, const uint64_t* __restrict__ tkey, uint32_t map_bits,
-                                 uint32_t slot, uint32_t kt, uint64_t key) {
+// The key's entry in the map table (an entry of its map and tag), or ~0 when it has none.  Probes its region from
+// the key's first slot until an empty entry (map_hash: the top map_bits bits pick the region).
+__device__ inline uint64_t tbl_find(const uint32_t* __restrict__ word, const uint64_t* __restrict__ tkey, uint32_t map_bits,
+                                    uint32_t slot, uint32_t kt, uint64_t key) {
   const uint64_t h = map_hash(slot, kt, key);
   const uint64_t base = (h >> (64 - map_bits)) * (uint64_t)kMapRegion;
   const uint32_t ident = (slot & kMwSlotMask) | ((kt & 3u) << 17) | kMwUsed;  // (mw_ident)
   uint32_t p = (uint32_t)h & (kMapRegion - 1);
   for (int step = 0; step < kMapRegion; ++step, p = (p + 1) & (kMapRegion - 1)) {
     const uint32_t w = word[base + p];
-    if (w == 0u) return false;
-    if ((w & kMwIdentMask) == ident && tkey[base + p] == key) return true;
+    if (w == 0u) return ~0ull;
+    if ((w & kMwIdentMask) == ident && tkey[base + p] == key) return base + p;
   }
-  return false;
+  return ~0ull;
 }
 
 // A map's java.util.HashMap while its table is small (capacity <= 64; map_small.hip, small_jhm.h): the nodes of the
@@ -419,11 +431,16 @@ struct SmallMap {
   uint8_t nx[kSmNodes], pv[kSmNodes], pa[kSmNodes], lf[kSmNodes], rt[kSmNodes];  // links: node + 1 (0 = null)
   uint8_t nb[kSmNodes];     // bit 0 TreeNode, bit 1 red
   uint8_t tab[64];          // bin heads: node + 1 (0 = null)
+  // (cold: read only when two live keys share a hash; k_small_replay keeps the part above in LDS, these in HBM)
+  uint64_t key[kSmNodes];   // node: the key (tag in kt), for putTreeVal's compareTo / tieBreakOrder and removeNode
+  uint8_t kt[kSmNodes];
 };
+constexpr uint32_t kSmHotBytes = (uint32_t)offsetof(SmallMap, key);
 constexpr uint32_t kSmIn = 1u;       // the table is still small (capacity <= 64): followed node for node
 constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin since the last clear
 constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (kept for the snapshot format; never set now)
-constexpr uint32_t kSmAmbig = 8u;    // two live keys with one hash (or a key the model does not hold): order unknown
+constexpr uint32_t kSmAmbig = 8u;    // a tree order the engine cannot know (two String keys with one hash in a tree bin;
+                                     // a removal of a key the model does not hold): an order-dependent answer refuses
 // per-map flags of the batch (cc_engine::d_msmall): bit 0 the table is small (events followed key by key), bit 1 the
 // batch asks the map's size / isEmpty (events followed for the in-stream answers); either keeps the map's keys out of
 // hot-key routing, so every such commit is a region record
@@ -455,6 +472,13 @@ __host__ __device__ inline uint32_t cap_level(uint64_t p) {
 // - lo) + 1 for a commit of row `row`, 2 * (b - lo) for boundary b (before row b), code 1 insert / 2 remove, so a
 // radix sort puts each map's commits and expiries in log order.  A sub-batch [lo, hi) owns the boundaries [bl, bh]:
 // bh = hi, bl = lo at the batch start and after a barrier row, lo + 1 after another sub-batch (which owned lo).
+// A map event's payload (map_small.hip), by emission slot: the sorted events carry the slot as their value.
+// aux = the key's HashMap hash for an insertion / removal, the batch row for a size / isEmpty query.
+struct EvPay {
+  uint64_t key;   // the key (its tag in ktag): a small map's model tells keys with one hash apart by them
+  uint32_t aux;
+  uint32_t ktag;
+};
 struct TtlEmit {
   const uint64_t* time;   // the batch's time column (null: the clock is clock_before throughout)
   uint64_t n;             // rows in the batch
@@ -466,6 +490,7 @@ struct TtlEmit {
   uint32_t hh_n;
   uint64_t* ev_key;        // the event buffer shared with launch_map_size's emission (SmallArgs::ev_key / ev_val)
   uint32_t* ev_val;
+  EvPay* ev_pay;
   uint32_t ev_cap;
   uint32_t* ctl;           // ctl[0]: events appended
 };
@@ -496,7 +521,8 @@ __device__ inline void ttl_expiry_event(const TtlEmit& t, uint64_t cb, uint32_t 
   const uint32_t at = atomicAdd(t.ctl, 1u);
   if (at < t.ev_cap) {
     t.ev_key[at] = ((uint64_t)(w & kMwSlotMask) << 44) | ((pos & ((1ull << 40) - 1)) << 4) | 2u;
-    t.ev_val[at] = jh;
+    t.ev_val[at] = at;
+    t.ev_pay[at] = EvPay{key, jh, (w >> 17) & 3u};
   }
 }
 

@@ -98,7 +98,7 @@ static void free_all(cc_engine* e) {
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
-                  e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp,
+                  e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp, e->d_sm_pay,
                   e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -142,10 +142,11 @@ static int ensure_small(cc_engine* e) {
   if (e->d_sm_key && e->sm_cap >= cap) return CC_OK;
   if (cap > 0xFFFFFFFFull) return set_err(CC_ERR_CAPACITY, "map event buffer beyond 2^32 entries");
   if (e->d_sm_key) {  // grown (TTL mode): the counters keep their buffer, the events are rebuilt per sub-batch
-    void* ps[] = {e->d_sm_key, e->d_sm_key2, e->d_sm_val, e->d_sm_val2, e->d_sm_temp};
+    void* ps[] = {e->d_sm_key, e->d_sm_key2, e->d_sm_val, e->d_sm_val2, e->d_sm_temp, e->d_sm_pay};
     for (void* p : ps) (void)hipFree(p);
     e->d_sm_key = e->d_sm_key2 = nullptr;
     e->d_sm_val = e->d_sm_val2 = nullptr;
+    e->d_sm_pay = nullptr;
     e->d_sm_temp = nullptr;
   }
   const size_t tb = std::max<size_t>(small_sort_temp_bytes((uint32_t)cap), 256);
@@ -153,6 +154,7 @@ static int ensure_small(cc_engine* e) {
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_key2, 8 * cap);
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_val, 4 * cap);
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_val2, 4 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->d_sm_pay, sizeof(EvPay) * cap);
   if (x == hipSuccess && !e->d_sm_seg) x = hipMalloc(&e->d_sm_seg, 4ull * (e->cfg.max_resources + 1));
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_temp, tb);
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events", x);
@@ -302,7 +304,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_mw_peak, sizeof(uint32_t) * cfg->max_resources);
     ALLOC(e->d_mw_drop, sizeof(uint64_t) * cfg->max_resources);
     ALLOC(e->d_mw_cgen, sizeof(uint64_t) * cfg->max_resources);
-    e->cset_mask = std::max<uint64_t>(4096, e->map_entries) - 1;  // (map_entries is a power of two)
+    e->cset_mask = std::max<uint64_t>(1u << 16, e->map_entries) - 1;  // (map_entries is a power of two)
     ALLOC(e->d_cset, sizeof(CsetEnt) * (e->cset_mask + 1));
     ALLOC(e->d_cset_full, sizeof(uint32_t));
     ALLOC(e->d_tbl_claim, sizeof(uint64_t) * e->map_entries);
@@ -568,7 +570,13 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
     for (auto& x : sm) x.flags = is_map ? kSmIn : 0u;  // (TTL mode too: its commit + expiry events are replayed)
     dev_copy(e, e->d_msm, sizeof(SmallMap) * first, sm.data(), sizeof(SmallMap) * count);
     dev_fill(e, e->d_msmall, first, is_map ? 1 : 0, count);
-    if (is_map && !e->ttl_live) e->small_live = true;
+    if (is_map && !e->ttl_live) {
+      e->small_live = true;
+      // the count of maps still small (ctl[1], k_small_count) is stale until the next sub-batch's recount: a
+      // nonzero one keeps the small-map events on for that sub-batch even if it emits none
+      const uint32_t pending = 1;
+      dev_copy(e, e->d_sm_ctl, sizeof(uint32_t), &pending, sizeof pending);
+    }
   }
   // fresh state: AtomicValueState() {value = null; current = null}
   dev_fill(e, e->d_val_meta, sizeof(uint32_t) * first, 0, sizeof(uint32_t) * count);
@@ -728,6 +736,7 @@ static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = null
   sa.ev_key2 = e->d_sm_key2;
   sa.ev_val = e->d_sm_val;
   sa.ev_val2 = e->d_sm_val2;
+  sa.ev_pay = e->d_sm_pay;
   sa.cap = (uint32_t)e->sm_cap;
   sa.temp = e->d_sm_temp;
   sa.temp_bytes = e->sm_temp_bytes;
@@ -764,6 +773,7 @@ static TtlEmit ttl_emit_args(const cc_engine* e, const uint64_t* time, uint64_t 
   t.hh_n = e->hh_n;
   t.ev_key = e->d_sm_key;
   t.ev_val = e->d_sm_val;
+  t.ev_pay = e->d_sm_pay;
   t.ev_cap = (uint32_t)e->sm_cap;
   t.ctl = e->d_sm_ctl;
   return t;
@@ -1200,6 +1210,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.hh_n = e->hh_n;
         za.ev_key = e->d_sm_key;
         za.ev_val = e->d_sm_val;
+        za.ev_pay = e->d_sm_pay;
         za.ev_cap = (uint32_t)e->sm_cap;
         za.sm_ctl = e->d_sm_ctl;
         za.map_row = e->d_map_row;
@@ -1250,6 +1261,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           za.hh_n = e->hh_n;
           za.ev_key = e->d_sm_key;
           za.ev_val = e->d_sm_val;
+          za.ev_pay = e->d_sm_pay;
           za.ev_cap = (uint32_t)e->sm_cap;
           za.sm_ctl = e->d_sm_ctl;
         }
@@ -1265,6 +1277,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sz.inst_res = e->d_inst_res;
           sz.ev_key = e->d_sm_key;
           sz.ev_val = e->d_sm_val;
+          sz.ev_pay = e->d_sm_pay;
           sz.cap = (uint32_t)e->sm_cap;
           sz.ctl = e->d_sm_ctl;
           sz.sorted_key = e->d_sm_key2;
@@ -1285,6 +1298,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.ev_key2 = e->d_sm_key2;
           sa.ev_val = e->d_sm_val;
           sa.ev_val2 = e->d_sm_val2;
+          sa.ev_pay = e->d_sm_pay;
           sa.cap = (uint32_t)e->sm_cap;
           sa.temp = e->d_sm_temp;
           sa.temp_bytes = e->sm_temp_bytes;
@@ -2412,6 +2426,10 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   if (e->has_mmaps && (rc = ensure_leak(e, kLeakCap))) return rc;
   e->sessions = std::move(sessions);
   e->small_live = e->map_bits && !e->ttl_live;  // (the next sub-batch recounts the maps still small)
+  if (e->small_live) {  // (ctl[1] nonzero until that recount: see resource creation)
+    const uint32_t pending[2] = {0, 1};
+    HIPCHECK(hipMemcpy(e->d_sm_ctl, pending, sizeof pending, hipMemcpyHostToDevice));
+  }
   {
     std::vector<uint64_t> hk(nh);
     std::vector<int32_t> hv(nh);

@@ -169,7 +169,8 @@ struct MapSizeArgs {
   const int32_t* hh_val;
   uint32_t hh_n;
   uint64_t* ev_key;            // [ev_cap] map << 44 | (index - idx0) << 4 | code
-  uint32_t* ev_val;            // [ev_cap] the key's HashMap hash
+  uint32_t* ev_val;            // [ev_cap] the emission slot (its payload: ev_pay)
+  EvPay* ev_pay;               // [ev_cap] key, tag and HashMap hash
   uint32_t ev_cap;
   uint32_t* sm_ctl;            // [0] events emitted
   const uint32_t* map_row;     // TTL mode: every map's commits emitted, positioned by batch row (common.h TtlEmit)
@@ -181,7 +182,8 @@ struct MapSizeArgs {
 int launch_map_size(const MapSizeArgs& a, hipStream_t st);
 struct SmallArgs {
   uint64_t *ev_key, *ev_key2;  // events and their sorted copy
-  uint32_t *ev_val, *ev_val2;
+  uint32_t *ev_val, *ev_val2;  // emission slots
+  const EvPay* ev_pay;         // payloads by emission slot
   uint32_t cap;
   void* temp;                  // hipcub radix-sort scratch
   size_t temp_bytes;
@@ -217,6 +219,7 @@ struct SizeArgs {
   const uint32_t* inst_res;
   uint64_t* ev_key;
   uint32_t* ev_val;
+  EvPay* ev_pay;
   uint32_t cap;
   uint32_t* ctl;                // [0] the event count
   const uint64_t* sorted_key;   // after the sort

@@ -169,7 +169,8 @@ struct cc_engine {
   uint32_t* d_cset_full = nullptr; // the set overflowed
   uint64_t* d_tbl_claim = nullptr; // [map_entries] log index at which each entry was first bound
   unsigned long long* d_lvl_at = nullptr;
-  uint64_t* d_half_count = nullptr;  // a batch applied as two calls (kBarCap): the second call's event count  // [max_resources * kLvlSlots] capacity-level timeline (common.h)
+  uint64_t* d_half_count = nullptr;
+  EvPay* d_sm_pay = nullptr;       // [sm_cap] map event payloads by emission slot (map_small.hip)  // a batch applied as two calls (kBarCap): the second call's event count  // [max_resources * kLvlSlots] capacity-level timeline (common.h)
   // exact map sizes / HashMap capacities (map_wide.hip launch_map_size; not in TTL mode)
   uint32_t* d_rst_msz = nullptr;   // [sub_batch + 4 kPT] each region map commit's map and size change, staging order
   uint32_t* d_hot_msz = nullptr;   // hot-key commits' size changes (HotArgs::hot_msz)

@@ -287,6 +287,7 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
     HIPCHECK(hipMemcpy(&clock, e->d_clock, sizeof clock, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(&last, e->d_last_index, sizeof last, hipMemcpyDeviceToHost));
     const bool pending = e->applied_pending;
+    const uint64_t applied0 = e->applied;
     const auto gtimers = e->gtimers;
     const uint64_t ev0 = ev_n;
     const uint8_t st0 = hout->status[pos];
@@ -299,6 +300,7 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
       HIPCHECK(hipMemcpy(e->d_clock, &clock, sizeof clock, hipMemcpyHostToDevice));
       HIPCHECK(hipMemcpy(e->d_last_index, &last, sizeof last, hipMemcpyHostToDevice));
       e->applied_pending = pending;
+      e->applied = applied0;
       e->gtimers = gtimers;
       ev_n = ev0;
       return finish(set_err(CC_ERR_CAPACITY, "a coordination collection is full (coord_cap): *applied rows were applied"));

@@ -47,16 +47,16 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
 // its events applied in log order (putVal of a new key, removeNode), the state written back.  A map whose table
 // passes 64 leaves the window (its later events are not followed).
 constexpr int kSrT = 64;                                               // runs per workgroup
-constexpr int kSrStride = (int)((sizeof(SmallMap) + 8) / 8) | 1;       // u64 words per run's copy (odd: fewer bank conflicts)
+constexpr int kSrStride = (int)((kSmHotBytes + 8) / 8) | 1;           // u64 words per run's copy (odd: fewer bank conflicts)
 __global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                       const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
+                                                       const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
                                                        const uint32_t* __restrict__ nseg, SmallMap* __restrict__ st,
                                                        uint8_t* __restrict__ msmall, uint32_t* __restrict__ mpcap,
                                                        unsigned long long* __restrict__ lvl_at, const uint64_t* __restrict__ idx0,
                                                        const uint64_t* __restrict__ index, uint64_t lo, bool ttl) {
   __shared__ uint64_t lds[kSrT * kSrStride];
-  static_assert(sizeof(SmallMap) % 8 == 0, "SmallMap copies are u64 words");
-  constexpr uint32_t W = sizeof(SmallMap) / 8;
+  static_assert(kSmHotBytes % 8 == 0, "SmallMap copies are u64 words");
+  constexpr uint32_t W = kSmHotBytes / 8;  // the hot part; the keys stay in HBM (small_jhm.h)
   SmallMap& lm = *reinterpret_cast<SmallMap*>(lds + threadIdx.x * kSrStride);
   const uint32_t E = ctl[0], ns = *nseg;
   for (uint32_t r = blockIdx.x * kSrT + threadIdx.x; r < ns; r += gridDim.x * kSrT) {
@@ -67,15 +67,15 @@ __global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restric
     const uint64_t* src = reinterpret_cast<const uint64_t*>(s);
     uint64_t* dst = reinterpret_cast<uint64_t*>(&lm);
     for (uint32_t q = 0; q < W; ++q) dst[q] = src[q];
-    SmallJhm j(lm);
+    SmallJhm j(lm, *s);
     for (uint32_t i = start; i < E; ++i) {
       const uint64_t k = key[i];
       if ((uint32_t)(k >> 44) != m) break;
       if (k & 8u) continue;  // a size / isEmpty query (k_size_answer)
-      const uint32_t x = val[i];
+      const EvPay x = pay[val[i]];
       if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
         const uint32_t lv0 = lm.lvl;
-        const bool stay = j.put(x);
+        const bool stay = j.put(x.aux, x.ktag, x.key);
         if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
           const uint64_t d = (k >> 4) & ((1ull << 40) - 1);
           // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restric
         }
         if (!stay) break;  // the table passed 64: out of the window
       } else if ((k & 3u) == 2u) {  // a key removed: removeNode
-        j.remove(x);
+        j.remove(x.aux, x.ktag, x.key);
       }
     }
     if (!(lm.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
@@ -198,8 +198,8 @@ __global__ void k_small_clear(SmallMap* __restrict__ st, uint32_t m) {
 __global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, uint64_t lo, uint64_t hi,
                             const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                             const uint64_t* __restrict__ index, const uint32_t* __restrict__ inst_res,
-                            uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val, uint32_t cap,
-                            uint32_t* __restrict__ ctl) {
+                            uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val, EvPay* __restrict__ ev_pay,
+                            uint32_t cap, uint32_t* __restrict__ ctl) {
   const uint64_t idx0 = index[lo];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < szq_n; q += gridDim.x * blockDim.x) {
     const uint32_t row = szq[q];
@@ -209,7 +209,8 @@ __global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, ui
     const uint32_t at = atomicAdd(ctl, 1u);
     if (at < cap) {
       ev_key[at] = ((uint64_t)m << 44) | (d << 4) | 8u | (op[row] == CC_OP_MAP_ISEMPTY ? 4u : 0u);
-      ev_val[at] = row;
+      ev_val[at] = at;
+      ev_pay[at] = EvPay{0, row, 0};
     }
   }
 }
@@ -217,7 +218,7 @@ __global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, ui
 // One wave per map run of the sorted buffer: the run's net change, then a wave-wide running count; each query row
 // gets the size before it (events with its index come first: a query follows the command whose index it carries).
 __global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                     const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
+                                                     const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
                                                      const uint32_t* __restrict__ nseg, const uint32_t* __restrict__ msize,
                                                      uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value) {
   const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict_
       }
       if (in && (k & 8u)) {
         const int32_t at = size + inc;  // (a query's own delta is 0: inc counts the events before it)
-        const uint32_t row = val[i];
+        const uint32_t row = pay[val[i]].aux;
         if (k & 4u) {  // isEmpty
           out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
           out_value[row] = at == 0 ? 1ull : 0ull;
@@ -277,12 +278,12 @@ __global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
 int launch_size_emit(const SizeArgs& a, hipStream_t st) {
   if (a.szq_n == 0) return 0;
   hipLaunchKernelGGL(k_size_emit, dim3(std::min<uint32_t>(1024, (a.szq_n + 255) / 256)), dim3(256), 0, st, a.szq, a.szq_n,
-                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.cap, a.ctl);
+                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.ev_pay, a.cap, a.ctl);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_size_answer(const SizeArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_size_answer, dim3(256), dim3(256), 0, st, a.sorted_key, a.sorted_val, a.ctl, a.seg, a.nseg,
+  hipLaunchKernelGGL(k_size_answer, dim3(256), dim3(256), 0, st, a.sorted_key, a.sorted_val, a.ev_pay, a.ctl, a.seg, a.nseg,
                      a.msize, a.out_status, a.out_value);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -307,7 +308,7 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
     if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (E + 255) / 256);
     hipLaunchKernelGGL(k_small_seg, dim3(grid), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg);
-    hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(kSrT), 0, st, a.ev_key2, a.ev_val2, a.ctl, a.seg, a.nseg, a.state,
+    hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(kSrT), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg, a.state,
                        a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
       hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap,

@@ -314,8 +314,9 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
         uint64_t ord = ins[e];
         if (sflags & kSmIn) {
           bool dup;
-          ord = small_chain_pos(small[slot], jh, dup);
-          if (dup || (16ull << small[slot].lvl) != cap) atomicOr(err, kErrMapOrder);
+          ord = small_chain_pos(small[slot], jh, (w >> 17) & 3, key[e], dup);
+          // (and a model that does not hold the map's live keys -- an engine fault -- refuses rather than guesses)
+          if (dup || (16ull << small[slot].lvl) != cap || (!dl && small[slot].n != ctl[C_PRES])) atomicOr(err, kErrMapOrder);
         }
         atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ord);
       }
@@ -332,13 +333,15 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
 }
 
 // The deciding bin's keys that the map bound since its last clear and that compaction dropped since (the set of
-// common.h CsetEnt; a key bound again now was counted among the table's entries by k_mw_order pass 1): added to the
-// per-level counts of the tree-bin test.  Runs only for an order-dependent containsValue decided inside one bin of a
+// common.h CsetEnt, with each key's earliest claim): added to the per-level counts of the tree-bin test, except at
+// the levels where k_mw_order pass 1 already counted the key's entry bound now (by that entry's own claim).  A key
+// bound again after a compaction thus counts once, by its earliest claim.  Runs only for an order-dependent containsValue decided inside one bin of a
 // table above 64 (all threads read the same ctl).  A set that overflowed counts as 9 (refuse).
 __global__ __launch_bounds__(kMwT) void k_mw_cset(const CsetEnt* __restrict__ set, uint64_t n, const uint32_t* __restrict__ full,
                                                  const uint64_t* __restrict__ cgen, uint32_t slot,
                                                  const uint32_t* __restrict__ word, const uint64_t* __restrict__ tkey,
-                                                 uint32_t map_bits, const uint32_t* __restrict__ mpcap,
+                                                 const uint64_t* __restrict__ claim, uint32_t map_bits,
+                                                 const uint32_t* __restrict__ mpcap,
                                                  const SmallMap* __restrict__ small, const uint64_t* __restrict__ hh_key,
                                                  const int32_t* __restrict__ hh_val, uint32_t hh_n,
                                                  const unsigned long long* __restrict__ lvl_at,
@@ -365,11 +368,17 @@ __global__ __launch_bounds__(kMwT) void k_mw_cset(const CsetEnt* __restrict__ se
       continue;
     }
     if ((jh & 127u) != (bb & 127u)) continue;  // not in the bin even at 128 (bins only split further above)
-    if (tbl_bound(word, tkey, map_bits, slot, kt, k)) continue;  // counted among the bound entries
+    // its entry bound now, as k_mw_order pass 1 counts entries (used, not dead, not unseen): that entry's claim
+    const uint64_t te = tbl_find(word, tkey, map_bits, slot, kt, k);
+    uint64_t tcl = ~0ull;
+    if (te != ~0ull) {
+      const uint32_t tw = word[te];
+      if (!(tw & kMwDead) && (tw & kMwUsed) && !(tw & kMwUnseen)) tcl = claim[te];
+    }
     const uint64_t cl = set[e].claim;
     for (uint32_t L = 3; L <= lv && L - 3 < 32; ++L) {
-      const uint64_t mk = (16ull << L) - 1;
-      if ((jh & mk) == (bb & mk) && cl <= lvl_left(lvl_at, slot, L)) atomicAdd(&ctl[C_TR0 + (L - 3)], 1ull);
+      const uint64_t mk = (16ull << L) - 1, left = lvl_left(lvl_at, slot, L);
+      if ((jh & mk) == (bb & mk) && cl <= left && !(tcl <= left)) atomicAdd(&ctl[C_TR0 + (L - 3)], 1ull);
     }
   }
 }
@@ -528,7 +537,7 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
     if (a.cset) {
       const uint32_t cg = (uint32_t)std::min<uint64_t>(2048, (a.cset_n + kMwT - 1) / kMwT);
       hipLaunchKernelGGL(k_mw_cset, dim3(cg), dim3(kMwT), 0, st, a.cset, a.cset_n, a.cset_full, a.cgen, a.slot, a.tbl_word,
-                         a.tbl_key, a.map_bits, a.mpcap, a.small, a.hh_key, a.hh_val, a.hh_n, a.lvl_at, a.ctl, a.err);
+                         a.tbl_key, a.tbl_claim, a.map_bits, a.mpcap, a.small, a.hh_key, a.hh_val, a.hh_n, a.lvl_at, a.ctl, a.err);
     }
   }
   if (a.msize) hipLaunchKernelGGL(k_mw_size, dim3(1), dim3(64), 0, st, a.slot, op, a.ctl, a.msize, a.err);
@@ -576,15 +585,17 @@ __device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_
 // sub-batch, or in TTL mode 2 * row offset + 1: common.h TtlEmit) and the key's HashMap hash.
 __device__ inline void map_event(uint32_t m, uint32_t code, uint64_t d, const MRec& xr, const uint64_t* __restrict__ hh_key,
                                  const int32_t* __restrict__ hh_val, uint32_t hh_n, uint64_t* __restrict__ ev_key,
-                                 uint32_t* __restrict__ ev_val, uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
-                                 uint32_t* __restrict__ err) {
+                                 uint32_t* __restrict__ ev_val, EvPay* __restrict__ ev_pay, uint32_t ev_cap,
+                                 uint32_t* __restrict__ sm_ctl, uint32_t* __restrict__ err) {
   bool ok;
-  const uint32_t jh = java_key_hash(CC_FLAG_KTAG(smeta_flags(xr.meta)), xr.key, hh_key, hh_val, hh_n, ok);
+  const uint32_t kt = CC_FLAG_KTAG(smeta_flags(xr.meta));
+  const uint32_t jh = java_key_hash(kt, xr.key, hh_key, hh_val, hh_n, ok);
   if (!ok || d >> 40) atomicOr(err, kErrHandleHash);  // an unregistered String key / a sub-batch spanning 2^40 indices
   const uint32_t at = atomicAdd(sm_ctl, 1u);
   if (at < ev_cap) {
     ev_key[at] = ((uint64_t)m << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
-    ev_val[at] = jh;
+    ev_val[at] = at;
+    ev_pay[at] = EvPay{xr.key, jh, kt};
   }
 }
 
@@ -598,7 +609,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
                                                       const uint64_t* __restrict__ idx0p, const uint64_t* __restrict__ hh_key,
                                                       const int32_t* __restrict__ hh_val, uint32_t hh_n,
                                                       uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val,
-                                                      uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
+                                                      EvPay* __restrict__ ev_pay, uint32_t ev_cap, uint32_t* __restrict__ sm_ctl,
                                                       const uint32_t* __restrict__ map_row, uint64_t lo,
                                                       uint32_t* __restrict__ err) {
   __shared__ uint32_t cnt[kMszPass];
@@ -661,10 +672,10 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
         const uint64_t g = (uint64_t)t * kTile + p;
         if (map_row)  // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip)
           map_event(x >> 2, code, 2 * ((uint64_t)map_row[g] - lo) + 1, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val,
-                    ev_cap, sm_ctl, err);
+                    ev_pay, ev_cap, sm_ctl, err);
         else if (msmall && msmall[x >> 2])  // small-window or size-queried map (map_small.hip)
-          map_event(x >> 2, code, xrec[g].idx - *idx0p, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_cap, sm_ctl,
-                    err);
+          map_event(x >> 2, code, xrec[g].idx - *idx0p, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_pay, ev_cap,
+                    sm_ctl, err);
       }
     }
     for (uint32_t i = threadIdx.x; i < nwords; i += kMszT) {  // one code word (16 list positions) per thread
@@ -861,7 +872,7 @@ int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
   if (a.tiles == 0) return 0;
   hipLaunchKernelGGL(k_msize_count, dim3(a.tiles), dim3(kMszT), 0, st, a.ttab, a.sb, a.k0, a.sb_hot, a.rst_msz, a.hot,
                      a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.max_resources, a.tcnt, a.list_n, a.msmall, a.mrec,
-                     a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_cap, a.sm_ctl, a.map_row, a.lo,
+                     a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_pay, a.ev_cap, a.sm_ctl, a.map_row, a.lo,
                      a.err);
   if (a.map_row) return hipGetLastError() == hipSuccess ? 0 : -1;  // TTL mode: sizes from the events (k_ttl_replay)
   hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,

@@ -15,16 +15,22 @@
 //           (resize() below capacity 64, else treeify); then ++size > threshold resizes;
 //   remove: removeNode(movable = true) — MapState.remove / removeIfPresent and the TTL timer call map.remove(key);
 //   resize: lists split in order (a tree bin exists only at 64, and a table of 128 leaves this window).
-// Keys are known by their HashMap hash only (the events of map_small.hip): two live keys with one hash make the
-// map's order unknown to the engine (kSmAmbig; an order-dependent answer then fails with CC_ERR_STATE).
+// Nodes carry their keys (tag + value, the events' payload, map_small.hip), so equal hashes are resolved as the JDK
+// does: putTreeVal / treeify compare two keys of one class with compareTo (Long, Integer signed; Boolean false <
+// true) and keys of different classes by tieBreakOrder (class names: Boolean < Integer < Long < String).  Two String
+// keys with one hash in a tree bin would need String.compareTo of texts the engine holds as handles: that order is
+// unknown (kSmAmbig; an order-dependent answer then fails with CC_ERR_STATE).  List bins need no comparison.
 #pragma once
+#include <cstddef>
+
 #include "common.h"
 
 namespace cc {
 
 struct SmallJhm {
-  SmallMap& s;
-  __device__ explicit SmallJhm(SmallMap& m) : s(m) {}
+  SmallMap& s;  // the hot part (links, hashes, bins): an LDS copy in k_small_replay
+  SmallMap& g;  // the keys (SmallMap::key / kt): the map's state in HBM
+  __device__ SmallJhm(SmallMap& m, SmallMap& keys) : s(m), g(keys) {}
 
   __device__ uint32_t cap() const { return 16u << s.lvl; }
   __device__ bool tree(uint32_t x) const { return s.nb[x - 1] & 1u; }
@@ -43,7 +49,7 @@ struct SmallJhm {
   __device__ void set_right(uint32_t x, uint32_t v) { s.rt[x - 1] = (uint8_t)v; }
   __device__ uint32_t hash(uint32_t x) const { return s.jh[x - 1]; }
 
-  __device__ uint32_t alloc(uint32_t h) {
+  __device__ uint32_t alloc(uint32_t h, uint32_t kt, uint64_t key) {
     const uint64_t free = ~s.used;
     if (!free) {
       s.flags |= kSmAmbig;  // (cannot happen: a table of 64 holds at most 49 nodes for a moment)
@@ -52,19 +58,33 @@ struct SmallJhm {
     const uint32_t i = (uint32_t)__builtin_ctzll(free);
     s.used |= 1ull << i;
     s.jh[i] = h;
+    g.key[i] = key;
+    g.kt[i] = (uint8_t)kt;
     s.nx[i] = s.pv[i] = s.pa[i] = s.lf[i] = s.rt[i] = 0;
     s.nb[i] = 0;
     return i + 1;
   }
   __device__ void release(uint32_t x) { s.used &= ~(1ull << (x - 1)); }
 
-  // putTreeVal's direction: the hash as a signed int (an equal hash needs the keys' compareTo: unknown here)
-  __device__ int dir_of(uint32_t h, uint32_t p) {
+  // putTreeVal's / treeify's direction for key (kt, key) with hash h at tree node p: the hash as a signed int, then
+  // compareComparables (same class), then tieBreakOrder (class names; a new key never equals a live one)
+  __device__ int dir_of(uint32_t h, uint32_t kt, uint64_t key, uint32_t p) {
     const int32_t ph = (int32_t)hash(p), hh = (int32_t)h;
     if (ph > hh) return -1;
     if (ph < hh) return 1;
-    s.flags |= kSmAmbig;
-    return 1;
+    const uint32_t pt = g.kt[p - 1];
+    const uint64_t pk = g.key[p - 1];
+    if (kt == pt) {
+      switch (kt) {
+        case 0: return (int64_t)key < (int64_t)pk ? -1 : 1;  // Long.compareTo
+        case 1: return (int32_t)key < (int32_t)pk ? -1 : 1;  // Integer.compareTo
+        case 2: return key < pk ? -1 : 1;                    // Boolean.compareTo (false < true)
+        default: s.flags |= kSmAmbig; return 1;              // String.compareTo of texts held as handles
+      }
+    }
+    // tieBreakOrder: getClass().getName() -- java.lang.Boolean < Integer < Long < String (tags 2, 1, 0, 3)
+    constexpr uint32_t rank[4] = {2, 1, 0, 3};
+    return rank[kt] < rank[pt] ? -1 : 1;
   }
   __device__ uint32_t root_of(uint32_t p) const {
     while (par(p)) p = par(p);
@@ -230,7 +250,7 @@ struct SmallJhm {
         continue;
       }
       for (uint32_t p = root;;) {
-        const int dir = dir_of(hash(x), p);
+        const int dir = dir_of(hash(x), g.kt[x - 1], g.key[x - 1], p);
         const uint32_t xp = p;
         if (!(p = dir <= 0 ? left(p) : right(p))) {
           set_par(x, xp);
@@ -290,19 +310,19 @@ struct SmallJhm {
     return true;
   }
   // putVal of a new key (an existing key's put changes no structure); false: the map left the window
-  __device__ bool put(uint32_t h) {
+  __device__ bool put(uint32_t h, uint32_t kt, uint64_t key) {
     const uint32_t i = (cap() - 1) & h;
     uint32_t p = s.tab[i];
     if (!p) {
-      const uint32_t x = alloc(h);
+      const uint32_t x = alloc(h, kt, key);
       s.tab[i] = (uint8_t)x;
     } else if (tree(p)) {  // putTreeVal: linked after its tree parent, then the root moves to the front
       const uint32_t root = root_of(p);
       for (uint32_t q = root;;) {
-        const int dir = dir_of(h, q);
+        const int dir = dir_of(h, kt, key, q);
         const uint32_t xp = q;
         if (!(q = dir <= 0 ? left(q) : right(q))) {
-          const uint32_t xpn = next(xp), x = alloc(h);
+          const uint32_t xpn = next(xp), x = alloc(h, kt, key);
           if (!x) return true;
           s.nb[x - 1] = 1u;
           set_next(x, xpn);
@@ -318,7 +338,7 @@ struct SmallJhm {
     } else {
       uint32_t bin = 0;
       while (next(p)) p = next(p), ++bin;
-      const uint32_t x = alloc(h);
+      const uint32_t x = alloc(h, kt, key);
       set_next(p, x);
       if (bin >= 7u && !treeify_bin(h)) return false;  // the chain now holds >= 9 nodes
     }
@@ -391,17 +411,14 @@ struct SmallJhm {
     }
     to_front(r);
   }
-  // removeNode(movable = true) of the live key with hash h
-  __device__ void remove(uint32_t h) {
+  // removeNode(movable = true) of the live key (kt, key) with hash h
+  __device__ void remove(uint32_t h, uint32_t kt, uint64_t key) {
     const uint32_t index = (cap() - 1) & h;
     uint32_t node = 0, prv = 0, pp = 0;
-    for (uint32_t q = s.tab[index]; q; pp = q, q = next(q))
-      if (hash(q) == h) {
-        if (node) {  // two live keys with one hash: which one left is unknown here
-          s.flags |= kSmAmbig;
-          break;
-        }
+    for (uint32_t q = s.tab[index], steps = 0; q && steps < kSmNodes; pp = q, q = next(q), ++steps)
+      if (hash(q) == h && g.kt[q - 1] == kt && g.key[q - 1] == key) {
         node = q, prv = pp;
+        break;
       }
     if (!node) {
       s.flags |= kSmAmbig;  // (a removal of a key this model does not hold: its order is no longer known)
@@ -415,19 +432,18 @@ struct SmallJhm {
   }
 };
 
-// The position of the live key with hash h in its bin's chain (iteration order inside the bin); dup: another live
-// key of the bin has the same hash (the order between the two is unknown here).
-__device__ inline uint32_t small_chain_pos(const SmallMap& s, uint32_t h, bool& dup) {
+// The position of the live key (kt, key) with hash h in its bin's chain (iteration order inside the bin); unknown:
+// the model does not hold it.
+__device__ inline uint32_t small_chain_pos(const SmallMap& s, uint32_t h, uint32_t kt, uint64_t key, bool& unknown) {
   const uint32_t index = ((16u << s.lvl) - 1u) & h;
-  uint32_t pos = 0, found = ~0u, steps = 0;
-  dup = false;
+  uint32_t pos = 0, steps = 0;
   for (uint32_t q = s.tab[index]; q && steps < kSmNodes; q = s.nx[q - 1], ++steps, ++pos)
-    if (s.jh[q - 1] == h) {
-      if (found != ~0u) dup = true;
-      else found = pos;
+    if (s.jh[q - 1] == h && s.kt[q - 1] == kt && s.key[q - 1] == key) {
+      unknown = false;
+      return pos;
     }
-  if (found == ~0u) dup = true;  // (not in the model: unknown)
-  return found;
+  unknown = true;
+  return ~0u;
 }
 
 }  // namespace cc

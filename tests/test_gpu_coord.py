@@ -290,16 +290,48 @@ def test_coordination_on_a_full_partition_fails_at_creation():
     assert ei.value.rc == abi.CC_ERR_CAPACITY
 
 
+def _barrier_event_batch(locks=256, K=4, maps=2, n=150_000):
+    """Lock traffic (coord_random_stream, kept whole) with 70,000 map rows (puts, then containsValue) between its rows."""
+    from copycat_amd.workload import coord_random_stream
+
+    max_inst = (locks + maps) * K + 8
+    # the lock stream stays whole (its client model keeps every queue within coord_cap); the map rows go between
+    rng = np.random.default_rng(811)
+    nm = 70_000
+    lk = coord_random_stream(n - nm, np.full(locks, L, np.uint8), K, max_inst, seed=811, p_delete=0.0)
+    rows = np.sort(rng.choice(n, nm, replace=False))
+    at = np.ones(n, bool)
+    at[rows] = False
+    cols = {}
+    for name, _ in abi.BATCH_COLUMNS:
+        src = getattr(lk, name)
+        col = np.zeros(n, src.dtype)
+        col[at] = src
+        cols[name] = col
+    cols["index"] = np.arange(1, n + 1, dtype=np.uint64)
+    cols["time"] = np.maximum.accumulate(cols["time"])  # (a map row takes the clock of the lock row before it)
+    mrow = rows[: nm // 10]  # some puts first, so the containsValue answers vary
+    cols["op"][rows] = abi.CC_OP_MAP_CONTAINSVALUE
+    cols["op"][mrow] = abi.CC_OP_MAP_PUT
+    cols["inst"][rows] = (locks + rng.integers(0, maps, nm)) * K + rng.integers(0, K, nm)
+    cols["key"][rows] = rng.integers(0, 64, nm).astype(np.uint64)
+    cols["a"][rows] = rng.integers(0, 4, nm).astype(np.uint64)
+    nul = rng.random(nm) < 0.05
+    cols["flags"][rows] = np.where(nul, abi.cc_flags(abi.CC_TAG_NULL, 0, 0), abi.cc_flags(abi.CC_TAG_LONG, 0, 0))
+    cols["aux"][rows] = 0
+    b = Batch.from_columns(**cols)
+    return b
+
+
 def test_more_barrier_rows_than_one_listing_with_events():
     """A batch with more whole-map rows than one barrier listing holds (kBarCap = 65,536) on an engine with an event
     stream runs as two consecutive calls: the second call's events follow the first's, their rows moved by the
     first half's length.  Lock traffic (events on almost every row) interleaved with 70,000 containsValue rows on two
     maps: every row and every event (row, target, code, payload) as the oracle publishes them."""
     from copycat_amd.engine import Engine
-    from copycat_amd.workload import coord_random_stream
     from oracle.oracle_py import Oracle
 
-    locks, K, maps, n = 32, 4, 2, 150_000
+    locks, K, maps, n = 256, 4, 2, 150_000  # (256 locks: every queue stays well within coord_cap)
     R = locks + maps
     max_inst = R * K + 8
     E = Engine(R, max_inst, n, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=1 << 20, map_capacity=4096)
@@ -311,18 +343,7 @@ def test_more_barrier_rows_than_one_listing_with_events():
         for k in range(K):
             E.instance_open(r * K + k, r, 1000 + r * K + k, 7 + k)
             O.instance_open(r * K + k, r, 1000 + r * K + k, 7 + k)
-    b = coord_random_stream(n, np.full(locks, L, np.uint8), K, max_inst, seed=811, p_delete=0.0)
-    rng = np.random.default_rng(811)
-    rows = np.sort(rng.choice(n, 70_000, replace=False))
-    mrow = rows[: len(rows) // 10]  # some puts first, so the containsValue answers vary
-    b.op[rows] = abi.CC_OP_MAP_CONTAINSVALUE
-    b.op[mrow] = abi.CC_OP_MAP_PUT
-    b.inst[rows] = (locks + rng.integers(0, maps, len(rows))) * K + rng.integers(0, K, len(rows))
-    b.key[rows] = rng.integers(0, 64, len(rows)).astype(np.uint64)
-    b.a[rows] = rng.integers(0, 4, len(rows)).astype(np.uint64)
-    nul = rng.random(len(rows)) < 0.05
-    b.flags[rows] = np.where(nul, abi.cc_flags(abi.CC_TAG_NULL, 0, 0), abi.cc_flags(abi.CC_TAG_LONG, 0, 0)).astype(np.uint8)
-    b.aux[rows] = 0
+    b = _barrier_event_batch(locks, K, maps, n)
     s, v, ev = _check_batch(E, O, b, capacity=4 * n)
     assert ev["pos"].max() >= n // 2  # events of the second call, at their own rows
     _check_state(E, O, [L] * locks)
