@@ -14,6 +14,29 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/kt -o run --output
 tail -1 $R/$OUT/kt.log | cut -c1-300
 STATS=$(find $R/$OUT/kt -name "*kernel_stats.csv" | head -1)
 cp $STATS $R/$OUT/kernel_stats.csv
+# per-kernel averages over the timed steps only: the last steps/(warmup+steps) of each kernel's launches in start
+# order (the warm-up step's launches -- fresh tables, first-touch binding -- run slower and are in kernel_stats too)
+TRACE=$(find $R/$OUT/kt -name "*kernel_trace.csv" | head -1)
+python3 - "$TRACE" "$@" > $R/$OUT/kt_timed.txt <<'PY'
+import csv, sys, collections
+trace, args = sys.argv[1], sys.argv[2:]
+def arg(name, dflt):
+    return int(args[args.index(name) + 1]) if name in args else dflt
+steps, warm = arg("--steps", 1), arg("--warmup", 1)
+ev = collections.defaultdict(list)
+for r in csv.DictReader(open(trace)):
+    n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("cc::", "")
+    ev[n].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+print(f"timed steps {steps} of {warm + steps}: per kernel, the last {steps}/{warm + steps} of its launches")
+print(f"{'kernel':44s} {'calls':>6s} {'avg_us':>10s} {'ms/step':>10s}")
+for n, v in sorted(ev.items(), key=lambda kv: -sum(d for _, d in kv[1])):
+    v.sort()
+    k = len(v) * steps // (warm + steps)
+    if k == 0:
+        continue
+    tail = [d for _, d in v[len(v) - k:]]
+    print(f"{n[:44]:44s} {k:6d} {sum(tail) / k / 1e3:10.1f} {sum(tail) / steps / 1e6:10.3f}")
+PY
 find $R/$OUT/kt -name "*kernel_trace.csv" -delete
 i=0
 for CNT in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU" "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY"; do
@@ -22,10 +45,7 @@ for CNT in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_
   (cd $R && python3 scripts/pmc_kernel_summary.py $OUT/pmc$i > $OUT/pmc${i}_summary.txt 2>&1)
   find $R/$OUT/pmc$i -name "*.csv" -delete
 done
-cd $R && python3 - <<'PY' > $OUT/kt_summary.txt
-import csv, sys
-rows = list(csv.DictReader(open("$OUT/kernel_stats.csv".replace("$OUT", sys.argv[1] if len(sys.argv) > 1 else "$OUT"))))
-PY
+cd $R
 python3 -c "
 import csv
 rows = list(csv.DictReader(open('$OUT/kernel_stats.csv')))
@@ -35,5 +55,6 @@ for r in rows:
     print(f\"{n[:44]:44s} {r['Calls']:>6s} {float(r['AverageNs'])/1e3:10.1f} {float(r['TotalDurationNs'])/1e6:10.3f}\")
 " > $OUT/kt_summary.txt
 head -25 $OUT/kt_summary.txt
+head -12 $OUT/kt_timed.txt
 du -sh $OUT
 echo done
