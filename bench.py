@@ -167,7 +167,35 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26):
+def c3_whole_map_rows(part, lo, cv_rate, clear_rate, seed):
+    """The whole-map variant of c3: in a generated block, a share cv_rate of the rows become
+    MapState.containsValue rows whose operand is the value a put of the block stored a little earlier (same map: the
+    row takes that put's instance; many answers are true), and a share clear_rate become MapState.clear rows.
+    Deterministic per (seed, block start): the parity gate regenerates the same rows."""
+    from copycat_amd import abi
+
+    if not cv_rate and not clear_rate:
+        return
+    rng = np.random.default_rng([seed, lo])
+    n = len(part)
+    if cv_rate:
+        rows = np.nonzero(rng.random(n) < cv_rate)[0]
+        puts = np.nonzero(part.op == abi.CC_OP_MAP_PUT)[0]
+        back = np.searchsorted(puts, rows) - 1 - rng.integers(0, 64, len(rows))
+        rows = rows[back >= 0]
+        src = puts[back[back >= 0]]
+        inst, a, tag = part.inst[src].copy(), part.a[src].copy(), (part.flags[src] & np.uint8(7)).copy()
+        part.op[rows] = abi.CC_OP_MAP_CONTAINSVALUE
+        part.inst[rows] = inst
+        part.a[rows] = a
+        part.flags[rows] = tag
+    if clear_rate:
+        cl = np.nonzero(rng.random(n) < clear_rate)[0]
+        cl = cl[part.op[cl] != abi.CC_OP_MAP_CONTAINSVALUE]
+        part.op[cl] = abi.CC_OP_MAP_CLEAR
+
+
+def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26, cv_rate=0.0, clear_rate=0.0):
     """Config-3 stream generated block by block on the host and copied into HBM-resident columns.
     Returns (host Batch of the first keep_host rows for the CPU baseline, DeviceBatch)."""
     from copycat_amd.batch import Batch
@@ -185,6 +213,7 @@ def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26):
         m = min(block, n - lo)
         part = host if m == len(host) else Batch(m)
         map_zipf_rows(lo, m, maps=maps, pairs=pairs, s=zipf, seed=SEED_C3 + rank, threads=threads, out=part)
+        c3_whole_map_rows(part, lo, cv_rate, clear_rate, SEED_C3 + rank)
         if lo == 0:
             keep = part.slice(0, min(keep_host, m))
         for k in names:
@@ -625,6 +654,7 @@ def c3_full_gate(n, R, args, rank, status0, value0, gpu_tab, block=1 << 26):
             m = min(block, n - lo)
             b = host if m == len(host) else Batch(m)
             map_zipf_rows(lo, m, maps=R, pairs=args.pairs, s=args.zipf, seed=SEED_C3 + rank, threads=threads, out=b)
+            c3_whole_map_rows(b, lo, args.cv_rate, args.clear_rate, SEED_C3 + rank)
             own = (b.inst % threads).astype(np.uint16)
             order = np.argsort(own, kind="stable")
             cuts = np.searchsorted(own[order], np.arange(threads + 1))
@@ -964,7 +994,8 @@ def run_c3(args, dev, rank, world, dist):
     R = args.resources or 4096
     cpu_sample = args.cpu_sample or 20_000_000
     t_gen = time.time()
-    batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample))
+    batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample), cv_rate=args.cv_rate,
+                          clear_rate=args.clear_rate)
     t_gen = time.time() - t_gen
     status = torch.full((n,), RESULT_SENTINEL, dtype=torch.uint8, device=dev)  # sentinel: unwritten rows show
     value = torch.full((n,), -1, dtype=torch.int64, device=dev)
@@ -1043,7 +1074,14 @@ def run_c3(args, dev, rank, world, dist):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": (f"c3: DistributedMap put/get/remove 45/45/10, Zipf({args.zipf}) over {args.pairs:,} "
-                                    f"(map, key) pairs in {R:,} MapState resources, {n:,} committed entries per GPU"),
+                                    f"(map, key) pairs in {R:,} MapState resources, {n:,} committed entries per GPU"
+                                    + (f"; whole-map variant: {args.cv_rate:.2%} containsValue (operands stored shortly "
+                                       f"before), {args.clear_rate:.3%} clear"
+                                       if args.cv_rate or args.clear_rate else "")),
+                       "whole_map": ({"containsValue_rate": args.cv_rate, "clear_rate": args.clear_rate,
+                                      "engine_counters": dict(zip(("barrier_rows", "in_stream_containsValue",
+                                                                   "sub_batches"), E.counters()))}
+                                     if args.cv_rate or args.clear_rate else None),
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]},
@@ -1116,6 +1154,8 @@ def main():
     ap.add_argument("--resources", type=int, default=0, help="default: 65536 resources (c2), 4096 maps (c3)")
     ap.add_argument("--pairs", type=int, default=1 << 20, help="c3: distinct (map, key) pairs")
     ap.add_argument("--zipf", type=float, default=0.99, help="c3: Zipf exponent of the pair rank (0 = uniform)")
+    ap.add_argument("--cv-rate", type=float, default=0.0, help="c3 whole-map variant: share of containsValue rows")
+    ap.add_argument("--clear-rate", type=float, default=0.0, help="c3 whole-map variant: share of clear rows")
     ap.add_argument("--sub-batch", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=0, help="c3: 20M, c5: 10M (c2 uses step 0's rows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

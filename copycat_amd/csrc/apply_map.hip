@@ -149,7 +149,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
                                                   const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ rst_msz, TtlEmit te, uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ rst_msz, TtlEmit te, CvCtx cv, uint32_t* __restrict__ err_out) {
   constexpr int MT = TTL ? 512 : CC_MAP_MT;  // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
   constexpr int MEPer = kMapRegion / MT;  // table entries per thread
   constexpr int kMPer = TTL ? 1 : CC_MAP_CHUNK / CC_MAP_MT;  // commits per thread per chunk
@@ -625,7 +625,10 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         bool wrote, created;
         const u64x2 x = rab[s];
         const int was = (sw & kMwPresent) != 0;
+        const uint32_t sw0 = sw;
+        const uint64_t sv0 = sv;
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, sw, sv, rv, wrote, created);
+        if (!TTL) cv_change(cv, sw0, sv0, sw, sv, [&]() { return xr[rpos[s]].idx; }, err);
         ress[rci[s]] = (uint8_t)st;
         resv[rci[s]] = rv;
         resd[rci[s]] = (int8_t)(((sw & kMwPresent) != 0) - was);
@@ -674,7 +677,10 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           dl = 0;
         }
         const int was = (wv & kMwPresent) != 0;  // (after the expiry: the commit's own change)
+        const uint32_t wv0 = wv;
+        const uint64_t vv0 = vv;
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, wv, vv, rv, wrote, created);
+        if (!TTL) cv_change(cv, wv0, vv0, wv, vv, [&]() { return xr[rpos[s]].idx; }, err);
         if (TTL) {  // a stored commit cancels the old timer and arms its own; a removal cancels it
           if (wrote) dl = rdl[s];
           else if (!(wv & kMwPresent)) dl = 0;
@@ -743,11 +749,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.ttl)
     hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
-                       a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, CvCtx{}, a.err);
   else
     hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, nullptr, nullptr, nullptr, nullptr, nullptr, false,
-                       a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.cv, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

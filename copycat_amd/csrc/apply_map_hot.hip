@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
     return false;  // a full region leaves the key cold
   };
   // a map still in its small-table window is followed commit by commit through its regions (map_small.hip)
-  auto small_map = [&](uint32_t id) { return msmall != nullptr && msmall[id & kMwSlotMask] != 0; };
+  auto small_map = [&](uint32_t id) { return msmall != nullptr && (msmall[id & kMwSlotMask] & (kMfSmall | kMfSize)) != 0; };
   uint32_t pos = 0;
   const bool found = valid && !small_map(ident) && probe(false, pos);
   __shared__ uint32_t bpos[kHotMax];
@@ -493,7 +493,7 @@ __device__ inline void materialize(const Comp& c, const HotS0 s0, const MRec* __
 // size change (1 insert, 2 remove, 0 none: the 2-bit codes of hot_msz)
 __device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t idx, uint32_t& w, uint64_t& v,
                                     uint64_t& ci, uint64_t& ins, uint8_t* __restrict__ rst_status,
-                                    uint64_t* __restrict__ rst_value, uint32_t& err) {
+                                    uint64_t* __restrict__ rst_value, const CvCtx& cv, uint32_t& err) {
   const uint32_t op = smeta_op(m);
   const int was = (w & kMwPresent) != 0;
   uint64_t rv;
@@ -502,7 +502,10 @@ __device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint
     st = map_orphan(op, m, smeta_flags(m), x.x, x.y, rv, err);
   } else {
     bool wrote, created;
+    const uint32_t w0 = w;
+    const uint64_t v0 = v;
     st = map_apply(op, smeta_flags(m), x.x, x.y, w, v, rv, wrote, created);
+    cv_change(cv, w0, v0, w, v, [&]() { return idx; }, err);
     if (wrote) ci = idx;
     if (created) ins = idx;
   }
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
                                                   uint64_t* __restrict__ tbl_val, uint32_t* __restrict__ tbl_word,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ hot_msz, uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ hot_msz, CvCtx cv, uint32_t* __restrict__ err_out) {
   __shared__ uint32_t pfx[kHotMax + 1];
   __shared__ Comp wtot[kHT / kWave];
   __shared__ Comp carry;
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
         uint32_t codes = 0;
         for (uint32_t q = 0; q < L; ++q) {
           const uint32_t g = cur.next();
-          codes |= hot_step(g, xr[g].meta, mrec_ab(xr[g], cb, row0, g), xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, err)
+          codes |= hot_step(g, xr[g].meta, mrec_ab(xr[g], cb, row0, g), xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, cv, err)
                    << (2 * (q % 16));
           if (q % 16 == 15 || q + 1 == L) {
             msz[q / 16] = codes;
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
       for (int q = 0; q < kHPer; ++q)
         if (p0 + q < e)
           codes |= hot_step(gs[q], ms[q], mrec_ab(xr[gs[q]], cb, row0, gs[q]), xr[gs[q]].idx, sw, sv, ci, ins, rst_status,
-                            rst_value, err) << (2 * q);
+                            rst_value, cv, err) << (2 * q);
       // (consecutive threads: consecutive words / halves / bytes of the code words, little-endian)
       if (kHPer == 16) msz[p0 / 16] = codes;
       else if (kHPer == 8) reinterpret_cast<uint16_t*>(msz)[p0 / 8] = (uint16_t)codes;
@@ -654,7 +657,7 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.mrec, a.cb, a.lo, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
-                     a.rst_value, a.hot_msz, a.err);
+                     a.rst_value, a.hot_msz, a.cv, a.err);
   a.mark(K_MAP_HOT, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

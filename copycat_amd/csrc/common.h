@@ -316,6 +316,7 @@ constexpr uint32_t kErrTime = 8u;  // the time column decreased inside a batch
 constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration order is undetermined (map_wide.hip)
 constexpr uint32_t kErrMapSize = 32u;   // a map's tracked size differs from its table at a barrier (internal check)
 constexpr uint32_t kErrHandleHash = 64u;  // a HANDLE map key whose String.hashCode was never registered (cc_handle_hashes)
+constexpr uint32_t kErrCvKey = 128u;     // in-stream containsValue: a fingerprint collision or a 2^40-index span (map_cv.hip)
 
 // java.util.HashMap placement of a map key: hash(key) = h ^ (h >>> 16), h = key.hashCode() -- Long (int)(v ^ v >>> 32),
 // Integer v, Boolean 1231 / 1237, String (HANDLE) its registered String.hashCode (hh: sorted handles + hashes);
@@ -445,6 +446,12 @@ constexpr uint32_t kSmAmbig = 8u;    // a tree order the engine cannot know (two
 // batch asks the map's size / isEmpty (events followed for the in-stream answers); either keeps the map's keys out of
 // hot-key routing, so every such commit is a region record
 constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
+// bit 2: the batch answers containsValue rows of the map in the stream (map_cv.hip): its commits report value changes
+constexpr uint8_t kMfCv = 4u;
+// the flag bytes are set by concurrent threads of one kernel: OR through the aligned word (the array is padded to it)
+__device__ inline void mflag_or(uint8_t* mflag, uint32_t m, uint8_t bit) {
+  atomicOr(reinterpret_cast<uint32_t*>(mflag + (m & ~3u)), (uint32_t)bit << (8 * (m & 3u)));
+}
 // a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
 __device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
   return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);
@@ -534,5 +541,83 @@ constexpr uint32_t kExtTimeCheck = 4u; // the partition checks time[i] >= time[i
 constexpr uint32_t kMetaTtl = 1u << 24;
 __host__ __device__ inline uint32_t mw_ident(uint32_t res, uint32_t ktag) { return (res & kMwSlotMask) | ((ktag & 3) << 17) | kMwUsed; }
 __host__ __device__ inline uint32_t mw_vtag(uint32_t w) { return (w >> 21) & 7; }
+
+
+// ---- containsValue in the stream (map_cv.hip) -------------------------------------------------------------------
+// A sub-batch's in-stream containsValue operands (map slot, value tag, canonical value) live in a device hash set
+// keyed by a 64-bit key: exact (bit 63 set) when the value fits 43 signed bits, else a fingerprint whose entries are
+// verified against the stored operand (a fingerprint shared by two operands fails the batch: kErrCvKey).
+struct CvEnt {
+  unsigned long long k64;  // 0: empty
+  uint64_t v;
+  uint32_t meta;           // slot | tag << 17
+  uint32_t pad;
+};
+__host__ __device__ inline uint64_t cv_key(uint32_t m, uint32_t tag, uint64_t v, bool& exact) {
+  const int64_t sv = (int64_t)v;
+  exact = ((int64_t)((uint64_t)sv << 21) >> 21) == sv;
+  if (exact) return (1ull << 63) | ((uint64_t)(tag & 7u) << 60) | ((uint64_t)(m & kMwSlotMask) << 43) | (v & ((1ull << 43) - 1));
+  uint64_t h = (v ^ ((uint64_t)(m & kMwSlotMask) << 3 | (tag & 7u)) * 0xC2B2AE3D27D4EB4Full) * 0x9E3779B97F4A7C15ull;
+  h ^= h >> 31;
+  h = (h * 0xBF58476D1CE4E5B9ull) & ~(1ull << 63);
+  return h ? h : 1ull;
+}
+__host__ __device__ inline uint32_t cv_slot0(uint64_t k64, uint32_t mask) {
+  uint64_t h = k64 * 0x9E3779B97F4A7C15ull;
+  return (uint32_t)(h >> 32) & mask;
+}
+// The operand's set position, or ~0 when the sub-batch asks no containsValue of it.
+__device__ inline uint32_t cv_find(const CvEnt* __restrict__ set, uint32_t mask, uint32_t m, uint32_t tag, uint64_t v) {
+  bool exact;
+  const uint64_t k = cv_key(m, tag, v, exact);
+  uint32_t p = cv_slot0(k, mask);
+  for (uint32_t step = 0; step <= mask; ++step, p = (p + 1) & mask) {
+    const uint64_t c = set[p].k64;
+    if (c == 0) return ~0u;
+    if (c == k) return (exact || (set[p].v == v && set[p].meta == ((m & kMwSlotMask) | (tag << 17)))) ? p : ~0u;
+  }
+  return ~0u;
+}
+// The containsValue context of a map apply kernel: the maps answered in the stream (mflag & kMfCv), their operand
+// set, and the event buffer (key = operand << 42 | (log index - the sub-batch's first) << 2 | kind: 0 a matching
+// value left an entry, 1 one entered it, 2 a query; value = the query's row - lo).  set == nullptr: off.
+struct CvCtx {
+  const uint8_t* mflag;
+  const CvEnt* set;
+  uint32_t mask;
+  uint64_t* ev_key;
+  uint32_t* ev_val;
+  uint32_t cap;
+  uint32_t* ctl;  // ctl[0]: events appended
+  const uint64_t* idx0p;
+};
+__device__ inline void cv_event(const CvCtx& cv, uint32_t q, uint64_t d, uint32_t kind, uint32_t val, uint32_t& err) {
+  if (d >> 40) err |= kErrCvKey;
+  const uint32_t at = atomicAdd(cv.ctl, 1u);
+  if (at < cv.cap) {
+    cv.ev_key[at] = ((uint64_t)q << 42) | ((d & ((1ull << 40) - 1)) << 2) | kind;
+    cv.ev_val[at] = val;
+  } else {
+    err |= kErrCapacity;
+  }
+}
+// One commit's change of an entry (word / value before and after) in a map answered in the stream: the operand
+// count events of the values that left and entered it.  idx(): the commit's log index (read only on an event).
+template <class IdxF>
+__device__ inline void cv_change(const CvCtx& cv, uint32_t w0, uint64_t v0, uint32_t w1, uint64_t v1, IdxF idx,
+                                 uint32_t& err) {
+  if (!cv.set) return;
+  const uint32_t m = w1 & kMwSlotMask;
+  if (!(cv.mflag[m] & kMfCv)) return;
+  const bool p0 = (w0 & kMwPresent) != 0, p1 = (w1 & kMwPresent) != 0;
+  const uint32_t t0 = mw_vtag(w0), t1 = mw_vtag(w1);
+  if (p0 == p1 && (!p0 || (t0 == t1 && v0 == v1))) return;
+  const uint32_t q0 = p0 ? cv_find(cv.set, cv.mask, m, t0, t0 ? v0 : 0) : ~0u;
+  const uint32_t q1 = p1 ? cv_find(cv.set, cv.mask, m, t1, t1 ? v1 : 0) : ~0u;
+  if (q0 == ~0u && q1 == ~0u) return;
+  const uint64_t d = idx() - *cv.idx0p;
+  if (q0 != ~0u) cv_event(cv, q0, d, 0u, 0u, err);
+  if (q1 != ~0u) cv_event(cv, q1, d, 1u, 0u, err);
+}
 
 }  // namespace cc

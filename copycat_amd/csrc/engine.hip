@@ -99,7 +99,10 @@ static void free_all(cc_engine* e) {
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
                   e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
                   e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp, e->d_sm_pay,
-                  e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb};
+                  e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb,
+                  e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
+                  e->d_cvset,    e->d_cvcnt,    e->d_cvev_key, e->d_cvev_key2, e->d_cvev_val, e->d_cvev_val2, e->d_cvev_ctl,
+                  e->d_cvseg,    e->d_cvtemp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -160,6 +163,52 @@ static int ensure_small(cc_engine* e) {
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events", x);
   e->sm_temp_bytes = tb;
   e->sm_cap = cap;
+  return CC_OK;
+}
+
+// containsValue in the stream (map_cv.hip): the batch's in-stream rows sorted (device) and copied to the host, which
+// cuts each sub-batch's slice of them.
+constexpr uint32_t kCvMaxRows = 1u << 21;  // in-stream containsValue rows per sub-batch (a denser run shortens it)
+static int cv_rows(cc_engine* e, uint32_t n2, hipStream_t st) {
+  e->isc_rows.clear();
+  if (n2 == 0) return CC_OK;
+  const size_t need = std::max<size_t>(cv_rows_temp_bytes(e->cvq_cap), 256);
+  if (!e->d_isc2 || need > e->cv_rtemp_bytes) {
+    if (e->d_isc2) HIPCHECK(hipFree(e->d_isc2));
+    if (e->d_cv_rtemp) HIPCHECK(hipFree(e->d_cv_rtemp));
+    e->d_isc2 = nullptr;
+    e->d_cv_rtemp = nullptr;
+    HIPCHECK(hipMalloc(&e->d_isc2, sizeof(uint32_t) * e->cvq_cap));
+    HIPCHECK(hipMalloc(&e->d_cv_rtemp, need));
+    e->cv_rtemp_bytes = need;
+  }
+  if (cv_sort_rows(e->d_isc, e->d_isc2, n2, e->d_cv_rtemp, e->cv_rtemp_bytes, st))
+    return set_err(CC_ERR_HIP, "containsValue row sort", hipGetLastError());
+  e->isc_rows.resize(n2);
+  HIPCHECK(hipMemcpyAsync(e->isc_rows.data(), e->d_isc2, sizeof(uint32_t) * n2, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  return CC_OK;
+}
+// the operand set (sized for kCvMaxRows operands) and the event buffers (two events per commit, one per query)
+static int ensure_cv(cc_engine* e) {
+  if (e->d_cvset) return CC_OK;
+  const uint32_t sc = 2 * kCvMaxRows;
+  const uint64_t ec = 2ull * e->sub_batch + kCvMaxRows;
+  if (ec > 0xFFFFFFFFull) return set_err(CC_ERR_CAPACITY, "containsValue event buffer beyond 2^32 entries");
+  const size_t tb = std::max<size_t>(cv_sort_temp_bytes((uint32_t)ec), 256);
+  hipError_t x = hipMalloc(&e->d_cvset, sizeof(CvEnt) * sc);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvcnt, sizeof(uint32_t) * sc);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvseg, sizeof(uint32_t) * (sc + 1));
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvev_key, 8 * ec);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvev_key2, 8 * ec);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvev_val, 4 * ec);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvev_val2, 4 * ec);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvev_ctl, sizeof(uint32_t) * 2);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvtemp, tb);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc containsValue buffers", x);
+  e->cvset_cap = sc;
+  e->cvev_cap = (uint32_t)ec;
+  e->cvtemp_bytes = tb;
   return CC_OK;
 }
 
@@ -311,7 +360,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_lvl_at, sizeof(unsigned long long) * kLvlSlots * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
-    ALLOC(e->d_msmall, cfg->max_resources);
+    ALLOC(e->d_msmall, (cfg->max_resources + 3) & ~3u);  // (padded to whole words: common.h mflag_or)
     ALLOC(e->d_sm_ctl, sizeof(uint32_t) * 4);
     ALLOC(e->d_rst_msz, sizeof(uint32_t) * (e->sub_batch + 4 * kPT));
     ALLOC(e->d_hot_msz, sizeof(uint32_t) * (kHotMaxPieces + kHotMax) * (kHotPiece / 16));
@@ -424,6 +473,9 @@ static int check_device_err(cc_engine* e) {
                                    "bin that may have been a red-black tree bin, or on a table capacity the engine's "
                                    "bounds leave open (TTL mode)");
     if (err & kErrMapSize) return set_err(CC_ERR_STATE, "internal check: a map's tracked size differs from its table");
+    if (err & kErrCvKey)
+      return set_err(CC_ERR_STATE, "in-stream containsValue: two operands share a 64-bit fingerprint, or a sub-batch "
+                                   "spans more than 2^40 log indices");
     if (err & kErrHandleHash)
       return set_err(CC_ERR_STATE, "a HANDLE map key's String.hashCode is not registered (cc_handle_hashes), or a "
                                    "sub-batch spans more than 2^40 log indices");
@@ -819,6 +871,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   e->bars.clear();
   uint64_t clock_before = 0;  // the engine clock before this batch (TTL mode and barrier rows need it on the host)
   e->szq_n = 0;
+  e->isc_rows.clear();
   if (e->map_bits || e->coord_on) {
     uint32_t nb = 0, ttl_seen = 0;
     // Outside TTL mode map size / isEmpty rows are answered in the stream (listed in szq, their maps flagged); a batch
@@ -830,6 +883,14 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         HIPCHECK(hipMalloc(&e->d_szq, sizeof(uint32_t) * e->szq_cap));
         HIPCHECK(hipMalloc(&e->d_szq_n, sizeof(uint32_t)));
       }
+      if (inline_size && !e->d_cvq) {  // containsValue candidates (map_cv.hip)
+        e->cvq_cap = 1u << 20;
+        HIPCHECK(hipMalloc(&e->d_cvq, sizeof(uint32_t) * e->cvq_cap));
+        HIPCHECK(hipMalloc(&e->d_isc, sizeof(uint32_t) * e->cvq_cap));
+        HIPCHECK(hipMalloc(&e->d_cvq_n, sizeof(uint32_t) * 2));
+        HIPCHECK(hipMalloc(&e->d_mfirst, sizeof(uint32_t) * e->cfg.max_resources));
+        HIPCHECK(hipMalloc(&e->d_maynull, e->cfg.max_resources));
+      }
       if (e->szq_flagged) {
         if (launch_mflag_clear(e->d_msmall, e->cfg.max_resources, st)) return set_err(CC_ERR_HIP, "map flags", hipGetLastError());
         e->szq_flagged = false;
@@ -837,17 +898,44 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       HIPCHECK(hipMemsetAsync(e->d_ttl_seen, 0, sizeof(uint32_t), st));
       if (launch_map_barriers(c->inst, c->op, c->aux, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar,
                               e->d_bar_n, kBarCap, e->d_ttl_seen, inline_size ? e->d_szq : nullptr,
-                              inline_size ? e->d_szq_n : nullptr, e->szq_cap, e->d_msmall, st))
+                              inline_size ? e->d_szq_n : nullptr, e->szq_cap, e->d_msmall,
+                              inline_size ? e->d_cvq : nullptr, inline_size ? e->d_cvq_n : nullptr, e->cvq_cap,
+                              inline_size ? e->d_mfirst : nullptr, e->cfg.max_resources, st))
         return set_err(CC_ERR_HIP, "map barrier scan launch", hipGetLastError());
-      uint32_t qn = 0;
+      if (inline_size) {  // containsValue candidates: in the stream, or barriers (map_cv.hip)
+        CvBatchArgs cb{};
+        cb.inst = c->inst;
+        cb.op = c->op;
+        cb.flags = c->flags;
+        cb.n = n;
+        cb.inst_res = e->d_inst_res;
+        cb.max_inst = e->cfg.max_instances;
+        cb.mflag = e->d_msmall;
+        cb.tbl_word = e->d_tbl_word;
+        cb.entries = e->map_entries;
+        cb.cvq = e->d_cvq;
+        cb.cvq_n = e->d_cvq_n;
+        cb.cvq_cap = e->cvq_cap;
+        cb.mfirst = e->d_mfirst;
+        cb.maynull = e->d_maynull;
+        cb.R = e->cfg.max_resources;
+        cb.bar = e->d_bar;
+        cb.bar_n = e->d_bar_n;
+        cb.bar_cap = kBarCap;
+        cb.isc = e->d_isc;
+        cb.isc_n = e->d_cvq_n + 1;
+        if (launch_cv_batch(cb, st)) return set_err(CC_ERR_HIP, "containsValue classify launch", hipGetLastError());
+      }
+      uint32_t qn = 0, cvn[2] = {0, 0};
       HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
       if (inline_size) HIPCHECK(hipMemcpyAsync(&qn, e->d_szq_n, sizeof qn, hipMemcpyDeviceToHost, st));
+      if (inline_size) HIPCHECK(hipMemcpyAsync(cvn, e->d_cvq_n, sizeof cvn, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
       if (!inline_size) break;
-      e->szq_flagged = qn > 0;
-      if (ttl_seen || pass > 1) {  // this batch turns TTL mode on: size / isEmpty become barriers again
+      e->szq_flagged = qn > 0 || cvn[0] > 0;
+      if (ttl_seen || pass > 1) {  // this batch turns TTL mode on: size / isEmpty / containsValue become barriers again
         inline_size = false;
         continue;
       }
@@ -858,7 +946,17 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         HIPCHECK(hipMalloc(&e->d_szq, sizeof(uint32_t) * e->szq_cap));
         continue;
       }
+      if (cvn[0] > e->cvq_cap) {
+        HIPCHECK(hipFree(e->d_cvq));
+        HIPCHECK(hipFree(e->d_isc));
+        e->cvq_cap = cvn[0];
+        HIPCHECK(hipMalloc(&e->d_cvq, sizeof(uint32_t) * e->cvq_cap));
+        HIPCHECK(hipMalloc(&e->d_isc, sizeof(uint32_t) * e->cvq_cap));
+        continue;
+      }
       e->szq_n = qn;
+      int rc = cv_rows(e, cvn[1], st);  // the in-stream rows, sorted, on the host too
+      if (rc) return rc;
       break;
     }
     if (ttl_seen && !e->ttl_live) {  // TTL mode for good: sizes and capacities from commit + expiry events
@@ -1013,8 +1111,22 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   const int action = (tim_b != ~0ull && tim_b <= bar_b) ? 2 : (bar_b != ~0ull ? 1 : 0);
   const uint64_t seg_lo = cur;
   const uint64_t seg_hi = action == 2 ? tim_b : (action == 1 ? bar_b : n);
-  for (uint64_t lo = seg_lo; lo < seg_hi; lo += e->sub_batch) {
-    const uint64_t hi = std::min(seg_hi, lo + e->sub_batch);
+  for (uint64_t lo = seg_lo, hi; lo < seg_hi; lo = hi) {
+    hi = std::min(seg_hi, lo + e->sub_batch);
+    // this sub-batch's in-stream containsValue rows (at most kCvMaxRows: a denser run ends the sub-batch earlier)
+    size_t cv_b = 0, cv_e = 0;
+    if (!e->isc_rows.empty()) {
+      cv_b = (size_t)(std::lower_bound(e->isc_rows.begin(), e->isc_rows.end(), (uint32_t)lo) - e->isc_rows.begin());
+      cv_e = (size_t)(std::lower_bound(e->isc_rows.begin(), e->isc_rows.end(), (uint32_t)hi) - e->isc_rows.begin());
+      if (cv_e - cv_b > kCvMaxRows) {
+        cv_e = cv_b + kCvMaxRows;
+        hi = e->isc_rows[cv_e];
+      }
+    }
+    const uint32_t cv_n = (uint32_t)(cv_e - cv_b);
+    CvSubArgs cva{};
+    ++e->stat_subbatches;
+    e->stat_isc += cv_n;
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
     SizeArgs sz{};       // this sub-batch's size / isEmpty rows (map_small.hip)
     bool sized = false;  // the event pipeline ran (its counters are reset after the answers)
@@ -1136,9 +1248,48 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.err = e->d_err;
     va.mark = marker_of(e);
     if ((e->has_values || !e->ext) && launch_apply_value(va, st)) return set_err(CC_ERR_HIP, "apply launch", hipGetLastError()); DBG_SYNC("apply launch");
+    if (cv_n) {  // in-stream containsValue: operand set, initial counts, query events (map_cv.hip)
+      int rc = ensure_cv(e);
+      if (rc) return rc;
+      uint32_t sc = 1024;
+      while (sc < 2 * cv_n) sc <<= 1;
+      cva.cv.mflag = e->d_msmall;
+      cva.cv.set = e->d_cvset;
+      cva.cv.mask = sc - 1;
+      cva.cv.ev_key = e->d_cvev_key;
+      cva.cv.ev_val = e->d_cvev_val;
+      cva.cv.cap = e->cvev_cap;
+      cva.cv.ctl = e->d_cvev_ctl;
+      cva.cv.idx0p = c->index + lo;
+      cva.set = e->d_cvset;
+      cva.cnt = e->d_cvcnt;
+      cva.isc = e->d_isc2 + cv_b;
+      cva.isc_n = cv_n;
+      cva.lo = lo;
+      cva.inst = c->inst;
+      cva.flags = c->flags;
+      cva.a = c->a;
+      cva.index = c->index;
+      cva.inst_res = e->d_inst_res;
+      cva.tbl_word = e->d_tbl_word;
+      cva.tbl_val = e->d_tbl_val;
+      cva.entries = e->map_entries;
+      cva.err = e->d_err;
+      cva.key2 = e->d_cvev_key2;
+      cva.val2 = e->d_cvev_val2;
+      cva.seg = e->d_cvseg;
+      cva.nseg = e->d_cvseg + e->cvset_cap;
+      cva.temp = e->d_cvtemp;
+      cva.temp_bytes = e->cvtemp_bytes;
+      cva.out_status = out->status;
+      cva.out_value = out->value;
+      if (launch_cv_prepare(cva, st)) return set_err(CC_ERR_HIP, "containsValue prepare launch", hipGetLastError());
+      ha.cv = cva.cv;
+    }
     if (e->map_bits) {
       if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
+      ma.cv = cva.cv;
       ma.mrec = e->d_mrec;
       ma.cb = c->b;
       ma.lo = lo;
@@ -1365,6 +1516,14 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.v3 = v3;
     ua.mark = marker_of(e);
     if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
+    if (cv_n) {  // in-stream containsValue answers over the unpermute's placeholders (map_cv.hip)
+      uint32_t E = 0;
+      HIPCHECK(hipMemcpyAsync(&E, e->d_cvev_ctl, sizeof E, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      const int rc = launch_cv_answer(cva, E, st);
+      if (rc) return rc == -2 ? set_err(CC_ERR_CAPACITY, "containsValue events exceed their buffer")
+                              : set_err(CC_ERR_HIP, "containsValue answer launch", hipGetLastError());
+    }
     if (sized) {  // size / isEmpty answers over the unpermute's placeholders; then the next sub-batch's counters
       if (e->szq_n && sized_events && launch_size_answer(sz, st))
         return set_err(CC_ERR_HIP, "size answer launch", hipGetLastError());
@@ -1424,6 +1583,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   }
   {  // the barrier row, against the state as it stands after the rows before it
     const uint64_t row = seg_hi;
+    ++e->stat_barriers;
     const BarRow& br = e->bar_rows[bi];
     const size_t bk = bi;
     cur = row + 1;
@@ -1585,6 +1745,13 @@ extern "C" int cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* strea
   e->last_stream = st;
   // the device copy of the last batch's last index (kept up to date stream-ordered by cc_apply_batch)
   HIPCHECK(hipMemcpyAsync(d_out, e->d_last_index, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  return CC_OK;
+}
+
+extern "C" int cc_engine_counters(cc_engine* e, uint64_t* out, uint32_t n) {
+  if (!e || (n && !out)) return CC_ERR_INVALID;
+  const uint64_t v[3] = {e->stat_barriers, e->stat_isc, e->stat_subbatches};
+  for (uint32_t i = 0; i < n && i < 3; ++i) out[i] = v[i];
   return CC_OK;
 }
 

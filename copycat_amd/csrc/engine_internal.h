@@ -99,6 +99,7 @@ int launch_apply_value_v3(const ValueArgs& a, hipStream_t st);
 int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct MapArgs {
+  CvCtx cv{};          // in-stream containsValue (map_cv.hip): value-change events of the flagged maps
   const MRec* mrec;
   const uint64_t* cb;  // the batch's b column (replaceIfPresent's compare value, mrec_ab)
   uint64_t lo;         // the sub-batch's first row
@@ -246,7 +247,62 @@ constexpr uint32_t kBarCap = 1u << 16;  // barrier rows per batch
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
                         uint32_t* ttl_seen, uint32_t* szq, uint32_t* szq_n, uint32_t szq_cap, uint8_t* mflag,
-                        hipStream_t st);
+                        uint32_t* cvq, uint32_t* cvq_n, uint32_t cvq_cap, uint32_t* mfirst, uint32_t R, hipStream_t st);
+// ---- containsValue in the stream (map_cv.hip) ----
+struct CvBatchArgs {  // per batch: classify the candidates listed by k_map_barriers
+  const uint32_t* inst;
+  const uint8_t* op;
+  const uint8_t* flags;
+  uint64_t n;
+  const uint32_t* inst_res;
+  uint32_t max_inst;
+  const uint8_t* mflag;
+  const uint32_t* tbl_word;
+  uint64_t entries;
+  const uint32_t* cvq;
+  const uint32_t* cvq_n;
+  uint32_t cvq_cap;
+  uint32_t* mfirst;   // per map: the first row that stores a null or deletes the map (~0: none)
+  uint8_t* maynull;   // per map: holds a null value at the batch start
+  uint32_t R;
+  uint32_t* bar;
+  uint32_t* bar_n;
+  uint32_t bar_cap;
+  uint32_t* isc;      // the rows answered in the stream (unsorted)
+  uint32_t* isc_n;
+};
+int launch_cv_batch(const CvBatchArgs& a, hipStream_t st);
+int cv_sort_rows(uint32_t* rows, uint32_t* rows2, uint32_t n, void* temp, size_t temp_bytes, hipStream_t st);
+size_t cv_rows_temp_bytes(uint32_t n);
+struct CvSubArgs {  // per sub-batch: the operand set, initial counts and query events, then the answers
+  CvCtx cv;           // set / mask / events (the apply kernels get the same)
+  CvEnt* set;
+  uint32_t* cnt;      // per set position: matching entries at the sub-batch start
+  const uint32_t* isc;  // this sub-batch's in-stream rows (sorted)
+  uint32_t isc_n;
+  uint64_t lo;
+  const uint32_t* inst;
+  const uint8_t* flags;
+  const uint64_t* a;
+  const uint64_t* index;
+  const uint32_t* inst_res;
+  const uint32_t* tbl_word;
+  const uint64_t* tbl_val;
+  uint64_t entries;
+  uint32_t* err;
+  // answers
+  uint64_t* key2;
+  uint32_t* val2;
+  uint32_t* seg;
+  uint32_t* nseg;
+  void* temp;
+  size_t temp_bytes;
+  uint8_t* out_status;
+  uint64_t* out_value;
+};
+int launch_cv_prepare(const CvSubArgs& a, hipStream_t st);
+int launch_cv_answer(const CvSubArgs& a, uint32_t E, hipStream_t st);
+size_t cv_sort_temp_bytes(uint32_t cap);
 struct MapWideArgs {
   uint32_t slot, op, atag;
   uint64_t apay;
@@ -310,6 +366,7 @@ int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st);
 
 constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
 struct HotArgs {
+  CvCtx cv{};  // in-stream containsValue (map_cv.hip)
   // detection (before the partition)
   const uint32_t* inst;
   const uint8_t* flags;

@@ -195,7 +195,31 @@ struct cc_engine {
   uint32_t* d_szq_n = nullptr;
   uint32_t szq_cap = 0;
   uint32_t szq_n = 0;              // this batch's
-  bool szq_flagged = false;        // maps carry kMfSize from the last batch (cleared before the next scan)
+  bool szq_flagged = false;        // maps carry kMfSize / kMfCv from the last batch (cleared before the next scan)
+  // containsValue in the stream (map_cv.hip)
+  uint32_t* d_cvq = nullptr;       // [cvq_cap] the batch's candidate rows
+  uint32_t* d_cvq_n = nullptr;     // [2]: candidates, rows kept in the stream
+  uint32_t cvq_cap = 0;
+  uint32_t* d_isc = nullptr;       // [cvq_cap] rows answered in the stream (sorted into d_isc2)
+  uint32_t* d_isc2 = nullptr;
+  uint32_t* d_mfirst = nullptr;    // [max_resources] first null-storing / deleting row of a flagged map
+  uint8_t* d_maynull = nullptr;    // [max_resources]
+  void* d_cv_rtemp = nullptr;      // row sort scratch
+  size_t cv_rtemp_bytes = 0;
+  std::vector<uint32_t> isc_rows;  // this batch's in-stream rows, ascending
+  CvEnt* d_cvset = nullptr;        // [cvset_cap] operand set of a sub-batch
+  uint32_t* d_cvcnt = nullptr;     // [cvset_cap]
+  uint32_t cvset_cap = 0;
+  uint64_t* d_cvev_key = nullptr;  // [cvev_cap] events (and sorted copies)
+  uint64_t* d_cvev_key2 = nullptr;
+  uint32_t* d_cvev_val = nullptr;
+  uint32_t* d_cvev_val2 = nullptr;
+  uint32_t* d_cvev_ctl = nullptr;
+  uint32_t* d_cvseg = nullptr;     // [cvset_cap + 1] run starts (+ count)
+  void* d_cvtemp = nullptr;
+  size_t cvtemp_bytes = 0;
+  uint32_t cvev_cap = 0;
+  uint64_t stat_barriers = 0, stat_isc = 0, stat_subbatches = 0;  // cc_engine_counters
   unsigned long long* d_mw_ctl = nullptr;  // [16]
   std::vector<uint32_t> bars;
   // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good

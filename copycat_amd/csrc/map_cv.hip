@@ -1,0 +1,246 @@
+// map_cv.hip — MapState.containsValue answered in the stream, outside TTL mode, for maps that hold no null value.
+//
+// MapState.containsValue (collections/src/main/java/io/atomix/collections/state/MapState.java:49-60) walks
+// map.values() and returns true at the first value equal to the operand; a stored null met first throws
+// NullPointerException.  With no null stored the answer is order-free: true iff some present entry of the
+// map holds the operand (same tag, same canonical payload) at the row.  Such rows need no barrier (map_wide.hip):
+//
+//   per batch   k_map_barriers lists the containsValue rows of maps (candidates) and flags their maps (kMfCv);
+//               k_cv_nullrows finds, per flagged map, the first row that stores a null value (put / putIfAbsent /
+//               replace / replaceIfPresent with a NULL value tag) or deletes the map; k_cv_maynull marks the flagged
+//               maps that hold a null at the batch start; k_cv_classify keeps a candidate in the stream when its map
+//               holds no null before it (else it becomes a barrier row, answered by map_wide.hip in HashMap order);
+//   per sub-batch  the in-stream rows' operands go into a device hash set (k_cv_query, one position per operand,
+//               plus a query event at the row's log position); k_cv_count0 counts, per operand, the present entries
+//               that hold it at the sub-batch start; the map apply kernels (k_apply_map, k_hot_apply) report every
+//               commit of a flagged map that moves a set operand into or out of an entry (common.h cv_change: an
+//               event at the commit's log position); after the apply the events are sorted by (operand, log
+//               position, kind) and one wave per operand walks its run: the count at each query = the initial count
+//               plus the changes before it; the answer is count > 0 (k_cv_answer writes the row's result over the
+//               placeholder the apply left, map_ops.h map_orphan).
+//
+// A query sorts after the commit whose index it carries (a query takes the index of the command before it) and
+// before the next command.  Cost per sub-batch with in-stream rows: one pass over the table words (and the values of
+// the flagged maps' entries), one set probe per value change of a flagged map, a sort of the events.
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+#include "engine_internal.h"
+
+namespace cc {
+
+__device__ inline bool cv_stores(uint32_t op) {
+  return op == CC_OP_MAP_PUT || op == CC_OP_MAP_PUTIFABSENT || op == CC_OP_MAP_REPLACE || op == CC_OP_MAP_REPLACEIFPRESENT;
+}
+
+// per batch: the first row of each flagged map that stores a null (or deletes the map: k_map_barriers lists those)
+__global__ void k_cv_nullrows(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
+                              const uint8_t* __restrict__ flags, uint64_t n, const uint32_t* __restrict__ inst_res,
+                              uint32_t max_inst, const uint8_t* __restrict__ mflag, const uint32_t* __restrict__ cvq_n,
+                              uint32_t* __restrict__ mfirst) {
+  if (*cvq_n == 0) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (!cv_stores(op[i]) || CC_FLAG_TAG_A(flags[i]) != CC_TAG_NULL) continue;
+    const uint32_t in = inst[i];
+    if (in >= max_inst) continue;
+    const uint32_t r = inst_res[in];
+    if (r == kNoRes || !(mflag[r] & kMfCv)) continue;
+    atomicMin(&mfirst[r], (uint32_t)i);
+  }
+}
+
+// per batch: flagged maps holding a null value now
+__global__ void k_cv_maynull(const uint32_t* __restrict__ word, uint64_t entries, const uint8_t* __restrict__ mflag,
+                             const uint32_t* __restrict__ cvq_n, uint8_t* __restrict__ maynull) {
+  if (*cvq_n == 0) return;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = word[e];
+    if (!(w & kMwUsed) || (w & kMwDead) || !(w & kMwPresent) || mw_vtag(w) != CC_TAG_NULL) continue;
+    const uint32_t m = w & kMwSlotMask;
+    if (mflag[m] & kMfCv) maynull[m] = 1;  // (every writer stores 1)
+  }
+}
+
+// per batch: each candidate in the stream or a barrier
+__global__ void k_cv_classify(const uint32_t* __restrict__ cvq, const uint32_t* __restrict__ cvq_n, uint32_t cvq_cap,
+                              const uint32_t* __restrict__ inst, const uint32_t* __restrict__ inst_res,
+                              const uint8_t* __restrict__ maynull, const uint32_t* __restrict__ mfirst,
+                              uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t bar_cap,
+                              uint32_t* __restrict__ isc, uint32_t* __restrict__ isc_n) {
+  const uint32_t n = min(*cvq_n, cvq_cap);
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const uint32_t row = cvq[q];
+    const uint32_t r = inst_res[inst[row]];  // (listed through the same registry: a map slot)
+    if (maynull[r] || row > mfirst[r]) {
+      const uint32_t k = atomicAdd(bar_n, 1u);
+      if (k < bar_cap) bar[k] = row;
+    } else {
+      isc[atomicAdd(isc_n, 1u)] = row;
+    }
+  }
+}
+
+int launch_cv_batch(const CvBatchArgs& a, hipStream_t st) {
+  if (hipMemsetAsync(a.maynull, 0, a.R, st) != hipSuccess) return -1;
+  if (hipMemsetAsync(a.isc_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (a.n + 255) / 256);
+  if (g1) hipLaunchKernelGGL(k_cv_nullrows, dim3(g1), dim3(256), 0, st, a.inst, a.op, a.flags, a.n, a.inst_res, a.max_inst,
+                             a.mflag, a.cvq_n, a.mfirst);
+  const uint32_t g2 = (uint32_t)std::min<uint64_t>(4096, (a.entries + 255) / 256);
+  if (g2) hipLaunchKernelGGL(k_cv_maynull, dim3(g2), dim3(256), 0, st, a.tbl_word, a.entries, a.mflag, a.cvq_n, a.maynull);
+  hipLaunchKernelGGL(k_cv_classify, dim3(1024), dim3(256), 0, st, a.cvq, a.cvq_n, a.cvq_cap, a.inst, a.inst_res, a.maynull,
+                     a.mfirst, a.bar, a.bar_n, a.bar_cap, a.isc, a.isc_n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t cv_rows_temp_bytes(uint32_t n) {
+  size_t need = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, need, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32, (hipStream_t)0);
+  return need;
+}
+int cv_sort_rows(uint32_t* rows, uint32_t* rows2, uint32_t n, void* temp, size_t temp_bytes, hipStream_t st) {
+  size_t tb = temp_bytes;
+  return hipcub::DeviceRadixSort::SortKeys(temp, tb, rows, rows2, (int)n, 0, 32, st) == hipSuccess ? 0 : -1;
+}
+
+// ---- per sub-batch -------------------------------------------------------------------------------------------
+__device__ inline void cv_operand(uint32_t row, const uint32_t* __restrict__ inst, const uint8_t* __restrict__ flags,
+                                  const uint64_t* __restrict__ a, const uint32_t* __restrict__ inst_res, uint32_t& m,
+                                  uint32_t& tag, uint64_t& v) {
+  m = inst_res[inst[row]];
+  tag = CC_FLAG_TAG_A(flags[row]);
+  v = tag ? a[row] : 0;
+}
+
+// the operands into the set (one position each), and a query event per row
+__global__ void k_cv_query(CvSubArgs a) {
+  uint32_t err = 0;
+  const uint64_t idx0 = a.index[a.lo];
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < a.isc_n; q += gridDim.x * blockDim.x) {
+    const uint32_t row = a.isc[q];
+    uint32_t m, tag;
+    uint64_t v;
+    cv_operand(row, a.inst, a.flags, a.a, a.inst_res, m, tag, v);
+    bool exact;
+    const uint64_t k = cv_key(m, tag, v, exact);
+    uint32_t p = cv_slot0(k, a.cv.mask);
+    for (;;) {
+      unsigned long long c = a.set[p].k64;
+      if (c == 0ull) {
+        c = atomicCAS(&a.set[p].k64, 0ull, (unsigned long long)k);
+        if (c == 0ull) {  // claimed: the operand itself, for the fingerprint check
+          a.set[p].v = v;
+          a.set[p].meta = (m & kMwSlotMask) | (tag << 17);
+          break;
+        }
+      }
+      if (c == k) break;
+      p = (p + 1) & a.cv.mask;
+    }
+    cv_event(a.cv, p, a.index[row] - idx0, 2u, row - (uint32_t)a.lo, err);
+  }
+  if (err) atomicOr(a.err, err);
+}
+
+// two operands that share a fingerprint cannot be told apart: the batch fails (kErrCvKey) instead of guessing
+__global__ void k_cv_verify(CvSubArgs a) {
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < a.isc_n; q += gridDim.x * blockDim.x) {
+    uint32_t m, tag;
+    uint64_t v;
+    cv_operand(a.isc[q], a.inst, a.flags, a.a, a.inst_res, m, tag, v);
+    bool exact;
+    const uint64_t k = cv_key(m, tag, v, exact);
+    if (exact) continue;
+    uint32_t p = cv_slot0(k, a.cv.mask);
+    while (a.set[p].k64 != k) p = (p + 1) & a.cv.mask;
+    if (a.set[p].v != v || a.set[p].meta != ((m & kMwSlotMask) | (tag << 17))) atomicOr(a.err, kErrCvKey);
+  }
+}
+
+// per operand: the flagged maps' present entries holding it at the sub-batch start
+__global__ void k_cv_count0(CvSubArgs a) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.entries; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = a.tbl_word[e];
+    if (!(w & kMwUsed) || (w & kMwDead) || !(w & kMwPresent)) continue;
+    const uint32_t m = w & kMwSlotMask;
+    if (!(a.cv.mflag[m] & kMfCv)) continue;
+    const uint32_t t = mw_vtag(w);
+    const uint32_t q = cv_find(a.set, a.cv.mask, m, t, t ? a.tbl_val[e] : 0);
+    if (q != ~0u) atomicAdd(&a.cnt[q], 1u);
+  }
+}
+
+int launch_cv_prepare(const CvSubArgs& a, hipStream_t st) {
+  if (hipMemsetAsync(a.set, 0, sizeof(CvEnt) * ((uint64_t)a.cv.mask + 1), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(a.cnt, 0, sizeof(uint32_t) * ((uint64_t)a.cv.mask + 1), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(a.cv.ctl, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  const uint32_t gq = std::min<uint32_t>(1024, (a.isc_n + 255) / 256);
+  hipLaunchKernelGGL(k_cv_query, dim3(gq), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_cv_verify, dim3(gq), dim3(256), 0, st, a);
+  const uint32_t ge = (uint32_t)std::min<uint64_t>(4096, (a.entries + 255) / 256);
+  hipLaunchKernelGGL(k_cv_count0, dim3(ge), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---- answers ----------------------------------------------------------------------------------------------------
+__global__ void k_cv_seg(const uint64_t* __restrict__ key, uint32_t E, uint32_t* __restrict__ seg, uint32_t* __restrict__ nseg) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x)
+    if (i == 0 || (key[i] >> 42) != (key[i - 1] >> 42)) seg[atomicAdd(nseg, 1u)] = i;
+}
+
+// one wave per operand run (sorted by log position): the running count of entries holding it; a query's answer
+__global__ __launch_bounds__(256) void k_cv_answer(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                   uint32_t E, const uint32_t* __restrict__ seg,
+                                                   const uint32_t* __restrict__ nseg, const uint32_t* __restrict__ cnt,
+                                                   uint64_t lo, uint8_t* __restrict__ out_status,
+                                                   uint64_t* __restrict__ out_value) {
+  const uint32_t ns = *nseg, l = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
+    const uint32_t start = seg[r];
+    const uint64_t q = key[start] >> 42;
+    int64_t c = cnt[q];
+    for (uint32_t b = start;; b += kWave) {
+      const uint32_t i = b + l;
+      const bool in = i < E && (key[i] >> 42) == q;
+      const uint32_t kind = in ? (uint32_t)(key[i] & 3u) : 3u;
+      const int32_t dlt = kind == 1u ? 1 : (kind == 0u ? -1 : 0);
+      int32_t inc = dlt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(inc, d, 64);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      if (kind == 2u) {
+        const uint64_t row = lo + val[i];
+        out_status[row] = (uint8_t)CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+        out_value[row] = c + inc > 0 ? 1ull : 0ull;
+      }
+      c += __shfl(inc, 63, 64);
+      if (__ballot(in) != ~0ull) break;
+    }
+  }
+}
+
+size_t cv_sort_temp_bytes(uint32_t cap) {
+  size_t need = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, need, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
+  return need;
+}
+
+int launch_cv_answer(const CvSubArgs& a, uint32_t E, hipStream_t st) {
+  if (E == 0) return 0;
+  if (E > a.cv.cap) return -2;
+  size_t tb = a.temp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(a.temp, tb, a.cv.ev_key, a.key2, a.cv.ev_val, a.val2, (int)E, 0, 64, st) != hipSuccess)
+    return -1;
+  if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  const uint32_t g = std::min<uint32_t>(1024, (E + 255) / 256);
+  hipLaunchKernelGGL(k_cv_seg, dim3(g), dim3(256), 0, st, a.key2, E, a.seg, a.nseg);
+  hipLaunchKernelGGL(k_cv_answer, dim3(1024), dim3(256), 0, st, a.key2, a.val2, E, a.seg, a.nseg, a.cnt, a.lo, a.out_status,
+                     a.out_value);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cc

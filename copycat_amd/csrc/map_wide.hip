@@ -54,7 +54,8 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
                                        const uint8_t* __restrict__ res_type, uint32_t max_inst, uint32_t* __restrict__ bar,
                                        uint32_t* __restrict__ bar_n, uint32_t cap, uint32_t* __restrict__ ttl_seen,
                                        uint32_t* __restrict__ szq, uint32_t* __restrict__ szq_n, uint32_t szq_cap,
-                                       uint8_t* __restrict__ mflag) {
+                                       uint8_t* __restrict__ mflag, uint32_t* __restrict__ cvq,
+                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap, uint32_t* __restrict__ mfirst) {
   bool wide = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
@@ -77,9 +78,18 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
     // (k_size_answer); its map's insertions and removals of the batch are followed (mflag bit 1)
     const uint32_t k = atomicAdd(szq_n, 1u);
     if (k < szq_cap) szq[k] = (uint32_t)i;
-    if (!(mflag[r] & kMfSize)) mflag[r] |= kMfSize;  // (a benign race: every writer stores the same bit set)
+    if (!(mflag[r] & kMfSize)) mflag_or(mflag, r, kMfSize);
     return;
   }
+  if (cvq && ty == CC_RES_MAP && o == CC_OP_MAP_CONTAINSVALUE) {
+    // MapState.containsValue (:49-60) outside TTL mode: a candidate for an answer in the stream (map_cv.hip
+    // k_cv_classify decides: a map that may hold a null at the row keeps it a barrier)
+    const uint32_t k = atomicAdd(cvq_n, 1u);
+    if (k < cvq_cap) cvq[k] = (uint32_t)i;
+    if (!(mflag[r] & kMfCv)) mflag_or(mflag, r, kMfCv);
+    return;
+  }
+  if (mfirst && ty == CC_RES_MAP && o == CC_OP_DELETE) atomicMin(&mfirst[r], (uint32_t)i);  // (k_cv_classify)
   if (!wide) {
     // not a barrier here: a row that arms a TTL timer on this map / set?
     if (!aux || !(ty == CC_RES_MAP ? ttl_op(o) && o != CC_OP_SET_ADD : o == CC_OP_SET_ADD) || (int64_t)aux[i] <= 0) return;
@@ -101,7 +111,9 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
                                                       uint32_t* __restrict__ bar, uint32_t* __restrict__ bar_n, uint32_t cap,
                                                       uint32_t* __restrict__ ttl_seen, uint32_t* __restrict__ szq,
                                                       uint32_t* __restrict__ szq_n, uint32_t szq_cap,
-                                                      uint8_t* __restrict__ mflag) {
+                                                      uint8_t* __restrict__ mflag, uint32_t* __restrict__ cvq,
+                                                      uint32_t* __restrict__ cvq_n, uint32_t cvq_cap,
+                                                      uint32_t* __restrict__ mfirst) {
   const uint64_t g = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   const uint64_t i0 = g * kMwRows;
   if (i0 >= n) return;
@@ -128,7 +140,8 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
     const uint32_t o = (wv[q / 4] >> (8 * (q % 4))) & 0xFFu;
     const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
     if (cand && i < n)
-      map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag);
+      map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag,
+                      cvq, cvq_n, cvq_cap, mfirst);
   }
 }
 
@@ -512,12 +525,14 @@ int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st) {
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
                         uint32_t* ttl_seen, uint32_t* szq, uint32_t* szq_n, uint32_t szq_cap, uint8_t* mflag,
-                        hipStream_t st) {
+                        uint32_t* cvq, uint32_t* cvq_n, uint32_t cvq_cap, uint32_t* mfirst, uint32_t R, hipStream_t st) {
   if (hipMemsetAsync(bar_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (szq_n && hipMemsetAsync(szq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (cvq_n && hipMemsetAsync(cvq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (mfirst && hipMemsetAsync(mfirst, 0xFF, sizeof(uint32_t) * R, st) != hipSuccess) return -1;
   const uint64_t groups = (n + kMwRows - 1) / kMwRows;
   hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((groups + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
-                     res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag);
+                     res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag, cvq, cvq_n, cvq_cap, mfirst);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -673,7 +688,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
         if (map_row)  // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip)
           map_event(x >> 2, code, 2 * ((uint64_t)map_row[g] - lo) + 1, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val,
                     ev_pay, ev_cap, sm_ctl, err);
-        else if (msmall && msmall[x >> 2])  // small-window or size-queried map (map_small.hip)
+        else if (msmall && (msmall[x >> 2] & (kMfSmall | kMfSize)))  // small-window or size-queried map (map_small.hip)
           map_event(x >> 2, code, xrec[g].idx - *idx0p, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_pay, ev_cap,
                     sm_ctl, err);
       }

@@ -66,6 +66,7 @@ def lib():
             "cc_memcpy": (i32, [P, P, u64, i32, P]),
             "cc_memset": (i32, [P, i32, u64, P]),
             "cc_applied_index": (i32, [P, P]),
+            "cc_engine_counters": (i32, [P, P, u32]),
             "cc_applied_index_async": (i32, [P, P, P]),
             "cc_read_value_state": (i32, [P, u32, u32, P, P, P]),
             "cc_read_value_retained": (i32, [P, u32, u32, P]),
@@ -374,6 +375,12 @@ class Engine:
 
     def stream(self):
         return self.L.cc_engine_stream(self.h)
+
+    def counters(self):
+        """(barrier rows applied, containsValue rows answered in the stream, sub-batches) since creation."""
+        out = np.zeros(3, np.uint64)
+        _check(self.L.cc_engine_counters(self.h, out.ctypes.data, 3))
+        return tuple(int(x) for x in out)
 
     def applied_index(self):
         out = C.c_uint64()

@@ -10,6 +10,8 @@ for w in "$@"; do
   case $w in
     c2) A="--steps 20 --warmup 2";;
     c3) A="--workload c3 --steps 2 --warmup 1";;
+    c3cv) A="--workload c3 --steps 2 --warmup 1 --cv-rate 0.001";;
+    c3w) A="--workload c3 --steps 1 --warmup 1 --cv-rate 0.001 --clear-rate 0.0001";;
     c4) A="--workload c4 --steps 50 --warmup 5";;
     c5) A="--workload c5 --steps 4 --warmup 1";;
   esac

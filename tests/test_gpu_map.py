@@ -294,6 +294,80 @@ def test_map_wide_ops_parity(n, maps, keys, rate, sub_batch, hot, p_hot, seed):
     assert (wide == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_INT)).any()  # some size rows landed on live maps
 
 
+def _cv_rows(b, rate, seed, clear_rate=0.0):
+    """Turn a share of a stream's rows into containsValue rows whose operand is the value an earlier put of the same
+    map stored (so many answers are true), and another share into clears."""
+    rng = np.random.default_rng(seed)
+    n = len(b)
+    rows = np.nonzero(rng.random(n) < rate)[0]
+    puts = np.nonzero(b.op == abi.CC_OP_MAP_PUT)[0]
+    back = np.searchsorted(puts, rows) - 1 - rng.integers(0, 40, len(rows))
+    src = puts[np.clip(back, 0, len(puts) - 1)]
+    inst, a, tag = b.inst[src].copy(), b.a[src].copy(), (b.flags[src] & np.uint8(7)).copy()
+    b.op[rows] = abi.CC_OP_MAP_CONTAINSVALUE
+    b.inst[rows] = inst
+    b.a[rows] = a
+    b.flags[rows] = tag
+    if clear_rate:
+        cl = np.nonzero(rng.random(n) < clear_rate)[0]
+        cl = cl[b.op[cl] != abi.CC_OP_MAP_CONTAINSVALUE]
+        b.op[cl] = abi.CC_OP_MAP_CLEAR
+    return rows
+
+
+@pytest.mark.parametrize("n,maps,keys,sub_batch,hot,p_hot,seed", [
+    (3_000, 2, 16, 0, 0, 0.0, 301),
+    (100_000, 16, 64, 8192, 2, 0.3, 302),
+    (400_000, 64, 256, 32768, 4, 0.4, 303),
+])
+def test_map_contains_value_in_stream_parity(n, maps, keys, sub_batch, hot, p_hot, seed):
+    """containsValue answered in the stream (map_cv.hip): maps with even slots store no null, so their containsValue
+    rows need no barrier; odd maps keep their nulls (their rows stay barriers, answered in HashMap order), and one even
+    map stores a null mid-batch (its rows after that become barriers).  Operands are values the stream stored; clears,
+    hot keys and several sub-batches run through the same batch.  Every row and every map as the oracle has them."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed, hot=hot, p_hot=p_hot)
+    even = (b.inst % 2) == 0
+    f = b.flags
+    ta, tb = f & 7, (f >> 3) & 7
+    f[even & (ta == abi.CC_TAG_NULL)] |= np.uint8(abi.CC_TAG_LONG)
+    f[even & (tb == abi.CC_TAG_NULL)] |= np.uint8(abi.CC_TAG_LONG << 3)
+    rows = _cv_rows(b, 0.02, seed, clear_rate=0.0005)
+    mid = n // 2
+    b.op[mid], b.inst[mid], b.flags[mid] = abi.CC_OP_MAP_PUT, 0, np.uint8(abi.CC_TAG_NULL)  # a null into map 0
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch)
+    c0 = E.counters()
+    gs, gv, os_, ov = _apply_both(E, O, [b])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    c1 = E.counters()
+    assert c1[1] > c0[1]  # rows answered in the stream
+    assert c1[0] > c0[0]  # and barrier rows (odd maps, map 0 after its null, clears)
+    ok_bool = gs[rows] == abi.cc_status(abi.CC_ST_OK, abi.CC_TAG_BOOL)
+    assert (gv[rows][ok_bool] == 1).any() and (gv[rows][ok_bool] == 0).any()
+
+
+def test_map_contains_value_in_stream_zipf():
+    """The c3 stream (Zipf 0.99 over 1M (map, key) pairs, 4096 maps, hot keys) with 0.1 % containsValue rows (operands:
+    values stored shortly before, 64-bit: fingerprinted operands) and 0.01 % clears: every containsValue row is
+    answered in the stream, every row as the oracle has it."""
+    from copycat_amd.workload import map_zipf_rows
+
+    n, maps = 2_000_000, 4096
+    b = map_zipf_rows(0, n, maps=maps)
+    rows = _cv_rows(b, 0.001, 911, clear_rate=0.0001)
+    E, O = _engines(maps, maps, n, 1 << 20)
+    c0 = E.counters()
+    gs, gv, os_, ov = _apply_both(E, O, [b])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(0, maps, 97))
+    c1 = E.counters()
+    assert c1[1] - c0[1] == len(rows)
+    assert (gv[rows] == 1).any() and (gv[rows] == 0).any()
+
+
 def test_map_contains_value_iteration_order():
     """A map holding both null values and matches: containsValue NPEs iff a null comes first in
     java.util.HashMap iteration order (A5, MapState.java:52).  Puts only, so the peak size (and with it the
