@@ -149,7 +149,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
                                                   const uint64_t* __restrict__ ctime, const uint64_t* __restrict__ caux,
                                                   const uint64_t* __restrict__ clock_base, bool deferred,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ rst_msz, TtlEmit te, CvCtx cv, uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ rst_msz, TtlEmit te, CvCtx cv, ClrCtx clr,
+                                                  uint32_t* __restrict__ err_out) {
   constexpr int MT = TTL ? 512 : CC_MAP_MT;  // threads (the TTL variant's LDS holds deadlines: 512-commit chunks)
   constexpr int MEPer = kMapRegion / MT;  // table entries per thread
   constexpr int kMPer = TTL ? 1 : CC_MAP_CHUNK / CC_MAP_MT;  // commits per thread per chunk
@@ -197,6 +198,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   __shared__ uint32_t wsum[MT / kWave];
   __shared__ uint32_t flag[3];
   __shared__ uint32_t used_total;
+  // the clear epoch each entry's state is at (map_clear.hip: clears in the stream; 0 = the sub-batch start)
+  __shared__ uint8_t eep[TTL ? 1 : kMapRegion];
 
   const uint32_t region = blockIdx.x, k = sb_val + region, t = threadIdx.x, w = t >> 6, l = t & 63;
   const uint64_t tb = (uint64_t)region * kMapRegion;
@@ -208,6 +211,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   if (t == 0) used_total = 0;
   for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
   for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = tnew[q] = tc1[q] = tc2[q] = 0;
+  if (!TTL)
+    for (uint32_t q = t; q < kMapRegion; q += MT) eep[q] = 0;
   {
     uint64_t ek[MEPer], ev[MEPer], edl[MEPer];
     uint32_t ew[MEPer], used = 0;
@@ -376,6 +381,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         const uint64_t brow = (uint64_t)(g[j] / kTile) * kTile + (rr >> 17);  // (mrec_ab)
         ab[j].y = 0;
         if (op == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(m[j])) != CC_TAG_NULL) ab[j].y = cb[row0 + brow];
+        if (!TTL && clr.mflag && (clr.mflag[res[j]] & kMfClr))  // its map is cleared in this sub-batch: its epoch
+          m[j] |= clr_epoch(clr, res[j], row0 + brow) << kMetaEpochShift;
         keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
         ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
         p[j] = (uint32_t)map_hash(res[j], CC_FLAG_KTAG(smeta_flags(m[j])), key[j]) & (kMapRegion - 1);
@@ -572,6 +579,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           const uint32_t e = rent[s];
           hd[q] = s == ecnt[e];
           el[q] = pc_element(rmeta[s], s);
+          // a clear since the entry's previous commit (or the epoch its state is at): absent first (CLEAR . el)
+          if (!TTL && (rmeta[s] >> kMetaEpochShift) != (hd[q] ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift))
+            el[q].P = el[q].A;
         }
         c = hd[q] ? el[q] : pc_compose(c, el[q]);
         ch |= hd[q];
@@ -605,7 +615,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         if (l > 0) pre = oh ? o : pc_compose(pre, o);
       }
       // walk this thread's commits from its prefix
-      uint32_t fe[kMPer], fw[kMPer], fcr[kMPer], fir[kMPer];
+      uint32_t fe[kMPer], fw[kMPer], fcr[kMPer], fir[kMPer], fep[kMPer];
       uint64_t fv[kMPer];
       bool fin[kMPer];
       PComp cur = pre;
@@ -621,6 +631,11 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         uint32_t sw, svr, snr;
         uint64_t sv;
         pc_materialize(cur, tword[e], tval[e], rmeta, rab, sw, sv, svr, snr);
+        const uint32_t ep = mm >> kMetaEpochShift;
+        if (!TTL && ep != (hd[q] ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift)) {  // cleared before it
+          sw &= ~(kMwPresent | kMwVtagMask);
+          sv = 0;
+        }
         uint64_t rv;
         bool wrote, created;
         const u64x2 x = rab[s];
@@ -628,7 +643,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         const uint32_t sw0 = sw;
         const uint64_t sv0 = sv;
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, sw, sv, rv, wrote, created);
-        if (!TTL) cv_change(cv, sw0, sv0, sw, sv, [&]() { return xr[rpos[s]].idx; }, err);
+        if (!TTL) cv_change(cv, sw0, sv0, sw, sv, [&]() { return xr[rpos[s]].idx; }, ep, err);
         ress[rci[s]] = (uint8_t)st;
         resv[rci[s]] = rv;
         resd[rci[s]] = (int8_t)(((sw & kMwPresent) != 0) - was);
@@ -637,6 +652,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
           fin[q] = true;
           fe[q] = e;
+          fep[q] = ep;
           uint32_t vr, nr;
           pc_materialize(cur, tword[e], tval[e], rmeta, rab, fw[q], fv[q], vr, nr);
           fcr[q] = vr != kOrig ? rpos[vr] : kNoRef;  // the rewriting commit's staging position
@@ -651,6 +667,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         tval[fe[q]] = fv[q];
         if (fcr[q] != kNoRef) tcr[fe[q]] = fcr[q];
         if (fir[q] != kNoRef) tir[fe[q]] = fir[q];
+        if (!TTL) eep[fe[q]] = (uint8_t)fep[q];
       }
     }
     PH(5);
@@ -676,11 +693,16 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           vv = 0;
           dl = 0;
         }
+        const uint32_t ep = mm >> kMetaEpochShift;
+        if (!TTL && ep != (s == s0 ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift)) {  // cleared before it
+          wv &= ~(kMwPresent | kMwVtagMask);
+          vv = 0;
+        }
         const int was = (wv & kMwPresent) != 0;  // (after the expiry: the commit's own change)
         const uint32_t wv0 = wv;
         const uint64_t vv0 = vv;
         const uint32_t st = map_apply(smeta_op(mm), smeta_flags(mm), x.x, x.y, wv, vv, rv, wrote, created);
-        if (!TTL) cv_change(cv, wv0, vv0, wv, vv, [&]() { return xr[rpos[s]].idx; }, err);
+        if (!TTL) cv_change(cv, wv0, vv0, wv, vv, [&]() { return xr[rpos[s]].idx; }, ep, err);
         if (TTL) {  // a stored commit cancels the old timer and arms its own; a removal cancels it
           if (wrote) dl = rdl[s];
           else if (!(wv & kMwPresent)) dl = 0;
@@ -695,6 +717,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       tword[e] = wv;
       tval[e] = vv;
       if (TTL) tdl[e] = dl;
+      else eep[e] = (uint8_t)(rmeta[s1 - 1] >> kMetaEpochShift);
       if (any_w) tcr[e] = ci;
       if (any_c) tir[e] = ins;
     }
@@ -713,6 +736,21 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     PH(6);
   }
 
+  // ---- clears in the stream: an entry whose state predates its map's last clear of the sub-batch is dropped
+  //      (k_map_drop's DEAD; the keys it held count toward the map's peak-size bound, as at a barrier clear) ----
+  if (!TTL && clr.mflag) {
+#pragma unroll
+    for (int q = 0; q < MEPer; ++q) {
+      const uint32_t e = q * MT + t;
+      const uint32_t wv = tword[e];
+      if (!(wv & kMwUsed) || (wv & kMwDead)) continue;
+      const uint32_t ms = wv & kMwSlotMask;
+      if ((clr.mflag[ms] & kMfClr) && eep[e] < clr.eend[ms]) {
+        tword[e] = (wv & ~(kMwPresent | kMwVtagMask)) | kMwDead;
+        if (dropped) atomicAdd(&dropped[ms], 1ull);
+      }
+    }
+  }
   // ---- write the region back ----
 #pragma unroll
   for (int q = 0; q < MEPer; ++q) {
@@ -749,11 +787,11 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.ttl)
     hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
-                       a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, CvCtx{}, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, CvCtx{}, ClrCtx{}, a.err);
   else
     hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, nullptr, nullptr, nullptr, nullptr, nullptr, false,
-                       a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.cv, a.err);
+                       a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.cv, a.clr, a.err);
   a.mark(K_APPLY_MAP, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
     return false;  // a full region leaves the key cold
   };
   // a map still in its small-table window is followed commit by commit through its regions (map_small.hip)
-  auto small_map = [&](uint32_t id) { return msmall != nullptr && (msmall[id & kMwSlotMask] & (kMfSmall | kMfSize)) != 0; };
+  auto small_map = [&](uint32_t id) { return msmall != nullptr && (msmall[id & kMwSlotMask] & (kMfSmall | kMfSize | kMfClr)) != 0; };
   uint32_t pos = 0;
   const bool found = valid && !small_map(ident) && probe(false, pos);
   __shared__ uint32_t bpos[kHotMax];
@@ -505,7 +505,7 @@ __device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint
     const uint32_t w0 = w;
     const uint64_t v0 = v;
     st = map_apply(op, smeta_flags(m), x.x, x.y, w, v, rv, wrote, created);
-    cv_change(cv, w0, v0, w, v, [&]() { return idx; }, err);
+    cv_change(cv, w0, v0, w, v, [&]() { return idx; }, 0u, err);  // (cleared maps are not hot-routed: epoch 0)
     if (wrote) ci = idx;
     if (created) ins = idx;
   }

@@ -448,6 +448,9 @@ constexpr uint32_t kSmAmbig = 8u;    // a tree order the engine cannot know (two
 constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
 // bit 2: the batch answers containsValue rows of the map in the stream (map_cv.hip): its commits report value changes
 constexpr uint8_t kMfCv = 4u;
+// bit 3: the batch clears the map in the stream (map_clear.hip): its sizes come from event replay, its keys are not
+// hot-routed, and its commits carry their clear epoch
+constexpr uint8_t kMfClr = 8u;
 // the flag bytes are set by concurrent threads of one kernel: OR through the aligned word (the array is padded to it)
 __device__ inline void mflag_or(uint8_t* mflag, uint32_t m, uint8_t bit) {
   atomicOr(reinterpret_cast<uint32_t*>(mflag + (m & ~3u)), (uint32_t)bit << (8 * (m & 3u)));
@@ -605,7 +608,7 @@ __device__ inline void cv_event(const CvCtx& cv, uint32_t q, uint64_t d, uint32_
 // count events of the values that left and entered it.  idx(): the commit's log index (read only on an event).
 template <class IdxF>
 __device__ inline void cv_change(const CvCtx& cv, uint32_t w0, uint64_t v0, uint32_t w1, uint64_t v1, IdxF idx,
-                                 uint32_t& err) {
+                                 uint32_t ep, uint32_t& err) {
   if (!cv.set) return;
   const uint32_t m = w1 & kMwSlotMask;
   if (!(cv.mflag[m] & kMfCv)) return;
@@ -616,8 +619,31 @@ __device__ inline void cv_change(const CvCtx& cv, uint32_t w0, uint64_t v0, uint
   const uint32_t q1 = p1 ? cv_find(cv.set, cv.mask, m, t1, t1 ? v1 : 0) : ~0u;
   if (q0 == ~0u && q1 == ~0u) return;
   const uint64_t d = idx() - *cv.idx0p;
-  if (q0 != ~0u) cv_event(cv, q0, d, 0u, 0u, err);
-  if (q1 != ~0u) cv_event(cv, q1, d, 1u, 0u, err);
+  if (q0 != ~0u) cv_event(cv, q0, d, 0u, ep, err);  // (value: the commit's clear epoch, map_clear.hip)
+  if (q1 != ~0u) cv_event(cv, q1, d, 1u, ep, err);
 }
 
+
+// ---- clear in the stream (map_clear.hip) ------------------------------------------------------------------------
+// A batch's in-stream clears as (map slot << 32 | row) sorted, with per-map offsets; per sub-batch, for every map the
+// clears before the sub-batch (base) and within it (eend, < 128).  A commit's epoch = the clears of its map in
+// [lo, row): a commit whose epoch differs from the one its entry was last at sees the entry absent first.
+struct ClrCtx {
+  const uint8_t* mflag;     // null: no clears in this sub-batch
+  const uint64_t* clr;      // [n] (slot << 32 | row), ascending
+  const uint32_t* off;      // [R + 1]
+  const uint32_t* base;     // [R] clears of the map before this sub-batch (positions in clr from off[m])
+  const uint8_t* eend;      // [R] clears of the map in this sub-batch
+  uint64_t lo;              // the sub-batch's first row
+};
+constexpr uint32_t kMetaEpochShift = 25;  // MRec meta bits 25-31 (in LDS, k_apply_map): the commit's clear epoch
+__device__ inline uint32_t clr_epoch(const ClrCtx& c, uint32_t m, uint64_t row) {
+  uint32_t a = c.off[m], b = c.off[m + 1];
+  const uint64_t k = ((uint64_t)m << 32) | row;
+  while (a < b) {
+    const uint32_t mid = (a + b) >> 1;
+    if (c.clr[mid] < k) a = mid + 1; else b = mid;
+  }
+  return a - c.off[m] - c.base[m];
+}
 }  // namespace cc

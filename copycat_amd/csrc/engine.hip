@@ -102,7 +102,8 @@ static void free_all(cc_engine* e) {
                   e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb,
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
                   e->d_cvset,    e->d_cvcnt,    e->d_cvev_key, e->d_cvev_key2, e->d_cvev_val, e->d_cvev_val2, e->d_cvev_ctl,
-                  e->d_cvseg,    e->d_cvtemp};
+                  e->d_cvseg,    e->d_cvtemp,   e->d_clrq,    e->d_clrq_n,   e->d_clr_keys,   e->d_clr_keys2, e->d_clr_off,
+                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -189,6 +190,42 @@ static int cv_rows(cc_engine* e, uint32_t n2, hipStream_t st) {
   HIPCHECK(hipStreamSynchronize(st));
   return CC_OK;
 }
+// clears in the stream (map_clear.hip): the batch's list sorted by (map, row) with per-map offsets on the device; the
+// host keeps the rows of any map cleared 128 times or more (a sub-batch holds at most 127 clears of one map)
+static int clr_rows(cc_engine* e, uint32_t n, const cc_batch* c, hipStream_t st) {
+  e->clr_n = n;
+  e->clr_heavy.clear();
+  if (n == 0) return CC_OK;
+  ClrBatchArgs cb{};
+  cb.rows = e->d_clrq;
+  cb.n = n;
+  cb.inst = c->inst;
+  cb.inst_res = e->d_inst_res;
+  cb.keys = e->d_clr_keys;
+  cb.keys2 = e->d_clr_keys2;
+  cb.off = e->d_clr_off;
+  cb.R = e->cfg.max_resources;
+  cb.temp = e->d_clr_temp;
+  cb.temp_bytes = e->clr_temp_bytes;
+  if (launch_clr_batch(cb, st)) return set_err(CC_ERR_HIP, "clear list launch", hipGetLastError());
+  if (n >= 128) {
+    std::vector<uint64_t> keys(n);
+    HIPCHECK(hipMemcpyAsync(keys.data(), e->d_clr_keys2, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    for (uint32_t a = 0; a < n;) {
+      uint32_t b = a;
+      while (b < n && (keys[b] >> 32) == (keys[a] >> 32)) ++b;
+      if (b - a >= 128) {
+        std::vector<uint32_t> rows(b - a);
+        for (uint32_t q = a; q < b; ++q) rows[q - a] = (uint32_t)keys[q];
+        e->clr_heavy.push_back(std::move(rows));
+      }
+      a = b;
+    }
+  }
+  return CC_OK;
+}
+
 // the operand set (sized for kCvMaxRows operands) and the event buffers (two events per commit, one per query)
 static int ensure_cv(cc_engine* e) {
   if (e->d_cvset) return CC_OK;
@@ -872,6 +909,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   uint64_t clock_before = 0;  // the engine clock before this batch (TTL mode and barrier rows need it on the host)
   e->szq_n = 0;
   e->isc_rows.clear();
+  e->clr_n = 0;
+  e->clr_heavy.clear();
   if (e->map_bits || e->coord_on) {
     uint32_t nb = 0, ttl_seen = 0;
     // Outside TTL mode map size / isEmpty rows are answered in the stream (listed in szq, their maps flagged); a batch
@@ -890,6 +929,16 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         HIPCHECK(hipMalloc(&e->d_cvq_n, sizeof(uint32_t) * 2));
         HIPCHECK(hipMalloc(&e->d_mfirst, sizeof(uint32_t) * e->cfg.max_resources));
         HIPCHECK(hipMalloc(&e->d_maynull, e->cfg.max_resources));
+        e->clrq_cap = 1u << 20;  // clears in the stream (map_clear.hip)
+        HIPCHECK(hipMalloc(&e->d_clrq, sizeof(uint32_t) * e->clrq_cap));
+        HIPCHECK(hipMalloc(&e->d_clrq_n, sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&e->d_clr_keys, sizeof(uint64_t) * e->clrq_cap));
+        HIPCHECK(hipMalloc(&e->d_clr_keys2, sizeof(uint64_t) * e->clrq_cap));
+        HIPCHECK(hipMalloc(&e->d_clr_off, sizeof(uint32_t) * (e->cfg.max_resources + 1)));
+        HIPCHECK(hipMalloc(&e->d_clr_base, sizeof(uint32_t) * e->cfg.max_resources));
+        HIPCHECK(hipMalloc(&e->d_clr_eend, e->cfg.max_resources));
+        e->clr_temp_bytes = std::max<size_t>(clr_sort_temp_bytes(e->clrq_cap), 256);
+        HIPCHECK(hipMalloc(&e->d_clr_temp, e->clr_temp_bytes));
       }
       if (e->szq_flagged) {
         if (launch_mflag_clear(e->d_msmall, e->cfg.max_resources, st)) return set_err(CC_ERR_HIP, "map flags", hipGetLastError());
@@ -900,7 +949,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
                               e->d_bar_n, kBarCap, e->d_ttl_seen, inline_size ? e->d_szq : nullptr,
                               inline_size ? e->d_szq_n : nullptr, e->szq_cap, e->d_msmall,
                               inline_size ? e->d_cvq : nullptr, inline_size ? e->d_cvq_n : nullptr, e->cvq_cap,
-                              inline_size ? e->d_mfirst : nullptr, e->cfg.max_resources, st))
+                              inline_size ? e->d_mfirst : nullptr, e->cfg.max_resources,
+                              inline_size ? e->d_clrq : nullptr, inline_size ? e->d_clrq_n : nullptr, e->clrq_cap, st))
         return set_err(CC_ERR_HIP, "map barrier scan launch", hipGetLastError());
       if (inline_size) {  // containsValue candidates: in the stream, or barriers (map_cv.hip)
         CvBatchArgs cb{};
@@ -926,15 +976,16 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         cb.isc_n = e->d_cvq_n + 1;
         if (launch_cv_batch(cb, st)) return set_err(CC_ERR_HIP, "containsValue classify launch", hipGetLastError());
       }
-      uint32_t qn = 0, cvn[2] = {0, 0};
+      uint32_t qn = 0, cvn[2] = {0, 0}, cln = 0;
       HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
       if (inline_size) HIPCHECK(hipMemcpyAsync(&qn, e->d_szq_n, sizeof qn, hipMemcpyDeviceToHost, st));
       if (inline_size) HIPCHECK(hipMemcpyAsync(cvn, e->d_cvq_n, sizeof cvn, hipMemcpyDeviceToHost, st));
+      if (inline_size) HIPCHECK(hipMemcpyAsync(&cln, e->d_clrq_n, sizeof cln, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
       if (!inline_size) break;
-      e->szq_flagged = qn > 0 || cvn[0] > 0;
+      e->szq_flagged = qn > 0 || cvn[0] > 0 || cln > 0;
       if (ttl_seen || pass > 1) {  // this batch turns TTL mode on: size / isEmpty / containsValue become barriers again
         inline_size = false;
         continue;
@@ -944,6 +995,19 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         e->d_szq = nullptr;
         e->szq_cap = qn;
         HIPCHECK(hipMalloc(&e->d_szq, sizeof(uint32_t) * e->szq_cap));
+        continue;
+      }
+      if (cln > e->clrq_cap) {
+        HIPCHECK(hipFree(e->d_clrq));
+        HIPCHECK(hipFree(e->d_clr_keys));
+        HIPCHECK(hipFree(e->d_clr_keys2));
+        HIPCHECK(hipFree(e->d_clr_temp));
+        e->clrq_cap = cln;
+        HIPCHECK(hipMalloc(&e->d_clrq, sizeof(uint32_t) * e->clrq_cap));
+        HIPCHECK(hipMalloc(&e->d_clr_keys, sizeof(uint64_t) * e->clrq_cap));
+        HIPCHECK(hipMalloc(&e->d_clr_keys2, sizeof(uint64_t) * e->clrq_cap));
+        e->clr_temp_bytes = std::max<size_t>(clr_sort_temp_bytes(e->clrq_cap), 256);
+        HIPCHECK(hipMalloc(&e->d_clr_temp, e->clr_temp_bytes));
         continue;
       }
       if (cvn[0] > e->cvq_cap) {
@@ -957,6 +1021,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       e->szq_n = qn;
       int rc = cv_rows(e, cvn[1], st);  // the in-stream rows, sorted, on the host too
       if (rc) return rc;
+      if ((rc = clr_rows(e, cln, c, st))) return rc;  // the in-stream clears: sorted by (map, row), offsets
       break;
     }
     if (ttl_seen && !e->ttl_live) {  // TTL mode for good: sizes and capacities from commit + expiry events
@@ -1113,6 +1178,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   const uint64_t seg_hi = action == 2 ? tim_b : (action == 1 ? bar_b : n);
   for (uint64_t lo = seg_lo, hi; lo < seg_hi; lo = hi) {
     hi = std::min(seg_hi, lo + e->sub_batch);
+    for (const auto& hv : e->clr_heavy) {  // at most 127 in-stream clears of one map per sub-batch (map_clear.hip)
+      const size_t q = (size_t)(std::lower_bound(hv.begin(), hv.end(), (uint32_t)lo) - hv.begin());
+      if (q + 127 < hv.size() && hv[q + 127] < hi) hi = hv[q + 127];
+    }
     // this sub-batch's in-stream containsValue rows (at most kCvMaxRows: a denser run ends the sub-batch earlier)
     size_t cv_b = 0, cv_e = 0;
     if (!e->isc_rows.empty()) {
@@ -1124,7 +1193,33 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       }
     }
     const uint32_t cv_n = (uint32_t)(cv_e - cv_b);
+    const bool clr_on = e->clr_n > 0;  // clears in the stream in this batch (map_clear.hip)
+    ClrSubArgs ca{};
+    ClrCtx cctx{};
+    if (clr_on) {
+      int rc = ensure_small(e);  // (the cleared maps' sizes ride the map event buffer)
+      if (rc) return rc;
+      ca.keys = e->d_clr_keys2;
+      ca.n = e->clr_n;
+      ca.off = e->d_clr_off;
+      ca.R = e->cfg.max_resources;
+      ca.lo = lo;
+      ca.hi = hi;
+      ca.base = e->d_clr_base;
+      ca.eend = e->d_clr_eend;
+      ca.err = e->d_err;
+      ca.index = c->index;
+      ca.ev_key = e->d_sm_key;
+      ca.ev_val = e->d_sm_val;
+      ca.ev_pay = e->d_sm_pay;
+      ca.ev_cap = (uint32_t)e->sm_cap;
+      ca.ev_ctl = e->d_sm_ctl;
+      ca.cgen = e->d_mw_cgen;
+      if (launch_clr_sub(ca, st)) return set_err(CC_ERR_HIP, "clear epochs launch", hipGetLastError());
+      cctx = ClrCtx{e->d_msmall, e->d_clr_keys2, e->d_clr_off, e->d_clr_base, e->d_clr_eend, lo};
+    }
     CvSubArgs cva{};
+    cva.clr = cctx;
     ++e->stat_subbatches;
     e->stat_isc += cv_n;
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
@@ -1173,7 +1268,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.hot_msz = e->d_hot_msz;
-      ha.msmall = (e->small_live || e->szq_n) ? e->d_msmall : nullptr;  // small / size-queried maps: not hot-routed
+      ha.msmall = (e->small_live || e->szq_n || clr_on) ? e->d_msmall : nullptr;  // small / size-queried / cleared maps: not hot-routed
       ha.err = e->d_err;
       ha.mark = marker_of(e);
       static const bool no_hot = diag_env("CC_NO_HOT");  // diagnostics: every key through its region
@@ -1290,6 +1385,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       if (!e->ttl_live && launch_map_hot_apply(ha, st)) return set_err(CC_ERR_HIP, "hot-key apply launch", hipGetLastError());
       MapArgs ma{};
       ma.cv = cva.cv;
+      ma.clr = cctx;
       ma.mrec = e->d_mrec;
       ma.cb = c->b;
       ma.lo = lo;
@@ -1330,6 +1426,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         ma.ttl_emit = te;
       }
       if (launch_apply_map(ma, st)) return set_err(CC_ERR_HIP, "map apply launch", hipGetLastError()); DBG_SYNC("map apply launch");
+      if (clr_on && launch_clr_gen(ca, st)) return set_err(CC_ERR_HIP, "clear generation launch", hipGetLastError());
       if (e->ttl_live) {  // exact sizes and capacities in TTL mode: the sub-batch's commits and expiries as events
         if (launch_ttl_scan(te, e->d_clock, e->d_tbl_word, e->d_tbl_key, e->d_tbl_dl, e->map_entries, e->d_err, st))
           return set_err(CC_ERR_HIP, "TTL scan launch", hipGetLastError());
@@ -1400,7 +1497,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.lvl_at = e->d_lvl_at;
         za.index = c->index;
         za.lo = lo;
-        if (e->small_live || e->szq_n) {  // small-window / size-queried maps: their insertions / removals (map_small.hip)
+        if (e->small_live || e->szq_n || clr_on) {  // small / size-queried / cleared maps: their insertions / removals
           int rc = ensure_small(e);
           if (rc) return rc;
           if (!c->index) return set_err(CC_ERR_INVALID, "an engine with maps needs the index column (log order)");
@@ -1440,7 +1537,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sz.out_value = out->value;
           if (launch_size_emit(sz, st)) return set_err(CC_ERR_HIP, "size query launch", hipGetLastError());
         }
-        if (e->small_live || e->szq_n) {
+        if (clr_on && launch_clr_events(ca, st)) return set_err(CC_ERR_HIP, "clear events launch", hipGetLastError());
+        if (e->small_live || e->szq_n || clr_on) {
           uint32_t ctl[2] = {0, 0};
           HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
           HIPCHECK(hipStreamSynchronize(st));
@@ -1527,6 +1625,23 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (sized) {  // size / isEmpty answers over the unpermute's placeholders; then the next sub-batch's counters
       if (e->szq_n && sized_events && launch_size_answer(sz, st))
         return set_err(CC_ERR_HIP, "size answer launch", hipGetLastError());
+      if (clr_on && sized_events) {  // the cleared maps' sizes, capacities and size / isEmpty rows (map_clear.hip)
+        ClrReplayArgs cr{};
+        cr.key = e->d_sm_key2;
+        cr.val = e->d_sm_val2;
+        cr.pay = e->d_sm_pay;
+        cr.ctl = e->d_sm_ctl;
+        cr.seg = e->d_sm_seg;
+        cr.nseg = e->d_sm_seg + e->cfg.max_resources;
+        cr.mflag = e->d_msmall;
+        cr.msize = e->d_msize;
+        cr.mpcap = e->d_mpcap;
+        cr.lvl_at = e->d_lvl_at;
+        cr.idx0 = c->index + lo;
+        cr.out_status = out->status;
+        cr.out_value = out->value;
+        if (launch_clr_replay(cr, st)) return set_err(CC_ERR_HIP, "clear replay launch", hipGetLastError());
+      }
       SmallArgs sf{};
       sf.ctl = e->d_sm_ctl;
       sf.msmall = e->d_msmall;

@@ -100,6 +100,7 @@ int launch_selfcheck(uint32_t* d_bad, hipStream_t st);
 
 struct MapArgs {
   CvCtx cv{};          // in-stream containsValue (map_cv.hip): value-change events of the flagged maps
+  ClrCtx clr{};        // clears in the stream (map_clear.hip): commit epochs, the end-of-launch drop
   const MRec* mrec;
   const uint64_t* cb;  // the batch's b column (replaceIfPresent's compare value, mrec_ab)
   uint64_t lo;         // the sub-batch's first row
@@ -247,7 +248,8 @@ constexpr uint32_t kBarCap = 1u << 16;  // barrier rows per batch
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
                         uint32_t* ttl_seen, uint32_t* szq, uint32_t* szq_n, uint32_t szq_cap, uint8_t* mflag,
-                        uint32_t* cvq, uint32_t* cvq_n, uint32_t cvq_cap, uint32_t* mfirst, uint32_t R, hipStream_t st);
+                        uint32_t* cvq, uint32_t* cvq_n, uint32_t cvq_cap, uint32_t* mfirst, uint32_t R,
+                        uint32_t* clrq, uint32_t* clrq_n, uint32_t clrq_cap, hipStream_t st);
 // ---- containsValue in the stream (map_cv.hip) ----
 struct CvBatchArgs {  // per batch: classify the candidates listed by k_map_barriers
   const uint32_t* inst;
@@ -276,6 +278,7 @@ int cv_sort_rows(uint32_t* rows, uint32_t* rows2, uint32_t n, void* temp, size_t
 size_t cv_rows_temp_bytes(uint32_t n);
 struct CvSubArgs {  // per sub-batch: the operand set, initial counts and query events, then the answers
   CvCtx cv;           // set / mask / events (the apply kernels get the same)
+  ClrCtx clr;         // clears in the stream: a query's epoch (map_clear.hip)
   CvEnt* set;
   uint32_t* cnt;      // per set position: matching entries at the sub-batch start
   const uint32_t* isc;  // this sub-batch's in-stream rows (sorted)
@@ -301,6 +304,57 @@ struct CvSubArgs {  // per sub-batch: the operand set, initial counts and query 
   uint64_t* out_value;
 };
 int launch_cv_prepare(const CvSubArgs& a, hipStream_t st);
+// ---- clear in the stream (map_clear.hip) ----
+struct ClrBatchArgs {
+  const uint32_t* rows;  // the batch's in-stream clear rows
+  uint32_t n;
+  const uint32_t* inst;
+  const uint32_t* inst_res;
+  uint64_t* keys;        // [n] scratch
+  uint64_t* keys2;       // [n] (slot << 32 | row), ascending
+  uint32_t* off;         // [R + 1]
+  uint32_t R;
+  void* temp;
+  size_t temp_bytes;
+};
+int launch_clr_batch(const ClrBatchArgs& a, hipStream_t st);
+size_t clr_sort_temp_bytes(uint32_t n);
+struct ClrSubArgs {
+  const uint64_t* keys;  // sorted
+  uint32_t n;
+  const uint32_t* off;
+  uint32_t R;
+  uint64_t lo, hi;
+  uint32_t* base;
+  uint8_t* eend;
+  uint32_t* err;
+  const uint64_t* index;
+  uint64_t* ev_key;
+  uint32_t* ev_val;
+  EvPay* ev_pay;
+  uint32_t ev_cap;
+  uint32_t* ev_ctl;
+  uint64_t* cgen;
+};
+int launch_clr_sub(const ClrSubArgs& a, hipStream_t st);
+int launch_clr_events(const ClrSubArgs& a, hipStream_t st);
+int launch_clr_gen(const ClrSubArgs& a, hipStream_t st);
+struct ClrReplayArgs {
+  const uint64_t* key;
+  const uint32_t* val;
+  const EvPay* pay;
+  const uint32_t* ctl;
+  const uint32_t* seg;
+  const uint32_t* nseg;
+  const uint8_t* mflag;
+  uint32_t* msize;
+  uint32_t* mpcap;
+  unsigned long long* lvl_at;
+  const uint64_t* idx0;
+  uint8_t* out_status;
+  uint64_t* out_value;
+};
+int launch_clr_replay(const ClrReplayArgs& a, hipStream_t st);
 int launch_cv_answer(const CvSubArgs& a, uint32_t E, hipStream_t st);
 size_t cv_sort_temp_bytes(uint32_t cap);
 struct MapWideArgs {

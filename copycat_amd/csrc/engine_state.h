@@ -220,6 +220,19 @@ struct cc_engine {
   size_t cvtemp_bytes = 0;
   uint32_t cvev_cap = 0;
   uint64_t stat_barriers = 0, stat_isc = 0, stat_subbatches = 0;  // cc_engine_counters
+  // clears in the stream (map_clear.hip)
+  uint32_t* d_clrq = nullptr;      // [clrq_cap] the batch's in-stream clear rows
+  uint32_t* d_clrq_n = nullptr;
+  uint32_t clrq_cap = 0;
+  uint64_t* d_clr_keys = nullptr;  // [clrq_cap] scratch, then (slot << 32 | row) ascending in d_clr_keys2
+  uint64_t* d_clr_keys2 = nullptr;
+  uint32_t* d_clr_off = nullptr;   // [max_resources + 1]
+  uint32_t* d_clr_base = nullptr;  // [max_resources]
+  uint8_t* d_clr_eend = nullptr;   // [max_resources]
+  void* d_clr_temp = nullptr;
+  size_t clr_temp_bytes = 0;
+  uint32_t clr_n = 0;              // this batch's
+  std::vector<std::vector<uint32_t>> clr_heavy;  // rows of the maps cleared >= 128 times in this batch (sub-batch cuts)
   unsigned long long* d_mw_ctl = nullptr;  // [16]
   std::vector<uint32_t> bars;
   // map TTL timers (apply_map.hip k_apply_map<true>): entered on the first map row with ttl > 0, for good

@@ -137,7 +137,9 @@ __global__ void k_cv_query(CvSubArgs a) {
       if (c == k) break;
       p = (p + 1) & a.cv.mask;
     }
-    cv_event(a.cv, p, a.index[row] - idx0, 2u, row - (uint32_t)a.lo, err);
+    // value: the row in the sub-batch | its clear epoch << 25 (map_clear.hip; 0 without clears in the stream)
+    const uint32_t ep = a.clr.mflag && (a.clr.mflag[m] & kMfClr) ? clr_epoch(a.clr, m, row) : 0u;
+    cv_event(a.cv, p, a.index[row] - idx0, 2u, (row - (uint32_t)a.lo) | (ep << 25), err);
   }
   if (err) atomicOr(a.err, err);
 }
@@ -188,7 +190,9 @@ __global__ void k_cv_seg(const uint64_t* __restrict__ key, uint32_t E, uint32_t*
     if (i == 0 || (key[i] >> 42) != (key[i - 1] >> 42)) seg[atomicAdd(nseg, 1u)] = i;
 }
 
-// one wave per operand run (sorted by log position): the running count of entries holding it; a query's answer
+// One wave per operand run (sorted by log position): the running count of entries holding it; a query's answer.
+// With clears in the stream every event carries its clear epoch (non-decreasing along the run): the count restarts
+// at 0 in each new epoch (cnt0, the count at the sub-batch start, belongs to epoch 0).
 __global__ __launch_bounds__(256) void k_cv_answer(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
                                                    uint32_t E, const uint32_t* __restrict__ seg,
                                                    const uint32_t* __restrict__ nseg, const uint32_t* __restrict__ cnt,
@@ -200,10 +204,13 @@ __global__ __launch_bounds__(256) void k_cv_answer(const uint64_t* __restrict__ 
     const uint32_t start = seg[r];
     const uint64_t q = key[start] >> 42;
     int64_t c = cnt[q];
+    uint32_t cep = 0;  // the epoch c belongs to
     for (uint32_t b = start;; b += kWave) {
       const uint32_t i = b + l;
       const bool in = i < E && (key[i] >> 42) == q;
       const uint32_t kind = in ? (uint32_t)(key[i] & 3u) : 3u;
+      const uint32_t vv = in ? val[i] : 0u;
+      const uint32_t ep = in ? (kind == 2u ? vv >> 25 : vv) : 0xFFFFFFFFu;
       const int32_t dlt = kind == 1u ? 1 : (kind == 0u ? -1 : 0);
       int32_t inc = dlt;
 #pragma unroll
@@ -211,13 +218,33 @@ __global__ __launch_bounds__(256) void k_cv_answer(const uint64_t* __restrict__ 
         const int32_t y = __shfl_up(inc, d, 64);
         if (l >= (uint32_t)d) inc += y;
       }
-      if (kind == 2u) {
-        const uint64_t row = lo + val[i];
-        out_status[row] = (uint8_t)CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
-        out_value[row] = c + inc > 0 ? 1ull : 0ull;
+      // the first lane of this lane's epoch in the chunk (epochs are non-decreasing along the run)
+      const uint32_t pep = __shfl_up(ep, 1, 64);
+      int32_t fs = (l == 0 || pep != ep) ? (int32_t)l : 0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(fs, d, 64);
+        if (l >= (uint32_t)d) fs = max(fs, y);
       }
-      c += __shfl(inc, 63, 64);
-      if (__ballot(in) != ~0ull) break;
+      // deltas before the epoch's lanes (every lane takes part in the shuffle: a lane reading an inactive one gets 0)
+      const int32_t at_prev = __shfl(inc, fs > 0 ? fs - 1 : 0, 64);
+      const int32_t before = fs == 0 ? 0 : at_prev;
+      const int64_t base = ep == cep ? c : 0;  // (a later epoch starts from an empty map)
+      if (in && kind == 2u) {
+        const uint64_t row = lo + (vv & ((1u << 25) - 1));
+        out_status[row] = (uint8_t)CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+        out_value[row] = base + (fs == 0 ? inc : inc - before) > 0 ? 1ull : 0ull;
+      }
+      // carry: the last in-lane's epoch and count
+      const uint64_t inb = __ballot(in);
+      const int32_t last = 63 - __clzll((long long)inb);
+      const uint32_t lep = (uint32_t)__shfl((int)ep, last, 64);
+      const int32_t lfs = __shfl(fs, last, 64), linc = __shfl(inc, last, 64);
+      const int32_t lat_prev = __shfl(inc, lfs > 0 ? lfs - 1 : 0, 64);
+      const int32_t lbefore = lfs == 0 ? 0 : lat_prev;
+      c = (lep == cep ? c : 0) + (lfs == 0 ? linc : linc - lbefore);
+      cep = lep;
+      if (inb != ~0ull) break;
     }
   }
 }

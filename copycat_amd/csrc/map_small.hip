@@ -72,6 +72,14 @@ __global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restric
       const uint64_t k = key[i];
       if ((uint32_t)(k >> 44) != m) break;
       if (k & 8u) continue;  // a size / isEmpty query (k_size_answer)
+      if ((k & 3u) == 3u) {  // MapState.clear in the stream (map_clear.hip): every key leaves, the table stays
+        for (uint32_t q = 0; q < 64; ++q) lm.tab[q] = 0;
+        lm.n = 0;
+        lm.used = 0;
+        lm.flags &= ~(kSmTree | kSmAmbig);
+        lm.tree_bins = 0;
+        continue;
+      }
       const EvPay x = pay[val[i]];
       if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
         const uint32_t lv0 = lm.lvl;

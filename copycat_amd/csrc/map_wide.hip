@@ -55,7 +55,8 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
                                        uint32_t* __restrict__ bar_n, uint32_t cap, uint32_t* __restrict__ ttl_seen,
                                        uint32_t* __restrict__ szq, uint32_t* __restrict__ szq_n, uint32_t szq_cap,
                                        uint8_t* __restrict__ mflag, uint32_t* __restrict__ cvq,
-                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap, uint32_t* __restrict__ mfirst) {
+                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap, uint32_t* __restrict__ mfirst,
+                                       uint32_t* __restrict__ clrq, uint32_t* __restrict__ clrq_n, uint32_t clrq_cap) {
   bool wide = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
@@ -89,6 +90,13 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
     if (!(mflag[r] & kMfCv)) mflag_or(mflag, r, kMfCv);
     return;
   }
+  if (clrq && ty == CC_RES_MAP && o == CC_OP_MAP_CLEAR) {
+    // MapState.clear (:255-274) outside TTL mode: applied in the stream as an epoch (map_clear.hip)
+    const uint32_t k = atomicAdd(clrq_n, 1u);
+    if (k < clrq_cap) clrq[k] = (uint32_t)i;
+    if (!(mflag[r] & kMfClr)) mflag_or(mflag, r, kMfClr);
+    return;
+  }
   if (mfirst && ty == CC_RES_MAP && o == CC_OP_DELETE) atomicMin(&mfirst[r], (uint32_t)i);  // (k_cv_classify)
   if (!wide) {
     // not a barrier here: a row that arms a TTL timer on this map / set?
@@ -113,7 +121,8 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
                                                       uint32_t* __restrict__ szq_n, uint32_t szq_cap,
                                                       uint8_t* __restrict__ mflag, uint32_t* __restrict__ cvq,
                                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap,
-                                                      uint32_t* __restrict__ mfirst) {
+                                                      uint32_t* __restrict__ mfirst, uint32_t* __restrict__ clrq,
+                                                      uint32_t* __restrict__ clrq_n, uint32_t clrq_cap) {
   const uint64_t g = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   const uint64_t i0 = g * kMwRows;
   if (i0 >= n) return;
@@ -141,7 +150,7 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
     const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
     if (cand && i < n)
       map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag,
-                      cvq, cvq_n, cvq_cap, mfirst);
+                      cvq, cvq_n, cvq_cap, mfirst, clrq, clrq_n, clrq_cap);
   }
 }
 
@@ -525,14 +534,17 @@ int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st) {
 int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t* aux, uint64_t n, const uint32_t* inst_res,
                         const uint8_t* res_type, uint32_t max_inst, uint32_t* bar, uint32_t* bar_n, uint32_t cap,
                         uint32_t* ttl_seen, uint32_t* szq, uint32_t* szq_n, uint32_t szq_cap, uint8_t* mflag,
-                        uint32_t* cvq, uint32_t* cvq_n, uint32_t cvq_cap, uint32_t* mfirst, uint32_t R, hipStream_t st) {
+                        uint32_t* cvq, uint32_t* cvq_n, uint32_t cvq_cap, uint32_t* mfirst, uint32_t R,
+                        uint32_t* clrq, uint32_t* clrq_n, uint32_t clrq_cap, hipStream_t st) {
   if (hipMemsetAsync(bar_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (szq_n && hipMemsetAsync(szq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (cvq_n && hipMemsetAsync(cvq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (clrq_n && hipMemsetAsync(clrq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (mfirst && hipMemsetAsync(mfirst, 0xFF, sizeof(uint32_t) * R, st) != hipSuccess) return -1;
   const uint64_t groups = (n + kMwRows - 1) / kMwRows;
   hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((groups + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
-                     res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag, cvq, cvq_n, cvq_cap, mfirst);
+                     res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag, cvq, cvq_n, cvq_cap, mfirst,
+                     clrq, clrq_n, clrq_cap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -682,13 +694,15 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     lds_barrier();
     for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
       const uint32_t x = w[p], code = x & 3u, m = (x >> 2) - base;
-      if (code && m < span) atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
+      // (a map cleared in the stream: its sizes come from event replay, map_clear.hip k_clr_replay)
+      if (code && m < span && !(msmall && (msmall[x >> 2] & kMfClr)))
+        atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
       if (code && base == 0) {
         const uint64_t g = (uint64_t)t * kTile + p;
         if (map_row)  // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip)
           map_event(x >> 2, code, 2 * ((uint64_t)map_row[g] - lo) + 1, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val,
                     ev_pay, ev_cap, sm_ctl, err);
-        else if (msmall && (msmall[x >> 2] & (kMfSmall | kMfSize)))  // small-window or size-queried map (map_small.hip)
+        else if (msmall && (msmall[x >> 2] & (kMfSmall | kMfSize | kMfClr)))  // small, size-queried or cleared map
           map_event(x >> 2, code, xrec[g].idx - *idx0p, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_pay, ev_cap,
                     sm_ctl, err);
       }

@@ -368,6 +368,41 @@ def test_map_contains_value_in_stream_zipf():
     assert (gv[rows] == 1).any() and (gv[rows] == 0).any()
 
 
+@pytest.mark.parametrize("n,maps,keys,clear_rate,sub_batch,hot,p_hot,seed", [
+    (4_000, 2, 16, 0.02, 0, 0, 0.0, 501),            # small maps (the HashMap model) cleared in the stream
+    (60_000, 4, 16, 0.05, 0, 0, 0.0, 502),           # > 127 clears of one map in one sub-batch: the host cuts it
+    (200_000, 16, 1024, 0.003, 16384, 2, 0.3, 503),  # large maps, several sub-batches, hot keys of other maps
+])
+def test_map_clear_in_stream_parity(n, maps, keys, clear_rate, sub_batch, hot, p_hot, seed):
+    """MapState.clear applied in the stream (map_clear.hip): a clear is an epoch; later commits see the map empty,
+    sizes restart at 0, the HashMap keeps its capacity.  Mixed into the same batch: size / isEmpty rows (answered by
+    the cleared maps' replay), containsValue rows on maps that store nulls (barriers, answered in HashMap order: the
+    capacity and the small maps' models went through the clears), and stored values.  Every row and map as the oracle
+    has them; no clear row is a barrier."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed, hot=hot, p_hot=p_hot)
+    rng = np.random.default_rng(seed)
+    rows = np.nonzero(rng.random(n) < clear_rate)[0]
+    b.op[rows] = abi.CC_OP_MAP_CLEAR
+    q = np.nonzero(rng.random(n) < 0.01)[0]
+    q = q[b.op[q] != abi.CC_OP_MAP_CLEAR]
+    b.op[q] = rng.choice(np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_ISEMPTY, abi.CC_OP_MAP_CONTAINSVALUE], np.uint8), len(q))
+    cv = q[b.op[q] == abi.CC_OP_MAP_CONTAINSVALUE]
+    b.a[cv] = rng.integers(0, 3, len(cv)).astype(np.uint64)
+    b.flags[cv] = (b.flags[cv] & np.uint8(0xF8)) | np.uint8(abi.CC_TAG_LONG)
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch)
+    c0 = E.counters()
+    gs, gv, os_, ov = _apply_both(E, O, [b])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    c1 = E.counters()
+    live = (b.inst[rows] < maps)
+    assert c1[0] - c0[0] <= len(q)  # barriers: containsValue rows only, never a clear
+    assert live.sum() > 0
+
+
 def test_map_contains_value_iteration_order():
     """A map holding both null values and matches: containsValue NPEs iff a null comes first in
     java.util.HashMap iteration order (A5, MapState.java:52).  Puts only, so the peak size (and with it the
