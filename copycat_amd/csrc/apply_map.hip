@@ -136,7 +136,7 @@ __device__ inline void claim_mark(uint32_t* tc1, uint32_t* tc2, uint32_t e) {
   if (atomicOr(&tc1[e >> 5], bit) & bit) atomicOr(&tc2[e >> 5], bit);
 }
 
-template <bool TTL>
+template <bool TTL, bool CLR>
 __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict__ xr, const uint64_t* __restrict__ cb, uint64_t row0,
                                                   const uint16_t* __restrict__ ttab,
                                                   uint32_t tiles, uint32_t sb, uint32_t sb_val, uint64_t* __restrict__ tbl_key,
@@ -202,6 +202,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   __shared__ uint8_t eep[TTL ? 1 : kMapRegion];
 
   const uint32_t region = blockIdx.x, k = sb_val + region, t = threadIdx.x, w = t >> 6, l = t & 63;
+  constexpr bool clr_live = !TTL && CLR;  // clears in the stream in this batch (map_clear.hip; its own instantiation)
   const uint64_t tb = (uint64_t)region * kMapRegion;
   uint32_t err = 0;
   PH_DECL
@@ -211,8 +212,6 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
   if (t == 0) used_total = 0;
   for (uint32_t q = t; q <= kMapRegion; q += MT) ecnt[q] = 0;
   for (uint32_t q = t; q < kMapRegion / 32; q += MT) eflag[q] = tnew[q] = tc1[q] = tc2[q] = 0;
-  if (!TTL)
-    for (uint32_t q = t; q < kMapRegion; q += MT) eep[q] = 0;
   {
     uint64_t ek[MEPer], ev[MEPer], edl[MEPer];
     uint32_t ew[MEPer], used = 0;
@@ -238,6 +237,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       tcr[e] = kNoRef;
       tir[e] = kNoRef;
       if (TTL) tdl[e] = compact ? 0 : edl[q];
+      else if (clr_live) eep[e] = compact ? 0 : clr.tbl_ep[tb + e];  // (a hot key's entry: its epoch after k_hot_apply)
     }
     lds_barrier();
     if (compact) {
@@ -270,6 +270,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           tbl_ins[tb + p] = eins[q];
           tbl_claim[tb + p] = ecl[q];
           if (TTL) tdl[p] = edl[q];
+          else if (clr_live) eep[p] = clr.tbl_ep[tb + q * MT + t];  // (written back only at the end of the launch)
         }
       }
       __syncthreads();
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         const uint64_t brow = (uint64_t)(g[j] / kTile) * kTile + (rr >> 17);  // (mrec_ab)
         ab[j].y = 0;
         if (op == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(m[j])) != CC_TAG_NULL) ab[j].y = cb[row0 + brow];
-        if (!TTL && clr.mflag && (clr.mflag[res[j]] & kMfClr))  // its map is cleared in this sub-batch: its epoch
+        if (clr_live && (clr.mflag[res[j]] & kMfClr))  // its map is cleared in this batch: the commit's epoch
           m[j] |= clr_epoch(clr, res[j], row0 + brow) << kMetaEpochShift;
         keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
         ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           hd[q] = s == ecnt[e];
           el[q] = pc_element(rmeta[s], s);
           // a clear since the entry's previous commit (or the epoch its state is at): absent first (CLEAR . el)
-          if (!TTL && (rmeta[s] >> kMetaEpochShift) != (hd[q] ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift))
+          if (clr_live && (rmeta[s] >> kMetaEpochShift) != (hd[q] ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift))
             el[q].P = el[q].A;
         }
         c = hd[q] ? el[q] : pc_compose(c, el[q]);
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         if (l > 0) pre = oh ? o : pc_compose(pre, o);
       }
       // walk this thread's commits from its prefix
-      uint32_t fe[kMPer], fw[kMPer], fcr[kMPer], fir[kMPer], fep[kMPer];
+      uint32_t fe[kMPer], fw[kMPer], fcr[kMPer], fir[kMPer];
       uint64_t fv[kMPer];
       bool fin[kMPer];
       PComp cur = pre;
@@ -631,8 +632,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         uint32_t sw, svr, snr;
         uint64_t sv;
         pc_materialize(cur, tword[e], tval[e], rmeta, rab, sw, sv, svr, snr);
-        const uint32_t ep = mm >> kMetaEpochShift;
-        if (!TTL && ep != (hd[q] ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift)) {  // cleared before it
+        const uint32_t ep = clr_live ? mm >> kMetaEpochShift : 0u;
+        if (clr_live && ep != (hd[q] ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift)) {  // cleared before it
           sw &= ~(kMwPresent | kMwVtagMask);
           sv = 0;
         }
@@ -652,7 +653,6 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         if (s + 1 == ecnt[e + 1]) {  // the run's last commit: the entry's new state
           fin[q] = true;
           fe[q] = e;
-          fep[q] = ep;
           uint32_t vr, nr;
           pc_materialize(cur, tword[e], tval[e], rmeta, rab, fw[q], fv[q], vr, nr);
           fcr[q] = vr != kOrig ? rpos[vr] : kNoRef;  // the rewriting commit's staging position
@@ -667,7 +667,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         tval[fe[q]] = fv[q];
         if (fcr[q] != kNoRef) tcr[fe[q]] = fcr[q];
         if (fir[q] != kNoRef) tir[fe[q]] = fir[q];
-        if (!TTL) eep[fe[q]] = (uint8_t)fep[q];
+        if (clr_live) eep[fe[q]] = (uint8_t)(rmeta[ecnt[fe[q] + 1] - 1] >> kMetaEpochShift);  // (its run's last commit)
       }
     }
     PH(5);
@@ -693,8 +693,8 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
           vv = 0;
           dl = 0;
         }
-        const uint32_t ep = mm >> kMetaEpochShift;
-        if (!TTL && ep != (s == s0 ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift)) {  // cleared before it
+        const uint32_t ep = clr_live ? mm >> kMetaEpochShift : 0u;
+        if (clr_live && ep != (s == s0 ? (uint32_t)eep[e] : rmeta[s - 1] >> kMetaEpochShift)) {  // cleared before it
           wv &= ~(kMwPresent | kMwVtagMask);
           vv = 0;
         }
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       tword[e] = wv;
       tval[e] = vv;
       if (TTL) tdl[e] = dl;
-      else eep[e] = (uint8_t)(rmeta[s1 - 1] >> kMetaEpochShift);
+      else if (clr_live) eep[e] = (uint8_t)(rmeta[s1 - 1] >> kMetaEpochShift);
       if (any_w) tcr[e] = ci;
       if (any_c) tir[e] = ins;
     }
@@ -738,7 +738,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
 
   // ---- clears in the stream: an entry whose state predates its map's last clear of the sub-batch is dropped
   //      (k_map_drop's DEAD; the keys it held count toward the map's peak-size bound, as at a barrier clear) ----
-  if (!TTL && clr.mflag) {
+  if (clr_live) {
 #pragma unroll
     for (int q = 0; q < MEPer; ++q) {
       const uint32_t e = q * MT + t;
@@ -765,6 +765,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       tbl_claim[tb + e] = one ? xr[tir[e]].idx : *idx0p;
     }
     if (TTL) tbl_dl[tb + e] = tdl[e];
+    else if (clr_live) clr.tbl_ep[tb + e] = 0;  // (the next sub-batch's hot keys write theirs before it reads)
   }
   PH(7);
   if (!TTL) PH_FLUSH(g_ph_map);
@@ -785,11 +786,15 @@ int launch_apply_map(const MapArgs& a, hipStream_t st) {
   if (a.map_bits == 0 || a.tiles == 0) return 0;
   a.mark(K_APPLY_MAP, 1, st);
   if (a.ttl)
-    hipLaunchKernelGGL(k_apply_map<true>, dim3(1u << a.map_bits), dim3(512), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+    hipLaunchKernelGGL((k_apply_map<true, false>), dim3(1u << a.map_bits), dim3(512), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, a.tbl_dl, a.map_row, a.time, a.aux, a.clock_base, a.deferred,
                        a.rst_status, a.rst_value, a.rst_msz, a.ttl_emit, CvCtx{}, ClrCtx{}, a.err);
+  else if (a.clr.mflag)
+    hipLaunchKernelGGL((k_apply_map<false, true>), dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+                       a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, nullptr, nullptr, nullptr, nullptr, nullptr, false,
+                       a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.cv, a.clr, a.err);
   else
-    hipLaunchKernelGGL(k_apply_map<false>, dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
+    hipLaunchKernelGGL((k_apply_map<false, false>), dim3(1u << a.map_bits), dim3(CC_MAP_MT), 0, st, a.mrec, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.sb_val, a.tbl_key, a.tbl_word, a.tbl_val, a.tbl_ci, a.tbl_ins,
                        a.tbl_claim, a.idx0, (unsigned long long*)a.dropped, a.cgen, a.cset, a.cset_mask, a.cset_full, nullptr, nullptr, nullptr, nullptr, nullptr, false,
                        a.rst_status, a.rst_value, a.rst_msz, TtlEmit{}, a.cv, a.clr, a.err);
   a.mark(K_APPLY_MAP, 0, st);

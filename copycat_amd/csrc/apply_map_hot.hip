@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kDetT) void k_hot_bind(const HotKey* __restrict__ c
     return false;  // a full region leaves the key cold
   };
   // a map still in its small-table window is followed commit by commit through its regions (map_small.hip)
-  auto small_map = [&](uint32_t id) { return msmall != nullptr && (msmall[id & kMwSlotMask] & (kMfSmall | kMfSize | kMfClr)) != 0; };
+  auto small_map = [&](uint32_t id) { (void)id; return false; };  // (every map's hot keys: k_hot_apply emits their events)
   uint32_t pos = 0;
   const bool found = valid && !small_map(ident) && probe(false, pos);
   __shared__ uint32_t bpos[kHotMax];
@@ -386,10 +386,39 @@ __device__ inline void hot_runs_lds(const uint32_t* __restrict__ hot_rpre, const
 }
 
 // (reads each hot commit's meta word from the compact copy k_part_ext writes, hot_meta, not from its 48-byte record)
+// A commit's clear epoch (map_clear.hip): the clears of its map in [lo, row); the row from its staging position.
+__device__ inline uint32_t hot_epoch(const HotClr& c, uint32_t slot, uint32_t g) {
+  const uint64_t row = c.lo + (uint64_t)(g / kTile) * kTile + (c.xr[g].rr >> 17);
+  return clr_epoch(c.clr, slot, row);
+}
+__device__ inline bool hot_cleared(const HotClr& c, uint32_t slot) {
+  return c.clr.mflag != nullptr && (c.clr.mflag[slot] & kMfClr) != 0;
+}
+// an insertion / removal of a map followed by events (a small map's HashMap model, size / isEmpty rows, a cleared
+// map's sizes): its event, as k_msize_count emits a region commit's (map_wide.hip map_event)
+__device__ inline bool hot_events(const HotClr& c, uint32_t slot) {
+  return c.mflag != nullptr && (c.mflag[slot] & (kMfSmall | kMfSize | kMfClr)) != 0;
+}
+__device__ inline void hot_map_event(const HotClr& c, uint32_t slot, uint32_t code, const MRec& r, uint32_t& err) {
+  if (!code) return;
+  bool ok;
+  const uint32_t kt = CC_FLAG_KTAG(smeta_flags(r.meta));
+  const uint32_t jh = java_key_hash(kt, r.key, c.hh_key, c.hh_val, c.hh_n, ok);
+  const uint64_t d = r.idx - *c.idx0p;
+  if (!ok || d >> 40) err |= kErrHandleHash;
+  const uint32_t at = wave_append(c.ev_ctl);
+  if (at < c.ev_cap) {
+    c.ev_key[at] = ((uint64_t)slot << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
+    c.ev_val[at] = at;
+    c.ev_pay[at] = EvPay{r.key, jh, kt};
+  }
+}
+
 __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ hot_meta, const uint32_t* __restrict__ hot_n,
                                                 const uint32_t* __restrict__ hot_len, const uint32_t* __restrict__ hot_rpre,
                                                 const uint32_t* __restrict__ hot_rstart, uint32_t tiles,
-                                                Comp* __restrict__ agg, uint32_t* __restrict__ hot_cond) {
+                                                Comp* __restrict__ agg, uint32_t* __restrict__ hot_cond,
+                                                const HotKey* __restrict__ hot, HotClr hc) {
   __shared__ uint32_t pfx[kHotMax + 1];
   __shared__ Comp wtot[kHT / kWave];
   __shared__ uint32_t lrpre[kMaxTiles + 1], lrst[kMaxTiles];
@@ -404,14 +433,27 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ ho
     ListCursor cur{lrpre, lrst, tiles, 0, 0, 0, 0};
     Comp c = comp_identity();
     bool cond = false;
+    const uint32_t slot = hot[h].ident & kMwSlotMask;
+    const bool fl = hot_cleared(hc, slot);  // (item-uniform)
     if (p0 < L) {
+      uint32_t pe = 0;  // the epoch of the commit before this thread's first (0: the sub-batch start)
+      if (fl && p0 > 0) {
+        cur.seek(p0 - 1);
+        pe = hot_epoch(hc, slot, cur.next());
+      }
       cur.seek(p0);
       const uint32_t e = p0 + kHPer < L ? p0 + kHPer : L;
       for (uint32_t q = p0; q < e; ++q) {
         const uint32_t g = cur.next();
         const uint32_t m = hot_meta[g];
         cond |= compares_value(m);
-        c = compose(c, element(m, g));
+        Comp el = element(m, g);
+        if (fl) {  // a clear since the commit before: CLEAR . el (map_clear.hip)
+          const uint32_t E = hot_epoch(hc, slot, g);
+          if (E != pe) el.P = el.A;
+          pe = E;
+        }
+        c = compose(c, el);
       }
     }
     if (cond) atomicOr(&hot_cond[h], 1u);
@@ -493,7 +535,7 @@ __device__ inline void materialize(const Comp& c, const HotS0 s0, const MRec* __
 // size change (1 insert, 2 remove, 0 none: the 2-bit codes of hot_msz)
 __device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint64_t idx, uint32_t& w, uint64_t& v,
                                     uint64_t& ci, uint64_t& ins, uint8_t* __restrict__ rst_status,
-                                    uint64_t* __restrict__ rst_value, const CvCtx& cv, uint32_t& err) {
+                                    uint64_t* __restrict__ rst_value, const CvCtx& cv, uint32_t ep, uint32_t& err) {
   const uint32_t op = smeta_op(m);
   const int was = (w & kMwPresent) != 0;
   uint64_t rv;
@@ -505,7 +547,7 @@ __device__ inline uint32_t hot_step(uint32_t g, uint32_t m, const u64x2& x, uint
     const uint32_t w0 = w;
     const uint64_t v0 = v;
     st = map_apply(op, smeta_flags(m), x.x, x.y, w, v, rv, wrote, created);
-    cv_change(cv, w0, v0, w, v, [&]() { return idx; }, 0u, err);  // (cleared maps are not hot-routed: epoch 0)
+    cv_change(cv, w0, v0, w, v, [&]() { return idx; }, ep, err);
     if (wrote) ci = idx;
     if (created) ins = idx;
   }
@@ -523,7 +565,8 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
                                                   uint64_t* __restrict__ tbl_val, uint32_t* __restrict__ tbl_word,
                                                   uint64_t* __restrict__ tbl_ci, uint64_t* __restrict__ tbl_ins,
                                                   uint8_t* __restrict__ rst_status, uint64_t* __restrict__ rst_value,
-                                                  uint32_t* __restrict__ hot_msz, CvCtx cv, uint32_t* __restrict__ err_out) {
+                                                  uint32_t* __restrict__ hot_msz, CvCtx cv, HotClr hc,
+                                                  uint32_t* __restrict__ err_out) {
   __shared__ uint32_t pfx[kHotMax + 1];
   __shared__ Comp wtot[kHT / kWave];
   __shared__ Comp carry;
@@ -542,16 +585,30 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
     // pfx[h] * kHotPiece / 16 + position / 16 (a thread's kHPer positions of a piece are whole bytes of one word)
     uint32_t* const msz = hot_msz + (uint64_t)pfx[h] * (kHotPiece / 16);
     ListCursor cur{lrpre, lrst, tiles, 0, 0, 0, 0};
+    const uint32_t slot = hot[h].ident & kMwSlotMask;
+    const bool fl = hot_cleared(hc, slot);  // its map is cleared in this sub-batch (item-uniform)
+    const bool evs = hot_events(hc, slot);  // its insertions / removals are map events
     if (hot_cond[h]) {  // value-comparing ops on this key: its whole list, in order, on one thread
       if (p == 0 && t == 0) {
         uint32_t sw = s0.w;
         uint64_t sv = s0.v, ci = s0.ci, ins = s0.ins;
         cur.seek(0);
-        uint32_t codes = 0;
+        uint32_t codes = 0, pe = 0;
         for (uint32_t q = 0; q < L; ++q) {
           const uint32_t g = cur.next();
-          codes |= hot_step(g, xr[g].meta, mrec_ab(xr[g], cb, row0, g), xr[g].idx, sw, sv, ci, ins, rst_status, rst_value, cv, err)
-                   << (2 * (q % 16));
+          uint32_t E = 0;
+          if (fl) {
+            E = hot_epoch(hc, slot, g);
+            if (E != pe) {  // cleared before it
+              sw &= ~(kMwPresent | kMwVtagMask);
+              sv = 0;
+            }
+            pe = E;
+          }
+          const uint32_t code = hot_step(g, xr[g].meta, mrec_ab(xr[g], cb, row0, g), xr[g].idx, sw, sv, ci, ins, rst_status,
+                                         rst_value, cv, E, err);
+          if (evs) hot_map_event(hc, slot, code, xr[g], err);
+          codes |= code << (2 * (q % 16));
           if (q % 16 == 15 || q + 1 == L) {
             msz[q / 16] = codes;
             codes = 0;
@@ -561,6 +618,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
         tbl_val[pos] = sv;
         tbl_ci[pos] = ci;
         tbl_ins[pos] = ins;
+        if (fl) hc.tbl_ep[pos] = (uint8_t)pe;  // (the region launch drops the entry if it predates the last clear)
       }
       continue;
     }
@@ -569,17 +627,30 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
     // this thread's commits and their composite
     const uint32_t p0 = p * kHotPiece + t * kHPer;
     const uint32_t e = p0 < L ? (p0 + kHPer < L ? p0 + kHPer : L) : p0;
-    uint32_t gs[kHPer], ms[kHPer];
+    uint32_t gs[kHPer], ms[kHPer], es[kHPer];
     Comp c = comp_identity();
+    uint32_t pe0 = 0;  // the epoch of the commit before this thread's first (clears in the stream)
+    if (fl && p0 > 0 && p0 < L) {
+      cur.seek(p0 - 1);
+      pe0 = hot_epoch(hc, slot, cur.next());
+    }
     if (p0 < L) cur.seek(p0);
+    uint32_t pe = pe0;
 #pragma unroll
     for (int q = 0; q < kHPer; ++q) {
       gs[q] = 0;
       ms[q] = 0;
+      es[q] = 0;
       if (p0 + q < e) {
         gs[q] = cur.next();
         ms[q] = xr[gs[q]].meta;
-        c = compose(c, element(ms[q], gs[q]));
+        Comp el = element(ms[q], gs[q]);
+        if (fl) {  // a clear since the commit before: CLEAR . el (as k_hot_agg)
+          es[q] = hot_epoch(hc, slot, gs[q]);
+          if (es[q] != pe) el.P = el.A;
+          pe = es[q];
+        }
+        c = compose(c, el);
       }
     }
     const Comp inc = wave_scan(c, l);
@@ -605,12 +676,20 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
       uint64_t sv, ci, ins;
       materialize(pre, s0, xr, sw, sv, ci, ins);
       static_assert(kHPer == 16 || kHPer == 8 || kHPer == 4, "size-change codes: whole bytes per thread and piece");
-      uint32_t codes = 0;
+      uint32_t codes = 0, qe = pe0;
 #pragma unroll
       for (int q = 0; q < kHPer; ++q)
-        if (p0 + q < e)
-          codes |= hot_step(gs[q], ms[q], mrec_ab(xr[gs[q]], cb, row0, gs[q]), xr[gs[q]].idx, sw, sv, ci, ins, rst_status,
-                            rst_value, cv, err) << (2 * q);
+        if (p0 + q < e) {
+          if (fl && es[q] != qe) {  // cleared before it
+            sw &= ~(kMwPresent | kMwVtagMask);
+            sv = 0;
+          }
+          qe = es[q];
+          const uint32_t code = hot_step(gs[q], ms[q], mrec_ab(xr[gs[q]], cb, row0, gs[q]), xr[gs[q]].idx, sw, sv, ci, ins,
+                                         rst_status, rst_value, cv, es[q], err);
+          if (evs) hot_map_event(hc, slot, code, xr[gs[q]], err);
+          codes |= code << (2 * q);
+        }
       // (consecutive threads: consecutive words / halves / bytes of the code words, little-endian)
       if (kHPer == 16) msz[p0 / 16] = codes;
       else if (kHPer == 8) reinterpret_cast<uint16_t*>(msz)[p0 / 8] = (uint16_t)codes;
@@ -620,6 +699,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
         tbl_val[pos] = sv;
         tbl_ci[pos] = ci;
         tbl_ins[pos] = ins;
+        if (fl) hc.tbl_ep[pos] = (uint8_t)qe;  // (the region launch drops the entry if it predates the last clear)
       }
     }
     __syncthreads();
@@ -652,12 +732,12 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
                      a.tbl_word, a.tbl_ci, a.tbl_ins, a.hot_rpre, a.hot_rstart, a.hot_len, a.hot_cond,
                      reinterpret_cast<HotS0*>(a.hot_s0));
   hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.hot_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
-                     a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond);
+                     a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond, a.hot, a.hc);
   hipLaunchKernelGGL(k_hot_carry, dim3(kHotMax), dim3(kHT), 0, st, a.hot_n, a.hot_len, reinterpret_cast<Comp*>(a.hot_agg));
   hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.mrec, a.cb, a.lo, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
-                     a.rst_value, a.hot_msz, a.cv, a.err);
+                     a.rst_value, a.hot_msz, a.cv, a.hc, a.err);
   a.mark(K_MAP_HOT, 0, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

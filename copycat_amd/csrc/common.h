@@ -101,6 +101,16 @@ __device__ inline uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 __device__ inline uint64_t ballot(bool p) { return __ballot(p); }
+// A slot in an append buffer for every active lane of the wave: one atomic per wave (an event buffer's counter is
+// one address: per-lane atomics on it serialise), lanes in lane order.
+__device__ inline uint32_t wave_append(uint32_t* ctr) {
+  const uint64_t act = __ballot(1);
+  const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+  uint32_t base = 0;
+  if (__lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(act));
+  base = (uint32_t)__shfl((int)base, (int)leader, 64);
+  return base + (uint32_t)__builtin_popcountll(act & lanemask_lt());
+}
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global load and
 // store of the wave (s_waitcnt vmcnt(0)), which would kill the cross-chunk prefetches the streaming kernels
@@ -528,7 +538,7 @@ __device__ inline void ttl_expiry_event(const TtlEmit& t, uint64_t cb, uint32_t 
   bool ok;
   const uint32_t jh = java_key_hash((w >> 17) & 3, key, t.hh_key, t.hh_val, t.hh_n, ok);
   if (!ok) err |= kErrHandleHash;
-  const uint32_t at = atomicAdd(t.ctl, 1u);
+  const uint32_t at = wave_append(t.ctl);
   if (at < t.ev_cap) {
     t.ev_key[at] = ((uint64_t)(w & kMwSlotMask) << 44) | ((pos & ((1ull << 40) - 1)) << 4) | 2u;
     t.ev_val[at] = at;
@@ -596,7 +606,7 @@ struct CvCtx {
 };
 __device__ inline void cv_event(const CvCtx& cv, uint32_t q, uint64_t d, uint32_t kind, uint32_t val, uint32_t& err) {
   if (d >> 40) err |= kErrCvKey;
-  const uint32_t at = atomicAdd(cv.ctl, 1u);
+  const uint32_t at = wave_append(cv.ctl);
   if (at < cv.cap) {
     cv.ev_key[at] = ((uint64_t)q << 42) | ((d & ((1ull << 40) - 1)) << 2) | kind;
     cv.ev_val[at] = val;
@@ -635,6 +645,7 @@ struct ClrCtx {
   const uint32_t* base;     // [R] clears of the map before this sub-batch (positions in clr from off[m])
   const uint8_t* eend;      // [R] clears of the map in this sub-batch
   uint64_t lo;              // the sub-batch's first row
+  uint8_t* tbl_ep;          // [map_entries] a hot key's entry's epoch after k_hot_apply (k_apply_map resets it to 0)
 };
 constexpr uint32_t kMetaEpochShift = 25;  // MRec meta bits 25-31 (in LDS, k_apply_map): the commit's clear epoch
 __device__ inline uint32_t clr_epoch(const ClrCtx& c, uint32_t m, uint64_t row) {

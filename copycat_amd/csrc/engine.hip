@@ -103,7 +103,7 @@ static void free_all(cc_engine* e) {
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
                   e->d_cvset,    e->d_cvcnt,    e->d_cvev_key, e->d_cvev_key2, e->d_cvev_val, e->d_cvev_val2, e->d_cvev_ctl,
                   e->d_cvseg,    e->d_cvtemp,   e->d_clrq,    e->d_clrq_n,   e->d_clr_keys,   e->d_clr_keys2, e->d_clr_off,
-                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp};
+                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -394,6 +394,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_cset, sizeof(CsetEnt) * (e->cset_mask + 1));
     ALLOC(e->d_cset_full, sizeof(uint32_t));
     ALLOC(e->d_tbl_claim, sizeof(uint64_t) * e->map_entries);
+    ALLOC(e->d_tbl_ep, e->map_entries);  // clears in the stream: hot entries' epochs (map_clear.hip)
     ALLOC(e->d_lvl_at, sizeof(unsigned long long) * kLvlSlots * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
@@ -453,6 +454,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_cset, 0, sizeof(CsetEnt) * (e->cset_mask + 1))) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_cset_full, 0, sizeof(uint32_t))) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_claim, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_tbl_ep, 0, e->map_entries)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_lvl_at, 0xFF, sizeof(unsigned long long) * kLvlSlots * cfg->max_resources)) != hipSuccess)
       return fail("memset", he);
     if ((he = hipMemset(e->d_msize, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
@@ -1207,6 +1209,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.hi = hi;
       ca.base = e->d_clr_base;
       ca.eend = e->d_clr_eend;
+      ca.mflag = e->d_msmall;
       ca.err = e->d_err;
       ca.index = c->index;
       ca.ev_key = e->d_sm_key;
@@ -1216,7 +1219,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.ev_ctl = e->d_sm_ctl;
       ca.cgen = e->d_mw_cgen;
       if (launch_clr_sub(ca, st)) return set_err(CC_ERR_HIP, "clear epochs launch", hipGetLastError());
-      cctx = ClrCtx{e->d_msmall, e->d_clr_keys2, e->d_clr_off, e->d_clr_base, e->d_clr_eend, lo};
+      cctx = ClrCtx{e->d_msmall, e->d_clr_keys2, e->d_clr_off, e->d_clr_base, e->d_clr_eend, lo, e->d_tbl_ep};
     }
     CvSubArgs cva{};
     cva.clr = cctx;
@@ -1268,7 +1271,26 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ha.rst_status = e->d_rst_status;
       ha.rst_value = e->d_rst_value;
       ha.hot_msz = e->d_hot_msz;
-      ha.msmall = (e->small_live || e->szq_n || clr_on) ? e->d_msmall : nullptr;  // small / size-queried / cleared maps: not hot-routed
+      ha.msmall = nullptr;  // (every map's keys are hot-routed)
+      if (e->small_live || e->szq_n || clr_on) {  // small / size-queried / cleared maps' hot commits: map events
+        int rc = ensure_small(e);
+        if (rc) return rc;
+        if (!c->index) return set_err(CC_ERR_INVALID, "an engine with maps needs the index column (log order)");
+        ha.hc.clr = cctx;  // (cleared maps: commit epochs, map_clear.hip)
+        ha.hc.mflag = e->d_msmall;
+        ha.hc.hh_key = e->d_hh_key;
+        ha.hc.hh_val = e->d_hh_val;
+        ha.hc.hh_n = e->hh_n;
+        ha.hc.xr = e->d_mrec;
+        ha.hc.lo = lo;
+        ha.hc.ev_key = e->d_sm_key;
+        ha.hc.ev_val = e->d_sm_val;
+        ha.hc.ev_pay = e->d_sm_pay;
+        ha.hc.ev_cap = (uint32_t)e->sm_cap;
+        ha.hc.ev_ctl = e->d_sm_ctl;
+        ha.hc.idx0p = c->index + lo;
+        ha.hc.tbl_ep = e->d_tbl_ep;
+      }
       ha.err = e->d_err;
       ha.mark = marker_of(e);
       static const bool no_hot = diag_env("CC_NO_HOT");  // diagnostics: every key through its region

@@ -327,6 +327,7 @@ struct ClrSubArgs {
   uint64_t lo, hi;
   uint32_t* base;
   uint8_t* eend;
+  uint8_t* mflag;  // kMfClr: cleared in this sub-batch
   uint32_t* err;
   const uint64_t* index;
   uint64_t* ev_key;
@@ -419,8 +420,29 @@ struct KeyedResultArgs {
 int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st);
 
 constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
+// clears in the stream for the hot-key scan (map_clear.hip): commit epochs from their rows, the cleared maps' size
+// events, the entry dropped when its state predates the map's last clear of the sub-batch
+struct HotClr {
+  ClrCtx clr;                // clr.mflag == nullptr: no clears in this batch
+  const MRec* xr;
+  uint64_t lo;
+  uint64_t* ev_key;          // the map event buffer (map_small.hip SmallArgs)
+  uint32_t* ev_val;
+  EvPay* ev_pay;
+  uint32_t ev_cap;
+  uint32_t* ev_ctl;
+  const uint64_t* idx0p;
+  uint8_t* tbl_ep;           // [map_entries] the clear epoch a hot key's entry ends at (read by k_apply_map)
+  // the map events of small / size-queried / cleared maps' hot commits (null: no such maps in this batch)
+  const uint8_t* mflag;
+  const uint64_t* hh_key;    // String.hashCode of HANDLE keys (java_key_hash)
+  const int32_t* hh_val;
+  uint32_t hh_n;
+  uint32_t* err;
+};
 struct HotArgs {
   CvCtx cv{};  // in-stream containsValue (map_cv.hip)
+  HotClr hc{};  // clears in the stream (map_clear.hip)
   // detection (before the partition)
   const uint32_t* inst;
   const uint8_t* flags;

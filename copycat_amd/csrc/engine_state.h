@@ -229,6 +229,7 @@ struct cc_engine {
   uint32_t* d_clr_off = nullptr;   // [max_resources + 1]
   uint32_t* d_clr_base = nullptr;  // [max_resources]
   uint8_t* d_clr_eend = nullptr;   // [max_resources]
+  uint8_t* d_tbl_ep = nullptr;     // [map_entries] hot entries' clear epochs within a sub-batch (0 between)
   void* d_clr_temp = nullptr;
   size_t clr_temp_bytes = 0;
   uint32_t clr_n = 0;              // this batch's

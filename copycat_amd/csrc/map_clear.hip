@@ -5,9 +5,10 @@
 // whose HashMap keeps its table).  As a barrier (map_wide.hip) a clear ends the segment: a host round trip, a
 // partition and a region apply for the rows before it, a scan of the table.  In the stream it is an epoch instead:
 //
-//   per batch      k_map_barriers lists the map clear rows and flags their maps (kMfClr, common.h ClrCtx); the list is
-//                  sorted by (map, row) with per-map offsets (k_clr_keys, k_clr_off);
-//   per sub-batch  k_clr_sub gives every map its clears before the sub-batch and within it (at most 127: the host
+//   per batch      k_map_barriers lists the map clear rows (common.h ClrCtx); the list is sorted by (map, row) with
+//                  per-map offsets (k_clr_keys, k_clr_off);
+//   per sub-batch  k_clr_sub flags the maps cleared in the sub-batch (kMfClr) and gives every map its clears before
+//                  the sub-batch and within it (at most 127: the host
 //                  ends a sub-batch earlier for a map cleared more often); a commit's epoch is the clears of its map
 //                  in [lo, row) (k_apply_map, at the top of its chunk: MRec meta bits 25-31 in LDS); a commit whose
 //                  epoch differs from the one its entry's state is at (the previous commit of the entry, or the epoch
@@ -69,7 +70,8 @@ size_t clr_sort_temp_bytes(uint32_t n) {
 
 // per sub-batch: every map's clears before [lo, hi) and within it
 __global__ void k_clr_sub(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off, uint32_t R, uint64_t lo,
-                          uint64_t hi, uint32_t* __restrict__ base, uint8_t* __restrict__ eend, uint32_t* __restrict__ err) {
+                          uint64_t hi, uint32_t* __restrict__ base, uint8_t* __restrict__ eend, uint8_t* __restrict__ mflag,
+                          uint32_t* __restrict__ err) {
   for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x) {
     const uint32_t a0 = off[m], b0 = off[m + 1];
     auto lb = [&](uint64_t row) {
@@ -85,6 +87,10 @@ __global__ void k_clr_sub(const uint64_t* __restrict__ keys, const uint32_t* __r
     base[m] = pl - a0;
     if (ph - pl > 127u) atomicOr(err, kErrCapacity);  // (the host cuts sub-batches so that this never holds)
     eend[m] = (uint8_t)min(ph - pl, 127u);
+    // kMfClr marks the maps cleared in THIS sub-batch: the others keep the exact size tracking and hot-key routing
+    const uint8_t f = mflag[m];
+    const uint8_t g = (uint8_t)((f & ~kMfClr) | (ph > pl ? kMfClr : 0u));
+    if (g != f) mflag[m] = g;
   }
 }
 
@@ -108,7 +114,7 @@ __global__ void k_clr_events(const uint64_t* __restrict__ keys, uint32_t n, uint
 
 int launch_clr_sub(const ClrSubArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_clr_sub, dim3((a.R + 255) / 256), dim3(256), 0, st, a.keys, a.off, a.R, a.lo, a.hi, a.base, a.eend,
-                     a.err);
+                     a.mflag, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_clr_events(const ClrSubArgs& a, hipStream_t st) {

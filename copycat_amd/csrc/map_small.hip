@@ -43,6 +43,102 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
     if (i == 0 || (key[i] >> 44) != (key[i - 1] >> 44)) seg[atomicAdd(nseg, 1u)] = i;
 }
 
+// Alternating runs of one key (a hot key of a small map: remove k, put k, remove k, put k, ... with no other event of
+// the map between): in a list bin the net effect of remove k . put k is k moved to its chain's end, with the size
+// back where it was (no resize) and a chain no longer than before (no treeifyBin: a list chain of 9 cannot persist
+// below capacity 64), so R P R P ... R P == R P and R P ... R == R.  One wave per run of a map still in the window
+// finds the maximal alternating chains (commit events only: a clear, a size query or another key ends one) and
+// stores, at the chain's first removal, how many events after it are implied (EvPay.ktag >> 4).  k_small_replay
+// skips them when the key's bin is a list bin at that removal (a tree bin replays every event).
+constexpr uint32_t kSkipShift = 4;
+__global__ __launch_bounds__(256) void k_small_chains(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                      EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl,
+                                                      const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
+                                                      const SmallMap* __restrict__ st) {
+  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
+  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
+    const uint32_t start = seg[r];
+    const uint32_t m = (uint32_t)(key[start] >> 44);
+    if (!(st[m].flags & kSmIn)) continue;  // (wave-uniform)
+    // the open chain, carried across chunks: its first event, its first removal, the previous event
+    uint32_t ca = 0xFFFFFFFFu, cr0 = 0xFFFFFFFFu, cf = 0;
+    uint64_t pkey = 0;
+    uint32_t pid = 0, pcode = 0;  // previous event's identity hash / code (0: not a commit event)
+    for (uint32_t b = start;; b += kWave) {
+      const uint32_t i = b + l;
+      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
+      const uint64_t k = in ? key[i] : 0;
+      const uint32_t code = in && !(k & 8u) && ((k & 3u) == 1u || (k & 3u) == 2u) ? (uint32_t)(k & 3u) : 0u;
+      const uint32_t v = in ? val[i] : 0u;
+      EvPay x{0, 0, 0};
+      if (code) x = pay[v];
+      const uint32_t id = x.aux ^ ((x.ktag & 3u) << 30);  // (with the key: the identity)
+      // the previous event (lane - 1, or the carried one for lane 0)
+      const uint64_t qk = __shfl_up(x.key, 1, 64);
+      const uint32_t qi = __shfl_up(id, 1, 64), qc = __shfl_up(code, 1, 64);
+      const uint64_t prk = l == 0 ? pkey : qk;
+      const uint32_t pri = l == 0 ? pid : qi, prc = l == 0 ? pcode : qc;
+      const bool link = code && prc && i > start && prk == x.key && pri == id && prc != code;
+      // chain starts: the last start at or before each lane (absolute index; none in the chunk: the carried one)
+      int32_t st_l = (in && !link) ? (int32_t)l : -1;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(st_l, d, 64);
+        if (l >= (uint32_t)d) st_l = max(st_l, y);
+      }
+      const uint32_t fcode = __shfl(code, st_l < 0 ? 0 : st_l, 64);  // the chain's first code (if it starts here)
+      const uint32_t a = st_l < 0 ? ca : b + (uint32_t)st_l;
+      const uint32_t f = st_l < 0 ? cf : fcode;
+      const uint32_t r0 = st_l < 0 ? cr0 : (f == 1u ? a + 1 : a);
+      // a chain ends at lane i when the next event does not link (lane 63: decided with the next chunk's lane 0)
+      const bool nlink = __shfl_down((int)link, 1, 64) != 0;
+      const bool end_here = in && l < 63 && !nlink;
+      const uint32_t vr0 = __shfl(v, (r0 >= b && r0 < b + 64) ? (int)(r0 - b) : 0, 64);
+      const uint32_t cb_code = code;  // the chain's last event's code, at its end lane
+      if (end_here && code && r0 != 0xFFFFFFFFu && i > r0) {
+        const uint32_t skip = cb_code == 1u ? i - r0 - 1 : i - r0;
+        if (skip && r0 >= b) pay[vr0].ktag |= skip << kSkipShift;
+        else if (skip) pay[val[r0]].ktag |= skip << kSkipShift;  // (its first removal in an earlier chunk)
+      }
+      // carry: the chain open at lane 63, the last event
+      const uint64_t inb = __ballot(in);
+      const bool full = inb == ~0ull;
+      ca = (uint32_t)__shfl((int)a, 63, 64);
+      cf = (uint32_t)__shfl((int)f, 63, 64);
+      cr0 = (uint32_t)__shfl((int)r0, 63, 64);
+      pkey = __shfl(x.key, 63, 64);
+      pid = (uint32_t)__shfl((int)id, 63, 64);
+      pcode = (uint32_t)__shfl((int)code, 63, 64);
+      const uint32_t last_code = pcode;
+      if (!full) break;
+      // lane 63's chain continues only if the next chunk's lane 0 links: checked there (l == 0 uses pkey / pid /
+      // pcode); if it does not, the chain ended at lane 63 of this chunk
+      const uint32_t i0 = b + kWave;
+      bool next_in = i0 < E && (uint32_t)(key[i0] >> 44) == m;
+      bool next_link = false;
+      if (next_in) {
+        const uint64_t k0 = key[i0];
+        const uint32_t c0 = !(k0 & 8u) && ((k0 & 3u) == 1u || (k0 & 3u) == 2u) ? (uint32_t)(k0 & 3u) : 0u;
+        if (c0 && last_code) {
+          const EvPay y = pay[val[i0]];
+          next_link = y.key == pkey && (y.aux ^ ((y.ktag & 3u) << 30)) == pid && c0 != last_code;
+        }
+      }
+      if (!next_link && last_code && cr0 != 0xFFFFFFFFu && b + 63 > cr0 && l == 0) {  // the carried chain ended at lane 63
+        const uint32_t ib = b + 63;
+        const uint32_t skip = last_code == 1u ? ib - cr0 - 1 : ib - cr0;
+        if (skip) pay[val[cr0]].ktag |= skip << kSkipShift;
+      }
+      if (!next_link) {
+        ca = cr0 = 0xFFFFFFFFu;
+        pcode = 0;  // (lane 0 of the next chunk starts a chain)
+      }
+      if (!next_in) break;
+    }
+  }
+}
+
 // One thread per run: the map's java.util.HashMap copied into LDS (small_jhm.h: node pool, chains, tree links),
 // its events applied in log order (putVal of a new key, removeNode), the state written back.  A map whose table
 // passes 64 leaves the window (its later events are not followed).
@@ -83,7 +179,7 @@ __global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restric
       const EvPay x = pay[val[i]];
       if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
         const uint32_t lv0 = lm.lvl;
-        const bool stay = j.put(x.aux, x.ktag, x.key);
+        const bool stay = j.put(x.aux, x.ktag & 3u, x.key);
         if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
           const uint64_t d = (k >> 4) & ((1ull << 40) - 1);
           // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
@@ -92,7 +188,11 @@ __global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restric
         }
         if (!stay) break;  // the table passed 64: out of the window
       } else if ((k & 3u) == 2u) {  // a key removed: removeNode
-        j.remove(x.aux, x.ktag, x.key);
+        j.remove(x.aux, x.ktag & 3u, x.key);
+        // an alternating run of this key follows (k_small_chains): implied by this removal and, if the run ends with
+        // a put, that put -- in a list bin
+        const uint32_t skip = x.ktag >> kSkipShift;
+        if (skip && j.list_bin(x.aux)) i += skip;
       }
     }
     if (!(lm.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
@@ -280,7 +380,7 @@ __global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict_
 
 __global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
   for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
-    mflag[m] &= (uint8_t)~(kMfSize | kMfCv);
+    mflag[m] &= (uint8_t)~(kMfSize | kMfCv | kMfClr);
 }
 
 int launch_size_emit(const SizeArgs& a, hipStream_t st) {
@@ -316,6 +416,9 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
     if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (E + 255) / 256);
     hipLaunchKernelGGL(k_small_seg, dim3(grid), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg);
+    if (!a.msize)  // (TTL mode replays its runs for sizes as well: every event there)
+      hipLaunchKernelGGL(k_small_chains, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, const_cast<EvPay*>(a.ev_pay), a.ctl,
+                         a.seg, a.nseg, a.state);
     hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(kSrT), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg, a.state,
                        a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity

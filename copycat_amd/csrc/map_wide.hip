@@ -93,8 +93,7 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
   if (clrq && ty == CC_RES_MAP && o == CC_OP_MAP_CLEAR) {
     // MapState.clear (:255-274) outside TTL mode: applied in the stream as an epoch (map_clear.hip)
     const uint32_t k = atomicAdd(clrq_n, 1u);
-    if (k < clrq_cap) clrq[k] = (uint32_t)i;
-    if (!(mflag[r] & kMfClr)) mflag_or(mflag, r, kMfClr);
+    if (k < clrq_cap) clrq[k] = (uint32_t)i;  // (k_clr_sub flags the map in the sub-batches that clear it)
     return;
   }
   if (mfirst && ty == CC_RES_MAP && o == CC_OP_DELETE) atomicMin(&mfirst[r], (uint32_t)i);  // (k_cv_classify)
@@ -618,7 +617,7 @@ __device__ inline void map_event(uint32_t m, uint32_t code, uint64_t d, const MR
   const uint32_t kt = CC_FLAG_KTAG(smeta_flags(xr.meta));
   const uint32_t jh = java_key_hash(kt, xr.key, hh_key, hh_val, hh_n, ok);
   if (!ok || d >> 40) atomicOr(err, kErrHandleHash);  // an unregistered String key / a sub-batch spanning 2^40 indices
-  const uint32_t at = atomicAdd(sm_ctl, 1u);
+  const uint32_t at = wave_append(sm_ctl);
   if (at < ev_cap) {
     ev_key[at] = ((uint64_t)m << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
     ev_val[at] = at;
@@ -715,6 +714,7 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
       }
       const uint32_t m = hsl[h] - base;
       if (m >= span) continue;
+      if (msmall && (msmall[hsl[h]] & kMfClr)) continue;  // (a cleared map: k_hot_apply emits its size events)
       const uint32_t lp0 = hl0[h], lp1 = hl1[h], wd = lp0 / 16 + (i - wpfx[h]);
       uint32_t x = hot_msz[(uint64_t)pfx[h] * kHotWords + wd];
       const uint32_t a = wd * 16 < lp0 ? lp0 - wd * 16 : 0u, b = lp1 - wd * 16 < 16u ? lp1 - wd * 16 : 16u;

@@ -48,6 +48,11 @@ struct SmallJhm {
   __device__ void set_left(uint32_t x, uint32_t v) { s.lf[x - 1] = (uint8_t)v; }
   __device__ void set_right(uint32_t x, uint32_t v) { s.rt[x - 1] = (uint8_t)v; }
   __device__ uint32_t hash(uint32_t x) const { return s.jh[x - 1]; }
+  // the bin of hash h is a list bin (or empty) at the current capacity
+  __device__ bool list_bin(uint32_t h) const {
+    const uint32_t hd = s.tab[(cap() - 1) & h];
+    return hd == 0 || !tree(hd);
+  }
 
   __device__ uint32_t alloc(uint32_t h, uint32_t kt, uint64_t key) {
     const uint64_t free = ~s.used;

@@ -39,7 +39,8 @@ for n, v in sorted(ev.items(), key=lambda kv: -sum(d for _, d in kv[1])):
 PY
 find $R/$OUT/kt -name "*kernel_trace.csv" -delete
 i=0
-for CNT in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU" "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY"; do
+[ -n "$KT_ONLY" ] && PMCS="" || PMCS=1
+for CNT in ${PMCS:+ "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU" "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY"}; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $CNT -d $R/$OUT/pmc$i -o run --output-format csv -- python3 $R/bench.py $BA > $R/$OUT/pmc$i.log 2>&1 || { echo "pmc $i ($CNT) failed"; tail -3 $R/$OUT/pmc$i.log; }
   (cd $R && python3 scripts/pmc_kernel_summary.py $OUT/pmc$i > $OUT/pmc${i}_summary.txt 2>&1)
