@@ -1080,7 +1080,7 @@ def run_c3(args, dev, rank, world, dist):
                                        if args.cv_rate or args.clear_rate else "")),
                        "whole_map": ({"containsValue_rate": args.cv_rate, "clear_rate": args.clear_rate,
                                       "engine_counters": dict(zip(("barrier_rows", "in_stream_containsValue",
-                                                                   "sub_batches"), E.counters()))}
+                                                                   "sub_batches", "map_events"), E.counters()))}
                                      if args.cv_rate or args.clear_rate else None),
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),

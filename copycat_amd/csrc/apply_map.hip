@@ -736,8 +736,12 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     PH(6);
   }
 
-  // ---- clears in the stream: an entry whose state predates its map's last clear of the sub-batch is dropped
-  //      (k_map_drop's DEAD; the keys it held count toward the map's peak-size bound, as at a barrier clear) ----
+  // ---- clears in the stream: an entry whose state predates its map's last clear of the sub-batch stays bound but
+  //      absent and UNSEEN (no key the map held since the clear: left out of the used count and the tree-bin test,
+  //      map_wide.hip), with the clear's index as its claim (a later put makes it seen again, claimed no earlier than
+  //      the clear); the keys it held count toward the map's peak-size bound, as at a barrier clear.  (Marking them
+  //      DEAD made every later put of the key bind a new slot: regions filled with dead entries, 4x the binding time.)
+  constexpr uint8_t kEpKilled = 0xFF;  // eep mark of an entry cleared here (its claim is written back below)
   if (clr_live) {
 #pragma unroll
     for (int q = 0; q < MEPer; ++q) {
@@ -746,8 +750,9 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
       if (!(wv & kMwUsed) || (wv & kMwDead)) continue;
       const uint32_t ms = wv & kMwSlotMask;
       if ((clr.mflag[ms] & kMfClr) && eep[e] < clr.eend[ms]) {
-        tword[e] = (wv & ~(kMwPresent | kMwVtagMask)) | kMwDead;
-        if (dropped) atomicAdd(&dropped[ms], 1ull);
+        tword[e] = (wv & ~(kMwPresent | kMwVtagMask)) | kMwUnseen;
+        if (dropped && !(wv & kMwUnseen)) atomicAdd(&dropped[ms], 1ull);
+        eep[e] = kEpKilled;
       }
     }
   }
@@ -760,7 +765,11 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
     tbl_val[tb + e] = tval[e];
     if (tcr[e] != kNoRef) tbl_ci[tb + e] = xr[tcr[e]].idx;
     if (tir[e] != kNoRef) tbl_ins[tb + e] = xr[tir[e]].idx;
-    if (((tnew[e >> 5] >> (e & 31)) & 1u) && (tword[e] & kMwUsed)) {  // bound by this launch: its claim
+    if (clr_live && eep[e] == kEpKilled) {  // cleared: claimed again no earlier than its map's last clear
+      const uint32_t ms = tword[e] & kMwSlotMask;
+      const uint32_t crow = (uint32_t)clr.clr[clr.off[ms] + clr.base[ms] + clr.eend[ms] - 1];
+      tbl_claim[tb + e] = idx0p[crow - clr.lo];
+    } else if (((tnew[e >> 5] >> (e & 31)) & 1u) && (tword[e] & kMwUsed)) {  // bound by this launch: its claim
       const bool one = ((tc1[e >> 5] >> (e & 31)) & 1u) && !((tc2[e >> 5] >> (e & 31)) & 1u) && tir[e] != kNoRef;
       tbl_claim[tb + e] = one ? xr[tir[e]].idx : *idx0p;
     }

@@ -453,13 +453,13 @@ constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (kept for t
 constexpr uint32_t kSmAmbig = 8u;    // a tree order the engine cannot know (two String keys with one hash in a tree bin;
                                      // a removal of a key the model does not hold): an order-dependent answer refuses
 // per-map flags of the batch (cc_engine::d_msmall): bit 0 the table is small (events followed key by key), bit 1 the
-// batch asks the map's size / isEmpty (events followed for the in-stream answers); either keeps the map's keys out of
-// hot-key routing, so every such commit is a region record
+// batch asks the map's size / isEmpty (events followed for the in-stream answers); either makes every insertion /
+// removal of the map an event (region commits: k_msize_count; hot-key commits: k_hot_apply)
 constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
 // bit 2: the batch answers containsValue rows of the map in the stream (map_cv.hip): its commits report value changes
 constexpr uint8_t kMfCv = 4u;
-// bit 3: the batch clears the map in the stream (map_clear.hip): its sizes come from event replay, its keys are not
-// hot-routed, and its commits carry their clear epoch
+// bit 3: the sub-batch clears the map in the stream (map_clear.hip): its sizes come from event replay and its commits
+// carry their clear epoch (region and hot-key commits alike)
 constexpr uint8_t kMfClr = 8u;
 // the flag bytes are set by concurrent threads of one kernel: OR through the aligned word (the array is padded to it)
 __device__ inline void mflag_or(uint8_t* mflag, uint32_t m, uint8_t bit) {
@@ -646,15 +646,19 @@ struct ClrCtx {
   const uint8_t* eend;      // [R] clears of the map in this sub-batch
   uint64_t lo;              // the sub-batch's first row
   uint8_t* tbl_ep;          // [map_entries] a hot key's entry's epoch after k_hot_apply (k_apply_map resets it to 0)
+  const uint8_t* btab;      // [R][nb] a cleared map's epoch at each row bucket's start (map_clear.hip k_clr_btab)
+  uint32_t nb, bshift;      // buckets per map, log2 of the rows per bucket
 };
 constexpr uint32_t kMetaEpochShift = 25;  // MRec meta bits 25-31 (in LDS, k_apply_map): the commit's clear epoch
+// the bucket's epoch, then the map's few clears inside the bucket before the row (usually none: one load to see it);
+// a binary search over the map's clears was ~10 dependent loads per commit of a cleared map
 __device__ inline uint32_t clr_epoch(const ClrCtx& c, uint32_t m, uint64_t row) {
-  uint32_t a = c.off[m], b = c.off[m + 1];
-  const uint64_t k = ((uint64_t)m << 32) | row;
-  while (a < b) {
-    const uint32_t mid = (a + b) >> 1;
-    if (c.clr[mid] < k) a = mid + 1; else b = mid;
+  uint32_t e = c.btab[(uint64_t)m * c.nb + (uint32_t)((row - c.lo) >> c.bshift)];
+  const uint32_t end = c.eend[m];
+  if (e < end) {
+    const uint64_t* p = c.clr + c.off[m] + c.base[m];  // the map's clears in this sub-batch, ascending
+    while (e < end && (uint32_t)p[e] < (uint32_t)row) ++e;
   }
-  return a - c.off[m] - c.base[m];
+  return e;
 }
 }  // namespace cc

@@ -103,7 +103,7 @@ static void free_all(cc_engine* e) {
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
                   e->d_cvset,    e->d_cvcnt,    e->d_cvev_key, e->d_cvev_key2, e->d_cvev_val, e->d_cvev_val2, e->d_cvev_ctl,
                   e->d_cvseg,    e->d_cvtemp,   e->d_clrq,    e->d_clrq_n,   e->d_clr_keys,   e->d_clr_keys2, e->d_clr_off,
-                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep};
+                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep, e->d_clr_scan, e->d_clr_stemp, e->d_clr_btab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -164,6 +164,21 @@ static int ensure_small(cc_engine* e) {
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events", x);
   e->sm_temp_bytes = tb;
   e->sm_cap = cap;
+  return CC_OK;
+}
+
+// the cleared maps' size scan (map_clear.hip): one element per map event, sized with the event buffer
+static int ensure_clr_scan(cc_engine* e) {
+  if (e->d_clr_scan && e->clr_scan_cap >= e->sm_cap) return CC_OK;
+  if (e->d_clr_scan) (void)hipFree(e->d_clr_scan);
+  if (e->d_clr_stemp) (void)hipFree(e->d_clr_stemp);
+  e->d_clr_scan = e->d_clr_stemp = nullptr;
+  const size_t tb = std::max<size_t>(clr_scan_temp_bytes((uint32_t)e->sm_cap), 256);
+  hipError_t x = hipMalloc(&e->d_clr_scan, clr_scan_bytes_per_event() * e->sm_cap);
+  if (x == hipSuccess) x = hipMalloc(&e->d_clr_stemp, tb);
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc clear size scan", x);
+  e->clr_scan_cap = e->sm_cap;
+  e->clr_stemp_bytes = tb;
   return CC_OK;
 }
 
@@ -1218,8 +1233,25 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.ev_cap = (uint32_t)e->sm_cap;
       ca.ev_ctl = e->d_sm_ctl;
       ca.cgen = e->d_mw_cgen;
+      {  // the epoch buckets: at most 1024 per map and ~64 MB in all
+        uint32_t nbmax = 16;
+        while (nbmax < 1024 && (uint64_t)(2 * nbmax) * e->cfg.max_resources <= (64ull << 20)) nbmax <<= 1;
+        uint32_t sh = 0;
+        while (((hi - lo + (1ull << sh) - 1) >> sh) > nbmax) ++sh;
+        ca.bshift = sh;
+        ca.nb = (uint32_t)((hi - lo + (1ull << sh) - 1) >> sh);
+        const size_t need = (size_t)nbmax * e->cfg.max_resources;
+        if (e->clr_btab_bytes < need) {
+          if (e->d_clr_btab) (void)hipFree(e->d_clr_btab);
+          e->d_clr_btab = nullptr;
+          HIPCHECK(hipMalloc(&e->d_clr_btab, need));
+          e->clr_btab_bytes = need;
+        }
+        ca.btab = e->d_clr_btab;
+      }
       if (launch_clr_sub(ca, st)) return set_err(CC_ERR_HIP, "clear epochs launch", hipGetLastError());
-      cctx = ClrCtx{e->d_msmall, e->d_clr_keys2, e->d_clr_off, e->d_clr_base, e->d_clr_eend, lo, e->d_tbl_ep};
+      cctx = ClrCtx{e->d_msmall, e->d_clr_keys2, e->d_clr_off, e->d_clr_base, e->d_clr_eend, lo, e->d_tbl_ep,
+                    e->d_clr_btab, ca.nb, ca.bshift};
     }
     CvSubArgs cva{};
     cva.clr = cctx;
@@ -1564,6 +1596,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           uint32_t ctl[2] = {0, 0};
           HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
           HIPCHECK(hipStreamSynchronize(st));
+          e->stat_events += ctl[0];
           SmallArgs sa{};
           sa.ev_key = e->d_sm_key;
           sa.ev_key2 = e->d_sm_key2;
@@ -1652,9 +1685,6 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         cr.key = e->d_sm_key2;
         cr.val = e->d_sm_val2;
         cr.pay = e->d_sm_pay;
-        cr.ctl = e->d_sm_ctl;
-        cr.seg = e->d_sm_seg;
-        cr.nseg = e->d_sm_seg + e->cfg.max_resources;
         cr.mflag = e->d_msmall;
         cr.msize = e->d_msize;
         cr.mpcap = e->d_mpcap;
@@ -1662,7 +1692,12 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         cr.idx0 = c->index + lo;
         cr.out_status = out->status;
         cr.out_value = out->value;
-        if (launch_clr_replay(cr, st)) return set_err(CC_ERR_HIP, "clear replay launch", hipGetLastError());
+        int rc = ensure_clr_scan(e);
+        if (rc) return rc;
+        cr.scan = e->d_clr_scan;
+        cr.temp = e->d_clr_stemp;
+        cr.temp_bytes = e->clr_stemp_bytes;
+        if (launch_clr_replay(cr, sized_events, st)) return set_err(CC_ERR_HIP, "clear replay launch", hipGetLastError());
       }
       SmallArgs sf{};
       sf.ctl = e->d_sm_ctl;
@@ -1887,8 +1922,8 @@ extern "C" int cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* strea
 
 extern "C" int cc_engine_counters(cc_engine* e, uint64_t* out, uint32_t n) {
   if (!e || (n && !out)) return CC_ERR_INVALID;
-  const uint64_t v[3] = {e->stat_barriers, e->stat_isc, e->stat_subbatches};
-  for (uint32_t i = 0; i < n && i < 3; ++i) out[i] = v[i];
+  const uint64_t v[4] = {e->stat_barriers, e->stat_isc, e->stat_subbatches, e->stat_events};
+  for (uint32_t i = 0; i < n && i < 4; ++i) out[i] = v[i];
   return CC_OK;
 }
 

@@ -328,6 +328,8 @@ struct ClrSubArgs {
   uint32_t* base;
   uint8_t* eend;
   uint8_t* mflag;  // kMfClr: cleared in this sub-batch
+  uint8_t* btab;   // [R][nb] epochs at the row buckets' starts (common.h ClrCtx)
+  uint32_t nb, bshift;
   uint32_t* err;
   const uint64_t* index;
   uint64_t* ev_key;
@@ -341,12 +343,9 @@ int launch_clr_sub(const ClrSubArgs& a, hipStream_t st);
 int launch_clr_events(const ClrSubArgs& a, hipStream_t st);
 int launch_clr_gen(const ClrSubArgs& a, hipStream_t st);
 struct ClrReplayArgs {
-  const uint64_t* key;
+  const uint64_t* key;  // the sorted map events
   const uint32_t* val;
   const EvPay* pay;
-  const uint32_t* ctl;
-  const uint32_t* seg;
-  const uint32_t* nseg;
   const uint8_t* mflag;
   uint32_t* msize;
   uint32_t* mpcap;
@@ -354,8 +353,13 @@ struct ClrReplayArgs {
   const uint64_t* idx0;
   uint8_t* out_status;
   uint64_t* out_value;
+  void* scan;         // [events] clr_scan_bytes_per_event() each
+  void* temp;
+  size_t temp_bytes;  // >= clr_scan_temp_bytes(events)
 };
-int launch_clr_replay(const ClrReplayArgs& a, hipStream_t st);
+int launch_clr_replay(const ClrReplayArgs& a, uint32_t E, hipStream_t st);
+size_t clr_scan_temp_bytes(uint32_t cap);
+size_t clr_scan_bytes_per_event();
 int launch_cv_answer(const CvSubArgs& a, uint32_t E, hipStream_t st);
 size_t cv_sort_temp_bytes(uint32_t cap);
 struct MapWideArgs {

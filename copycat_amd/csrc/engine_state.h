@@ -188,6 +188,11 @@ struct cc_engine {
   uint32_t* d_sm_seg = nullptr;    // [max_resources + 1] run starts + count
   void* d_sm_temp = nullptr;
   size_t sm_temp_bytes = 0;
+  void* d_clr_scan = nullptr;  // the cleared maps' size scan (map_clear.hip), one element per map event
+  void* d_clr_stemp = nullptr;
+  size_t clr_scan_cap = 0, clr_stemp_bytes = 0;
+  uint8_t* d_clr_btab = nullptr;  // [R][nb] clear epochs per row bucket (common.h ClrCtx)
+  size_t clr_btab_bytes = 0;
   uint64_t sm_cap = 0;             // events the buffers hold (engine.hip small_cap_needed)
   bool small_live = false;         // some map may still be in the window (the host then reads the event count)
   // map size / isEmpty rows answered in the stream (outside TTL mode; map_small.hip k_size_answer)
@@ -219,7 +224,7 @@ struct cc_engine {
   void* d_cvtemp = nullptr;
   size_t cvtemp_bytes = 0;
   uint32_t cvev_cap = 0;
-  uint64_t stat_barriers = 0, stat_isc = 0, stat_subbatches = 0;  // cc_engine_counters
+  uint64_t stat_barriers = 0, stat_isc = 0, stat_subbatches = 0, stat_events = 0;  // cc_engine_counters
   // clears in the stream (map_clear.hip)
   uint32_t* d_clrq = nullptr;      // [clrq_cap] the batch's in-stream clear rows
   uint32_t* d_clrq_n = nullptr;

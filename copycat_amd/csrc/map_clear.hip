@@ -15,10 +15,11 @@
 //                  the entry reached in an earlier chunk) sees the entry absent before it -- the transformer CLEAR.el
 //                  of map_ops.h's family (a commit is still one element of the scan); at the end of the launch an
 //                  entry whose state predates its map's last clear of the sub-batch is dropped (DEAD, as k_map_drop);
-//                  a cleared map's keys are not hot-routed (k_hot_bind);
+//                  a cleared map's hot keys take the same epochs in the hot-key path (apply_map_hot.hip: CLEAR.el in the
+//                  piece scan, the state cleared before a commit of a later epoch);
 //   sizes          the flagged maps' insertions / removals are events (k_msize_count; their per-tile counts are left
-//                  out of the exact tracking), the clears join them (k_clr_events), and after the sort one wave per map
-//                  replays its run forward from the size at the sub-batch start: +1 / -1 / reset to 0, the peak ->
+//                  out of the exact tracking), the clears join them (k_clr_events), and after the sort a scan with resets
+//                  over all events gives each map's sizes from the one at the sub-batch start: +1 / -1 / 0, the peak ->
 //                  the capacity level (HashMap.resize never shrinks; clear() keeps the table) and its timeline, the
 //                  size / isEmpty rows answered on the way (k_clr_replay); a small map's HashMap model is emptied at
 //                  the clear (map_small.hip k_small_replay);
@@ -94,6 +95,26 @@ __global__ void k_clr_sub(const uint64_t* __restrict__ keys, const uint32_t* __r
   }
 }
 
+// per sub-batch: a cleared map's epoch at the start of each row bucket (clr_epoch's first step)
+__global__ void k_clr_btab(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
+                           const uint32_t* __restrict__ base, const uint8_t* __restrict__ eend,
+                           const uint8_t* __restrict__ mflag, uint32_t R, uint32_t nb, uint32_t bshift, uint64_t lo,
+                           uint8_t* __restrict__ btab) {
+  const uint64_t total = (uint64_t)R * nb;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t m = (uint32_t)(x / nb), b = (uint32_t)(x % nb);
+    if (!(mflag[m] & kMfClr)) continue;
+    const uint64_t* p = keys + off[m] + base[m];
+    const uint64_t row = lo + ((uint64_t)b << bshift);
+    uint32_t a = 0, c = eend[m];
+    while (a < c) {  // the clears before the bucket's first row
+      const uint32_t mid = (a + c) >> 1;
+      if ((p[mid] & 0xFFFFFFFFull) < row) a = mid + 1; else c = mid;
+    }
+    btab[x] = (uint8_t)a;
+  }
+}
+
 // per sub-batch: the clears of [lo, hi) join the map events (code 3: the size resets to 0)
 __global__ void k_clr_events(const uint64_t* __restrict__ keys, uint32_t n, uint64_t lo, uint64_t hi,
                              const uint64_t* __restrict__ index, uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val,
@@ -115,6 +136,9 @@ __global__ void k_clr_events(const uint64_t* __restrict__ keys, uint32_t n, uint
 int launch_clr_sub(const ClrSubArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_clr_sub, dim3((a.R + 255) / 256), dim3(256), 0, st, a.keys, a.off, a.R, a.lo, a.hi, a.base, a.eend,
                      a.mflag, a.err);
+  const uint64_t cells = (uint64_t)a.R * a.nb;
+  hipLaunchKernelGGL(k_clr_btab, dim3((uint32_t)std::min<uint64_t>(4096, (cells + 255) / 256)), dim3(256), 0, st, a.keys,
+                     a.off, a.base, a.eend, a.mflag, a.R, a.nb, a.bshift, a.lo, a.btab);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_clr_events(const ClrSubArgs& a, hipStream_t st) {
@@ -134,82 +158,113 @@ int launch_clr_gen(const ClrSubArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// One wave per run of a cleared map (the sorted event buffer, map_small.hip k_small_seg): the size from the sub-batch
-// start, +1 insert / -1 removal / 0 at a clear, in log order (a segmented scan: a clear starts a segment at 0); the
-// peak -> capacity level and the level timeline; size / isEmpty rows answered with the size before them.
-__global__ __launch_bounds__(256) void k_clr_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                    const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl,
-                                                    const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
+// The cleared maps' sizes over the sorted event buffer (map_small.hip k_small_seg's order: one map's events together, in
+// log order), flat over all events: the size after each event is a scan with resets -- +1 insert, -1 removal, reset
+// to 0 at a clear, reset to (size at the sub-batch start +- the event) at a map's first event -- and the peak since the
+// map's first event rides the same scan (a running maximum split at the first reset: before it relative, after it
+// absolute).  One hipcub scan of 16-byte elements, then one pass per event answers size / isEmpty rows, records the
+// capacity-level timeline and, at a map's last event, writes its size and capacity level.  (It was one wave per map
+// walking its run 64 events per step: a hot map's ~1M events per sub-batch took 3.4 ms of serial chunks.)
+constexpr int32_t kClrNeg = -(1 << 30);  // "no value" of a running maximum (sizes stay below 2^30)
+struct ClrS {
+  int32_t v;     // the size after the span (absolute when f & 1, else the span's net change)
+  int32_t pre;   // the highest size before the span's first reset, relative to the size entering it
+  int32_t post;  // the highest absolute size from the span's first reset on
+  uint32_t f;    // 1: the span holds a reset (a clear or a map's first event); 2: it holds a map's first event
+};
+struct ClrCompose {
+  __device__ ClrS operator()(const ClrS& a, const ClrS& b) const {
+    if (b.f & 2u) return b;  // (a map's first event: nothing before it matters)
+    ClrS r;
+    r.f = a.f | b.f;
+    r.v = (b.f & 1u) ? b.v : a.v + b.v;
+    const int32_t mid = a.v + b.pre;  // b's values before its first reset, on top of a
+    if (a.f & 1u) {
+      r.pre = a.pre;
+      r.post = max(max(a.post, mid), (b.f & 1u) ? b.post : kClrNeg);
+    } else {
+      r.pre = max(a.pre, mid);
+      r.post = (b.f & 1u) ? b.post : kClrNeg;
+    }
+    return r;
+  }
+};
+__device__ inline int32_t clr_delta(uint64_t k) {
+  if (k & 8u) return 0;  // a size / isEmpty query
+  const uint32_t c = (uint32_t)(k & 3u);
+  return c == 1u ? 1 : (c == 2u ? -1 : 0);
+}
+struct ClrElem {
+  const uint64_t* key;
+  const uint32_t* msize;
+  __device__ ClrS operator()(uint32_t i) const {
+    const uint64_t k = key[i];
+    const uint32_t m = (uint32_t)(k >> 44);
+    const bool clear = !(k & 8u) && (k & 3u) == 3u;
+    const int32_t d = clr_delta(k);
+    if (i == 0 || (uint32_t)(key[i - 1] >> 44) != m) {  // the map's first event: from its size at the sub-batch start
+      const int32_t s0 = (int32_t)msize[m];
+      const int32_t v = clear ? 0 : s0 + d;
+      return ClrS{v, kClrNeg, max(s0, v), 3u};
+    }
+    if (clear) return ClrS{0, kClrNeg, 0, 1u};
+    return ClrS{d, d, kClrNeg, 0u};
+  }
+};
+using ClrIt = hipcub::TransformInputIterator<ClrS, ClrElem, hipcub::CountingInputIterator<uint32_t>>;
+
+__global__ __launch_bounds__(256) void k_clr_finish(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                    const EvPay* __restrict__ pay, const ClrS* __restrict__ S, uint32_t E,
                                                     const uint8_t* __restrict__ mflag, uint32_t* __restrict__ msize,
                                                     uint32_t* __restrict__ mpcap, unsigned long long* __restrict__ lvl_at,
                                                     const uint64_t* __restrict__ idx0p, uint8_t* __restrict__ out_status,
                                                     uint64_t* __restrict__ out_value) {
-  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
-  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
-  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
-    const uint32_t start = seg[r];
-    const uint32_t m = (uint32_t)(key[start] >> 44);
-    if (!(mflag[m] & kMfClr)) continue;
-    int64_t size = msize[m];  // at the sub-batch start (the exact tracking leaves this map's counts out)
-    int64_t peak = size;      // (within the sub-batch: the level reached before is mpcap already)
-    for (uint32_t b = start;; b += kWave) {
-      const uint32_t i = b + l;
-      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
-      const uint64_t k = in ? key[i] : 0;
-      const bool query = in && (k & 8u);
-      const bool reset = in && !query && (k & 3u) == 3u;
-      const int32_t dlt = !in || query || reset ? 0 : ((k & 3u) == 1u ? 1 : ((k & 3u) == 2u ? -1 : 0));
-      int32_t inc = dlt;  // inclusive prefix of the deltas
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t y = __shfl_up(inc, d, 64);
-        if (l >= (uint32_t)d) inc += y;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
+    const uint64_t k = key[i];
+    const uint32_t m = (uint32_t)(k >> 44);
+    if (!(mflag[m] & kMfClr)) continue;  // (small / size-queried maps: map_small.hip)
+    const ClrS x = S[i];
+    const int32_t v = x.v;
+    if (k & 8u) {
+      const uint32_t row = pay[val[i]].aux;
+      if (k & 4u) {  // isEmpty
+        out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+        out_value[row] = v == 0 ? 1ull : 0ull;
+      } else {  // size: an int
+        out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_INT);
+        out_value[row] = (uint64_t)v;
       }
-      int32_t lr = reset ? (int32_t)l : -1;  // the last reset at or before this lane
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t y = __shfl_up(lr, d, 64);
-        if (l >= (uint32_t)d) lr = max(lr, y);
-      }
-      const int32_t at_reset = __shfl(inc, lr < 0 ? 0 : lr, 64);
-      const int64_t v = lr < 0 ? size + inc : (int64_t)(inc - at_reset);  // the size after this event
-      if (query) {
-        const uint32_t row = pay[val[i]].aux;
-        if (k & 4u) {  // isEmpty
-          out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
-          out_value[row] = v == 0 ? 1ull : 0ull;
-        } else {  // size: an int
-          out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_INT);
-          out_value[row] = (uint64_t)v;
-        }
-      }
-      // the peak so far (the running maximum over the lanes before this one and the chunk start's)
-      int64_t pk = in ? v : INT64_MIN;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int64_t y = __shfl_up(pk, d, 64);
-        if (l >= (uint32_t)d) pk = max(pk, y);
-      }
-      const int64_t pk_prev = __shfl_up(pk, 1, 64);  // (every lane shuffles: a read of an inactive lane is 0)
-      const int64_t before = l == 0 ? peak : max(peak, pk_prev);
-      if (lvl_at && in && dlt > 0 && v > before)  // an insertion growing the table (the capacity-level timeline)
-        lvl_reached(lvl_at, m, cap_level((uint64_t)max<int64_t>(before, 0)), cap_level((uint64_t)v),
-                    *idx0p + ((k >> 4) & ((1ull << 40) - 1)));
-      peak = max(peak, (int64_t)__shfl(pk, 63, 64));
-      const int32_t lr63 = __shfl(lr, 63, 64), inc63 = __shfl(inc, 63, 64), inc_lr = __shfl(inc, lr63 < 0 ? 0 : lr63, 64);
-      size = lr63 < 0 ? size + inc63 : (int64_t)(inc63 - inc_lr);
-      if (__ballot(in) != ~0ull) break;
     }
-    if (l == 0) {
-      msize[m] = (uint32_t)max<int64_t>(size, 0);
-      atomicMax(&mpcap[m], cap_level((uint64_t)max<int64_t>(peak, 0)));
+    const bool first = i == 0 || (uint32_t)(key[i - 1] >> 44) != m;
+    if (lvl_at && clr_delta(k) > 0) {  // an insertion growing the table (the capacity-level timeline)
+      const int32_t before = first ? v - 1 : S[i - 1].post;  // (the peak so far, the start size included)
+      if (v > before)
+        lvl_reached(lvl_at, m, cap_level((uint64_t)max(before, 0)), cap_level((uint64_t)v),
+                    *idx0p + ((k >> 4) & ((1ull << 40) - 1)));
+    }
+    if (i + 1 == E || (uint32_t)(key[i + 1] >> 44) != m) {  // the map's last event
+      msize[m] = (uint32_t)max(v, 0);
+      atomicMax(&mpcap[m], cap_level((uint64_t)max(x.post, 0)));
     }
   }
 }
 
-int launch_clr_replay(const ClrReplayArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_clr_replay, dim3(256), dim3(256), 0, st, a.key, a.val, a.pay, a.ctl, a.seg, a.nseg, a.mflag, a.msize,
-                     a.mpcap, a.lvl_at, a.idx0, a.out_status, a.out_value);
+size_t clr_scan_temp_bytes(uint32_t cap) {
+  size_t need = 0;
+  ClrIt it(hipcub::CountingInputIterator<uint32_t>(0), ClrElem{nullptr, nullptr});
+  (void)hipcub::DeviceScan::InclusiveScan(nullptr, need, it, (ClrS*)nullptr, ClrCompose{}, (int)cap, (hipStream_t)0);
+  return need;
+}
+size_t clr_scan_bytes_per_event() { return sizeof(ClrS); }
+
+int launch_clr_replay(const ClrReplayArgs& a, uint32_t E, hipStream_t st) {
+  if (E == 0) return 0;
+  ClrIt it(hipcub::CountingInputIterator<uint32_t>(0), ClrElem{a.key, a.msize});
+  size_t tb = a.temp_bytes;
+  ClrS* S = static_cast<ClrS*>(a.scan);
+  if (hipcub::DeviceScan::InclusiveScan(a.temp, tb, it, S, ClrCompose{}, (int)E, st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_clr_finish, dim3(std::min<uint32_t>(2048, (E + 255) / 256)), dim3(256), 0, st, a.key, a.val, a.pay, S,
+                     E, a.mflag, a.msize, a.mpcap, a.lvl_at, a.idx0, a.out_status, a.out_value);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

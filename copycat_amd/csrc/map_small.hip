@@ -12,9 +12,10 @@
 // replays its insertions and removals in log order:
 //   1. launch_map_size's count kernel (k_msize_count) emits one event per region commit of a small map that inserted
 //      or removed a key: key (map << 44 | (log index - the sub-batch's first) << 4 | insert / remove), value = the
-//      key's HashMap hash (hot-key routing is off for small maps, k_hot_bind, so every such commit is a region one);
+//      key's HashMap hash (k_hot_apply emits the same for the map's hot-key commits);
 //   2. a radix sort by that key puts each map's events in log order (hipcub);
-//   3. one thread per map replays them on an LDS copy of its HashMap: putVal (a chain of 9 calls treeifyBin: a
+//   3. alternating remove / put chains of one key are marked for skipping (k_small_chains), then one wave per map
+//      stages its events in LDS and lane 0 replays them on an LDS copy of its HashMap: putVal (a chain of 9 calls treeifyBin: a
 //      resize below 64, a red-black tree bin at 64), resize, removeNode.  The map leaves the window when its capacity
 //      passes 64; a bin that was a tree bin there keeps its mark (tree_bins; see map_wide.hip k_mw_order for the
 //      checks above 64).  Inside the window an order-dependent containsValue reads a bin's chain from this model.
@@ -46,163 +47,187 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
 // Alternating runs of one key (a hot key of a small map: remove k, put k, remove k, put k, ... with no other event of
 // the map between): in a list bin the net effect of remove k . put k is k moved to its chain's end, with the size
 // back where it was (no resize) and a chain no longer than before (no treeifyBin: a list chain of 9 cannot persist
-// below capacity 64), so R P R P ... R P == R P and R P ... R == R.  One wave per run of a map still in the window
-// finds the maximal alternating chains (commit events only: a clear, a size query or another key ends one) and
-// stores, at the chain's first removal, how many events after it are implied (EvPay.ktag >> 4).  k_small_replay
-// skips them when the key's bin is a list bin at that removal (a tree bin replays every event).
+// below capacity 64), so R P R P ... R P == R P and R P ... R == R.  The maximal alternating chains (commit events
+// only: a clear, a size query or another key ends one) are found flat over the sorted events: event i links to i - 1
+// when both are commits of the same map and key with different codes; a max-scan of (i if it does not link) gives
+// every event its chain's start; at each chain's end the number of events implied after its first removal is stored
+// there (EvPay.ktag >> 4).  k_small_replay skips them when the key's bin is a list bin at that removal (a tree bin
+// replays every event).  (It was one wave per map walking 64 events per step: ~5.5 ms per sub-batch for a hot map.)
 constexpr uint32_t kSkipShift = 4;
+__device__ inline uint32_t chain_code(uint64_t k) {
+  return !(k & 8u) && ((k & 3u) == 1u || (k & 3u) == 2u) ? (uint32_t)(k & 3u) : 0u;
+}
+struct ChainStart {  // i when event i starts a chain (does not link to i - 1), else 0
+  const uint64_t* key;
+  const uint32_t* val;
+  const EvPay* pay;
+  __device__ uint32_t operator()(uint32_t i) const {
+    if (i == 0) return 0;
+    const uint64_t k = key[i], q = key[i - 1];
+    const uint32_t c = chain_code(k), cq = chain_code(q);
+    if (!c || !cq || c == cq || (k >> 44) != (q >> 44)) return i;
+    const EvPay x = pay[val[i]], y = pay[val[i - 1]];
+    const bool link = x.key == y.key && x.aux == y.aux && (x.ktag & 3u) == (y.ktag & 3u);
+    return link ? 0u : i;
+  }
+};
+using ChainIt = hipcub::TransformInputIterator<uint32_t, ChainStart, hipcub::CountingInputIterator<uint32_t>>;
+size_t chain_scan_temp_bytes(uint32_t cap) {
+  size_t need = 0;
+  ChainIt it(hipcub::CountingInputIterator<uint32_t>(0), ChainStart{nullptr, nullptr, nullptr});
+  (void)hipcub::DeviceScan::InclusiveScan(nullptr, need, it, (uint32_t*)nullptr, hipcub::Max(), (int)cap, (hipStream_t)0);
+  return need;
+}
 __global__ __launch_bounds__(256) void k_small_chains(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                      EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl,
-                                                      const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
+                                                      EvPay* __restrict__ pay, const uint32_t* __restrict__ start, uint32_t E,
                                                       const SmallMap* __restrict__ st) {
-  const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
-  const uint32_t waves = gridDim.x * (blockDim.x / kWave);
-  for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
-    const uint32_t start = seg[r];
-    const uint32_t m = (uint32_t)(key[start] >> 44);
-    if (!(st[m].flags & kSmIn)) continue;  // (wave-uniform)
-    // the open chain, carried across chunks: its first event, its first removal, the previous event
-    uint32_t ca = 0xFFFFFFFFu, cr0 = 0xFFFFFFFFu, cf = 0;
-    uint64_t pkey = 0;
-    uint32_t pid = 0, pcode = 0;  // previous event's identity hash / code (0: not a commit event)
-    for (uint32_t b = start;; b += kWave) {
-      const uint32_t i = b + l;
-      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
-      const uint64_t k = in ? key[i] : 0;
-      const uint32_t code = in && !(k & 8u) && ((k & 3u) == 1u || (k & 3u) == 2u) ? (uint32_t)(k & 3u) : 0u;
-      const uint32_t v = in ? val[i] : 0u;
-      EvPay x{0, 0, 0};
-      if (code) x = pay[v];
-      const uint32_t id = x.aux ^ ((x.ktag & 3u) << 30);  // (with the key: the identity)
-      // the previous event (lane - 1, or the carried one for lane 0)
-      const uint64_t qk = __shfl_up(x.key, 1, 64);
-      const uint32_t qi = __shfl_up(id, 1, 64), qc = __shfl_up(code, 1, 64);
-      const uint64_t prk = l == 0 ? pkey : qk;
-      const uint32_t pri = l == 0 ? pid : qi, prc = l == 0 ? pcode : qc;
-      const bool link = code && prc && i > start && prk == x.key && pri == id && prc != code;
-      // chain starts: the last start at or before each lane (absolute index; none in the chunk: the carried one)
-      int32_t st_l = (in && !link) ? (int32_t)l : -1;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t y = __shfl_up(st_l, d, 64);
-        if (l >= (uint32_t)d) st_l = max(st_l, y);
-      }
-      const uint32_t fcode = __shfl(code, st_l < 0 ? 0 : st_l, 64);  // the chain's first code (if it starts here)
-      const uint32_t a = st_l < 0 ? ca : b + (uint32_t)st_l;
-      const uint32_t f = st_l < 0 ? cf : fcode;
-      const uint32_t r0 = st_l < 0 ? cr0 : (f == 1u ? a + 1 : a);
-      // a chain ends at lane i when the next event does not link (lane 63: decided with the next chunk's lane 0)
-      const bool nlink = __shfl_down((int)link, 1, 64) != 0;
-      const bool end_here = in && l < 63 && !nlink;
-      const uint32_t vr0 = __shfl(v, (r0 >= b && r0 < b + 64) ? (int)(r0 - b) : 0, 64);
-      const uint32_t cb_code = code;  // the chain's last event's code, at its end lane
-      if (end_here && code && r0 != 0xFFFFFFFFu && i > r0) {
-        const uint32_t skip = cb_code == 1u ? i - r0 - 1 : i - r0;
-        if (skip && r0 >= b) pay[vr0].ktag |= skip << kSkipShift;
-        else if (skip) pay[val[r0]].ktag |= skip << kSkipShift;  // (its first removal in an earlier chunk)
-      }
-      // carry: the chain open at lane 63, the last event
-      const uint64_t inb = __ballot(in);
-      const bool full = inb == ~0ull;
-      ca = (uint32_t)__shfl((int)a, 63, 64);
-      cf = (uint32_t)__shfl((int)f, 63, 64);
-      cr0 = (uint32_t)__shfl((int)r0, 63, 64);
-      pkey = __shfl(x.key, 63, 64);
-      pid = (uint32_t)__shfl((int)id, 63, 64);
-      pcode = (uint32_t)__shfl((int)code, 63, 64);
-      const uint32_t last_code = pcode;
-      if (!full) break;
-      // lane 63's chain continues only if the next chunk's lane 0 links: checked there (l == 0 uses pkey / pid /
-      // pcode); if it does not, the chain ended at lane 63 of this chunk
-      const uint32_t i0 = b + kWave;
-      bool next_in = i0 < E && (uint32_t)(key[i0] >> 44) == m;
-      bool next_link = false;
-      if (next_in) {
-        const uint64_t k0 = key[i0];
-        const uint32_t c0 = !(k0 & 8u) && ((k0 & 3u) == 1u || (k0 & 3u) == 2u) ? (uint32_t)(k0 & 3u) : 0u;
-        if (c0 && last_code) {
-          const EvPay y = pay[val[i0]];
-          next_link = y.key == pkey && (y.aux ^ ((y.ktag & 3u) << 30)) == pid && c0 != last_code;
-        }
-      }
-      if (!next_link && last_code && cr0 != 0xFFFFFFFFu && b + 63 > cr0 && l == 0) {  // the carried chain ended at lane 63
-        const uint32_t ib = b + 63;
-        const uint32_t skip = last_code == 1u ? ib - cr0 - 1 : ib - cr0;
-        if (skip) pay[val[cr0]].ktag |= skip << kSkipShift;
-      }
-      if (!next_link) {
-        ca = cr0 = 0xFFFFFFFFu;
-        pcode = 0;  // (lane 0 of the next chunk starts a chain)
-      }
-      if (!next_in) break;
-    }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
+    const uint32_t s0 = start[i];
+    if (s0 == i) continue;                               // (a chain of one event)
+    if (i + 1 < E && start[i + 1] != i + 1) continue;    // not the chain's end
+    const uint64_t k = key[i];
+    if (!(st[k >> 44].flags & kSmIn)) continue;          // (out of the window: not replayed)
+    const uint32_t r0 = (key[s0] & 3u) == 1u ? s0 + 1 : s0;  // the chain's first removal
+    if (i <= r0) continue;
+    const uint32_t skip = (k & 3u) == 1u ? i - r0 - 1 : i - r0;
+    if (skip) pay[val[r0]].ktag |= skip << kSkipShift;
   }
 }
 
-// One thread per run: the map's java.util.HashMap copied into LDS (small_jhm.h: node pool, chains, tree links),
-// its events applied in log order (putVal of a new key, removeNode), the state written back.  A map whose table
-// passes 64 leaves the window (its later events are not followed).
-constexpr int kSrT = 64;                                               // runs per workgroup
-constexpr int kSrStride = (int)((kSmHotBytes + 8) / 8) | 1;           // u64 words per run's copy (odd: fewer bank conflicts)
-__global__ __launch_bounds__(kSrT) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                       const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl, const uint32_t* __restrict__ seg,
-                                                       const uint32_t* __restrict__ nseg, SmallMap* __restrict__ st,
-                                                       uint8_t* __restrict__ msmall, uint32_t* __restrict__ mpcap,
-                                                       unsigned long long* __restrict__ lvl_at, const uint64_t* __restrict__ idx0,
-                                                       const uint64_t* __restrict__ index, uint64_t lo, bool ttl) {
-  __shared__ uint64_t lds[kSrT * kSrStride];
-  static_assert(kSmHotBytes % 8 == 0, "SmallMap copies are u64 words");
-  constexpr uint32_t W = kSmHotBytes / 8;  // the hot part; the keys stay in HBM (small_jhm.h)
-  SmallMap& lm = *reinterpret_cast<SmallMap*>(lds + threadIdx.x * kSrStride);
+// One wave per run: the map's java.util.HashMap copied whole into LDS (small_jhm.h: node pool, chains, tree links and
+// the keys), its events staged 64 at a time into LDS by the wave (keys and payloads: coalesced loads and one gather),
+// then applied in log order by lane 0 (putVal of a new key, removeNode), the state written back.  A map whose table
+// passes 64 leaves the window (its later events are not followed).  (One thread per run walked the events with three
+// dependent global loads each, plus the keys' HBM copy in removeNode: ~2.4 ms per c3 sub-batch for a hot map.)
+#ifdef CC_PHASE_TIMING  // diagnostics build (CC_SMALL_PHASES=1 cc_debug_phases(K_APPLY_MAP)): the replay's serial work
+__device__ unsigned long long g_ph_small[kPhases];  // events applied, max per map, runs, ticks, max ticks, max run length
+int phase_read_small(uint64_t* out) {
+  unsigned long long z[kPhases] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ph_small), sizeof z) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_ph_small), z, sizeof z) != hipSuccess)
+    return CC_ERR_HIP;
+  return CC_OK;
+}
+#endif
+constexpr int kSrW = 4;                                    // runs (waves) per workgroup
+constexpr int kSrWords = (int)(sizeof(SmallMap) / 8);      // u64 words per map copy
+static_assert(sizeof(SmallMap) % 8 == 0, "SmallMap copies are u64 words");
+__device__ inline void wave_lds_sync() {  // the wave's LDS writes visible to its own later reads (no workgroup barrier)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                              const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl,
+                                                              const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
+                                                              SmallMap* __restrict__ st, uint8_t* __restrict__ msmall,
+                                                              uint32_t* __restrict__ mpcap, unsigned long long* __restrict__ lvl_at,
+                                                              const uint64_t* __restrict__ idx0, const uint64_t* __restrict__ index,
+                                                              uint64_t lo, bool ttl) {
+  __shared__ uint64_t lds[kSrW][kSrWords];
+  __shared__ uint64_t bk[kSrW][kWave];  // the staged events' keys (~0: not this map's)
+  __shared__ EvPay bp[kSrW][kWave];
+  const uint32_t wv = threadIdx.x / kWave, l = __lane_id();
+  SmallMap& lm = *reinterpret_cast<SmallMap*>(lds[wv]);
   const uint32_t E = ctl[0], ns = *nseg;
-  for (uint32_t r = blockIdx.x * kSrT + threadIdx.x; r < ns; r += gridDim.x * kSrT) {
+  for (uint32_t r = blockIdx.x * kSrW + wv; r < ns; r += gridDim.x * kSrW) {  // (wave-uniform)
     const uint32_t start = seg[r];
     const uint32_t m = (uint32_t)(key[start] >> 44);
     SmallMap* s = st + m;
     if (!(s->flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
     const uint64_t* src = reinterpret_cast<const uint64_t*>(s);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(&lm);
-    for (uint32_t q = 0; q < W; ++q) dst[q] = src[q];
-    SmallJhm j(lm, *s);
-    for (uint32_t i = start; i < E; ++i) {
-      const uint64_t k = key[i];
-      if ((uint32_t)(k >> 44) != m) break;
-      if (k & 8u) continue;  // a size / isEmpty query (k_size_answer)
-      if ((k & 3u) == 3u) {  // MapState.clear in the stream (map_clear.hip): every key leaves, the table stays
-        for (uint32_t q = 0; q < 64; ++q) lm.tab[q] = 0;
+    for (uint32_t q = l; q < (uint32_t)kSrWords; q += kWave) lds[wv][q] = src[q];
+    SmallJhm j(lm, lm);
+#ifdef CC_PHASE_TIMING
+    const uint64_t t_run = wall_clock64();
+    uint32_t n_app = 0;
+#endif
+    uint32_t i = start;
+    for (;;) {  // (wave-uniform: i and the end are broadcast from lane 0)
+      const uint32_t ii = i + l;
+      uint64_t k = ~0ull;
+      EvPay x{0, 0, 0};
+      if (ii < E) {
+        const uint64_t kk = key[ii];
+        if ((uint32_t)(kk >> 44) == m) {
+          k = kk;
+          if (!(kk & 8u) && (kk & 3u) != 3u) x = pay[val[ii]];  // (a commit: its key; a clear or a query has none)
+        }
+      }
+      bk[wv][l] = k;
+      bp[wv][l] = x;
+      wave_lds_sync();
+      uint32_t nxt = 0, fin = 0;
+      if (l == 0) {
+        uint32_t q = 0;
+        for (; q < (uint32_t)kWave; ++q) {
+          const uint64_t kk = bk[wv][q];
+          if (kk == ~0ull) {  // the map's run ended
+            fin = 1;
+            break;
+          }
+          if (kk & 8u) continue;  // a size / isEmpty query (k_size_answer)
+          if ((kk & 3u) == 3u) {  // MapState.clear in the stream (map_clear.hip): every key leaves, the table stays
+            for (uint32_t b = 0; b < 64; ++b) lm.tab[b] = 0;
+            lm.n = 0;
+            lm.used = 0;
+            lm.flags &= ~(kSmTree | kSmAmbig);
+            lm.tree_bins = 0;
+            continue;
+          }
+          const EvPay y = bp[wv][q];
+#ifdef CC_PHASE_TIMING
+          ++n_app;
+#endif
+          if ((kk & 3u) == 1u) {  // a new key: HashMap.putVal
+            const uint32_t lv0 = lm.lvl;
+            const bool stay = j.put(y.aux, y.ktag & 3u, y.key);
+            if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
+              const uint64_t d = (kk >> 4) & ((1ull << 40) - 1);
+              // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
+              if (ttl ? index != nullptr : idx0 != nullptr)
+                lvl_reached(lvl_at, m, lv0, lm.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
+            }
+            if (!stay) {  // the table passed 64: out of the window
+              fin = 1;
+              break;
+            }
+          } else if ((kk & 3u) == 2u) {  // a key removed: removeNode
+            j.remove(y.aux, y.ktag & 3u, y.key);
+            // an alternating run of this key follows (k_small_chains): implied by this removal and, if the run ends
+            // with a put, that put -- in a list bin
+            const uint32_t skip = y.ktag >> kSkipShift;
+            if (skip && j.list_bin(y.aux)) q += skip;
+          }
+        }
+        nxt = i + q;
+      }
+      i = (uint32_t)__shfl((int)nxt, 0, kWave);
+      fin = (uint32_t)__shfl((int)fin, 0, kWave);
+      if (fin || i >= E) break;
+      wave_lds_sync();  // (lane 0 is done with the staged events)
+    }
+    if (l == 0) {
+#ifdef CC_PHASE_TIMING
+      const uint64_t dt = wall_clock64() - t_run;
+      atomicAdd(&g_ph_small[0], (unsigned long long)n_app);
+      atomicMax(&g_ph_small[1], (unsigned long long)n_app);
+      atomicAdd(&g_ph_small[2], 1ull);
+      atomicAdd(&g_ph_small[3], (unsigned long long)dt);
+      atomicMax(&g_ph_small[4], (unsigned long long)dt);
+      atomicMax(&g_ph_small[5], (unsigned long long)(i - start));
+#endif
+      if (!(lm.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
         lm.n = 0;
         lm.used = 0;
-        lm.flags &= ~(kSmTree | kSmAmbig);
-        lm.tree_bins = 0;
-        continue;
       }
-      const EvPay x = pay[val[i]];
-      if ((k & 3u) == 1u) {  // a new key: HashMap.putVal
-        const uint32_t lv0 = lm.lvl;
-        const bool stay = j.put(x.aux, x.ktag & 3u, x.key);
-        if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
-          const uint64_t d = (k >> 4) & ((1ull << 40) - 1);
-          // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
-          if (ttl ? index != nullptr : idx0 != nullptr)
-            lvl_reached(lvl_at, m, lv0, lm.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
-        }
-        if (!stay) break;  // the table passed 64: out of the window
-      } else if ((k & 3u) == 2u) {  // a key removed: removeNode
-        j.remove(x.aux, x.ktag & 3u, x.key);
-        // an alternating run of this key follows (k_small_chains): implied by this removal and, if the run ends with
-        // a put, that put -- in a list bin
-        const uint32_t skip = x.ktag >> kSkipShift;
-        if (skip && j.list_bin(x.aux)) i += skip;
-      }
+      msmall[m] = (uint8_t)((msmall[m] & ~kMfSmall) | ((lm.flags & kSmIn) ? kMfSmall : 0u));
+      atomicMax(&mpcap[m], lm.lvl);
     }
-    if (!(lm.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
-      lm.n = 0;
-      lm.used = 0;
-    }
+    wave_lds_sync();
     uint64_t* back = reinterpret_cast<uint64_t*>(s);
-    for (uint32_t q = 0; q < W; ++q) back[q] = dst[q];
-    msmall[m] = (uint8_t)((msmall[m] & ~kMfSmall) | ((lm.flags & kSmIn) ? kMfSmall : 0u));
-    atomicMax(&mpcap[m], lm.lvl);
+    for (uint32_t q = l; q < (uint32_t)kSrWords; q += kWave) back[q] = lds[wv][q];
+    wave_lds_sync();  // (the next run's copy overwrites lds[wv])
   }
 }
 
@@ -416,10 +441,15 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
     if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (E + 255) / 256);
     hipLaunchKernelGGL(k_small_seg, dim3(grid), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg);
-    if (!a.msize)  // (TTL mode replays its runs for sizes as well: every event there)
-      hipLaunchKernelGGL(k_small_chains, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, const_cast<EvPay*>(a.ev_pay), a.ctl,
-                         a.seg, a.nseg, a.state);
-    hipLaunchKernelGGL(k_small_replay, dim3(256), dim3(kSrT), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg, a.state,
+    if (!a.msize) {  // (TTL mode replays its runs for sizes as well: every event there)
+      // chain starts into the unsorted values' buffer (free after the sort)
+      ChainIt it(hipcub::CountingInputIterator<uint32_t>(0), ChainStart{a.ev_key2, a.ev_val2, a.ev_pay});
+      size_t tb = a.temp_bytes;
+      if (hipcub::DeviceScan::InclusiveScan(a.temp, tb, it, a.ev_val, hipcub::Max(), (int)E, st) != hipSuccess) return -1;
+      hipLaunchKernelGGL(k_small_chains, dim3(std::min<uint32_t>(2048, (E + 255) / 256)), dim3(256), 0, st, a.ev_key2,
+                         a.ev_val2, const_cast<EvPay*>(a.ev_pay), a.ev_val, E, a.state);
+    }
+    hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg, a.state,
                        a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
       hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap,
@@ -440,7 +470,7 @@ size_t small_sort_temp_bytes(uint32_t cap) {
   size_t need = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, need, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
-  return need;
+  return std::max(need, chain_scan_temp_bytes(cap));  // (the same scratch serves k_small_chains' scan)
 }
 
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st) {

@@ -609,15 +609,15 @@ __device__ inline void hot_pfx(const uint32_t* __restrict__ hot_n, const uint32_
 
 // A map commit's insertion / removal as an event (map_small.hip): its position (the log index's offset in the
 // sub-batch, or in TTL mode 2 * row offset + 1: common.h TtlEmit) and the key's HashMap hash.
-__device__ inline void map_event(uint32_t m, uint32_t code, uint64_t d, const MRec& xr, const uint64_t* __restrict__ hh_key,
-                                 const int32_t* __restrict__ hh_val, uint32_t hh_n, uint64_t* __restrict__ ev_key,
-                                 uint32_t* __restrict__ ev_val, EvPay* __restrict__ ev_pay, uint32_t ev_cap,
-                                 uint32_t* __restrict__ sm_ctl, uint32_t* __restrict__ err) {
+// (at: its slot in the event buffer)
+__device__ inline void map_event(uint32_t at, uint32_t m, uint32_t code, uint64_t d, const MRec& xr,
+                                 const uint64_t* __restrict__ hh_key, const int32_t* __restrict__ hh_val, uint32_t hh_n,
+                                 uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val, EvPay* __restrict__ ev_pay,
+                                 uint32_t ev_cap, uint32_t* __restrict__ err) {
   bool ok;
   const uint32_t kt = CC_FLAG_KTAG(smeta_flags(xr.meta));
   const uint32_t jh = java_key_hash(kt, xr.key, hh_key, hh_val, hh_n, ok);
   if (!ok || d >> 40) atomicOr(err, kErrHandleHash);  // an unregistered String key / a sub-batch spanning 2^40 indices
-  const uint32_t at = wave_append(sm_ctl);
   if (at < ev_cap) {
     ev_key[at] = ((uint64_t)m << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
     ev_val[at] = at;
@@ -687,6 +687,45 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
   const uint32_t b0 = row[k0], b1 = row[sb_hot];
   const uint32_t* w = msz + (uint64_t)t * kTile;
   uint32_t* out = tcnt + (uint64_t)t * R;
+  if (map_row || msmall) {
+    // the tile's map events: counted per thread, one event-buffer reservation for the workgroup, then written (one
+    // global atomic per tile: a wave_append per wave and step was ~250K atomics on one counter per c3 sub-batch)
+    auto evm = [&](uint32_t x) {
+      return (x & 3u) && (map_row || (msmall[x >> 2] & (kMfSmall | kMfSize | kMfClr)));
+    };
+    uint32_t my = 0;
+    for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) my += evm(w[p]) ? 1u : 0u;
+    __shared__ uint32_t wsum[kMszT / kWave], ebase;
+    const uint32_t l = __lane_id(), wv = threadIdx.x / kWave;
+    uint32_t inc = my;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, kWave);
+      if (l >= (uint32_t)d) inc += y;
+    }
+    if (l == kWave - 1) wsum[wv] = inc;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (uint32_t q = 0; q < kMszT / kWave; ++q) {
+        const uint32_t c = wsum[q];
+        wsum[q] = tot;
+        tot += c;
+      }
+      ebase = tot ? atomicAdd(sm_ctl, tot) : 0u;
+    }
+    lds_barrier();
+    uint32_t at = ebase + wsum[wv] + inc - my;
+    for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
+      const uint32_t x = w[p];
+      if (!evm(x)) continue;
+      const uint64_t g = (uint64_t)t * kTile + p;
+      // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip); else small,
+      // size-queried or cleared maps' commits by log index
+      const uint64_t d = map_row ? 2 * ((uint64_t)map_row[g] - lo) + 1 : xrec[g].idx - *idx0p;
+      map_event(at++, x >> 2, x & 3u, d, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_pay, ev_cap, err);
+    }
+  }
   for (uint32_t base = 0; base < R; base += kMszPass) {
     const uint32_t span = min(kMszPass, R - base);
     for (uint32_t q = threadIdx.x; q < span; q += kMszT) cnt[q] = 0;
@@ -696,15 +735,6 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
       // (a map cleared in the stream: its sizes come from event replay, map_clear.hip k_clr_replay)
       if (code && m < span && !(msmall && (msmall[x >> 2] & kMfClr)))
         atomicAdd(&cnt[m], code == 1u ? 1u : 0x10000u);  // <= 16384 each: halves never carry
-      if (code && base == 0) {
-        const uint64_t g = (uint64_t)t * kTile + p;
-        if (map_row)  // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip)
-          map_event(x >> 2, code, 2 * ((uint64_t)map_row[g] - lo) + 1, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val,
-                    ev_pay, ev_cap, sm_ctl, err);
-        else if (msmall && (msmall[x >> 2] & (kMfSmall | kMfSize | kMfClr)))  // small, size-queried or cleared map
-          map_event(x >> 2, code, xrec[g].idx - *idx0p, xrec[g], hh_key, hh_val, hh_n, ev_key, ev_val, ev_pay, ev_cap,
-                    sm_ctl, err);
-      }
     }
     for (uint32_t i = threadIdx.x; i < nwords; i += kMszT) {  // one code word (16 list positions) per thread
       uint32_t h = 0, hb = nh;  // the last key whose words start at or before i (keys without words are skipped)

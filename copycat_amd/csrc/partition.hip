@@ -130,12 +130,14 @@ __global__ __launch_bounds__(NT) void k_unpermute(const uint16_t* __restrict__ c
 int phase_read_value(uint64_t* out);
 int phase_read_coord(uint64_t* out);
 int phase_read_map(uint64_t* out);
+int phase_read_small(uint64_t* out);
 int phase_read_partx(uint64_t* out);
 int phase_read_v3(int kernel, uint64_t* out);
 int phase_read(int kernel, uint64_t* out) {
 #ifdef CC_PHASE_TIMING
   if ((kernel == K_PART_TILE || kernel == K_APPLY_VALUE) && getenv("CC_V3_PHASES")) return phase_read_v3(kernel, out);
   if (kernel == K_APPLY_VALUE) return phase_read_value(out);
+  if (kernel == K_APPLY_MAP && getenv("CC_SMALL_PHASES")) return phase_read_small(out);
   if (kernel == K_APPLY_MAP) return phase_read_map(out);
   if (kernel == K_PART_TILE && getenv("CC_PART_EXT_PHASES")) return phase_read_partx(out);
   if (kernel == K_APPLY_COORD) return phase_read_coord(out);

@@ -377,9 +377,9 @@ class Engine:
         return self.L.cc_engine_stream(self.h)
 
     def counters(self):
-        """(barrier rows applied, containsValue rows answered in the stream, sub-batches) since creation."""
-        out = np.zeros(3, np.uint64)
-        _check(self.L.cc_engine_counters(self.h, out.ctypes.data, 3))
+        """(barrier rows applied, containsValue rows answered in the stream, sub-batches, map events) since creation."""
+        out = np.zeros(4, np.uint64)
+        _check(self.L.cc_engine_counters(self.h, out.ctypes.data, 4))
         return tuple(int(x) for x in out)
 
     def applied_index(self):

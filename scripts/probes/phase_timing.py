@@ -100,7 +100,14 @@ def run_c3(args):
     from copycat_amd.workload import map_zipf_rows
 
     n, R = args.commits, 4096
-    db = DeviceBatch.upload(map_zipf_rows(0, n, maps=R, pairs=1 << 20, threads=8), device="cuda:0")
+    hb = map_zipf_rows(0, n, maps=R, pairs=1 << 20, threads=8)
+    if args.cv_rate or args.clear_rate:  # bench.py's whole-map variant
+        sys.path.insert(0, ROOT)
+        from bench import c3_whole_map_rows
+        from copycat_amd.workload import SEED_C3
+
+        c3_whole_map_rows(hb, 0, args.cv_rate, args.clear_rate, SEED_C3)
+    db = DeviceBatch.upload(hb, device="cuda:0")
     st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
     va = torch.zeros(n, dtype=torch.int64, device="cuda:0")
     E = Engine(R, R, n, device=0, sub_batch=args.sub_batch, map_capacity=1 << 20)
@@ -114,6 +121,9 @@ def run_c3(args):
     E.sync()
     for k in (0, 3):
         L.cc_debug_phases(E.h, k, ticks)
+    os.environ["CC_SMALL_PHASES"] = "1"
+    L.cc_debug_phases(E.h, 3, ticks)
+    del os.environ["CC_SMALL_PHASES"]
     E.profile(True)
     for _ in range(args.steps):
         E.apply(db, st, va)
@@ -133,6 +143,12 @@ def run_c3(args):
             if ticks[q]:
                 print(f"   {PHASES[k][q]:18s} {ticks[q] * 10e-3 / wgs[k]:9.2f} us/WG  {100.0 * ticks[q] / tot:5.1f} %")
     print({k: round(v[0] / args.steps, 3) for k, v in prof.items()})
+    os.environ["CC_SMALL_PHASES"] = "1"
+    assert L.cc_debug_phases(E.h, 3, ticks) == 0
+    t = list(ticks)
+    print(f"k_small_replay over {args.steps} steps: events applied {t[0]}, max per map {t[1]}, runs {t[2]}, "
+          f"lane-0 time {t[3] * 10e-3:.0f} us total, max per map {t[4] * 10e-3:.0f} us, longest run {t[5]} events")
+    print("counters", E.counters())
 
 
 PHASES_PARTX = ["route+hist+ttab", "rank", "wave-prefix", "run-start scan", "place", "write-out", "top(clear,issue)", "-"]
@@ -249,6 +265,8 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--sub-batch", type=int, default=0)
     ap.add_argument("--c5", action="store_true", help="the coordination kernel on the c5 stream")
+    ap.add_argument("--cv-rate", type=float, default=0.0, help="--c3: share of containsValue rows (bench.py)")
+    ap.add_argument("--clear-rate", type=float, default=0.0, help="--c3: share of clear rows (bench.py)")
     ap.add_argument("--interleave", action="store_true", help="--c5: slot r holds type r %% len(types)")
     ap.add_argument("--group64", action="store_true", help="--c5: 64-slot groups of one type, types in turn")
     ap.add_argument("--manager", action="store_true", help="--c5: resources created through cc_create_resource in turn")
