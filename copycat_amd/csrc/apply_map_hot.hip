@@ -399,19 +399,22 @@ __device__ inline bool hot_cleared(const HotClr& c, uint32_t slot) {
 __device__ inline bool hot_events(const HotClr& c, uint32_t slot) {
   return c.mflag != nullptr && (c.mflag[slot] & (kMfSmall | kMfSize | kMfClr)) != 0;
 }
-__device__ inline void hot_map_event(const HotClr& c, uint32_t slot, uint32_t code, const MRec& r, uint32_t& err) {
-  if (!code) return;
+// (at: its slot in the event buffer, reserved by the caller)
+__device__ inline void hot_map_event_at(const HotClr& c, uint32_t slot, uint32_t code, const MRec& r, uint32_t at,
+                                        uint32_t& err) {
   bool ok;
   const uint32_t kt = CC_FLAG_KTAG(smeta_flags(r.meta));
   const uint32_t jh = java_key_hash(kt, r.key, c.hh_key, c.hh_val, c.hh_n, ok);
   const uint64_t d = r.idx - *c.idx0p;
   if (!ok || d >> 40) err |= kErrHandleHash;
-  const uint32_t at = wave_append(c.ev_ctl);
   if (at < c.ev_cap) {
     c.ev_key[at] = ((uint64_t)slot << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
     c.ev_val[at] = at;
     c.ev_pay[at] = EvPay{r.key, jh, kt};
   }
+}
+__device__ inline void hot_map_event(const HotClr& c, uint32_t slot, uint32_t code, const MRec& r, uint32_t& err) {
+  if (code) hot_map_event_at(c, slot, code, r, wave_append(c.ev_ctl), err);
 }
 
 __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ hot_meta, const uint32_t* __restrict__ hot_n,
@@ -571,6 +574,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
   __shared__ Comp wtot[kHT / kWave];
   __shared__ Comp carry;
   __shared__ uint32_t lrpre[kMaxTiles + 1], lrst[kMaxTiles];
+  __shared__ uint32_t evw[kHT / kWave], evbase;  // the item's map events: per-wave counts, the workgroup's reservation
   uint32_t nh;
   hot_items(hot_n, hot_len, pfx, nh);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
@@ -671,12 +675,13 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
       if (l > 0) lanes = o;
     }
     pre = compose(pre, lanes);
+    uint32_t codes = 0;
     if (p0 < L) {
       uint32_t sw;
       uint64_t sv, ci, ins;
       materialize(pre, s0, xr, sw, sv, ci, ins);
       static_assert(kHPer == 16 || kHPer == 8 || kHPer == 4, "size-change codes: whole bytes per thread and piece");
-      uint32_t codes = 0, qe = pe0;
+      uint32_t qe = pe0;
 #pragma unroll
       for (int q = 0; q < kHPer; ++q)
         if (p0 + q < e) {
@@ -687,7 +692,6 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
           qe = es[q];
           const uint32_t code = hot_step(gs[q], ms[q], mrec_ab(xr[gs[q]], cb, row0, gs[q]), xr[gs[q]].idx, sw, sv, ci, ins,
                                          rst_status, rst_value, cv, es[q], err);
-          if (evs) hot_map_event(hc, slot, code, xr[gs[q]], err);
           codes |= code << (2 * q);
         }
       // (consecutive threads: consecutive words / halves / bytes of the code words, little-endian)
@@ -700,6 +704,34 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
         tbl_ci[pos] = ci;
         tbl_ins[pos] = ins;
         if (fl) hc.tbl_ep[pos] = (uint8_t)qe;  // (the region launch drops the entry if it predates the last clear)
+      }
+    }
+    if (evs) {  // (item-uniform) the map events of the item's insertions / removals: one reservation for the
+                // workgroup (a wave_append per commit step was ~80K atomics on one counter per c3 sub-batch)
+      const uint32_t mine = __popc((codes | (codes >> 1)) & 0x55555555u);
+      uint32_t inc = mine;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, kWave);
+        if (l >= (uint32_t)d) inc += y;
+      }
+      if (l == kWave - 1) evw[w] = inc;
+      __syncthreads();
+      if (t == 0) {
+        uint32_t tot = 0;
+        for (int q = 0; q < kHT / kWave; ++q) {
+          const uint32_t c = evw[q];
+          evw[q] = tot;
+          tot += c;
+        }
+        evbase = tot ? atomicAdd(hc.ev_ctl, tot) : 0u;
+      }
+      __syncthreads();
+      uint32_t at = evbase + evw[w] + inc - mine;
+#pragma unroll
+      for (int q = 0; q < kHPer; ++q) {
+        const uint32_t code = (codes >> (2 * q)) & 3u;
+        if (code) hot_map_event_at(hc, slot, code, xr[gs[q]], at++, err);
       }
     }
     __syncthreads();

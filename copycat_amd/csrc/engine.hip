@@ -103,7 +103,7 @@ static void free_all(cc_engine* e) {
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
                   e->d_cvset,    e->d_cvcnt,    e->d_cvev_key, e->d_cvev_key2, e->d_cvev_val, e->d_cvev_val2, e->d_cvev_ctl,
                   e->d_cvseg,    e->d_cvtemp,   e->d_clrq,    e->d_clrq_n,   e->d_clr_keys,   e->d_clr_keys2, e->d_clr_off,
-                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep, e->d_clr_scan, e->d_clr_stemp, e->d_clr_btab};
+                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep, e->d_clr_scan, e->d_clr_stemp, e->d_clr_btab, e->d_sm_cseg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -160,6 +160,7 @@ static int ensure_small(cc_engine* e) {
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_val2, 4 * cap);
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_pay, sizeof(EvPay) * cap);
   if (x == hipSuccess && !e->d_sm_seg) x = hipMalloc(&e->d_sm_seg, 4ull * (e->cfg.max_resources + 1));
+  if (x == hipSuccess && !e->d_sm_cseg) x = hipMalloc(&e->d_sm_cseg, 4ull * (e->cfg.max_resources + 2));
   if (x == hipSuccess) x = hipMalloc(&e->d_sm_temp, tb);
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events", x);
   e->sm_temp_bytes = tb;
@@ -1609,6 +1610,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.ctl = e->d_sm_ctl;
           sa.seg = e->d_sm_seg;
           sa.nseg = e->d_sm_seg + e->cfg.max_resources;
+          sa.cseg = e->d_sm_cseg;
           sa.state = e->d_msm;
           sa.msmall = e->d_msmall;
           sa.mpcap = e->d_mpcap;

@@ -192,6 +192,10 @@ struct SmallArgs {
   uint32_t* ctl;               // [0] events, [1] maps still in the window (after the replay)
   uint32_t* seg;               // [max_resources] run starts
   uint32_t* nseg;
+  // outside TTL mode: the replayed maps' events without the ones alternating chains imply (k_small_chains), as
+  // positions in the sorted buffer (written over ev_key), their count and runs: [max_resources] starts, then the
+  // run count, then the event count (null: every event is replayed, TTL mode)
+  uint32_t* cseg;
   SmallMap* state;             // [max_resources]
   uint8_t* msmall;
   uint32_t* mpcap;

@@ -186,6 +186,7 @@ struct cc_engine {
   uint64_t *d_sm_key = nullptr, *d_sm_key2 = nullptr;  // [sm_cap] map events (small / size-queried maps; TTL mode: all)
   uint32_t *d_sm_val = nullptr, *d_sm_val2 = nullptr;
   uint32_t* d_sm_seg = nullptr;    // [max_resources + 1] run starts + count
+  uint32_t* d_sm_cseg = nullptr;  // the replayed events without implied chain events: runs, counts (map_small.hip)
   void* d_sm_temp = nullptr;
   size_t sm_temp_bytes = 0;
   void* d_clr_scan = nullptr;  // the cleared maps' size scan (map_clear.hip), one element per map event

@@ -45,14 +45,15 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
 }
 
 // Alternating runs of one key (a hot key of a small map: remove k, put k, remove k, put k, ... with no other event of
-// the map between): in a list bin the net effect of remove k . put k is k moved to its chain's end, with the size
-// back where it was (no resize) and a chain no longer than before (no treeifyBin: a list chain of 9 cannot persist
-// below capacity 64), so R P R P ... R P == R P and R P ... R == R.  The maximal alternating chains (commit events
-// only: a clear, a size query or another key ends one) are found flat over the sorted events: event i links to i - 1
-// when both are commits of the same map and key with different codes; a max-scan of (i if it does not link) gives
-// every event its chain's start; at each chain's end the number of events implied after its first removal is stored
-// there (EvPay.ktag >> 4).  k_small_replay skips them when the key's bin is a list bin at that removal (a tree bin
-// replays every event).  (It was one wave per map walking 64 events per step: ~5.5 ms per sub-batch for a hot map.)
+// the map between): in a list bin of <= 7 nodes after the removal, the net effect of remove k . put k is k moved to
+// its chain's end, with the size back where it was (no resize) and a chain of <= 8 (no treeifyBin), so
+// R P R P ... R P == R P and R P ... R == R.  (A list chain of 9 does persist below capacity 64 -- treeifyBin's
+// resize keeps it whole when its keys share the new bit -- and a put into it calls treeifyBin again: such a bin, and
+// a tree bin, replays every event.)  The maximal alternating chains (commit events only: a clear, a size query or
+// another key ends one) are found flat over the sorted events: event i links to i - 1 when both are commits of the
+// same map and key with different codes; a max-scan of (i if it does not link) gives every event its chain's start;
+// at each chain's end the number of events implied after its first removal is stored there (EvPay.ktag >> 4), and
+// k_small_replay checks the bin at that removal.  (It was one wave per map walking 64 events per step: ~5.5 ms per sub-batch for a hot map.)
 constexpr uint32_t kSkipShift = 4;
 __device__ inline uint32_t chain_code(uint64_t k) {
   return !(k & 8u) && ((k & 3u) == 1u || (k & 3u) == 2u) ? (uint32_t)(k & 3u) : 0u;
@@ -93,6 +94,41 @@ __global__ __launch_bounds__(256) void k_small_chains(const uint64_t* __restrict
     if (skip) pay[val[r0]].ktag |= skip << kSkipShift;
   }
 }
+// The events k_small_replay walks: those of maps in the window, less the ones a chain implies (after its first
+// removal, all but a final put).  Compacted once (hipcub select), the hot map's ~180K events per c3 sub-batch are
+// ~2.5K to replay, read 64 at a time, instead of a fresh dependent read at every chain end.  The replay steps into
+// the implied ones only when the chain's bin is a tree bin there (rare: tables of 64 with a bin of 9).
+struct ChainKeep {
+  const uint64_t* key;
+  const uint32_t* start;
+  const SmallMap* st;
+  uint32_t E;
+  __device__ uint8_t operator()(uint32_t i) const {
+    const uint64_t k = key[i];
+    if (!(st[k >> 44].flags & kSmIn)) return 0;  // (not replayed)
+    const uint32_t s0 = start[i];
+    if (s0 == i) return 1;
+    const uint32_t r0 = (key[s0] & 3u) == 1u ? s0 + 1 : s0;
+    if (i <= r0) return 1;
+    const bool end = i + 1 == E || start[i + 1] == i + 1;
+    return end && (k & 3u) == 1u ? 1 : 0;
+  }
+};
+using KeepIt = hipcub::TransformInputIterator<uint8_t, ChainKeep, hipcub::CountingInputIterator<uint32_t>>;
+size_t keep_select_temp_bytes(uint32_t cap) {
+  size_t need = 0;
+  KeepIt it(hipcub::CountingInputIterator<uint32_t>(0), ChainKeep{nullptr, nullptr, nullptr, 0});
+  (void)hipcub::DeviceSelect::Flagged(nullptr, need, hipcub::CountingInputIterator<uint32_t>(0), it, (uint32_t*)nullptr,
+                                      (uint32_t*)nullptr, (int)cap, (hipStream_t)0);
+  return need;
+}
+// the compacted events' runs (one per map)
+__global__ void k_small_cseg(const uint64_t* __restrict__ key, const uint32_t* __restrict__ orig, uint32_t* __restrict__ cseg,
+                             uint32_t R) {
+  const uint32_t n = cseg[R + 1];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    if (i == 0 || (key[orig[i]] >> 44) != (key[orig[i - 1]] >> 44)) cseg[atomicAdd(&cseg[R], 1u)] = i;
+}
 
 // One wave per run: the map's java.util.HashMap copied whole into LDS (small_jhm.h: node pool, chains, tree links and
 // the keys), its events staged 64 at a time into LDS by the wave (keys and payloads: coalesced loads and one gather),
@@ -118,7 +154,8 @@ __device__ inline void wave_lds_sync() {  // the wave's LDS writes visible to it
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                                              const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl,
+                                                              const EvPay* __restrict__ pay, const uint32_t* __restrict__ orig,
+                                                              const uint32_t* __restrict__ ctl,
                                                               const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
                                                               SmallMap* __restrict__ st, uint8_t* __restrict__ msmall,
                                                               uint32_t* __restrict__ mpcap, unsigned long long* __restrict__ lvl_at,
@@ -127,12 +164,13 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
   __shared__ uint64_t lds[kSrW][kSrWords];
   __shared__ uint64_t bk[kSrW][kWave];  // the staged events' keys (~0: not this map's)
   __shared__ EvPay bp[kSrW][kWave];
+  __shared__ uint32_t bo[kSrW][kWave];  // their positions in the sorted buffer
   const uint32_t wv = threadIdx.x / kWave, l = __lane_id();
   SmallMap& lm = *reinterpret_cast<SmallMap*>(lds[wv]);
   const uint32_t E = ctl[0], ns = *nseg;
   for (uint32_t r = blockIdx.x * kSrW + wv; r < ns; r += gridDim.x * kSrW) {  // (wave-uniform)
     const uint32_t start = seg[r];
-    const uint32_t m = (uint32_t)(key[start] >> 44);
+    const uint32_t m = (uint32_t)(key[orig ? orig[start] : start] >> 44);
     SmallMap* s = st + m;
     if (!(s->flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
     const uint64_t* src = reinterpret_cast<const uint64_t*>(s);
@@ -147,17 +185,39 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
       const uint32_t ii = i + l;
       uint64_t k = ~0ull;
       EvPay x{0, 0, 0};
+      uint32_t o = 0;
       if (ii < E) {
-        const uint64_t kk = key[ii];
+        o = orig ? orig[ii] : ii;
+        const uint64_t kk = key[o];
         if ((uint32_t)(kk >> 44) == m) {
           k = kk;
-          if (!(kk & 8u) && (kk & 3u) != 3u) x = pay[val[ii]];  // (a commit: its key; a clear or a query has none)
+          if (!(kk & 8u) && (kk & 3u) != 3u) x = pay[val[o]];  // (a commit: its key; a clear or a query has none)
         }
       }
       bk[wv][l] = k;
       bp[wv][l] = x;
+      bo[wv][l] = o;
       wave_lds_sync();
       uint32_t nxt = 0, fin = 0;
+      // one insertion / removal on the model; false: the table passed 64 (out of the window)
+      auto apply = [&](uint64_t kk, const EvPay& y) -> bool {
+#ifdef CC_PHASE_TIMING
+        ++n_app;
+#endif
+        if ((kk & 3u) == 1u) {  // a new key: HashMap.putVal
+          const uint32_t lv0 = lm.lvl;
+          const bool stay = j.put(y.aux, y.ktag & 3u, y.key);
+          if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
+            const uint64_t d = (kk >> 4) & ((1ull << 40) - 1);
+            // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
+            if (ttl ? index != nullptr : idx0 != nullptr)
+              lvl_reached(lvl_at, m, lv0, lm.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
+          }
+          return stay;
+        }
+        j.remove(y.aux, y.ktag & 3u, y.key);  // a key removed: removeNode
+        return true;
+      };
       if (l == 0) {
         uint32_t q = 0;
         for (; q < (uint32_t)kWave; ++q) {
@@ -176,28 +236,35 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
             continue;
           }
           const EvPay y = bp[wv][q];
-#ifdef CC_PHASE_TIMING
-          ++n_app;
-#endif
-          if ((kk & 3u) == 1u) {  // a new key: HashMap.putVal
-            const uint32_t lv0 = lm.lvl;
-            const bool stay = j.put(y.aux, y.ktag & 3u, y.key);
-            if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
-              const uint64_t d = (kk >> 4) & ((1ull << 40) - 1);
-              // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
-              if (ttl ? index != nullptr : idx0 != nullptr)
-                lvl_reached(lvl_at, m, lv0, lm.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
+          // a removal followed by the put of the same key (a hot key's remove / put, or the two ends of a compacted
+          // alternating run): a no-op when the key is the last node of a list bin of <= 8 nodes
+          if ((kk & 3u) == 2u && q + 1 < (uint32_t)kWave) {
+            const uint64_t kn = bk[wv][q + 1];
+            const EvPay yn = bp[wv][q + 1];
+            if (kn != ~0ull && chain_code(kn) == 1u && yn.key == y.key && yn.aux == y.aux &&
+                (yn.ktag & 3u) == (y.ktag & 3u) && j.list_tail(y.aux, y.ktag & 3u, y.key, 8)) {
+              ++q;  // (and every remove / put pair the run implies between them: the key stays the tail)
+              continue;
             }
-            if (!stay) {  // the table passed 64: out of the window
-              fin = 1;
-              break;
+          }
+          if (!apply(kk, y)) {  // the table passed 64: out of the window
+            fin = 1;
+            break;
+          }
+          // a removal starting an alternating run of its key (k_small_chains): in a list bin of <= 7 nodes after it
+          // the run's events after it are implied (the compacted events leave them out; else skipped here); in a
+          // tree bin, or a list bin long enough for a put to call treeifyBin, each is applied
+          const uint32_t skip = (kk & 3u) == 2u ? y.ktag >> kSkipShift : 0u;
+          if (skip) {
+            const bool implied = j.list_len(y.aux) <= 7u;
+            if (!orig) {
+              if (implied) q += skip;
+            } else if (!implied) {
+              const uint32_t o0 = bo[wv][q];
+              for (uint32_t u = o0 + 1; u <= o0 + skip && !fin; ++u)
+                if (!apply(key[u], pay[val[u]])) fin = 1;
+              if (fin) break;
             }
-          } else if ((kk & 3u) == 2u) {  // a key removed: removeNode
-            j.remove(y.aux, y.ktag & 3u, y.key);
-            // an alternating run of this key follows (k_small_chains): implied by this removal and, if the run ends
-            // with a put, that put -- in a list bin
-            const uint32_t skip = y.ktag >> kSkipShift;
-            if (skip && j.list_bin(y.aux)) q += skip;
           }
         }
         nxt = i + q;
@@ -449,7 +516,21 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
       hipLaunchKernelGGL(k_small_chains, dim3(std::min<uint32_t>(2048, (E + 255) / 256)), dim3(256), 0, st, a.ev_key2,
                          a.ev_val2, const_cast<EvPay*>(a.ev_pay), a.ev_val, E, a.state);
     }
-    hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg, a.state,
+    const bool cmp = a.cseg != nullptr && !a.msize;  // the compacted events (outside TTL mode)
+    uint32_t* const orig = reinterpret_cast<uint32_t*>(a.ev_key);  // (free after the sort)
+    if (cmp) {
+      KeepIt it(hipcub::CountingInputIterator<uint32_t>(0), ChainKeep{a.ev_key2, a.ev_val, a.state, E});
+      size_t tb = a.temp_bytes;
+      if (hipMemsetAsync(a.cseg + a.max_resources, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+      if (hipcub::DeviceSelect::Flagged(a.temp, tb, hipcub::CountingInputIterator<uint32_t>(0), it, orig,
+                                        a.cseg + a.max_resources + 1, (int)E, st) != hipSuccess)
+        return -1;
+      hipLaunchKernelGGL(k_small_cseg, dim3(std::min<uint32_t>(1024, (E + 255) / 256)), dim3(256), 0, st, a.ev_key2, orig,
+                         a.cseg, a.max_resources);
+    }
+    hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, st, a.ev_key2, a.ev_val2, a.ev_pay,
+                       cmp ? orig : nullptr, cmp ? a.cseg + a.max_resources + 1 : a.ctl, cmp ? a.cseg : a.seg,
+                       cmp ? a.cseg + a.max_resources : a.nseg, a.state,
                        a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
       hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap,
@@ -470,7 +551,8 @@ size_t small_sort_temp_bytes(uint32_t cap) {
   size_t need = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, need, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
-  return std::max(need, chain_scan_temp_bytes(cap));  // (the same scratch serves k_small_chains' scan)
+  // (the same scratch serves k_small_chains' scan and the compaction's select)
+  return std::max(need, std::max(chain_scan_temp_bytes(cap), keep_select_temp_bytes(cap)));
 }
 
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st) {

@@ -53,6 +53,25 @@ struct SmallJhm {
     const uint32_t hd = s.tab[(cap() - 1) & h];
     return hd == 0 || !tree(hd);
   }
+  // the chain length of a list bin (a tree bin: kSmNodes + 1)
+  __device__ uint32_t list_len(uint32_t h) const {
+    uint32_t q = s.tab[(cap() - 1) & h], n = 0;
+    if (q && tree(q)) return kSmNodes + 1;
+    for (; q && n <= kSmNodes; q = next(q)) ++n;
+    return n;
+  }
+  // the live key (kt, key) with hash h is the last node of a list bin of at most `most` nodes: removeNode then putVal
+  // of it changes nothing (it is linked back where it was, no treeifyBin, the size and threshold as before)
+  __device__ bool list_tail(uint32_t h, uint32_t kt, uint64_t key, uint32_t most) const {
+    uint32_t q = s.tab[(cap() - 1) & h];
+    if (!q || tree(q)) return false;
+    for (uint32_t n = 1; n <= most; ++n, q = next(q)) {
+      const uint32_t nx = next(q);
+      if (hash(q) == h && g.kt[q - 1] == kt && g.key[q - 1] == key) return nx == 0;
+      if (!nx) return false;
+    }
+    return false;
+  }
 
   __device__ uint32_t alloc(uint32_t h, uint32_t kt, uint64_t key) {
     const uint64_t free = ~s.used;

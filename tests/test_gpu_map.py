@@ -721,3 +721,48 @@ def test_map_contains_value_compacting_churn_parity(seed):
                 mb = [kk & 1023 for kk, vv in live[m].items() if vv == v]
                 same += bool(nb and mb and min(nb) == min(mb))
     assert same >= 20, same
+
+
+@pytest.mark.parametrize("seed,nbin", [(601, 11), (602, 11), (603, 9)])
+def test_small_map_alternating_chains_tree_bin(seed, nbin):
+    """A small map (capacity <= 64) whose bin 5 holds nbin Long keys i * 2^22 + 5: 11 make it a red-black tree bin;
+    9 leave a list chain of 9 at capacity 32 (treeifyBin's resize keeps it whole), where a put after a removal calls
+    treeifyBin again (resize to 64, then a tree bin).  Long alternating remove / put chains of one key of that bin and
+    of one key in a list bin, stored nulls, and containsValue rows whose answer is decided inside a bin
+    (map_small.hip: chains compacted away in short list bins, applied one by one otherwise; the small model gives
+    the bin's order).  Several sub-batches, hot keys."""
+    rng = np.random.default_rng(seed)
+    tree = [(i << 22) + 5 for i in range(nbin)]
+    lst = [7, 8, 9, 40]
+    L, N = abi.CC_TAG_LONG, abi.CC_TAG_NULL
+    rows = [(abi.CC_OP_MAP_PUT, k, L, 1 + k % 3) for k in tree + lst]
+    hot = [tree[3], lst[0]]
+    while len(rows) < 60_000:
+        u = rng.random()
+        if u < 0.75:
+            h = hot[int(rng.integers(2))]
+            for _ in range(int(rng.integers(1, 14))):
+                rows.append((abi.CC_OP_MAP_REMOVE, h, N, 0))
+                rows.append((abi.CC_OP_MAP_PUT, h, L, int(rng.integers(1, 4))))
+        elif u < 0.87:
+            k = tree[int(rng.integers(len(tree)))]
+            rows.append((abi.CC_OP_MAP_PUT, k, N if rng.random() < 0.3 else L, int(rng.integers(1, 4))))
+        elif u < 0.93:
+            k = (tree + lst)[int(rng.integers(len(tree) + len(lst)))]
+            rows.append((abi.CC_OP_MAP_REMOVE, k, N, 0))
+            if rng.random() < 0.7:
+                rows.append((abi.CC_OP_MAP_PUT, k, L, int(rng.integers(1, 4))))
+        else:
+            rows.append((abi.CC_OP_MAP_CONTAINSVALUE, 0, L, int(rng.integers(1, 4))))
+    op, key, tag, val = (np.array(c) for c in zip(*rows))
+    n = len(op)
+    b = Batch.from_columns(index=np.arange(1, n + 1, dtype=np.uint64), inst=np.zeros(n, np.uint32),
+                           op=op.astype(np.uint8), flags=np.array([abi.cc_flags(int(t), 0, 0) for t in tag], np.uint8),
+                           key=key.astype(np.uint64), a=val.astype(np.uint64))
+    E, O = _engines(1, 4, n, 4096, sub_batch=16384)
+    gs, gv, os_, ov = _apply_both(E, O, [b.slice(0, n // 3), b.slice(n // 3, n)])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, [0])
+    cv = np.nonzero(op == abi.CC_OP_MAP_CONTAINSVALUE)[0]
+    npe = int((gs[cv] == abi.cc_status(abi.CC_ST_NULL_POINTER, abi.CC_TAG_NULL)).sum())
+    assert 0 < npe < len(cv)  # both outcomes occur
