@@ -465,6 +465,9 @@ constexpr uint8_t kMfClr = 8u;
 __device__ inline void mflag_or(uint8_t* mflag, uint32_t m, uint8_t bit) {
   atomicOr(reinterpret_cast<uint32_t*>(mflag + (m & ~3u)), (uint32_t)bit << (8 * (m & 3u)));
 }
+__device__ inline void mflag_and(uint8_t* mflag, uint32_t m, uint8_t keep) {
+  atomicAnd(reinterpret_cast<uint32_t*>(mflag + (m & ~3u)), ~((uint32_t)(uint8_t)~keep << (8 * (m & 3u))));
+}
 // a map commit's size change for the exact size tracking (map_wide.hip launch_map_size): slot << 2 | 1 insert, 2 remove
 __device__ inline uint32_t msz_word(uint32_t slot, bool was, bool now) {
   return (slot << 2) | (now && !was ? 1u : !now && was ? 2u : 0u);

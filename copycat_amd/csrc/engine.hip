@@ -110,6 +110,13 @@ static void free_all(cc_engine* e) {
     if (p) (void)hipFree(p), p = nullptr;
   if (e->d_hh_key) (void)hipFree(e->d_hh_key);
   if (e->d_hh_val) (void)hipFree(e->d_hh_val);
+  if (e->side_st) (void)hipStreamSynchronize(e->side_st);
+  void* alt[] = {e->sm_alt.key, e->sm_alt.key2, e->sm_alt.val, e->sm_alt.val2, e->sm_alt.pay, e->sm_alt.cseg};
+  for (void* p : alt)
+    if (p) (void)hipFree(p);
+  for (hipEvent_t ev : {e->ev_prep, e->ev_rep[0], e->ev_rep[1]})
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->side_st) (void)hipStreamDestroy(e->side_st);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
 
@@ -141,11 +148,21 @@ static int ensure_leak(cc_engine* e, uint64_t need) {
 static uint64_t small_cap_needed(const cc_engine* e) {
   return e->ttl_live ? 2 * e->sub_batch + e->map_entries : e->sub_batch;
 }
+static void free_sm_alt(cc_engine* e) {
+  if (e->side_st) (void)hipStreamSynchronize(e->side_st);
+  e->rep_pending[0] = e->rep_pending[1] = false;
+  void* alt[] = {e->sm_alt.key, e->sm_alt.key2, e->sm_alt.val, e->sm_alt.val2, e->sm_alt.pay, e->sm_alt.cseg};
+  for (void* p : alt)
+    if (p) (void)hipFree(p);
+  e->sm_alt = cc_engine::SmSet{};
+  e->sm_alt_on = false;
+}
 static int ensure_small(cc_engine* e) {
   const uint64_t cap = small_cap_needed(e);
   if (e->d_sm_key && e->sm_cap >= cap) return CC_OK;
   if (cap > 0xFFFFFFFFull) return set_err(CC_ERR_CAPACITY, "map event buffer beyond 2^32 entries");
   if (e->d_sm_key) {  // grown (TTL mode): the counters keep their buffer, the events are rebuilt per sub-batch
+    free_sm_alt(e);  // (the side stream's replay is done with either set)
     void* ps[] = {e->d_sm_key, e->d_sm_key2, e->d_sm_val, e->d_sm_val2, e->d_sm_temp, e->d_sm_pay};
     for (void* p : ps) (void)hipFree(p);
     e->d_sm_key = e->d_sm_key2 = nullptr;
@@ -165,6 +182,33 @@ static int ensure_small(cc_engine* e) {
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events", x);
   e->sm_temp_bytes = tb;
   e->sm_cap = cap;
+  return CC_OK;
+}
+// the second event-buffer set and the side stream of the overlapped small-map replay (engine_state.h SmSet)
+static int ensure_sm_alt(cc_engine* e) {
+  if (e->sm_alt_on) return CC_OK;
+  const uint64_t cap = e->sm_cap;
+  hipError_t x = hipSuccess;
+  if (!e->side_st) x = hipStreamCreateWithFlags(&e->side_st, hipStreamNonBlocking);
+  for (hipEvent_t* ev : {&e->ev_prep, &e->ev_rep[0], &e->ev_rep[1]})
+    if (x == hipSuccess && !*ev) x = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+  if (x == hipSuccess) x = hipMalloc(&e->sm_alt.key, 8 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->sm_alt.key2, 8 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->sm_alt.val, 4 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->sm_alt.val2, 4 * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->sm_alt.pay, sizeof(EvPay) * cap);
+  if (x == hipSuccess) x = hipMalloc(&e->sm_alt.cseg, 4ull * (e->cfg.max_resources + 2));
+  if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc map events (second set)", x);
+  e->sm_alt_on = true;
+  return CC_OK;
+}
+// the engine stream waits for the side stream's replays (before barrier rows, timers, and the batch's end)
+static int join_replay(cc_engine* e, hipStream_t st) {
+  for (int k = 0; k < 2; ++k)
+    if (e->rep_pending[k]) {
+      HIPCHECK(hipStreamWaitEvent(st, e->ev_rep[k], 0));
+      e->rep_pending[k] = false;
+    }
   return CC_OK;
 }
 
@@ -858,7 +902,11 @@ static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = null
   sa.lvl_at = e->d_lvl_at;
   sa.index = index;  // (null for the expiry-only flushes: they grow no table)
   sa.lo = lo;
-  const int rs = launch_small_replay(sa, ctl[0], st);
+  {
+    int rc = join_replay(e, st);  // (an overlapped replay of an earlier sub-batch: the models it writes)
+    if (rc) return rc;
+  }
+  const int rs = launch_small_replay(sa, ctl[0], st, st);
   if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "TTL map events launch", hipGetLastError())
                           : set_err(CC_ERR_STATE, "TTL map events exceed their buffer");
   if (launch_small_finish(sa, st)) return set_err(CC_ERR_HIP, "map event counters", hipGetLastError());
@@ -1196,6 +1244,19 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   const uint64_t seg_hi = action == 2 ? tim_b : (action == 1 ? bar_b : n);
   for (uint64_t lo = seg_lo, hi; lo < seg_hi; lo = hi) {
     hi = std::min(seg_hi, lo + e->sub_batch);
+    if (e->sm_alt_on && !e->ttl_live) {  // the other event-buffer set, once its replay is done (engine_state.h SmSet)
+      std::swap(e->d_sm_key, e->sm_alt.key);
+      std::swap(e->d_sm_key2, e->sm_alt.key2);
+      std::swap(e->d_sm_val, e->sm_alt.val);
+      std::swap(e->d_sm_val2, e->sm_alt.val2);
+      std::swap(e->d_sm_pay, e->sm_alt.pay);
+      std::swap(e->d_sm_cseg, e->sm_alt.cseg);
+      e->sm_cur ^= 1;
+      if (e->rep_pending[e->sm_cur]) {
+        HIPCHECK(hipStreamWaitEvent(st, e->ev_rep[e->sm_cur], 0));
+        e->rep_pending[e->sm_cur] = false;
+      }
+    }
     for (const auto& hv : e->clr_heavy) {  // at most 127 in-stream clears of one map per sub-batch (map_clear.hip)
       const size_t q = (size_t)(std::lower_bound(hv.begin(), hv.end(), (uint32_t)lo) - hv.begin());
       if (q + 127 < hv.size() && hv[q + 127] < hi) hi = hv[q + 127];
@@ -1617,7 +1678,18 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.max_resources = e->cfg.max_resources;
           sa.lvl_at = e->d_lvl_at;
           sa.idx0 = c->index + lo;
-          const int rs = launch_small_replay(sa, ctl[0], st);
+          hipStream_t rst = st;  // the replay overlaps the next sub-batch on the side stream (engine_state.h SmSet)
+          if (ctl[0] && !getenv("CC_NO_SIDE_REPLAY")) {
+            int rc = ensure_sm_alt(e);
+            if (rc) return rc;
+            rst = e->side_st;
+            sa.ev_prep = e->ev_prep;
+          }
+          const int rs = launch_small_replay(sa, ctl[0], st, rst);
+          if (rst != st) {
+            HIPCHECK(hipEventRecord(e->ev_rep[e->sm_cur], rst));
+            e->rep_pending[e->sm_cur] = true;
+          }
           if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "small-map replay launch", hipGetLastError())
                                   : set_err(CC_ERR_STATE, "small-map events exceed their buffer");
           if (e->small_live && ctl[0] == 0 && ctl[1] == 0) e->small_live = false;  // (ctl[1]: maps small after the last replay)
@@ -1738,6 +1810,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ea.mark = marker_of(e);
       if (launch_events(ea, st)) return set_err(CC_ERR_HIP, "events launch", hipGetLastError()); DBG_SYNC("events launch");
     }
+  }
+  {
+    int rc = join_replay(e, st);  // (barrier rows, timers and the caller read the small maps' models)
+    if (rc) return rc;
   }
   if (action == 2) {  // a group timer fires here (MembershipGroupState.java:92-98)
     cc_engine::GroupTimer gt = e->gtimers[tk];

@@ -196,6 +196,7 @@ struct SmallArgs {
   // positions in the sorted buffer (written over ev_key), their count and runs: [max_resources] starts, then the
   // run count, then the event count (null: every event is replayed, TTL mode)
   uint32_t* cseg;
+  hipEvent_t ev_prep;          // (a replay on another stream: recorded after the sort and compaction)
   SmallMap* state;             // [max_resources]
   uint8_t* msmall;
   uint32_t* mpcap;
@@ -211,7 +212,8 @@ struct SmallArgs {
 // TTL mode: the table entries whose timers fire at a boundary the sub-batch owns -> expiry events (common.h TtlEmit)
 int launch_ttl_scan(const TtlEmit& t, const uint64_t* clock_base, const uint32_t* word, const uint64_t* key,
                     const uint64_t* dl, uint64_t entries, uint32_t* err, hipStream_t st);
-int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st);  // sort, runs, replay (E events)
+// sort, runs, replay (E events); the replay kernel itself on stream rst (after a.ev_prep, when rst != st)
+int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStream_t rst);
 int launch_small_finish(const SmallArgs& a, hipStream_t st);              // counters for the next sub-batch
 // size / isEmpty rows of the sub-batch [lo, hi): emitted into the event buffer before the sort (query entries), then
 // answered from the sorted buffer after the unpermute (the row's staged result is a placeholder)

@@ -187,6 +187,21 @@ struct cc_engine {
   uint32_t *d_sm_val = nullptr, *d_sm_val2 = nullptr;
   uint32_t* d_sm_seg = nullptr;    // [max_resources + 1] run starts + count
   uint32_t* d_sm_cseg = nullptr;  // the replayed events without implied chain events: runs, counts (map_small.hip)
+  // Outside TTL mode the small-map replay of sub-batch i runs on a side stream while sub-batch i + 1 runs on the
+  // engine's: the event buffers alternate between two sets (swapped at each sub-batch start), a set is reused only
+  // after its replay finished (ev_rep), and the engine stream waits for the side stream before barrier rows, timers
+  // and the batch's end (join_replay).
+  struct SmSet {
+    uint64_t *key = nullptr, *key2 = nullptr;
+    uint32_t *val = nullptr, *val2 = nullptr;
+    EvPay* pay = nullptr;
+    uint32_t* cseg = nullptr;
+  } sm_alt;
+  bool sm_alt_on = false;
+  hipStream_t side_st = nullptr;
+  hipEvent_t ev_prep = nullptr, ev_rep[2] = {nullptr, nullptr};
+  bool rep_pending[2] = {false, false};
+  int sm_cur = 0;
   void* d_sm_temp = nullptr;
   size_t sm_temp_bytes = 0;
   void* d_clr_scan = nullptr;  // the cleared maps' size scan (map_clear.hip), one element per map event

@@ -88,10 +88,11 @@ __global__ void k_clr_sub(const uint64_t* __restrict__ keys, const uint32_t* __r
     base[m] = pl - a0;
     if (ph - pl > 127u) atomicOr(err, kErrCapacity);  // (the host cuts sub-batches so that this never holds)
     eend[m] = (uint8_t)min(ph - pl, 127u);
-    // kMfClr marks the maps cleared in THIS sub-batch: the others keep the exact size tracking and hot-key routing
+    // kMfClr marks the maps cleared in THIS sub-batch: the others keep the exact size tracking (atomic on the flag
+    // word: an overlapped small-map replay may update the map's kMfSmall meanwhile)
     const uint8_t f = mflag[m];
-    const uint8_t g = (uint8_t)((f & ~kMfClr) | (ph > pl ? kMfClr : 0u));
-    if (g != f) mflag[m] = g;
+    if (ph > pl && !(f & kMfClr)) mflag_or(mflag, m, kMfClr);
+    else if (ph == pl && (f & kMfClr)) mflag_and(mflag, m, (uint8_t)~kMfClr);
   }
 }
 

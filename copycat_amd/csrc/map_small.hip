@@ -130,11 +130,12 @@ __global__ void k_small_cseg(const uint64_t* __restrict__ key, const uint32_t* _
     if (i == 0 || (key[orig[i]] >> 44) != (key[orig[i - 1]] >> 44)) cseg[atomicAdd(&cseg[R], 1u)] = i;
 }
 
-// One wave per run: the map's java.util.HashMap copied whole into LDS (small_jhm.h: node pool, chains, tree links and
-// the keys), its events staged 64 at a time into LDS by the wave (keys and payloads: coalesced loads and one gather),
-// then applied in log order by lane 0 (putVal of a new key, removeNode), the state written back.  A map whose table
-// passes 64 leaves the window (its later events are not followed).  (One thread per run walked the events with three
-// dependent global loads each, plus the keys' HBM copy in removeNode: ~2.4 ms per c3 sub-batch for a hot map.)
+// One wave per run: the map's java.util.HashMap loaded into the wave's registers (small_jhm.h: node i and bin i in
+// lane i), its events staged 64 at a time, one per lane (coalesced loads and one gather), then applied in log order
+// by the whole wave in lockstep (putVal of a new key, removeNode; every value uniform, each event read from its lane
+// with v_readlane), the state written back.  A map whose table passes 64 leaves the window (its later events are not
+// followed).  (One thread per run walked the events with three dependent global loads each: ~2.4 ms per c3
+// sub-batch for a hot map; an LDS copy walked by one lane still paid ~100 cycles per dependent field access.)
 #ifdef CC_PHASE_TIMING  // diagnostics build (CC_SMALL_PHASES=1 cc_debug_phases(K_APPLY_MAP)): the replay's serial work
 __device__ unsigned long long g_ph_small[kPhases];  // events applied, max per map, runs, ticks, max ticks, max run length
 int phase_read_small(uint64_t* out) {
@@ -145,13 +146,10 @@ int phase_read_small(uint64_t* out) {
   return CC_OK;
 }
 #endif
-constexpr int kSrW = 4;                                    // runs (waves) per workgroup
-constexpr int kSrWords = (int)(sizeof(SmallMap) / 8);      // u64 words per map copy
-static_assert(sizeof(SmallMap) % 8 == 0, "SmallMap copies are u64 words");
-__device__ inline void wave_lds_sync() {  // the wave's LDS writes visible to its own later reads (no workgroup barrier)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+constexpr int kSrW = 4;  // runs (waves) per workgroup
+__device__ inline uint32_t rlane(uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); }
+__device__ inline uint64_t rlane64(uint64_t v, uint32_t i) {
+  return (uint64_t)rlane((uint32_t)(v >> 32), i) << 32 | rlane((uint32_t)v, i);
 }
 __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
                                                               const EvPay* __restrict__ pay, const uint32_t* __restrict__ orig,
@@ -161,121 +159,125 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
                                                               uint32_t* __restrict__ mpcap, unsigned long long* __restrict__ lvl_at,
                                                               const uint64_t* __restrict__ idx0, const uint64_t* __restrict__ index,
                                                               uint64_t lo, bool ttl) {
-  __shared__ uint64_t lds[kSrW][kSrWords];
-  __shared__ uint64_t bk[kSrW][kWave];  // the staged events' keys (~0: not this map's)
-  __shared__ EvPay bp[kSrW][kWave];
-  __shared__ uint32_t bo[kSrW][kWave];  // their positions in the sorted buffer
   const uint32_t wv = threadIdx.x / kWave, l = __lane_id();
-  SmallMap& lm = *reinterpret_cast<SmallMap*>(lds[wv]);
   const uint32_t E = ctl[0], ns = *nseg;
   for (uint32_t r = blockIdx.x * kSrW + wv; r < ns; r += gridDim.x * kSrW) {  // (wave-uniform)
     const uint32_t start = seg[r];
     const uint32_t m = (uint32_t)(key[orig ? orig[start] : start] >> 44);
     SmallMap* s = st + m;
     if (!(s->flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(s);
-    for (uint32_t q = l; q < (uint32_t)kSrWords; q += kWave) lds[wv][q] = src[q];
-    SmallJhm j(lm, lm);
+    SmallJhm j;
+    j.load(*s);
 #ifdef CC_PHASE_TIMING
     const uint64_t t_run = wall_clock64();
     uint32_t n_app = 0;
 #endif
+    // one insertion / removal on the model (the whole wave, uniform arguments); false: the table passed 64
+    auto apply = [&](uint64_t kk, uint64_t ykey, uint32_t yh, uint32_t ykt) -> bool {
+#ifdef CC_PHASE_TIMING
+      ++n_app;
+#endif
+      if ((kk & 3u) == 1u) {  // a new key: HashMap.putVal
+        const uint32_t lv0 = j.lvl;
+        const bool stay = j.put(yh, ykt, ykey);
+        if (j.lvl > lv0 && lvl_at && l == 0) {  // the table grew at this commit: the capacity-level timeline (common.h)
+          const uint64_t d = (kk >> 4) & ((1ull << 40) - 1);
+          // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
+          if (ttl ? index != nullptr : idx0 != nullptr)
+            lvl_reached(lvl_at, m, lv0, j.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
+        }
+        return stay;
+      }
+      j.remove(yh, ykt, ykey);  // a key removed: removeNode
+      return true;
+    };
     uint32_t i = start;
-    for (;;) {  // (wave-uniform: i and the end are broadcast from lane 0)
+    bool fin = false;
+#ifdef CC_PHASE_TIMING
+    uint64_t t_stage = 0;
+#endif
+    while (!fin && i < E) {  // (wave-uniform)
+#ifdef CC_PHASE_TIMING
+      const uint64_t ts0 = wall_clock64();
+#endif
+      // lane l stages event i + l: its key (~0: another map's, or past the end), payload, sorted position
       const uint32_t ii = i + l;
-      uint64_t k = ~0ull;
-      EvPay x{0, 0, 0};
-      uint32_t o = 0;
+      uint64_t k = ~0ull, xkey = 0;
+      uint32_t xaux = 0, xkt = 0, o = 0;
       if (ii < E) {
         o = orig ? orig[ii] : ii;
         const uint64_t kk = key[o];
         if ((uint32_t)(kk >> 44) == m) {
           k = kk;
-          if (!(kk & 8u) && (kk & 3u) != 3u) x = pay[val[o]];  // (a commit: its key; a clear or a query has none)
+          if (!(kk & 8u) && (kk & 3u) != 3u) {  // (a commit: its key; a clear or a query has none)
+            const EvPay x = pay[val[o]];
+            xkey = x.key;
+            xaux = x.aux;
+            xkt = x.ktag;
+          }
         }
       }
-      bk[wv][l] = k;
-      bp[wv][l] = x;
-      bo[wv][l] = o;
-      wave_lds_sync();
-      uint32_t nxt = 0, fin = 0;
-      // one insertion / removal on the model; false: the table passed 64 (out of the window)
-      auto apply = [&](uint64_t kk, const EvPay& y) -> bool {
 #ifdef CC_PHASE_TIMING
-        ++n_app;
+      {  // (the staged values must have landed: a use of each)
+        const uint32_t dep = (uint32_t)k ^ (uint32_t)xkey ^ xaux ^ xkt ^ o;
+        if (__builtin_amdgcn_readfirstlane((int)dep) == 0x7FFFFFFF) n_app += 0;
+        t_stage += wall_clock64() - ts0;
+      }
 #endif
-        if ((kk & 3u) == 1u) {  // a new key: HashMap.putVal
-          const uint32_t lv0 = lm.lvl;
-          const bool stay = j.put(y.aux, y.ktag & 3u, y.key);
-          if (lm.lvl > lv0 && lvl_at) {  // the table grew at this commit: the capacity-level timeline (common.h)
-            const uint64_t d = (kk >> 4) & ((1ull << 40) - 1);
-            // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
-            if (ttl ? index != nullptr : idx0 != nullptr)
-              lvl_reached(lvl_at, m, lv0, lm.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
-          }
-          return stay;
+      uint32_t q = 0;
+      for (; q < (uint32_t)kWave; ++q) {
+        const uint64_t kk = rlane64(k, q);
+        if (kk == ~0ull) {  // the map's run ended
+          fin = true;
+          break;
         }
-        j.remove(y.aux, y.ktag & 3u, y.key);  // a key removed: removeNode
-        return true;
-      };
-      if (l == 0) {
-        uint32_t q = 0;
-        for (; q < (uint32_t)kWave; ++q) {
-          const uint64_t kk = bk[wv][q];
-          if (kk == ~0ull) {  // the map's run ended
-            fin = 1;
-            break;
-          }
-          if (kk & 8u) continue;  // a size / isEmpty query (k_size_answer)
-          if ((kk & 3u) == 3u) {  // MapState.clear in the stream (map_clear.hip): every key leaves, the table stays
-            for (uint32_t b = 0; b < 64; ++b) lm.tab[b] = 0;
-            lm.n = 0;
-            lm.used = 0;
-            lm.flags &= ~(kSmTree | kSmAmbig);
-            lm.tree_bins = 0;
+        if (kk & 8u) continue;  // a size / isEmpty query (k_size_answer)
+        if ((kk & 3u) == 3u) {  // MapState.clear in the stream (map_clear.hip): every key leaves, the table stays
+          j.w1 &= ~0xFF0000u;   // (every bin head)
+          j.n = 0;
+          j.used = 0;
+          j.flags &= ~(kSmTree | kSmAmbig);
+          j.tree_bins = 0;
+          continue;
+        }
+        const uint64_t ykey = rlane64(xkey, q);
+        const uint32_t yh = rlane(xaux, q), ykt = rlane(xkt, q);
+        // a removal followed by the put of the same key (a hot key's remove / put, or the two ends of a compacted
+        // alternating run): a no-op when the key is the last node of a list bin of <= 8 nodes
+        if ((kk & 3u) == 2u && q + 1 < (uint32_t)kWave) {
+          const uint64_t kn = rlane64(k, q + 1);
+          if (kn != ~0ull && chain_code(kn) == 1u && rlane64(xkey, q + 1) == ykey && rlane(xaux, q + 1) == yh &&
+              (rlane(xkt, q + 1) & 3u) == (ykt & 3u) && j.list_tail(yh, ykt & 3u, ykey, 8)) {
+            ++q;  // (and every remove / put pair the run implies between them: the key stays the tail)
             continue;
           }
-          const EvPay y = bp[wv][q];
-          // a removal followed by the put of the same key (a hot key's remove / put, or the two ends of a compacted
-          // alternating run): a no-op when the key is the last node of a list bin of <= 8 nodes
-          if ((kk & 3u) == 2u && q + 1 < (uint32_t)kWave) {
-            const uint64_t kn = bk[wv][q + 1];
-            const EvPay yn = bp[wv][q + 1];
-            if (kn != ~0ull && chain_code(kn) == 1u && yn.key == y.key && yn.aux == y.aux &&
-                (yn.ktag & 3u) == (y.ktag & 3u) && j.list_tail(y.aux, y.ktag & 3u, y.key, 8)) {
-              ++q;  // (and every remove / put pair the run implies between them: the key stays the tail)
-              continue;
+        }
+        if (!apply(kk, ykey, yh, ykt & 3u)) {  // the table passed 64: out of the window
+          fin = true;
+          break;
+        }
+        // a removal starting an alternating run of its key (k_small_chains): in a list bin of <= 7 nodes after it
+        // the run's events after it are implied (the compacted events leave them out; else skipped here); in a tree
+        // bin, or a list bin long enough for a put to call treeifyBin, each is applied
+        const uint32_t skip = (kk & 3u) == 2u ? ykt >> kSkipShift : 0u;
+        if (skip) {
+          const bool implied = j.list_len(yh) <= 7u;
+          if (!orig) {
+            if (implied) q += skip;
+          } else if (!implied) {
+            const uint32_t o0 = rlane(o, q);
+            for (uint32_t u = o0 + 1; u <= o0 + skip && !fin; ++u) {
+              const EvPay z = pay[val[u]];
+              if (!apply(key[u], z.key, z.aux, z.ktag & 3u)) fin = true;
             }
-          }
-          if (!apply(kk, y)) {  // the table passed 64: out of the window
-            fin = 1;
-            break;
-          }
-          // a removal starting an alternating run of its key (k_small_chains): in a list bin of <= 7 nodes after it
-          // the run's events after it are implied (the compacted events leave them out; else skipped here); in a
-          // tree bin, or a list bin long enough for a put to call treeifyBin, each is applied
-          const uint32_t skip = (kk & 3u) == 2u ? y.ktag >> kSkipShift : 0u;
-          if (skip) {
-            const bool implied = j.list_len(y.aux) <= 7u;
-            if (!orig) {
-              if (implied) q += skip;
-            } else if (!implied) {
-              const uint32_t o0 = bo[wv][q];
-              for (uint32_t u = o0 + 1; u <= o0 + skip && !fin; ++u)
-                if (!apply(key[u], pay[val[u]])) fin = 1;
-              if (fin) break;
-            }
+            if (fin) break;
           }
         }
-        nxt = i + q;
       }
-      i = (uint32_t)__shfl((int)nxt, 0, kWave);
-      fin = (uint32_t)__shfl((int)fin, 0, kWave);
-      if (fin || i >= E) break;
-      wave_lds_sync();  // (lane 0 is done with the staged events)
+      i += q;
     }
-    if (l == 0) {
 #ifdef CC_PHASE_TIMING
+    if (l == 0) {
       const uint64_t dt = wall_clock64() - t_run;
       atomicAdd(&g_ph_small[0], (unsigned long long)n_app);
       atomicMax(&g_ph_small[1], (unsigned long long)n_app);
@@ -283,18 +285,19 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
       atomicAdd(&g_ph_small[3], (unsigned long long)dt);
       atomicMax(&g_ph_small[4], (unsigned long long)dt);
       atomicMax(&g_ph_small[5], (unsigned long long)(i - start));
-#endif
-      if (!(lm.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
-        lm.n = 0;
-        lm.used = 0;
-      }
-      msmall[m] = (uint8_t)((msmall[m] & ~kMfSmall) | ((lm.flags & kSmIn) ? kMfSmall : 0u));
-      atomicMax(&mpcap[m], lm.lvl);
+      atomicAdd(&g_ph_small[6], (unsigned long long)t_stage);
     }
-    wave_lds_sync();
-    uint64_t* back = reinterpret_cast<uint64_t*>(s);
-    for (uint32_t q = l; q < (uint32_t)kSrWords; q += kWave) back[q] = lds[wv][q];
-    wave_lds_sync();  // (the next run's copy overwrites lds[wv])
+#endif
+    if (!(j.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
+      j.n = 0;
+      j.used = 0;
+    }
+    j.store(*s);
+    if (l == 0) {  // (atomic on the flag word: the next sub-batch's kernels may set other flags of the map meanwhile)
+      if (j.flags & kSmIn) mflag_or(msmall, m, kMfSmall);
+      else mflag_and(msmall, m, (uint8_t)~kMfSmall);
+      atomicMax(&mpcap[m], j.lvl);
+    }
   }
 }
 
@@ -493,7 +496,7 @@ int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
+int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStream_t rst) {
   if (E > a.cap) return -2;
   if (E) {
     size_t need = 0;
@@ -528,7 +531,10 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st) {
       hipLaunchKernelGGL(k_small_cseg, dim3(std::min<uint32_t>(1024, (E + 255) / 256)), dim3(256), 0, st, a.ev_key2, orig,
                          a.cseg, a.max_resources);
     }
-    hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, st, a.ev_key2, a.ev_val2, a.ev_pay,
+    if (rst != st) {  // the replay overlaps what the engine stream does next
+      if (hipEventRecord(a.ev_prep, st) != hipSuccess || hipStreamWaitEvent(rst, a.ev_prep, 0) != hipSuccess) return -1;
+    }
+    hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, rst, a.ev_key2, a.ev_val2, a.ev_pay,
                        cmp ? orig : nullptr, cmp ? a.cseg + a.max_resources + 1 : a.ctl, cmp ? a.cseg : a.seg,
                        cmp ? a.cseg + a.max_resources : a.nseg, a.state,
                        a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);

@@ -827,7 +827,13 @@ __global__ __launch_bounds__(kMszScanW * kWave) void k_msize_scan(const uint8_t*
     int64_t total = 0;
     for (int q = 0; q < kMszScanW; ++q) total += csum[q][l];
     msize[m] = (uint32_t)((int64_t)s0 + total);
-    mpcap[m] = lv | inexact | (mp & kMpInexact);
+    // (merged: an overlapped small-map replay may raise the level meanwhile, map_small.hip)
+    for (uint32_t old = mp;;) {
+      const uint32_t nv = max(old & ~kMpInexact, lv) | inexact | (old & kMpInexact);
+      const uint32_t got = atomicCAS(&mpcap[m], old, nv);
+      if (got == old) break;
+      old = got;
+    }
   }
 }
 

@@ -27,94 +27,151 @@
 
 namespace cc {
 
+// The model lives in the registers of one wave, node i and bin i in lane i (a java.util.HashMap window holds at most
+// 64 nodes and 64 bins): every lane runs the same walk, node fields are read with v_readlane (a few cycles) and
+// written by the owning lane's select, the scalars (size, level, flags, the node pool) are uniform registers.  (A
+// copy in LDS cost a dependent LDS round trip of ~100 cycles per field: ~0.5 us per event of a hot small map.)
+// Every method must be called by the whole wave with uniform arguments.
 struct SmallJhm {
-  SmallMap& s;  // the hot part (links, hashes, bins): an LDS copy in k_small_replay
-  SmallMap& g;  // the keys (SmallMap::key / kt): the map's state in HBM
-  __device__ SmallJhm(SmallMap& m, SmallMap& keys) : s(m), g(keys) {}
+  uint32_t w0;     // lane i: node i + 1's next | prev << 8 | parent << 16 | left << 24
+  uint32_t w1;     // lane i: node i + 1's right | flags (bit 0 TreeNode, bit 1 red) << 8 | bin i's head << 16
+  uint32_t wjh;    // lane i: node i + 1's hash
+  uint32_t wkt;    // lane i: node i + 1's key tag
+  uint32_t wklo, wkhi;  // lane i: node i + 1's key
+  uint32_t n, lvl, flags;
+  uint64_t used, tree_bins;
+  uint32_t lane;
 
-  __device__ uint32_t cap() const { return 16u << s.lvl; }
-  __device__ bool tree(uint32_t x) const { return s.nb[x - 1] & 1u; }
-  __device__ bool red(uint32_t x) const { return x && (s.nb[x - 1] & 2u); }
-  __device__ void set_red(uint32_t x, bool r) { s.nb[x - 1] = (uint8_t)((s.nb[x - 1] & ~2u) | (r ? 2u : 0u)); }
+  __device__ __forceinline__ void load(const SmallMap& m) {
+    lane = __lane_id();
+    w0 = m.nx[lane] | (uint32_t)m.pv[lane] << 8 | (uint32_t)m.pa[lane] << 16 | (uint32_t)m.lf[lane] << 24;
+    w1 = m.rt[lane] | (uint32_t)m.nb[lane] << 8 | (uint32_t)m.tab[lane] << 16;
+    wjh = m.jh[lane];
+    wkt = m.kt[lane];
+    wklo = (uint32_t)m.key[lane];
+    wkhi = (uint32_t)(m.key[lane] >> 32);
+    n = m.n;
+    lvl = m.lvl;
+    flags = m.flags;
+    used = m.used;
+    tree_bins = m.tree_bins;
+  }
+  __device__ __forceinline__ void store(SmallMap& m) const {
+    m.nx[lane] = (uint8_t)w0;
+    m.pv[lane] = (uint8_t)(w0 >> 8);
+    m.pa[lane] = (uint8_t)(w0 >> 16);
+    m.lf[lane] = (uint8_t)(w0 >> 24);
+    m.rt[lane] = (uint8_t)w1;
+    m.nb[lane] = (uint8_t)(w1 >> 8);
+    m.tab[lane] = (uint8_t)(w1 >> 16);
+    m.jh[lane] = wjh;
+    m.kt[lane] = (uint8_t)wkt;
+    m.key[lane] = (uint64_t)wkhi << 32 | wklo;
+    if (lane == 0) {
+      m.n = n;
+      m.lvl = lvl;
+      m.flags = flags;
+      m.used = used;
+      m.tree_bins = tree_bins;
+    }
+  }
+  __device__ __forceinline__ static uint32_t rl(uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); }
+  __device__ __forceinline__ void put8(uint32_t& w, uint32_t i, uint32_t sh, uint32_t v) {
+    if (lane == i) w = (w & ~(0xFFu << sh)) | ((v & 0xFFu) << sh);
+  }
+
+  __device__ __forceinline__ uint32_t cap() const { return 16u << lvl; }
+  __device__ __forceinline__ uint32_t nb(uint32_t x) const { return (rl(w1, x - 1) >> 8) & 0xFFu; }
+  __device__ __forceinline__ void set_nb(uint32_t x, uint32_t v) { put8(w1, x - 1, 8, v); }
+  __device__ __forceinline__ uint32_t tab(uint32_t b) const { return (rl(w1, b) >> 16) & 0xFFu; }
+  __device__ __forceinline__ void set_tab(uint32_t b, uint32_t v) { put8(w1, b, 16, v); }
+  __device__ __forceinline__ bool tree(uint32_t x) const { return nb(x) & 1u; }
+  __device__ __forceinline__ bool red(uint32_t x) const { return x && (nb(x) & 2u); }
+  __device__ __forceinline__ void set_red(uint32_t x, bool r) { set_nb(x, (nb(x) & ~2u) | (r ? 2u : 0u)); }
   // links are node + 1 (0: null)
-  __device__ uint32_t next(uint32_t x) const { return s.nx[x - 1]; }
-  __device__ uint32_t prev(uint32_t x) const { return s.pv[x - 1]; }
-  __device__ uint32_t par(uint32_t x) const { return s.pa[x - 1]; }
-  __device__ uint32_t left(uint32_t x) const { return s.lf[x - 1]; }
-  __device__ uint32_t right(uint32_t x) const { return s.rt[x - 1]; }
-  __device__ void set_next(uint32_t x, uint32_t v) { s.nx[x - 1] = (uint8_t)v; }
-  __device__ void set_prev(uint32_t x, uint32_t v) { s.pv[x - 1] = (uint8_t)v; }
-  __device__ void set_par(uint32_t x, uint32_t v) { s.pa[x - 1] = (uint8_t)v; }
-  __device__ void set_left(uint32_t x, uint32_t v) { s.lf[x - 1] = (uint8_t)v; }
-  __device__ void set_right(uint32_t x, uint32_t v) { s.rt[x - 1] = (uint8_t)v; }
-  __device__ uint32_t hash(uint32_t x) const { return s.jh[x - 1]; }
+  __device__ __forceinline__ uint32_t next(uint32_t x) const { return rl(w0, x - 1) & 0xFFu; }
+  __device__ __forceinline__ uint32_t prev(uint32_t x) const { return (rl(w0, x - 1) >> 8) & 0xFFu; }
+  __device__ __forceinline__ uint32_t par(uint32_t x) const { return (rl(w0, x - 1) >> 16) & 0xFFu; }
+  __device__ __forceinline__ uint32_t left(uint32_t x) const { return rl(w0, x - 1) >> 24; }
+  __device__ __forceinline__ uint32_t right(uint32_t x) const { return rl(w1, x - 1) & 0xFFu; }
+  __device__ __forceinline__ void set_next(uint32_t x, uint32_t v) { put8(w0, x - 1, 0, v); }
+  __device__ __forceinline__ void set_prev(uint32_t x, uint32_t v) { put8(w0, x - 1, 8, v); }
+  __device__ __forceinline__ void set_par(uint32_t x, uint32_t v) { put8(w0, x - 1, 16, v); }
+  __device__ __forceinline__ void set_left(uint32_t x, uint32_t v) { put8(w0, x - 1, 24, v); }
+  __device__ __forceinline__ void set_right(uint32_t x, uint32_t v) { put8(w1, x - 1, 0, v); }
+  __device__ __forceinline__ uint32_t hash(uint32_t x) const { return rl(wjh, x - 1); }
+  __device__ __forceinline__ uint32_t ktv(uint32_t x) const { return rl(wkt, x - 1); }
+  __device__ __forceinline__ uint64_t keyv(uint32_t x) const { return (uint64_t)rl(wkhi, x - 1) << 32 | rl(wklo, x - 1); }
   // the bin of hash h is a list bin (or empty) at the current capacity
-  __device__ bool list_bin(uint32_t h) const {
-    const uint32_t hd = s.tab[(cap() - 1) & h];
+  __device__ __forceinline__ bool list_bin(uint32_t h) const {
+    const uint32_t hd = tab((cap() - 1) & h);
     return hd == 0 || !tree(hd);
   }
   // the chain length of a list bin (a tree bin: kSmNodes + 1)
-  __device__ uint32_t list_len(uint32_t h) const {
-    uint32_t q = s.tab[(cap() - 1) & h], n = 0;
+  __device__ __forceinline__ uint32_t list_len(uint32_t h) const {
+    uint32_t q = tab((cap() - 1) & h), c = 0;
     if (q && tree(q)) return kSmNodes + 1;
-    for (; q && n <= kSmNodes; q = next(q)) ++n;
-    return n;
+    for (; q && c <= kSmNodes; q = next(q)) ++c;
+    return c;
   }
   // the live key (kt, key) with hash h is the last node of a list bin of at most `most` nodes: removeNode then putVal
   // of it changes nothing (it is linked back where it was, no treeifyBin, the size and threshold as before)
-  __device__ bool list_tail(uint32_t h, uint32_t kt, uint64_t key, uint32_t most) const {
-    uint32_t q = s.tab[(cap() - 1) & h];
+  __device__ __forceinline__ bool list_tail(uint32_t h, uint32_t kt, uint64_t key, uint32_t most) const {
+    uint32_t q = tab((cap() - 1) & h);
     if (!q || tree(q)) return false;
-    for (uint32_t n = 1; n <= most; ++n, q = next(q)) {
+    for (uint32_t c = 1; c <= most; ++c, q = next(q)) {
       const uint32_t nx = next(q);
-      if (hash(q) == h && g.kt[q - 1] == kt && g.key[q - 1] == key) return nx == 0;
+      if (hash(q) == h && ktv(q) == kt && keyv(q) == key) return nx == 0;
       if (!nx) return false;
     }
     return false;
   }
 
-  __device__ uint32_t alloc(uint32_t h, uint32_t kt, uint64_t key) {
-    const uint64_t free = ~s.used;
+  __device__ __forceinline__ uint32_t alloc(uint32_t h, uint32_t kt, uint64_t key) {
+    const uint64_t free = ~used;
     if (!free) {
-      s.flags |= kSmAmbig;  // (cannot happen: a table of 64 holds at most 49 nodes for a moment)
+      flags |= kSmAmbig;  // (cannot happen: a table of 64 holds at most 49 nodes for a moment)
       return 0;
     }
     const uint32_t i = (uint32_t)__builtin_ctzll(free);
-    s.used |= 1ull << i;
-    s.jh[i] = h;
-    g.key[i] = key;
-    g.kt[i] = (uint8_t)kt;
-    s.nx[i] = s.pv[i] = s.pa[i] = s.lf[i] = s.rt[i] = 0;
-    s.nb[i] = 0;
+    used |= 1ull << i;
+    if (lane == i) {
+      wjh = h;
+      wkt = kt;
+      wklo = (uint32_t)key;
+      wkhi = (uint32_t)(key >> 32);
+      w0 = 0;
+      w1 &= 0xFF0000u;  // (the lane's bin head stays)
+    }
     return i + 1;
   }
-  __device__ void release(uint32_t x) { s.used &= ~(1ull << (x - 1)); }
+  __device__ __forceinline__ void release(uint32_t x) { used &= ~(1ull << (x - 1)); }
 
   // putTreeVal's / treeify's direction for key (kt, key) with hash h at tree node p: the hash as a signed int, then
   // compareComparables (same class), then tieBreakOrder (class names; a new key never equals a live one)
-  __device__ int dir_of(uint32_t h, uint32_t kt, uint64_t key, uint32_t p) {
+  __device__ __forceinline__ int dir_of(uint32_t h, uint32_t kt, uint64_t key, uint32_t p) {
     const int32_t ph = (int32_t)hash(p), hh = (int32_t)h;
     if (ph > hh) return -1;
     if (ph < hh) return 1;
-    const uint32_t pt = g.kt[p - 1];
-    const uint64_t pk = g.key[p - 1];
+    const uint32_t pt = ktv(p);
+    const uint64_t pk = keyv(p);
     if (kt == pt) {
       switch (kt) {
         case 0: return (int64_t)key < (int64_t)pk ? -1 : 1;  // Long.compareTo
         case 1: return (int32_t)key < (int32_t)pk ? -1 : 1;  // Integer.compareTo
         case 2: return key < pk ? -1 : 1;                    // Boolean.compareTo (false < true)
-        default: s.flags |= kSmAmbig; return 1;              // String.compareTo of texts held as handles
+        default: flags |= kSmAmbig; return 1;              // String.compareTo of texts held as handles
       }
     }
     // tieBreakOrder: getClass().getName() -- java.lang.Boolean < Integer < Long < String (tags 2, 1, 0, 3)
-    constexpr uint32_t rank[4] = {2, 1, 0, 3};
-    return rank[kt] < rank[pt] ? -1 : 1;
+    auto rank = [](uint32_t t) { return (0x3012u >> (4 * t)) & 0xFu; };  // {2, 1, 0, 3} (no indexed array: scratch)
+    return rank(kt) < rank(pt) ? -1 : 1;
   }
-  __device__ uint32_t root_of(uint32_t p) const {
+  __device__ __forceinline__ uint32_t root_of(uint32_t p) const {
     while (par(p)) p = par(p);
     return p;
   }
-  __device__ uint32_t rotate_left(uint32_t root, uint32_t p) {
+  __device__ __forceinline__ uint32_t rotate_left(uint32_t root, uint32_t p) {
     uint32_t r, pp, rl;
     if (p && (r = right(p))) {
       rl = left(r);
@@ -130,7 +187,7 @@ struct SmallJhm {
     }
     return root;
   }
-  __device__ uint32_t rotate_right(uint32_t root, uint32_t p) {
+  __device__ __forceinline__ uint32_t rotate_right(uint32_t root, uint32_t p) {
     uint32_t l, pp, lr;
     if (p && (l = left(p))) {
       lr = right(l);
@@ -146,7 +203,7 @@ struct SmallJhm {
     }
     return root;
   }
-  __device__ uint32_t balance_insertion(uint32_t root, uint32_t x) {
+  __device__ __forceinline__ uint32_t balance_insertion(uint32_t root, uint32_t x) {
     set_red(x, true);
     for (uint32_t xp, xpp, xppl, xppr;;) {
       if (!(xp = par(x))) {
@@ -183,7 +240,7 @@ struct SmallJhm {
       }
     }
   }
-  __device__ uint32_t balance_deletion(uint32_t root, uint32_t x) {
+  __device__ __forceinline__ uint32_t balance_deletion(uint32_t root, uint32_t x) {
     for (uint32_t xp, xpl, xpr;;) {
       if (!x || x == root) return root;
       if (!(xp = par(x))) {
@@ -251,12 +308,12 @@ struct SmallJhm {
       }
     }
   }
-  __device__ void to_front(uint32_t root) {  // moveRootToFront
+  __device__ __forceinline__ void to_front(uint32_t root) {  // moveRootToFront
     if (!root) return;
     const uint32_t index = (cap() - 1) & hash(root);
-    const uint32_t first = s.tab[index];
+    const uint32_t first = tab(index);
     if (root == first) return;
-    s.tab[index] = (uint8_t)root;
+    set_tab(index, root);
     const uint32_t rp = prev(root), rn = next(root);
     if (rn) set_prev(rn, rp);
     if (rp) set_next(rp, rn);
@@ -264,7 +321,7 @@ struct SmallJhm {
     set_next(root, first);
     set_prev(root, 0);
   }
-  __device__ void treeify(uint32_t hd) {
+  __device__ __forceinline__ void treeify(uint32_t hd) {
     uint32_t root = 0;
     for (uint32_t x = hd, nxt; x; x = nxt) {
       nxt = next(x);
@@ -274,7 +331,7 @@ struct SmallJhm {
         continue;
       }
       for (uint32_t p = root;;) {
-        const int dir = dir_of(hash(x), g.kt[x - 1], g.key[x - 1], p);
+        const int dir = dir_of(hash(x), ktv(x), keyv(x), p);
         const uint32_t xp = p;
         if (!(p = dir <= 0 ? left(p) : right(p))) {
           set_par(x, xp);
@@ -287,27 +344,27 @@ struct SmallJhm {
     }
     to_front(root);
   }
-  __device__ uint32_t untreeify(uint32_t hd) {
+  __device__ __forceinline__ uint32_t untreeify(uint32_t hd) {
     for (uint32_t q = hd; q; q = next(q)) {
-      s.nb[q - 1] = 0;
+      set_nb(q, 0);
       set_par(q, 0), set_left(q, 0), set_right(q, 0), set_prev(q, 0);
     }
     return hd;
   }
   // resize (the window holds list bins only below 64, where nothing is a tree): chains split in order; a table of
   // 128 leaves the window (returns false)
-  __device__ bool resize() {
+  __device__ __forceinline__ bool resize() {
     const uint32_t old = cap();
-    if (s.lvl + 1 >= 3u) {
-      ++s.lvl;
-      s.flags &= ~kSmIn;
+    if (lvl + 1 >= 3u) {
+      ++lvl;
+      flags &= ~kSmIn;
       return false;
     }
-    ++s.lvl;
+    ++lvl;
     // in place: bins [old, 2 old) are unused at the old capacity, and bin j splits into j and j + old only
     for (uint32_t j = 0; j < old; ++j) {
       uint32_t lo = 0, lot = 0, hi = 0, hit = 0;
-      for (uint32_t q = s.tab[j], nxt; q; q = nxt) {
+      for (uint32_t q = tab(j), nxt; q; q = nxt) {
         nxt = next(q);
         set_next(q, 0);
         if ((hash(q) & old) == 0) {
@@ -318,28 +375,28 @@ struct SmallJhm {
           hit = q;
         }
       }
-      s.tab[j] = (uint8_t)lo;
-      s.tab[j + old] = (uint8_t)hi;
+      set_tab(j, lo);
+      set_tab(j + old, hi);
     }
     return true;
   }
-  __device__ bool treeify_bin(uint32_t h) {
+  __device__ __forceinline__ bool treeify_bin(uint32_t h) {
     if (cap() < 64) return resize();  // MIN_TREEIFY_CAPACITY: resize instead
     const uint32_t index = (cap() - 1) & h;
     uint32_t tl = 0;
-    for (uint32_t q = s.tab[index]; q; q = next(q)) s.nb[q - 1] |= 1u, set_prev(q, tl), tl = q;
-    if (s.tab[index]) treeify(s.tab[index]);
-    s.flags |= kSmTree;
-    s.tree_bins |= 1ull << (index & 63u);
+    for (uint32_t q = tab(index); q; q = next(q)) set_nb(q, nb(q) | 1u), set_prev(q, tl), tl = q;
+    if (tab(index)) treeify(tab(index));
+    flags |= kSmTree;
+    tree_bins |= 1ull << (index & 63u);
     return true;
   }
   // putVal of a new key (an existing key's put changes no structure); false: the map left the window
-  __device__ bool put(uint32_t h, uint32_t kt, uint64_t key) {
+  __device__ __forceinline__ bool put(uint32_t h, uint32_t kt, uint64_t key) {
     const uint32_t i = (cap() - 1) & h;
-    uint32_t p = s.tab[i];
+    uint32_t p = tab(i);
     if (!p) {
       const uint32_t x = alloc(h, kt, key);
-      s.tab[i] = (uint8_t)x;
+      set_tab(i, x);
     } else if (tree(p)) {  // putTreeVal: linked after its tree parent, then the root moves to the front
       const uint32_t root = root_of(p);
       for (uint32_t q = root;;) {
@@ -348,7 +405,7 @@ struct SmallJhm {
         if (!(q = dir <= 0 ? left(q) : right(q))) {
           const uint32_t xpn = next(xp), x = alloc(h, kt, key);
           if (!x) return true;
-          s.nb[x - 1] = 1u;
+          set_nb(x, 1u);
           set_next(x, xpn);
           if (dir <= 0) set_left(xp, x);
           else set_right(xp, x);
@@ -366,19 +423,19 @@ struct SmallJhm {
       set_next(p, x);
       if (bin >= 7u && !treeify_bin(h)) return false;  // the chain now holds >= 9 nodes
     }
-    if (++s.n > (12u << s.lvl)) return resize();  // ++size > threshold
+    if (++n > (12u << lvl)) return resize();  // ++size > threshold
     return true;
   }
-  __device__ void remove_tree_node(uint32_t self, uint32_t index) {  // TreeNode.removeTreeNode(map, tab, movable = true)
-    uint32_t first = s.tab[index], root = first, rl;
+  __device__ __forceinline__ void remove_tree_node(uint32_t self, uint32_t index) {  // TreeNode.removeTreeNode(map, tab, movable = true)
+    uint32_t first = tab(index), root = first, rl;
     const uint32_t succ = next(self), pred = prev(self);
-    if (!pred) s.tab[index] = (uint8_t)(first = succ);
+    if (!pred) set_tab(index, first = succ);
     else set_next(pred, succ);
     if (succ) set_prev(succ, pred);
     if (!first) return;
     if (par(root)) root = root_of(root);
     if (!right(root) || !(rl = left(root)) || !left(rl)) {
-      s.tab[index] = (uint8_t)untreeify(first);  // too small
+      set_tab(index, untreeify(first));  // too small
       return;
     }
     const uint32_t p = self, pl = left(p), pr = right(p);
@@ -436,23 +493,23 @@ struct SmallJhm {
     to_front(r);
   }
   // removeNode(movable = true) of the live key (kt, key) with hash h
-  __device__ void remove(uint32_t h, uint32_t kt, uint64_t key) {
+  __device__ __forceinline__ void remove(uint32_t h, uint32_t kt, uint64_t key) {
     const uint32_t index = (cap() - 1) & h;
     uint32_t node = 0, prv = 0, pp = 0;
-    for (uint32_t q = s.tab[index], steps = 0; q && steps < kSmNodes; pp = q, q = next(q), ++steps)
-      if (hash(q) == h && g.kt[q - 1] == kt && g.key[q - 1] == key) {
+    for (uint32_t q = tab(index), steps = 0; q && steps < kSmNodes; pp = q, q = next(q), ++steps)
+      if (hash(q) == h && ktv(q) == kt && keyv(q) == key) {
         node = q, prv = pp;
         break;
       }
     if (!node) {
-      s.flags |= kSmAmbig;  // (a removal of a key this model does not hold: its order is no longer known)
+      flags |= kSmAmbig;  // (a removal of a key this model does not hold: its order is no longer known)
       return;
     }
     if (tree(node)) remove_tree_node(node, index);
-    else if (!prv) s.tab[index] = (uint8_t)next(node);
+    else if (!prv) set_tab(index, next(node));
     else set_next(prv, next(node));
     release(node);
-    --s.n;
+    --n;
   }
 };
 

@@ -147,7 +147,8 @@ def run_c3(args):
     assert L.cc_debug_phases(E.h, 3, ticks) == 0
     t = list(ticks)
     print(f"k_small_replay over {args.steps} steps: events applied {t[0]}, max per map {t[1]}, runs {t[2]}, "
-          f"lane-0 time {t[3] * 10e-3:.0f} us total, max per map {t[4] * 10e-3:.0f} us, longest run {t[5]} events")
+          f"lane-0 time {t[3] * 10e-3:.0f} us total, max per map {t[4] * 10e-3:.0f} us, longest run {t[5]} events, "
+          f"staging {t[6] * 10e-3:.0f} us total")
     print("counters", E.counters())
 
 
