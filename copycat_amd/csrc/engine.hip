@@ -878,7 +878,8 @@ static const bool g_dbg_sync = getenv("CC_DEBUG_SYNC") != nullptr;
 
 // TTL mode: the map events appended so far (commits, expiries) -> every map's size and capacity, the small maps' key
 // sets (map_small.hip: sort, runs, k_small_replay + k_ttl_replay), then the counters for the next round.
-static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = nullptr, uint64_t lo = 0) {
+static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = nullptr, uint64_t lo = 0,
+                      const cc_results* out = nullptr) {
   uint32_t ctl[2] = {0, 0};
   HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
@@ -902,6 +903,8 @@ static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = null
   sa.lvl_at = e->d_lvl_at;
   sa.index = index;  // (null for the expiry-only flushes: they grow no table)
   sa.lo = lo;
+  sa.out_status = out ? out->status : nullptr;  // (the sub-batch's size / isEmpty rows among the events)
+  sa.out_value = out ? out->value : nullptr;
   {
     int rc = join_replay(e, st);  // (an overlapped replay of an earlier sub-batch: the models it writes)
     if (rc) return rc;
@@ -979,11 +982,13 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   e->clr_heavy.clear();
   if (e->map_bits || e->coord_on) {
     uint32_t nb = 0, ttl_seen = 0;
-    // Outside TTL mode map size / isEmpty rows are answered in the stream (listed in szq, their maps flagged); a batch
-    // that turns TTL mode on (or lists more than szq holds) is scanned again with them as barriers (or a larger list).
+    // Outside TTL mode map size / isEmpty, containsValue and clear rows are answered in the stream (listed, their maps
+    // flagged); in TTL mode size / isEmpty rows are (the event replay answers them), the others are barriers.  A batch
+    // that turns TTL mode on (or lists more than a list holds) is scanned again with TTL mode's lists (or larger ones).
     bool inline_size = e->map_bits && !e->ttl_live;
+    bool inline_ttl = e->map_bits && e->ttl_live;
     for (int pass = 0;; ++pass) {
-      if (inline_size && !e->d_szq) {
+      if ((inline_size || inline_ttl) && !e->d_szq) {
         e->szq_cap = 1u << 20;
         HIPCHECK(hipMalloc(&e->d_szq, sizeof(uint32_t) * e->szq_cap));
         HIPCHECK(hipMalloc(&e->d_szq_n, sizeof(uint32_t)));
@@ -1012,8 +1017,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       }
       HIPCHECK(hipMemsetAsync(e->d_ttl_seen, 0, sizeof(uint32_t), st));
       if (launch_map_barriers(c->inst, c->op, c->aux, n, e->d_inst_res, e->d_res_type, e->cfg.max_instances, e->d_bar,
-                              e->d_bar_n, kBarCap, e->d_ttl_seen, inline_size ? e->d_szq : nullptr,
-                              inline_size ? e->d_szq_n : nullptr, e->szq_cap, e->d_msmall,
+                              e->d_bar_n, kBarCap, e->d_ttl_seen, inline_size || inline_ttl ? e->d_szq : nullptr,
+                              inline_size || inline_ttl ? e->d_szq_n : nullptr, e->szq_cap, e->d_msmall,
                               inline_size ? e->d_cvq : nullptr, inline_size ? e->d_cvq_n : nullptr, e->cvq_cap,
                               inline_size ? e->d_mfirst : nullptr, e->cfg.max_resources,
                               inline_size ? e->d_clrq : nullptr, inline_size ? e->d_clrq_n : nullptr, e->clrq_cap, st))
@@ -1046,14 +1051,15 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
-      if (inline_size) HIPCHECK(hipMemcpyAsync(&qn, e->d_szq_n, sizeof qn, hipMemcpyDeviceToHost, st));
+      if (inline_size || inline_ttl) HIPCHECK(hipMemcpyAsync(&qn, e->d_szq_n, sizeof qn, hipMemcpyDeviceToHost, st));
       if (inline_size) HIPCHECK(hipMemcpyAsync(cvn, e->d_cvq_n, sizeof cvn, hipMemcpyDeviceToHost, st));
       if (inline_size) HIPCHECK(hipMemcpyAsync(&cln, e->d_clrq_n, sizeof cln, hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
-      if (!inline_size) break;
+      if (!inline_size && !inline_ttl) break;
       e->szq_flagged = qn > 0 || cvn[0] > 0 || cln > 0;
-      if (ttl_seen || pass > 1) {  // this batch turns TTL mode on: size / isEmpty / containsValue become barriers again
-        inline_size = false;
+      if (inline_size && (ttl_seen || pass > 2)) {  // this batch turns TTL mode on: containsValue and clear become
+        inline_size = false;                        // barriers again, size / isEmpty stay in the stream
+        inline_ttl = pass <= 2;
         continue;
       }
       if (qn > e->szq_cap) {  // a larger list, then the same scan again
@@ -1085,6 +1091,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         continue;
       }
       e->szq_n = qn;
+      if (inline_ttl) break;  // (TTL mode lists size / isEmpty rows only)
       int rc = cv_rows(e, cvn[1], st);  // the in-stream rows, sorted, on the host too
       if (rc) return rc;
       if ((rc = clr_rows(e, cln, c, st))) return rc;  // the in-stream clears: sorted by (map, row), offsets
@@ -1322,6 +1329,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     const uint32_t tiles = (uint32_t)((hi - lo + kTile - 1) / kTile);
     SizeArgs sz{};       // this sub-batch's size / isEmpty rows (map_small.hip)
     bool sized = false;  // the event pipeline ran (its counters are reset after the answers)
+    bool ttl_pending = false;  // TTL mode: the sub-batch's event replay, after the unpermute
     uint32_t sized_events = 0;
     if (e->map_bits && e->ttl_live) {  // TTL mode: every key goes through its region (timers are walked in order)
       HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
@@ -1584,8 +1592,24 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         za.err = e->d_err;
         if (launch_map_size(za, st)) return set_err(CC_ERR_HIP, "map size launch", hipGetLastError());
         own_lo = hi + 1;
-        int rc = ttl_replay(e, st, c->index, lo);
-        if (rc) return rc;
+        if (e->szq_n) {  // this sub-batch's size / isEmpty rows join the events at their rows' positions
+          sz.szq = e->d_szq;
+          sz.szq_n = e->szq_n;
+          sz.lo = lo;
+          sz.hi = hi;
+          sz.inst = c->inst;
+          sz.op = c->op;
+          sz.index = c->index;
+          sz.inst_res = e->d_inst_res;
+          sz.ev_key = e->d_sm_key;
+          sz.ev_val = e->d_sm_val;
+          sz.ev_pay = e->d_sm_pay;
+          sz.cap = (uint32_t)e->sm_cap;
+          sz.ctl = e->d_sm_ctl;
+          sz.ttl = true;
+          if (launch_size_emit(sz, st)) return set_err(CC_ERR_HIP, "size query launch", hipGetLastError());
+        }
+        ttl_pending = true;  // (the replay answers them: after the unpermute's placeholders)
       } else {  // exact map sizes and HashMap capacities (containsValue's iteration order)
         MapSizeArgs za{};
         za.ttab = e->d_ttab;
@@ -1679,7 +1703,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.lvl_at = e->d_lvl_at;
           sa.idx0 = c->index + lo;
           hipStream_t rst = st;  // the replay overlaps the next sub-batch on the side stream (engine_state.h SmSet)
-          if (ctl[0] && !getenv("CC_NO_SIDE_REPLAY")) {
+          static const bool no_side = diag_env("CC_NO_SIDE_REPLAY");  // diagnostics: the replay on the engine stream
+          if (ctl[0] && !no_side) {
             int rc = ensure_sm_alt(e);
             if (rc) return rc;
             rst = e->side_st;
@@ -1750,6 +1775,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       const int rc = launch_cv_answer(cva, E, st);
       if (rc) return rc == -2 ? set_err(CC_ERR_CAPACITY, "containsValue events exceed their buffer")
                               : set_err(CC_ERR_HIP, "containsValue answer launch", hipGetLastError());
+    }
+    if (ttl_pending) {  // TTL mode: sizes, capacities, small maps' key sets, and the size / isEmpty rows' answers
+      int rc = ttl_replay(e, st, c->index, lo, out);
+      if (rc) return rc;
     }
     if (sized) {  // size / isEmpty answers over the unpermute's placeholders; then the next sub-batch's counters
       if (e->szq_n && sized_events && launch_size_answer(sz, st))

@@ -197,6 +197,8 @@ struct SmallArgs {
   // run count, then the event count (null: every event is replayed, TTL mode)
   uint32_t* cseg;
   hipEvent_t ev_prep;          // (a replay on another stream: recorded after the sort and compaction)
+  uint8_t* out_status;         // TTL mode: the size / isEmpty rows among the events are answered here (else null)
+  uint64_t* out_value;
   SmallMap* state;             // [max_resources]
   uint8_t* msmall;
   uint32_t* mpcap;
@@ -237,6 +239,7 @@ struct SizeArgs {
   const uint32_t* msize;        // [max_resources] live sizes at the sub-batch end (exact tracking)
   uint8_t* out_status;          // the batch's result columns (absolute rows)
   uint64_t* out_value;
+  bool ttl;                     // TTL mode: queries positioned by row (common.h TtlEmit), answered by k_ttl_replay
 };
 int launch_size_emit(const SizeArgs& a, hipStream_t st);
 int launch_size_answer(const SizeArgs& a, hipStream_t st);

@@ -93,7 +93,7 @@ __device__ inline uint32_t map_orphan(uint32_t op, uint32_t meta, uint32_t flags
                                       uint32_t& err) {
   rv = 0;
   if (!op_registered(CC_RES_MAP, op)) return CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
-  // size / isEmpty outside TTL mode are answered in the stream after the sub-batch (map_small.hip k_size_answer),
+  // size / isEmpty are answered in the stream after the sub-batch (map_small.hip k_size_answer; k_ttl_replay in TTL mode),
   // containsValue rows that reach a region (the batch answers them in the stream) by map_cv.hip k_cv_answer; a clear
   // that reaches a region is applied in the stream (map_clear.hip: MapState.clear returns nothing)
   if (op == CC_OP_MAP_SIZE || op == CC_OP_MAP_ISEMPTY || op == CC_OP_MAP_CONTAINSVALUE || op == CC_OP_MAP_CLEAR)

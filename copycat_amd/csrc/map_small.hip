@@ -322,12 +322,14 @@ __global__ void k_ttl_scan(TtlEmit t, const uint64_t* __restrict__ clock_base, c
 }
 
 // One wave per map run of the sorted events: the size at the run's start (msize), the running size over its commits
-// and expiries in log order, its peak -> the capacity level (HashMap.resize never shrinks), the size at the end.
-__global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ ctl,
+// and expiries in log order, its peak -> the capacity level (HashMap.resize never shrinks), the size at the end; a
+// size / isEmpty row among them (MapState.size :233-239, isEmpty :244-250) gets the size before it.
+__global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                    const EvPay* __restrict__ pay, const uint32_t* __restrict__ ctl,
                                                     const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
                                                     uint32_t* __restrict__ msize, uint32_t* __restrict__ mpcap,
                                                     unsigned long long* __restrict__ lvl_at, const uint64_t* __restrict__ index,
-                                                    uint64_t lo) {
+                                                    uint64_t lo, uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value) {
   const uint32_t E = ctl[0], ns = *nseg, l = __lane_id();
   const uint32_t waves = gridDim.x * (blockDim.x / kWave);
   for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
@@ -344,6 +346,17 @@ __global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__
       for (int d = 1; d < 64; d <<= 1) {
         const int32_t y = __shfl_up(inc, d, 64);
         if (l >= (uint32_t)d) inc += y;
+      }
+      if (in && (k & 8u) && out_status) {  // a query: the size before it (its own delta is 0)
+        const int64_t at = size + inc;
+        const uint32_t row = pay[val[i]].aux;
+        if (k & 4u) {  // isEmpty
+          out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_BOOL);
+          out_value[row] = at == 0 ? 1ull : 0ull;
+        } else {  // size: an int
+          out_status[row] = CC_STATUS(CC_ST_OK, CC_TAG_INT);
+          out_value[row] = (uint64_t)at;
+        }
       }
       int32_t mx = inc;
 #pragma unroll
@@ -398,17 +411,19 @@ __global__ void k_small_clear(SmallMap* __restrict__ st, uint32_t m) {
 // the sub-batch, plus those before the row.  The map's insertions / removals are the events k_msize_count emits for
 // flagged maps; the queries join them in the same buffer (key bit 3, after the commit whose index they carry: a
 // query takes the index of the command before it), so the radix sort puts each map's events and queries in log order.
+// In TTL mode a query sits at its row's position 2 (row - lo) + 1 (common.h TtlEmit): after the timers that fire at
+// its boundary, before the commits after it; k_ttl_replay answers it with the running size.
 __global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, uint64_t lo, uint64_t hi,
                             const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                             const uint64_t* __restrict__ index, const uint32_t* __restrict__ inst_res,
                             uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val, EvPay* __restrict__ ev_pay,
-                            uint32_t cap, uint32_t* __restrict__ ctl) {
-  const uint64_t idx0 = index[lo];
+                            uint32_t cap, uint32_t* __restrict__ ctl, bool ttl) {
+  const uint64_t idx0 = ttl ? 0 : index[lo];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < szq_n; q += gridDim.x * blockDim.x) {
     const uint32_t row = szq[q];
     if (row < lo || row >= hi) continue;
     const uint32_t m = inst_res[inst[row]];  // (listed by the barrier scan on a live map: the registry is fixed in a batch)
-    const uint64_t d = (index[row] - idx0) & ((1ull << 40) - 1);
+    const uint64_t d = (ttl ? 2 * (row - lo) + 1 : index[row] - idx0) & ((1ull << 40) - 1);
     const uint32_t at = atomicAdd(ctl, 1u);
     if (at < cap) {
       ev_key[at] = ((uint64_t)m << 44) | (d << 4) | 8u | (op[row] == CC_OP_MAP_ISEMPTY ? 4u : 0u);
@@ -481,7 +496,7 @@ __global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
 int launch_size_emit(const SizeArgs& a, hipStream_t st) {
   if (a.szq_n == 0) return 0;
   hipLaunchKernelGGL(k_size_emit, dim3(std::min<uint32_t>(1024, (a.szq_n + 255) / 256)), dim3(256), 0, st, a.szq, a.szq_n,
-                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.ev_pay, a.cap, a.ctl);
+                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.ev_pay, a.cap, a.ctl, a.ttl);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -539,8 +554,8 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
                        cmp ? a.cseg + a.max_resources : a.nseg, a.state,
                        a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
-      hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ctl, a.seg, a.nseg, a.msize, a.mpcap,
-                         a.lvl_at, a.index, a.lo);
+      hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg,
+                         a.msize, a.mpcap, a.lvl_at, a.index, a.lo, a.out_status, a.out_value);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -75,8 +75,9 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
   else return;
   if ((ty == CC_RES_GROUP || ty == CC_RES_MULTIMAP) && !wide) return;
   if (szq && ty == CC_RES_MAP && (o == CC_OP_MAP_SIZE || o == CC_OP_MAP_ISEMPTY)) {
-    // MapState.size / isEmpty (:233-250) outside TTL mode: an ordinary row, answered from the exact size tracking
-    // (k_size_answer); its map's insertions and removals of the batch are followed (mflag bit 1)
+    // MapState.size / isEmpty (:233-250): an ordinary row, answered from the exact size tracking (k_size_answer; in
+    // TTL mode from the event replay, k_ttl_replay); its map's insertions and removals of the batch are followed
+    // (mflag bit 1)
     const uint32_t k = atomicAdd(szq_n, 1u);
     if (k < szq_cap) szq[k] = (uint32_t)i;
     if (!(mflag[r] & kMfSize)) mflag_or(mflag, r, kMfSize);

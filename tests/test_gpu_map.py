@@ -766,3 +766,33 @@ def test_small_map_alternating_chains_tree_bin(seed, nbin):
     cv = np.nonzero(op == abi.CC_OP_MAP_CONTAINSVALUE)[0]
     npe = int((gs[cv] == abi.cc_status(abi.CC_ST_NULL_POINTER, abi.CC_TAG_NULL)).sum())
     assert 0 < npe < len(cv)  # both outcomes occur
+
+
+@pytest.mark.parametrize("flags", [abi.CC_CFG_TIMERS_DEFERRED, 0], ids=["manager", "module"])
+@pytest.mark.parametrize("n,maps,keys,sub_batch,rate,seed", [
+    (20_000, 3, 24, 0, 0.01, 701),               # sizes around the thresholds, timers firing between the rows
+    (200_000, 40, 64, 16384 * 2, 0.003, 702),    # several sub-batches (boundaries owned by the next sub-batch)
+])
+def test_map_ttl_size_rows_in_stream(flags, n, maps, keys, sub_batch, rate, seed):
+    """TTL mode: MapState.size / isEmpty rows are answered in the stream (k_ttl_replay: each query sits at its row's
+    position among the commits and the expiries that fire at the boundaries before it), not as barriers; every answer,
+    every map's entries and the applied index match the oracle, in both timer orders (A8)."""
+    from copycat_amd.workload import map_random_stream
+
+    max_inst = maps + 8
+    b = map_random_stream(n, maps, max_inst, keys=keys, seed=seed)
+    _with_ttl(b, seed, p_ttl=0.3, max_ttl=150, step=4)
+    rows = _with_barriers(b, rate, seed, ops=np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_ISEMPTY], np.uint8))
+    E, O = _engines(maps, max_inst, n, 65536, sub_batch=sub_batch, flags=flags)
+    cut = n // 3
+    gs0, gv0, os0, ov0 = _apply_both(E, O, [b.slice(0, cut)])  # (this batch turns TTL mode on)
+    _assert_rows(gs0, gv0, os0, ov0)
+    c0 = E.counters()
+    gs, gv, os_, ov = _apply_both(E, O, [b.slice(cut, n)])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    assert E.counters()[0] == c0[0]  # no barrier row in the TTL-mode batch
+    later = rows[rows >= cut] - cut
+    assert len(later) > 0
+    sizes = gv[later][b.op[later + cut] == abi.CC_OP_MAP_SIZE]
+    assert len(np.unique(sizes)) > 2  # the sizes move
