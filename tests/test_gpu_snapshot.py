@@ -146,3 +146,46 @@ def test_snapshot_corrupt_counts_rejected_before_any_state_changes():
     O.apply(b)
     for x, y in zip(F.value_state(), O.value_state()):
         assert np.array_equal(x, y)
+
+
+def test_snapshot_after_overlapped_small_map_replay():
+    """Outside TTL mode the small maps' HashMap replay of a sub-batch runs on a side stream while the next sub-batch
+    runs (map_small.hip); a snapshot taken right after the batch, barrier rows in the batch (order-dependent
+    containsValue on maps holding nulls), in-stream containsValue / clear / size rows and hot keys: the restored engine
+    continues bit-exact against the oracle that never stopped, order-dependent answers included."""
+    from copycat_amd.engine import Engine
+    from copycat_amd.workload import map_random_stream
+    from oracle.oracle_py import Oracle
+    from tests.handles import register_key_strings
+    from tests.test_gpu_map import _cv_rows, _with_barriers
+
+    M, n = 12, 160_000
+    slots, max_inst = M, M + 8
+    b = map_random_stream(n, M, max_inst, keys=20, seed=111, hot=2, p_hot=0.4)  # small tables (<= 20 keys)
+    _cv_rows(b, 0.004, 111, clear_rate=0.0005)
+    _with_barriers(b, 0.0015, 112, ops=np.array([abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_SIZE], np.uint8), p=[0.7, 0.3])
+
+    def engine():
+        E = Engine(slots, max_inst, n, map_capacity=16384, sub_batch=16384)
+        return E
+
+    E = engine()
+    E.resource_create_range(0, M, abi.CC_RES_MAP)
+    E.instance_open_range(0, M, 0, 1000, 7)
+    O = Oracle(slots, max_inst)
+    for r in range(M):
+        O.resource_create(r, abi.CC_RES_MAP)
+        O.instance_open(r, r, 1000 + r, 7)
+    register_key_strings(E, O)
+    cut = n // 2
+    _rows_equal(E.apply_host(b.slice(0, cut)), O.apply(b.slice(0, cut)))
+    assert E.counters()[3] > 0  # the small maps' events were replayed
+    snap = E.snapshot()
+    del E
+    E2 = engine()
+    E2.restore(snap)
+    _rows_equal(E2.apply_host(b.slice(cut, n)), O.apply(b.slice(cut, n)))
+    for m in range(M):
+        for x, y in zip(E2.map_entries(m), O.map_entries(m)):
+            assert np.array_equal(x, y)
+    assert E2.applied_index() == O.applied_index()
