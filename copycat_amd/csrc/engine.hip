@@ -1330,6 +1330,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     SizeArgs sz{};       // this sub-batch's size / isEmpty rows (map_small.hip)
     bool sized = false;  // the event pipeline ran (its counters are reset after the answers)
     bool ttl_pending = false;  // TTL mode: the sub-batch's event replay, after the unpermute
+    uint32_t cv_E = 0;         // in-stream containsValue events (final once the map apply kernels ran)
+    bool cv_known = false;     // (read with the map events' count: one host round trip per sub-batch, not two)
     uint32_t sized_events = 0;
     if (e->map_bits && e->ttl_live) {  // TTL mode: every key goes through its region (timers are walked in order)
       HIPCHECK(hipMemsetAsync(e->d_hot_n, 0, sizeof(uint32_t), st));
@@ -1681,7 +1683,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         if (e->small_live || e->szq_n || clr_on) {
           uint32_t ctl[2] = {0, 0};
           HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
+          if (cv_n) HIPCHECK(hipMemcpyAsync(&cv_E, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
           HIPCHECK(hipStreamSynchronize(st));
+          cv_known = cv_n != 0;
           e->stat_events += ctl[0];
           SmallArgs sa{};
           sa.ev_key = e->d_sm_key;
@@ -1769,10 +1773,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     ua.mark = marker_of(e);
     if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
     if (cv_n) {  // in-stream containsValue answers over the unpermute's placeholders (map_cv.hip)
-      uint32_t E = 0;
-      HIPCHECK(hipMemcpyAsync(&E, e->d_cvev_ctl, sizeof E, hipMemcpyDeviceToHost, st));
-      HIPCHECK(hipStreamSynchronize(st));
-      const int rc = launch_cv_answer(cva, E, st);
+      if (!cv_known) {
+        HIPCHECK(hipMemcpyAsync(&cv_E, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+      }
+      const int rc = launch_cv_answer(cva, cv_E, st);
       if (rc) return rc == -2 ? set_err(CC_ERR_CAPACITY, "containsValue events exceed their buffer")
                               : set_err(CC_ERR_HIP, "containsValue answer launch", hipGetLastError());
     }

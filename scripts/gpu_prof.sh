@@ -37,6 +37,38 @@ for n, v in sorted(ev.items(), key=lambda kv: -sum(d for _, d in kv[1])):
     tail = [d for _, d in v[len(v) - k:]]
     print(f"{n[:44]:44s} {k:6d} {sum(tail) / k / 1e3:10.1f} {sum(tail) / steps / 1e6:10.3f}")
 PY
+# idle gaps of the timed steps: the union of all kernels' intervals after the warm-up share of launches, and the
+# largest gaps with the kernels on either side (host round trips show up here)
+python3 - "$TRACE" "$@" > $R/$OUT/kt_gaps.txt <<'PY'
+import csv, sys
+trace, args = sys.argv[1], sys.argv[2:]
+def arg(name, dflt):
+    return int(args[args.index(name) + 1]) if name in args else dflt
+steps, warm = arg("--steps", 1), arg("--warmup", 1)
+ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].replace("void ", "").replace("cc::", "")[:40])
+            for r in csv.DictReader(open(trace)))
+if not ev:
+    sys.exit()
+k0 = [i for i, e in enumerate(ev) if e[2].startswith("k_part")]
+start = ev[k0[len(k0) * warm // (warm + steps)]][0] if k0 else ev[0][0]
+ev = [e for e in ev if e[0] >= start]
+busy, gaps = 0, []
+cs, ce, last = ev[0][0], ev[0][1], ev[0][2]
+for s, e, n in ev[1:]:
+    if s > ce:  # an idle gap before this kernel
+        busy += ce - cs
+        gaps.append((s - ce, last, n))
+        cs, ce, last = s, e, n
+    elif e > ce:
+        ce, last = e, n
+busy += ce - cs
+cur_end = ce
+span = cur_end - ev[0][0]
+print(f"timed window {span / 1e6:.3f} ms, kernels busy (union) {busy / 1e6:.3f} ms, idle {(span - busy) / 1e6:.3f} ms "
+      f"in {len(gaps)} gaps ({sum(g[0] for g in gaps if g[0] > 10000) / 1e6:.3f} ms in gaps > 10 us)")
+for g in sorted(gaps, reverse=True)[:25]:
+    print(f"  {g[0] / 1e3:9.1f} us  after {g[1]:40s} before {g[2]}")
+PY
 find $R/$OUT/kt -name "*kernel_trace.csv" -delete
 i=0
 [ -n "$KT_ONLY" ] && PMCS="" || PMCS=1
