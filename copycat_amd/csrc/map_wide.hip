@@ -48,15 +48,17 @@ __device__ inline bool ttl_op(uint32_t op) {
          op == CC_OP_SET_ADD;
 }
 
+// The row lists k_map_barriers fills: barrier rows, then (null: not listed) in-stream size / isEmpty, containsValue
+// candidates and clears.
+enum { kLsBar = 0, kLsSz, kLsCv, kLsClr, kLists };
 // One candidate row (its op is whole-map / set / multimap / schedule, or may arm a TTL timer): resolve its resource.
+// push(list, row) appends the row to a list.
+template <class Push>
 __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* __restrict__ inst,
                                        const uint64_t* __restrict__ aux, const uint32_t* __restrict__ inst_res,
-                                       const uint8_t* __restrict__ res_type, uint32_t max_inst, uint32_t* __restrict__ bar,
-                                       uint32_t* __restrict__ bar_n, uint32_t cap, uint32_t* __restrict__ ttl_seen,
-                                       uint32_t* __restrict__ szq, uint32_t* __restrict__ szq_n, uint32_t szq_cap,
-                                       uint8_t* __restrict__ mflag, uint32_t* __restrict__ cvq,
-                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap, uint32_t* __restrict__ mfirst,
-                                       uint32_t* __restrict__ clrq, uint32_t* __restrict__ clrq_n, uint32_t clrq_cap) {
+                                       const uint8_t* __restrict__ res_type, uint32_t max_inst,
+                                       uint32_t* __restrict__ ttl_seen, bool szq, uint8_t* __restrict__ mflag, bool cvq,
+                                       uint32_t* __restrict__ mfirst, bool clrq, Push push) {
   bool wide = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE;
   const bool ttl = aux && ttl_op(o);
   if (!wide && !ttl) return;
@@ -78,23 +80,20 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
     // MapState.size / isEmpty (:233-250): an ordinary row, answered from the exact size tracking (k_size_answer; in
     // TTL mode from the event replay, k_ttl_replay); its map's insertions and removals of the batch are followed
     // (mflag bit 1)
-    const uint32_t k = atomicAdd(szq_n, 1u);
-    if (k < szq_cap) szq[k] = (uint32_t)i;
+    push(kLsSz, (uint32_t)i);
     if (!(mflag[r] & kMfSize)) mflag_or(mflag, r, kMfSize);
     return;
   }
   if (cvq && ty == CC_RES_MAP && o == CC_OP_MAP_CONTAINSVALUE) {
     // MapState.containsValue (:49-60) outside TTL mode: a candidate for an answer in the stream (map_cv.hip
     // k_cv_classify decides: a map that may hold a null at the row keeps it a barrier)
-    const uint32_t k = atomicAdd(cvq_n, 1u);
-    if (k < cvq_cap) cvq[k] = (uint32_t)i;
+    push(kLsCv, (uint32_t)i);
     if (!(mflag[r] & kMfCv)) mflag_or(mflag, r, kMfCv);
     return;
   }
   if (clrq && ty == CC_RES_MAP && o == CC_OP_MAP_CLEAR) {
     // MapState.clear (:255-274) outside TTL mode: applied in the stream as an epoch (map_clear.hip)
-    const uint32_t k = atomicAdd(clrq_n, 1u);
-    if (k < clrq_cap) clrq[k] = (uint32_t)i;  // (k_clr_sub flags the map in the sub-batches that clear it)
+    push(kLsClr, (uint32_t)i);  // (k_clr_sub flags the map in the sub-batches that clear it)
     return;
   }
   if (mfirst && ty == CC_RES_MAP && o == CC_OP_DELETE) atomicMin(&mfirst[r], (uint32_t)i);  // (k_cv_classify)
@@ -104,14 +103,16 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
     *ttl_seen = 1u;
     return;
   }
-  const uint32_t k = atomicAdd(bar_n, 1u);
-  if (k < cap) bar[k] = (uint32_t)i;
+  push(kLsBar, (uint32_t)i);
 }
 
 // Rows whose instance is open on a live map and whose op reads or resets the whole map; and whether any map row
 // arms a TTL timer (the engine then switches to TTL mode for good).  Each thread scans 16 rows of the op column with one 16-byte load (a row per thread spent the
 // launch on issuing 64-byte loads: 2.2 ms per 1e9 rows); candidate rows (rare) are resolved one by one.
 constexpr int kMwRows = 16;
+// The lists are staged per workgroup in LDS and reserved with one global atomic per list and workgroup (an atomic
+// per listed row on one counter was ~11 ms per 1B-row batch with 0.1 % in-stream containsValue rows).
+constexpr uint32_t kMwStage = 256;  // staged rows per list and workgroup (more: appended one by one)
 __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                                                       const uint64_t* __restrict__ aux, uint64_t n,
                                                       const uint32_t* __restrict__ inst_res,
@@ -123,34 +124,63 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
                                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap,
                                                       uint32_t* __restrict__ mfirst, uint32_t* __restrict__ clrq,
                                                       uint32_t* __restrict__ clrq_n, uint32_t clrq_cap) {
+  __shared__ uint32_t lrow[kLists][kMwStage];
+  __shared__ uint32_t lcnt[kLists], lbase[kLists];
+  uint32_t* const gl[kLists] = {bar, szq, cvq, clrq};
+  uint32_t* const gn[kLists] = {bar_n, szq_n, cvq_n, clrq_n};
+  const uint32_t gcap[kLists] = {cap, szq_cap, cvq_cap, clrq_cap};
+  if (threadIdx.x < kLists) lcnt[threadIdx.x] = 0;
+  __syncthreads();
+  auto push = [&](int ls, uint32_t row) {
+    const uint32_t k = atomicAdd(&lcnt[ls], 1u);
+    if (k < kMwStage) {
+      lrow[ls][k] = row;
+    } else {  // (the workgroup's stage is full: this row goes straight to the list)
+      const uint32_t g = atomicAdd(gn[ls], 1u);
+      if (g < gcap[ls]) gl[ls][g] = row;
+    }
+  };
   const uint64_t g = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
   const uint64_t i0 = g * kMwRows;
-  if (i0 >= n) return;
-  uint32_t wv[kMwRows / 4];
-  if (i0 + kMwRows <= n && (reinterpret_cast<uintptr_t>(op) & 15) == 0) {
-    const uint4 v = reinterpret_cast<const uint4*>(op)[g];
-    wv[0] = v.x;
-    wv[1] = v.y;
-    wv[2] = v.z;
-    wv[3] = v.w;
-  } else {
+  if (i0 < n) {
+    uint32_t wv[kMwRows / 4];
+    if (i0 + kMwRows <= n && (reinterpret_cast<uintptr_t>(op) & 15) == 0) {
+      const uint4 v = reinterpret_cast<const uint4*>(op)[g];
+      wv[0] = v.x;
+      wv[1] = v.y;
+      wv[2] = v.z;
+      wv[3] = v.w;
+    } else {
 #pragma unroll
-    for (int q = 0; q < kMwRows / 4; ++q) {
-      wv[q] = 0;
-      for (int b = 0; b < 4; ++b) {
-        const uint64_t i = i0 + 4 * q + b;
-        if (i < n) wv[q] |= (uint32_t)op[i] << (8 * b);
+      for (int q = 0; q < kMwRows / 4; ++q) {
+        wv[q] = 0;
+        for (int b = 0; b < 4; ++b) {
+          const uint64_t i = i0 + 4 * q + b;
+          if (i < n) wv[q] |= (uint32_t)op[i] << (8 * b);
+        }
       }
     }
-  }
 #pragma unroll
-  for (int q = 0; q < kMwRows; ++q) {
-    const uint64_t i = i0 + q;
-    const uint32_t o = (wv[q / 4] >> (8 * (q % 4))) & 0xFFu;
-    const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
-    if (cand && i < n)
-      map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag,
-                      cvq, cvq_n, cvq_cap, mfirst, clrq, clrq_n, clrq_cap);
+    for (int q = 0; q < kMwRows; ++q) {
+      const uint64_t i = i0 + q;
+      const uint32_t o = (wv[q / 4] >> (8 * (q % 4))) & 0xFFu;
+      const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
+      if (cand && i < n)
+        map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, ttl_seen, szq != nullptr, mflag, cvq != nullptr,
+                        mfirst, clrq != nullptr, push);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kLists) {
+    const uint32_t c = lcnt[threadIdx.x] < kMwStage ? lcnt[threadIdx.x] : kMwStage;
+    lbase[threadIdx.x] = c ? atomicAdd(gn[threadIdx.x], c) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int ls = 0; ls < kLists; ++ls) {
+    const uint32_t c = lcnt[ls] < kMwStage ? lcnt[ls] : kMwStage;
+    for (uint32_t q = threadIdx.x; q < c; q += kMwT)
+      if (lbase[ls] + q < gcap[ls]) gl[ls][lbase[ls] + q] = lrow[ls][q];
   }
 }
 
