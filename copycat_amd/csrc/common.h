@@ -601,6 +601,8 @@ struct CvCtx {
   const uint8_t* mflag;
   const CvEnt* set;
   uint32_t mask;
+  const uint32_t* bloom;  // a bit per operand key (cv_bloom_bit): a commit's value that is no operand skips the set
+  uint32_t bbits;         // log2 of the filter's bits
   uint64_t* ev_key;
   uint32_t* ev_val;
   uint32_t cap;
@@ -617,6 +619,18 @@ __device__ inline void cv_event(const CvCtx& cv, uint32_t q, uint64_t d, uint32_
     err |= kErrCapacity;
   }
 }
+__host__ __device__ inline uint32_t cv_bloom_bit(uint64_t k64, uint32_t bbits) {
+  return (uint32_t)((k64 * 0xD6E8FEB86659FD93ull) >> (64 - bbits));
+}
+// cv_find behind the filter (one L2-resident bit instead of a probe of the 24-byte-entry set: nearly every stored
+// value is no operand)
+__device__ inline uint32_t cv_lookup(const CvCtx& cv, uint32_t m, uint32_t tag, uint64_t v) {
+  bool exact;
+  const uint64_t k = cv_key(m, tag, v, exact);
+  const uint32_t b = cv_bloom_bit(k, cv.bbits);
+  if (!((cv.bloom[b >> 5] >> (b & 31)) & 1u)) return ~0u;
+  return cv_find(cv.set, cv.mask, m, tag, v);
+}
 // One commit's change of an entry (word / value before and after) in a map answered in the stream: the operand
 // count events of the values that left and entered it.  idx(): the commit's log index (read only on an event).
 template <class IdxF>
@@ -628,8 +642,8 @@ __device__ inline void cv_change(const CvCtx& cv, uint32_t w0, uint64_t v0, uint
   const bool p0 = (w0 & kMwPresent) != 0, p1 = (w1 & kMwPresent) != 0;
   const uint32_t t0 = mw_vtag(w0), t1 = mw_vtag(w1);
   if (p0 == p1 && (!p0 || (t0 == t1 && v0 == v1))) return;
-  const uint32_t q0 = p0 ? cv_find(cv.set, cv.mask, m, t0, t0 ? v0 : 0) : ~0u;
-  const uint32_t q1 = p1 ? cv_find(cv.set, cv.mask, m, t1, t1 ? v1 : 0) : ~0u;
+  const uint32_t q0 = p0 ? cv_lookup(cv, m, t0, t0 ? v0 : 0) : ~0u;
+  const uint32_t q1 = p1 ? cv_lookup(cv, m, t1, t1 ? v1 : 0) : ~0u;
   if (q0 == ~0u && q1 == ~0u) return;
   const uint64_t d = idx() - *cv.idx0p;
   if (q0 != ~0u) cv_event(cv, q0, d, 0u, ep, err);  // (value: the commit's clear epoch, map_clear.hip)

@@ -103,7 +103,7 @@ static void free_all(cc_engine* e) {
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
                   e->d_cvset,    e->d_cvcnt,    e->d_cvev_key, e->d_cvev_key2, e->d_cvev_val, e->d_cvev_val2, e->d_cvev_ctl,
                   e->d_cvseg,    e->d_cvtemp,   e->d_clrq,    e->d_clrq_n,   e->d_clr_keys,   e->d_clr_keys2, e->d_clr_off,
-                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep, e->d_clr_scan, e->d_clr_stemp, e->d_clr_btab, e->d_sm_cseg};
+                  e->d_clr_base, e->d_clr_eend, e->d_clr_temp, e->d_tbl_ep, e->d_clr_scan, e->d_clr_stemp, e->d_clr_btab, e->d_sm_cseg, e->d_cvbloom};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void*& p : e->hw_buf)
@@ -287,6 +287,7 @@ static int clr_rows(cc_engine* e, uint32_t n, const cc_batch* c, hipStream_t st)
 }
 
 // the operand set (sized for kCvMaxRows operands) and the event buffers (two events per commit, one per query)
+constexpr uint32_t kCvBloomMaxBits = 25;  // the operand filter: ~16 bits per operand, 2^16 .. 2^25 bits
 static int ensure_cv(cc_engine* e) {
   if (e->d_cvset) return CC_OK;
   const uint32_t sc = 2 * kCvMaxRows;
@@ -302,6 +303,7 @@ static int ensure_cv(cc_engine* e) {
   if (x == hipSuccess) x = hipMalloc(&e->d_cvev_val2, 4 * ec);
   if (x == hipSuccess) x = hipMalloc(&e->d_cvev_ctl, sizeof(uint32_t) * 2);
   if (x == hipSuccess) x = hipMalloc(&e->d_cvtemp, tb);
+  if (x == hipSuccess) x = hipMalloc(&e->d_cvbloom, (1ull << kCvBloomMaxBits) / 8);
   if (x != hipSuccess) return set_err(CC_ERR_HIP, "hipMalloc containsValue buffers", x);
   e->cvset_cap = sc;
   e->cvev_cap = (uint32_t)ec;
@@ -1477,6 +1479,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       cva.cv.mflag = e->d_msmall;
       cva.cv.set = e->d_cvset;
       cva.cv.mask = sc - 1;
+      cva.cv.bloom = e->d_cvbloom;
+      cva.cv.bbits = 16;
+      while (cva.cv.bbits < kCvBloomMaxBits && (1ull << cva.cv.bbits) < 16ull * cv_n) ++cva.cv.bbits;
       cva.cv.ev_key = e->d_cvev_key;
       cva.cv.ev_val = e->d_cvev_val;
       cva.cv.cap = e->cvev_cap;

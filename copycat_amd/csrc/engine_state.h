@@ -186,6 +186,7 @@ struct cc_engine {
   uint64_t *d_sm_key = nullptr, *d_sm_key2 = nullptr;  // [sm_cap] map events (small / size-queried maps; TTL mode: all)
   uint32_t *d_sm_val = nullptr, *d_sm_val2 = nullptr;
   uint32_t* d_sm_seg = nullptr;    // [max_resources + 1] run starts + count
+  uint32_t* d_cvbloom = nullptr;  // the in-stream containsValue operands' filter (common.h CvCtx)
   uint32_t* d_sm_cseg = nullptr;  // the replayed events without implied chain events: runs, counts (map_small.hip)
   // Outside TTL mode the small-map replay of sub-batch i runs on a side stream while sub-batch i + 1 runs on the
   // engine's: the event buffers alternate between two sets (swapped at each sub-batch start), a set is reused only

@@ -123,6 +123,8 @@ __global__ void k_cv_query(CvSubArgs a) {
     cv_operand(row, a.inst, a.flags, a.a, a.inst_res, m, tag, v);
     bool exact;
     const uint64_t k = cv_key(m, tag, v, exact);
+    const uint32_t b = cv_bloom_bit(k, a.cv.bbits);
+    atomicOr(const_cast<uint32_t*>(a.cv.bloom) + (b >> 5), 1u << (b & 31));
     uint32_t p = cv_slot0(k, a.cv.mask);
     for (;;) {
       unsigned long long c = a.set[p].k64;
@@ -167,7 +169,7 @@ __global__ void k_cv_count0(CvSubArgs a) {
     const uint32_t m = w & kMwSlotMask;
     if (!(a.cv.mflag[m] & kMfCv)) continue;
     const uint32_t t = mw_vtag(w);
-    const uint32_t q = cv_find(a.set, a.cv.mask, m, t, t ? a.tbl_val[e] : 0);
+    const uint32_t q = cv_lookup(a.cv, m, t, t ? a.tbl_val[e] : 0);
     if (q != ~0u) atomicAdd(&a.cnt[q], 1u);
   }
 }
@@ -176,6 +178,7 @@ int launch_cv_prepare(const CvSubArgs& a, hipStream_t st) {
   if (hipMemsetAsync(a.set, 0, sizeof(CvEnt) * ((uint64_t)a.cv.mask + 1), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.cnt, 0, sizeof(uint32_t) * ((uint64_t)a.cv.mask + 1), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.cv.ctl, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(const_cast<uint32_t*>(a.cv.bloom), 0, (1ull << a.cv.bbits) / 8, st) != hipSuccess) return -1;
   const uint32_t gq = std::min<uint32_t>(1024, (a.isc_n + 255) / 256);
   hipLaunchKernelGGL(k_cv_query, dim3(gq), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_cv_verify, dim3(gq), dim3(256), 0, st, a);
