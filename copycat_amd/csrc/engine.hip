@@ -202,8 +202,23 @@ static int ensure_sm_alt(cc_engine* e) {
   e->sm_alt_on = true;
   return CC_OK;
 }
+// the deferred replay on the side stream, after what the engine stream has queued so far
+static int launch_pending_replay(cc_engine* e, hipStream_t st) {
+  if (!e->pend) return CC_OK;
+  e->pend = false;
+  HIPCHECK(hipEventRecord(e->ev_prep, st));
+  HIPCHECK(hipStreamWaitEvent(e->side_st, e->ev_prep, 0));
+  if (launch_small_replay_kernel(e->pend_sa, e->side_st)) return set_err(CC_ERR_HIP, "small-map replay launch", hipGetLastError());
+  HIPCHECK(hipEventRecord(e->ev_rep[e->pend_set], e->side_st));
+  e->rep_pending[e->pend_set] = true;
+  return CC_OK;
+}
 // the engine stream waits for the side stream's replays (before barrier rows, timers, and the batch's end)
 static int join_replay(cc_engine* e, hipStream_t st) {
+  {
+    int rc = launch_pending_replay(e, st);
+    if (rc) return rc;
+  }
   for (int k = 0; k < 2; ++k)
     if (e->rep_pending[k]) {
       HIPCHECK(hipStreamWaitEvent(st, e->ev_rep[k], 0));
@@ -1449,6 +1464,10 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       return set_err(CC_ERR_HIP, "partition launch", x);
     }
     DBG_SYNC("partition launch");
+    {
+      int rc = launch_pending_replay(e, st);  // (the previous sub-batch's small-map replay, beside this one's work)
+      if (rc) return rc;
+    }
     if (e->map_bits && e->ttl_live && launch_map_rows(e->d_cpos, lo, hi, e->d_map_row, st))
       return set_err(CC_ERR_HIP, "map rows launch", hipGetLastError());
     ValueArgs va{};
@@ -1711,18 +1730,19 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.max_resources = e->cfg.max_resources;
           sa.lvl_at = e->d_lvl_at;
           sa.idx0 = c->index + lo;
-          hipStream_t rst = st;  // the replay overlaps the next sub-batch on the side stream (engine_state.h SmSet)
+          // the replay overlaps the next sub-batch on the side stream (engine_state.h SmSet), launched once that
+          // sub-batch's partition is queued (launch_pending_replay)
           static const bool no_side = diag_env("CC_NO_SIDE_REPLAY");  // diagnostics: the replay on the engine stream
           if (ctl[0] && !no_side) {
             int rc = ensure_sm_alt(e);
             if (rc) return rc;
-            rst = e->side_st;
-            sa.ev_prep = e->ev_prep;
+            sa.defer = true;
           }
-          const int rs = launch_small_replay(sa, ctl[0], st, rst);
-          if (rst != st) {
-            HIPCHECK(hipEventRecord(e->ev_rep[e->sm_cur], rst));
-            e->rep_pending[e->sm_cur] = true;
+          const int rs = launch_small_replay(sa, ctl[0], st, st);
+          if (sa.defer && !rs) {
+            e->pend_sa = sa;
+            e->pend = true;
+            e->pend_set = e->sm_cur;
           }
           if (rs) return rs == -1 ? set_err(CC_ERR_HIP, "small-map replay launch", hipGetLastError())
                                   : set_err(CC_ERR_STATE, "small-map events exceed their buffer");

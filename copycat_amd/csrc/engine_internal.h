@@ -197,6 +197,8 @@ struct SmallArgs {
   // run count, then the event count (null: every event is replayed, TTL mode)
   uint32_t* cseg;
   hipEvent_t ev_prep;          // (a replay on another stream: recorded after the sort and compaction)
+  bool defer;                  // outside TTL mode: sort and compact only; the replay kernel comes later
+                               // (launch_small_replay_kernel)
   uint8_t* out_status;         // TTL mode: the size / isEmpty rows among the events are answered here (else null)
   uint64_t* out_value;
   SmallMap* state;             // [max_resources]
@@ -216,6 +218,7 @@ int launch_ttl_scan(const TtlEmit& t, const uint64_t* clock_base, const uint32_t
                     const uint64_t* dl, uint64_t entries, uint32_t* err, hipStream_t st);
 // sort, runs, replay (E events); the replay kernel itself on stream rst (after a.ev_prep, when rst != st)
 int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStream_t rst);
+int launch_small_replay_kernel(const SmallArgs& a, hipStream_t rst);
 int launch_small_finish(const SmallArgs& a, hipStream_t st);              // counters for the next sub-batch
 // size / isEmpty rows of the sub-batch [lo, hi): emitted into the event buffer before the sort (query entries), then
 // answered from the sorted buffer after the unpermute (the row's staged result is a placeholder)

@@ -203,6 +203,11 @@ struct cc_engine {
   hipEvent_t ev_prep = nullptr, ev_rep[2] = {nullptr, nullptr};
   bool rep_pending[2] = {false, false};
   int sm_cur = 0;
+  // a sub-batch's replay waits to be launched until the next sub-batch's partition is running: the partition's
+  // equal-sized tiles run in lockstep rounds over every CU, and a CU held by the replay cost them a round
+  SmallArgs pend_sa{};
+  bool pend = false;
+  int pend_set = 0;
   void* d_sm_temp = nullptr;
   size_t sm_temp_bytes = 0;
   void* d_clr_scan = nullptr;  // the cleared maps' size scan (map_clear.hip), one element per map event

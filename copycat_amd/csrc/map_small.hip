@@ -546,6 +546,7 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
       hipLaunchKernelGGL(k_small_cseg, dim3(std::min<uint32_t>(1024, (E + 255) / 256)), dim3(256), 0, st, a.ev_key2, orig,
                          a.cseg, a.max_resources);
     }
+    if (a.defer && cmp) return hipGetLastError() == hipSuccess ? 0 : -1;  // (launch_small_replay_kernel, later)
     if (rst != st) {  // the replay overlaps what the engine stream does next
       if (hipEventRecord(a.ev_prep, st) != hipSuccess || hipStreamWaitEvent(rst, a.ev_prep, 0) != hipSuccess) return -1;
     }
@@ -557,6 +558,15 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
       hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg,
                          a.msize, a.mpcap, a.lvl_at, a.index, a.lo, a.out_status, a.out_value);
   }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// A deferred replay (SmallArgs::defer: its events sorted and compacted by launch_small_replay) on stream rst.
+int launch_small_replay_kernel(const SmallArgs& a, hipStream_t rst) {
+  uint32_t* const orig = reinterpret_cast<uint32_t*>(a.ev_key);
+  hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, rst, a.ev_key2, a.ev_val2, a.ev_pay, orig,
+                     a.cseg + a.max_resources + 1, a.cseg, a.cseg + a.max_resources, a.state, a.msmall, a.mpcap, a.lvl_at,
+                     a.idx0, a.index, a.lo, false);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
