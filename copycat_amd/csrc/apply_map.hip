@@ -382,8 +382,7 @@ __global__ __launch_bounds__(CC_MAP_MT) void k_apply_map(const MRec* __restrict_
         const uint64_t brow = (uint64_t)(g[j] / kTile) * kTile + (rr >> 17);  // (mrec_ab)
         ab[j].y = 0;
         if (op == CC_OP_MAP_REPLACEIFPRESENT && CC_FLAG_TAG_B(smeta_flags(m[j])) != CC_TAG_NULL) ab[j].y = cb[row0 + brow];
-        if (clr_live && (clr.mflag[res[j]] & kMfClr))  // its map is cleared in this batch: the commit's epoch
-          m[j] |= clr_epoch(clr, res[j], row0 + brow) << kMetaEpochShift;
+        // (a map cleared in this sub-batch: the commit's clear epoch is in meta bits 25-31, from k_part_ext)
         keyop[j] = map_key_op(op) && (TTL || !(map_reads_ttl(op) && (m[j] & kMetaTtl)));
         ident[j] = map_ident_of(res[j], smeta_flags(m[j]));
         p[j] = (uint32_t)map_hash(res[j], CC_FLAG_KTAG(smeta_flags(m[j])), key[j]) & (kMapRegion - 1);

@@ -386,11 +386,8 @@ __device__ inline void hot_runs_lds(const uint32_t* __restrict__ hot_rpre, const
 }
 
 // (reads each hot commit's meta word from the compact copy k_part_ext writes, hot_meta, not from its 48-byte record)
-// A commit's clear epoch (map_clear.hip): the clears of its map in [lo, row); the row from its staging position.
-__device__ inline uint32_t hot_epoch(const HotClr& c, uint32_t slot, uint32_t g) {
-  const uint64_t row = c.lo + (uint64_t)(g / kTile) * kTile + (c.xr[g].rr >> 17);
-  return clr_epoch(c.clr, slot, row);
-}
+// A commit's clear epoch (map_clear.hip: the clears of its map in [lo, row)), written into its meta word by k_part_ext.
+__device__ inline uint32_t hot_epoch(uint32_t meta) { return meta >> kMetaEpochShift; }
 __device__ inline bool hot_cleared(const HotClr& c, uint32_t slot) {
   return c.clr.mflag != nullptr && (c.clr.mflag[slot] & kMfClr) != 0;
 }
@@ -442,7 +439,7 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ ho
       uint32_t pe = 0;  // the epoch of the commit before this thread's first (0: the sub-batch start)
       if (fl && p0 > 0) {
         cur.seek(p0 - 1);
-        pe = hot_epoch(hc, slot, cur.next());
+        pe = hot_epoch(hot_meta[cur.next()]);
       }
       cur.seek(p0);
       const uint32_t e = p0 + kHPer < L ? p0 + kHPer : L;
@@ -452,7 +449,7 @@ __global__ __launch_bounds__(kHT) void k_hot_agg(const uint32_t* __restrict__ ho
         cond |= compares_value(m);
         Comp el = element(m, g);
         if (fl) {  // a clear since the commit before: CLEAR . el (map_clear.hip)
-          const uint32_t E = hot_epoch(hc, slot, g);
+          const uint32_t E = hot_epoch(m);
           if (E != pe) el.P = el.A;
           pe = E;
         }
@@ -602,7 +599,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
           const uint32_t g = cur.next();
           uint32_t E = 0;
           if (fl) {
-            E = hot_epoch(hc, slot, g);
+            E = hot_epoch(xr[g].meta);
             if (E != pe) {  // cleared before it
               sw &= ~(kMwPresent | kMwVtagMask);
               sv = 0;
@@ -636,7 +633,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
     uint32_t pe0 = 0;  // the epoch of the commit before this thread's first (clears in the stream)
     if (fl && p0 > 0 && p0 < L) {
       cur.seek(p0 - 1);
-      pe0 = hot_epoch(hc, slot, cur.next());
+      pe0 = hot_epoch(xr[cur.next()].meta);
     }
     if (p0 < L) cur.seek(p0);
     uint32_t pe = pe0;
@@ -650,7 +647,7 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
         ms[q] = xr[gs[q]].meta;
         Comp el = element(ms[q], gs[q]);
         if (fl) {  // a clear since the commit before: CLEAR . el (as k_hot_agg)
-          es[q] = hot_epoch(hc, slot, gs[q]);
+          es[q] = hot_epoch(ms[q]);
           if (es[q] != pe) el.P = el.A;
           pe = es[q];
         }

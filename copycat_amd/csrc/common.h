@@ -667,10 +667,13 @@ struct ClrCtx {
   uint32_t nb, bshift;      // buckets per map, log2 of the rows per bucket
 };
 constexpr uint32_t kMetaEpochShift = 25;  // MRec meta bits 25-31 (in LDS, k_apply_map): the commit's clear epoch
-// the bucket's epoch, then the map's few clears inside the bucket before the row (usually none: one load to see it);
-// a binary search over the map's clears was ~10 dependent loads per commit of a cleared map
+// the bucket's epoch (bit 7: a clear of the map falls inside the bucket), then only in such a bucket the map's few
+// clears before the row: one load for most commits (0 for a map not cleared in the sub-batch); a binary search over
+// the map's clears was ~10 dependent loads per commit of a cleared map
 __device__ inline uint32_t clr_epoch(const ClrCtx& c, uint32_t m, uint64_t row) {
   uint32_t e = c.btab[(uint64_t)m * c.nb + (uint32_t)((row - c.lo) >> c.bshift)];
+  if (!(e & 0x80u)) return e;
+  e &= 0x7Fu;
   const uint32_t end = c.eend[m];
   if (e < end) {
     const uint64_t* p = c.clr + c.off[m] + c.base[m];  // the map's clears in this sub-batch, ascending

@@ -1451,6 +1451,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.xrec = e->d_xrec;
     pa.mrec = e->d_mrec;
     pa.hot_meta = e->d_hot_meta;
+    pa.clr = cctx;  // (each map commit's clear epoch into its meta word)
     pa.cpos = e->d_cpos;
     pa.ttab = e->d_ttab;
     pa.dummy = e->sub_batch;

@@ -63,6 +63,7 @@ struct PartArgs {
   XRec* xrec;         // extended staging records (k_part_ext): coordination and value-event commits
   MRec* mrec;         // map / set / multimap commits' 32-byte records (same staging positions)
   uint32_t* hot_meta; // maps: the meta word of each hot-bucket record again, compact (k_hot_agg reads only these)
+  ClrCtx clr{};       // clears in the stream: each map commit's clear epoch into its meta (bits 25-31, map_clear.hip)
   uint16_t* cpos;     // [sub_batch] tile-local staging position of commit lo+i (0xFFFF: unknown session)
   uint16_t* ttab;     // [tiles][sb+1] tile-local run starts (+ live count)
   uint64_t dummy;     // first of the kPT dummy staging rows after the staging area (= sub_batch)

@@ -96,7 +96,8 @@ __global__ void k_clr_sub(const uint64_t* __restrict__ keys, const uint32_t* __r
   }
 }
 
-// per sub-batch: a cleared map's epoch at the start of each row bucket (clr_epoch's first step)
+// per sub-batch: every map's epoch at the start of each row bucket, bit 7 set when one of its clears falls inside the
+// bucket (clr_epoch's first step; 0 for a map not cleared in the sub-batch)
 __global__ void k_clr_btab(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
                            const uint32_t* __restrict__ base, const uint8_t* __restrict__ eend,
                            const uint8_t* __restrict__ mflag, uint32_t R, uint32_t nb, uint32_t bshift, uint64_t lo,
@@ -104,15 +105,20 @@ __global__ void k_clr_btab(const uint64_t* __restrict__ keys, const uint32_t* __
   const uint64_t total = (uint64_t)R * nb;
   for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t m = (uint32_t)(x / nb), b = (uint32_t)(x % nb);
-    if (!(mflag[m] & kMfClr)) continue;
+    if (!(mflag[m] & kMfClr)) {
+      btab[x] = 0;
+      continue;
+    }
     const uint64_t* p = keys + off[m] + base[m];
     const uint64_t row = lo + ((uint64_t)b << bshift);
-    uint32_t a = 0, c = eend[m];
+    const uint32_t ne = eend[m];
+    uint32_t a = 0, c = ne;
     while (a < c) {  // the clears before the bucket's first row
       const uint32_t mid = (a + c) >> 1;
       if ((p[mid] & 0xFFFFFFFFull) < row) a = mid + 1; else c = mid;
     }
-    btab[x] = (uint8_t)a;
+    const bool inside = a < ne && (p[a] & 0xFFFFFFFFull) < row + (1ull << bshift);  // a clear inside the bucket
+    btab[x] = (uint8_t)(a | (inside ? 0x80u : 0u));
   }
 }
 

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     const HotKey* __restrict__ hot, const uint32_t* __restrict__ hot_n, uint32_t* __restrict__ st_meta,
     u64x2* __restrict__ st_ab, XRec* __restrict__ xrec, MRec* __restrict__ mrec, uint32_t* __restrict__ hot_meta,
     uint16_t* __restrict__ cpos,
-    uint16_t* __restrict__ ttab, uint32_t* __restrict__ err_out) {
+    uint16_t* __restrict__ ttab, ClrCtx clr, uint32_t* __restrict__ err_out) {
   constexpr int J = C / kPT;       // commits per thread per chunk
   constexpr int kXCh = kTile / C;  // chunks per tile
   static_assert(J * kXCh == kXQ && (J == 1 || J == 2), "chunk geometry");
@@ -374,6 +374,9 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
         // map slot | row in the tile << 17 (MRec.rr: replaceIfPresent's b is read from the batch by row)
         xs[j] = res[j] | ((uint32_t)(w * (kWave * J) + j * kWave + l + ch * C) << 17);
         if ((int64_t)xa[j] > 0 && ty != CC_RES_MULTIMAP) meta[j] |= kMetaTtl;
+        // a map cleared in this sub-batch: the commit's clear epoch (the map kernels read it from the meta word)
+        if (clr.mflag && ty == CC_RES_MAP)  // (0 for a map not cleared in the sub-batch: one load, no flag test)
+          meta[j] |= clr_epoch(clr, res[j], cbase + (uint64_t)w * (kWave * J) + (uint64_t)j * kWave + l) << kMetaEpochShift;
       } else if (tyb & kTpWalk) {
         value_encode(meta[j] & 0xFF, (meta[j] >> 8) & 0xFF, ab[j].x, ab[j].y, meta[j], ab[j]);
       } else if (ty == CC_RES_LOCK) {
@@ -542,7 +545,7 @@ int launch_part_ext(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(tiles), dim3(kPT), tile_lds_bytes(a.sb, true, c, a.inst_id != nullptr), st, a.inst, a.op,
                      a.flags, a.a, a.b, a.key, a.index, a.aux, a.time, a.clock_base, a.ext_flags, a.lo, a.hi, a.inst_id, a.inst_res,
                      a.res_type, a.sb_kind, a.max_inst, a.sb, a.sb_val, a.map_bits, a.sbq_base, a.hot, a.hot_n,
-                     a.st_meta, a.st_ab, a.xrec, a.mrec, a.map_bits ? a.hot_meta : nullptr, a.cpos, a.ttab, a.err);
+                     a.st_meta, a.st_ab, a.xrec, a.mrec, a.map_bits ? a.hot_meta : nullptr, a.cpos, a.ttab, a.clr, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
