@@ -403,9 +403,9 @@ __device__ inline void hot_map_event_at(const HotClr& c, uint32_t slot, uint32_t
   const uint32_t kt = CC_FLAG_KTAG(smeta_flags(r.meta));
   const uint32_t jh = java_key_hash(kt, r.key, c.hh_key, c.hh_val, c.hh_n, ok);
   const uint64_t d = r.idx - *c.idx0p;
-  if (!ok || d >> 40) err |= kErrHandleHash;
+  if (!ok || d >> kEvPosBits) err |= kErrHandleHash;
   if (at < c.ev_cap) {
-    c.ev_key[at] = ((uint64_t)slot << 44) | ((d & ((1ull << 40) - 1)) << 4) | code;
+    c.ev_key[at] = ((uint64_t)slot << kEvMapShift) | ((d & kEvPosMask) << 4) | code;
     c.ev_val[at] = at;
     c.ev_pay[at] = EvPay{r.key, jh, kt};
   }

@@ -491,12 +491,15 @@ __host__ __device__ inline uint32_t cap_level(uint64_t p) {
 // In TTL mode a map's size also drops when a timer fires (MapState.java:91-93: the scheduled map.remove(key)), with no
 // commit.  Every expiry becomes an event at the boundary where the reference fires it: the first row of the batch
 // whose clock max(clock_before, time[r]) reaches the deadline, before that row (module mode) or after it (manager
-// mode, deferred: boundary r + 1).  Events are keyed map << 44 | position << 4 | code, position 2 * (row
+// mode, deferred: boundary r + 1).  Events are keyed map << 36 | position << 4 | code, position 2 * (row
 // - lo) + 1 for a commit of row `row`, 2 * (b - lo) for boundary b (before row b), code 1 insert / 2 remove, so a
 // radix sort puts each map's commits and expiries in log order.  A sub-batch [lo, hi) owns the boundaries [bl, bh]:
 // bh = hi, bl = lo at the batch start and after a barrier row, lo + 1 after another sub-batch (which owned lo).
 // A map event's payload (map_small.hip), by emission slot: the sorted events carry the slot as their value.
 // aux = the key's HashMap hash for an insertion / removal, the batch row for a size / isEmpty query.
+constexpr uint32_t kEvPosBits = 32;                      // a map event's position field (a sub-batch's span)
+constexpr uint32_t kEvMapShift = 4 + kEvPosBits;          // its map slot above it (the sort's key bits end there)
+constexpr uint64_t kEvPosMask = (1ull << kEvPosBits) - 1;
 struct EvPay {
   uint64_t key;   // the key (its tag in ktag): a small map's model tells keys with one hash apart by them
   uint32_t aux;
@@ -543,7 +546,7 @@ __device__ inline void ttl_expiry_event(const TtlEmit& t, uint64_t cb, uint32_t 
   if (!ok) err |= kErrHandleHash;
   const uint32_t at = wave_append(t.ctl);
   if (at < t.ev_cap) {
-    t.ev_key[at] = ((uint64_t)(w & kMwSlotMask) << 44) | ((pos & ((1ull << 40) - 1)) << 4) | 2u;
+    t.ev_key[at] = ((uint64_t)(w & kMwSlotMask) << kEvMapShift) | ((pos & kEvPosMask) << 4) | 2u;
     t.ev_val[at] = at;
     t.ev_pay[at] = EvPay{key, jh, (w >> 17) & 3u};
   }

@@ -594,7 +594,7 @@ static int check_device_err(cc_engine* e) {
                                    "spans more than 2^40 log indices");
     if (err & kErrHandleHash)
       return set_err(CC_ERR_STATE, "a HANDLE map key's String.hashCode is not registered (cc_handle_hashes), or a "
-                                   "sub-batch spans more than 2^40 log indices");
+                                   "sub-batch spans more than 2^32 log indices");
     if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
     if (err & kErrCapacity)
       return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, lock queue, listeners, members)");
@@ -1633,6 +1633,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sz.ev_pay = e->d_sm_pay;
           sz.cap = (uint32_t)e->sm_cap;
           sz.ctl = e->d_sm_ctl;
+          sz.err = e->d_err;
           sz.ttl = true;
           if (launch_size_emit(sz, st)) return set_err(CC_ERR_HIP, "size query launch", hipGetLastError());
         }
@@ -1695,6 +1696,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sz.ev_pay = e->d_sm_pay;
           sz.cap = (uint32_t)e->sm_cap;
           sz.ctl = e->d_sm_ctl;
+          sz.err = e->d_err;
           sz.sorted_key = e->d_sm_key2;
           sz.sorted_val = e->d_sm_val2;
           sz.seg = e->d_sm_seg;

@@ -171,7 +171,7 @@ struct MapSizeArgs {
   const uint64_t* hh_key;      // String.hashCode of HANDLE keys (cc_handle_hashes), sorted by handle
   const int32_t* hh_val;
   uint32_t hh_n;
-  uint64_t* ev_key;            // [ev_cap] map << 44 | (index - idx0) << 4 | code
+  uint64_t* ev_key;            // [ev_cap] map << kEvMapShift | (index - idx0) << 4 | code
   uint32_t* ev_val;            // [ev_cap] the emission slot (its payload: ev_pay)
   EvPay* ev_pay;               // [ev_cap] key, tag and HashMap hash
   uint32_t ev_cap;
@@ -244,6 +244,7 @@ struct SizeArgs {
   uint8_t* out_status;          // the batch's result columns (absolute rows)
   uint64_t* out_value;
   bool ttl;                     // TTL mode: queries positioned by row (common.h TtlEmit), answered by k_ttl_replay
+  uint32_t* err;                // kErrHandleHash: a sub-batch spanning 2^32 log indices
 };
 int launch_size_emit(const SizeArgs& a, hipStream_t st);
 int launch_size_answer(const SizeArgs& a, hipStream_t st);

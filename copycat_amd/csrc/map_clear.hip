@@ -125,15 +125,16 @@ __global__ void k_clr_btab(const uint64_t* __restrict__ keys, const uint32_t* __
 // per sub-batch: the clears of [lo, hi) join the map events (code 3: the size resets to 0)
 __global__ void k_clr_events(const uint64_t* __restrict__ keys, uint32_t n, uint64_t lo, uint64_t hi,
                              const uint64_t* __restrict__ index, uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val,
-                             EvPay* __restrict__ ev_pay, uint32_t cap, uint32_t* __restrict__ ctl) {
+                             EvPay* __restrict__ ev_pay, uint32_t cap, uint32_t* __restrict__ ctl, uint32_t* __restrict__ err) {
   const uint64_t idx0 = index[lo];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint64_t k = keys[i], row = k & 0xFFFFFFFFull, m = k >> 32;
     if (row < lo || row >= hi) continue;
-    const uint64_t d = (index[row] - idx0) & ((1ull << 40) - 1);
+    const uint64_t d = index[row] - idx0;
+    if (d >> kEvPosBits) atomicOr(err, kErrHandleHash);
     const uint32_t at = atomicAdd(ctl, 1u);
     if (at < cap) {
-      ev_key[at] = (m << 44) | (d << 4) | 3u;
+      ev_key[at] = (m << kEvMapShift) | ((d & kEvPosMask) << 4) | 3u;
       ev_val[at] = at;
       ev_pay[at] = EvPay{0, (uint32_t)row, 0};
     }
@@ -151,7 +152,7 @@ int launch_clr_sub(const ClrSubArgs& a, hipStream_t st) {
 int launch_clr_events(const ClrSubArgs& a, hipStream_t st) {
   if (a.n == 0) return 0;
   hipLaunchKernelGGL(k_clr_events, dim3(std::min<uint32_t>(1024, (a.n + 255) / 256)), dim3(256), 0, st, a.keys, a.n, a.lo,
-                     a.hi, a.index, a.ev_key, a.ev_val, a.ev_pay, a.ev_cap, a.ev_ctl);
+                     a.hi, a.index, a.ev_key, a.ev_val, a.ev_pay, a.ev_cap, a.ev_ctl, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -206,10 +207,10 @@ struct ClrElem {
   const uint32_t* msize;
   __device__ ClrS operator()(uint32_t i) const {
     const uint64_t k = key[i];
-    const uint32_t m = (uint32_t)(k >> 44);
+    const uint32_t m = (uint32_t)(k >> kEvMapShift);
     const bool clear = !(k & 8u) && (k & 3u) == 3u;
     const int32_t d = clr_delta(k);
-    if (i == 0 || (uint32_t)(key[i - 1] >> 44) != m) {  // the map's first event: from its size at the sub-batch start
+    if (i == 0 || (uint32_t)(key[i - 1] >> kEvMapShift) != m) {  // the map's first event: from its size at the sub-batch start
       const int32_t s0 = (int32_t)msize[m];
       const int32_t v = clear ? 0 : s0 + d;
       return ClrS{v, kClrNeg, max(s0, v), 3u};
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(256) void k_clr_finish(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ out_value) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
     const uint64_t k = key[i];
-    const uint32_t m = (uint32_t)(k >> 44);
+    const uint32_t m = (uint32_t)(k >> kEvMapShift);
     if (!(mflag[m] & kMfClr)) continue;  // (small / size-queried maps: map_small.hip)
     const ClrS x = S[i];
     const int32_t v = x.v;
@@ -242,14 +243,14 @@ __global__ __launch_bounds__(256) void k_clr_finish(const uint64_t* __restrict__
         out_value[row] = (uint64_t)v;
       }
     }
-    const bool first = i == 0 || (uint32_t)(key[i - 1] >> 44) != m;
+    const bool first = i == 0 || (uint32_t)(key[i - 1] >> kEvMapShift) != m;
     if (lvl_at && clr_delta(k) > 0) {  // an insertion growing the table (the capacity-level timeline)
       const int32_t before = first ? v - 1 : S[i - 1].post;  // (the peak so far, the start size included)
       if (v > before)
         lvl_reached(lvl_at, m, cap_level((uint64_t)max(before, 0)), cap_level((uint64_t)v),
-                    *idx0p + ((k >> 4) & ((1ull << 40) - 1)));
+                    *idx0p + ((k >> 4) & kEvPosMask));
     }
-    if (i + 1 == E || (uint32_t)(key[i + 1] >> 44) != m) {  // the map's last event
+    if (i + 1 == E || (uint32_t)(key[i + 1] >> kEvMapShift) != m) {  // the map's last event
       msize[m] = (uint32_t)max(v, 0);
       atomicMax(&mpcap[m], cap_level((uint64_t)max(x.post, 0)));
     }

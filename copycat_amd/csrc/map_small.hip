@@ -11,7 +11,7 @@
 // Per map in that window the engine keeps the map's HashMap node for node (small_jhm.h: at most 49 nodes) and
 // replays its insertions and removals in log order:
 //   1. launch_map_size's count kernel (k_msize_count) emits one event per region commit of a small map that inserted
-//      or removed a key: key (map << 44 | (log index - the sub-batch's first) << 4 | insert / remove), value = the
+//      or removed a key: key (map << 36 | (log index - the sub-batch's first) << 4 | insert / remove), value = the
 //      key's HashMap hash (k_hot_apply emits the same for the map's hot-key commits);
 //   2. a radix sort by that key puts each map's events in log order (hipcub);
 //   3. alternating remove / put chains of one key are marked for skipping (k_small_chains), then one wave per map
@@ -41,7 +41,7 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
                             uint32_t* __restrict__ nseg) {
   const uint32_t E = ctl[0];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x)
-    if (i == 0 || (key[i] >> 44) != (key[i - 1] >> 44)) seg[atomicAdd(nseg, 1u)] = i;
+    if (i == 0 || (key[i] >> kEvMapShift) != (key[i - 1] >> kEvMapShift)) seg[atomicAdd(nseg, 1u)] = i;
 }
 
 // Alternating runs of one key (a hot key of a small map: remove k, put k, remove k, put k, ... with no other event of
@@ -66,7 +66,7 @@ struct ChainStart {  // i when event i starts a chain (does not link to i - 1), 
     if (i == 0) return 0;
     const uint64_t k = key[i], q = key[i - 1];
     const uint32_t c = chain_code(k), cq = chain_code(q);
-    if (!c || !cq || c == cq || (k >> 44) != (q >> 44)) return i;
+    if (!c || !cq || c == cq || (k >> kEvMapShift) != (q >> kEvMapShift)) return i;
     const EvPay x = pay[val[i]], y = pay[val[i - 1]];
     const bool link = x.key == y.key && x.aux == y.aux && (x.ktag & 3u) == (y.ktag & 3u);
     return link ? 0u : i;
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_small_chains(const uint64_t* __restrict
     if (s0 == i) continue;                               // (a chain of one event)
     if (i + 1 < E && start[i + 1] != i + 1) continue;    // not the chain's end
     const uint64_t k = key[i];
-    if (!(st[k >> 44].flags & kSmIn)) continue;          // (out of the window: not replayed)
+    if (!(st[k >> kEvMapShift].flags & kSmIn)) continue;          // (out of the window: not replayed)
     const uint32_t r0 = (key[s0] & 3u) == 1u ? s0 + 1 : s0;  // the chain's first removal
     if (i <= r0) continue;
     const uint32_t skip = (k & 3u) == 1u ? i - r0 - 1 : i - r0;
@@ -105,7 +105,7 @@ struct ChainKeep {
   uint32_t E;
   __device__ uint8_t operator()(uint32_t i) const {
     const uint64_t k = key[i];
-    if (!(st[k >> 44].flags & kSmIn)) return 0;  // (not replayed)
+    if (!(st[k >> kEvMapShift].flags & kSmIn)) return 0;  // (not replayed)
     const uint32_t s0 = start[i];
     if (s0 == i) return 1;
     const uint32_t r0 = (key[s0] & 3u) == 1u ? s0 + 1 : s0;
@@ -127,7 +127,7 @@ __global__ void k_small_cseg(const uint64_t* __restrict__ key, const uint32_t* _
                              uint32_t R) {
   const uint32_t n = cseg[R + 1];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    if (i == 0 || (key[orig[i]] >> 44) != (key[orig[i - 1]] >> 44)) cseg[atomicAdd(&cseg[R], 1u)] = i;
+    if (i == 0 || (key[orig[i]] >> kEvMapShift) != (key[orig[i - 1]] >> kEvMapShift)) cseg[atomicAdd(&cseg[R], 1u)] = i;
 }
 
 // One wave per run: the map's java.util.HashMap loaded into the wave's registers (small_jhm.h: node i and bin i in
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
   const uint32_t E = ctl[0], ns = *nseg;
   for (uint32_t r = blockIdx.x * kSrW + wv; r < ns; r += gridDim.x * kSrW) {  // (wave-uniform)
     const uint32_t start = seg[r];
-    const uint32_t m = (uint32_t)(key[orig ? orig[start] : start] >> 44);
+    const uint32_t m = (uint32_t)(key[orig ? orig[start] : start] >> kEvMapShift);
     SmallMap* s = st + m;
     if (!(s->flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
     SmallJhm j;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
         const uint32_t lv0 = j.lvl;
         const bool stay = j.put(yh, ykt, ykey);
         if (j.lvl > lv0 && lvl_at && l == 0) {  // the table grew at this commit: the capacity-level timeline (common.h)
-          const uint64_t d = (kk >> 4) & ((1ull << 40) - 1);
+          const uint64_t d = (kk >> 4) & kEvPosMask;
           // (an index that cannot be known is not recorded: "not left yet" only over-counts, toward refusing)
           if (ttl ? index != nullptr : idx0 != nullptr)
             lvl_reached(lvl_at, m, lv0, j.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
       if (ii < E) {
         o = orig ? orig[ii] : ii;
         const uint64_t kk = key[o];
-        if ((uint32_t)(kk >> 44) == m) {
+        if ((uint32_t)(kk >> kEvMapShift) == m) {
           k = kk;
           if (!(kk & 8u) && (kk & 3u) != 3u) {  // (a commit: its key; a clear or a query has none)
             const EvPay x = pay[val[o]];
@@ -334,11 +334,11 @@ __global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__
   const uint32_t waves = gridDim.x * (blockDim.x / kWave);
   for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
     const uint32_t start = seg[r];
-    const uint32_t m = (uint32_t)(key[start] >> 44);
+    const uint32_t m = (uint32_t)(key[start] >> kEvMapShift);
     int64_t size = msize[m], peak = size;
     for (uint32_t b = start;; b += kWave) {
       const uint32_t i = b + l;
-      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
+      const bool in = i < E && (uint32_t)(key[i] >> kEvMapShift) == m;
       const uint64_t k = in ? key[i] : 0;
       const int32_t dlt = !in || (k & 8u) ? 0 : ((k & 3u) == 1u ? 1 : ((k & 3u) == 2u ? -1 : 0));
       int32_t inc = dlt;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void k_ttl_replay(const uint64_t* __restrict__
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
       if (lvl_at && index && dlt > 0 && size + inc > peak) {  // a commit growing the table (common.h timeline)
-        const uint64_t d = (k >> 4) & ((1ull << 40) - 1);  // (commits sit at odd positions 2 (row - lo) + 1)
+        const uint64_t d = (k >> 4) & kEvPosMask;  // (commits sit at odd positions 2 (row - lo) + 1)
         lvl_reached(lvl_at, m, cap_level((uint64_t)max<int64_t>(peak, 0)), cap_level((uint64_t)(size + inc)),
                     index[lo + (d - 1) / 2]);
       }
@@ -417,16 +417,17 @@ __global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, ui
                             const uint32_t* __restrict__ inst, const uint8_t* __restrict__ op,
                             const uint64_t* __restrict__ index, const uint32_t* __restrict__ inst_res,
                             uint64_t* __restrict__ ev_key, uint32_t* __restrict__ ev_val, EvPay* __restrict__ ev_pay,
-                            uint32_t cap, uint32_t* __restrict__ ctl, bool ttl) {
+                            uint32_t cap, uint32_t* __restrict__ ctl, bool ttl, uint32_t* __restrict__ err) {
   const uint64_t idx0 = ttl ? 0 : index[lo];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < szq_n; q += gridDim.x * blockDim.x) {
     const uint32_t row = szq[q];
     if (row < lo || row >= hi) continue;
     const uint32_t m = inst_res[inst[row]];  // (listed by the barrier scan on a live map: the registry is fixed in a batch)
-    const uint64_t d = (ttl ? 2 * (row - lo) + 1 : index[row] - idx0) & ((1ull << 40) - 1);
+    const uint64_t d = ttl ? 2 * (row - lo) + 1 : index[row] - idx0;
+    if (d >> kEvPosBits) atomicOr(err, kErrHandleHash);
     const uint32_t at = atomicAdd(ctl, 1u);
     if (at < cap) {
-      ev_key[at] = ((uint64_t)m << 44) | (d << 4) | 8u | (op[row] == CC_OP_MAP_ISEMPTY ? 4u : 0u);
+      ev_key[at] = ((uint64_t)m << kEvMapShift) | ((d & kEvPosMask) << 4) | 8u | (op[row] == CC_OP_MAP_ISEMPTY ? 4u : 0u);
       ev_val[at] = at;
       ev_pay[at] = EvPay{0, row, 0};
     }
@@ -443,13 +444,13 @@ __global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict_
   const uint32_t waves = gridDim.x * (blockDim.x / kWave);
   for (uint32_t r = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave); r < ns; r += waves) {
     const uint32_t start = seg[r];
-    const uint32_t m = (uint32_t)(key[start] >> 44);
+    const uint32_t m = (uint32_t)(key[start] >> kEvMapShift);
     int32_t net = 0;
     bool queries = false;
     uint32_t end = start;
     for (uint32_t b = start;; b += kWave) {  // pass 1: the run's end, net change, and whether it holds a query
       const uint32_t i = b + l;
-      const bool in = i < E && (uint32_t)(key[i] >> 44) == m;
+      const bool in = i < E && (uint32_t)(key[i] >> kEvMapShift) == m;
       const uint64_t k = in ? key[i] : 0;
       const int32_t dlt = !in || (k & 8u) ? 0 : ((k & 3u) == 1u ? 1 : ((k & 3u) == 2u ? -1 : 0));
       int32_t sum = dlt;
@@ -496,7 +497,7 @@ __global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
 int launch_size_emit(const SizeArgs& a, hipStream_t st) {
   if (a.szq_n == 0) return 0;
   hipLaunchKernelGGL(k_size_emit, dim3(std::min<uint32_t>(1024, (a.szq_n + 255) / 256)), dim3(256), 0, st, a.szq, a.szq_n,
-                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.ev_pay, a.cap, a.ctl, a.ttl);
+                     a.lo, a.hi, a.inst, a.op, a.index, a.inst_res, a.ev_key, a.ev_val, a.ev_pay, a.cap, a.ctl, a.ttl, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -514,13 +515,16 @@ int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st) {
 int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStream_t rst) {
   if (E > a.cap) return -2;
   if (E) {
+    // the key bits in use: the position and code, then the map slot (< max_resources): 6 digit passes for 4096 maps
+    int end_bit = (int)kEvMapShift;
+    while (end_bit < 64 && (a.max_resources - 1) >> (end_bit - kEvMapShift)) ++end_bit;
     size_t need = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, need, a.ev_key, a.ev_key2, a.ev_val, a.ev_val2, (int)E, 0, 64, st) !=
-        hipSuccess)
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, need, a.ev_key, a.ev_key2, a.ev_val, a.ev_val2, (int)E, 0, end_bit,
+                                           st) != hipSuccess)
       return -1;
     if (need > a.temp_bytes) return -3;  // (sized for cap events at creation)
     size_t tb = a.temp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(a.temp, tb, a.ev_key, a.ev_key2, a.ev_val, a.ev_val2, (int)E, 0, 64, st) !=
+    if (hipcub::DeviceRadixSort::SortPairs(a.temp, tb, a.ev_key, a.ev_key2, a.ev_val, a.ev_val2, (int)E, 0, end_bit, st) !=
         hipSuccess)
       return -1;
     if (hipMemsetAsync(a.nseg, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
