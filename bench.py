@@ -676,8 +676,12 @@ def c3_full_gate(n, R, args, rank, status0, value0, gpu_tab, block=1 << 26):
                 v_ref[rows] = res[t][1]
             s_gpu = status0[lo:lo + m].cpu().numpy()
             v_gpu = value0[lo:lo + m].cpu().numpy().view(np.uint64)
-            mism += int(np.count_nonzero((s_gpu != s_ref) | (v_gpu != v_ref)))
+            bad_rows = np.flatnonzero((s_gpu != s_ref) | (v_gpu != v_ref))
+            mism += len(bad_rows)
             unwritten += int(np.count_nonzero(s_gpu == RESULT_SENTINEL))
+            for r in bad_rows[:8]:  # (a failing gate names its first rows)
+                sys.stderr.write(f"c3 mismatch row {lo + r}: inst {b.inst[r]} op {b.op[r]} key {b.key[r]} gpu "
+                                 f"({s_gpu[r]}, {v_gpu[r]}) ref ({s_ref[r]}, {v_ref[r]})\n")
             del subs, res
     sl, kt, k, vt, v, ci = gpu_tab
     bounds = np.searchsorted(sl, np.arange(R + 1))

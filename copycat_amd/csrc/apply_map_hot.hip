@@ -378,8 +378,10 @@ __device__ inline uint32_t hot_item_key(const uint32_t* pfx, uint32_t nh, uint32
   return a;
 }
 __device__ inline void hot_runs_lds(const uint32_t* __restrict__ hot_rpre, const uint32_t* __restrict__ hot_rstart,
-                                    uint32_t h, uint32_t tiles, uint32_t* lrpre, uint32_t* lrst) {
+                                    uint32_t h, uint32_t tiles, uint32_t* lrpre, uint32_t* lrst,
+                                    uint32_t* lflag = nullptr, uint32_t flag = 0) {
   __syncthreads();
+  if (lflag && threadIdx.x == 0) *lflag = flag;  // (thread 0's value for the whole workgroup)
   for (uint32_t q = threadIdx.x; q <= tiles; q += blockDim.x) lrpre[q] = hot_rpre[(uint64_t)h * (kMaxTiles + 1) + q];
   for (uint32_t q = threadIdx.x; q < tiles; q += blockDim.x) lrst[q] = hot_rstart[(uint64_t)h * kMaxTiles + q];
   __syncthreads();
@@ -572,13 +574,19 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
   __shared__ Comp carry;
   __shared__ uint32_t lrpre[kMaxTiles + 1], lrst[kMaxTiles];
   __shared__ uint32_t evw[kHT / kWave], evbase;  // the item's map events: per-wave counts, the workgroup's reservation
+  __shared__ uint32_t iflag;                      // the item's map flags (bit 0 events, bit 1 cleared)
   uint32_t nh;
   hot_items(hot_n, hot_len, pfx, nh);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   uint32_t err = 0;
   for (uint32_t item = blockIdx.x; item < pfx[nh]; item += gridDim.x) {
     const uint32_t h = hot_item_key(pfx, nh, item);
-    hot_runs_lds(hot_rpre, hot_rstart, h, tiles, lrpre, lrst);
+    const uint32_t slot = hot[h].ident & kMwSlotMask;
+    // The map's flags are read once, by thread 0, for the whole workgroup: the previous sub-batch's small-map replay
+    // (map_small.hip, on the side stream) may clear kMfSmall while this kernel runs, and threads that read the byte
+    // at different times took different branches around the barriers of the event reservation below.
+    const uint32_t f0 = t == 0 ? (hot_events(hc, slot) ? 1u : 0u) | (hot_cleared(hc, slot) ? 2u : 0u) : 0u;
+    hot_runs_lds(hot_rpre, hot_rstart, h, tiles, lrpre, lrst, &iflag, f0);
     const uint32_t p = item - pfx[h], L = hot_len[h], P = pfx[h + 1] - pfx[h];
     const HotS0 s0 = hot_s0[h];
     const uint32_t pos = hot[h].pos;
@@ -586,9 +594,8 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
     // pfx[h] * kHotPiece / 16 + position / 16 (a thread's kHPer positions of a piece are whole bytes of one word)
     uint32_t* const msz = hot_msz + (uint64_t)pfx[h] * (kHotPiece / 16);
     ListCursor cur{lrpre, lrst, tiles, 0, 0, 0, 0};
-    const uint32_t slot = hot[h].ident & kMwSlotMask;
-    const bool fl = hot_cleared(hc, slot);  // its map is cleared in this sub-batch (item-uniform)
-    const bool evs = hot_events(hc, slot);  // its insertions / removals are map events
+    const bool fl = (iflag & 2u) != 0;   // its map is cleared in this sub-batch (item-uniform)
+    const bool evs = (iflag & 1u) != 0;  // its insertions / removals are map events (item-uniform)
     if (hot_cond[h]) {  // value-comparing ops on this key: its whole list, in order, on one thread
       if (p == 0 && t == 0) {
         uint32_t sw = s0.w;
@@ -760,10 +767,10 @@ int launch_map_hot_apply(const HotArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_hot_lists, dim3(kHotMax), dim3(kHT), 0, st, a.ttab, a.tiles, a.sb, sb_hot, a.hot, a.hot_n, a.tbl_val,
                      a.tbl_word, a.tbl_ci, a.tbl_ins, a.hot_rpre, a.hot_rstart, a.hot_len, a.hot_cond,
                      reinterpret_cast<HotS0*>(a.hot_s0));
-  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGrid), dim3(kHT), 0, st, a.hot_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
+  hipLaunchKernelGGL(k_hot_agg, dim3(kHotGridAgg), dim3(kHT), 0, st, a.hot_meta, a.hot_n, a.hot_len, a.hot_rpre, a.hot_rstart,
                      a.tiles, reinterpret_cast<Comp*>(a.hot_agg), a.hot_cond, a.hot, a.hc);
   hipLaunchKernelGGL(k_hot_carry, dim3(kHotMax), dim3(kHT), 0, st, a.hot_n, a.hot_len, reinterpret_cast<Comp*>(a.hot_agg));
-  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGrid), dim3(kHT), 0, st, a.mrec, a.cb, a.lo, a.hot_n, a.hot, a.hot_len,
+  hipLaunchKernelGGL(k_hot_apply, dim3(kHotGridApply), dim3(kHT), 0, st, a.mrec, a.cb, a.lo, a.hot_n, a.hot, a.hot_len,
                      a.hot_rpre, a.hot_rstart, a.tiles, reinterpret_cast<const Comp*>(a.hot_agg), a.hot_cond,
                      reinterpret_cast<const HotS0*>(a.hot_s0), a.tbl_val, a.tbl_word, a.tbl_ci, a.tbl_ins, a.rst_status,
                      a.rst_value, a.hot_msz, a.cv, a.hc, a.err);

@@ -437,7 +437,15 @@ struct KeyedResultArgs {
 };
 int launch_keyed_results(const KeyedResultArgs& a, hipStream_t st);
 
-constexpr int kHotGrid = 1024;  // workgroups of the hot-key scan kernels (grid-stride over pieces)
+#ifndef CC_HOT_GRID_AGG
+#define CC_HOT_GRID_AGG 1024
+#endif
+#ifndef CC_HOT_GRID_APPLY
+#define CC_HOT_GRID_APPLY 1024
+#endif
+// workgroups of the hot-key scan kernels (grid-stride over pieces; -D overrides for A/B builds only)
+constexpr int kHotGridAgg = CC_HOT_GRID_AGG;
+constexpr int kHotGridApply = CC_HOT_GRID_APPLY;
 // clears in the stream for the hot-key scan (map_clear.hip): commit epochs from their rows, the cleared maps' size
 // events, the entry dropped when its state predates the map's last clear of the sub-batch
 struct HotClr {

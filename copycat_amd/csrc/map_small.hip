@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict_
 
 __global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
   for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
-    mflag[m] &= (uint8_t)~(kMfSize | kMfCv | kMfClr);
+    mflag_and(mflag, m, (uint8_t)~(kMfSize | kMfCv | kMfClr));  // (atomic: a side-stream replay may clear kMfSmall)
 }
 
 int launch_size_emit(const SizeArgs& a, hipStream_t st) {

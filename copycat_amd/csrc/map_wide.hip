@@ -724,8 +724,15 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     auto evm = [&](uint32_t x) {
       return (x & 3u) && (map_row || (msmall[x >> 2] & (kMfSmall | kMfSize | kMfClr)));
     };
-    uint32_t my = 0;
-    for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) my += evm(w[p]) ? 1u : 0u;
+    // (each position's decision is taken once and kept in a bit mask: the previous sub-batch's small-map replay on
+    // the side stream may clear a map's kMfSmall between two reads, and the writes must match the reservation)
+    static_assert(kTile / kMszT <= 32, "one mask bit per position of a thread");
+    uint32_t my = 0, emask = 0;
+    for (uint32_t p = b0 + threadIdx.x, j = 0; p < b1; p += kMszT, ++j)
+      if (evm(w[p])) {
+        ++my;
+        emask |= 1u << j;
+      }
     __shared__ uint32_t wsum[kMszT / kWave], ebase;
     const uint32_t l = __lane_id(), wv = threadIdx.x / kWave;
     uint32_t inc = my;
@@ -747,9 +754,9 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     }
     lds_barrier();
     uint32_t at = ebase + wsum[wv] + inc - my;
-    for (uint32_t p = b0 + threadIdx.x; p < b1; p += kMszT) {
+    for (uint32_t p = b0 + threadIdx.x, j = 0; p < b1; p += kMszT, ++j) {
+      if (!((emask >> j) & 1u)) continue;
       const uint32_t x = w[p];
-      if (!evm(x)) continue;
       const uint64_t g = (uint64_t)t * kTile + p;
       // TTL mode: every map's commits, positioned by row (expiries join them: map_small.hip); else small,
       // size-queried or cleared maps' commits by log index
