@@ -246,6 +246,23 @@ def test_map_zipf_stream_parity():
     _assert_maps(E, O, range(0, maps, 97))
 
 
+@pytest.mark.parametrize("sub_batch", [16384, 65536])
+def test_small_maps_leave_window_beside_hot_keys(sub_batch):
+    """Maps that start empty and pass 64 entries one sub-batch after another, hot keys among them.  Each sub-batch's
+    small-map replay runs on the side stream and clears a map's small flag while the next sub-batch's hot-key and
+    region kernels decide whether its commits are map events (a flag they must read once per workgroup item and
+    per position: DESIGN.md, round 5).  Short sub-batches make every replay overlap the next sub-batch."""
+    from copycat_amd.workload import map_zipf_rows
+
+    n, maps = 1_500_000, 256
+    b = map_zipf_rows(0, n, maps=maps, pairs=1 << 16, s=0.99, seed=777)
+    E, O = _engines(maps, maps, n, 1 << 18, sub_batch=sub_batch)
+    parts = [b.slice(0, n // 3), b.slice(n // 3, n)]
+    _assert_rows(*_apply_both(E, O, parts))
+    _assert_maps(E, O, range(maps))
+    assert E.counters()[3] > 0  # the small maps' events were followed
+
+
 # ---- whole-map ops: containsValue / size / isEmpty / clear / Delete (MapState.java:49-60, 233-274) ----------
 
 _WIDE = np.array([abi.CC_OP_MAP_SIZE, abi.CC_OP_MAP_ISEMPTY, abi.CC_OP_MAP_CONTAINSVALUE, abi.CC_OP_MAP_CLEAR,
