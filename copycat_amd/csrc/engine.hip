@@ -110,6 +110,7 @@ static void free_all(cc_engine* e) {
     if (p) (void)hipFree(p), p = nullptr;
   if (e->d_hh_key) (void)hipFree(e->d_hh_key);
   if (e->d_hh_val) (void)hipFree(e->d_hh_val);
+  if (e->h_pin) (void)hipHostFree(e->h_pin);
   if (e->side_st) (void)hipStreamSynchronize(e->side_st);
   void* alt[] = {e->sm_alt.key, e->sm_alt.key2, e->sm_alt.val, e->sm_alt.val2, e->sm_alt.pay, e->sm_alt.cseg};
   for (void* p : alt)
@@ -497,6 +498,10 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
   ALLOC(e->d_rst_status, e->sub_batch + 4 * kPT);  // + dummy rows for unconditional result stores
   ALLOC(e->d_rst_value, sizeof(uint64_t) * (e->sub_batch + 4 * kPT));
   ALLOC(e->d_err, sizeof(uint32_t));
+  {
+    hipError_t x = hipHostMalloc((void**)&e->h_pin, 8 * sizeof(uint64_t), hipHostMallocDefault);
+    if (x != hipSuccess) return fail("hipHostMalloc (counter readbacks)", x);
+  }
   ALLOC(e->d_bar, sizeof(uint32_t) * kBarCap);
   ALLOC(e->d_bar_n, sizeof(uint32_t));
   ALLOC(e->d_ttl_seen, sizeof(uint32_t));
@@ -1065,13 +1070,22 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         if (launch_cv_batch(cb, st)) return set_err(CC_ERR_HIP, "containsValue classify launch", hipGetLastError());
       }
       uint32_t qn = 0, cvn[2] = {0, 0}, cln = 0;
-      HIPCHECK(hipMemcpyAsync(&nb, e->d_bar_n, sizeof nb, hipMemcpyDeviceToHost, st));
-      HIPCHECK(hipMemcpyAsync(&ttl_seen, e->d_ttl_seen, sizeof ttl_seen, hipMemcpyDeviceToHost, st));
-      HIPCHECK(hipMemcpyAsync(&clock_before, e->d_clock, sizeof clock_before, hipMemcpyDeviceToHost, st));
-      if (inline_size || inline_ttl) HIPCHECK(hipMemcpyAsync(&qn, e->d_szq_n, sizeof qn, hipMemcpyDeviceToHost, st));
-      if (inline_size) HIPCHECK(hipMemcpyAsync(cvn, e->d_cvq_n, sizeof cvn, hipMemcpyDeviceToHost, st));
-      if (inline_size) HIPCHECK(hipMemcpyAsync(&cln, e->d_clrq_n, sizeof cln, hipMemcpyDeviceToHost, st));
-      HIPCHECK(hipStreamSynchronize(st));
+      {  // (one round trip: every counter into the pinned words, then one synchronize)
+        uint64_t* const pin = e->h_pin;
+        uint32_t* const p32 = reinterpret_cast<uint32_t*>(pin + 1);
+        HIPCHECK(hipMemcpyAsync(pin, e->d_clock, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(p32 + 0, e->d_bar_n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(p32 + 1, e->d_ttl_seen, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        if (inline_size || inline_ttl) HIPCHECK(hipMemcpyAsync(p32 + 2, e->d_szq_n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        if (inline_size) HIPCHECK(hipMemcpyAsync(p32 + 3, e->d_cvq_n, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        if (inline_size) HIPCHECK(hipMemcpyAsync(p32 + 5, e->d_clrq_n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        clock_before = pin[0];
+        nb = p32[0];
+        ttl_seen = p32[1];
+        if (inline_size || inline_ttl) qn = p32[2];
+        if (inline_size) cvn[0] = p32[3], cvn[1] = p32[4], cln = p32[5];
+      }
       if (!inline_size && !inline_ttl) break;
       e->szq_flagged = qn > 0 || cvn[0] > 0 || cln > 0;
       if (inline_size && (ttl_seen || pass > 2)) {  // this batch turns TTL mode on: containsValue and clear become
@@ -1709,9 +1723,13 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         if (clr_on && launch_clr_events(ca, st)) return set_err(CC_ERR_HIP, "clear events launch", hipGetLastError());
         if (e->small_live || e->szq_n || clr_on) {
           uint32_t ctl[2] = {0, 0};
-          HIPCHECK(hipMemcpyAsync(ctl, e->d_sm_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
-          if (cv_n) HIPCHECK(hipMemcpyAsync(&cv_E, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
+          uint32_t* const p32 = reinterpret_cast<uint32_t*>(e->h_pin);  // (pinned: one round trip for both)
+          HIPCHECK(hipMemcpyAsync(p32, e->d_sm_ctl, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+          if (cv_n) HIPCHECK(hipMemcpyAsync(p32 + 2, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
           HIPCHECK(hipStreamSynchronize(st));
+          ctl[0] = p32[0];
+          ctl[1] = p32[1];
+          if (cv_n) memcpy(&cv_E, p32 + 2, sizeof cv_E);
           cv_known = cv_n != 0;
           e->stat_events += ctl[0];
           SmallArgs sa{};
@@ -1802,8 +1820,9 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
     if (cv_n) {  // in-stream containsValue answers over the unpermute's placeholders (map_cv.hip)
       if (!cv_known) {
-        HIPCHECK(hipMemcpyAsync(&cv_E, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(e->h_pin, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        memcpy(&cv_E, e->h_pin, sizeof cv_E);
       }
       const int rc = launch_cv_answer(cva, cv_E, st);
       if (rc) return rc == -2 ? set_err(CC_ERR_CAPACITY, "containsValue events exceed their buffer")

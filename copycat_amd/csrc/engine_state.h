@@ -139,6 +139,9 @@ struct cc_engine {
   uint8_t* d_rst_status = nullptr;
   uint64_t* d_rst_value = nullptr;
   uint32_t* d_err = nullptr;
+  // pinned host words for the per-batch / per-sub-batch counter readbacks: a copy into pageable memory returns only
+  // after its own round trip, so two counters read back cost two idle gaps of ~200 us on the GPU
+  uint64_t* h_pin = nullptr;
   // map table (apply_map.hip) + map staging columns
   uint64_t* d_tbl_key = nullptr;
   uint32_t* d_tbl_word = nullptr;
