@@ -115,7 +115,7 @@ static void free_all(cc_engine* e) {
   void* alt[] = {e->sm_alt.key, e->sm_alt.key2, e->sm_alt.val, e->sm_alt.val2, e->sm_alt.pay, e->sm_alt.cseg};
   for (void* p : alt)
     if (p) (void)hipFree(p);
-  for (hipEvent_t ev : {e->ev_prep, e->ev_rep[0], e->ev_rep[1]})
+  for (hipEvent_t ev : {e->ev_prep, e->ev_rep[0], e->ev_rep[1], e->ev_rb})
     if (ev) (void)hipEventDestroy(ev);
   if (e->side_st) (void)hipStreamDestroy(e->side_st);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -1471,6 +1471,28 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     pa.dummy = e->sub_batch;
     const bool v3 = !e->ext;  // value-only engines: value_path.hip
     pa.v3 = v3;
+    // the sub-batch's results back to log order (every staged result is written by then); launched early, beside
+    // the host's counter readback, when nothing after that point writes staged results (below)
+    bool unpermuted = false;
+    auto unpermute = [&]() -> int {
+      UnpermuteArgs ua{};
+      ua.cpos = e->d_cpos;
+      ua.ttab = e->d_ttab;
+      ua.sb = e->sb_total();
+      ua.lo = lo;
+      ua.hi = hi;
+      ua.rst_status = e->d_rst_status;
+      ua.rst_value = e->d_rst_value;
+      ua.out_status = out->status;
+      ua.out_value = out->value;
+      ua.dummy_status = e->d_rst_status + e->sub_batch;
+      ua.dummy_value = e->d_rst_value + e->sub_batch;
+      ua.v3 = v3;
+      ua.mark = marker_of(e);
+      if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
+      unpermuted = true;
+      return CC_OK;
+    };
 
     pa.mark = marker_of(e);
     if (launch_partition(pa, st)) {
@@ -1726,7 +1748,15 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           uint32_t* const p32 = reinterpret_cast<uint32_t*>(e->h_pin);  // (pinned: one round trip for both)
           HIPCHECK(hipMemcpyAsync(p32, e->d_sm_ctl, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
           if (cv_n) HIPCHECK(hipMemcpyAsync(p32 + 2, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));
-          HIPCHECK(hipStreamSynchronize(st));
+          if (!e->coord_on) {  // (the coordination apply, launched below, writes staged results: then no early unpermute)
+            if (!e->ev_rb) HIPCHECK(hipEventCreateWithFlags(&e->ev_rb, hipEventDisableTiming));
+            HIPCHECK(hipEventRecord(e->ev_rb, st));
+            int rc = unpermute();  // (on the GPU while the host waits for the counters)
+            if (rc) return rc;
+            HIPCHECK(hipEventSynchronize(e->ev_rb));
+          } else {
+            HIPCHECK(hipStreamSynchronize(st));
+          }
           ctl[0] = p32[0];
           ctl[1] = p32[1];
           if (cv_n) memcpy(&cv_E, p32 + 2, sizeof cv_E);
@@ -1803,21 +1833,11 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ca.mark = marker_of(e);
       if (launch_apply_coord(ca, st)) return set_err(CC_ERR_HIP, "coordination apply launch", hipGetLastError()); DBG_SYNC("coordination apply launch");
     }
-    UnpermuteArgs ua{};
-    ua.cpos = e->d_cpos;
-    ua.ttab = e->d_ttab;
-    ua.sb = e->sb_total();
-    ua.lo = lo;
-    ua.hi = hi;
-    ua.rst_status = e->d_rst_status;
-    ua.rst_value = e->d_rst_value;
-    ua.out_status = out->status;
-    ua.out_value = out->value;
-    ua.dummy_status = e->d_rst_status + e->sub_batch;
-    ua.dummy_value = e->d_rst_value + e->sub_batch;
-    ua.v3 = v3;
-    ua.mark = marker_of(e);
-    if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError()); DBG_SYNC("unpermute launch");
+    if (!unpermuted) {
+      int rc = unpermute();
+      if (rc) return rc;
+    }
+    DBG_SYNC("unpermute launch");
     if (cv_n) {  // in-stream containsValue answers over the unpermute's placeholders (map_cv.hip)
       if (!cv_known) {
         HIPCHECK(hipMemcpyAsync(e->h_pin, e->d_cvev_ctl, sizeof cv_E, hipMemcpyDeviceToHost, st));

@@ -204,6 +204,7 @@ struct cc_engine {
   bool sm_alt_on = false;
   hipStream_t side_st = nullptr;
   hipEvent_t ev_prep = nullptr, ev_rep[2] = {nullptr, nullptr};
+  hipEvent_t ev_rb = nullptr;  // after the per-sub-batch counter readback (the unpermute runs while the host waits)
   bool rep_pending[2] = {false, false};
   int sm_cur = 0;
   // a sub-batch's replay waits to be launched until the next sub-batch's partition is running: the partition's
