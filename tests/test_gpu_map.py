@@ -187,6 +187,22 @@ def test_map_capacity_error():
     assert ei.value.rc == abi.CC_ERR_CAPACITY
 
 
+def test_map_event_position_span_error():
+    """A small map's insertions are followed as events keyed by their log index within the sub-batch (32 bits): a
+    sub-batch spanning 2^32 log indices fails the call instead of mis-ordering them; the same rows with a dense
+    index apply."""
+    from copycat_amd.engine import EngineError
+
+    b = _puts(np.arange(40, dtype=np.uint64), 0)
+    b.index[20:] += np.uint64(1 << 33)
+    E, _ = _engines(1, 4, 64, 1024)
+    with pytest.raises(EngineError) as ei:
+        E.apply_host(b)
+    assert ei.value.rc == abi.CC_ERR_STATE
+    E, O = _engines(1, 4, 64, 1024)
+    _assert_rows(*_apply_both(E, O, [_puts(np.arange(40, dtype=np.uint64), 0)]))
+
+
 def test_map_get_with_positive_aux_is_applied():
     """ttl is read by put/putIfAbsent/replace/replaceIfPresent only: a get row whose aux column holds a
     positive number is an ordinary get (MapCommands.java: Get carries no ttl)."""
