@@ -1514,6 +1514,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     va.tiles = v3 ? (uint32_t)((hi - lo + kV3Tile - 1) / kV3Tile) : tiles;
     va.v3 = v3;
 
+    va.ca = c->a;
     va.cb = c->b;
     va.lo = lo;
     va.sb = e->sb_total();

@@ -90,8 +90,9 @@ struct ValueArgs {
   uint64_t* rst_value;
   uint64_t dummy;        // first of the dummy result rows after the staging area (= sub_batch)
   uint32_t* err;
-  bool v3;               // value_path.hip: 16-byte records, 8192-commit tiles
-  const uint64_t* cb;    //   the batch's b column (escaped CAS updates) and the sub-batch's first row
+  bool v3;               // value_path.hip: 8-byte records, 8192-commit tiles
+  const uint64_t* ca;    //   the batch's a / b columns (operands of escaped records) and the sub-batch's first row
+  const uint64_t* cb;
   uint64_t lo;
   Marker mark;
 };

@@ -1,17 +1,13 @@
 // value_path.hip — the value-only engine pipeline (the c2 headline): k_part_v4 -> k_apply_value_v3 -> k_unpermute.
 //
-// Same algorithm as partition_value.hip k_part_v2 + apply_value.hip k_apply_value_ws + partition.hip k_unpermute
-// (a stable group-by of the sub-batch by super-bucket = 256 AtomicValueState slots, then one walk per slot in log
-// order, then the results back to log order), with two changes aimed at HBM bytes and CU occupancy:
+// A stable group-by of the sub-batch by super-bucket (256 AtomicValueState slots), one walk per slot in log order,
+// then the results back to log order, shaped for HBM bytes and CU occupancy:
 //
-//  * one 16-byte staging record per commit instead of a 4-byte meta word + a 16-byte operand pair (20 B): the meta
-//    (slot, op class, the two value tags) shares the second word with the CAS update stored as a 33-bit difference
-//    from the expected value (a DistributedAtomicLong CAS loop updates by a small delta, DistributedAtomicLong.java
-//    :117-146).  A CAS whose difference does not fit keeps its row in the tile instead and the apply reads its update
-//    from the batch's b column (exact for every input; only the bytes moved differ);
-//  * 8192-commit tiles partitioned by 512-thread workgroups (two per CU: one workgroup's per-tile prologue -- the
-//    instance loads and the instance -> resource gathers -- overlaps the other's chunk loop) and unpermuted by
-//    512-thread workgroups.
+//  * one 8-byte staging record per commit: the meta (slot, op class, the two value tags) and the operands packed as
+//    small two's complement numbers (the CAS update as a difference from the expected value); a commit whose
+//    operands do not fit keeps its row in the tile instead and the apply reads them from the batch's a / b columns;
+//  * 8192-commit tiles, each ranked whole in one persistent 1024-thread workgroup per CU and written out of an LDS
+//    image in full lines; the apply walks each slot in registers while loader waves stage the next chunk.
 //
 // Reference semantics are AtomicValueState's (atomic/src/main/java/io/atomix/atomic/state/AtomicValueState.java):
 // get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144, delete :146-157; dispatch and unknown
@@ -33,70 +29,66 @@ int phase_read_v3(int kernel, uint64_t* out) {
 #endif
 
 
-// ---- the 16-byte value record -------------------------------------------------------------------------------
-// w0 = the payload the op carries (CAS: canonical expected value; set / getAndSet: canonical new value; else 0)
-// w1 = meta (18 bits) | row (13 bits) << 18 | delta (33 bits) << 31
+// ---- the 8-byte value record -------------------------------------------------------------------------------
+// w = meta (18 bits) | payload (46 bits) << 18
 //   meta: slot-in-super-bucket 0..7 | class 8..10 | compare tag 11..13 | new tag 14..16 | escaped 17
-//   row: the commit's row in its 8192-commit tile (where an escaped CAS's update is read from)
-//   delta (CAS): update - expected, two's complement; escaped (does not fit): the update is read from the b column
+//   payload, set / getAndSet: the canonical new value as a 46-bit two's complement number (sign-extended back);
+//            CAS: the canonical expected value as a 32-bit two's complement number | (update - expected) as a 14-bit
+//            one << 32;
+//            escaped (an operand that does not fit): the commit's row in its 8192-commit tile; the apply reads the
+//            operands from the batch's a / b columns there (exact for every input; only the bytes moved differ).
+// A DistributedAtomicLong CAS loop (DistributedAtomicLong.java:117-146) expects a value the resource holds and updates
+// it by a small delta, so its records never escape while the values stay within +-2^31; the 16-byte record of round 3
+// (full expected value + 33-bit delta) moved 8 more bytes per commit through the partition's writes and the apply's
+// reads.
 enum : uint32_t { kC3Get = 0, kC3Set = 1, kC3Cas = 2, kC3Gas = 3, kC3Del = 4, kC3Lis = 5, kC3Unk = 6 };
-constexpr int kV3DeltaBits = 33;
+constexpr int kV3ExpBits = 32, kV3DeltaBits = 14, kV3SetBits = 46;
+static_assert(kV3ExpBits + kV3DeltaBits == kV3SetBits && 18 + kV3SetBits == 64, "the record's payload field");
 static_assert(kV3Tile <= (1 << 13), "the record's row field");
 
-// (The row, < 8192, is ORed into bits 18..30 of w1 where the partition places the record: v3_set_row.  Keeping it
-// out of the encode keeps the partition within its VGPR budget.)
-__device__ inline uint4 v3_encode(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t slot) {
+__device__ inline bool v3_fits(uint64_t x, int bits) {  // x == sign-extension of its low `bits` bits
+  return (uint64_t)(((int64_t)(x << (64 - bits))) >> (64 - bits)) == x;
+}
+
+// (An escaped record's row, < 8192, is ORed in where the partition places the record: v3_set_row.)
+__device__ inline uint64_t v3_encode(uint32_t op, uint32_t flags, uint64_t a, uint64_t b, uint32_t slot) {
   const uint32_t ta = CC_FLAG_TAG_A(flags), tb = CC_FLAG_TAG_B(flags);
   const uint64_t pa = ta ? a : 0, pb = tb ? b : 0;  // canonical NULL payload
   uint32_t cls = kC3Unk, ct = 0, nt = 0, esc = 0;
-  uint64_t w0 = 0, hi = 0;
+  uint64_t pl = 0;
   if (op == CC_OP_VALUE_GET) {
     cls = kC3Get;
   } else if (op == CC_OP_VALUE_SET || op == CC_OP_VALUE_GETANDSET) {
     cls = op == CC_OP_VALUE_SET ? kC3Set : kC3Gas;
     nt = ta;
-    w0 = pa;
+    esc = v3_fits(pa, kV3SetBits) ? 0u : 1u;
+    pl = pa;
   } else if (op == CC_OP_VALUE_CAS) {
     cls = kC3Cas;
     ct = ta;
     nt = tb;
-    w0 = pa;
-    const uint64_t d = pb - pa;  // fits iff sign-extending its low 33 bits gives it back
-    esc = (uint64_t)(((int64_t)(d << (64 - kV3DeltaBits))) >> (64 - kV3DeltaBits)) == d ? 0u : 1u;
-    hi = esc ? 0ull : d;  // hi << 31 below keeps the low 33 bits
+    const uint64_t d = pb - pa;
+    esc = v3_fits(pa, kV3ExpBits) && v3_fits(d, kV3DeltaBits) ? 0u : 1u;
+    pl = (pa & 0xFFFFFFFFull) | (d << kV3ExpBits);
   } else if (op == CC_OP_DELETE) {
     cls = kC3Del;
   } else if (op == CC_OP_VALUE_LISTEN || op == CC_OP_VALUE_UNLISTEN) {
     cls = kC3Lis;
   }
-  const uint64_t w1 = (uint64_t)(slot | (cls << 8) | (ct << 11) | (nt << 14) | (esc << 17)) | (hi << 31);
-  return make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+  pl = esc ? 0ull : pl;
+  return (uint64_t)(slot | (cls << 8) | (ct << 11) | (nt << 14) | (esc << 17)) | (pl << 18);
 }
-__device__ inline uint32_t v3_slot(const uint4& r) { return r.z & 0xFFu; }
-__device__ inline uint4 v3_set_row(uint4 r, uint32_t row) {
-  r.z |= row << 18;
-  return r;
-}
-__device__ inline uint32_t v3_row(const uint4& r) { return (r.z >> 18) & (kV3Tile - 1); }
-// k_part_v4 also stores an escaped CAS's row relative to the sub-batch start in its (unused) delta field (a reader
-// that does not know the record's tile can fetch the update from the b column; k_apply_value_v3 uses the tile row).
-__device__ inline uint4 v3_set_rows(uint4 r, uint32_t row, uint32_t rel) {
-  r.z |= row << 18;
-  if ((r.z >> 17) & 1u) {
-    r.z |= (rel & 1u) << 31;
-    r.w |= rel >> 1;
-  }
-  return r;
+__device__ inline uint32_t v3_slot(uint64_t r) { return (uint32_t)r & 0xFFu; }
+__device__ inline uint64_t v3_set_row(uint64_t r, uint32_t row) {
+  return ((r >> 17) & 1u) ? (r | ((uint64_t)row << 18)) : r;
 }
 
 // The record -> value_walk's form (common.h value_encode: meta word, canonical compare value x, canonical new
-// value y).  tile_row0 = the batch row of the record's tile start (escaped CAS updates are read from cb there).
-__device__ inline void v3_decode(const uint4& r, const uint64_t* __restrict__ cb, uint64_t tile_row0, uint32_t& m,
-                                 uint64_t& x, uint64_t& y) {
-  const uint32_t lo = r.z;
+// value y).  tile_row0 = the batch row of the record's tile start (escaped operands are read from ca / cb there).
+__device__ inline void v3_decode(uint64_t r, const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb,
+                                 uint64_t tile_row0, uint32_t& m, uint64_t& x, uint64_t& y) {
+  const uint32_t lo = (uint32_t)r;
   const uint32_t slot = lo & 0xFFu, cls = (lo >> 8) & 7u, ct = (lo >> 11) & 7u, nt = (lo >> 14) & 7u;
-  const uint64_t w0 = (uint64_t)r.x | ((uint64_t)r.y << 32);
-  const uint64_t w1 = (uint64_t)r.z | ((uint64_t)r.w << 32);
   // class -> the walk's op bits (value_encode): get R, set W, CAS C + status OK|BOOL, getAndSet W|R, delete D,
   // listen / unlisten L (not applied here: flagged), anything else the precomputed UNKNOWN_OP status
   uint32_t bits = CC_STATUS(CC_ST_UNKNOWN_OP, CC_TAG_NULL);
@@ -107,12 +99,15 @@ __device__ inline void v3_decode(const uint4& r, const uint64_t* __restrict__ cb
   bits = cls == kC3Del ? kVrD : bits;
   bits = cls == kC3Lis ? kVrL : bits;
   m = bits | (nt << 13) | (slot << 16) | (ct << 24);
-  const bool cas = cls == kC3Cas;
-  x = cas ? w0 : 0;
-  y = (cls == kC3Set || cls == kC3Gas) ? w0 : 0;
-  if (cas) {
-    if ((lo >> 17) & 1u) y = nt ? cb[tile_row0 + ((lo >> 18) & (kV3Tile - 1))] : 0;  // escaped: from the b column
-    else y = w0 + (uint64_t)((int64_t)w1 >> 31);
+  const bool cas = cls == kC3Cas, wr = cls == kC3Set || cls == kC3Gas;
+  if ((lo >> 17) & 1u) {  // escaped (rare): the operands from the batch columns
+    const uint64_t row = tile_row0 + ((r >> 18) & (kV3Tile - 1));
+    x = cas && ct ? ca[row] : 0;
+    y = cas ? (nt ? cb[row] : 0) : (wr && nt ? ca[row] : 0);
+  } else {
+    const uint64_t e = (uint64_t)(int64_t)(int32_t)(uint32_t)(r >> 18);
+    x = cas ? e : 0;
+    y = cas ? e + (uint64_t)((int64_t)r >> (64 - kV3DeltaBits)) : (wr ? (uint64_t)((int64_t)r >> 18) : 0);
   }
 }
 
@@ -137,9 +132,9 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
                                                 const uint8_t* __restrict__ flags, const uint64_t* __restrict__ ca,
                                                 const uint64_t* __restrict__ cb, uint64_t lo, uint64_t hi,
                                                 const uint32_t* __restrict__ inst_res, uint32_t max_inst, uint32_t sb,
-                                                uint32_t tiles, uint4* __restrict__ st_rec, uint16_t* __restrict__ cpos,
+                                                uint32_t tiles, uint64_t* __restrict__ st_rec, uint16_t* __restrict__ cpos,
                                                 uint16_t* __restrict__ ttab) {
-  __shared__ uint4 img[kV3Tile];             // the tile's records in staging order
+  __shared__ uint64_t img[kV3Tile];          // the tile's records in staging order
   __shared__ uint32_t wc[kP4W][kMaxSb / 2];  // per-wave counters (packed u16 pairs) -> per-wave exclusive prefixes
   __shared__ uint16_t kst[kMaxSb + 1];       // tile-local run starts (+ live count)
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
@@ -275,7 +270,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
         const uint32_t k = r[j] >> KSB, sh = 16 * (k & 1);
         const uint32_t sp = kst[k] + ((wc[w][k >> 1] >> sh) & 0xFFFFu) + loc[j];
         const uint32_t ofj = of2[j / 2] >> (16 * (j % 2));
-        img[sp] = v3_set_rows(v3_encode(ofj & 0xFFu, (ofj >> 8) & 0xFFu, av[j], bv[j], r[j] & ((1u << KSB) - 1)), q, tbase + q);
+        img[sp] = v3_set_row(v3_encode(ofj & 0xFFu, (ofj >> 8) & 0xFFu, av[j], bv[j], r[j] & ((1u << KSB) - 1)), q);
         cp = sp;
       }
       if (q < nrow) cpos[tbase + q] = (uint16_t)cp;
@@ -285,9 +280,10 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
     PH(4);
     lds_barrier();             // B3: the image is complete
     PH(5);
-    // whole tile region, unconditionally (a fixed store count; rows past the live count are never read)
+    // whole tile region, unconditionally (a fixed store count; rows past the live count are never read), 16 B a lane
 #pragma unroll
-    for (int m = 0; m < kP4J; ++m) st_rec[tbase + t + m * kP4T] = img[t + m * kP4T];
+    for (int m = 0; m < kP4J / 2; ++m)
+      reinterpret_cast<uint4*>(st_rec + tbase)[t + m * kP4T] = reinterpret_cast<const uint4*>(img)[t + m * kP4T];
     PH(6);
     if (Tn >= tiles) break;
     T = Tn;
@@ -297,7 +293,7 @@ __global__ __launch_bounds__(kP4T) void k_part_v4(const uint32_t* __restrict__ i
 #endif
 }
 
-// ---- k_apply_value_v3: walker / loader waves (apply_value.hip k_apply_value_ws) over 16-byte records -----------
+// ---- k_apply_value_v3: walker / loader waves (apply_value.hip k_apply_value_ws) over 8-byte records ------------
 // One 1024-thread workgroup per super-bucket: waves 0-3 walk (thread t = slot t, AtomicValueState in registers),
 // waves 4-15 load, decode, rank and place the next chunk (3072 records) into the other LDS buffer and store the
 // previous chunk's results.  The super-bucket's list is its run in every 8192-commit tile, in tile (= log) order.
@@ -363,7 +359,8 @@ __device__ inline void v3_loader_barrier(uint32_t* ctr, uint32_t target) {
 }
 
 template <int NS>
-__global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(const uint4* __restrict__ st_rec, const uint64_t* __restrict__ cb,
+__global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(const uint64_t* __restrict__ st_rec,
+                                                        const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb,
                                                         uint64_t lo, const uint16_t* __restrict__ ttab, uint32_t tiles,
                                                         uint32_t sb, uint32_t* __restrict__ val_meta,
                                                         uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
@@ -456,7 +453,7 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
   // loader registers: the chunk to place next (rr, g; loaded one chunk ahead), the sorted / staging positions of the
   // chunk being walked (pp, gp) and of the chunk before it (qp, gq: its results are stored during the walk)
 #define CC_J4(X) X(0) X(1) X(2) X(3)
-#define CC_DECL(J) uint32_t g##J = kNoPos3, pp##J = 0, gp##J = kNoPos3, qp##J = 0, gq##J = kNoPos3; uint4 rr##J = make_uint4(0, 0, 0, 0);
+#define CC_DECL(J) uint32_t g##J = kNoPos3, pp##J = 0, gp##J = kNoPos3, qp##J = 0, gq##J = kNoPos3; uint64_t rr##J = 0;
   CC_J4(CC_DECL)
 #undef CC_DECL
   // record c0 + lw*256 + j*64 + l of the list (log order = (loader wave, j, lane)); past the end: staging position 0.
@@ -510,7 +507,7 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
   // rank / place the registers' chunk into buffer b (loaders only)
   auto prepare = [&](uint32_t b) {
     uint32_t rank[kWsPer], slot[kWsPer];
-    const uint4 rv4[kWsPer] = {rr0, rr1, rr2, rr3};
+    const uint64_t rv4[kWsPer] = {rr0, rr1, rr2, rr3};
     const uint32_t gv[kWsPer] = {g0, g1, g2, g3};
 #pragma unroll
     for (int j = 0; j < kWsPer; ++j) {
@@ -571,7 +568,7 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
       if (g##J != kNoPos3) {                                                        \
         uint32_t m_;                                                                \
         uint64_t x_, y_;                                                            \
-        v3_decode(rr##J, cb, lo + (uint64_t)(g##J / kV3Tile) * kV3Tile, m_, x_, y_); \
+        v3_decode(rr##J, ca, cb, lo + (uint64_t)(g##J / kV3Tile) * kV3Tile, m_, x_, y_); \
         pp##J = pbase[lw][slot[J]] + rank[J];                                       \
         sm[b][pp##J] = m_;                                                          \
         sab[b][pp##J] = u64x2{x_, y_};                                              \
@@ -677,7 +674,7 @@ int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
   const uint32_t kp = (a.sb + kWave - 1) / kWave;  // super-buckets per lane of the scan wave
 #define CC_LAUNCH4(KP)                                                                                                 \
   hipLaunchKernelGGL((k_part_v4<KP, 8>), dim3(grid), dim3(kP4T), 0, st, a.inst, a.op, a.flags, a.a, a.b, a.lo, a.hi,   \
-                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint4*>(a.st_ab), a.cpos, a.ttab)
+                     a.inst_res, a.max_inst, a.sb, tiles, reinterpret_cast<uint64_t*>(a.st_ab), a.cpos, a.ttab)
   if (kp <= 2) CC_LAUNCH4(2);
   else if (kp <= 4) CC_LAUNCH4(4);
   else CC_LAUNCH4(8);
@@ -688,7 +685,7 @@ int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
   if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
   hipLaunchKernelGGL(k_apply_value_v3<256>, dim3(a.sb_val), dim3(V3A<256>::T), 0, st,
-                     reinterpret_cast<const uint4*>(a.st_ab), a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
+                     reinterpret_cast<const uint64_t*>(a.st_ab), a.ca, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
                      a.rst_status, a.rst_value, a.dummy, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

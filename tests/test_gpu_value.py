@@ -114,13 +114,11 @@ def test_device_resident_apply_matches_host_path():
 
 @pytest.mark.parametrize("map_capacity", [0, 1024])
 def test_cas_update_deltas_at_the_record_boundary(map_capacity):
-    """value_path.hip stores a CAS update as a 33-bit two's-complement difference from the expected value
-    (kV3DeltaBits); a difference that does not fit escapes: its row is kept and the update is read from the batch's b
-    column.  Chains of CASes that always succeed (AtomicValueState.compareAndSet :123-133), with differences on both
-    sides of the 33-bit boundary (2^32 - 1 and -2^32 fit; 2^32 and -2^32 - 1 escape) and across the i64 wrap, tag
-    changes (Long -> Integer -> null) and expected NULLs, are bit-exact against the oracle -- on the value-only
-    pipeline (k_part_v4 -> k_apply_value_v3) and, with map_capacity > 0, on the extended one (k_part_ext ->
-    k_apply_value_ws, which carries whole operands)."""
+    """Chains of CASes that always succeed (AtomicValueState.compareAndSet :123-133), with differences of every size
+    (0, +-1, both sides of 2^32, the i64 wrap), tag changes (Long -> Integer -> null) and expected NULLs, are bit-exact
+    against the oracle -- on the value-only pipeline (k_part_v4 -> k_apply_value_v3, whose 8-byte records escape to
+    the batch columns for every difference past 14 bits) and, with map_capacity > 0, on the extended one (k_part_ext
+    -> k_apply_value_ws, which carries whole operands)."""
     R, steps = 512, 48
     deltas = [0, 1, -1, (1 << 32) - 1, -(1 << 32), 1 << 32, -(1 << 32) - 1, (1 << 32) + 1, -(1 << 32) + 1,
               (1 << 31), -(1 << 31) - 1, (1 << 63), (1 << 64) - 1, 12345678901234, -(1 << 62), (1 << 46) + 3]
@@ -199,3 +197,50 @@ def test_value_partition_byte_columns_at_any_alignment(offset):
     assert np.array_equal(va.cpu().numpy().view(np.uint64), v1)
     for x, y in zip(E1.value_state(), E2.value_state()):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("map_capacity", [0, 1024])
+def test_value_record_operand_boundaries(map_capacity):
+    """value_path.hip's 8-byte record packs a CAS's expected value as a 32-bit and its update as a 14-bit two's
+    complement difference, and a set / getAndSet value as a 46-bit number; a commit whose operands do not fit escapes
+    (its tile row is kept and the apply reads the a / b columns).  Values and differences on both sides of each
+    boundary (2^31 - 1 / -2^31 fit, 2^31 / -2^31 - 1 escape; 8191 / -8192 fit, 8192 / -8193 escape; 2^45 - 1 / -2^45
+    fit, 2^45 / -2^45 - 1 escape), with Long / Integer / null tags, and failing CASes on each side, are bit-exact
+    against the oracle (AtomicValueState.java get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144)."""
+    R = 256
+    M = 1 << 64
+    exps = [0, 1, -1, (1 << 31) - 1, -(1 << 31), 1 << 31, -(1 << 31) - 1, (1 << 32), 1 << 62, -(1 << 63)]
+    dels = [0, 1, -1, 8191, -8192, 8192, -8193, 1 << 20, -(1 << 40)]
+    sets = [0, 5, -5, (1 << 45) - 1, -(1 << 45), 1 << 45, -(1 << 45) - 1, (1 << 63) - 1, -(1 << 63)]
+    rng = np.random.default_rng(11)
+    L, I, N = abi.CC_TAG_LONG, abi.CC_TAG_INT, abi.CC_TAG_NULL
+    rows = []
+    for k in range(40):
+        for r in range(R):
+            e = exps[(k * 7 + r) % len(exps)]
+            d = dels[(k * 3 + r) % len(dels)]
+            sv = sets[(k + r * 5) % len(sets)]
+            et = L if (k + r) % 9 else I
+            if et == I:
+                e &= 0x7FFFFFFF
+            # set the expected value, then a CAS from it (succeeds), a CAS from a stale value (fails), a get,
+            # a getAndSet to a set value, and a set to null every so often
+            rows.append((r, abi.CC_OP_VALUE_SET, et, e % M, 0))
+            rows.append((r, abi.CC_OP_VALUE_CAS, et | (L << 3), e % M, (e + d) % M))
+            rows.append((r, abi.CC_OP_VALUE_CAS, L | (L << 3), (e + d + 1) % M, (e + 2 * d + 3) % M))
+            rows.append((r, abi.CC_OP_VALUE_GET, 0, 0, 0))
+            rows.append((r, abi.CC_OP_VALUE_GETANDSET, L, sv % M, 0))
+            if (k + r) % 5 == 0:
+                rows.append((r, abi.CC_OP_VALUE_SET, N, int(rng.integers(0, 1 << 62)), 0))
+                rows.append((r, abi.CC_OP_VALUE_CAS, N | (L << 3), int(rng.integers(0, 1 << 62)), d % M))
+    perm = np.arange(len(rows))
+    n = len(rows)
+    arr = np.array(rows, dtype=object)[perm]
+    b = Batch.from_columns(index=np.arange(1, n + 1, dtype=np.uint64), time=np.arange(1, n + 1, dtype=np.uint64),
+                           inst=np.array(arr[:, 0], np.uint32), op=np.array(arr[:, 1], np.uint8),
+                           flags=np.array(arr[:, 2], np.uint8), a=np.array([int(x) for x in arr[:, 3]], np.uint64),
+                           b=np.array([int(x) for x in arr[:, 4]], np.uint64))
+    E, O, gs, gv, os_, ov = _run_both(b, R, R, sub_batch=16384 * 2, map_capacity=map_capacity)
+    _assert_same(E, O, gs, gv, os_, ov, R)
+    cas = b.op == abi.CC_OP_VALUE_CAS
+    assert 0 < int(np.sum(gv[cas] == 1)) < int(np.sum(cas))  # both outcomes occur
