@@ -1488,6 +1488,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       ua.dummy_status = e->d_rst_status + e->sub_batch;
       ua.dummy_value = e->d_rst_value + e->sub_batch;
       ua.v3 = v3;
+      ua.words = reinterpret_cast<const uint64_t*>(e->d_st_ab);
       ua.mark = marker_of(e);
       if (launch_unpermute(ua, st)) return set_err(CC_ERR_HIP, "unpermute launch", hipGetLastError());
       unpermuted = true;

@@ -78,7 +78,7 @@ size_t part_ext_chunk(uint32_t sb, bool maps, bool ids);  // k_part_ext's chunk 
 
 struct ValueArgs {
   const uint32_t* st_meta;
-  const u64x2* st_ab;
+  u64x2* st_ab;  // (value_path.hip: the records, then the packed results over them)
   const uint16_t* ttab;
   uint32_t tiles;
   uint32_t sb;           // total super-buckets (ttab row width - 1)
@@ -641,10 +641,12 @@ struct UnpermuteArgs {
   uint64_t* out_value;
   uint8_t* dummy_status;  // 4 x kPT dummy result rows (after the staging area) for unconditional stores
   uint64_t* dummy_value;
-  bool v3;                // value_path.hip tiles (8192 commits)
+  bool v3;                // value_path.hip tiles (8192 commits): packed result words in `words` (the records' area)
+  const uint64_t* words;
   Marker mark;
 };
 int launch_unpermute(const UnpermuteArgs& a, hipStream_t st);
+int launch_unpermute_v3(const UnpermuteArgs& a, const uint64_t* words, hipStream_t st);
 
 // The bulk compaction view (retained.hip, cc_retained_bitmap): bit (i - first) of bitmap set iff log index i is held
 // by a state machine without clean().

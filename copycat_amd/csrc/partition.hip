@@ -170,11 +170,8 @@ int launch_unpermute(const UnpermuteArgs& a, hipStream_t st) {
   const uint64_t tiles = (n + kTile - 1) / kTile;
   if (tiles == 0) return 0;
   a.mark(K_UNPERMUTE, 1, st);
-  if (a.v3) {  // value_path.hip tiles: two 512-thread workgroups per CU
-    const uint64_t t3 = (n + kV3Tile - 1) / kV3Tile;
-    const uint32_t grid = (uint32_t)(t3 < 2 * kPersistGrid ? t3 : 2 * kPersistGrid);
-    hipLaunchKernelGGL((k_unpermute<512, kV3Tile>), dim3(grid), dim3(512), 0, st, a.cpos, (uint32_t)t3, n, a.rst_status,
-                       a.rst_value, a.out_status + a.lo, a.out_value + a.lo, a.dummy_status, a.dummy_value);
+  if (a.v3) {  // value_path.hip: packed result words over the records (k_unpermute_v3)
+    if (launch_unpermute_v3(a, a.words, st)) return -1;
   } else {
     const uint32_t grid = (uint32_t)(tiles < kPersistGrid ? tiles : kPersistGrid);
     hipLaunchKernelGGL((k_unpermute<kPT, kTile>), dim3(grid), dim3(kPT), 0, st, a.cpos, (uint32_t)tiles, n, a.rst_status,

@@ -111,6 +111,16 @@ __device__ inline void v3_decode(uint64_t r, const uint64_t* __restrict__ ca, co
   }
 }
 
+// ---- the packed result ----------------------------------------------------------------------------------------
+// The apply writes each result over its record: payload (56-bit two's complement) | status (7 bits: code | tag << 4,
+// tags <= 6) << 56 | escaped << 63.  A payload that does not fit (escaped) is written whole to rst_value at the
+// same staging position, where the unpermute reads it.  (9 B per commit in two arrays before: a status byte array
+// whose lines were written in ~32-byte pieces by different workgroups, and the value array.)
+constexpr int kV3ResBits = 56;
+__device__ inline uint64_t v3_pack_result(uint32_t status, uint64_t v, bool esc) {
+  return (esc ? (1ull << 63) : (v & ((1ull << kV3ResBits) - 1))) | ((uint64_t)(status & 0x7Fu) << kV3ResBits);
+}
+
 // ---- k_part_v4: one persistent 1024-thread workgroup per CU, one pass per 8192-commit tile --------------------
 // Same output as the round-3 k_part_v3 (the tile's records grouped by super-bucket in log order, its ttab row and cpos), but
 // the whole tile is ranked at once and placed into a 128 KiB LDS image of the tile's staging region, which is then
@@ -359,12 +369,12 @@ __device__ inline void v3_loader_barrier(uint32_t* ctr, uint32_t target) {
 }
 
 template <int NS>
-__global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(const uint64_t* __restrict__ st_rec,
+__global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(uint64_t* __restrict__ st_rec,
                                                         const uint64_t* __restrict__ ca, const uint64_t* __restrict__ cb,
                                                         uint64_t lo, const uint16_t* __restrict__ ttab, uint32_t tiles,
                                                         uint32_t sb, uint32_t* __restrict__ val_meta,
-                                                        uint64_t* __restrict__ val_v, uint8_t* __restrict__ rst_status,
-                                                        uint64_t* __restrict__ rst_value, uint64_t dummy,
+                                                        uint64_t* __restrict__ val_v, uint64_t* __restrict__ rst_value,
+                                                        uint64_t dummy,
                                                         uint32_t* __restrict__ err_out) {
   using P = V3A<NS>;
 #ifdef CC_DIAG  // diagnostics build only (-DCC_DIAG=1: no walk, 2: contiguous positions -- wrong results by design)
@@ -578,14 +588,17 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
 #undef CC_PLACE1
     WPH(6);
   };
-  // the previous chunk's results (buffer b) back to the records' staging positions; unconditional stores
+  // the previous chunk's results (buffer b) back to the records' staging positions, over the records themselves
+  // (each record is read once, by this workgroup, a chunk earlier): one packed word per result (v3_pack_result),
+  // unconditional stores (rows past the end go to the dummy words); an escaped value also goes to rst_value
   auto store_results = [&](uint32_t b) {
 #define CC_STORE1(J)                                                                \
     {                                                                               \
       const uint64_t gx = gq##J != kNoPos3 ? (uint64_t)gq##J : dummy + t;           \
       const u64x2 r_ = sab[b][qp##J];                                               \
-      rst_status[gx] = (uint8_t)r_.y;                                               \
-      rst_value[gx] = r_.x;                                                         \
+      const bool esc_ = !v3_fits(r_.x, kV3ResBits);                                 \
+      st_rec[gx] = v3_pack_result((uint32_t)r_.y, r_.x, esc_);                      \
+      if (esc_ && gq##J != kNoPos3) rst_value[gx] = r_.x;                            \
     }
     CC_J4(CC_STORE1)
 #undef CC_STORE1
@@ -665,6 +678,95 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(co
   if (err) atomicOr(err_out, err);
 }
 
+// ---- k_unpermute_v3: the packed results back to log order ----------------------------------------------------
+// partition.hip k_unpermute over packed result words: per 8192-commit tile (persistent, two 512-thread workgroups per
+// CU), the tile's staged words are read contiguously into LDS (the next tile's are loaded into registers meanwhile),
+// then each thread writes 4-row groups in log order through cpos: status bytes as one u32, values as two 16-byte
+// stores.  Unknown-session rows (cpos 0xFFFF) get UNKNOWN_SESSION here (ResourceManager.java:60-69).
+constexpr int kU3T = 512;
+template <int NT, int TL>
+__global__ __launch_bounds__(NT) void k_unpermute_v3(const uint16_t* __restrict__ cpos, uint32_t tiles, uint64_t n,
+                                                   const uint64_t* __restrict__ words, const uint64_t* __restrict__ esc_value,
+                                                   uint8_t* __restrict__ out_status, uint64_t* __restrict__ out_value,
+                                                   uint8_t* __restrict__ dummy_status, uint64_t* __restrict__ dummy_value) {
+  constexpr int kUnVal = TL / (2 * NT);  // 16-byte word-pair loads per thread per tile (8)
+  constexpr int kUnPos = TL / (4 * NT);  // 4-commit cpos groups per thread per tile (4)
+  static_assert(kUnVal == 8 && kUnPos == 4, "unpermute prefetch registers");
+  __shared__ uint4 lw2[TL / 2];
+  const uint64_t* lw = reinterpret_cast<const uint64_t*>(lw2);
+  const uint32_t t = threadIdx.x;
+  // prefetch registers as named scalars (an array would live in scratch and make every prefetch wait)
+  uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+  uint2 p0, p1, p2, p3;
+  auto load = [&](uint32_t TT) {
+    const uint64_t i0 = (uint64_t)TT * TL;
+    const uint4* sv = reinterpret_cast<const uint4*>(words + i0) + t;
+    const uint2* sp = reinterpret_cast<const uint2*>(cpos + i0) + t;
+    v0 = sv[0 * NT]; v1 = sv[1 * NT]; v2 = sv[2 * NT]; v3 = sv[3 * NT];
+    v4 = sv[4 * NT]; v5 = sv[5 * NT]; v6 = sv[6 * NT]; v7 = sv[7 * NT];
+    p0 = sp[0 * NT]; p1 = sp[1 * NT]; p2 = sp[2 * NT]; p3 = sp[3 * NT];
+  };
+  uint32_t T = blockIdx.x;
+  load(T < tiles ? T : tiles - 1);
+  const uint8_t unk = CC_STATUS(CC_ST_UNKNOWN_SESSION, CC_TAG_NULL);
+  uint64_t tail_i = ~0ull, tail_v0 = 0, tail_v1 = 0, tail_v2 = 0;
+  uint32_t tail_sw = 0;
+  for (; T < tiles; T += gridDim.x) {
+    lds_barrier();  // the previous tile's scatter is done reading LDS
+    lw2[t + 0 * NT] = v0; lw2[t + 1 * NT] = v1; lw2[t + 2 * NT] = v2; lw2[t + 3 * NT] = v3;
+    lw2[t + 4 * NT] = v4; lw2[t + 5 * NT] = v5; lw2[t + 6 * NT] = v6; lw2[t + 7 * NT] = v7;
+    const uint2 pp[kUnPos] = {p0, p1, p2, p3};
+    lds_barrier();
+    load(T + gridDim.x < tiles ? T + gridDim.x : tiles - 1);
+    const uint64_t i0 = (uint64_t)T * TL;
+#pragma unroll
+    for (int k = 0; k < kUnPos; ++k) {
+      const uint64_t i = i0 + 4 * (uint64_t)(t + k * NT);  // commits i .. i+3
+      const uint32_t p[4] = {pp[k].x & 0xFFFF, pp[k].x >> 16, pp[k].y & 0xFFFF, pp[k].y >> 16};
+      uint32_t sw = 0;
+      uint64_t v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = p[q] != 0xFFFF;
+        const uint64_t wd = ok ? lw[p[q]] : 0;
+        uint64_t x = (uint64_t)(((int64_t)(wd << (64 - kV3ResBits))) >> (64 - kV3ResBits));
+        if (wd >> 63) x = esc_value[i0 + p[q]];  // escaped payload (rare)
+        sw |= (uint32_t)(ok ? (uint32_t)(wd >> kV3ResBits) & 0x7Fu : unk) << (8 * q);
+        v[q] = x;
+      }
+      const bool in = i + 4 <= n;
+      uint32_t* os = in ? reinterpret_cast<uint32_t*>(out_status) + i / 4 : reinterpret_cast<uint32_t*>(dummy_status) + t;
+      u64x2* ov = in ? reinterpret_cast<u64x2*>(out_value) + i / 2 : reinterpret_cast<u64x2*>(dummy_value) + 2 * t;
+      *os = sw;
+      ov[0] = u64x2{v[0], v[1]};
+      ov[1] = u64x2{v[2], v[3]};
+      if (!in && i < n) {  // the straddling group (at most one in the grid): written after the loop
+        tail_sw = sw;
+        tail_v0 = v[0];
+        tail_v1 = v[1];
+        tail_v2 = v[2];
+        tail_i = i;
+      }
+    }
+  }
+  if (tail_i != ~0ull) {  // commits tail_i .. n-1 (1 to 3 of them)
+    const uint64_t vv[3] = {tail_v0, tail_v1, tail_v2};
+    for (int q = 0; q < 3 && tail_i + q < n; ++q) {
+      out_status[tail_i + q] = (uint8_t)(tail_sw >> (8 * q));
+      out_value[tail_i + q] = vv[q];
+    }
+  }
+}
+
+int launch_unpermute_v3(const UnpermuteArgs& a, const uint64_t* words, hipStream_t st) {
+  const uint64_t n = a.hi - a.lo;
+  const uint64_t t3 = (n + kV3Tile - 1) / kV3Tile;
+  const uint32_t grid = (uint32_t)(t3 < 2 * kPersistGrid ? t3 : 2 * kPersistGrid);
+  hipLaunchKernelGGL((k_unpermute_v3<kU3T, kV3Tile>), dim3(grid), dim3(kU3T), 0, st, a.cpos, (uint32_t)t3, n, words,
+                     a.rst_value, a.out_status + a.lo, a.out_value + a.lo, a.dummy_status, a.dummy_value);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Slots per value super-bucket: 256.  (128-slot buckets -- two 512-thread apply workgroups per CU -- measured slower
 // on c2: apply 0.91 -> 0.98, partition 0.88 -> 0.92 ms/step, profiles/r03/ab_ns128: the apply is bound by the loaders'
 // instruction and LDS throughput, not by the latency a second workgroup would hide, and 16-record runs over-fetch.)
@@ -685,8 +787,8 @@ int launch_part_v3(const PartArgs& a, uint32_t tiles, hipStream_t st) {
 int launch_apply_value_v3(const ValueArgs& a, hipStream_t st) {
   if (a.tiles > (uint32_t)kV3MaxTiles) return -1;
   hipLaunchKernelGGL(k_apply_value_v3<256>, dim3(a.sb_val), dim3(V3A<256>::T), 0, st,
-                     reinterpret_cast<const uint64_t*>(a.st_ab), a.ca, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
-                     a.rst_status, a.rst_value, a.dummy, a.err);
+                     reinterpret_cast<uint64_t*>(a.st_ab), a.ca, a.cb, a.lo, a.ttab, a.tiles, a.sb, a.val_meta, a.val_v,
+                     a.rst_value, a.dummy, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

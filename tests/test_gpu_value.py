@@ -206,12 +206,14 @@ def test_value_record_operand_boundaries(map_capacity):
     (its tile row is kept and the apply reads the a / b columns).  Values and differences on both sides of each
     boundary (2^31 - 1 / -2^31 fit, 2^31 / -2^31 - 1 escape; 8191 / -8192 fit, 8192 / -8193 escape; 2^45 - 1 / -2^45
     fit, 2^45 / -2^45 - 1 escape), with Long / Integer / null tags, and failing CASes on each side, are bit-exact
-    against the oracle (AtomicValueState.java get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144)."""
+    against the oracle; so are results on both sides of the packed result word's 56-bit payload (get / getAndSet of
+    2^55 - 1 / -2^55, packed, and 2^55 / -2^55 - 1, escaped to the value array) (AtomicValueState.java get :77-83, set :114-118, compareAndSet :123-133, getAndSet :138-144)."""
     R = 256
     M = 1 << 64
     exps = [0, 1, -1, (1 << 31) - 1, -(1 << 31), 1 << 31, -(1 << 31) - 1, (1 << 32), 1 << 62, -(1 << 63)]
     dels = [0, 1, -1, 8191, -8192, 8192, -8193, 1 << 20, -(1 << 40)]
-    sets = [0, 5, -5, (1 << 45) - 1, -(1 << 45), 1 << 45, -(1 << 45) - 1, (1 << 63) - 1, -(1 << 63)]
+    sets = [0, 5, -5, (1 << 45) - 1, -(1 << 45), 1 << 45, -(1 << 45) - 1, (1 << 63) - 1, -(1 << 63),
+            (1 << 55) - 1, -(1 << 55), 1 << 55, -(1 << 55) - 1]
     rng = np.random.default_rng(11)
     L, I, N = abi.CC_TAG_LONG, abi.CC_TAG_INT, abi.CC_TAG_NULL
     rows = []
