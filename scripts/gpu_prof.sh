@@ -8,36 +8,39 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-BA="--no-cpu-baseline --no-parity --no-e2e $@"
+BA="--no-cpu-baseline --no-parity --no-e2e --no-c3 --window-markers $@"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/kt -o run --output-format csv -- python3 $R/bench.py $BA > $R/$OUT/kt.log 2>&1 || { echo kt failed; tail -3 $R/$OUT/kt.log; exit 1; }
 tail -1 $R/$OUT/kt.log | cut -c1-300
 STATS=$(find $R/$OUT/kt -name "*kernel_stats.csv" | head -1)
 cp $STATS $R/$OUT/kernel_stats.csv
-# per-kernel averages over the timed steps only: the last steps/(warmup+steps) of each kernel's launches in start
-# order (the warm-up step's launches -- fresh tables, first-touch binding -- run slower and are in kernel_stats too)
+# per-kernel averages over the timed steps only: the kernels that start between the bench's two window markers
+# (bench.py --window-markers: a spin_kernel right before the first timed step and right after the closing sync), so
+# neither the warm-up steps nor set-up launches (fills, creation) are charged to a step
 TRACE=$(find $R/$OUT/kt -name "*kernel_trace.csv" | head -1)
 python3 - "$TRACE" "$@" > $R/$OUT/kt_timed.txt <<'PY'
 import csv, sys, collections
 trace, args = sys.argv[1], sys.argv[2:]
 def arg(name, dflt):
     return int(args[args.index(name) + 1]) if name in args else dflt
-steps, warm = arg("--steps", 1), arg("--warmup", 1)
+steps = arg("--steps", 1)
+rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(trace))]
+marks = sorted(s for s, e, n in rows if "spin_kernel" in n)
+assert len(marks) >= 2, "no timed-window markers in the trace (bench.py --window-markers)"
+w0, w1 = marks[0], marks[-1]
 ev = collections.defaultdict(list)
-for r in csv.DictReader(open(trace)):
-    n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("cc::", "")
-    ev[n].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-print(f"timed steps {steps} of {warm + steps}: per kernel, the last {steps}/{warm + steps} of its launches")
+for s, e, n in rows:
+    if w0 < s < w1 and "spin_kernel" not in n:
+        n = n.split("(")[0].replace("void ", "").replace("cc::", "")
+        ev[n].append(e - s)
+tot = sum(sum(v) for v in ev.values())
+print(f"timed window {(w1 - w0) / 1e6:.3f} ms over {steps} steps ({(w1 - w0) / 1e6 / steps:.3f} ms/step between the "
+      f"markers); kernels in it {tot / 1e6 / steps:.3f} ms/step")
 print(f"{'kernel':44s} {'calls':>6s} {'avg_us':>10s} {'ms/step':>10s}")
-for n, v in sorted(ev.items(), key=lambda kv: -sum(d for _, d in kv[1])):
-    v.sort()
-    k = len(v) * steps // (warm + steps)
-    if k == 0:
-        continue
-    tail = [d for _, d in v[len(v) - k:]]
-    print(f"{n[:44]:44s} {k:6d} {sum(tail) / k / 1e3:10.1f} {sum(tail) / steps / 1e6:10.3f}")
+for n, v in sorted(ev.items(), key=lambda kv: -sum(kv[1])):
+    print(f"{n[:44]:44s} {len(v):6d} {sum(v) / len(v) / 1e3:10.1f} {sum(v) / steps / 1e6:10.3f}")
 PY
-# idle gaps of the timed steps: the union of all kernels' intervals after the warm-up share of launches, and the
+# idle gaps of the timed steps: the union of all kernels' intervals between the window markers, and the
 # largest gaps with the kernels on either side (host round trips show up here)
 python3 - "$TRACE" "$@" > $R/$OUT/kt_gaps.txt <<'PY'
 import csv, sys
@@ -49,9 +52,8 @@ ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"
             for r in csv.DictReader(open(trace)))
 if not ev:
     sys.exit()
-k0 = [i for i, e in enumerate(ev) if e[2].startswith("k_part")]
-start = ev[k0[len(k0) * warm // (warm + steps)]][0] if k0 else ev[0][0]
-ev = [e for e in ev if e[0] >= start]
+marks = [e[0] for e in ev if "spin_kernel" in e[2]]
+ev = [e for e in ev if marks[0] < e[0] < marks[-1] and "spin_kernel" not in e[2]] if len(marks) >= 2 else ev
 busy, gaps = 0, []
 cs, ce, last = ev[0][0], ev[0][1], ev[0][2]
 for s, e, n in ev[1:]:
