@@ -309,7 +309,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         } else if (timeout == 0) {
           ev(r.inst, CC_EV_LOCK, CC_TAG_BOOL, 0);
         } else if (h.n == E.cap) {
-          err |= kErrCapacity;
+          err |= kErrCoordFull;
         } else {
           E.put((h.head + h.n) & (E.cap - 1), CoordEnt{timeout > 0 ? clk + (uint64_t)timeout : kNoDeadline, r.idx, r.inst, 0});
           ++h.n;
@@ -364,7 +364,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         ev(r.inst, CC_EV_ELECT, CC_TAG_LONG, r.idx);
       }
       if (listen && held && !found) {
-        if (h.n == E.cap) err |= kErrCapacity;
+        if (h.n == E.cap) err |= kErrCoordFull;
         else E.put(h.n++, CoordEnt{r.iid, r.idx, r.inst, 0});
       }
       // the leader unlistens: the next listener (entry 0) leads; a listener unlistens: its entry goes
@@ -421,7 +421,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
       const bool join = r.op == CC_OP_GROUP_JOIN, leave = r.op == CC_OP_GROUP_LEAVE;
       const bool full = h.n == E.cap;
       const bool ins = join && !hit && !full, rem = leave && hit;
-      if (join && !hit && full) err |= kErrCapacity;
+      if (join && !hit && full) err |= kErrCoordFull;
       if (join && hit) {  // previous.clean(): the member's commit is replaced
         CoordEnt e = E.get(p);
         e.idx = r.idx;
@@ -496,7 +496,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
         case CC_OP_QUEUE_ADD:    // add :51-59
         case CC_OP_QUEUE_OFFER:  // offer :64-72 — both answer false
           if (h.n == E.cap) {
-            err |= kErrCapacity;
+            err |= kErrCoordFull;
           } else {
             set_at(h.n, CoordEnt{pa, r.idx, r.inst, ta});
             ++h.n;
@@ -586,7 +586,7 @@ __device__ inline uint32_t coord_apply(uint32_t type_rt, uint32_t slot, const Re
             }
           }
           if (!found) {
-            if (h.n == E.cap) err |= kErrCapacity;
+            if (h.n == E.cap) err |= kErrCoordFull;
             else E.put(h.n++, CoordEnt{0, r.idx, r.inst, 0});
           }
           break;

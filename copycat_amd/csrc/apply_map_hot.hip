@@ -582,9 +582,10 @@ __global__ __launch_bounds__(kHT) void k_hot_apply(const MRec* __restrict__ xr, 
   for (uint32_t item = blockIdx.x; item < pfx[nh]; item += gridDim.x) {
     const uint32_t h = hot_item_key(pfx, nh, item);
     const uint32_t slot = hot[h].ident & kMwSlotMask;
-    // The map's flags are read once, by thread 0, for the whole workgroup: the previous sub-batch's small-map replay
-    // (map_small.hip, on the side stream) may clear kMfSmall while this kernel runs, and threads that read the byte
-    // at different times took different branches around the barriers of the event reservation below.
+    // The map's flags are read once, by thread 0, for the whole workgroup (every branch around the event
+    // reservation's barriers below is item-uniform).  They do not change while this kernel runs: d_msmall is written
+    // on the engine stream only (common.h, the small-map window invariant; a replay on the side stream marks its own
+    // buffer, folded in after the engine stream waited for it).
     const uint32_t f0 = t == 0 ? (hot_events(hc, slot) ? 1u : 0u) | (hot_cleared(hc, slot) ? 2u : 0u) : 0u;
     hot_runs_lds(hot_rpre, hot_rstart, h, tiles, lrpre, lrst, &iflag, f0);
     const uint32_t p = item - pfx[h], L = hot_len[h], P = pfx[h + 1] - pfx[h];

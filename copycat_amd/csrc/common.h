@@ -326,6 +326,8 @@ constexpr uint32_t kErrTime = 8u;  // the time column decreased inside a batch
 constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration order is undetermined (map_wide.hip)
 constexpr uint32_t kErrMapSize = 32u;   // a map's tracked size differs from its table at a barrier (internal check)
 constexpr uint32_t kErrHandleHash = 64u;  // a HANDLE map key whose String.hashCode was never registered (cc_handle_hashes)
+constexpr uint32_t kErrSmallFlag = 256u;
+constexpr uint32_t kErrCoordFull = 512u;  // a coordination collection (lock queue, listeners, members, queue) is full  // (CC_DIAG builds) a map in the small-map window without its snapshot flag
 constexpr uint32_t kErrCvKey = 128u;     // in-stream containsValue: a fingerprint collision or a 2^40-index span (map_cv.hip)
 
 // java.util.HashMap placement of a map key: hash(key) = h ^ (h >>> 16), h = key.hashCode() -- Long (int)(v ^ v >>> 32),
@@ -452,7 +454,8 @@ constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin since the last c
 constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (kept for the snapshot format; never set now)
 constexpr uint32_t kSmAmbig = 8u;    // a tree order the engine cannot know (two String keys with one hash in a tree bin;
                                      // a removal of a key the model does not hold): an order-dependent answer refuses
-// per-map flags of the batch (cc_engine::d_msmall): bit 0 the table is small (events followed key by key), bit 1 the
+// per-map flags of the batch (cc_engine::d_msmall), written on the engine stream only: bit 0 the table is small (events
+// followed key by key; a SNAPSHOT of the small-map models' kSmIn, see below), bit 1 the
 // batch asks the map's size / isEmpty (events followed for the in-stream answers); either makes every insertion /
 // removal of the map an event (region commits: k_msize_count; hot-key commits: k_hot_apply)
 constexpr uint8_t kMfSmall = 1u, kMfSize = 2u;
@@ -461,6 +464,15 @@ constexpr uint8_t kMfCv = 4u;
 // bit 3: the sub-batch clears the map in the stream (map_clear.hip): its sizes come from event replay and its commits
 // carry their clear epoch (region and hot-key commits alike)
 constexpr uint8_t kMfClr = 8u;
+// The small-map window invariant (race-free by construction, engine_state.h SmSet): a map's kSmIn (its model, written
+// by k_small_replay) and its kMfSmall snapshot only go 1 -> 0 inside a batch (a table only grows past 64; they go to
+// 1 only at resource creation / snapshot restore, between batches, with no replay pending).  The replay, which may
+// run on the side stream beside the next sub-batch, never writes d_msmall: it marks a map that left the window in its
+// own buffer (cc_engine::d_msm_left, one per event-buffer set), and k_small_fold clears kMfSmall from those marks on
+// the engine stream once that stream has waited for the replay.  So no kernel of a sub-batch reads a byte another
+// stream writes meanwhile; the snapshot may lag the models by one sub-batch (a map that left still emits its events
+// for one more sub-batch, and the replay skips them: its model says it left).  Engine-stream kernels read the
+// snapshot, never a model's kSmIn, while a replay may be pending (k_small_chains, ChainKeep).
 // the flag bytes are set by concurrent threads of one kernel: OR through the aligned word (the array is padded to it)
 __device__ inline void mflag_or(uint8_t* mflag, uint32_t m, uint8_t bit) {
   atomicOr(reinterpret_cast<uint32_t*>(mflag + (m & ~3u)), (uint32_t)bit << (8 * (m & 3u)));

@@ -97,7 +97,7 @@ static void free_all(cc_engine* e) {
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,    e->d_mw_cgen, e->d_cset, e->d_cset_full, e->d_tbl_claim, e->d_lvl_at, e->d_half_count,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
-                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,
+                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,  e->d_msm_left,
                   e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp, e->d_sm_pay,
                   e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb,
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
@@ -149,7 +149,16 @@ static int ensure_leak(cc_engine* e, uint64_t need) {
 static uint64_t small_cap_needed(const cc_engine* e) {
   return e->ttl_live ? 2 * e->sub_batch + e->map_entries : e->sub_batch;
 }
+static int launch_pending_replay(cc_engine* e, hipStream_t st);
+static int wait_replay(cc_engine* e, int k, hipStream_t st);
 static void free_sm_alt(cc_engine* e) {
+  // (inside a batch: a replay not yet launched runs now, and every replay's exit marks fold into the snapshot on the
+  // engine stream -- e->last_stream -- before the buffers go)
+  if (e->last_stream) {
+    (void)launch_pending_replay(e, e->last_stream);
+    for (int k = 0; k < 2; ++k) (void)wait_replay(e, k, e->last_stream);
+    (void)hipStreamSynchronize(e->last_stream);
+  }
   if (e->side_st) (void)hipStreamSynchronize(e->side_st);
   e->rep_pending[0] = e->rep_pending[1] = false;
   void* alt[] = {e->sm_alt.key, e->sm_alt.key2, e->sm_alt.val, e->sm_alt.val2, e->sm_alt.pay, e->sm_alt.cseg};
@@ -214,17 +223,26 @@ static int launch_pending_replay(cc_engine* e, hipStream_t st) {
   e->rep_pending[e->pend_set] = true;
   return CC_OK;
 }
+// the engine stream waits for the side-stream replay of event-buffer set k, then folds its exit marks into the
+// d_msmall snapshot (common.h, the small-map window invariant: the only place a replay's result reaches the flags)
+static int wait_replay(cc_engine* e, int k, hipStream_t st) {
+  if (!e->rep_pending[k]) return CC_OK;
+  HIPCHECK(hipStreamWaitEvent(st, e->ev_rep[k], 0));
+  e->rep_pending[k] = false;
+  if (launch_small_fold(e->d_msm_left + (size_t)k * e->cfg.max_resources, e->d_msmall, e->cfg.max_resources, st))
+    return set_err(CC_ERR_HIP, "small-map fold launch", hipGetLastError());
+  return CC_OK;
+}
 // the engine stream waits for the side stream's replays (before barrier rows, timers, and the batch's end)
 static int join_replay(cc_engine* e, hipStream_t st) {
   {
     int rc = launch_pending_replay(e, st);
     if (rc) return rc;
   }
-  for (int k = 0; k < 2; ++k)
-    if (e->rep_pending[k]) {
-      HIPCHECK(hipStreamWaitEvent(st, e->ev_rep[k], 0));
-      e->rep_pending[k] = false;
-    }
+  for (int k = 0; k < 2; ++k) {
+    int rc = wait_replay(e, k, st);
+    if (rc) return rc;
+  }
   return CC_OK;
 }
 
@@ -477,6 +495,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
     ALLOC(e->d_msmall, (cfg->max_resources + 3) & ~3u);  // (padded to whole words: common.h mflag_or)
+    ALLOC(e->d_msm_left, 3ull * cfg->max_resources);
     ALLOC(e->d_sm_ctl, sizeof(uint32_t) * 4);
     ALLOC(e->d_rst_msz, sizeof(uint32_t) * (e->sub_batch + 4 * kPT));
     ALLOC(e->d_hot_msz, sizeof(uint32_t) * (kHotMaxPieces + kHotMax) * (kHotPiece / 16));
@@ -543,6 +562,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_mpcap, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msm, 0, sizeof(SmallMap) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msmall, 0, cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_msm_left, 0, 3ull * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_sm_ctl, 0, sizeof(uint32_t) * 4)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_tbl_dl, 0, sizeof(uint64_t) * e->map_entries)) != hipSuccess) return fail("memset", he);
   }
@@ -586,6 +606,7 @@ extern "C" void* cc_engine_stream(cc_engine* e) { return e ? (void*)e->own_strea
 static int check_device_err(cc_engine* e) {
   uint32_t err = 0;
   HIPCHECK(hipMemcpy(&err, e->d_err, sizeof err, hipMemcpyDeviceToHost));
+  e->last_err_bits = err;  // (cc_apply_batch_host_prefix tells a full coordination collection from other failures)
   if (err) {
     HIPCHECK(hipMemset(e->d_err, 0, sizeof(uint32_t)));
     if (err & kErrTime) return set_err(CC_ERR_INVALID, "the time column must be non-decreasing within a batch");
@@ -597,12 +618,17 @@ static int check_device_err(cc_engine* e) {
     if (err & kErrCvKey)
       return set_err(CC_ERR_STATE, "in-stream containsValue: two operands share a 64-bit fingerprint, or a sub-batch "
                                    "spans more than 2^40 log indices");
+    if (err & kErrSmallFlag)
+      return set_err(CC_ERR_STATE, "internal check (CC_DIAG): a map in the small-map window without its snapshot flag");
     if (err & kErrHandleHash)
       return set_err(CC_ERR_STATE, "a HANDLE map key's String.hashCode is not registered (cc_handle_hashes), or a "
                                    "sub-batch spans more than 2^32 log indices");
     if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
     if (err & kErrCapacity)
-      return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, lock queue, listeners, members)");
+      return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, leak log, event buffer)");
+    if (err & kErrCoordFull)
+      return set_err(CC_ERR_CAPACITY, "a coordination collection is full (coord_cap: lock queue, listeners, members, "
+                                      "queue elements)");
     if (err & kErrUnsupported)
       return set_err(CC_ERR_UNSUPPORTED,
                      "batch contained an op this build does not apply on the GPU (AtomicValue Listen/Unlisten without "
@@ -919,6 +945,8 @@ static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = null
   sa.nseg = e->d_sm_seg + e->cfg.max_resources;
   sa.state = e->d_msm;
   sa.msmall = e->d_msmall;
+  sa.left = e->d_msm_left + 2ull * e->cfg.max_resources;  // (an engine-stream replay: folded right after it)
+  sa.err = e->d_err;
   sa.mpcap = e->d_mpcap;
   sa.max_resources = e->cfg.max_resources;
   sa.msize = e->d_msize;
@@ -1290,10 +1318,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       std::swap(e->d_sm_pay, e->sm_alt.pay);
       std::swap(e->d_sm_cseg, e->sm_alt.cseg);
       e->sm_cur ^= 1;
-      if (e->rep_pending[e->sm_cur]) {
-        HIPCHECK(hipStreamWaitEvent(st, e->ev_rep[e->sm_cur], 0));
-        e->rep_pending[e->sm_cur] = false;
-      }
+      int rc = wait_replay(e, e->sm_cur, st);  // (its replay's exit marks fold into the snapshot here)
+      if (rc) return rc;
     }
     for (const auto& hv : e->clr_heavy) {  // at most 127 in-stream clears of one map per sub-batch (map_clear.hip)
       const size_t q = (size_t)(std::lower_bound(hv.begin(), hv.end(), (uint32_t)lo) - hv.begin());
@@ -1779,6 +1805,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.cseg = e->d_sm_cseg;
           sa.state = e->d_msm;
           sa.msmall = e->d_msmall;
+          sa.left = e->d_msm_left + 2ull * e->cfg.max_resources;  // (on this stream: folded right after it)
+          sa.err = e->d_err;
           sa.mpcap = e->d_mpcap;
           sa.max_resources = e->cfg.max_resources;
           sa.lvl_at = e->d_lvl_at;
@@ -1790,6 +1818,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
             int rc = ensure_sm_alt(e);
             if (rc) return rc;
             sa.defer = true;
+            sa.left = e->d_msm_left + (size_t)e->sm_cur * e->cfg.max_resources;  // (folded by wait_replay)
           }
           const int rs = launch_small_replay(sa, ctl[0], st, st);
           if (sa.defer && !rs) {
@@ -2946,6 +2975,8 @@ extern "C" int cc_snapshot_restore(cc_engine* e, const void* h_buf, uint64_t siz
   if (e->has_mmaps && (rc = ensure_leak(e, kLeakCap))) return rc;
   e->sessions = std::move(sessions);
   e->small_live = e->map_bits && !e->ttl_live;  // (the next sub-batch recounts the maps still small)
+  if (e->map_bits)  // (no replay is pending here: the restored snapshot flags start with no exit marks)
+    HIPCHECK(hipMemset(e->d_msm_left, 0, 3ull * e->cfg.max_resources));
   if (e->small_live) {  // (ctl[1] nonzero until that recount: see resource creation)
     const uint32_t pending[2] = {0, 1};
     HIPCHECK(hipMemcpy(e->d_sm_ctl, pending, sizeof pending, hipMemcpyHostToDevice));

@@ -204,7 +204,10 @@ struct SmallArgs {
   uint8_t* out_status;         // TTL mode: the size / isEmpty rows among the events are answered here (else null)
   uint64_t* out_value;
   SmallMap* state;             // [max_resources]
-  uint8_t* msmall;
+  uint8_t* msmall;             // the engine stream's snapshot of the window (common.h): read, never written, by the replay
+  uint8_t* left;               // [max_resources] the replay's exit marks (one buffer per event-buffer set), folded by
+                               // launch_small_fold on the engine stream after it waited for the replay
+  uint32_t* err;
   uint32_t* mpcap;
   uint32_t max_resources;
   uint32_t* msize;             // TTL mode: every map's size / capacity from its events (k_ttl_replay); else null
@@ -250,6 +253,7 @@ struct SizeArgs {
 int launch_size_emit(const SizeArgs& a, hipStream_t st);
 int launch_size_answer(const SizeArgs& a, hipStream_t st);
 int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st);
+int launch_small_fold(uint8_t* left, uint8_t* msmall, uint32_t R, hipStream_t st);
 size_t small_sort_temp_bytes(uint32_t cap);
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, uint64_t* cgen, hipStream_t st);

@@ -185,6 +185,8 @@ struct cc_engine {
   // maps whose HashMap table is still small (capacity <= 64): early resizes and tree bins (map_small.hip)
   SmallMap* d_msm = nullptr;       // [max_resources]
   uint8_t* d_msmall = nullptr;     // [max_resources] 1: in the window
+  uint8_t* d_msm_left = nullptr;   // [3][max_resources] maps a replay saw leave the window: sets 0 / 1 (side-stream
+                                   // replays), 2 (engine-stream replays); folded into d_msmall on the engine stream
   uint32_t* d_sm_ctl = nullptr;    // [4] events of the sub-batch, maps still in the window
   uint64_t *d_sm_key = nullptr, *d_sm_key2 = nullptr;  // [sm_cap] map events (small / size-queried maps; TTL mode: all)
   uint32_t *d_sm_val = nullptr, *d_sm_val2 = nullptr;
@@ -194,7 +196,11 @@ struct cc_engine {
   // Outside TTL mode the small-map replay of sub-batch i runs on a side stream while sub-batch i + 1 runs on the
   // engine's: the event buffers alternate between two sets (swapped at each sub-batch start), a set is reused only
   // after its replay finished (ev_rep), and the engine stream waits for the side stream before barrier rows, timers
-  // and the batch's end (join_replay).
+  // and the batch's end (join_replay).  Race-free by construction (common.h, the small-map window invariant): the
+  // replay writes only its models (d_msm, read by no engine-stream kernel while it may run), its set's exit marks
+  // (d_msm_left) and, atomically, the capacity levels (mpcap, lvl_at: atomic max / min on both streams, and the one
+  // engine-stream reader of mpcap inside a sub-batch, k_msize_scan, loads it atomically); every wait for a replay
+  // (wait_replay) is followed on the engine stream by the fold of its marks into the d_msmall snapshot.
   struct SmSet {
     uint64_t *key = nullptr, *key2 = nullptr;
     uint32_t *val = nullptr, *val2 = nullptr;
@@ -318,6 +324,7 @@ struct cc_engine {
   std::map<uint32_t, std::vector<uint64_t>> leaks;  // ordered: snapshots are byte-deterministic
   uint64_t applied = 0;
   bool applied_pending = false;
+  uint32_t last_err_bits = 0;  // the device error bits the last check_device_err read (common.h kErr*)
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
   // device staging of the host-memory entry points (host_path.hip): grown on demand, kept between calls
   void* hw_buf[24] = {};

@@ -175,12 +175,18 @@ extern "C" int cc_apply_batch_host_events(cc_engine* e, const cc_batch* h_cols, 
 // it are not applied (their results are not written), so the host can act (a larger engine from a snapshot, or the
 // commit failed) and resume at that row.
 //   1. Rows that can add an entry (lock with a timeout != 0, election listen, group join, value listen, queue
-//      add / offer) are counted per resource on the host (the registry mirror); a resource whose current entries
-//      plus those rows fit its block cannot overflow, and if every one fits the batch is applied as one call.
-//   2. Otherwise the rows before the first one that could overflow (running count > room) go as one call, and that
-//      row alone: if it overflows, its resource block, the clock, the applied index and the pending group timers
-//      are restored (the engine skips the entry it cannot hold, so nothing else moved) and the call stops there.
-// Other fixed capacities (a full map table region, max_events) still fail the call after applying it.
+//      add / offer) are the only ones that can overflow.  Every resource they address starts with its block's entry
+//      count (one strided copy of the block headers), and one pass over the batch keeps an upper bound per resource
+//      (+1 per adding row; removals are not counted, so it never falls short).  The rows before the first adding
+//      row whose bound would pass coord_cap go as one call.
+//   2. At that row the resource's count is read again (after the rows before it: the bound's slack is gone); if the
+//      row fits, the pass goes on.  Else the row goes alone: if the device reports a full collection (kErrCoordFull,
+//      and nothing else), its resource block, the clock, the applied index and the pending group timers are restored
+//      (the engine skips the entry it cannot hold, so nothing else moved) and the call stops there; if it applied
+//      (the op did not add after all), the count is read once more and the pass goes on.
+// Each row is scanned once, and a stop costs one header read: a queue that stays near coord_cap under churn costs a
+// call per stop, not a rescan of the batch.  Other fixed capacities (a full map table region, max_events) still fail
+// the call after applying it.
 namespace {
 
 bool adds_entry(uint8_t type, uint8_t op, uint64_t aux) {
@@ -229,6 +235,12 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
     if (hev) *hev->count = ev_n;
     return rc;
   };
+  if (!e->coord_on) {  // no coordination collection to overflow: one call
+    const int rc = n ? apply_part(e, h, 0, n, hout, hev, &ev_n) : CC_OK;
+    if (!rc) *h_applied = n;
+    return finish(rc);
+  }
+  HIPCHECK(hipSetDevice(e->device));
   const uint32_t max_inst = e->cfg.max_instances;
   auto res_of = [&](uint64_t i) -> uint32_t {
     const uint32_t in = h->inst[i];
@@ -239,48 +251,63 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
   auto adds = [&](uint64_t i, uint32_t r) {
     return r != kNoRes && r < e->res_type.size() && adds_entry(e->res_type[r], h->op[i], h->aux ? h->aux[i] : 0);
   };
-  auto entries = [&](uint32_t r, uint32_t* out) -> int {  // the block's current entry count (CoordHdr.n)
+  auto entries = [&](uint32_t r, uint32_t* out) -> int {  // one block's current entry count (CoordHdr.n)
     CoordHdr hd{};
     HIPCHECK(hipMemcpy(&hd, e->d_coord + (uint64_t)r * blk, sizeof hd, hipMemcpyDeviceToHost));
     *out = hd.n;
     return CC_OK;
   };
-  uint64_t pos = 0;
-  while (pos < n) {
-    // the first row at or after pos that could overflow its resource's block (none: the rest applies as one call)
-    uint64_t stop = n;
-    if (e->coord_on) {
-      std::unordered_map<uint32_t, uint64_t> cnt;
-      for (uint64_t i = pos; i < n; ++i) {
+  // the upper bound of every addressed resource's entry count, from one strided copy of the block headers over the
+  // slot range the adding rows address
+  std::unordered_map<uint32_t, uint64_t> bound;
+  {
+    uint32_t rlo = ~0u, rhi = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint32_t r = res_of(i);
+      if (adds(i, r)) rlo = std::min(rlo, r), rhi = std::max(rhi, r);
+    }
+    if (rlo <= rhi) {
+      std::vector<CoordHdr> hdr(rhi - rlo + 1);
+      HIPCHECK(hipMemcpy2D(hdr.data(), sizeof(CoordHdr), e->d_coord + (uint64_t)rlo * blk, blk, sizeof(CoordHdr),
+                           hdr.size(), hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < n; ++i) {
         const uint32_t r = res_of(i);
-        if (adds(i, r)) ++cnt[r];
+        if (adds(i, r) && !bound.count(r)) bound[r] = hdr[r - rlo].n;
       }
-      std::unordered_map<uint32_t, int64_t> room;  // resources that may overflow: entries they can still take
-      for (auto& kv : cnt) {
-        uint32_t cur = 0;
-        int rc = entries(kv.first, &cur);
-        if (rc) return finish(rc);
-        if (cur + kv.second > cap) room[kv.first] = (int64_t)cap - (int64_t)cur;
+    }
+  }
+  uint64_t pos = 0, i = 0;  // rows [0, pos) applied; rows [pos, i) scanned (their adds are in the bounds)
+  while (pos < n) {
+    uint64_t stop = n;  // the first row whose bound would pass coord_cap
+    for (; i < n; ++i) {
+      const uint32_t r = res_of(i);
+      if (!adds(i, r)) continue;
+      uint64_t& b = bound[r];
+      if (b + 1 > cap) {
+        stop = i;
+        break;
       }
-      if (!room.empty())
-        for (uint64_t i = pos; i < n; ++i) {
-          const uint32_t r = res_of(i);
-          auto it = room.find(r);
-          if (it != room.end() && adds(i, r) && --it->second < 0) {
-            stop = i;
-            break;
-          }
-        }
+      ++b;
     }
     if (stop > pos) {
       const int rc = apply_part(e, h, pos, stop, hout, hev, &ev_n);
       if (rc) return finish(rc);
       pos = stop;
       *h_applied = pos;
+      if (pos == n) break;
+    }
+    // row pos (= stop) may overflow: its resource's count now (rows before it applied)
+    const uint32_t r = res_of(pos);
+    uint32_t cur = 0;
+    {
+      int rc = entries(r, &cur);
+      if (rc) return finish(rc);
+    }
+    if ((uint64_t)cur + 1 <= cap) {  // it fits: the pass goes on from this row with the exact count
+      bound[r] = cur;
       continue;
     }
-    // row `pos` alone: its resource's block, the clock, the applied index and the group timers are saved first
-    const uint32_t r = res_of(pos);
+    // row pos alone: its resource's block, the clock, the applied index and the group timers are saved first
     std::vector<uint8_t> saved(blk);
     uint64_t clock = 0, last = 0;
     HIPCHECK(hipMemcpy(saved.data(), e->d_coord + (uint64_t)r * blk, blk, hipMemcpyDeviceToHost));
@@ -293,7 +320,8 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
     const uint8_t st0 = hout->status[pos];
     const uint64_t va0 = hout->value[pos];
     const int rc = apply_part(e, h, pos, pos + 1, hout, hev, &ev_n);
-    if (rc == CC_ERR_CAPACITY) {
+    // (only a full coordination collection, and nothing else, is rolled back: any other failure is returned as is)
+    if (rc == CC_ERR_CAPACITY && e->last_err_bits == kErrCoordFull) {
       hout->status[pos] = st0;  // (the row is not applied: its result row keeps what the caller had there)
       hout->value[pos] = va0;
       HIPCHECK(hipMemcpy(e->d_coord + (uint64_t)r * blk, saved.data(), blk, hipMemcpyHostToDevice));
@@ -307,7 +335,13 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
     }
     if (rc) return finish(rc);
     pos += 1;
+    i = pos;
     *h_applied = pos;
+    {
+      int rc2 = entries(r, &cur);
+      if (rc2) return finish(rc2);
+    }
+    bound[r] = cur;
   }
   return finish(CC_OK);
 }

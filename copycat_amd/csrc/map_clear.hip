@@ -89,7 +89,7 @@ __global__ void k_clr_sub(const uint64_t* __restrict__ keys, const uint32_t* __r
     if (ph - pl > 127u) atomicOr(err, kErrCapacity);  // (the host cuts sub-batches so that this never holds)
     eend[m] = (uint8_t)min(ph - pl, 127u);
     // kMfClr marks the maps cleared in THIS sub-batch: the others keep the exact size tracking (atomic on the flag
-    // word: an overlapped small-map replay may update the map's kMfSmall meanwhile)
+    // word: neighbouring maps' bytes share it; only the engine stream writes the flags, common.h)
     const uint8_t f = mflag[m];
     if (ph > pl && !(f & kMfClr)) mflag_or(mflag, m, kMfClr);
     else if (ph == pl && (f & kMfClr)) mflag_and(mflag, m, (uint8_t)~kMfClr);

@@ -81,13 +81,15 @@ size_t chain_scan_temp_bytes(uint32_t cap) {
 }
 __global__ __launch_bounds__(256) void k_small_chains(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
                                                       EvPay* __restrict__ pay, const uint32_t* __restrict__ start, uint32_t E,
-                                                      const SmallMap* __restrict__ st) {
+                                                      const uint8_t* __restrict__ msmall) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < E; i += gridDim.x * blockDim.x) {
     const uint32_t s0 = start[i];
     if (s0 == i) continue;                               // (a chain of one event)
     if (i + 1 < E && start[i + 1] != i + 1) continue;    // not the chain's end
     const uint64_t k = key[i];
-    if (!(st[k >> kEvMapShift].flags & kSmIn)) continue;          // (out of the window: not replayed)
+    // (out of the window: not replayed.  The snapshot, not the model's kSmIn: an earlier sub-batch's replay may be
+    // writing the model meanwhile; a map the snapshot still shows in the window is skipped by the replay itself)
+    if (!(msmall[k >> kEvMapShift] & kMfSmall)) continue;
     const uint32_t r0 = (key[s0] & 3u) == 1u ? s0 + 1 : s0;  // the chain's first removal
     if (i <= r0) continue;
     const uint32_t skip = (k & 3u) == 1u ? i - r0 - 1 : i - r0;
@@ -101,11 +103,11 @@ __global__ __launch_bounds__(256) void k_small_chains(const uint64_t* __restrict
 struct ChainKeep {
   const uint64_t* key;
   const uint32_t* start;
-  const SmallMap* st;
+  const uint8_t* msmall;  // the engine stream's snapshot (common.h, the small-map window invariant)
   uint32_t E;
   __device__ uint8_t operator()(uint32_t i) const {
     const uint64_t k = key[i];
-    if (!(st[k >> kEvMapShift].flags & kSmIn)) return 0;  // (not replayed)
+    if (!(msmall[k >> kEvMapShift] & kMfSmall)) return 0;  // (not replayed)
     const uint32_t s0 = start[i];
     if (s0 == i) return 1;
     const uint32_t r0 = (key[s0] & 3u) == 1u ? s0 + 1 : s0;
@@ -155,17 +157,25 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
                                                               const EvPay* __restrict__ pay, const uint32_t* __restrict__ orig,
                                                               const uint32_t* __restrict__ ctl,
                                                               const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
-                                                              SmallMap* __restrict__ st, uint8_t* __restrict__ msmall,
+                                                              SmallMap* __restrict__ st, uint8_t* __restrict__ left,
+                                                              const uint8_t* __restrict__ msmall,
                                                               uint32_t* __restrict__ mpcap, unsigned long long* __restrict__ lvl_at,
                                                               const uint64_t* __restrict__ idx0, const uint64_t* __restrict__ index,
-                                                              uint64_t lo, bool ttl) {
+                                                              uint64_t lo, bool ttl, uint32_t* __restrict__ err) {
   const uint32_t wv = threadIdx.x / kWave, l = __lane_id();
   const uint32_t E = ctl[0], ns = *nseg;
   for (uint32_t r = blockIdx.x * kSrW + wv; r < ns; r += gridDim.x * kSrW) {  // (wave-uniform)
     const uint32_t start = seg[r];
     const uint32_t m = (uint32_t)(key[orig ? orig[start] : start] >> kEvMapShift);
     SmallMap* s = st + m;
-    if (!(s->flags & kSmIn)) continue;  // (left the window earlier: no events are emitted for it)
+    if (!(s->flags & kSmIn)) continue;  // (left the window earlier: its events in a lagging snapshot are skipped)
+#ifdef CC_DIAG  // the window invariant: the snapshot keeps every map whose model is in the window (no 0 -> 1 flip)
+    if (l == 0 && !(__hip_atomic_load(&msmall[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMfSmall))
+      atomicOr(err, kErrSmallFlag);
+#else
+    (void)msmall;
+    (void)err;
+#endif
     SmallJhm j;
     j.load(*s);
 #ifdef CC_PHASE_TIMING
@@ -293,9 +303,8 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
       j.used = 0;
     }
     j.store(*s);
-    if (l == 0) {  // (atomic on the flag word: the next sub-batch's kernels may set other flags of the map meanwhile)
-      if (j.flags & kSmIn) mflag_or(msmall, m, kMfSmall);
-      else mflag_and(msmall, m, (uint8_t)~kMfSmall);
+    if (l == 0) {  // the map left the window: a mark for the engine stream's fold (d_msmall is not written here)
+      if (!(j.flags & kSmIn)) left[m] = 1;
       atomicMax(&mpcap[m], j.lvl);
     }
   }
@@ -491,7 +500,28 @@ __global__ __launch_bounds__(256) void k_size_answer(const uint64_t* __restrict_
 
 __global__ void k_mflag_clear(uint8_t* __restrict__ mflag, uint32_t R) {
   for (uint32_t m = blockIdx.x * blockDim.x + threadIdx.x; m < R; m += gridDim.x * blockDim.x)
-    mflag_and(mflag, m, (uint8_t)~(kMfSize | kMfCv | kMfClr));  // (atomic: a side-stream replay may clear kMfSmall)
+    mflag_and(mflag, m, (uint8_t)~(kMfSize | kMfCv | kMfClr));
+}
+
+// The fold of a finished replay's exit marks into the engine stream's snapshot (common.h, the small-map window
+// invariant): launched on the engine stream right after it waits for that replay; the marks are cleared for the
+// set's next replay.  A word of 4 maps per thread (the byte arrays are padded to whole words).
+__global__ void k_small_fold(uint8_t* __restrict__ left, uint8_t* __restrict__ msmall, uint32_t R) {
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; 4 * q < R; q += gridDim.x * blockDim.x) {
+    uint32_t lw = 0;
+    for (uint32_t b = 0; b < 4 && 4 * q + b < R; ++b) lw |= (uint32_t)left[4 * q + b] << (8 * b);
+    if (!lw) continue;
+    uint32_t keep = ~0u;
+    for (uint32_t b = 0; b < 4; ++b)
+      if ((lw >> (8 * b)) & 0xFFu) keep &= ~((uint32_t)kMfSmall << (8 * b));
+    reinterpret_cast<uint32_t*>(msmall)[q] &= keep;
+    for (uint32_t b = 0; b < 4 && 4 * q + b < R; ++b) left[4 * q + b] = 0;
+  }
+}
+
+int launch_small_fold(uint8_t* left, uint8_t* msmall, uint32_t R, hipStream_t st) {
+  hipLaunchKernelGGL(k_small_fold, dim3(std::min<uint32_t>(256, (R / 4 + 256) / 256)), dim3(256), 0, st, left, msmall, R);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_size_emit(const SizeArgs& a, hipStream_t st) {
@@ -536,12 +566,12 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
       size_t tb = a.temp_bytes;
       if (hipcub::DeviceScan::InclusiveScan(a.temp, tb, it, a.ev_val, hipcub::Max(), (int)E, st) != hipSuccess) return -1;
       hipLaunchKernelGGL(k_small_chains, dim3(std::min<uint32_t>(2048, (E + 255) / 256)), dim3(256), 0, st, a.ev_key2,
-                         a.ev_val2, const_cast<EvPay*>(a.ev_pay), a.ev_val, E, a.state);
+                         a.ev_val2, const_cast<EvPay*>(a.ev_pay), a.ev_val, E, a.msmall);
     }
     const bool cmp = a.cseg != nullptr && !a.msize;  // the compacted events (outside TTL mode)
     uint32_t* const orig = reinterpret_cast<uint32_t*>(a.ev_key);  // (free after the sort)
     if (cmp) {
-      KeepIt it(hipcub::CountingInputIterator<uint32_t>(0), ChainKeep{a.ev_key2, a.ev_val, a.state, E});
+      KeepIt it(hipcub::CountingInputIterator<uint32_t>(0), ChainKeep{a.ev_key2, a.ev_val, a.msmall, E});
       size_t tb = a.temp_bytes;
       if (hipMemsetAsync(a.cseg + a.max_resources, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
       if (hipcub::DeviceSelect::Flagged(a.temp, tb, hipcub::CountingInputIterator<uint32_t>(0), it, orig,
@@ -557,7 +587,9 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
     hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, rst, a.ev_key2, a.ev_val2, a.ev_pay,
                        cmp ? orig : nullptr, cmp ? a.cseg + a.max_resources + 1 : a.ctl, cmp ? a.cseg : a.seg,
                        cmp ? a.cseg + a.max_resources : a.nseg, a.state,
-                       a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr);
+                       a.left, a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr, a.err);
+    // (on this stream: its exit marks fold into the snapshot right after it)
+    if (rst == st && launch_small_fold(a.left, a.msmall, a.max_resources, st)) return -1;
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
       hipLaunchKernelGGL(k_ttl_replay, dim3(256), dim3(256), 0, st, a.ev_key2, a.ev_val2, a.ev_pay, a.ctl, a.seg, a.nseg,
                          a.msize, a.mpcap, a.lvl_at, a.index, a.lo, a.out_status, a.out_value);
@@ -569,8 +601,8 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
 int launch_small_replay_kernel(const SmallArgs& a, hipStream_t rst) {
   uint32_t* const orig = reinterpret_cast<uint32_t*>(a.ev_key);
   hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, rst, a.ev_key2, a.ev_val2, a.ev_pay, orig,
-                     a.cseg + a.max_resources + 1, a.cseg, a.cseg + a.max_resources, a.state, a.msmall, a.mpcap, a.lvl_at,
-                     a.idx0, a.index, a.lo, false);
+                     a.cseg + a.max_resources + 1, a.cseg, a.cseg + a.max_resources, a.state, a.left, a.msmall, a.mpcap,
+                     a.lvl_at, a.idx0, a.index, a.lo, false, a.err);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -107,9 +107,14 @@ __device__ inline void map_barrier_row(uint64_t i, uint32_t o, const uint32_t* _
 }
 
 // Rows whose instance is open on a live map and whose op reads or resets the whole map; and whether any map row
-// arms a TTL timer (the engine then switches to TTL mode for good).  Each thread scans 16 rows of the op column with one 16-byte load (a row per thread spent the
-// launch on issuing 64-byte loads: 2.2 ms per 1e9 rows); candidate rows (rare) are resolved one by one.
-constexpr int kMwRows = 16;
+// arms a TTL timer (the engine then switches to TTL mode for good).  A persistent grid-stride scan of the op column:
+// each wave reads 4 KB per step (four fully coalesced 16-byte loads per lane, 64 rows per thread), every op byte is
+// looked up in a 256-entry LDS table of candidate ops, and only a wave holding a candidate row (rare) leaves the fast
+// path to resolve it.  (One 16-row thread per 16-byte load, each row tested by a chain of compares behind a divergent
+// branch, was 976,564 waves and 1.38 G scalar instructions per 1e9 rows: 2.30 ms.)
+constexpr int kMwLd = 4;                      // 16-byte loads per thread and step
+constexpr int kMwRows = 16 * kMwLd;           // rows per thread and step
+constexpr uint32_t kMwWaveBytes = kWave * kMwRows;  // op bytes per wave and step
 // The lists are staged per workgroup in LDS and reserved with one global atomic per list and workgroup (an atomic
 // per listed row on one counter was ~11 ms per 1B-row batch with 0.1 % in-stream containsValue rows).
 constexpr uint32_t kMwStage = 256;  // staged rows per list and workgroup (more: appended one by one)
@@ -124,12 +129,19 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
                                                       uint32_t* __restrict__ cvq_n, uint32_t cvq_cap,
                                                       uint32_t* __restrict__ mfirst, uint32_t* __restrict__ clrq,
                                                       uint32_t* __restrict__ clrq_n, uint32_t clrq_cap) {
+  static_assert(kMwT == 256, "one candidate-table entry per thread");
   __shared__ uint32_t lrow[kLists][kMwStage];
   __shared__ uint32_t lcnt[kLists], lbase[kLists];
+  __shared__ uint8_t lut[256];  // 1: the op may make its row a listed row (resolved by map_barrier_row)
   uint32_t* const gl[kLists] = {bar, szq, cvq, clrq};
   uint32_t* const gn[kLists] = {bar_n, szq_n, cvq_n, clrq_n};
   const uint32_t gcap[kLists] = {cap, szq_cap, cvq_cap, clrq_cap};
-  if (threadIdx.x < kLists) lcnt[threadIdx.x] = 0;
+  const uint32_t t = threadIdx.x, l = t & 63;
+  {
+    const uint32_t o = t;
+    lut[t] = (map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o))) ? 1 : 0;
+  }
+  if (t < kLists) lcnt[t] = 0;
   __syncthreads();
   auto push = [&](int ls, uint32_t row) {
     const uint32_t k = atomicAdd(&lcnt[ls], 1u);
@@ -140,46 +152,55 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
       if (g < gcap[ls]) gl[ls][g] = row;
     }
   };
-  const uint64_t g = (uint64_t)blockIdx.x * kMwT + threadIdx.x;
-  const uint64_t i0 = g * kMwRows;
-  if (i0 < n) {
-    uint32_t wv[kMwRows / 4];
-    if (i0 + kMwRows <= n && (reinterpret_cast<uintptr_t>(op) & 15) == 0) {
-      const uint4 v = reinterpret_cast<const uint4*>(op)[g];
-      wv[0] = v.x;
-      wv[1] = v.y;
-      wv[2] = v.z;
-      wv[3] = v.w;
-    } else {
+  const bool al = (reinterpret_cast<uintptr_t>(op) & 15) == 0;
+  const uint64_t waves = (uint64_t)gridDim.x * (kMwT / kWave);
+  // wave step s covers op bytes [s * kMwWaveBytes, +kMwWaveBytes); lane l's load k reads bytes k * 1024 + 16 l .. +15
+  for (uint64_t s = (uint64_t)blockIdx.x * (kMwT / kWave) + (t >> 6); s * kMwWaveBytes < n; s += waves) {
+    const uint64_t b0 = s * kMwWaveBytes;
+    uint4 v[kMwLd];
+    if (al && b0 + kMwWaveBytes <= n) {
 #pragma unroll
-      for (int q = 0; q < kMwRows / 4; ++q) {
-        wv[q] = 0;
-        for (int b = 0; b < 4; ++b) {
-          const uint64_t i = i0 + 4 * q + b;
-          if (i < n) wv[q] |= (uint32_t)op[i] << (8 * b);
+      for (int k = 0; k < kMwLd; ++k) v[k] = *reinterpret_cast<const uint4*>(op + b0 + k * (16 * kWave) + 16 * l);
+    } else {  // the last, partial step: bytes past the end read as op 0 (no candidate)
+#pragma unroll
+      for (int k = 0; k < kMwLd; ++k) {
+        uint32_t w4[4] = {0, 0, 0, 0};
+        for (int q = 0; q < 16; ++q) {
+          const uint64_t i = b0 + k * (16 * kWave) + 16 * l + q;
+          if (i < n) w4[q / 4] |= (uint32_t)op[i] << (8 * (q % 4));
         }
+        v[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
     }
+    uint32_t any = 0;  // a candidate op among the thread's 64 rows
 #pragma unroll
-    for (int q = 0; q < kMwRows; ++q) {
-      const uint64_t i = i0 + q;
-      const uint32_t o = (wv[q / 4] >> (8 * (q % 4))) & 0xFFu;
-      const bool cand = map_wide_op(o) || set_wide_op(o) || mmap_wide_op(o) || o == CC_OP_GROUP_SCHEDULE || (aux && ttl_op(o));
-      if (cand && i < n)
-        map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, ttl_seen, szq != nullptr, mflag, cvq != nullptr,
-                        mfirst, clrq != nullptr, push);
+    for (int k = 0; k < kMwLd; ++k) {
+      const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) any |= lut[(w4[q / 4] >> (8 * (q % 4))) & 0xFFu];
+    }
+    if (__ballot(any != 0) == 0) continue;  // (wave-uniform: the common case)
+    if (any) {  // (rare) the rows again, op bytes re-read from the cache
+      for (uint32_t q = 0; q < (uint32_t)kMwRows; ++q) {
+        const uint64_t i = b0 + (q >> 4) * (16 * kWave) + 16 * l + (q & 15u);
+        if (i >= n) continue;
+        const uint32_t o = op[i];
+        if (lut[o])
+          map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, ttl_seen, szq != nullptr, mflag, cvq != nullptr,
+                          mfirst, clrq != nullptr, push);
+      }
     }
   }
   __syncthreads();
-  if (threadIdx.x < kLists) {
-    const uint32_t c = lcnt[threadIdx.x] < kMwStage ? lcnt[threadIdx.x] : kMwStage;
-    lbase[threadIdx.x] = c ? atomicAdd(gn[threadIdx.x], c) : 0u;
+  if (t < kLists) {
+    const uint32_t c = lcnt[t] < kMwStage ? lcnt[t] : kMwStage;
+    lbase[t] = c ? atomicAdd(gn[t], c) : 0u;
   }
   __syncthreads();
 #pragma unroll
   for (int ls = 0; ls < kLists; ++ls) {
     const uint32_t c = lcnt[ls] < kMwStage ? lcnt[ls] : kMwStage;
-    for (uint32_t q = threadIdx.x; q < c; q += kMwT)
+    for (uint32_t q = t; q < c; q += kMwT)
       if (lbase[ls] + q < gcap[ls]) gl[ls][lbase[ls] + q] = lrow[ls][q];
   }
 }
@@ -571,8 +592,10 @@ int launch_map_barriers(const uint32_t* inst, const uint8_t* op, const uint64_t*
   if (cvq_n && hipMemsetAsync(cvq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (clrq_n && hipMemsetAsync(clrq_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (mfirst && hipMemsetAsync(mfirst, 0xFF, sizeof(uint32_t) * R, st) != hipSuccess) return -1;
-  const uint64_t groups = (n + kMwRows - 1) / kMwRows;
-  hipLaunchKernelGGL(k_map_barriers, dim3((uint32_t)((groups + kMwT - 1) / kMwT)), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
+  // persistent: 8 workgroups per CU at most (each wave then takes ~30 4-KB steps of a 1e9-row batch)
+  const uint64_t steps = (n + kMwWaveBytes - 1) / kMwWaveBytes, wpg = kMwT / kWave;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8 * kPersistGrid, (steps + wpg - 1) / wpg));
+  hipLaunchKernelGGL(k_map_barriers, dim3(grid), dim3(kMwT), 0, st, inst, op, aux, n, inst_res,
                      res_type, max_inst, bar, bar_n, cap, ttl_seen, szq, szq_n, szq_cap, mflag, cvq, cvq_n, cvq_cap, mfirst,
                      clrq, clrq_n, clrq_cap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -724,8 +747,8 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
     auto evm = [&](uint32_t x) {
       return (x & 3u) && (map_row || (msmall[x >> 2] & (kMfSmall | kMfSize | kMfClr)));
     };
-    // (each position's decision is taken once and kept in a bit mask: the previous sub-batch's small-map replay on
-    // the side stream may clear a map's kMfSmall between two reads, and the writes must match the reservation)
+    // (each position's decision is taken once and kept in a bit mask, so the writes match the reservation by
+    // construction; the flags are the engine stream's snapshot and do not change during the launch, common.h)
     static_assert(kTile / kMszT <= 32, "one mask bit per position of a thread");
     uint32_t my = 0, emask = 0;
     for (uint32_t p = b0 + threadIdx.x, j = 0; p < b1; p += kMszT, ++j)
@@ -819,7 +842,9 @@ __global__ __launch_bounds__(kMszScanW * kWave) void k_msize_scan(const uint8_t*
   }
   csum[w][l] = sum;
   lds_barrier();
-  const uint32_t s0 = ok ? msize[m] : 0u, mp = ok ? mpcap[m] : 0u;
+  // (mpcap is raised atomically by an overlapped small-map replay on the side stream: an atomic load here; a stale
+  // level only lists more tiles for the exact pass, and the CAS merge below keeps the higher one)
+  const uint32_t s0 = ok ? msize[m] : 0u, mp = ok ? __hip_atomic_load(&mpcap[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   int64_t start = s0;
   for (uint32_t q = 0; q < w; ++q) start += csum[q][l];
   // lower bounds: the highest level every tile's counts prove (with the level reached so far)

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(V3A<NS>::T, V3A<NS>::MINW) void k_apply_value_v3(ui
                                                         uint64_t dummy,
                                                         uint32_t* __restrict__ err_out) {
   using P = V3A<NS>;
-#ifdef CC_DIAG  // diagnostics build only (-DCC_DIAG=1: no walk, 2: contiguous positions -- wrong results by design)
+#ifdef CC_DIAG  // diagnostics build only (-DCC_DIAG=1: no walk, 2: contiguous positions -- wrong results by design; 4: internal checks only, common.h kErrSmallFlag)
   constexpr uint32_t diag = CC_DIAG;
 #else
   constexpr uint32_t diag = 0;

@@ -408,3 +408,63 @@ def test_prefix_apply_stops_before_a_full_lock_queue_and_resumes():
     got = _canon(*(ev3[k] for k in ("pos", "src", "target", "code", "tag", "payload")))
     assert got == _canon(oe["pos"], oe["src"], oe["target"], oe["code"], oe["tag"], oe["payload"])
     _check_state(E, O, [L] * R)
+
+
+def test_prefix_apply_churned_near_full_lock_queue_scans_once():
+    """cc_apply_batch_host_prefix (ABI 5) on a lock queue that stays at coord_cap under churn: the holder unlocks (its
+    first waiter takes the lock, LockState.java:73-85) and a new client queues, 1,500 times, while 255 other locks take
+    random traffic.  Every add on the hot lock meets the upper bound, so the call re-reads that lock's count at each one
+    and goes on (one scan of the batch, one header read per stop: ADVICE r5); nothing overflows, every row applies, and
+    results, events and lock queues equal the oracle's.  The run time is bounded (the round-5 form rescanned the rest of
+    the batch and read one header per addressed lock at every stop)."""
+    import time as _time
+
+    from copycat_amd.engine import Engine
+    from oracle.oracle_py import Oracle
+
+    R, churn = 256, 1500
+    hot = 65 + churn           # clients of lock 0: the holder, 64 waiters, then one new client per churn step
+    K = 8                      # clients of every other lock
+    max_inst = hot + (R - 1) * K + 8
+    E = Engine(R, max_inst, 1 << 16, flags=abi.CC_CFG_TIMERS_DEFERRED, max_events=1 << 18)
+    O = Oracle(R, max_inst, abi.CC_CFG_TIMERS_DEFERRED)
+    for r in range(R):
+        E.resource_create(r, L)
+        O.resource_create(r, L)
+    inst_of = []
+    for k in range(hot):
+        inst_of.append((k, 0))
+    for r in range(1, R):
+        for k in range(K):
+            inst_of.append((hot + (r - 1) * K + k, r))
+    for i, r in inst_of:
+        E.instance_open(i, r, 1000 + i, 7 + i)
+        O.instance_open(i, r, 1000 + i, 7 + i)
+    rng = np.random.default_rng(17)
+    rows = [(k, abi.CC_OP_LOCK_LOCK, -1) for k in range(65)]  # holder 0 + 64 waiters: the queue is full
+    for j in range(churn):
+        rows.append((j, abi.CC_OP_LOCK_UNLOCK, 0))              # the holder leaves, waiter j + 1 holds
+        rows.append((65 + j, abi.CC_OP_LOCK_LOCK, -1))          # a new waiter: back at coord_cap
+        for _ in range(2):                                      # other locks' traffic (adds among it)
+            r = int(rng.integers(1, R))
+            k = int(rng.integers(0, K))
+            rows.append((hot + (r - 1) * K + k, abi.CC_OP_LOCK_LOCK if rng.random() < 0.5 else abi.CC_OP_LOCK_UNLOCK,
+                         int(rng.choice([-1, 0, 50]))))
+    n = len(rows)
+    b = Batch(n)
+    b.index[:] = np.arange(1, n + 1, dtype=np.uint64)
+    b.time[:] = np.arange(n, dtype=np.uint64)
+    b.inst[:] = [x[0] for x in rows]
+    b.op[:] = [x[1] for x in rows]
+    b.aux[:] = np.array([x[2] for x in rows], np.int64).view(np.uint64)
+    t0 = _time.perf_counter()
+    applied, s, v, ev = E.apply_host_prefix(b)
+    dt = _time.perf_counter() - t0
+    assert applied == n
+    s2, v2 = O.apply(b)
+    assert np.array_equal(s, s2) and np.array_equal(v, v2)
+    oe, _, _ = _oracle_events(O)
+    got = _canon(*(ev[k] for k in ("pos", "src", "target", "code", "tag", "payload")))
+    assert got == _canon(oe["pos"], oe["src"], oe["target"], oe["code"], oe["tag"], oe["payload"])
+    _check_state(E, O, [L] * R)
+    assert dt < 30.0, f"{dt:.1f} s for {churn} stops"
