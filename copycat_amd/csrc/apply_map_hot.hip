@@ -405,7 +405,8 @@ __device__ inline void hot_map_event_at(const HotClr& c, uint32_t slot, uint32_t
   const uint32_t kt = CC_FLAG_KTAG(smeta_flags(r.meta));
   const uint32_t jh = java_key_hash(kt, r.key, c.hh_key, c.hh_val, c.hh_n, ok);
   const uint64_t d = r.idx - *c.idx0p;
-  if (!ok || d >> kEvPosBits) err |= kErrHandleHash;
+  if (!ok) err |= kErrHandleHash;
+  if (d >> kEvPosBits) err |= kErrSpan;
   if (at < c.ev_cap) {
     c.ev_key[at] = ((uint64_t)slot << kEvMapShift) | ((d & kEvPosMask) << 4) | code;
     c.ev_val[at] = at;

@@ -327,8 +327,9 @@ constexpr uint32_t kErrMapOrder = 16u;  // containsValue's HashMap iteration ord
 constexpr uint32_t kErrMapSize = 32u;   // a map's tracked size differs from its table at a barrier (internal check)
 constexpr uint32_t kErrHandleHash = 64u;  // a HANDLE map key whose String.hashCode was never registered (cc_handle_hashes)
 constexpr uint32_t kErrSmallFlag = 256u;
-constexpr uint32_t kErrCoordFull = 512u;  // a coordination collection (lock queue, listeners, members, queue) is full  // (CC_DIAG builds) a map in the small-map window without its snapshot flag
-constexpr uint32_t kErrCvKey = 128u;     // in-stream containsValue: a fingerprint collision or a 2^40-index span (map_cv.hip)
+constexpr uint32_t kErrCoordFull = 512u;
+constexpr uint32_t kErrSpan = 1024u;      // a sub-batch with map events spans 2^32 log indices (the host cuts them first)  // a coordination collection (lock queue, listeners, members, queue) is full  // (CC_DIAG builds) a map in the small-map window without its snapshot flag
+constexpr uint32_t kErrCvKey = 128u;     // in-stream containsValue: an event past a 2^40-index span (internal check)
 
 // java.util.HashMap placement of a map key: hash(key) = h ^ (h >>> 16), h = key.hashCode() -- Long (int)(v ^ v >>> 32),
 // Integer v, Boolean 1231 / 1237, String (HANDLE) its registered String.hashCode (hh: sorted handles + hashes);
@@ -577,7 +578,7 @@ __host__ __device__ inline uint32_t mw_vtag(uint32_t w) { return (w >> 21) & 7; 
 // ---- containsValue in the stream (map_cv.hip) -------------------------------------------------------------------
 // A sub-batch's in-stream containsValue operands (map slot, value tag, canonical value) live in a device hash set
 // keyed by a 64-bit key: exact (bit 63 set) when the value fits 43 signed bits, else a fingerprint whose entries are
-// verified against the stored operand (a fingerprint shared by two operands fails the batch: kErrCvKey).
+// verified against the stored operand (two operands that share a fingerprint get a position each: map_cv.hip k_cv_fix).
 struct CvEnt {
   unsigned long long k64;  // 0: empty
   uint64_t v;
@@ -597,7 +598,9 @@ __host__ __device__ inline uint32_t cv_slot0(uint64_t k64, uint32_t mask) {
   uint64_t h = k64 * 0x9E3779B97F4A7C15ull;
   return (uint32_t)(h >> 32) & mask;
 }
-// The operand's set position, or ~0 when the sub-batch asks no containsValue of it.
+// The operand's set position, or ~0 when the sub-batch asks no containsValue of it.  A hashed fingerprint (an operand
+// past 43 bits) may be shared by two operands: the set then holds each at its own position, the second one further
+// along the probe sequence (map_cv.hip k_cv_fix), so a position counts only when the operand itself matches.
 __device__ inline uint32_t cv_find(const CvEnt* __restrict__ set, uint32_t mask, uint32_t m, uint32_t tag, uint64_t v) {
   bool exact;
   const uint64_t k = cv_key(m, tag, v, exact);
@@ -605,7 +608,7 @@ __device__ inline uint32_t cv_find(const CvEnt* __restrict__ set, uint32_t mask,
   for (uint32_t step = 0; step <= mask; ++step, p = (p + 1) & mask) {
     const uint64_t c = set[p].k64;
     if (c == 0) return ~0u;
-    if (c == k) return (exact || (set[p].v == v && set[p].meta == ((m & kMwSlotMask) | (tag << 17)))) ? p : ~0u;
+    if (c == k && (exact || (set[p].v == v && set[p].meta == ((m & kMwSlotMask) | (tag << 17))))) return p;
   }
   return ~0u;
 }

@@ -97,7 +97,7 @@ static void free_all(cc_engine* e) {
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,    e->d_mw_cgen, e->d_cset, e->d_cset_full, e->d_tbl_claim, e->d_lvl_at, e->d_half_count,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
-                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,  e->d_msm_left,
+                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,  e->d_msm_left, e->d_span_cut,
                   e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp, e->d_sm_pay,
                   e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb,
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
@@ -496,6 +496,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
     ALLOC(e->d_msmall, (cfg->max_resources + 3) & ~3u);  // (padded to whole words: common.h mflag_or)
     ALLOC(e->d_msm_left, 3ull * cfg->max_resources);
+    ALLOC(e->d_span_cut, sizeof(uint64_t));
     ALLOC(e->d_sm_ctl, sizeof(uint32_t) * 4);
     ALLOC(e->d_rst_msz, sizeof(uint32_t) * (e->sub_batch + 4 * kPT));
     ALLOC(e->d_hot_msz, sizeof(uint32_t) * (kHotMaxPieces + kHotMax) * (kHotPiece / 16));
@@ -616,13 +617,14 @@ static int check_device_err(cc_engine* e) {
                                    "bounds leave open (TTL mode)");
     if (err & kErrMapSize) return set_err(CC_ERR_STATE, "internal check: a map's tracked size differs from its table");
     if (err & kErrCvKey)
-      return set_err(CC_ERR_STATE, "in-stream containsValue: two operands share a 64-bit fingerprint, or a sub-batch "
-                                   "spans more than 2^40 log indices");
+      return set_err(CC_ERR_STATE, "internal check: an in-stream containsValue event spans more than 2^40 log indices");
     if (err & kErrSmallFlag)
       return set_err(CC_ERR_STATE, "internal check (CC_DIAG): a map in the small-map window without its snapshot flag");
     if (err & kErrHandleHash)
-      return set_err(CC_ERR_STATE, "a HANDLE map key's String.hashCode is not registered (cc_handle_hashes), or a "
-                                   "sub-batch spans more than 2^32 log indices");
+      return set_err(CC_ERR_STATE, "a HANDLE map key's String.hashCode is not registered (cc_handle_hashes)");
+    if (err & kErrSpan)
+      return set_err(CC_ERR_STATE, "internal check: a sub-batch with map events spans 2^32 log indices (the index "
+                                   "column must increase in log order)");
     if (err & kErrEvents) return set_err(CC_ERR_CAPACITY, "more events than the event stream / max_events holds");
     if (err & kErrCapacity)
       return set_err(CC_ERR_CAPACITY, "a fixed capacity was exceeded (map table region, leak log, event buffer)");
@@ -1107,7 +1109,15 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         if (inline_size || inline_ttl) HIPCHECK(hipMemcpyAsync(p32 + 2, e->d_szq_n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         if (inline_size) HIPCHECK(hipMemcpyAsync(p32 + 3, e->d_cvq_n, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         if (inline_size) HIPCHECK(hipMemcpyAsync(p32 + 5, e->d_clrq_n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        if (e->map_bits) {  // the batch's first and last log index (map event positions, below)
+          HIPCHECK(hipMemcpyAsync(pin + 4, c->index, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+          HIPCHECK(hipMemcpyAsync(pin + 5, c->index + n - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        }
         HIPCHECK(hipStreamSynchronize(st));
+        // Map events are keyed by their position (log index - the sub-batch's first, 32 bits: common.h kEvPosBits).
+        // A batch whose whole index range fits needs no cut; else each sub-batch ends before its first row 2^32 past
+        // its start (k_span_cut, one round trip per sub-batch, only then)
+        if (e->map_bits) e->span_cut = n && pin[5] - pin[4] >= (1ull << kEvPosBits);
         clock_before = pin[0];
         nb = p32[0];
         ttl_seen = p32[1];
@@ -1334,6 +1344,15 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
         cv_e = cv_b + kCvMaxRows;
         hi = e->isc_rows[cv_e];
       }
+    }
+    if (e->span_cut && !e->ttl_live) {  // (TTL mode positions events by row, 2 (row - lo) + 1: always within 32 bits)
+      HIPCHECK(hipMemsetAsync(e->d_span_cut, 0xFF, sizeof(uint64_t), st));
+      if (launch_span_cut(c->index, lo, hi, e->d_span_cut, st)) return set_err(CC_ERR_HIP, "span cut launch", hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(e->h_pin + 6, e->d_span_cut, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (e->h_pin[6] > lo && e->h_pin[6] < hi) hi = e->h_pin[6];
+      if (!e->isc_rows.empty())  // (the in-stream containsValue rows of the shortened sub-batch)
+        cv_e = (size_t)(std::lower_bound(e->isc_rows.begin(), e->isc_rows.end(), (uint32_t)hi) - e->isc_rows.begin());
     }
     const uint32_t cv_n = (uint32_t)(cv_e - cv_b);
     const bool clr_on = e->clr_n > 0;  // clears in the stream in this batch (map_clear.hip)
@@ -1589,6 +1608,8 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
       cva.val2 = e->d_cvev_val2;
       cva.seg = e->d_cvseg;
       cva.nseg = e->d_cvseg + e->cvset_cap;
+      cva.coll = e->d_cvseg;          // (free until the answers' runs: the prepare's collision list)
+      cva.coll_n = e->d_cvev_ctl + 1;
       cva.temp = e->d_cvtemp;
       cva.temp_bytes = e->cvtemp_bytes;
       cva.out_status = out->status;

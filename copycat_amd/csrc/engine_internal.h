@@ -248,12 +248,13 @@ struct SizeArgs {
   uint8_t* out_status;          // the batch's result columns (absolute rows)
   uint64_t* out_value;
   bool ttl;                     // TTL mode: queries positioned by row (common.h TtlEmit), answered by k_ttl_replay
-  uint32_t* err;                // kErrHandleHash: a sub-batch spanning 2^32 log indices
+  uint32_t* err;                // kErrSpan: a sub-batch spanning 2^32 log indices
 };
 int launch_size_emit(const SizeArgs& a, hipStream_t st);
 int launch_size_answer(const SizeArgs& a, hipStream_t st);
 int launch_mflag_clear(uint8_t* mflag, uint32_t R, hipStream_t st);
 int launch_small_fold(uint8_t* left, uint8_t* msmall, uint32_t R, hipStream_t st);
+int launch_span_cut(const uint64_t* index, uint64_t lo, uint64_t hi, uint64_t* out, hipStream_t st);
 size_t small_sort_temp_bytes(uint32_t cap);
 int launch_small_clear(SmallMap* state, uint32_t m, hipStream_t st);
 int launch_map_drop_resource(uint32_t* tbl_word, uint64_t entries, uint32_t slot, uint64_t* cgen, hipStream_t st);
@@ -312,6 +313,8 @@ struct CvSubArgs {  // per sub-batch: the operand set, initial counts and query 
   const uint64_t* tbl_val;
   uint64_t entries;
   uint32_t* err;
+  uint32_t* coll;     // operands whose fingerprint another claimed (k_cv_verify -> k_cv_fix), and their count
+  uint32_t* coll_n;
   // answers
   uint64_t* key2;
   uint32_t* val2;

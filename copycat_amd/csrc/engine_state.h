@@ -324,7 +324,9 @@ struct cc_engine {
   std::map<uint32_t, std::vector<uint64_t>> leaks;  // ordered: snapshots are byte-deterministic
   uint64_t applied = 0;
   bool applied_pending = false;
-  uint32_t last_err_bits = 0;  // the device error bits the last check_device_err read (common.h kErr*)
+  uint32_t last_err_bits = 0;
+  bool span_cut = false;             // this batch's index range passes 2^32: sub-batches are cut at k_span_cut's row
+  uint64_t* d_span_cut = nullptr;  // the device error bits the last check_device_err read (common.h kErr*)
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
   // device staging of the host-memory entry points (host_path.hip): grown on demand, kept between calls
   void* hw_buf[24] = {};

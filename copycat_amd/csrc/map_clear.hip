@@ -131,7 +131,7 @@ __global__ void k_clr_events(const uint64_t* __restrict__ keys, uint32_t n, uint
     const uint64_t k = keys[i], row = k & 0xFFFFFFFFull, m = k >> 32;
     if (row < lo || row >= hi) continue;
     const uint64_t d = index[row] - idx0;
-    if (d >> kEvPosBits) atomicOr(err, kErrHandleHash);
+    if (d >> kEvPosBits) atomicOr(err, kErrSpan);
     const uint32_t at = atomicAdd(ctl, 1u);
     if (at < cap) {
       ev_key[at] = (m << kEvMapShift) | ((d & kEvPosMask) << 4) | 3u;

@@ -112,10 +112,9 @@ __device__ inline void cv_operand(uint32_t row, const uint32_t* __restrict__ ins
   v = tag ? a[row] : 0;
 }
 
-// the operands into the set (one position each), and a query event per row
+// the operands into the set by fingerprint (one position each; k_cv_verify / k_cv_fix give two operands that share a
+// fingerprint a position each)
 __global__ void k_cv_query(CvSubArgs a) {
-  uint32_t err = 0;
-  const uint64_t idx0 = a.index[a.lo];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < a.isc_n; q += gridDim.x * blockDim.x) {
     const uint32_t row = a.isc[q];
     uint32_t m, tag;
@@ -139,14 +138,11 @@ __global__ void k_cv_query(CvSubArgs a) {
       if (c == k) break;
       p = (p + 1) & a.cv.mask;
     }
-    // value: the row in the sub-batch | its clear epoch << 25 (map_clear.hip; 0 without clears in the stream)
-    const uint32_t ep = a.clr.mflag && (a.clr.mflag[m] & kMfClr) ? clr_epoch(a.clr, m, row) : 0u;
-    cv_event(a.cv, p, a.index[row] - idx0, 2u, (row - (uint32_t)a.lo) | (ep << 25), err);
   }
-  if (err) atomicOr(a.err, err);
 }
 
-// two operands that share a fingerprint cannot be told apart: the batch fails (kErrCvKey) instead of guessing
+// Operands whose fingerprint another operand claimed (after k_cv_query: every claimer's operand is written) are
+// listed (a.coll); the fingerprint hash is 63 bits, so this is adversarial input only.
 __global__ void k_cv_verify(CvSubArgs a) {
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < a.isc_n; q += gridDim.x * blockDim.x) {
     uint32_t m, tag;
@@ -157,8 +153,51 @@ __global__ void k_cv_verify(CvSubArgs a) {
     if (exact) continue;
     uint32_t p = cv_slot0(k, a.cv.mask);
     while (a.set[p].k64 != k) p = (p + 1) & a.cv.mask;
-    if (a.set[p].v != v || a.set[p].meta != ((m & kMwSlotMask) | (tag << 17))) atomicOr(a.err, kErrCvKey);
+    if (a.set[p].v != v || a.set[p].meta != ((m & kMwSlotMask) | (tag << 17))) a.coll[atomicAdd(a.coll_n, 1u)] = q;
   }
+}
+
+// The listed operands, one thread in list order: each gets a position of its own with its fingerprint, further along
+// the probe sequence (an operand listed twice finds the position its first listing claimed).  cv_find matches the
+// operand itself at every position that carries a hashed fingerprint.
+__global__ void k_cv_fix(CvSubArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t nc = *a.coll_n;
+  for (uint32_t i = 0; i < nc; ++i) {
+    uint32_t m, tag;
+    uint64_t v;
+    cv_operand(a.isc[a.coll[i]], a.inst, a.flags, a.a, a.inst_res, m, tag, v);
+    bool exact;
+    const uint64_t k = cv_key(m, tag, v, exact);
+    const uint32_t meta = (m & kMwSlotMask) | (tag << 17);
+    for (uint32_t p = cv_slot0(k, a.cv.mask);; p = (p + 1) & a.cv.mask) {
+      const uint64_t c = a.set[p].k64;
+      if (c == k && a.set[p].v == v && a.set[p].meta == meta) break;  // (listed before)
+      if (c == 0) {
+        a.set[p].k64 = k;
+        a.set[p].v = v;
+        a.set[p].meta = meta;
+        break;
+      }
+    }
+  }
+}
+
+// a query event per row, at its operand's own position
+__global__ void k_cv_qevents(CvSubArgs a) {
+  uint32_t err = 0;
+  const uint64_t idx0 = a.index[a.lo];
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < a.isc_n; q += gridDim.x * blockDim.x) {
+    const uint32_t row = a.isc[q];
+    uint32_t m, tag;
+    uint64_t v;
+    cv_operand(row, a.inst, a.flags, a.a, a.inst_res, m, tag, v);
+    const uint32_t p = cv_find(a.set, a.cv.mask, m, tag, v);
+    // value: the row in the sub-batch | its clear epoch << 25 (map_clear.hip; 0 without clears in the stream)
+    const uint32_t ep = a.clr.mflag && (a.clr.mflag[m] & kMfClr) ? clr_epoch(a.clr, m, row) : 0u;
+    cv_event(a.cv, p, a.index[row] - idx0, 2u, (row - (uint32_t)a.lo) | (ep << 25), err);
+  }
+  if (err) atomicOr(a.err, err);
 }
 
 // per operand: the flagged maps' present entries holding it at the sub-batch start
@@ -180,8 +219,11 @@ int launch_cv_prepare(const CvSubArgs& a, hipStream_t st) {
   if (hipMemsetAsync(a.cv.ctl, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(const_cast<uint32_t*>(a.cv.bloom), 0, (1ull << a.cv.bbits) / 8, st) != hipSuccess) return -1;
   const uint32_t gq = std::min<uint32_t>(1024, (a.isc_n + 255) / 256);
+  if (hipMemsetAsync(a.coll_n, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
   hipLaunchKernelGGL(k_cv_query, dim3(gq), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_cv_verify, dim3(gq), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_cv_fix, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(k_cv_qevents, dim3(gq), dim3(256), 0, st, a);
   const uint32_t ge = (uint32_t)std::min<uint64_t>(4096, (a.entries + 255) / 256);
   hipLaunchKernelGGL(k_cv_count0, dim3(ge), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -433,7 +433,7 @@ __global__ void k_size_emit(const uint32_t* __restrict__ szq, uint32_t szq_n, ui
     if (row < lo || row >= hi) continue;
     const uint32_t m = inst_res[inst[row]];  // (listed by the barrier scan on a live map: the registry is fixed in a batch)
     const uint64_t d = ttl ? 2 * (row - lo) + 1 : index[row] - idx0;
-    if (d >> kEvPosBits) atomicOr(err, kErrHandleHash);
+    if (d >> kEvPosBits) atomicOr(err, kErrSpan);
     const uint32_t at = atomicAdd(ctl, 1u);
     if (at < cap) {
       ev_key[at] = ((uint64_t)m << kEvMapShift) | ((d & kEvPosMask) << 4) | 8u | (op[row] == CC_OP_MAP_ISEMPTY ? 4u : 0u);
@@ -534,6 +534,25 @@ int launch_size_emit(const SizeArgs& a, hipStream_t st) {
 int launch_size_answer(const SizeArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_size_answer, dim3(256), dim3(256), 0, st, a.sorted_key, a.sorted_val, a.ev_pay, a.ctl, a.seg, a.nseg,
                      a.msize, a.out_status, a.out_value);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The first row of [lo, hi) whose log index is 2^32 or more past index[lo] (kEvPosBits: a map event's position), by
+// binary search over the increasing index column; *out stays ~0 when none is.
+__global__ void k_span_cut(const uint64_t* __restrict__ index, uint64_t lo, uint64_t hi, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const uint64_t i0 = index[lo];
+  uint64_t a = lo, b = hi;  // the first row in [a, b) past the span
+  while (a < b) {
+    const uint64_t mid = a + (b - a) / 2;
+    if (index[mid] - i0 >= (1ull << kEvPosBits)) b = mid;
+    else a = mid + 1;
+  }
+  if (a < hi) *out = a;
+}
+
+int launch_span_cut(const uint64_t* index, uint64_t lo, uint64_t hi, uint64_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_span_cut, dim3(1), dim3(64), 0, st, index, lo, hi, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -671,7 +671,8 @@ __device__ inline void map_event(uint32_t at, uint32_t m, uint32_t code, uint64_
   bool ok;
   const uint32_t kt = CC_FLAG_KTAG(smeta_flags(xr.meta));
   const uint32_t jh = java_key_hash(kt, xr.key, hh_key, hh_val, hh_n, ok);
-  if (!ok || d >> kEvPosBits) atomicOr(err, kErrHandleHash);  // an unregistered String key / a sub-batch spanning 2^32 indices
+  if (!ok) atomicOr(err, kErrHandleHash);  // an unregistered String key
+  if (d >> kEvPosBits) atomicOr(err, kErrSpan);  // a sub-batch spanning 2^32 indices (the host cuts them: never)
   if (at < ev_cap) {
     ev_key[at] = ((uint64_t)m << kEvMapShift) | ((d & kEvPosMask) << 4) | code;
     ev_val[at] = at;

@@ -187,20 +187,28 @@ def test_map_capacity_error():
     assert ei.value.rc == abi.CC_ERR_CAPACITY
 
 
-def test_map_event_position_span_error():
-    """A small map's insertions are followed as events keyed by their log index within the sub-batch (32 bits): a
-    sub-batch spanning 2^32 log indices fails the call instead of mis-ordering them; the same rows with a dense
-    index apply."""
-    from copycat_amd.engine import EngineError
+@pytest.mark.parametrize("sub_batch", [0, 32768])
+def test_map_event_positions_across_index_gaps(sub_batch):
+    """A small map's insertions (and size / containsValue rows' maps') are followed as events keyed by their log index
+    within the sub-batch, 32 bits (common.h kEvPosBits).  A batch whose index column jumps by 2^33 several times (inside
+    sub-batches, and across the batch) is cut by the host before each row 2^32 past its sub-batch's first
+    (k_span_cut: round 5 failed such a call with CC_ERR_STATE); every row, every map and the applied index equal the
+    oracle's, with random key ops, stored nulls, size / isEmpty and containsValue rows on small maps."""
+    from copycat_amd.workload import map_random_stream
 
-    b = _puts(np.arange(40, dtype=np.uint64), 0)
-    b.index[20:] += np.uint64(1 << 33)
-    E, _ = _engines(1, 4, 64, 1024)
-    with pytest.raises(EngineError) as ei:
-        E.apply_host(b)
-    assert ei.value.rc == abi.CC_ERR_STATE
-    E, O = _engines(1, 4, 64, 1024)
-    _assert_rows(*_apply_both(E, O, [_puts(np.arange(40, dtype=np.uint64), 0)]))
+    n, maps = 120_000, 6
+    b = map_random_stream(n, maps, maps, keys=40, seed=29)
+    rng = np.random.default_rng(29)
+    rows = rng.choice(n, 900, replace=False)
+    b.op[rows[:300]] = abi.CC_OP_MAP_SIZE
+    b.op[rows[300:600]] = abi.CC_OP_MAP_ISEMPTY
+    b.op[rows[600:]] = abi.CC_OP_MAP_CONTAINSVALUE
+    b.aux[rows] = 0
+    for at in sorted(rng.choice(np.arange(1, n), 7, replace=False)):
+        b.index[at:] += np.uint64(1 << 33)
+    E, O = _engines(maps, maps, n, 4096, sub_batch=sub_batch)
+    _assert_rows(*_apply_both(E, O, [b]))
+    _assert_maps(E, O, range(maps))
 
 
 def test_map_get_with_positive_aux_is_applied():
@@ -399,6 +407,73 @@ def test_map_contains_value_in_stream_zipf():
     c1 = E.counters()
     assert c1[1] - c0[1] == len(rows)
     assert (gv[rows] == 1).any() and (gv[rows] == 0).any()
+
+
+def _cv_fingerprint(m, tag, v):
+    """common.h cv_key for an operand past 43 bits: the 63-bit hashed fingerprint (restated for the collision test)."""
+    M = (1 << 64) - 1
+    h = ((v ^ ((((m & 0x1FFFF) << 3) | (tag & 7)) * 0xC2B2AE3D27D4EB4F & M)) * 0x9E3779B97F4A7C15) & M
+    h ^= h >> 31
+    h = (h * 0xBF58476D1CE4E5B9) & M & ~(1 << 63)
+    return h or 1
+
+
+def _cv_colliding_value(m, tag, v1):
+    """A second operand of map m (same tag) whose fingerprint equals v1's: invert the hash chain from v1's pre-mask
+    value with bit 63 flipped (both mask to the same 63 bits)."""
+    M = (1 << 64) - 1
+    s = ((((m & 0x1FFFF) << 3) | (tag & 7)) * 0xC2B2AE3D27D4EB4F) & M
+    x = ((v1 ^ s) * 0x9E3779B97F4A7C15) & M
+    x ^= x >> 31
+    z = (x * 0xBF58476D1CE4E5B9) & M
+    z ^= 1 << 63
+    u = (z * pow(0xBF58476D1CE4E5B9, -1, 1 << 64)) & M
+    u ^= (u >> 31) ^ (u >> 62)  # the inverse of x ^= x >> 31
+    w = (u * pow(0x9E3779B97F4A7C15, -1, 1 << 64)) & M
+    v2 = w ^ s
+    assert v2 != v1 and _cv_fingerprint(m, tag, v2) == _cv_fingerprint(m, tag, v1)
+    return v2
+
+
+def test_map_contains_value_fingerprint_collision_in_stream():
+    """Two containsValue operands of one map whose 63-bit fingerprints are equal (constructed by inverting the hash):
+    round 5 failed the call (kErrCvKey); now each gets its own set position (map_cv.hip k_cv_verify -> k_cv_fix) and
+    every answer follows its own operand (MapState.containsValue :49-60): puts and removes of either value, queries of
+    both, interleaved, several pairs and maps, against the oracle."""
+    rng = np.random.default_rng(77)
+    maps, n = 3, 6000
+    pairs = []
+    for m in range(maps):
+        for _ in range(3):
+            v1 = int(rng.integers(1 << 50, 1 << 62))
+            pairs.append((m, v1, _cv_colliding_value(m, abi.CC_TAG_LONG, v1)))
+    cols = {k: np.zeros(n, np.uint64) for k in ("index", "key", "a", "b", "aux", "time")}
+    inst = np.zeros(n, np.uint32)
+    op = np.zeros(n, np.uint8)
+    fl = np.full(n, abi.cc_flags(abi.CC_TAG_LONG, 0, 0), np.uint8)
+    for i in range(n):
+        m, v1, v2 = pairs[int(rng.integers(0, len(pairs)))]
+        inst[i] = m
+        x = rng.random()
+        cols["key"][i] = int(rng.integers(0, 8))
+        if x < 0.45:
+            op[i] = abi.CC_OP_MAP_PUT
+            cols["a"][i] = v1 if rng.random() < 0.5 else v2
+        elif x < 0.6:
+            op[i] = abi.CC_OP_MAP_REMOVE
+        else:
+            op[i] = abi.CC_OP_MAP_CONTAINSVALUE
+            cols["a"][i] = v1 if rng.random() < 0.5 else v2
+    cols["index"][:] = np.arange(1, n + 1, dtype=np.uint64)
+    b = Batch.from_columns(index=cols["index"], inst=inst, op=op, flags=fl, key=cols["key"], a=cols["a"])
+    E, O = _engines(maps, maps, n, 4096)
+    c0 = E.counters()
+    gs, gv, os_, ov = _apply_both(E, O, [b])
+    _assert_rows(gs, gv, os_, ov)
+    _assert_maps(E, O, range(maps))
+    cvr = op == abi.CC_OP_MAP_CONTAINSVALUE
+    assert E.counters()[1] - c0[1] == int(cvr.sum())  # every one answered in the stream
+    assert (gv[cvr] == 1).any() and (gv[cvr] == 0).any()
 
 
 @pytest.mark.parametrize("n,maps,keys,clear_rate,sub_batch,hot,p_hot,seed", [
