@@ -697,11 +697,31 @@ static void mark_dirty(uint64_t& lo, uint64_t& hi, uint64_t a, uint64_t b) {
 }
 
 int cc::dev_flush(cc_engine* e) {
-  for (auto& kv : e->dev_pend)
-    for (auto& w : kv.second) {
-      if (w.fill >= 0) HIPCHECK(hipMemset(w.dst, w.fill, w.bytes));
-      else HIPCHECK(hipMemcpy(w.dst, w.data.data(), w.bytes, hipMemcpyHostToDevice));
+  // A run of consecutive fills of one value is written as its merged intervals (order inside such a run does not
+  // matter; a copy or another value ends it): resources created one by one land in type-pure 64-slot groups, so their
+  // blocks are not adjacent in creation order, and each had cost a fill of its own (~98K fills for c5's 32,768).
+  for (auto& kv : e->dev_pend) {
+    auto& v = kv.second;
+    for (size_t a = 0; a < v.size();) {
+      if (v[a].fill < 0) {
+        HIPCHECK(hipMemcpy(v[a].dst, v[a].data.data(), v[a].bytes, hipMemcpyHostToDevice));
+        ++a;
+        continue;
+      }
+      size_t b = a + 1;
+      while (b < v.size() && v[b].fill == v[a].fill) ++b;
+      std::vector<std::pair<uint8_t*, uint64_t>> iv;  // [dst, dst + bytes)
+      for (size_t k = a; k < b; ++k) iv.push_back({v[k].dst, v[k].bytes});
+      std::sort(iv.begin(), iv.end());
+      for (size_t k = 0; k < iv.size();) {
+        uint8_t* lo = iv[k].first;
+        uint8_t* hi = lo + iv[k].second;
+        for (++k; k < iv.size() && iv[k].first <= hi; ++k) hi = std::max(hi, iv[k].first + iv[k].second);
+        HIPCHECK(hipMemset(lo, v[a].fill, (size_t)(hi - lo)));
+      }
+      a = b;
     }
+  }
   e->dev_pend.clear();
   if (e->res_dirty_hi) {
     HIPCHECK(hipMemcpy(e->d_res_type + e->res_dirty_lo, e->res_type.data() + e->res_dirty_lo,

@@ -180,14 +180,22 @@ __global__ __launch_bounds__(kMwT) void k_map_barriers(const uint32_t* __restric
       for (int q = 0; q < 16; ++q) any |= lut[(w4[q / 4] >> (8 * (q % 4))) & 0xFFu];
     }
     if (__ballot(any != 0) == 0) continue;  // (wave-uniform: the common case)
-    if (any) {  // (rare) the rows again, op bytes re-read from the cache
-      for (uint32_t q = 0; q < (uint32_t)kMwRows; ++q) {
-        const uint64_t i = b0 + (q >> 4) * (16 * kWave) + 16 * l + (q & 15u);
+    if (any) {  // (rare per thread) its candidate rows: a bit mask, then each row's op byte again from the cache
+      uint64_t cm = 0;
+#pragma unroll
+      for (int k = 0; k < kMwLd; ++k) {
+        const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cm |= (uint64_t)lut[(w4[q / 4] >> (8 * (q % 4))) & 0xFFu] << (16 * k + q);
+      }
+      while (cm) {
+        const uint32_t bit = (uint32_t)__ffsll((long long)cm) - 1;
+        cm &= cm - 1;
+        const uint64_t i = b0 + (bit >> 4) * (16 * kWave) + 16 * l + (bit & 15u);
         if (i >= n) continue;
         const uint32_t o = op[i];
-        if (lut[o])
-          map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, ttl_seen, szq != nullptr, mflag, cvq != nullptr,
-                          mfirst, clrq != nullptr, push);
+        map_barrier_row(i, o, inst, aux, inst_res, res_type, max_inst, ttl_seen, szq != nullptr, mflag, cvq != nullptr,
+                        mfirst, clrq != nullptr, push);
       }
     }
   }
