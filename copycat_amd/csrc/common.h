@@ -494,10 +494,9 @@ __device__ inline u64x2 mrec_ab(const MRec& r, const uint64_t* __restrict__ cb, 
 }
 
 // log2(HashMap capacity / 16) after the size peaked at p (resize doubles the table when ++size > 0.75 capacity)
-__host__ __device__ inline uint32_t cap_level(uint64_t p) {
-  uint32_t lv = 0;
-  for (uint64_t thr = 12; p > thr; thr <<= 1) ++lv;
-  return lv;
+__host__ __device__ inline uint32_t cap_level(uint64_t p) {  // the least lv with p <= 12 << lv (closed form)
+  const uint64_t q = (p + 11) / 12;                          // ceil(p / 12): lv = ceil(log2(q))
+  return q <= 1 ? 0u : (uint32_t)(64 - __builtin_clzll(q - 1));
 }
 
 // ---- TTL mode: map timers as size events (map_small.hip) -------------------------------------------------------

@@ -831,73 +831,83 @@ __global__ __launch_bounds__(kMszT) void k_msize_count(const uint16_t* __restric
 
 __device__ inline int32_t msz_net(uint32_t c) { return (int32_t)(c & 0xFFFFu) - (int32_t)(c >> 16); }
 
-constexpr int kMszScanW = 16;                         // waves per scan workgroup = tile chunks
+constexpr int kMszScanW = 16;  // waves per scan workgroup
+constexpr int kMszMaps = 16;   // maps per scan workgroup: lane = map (l % 16) and quarter (l / 16) of its wave's tiles
+constexpr int kMszSub = (kWave / kMszMaps) * kMszScanW;  // tile sub-chunks in log order: (wave, quarter)
 __global__ __launch_bounds__(kMszScanW * kWave) void k_msize_scan(const uint8_t* __restrict__ res_type, uint32_t R,
                                                                  uint32_t tiles, const uint32_t* __restrict__ tcnt,
                                                                  uint32_t* __restrict__ msize, uint32_t* __restrict__ mpcap,
                                                                  uint4* __restrict__ list, uint32_t* __restrict__ list_n) {
-  __shared__ int32_t csum[kMszScanW][kWave];
-  __shared__ uint32_t clv[kMszScanW][kWave];
-  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, m = blockIdx.x * kWave + l;
+  __shared__ int32_t csum[kMszSub][kMszMaps];
+  __shared__ uint32_t clv[kMszSub][kMszMaps];
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, ml = l % kMszMaps, h = l / kMszMaps;
+  const uint32_t m = blockIdx.x * kMszMaps + ml, sc = (kWave / kMszMaps) * w + h;  // this lane's map and sub-chunk
   const bool ok = m < R && is_keyed(res_type[m]);
-  const uint32_t per = (tiles + kMszScanW - 1) / kMszScanW, t0 = min(w * per, tiles), t1 = min(t0 + per, tiles);
-  // chunk w's tiles [t0, t1) in log order (row t of tcnt: coalesced over the lanes); three passes re-read the
-  // rows (16 KB per tile at 4096 maps: L2 / MALL-resident) instead of holding them in registers
+  const uint32_t per = (tiles + kMszSub - 1) / kMszSub, t0 = min(sc * per, tiles), t1 = min(t0 + per, tiles);
+  // sub-chunk sc's tiles [t0, t1) in log order (row t of tcnt: 16 maps' words per quarter-wave), loaded once into
+  // registers, all in flight together, for the three passes below (64 maps per workgroup re-reading the rows per pass
+  // was ~53 us per c3 sub-batch on 64 workgroups)
+  constexpr int kPerMax = kMaxTiles / kMszSub;
   const uint32_t* c = tcnt + m;
+  uint32_t xc[kPerMax];
+#pragma unroll
+  for (int q = 0; q < kPerMax; ++q) xc[q] = ok && t0 + q < t1 ? c[(uint64_t)(t0 + q) * R] : 0u;
   int32_t sum = 0;
-  if (ok) {
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) sum += msz_net(c[(uint64_t)t * R]);
-  }
-  csum[w][l] = sum;
+#pragma unroll
+  for (int q = 0; q < kPerMax; ++q) sum += msz_net(xc[q]);
+  csum[sc][ml] = sum;
   lds_barrier();
   // (mpcap is raised atomically by an overlapped small-map replay on the side stream: an atomic load here; a stale
   // level only lists more tiles for the exact pass, and the CAS merge below keeps the higher one)
   const uint32_t s0 = ok ? msize[m] : 0u, mp = ok ? __hip_atomic_load(&mpcap[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  int64_t start = s0;
-  for (uint32_t q = 0; q < w; ++q) start += csum[q][l];
+  int32_t start = (int32_t)s0;  // (sizes are < 2^31: map_capacity <= 2M live entries)
+  for (uint32_t q = 0; q < sc; ++q) start += csum[q][ml];
   // lower bounds: the highest level every tile's counts prove (with the level reached so far)
   uint32_t lv = mp & ~kMpInexact;
   if (ok) {
-    int64_t s = start;
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t x = c[(uint64_t)t * R];
-      const int64_t fin = s + msz_net(x);
-      if (x) lv = max(lv, cap_level((uint64_t)max(s, fin)));
+    int32_t s = start;
+#pragma unroll
+    for (int q = 0; q < kPerMax; ++q) {
+      const uint32_t x = xc[q];
+      const int32_t fin = s + msz_net(x);
+      if (x) lv = max(lv, cap_level((uint64_t)(int64_t)max(s, fin)));
       s = fin;
     }
   }
-  clv[w][l] = lv;
+  clv[sc][ml] = lv;
   lds_barrier();
-  for (int q = 0; q < kMszScanW; ++q) lv = max(lv, clv[q][l]);
+  uint32_t lr = mp & ~kMpInexact;  // the level proven at this sub-chunk's start: before the sub-batch, and earlier ones
+#pragma unroll 4
+  for (uint32_t q = 0; q < (uint32_t)kMszSub; ++q) {  // (one pass: the values are not kept for a second)
+    const uint32_t x = clv[q][ml];
+    lv = max(lv, x);
+    if (q < sc) lr = max(lr, x);
+  }
   // tiles that may cross a resize threshold above the level proven before them: replayed by k_msize_exact, which
   // also records where each resize happened (the capacity-level timeline of the tree-bin test, common.h)
   uint32_t inexact = 0;
   if (ok) {
-    int64_t s = start;
-    uint32_t lr = mp & ~kMpInexact;  // the level proven at this chunk's start: before the sub-batch, and earlier chunks
-    for (uint32_t q = 0; q < w; ++q) lr = max(lr, clv[q][l]);
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t x = c[(uint64_t)t * R];
-      if ((uint64_t)(s + (x & 0xFFFFu)) > (12ull << lr)) {  // level(p) <= lr  <=>  p <= 12 << lr
+    int32_t s = start;
+#pragma unroll
+    for (int q = 0; q < kPerMax; ++q) {
+      const uint32_t x = xc[q], t = t0 + q;
+      if (t < t1 && (int64_t)s + (int64_t)(x & 0xFFFFu) > (int64_t)(12ull << lr)) {  // level(p) <= lr  <=>  p <= 12 << lr
         const uint32_t k = atomicAdd(list_n, 1u);
         if (k < kMszListCap) list[k] = make_uint4(t, m, (uint32_t)s, 0u);
         else inexact = kMpInexact;
       }
-      const int64_t fin = s + msz_net(x);
-      if (x) lr = max(lr, cap_level((uint64_t)max(s, fin)));
+      const int32_t fin = s + msz_net(x);
+      if (x) lr = max(lr, cap_level((uint64_t)(int64_t)max(s, fin)));
       s = fin;
     }
   }
   lds_barrier();  // every lane read clv
-  clv[w][l] = inexact;
+  clv[sc][ml] = inexact;
   lds_barrier();
-  if (w == 0 && ok) {
-    for (int q = 0; q < kMszScanW; ++q) inexact |= clv[q][l];
+  if (sc == 0 && ok) {
+    for (int q = 0; q < kMszSub; ++q) inexact |= clv[q][ml];
     int64_t total = 0;
-    for (int q = 0; q < kMszScanW; ++q) total += csum[q][l];
+    for (int q = 0; q < kMszSub; ++q) total += csum[q][ml];
     msize[m] = (uint32_t)((int64_t)s0 + total);
     // (merged: an overlapped small-map replay may raise the level meanwhile, map_small.hip)
     for (uint32_t old = mp;;) {
@@ -1012,7 +1022,7 @@ int launch_map_size(const MapSizeArgs& a, hipStream_t st) {
                      a.idx0, a.hh_key, a.hh_val, a.hh_n, a.ev_key, a.ev_val, a.ev_pay, a.ev_cap, a.sm_ctl, a.map_row, a.lo,
                      a.err);
   if (a.map_row) return hipGetLastError() == hipSuccess ? 0 : -1;  // TTL mode: sizes from the events (k_ttl_replay)
-  hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kWave - 1) / kWave), dim3(kMszScanW * kWave), 0, st,
+  hipLaunchKernelGGL(k_msize_scan, dim3((a.max_resources + kMszMaps - 1) / kMszMaps), dim3(kMszScanW * kWave), 0, st,
                      a.res_type, a.max_resources, a.tiles, a.tcnt, a.msize, a.mpcap, a.list, a.list_n);
   hipLaunchKernelGGL(k_msize_exact, dim3(256), dim3(kMszT), 0, st, a.ttab, a.cpos, a.rows, a.sb, a.k0, a.k1, a.sb_hot,
                      a.rst_msz, a.hot, a.hot_n, a.hot_len, a.hot_rpre, a.hot_msz, a.list, a.list_n, a.mpcap, a.lvl_at,
