@@ -135,29 +135,27 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
 #endif
   for (int hq = 0; hq < kXQ; hq += kXQ / CC_PART_EXT_ROUTE_SPLIT) {
     constexpr int H = kXQ / CC_PART_EXT_ROUTE_SPLIT;
-    uint32_t rr[H];
+    uint32_t rr[H], fl[H];
+    uint64_t ky[H];
+    // an engine with maps loads every row's key and flags with its instance (one HBM round trip, not a fourth one
+    // after the instance -> resource -> type gathers; rows that are not keyed ignore them)
 #pragma unroll
     for (int u = 0; u < H; ++u) {
       const uint64_t i = row_of(hq + u);
       rr[u] = i < tile1 ? inst[i] : kNoRes;
+      fl[u] = 0;
+      ky[u] = 0;
+      if (map_bits) {  // (block-uniform)
+        const uint64_t ic = i < tile1 ? i : tile0;
+        fl[u] = flags[ic];
+        ky[u] = ckey[ic];
+      }
     }
 #pragma unroll
     for (int u = 0; u < H; ++u) rr[u] = rr[u] < max_inst ? inst_res[rr[u]] : kNoRes;
     uint32_t ty[H];
 #pragma unroll
     for (int u = 0; u < H; ++u) ty[u] = rr[u] != kNoRes ? res_type[rr[u]] : 0u;
-    uint32_t fl[H];
-    uint64_t ky[H];
-#pragma unroll
-    for (int u = 0; u < H; ++u) {
-      fl[u] = 0;
-      ky[u] = 0;
-      if (is_keyed(ty[u])) {
-        const uint64_t i = row_of(hq + u);
-        fl[u] = flags[i];
-        ky[u] = ckey[i];
-      }
-    }
 #pragma unroll
     for (int u = 0; u < H; ++u) {
       const int q = hq + u;
@@ -479,12 +477,14 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     }
     // write the chunk out run by run (contiguous): k_apply_value records as (meta, operands) columns, map records as
     // one 32-byte MRec (2 pieces), every other record as one 48-byte XRec.  Lanes take consecutive 16-byte pieces
-    // (piece p = part p % 3 of sorted record p / 3), so a wave's store covers a run contiguously; one lane per record
+    // (piece p = part p % np of sorted record p / np), so a wave's store covers a run contiguously; one lane per record
     // (three stores at a 48-byte stride) left every piece its own partial-line write request (WRITE_SIZE 99 B per
-    // commit against 50).
+    // commit against 50).  np = 2 when no record is an XRec (no coordination, no value events): a map record's two
+    // pieces then take two lanes, not three with one idle (c3: the write-out was 37 % of the partition).
     const uint32_t map_lim = sb_hot + (map_bits ? (uint32_t)kHotMax : 0u);  // map regions + hot-key buckets
-    for (uint32_t p = t; p < 3 * nlive; p += kPT) {
-      const uint32_t s = p / 3, part = p - 3 * s;
+    const uint32_t np = (IDS || sbq_base || (ext_flags & kExtValue)) ? 3u : 2u;  // (block-uniform)
+    for (uint32_t p = t; p < np * nlive; p += kPT) {
+      const uint32_t s = np == 2u ? p >> 1 : p / 3, part = p - np * s;
       const uint32_t k = rsb[s];
       const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
       if (k < sb_val && !skind[k]) {
