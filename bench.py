@@ -179,17 +179,24 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def c3_whole_map_rows(part, lo, cv_rate, clear_rate, seed):
+def c3_whole_map_rows(part, lo, cv_rate, clear_rate, seed, null_rate=0.0, delete_rate=0.0):
     """The whole-map variant of c3: in a generated block, a share cv_rate of the rows become
     MapState.containsValue rows whose operand is the value a put of the block stored a little earlier (same map: the
-    row takes that put's instance; many answers are true), and a share clear_rate become MapState.clear rows.
-    Deterministic per (seed, block start): the parity gate regenerates the same rows."""
+    row takes that put's instance; many answers are true), and a share clear_rate become MapState.clear rows.  The
+    barrier variant adds null-valued puts (null_rate of the rows: a containsValue row on a map that
+    may hold a null is a barrier, answered in HashMap order, MapState.java:49-60) and ResourceStateMachine.Delete rows
+    (delete_rate: MapState.delete :264-274, a barrier).  Deterministic per (seed, block start): the parity gate
+    regenerates the same rows."""
     from copycat_amd import abi
 
-    if not cv_rate and not clear_rate:
+    if not cv_rate and not clear_rate and not null_rate and not delete_rate:
         return
     rng = np.random.default_rng([seed, lo])
     n = len(part)
+    if null_rate:  # puts that store a null (value tag NULL)
+        nr = np.nonzero(rng.random(n) < null_rate)[0]
+        nr = nr[part.op[nr] == abi.CC_OP_MAP_PUT]
+        part.flags[nr] = part.flags[nr] & np.uint8(0xF8)
     if cv_rate:
         rows = np.nonzero(rng.random(n) < cv_rate)[0]
         puts = np.nonzero(part.op == abi.CC_OP_MAP_PUT)[0]
@@ -205,9 +212,14 @@ def c3_whole_map_rows(part, lo, cv_rate, clear_rate, seed):
         cl = np.nonzero(rng.random(n) < clear_rate)[0]
         cl = cl[part.op[cl] != abi.CC_OP_MAP_CONTAINSVALUE]
         part.op[cl] = abi.CC_OP_MAP_CLEAR
+    if delete_rate:
+        dl = np.nonzero(rng.random(n) < delete_rate)[0]
+        dl = dl[part.op[dl] != abi.CC_OP_MAP_CONTAINSVALUE]
+        part.op[dl] = abi.CC_OP_DELETE
 
 
-def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26, cv_rate=0.0, clear_rate=0.0):
+def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26, cv_rate=0.0, clear_rate=0.0, null_rate=0.0,
+              delete_rate=0.0):
     """Config-3 stream generated block by block on the host and copied into HBM-resident columns.
     Returns (host Batch of the first keep_host rows for the CPU baseline, DeviceBatch)."""
     from copycat_amd.batch import Batch
@@ -225,7 +237,7 @@ def upload_c3(n, maps, pairs, zipf, rank, dev, keep_host, block=1 << 26, cv_rate
         m = min(block, n - lo)
         part = host if m == len(host) else Batch(m)
         map_zipf_rows(lo, m, maps=maps, pairs=pairs, s=zipf, seed=SEED_C3 + rank, threads=threads, out=part)
-        c3_whole_map_rows(part, lo, cv_rate, clear_rate, SEED_C3 + rank)
+        c3_whole_map_rows(part, lo, cv_rate, clear_rate, SEED_C3 + rank, null_rate, delete_rate)
         if lo == 0:
             keep = part.slice(0, min(keep_host, m))
         for k in names:
@@ -670,7 +682,7 @@ def c3_full_gate(n, R, args, rank, status0, value0, gpu_tab, block=1 << 26):
             m = min(block, n - lo)
             b = host if m == len(host) else Batch(m)
             map_zipf_rows(lo, m, maps=R, pairs=args.pairs, s=args.zipf, seed=SEED_C3 + rank, threads=threads, out=b)
-            c3_whole_map_rows(b, lo, args.cv_rate, args.clear_rate, SEED_C3 + rank)
+            c3_whole_map_rows(b, lo, args.cv_rate, args.clear_rate, SEED_C3 + rank, args.null_rate, args.delete_rate)
             own = (b.inst % threads).astype(np.uint16)
             order = np.argsort(own, kind="stable")
             cuts = np.searchsorted(own[order], np.arange(threads + 1))
@@ -887,7 +899,7 @@ def c3_subrecord(args, dev):
     import argparse as _ap
 
     a = _ap.Namespace(**vars(args))
-    a.cv_rate = a.clear_rate = 0.0
+    a.cv_rate = a.clear_rate = a.null_rate = a.delete_rate = 0.0
     a.pairs, a.zipf, a.sub_batch, a.cpu_sample = 1 << 20, 0.99, 0, 20_000_000
     t = time.time()
     out, bad = measure_c3(a, dev, 0, 1, None, 1_000_000_000, 3, 1, 4096)
@@ -1058,7 +1070,7 @@ def measure_c3(args, dev, rank, world, dist, n, steps, warmup, R):
     cpu_sample = args.cpu_sample or 20_000_000
     t_gen = time.time()
     batch, db = upload_c3(n, R, args.pairs, args.zipf, rank, dev, keep_host=min(n, cpu_sample), cv_rate=args.cv_rate,
-                          clear_rate=args.clear_rate)
+                          clear_rate=args.clear_rate, null_rate=args.null_rate, delete_rate=args.delete_rate)
     t_gen = time.time() - t_gen
     status = torch.full((n,), RESULT_SENTINEL, dtype=torch.uint8, device=dev)  # sentinel: unwritten rows show
     value = torch.full((n,), -1, dtype=torch.int64, device=dev)
@@ -1111,8 +1123,8 @@ def measure_c3(args, dev, rank, world, dist, n, steps, warmup, R):
         elapsed = float(t.item())
     prof = E.profile_read() if not args.no_profile else {}
     ms_per_step = elapsed * 1e3 / steps
-    roofline = roofline_step(prof, "c3" + ("w" if args.cv_rate or args.clear_rate else ""), n, steps, ms_per_step,
-                             B_OP_C3)
+    variant = "b" if args.null_rate or args.delete_rate else ("w" if args.cv_rate or args.clear_rate else "")
+    roofline = roofline_step(prof, "c3" + variant, n, steps, ms_per_step, B_OP_C3)
     cpu = parity = cpu_all = None
     if rank == 0 and (not args.no_parity or (world == 1 and not args.no_cpu_baseline)):
         from oracle.oracle_py import Oracle
@@ -1144,11 +1156,14 @@ def measure_c3(args, dev, rank, world, dist, n, steps, warmup, R):
                                     f"(map, key) pairs in {R:,} MapState resources, {n:,} committed entries per GPU"
                                     + (f"; whole-map variant: {args.cv_rate:.2%} containsValue (operands stored shortly "
                                        f"before), {args.clear_rate:.3%} clear"
-                                       if args.cv_rate or args.clear_rate else "")),
+                                       if args.cv_rate or args.clear_rate else "")
+                                    + (f"; barrier variant: {args.null_rate:.2%} null-valued puts, {args.delete_rate:.4%} "
+                                       f"Delete" if args.null_rate or args.delete_rate else "")),
                        "whole_map": ({"containsValue_rate": args.cv_rate, "clear_rate": args.clear_rate,
+                                      "null_put_rate": args.null_rate, "delete_rate": args.delete_rate,
                                       "engine_counters": dict(zip(("barrier_rows", "in_stream_containsValue",
                                                                    "sub_batches", "map_events"), E.counters()))}
-                                     if args.cv_rate or args.clear_rate else None),
+                                     if args.cv_rate or args.clear_rate or args.null_rate or args.delete_rate else None),
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]},
@@ -1220,6 +1235,8 @@ def main():
     ap.add_argument("--zipf", type=float, default=0.99, help="c3: Zipf exponent of the pair rank (0 = uniform)")
     ap.add_argument("--cv-rate", type=float, default=0.0, help="c3 whole-map variant: share of containsValue rows")
     ap.add_argument("--clear-rate", type=float, default=0.0, help="c3 whole-map variant: share of clear rows")
+    ap.add_argument("--null-rate", type=float, default=0.0, help="c3 barrier variant: share of null-valued put rows")
+    ap.add_argument("--delete-rate", type=float, default=0.0, help="c3 barrier variant: share of Delete rows")
     ap.add_argument("--sub-batch", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=0, help="c3: 20M, c5: 10M (c2 uses step 0's rows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
