@@ -111,6 +111,7 @@ static void free_all(cc_engine* e) {
   if (e->d_hh_key) (void)hipFree(e->d_hh_key);
   if (e->d_hh_val) (void)hipFree(e->d_hh_val);
   if (e->h_pin) (void)hipHostFree(e->h_pin);
+  if (e->d_ckpt) (void)hipFree(e->d_ckpt);
   if (e->side_st) (void)hipStreamSynchronize(e->side_st);
   void* alt[] = {e->sm_alt.key, e->sm_alt.key2, e->sm_alt.val, e->sm_alt.val2, e->sm_alt.pay, e->sm_alt.cseg};
   for (void* p : alt)
@@ -2794,6 +2795,70 @@ static std::vector<Section> snap_sections(cc_engine* e) {
   }
   if (e->coord_on) v.push_back({e->d_coord, nullptr, coord_block(e->coord_cap) * slots});
   return v;
+}
+
+// ---- the prefix apply's checkpoint (host_path.hip cc_apply_batch_host_prefix) -------------------------------------
+// The device sections of a snapshot (the state every batch apply may write), the applied index and the leak log's
+// count, copied device to device into one engine-owned buffer; the host fields a batch moves beside them.
+static std::vector<Section> ckpt_sections(cc_engine* e) {
+  std::vector<Section> v;
+  for (const Section& x : snap_sections(e))
+    if (x.dev) v.push_back(x);
+  v.push_back({e->d_last_index, nullptr, sizeof(uint64_t)});
+  if (e->d_leak_n) v.push_back({e->d_leak_n, nullptr, sizeof(unsigned long long)});
+  return v;
+}
+
+int cc::ckpt_save(cc_engine* e) {
+  int rc = quiesce(e);
+  if (rc) return rc;
+  const auto secs = ckpt_sections(e);
+  uint64_t need = 0;
+  for (const Section& x : secs) need += (x.bytes + 255) & ~255ull;
+  if (need > e->ckpt_bytes) {
+    if (e->d_ckpt) HIPCHECK(hipFree(e->d_ckpt));
+    e->d_ckpt = nullptr;
+    e->ckpt_bytes = 0;
+    HIPCHECK(hipMalloc(&e->d_ckpt, need));
+    e->ckpt_bytes = need;
+  }
+  uint8_t* p = (uint8_t*)e->d_ckpt;
+  for (const Section& x : secs) {
+    HIPCHECK(hipMemcpyAsync(p, x.dev, x.bytes, hipMemcpyDeviceToDevice, e->last_stream));
+    p += (x.bytes + 255) & ~255ull;
+  }
+  HIPCHECK(hipStreamSynchronize(e->last_stream));
+  e->ckpt.applied = e->applied;
+  e->ckpt.applied_pending = e->applied_pending;
+  e->ckpt.ttl_live = e->ttl_live;
+  e->ckpt.small_live = e->small_live;
+  e->ckpt.gtimers = e->gtimers;
+  e->ckpt.gtimer_seq = e->gtimer_seq;
+  e->ckpt.leaks = e->leaks;
+  return CC_OK;
+}
+
+int cc::ckpt_restore(cc_engine* e) {
+  (void)hipStreamSynchronize(e->last_stream);  // (a failed call may have left work queued)
+  if (e->side_st) (void)hipStreamSynchronize(e->side_st);
+  uint8_t* p = (uint8_t*)e->d_ckpt;
+  for (const Section& x : ckpt_sections(e)) {
+    HIPCHECK(hipMemcpyAsync(x.dev, p, x.bytes, hipMemcpyDeviceToDevice, e->last_stream));
+    p += (x.bytes + 255) & ~255ull;
+  }
+  HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), e->last_stream));
+  if (e->map_bits) HIPCHECK(hipMemsetAsync(e->d_msm_left, 0, 3ull * e->cfg.max_resources, e->last_stream));
+  HIPCHECK(hipStreamSynchronize(e->last_stream));
+  e->applied = e->ckpt.applied;
+  e->applied_pending = e->ckpt.applied_pending;
+  e->ttl_live = e->ckpt.ttl_live;
+  e->small_live = e->ckpt.small_live;
+  e->gtimers = e->ckpt.gtimers;
+  e->gtimer_seq = e->ckpt.gtimer_seq;
+  e->leaks = e->ckpt.leaks;
+  e->rep_pending[0] = e->rep_pending[1] = false;
+  e->pend = false;
+  return CC_OK;
 }
 
 static uint64_t leak_entries(const cc_engine* e) {

@@ -26,6 +26,10 @@ int open_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t res_first,
                uint64_t client);
 int delete_slot(cc_engine* e, uint32_t slot);
 int drain_leaks(cc_engine* e);  // the device leak log -> cc_engine::leaks
+// a device checkpoint of the state a batch apply writes (engine.hip; synchronous): saved before an attempt of the
+// prefix apply, restored when the attempt failed on a fixed capacity
+int ckpt_save(cc_engine* e);
+int ckpt_restore(cc_engine* e);
 
 // Occupancy bitmap of a slot space with lowest-free / highest-free search (control-plane allocation: rare, so a
 // word scan from a hint is enough).
@@ -324,9 +328,20 @@ struct cc_engine {
   std::map<uint32_t, std::vector<uint64_t>> leaks;  // ordered: snapshots are byte-deterministic
   uint64_t applied = 0;
   bool applied_pending = false;
-  uint32_t last_err_bits = 0;
+  uint32_t last_err_bits = 0;        // the device error bits the last check_device_err read (common.h kErr*)
   bool span_cut = false;             // this batch's index range passes 2^32: sub-batches are cut at k_span_cut's row
-  uint64_t* d_span_cut = nullptr;  // the device error bits the last check_device_err read (common.h kErr*)
+  uint64_t* d_span_cut = nullptr;
+  // the prefix apply's device checkpoint (cc_apply_batch_host_prefix): every device section the data path writes, as
+  // one device-to-device copy, and the host fields it moves
+  void* d_ckpt = nullptr;
+  uint64_t ckpt_bytes = 0;
+  struct Ckpt {
+    uint64_t applied = 0;
+    bool applied_pending = false, ttl_live = false, small_live = false;
+    std::vector<GroupTimer> gtimers;
+    uint64_t gtimer_seq = 0;
+    std::map<uint32_t, std::vector<uint64_t>> leaks;
+  } ckpt;
   uint64_t* d_last_index = nullptr;  // index[n-1] of the last batch (device copy)
   // device staging of the host-memory entry points (host_path.hip): grown on demand, kept between calls
   void* hw_buf[24] = {};

@@ -101,12 +101,15 @@ int hw_events_back(cc_engine* e, const cc_events* h, const cc_events* d) {
     HIPCHECK(hipMemcpyAsync(h->payload, d->payload, 8 * m, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
   }
-  return cnt > h->capacity ? set_err(CC_ERR_CAPACITY, "more events than the host event stream holds") : CC_OK;
+  if (cnt <= h->capacity) return CC_OK;
+  e->last_err_bits |= kErrEvents;  // (cc_apply_batch_host_prefix: a full event stream, like a full max_events arena)
+  return set_err(CC_ERR_CAPACITY, "more events than the host event stream holds");
 }
 
 int apply_host(cc_engine* e, const cc_batch* h, uint64_t n, const cc_results* hout, const cc_events* hev) {
   if (!e || !h || !hout || (n && (!hout->status || !hout->value))) return set_err(CC_ERR_INVALID, "null argument");
   HIPCHECK(hipSetDevice(e->device));
+  e->last_err_bits = 0;
   hipStream_t st = e->own_stream;
   if (st != e->last_stream) HIPCHECK(hipStreamSynchronize(e->last_stream));
   e->last_stream = st;
@@ -235,12 +238,73 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
     if (hev) *hev->count = ev_n;
     return rc;
   };
-  if (!e->coord_on) {  // no coordination collection to overflow: one call
-    const int rc = n ? apply_part(e, h, 0, n, hout, hev, &ev_n) : CC_OK;
+  HIPCHECK(hipSetDevice(e->device));
+  // Rows [lo, hi) as one part.  On an engine with maps or with an event stream, a part may also fail on a full map
+  // table region or a full event stream (kErrCapacity / kErrEvents, and nothing else): the state before the part is a
+  // device checkpoint (ckpt_save), and the longest prefix of the part that applies is found by bisection (restore, apply
+  // [lo, mid)); the state is then the one after that prefix, its results and events written, the rows after it keep
+  // what the caller had there.  *done = the first row not applied (hi on success).
+  const bool ck = e->map_bits != 0 || hev != nullptr;
+  auto cap_only = [&](int rc) {
+    const uint32_t b = e->last_err_bits;
+    return rc == CC_ERR_CAPACITY && b && !(b & ~(kErrCapacity | kErrEvents));
+  };
+  auto attempt = [&](uint64_t lo, uint64_t hi, uint64_t* done) -> int {
+    *done = lo;
+    if (!ck) {
+      const int rc = apply_part(e, h, lo, hi, hout, hev, &ev_n);
+      if (!rc) *done = hi;
+      return rc;
+    }
+    std::vector<uint8_t> s0(hout->status + lo, hout->status + hi);  // (the caller's rows, for the rows not applied)
+    std::vector<uint64_t> v0(hout->value + lo, hout->value + hi);
+    const uint64_t ev0 = ev_n;
+    int rc = ckpt_save(e);
+    if (rc) return rc;
+    rc = apply_part(e, h, lo, hi, hout, hev, &ev_n);
+    if (!rc) {
+      *done = hi;
+      return CC_OK;
+    }
+    if (!cap_only(rc)) return rc;
+    uint64_t good = lo, bad = hi;  // [lo, good) applies, [lo, bad) does not
+    bool at_good = false;          // the engine's state is the one after [lo, good)
+    while (bad - good > 1) {
+      const uint64_t mid = good + (bad - good) / 2;
+      if ((rc = ckpt_restore(e))) return rc;
+      ev_n = ev0;
+      rc = apply_part(e, h, lo, mid, hout, hev, &ev_n);
+      if (!rc) {
+        good = mid;
+        at_good = true;
+      } else if (cap_only(rc)) {
+        bad = mid;
+        at_good = false;
+      } else {
+        return rc;
+      }
+    }
+    if (!at_good) {
+      if ((rc = ckpt_restore(e))) return rc;
+      ev_n = ev0;
+      if (good > lo && (rc = apply_part(e, h, lo, good, hout, hev, &ev_n))) return rc;
+    }
+    std::copy(s0.begin() + (good - lo), s0.end(), hout->status + good);
+    std::copy(v0.begin() + (good - lo), v0.end(), hout->value + good);
+    *done = good;
+    return CC_ERR_CAPACITY;
+  };
+  auto full = [&](uint64_t row) {
+    *h_applied = row;
+    return finish(set_err(CC_ERR_CAPACITY, "a map table region or the event stream is full: *applied rows were applied"));
+  };
+  if (!e->coord_on) {  // no coordination collection to overflow: one part
+    uint64_t done = 0;
+    const int rc = n ? attempt(0, n, &done) : CC_OK;
+    if (rc == CC_ERR_CAPACITY && done < n) return full(done);
     if (!rc) *h_applied = n;
     return finish(rc);
   }
-  HIPCHECK(hipSetDevice(e->device));
   const uint32_t max_inst = e->cfg.max_instances;
   auto res_of = [&](uint64_t i) -> uint32_t {
     const uint32_t in = h->inst[i];
@@ -290,7 +354,9 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
       ++b;
     }
     if (stop > pos) {
-      const int rc = apply_part(e, h, pos, stop, hout, hev, &ev_n);
+      uint64_t done = pos;
+      const int rc = attempt(pos, stop, &done);
+      if (rc == CC_ERR_CAPACITY && done < stop) return full(done);
       if (rc) return finish(rc);
       pos = stop;
       *h_applied = pos;
@@ -319,7 +385,9 @@ extern "C" int cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h, uint6
     const uint64_t ev0 = ev_n;
     const uint8_t st0 = hout->status[pos];
     const uint64_t va0 = hout->value[pos];
-    const int rc = apply_part(e, h, pos, pos + 1, hout, hev, &ev_n);
+    uint64_t done1 = pos;
+    const int rc = attempt(pos, pos + 1, &done1);
+    if (rc == CC_ERR_CAPACITY && e->last_err_bits != kErrCoordFull) return full(pos);
     // (only a full coordination collection, and nothing else, is rolled back: any other failure is returned as is)
     if (rc == CC_ERR_CAPACITY && e->last_err_bits == kErrCoordFull) {
       hout->status[pos] = st0;  // (the row is not applied: its result row keeps what the caller had there)

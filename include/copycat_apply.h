@@ -529,7 +529,11 @@ int  cc_wire_decode(cc_engine* e, const cc_wire_codec* codec, cc_wire_interner* 
  * state is exactly the state after rows [0, *h_applied), the events of those rows are in h_events, and rows from
  * *h_applied on are not applied (their result rows keep what the caller put there).  The host resumes at that row
  * (e.g. on an engine with a larger coord_cap restored from a snapshot, or treating the commit as failed).  On success
- * *h_applied = n.  Other fixed capacities (a map table region, max_events) fail the call as cc_apply_batch does. */
+ * *h_applied = n.  Round 6: the same holds for a row whose map / set / multimap entry a full table region cannot
+ * hold, and for a row whose events do not fit h_events' capacity (or max_events): the engine takes a device
+ * checkpoint before each part of the batch and, when a part fails on one of those capacities, restores it and
+ * applies the longest prefix that fits (bisection), so *h_applied is exactly that row and the state, results and
+ * events are those after the rows before it.  A host with a full event stream drains it and resumes at that row. */
 int  cc_apply_batch_host_prefix(cc_engine* e, const cc_batch* h_cols, uint64_t n, const cc_results* h_out,
                                 const cc_events* h_events, uint64_t* h_applied);
 
