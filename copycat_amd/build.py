@@ -11,8 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 
-ENGINE_SRCS = ["engine.hip", "partition.hip", "partition_ext.hip", "apply_value.hip", "value_path.hip", "apply_map.hip", "apply_map_hot.hip", "apply_coord.hip", "events.hip", "quorum.hip", "close.hip", "map_wide.hip", "live.hip", "manager.hip", "retained.hip", "host_path.hip", "map_small.hip", "map_cv.hip", "map_clear.hip", "wire.cpp", "split.cpp"]
-ENGINE_HDRS = ["common.h", "engine_internal.h", "engine_state.h", "map_ops.h", "java_hashmap.h", "small_jhm.h"]
+ENGINE_SRCS = ["engine.hip", "map_big.hip", "partition.hip", "partition_ext.hip", "apply_value.hip", "value_path.hip", "apply_map.hip", "apply_map_hot.hip", "apply_coord.hip", "events.hip", "quorum.hip", "close.hip", "map_wide.hip", "live.hip", "manager.hip", "retained.hip", "host_path.hip", "map_small.hip", "map_cv.hip", "map_clear.hip", "wire.cpp", "split.cpp"]
+ENGINE_HDRS = ["common.h", "engine_internal.h", "engine_state.h", "map_ops.h", "java_hashmap.h", "small_jhm.h", "jhm_tree.h", "big_jhm.h"]
 ENGINE_SO = os.path.join(HERE, "libcopycat_apply.so")
 WORKLOAD_SO = os.path.join(HERE, "libcopycat_workload.so")
 ARCH = os.environ.get("CC_OFFLOAD_ARCH", "gfx950")

@@ -438,7 +438,7 @@ __device__ inline uint64_t tbl_find(const uint32_t* __restrict__ word, const uin
 // node for node here; after the window (capacity 128) such a bin's order is no longer followed (tree_bins, sticky).
 constexpr uint32_t kSmNodes = 64;
 struct SmallMap {
-  uint32_t n, lvl, flags, pad;
+  uint32_t n, lvl, flags, pad;  // (pad: the big model's slot while kSmBig; see kSmBigNew)
   uint64_t tree_bins;
   uint64_t used;            // node pool occupancy
   uint32_t jh[kSmNodes];    // node: the key's HashMap hash
@@ -455,6 +455,40 @@ constexpr uint32_t kSmTree = 2u;     // a bin became a tree bin since the last c
 constexpr uint32_t kSmUnknown = 4u;  // tracking stopped while small (kept for the snapshot format; never set now)
 constexpr uint32_t kSmAmbig = 8u;    // a tree order the engine cannot know (two String keys with one hash in a tree bin;
                                      // a removal of a key the model does not hold): an order-dependent answer refuses
+constexpr uint32_t kSmBig = 16u;     // the table left the window with a tree bin: followed node for node by a big model
+                                     // (BigMap, big_jhm.h; SmallMap::pad is its slot)
+constexpr uint32_t kSmBigNew = 32u;  // ... from this sub-batch's replay on: the small model's nodes are still here, and
+                                     // SmallMap::pad is the position of the event that grew the table
+
+// A map's java.util.HashMap after its table left the small window (capacity 128 and up) with a tree bin since its
+// last clear (big_jhm.h, map_big.hip): every bin followed node for node, tree bins through HashMap.resize's
+// TreeNode.split, so an order-dependent containsValue there is answered instead of refused.  An engine holds
+// kBigSlots of them; a map that finds none free, or outgrows one (kBigNodes live keys, capacity 16 << kBigMaxLvl),
+// falls back to the bounds of map_wide.hip k_mw_order (which refuse such an answer).
+constexpr uint32_t kBigSlots = 16;
+constexpr uint32_t kBigNodes = 4096;
+constexpr uint32_t kBigMaxLvl = 9;  // capacity 8,192
+constexpr uint32_t kBigTab = 16u << kBigMaxLvl;
+struct BigNode {
+  uint64_t key;
+  uint32_t jh;                  // the key's HashMap hash
+  uint16_t nx, pv, pa, lf, rt;  // links: node + 1 (0 = null)
+  uint8_t nb, kt;               // bit 0 TreeNode, bit 1 red; the key's tag
+};
+struct BigHdr {
+  uint32_t owner;  // map slot + 1 (0: free)
+  uint32_t n, lvl, flags;
+  uint32_t top;    // nodes [1, top] handed out so far
+  uint32_t free;   // released nodes, linked through nx
+  unsigned long long resume;  // kBigResume: the position of the event at which the map left the window
+};
+struct BigMap {
+  BigHdr h;
+  uint16_t tab[kBigTab];  // bin heads: node + 1
+  BigNode nd[kBigNodes];
+};
+constexpr uint32_t kBigResume = 0x100u;  // BigHdr::flags: converted from the small model this sub-batch, before its
+                                         // resize to 128; events up to `resume` were applied by the small replay
 // per-map flags of the batch (cc_engine::d_msmall), written on the engine stream only: bit 0 the table is small (events
 // followed key by key; a SNAPSHOT of the small-map models' kSmIn, see below), bit 1 the
 // batch asks the map's size / isEmpty (events followed for the in-stream answers); either makes every insertion /
@@ -515,8 +549,9 @@ constexpr uint64_t kEvPosMask = (1ull << kEvPosBits) - 1;
 struct EvPay {
   uint64_t key;   // the key (its tag in ktag): a small map's model tells keys with one hash apart by them
   uint32_t aux;
-  uint32_t ktag;
+  uint32_t ktag;  // the key's tag (bits 0-1); at an alternating run's first removal, the events it implies << kSkipShift
 };
+constexpr uint32_t kSkipShift = 4;  // (map_small.hip k_small_chains)
 struct TtlEmit {
   const uint64_t* time;   // the batch's time column (null: the clock is clock_before throughout)
   uint64_t n;             // rows in the batch

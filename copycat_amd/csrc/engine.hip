@@ -97,7 +97,7 @@ static void free_all(cc_engine* e) {
                   e->d_bar,      e->d_bar_n,    e->d_mw_peak,   e->d_mw_drop,   e->d_mw_ctl,    e->d_mw_cgen, e->d_cset, e->d_cset_full, e->d_tbl_claim, e->d_lvl_at, e->d_half_count,
                   e->d_tbl_dl,   e->d_map_row,  e->d_ttl_seen, e->d_val_live, e->d_val_wrow,
                   e->d_leak,     e->d_leak_n,   e->d_ev_bucket, e->d_ev_ccnt, e->d_rst_msz, e->d_hot_msz, e->d_msize,
-                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_msmall,  e->d_msm_left, e->d_span_cut,
+                  e->d_mpcap,    e->d_msz_tcnt, e->d_msz_list, e->d_msz_list_n, e->d_msm,     e->d_mbig,     e->d_msmall,  e->d_msm_left, e->d_span_cut,
                   e->d_sm_ctl,   e->d_sm_key,   e->d_sm_key2,  e->d_sm_val,   e->d_sm_val2,    e->d_sm_seg, e->d_sm_temp, e->d_sm_pay,
                   e->d_szq,      e->d_szq_n,    e->d_mrec,    e->d_bar_rows, e->d_fb,
                   e->d_cvq,      e->d_cvq_n,    e->d_isc,     e->d_isc2,     e->d_mfirst,     e->d_maynull, e->d_cv_rtemp,
@@ -495,6 +495,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     ALLOC(e->d_lvl_at, sizeof(unsigned long long) * kLvlSlots * cfg->max_resources);
     ALLOC(e->d_mw_ctl, sizeof(unsigned long long) * 64);
     ALLOC(e->d_msm, sizeof(SmallMap) * cfg->max_resources);
+    ALLOC(e->d_mbig, sizeof(BigMap) * kBigSlots);
     ALLOC(e->d_msmall, (cfg->max_resources + 3) & ~3u);  // (padded to whole words: common.h mflag_or)
     ALLOC(e->d_msm_left, 3ull * cfg->max_resources);
     ALLOC(e->d_span_cut, sizeof(uint64_t));
@@ -563,6 +564,7 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
     if ((he = hipMemset(e->d_msize, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_mpcap, 0, sizeof(uint32_t) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msm, 0, sizeof(SmallMap) * cfg->max_resources)) != hipSuccess) return fail("memset", he);
+    if ((he = hipMemset(e->d_mbig, 0, sizeof(BigMap) * kBigSlots)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msmall, 0, cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_msm_left, 0, 3ull * cfg->max_resources)) != hipSuccess) return fail("memset", he);
     if ((he = hipMemset(e->d_sm_ctl, 0, sizeof(uint32_t) * 4)) != hipSuccess) return fail("memset", he);
@@ -724,6 +726,11 @@ int cc::dev_flush(cc_engine* e) {
     }
   }
   e->dev_pend.clear();
+  for (const auto& r : e->big_rel) {  // (the new maps' slots: a big model of the map deleted from one is freed)
+    if (launch_big_release(e->d_mbig, r.first, r.second, nullptr)) return set_err(CC_ERR_HIP, "big-model release", hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(nullptr));
+  }
+  e->big_rel.clear();
   if (e->res_dirty_hi) {
     HIPCHECK(hipMemcpy(e->d_res_type + e->res_dirty_lo, e->res_type.data() + e->res_dirty_lo,
                        e->res_dirty_hi - e->res_dirty_lo, hipMemcpyHostToDevice));
@@ -791,6 +798,7 @@ int cc::create_range(cc_engine* e, uint32_t first, uint32_t count, uint32_t type
     const bool is_map = type == CC_RES_MAP;
     for (auto& x : sm) x.flags = is_map ? kSmIn : 0u;  // (TTL mode too: its commit + expiry events are replayed)
     dev_copy(e, e->d_msm, sizeof(SmallMap) * first, sm.data(), sizeof(SmallMap) * count);
+    if (e->d_mbig) e->big_rel.push_back({first, count});
     dev_fill(e, e->d_msmall, first, is_map ? 1 : 0, count);
     if (is_map && !e->ttl_live) {
       e->small_live = true;
@@ -967,6 +975,7 @@ static int ttl_replay(cc_engine* e, hipStream_t st, const uint64_t* index = null
   sa.seg = e->d_sm_seg;
   sa.nseg = e->d_sm_seg + e->cfg.max_resources;
   sa.state = e->d_msm;
+  sa.big = e->d_mbig;
   sa.msmall = e->d_msmall;
   sa.left = e->d_msm_left + 2ull * e->cfg.max_resources;  // (an engine-stream replay: folded right after it)
   sa.err = e->d_err;
@@ -1846,6 +1855,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
           sa.nseg = e->d_sm_seg + e->cfg.max_resources;
           sa.cseg = e->d_sm_cseg;
           sa.state = e->d_msm;
+          sa.big = e->d_mbig;
           sa.msmall = e->d_msmall;
           sa.left = e->d_msm_left + 2ull * e->cfg.max_resources;  // (on this stream: folded right after it)
           sa.err = e->d_err;
@@ -2084,6 +2094,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.mpcap = e->d_mpcap;
     mw.ctl = e->d_mw_ctl;
     mw.small = e->res_type[res] == CC_RES_MAP ? e->d_msm : nullptr;
+    mw.big = e->d_mbig;
     mw.hh_key = e->d_hh_key;
     mw.hh_val = e->d_hh_val;
     mw.hh_n = e->hh_n;
@@ -2092,7 +2103,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
     mw.err = e->d_err;
     if (launch_map_wide(mw, st)) return set_err(CC_ERR_HIP, "whole-map op launch", hipGetLastError()); DBG_SYNC("whole-map op launch");
     if (e->res_type[res] == CC_RES_MAP && (mw.op == CC_OP_MAP_CLEAR || mw.op == CC_OP_DELETE) &&
-        launch_small_clear(e->d_msm, res, st))
+        (launch_big_clear(e->d_mbig, e->d_msm, res, st) || launch_small_clear(e->d_msm, res, st)))
       return set_err(CC_ERR_HIP, "small-map clear launch", hipGetLastError());
   }
   }
@@ -2736,7 +2747,7 @@ static const char* kKernelNames[K_NUM] = {"k_part_tile", "k_apply_value", "k_unp
 // Layout: SnapHdr, then the sections below in order, each a u64 byte count followed by the bytes.  Host
 // mirrors travel with the device arrays so a fresh engine of the same configuration resumes exactly.
 namespace {
-constexpr uint64_t kSnapMagic = 0x36304E5053434343ull;  // "CCCSPN06"
+constexpr uint64_t kSnapMagic = 0x37304E5053434343ull;  // "CCCSPN07"
 constexpr uint32_t kSnapRetained = 4u;                   // SnapHdr.flags: CC_CFG_VALUE_RETAINED section present
 struct SnapHdr {
   uint64_t magic;
@@ -2791,6 +2802,7 @@ static std::vector<Section> snap_sections(cc_engine* e) {
     v.push_back({e->d_msize, nullptr, 4 * mr});
     v.push_back({e->d_mpcap, nullptr, 4 * mr});
     v.push_back({e->d_msm, nullptr, sizeof(SmallMap) * mr});
+    v.push_back({e->d_mbig, nullptr, sizeof(BigMap) * kBigSlots});
     v.push_back({e->d_msmall, nullptr, mr});
   }
   if (e->coord_on) v.push_back({e->d_coord, nullptr, coord_block(e->coord_cap) * slots});

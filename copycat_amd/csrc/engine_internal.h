@@ -204,6 +204,7 @@ struct SmallArgs {
   uint8_t* out_status;         // TTL mode: the size / isEmpty rows among the events are answered here (else null)
   uint64_t* out_value;
   SmallMap* state;             // [max_resources]
+  BigMap* big;                 // [kBigSlots] the models of maps that left the window with a tree bin (null: none)
   uint8_t* msmall;             // the engine stream's snapshot of the window (common.h): read, never written, by the replay
   uint8_t* left;               // [max_resources] the replay's exit marks (one buffer per event-buffer set), folded by
                                // launch_small_fold on the engine stream after it waited for the replay
@@ -224,6 +225,14 @@ int launch_ttl_scan(const TtlEmit& t, const uint64_t* clock_base, const uint32_t
 // sort, runs, replay (E events); the replay kernel itself on stream rst (after a.ev_prep, when rst != st)
 int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStream_t rst);
 int launch_small_replay_kernel(const SmallArgs& a, hipStream_t rst);
+// map_big.hip: the big models' replay, over the same events as the small replay (orig: compacted positions, else
+// every event; cnt: the event count; seg / nseg: the runs), on the small replay's stream after it
+int launch_big_replay(const SmallArgs& a, const uint32_t* orig, const uint32_t* cnt, const uint32_t* seg,
+                      const uint32_t* nseg, hipStream_t rst);
+// a whole-map barrier's clear / Delete of map m on its big model
+int launch_big_clear(BigMap* big, const SmallMap* state, uint32_t m, hipStream_t st);
+// resource creation: the big models of the slots [first, first + count) are freed
+int launch_big_release(BigMap* big, uint32_t first, uint32_t count, hipStream_t st);
 int launch_small_finish(const SmallArgs& a, hipStream_t st);              // counters for the next sub-batch
 // size / isEmpty rows of the sub-batch [lo, hi): emitted into the event buffer before the sort (query entries), then
 // answered from the sorted buffer after the unpermute (the row's staged result is a placeholder)
@@ -408,6 +417,7 @@ struct MapWideArgs {
   const uint32_t* mpcap;       //   log2(capacity / 16) of the peak (in TTL mode a lower bound for the bounds above)
   unsigned long long* ctl;     // [C_N] scratch
   const SmallMap* small;       // [max_resources] the small-table state (early resizes, tree bins; map_small.hip)
+  const BigMap* big;           // [kBigSlots] the models of maps past the window with a tree bin (map_big.hip)
   const uint64_t* hh_key;      // String.hashCode of HANDLE keys (sorted by handle)
   const int32_t* hh_val;
   uint32_t hh_n;

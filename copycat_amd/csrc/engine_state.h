@@ -127,7 +127,9 @@ struct cc_engine {
   std::map<const void*, std::vector<DevWrite>> dev_pend;
   uint64_t res_dirty_lo = ~0ull, res_dirty_hi = 0, inst_dirty_lo = ~0ull, inst_dirty_hi = 0;
   bool sb_kind_dirty = false;
-  bool dev_dirty() const { return !dev_pend.empty() || res_dirty_hi || inst_dirty_hi || sb_kind_dirty; }
+  bool dev_dirty() const {
+    return !dev_pend.empty() || !big_rel.empty() || res_dirty_hi || inst_dirty_hi || sb_kind_dirty;
+  }
   // device registry + state
   uint32_t* d_inst_res = nullptr;
   uint8_t* d_res_type = nullptr;
@@ -188,6 +190,9 @@ struct cc_engine {
   uint32_t* d_msz_list_n = nullptr;
   // maps whose HashMap table is still small (capacity <= 64): early resizes and tree bins (map_small.hip)
   SmallMap* d_msm = nullptr;       // [max_resources]
+  BigMap* d_mbig = nullptr;        // [kBigSlots] maps that left the window with a tree bin (map_big.hip)
+  std::vector<std::pair<uint32_t, uint32_t>> big_rel;  // resource slots created since the last flush: their big
+                                                       // models are freed there (dev_flush, launch_big_release)
   uint8_t* d_msmall = nullptr;     // [max_resources] 1: in the window
   uint8_t* d_msm_left = nullptr;   // [3][max_resources] maps a replay saw leave the window: sets 0 / 1 (side-stream
                                    // replays), 2 (engine-stream replays); folded into d_msmall on the engine stream

@@ -54,7 +54,6 @@ __global__ void k_small_seg(const uint64_t* __restrict__ key, const uint32_t* __
 // same map and key with different codes; a max-scan of (i if it does not link) gives every event its chain's start;
 // at each chain's end the number of events implied after its first removal is stored there (EvPay.ktag >> 4), and
 // k_small_replay checks the bin at that removal.  (It was one wave per map walking 64 events per step: ~5.5 ms per sub-batch for a hot map.)
-constexpr uint32_t kSkipShift = 4;
 __device__ inline uint32_t chain_code(uint64_t k) {
   return !(k & 8u) && ((k & 3u) == 1u || (k & 3u) == 2u) ? (uint32_t)(k & 3u) : 0u;
 }
@@ -157,7 +156,8 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
                                                               const EvPay* __restrict__ pay, const uint32_t* __restrict__ orig,
                                                               const uint32_t* __restrict__ ctl,
                                                               const uint32_t* __restrict__ seg, const uint32_t* __restrict__ nseg,
-                                                              SmallMap* __restrict__ st, uint8_t* __restrict__ left,
+                                                              SmallMap* __restrict__ st, BigMap* __restrict__ big,
+                                                              uint8_t* __restrict__ left,
                                                               const uint8_t* __restrict__ msmall,
                                                               uint32_t* __restrict__ mpcap, unsigned long long* __restrict__ lvl_at,
                                                               const uint64_t* __restrict__ idx0, const uint64_t* __restrict__ index,
@@ -182,6 +182,7 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
     const uint64_t t_run = wall_clock64();
     uint32_t n_app = 0;
 #endif
+    uint64_t leave_pos = 0;  // the event that grew the table past 64
     // one insertion / removal on the model (the whole wave, uniform arguments); false: the table passed 64
     auto apply = [&](uint64_t kk, uint64_t ykey, uint32_t yh, uint32_t ykt) -> bool {
 #ifdef CC_PHASE_TIMING
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
           if (ttl ? index != nullptr : idx0 != nullptr)
             lvl_reached(lvl_at, m, lv0, j.lvl, ttl ? index[lo + (d - 1) / 2] : *idx0 + d);
         }
+        if (!stay) leave_pos = (kk >> 4) & kEvPosMask;
         return stay;
       }
       j.remove(yh, ykt, ykey);  // a key removed: removeNode
@@ -298,13 +300,18 @@ __global__ __launch_bounds__(kSrW * kWave) void k_small_replay(const uint64_t* _
       atomicAdd(&g_ph_small[6], (unsigned long long)t_stage);
     }
 #endif
-    if (!(j.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
+    // with a tree bin since the last clear: a big model follows the map from here (map_big.hip k_big_replay takes the
+    // model over, right after this kernel; the map keeps its events)
+    const bool to_big = !(j.flags & kSmIn) && big && (j.flags & kSmTree);
+    if (to_big) j.flags |= kSmBig | kSmBigNew;
+    else if (!(j.flags & kSmIn)) {  // only the capacity level and the tree bins matter from here on
       j.n = 0;
       j.used = 0;
     }
     j.store(*s);
     if (l == 0) {  // the map left the window: a mark for the engine stream's fold (d_msmall is not written here)
-      if (!(j.flags & kSmIn)) left[m] = 1;
+      if (to_big) s->pad = (uint32_t)leave_pos;
+      else if (!(j.flags & kSmIn)) left[m] = 1;
       atomicMax(&mpcap[m], j.lvl);
     }
   }
@@ -605,8 +612,12 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
     }
     hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, rst, a.ev_key2, a.ev_val2, a.ev_pay,
                        cmp ? orig : nullptr, cmp ? a.cseg + a.max_resources + 1 : a.ctl, cmp ? a.cseg : a.seg,
-                       cmp ? a.cseg + a.max_resources : a.nseg, a.state,
+                       cmp ? a.cseg + a.max_resources : a.nseg, a.state, a.big,
                        a.left, a.msmall, a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, a.msize != nullptr, a.err);
+    // (the maps a big model follows, after the small replay on its stream)
+    if (launch_big_replay(a, cmp ? orig : nullptr, cmp ? a.cseg + a.max_resources + 1 : a.ctl, cmp ? a.cseg : a.seg,
+                          cmp ? a.cseg + a.max_resources : a.nseg, rst))
+      return -1;
     // (on this stream: its exit marks fold into the snapshot right after it)
     if (rst == st && launch_small_fold(a.left, a.msmall, a.max_resources, st)) return -1;
     if (a.msize)  // TTL mode: every map's events (commits and expiries) set its size and capacity
@@ -620,8 +631,9 @@ int launch_small_replay(const SmallArgs& a, uint32_t E, hipStream_t st, hipStrea
 int launch_small_replay_kernel(const SmallArgs& a, hipStream_t rst) {
   uint32_t* const orig = reinterpret_cast<uint32_t*>(a.ev_key);
   hipLaunchKernelGGL(k_small_replay, dim3(1024), dim3(kSrW * kWave), 0, rst, a.ev_key2, a.ev_val2, a.ev_pay, orig,
-                     a.cseg + a.max_resources + 1, a.cseg, a.cseg + a.max_resources, a.state, a.left, a.msmall, a.mpcap,
-                     a.lvl_at, a.idx0, a.index, a.lo, false, a.err);
+                     a.cseg + a.max_resources + 1, a.cseg, a.cseg + a.max_resources, a.state, a.big, a.left, a.msmall,
+                     a.mpcap, a.lvl_at, a.idx0, a.index, a.lo, false, a.err);
+  if (launch_big_replay(a, orig, a.cseg + a.max_resources + 1, a.cseg, a.cseg + a.max_resources, rst)) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -26,6 +26,7 @@
 
 #include "common.h"
 #include "engine_internal.h"
+#include "big_jhm.h"
 #include "small_jhm.h"
 
 namespace cc {
@@ -347,6 +348,7 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
                                                   const uint64_t* __restrict__ dl, uint64_t fire, uint64_t entries, uint32_t slot, uint32_t op, uint32_t atag, uint64_t apay,
                                                   const uint32_t* __restrict__ peak_lo, const unsigned long long* __restrict__ dropped,
                                                   const uint32_t* __restrict__ mpcap, bool exact, const SmallMap* __restrict__ small,
+                                                  const BigMap* __restrict__ big,
                                                   const uint64_t* __restrict__ hh_key, const int32_t* __restrict__ hh_val,
                                                   uint32_t hh_n, int pass, const uint64_t* __restrict__ claim,
                                                   const unsigned long long* __restrict__ lvl_at,
@@ -391,16 +393,22 @@ __global__ __launch_bounds__(kMwT) void k_mw_order(const uint32_t* __restrict__ 
     } else {
       if (cand && b == bb) {
         // the order inside the bin: creation order (tbl_ins) for a list bin; a small map's bin chain from its HashMap
-        // model (small_jhm.h), tree bins included
+        // model (small_jhm.h), tree bins included; past the window, a map with a tree bin from its big model
         uint64_t ord = ins[e];
         if (sflags & kSmIn) {
           bool dup;
           ord = small_chain_pos(small[slot], jh, (w >> 17) & 3, key[e], dup);
           // (and a model that does not hold the map's live keys -- an engine fault -- refuses rather than guesses)
           if (dup || (16ull << small[slot].lvl) != cap || (!dl && small[slot].n != ctl[C_PRES])) atomicOr(err, kErrMapOrder);
+        } else if (sflags & kSmBig) {
+          const BigMap& B = big[small[slot].pad];
+          bool dup;
+          ord = big_chain_pos(B, jh, (w >> 17) & 3, key[e], dup);
+          if (dup || (16ull << B.h.lvl) != cap || (!dl && B.h.n != ctl[C_PRES])) atomicOr(err, kErrMapOrder);
         }
         atomicMin(&ctl[isnull ? C_IN : C_IM], (unsigned long long)ord);
       }
+      if (sflags & kSmBig) continue;  // (every bin followed: no bounds test)
       // every key the map bound since its last clear (present or not) that shares the deciding bin at a capacity
       // >= 128 and was bound before the table grew past that capacity: a tree bin there needs >= 9 of them at once
       // (HashMap.treeifyBin, TREEIFY_THRESHOLD)
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(kMwT) void k_mw_cset(const CsetEnt* __restrict__ se
                                                  const unsigned long long* __restrict__ lvl_at,
                                                  unsigned long long* __restrict__ ctl, uint32_t* __restrict__ err) {
   if (ctl[C_NULLS] == 0 || ctl[C_MATCH] == 0 || ctl[C_BN] != ctl[C_BM]) return;
-  if (small && (small[slot].flags & kSmIn)) return;  // (a small table's order is its model's)
+  if (small && (small[slot].flags & (kSmIn | kSmBig))) return;  // (a followed table's order is its model's)
   const uint32_t lv = mpcap ? (mpcap[slot] & ~kMpInexact) : 0u;
   if (lv < 3) return;
   if (*full) {
@@ -479,7 +487,8 @@ __global__ void k_mw_size(uint32_t slot, uint32_t op, const unsigned long long* 
 __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsigned long long* __restrict__ ctl,
                             uint32_t* __restrict__ peak_lo, unsigned long long* __restrict__ dropped,
                             uint8_t* __restrict__ out_status,
-                            uint64_t* __restrict__ out_value, const SmallMap* __restrict__ small, uint32_t* __restrict__ err) {
+                            uint64_t* __restrict__ out_value, const SmallMap* __restrict__ small,
+                            const BigMap* __restrict__ big, uint32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
   const uint64_t pres = ctl[C_PRES];
   uint32_t st = CC_STATUS(CC_ST_OK, CC_TAG_NULL);
@@ -502,11 +511,14 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
         const uint64_t bn = ctl[C_BN], bm = ctl[C_BM];
         npe = bn != bm ? bn < bm : ctl[C_IN] < ctl[C_IM];
         if (bn == bm) {  // decided inside one bin: by the bin's chain order
-          bool tree = false;
+          bool tree = false, followed = false;
           if (small) {
             const SmallMap& sm = small[slot];
             if (sm.flags & kSmIn) {
               tree = (sm.flags & kSmAmbig) != 0;  // the chain read from the map's HashMap model (k_mw_order)
+            } else if (sm.flags & kSmBig) {  // the chain read from the map's big model (k_mw_order)
+              tree = (big[sm.pad].h.flags & kSmAmbig) != 0;
+              followed = true;
             } else {  // a bin that was a tree bin while the table was small (mod 64)
               tree = ((sm.flags & kSmTree) && ((sm.tree_bins >> (bn & 63u)) & 1ull)) || (sm.flags & kSmUnknown);
             }
@@ -514,7 +526,7 @@ __global__ void k_mw_finish(uint32_t slot, uint32_t op, uint64_t row, const unsi
           // above capacity 64: creation order unless the bin could have been a tree bin, which needs 9 keys in it at
           // once since the last clear (that wipes every bin); the bin's distinct keys since then are at most its
           // bound keys plus the keys compacted away (k_mw_order pass 1, k_mw_cset)
-          for (int q = 0; q < 32; ++q) tree |= ctl[C_TR0 + q] >= 9;
+          for (int q = 0; q < 32 && !followed; ++q) tree |= ctl[C_TR0 + q] >= 9;
           if (tree) atomicOr(err, kErrMapOrder);
         }
       }
@@ -620,7 +632,7 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
     for (int pass = 0; pass < 2; ++pass)
       hipLaunchKernelGGL(k_mw_order, dim3(grid), dim3(kMwT), 0, st, a.tbl_word, a.tbl_key, a.tbl_val, a.tbl_ins, a.tbl_dl,
                          a.fire_clock, a.entries, a.slot, op, atag, apay, a.peak_lo,
-                         (const unsigned long long*)a.dropped, a.mpcap, a.msize != nullptr, a.small, a.hh_key, a.hh_val,
+                         (const unsigned long long*)a.dropped, a.mpcap, a.msize != nullptr, a.small, a.big, a.hh_key, a.hh_val,
                          a.hh_n, pass, a.tbl_claim, a.lvl_at, a.ctl, a.err);
     if (a.cset) {
       const uint32_t cg = (uint32_t)std::min<uint64_t>(2048, (a.cset_n + kMwT - 1) / kMwT);
@@ -630,7 +642,7 @@ int launch_map_wide(const MapWideArgs& a, hipStream_t st) {
   }
   if (a.msize) hipLaunchKernelGGL(k_mw_size, dim3(1), dim3(64), 0, st, a.slot, op, a.ctl, a.msize, a.err);
   hipLaunchKernelGGL(k_mw_finish, dim3(1), dim3(64), 0, st, a.slot, op, a.row, a.ctl, a.peak_lo,
-                     (unsigned long long*)a.dropped, a.out_status, a.out_value, a.small, a.err);
+                     (unsigned long long*)a.dropped, a.out_status, a.out_value, a.small, a.big, a.err);
   if (hipGetLastError() != hipSuccess) return -1;
   if (op == CC_OP_MAP_CLEAR || op == CC_OP_DELETE)
     return launch_map_drop_resource(a.tbl_word, a.entries, a.slot, a.cgen, st);

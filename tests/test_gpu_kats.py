@@ -23,13 +23,13 @@ def test_gpu_kat_coverage():
             "election_next_on_close", "A10_close_publishes_leave_for_non_member", "A11_lock_survives_holder_close",
             "manager_create_concurrency", "manager_get_create_concurrency", "manager_operate_many",
             "manager_get_reuses_instance", "A13_delete_resource_by_instance_id", "A18_multimap_put_never_stores"} <= names
-    # every KAT runs through the engine; the ones it refuses (a containsValue decided inside a java.util.HashMap tree
-    # bin) must fail loudly: test_kat_refused_on_gpu
+    # every KAT runs through the engine; one it refused would have to fail loudly (test_kat_refused_on_gpu)
     assert len(KATS) + len(REFUSED) == len(all_kats())
     assert {"A5_contains_value_treeify_resize", "A5_contains_value_string_hash_order", "A5_contains_value_tree_bin_order",
-            "A5_tree_bin_put_after_treeify", "A5_tree_bin_remove_and_untreeify", "A12_close_after_tree_bin_removal"} <= names
-    # the one refusal left: a bin that was a tree bin while the table was small, asked after the table grew past 64
-    assert {k["name"] for k in REFUSED} == {"A5_tree_bin_leaves_small_window"}
+            "A5_tree_bin_put_after_treeify", "A5_tree_bin_remove_and_untreeify", "A12_close_after_tree_bin_removal",
+            "A5_tree_bin_leaves_small_window"} <= names
+    # none left: a bin that was a tree bin while the table was small is followed past 64 by the map's big model
+    assert not REFUSED
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
@@ -39,9 +39,8 @@ def test_kat_on_gpu(kat):
 
 @pytest.mark.parametrize("kat", REFUSED, ids=[k["name"] for k in REFUSED])
 def test_kat_refused_on_gpu(kat):
-    """A containsValue whose answer is decided inside a bin that was a red-black tree bin (HashMap.treeifyBin at
-    capacity 64) after the table grew past 64 fails the batch with CC_ERR_STATE: the engine follows tree-bin order
-    node for node only while the table is small (map_small.hip), and never guesses."""
+    """A KAT marked `"gpu": "refuses"` must fail the batch with CC_ERR_STATE: the engine never guesses an order it
+    does not follow (none is marked now)."""
     from copycat_amd import abi
     from copycat_amd.engine import EngineError
 
