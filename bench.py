@@ -1162,8 +1162,10 @@ def measure_c3(args, dev, rank, world, dist, n, steps, warmup, R):
                        "whole_map": ({"containsValue_rate": args.cv_rate, "clear_rate": args.clear_rate,
                                       "null_put_rate": args.null_rate, "delete_rate": args.delete_rate,
                                       "engine_counters": dict(zip(("barrier_rows", "in_stream_containsValue",
-                                                                   "sub_batches", "map_events"), E.counters()))}
+                                                                   "sub_batches", "map_events", "big_models"),
+                                                                  E.counters()))}
                                      if args.cv_rate or args.clear_rate or args.null_rate or args.delete_rate else None),
+                       "map_big_models": E.counters()[4],  # maps followed past 64 for a tree bin (map_big.hip)
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
                        "sub_batch": args.sub_batch or "default(16M)", "gen_s": round(t_gen, 2),
                        "watermarks": wm_all.cpu().tolist() if dist is not None else [int(wm_local.item())]},

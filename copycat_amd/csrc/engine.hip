@@ -2185,8 +2185,16 @@ extern "C" int cc_applied_index_async(cc_engine* e, uint64_t* d_out, void* strea
 
 extern "C" int cc_engine_counters(cc_engine* e, uint64_t* out, uint32_t n) {
   if (!e || (n && !out)) return CC_ERR_INVALID;
-  const uint64_t v[4] = {e->stat_barriers, e->stat_isc, e->stat_subbatches, e->stat_events};
-  for (uint32_t i = 0; i < n && i < 4; ++i) out[i] = v[i];
+  uint64_t v[5] = {e->stat_barriers, e->stat_isc, e->stat_subbatches, e->stat_events, 0};
+  if (n > 4 && e->d_mbig) {  // (the owners of the big models: one strided read after the stream drains)
+    int rc = cc_sync(e);
+    if (rc) return rc;
+    uint32_t own[kBigSlots];
+    HIPCHECK(hipMemcpy2D(own, sizeof(uint32_t), &e->d_mbig->h.owner, sizeof(BigMap), sizeof(uint32_t), kBigSlots,
+                         hipMemcpyDeviceToHost));
+    for (uint32_t b = 0; b < kBigSlots; ++b) v[4] += own[b] != 0;
+  }
+  for (uint32_t i = 0; i < n && i < 5; ++i) out[i] = v[i];
   return CC_OK;
 }
 

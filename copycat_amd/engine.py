@@ -377,9 +377,10 @@ class Engine:
         return self.L.cc_engine_stream(self.h)
 
     def counters(self):
-        """(barrier rows applied, containsValue rows answered in the stream, sub-batches, map events) since creation."""
-        out = np.zeros(4, np.uint64)
-        _check(self.L.cc_engine_counters(self.h, out.ctypes.data, 4))
+        """(barrier rows applied, containsValue rows answered in the stream, sub-batches, map events) since creation,
+        and the big HashMap models held now (maps past capacity 64 with a tree bin)."""
+        out = np.zeros(5, np.uint64)
+        _check(self.L.cc_engine_counters(self.h, out.ctypes.data, 5))
         return tuple(int(x) for x in out)
 
     def applied_index(self):

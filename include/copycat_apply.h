@@ -340,8 +340,9 @@ int  cc_apply_batch_host_events(cc_engine* e, const cc_batch* h_cols, uint64_t n
 int  cc_applied_index(cc_engine* e, uint64_t* out);
 /* Cumulative path counters of the engine (observability; ABI 5): out[0] whole-map / schedule rows applied as batch
  * barriers, out[1] map containsValue rows answered in the stream (map_cv.hip), out[2] sub-batches launched,
- * out[3] map events sorted and replayed (small maps' HashMap models, size rows, cleared maps' sizes: map_small.hip).
- * n = entries of `out` to fill (at most 4). */
+ * out[3] map events sorted and replayed (small maps' HashMap models, size rows, cleared maps' sizes: map_small.hip),
+ * out[4] big HashMap models held now (maps past capacity 64 with a tree bin: map_big.hip; reading it syncs).
+ * n = entries of `out` to fill (at most 5). */
 int  cc_engine_counters(cc_engine* e, uint64_t* out, uint32_t n);
 /* The same watermark written stream-ordered into device memory (u64 at d_out) without a host sync: what a rank feeds
  * to the RCCL all-gather of applied watermarks after each batch. */

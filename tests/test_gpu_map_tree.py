@@ -117,6 +117,7 @@ def test_tree_bin_grows_past_64_under_churn(seed, n_tree, n_other, sub_batch):
     cv = np.nonzero(b.op == abi.CC_OP_MAP_CONTAINSVALUE)[0]
     npe = int((gs[cv] == abi.cc_status(abi.CC_ST_NULL_POINTER, abi.CC_TAG_NULL)).sum())
     assert 0 < npe < len(cv)
+    assert E.counters()[4] == 1  # the map is followed by a big model
 
 
 def test_tree_bin_past_64_with_clears():
@@ -152,6 +153,7 @@ def test_tree_bin_maps_many_and_delete():
     gs, gv, os_, ov = _apply_both(E, O, [b])
     _assert_rows(gs, gv, os_, ov)
     _assert_maps(E, O, range(maps))
+    assert E.counters()[4] == maps
     d = _batch([(abi.CC_OP_DELETE, 0, N, 0)] * 2, len(b) + 1, [1, 4])
     r2 = _tree_rows(rng, 30, 300, 6_000, shift=26)
     b2 = _batch(r2 + r2, len(b) + 3, [1] * len(r2) + [4] * len(r2))
