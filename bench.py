@@ -861,7 +861,7 @@ def run_c2(args, dev, rank, world, dist):
                                     f"{n:,} committed entries per step over {R:,} AtomicValueState resources per GPU, "
                                     "a new client-model batch every step"),
                        "commits_per_step_per_gpu": n, "resources_per_gpu": R, "parallelism": f"shard{world}",
-                       "sub_batch": args.sub_batch or "default(16M)", "resident_streams": nstreams,
+                       "sub_batch": args.sub_batch or "default(24Mi)", "resident_streams": nstreams,
                        "cas_success_share": {"min": round(min(shares), 4), "mean": round(sum(shares) / len(shares), 4)},
                        "watermarks": watermarks, "gen_s": round(t_gen, 2)},
             "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all,

@@ -27,7 +27,7 @@ constexpr int kScanGroups = 16;           // row groups of the tile-prefix scan 
 constexpr int kMaxTiles = 1024;           // tiles per sub-batch => sub-batch <= 16M commits
 constexpr int kPersistGrid = 256;         // persistent tile loops: one 1024-thread workgroup per CU
 constexpr int kV3Tile = 8192;             // value-only pipeline (value_path.hip): commits per partition tile
-constexpr int kV3MaxTiles = 2048;         //   tiles per sub-batch (sub-batch <= 16M commits)
+constexpr int kV3MaxTiles = 3072;         //   tiles per sub-batch (a value-only engine's sub-batch <= 24 Mi commits)
 constexpr uint32_t kNoRes = 0xFFFFFFFFu;
 
 // device error bits (d_err)

@@ -430,13 +430,19 @@ extern "C" int cc_engine_create(const cc_config* cfg, cc_engine** out) {
       return set_err(CC_ERR_CAPACITY, "map_capacity and max_resources together exceed the partition's bucket capacity");
     }
   }
-  // sub-batch: a multiple of the partition tile (keeps every sub-batch start 16 KiB-aligned)
-  uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)16 << 20;
+  // sub-batch: a multiple of the partition tile (keeps every sub-batch start 16 KiB-aligned).  The value-only pipeline
+  // (value_path.hip: 8,192-commit tiles, kV3MaxTiles of them) takes up to 24 Mi commits per sub-batch, 24 Mi by default:
+  // 100M commits in 4 sub-batches instead of 6, 12 launches per step instead of 18.  The extended path (maps,
+  // coordination, value events; kMaxTiles tiles of kTile) stays at 16 Mi: sub_ext, used once the engine turns ext.
+  uint64_t sub = cfg->sub_batch ? cfg->sub_batch : (uint64_t)kV3MaxTiles * kV3Tile;
   sub = std::min<uint64_t>(sub, cfg->max_batch);
   sub = (sub + kTile - 1) / kTile * kTile;
-  sub = std::min<uint64_t>(sub, (uint64_t)kMaxTiles * kTile);
+  sub = std::min<uint64_t>(sub, (uint64_t)kV3MaxTiles * kV3Tile);
+  static_assert((uint64_t)kV3MaxTiles * kV3Tile >= (uint64_t)kMaxTiles * kTile, "the value-only sub-batch is the larger");
+  static_assert(((uint64_t)kV3MaxTiles * kV3Tile) % kTile == 0, "a multiple of the partition tile");
   e->sub_batch = sub;
-  e->max_tiles = sub / kTile;
+  e->sub_ext = std::min<uint64_t>(sub, (uint64_t)kMaxTiles * kTile);
+  e->max_tiles = (sub + kTile - 1) / kTile;
 
   const uint64_t slots = (uint64_t)e->sb << kSbShift;
   e->res_type.assign(slots, CC_RES_NONE);
@@ -1349,7 +1355,7 @@ extern "C" int cc_apply_batch(cc_engine* e, const cc_batch* c, uint64_t n, const
   const uint64_t seg_lo = cur;
   const uint64_t seg_hi = action == 2 ? tim_b : (action == 1 ? bar_b : n);
   for (uint64_t lo = seg_lo, hi; lo < seg_hi; lo = hi) {
-    hi = std::min(seg_hi, lo + e->sub_batch);
+    hi = std::min(seg_hi, lo + (e->ext ? e->sub_ext : e->sub_batch));
     if (e->sm_alt_on && !e->ttl_live) {  // the other event-buffer set, once its replay is done (engine_state.h SmSet)
       std::swap(e->d_sm_key, e->sm_alt.key);
       std::swap(e->d_sm_key2, e->sm_alt.key2);

@@ -90,7 +90,7 @@ struct cc_engine {
   bool quarter = false;
   uint32_t sbq_base() const { return sb + (map_bits ? (1u << map_bits) + kHotMax : 0u); }
   uint32_t sb_total() const { return sbq_base() + (quarter ? 4 * sb : 0u); }
-  uint64_t sub_batch = 0, max_tiles = 0;
+  uint64_t sub_batch = 0, sub_ext = 0, max_tiles = 0;  // sub_ext: the sub-batch once the engine is ext (<= 16 Mi)
   // host mirrors of the registry
   std::vector<uint8_t> res_type;     // [sb*256]
   std::vector<uint32_t> inst_res;    // [max_inst]

@@ -186,8 +186,9 @@ typedef struct cc_config {
                                2M: the table has 2^k regions of 2048 entries, >= 2 x map_capacity) */
   int32_t  device;          /* HIP device ordinal                                                  */
   uint32_t flags;           /* CC_CFG_* */
-  uint64_t sub_batch;       /* commits per internal sub-batch (0 = default 16M; rounded up to a multiple
-                               of 16384, at most 16M)                                              */
+  uint64_t sub_batch;       /* commits per internal sub-batch (0 = default 24Mi; rounded up to a multiple
+                               of 16384, at most 24Mi; an engine with maps, coordination resources or
+                               value events runs its batches in sub-batches of at most 16Mi)        */
   uint32_t coord_cap;       /* entries per coordination resource: lock waiters, election listeners, group
                                members, value listeners, queue elements (0 = 64 = CC_LOCK_QUEUE; else a power
                                of two in [64, 65536]; CC_ERR_CAPACITY beyond).  Device memory per resource slot:
