@@ -29,6 +29,9 @@ namespace cc {
 #define CC_PART_EXT_UNROLL 0  // 1: the chunk loop fully unrolled (bigger code, fewer spills)
 #endif
 namespace {
+enum : uint32_t { kRgXRec = 0, kRgValue = 1, kRgMap = 2, kRgHot = 3 };  // record kinds of the write-out plane (rg)
+constexpr uint32_t kRgPos = (1u << 14) - 1;
+static_assert(kTile <= (int)kRgPos + 1, "tile-local staging positions in 14 bits");
 constexpr int kXQ = kTile / kPT;  // commits per thread per tile (16)
 constexpr uint32_t kRpDead = 0xFFFFFFFFu;
 constexpr uint32_t kTpWalk = 0x80u;  // type byte flag: a value commit of a super-bucket k_apply_value walks
@@ -69,6 +72,9 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   uint64_t* ridx = rkey + C;
   uint32_t* rres = reinterpret_cast<uint32_t*>(ridx + C);
   uint32_t* rmeta = rres + C;
+  // per sorted record: its tile-local staging position | kind << 14 (kRgXRec / kRgValue / kRgMap / kRgHot), written by
+  // the thread that places it: the write-out's pieces find their destination with one LDS read instead of the bucket
+  // lookups bucket -> toff / trun / kstart / skind (three dependent LDS levels per 16-byte piece)
   uint16_t* rsb = reinterpret_cast<uint16_t*>(rmeta + C);
   uint32_t* wc = reinterpret_cast<uint32_t*>(rsb + C);  // [kPW][hw] packed u16 pairs
   const uint32_t hw = (sb + 1) / 2;
@@ -117,6 +123,7 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
   }
   lds_barrier();
   const uint32_t sb_hot = sb_val + (map_bits ? (1u << map_bits) : 0u);
+  const uint32_t map_lim = sb_hot + (map_bits ? (uint32_t)kHotMax : 0u);  // map regions + hot-key buckets
   const uint64_t tile0 = lo + (uint64_t)blockIdx.x * kTile;
   const uint64_t tile1 = tile0 + kTile < hi ? tile0 + kTile : hi;
   const uint32_t tbase = blockIdx.x * kTile;
@@ -439,12 +446,14 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
       const uint32_t s = kstart[sk[j]] + within;
       rab[s] = ab[j];
       rmeta[s] = meta[j] | ((res[j] & ((1u << kSbShift) - 1)) << 16);
-      rsb[s] = (uint16_t)sk[j];
       rres[s] = xs[j];
       rkey[s] = kk[j];
       ridx[s] = ii[j];
       if (IDS) rpad[s] = idv[j];
       cp[j] = toff[sk[j]] + trun[sk[j]] + within;
+      const uint32_t k = sk[j];
+      const uint32_t kind = k < sb_val && !skind[k] ? kRgValue : (k >= sb_val && k < map_lim ? (k >= sb_hot ? kRgHot : kRgMap) : kRgXRec);
+      rsb[s] = (uint16_t)(cp[j] | (kind << 14));
     }
     lds_barrier();
     PH(4);
@@ -481,20 +490,18 @@ __global__ __launch_bounds__(kPT, 4) void k_part_ext(
     // (three stores at a 48-byte stride) left every piece its own partial-line write request (WRITE_SIZE 99 B per
     // commit against 50).  np = 2 when no record is an XRec (no coordination, no value events): a map record's two
     // pieces then take two lanes, not three with one idle (c3: the write-out was 37 % of the partition).
-    const uint32_t map_lim = sb_hot + (map_bits ? (uint32_t)kHotMax : 0u);  // map regions + hot-key buckets
     const uint32_t np = (IDS || sbq_base || (ext_flags & kExtValue)) ? 3u : 2u;  // (block-uniform)
     for (uint32_t p = t; p < np * nlive; p += kPT) {
       const uint32_t s = np == 2u ? p >> 1 : p / 3, part = p - np * s;
-      const uint32_t k = rsb[s];
-      const uint32_t g = tbase + toff[k] + trun[k] + (s - kstart[k]);
-      if (k < sb_val && !skind[k]) {
+      const uint32_t gw = rsb[s], g = tbase + (gw & kRgPos), kind = gw >> 14;
+      if (kind == kRgValue) {
         if (part == 0) {
           st_meta[g] = rmeta[s];
           st_ab[g] = rab[s];
         }
-      } else if (k >= sb_val && k < map_lim) {
+      } else if (kind >= kRgMap) {
         if (part == 2) continue;
-        if (part == 0 && hot_meta && k >= sb_hot) hot_meta[g] = rmeta[s];
+        if (part == 0 && hot_meta && kind == kRgHot) hot_meta[g] = rmeta[s];
         const u64x2 v = part == 0 ? u64x2{rab[s].x, rkey[s]} : u64x2{ridx[s], (uint64_t)rmeta[s] | ((uint64_t)rres[s] << 32)};
         reinterpret_cast<u64x2*>(mrec + g)[part] = v;
       } else {

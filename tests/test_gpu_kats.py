@@ -23,7 +23,8 @@ def test_gpu_kat_coverage():
             "election_next_on_close", "A10_close_publishes_leave_for_non_member", "A11_lock_survives_holder_close",
             "manager_create_concurrency", "manager_get_create_concurrency", "manager_operate_many",
             "manager_get_reuses_instance", "A13_delete_resource_by_instance_id", "A18_multimap_put_never_stores"} <= names
-    # every KAT runs through the engine; one it refused would have to fail loudly (test_kat_refused_on_gpu)
+    # every KAT runs through the engine (a KAT marked "gpu": "refuses" would have to fail the batch loudly with
+    # CC_ERR_STATE; none is marked any more)
     assert len(KATS) + len(REFUSED) == len(all_kats())
     assert {"A5_contains_value_treeify_resize", "A5_contains_value_string_hash_order", "A5_contains_value_tree_bin_order",
             "A5_tree_bin_put_after_treeify", "A5_tree_bin_remove_and_untreeify", "A12_close_after_tree_bin_removal",
@@ -35,15 +36,3 @@ def test_gpu_kat_coverage():
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
 def test_kat_on_gpu(kat):
     KatRun(kat, EngineBackend(kat)).run()
-
-
-@pytest.mark.parametrize("kat", REFUSED, ids=[k["name"] for k in REFUSED])
-def test_kat_refused_on_gpu(kat):
-    """A KAT marked `"gpu": "refuses"` must fail the batch with CC_ERR_STATE: the engine never guesses an order it
-    does not follow (none is marked now)."""
-    from copycat_amd import abi
-    from copycat_amd.engine import EngineError
-
-    with pytest.raises(EngineError) as ei:
-        KatRun(kat, EngineBackend(kat)).run()
-    assert ei.value.rc == abi.CC_ERR_STATE
