@@ -126,3 +126,32 @@ def test_c2_continued_steps():
         for x, y in zip(E.value_state(), O.value_state()):
             assert np.array_equal(x, y)
     assert E.applied_index() == O.applied_index() == 3 * n
+
+
+def test_c2_two_sub_batches_at_the_24mi_default():
+    """A value-only batch longer than the default sub-batch (24 Mi = 3,072 tiles of 8,192, the apply's LDS run-table
+    limit): the first sub-batch uses every tile slot, the second is ragged; every row and the final state against the
+    oracle, then a second batch continues the state."""
+    from copycat_amd.engine import Engine
+    from copycat_amd.workload import AtomicLongClients
+    from oracle.oracle_py import Oracle
+
+    n, R = 24 * (1 << 20) + 3_000_001, 65536
+    E = Engine(R, R, n)
+    E.resource_create_range(0, R, abi.CC_RES_VALUE)
+    E.instance_open_range(0, R, 0, 1, 1)
+    O = Oracle(R, R)
+    for r in range(R):
+        O.resource_create(r, abi.CC_RES_VALUE)
+        O.instance_open(r, r, 1 + r, 1)
+    clients = AtomicLongClients(R, threads=8)
+    subs0 = E.counters()[2]  # (barrier rows, in-stream containsValue rows, sub-batches, map events, big models)
+    for step in range(2):
+        b = clients.next(n if step == 0 else 5_000_000)
+        s, v = E.apply_host(b)
+        s2, v2 = O.apply(b)
+        assert np.array_equal(s, s2) and np.array_equal(v, v2), step
+        for x, y in zip(E.value_state(), O.value_state()):
+            assert np.array_equal(x, y)
+    assert E.counters()[2] - subs0 == 3  # (2 for the first batch, 1 for the second)
+    assert E.applied_index() == O.applied_index() == n + 5_000_000
