@@ -110,13 +110,15 @@ __device__ inline CoordEnt* ents(uint8_t* blk) { return reinterpret_cast<CoordEn
 // (copied in at kernel start, back at the end), the rest stay in the global block.  Small lock queues / listener
 // and member lists (the common case) then never wait on global memory inside a slot's sequential walk, and a
 // one-entry list (a lock with one waiter, a group with one member) never waits on LDS either.
-constexpr uint32_t kECache = 4;  // (4, not 8: k_apply_coord fits three workgroups per CU)
+// (2: entry 0 in registers, entry 1 in LDS -- the LDS this frees holds more event slots per walking lane, kEvLane)
+constexpr uint32_t kECache = 2;
 // Reads and writes select on the index, never on the pointer: each access keeps its address space (ds_read /
 // global_load), so an LDS hit does not wait behind the walk's outstanding global stores as a flat access would.
 typedef __attribute__((address_space(1))) CoordEnt GlbEnt;
 struct Ents {
-  // this lane's column of the entry planes (one pointer: three planes per entry, lane-minor): entry p's x at
-  // [(3p) * kLanes], idx at [(3p + 1) * kLanes], inst | pad << 32 at [(3p + 2) * kLanes]
+  // this lane's column of the entry planes (one pointer: three planes per cached entry, lane-minor; entry 0 lives in
+  // r0, so entry p >= 1 has planes 3(p - 1) ..): x at [3(p - 1) * kLanes], idx at [(3(p - 1) + 1) * kLanes],
+  // inst | pad << 32 at [(3(p - 1) + 2) * kLanes]
   LdsU64* lc;
   GlbEnt* glb;
   uint32_t cap;  // entries of the block (cc_config.coord_cap, a power of two)
@@ -127,9 +129,9 @@ struct Ents {
     if (p == 0) return r0;
     CoordEnt e;
     if (p < kECache) {
-      e.x = lc[(3 * p) * kLanes];
-      e.idx = lc[(3 * p + 1) * kLanes];
-      const uint64_t ip = lc[(3 * p + 2) * kLanes];
+      e.x = lc[(3 * (p - 1)) * kLanes];
+      e.idx = lc[(3 * (p - 1) + 1) * kLanes];
+      const uint64_t ip = lc[(3 * (p - 1) + 2) * kLanes];
       e.inst = (uint32_t)ip;
       e.pad = (uint32_t)(ip >> 32);
       return e;
@@ -160,9 +162,9 @@ struct Ents {
       return;
     }
     if (p < kECache) {
-      lc[(3 * p) * kLanes] = v.x;
-      lc[(3 * p + 1) * kLanes] = v.idx;
-      lc[(3 * p + 2) * kLanes] = (uint64_t)v.inst | ((uint64_t)v.pad << 32);
+      lc[(3 * (p - 1)) * kLanes] = v.x;
+      lc[(3 * (p - 1) + 1) * kLanes] = v.idx;
+      lc[(3 * (p - 1) + 2) * kLanes] = (uint64_t)v.inst | ((uint64_t)v.pad << 32);
       return;
     }
     __builtin_nontemporal_store(v.x, &glb[p].x);
@@ -638,7 +640,10 @@ constexpr int kCT2 = 256;                  // threads per workgroup
 constexpr int kCW2 = kCT2 / kWave;
 constexpr int kCPer2 = 2;                  // commits per thread per chunk
 constexpr int kCCh2 = kCT2 * kCPer2;       // 512 commits of the super-bucket per chunk
-constexpr int kEvLane = 8;                 // LDS event slots per walking lane per chunk (more: straight to the arena)
+// LDS event slots per walking lane per chunk; more go straight to the arena, one global atomic on the arena counter
+// each, which the wave waits for (a group lane publishes ~4 events per chunk on c5: with 8 slots ~6 % of lanes
+// overflowed every chunk)
+constexpr int kEvLane = 11;  // (LDS 52,800 B: three workgroups per CU need <= 53,248 at the 2 KiB allocation granularity)
 
 __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict__ xr, const uint16_t* __restrict__ ttab,
                                                      uint32_t tiles, uint32_t sb, uint32_t sbq_base,
@@ -665,7 +670,7 @@ __global__ __launch_bounds__(kCT2, 3) void k_apply_coord(const XRec* __restrict_
   __shared__ uint32_t wsum[kCW2];
   __shared__ uint64_t evp[kEvLane * 3 * kQ];    // the walkers' event buffers (lane-minor planes, see kLanes)
   __shared__ uint32_t evoff[kQ + 1];
-  __shared__ uint64_t ecache[3 * kECache * kQ];  // the walkers' first entries (Ents), lane-minor
+  __shared__ uint64_t ecache[3 * (kECache - 1) * kQ];  // the walkers' entries 1 .. kECache-1 (Ents), lane-minor
   __shared__ unsigned long long evbase;
 
   const uint32_t s = blockIdx.x / kQPerSb, q0 = (blockIdx.x % kQPerSb) * kQ;

@@ -1,6 +1,8 @@
-// Probe (argument: dynamic LDS bytes per workgroup): where do the waves of k_apply_coord-shaped workgroups land?  516 workgroups of 256 threads with the
-// kernel's LDS footprint (52,800 B, three per CU); every wave records its hardware id (XCC, SE, CU, SIMD).  The
-// question: do the wave-0s of the workgroups sharing a CU (k_apply_coord's walkers) share one SIMD?
+// Probe (argument: dynamic LDS bytes per workgroup): where do the waves of k_apply_coord-shaped workgroups land, and
+// how many run on one CU at once?  516 workgroups of 256 threads; every wave records its hardware id (XCC, SE, CU,
+// SIMD) and every workgroup its start / end clock, so co-residency is counted from overlapping intervals (a workgroup
+// dispatched onto a CU after another finished is not co-resident with it).  The questions: do the wave-0s of the
+// workgroups sharing a CU (k_apply_coord's walkers) share one SIMD, and at which LDS size do three stop fitting?
 //   hipcc --offload-arch=gfx950 -O2 simd_probe.hip -o /tmp/simd_probe && /tmp/simd_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -9,7 +11,7 @@
 #include <tuple>
 #include <vector>
 
-__global__ __launch_bounds__(256, 3) void k_probe(uint32_t* out, uint32_t spin) {
+__global__ __launch_bounds__(256, 3) void k_probe(uint32_t* out, unsigned long long* times, uint32_t spin) {
   extern __shared__ uint32_t pad[];
   const uint32_t t = threadIdx.x, w = t >> 6;
   pad[t] = t;
@@ -25,6 +27,10 @@ __global__ __launch_bounds__(256, 3) void k_probe(uint32_t* out, uint32_t spin) 
   uint64_t t0 = wall_clock64();
   while (wall_clock64() - t0 < spin) __builtin_amdgcn_s_sleep(2);
   if (pad[(t + 1) & 255] == 0xFFFFFFFFu) out[0] = 0;
+  if (t == 0) {
+    times[2 * blockIdx.x] = t0;
+    times[2 * blockIdx.x + 1] = wall_clock64();
+  }
 }
 
 int main(int argc, char** argv) {
@@ -32,11 +38,15 @@ int main(int argc, char** argv) {
   const unsigned lds = argc > 1 ? (unsigned)atoi(argv[1]) : 52800u;
   printf("LDS %u B per workgroup\n", lds);
   uint32_t* d;
+  unsigned long long* dt;
   (void)hipMalloc(&d, G * 4 * 2 * 4);
-  hipLaunchKernelGGL(k_probe, dim3(G), dim3(256), lds, 0, d, 20000u);
+  (void)hipMalloc(&dt, G * 2 * 8);
+  hipLaunchKernelGGL(k_probe, dim3(G), dim3(256), lds, 0, d, dt, 20000u);
   if (hipDeviceSynchronize() != hipSuccess) { printf("fail\n"); return 1; }
   std::vector<uint32_t> h(G * 8);
   (void)hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost);
+  std::vector<unsigned long long> tm(G * 2);
+  (void)hipMemcpy(tm.data(), dt, tm.size() * 8, hipMemcpyDeviceToHost);
   // per CU: the SIMDs of each resident workgroup's waves
   std::map<std::tuple<int, int, int, int>, std::vector<std::pair<int, std::vector<int>>>> cu;
   int same_simd_all = 0;
@@ -71,9 +81,19 @@ int main(int argc, char** argv) {
       same_simd_all += all;
     }
   }
-  int max_per_cu = 0;
-  for (auto& kv : cu) max_per_cu = kv.second.size() > (size_t)max_per_cu ? (int)kv.second.size() : max_per_cu;
-  printf("max workgroups on one CU %d\n", max_per_cu);
+  // co-resident workgroups per CU: the most intervals [start, end) of one CU that overlap at one instant
+  int max_per_cu = 0, late = 0;
+  unsigned long long first = ~0ull;
+  for (int b = 0; b < G; ++b) first = tm[2 * b] < first ? tm[2 * b] : first;
+  for (int b = 0; b < G; ++b) late += tm[2 * b] > first + 10000;  // started > 100 us after the first
+  for (auto& kv : cu) {
+    for (auto& p : kv.second) {
+      int c = 0;
+      for (auto& q : kv.second) c += tm[2 * q.first] <= tm[2 * p.first] && tm[2 * p.first] < tm[2 * q.first + 1];
+      max_per_cu = c > max_per_cu ? c : max_per_cu;
+    }
+  }
+  printf("max co-resident workgroups on one CU %d; workgroups starting > 100 us late %d\n", max_per_cu, late);
   printf("CUs used %zu; CUs by distinct wave-0 SIMDs: 1:%d 2:%d 3:%d 4:%d; CUs with >=2 WGs all wave-0 on one SIMD: %d\n",
          cu.size(), hist[1], hist[2], hist[3], hist[4], same_simd_all);
   return 0;
